@@ -1,0 +1,150 @@
+"""ctypes binding of libacme_hip.so (the C ABI declared in include/acme_hip.h).
+
+The product path has no CPU fallback: if the library is missing or cannot be loaded
+on a GPU machine, `lib()` raises.  torch is imported first so that the HIP runtime the
+library links against (SONAME libamdhip64.so.7) resolves to the one torch already
+loaded — one runtime, one device context, shared pointers and streams.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must load the HIP runtime before libacme_hip.so)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libacme_hip.so")
+
+ACME_OK = 0
+ACME_ERR_INVALID = -1
+ACME_ERR_HIP = -2
+ACME_ERR_EMPTY = -3
+ACME_ERR_OOM = -4
+
+MAX_FIELDS = 8
+MAX_MLP_LAYERS = 8
+
+c_i32, c_i64, c_u64, c_f32, c_f64, c_vp = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64,
+                                          ctypes.c_float, ctypes.c_double, ctypes.c_void_p)
+
+
+class ReplayConfig(ctypes.Structure):
+    _fields_ = [("capacity", c_i64), ("sampler", c_i32), ("num_fields", c_i32),
+                ("priority_exponent", c_f64), ("seed", c_u64),
+                ("field_bytes", c_i64 * MAX_FIELDS)]
+
+
+class DQNConfig(ctypes.Structure):
+    _fields_ = [("network", c_i32), ("obs_dtype", c_i32), ("num_actions", c_i32),
+                ("max_batch", c_i32), ("obs_dim", c_i32), ("num_hidden", c_i32),
+                ("hidden", c_i32 * MAX_MLP_LAYERS), ("discount", c_f32),
+                ("importance_sampling_exponent", c_f32), ("learning_rate", c_f32),
+                ("huber_loss_parameter", c_f32), ("adam_beta1", c_f32), ("adam_beta2", c_f32),
+                ("adam_epsilon", c_f32), ("target_update_period", c_i32),
+                ("max_abs_reward", c_f32)]
+
+
+class TransitionBatch(ctypes.Structure):
+    _fields_ = [("o_tm1", c_vp), ("a_tm1", c_vp), ("r_t", c_vp), ("d_t", c_vp), ("o_t", c_vp),
+                ("probabilities", c_vp), ("batch", c_i64), ("global_min_probability", c_vp)]
+
+
+class DQNOutputs(ctypes.Structure):
+    _fields_ = [("loss", c_vp), ("td_error", c_vp), ("priorities", c_vp), ("q_tm1", c_vp)]
+
+
+_SIGS = {
+    "acme_last_error": (ctypes.c_char_p, []),
+    "acme_version": (ctypes.c_char_p, []),
+    "acme_target_arch": (ctypes.c_char_p, []),
+    "acme_replay_create": (c_i32, [ctypes.POINTER(ReplayConfig), ctypes.POINTER(c_vp)]),
+    "acme_replay_destroy": (c_i32, [c_vp]),
+    "acme_replay_insert": (c_i32, [c_vp, ctypes.POINTER(c_vp), c_i64, c_vp, c_i32, c_vp, c_vp]),
+    "acme_replay_fill_synthetic": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_u64, c_vp]),
+    "acme_replay_sample": (c_i32, [c_vp, c_i64, c_u64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "acme_replay_gather": (c_i32, [c_vp, c_vp, c_i64, ctypes.POINTER(c_vp), c_vp]),
+    "acme_replay_update_priorities": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "acme_replay_size": (c_i64, [c_vp]),
+    "acme_replay_capacity": (c_i64, [c_vp]),
+    "acme_replay_debug_leaves": (c_i32, [c_vp, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp),
+                                         ctypes.POINTER(c_vp)]),
+    "acme_dqn_create": (c_i32, [ctypes.POINTER(DQNConfig), ctypes.POINTER(c_vp)]),
+    "acme_dqn_destroy": (c_i32, [c_vp]),
+    "acme_dqn_num_params": (c_i64, [c_vp]),
+    "acme_dqn_flat_size": (c_i64, [c_vp]),
+    "acme_dqn_num_tensors": (c_i32, [c_vp]),
+    "acme_dqn_tensor_info": (c_i32, [c_vp, c_i32, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64),
+                                     ctypes.POINTER(c_i32), ctypes.POINTER(c_i64),
+                                     ctypes.POINTER(ctypes.c_char_p)]),
+    "acme_dqn_bind": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "acme_dqn_forward_backward": (c_i32, [c_vp, ctypes.POINTER(TransitionBatch),
+                                          ctypes.POINTER(DQNOutputs), c_vp]),
+    "acme_dqn_apply": (c_i32, [c_vp, c_vp]),
+    "acme_dqn_step": (c_i32, [c_vp, ctypes.POINTER(TransitionBatch), ctypes.POINTER(DQNOutputs),
+                              c_vp]),
+    "acme_dqn_q_values": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp]),
+    "acme_dqn_num_steps": (c_i64, [c_vp]),
+    "acme_dqn_set_num_steps": (c_i32, [c_vp, c_i64]),
+    "acme_min_f64": (c_i32, [c_vp, c_i64, c_vp, c_vp]),
+    "acme_adam_update": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_f32, c_f32, c_f32, c_f32, c_i64,
+                                 c_vp]),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGS)
+
+_lib = None
+_lock = threading.Lock()
+
+
+class AcmeError(RuntimeError):
+    pass
+
+
+def lib() -> ctypes.CDLL:
+    """Loads libacme_hip.so (raises if absent: there is no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ImportError(
+                    f"{LIB_PATH} not found: run `python -m acme_amd._build` (or "
+                    "__graft_entry__.build()) to compile the HIP library for gfx950.")
+            L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+            for name, (res, args) in _SIGS.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc == ACME_OK:
+        return
+    msg = lib().acme_last_error().decode(errors="replace")
+    if what:
+        msg = f"{what}: {msg}"
+    if rc == ACME_ERR_INVALID:
+        raise ValueError(msg)
+    if rc == ACME_ERR_OOM:
+        raise MemoryError(msg)
+    raise AcmeError(msg)
+
+
+def require_gpu() -> None:
+    if not torch.cuda.is_available():
+        raise RuntimeError("acme_amd's learner and replay run on an AMD GPU (gfx950); "
+                           "no GPU is visible and there is no CPU fallback.")
+
+
+def stream_ptr(stream=None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def ptr(t) -> int:
+    return 0 if t is None else int(t.data_ptr())

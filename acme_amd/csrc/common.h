@@ -1,0 +1,58 @@
+// Shared helpers for the acme_amd HIP library (gfx950 / CDNA4 only).
+//
+// Error model of the C-ABI (include/acme_hip.h): every entry point returns
+// ACME_OK (0) or a negative acme_status and records a human-readable message
+// in a thread-local buffer readable through acme_last_error().  The Python
+// shims map the status to ValueError / RuntimeError, mirroring how the
+// reference surfaces failures as Python exceptions.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+
+#include "../../include/acme_hip.h"
+
+namespace acme {
+
+void set_error(const char* fmt, ...);
+
+#define ACME_HIP_TRY(expr)                                                   \
+  do {                                                                       \
+    hipError_t _e = (expr);                                                  \
+    if (_e != hipSuccess) {                                                  \
+      ::acme::set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), \
+                        __FILE__, __LINE__);                                 \
+      return ACME_ERR_HIP;                                                   \
+    }                                                                        \
+  } while (0)
+
+#define ACME_CHECK_ARG(cond, ...)                                            \
+  do {                                                                       \
+    if (!(cond)) {                                                           \
+      ::acme::set_error(__VA_ARGS__);                                        \
+      return ACME_ERR_INVALID;                                               \
+    }                                                                        \
+  } while (0)
+
+#define ACME_LAUNCH_CHECK()                                                  \
+  do {                                                                       \
+    hipError_t _e = hipGetLastError();                                       \
+    if (_e != hipSuccess) {                                                  \
+      ::acme::set_error("kernel launch failed: %s (%s:%d)",                  \
+                        hipGetErrorString(_e), __FILE__, __LINE__);          \
+      return ACME_ERR_HIP;                                                   \
+    }                                                                        \
+  } while (0)
+
+static inline hipStream_t as_stream(void* s) {
+  return reinterpret_cast<hipStream_t>(s);
+}
+
+static inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+constexpr int kWave = 64;  // CDNA wavefront width; never 32.
+
+}  // namespace acme

@@ -1,0 +1,602 @@
+// DQN learner step for MI355X: the replacement of DQNLearner._step
+// (acme/agents/tf/dqn/learning.py:112-168) behind the C ABI (include/acme_hip.h).
+//
+// One call = the whole SGD step on one stream, no host synchronisation:
+//   online forward on [o_tm1; o_t] (2B rows, shared weights: q_tm1 and q_t_selector)
+//   target forward on o_t (B rows: q_t_value)                        (:123-125)
+//   fused loss kernel: reward clip, discount, double-Q target, TD,    (:128-144)
+//     Huber(delta), f64 importance weights / max, weighted mean, |td| priorities
+//   backward through the duelling head, FC and three convolutions    (:147)
+//   snt.Adam over the flat parameter buffer                          (:148)
+//   target <- online when num_steps % period == 0, then num_steps++  (:157-161)
+//
+// Networks: DQNAtariNetwork = AtariTorso + DuellingMLP([512])
+// (acme/tf/networks/atari.py:36-69, duelling.py:27-59) or snt.nets.MLP([..., A])
+// (examples/bsuite/run_dqn.py:46-49).  The duelling value/advantage first layers are
+// fused into one [7744, 1024] GEMM (columns 0..511 value, 512..1023 advantage).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "conv.h"
+#include "gemm.h"
+#include "kernels.h"
+
+using namespace acme;
+using namespace acme::conv;
+using acme::gemm::launch_gemm;
+
+namespace {
+
+// Nature DQN torso geometry (TF SAME padding, NHWC).
+using G1 = Geom<84, 84, 4, 21, 21, 32, 8, 8, 4, 2, 2>;
+using G2 = Geom<21, 21, 32, 11, 11, 64, 4, 4, 2, 1, 1>;
+using G3 = Geom<11, 11, 64, 11, 11, 64, 3, 3, 1, 1, 1>;
+constexpr int kFlat = 11 * 11 * 64;  // 7744
+constexpr int kHidden = 512;          // DuellingMLP hidden size
+constexpr int kObsBytes = 84 * 84 * 4;
+
+struct Tensor {
+  std::string name;
+  int64_t offset = 0, numel = 0;
+  int ndim = 0;
+  int64_t shape[4] = {1, 1, 1, 1};
+};
+
+struct Layer {  // dense layer of the MLP network
+  int in = 0, out = 0;
+  int w = -1, b = -1;  // tensor indices
+  bool relu = true;
+};
+
+}  // namespace
+
+struct acme_dqn {
+  acme_dqn_config cfg;
+  std::vector<Tensor> tensors;
+  int64_t flat = 0, logical = 0;
+  float *params = nullptr, *target = nullptr, *grads = nullptr, *m = nullptr, *v = nullptr;
+  int64_t num_steps = 0;
+  // Nature tensors
+  int t_c1w = -1, t_c1b, t_c2w, t_c2b, t_c3w, t_c3b, t_fcw, t_fcb, t_vw, t_vb, t_aw, t_ab;
+  // MLP
+  std::vector<Layer> layers;
+  // Workspace (device)
+  std::vector<void*> allocs;
+  float *x1 = nullptr, *x2 = nullptr, *x3 = nullptr, *hid = nullptr;  // online (2B rows)
+  float *t1 = nullptr, *t2 = nullptr, *t3 = nullptr, *thid = nullptr; // target (B rows)
+  std::vector<float*> mlp_act, mlp_tact, mlp_dz;                     // MLP activations
+  float *q_on = nullptr, *q_tg = nullptr;
+  float *dzh = nullptr, *dz3 = nullptr, *dz2 = nullptr, *dz1 = nullptr;
+  float* slab = nullptr;
+  int64_t slab_floats = 0;
+  float* colsum = nullptr;
+  int64_t colsum_floats = 0;
+  float* g = nullptr;  // per-sample dLoss/dq_tm1[a]
+  int32_t* a_cache = nullptr;  // actions of the current batch (for the backward kernels)
+  float* loss_tmp = nullptr;
+  float* td_tmp = nullptr;
+  double* prio_tmp = nullptr;
+};
+
+namespace {
+
+int64_t align64(int64_t x) { return (x + 63) & ~int64_t(63); }
+
+int add_tensor(acme_dqn* l, const char* name, std::initializer_list<int64_t> shape) {
+  Tensor t;
+  t.name = name;
+  t.ndim = (int)shape.size();
+  t.numel = 1;
+  int i = 0;
+  for (int64_t s : shape) {
+    t.shape[i++] = s;
+    t.numel *= s;
+  }
+  t.offset = l->flat;
+  l->flat = align64(l->flat + t.numel);
+  l->logical += t.numel;
+  l->tensors.push_back(t);
+  return (int)l->tensors.size() - 1;
+}
+
+template <class T>
+int dev_alloc(acme_dqn* l, T** p, int64_t count) {
+  void* q = nullptr;
+  if (hipMalloc(&q, std::max<int64_t>(count, 1) * sizeof(T)) != hipSuccess) {
+    set_error("hipMalloc of %lld bytes failed", (long long)(count * sizeof(T)));
+    return ACME_ERR_OOM;
+  }
+  l->allocs.push_back(q);
+  *p = static_cast<T*>(q);
+  return ACME_OK;
+}
+
+inline const float* P(const acme_dqn* l, const float* base, int t) {
+  return base + l->tensors[t].offset;
+}
+inline float* Pm(const acme_dqn* l, float* base, int t) { return base + l->tensors[t].offset; }
+
+// Split-K helper: chunk size (multiple of BK) for `splits` splits of K.
+inline int chunk_for(int K, int splits) {
+  int c = (int)ceil_div(K, splits);
+  return (int)ceil_div(c, gemm::BK) * gemm::BK;
+}
+
+#define ACME_GEMM(BM, BN, WM, WN, prob, splits)                                      \
+  do {                                                                               \
+    hipError_t _e = launch_gemm<BM, BN, WM, WN>(prob, splits, st);                  \
+    if (_e != hipSuccess) {                                                          \
+      set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
+      return ACME_ERR_HIP;                                                           \
+    }                                                                                \
+  } while (0)
+
+// ---------------------------------------------------------------- Nature forward
+// rows = number of observations; first `split` rows from obs_a, the rest from obs_b.
+int nature_forward(acme_dqn* l, const float* prm, const void* obs_a, const void* obs_b,
+                   int split, int rows, float* x1, float* x2, float* x3, float* hid,
+                   float* q, hipStream_t st) {
+  const bool u8 = l->cfg.obs_dtype == ACME_OBS_U8_SCALED;
+  if (u8) {
+    ConvFwd<G1, InU8> p;
+    p.M = rows * G1::OPIX; p.N = G1::CO; p.K = G1::K; p.k_chunk = G1::K;
+    p.x = static_cast<const uint8_t*>(obs_a); p.x2 = static_cast<const uint8_t*>(obs_b);
+    p.split_b = split; p.w = P(l, prm, l->t_c1w); p.bias = P(l, prm, l->t_c1b); p.y = x1;
+    ACME_GEMM(256, 32, 4, 1, p, 1);
+  } else {
+    ConvFwd<G1, InF32> p;
+    p.M = rows * G1::OPIX; p.N = G1::CO; p.K = G1::K; p.k_chunk = G1::K;
+    p.x = static_cast<const float*>(obs_a); p.x2 = static_cast<const float*>(obs_b);
+    p.split_b = split; p.w = P(l, prm, l->t_c1w); p.bias = P(l, prm, l->t_c1b); p.y = x1;
+    ACME_GEMM(256, 32, 4, 1, p, 1);
+  }
+  {
+    ConvFwd<G2, InF32> p;
+    p.M = rows * G2::OPIX; p.N = G2::CO; p.K = G2::K; p.k_chunk = G2::K;
+    p.x = x1; p.x2 = x1; p.split_b = rows; p.w = P(l, prm, l->t_c2w);
+    p.bias = P(l, prm, l->t_c2b); p.y = x2;
+    ACME_GEMM(128, 64, 2, 2, p, 1);
+  }
+  {
+    ConvFwd<G3, InF32> p;
+    p.M = rows * G3::OPIX; p.N = G3::CO; p.K = G3::K; p.k_chunk = G3::K;
+    p.x = x2; p.x2 = x2; p.split_b = rows; p.w = P(l, prm, l->t_c3w);
+    p.bias = P(l, prm, l->t_c3b); p.y = x3;
+    ACME_GEMM(128, 64, 2, 2, p, 1);
+  }
+  {
+    DenseFwd<true> p;
+    p.M = rows; p.N = 2 * kHidden; p.K = kFlat; p.k_chunk = kFlat;
+    p.x = x3; p.x2 = x3; p.split_b = rows; p.ldx = kFlat;
+    p.w = P(l, prm, l->t_fcw); p.bias = P(l, prm, l->t_fcb); p.y = hid; p.act = ACT_RELU;
+    ACME_GEMM(64, 64, 2, 2, p, 1);
+  }
+  return launch_duel_head(hid, rows, kHidden, l->cfg.num_actions, P(l, prm, l->t_vw),
+                          P(l, prm, l->t_vb), P(l, prm, l->t_aw), P(l, prm, l->t_ab), q, st);
+}
+
+// ---------------------------------------------------------------- MLP forward
+template <class In>
+int mlp_layer0(acme_dqn* l, const float* prm, const Layer& L, const void* a, const void* b,
+               int split, int rows, float* y, hipStream_t st) {
+  const bool vec = L.in % 4 == 0 && L.out % 4 == 0;
+  if (vec) {
+    DenseFwd<true, In> p;
+    p.M = rows; p.N = L.out; p.K = L.in; p.k_chunk = L.in;
+    p.x = static_cast<const typename In::T*>(a); p.x2 = static_cast<const typename In::T*>(b);
+    p.split_b = split; p.ldx = L.in; p.w = P(l, prm, L.w); p.bias = P(l, prm, L.b); p.y = y;
+    p.act = L.relu ? ACT_RELU : ACT_NONE;
+    ACME_GEMM(64, 64, 2, 2, p, 1);
+  } else {
+    DenseFwd<false, In> p;
+    p.M = rows; p.N = L.out; p.K = L.in; p.k_chunk = L.in;
+    p.x = static_cast<const typename In::T*>(a); p.x2 = static_cast<const typename In::T*>(b);
+    p.split_b = split; p.ldx = L.in; p.w = P(l, prm, L.w); p.bias = P(l, prm, L.b); p.y = y;
+    p.act = L.relu ? ACT_RELU : ACT_NONE;
+    ACME_GEMM(64, 64, 2, 2, p, 1);
+  }
+  return ACME_OK;
+}
+
+int mlp_forward(acme_dqn* l, const float* prm, const void* obs_a, const void* obs_b, int split,
+                int rows, std::vector<float*>& act, float* q, hipStream_t st) {
+  const int nl = (int)l->layers.size();
+  for (int i = 0; i < nl; ++i) {
+    const Layer& L = l->layers[i];
+    float* y = i == nl - 1 ? q : act[i];
+    int rc;
+    if (i == 0) {
+      rc = l->cfg.obs_dtype == ACME_OBS_U8_SCALED
+               ? mlp_layer0<InU8>(l, prm, L, obs_a, obs_b, split, rows, y, st)
+               : mlp_layer0<InF32>(l, prm, L, obs_a, obs_b, split, rows, y, st);
+    } else {
+      rc = mlp_layer0<InF32>(l, prm, L, act[i - 1], act[i - 1], rows, rows, y, st);
+    }
+    if (rc != ACME_OK) return rc;
+  }
+  return ACME_OK;
+}
+
+// ---------------------------------------------------------------- backward helpers
+// Bias gradient = column sums of dZ [rows][n] (deterministic two-pass reduction).
+int bias_grad(acme_dqn* l, const float* dz, int64_t rows, int n, float* out, hipStream_t st) {
+  const int64_t chunks = std::min<int64_t>(ceil_div(rows, 256), l->colsum_floats / n);
+  return launch_colsum(dz, rows, n, (int)chunks, l->colsum, out, st);
+}
+
+int reduce_slab(const float* slab, int splits, int64_t count, float* out, hipStream_t st) {
+  return launch_slab_reduce(slab, splits, count, out, st);
+}
+
+template <class G, class In>
+int conv_wgrad(acme_dqn* l, const typename In::T* x, const float* dz, int batch, int splits,
+               float* dw, float* db, hipStream_t st) {
+  ConvWgrad<G, In> p;
+  p.M = G::K; p.N = G::CO; p.K = batch * G::OPIX; p.k_chunk = chunk_for(p.K, splits);
+  p.x = x; p.dz = dz; p.slab = l->slab;
+  if ((int64_t)splits * p.M * p.N > l->slab_floats) {
+    set_error("slab workspace too small");
+    return ACME_ERR_INVALID;
+  }
+  if (G::CO == 32) {
+    ACME_GEMM(64, 32, 2, 1, p, splits);
+  } else {
+    ACME_GEMM(64, 64, 2, 2, p, splits);
+  }
+  int rc = reduce_slab(l->slab, splits, (int64_t)p.M * p.N, dw, st);
+  if (rc != ACME_OK) return rc;
+  return bias_grad(l, dz, (int64_t)batch * G::OPIX, G::CO, db, st);
+}
+
+int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st) {
+  const float* prm = l->params;
+  float* gr = l->grads;
+  const int A = l->cfg.num_actions;
+  // Head: dZ of the fused hidden layer (masked by its ReLU) and head weight grads.
+  int rc = launch_duel_head_backward(l->hid, l->g, l->a_cache, B, kHidden, A, P(l, prm, l->t_vw),
+                                     P(l, prm, l->t_aw), l->dzh, Pm(l, gr, l->t_vw),
+                                     Pm(l, gr, l->t_vb), Pm(l, gr, l->t_aw), Pm(l, gr, l->t_ab), st);
+  if (rc != ACME_OK) return rc;
+  // FC weight grad: [7744, 1024] = x3^T dZh (reduction over the batch).
+  {
+    DenseWgrad<true> p;
+    p.M = kFlat; p.N = 2 * kHidden; p.K = B; p.k_chunk = B;
+    p.x = l->x3; p.ldx = kFlat; p.dz = l->dzh; p.out = Pm(l, gr, l->t_fcw);
+    ACME_GEMM(128, 128, 2, 2, p, 1);
+  }
+  if ((rc = bias_grad(l, l->dzh, B, 2 * kHidden, Pm(l, gr, l->t_fcb), st)) != ACME_OK) return rc;
+  // FC input grad -> dZ3 (masked by conv3's ReLU).
+  {
+    DenseDgrad<true> p;
+    p.M = B; p.N = kFlat; p.K = 2 * kHidden; p.k_chunk = p.K;
+    p.dz = l->dzh; p.w = P(l, prm, l->t_fcw); p.xprev = l->x3; p.ldx = kFlat; p.dx = l->dz3;
+    ACME_GEMM(64, 128, 2, 2, p, 1);
+  }
+  // conv3
+  if ((rc = conv_wgrad<G3, InF32>(l, l->x2, l->dz3, B, 64, Pm(l, gr, l->t_c3w),
+                                  Pm(l, gr, l->t_c3b), st)) != ACME_OK)
+    return rc;
+  {
+    ConvDgrad<G3> p;
+    p.M = B * G3::IPIX; p.N = G3::CI; p.K = G3::KH * G3::KW * G3::CO; p.k_chunk = p.K;
+    p.dz = l->dz3; p.w = P(l, prm, l->t_c3w); p.xprev = l->x2; p.dx = l->dz2;
+    ACME_GEMM(128, 64, 2, 2, p, 1);
+  }
+  // conv2
+  if ((rc = conv_wgrad<G2, InF32>(l, l->x1, l->dz2, B, 64, Pm(l, gr, l->t_c2w),
+                                  Pm(l, gr, l->t_c2b), st)) != ACME_OK)
+    return rc;
+  {
+    ConvDgrad<G2> p;
+    p.M = B * G2::IPIX; p.N = G2::CI; p.K = G2::KH * G2::KW * G2::CO; p.k_chunk = p.K;
+    p.dz = l->dz2; p.w = P(l, prm, l->t_c2w); p.xprev = l->x1; p.dx = l->dz1;
+    ACME_GEMM(256, 32, 4, 1, p, 1);
+  }
+  // conv1 (no input gradient needed)
+  if (l->cfg.obs_dtype == ACME_OBS_U8_SCALED) {
+    rc = conv_wgrad<G1, InU8>(l, static_cast<const uint8_t*>(o_tm1), l->dz1, B, 128,
+                              Pm(l, gr, l->t_c1w), Pm(l, gr, l->t_c1b), st);
+  } else {
+    rc = conv_wgrad<G1, InF32>(l, static_cast<const float*>(o_tm1), l->dz1, B, 128,
+                               Pm(l, gr, l->t_c1w), Pm(l, gr, l->t_c1b), st);
+  }
+  return rc;
+}
+
+template <class In>
+int mlp_wgrad(acme_dqn* l, const Layer& L, const void* x, const float* dz, int B, float* dw,
+              hipStream_t st) {
+  if (L.in % 4 == 0 && L.out % 4 == 0) {
+    DenseWgrad<true, In> p;
+    p.M = L.in; p.N = L.out; p.K = B; p.k_chunk = B;
+    p.x = static_cast<const typename In::T*>(x); p.ldx = L.in; p.dz = dz; p.out = dw;
+    ACME_GEMM(64, 64, 2, 2, p, 1);
+  } else {
+    DenseWgrad<false, In> p;
+    p.M = L.in; p.N = L.out; p.K = B; p.k_chunk = B;
+    p.x = static_cast<const typename In::T*>(x); p.ldx = L.in; p.dz = dz; p.out = dw;
+    ACME_GEMM(64, 64, 2, 2, p, 1);
+  }
+  return ACME_OK;
+}
+
+int mlp_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st) {
+  const int nl = (int)l->layers.size();
+  const float* prm = l->params;
+  float* gr = l->grads;
+  // dZ of the linear head: g_b at a_b.
+  int rc = launch_onehot_dq(l->g, l->a_cache, B, l->cfg.num_actions, l->mlp_dz[nl - 1], st);
+  if (rc != ACME_OK) return rc;
+  for (int i = nl - 1; i >= 0; --i) {
+    const Layer& L = l->layers[i];
+    const float* dz = l->mlp_dz[i];
+    if (i == 0) {
+      rc = l->cfg.obs_dtype == ACME_OBS_U8_SCALED
+               ? mlp_wgrad<InU8>(l, L, o_tm1, dz, B, Pm(l, gr, L.w), st)
+               : mlp_wgrad<InF32>(l, L, o_tm1, dz, B, Pm(l, gr, L.w), st);
+    } else {
+      rc = mlp_wgrad<InF32>(l, L, l->mlp_act[i - 1], dz, B, Pm(l, gr, L.w), st);
+    }
+    if (rc != ACME_OK) return rc;
+    if ((rc = bias_grad(l, dz, B, L.out, Pm(l, gr, L.b), st)) != ACME_OK) return rc;
+    if (i > 0) {
+      if (L.in % 4 == 0 && L.out % 4 == 0) {
+        DenseDgrad<true> p;
+        p.M = B; p.N = L.in; p.K = L.out; p.k_chunk = L.out;
+        p.dz = dz; p.w = P(l, prm, L.w); p.xprev = l->mlp_act[i - 1]; p.ldx = L.in;
+        p.dx = l->mlp_dz[i - 1];
+        ACME_GEMM(64, 64, 2, 2, p, 1);
+      } else {
+        DenseDgrad<false> p;
+        p.M = B; p.N = L.in; p.K = L.out; p.k_chunk = L.out;
+        p.dz = dz; p.w = P(l, prm, L.w); p.xprev = l->mlp_act[i - 1]; p.ldx = L.in;
+        p.dx = l->mlp_dz[i - 1];
+        ACME_GEMM(64, 64, 2, 2, p, 1);
+      }
+    }
+  }
+  return ACME_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
+  ACME_CHECK_ARG(cfg && out, "null argument");
+  ACME_CHECK_ARG(cfg->num_actions >= 1 && cfg->num_actions <= 63, "num_actions must be in [1, 63]");
+  ACME_CHECK_ARG(cfg->max_batch >= 1 && cfg->max_batch <= 65536, "max_batch must be in [1, 65536]");
+  ACME_CHECK_ARG(cfg->network == ACME_NET_NATURE_DQN || cfg->network == ACME_NET_MLP,
+                 "unknown network kind %d", cfg->network);
+  ACME_CHECK_ARG(cfg->obs_dtype == ACME_OBS_U8_SCALED || cfg->obs_dtype == ACME_OBS_F32,
+                 "unknown observation dtype %d", cfg->obs_dtype);
+  ACME_CHECK_ARG(cfg->huber_loss_parameter >= 0.f, "quadratic_linear_boundary must be >= 0.");
+  ACME_CHECK_ARG(cfg->target_update_period >= 1, "target_update_period must be >= 1");
+  acme_dqn* l = new acme_dqn();
+  l->cfg = *cfg;
+  const int A = cfg->num_actions;
+  const int B = cfg->max_batch;
+  int rc = ACME_OK;
+  auto fail = [&](int code) {
+    acme_dqn_destroy(l);
+    return code;
+  };
+  if (cfg->network == ACME_NET_NATURE_DQN) {
+    l->t_c1w = add_tensor(l, "atari_torso/conv2_d/w", {8, 8, 4, 32});
+    l->t_c1b = add_tensor(l, "atari_torso/conv2_d/b", {32});
+    l->t_c2w = add_tensor(l, "atari_torso/conv2_d_1/w", {4, 4, 32, 64});
+    l->t_c2b = add_tensor(l, "atari_torso/conv2_d_1/b", {64});
+    l->t_c3w = add_tensor(l, "atari_torso/conv2_d_2/w", {3, 3, 64, 64});
+    l->t_c3b = add_tensor(l, "atari_torso/conv2_d_2/b", {64});
+    // Fused [value_mlp/linear_0 | advantage_mlp/linear_0].
+    l->t_fcw = add_tensor(l, "duelling_q_network/hidden/w", {kFlat, 2 * kHidden});
+    l->t_fcb = add_tensor(l, "duelling_q_network/hidden/b", {2 * kHidden});
+    l->t_vw = add_tensor(l, "duelling_q_network/mlp/linear_1/w", {kHidden, 1});
+    l->t_vb = add_tensor(l, "duelling_q_network/mlp/linear_1/b", {1});
+    l->t_aw = add_tensor(l, "duelling_q_network/mlp_1/linear_1/w", {kHidden, A});
+    l->t_ab = add_tensor(l, "duelling_q_network/mlp_1/linear_1/b", {A});
+    const int R2 = 2 * B;
+    if ((rc = dev_alloc(l, &l->x1, (int64_t)R2 * G1::OPIX * G1::CO)) ||
+        (rc = dev_alloc(l, &l->x2, (int64_t)R2 * kFlat)) ||
+        (rc = dev_alloc(l, &l->x3, (int64_t)R2 * kFlat)) ||
+        (rc = dev_alloc(l, &l->hid, (int64_t)R2 * 2 * kHidden)) ||
+        (rc = dev_alloc(l, &l->t1, (int64_t)B * G1::OPIX * G1::CO)) ||
+        (rc = dev_alloc(l, &l->t2, (int64_t)B * kFlat)) ||
+        (rc = dev_alloc(l, &l->t3, (int64_t)B * kFlat)) ||
+        (rc = dev_alloc(l, &l->thid, (int64_t)B * 2 * kHidden)) ||
+        (rc = dev_alloc(l, &l->dzh, (int64_t)B * 2 * kHidden)) ||
+        (rc = dev_alloc(l, &l->dz3, (int64_t)B * kFlat)) ||
+        (rc = dev_alloc(l, &l->dz2, (int64_t)B * kFlat)) ||
+        (rc = dev_alloc(l, &l->dz1, (int64_t)B * G1::OPIX * G1::CO)))
+      return fail(rc);
+    l->slab_floats = std::max<int64_t>({128LL * G1::K * G1::CO, 64LL * G2::K * G2::CO,
+                                        64LL * G3::K * G3::CO});
+  } else {
+    ACME_CHECK_ARG(cfg->obs_dim >= 1, "obs_dim must be >= 1");
+    ACME_CHECK_ARG(cfg->num_hidden >= 0 && cfg->num_hidden <= ACME_MAX_MLP_LAYERS,
+                   "num_hidden must be in [0, %d]", ACME_MAX_MLP_LAYERS);
+    int in = cfg->obs_dim;
+    char name[64];
+    for (int i = 0; i <= cfg->num_hidden; ++i) {
+      Layer L;
+      L.in = in;
+      L.out = i < cfg->num_hidden ? cfg->hidden[i] : A;
+      L.relu = i < cfg->num_hidden;
+      if (L.out < 1) return fail((set_error("hidden sizes must be >= 1"), ACME_ERR_INVALID));
+      snprintf(name, sizeof(name), "mlp/linear_%d/w", i);
+      L.w = add_tensor(l, name, {L.in, L.out});
+      snprintf(name, sizeof(name), "mlp/linear_%d/b", i);
+      L.b = add_tensor(l, name, {L.out});
+      l->layers.push_back(L);
+      in = L.out;
+    }
+    for (size_t i = 0; i < l->layers.size(); ++i) {
+      float *a = nullptr, *ta = nullptr, *dz = nullptr;
+      const int w = l->layers[i].out;
+      if ((rc = dev_alloc(l, &a, (int64_t)2 * B * w)) || (rc = dev_alloc(l, &ta, (int64_t)B * w)) ||
+          (rc = dev_alloc(l, &dz, (int64_t)B * w)))
+        return fail(rc);
+      l->mlp_act.push_back(a);
+      l->mlp_tact.push_back(ta);
+      l->mlp_dz.push_back(dz);
+    }
+    l->slab_floats = 1;
+  }
+  l->colsum_floats = std::max<int64_t>(256LL * 1024, (int64_t)ceil_div(2LL * B * 441, 256) * 64);
+  if ((rc = dev_alloc(l, &l->q_on, (int64_t)2 * B * A)) ||
+      (rc = dev_alloc(l, &l->q_tg, (int64_t)B * A)) ||
+      (rc = dev_alloc(l, &l->slab, l->slab_floats)) ||
+      (rc = dev_alloc(l, &l->colsum, l->colsum_floats)) ||
+      (rc = dev_alloc(l, &l->g, (int64_t)B)) || (rc = dev_alloc(l, &l->a_cache, (int64_t)B)) ||
+      (rc = dev_alloc(l, &l->loss_tmp, 4)) || (rc = dev_alloc(l, &l->td_tmp, (int64_t)B)) ||
+      (rc = dev_alloc(l, &l->prio_tmp, (int64_t)B)))
+    return fail(rc);
+  *out = l;
+  return ACME_OK;
+}
+
+int acme_dqn_destroy(acme_dqn* l) {
+  if (!l) return ACME_OK;
+  (void)hipDeviceSynchronize();
+  for (void* p : l->allocs) (void)hipFree(p);
+  delete l;
+  return ACME_OK;
+}
+
+int64_t acme_dqn_num_params(const acme_dqn* l) { return l ? l->logical : 0; }
+int64_t acme_dqn_flat_size(const acme_dqn* l) { return l ? l->flat : 0; }
+int32_t acme_dqn_num_tensors(const acme_dqn* l) { return l ? (int32_t)l->tensors.size() : 0; }
+
+int acme_dqn_tensor_info(const acme_dqn* l, int32_t i, int64_t* offset, int64_t* numel,
+                         int32_t* ndim, int64_t* shape4, const char** name) {
+  ACME_CHECK_ARG(l && i >= 0 && i < (int32_t)l->tensors.size(), "tensor index out of range");
+  const Tensor& t = l->tensors[i];
+  if (offset) *offset = t.offset;
+  if (numel) *numel = t.numel;
+  if (ndim) *ndim = t.ndim;
+  if (shape4)
+    for (int k = 0; k < 4; ++k) shape4[k] = t.shape[k];
+  if (name) *name = t.name.c_str();
+  return ACME_OK;
+}
+
+int acme_dqn_bind(acme_dqn* l, float* params, float* target, float* grads, float* adam_m,
+                  float* adam_v) {
+  ACME_CHECK_ARG(l && params && target && grads && adam_m && adam_v, "null buffer");
+  for (const float* p : {params, target, grads, adam_m, adam_v})
+    ACME_CHECK_ARG(reinterpret_cast<uintptr_t>(p) % 16 == 0, "buffers must be 16-byte aligned");
+  l->params = params;
+  l->target = target;
+  l->grads = grads;
+  l->m = adam_m;
+  l->v = adam_v;
+  return ACME_OK;
+}
+
+int64_t acme_dqn_num_steps(const acme_dqn* l) { return l ? l->num_steps : 0; }
+int acme_dqn_set_num_steps(acme_dqn* l, int64_t n) {
+  ACME_CHECK_ARG(l && n >= 0, "bad argument");
+  l->num_steps = n;
+  return ACME_OK;
+}
+
+int acme_dqn_q_values(acme_dqn* l, const void* obs, int64_t batch, int32_t use_target,
+                      float* q_out, void* stream) {
+  ACME_CHECK_ARG(l && obs && q_out && l->params, "null argument or unbound learner");
+  ACME_CHECK_ARG(batch >= 1 && batch <= l->cfg.max_batch, "batch must be in [1, max_batch]");
+  hipStream_t st = as_stream(stream);
+  const float* prm = use_target ? l->target : l->params;
+  const int B = (int)batch;
+  if (l->cfg.network == ACME_NET_NATURE_DQN)
+    return nature_forward(l, prm, obs, obs, B, B, l->t1, l->t2, l->t3, l->thid, q_out, st);
+  return mlp_forward(l, prm, obs, obs, B, B, l->mlp_tact, q_out, st);
+}
+
+int acme_dqn_forward_backward(acme_dqn* l, const acme_transition_batch* batch,
+                              const acme_dqn_outputs* out, void* stream) {
+  ACME_CHECK_ARG(l && batch && l->params, "null argument or unbound learner");
+  ACME_CHECK_ARG(batch->o_tm1 && batch->a_tm1 && batch->r_t && batch->d_t && batch->o_t &&
+                     batch->probabilities,
+                 "transition batch has null fields");
+  ACME_CHECK_ARG(batch->batch >= 1 && batch->batch <= l->cfg.max_batch,
+                 "batch %lld outside [1, max_batch=%d]", (long long)batch->batch, l->cfg.max_batch);
+  hipStream_t st = as_stream(stream);
+  const int B = (int)batch->batch;
+  const int A = l->cfg.num_actions;
+  int rc;
+  ACME_HIP_TRY(hipMemsetAsync(l->grads, 0, l->flat * sizeof(float), st));
+  // Forward: online on [o_tm1; o_t] (q_tm1 rows 0..B-1, q_t_selector rows B..2B-1),
+  // target on o_t (q_t_value).
+  if (l->cfg.network == ACME_NET_NATURE_DQN) {
+    if ((rc = nature_forward(l, l->params, batch->o_tm1, batch->o_t, B, 2 * B, l->x1, l->x2, l->x3,
+                             l->hid, l->q_on, st)) != ACME_OK)
+      return rc;
+    if ((rc = nature_forward(l, l->target, batch->o_t, batch->o_t, B, B, l->t1, l->t2, l->t3,
+                             l->thid, l->q_tg, st)) != ACME_OK)
+      return rc;
+  } else {
+    if ((rc = mlp_forward(l, l->params, batch->o_tm1, batch->o_t, B, 2 * B, l->mlp_act, l->q_on,
+                          st)) != ACME_OK)
+      return rc;
+    if ((rc = mlp_forward(l, l->target, batch->o_t, batch->o_t, B, B, l->mlp_tact, l->q_tg, st)) !=
+        ACME_OK)
+      return rc;
+  }
+  float* loss = out && out->loss ? out->loss : l->loss_tmp;
+  float* td = out && out->td_error ? out->td_error : l->td_tmp;
+  double* prio = out && out->priorities ? out->priorities : l->prio_tmp;
+  LossArgs la;
+  la.q_on = l->q_on;
+  la.q_tg = l->q_tg;
+  la.a = batch->a_tm1;
+  la.r = batch->r_t;
+  la.d = batch->d_t;
+  la.probs = batch->probabilities;
+  la.global_min_prob = batch->global_min_probability;
+  la.B = B;
+  la.A = A;
+  la.discount = l->cfg.discount;
+  la.beta = l->cfg.importance_sampling_exponent;
+  la.delta = l->cfg.huber_loss_parameter;
+  la.max_abs_reward = l->cfg.max_abs_reward;
+  la.loss = loss;
+  la.td = td;
+  la.prio = prio;
+  la.g = l->g;
+  la.a_cache = l->a_cache;
+  if ((rc = launch_dqn_loss(la, st)) != ACME_OK) return rc;
+  if (out && out->q_tm1)
+    ACME_HIP_TRY(hipMemcpyAsync(out->q_tm1, l->q_on, (size_t)B * A * sizeof(float),
+                                hipMemcpyDeviceToDevice, st));
+  return l->cfg.network == ACME_NET_NATURE_DQN ? nature_backward(l, batch->o_tm1, B, st)
+                                               : mlp_backward(l, batch->o_tm1, B, st);
+}
+
+int acme_dqn_apply(acme_dqn* l, void* stream) {
+  ACME_CHECK_ARG(l && l->params, "unbound learner");
+  hipStream_t st = as_stream(stream);
+  const int64_t t = l->num_steps + 1;  // snt.Adam increments its step before the update
+  int rc = acme_adam_update(l->params, l->grads, l->m, l->v, l->flat, l->cfg.learning_rate,
+                            l->cfg.adam_beta1, l->cfg.adam_beta2, l->cfg.adam_epsilon, t, stream);
+  if (rc != ACME_OK) return rc;
+  if (l->num_steps % l->cfg.target_update_period == 0)
+    ACME_HIP_TRY(hipMemcpyAsync(l->target, l->params, l->flat * sizeof(float),
+                                hipMemcpyDeviceToDevice, st));
+  l->num_steps += 1;
+  return ACME_OK;
+}
+
+int acme_dqn_step(acme_dqn* l, const acme_transition_batch* batch, const acme_dqn_outputs* out,
+                  void* stream) {
+  int rc = acme_dqn_forward_backward(l, batch, out, stream);
+  if (rc != ACME_OK) return rc;
+  return acme_dqn_apply(l, stream);
+}
+
+}  // extern "C"

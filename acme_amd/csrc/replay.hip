@@ -1,0 +1,648 @@
+// GPU-resident replay table: the MI355X replacement for the Reverb table the agents
+// build (acme/agents/tf/dqn/agent.py:95-102, acme/agents/tf/d4pg/agent.py:96-102).
+//
+// Layout in HBM (one hipMalloc per array, struct-of-arrays):
+//   field[f]     [capacity, field_bytes[f]]   item payloads (u8 Atari frames, f32 ...)
+//   keys         [capacity] u64               key of the item in each ring slot
+//   raw_prio     [capacity] f64               priority as given by adder / learner
+//   level[0]     [S0] f64                     sum-tree leaves = raw_prio^alpha
+//   level[l]     [S_l] f64                    64-ary sum tree: level[l][j] =
+//                                             wave_scan_total(level[l-1][64j..64j+63])
+// S0 = roundup(capacity, 64); S_{l+1} = roundup(S_l / 64, 64) until S_l == 64 (the top
+// level has exactly 64 entries; the root total is recomputed by the sampling wave).
+//
+// The fan-out is the wavefront width: one wave reads the 64 children of a node in one
+// coalesced 512-B load, prefix-sums them with a 6-step shuffle scan, and picks the child
+// with a ballot.  A 1 M-slot table is 4 levels, so a draw is 4 dependent 512-B reads
+// instead of the 20 dependent 8-B reads of a binary tree.
+//
+// Sampling (Reverb Prioritized(alpha)): target t = u * total, u = Philox4x32-10 53-bit
+// uniform of counter (j, step); descend choosing the first child whose inclusive prefix
+// exceeds t.  Uniform(): slot = floor(u * size).  FIFO remover: slot = key % capacity.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "common.h"
+#include "detmath.h"
+
+using namespace acme;
+
+struct acme_replay {
+  acme_replay_config cfg;
+  int nlevels = 0;
+  int64_t level_size[8] = {};
+  double* levels[8] = {};
+  double* raw_prio = nullptr;
+  uint64_t* keys = nullptr;
+  int32_t* winner = nullptr;  // per-slot scratch for last-wins priority updates
+  int64_t* upd_slots = nullptr;  // per-update scratch (resolved slot)
+  int32_t* upd_valid = nullptr;  // per-update scratch (key still present)
+  int64_t upd_cap = 0;
+  uint8_t* fields[ACME_MAX_FIELDS] = {};
+  int64_t inserted = 0;  // total items ever inserted (host side; = next key)
+  std::mutex mu;
+};
+
+namespace {
+
+// Inclusive Hillis-Steele scan over the 64 lanes of a wave, f64.  The order of the
+// additions is fixed (round d adds the value d lanes below), which the oracle
+// restates exactly (oracle/replay_oracle.c: wave_scan64).
+__device__ __forceinline__ double wave_scan64(double x) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    double y = __shfl_up(x, d, 64);
+    if (lane >= d) x = y + x;
+  }
+  return x;
+}
+
+__device__ __forceinline__ int select_child(double v, double s, double t) {
+  const uint64_t le = __ballot(s <= t);
+  const uint64_t nz = __ballot(v > 0.0);
+  int idx = __popcll(le);
+  const int last = nz ? 63 - __clzll(nz) : 0;
+  if (idx > last) idx = last;
+  return idx;
+}
+
+// One wave per draw.  levels passed top-first in a small struct by value.
+struct TreeView {
+  const double* level[8];
+  int nlevels;
+};
+
+__global__ void __launch_bounds__(256) sample_prioritized_kernel(
+    TreeView tree, const double* __restrict__ raw_prio, const uint64_t* __restrict__ keys,
+    int64_t batch, int64_t size, uint64_t seed, uint64_t step, int64_t* out_slots,
+    uint64_t* out_keys, double* out_probs, int64_t* out_size, double* out_prio) {
+  const int lane = threadIdx.x & 63;
+  const int64_t j = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (j >= batch) return;  // wave-uniform
+  const double u = sample_uniform(seed, step, (uint32_t)j);
+
+  int64_t node = 0;
+  double t = 0.0, total = 0.0, leaf_value = 0.0;
+  for (int l = tree.nlevels - 1; l >= 0; --l) {
+    const int64_t base = node * 64;
+    const double v = tree.level[l][base + lane];
+    const double s = wave_scan64(v);
+    if (l == tree.nlevels - 1) {
+      total = __shfl(s, 63, 64);
+      if (!(total > 0.0)) break;
+      t = u * total;
+    }
+    const int idx = select_child(v, s, t);
+    const double excl = idx > 0 ? __shfl(s, idx - 1, 64) : 0.0;
+    leaf_value = __shfl(v, idx, 64);
+    t = t - excl;
+    node = base + idx;
+  }
+  int64_t slot;
+  double prob;
+  if (!(total > 0.0)) {  // every priority is zero: uniform fallback
+    slot = (int64_t)(u * (double)size);
+    if (slot >= size) slot = size - 1;
+    prob = 1.0 / (double)size;
+  } else {
+    slot = node;
+    prob = leaf_value / total;
+  }
+  if (lane == 0) {
+    out_slots[j] = slot;
+    if (out_keys) out_keys[j] = keys[slot];
+    if (out_probs) out_probs[j] = prob;
+    if (out_size) out_size[j] = size;
+    if (out_prio) out_prio[j] = raw_prio[slot];
+  }
+}
+
+__global__ void sample_uniform_kernel(const double* __restrict__ raw_prio,
+                                      const uint64_t* __restrict__ keys, int64_t batch,
+                                      int64_t size, uint64_t seed, uint64_t step,
+                                      int64_t* out_slots, uint64_t* out_keys,
+                                      double* out_probs, int64_t* out_size,
+                                      double* out_prio) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= batch) return;
+  const double u = sample_uniform(seed, step, (uint32_t)j);
+  int64_t slot = (int64_t)(u * (double)size);
+  if (slot >= size) slot = size - 1;
+  out_slots[j] = slot;
+  if (out_keys) out_keys[j] = keys[slot];
+  if (out_probs) out_probs[j] = 1.0 / (double)size;
+  if (out_size) out_size[j] = size;
+  if (out_prio) out_prio[j] = raw_prio[slot];
+}
+
+// Row gather for wide fields: one workgroup per (row, field); 16-B vector copies.
+struct GatherArgs {
+  const uint8_t* src[ACME_MAX_FIELDS];
+  uint8_t* dst[ACME_MAX_FIELDS];
+  int64_t bytes[ACME_MAX_FIELDS];
+};
+
+__global__ void __launch_bounds__(256) gather_wide_kernel(GatherArgs g,
+                                                          const int64_t* __restrict__ slots,
+                                                          int field0) {
+  const int f = field0 + blockIdx.y;
+  const int64_t row = blockIdx.x;
+  const int64_t slot = slots[row];
+  const int64_t nvec = g.bytes[f] >> 4;
+  const uint4* __restrict__ s = reinterpret_cast<const uint4*>(g.src[f] + slot * g.bytes[f]);
+  uint4* __restrict__ d = reinterpret_cast<uint4*>(g.dst[f] + row * g.bytes[f]);
+  // Issue all loads of this thread before the stores (ILP: up to 8 in flight).
+  for (int64_t i0 = threadIdx.x; i0 < nvec; i0 += 8 * blockDim.x) {
+    uint4 r[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int64_t i = i0 + (int64_t)k * blockDim.x;
+      if (i < nvec) r[k] = s[i];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int64_t i = i0 + (int64_t)k * blockDim.x;
+      if (i < nvec) d[i] = r[k];
+    }
+  }
+}
+
+// Narrow fields (4..15 B per row, multiples of 4): one thread per 4-byte word.
+__global__ void gather_narrow_kernel(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                                     const int64_t* __restrict__ slots, int64_t batch,
+                                     int64_t words) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= batch * words) return;
+  const int64_t row = i / words, w = i - row * words;
+  dst[i] = src[slots[row] * words + w];
+}
+
+// Recompute level[l] nodes from their 64 children (one wave per node).
+// Mode A: contiguous node range [node_begin, node_begin + count).
+// Mode B: node = slots[j] >> (6 l) for j < count (duplicates recompute identically).
+__global__ void __launch_bounds__(256) level_update_kernel(
+    const double* __restrict__ child, double* __restrict__ parent, int64_t node_begin,
+    int64_t count, const int64_t* __restrict__ slots, const int32_t* __restrict__ valid,
+    int shift) {
+  const int lane = threadIdx.x & 63;
+  const int64_t j = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (j >= count) return;
+  int64_t node;
+  if (slots) {
+    if (valid && !valid[j]) return;
+    node = slots[j] >> shift;
+  } else {
+    node = node_begin + j;
+  }
+  const double v = child[node * 64 + lane];
+  const double s = wave_scan64(v);
+  if (lane == 63) parent[node] = s;
+}
+
+// Priority updates from the learner (device keys).  Pass 1: resolve slots, check the
+// key still lives in its slot, and elect the LAST update of each slot with atomicMax.
+__global__ void prio_resolve_kernel(const uint64_t* __restrict__ upd_keys, int64_t n,
+                                    const uint64_t* __restrict__ keys, int64_t capacity,
+                                    int64_t* __restrict__ out_slots,
+                                    int32_t* __restrict__ valid, int32_t* __restrict__ winner) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint64_t k = upd_keys[j];
+  const int64_t slot = (int64_t)(k % (uint64_t)capacity);
+  const int ok = keys[slot] == k;
+  out_slots[j] = slot;
+  valid[j] = ok;
+  if (ok) atomicMax(&winner[slot], (int32_t)j);
+}
+
+// Pass 2: the elected update writes raw priority and leaf = p^alpha.
+__global__ void prio_write_kernel(const double* __restrict__ prios, int64_t n,
+                                  const int64_t* __restrict__ slots,
+                                  const int32_t* __restrict__ valid,
+                                  const int32_t* __restrict__ winner, double alpha,
+                                  double* __restrict__ raw_prio, double* __restrict__ leaves) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n || !valid[j]) return;
+  const int64_t slot = slots[j];
+  if (winner[slot] != (int32_t)j) return;
+  const double p = prios[j];
+  raw_prio[slot] = p;
+  leaves[slot] = det_pow_priority(p, alpha);
+}
+
+// Pass 3 (after all writes): reset the election scratch.
+__global__ void prio_reset_kernel(const int64_t* __restrict__ slots,
+                                  const int32_t* __restrict__ valid, int64_t n,
+                                  int32_t* __restrict__ winner) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n || !valid[j]) return;
+  winner[slots[j]] = -1;
+}
+
+__global__ void fill_i32_kernel(int32_t* p, int64_t n, int32_t v) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+// Synthetic item generator (bench / tests): Philox stream per 16-B chunk.
+__device__ __forceinline__ u32x4 fill_rand(uint64_t seed, uint64_t item, uint32_t chunk,
+                                          uint32_t field) {
+  u32x4 c = {chunk, (uint32_t)item, (uint32_t)(item >> 32) ^ (field << 24), kFillTag};
+  return philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+__global__ void __launch_bounds__(256) fill_bytes_kernel(uint8_t* __restrict__ field,
+                                                         int64_t row_bytes, int64_t capacity,
+                                                         int64_t first_key, int64_t n,
+                                                         uint64_t seed, uint32_t field_id) {
+  const int64_t nvec = row_bytes >> 4;
+  const int64_t total = n * nvec;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t item = i / nvec, v = i - item * nvec;
+    const int64_t key = first_key + item;
+    const int64_t slot = key % capacity;
+    const u32x4 r = fill_rand(seed, (uint64_t)key, (uint32_t)v, field_id);
+    uint4 w = {r.x, r.y, r.z, r.w};
+    reinterpret_cast<uint4*>(field + slot * row_bytes)[v] = w;
+  }
+}
+
+__global__ void fill_f32_normal_kernel(float* __restrict__ field, int64_t row_floats,
+                                       int64_t capacity, int64_t first_key, int64_t n,
+                                       uint64_t seed, uint32_t field_id, float lo, float hi,
+                                       int uniform) {
+  const int64_t total = n * row_floats;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t item = i / row_floats, c = i - item * row_floats;
+    const int64_t key = first_key + item;
+    const u32x4 r = fill_rand(seed, (uint64_t)key, (uint32_t)c, field_id);
+    const double u1 = u01_53(r.x, r.y), u2 = u01_53(r.z, r.w);
+    float x;
+    if (uniform) {
+      x = lo + (hi - lo) * (float)u1;
+    } else {
+      x = (float)(sqrt(-2.0 * log(1.0 - u1)) * cos(6.283185307179586 * u2));
+    }
+    field[(key % capacity) * row_floats + c] = x;
+  }
+}
+
+// Scalar fields of the synthetic transition (action, reward, discount) + keys/prio.
+__global__ void fill_scalars_kernel(int32_t* __restrict__ action, float* __restrict__ reward,
+                                    float* __restrict__ discount, int reward_uniform,
+                                    float p_zero_discount, float nonzero_discount,
+                                    int32_t num_actions, int64_t capacity, int64_t first_key,
+                                    int64_t n, uint64_t seed, uint64_t* __restrict__ keys,
+                                    double* __restrict__ raw_prio, double* __restrict__ leaves) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t key = first_key + i;
+  const int64_t slot = key % capacity;
+  const u32x4 r = fill_rand(seed, (uint64_t)key, 0xFFFFu, 0xFFu);
+  if (action) action[slot] = (int32_t)(r.x % (uint32_t)num_actions);
+  const double u1 = u01_53(r.y, r.z);
+  const double u2 = u01_53(r.w, r.x);
+  if (reward_uniform) {
+    reward[slot] = (float)(5.0 * u1);
+  } else {
+    reward[slot] = (float)(sqrt(-2.0 * log(1.0 - u1)) * cos(6.283185307179586 * u2));
+  }
+  const double u3 = u01_53(r.z ^ 0x9E3779B9u, r.w ^ 0x7F4A7C15u);
+  discount[slot] = u3 < (double)p_zero_discount ? 0.0f : nonzero_discount;
+  keys[slot] = (uint64_t)key;
+  raw_prio[slot] = 1.0;
+  leaves[slot] = 1.0;
+}
+
+// Recompute all internal levels over the slot range touched by an insert.
+int refresh_range(acme_replay* r, int64_t first_key, int64_t n, hipStream_t st) {
+  const int64_t C = r->cfg.capacity;
+  if (n <= 0) return ACME_OK;
+  if (n > C) {
+    first_key += n - C;
+    n = C;
+  }
+  const int64_t s0 = first_key % C;
+  // Up to two contiguous slot segments.
+  int64_t seg_begin[2] = {s0, 0};
+  int64_t seg_len[2] = {std::min(n, C - s0), n - std::min(n, C - s0)};
+  for (int l = 1; l < r->nlevels; ++l) {
+    const int shift = 6 * l;
+    for (int s = 0; s < 2; ++s) {
+      if (seg_len[s] <= 0) continue;
+      const int64_t nb = seg_begin[s] >> shift;
+      const int64_t ne = (seg_begin[s] + seg_len[s] - 1) >> shift;
+      const int64_t count = ne - nb + 1;
+      level_update_kernel<<<(unsigned)ceil_div(count, 4), 256, 0, st>>>(
+          r->levels[l - 1], r->levels[l], nb, count, nullptr, nullptr, 0);
+      ACME_LAUNCH_CHECK();
+    }
+  }
+  return ACME_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int acme_replay_create(const acme_replay_config* cfg, acme_replay** out) {
+  ACME_CHECK_ARG(cfg && out, "null argument");
+  ACME_CHECK_ARG(cfg->capacity > 0 && cfg->capacity < (int64_t(1) << 40),
+                 "capacity must be in [1, 2^40), got %lld", (long long)cfg->capacity);
+  ACME_CHECK_ARG(cfg->sampler == ACME_SAMPLER_UNIFORM || cfg->sampler == ACME_SAMPLER_PRIORITIZED,
+                 "unknown sampler %d", cfg->sampler);
+  ACME_CHECK_ARG(cfg->num_fields >= 0 && cfg->num_fields <= ACME_MAX_FIELDS,
+                 "num_fields must be in [0, %d]", ACME_MAX_FIELDS);
+  ACME_CHECK_ARG(cfg->priority_exponent >= 0.0, "priority_exponent must be >= 0");
+  for (int f = 0; f < cfg->num_fields; ++f)
+    ACME_CHECK_ARG(cfg->field_bytes[f] > 0 && cfg->field_bytes[f] % 4 == 0,
+                   "field %d: bytes per item must be a positive multiple of 4", f);
+
+  acme_replay* r = new acme_replay();
+  r->cfg = *cfg;
+  // Level sizes.
+  int64_t s = ceil_div(cfg->capacity, 64) * 64;
+  r->level_size[0] = s;
+  r->nlevels = 1;
+  while (s > 64) {
+    s = ceil_div(s / 64, 64) * 64;
+    r->level_size[r->nlevels++] = s;
+  }
+  auto fail = [&](const char* what) {
+    acme_replay_destroy(r);
+    set_error("hipMalloc failed for %s", what);
+    return ACME_ERR_OOM;
+  };
+  for (int l = 0; l < r->nlevels; ++l) {
+    if (hipMalloc(&r->levels[l], r->level_size[l] * sizeof(double)) != hipSuccess)
+      return fail("sum tree");
+    if (hipMemset(r->levels[l], 0, r->level_size[l] * sizeof(double)) != hipSuccess)
+      return fail("sum tree memset");
+  }
+  if (hipMalloc(&r->raw_prio, cfg->capacity * sizeof(double)) != hipSuccess) return fail("prio");
+  if (hipMalloc(&r->keys, cfg->capacity * sizeof(uint64_t)) != hipSuccess) return fail("keys");
+  if (hipMalloc(&r->winner, cfg->capacity * sizeof(int32_t)) != hipSuccess) return fail("winner");
+  (void)hipMemset(r->raw_prio, 0, cfg->capacity * sizeof(double));
+  // Keys of never-written slots must not match any real key: fill with all-ones.
+  (void)hipMemset(r->keys, 0xFF, cfg->capacity * sizeof(uint64_t));
+  fill_i32_kernel<<<(unsigned)ceil_div(cfg->capacity, 256), 256>>>(r->winner, cfg->capacity, -1);
+  for (int f = 0; f < cfg->num_fields; ++f) {
+    if (hipMalloc(&r->fields[f], cfg->capacity * cfg->field_bytes[f]) != hipSuccess)
+      return fail("field storage");
+  }
+  if (hipDeviceSynchronize() != hipSuccess) return fail("init sync");
+  *out = r;
+  return ACME_OK;
+}
+
+int acme_replay_destroy(acme_replay* r) {
+  if (!r) return ACME_OK;
+  (void)hipDeviceSynchronize();
+  for (int l = 0; l < 8; ++l)
+    if (r->levels[l]) (void)hipFree(r->levels[l]);
+  if (r->raw_prio) (void)hipFree(r->raw_prio);
+  if (r->keys) (void)hipFree(r->keys);
+  if (r->winner) (void)hipFree(r->winner);
+  if (r->upd_slots) (void)hipFree(r->upd_slots);
+  if (r->upd_valid) (void)hipFree(r->upd_valid);
+  for (int f = 0; f < ACME_MAX_FIELDS; ++f)
+    if (r->fields[f]) (void)hipFree(r->fields[f]);
+  delete r;
+  return ACME_OK;
+}
+
+int64_t acme_replay_size(const acme_replay* r) {
+  if (!r) return 0;
+  return std::min(r->inserted, r->cfg.capacity);
+}
+
+int64_t acme_replay_capacity(const acme_replay* r) { return r ? r->cfg.capacity : 0; }
+
+int acme_replay_debug_leaves(const acme_replay* r, const double** leaf_values,
+                             const double** raw_priorities, const uint64_t** keys) {
+  ACME_CHECK_ARG(r, "null replay");
+  if (leaf_values) *leaf_values = r->levels[0];
+  if (raw_priorities) *raw_priorities = r->raw_prio;
+  if (keys) *keys = r->keys;
+  return ACME_OK;
+}
+
+int acme_replay_insert(acme_replay* r, const void* const* fields, int64_t n,
+                       const double* priorities, int32_t src_on_device, uint64_t* out_keys,
+                       void* stream) {
+  ACME_CHECK_ARG(r && (n == 0 || fields), "null argument");
+  ACME_CHECK_ARG(n >= 0, "negative item count");
+  if (n == 0) return ACME_OK;
+  std::lock_guard<std::mutex> lock(r->mu);
+  hipStream_t st = as_stream(stream);
+  const int64_t C = r->cfg.capacity;
+  const int64_t first_key = r->inserted;
+  // Host-side metadata: keys, raw priorities, leaf weights (same det_pow code as device).
+  std::vector<uint64_t> hkeys(n);
+  std::vector<double> hprio(n), hleaf(n);
+  for (int64_t i = 0; i < n; ++i) {
+    hkeys[i] = (uint64_t)(first_key + i);
+    const double p = priorities ? priorities[i] : 1.0;
+    if (!(p >= 0.0)) {
+      set_error("priority %g at item %lld must be >= 0", p, (long long)i);
+      return ACME_ERR_INVALID;
+    }
+    hprio[i] = p;
+    hleaf[i] = r->cfg.sampler == ACME_SAMPLER_PRIORITIZED
+                   ? det_pow_priority(p, r->cfg.priority_exponent)
+                   : 1.0;
+  }
+  if (out_keys) std::memcpy(out_keys, hkeys.data(), n * sizeof(uint64_t));
+  // Only the last C items survive an over-capacity insert.
+  int64_t skip = n > C ? n - C : 0;
+  int64_t done = skip;
+  const hipMemcpyKind kind = src_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+  while (done < n) {
+    const int64_t slot = (first_key + done) % C;
+    const int64_t len = std::min(n - done, C - slot);
+    for (int f = 0; f < r->cfg.num_fields; ++f) {
+      const int64_t b = r->cfg.field_bytes[f];
+      const uint8_t* src = static_cast<const uint8_t*>(fields[f]) + done * b;
+      ACME_HIP_TRY(hipMemcpyAsync(r->fields[f] + slot * b, src, len * b, kind, st));
+    }
+    ACME_HIP_TRY(hipMemcpyAsync(r->keys + slot, hkeys.data() + done, len * sizeof(uint64_t),
+                                hipMemcpyHostToDevice, st));
+    ACME_HIP_TRY(hipMemcpyAsync(r->raw_prio + slot, hprio.data() + done, len * sizeof(double),
+                                hipMemcpyHostToDevice, st));
+    ACME_HIP_TRY(hipMemcpyAsync(r->levels[0] + slot, hleaf.data() + done, len * sizeof(double),
+                                hipMemcpyHostToDevice, st));
+    done += len;
+  }
+  int rc = refresh_range(r, first_key, n, st);
+  if (rc != ACME_OK) return rc;
+  // The host vectors above are pageable: make sure the copies have consumed them.
+  ACME_HIP_TRY(hipStreamSynchronize(st));
+  r->inserted += n;
+  return ACME_OK;
+}
+
+int acme_replay_fill_synthetic(acme_replay* r, int64_t n, int32_t layout, int32_t num_actions,
+                               uint64_t seed, void* stream) {
+  ACME_CHECK_ARG(r, "null replay");
+  ACME_CHECK_ARG(n >= 0, "negative count");
+  ACME_CHECK_ARG(layout == 0 || layout == 1, "unknown synthetic layout %d", layout);
+  ACME_CHECK_ARG(r->cfg.num_fields == 5, "synthetic transitions need 5 fields");
+  ACME_CHECK_ARG((layout == 1 || r->cfg.field_bytes[1] == 4) && r->cfg.field_bytes[2] == 4 &&
+                     r->cfg.field_bytes[3] == 4,
+                 "field layout does not match a transition (o, a, r, d, o_t)");
+  ACME_CHECK_ARG(layout == 1 || num_actions > 0, "num_actions must be > 0");
+  if (n == 0) return ACME_OK;
+  std::lock_guard<std::mutex> lock(r->mu);
+  hipStream_t st = as_stream(stream);
+  const int64_t C = r->cfg.capacity;
+  const int64_t first_key = r->inserted;
+  int64_t skip = n > C ? n - C : 0;
+  const int64_t k0 = first_key + skip, cnt = n - skip;
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(cnt * 64, 256), 8192);
+  if (layout == 0) {
+    ACME_CHECK_ARG(r->cfg.field_bytes[0] % 16 == 0 && r->cfg.field_bytes[4] == r->cfg.field_bytes[0],
+                   "Atari observation rows must be equal multiples of 16 bytes");
+    for (int f : {0, 4}) {
+      fill_bytes_kernel<<<grid, 256, 0, st>>>(r->fields[f], r->cfg.field_bytes[f], C, k0, cnt,
+                                              seed, (uint32_t)f);
+      ACME_LAUNCH_CHECK();
+    }
+    // Discount: 0.99^4 (n = 5 with agent discount applied n-1 times by the adder).
+    const float d4 = 0.99f * 0.99f * 0.99f * 0.99f;
+    fill_scalars_kernel<<<(unsigned)ceil_div(cnt, 256), 256, 0, st>>>(
+        reinterpret_cast<int32_t*>(r->fields[1]), reinterpret_cast<float*>(r->fields[2]),
+        reinterpret_cast<float*>(r->fields[3]), 0, 0.01f, d4, num_actions, C, k0, cnt, seed,
+        r->keys, r->raw_prio, r->levels[0]);
+    ACME_LAUNCH_CHECK();
+  } else {
+    fill_f32_normal_kernel<<<grid, 256, 0, st>>>(reinterpret_cast<float*>(r->fields[0]),
+                                                 r->cfg.field_bytes[0] / 4, C, k0, cnt, seed, 0,
+                                                 0.f, 0.f, 0);
+    ACME_LAUNCH_CHECK();
+    fill_f32_normal_kernel<<<grid, 256, 0, st>>>(reinterpret_cast<float*>(r->fields[1]),
+                                                 r->cfg.field_bytes[1] / 4, C, k0, cnt, seed, 1,
+                                                 -1.f, 1.f, 1);
+    ACME_LAUNCH_CHECK();
+    fill_f32_normal_kernel<<<grid, 256, 0, st>>>(reinterpret_cast<float*>(r->fields[4]),
+                                                 r->cfg.field_bytes[4] / 4, C, k0, cnt, seed, 4,
+                                                 0.f, 0.f, 0);
+    ACME_LAUNCH_CHECK();
+    const float d4 = 0.99f * 0.99f * 0.99f * 0.99f;
+    fill_scalars_kernel<<<(unsigned)ceil_div(cnt, 256), 256, 0, st>>>(
+        nullptr, reinterpret_cast<float*>(r->fields[2]), reinterpret_cast<float*>(r->fields[3]),
+        1, 0.001f, d4, 1, C, k0, cnt, seed, r->keys, r->raw_prio, r->levels[0]);
+    ACME_LAUNCH_CHECK();
+  }
+  int rc = refresh_range(r, k0, cnt, st);
+  if (rc != ACME_OK) return rc;
+  r->inserted += n;
+  return ACME_OK;
+}
+
+int acme_replay_sample(acme_replay* r, int64_t batch, uint64_t step_counter, int64_t* slots,
+                       uint64_t* keys, double* probabilities, int64_t* table_size,
+                       double* priorities, void* stream) {
+  ACME_CHECK_ARG(r && slots, "null argument");
+  ACME_CHECK_ARG(batch > 0 && batch <= (int64_t(1) << 31), "batch must be in [1, 2^31]");
+  const int64_t size = acme_replay_size(r);
+  if (size <= 0) {
+    set_error("cannot sample from an empty table (rate limiter MinSize(1))");
+    return ACME_ERR_EMPTY;
+  }
+  hipStream_t st = as_stream(stream);
+  if (r->cfg.sampler == ACME_SAMPLER_PRIORITIZED) {
+    TreeView tv;
+    for (int l = 0; l < 8; ++l) tv.level[l] = r->levels[l];
+    tv.nlevels = r->nlevels;
+    sample_prioritized_kernel<<<(unsigned)ceil_div(batch, 4), 256, 0, st>>>(
+        tv, r->raw_prio, r->keys, batch, size, r->cfg.seed, step_counter, slots, keys,
+        probabilities, table_size, priorities);
+  } else {
+    sample_uniform_kernel<<<(unsigned)ceil_div(batch, 256), 256, 0, st>>>(
+        r->raw_prio, r->keys, batch, size, r->cfg.seed, step_counter, slots, keys,
+        probabilities, table_size, priorities);
+  }
+  ACME_LAUNCH_CHECK();
+  return ACME_OK;
+}
+
+int acme_replay_gather(acme_replay* r, const int64_t* slots, int64_t batch,
+                       void* const* out_fields, void* stream) {
+  ACME_CHECK_ARG(r && slots && out_fields, "null argument");
+  ACME_CHECK_ARG(batch > 0 && batch < (int64_t(1) << 31), "bad batch");
+  hipStream_t st = as_stream(stream);
+  GatherArgs g = {};
+  for (int f = 0; f < r->cfg.num_fields; ++f) {
+    g.src[f] = r->fields[f];
+    g.dst[f] = static_cast<uint8_t*>(out_fields[f]);
+    g.bytes[f] = r->cfg.field_bytes[f];
+  }
+  // Wide (16-B multiple, >= 64 B) fields: one workgroup per row; consecutive wide
+  // fields with the same row size share one launch (gridDim.y = field).
+  int f = 0;
+  while (f < r->cfg.num_fields) {
+    const int64_t b = g.bytes[f];
+    const bool wide = b >= 64 && b % 16 == 0 &&
+                      (reinterpret_cast<uintptr_t>(g.dst[f]) % 16) == 0;
+    if (wide) {
+      gather_wide_kernel<<<dim3((unsigned)batch, 1), 256, 0, st>>>(g, slots, f);
+    } else {
+      const int64_t words = b / 4;
+      gather_narrow_kernel<<<(unsigned)ceil_div(batch * words, 256), 256, 0, st>>>(
+          reinterpret_cast<const uint32_t*>(g.src[f]), reinterpret_cast<uint32_t*>(g.dst[f]),
+          slots, batch, words);
+    }
+    ACME_LAUNCH_CHECK();
+    ++f;
+  }
+  return ACME_OK;
+}
+
+int acme_replay_update_priorities(acme_replay* r, const uint64_t* keys, const double* prios,
+                                  int64_t n, void* stream) {
+  ACME_CHECK_ARG(r && (n == 0 || (keys && prios)), "null argument");
+  ACME_CHECK_ARG(n >= 0 && n < (int64_t(1) << 31), "bad update count");
+  if (n == 0) return ACME_OK;
+  hipStream_t st = as_stream(stream);
+  std::lock_guard<std::mutex> lock(r->mu);
+  // Scratch for resolved slots / validity (grown on demand; growth drains the device).
+  if (n > r->upd_cap) {
+    if (r->upd_slots) {
+      ACME_HIP_TRY(hipDeviceSynchronize());
+      (void)hipFree(r->upd_slots);
+      (void)hipFree(r->upd_valid);
+    }
+    r->upd_cap = std::max<int64_t>(n, 4096);
+    ACME_HIP_TRY(hipMalloc(&r->upd_slots, r->upd_cap * sizeof(int64_t)));
+    ACME_HIP_TRY(hipMalloc(&r->upd_valid, r->upd_cap * sizeof(int32_t)));
+  }
+  int64_t* t_slots = r->upd_slots;
+  int32_t* t_valid = r->upd_valid;
+  const unsigned g = (unsigned)ceil_div(n, 256);
+  const double alpha =
+      r->cfg.sampler == ACME_SAMPLER_PRIORITIZED ? r->cfg.priority_exponent : 0.0;
+  prio_resolve_kernel<<<g, 256, 0, st>>>(keys, n, r->keys, r->cfg.capacity, t_slots, t_valid,
+                                         r->winner);
+  ACME_LAUNCH_CHECK();
+  prio_write_kernel<<<g, 256, 0, st>>>(prios, n, t_slots, t_valid, r->winner, alpha,
+                                       r->raw_prio, r->levels[0]);
+  ACME_LAUNCH_CHECK();
+  for (int l = 1; l < r->nlevels; ++l) {
+    level_update_kernel<<<(unsigned)ceil_div(n, 4), 256, 0, st>>>(
+        r->levels[l - 1], r->levels[l], 0, n, t_slots, t_valid, 6 * l);
+    ACME_LAUNCH_CHECK();
+  }
+  prio_reset_kernel<<<g, 256, 0, st>>>(t_slots, t_valid, n, r->winner);
+  ACME_LAUNCH_CHECK();
+  return ACME_OK;
+}
+
+}  // extern "C"

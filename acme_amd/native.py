@@ -1,0 +1,320 @@
+"""Thin owners of the native objects behind the drop-in API.
+
+`NativeReplay` wraps an acme_replay (GPU table); `NativeDQN` wraps an acme_dqn learner and
+owns its flat device buffers (params / target / grads / Adam m, v) as torch tensors so
+that torch.distributed (RCCL) can all-reduce the gradient buffer in place.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from acme_amd import _lib
+from acme_amd._lib import check, lib, ptr, stream_ptr
+
+SAMPLER_UNIFORM = 0
+SAMPLER_PRIORITIZED = 1
+
+
+class NativeReplay:
+    """Device-resident FIFO table with a 64-ary sum-tree sampler (see csrc/replay.hip)."""
+
+    def __init__(self, capacity: int, field_bytes: Sequence[int], prioritized: bool,
+                 priority_exponent: float = 0.6, seed: int = 1234, device=None):
+        _lib.require_gpu()
+        if len(field_bytes) > _lib.MAX_FIELDS:
+            raise ValueError(f"at most {_lib.MAX_FIELDS} flattened fields per item")
+        cfg = _lib.ReplayConfig()
+        cfg.capacity = int(capacity)
+        cfg.sampler = SAMPLER_PRIORITIZED if prioritized else SAMPLER_UNIFORM
+        cfg.num_fields = len(field_bytes)
+        cfg.priority_exponent = float(priority_exponent)
+        cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        for i, b in enumerate(field_bytes):
+            cfg.field_bytes[i] = int(b)
+        self.field_bytes = [int(b) for b in field_bytes]
+        self.capacity = int(capacity)
+        self.prioritized = prioritized
+        self.priority_exponent = float(priority_exponent)
+        self.seed = cfg.seed
+        self.device = torch.device(device or "cuda")
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(lib().acme_replay_create(ctypes.byref(cfg), ctypes.byref(h)), "replay create")
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                lib().acme_replay_destroy(h)
+            except Exception:  # interpreter shutdown
+                pass
+            self._h = None
+
+    @property
+    def handle(self):
+        return self._h
+
+    def size(self) -> int:
+        return int(lib().acme_replay_size(self._h))
+
+    def insert(self, fields: Sequence, priorities: Optional[np.ndarray] = None,
+               stream=None) -> np.ndarray:
+        """fields: per-field arrays/tensors with leading dim n (host numpy or device tensors)."""
+        n = int(fields[0].shape[0])
+        keys = np.empty(n, np.uint64)
+        on_dev = isinstance(fields[0], torch.Tensor) and fields[0].is_cuda
+        keep = []
+        ptrs = (ctypes.c_void_p * len(fields))()
+        for i, f in enumerate(fields):
+            if on_dev:
+                t = f.contiguous()
+                keep.append(t)
+                ptrs[i] = t.data_ptr()
+            else:
+                a = np.ascontiguousarray(f)
+                keep.append(a)
+                ptrs[i] = a.ctypes.data
+            nbytes = keep[-1].nbytes if not on_dev else keep[-1].numel() * keep[-1].element_size()
+            if nbytes != n * self.field_bytes[i]:
+                raise ValueError(f"field {i}: expected {n * self.field_bytes[i]} bytes, got {nbytes}")
+        pr = None
+        if priorities is not None:
+            pr = np.ascontiguousarray(priorities, np.float64)
+            if pr.shape != (n,):
+                raise ValueError("priorities must have shape [n]")
+        check(lib().acme_replay_insert(self._h, ptrs, n, None if pr is None else pr.ctypes.data,
+                                       1 if on_dev else 0, keys.ctypes.data, stream_ptr(stream)),
+              "replay insert")
+        return keys
+
+    def fill_synthetic(self, n: int, layout: int, num_actions: int = 18, seed: int = 0,
+                       stream=None) -> None:
+        check(lib().acme_replay_fill_synthetic(self._h, int(n), int(layout), int(num_actions),
+                                               int(seed), stream_ptr(stream)), "fill_synthetic")
+
+    def sample(self, batch: int, step: int, out: Optional[Dict[str, torch.Tensor]] = None,
+               stream=None) -> Dict[str, torch.Tensor]:
+        if out is None:
+            out = self.alloc_sample_info(batch)
+        check(lib().acme_replay_sample(self._h, int(batch), int(step) & 0xFFFFFFFFFFFFFFFF,
+                                       ptr(out["slots"]), ptr(out["keys"]),
+                                       ptr(out["probabilities"]), ptr(out["table_size"]),
+                                       ptr(out["priorities"]), stream_ptr(stream)),
+              "replay sample")
+        return out
+
+    def alloc_sample_info(self, batch: int) -> Dict[str, torch.Tensor]:
+        d = self.device
+        return dict(slots=torch.empty(batch, dtype=torch.int64, device=d),
+                    keys=torch.empty(batch, dtype=torch.uint64, device=d),
+                    probabilities=torch.empty(batch, dtype=torch.float64, device=d),
+                    table_size=torch.empty(batch, dtype=torch.int64, device=d),
+                    priorities=torch.empty(batch, dtype=torch.float64, device=d))
+
+    def gather(self, slots: torch.Tensor, outs: Sequence[torch.Tensor], stream=None) -> None:
+        ptrs = (ctypes.c_void_p * len(outs))(*[o.data_ptr() for o in outs])
+        check(lib().acme_replay_gather(self._h, ptr(slots), int(slots.numel()), ptrs,
+                                       stream_ptr(stream)), "replay gather")
+
+    def update_priorities(self, keys: torch.Tensor, priorities: torch.Tensor, stream=None) -> None:
+        keys = keys.to(self.device, torch.uint64).contiguous()
+        priorities = priorities.to(self.device, torch.float64).contiguous()
+        check(lib().acme_replay_update_priorities(self._h, ptr(keys), ptr(priorities),
+                                                  int(keys.numel()), stream_ptr(stream)),
+              "update_priorities")
+
+    def debug_state(self) -> Dict[str, np.ndarray]:
+        """Host copies of leaf weights / raw priorities / keys (tests)."""
+        lv, rp, ks = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        check(lib().acme_replay_debug_leaves(self._h, ctypes.byref(lv), ctypes.byref(rp),
+                                             ctypes.byref(ks)))
+        torch.cuda.synchronize(self.device)
+        n = self.capacity
+        out = {}
+        for name, p, dt, cnt in (("leaves", lv, np.float64, n), ("raw", rp, np.float64, n),
+                                 ("keys", ks, np.uint64, n)):
+            out[name] = _device_array(p.value, cnt, dt, self.device).cpu().numpy().view(dt).copy()
+        return out
+
+
+def _device_array(address: int, count: int, dtype, device) -> torch.Tensor:
+    """Copies `count` elements at a raw device address into a new tensor (test helper)."""
+    nbytes = count * np.dtype(dtype).itemsize
+    dst = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    torch.cuda.synchronize(device)
+    _memcpy_dtod(dst.data_ptr(), address, nbytes)
+    return dst
+
+
+_hip = None
+
+
+def _memcpy_dtod(dst: int, src: int, nbytes: int) -> None:
+    global _hip
+    if _hip is None:
+        _hip = ctypes.CDLL("libamdhip64.so.7")
+        _hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        _hip.hipMemcpy.restype = ctypes.c_int
+    rc = _hip.hipMemcpy(ctypes.c_void_p(dst), ctypes.c_void_p(src), ctypes.c_size_t(nbytes), 3)
+    if rc != 0:
+        raise RuntimeError(f"hipMemcpy failed ({rc})")
+
+
+NET_NATURE = 0
+NET_MLP = 1
+OBS_U8 = 0
+OBS_F32 = 1
+
+
+class NativeDQN:
+    """acme_dqn learner + its flat buffers."""
+
+    def __init__(self, *, network: str, num_actions: int, max_batch: int, obs_dtype: str,
+                 obs_dim: int = 0, hidden: Sequence[int] = (), discount: float = 0.99,
+                 importance_sampling_exponent: float = 0.2, learning_rate: float = 1e-3,
+                 huber_loss_parameter: float = 1.0, target_update_period: int = 100,
+                 max_abs_reward: float = 1.0, adam_beta1: float = 0.9, adam_beta2: float = 0.999,
+                 adam_epsilon: float = 1e-8, device=None):
+        _lib.require_gpu()
+        if huber_loss_parameter < 0:
+            raise ValueError("quadratic_linear_boundary must be >= 0.")
+        cfg = _lib.DQNConfig()
+        cfg.network = NET_NATURE if network == "nature" else NET_MLP
+        cfg.obs_dtype = OBS_U8 if obs_dtype == "uint8" else OBS_F32
+        cfg.num_actions = int(num_actions)
+        cfg.max_batch = int(max_batch)
+        cfg.obs_dim = int(obs_dim)
+        if len(hidden) > _lib.MAX_MLP_LAYERS:
+            raise ValueError(f"at most {_lib.MAX_MLP_LAYERS} hidden layers")
+        cfg.num_hidden = len(hidden)
+        for i, h in enumerate(hidden):
+            cfg.hidden[i] = int(h)
+        cfg.discount = discount
+        cfg.importance_sampling_exponent = importance_sampling_exponent
+        cfg.learning_rate = learning_rate
+        cfg.huber_loss_parameter = huber_loss_parameter
+        cfg.adam_beta1, cfg.adam_beta2, cfg.adam_epsilon = adam_beta1, adam_beta2, adam_epsilon
+        cfg.target_update_period = int(target_update_period)
+        cfg.max_abs_reward = max_abs_reward
+        self.cfg = cfg
+        self.network = network
+        self.num_actions = int(num_actions)
+        self.max_batch = int(max_batch)
+        self.device = torch.device(device or "cuda")
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(lib().acme_dqn_create(ctypes.byref(cfg), ctypes.byref(h)), "dqn create")
+        self._h = h
+        L = lib()
+        self.flat_size = int(L.acme_dqn_flat_size(h))
+        self.num_params = int(L.acme_dqn_num_params(h))
+        self.tensors: List[Tuple[str, int, Tuple[int, ...]]] = []
+        for i in range(L.acme_dqn_num_tensors(h)):
+            off, numel, nd = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int32()
+            shape = (ctypes.c_int64 * 4)()
+            name = ctypes.c_char_p()
+            check(L.acme_dqn_tensor_info(h, i, ctypes.byref(off), ctypes.byref(numel),
+                                         ctypes.byref(nd), shape, ctypes.byref(name)))
+            self.tensors.append((name.value.decode(), int(off.value),
+                                 tuple(int(shape[k]) for k in range(nd.value))))
+        d = self.device
+        z = lambda: torch.zeros(self.flat_size, dtype=torch.float32, device=d)  # noqa: E731
+        self.params, self.target, self.grads, self.m, self.v = z(), z(), z(), z(), z()
+        check(L.acme_dqn_bind(h, ptr(self.params), ptr(self.target), ptr(self.grads),
+                              ptr(self.m), ptr(self.v)), "dqn bind")
+        self.loss = torch.zeros(1, dtype=torch.float32, device=d)
+        self.td_error = torch.zeros(max_batch, dtype=torch.float32, device=d)
+        self.priorities = torch.zeros(max_batch, dtype=torch.float64, device=d)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                lib().acme_dqn_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    # --------------------------------------------------------------- parameters
+    def views(self, flat: torch.Tensor) -> Dict[str, torch.Tensor]:
+        out = {}
+        for name, off, shape in self.tensors:
+            n = int(np.prod(shape))
+            out[name] = flat[off:off + n].view(shape)
+        return out
+
+    def set_params(self, params: Dict[str, np.ndarray], target: Optional[Dict] = None) -> None:
+        for flat, src in ((self.params, params), (self.target, target if target is not None else params)):
+            v = self.views(flat)
+            for name, t in v.items():
+                t.copy_(torch.as_tensor(np.asarray(src[name], np.float32)).view(t.shape))
+
+    def get_params(self, which: str = "params") -> Dict[str, np.ndarray]:
+        flat = getattr(self, which)
+        return {k: v.detach().cpu().numpy().copy() for k, v in self.views(flat).items()}
+
+    @property
+    def num_steps(self) -> int:
+        return int(lib().acme_dqn_num_steps(self._h))
+
+    @num_steps.setter
+    def num_steps(self, n: int) -> None:
+        check(lib().acme_dqn_set_num_steps(self._h, int(n)))
+
+    # --------------------------------------------------------------- step
+    def _batch(self, o_tm1, a_tm1, r_t, d_t, o_t, probabilities, global_min_probability=None):
+        B = int(a_tm1.shape[0])
+        for name, t in (("o_tm1", o_tm1), ("a_tm1", a_tm1), ("r_t", r_t), ("d_t", d_t),
+                        ("o_t", o_t), ("probabilities", probabilities)):
+            if not (isinstance(t, torch.Tensor) and t.is_cuda and t.is_contiguous()):
+                raise ValueError(f"{name} must be a contiguous device tensor")
+            if t.shape[0] != B:
+                raise ValueError(f"{name} has leading dim {t.shape[0]}, expected {B}")
+        if a_tm1.dtype != torch.int32 or r_t.dtype != torch.float32 or d_t.dtype != torch.float32:
+            raise ValueError("a_tm1 must be int32, r_t and d_t float32")
+        if probabilities.dtype != torch.float64:
+            raise ValueError("probabilities must be float64")
+        want = torch.uint8 if self.cfg.obs_dtype == OBS_U8 else torch.float32
+        if o_tm1.dtype != want or o_t.dtype != want:
+            raise ValueError(f"observations must be {want}")
+        tb = _lib.TransitionBatch()
+        tb.o_tm1, tb.a_tm1, tb.r_t, tb.d_t, tb.o_t = (ptr(o_tm1), ptr(a_tm1), ptr(r_t), ptr(d_t),
+                                                      ptr(o_t))
+        tb.probabilities = ptr(probabilities)
+        tb.batch = B
+        tb.global_min_probability = ptr(global_min_probability)
+        return tb
+
+    def _outputs(self, q_tm1=None):
+        o = _lib.DQNOutputs()
+        o.loss, o.td_error, o.priorities = ptr(self.loss), ptr(self.td_error), ptr(self.priorities)
+        o.q_tm1 = ptr(q_tm1)
+        return o
+
+    def forward_backward(self, *batch, global_min_probability=None, q_tm1=None, stream=None):
+        tb = self._batch(*batch, global_min_probability=global_min_probability)
+        out = self._outputs(q_tm1)
+        check(lib().acme_dqn_forward_backward(self._h, ctypes.byref(tb), ctypes.byref(out),
+                                              stream_ptr(stream)), "dqn forward_backward")
+
+    def apply(self, stream=None):
+        check(lib().acme_dqn_apply(self._h, stream_ptr(stream)), "dqn apply")
+
+    def step(self, *batch, q_tm1=None, stream=None):
+        tb = self._batch(*batch)
+        out = self._outputs(q_tm1)
+        check(lib().acme_dqn_step(self._h, ctypes.byref(tb), ctypes.byref(out),
+                                  stream_ptr(stream)), "dqn step")
+
+    def q_values(self, obs: torch.Tensor, use_target: bool = False, stream=None) -> torch.Tensor:
+        B = int(obs.shape[0])
+        q = torch.empty(B, self.num_actions, dtype=torch.float32, device=self.device)
+        check(lib().acme_dqn_q_values(self._h, ptr(obs.contiguous()), B, 1 if use_target else 0,
+                                      ptr(q), stream_ptr(stream)), "dqn q_values")
+        return q

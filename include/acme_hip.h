@@ -1,0 +1,204 @@
+/*
+ * acme_hip.h — C ABI of the MI355X-native Acme learner core (libacme_hip.so).
+ *
+ * Plain C types only (no torch / HIP types in the signatures): device buffers are
+ * `void*` device pointers, streams are `void*` (a hipStream_t, NULL = default).
+ * Every function returns ACME_OK (0) or a negative acme_status and leaves a message
+ * in a thread-local buffer (acme_last_error()).
+ *
+ * What each entry point replaces in the reference (tmtlakmal/acme @ 2025-02-05):
+ *
+ *   acme_replay_*       the Reverb table/server the agents construct
+ *                       (acme/agents/tf/dqn/agent.py:95-102 Prioritized + Fifo + MinSize;
+ *                        acme/agents/tf/d4pg/agent.py:96-102 Uniform) and
+ *     _insert           reverb.Writer.append + create_item, driven by
+ *                       NStepTransitionAdder._write (acme/adders/reverb/transition.py:374-378)
+ *     _sample/_gather   reverb.ReplayDataset + tf.data batch (acme/datasets/reverb.py:93-139)
+ *                       producing ReplaySample(info=SampleInfo(key, probability,
+ *                       table_size, priority), data=...)  (acme/testing/fakes.py:249-260)
+ *     _update_priorities reverb.TFClient.update_priorities
+ *                       (acme/agents/tf/dqn/learning.py:151-154) and
+ *                       Client.mutate_priorities (acme/agents/jax/dqn/learning.py:131-134)
+ *   acme_dqn_*          DQNLearner._step (acme/agents/tf/dqn/learning.py:112-168):
+ *                       three Q forwards, double-Q n-step TD, Huber, f64 IS weights,
+ *                       backward, snt.Adam, post-step periodic target copy.
+ *
+ * Threading: one learner stream; acme_replay_insert may be called from actor threads
+ * (internal mutex).  Ordering between an insert's side stream and the sampling stream
+ * is the caller's (the Python Table records an event after each insert flush).
+ */
+#ifndef ACME_HIP_H_
+#define ACME_HIP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum acme_status {
+  ACME_OK = 0,
+  ACME_ERR_INVALID = -1, /* bad argument -> ValueError */
+  ACME_ERR_HIP = -2,     /* HIP runtime failure -> RuntimeError */
+  ACME_ERR_EMPTY = -3,   /* sampling below the table's min size -> RuntimeError */
+  ACME_ERR_OOM = -4      /* device allocation failure -> MemoryError */
+} acme_status;
+
+const char* acme_last_error(void);
+/* Library version string (build id). */
+const char* acme_version(void);
+/* Name of the GPU the library was built for ("gfx950"). */
+const char* acme_target_arch(void);
+
+/* ------------------------------------------------------------------ replay -- */
+
+#define ACME_MAX_FIELDS 8
+
+enum { ACME_SAMPLER_UNIFORM = 0, ACME_SAMPLER_PRIORITIZED = 1 };
+
+typedef struct acme_replay_config {
+  int64_t capacity;          /* max_size of the table (FIFO eviction beyond it)     */
+  int32_t sampler;           /* ACME_SAMPLER_*                                      */
+  int32_t num_fields;        /* number of flattened data fields per item            */
+  double priority_exponent;  /* Prioritized(alpha); ignored for uniform             */
+  uint64_t seed;             /* Philox key for sampling                             */
+  int64_t field_bytes[ACME_MAX_FIELDS]; /* bytes per item of each field (mult. of 4) */
+} acme_replay_config;
+
+typedef struct acme_replay acme_replay;
+
+int acme_replay_create(const acme_replay_config* cfg, acme_replay** out);
+int acme_replay_destroy(acme_replay* r);
+
+/* Insert n items.  fields[f] points at n * field_bytes[f] contiguous bytes, on the
+ * host (pinned for true asynchrony) when src_on_device == 0, else on the device.
+ * priorities: n raw priorities (host).  out_keys (host, optional): the keys assigned.
+ * Items go to ring slots (insert_count + i) % capacity (Fifo remover). */
+int acme_replay_insert(acme_replay* r, const void* const* fields, int64_t n,
+                       const double* priorities, int32_t src_on_device,
+                       uint64_t* out_keys, void* stream);
+
+/* Fill n items with synthetic data generated on the device (benchmark/test helper,
+ * no host traffic).  layout: 0 = DQN Atari transition (o_tm1 u8, a i32, r f32, d f32,
+ * o_t u8), 1 = control transition with f32 fields
+ * (o f32, a f32, r f32, d f32, o_t f32; config 3).  All priorities set to 1.0. */
+int acme_replay_fill_synthetic(acme_replay* r, int64_t n, int32_t layout,
+                               int32_t num_actions, uint64_t seed, void* stream);
+
+/* Draw `batch` items.  Device outputs: slots (i64), keys (u64), probabilities (f64,
+ * P(i) = p_i^alpha / sum_j p_j^alpha or 1/size), table_size (i64), priorities (f64).
+ * Any output pointer except slots may be NULL.  step_counter selects the Philox
+ * counter block, so (seed, step_counter) fully determines the draw. */
+int acme_replay_sample(acme_replay* r, int64_t batch, uint64_t step_counter,
+                       int64_t* slots, uint64_t* keys, double* probabilities,
+                       int64_t* table_size, double* priorities, void* stream);
+
+/* Copy the items at `slots` into batch-major device buffers out_fields[f]
+ * (batch * field_bytes[f] bytes each). */
+int acme_replay_gather(acme_replay* r, const int64_t* slots, int64_t batch,
+                       void* const* out_fields, void* stream);
+
+/* Set priorities of the items identified by device arrays keys/priorities.  Keys no
+ * longer in the table are ignored; for repeated keys the last one wins (Reverb
+ * applies updates in order). */
+int acme_replay_update_priorities(acme_replay* r, const uint64_t* keys,
+                                  const double* priorities, int64_t n, void* stream);
+
+int64_t acme_replay_size(const acme_replay* r);
+int64_t acme_replay_capacity(const acme_replay* r);
+/* Device pointer to the sum-tree total (f64) — test/diagnostic use. */
+int acme_replay_debug_leaves(const acme_replay* r, const double** leaf_values,
+                             const double** raw_priorities, const uint64_t** keys);
+
+/* -------------------------------------------------------------------- DQN -- */
+
+enum { ACME_NET_NATURE_DQN = 0, ACME_NET_MLP = 1 };
+enum { ACME_OBS_U8_SCALED = 0, ACME_OBS_F32 = 1 };
+
+#define ACME_MAX_MLP_LAYERS 8
+
+typedef struct acme_dqn_config {
+  int32_t network;           /* ACME_NET_*                                          */
+  int32_t obs_dtype;         /* ACME_OBS_U8_SCALED: uint8 / 255 (AtariWrapper to_float) */
+  int32_t num_actions;
+  int32_t max_batch;
+  /* Nature DQN: obs is [84, 84, 4] NHWC.  MLP: obs_dim inputs, hidden sizes below
+   * (ReLU), final Linear(num_actions) (snt.nets.MLP([..., A])). */
+  int32_t obs_dim;
+  int32_t num_hidden;
+  int32_t hidden[ACME_MAX_MLP_LAYERS];
+  float discount;            /* agent discount, applied to the n-step D           */
+  float importance_sampling_exponent;
+  float learning_rate;
+  float huber_loss_parameter;
+  float adam_beta1, adam_beta2, adam_epsilon;
+  int32_t target_update_period;
+  float max_abs_reward;      /* reward clip (TF DQN clips to [-1, 1])               */
+} acme_dqn_config;
+
+typedef struct acme_dqn acme_dqn;
+
+int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out);
+int acme_dqn_destroy(acme_dqn* l);
+/* Number of f32 parameters (logical) and of the padded flat buffer the learner uses. */
+int64_t acme_dqn_num_params(const acme_dqn* l);
+int64_t acme_dqn_flat_size(const acme_dqn* l);
+/* Per-tensor layout of the flat buffer: offsets/sizes (in floats) of tensor i. */
+int32_t acme_dqn_num_tensors(const acme_dqn* l);
+int acme_dqn_tensor_info(const acme_dqn* l, int32_t i, int64_t* offset, int64_t* numel,
+                         int32_t* ndim, int64_t* shape4, const char** name);
+
+/* Bind caller-owned device buffers (each acme_dqn_flat_size floats): online params,
+ * target params, gradients, Adam first/second moments. */
+int acme_dqn_bind(acme_dqn* l, float* params, float* target, float* grads, float* adam_m,
+                  float* adam_v);
+
+typedef struct acme_transition_batch {
+  const void* o_tm1;   /* [B, obs...]  u8 or f32 */
+  const int32_t* a_tm1;/* [B] */
+  const float* r_t;    /* [B] n-step return */
+  const float* d_t;    /* [B] n-step discount */
+  const void* o_t;     /* [B, obs...] */
+  const double* probabilities; /* [B] f64 sampling probabilities (info.probability) */
+  int64_t batch;
+  /* If non-NULL: the minimum probability over the GLOBAL batch (data-parallel),
+   * else the local batch minimum is used for the IS-weight max. */
+  const double* global_min_probability;
+} acme_transition_batch;
+
+typedef struct acme_dqn_outputs {
+  float* loss;         /* [1] device: mean weighted Huber loss */
+  float* td_error;     /* [B] device (optional) */
+  double* priorities;  /* [B] device |td| as f64 (optional) */
+  float* q_tm1;        /* [B, A] device (optional) online q(o_tm1) */
+} acme_dqn_outputs;
+
+/* Forward + backward: fills grads (flat) and outputs.  Does not touch params. */
+int acme_dqn_forward_backward(acme_dqn* l, const acme_transition_batch* batch,
+                              const acme_dqn_outputs* out, void* stream);
+/* Adam on (params, grads), then target <- params when num_steps % period == 0, then
+ * num_steps += 1 (acme/agents/tf/dqn/learning.py:147-161). */
+int acme_dqn_apply(acme_dqn* l, void* stream);
+/* forward_backward + apply. */
+int acme_dqn_step(acme_dqn* l, const acme_transition_batch* batch,
+                  const acme_dqn_outputs* out, void* stream);
+/* Q forward only (online or target network) — actor/eval helper. */
+int acme_dqn_q_values(acme_dqn* l, const void* obs, int64_t batch, int32_t use_target,
+                      float* q_out, void* stream);
+int64_t acme_dqn_num_steps(const acme_dqn* l);
+int acme_dqn_set_num_steps(acme_dqn* l, int64_t n);
+/* Minimum of a device f64 array (for the data-parallel IS normaliser). */
+int acme_min_f64(const double* x, int64_t n, double* out_dev, void* stream);
+
+/* ----------------------------------------------------------- elementwise ops -- */
+
+/* snt.optimizers.Adam update over a flat f32 buffer (t = 1-based step). */
+int acme_adam_update(float* params, const float* grads, float* m, float* v, int64_t n,
+                     float lr, float beta1, float beta2, float eps, int64_t t,
+                     void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ACME_HIP_H_ */
