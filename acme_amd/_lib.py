@@ -86,8 +86,16 @@ _SIGS = {
                               c_vp]),
     "acme_dqn_q_values": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp]),
     "acme_dqn_num_steps": (c_i64, [c_vp]),
+    "acme_dqn_debug_buffer": (c_i32, [c_vp, ctypes.c_char_p, ctypes.POINTER(c_vp),
+                                      ctypes.POINTER(c_i64)]),
     "acme_dqn_set_num_steps": (c_i32, [c_vp, c_i64]),
     "acme_min_f64": (c_i32, [c_vp, c_i64, c_vp, c_vp]),
+    "acme_profile_enable": (c_i32, [c_i32]),
+    "acme_profile_reset": (c_i32, []),
+    "acme_profile_num_sections": (c_i32, []),
+    "acme_profile_query": (c_i32, [c_i32, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(c_f64),
+                                   ctypes.POINTER(c_i64), ctypes.POINTER(c_f64),
+                                   ctypes.POINTER(c_f64)]),
     "acme_adam_update": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_f32, c_f32, c_f32, c_f32, c_i64,
                                  c_vp]),
 }

@@ -26,6 +26,7 @@
 #include "conv.h"
 #include "gemm.h"
 #include "kernels.h"
+#include "profiler.h"
 
 using namespace acme;
 using namespace acme::conv;
@@ -136,6 +137,14 @@ inline int chunk_for(int K, int splits) {
       return ACME_ERR_HIP;                                                           \
     }                                                                                \
   } while (0)
+// Profiled launch: `flops` = algorithmic FLOPs of the launch (2 * useful MACs).
+#define ACME_GEMM_F(name, flops, BM, BN, WM, WN, prob, splits) \
+  do {                                                          \
+    ACME_PROF(name, st, (double)(flops), 0.0);                  \
+    ACME_GEMM(BM, BN, WM, WN, prob, splits);                    \
+  } while (0)
+#define ACME_GEMM_N(name, BM, BN, WM, WN, prob, splits) \
+  ACME_GEMM_F(name, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, BM, BN, WM, WN, prob, splits)
 
 // ---------------------------------------------------------------- Nature forward
 // rows = number of observations; first `split` rows from obs_a, the rest from obs_b.
@@ -148,35 +157,36 @@ int nature_forward(acme_dqn* l, const float* prm, const void* obs_a, const void*
     p.M = rows * G1::OPIX; p.N = G1::CO; p.K = G1::K; p.k_chunk = G1::K;
     p.x = static_cast<const uint8_t*>(obs_a); p.x2 = static_cast<const uint8_t*>(obs_b);
     p.split_b = split; p.w = P(l, prm, l->t_c1w); p.bias = P(l, prm, l->t_c1b); p.y = x1;
-    ACME_GEMM(256, 32, 4, 1, p, 1);
+    ACME_GEMM_N("conv1_fwd", 256, 32, 4, 1, p, 1);
   } else {
     ConvFwd<G1, InF32> p;
     p.M = rows * G1::OPIX; p.N = G1::CO; p.K = G1::K; p.k_chunk = G1::K;
     p.x = static_cast<const float*>(obs_a); p.x2 = static_cast<const float*>(obs_b);
     p.split_b = split; p.w = P(l, prm, l->t_c1w); p.bias = P(l, prm, l->t_c1b); p.y = x1;
-    ACME_GEMM(256, 32, 4, 1, p, 1);
+    ACME_GEMM_N("conv1_fwd", 256, 32, 4, 1, p, 1);
   }
   {
     ConvFwd<G2, InF32> p;
     p.M = rows * G2::OPIX; p.N = G2::CO; p.K = G2::K; p.k_chunk = G2::K;
     p.x = x1; p.x2 = x1; p.split_b = rows; p.w = P(l, prm, l->t_c2w);
     p.bias = P(l, prm, l->t_c2b); p.y = x2;
-    ACME_GEMM(128, 64, 2, 2, p, 1);
+    ACME_GEMM_N("conv2_fwd", 128, 64, 2, 2, p, 1);
   }
   {
     ConvFwd<G3, InF32> p;
     p.M = rows * G3::OPIX; p.N = G3::CO; p.K = G3::K; p.k_chunk = G3::K;
     p.x = x2; p.x2 = x2; p.split_b = rows; p.w = P(l, prm, l->t_c3w);
     p.bias = P(l, prm, l->t_c3b); p.y = x3;
-    ACME_GEMM(128, 64, 2, 2, p, 1);
+    ACME_GEMM_N("conv3_fwd", 128, 64, 2, 2, p, 1);
   }
   {
     DenseFwd<true> p;
     p.M = rows; p.N = 2 * kHidden; p.K = kFlat; p.k_chunk = kFlat;
     p.x = x3; p.x2 = x3; p.split_b = rows; p.ldx = kFlat;
     p.w = P(l, prm, l->t_fcw); p.bias = P(l, prm, l->t_fcb); p.y = hid; p.act = ACT_RELU;
-    ACME_GEMM(64, 64, 2, 2, p, 1);
+    ACME_GEMM_N("fc_fwd", 64, 64, 2, 2, p, 1);
   }
+  ACME_PROF("head_fwd", st, 2.0 * rows * kHidden * (l->cfg.num_actions + 1), 0.0);
   return launch_duel_head(hid, rows, kHidden, l->cfg.num_actions, P(l, prm, l->t_vw),
                           P(l, prm, l->t_vb), P(l, prm, l->t_aw), P(l, prm, l->t_ab), q, st);
 }
@@ -192,14 +202,14 @@ int mlp_layer0(acme_dqn* l, const float* prm, const Layer& L, const void* a, con
     p.x = static_cast<const typename In::T*>(a); p.x2 = static_cast<const typename In::T*>(b);
     p.split_b = split; p.ldx = L.in; p.w = P(l, prm, L.w); p.bias = P(l, prm, L.b); p.y = y;
     p.act = L.relu ? ACT_RELU : ACT_NONE;
-    ACME_GEMM(64, 64, 2, 2, p, 1);
+    ACME_GEMM_N("mlp_fwd", 64, 64, 2, 2, p, 1);
   } else {
     DenseFwd<false, In> p;
     p.M = rows; p.N = L.out; p.K = L.in; p.k_chunk = L.in;
     p.x = static_cast<const typename In::T*>(a); p.x2 = static_cast<const typename In::T*>(b);
     p.split_b = split; p.ldx = L.in; p.w = P(l, prm, L.w); p.bias = P(l, prm, L.b); p.y = y;
     p.act = L.relu ? ACT_RELU : ACT_NONE;
-    ACME_GEMM(64, 64, 2, 2, p, 1);
+    ACME_GEMM_N("mlp_fwd", 64, 64, 2, 2, p, 1);
   }
   return ACME_OK;
 }
@@ -227,10 +237,12 @@ int mlp_forward(acme_dqn* l, const float* prm, const void* obs_a, const void* ob
 // Bias gradient = column sums of dZ [rows][n] (deterministic two-pass reduction).
 int bias_grad(acme_dqn* l, const float* dz, int64_t rows, int n, float* out, hipStream_t st) {
   const int64_t chunks = std::min<int64_t>(ceil_div(rows, 256), l->colsum_floats / n);
+  ACME_PROF("bias_grad", st, 0.0, 4.0 * (double)rows * n);
   return launch_colsum(dz, rows, n, (int)chunks, l->colsum, out, st);
 }
 
 int reduce_slab(const float* slab, int splits, int64_t count, float* out, hipStream_t st) {
+  ACME_PROF("slab_reduce", st, 0.0, 4.0 * (double)(splits + 1) * count);
   return launch_slab_reduce(slab, splits, count, out, st);
 }
 
@@ -244,10 +256,11 @@ int conv_wgrad(acme_dqn* l, const typename In::T* x, const float* dz, int batch,
     set_error("slab workspace too small");
     return ACME_ERR_INVALID;
   }
+  const char* wname = G::K == 256 ? "conv1_wgrad" : (G::K == 512 ? "conv2_wgrad" : "conv3_wgrad");
   if (G::CO == 32) {
-    ACME_GEMM(64, 32, 2, 1, p, splits);
+    ACME_GEMM_N(wname, 64, 32, 2, 1, p, splits);
   } else {
-    ACME_GEMM(64, 64, 2, 2, p, splits);
+    ACME_GEMM_N(wname, 64, 64, 2, 2, p, splits);
   }
   int rc = reduce_slab(l->slab, splits, (int64_t)p.M * p.N, dw, st);
   if (rc != ACME_OK) return rc;
@@ -259,16 +272,20 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st) {
   float* gr = l->grads;
   const int A = l->cfg.num_actions;
   // Head: dZ of the fused hidden layer (masked by its ReLU) and head weight grads.
-  int rc = launch_duel_head_backward(l->hid, l->g, l->a_cache, B, kHidden, A, P(l, prm, l->t_vw),
+  int rc;
+  {
+  ACME_PROF("head_bwd", st, 0.0, 0.0);
+  rc = launch_duel_head_backward(l->hid, l->g, l->a_cache, B, kHidden, A, P(l, prm, l->t_vw),
                                      P(l, prm, l->t_aw), l->dzh, Pm(l, gr, l->t_vw),
                                      Pm(l, gr, l->t_vb), Pm(l, gr, l->t_aw), Pm(l, gr, l->t_ab), st);
+  }
   if (rc != ACME_OK) return rc;
   // FC weight grad: [7744, 1024] = x3^T dZh (reduction over the batch).
   {
     DenseWgrad<true> p;
     p.M = kFlat; p.N = 2 * kHidden; p.K = B; p.k_chunk = B;
     p.x = l->x3; p.ldx = kFlat; p.dz = l->dzh; p.out = Pm(l, gr, l->t_fcw);
-    ACME_GEMM(128, 128, 2, 2, p, 1);
+    ACME_GEMM_N("fc_wgrad", 128, 128, 2, 2, p, 1);
   }
   if ((rc = bias_grad(l, l->dzh, B, 2 * kHidden, Pm(l, gr, l->t_fcb), st)) != ACME_OK) return rc;
   // FC input grad -> dZ3 (masked by conv3's ReLU).
@@ -276,7 +293,7 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st) {
     DenseDgrad<true> p;
     p.M = B; p.N = kFlat; p.K = 2 * kHidden; p.k_chunk = p.K;
     p.dz = l->dzh; p.w = P(l, prm, l->t_fcw); p.xprev = l->x3; p.ldx = kFlat; p.dx = l->dz3;
-    ACME_GEMM(64, 128, 2, 2, p, 1);
+    ACME_GEMM_N("fc_dgrad", 64, 128, 2, 2, p, 1);
   }
   // conv3
   if ((rc = conv_wgrad<G3, InF32>(l, l->x2, l->dz3, B, 64, Pm(l, gr, l->t_c3w),
@@ -286,7 +303,7 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st) {
     ConvDgrad<G3> p;
     p.M = B * G3::IPIX; p.N = G3::CI; p.K = G3::KH * G3::KW * G3::CO; p.k_chunk = p.K;
     p.dz = l->dz3; p.w = P(l, prm, l->t_c3w); p.xprev = l->x2; p.dx = l->dz2;
-    ACME_GEMM(128, 64, 2, 2, p, 1);
+    ACME_GEMM_N("conv3_dgrad", 128, 64, 2, 2, p, 1);
   }
   // conv2
   if ((rc = conv_wgrad<G2, InF32>(l, l->x1, l->dz2, B, 64, Pm(l, gr, l->t_c2w),
@@ -296,7 +313,7 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st) {
     ConvDgrad<G2> p;
     p.M = B * G2::IPIX; p.N = G2::CI; p.K = G2::KH * G2::KW * G2::CO; p.k_chunk = p.K;
     p.dz = l->dz2; p.w = P(l, prm, l->t_c2w); p.xprev = l->x1; p.dx = l->dz1;
-    ACME_GEMM(256, 32, 4, 1, p, 1);
+    ACME_GEMM_F("conv2_dgrad", 2.0 * B * G2::OPIX * G2::CO * G2::K, 256, 32, 4, 1, p, 1);
   }
   // conv1 (no input gradient needed)
   if (l->cfg.obs_dtype == ACME_OBS_U8_SCALED) {
@@ -316,12 +333,12 @@ int mlp_wgrad(acme_dqn* l, const Layer& L, const void* x, const float* dz, int B
     DenseWgrad<true, In> p;
     p.M = L.in; p.N = L.out; p.K = B; p.k_chunk = B;
     p.x = static_cast<const typename In::T*>(x); p.ldx = L.in; p.dz = dz; p.out = dw;
-    ACME_GEMM(64, 64, 2, 2, p, 1);
+    ACME_GEMM_N("mlp_wgrad", 64, 64, 2, 2, p, 1);
   } else {
     DenseWgrad<false, In> p;
     p.M = L.in; p.N = L.out; p.K = B; p.k_chunk = B;
     p.x = static_cast<const typename In::T*>(x); p.ldx = L.in; p.dz = dz; p.out = dw;
-    ACME_GEMM(64, 64, 2, 2, p, 1);
+    ACME_GEMM_N("mlp_wgrad", 64, 64, 2, 2, p, 1);
   }
   return ACME_OK;
 }
@@ -351,13 +368,13 @@ int mlp_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st) {
         p.M = B; p.N = L.in; p.K = L.out; p.k_chunk = L.out;
         p.dz = dz; p.w = P(l, prm, L.w); p.xprev = l->mlp_act[i - 1]; p.ldx = L.in;
         p.dx = l->mlp_dz[i - 1];
-        ACME_GEMM(64, 64, 2, 2, p, 1);
+        ACME_GEMM_N("mlp_dgrad", 64, 64, 2, 2, p, 1);
       } else {
         DenseDgrad<false> p;
         p.M = B; p.N = L.in; p.K = L.out; p.k_chunk = L.out;
         p.dz = dz; p.w = P(l, prm, L.w); p.xprev = l->mlp_act[i - 1]; p.ldx = L.in;
         p.dx = l->mlp_dz[i - 1];
-        ACME_GEMM(64, 64, 2, 2, p, 1);
+        ACME_GEMM_N("mlp_dgrad", 64, 64, 2, 2, p, 1);
       }
     }
   }
@@ -506,6 +523,39 @@ int acme_dqn_set_num_steps(acme_dqn* l, int64_t n) {
   return ACME_OK;
 }
 
+int acme_dqn_debug_buffer(const acme_dqn* l, const char* name, const float** out,
+                          int64_t* count) {
+  ACME_CHECK_ARG(l && name && out && count, "null argument");
+  const int64_t B = l->cfg.max_batch;
+  struct {
+    const char* n;
+    const float* p;
+    int64_t c;
+  } tab[] = {{"x1", l->x1, 2 * B * 441 * 32}, {"x2", l->x2, 2 * B * kFlat},
+             {"x3", l->x3, 2 * B * kFlat},    {"hid", l->hid, 2 * B * 2 * kHidden},
+             {"dzh", l->dzh, B * 2 * kHidden}, {"dz3", l->dz3, B * kFlat},
+             {"dz2", l->dz2, B * kFlat},       {"dz1", l->dz1, B * 441 * 32},
+             {"q_on", l->q_on, 2 * B * l->cfg.num_actions},
+             {"q_tg", l->q_tg, B * l->cfg.num_actions}, {"g", l->g, B}};
+  for (auto& e : tab)
+    if (e.p && std::strcmp(e.n, name) == 0) {
+      *out = e.p;
+      *count = e.c;
+      return ACME_OK;
+    }
+  for (size_t i = 0; i < l->mlp_act.size(); ++i) {  // MLP layer outputs "act<i>" (2B rows)
+    char nm[16];
+    snprintf(nm, sizeof(nm), "act%zu", i);
+    if (std::strcmp(nm, name) == 0) {
+      *out = l->mlp_act[i];
+      *count = 2 * B * l->layers[i].out;
+      return ACME_OK;
+    }
+  }
+  set_error("unknown debug buffer '%s'", name);
+  return ACME_ERR_INVALID;
+}
+
 int acme_dqn_q_values(acme_dqn* l, const void* obs, int64_t batch, int32_t use_target,
                       float* q_out, void* stream) {
   ACME_CHECK_ARG(l && obs && q_out && l->params, "null argument or unbound learner");
@@ -570,7 +620,10 @@ int acme_dqn_forward_backward(acme_dqn* l, const acme_transition_batch* batch,
   la.prio = prio;
   la.g = l->g;
   la.a_cache = l->a_cache;
-  if ((rc = launch_dqn_loss(la, st)) != ACME_OK) return rc;
+  {
+    ACME_PROF("loss", st, 0.0, 0.0);
+    if ((rc = launch_dqn_loss(la, st)) != ACME_OK) return rc;
+  }
   if (out && out->q_tm1)
     ACME_HIP_TRY(hipMemcpyAsync(out->q_tm1, l->q_on, (size_t)B * A * sizeof(float),
                                 hipMemcpyDeviceToDevice, st));
@@ -582,12 +635,15 @@ int acme_dqn_apply(acme_dqn* l, void* stream) {
   ACME_CHECK_ARG(l && l->params, "unbound learner");
   hipStream_t st = as_stream(stream);
   const int64_t t = l->num_steps + 1;  // snt.Adam increments its step before the update
+  ACME_PROF("adam", st, 0.0, 28.0 * (double)l->logical);
   int rc = acme_adam_update(l->params, l->grads, l->m, l->v, l->flat, l->cfg.learning_rate,
                             l->cfg.adam_beta1, l->cfg.adam_beta2, l->cfg.adam_epsilon, t, stream);
   if (rc != ACME_OK) return rc;
-  if (l->num_steps % l->cfg.target_update_period == 0)
+  if (l->num_steps % l->cfg.target_update_period == 0) {
+    ACME_PROF("target_copy", st, 0.0, 8.0 * (double)l->logical);
     ACME_HIP_TRY(hipMemcpyAsync(l->target, l->params, l->flat * sizeof(float),
                                 hipMemcpyDeviceToDevice, st));
+  }
   l->num_steps += 1;
   return ACME_OK;
 }

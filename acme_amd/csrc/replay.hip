@@ -29,6 +29,7 @@
 
 #include "common.h"
 #include "detmath.h"
+#include "profiler.h"
 
 using namespace acme;
 
@@ -558,6 +559,7 @@ int acme_replay_sample(acme_replay* r, int64_t batch, uint64_t step_counter, int
     return ACME_ERR_EMPTY;
   }
   hipStream_t st = as_stream(stream);
+  ACME_PROF("replay_sample", st, 0.0, (double)batch * (r->cfg.sampler == ACME_SAMPLER_PRIORITIZED ? 512.0 * r->nlevels + 40.0 : 48.0));
   if (r->cfg.sampler == ACME_SAMPLER_PRIORITIZED) {
     TreeView tv;
     for (int l = 0; l < 8; ++l) tv.level[l] = r->levels[l];
@@ -587,6 +589,9 @@ int acme_replay_gather(acme_replay* r, const int64_t* slots, int64_t batch,
   }
   // Wide (16-B multiple, >= 64 B) fields: one workgroup per row; consecutive wide
   // fields with the same row size share one launch (gridDim.y = field).
+  double row_bytes = 0;
+  for (int k = 0; k < r->cfg.num_fields; ++k) row_bytes += (double)r->cfg.field_bytes[k];
+  ACME_PROF("replay_gather", st, 0.0, 2.0 * row_bytes * (double)batch + 8.0 * (double)batch);
   int f = 0;
   while (f < r->cfg.num_fields) {
     const int64_t b = g.bytes[f];
@@ -629,6 +634,7 @@ int acme_replay_update_priorities(acme_replay* r, const uint64_t* keys, const do
   const unsigned g = (unsigned)ceil_div(n, 256);
   const double alpha =
       r->cfg.sampler == ACME_SAMPLER_PRIORITIZED ? r->cfg.priority_exponent : 0.0;
+  ACME_PROF("replay_update", st, 0.0, (double)n * (16.0 + 8.0 * 3 + 512.0 * (r->nlevels - 1)));
   prio_resolve_kernel<<<g, 256, 0, st>>>(keys, n, r->keys, r->cfg.capacity, t_slots, t_valid,
                                          r->winner);
   ACME_LAUNCH_CHECK();

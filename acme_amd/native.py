@@ -267,6 +267,13 @@ class NativeDQN:
     def num_steps(self, n: int) -> None:
         check(lib().acme_dqn_set_num_steps(self._h, int(n)))
 
+    def debug_buffer(self, name: str) -> np.ndarray:
+        p, n = ctypes.c_void_p(), ctypes.c_int64()
+        check(lib().acme_dqn_debug_buffer(self._h, name.encode(), ctypes.byref(p),
+                                          ctypes.byref(n)))
+        return _device_array(p.value, n.value, np.float32, self.device).cpu().numpy().view(
+            np.float32).copy()
+
     # --------------------------------------------------------------- step
     def _batch(self, o_tm1, a_tm1, r_t, d_t, o_t, probabilities, global_min_probability=None):
         B = int(a_tm1.shape[0])

@@ -1,0 +1,136 @@
+"""Network descriptors for the native learners.
+
+The reference builds Sonnet modules (acme/tf/networks/atari.py:36-69 DQNAtariNetwork,
+acme/tf/networks/duelling.py:27-59 DuellingMLP, snt.nets.MLP in
+examples/bsuite/run_dqn.py:46-49).  Here a network is a small descriptor: the learner's
+HIP kernels implement the layers, and the descriptor fixes the architecture, the input
+dtype and the initial parameters (Sonnet defaults: TruncatedNormal(stddev=1/sqrt(fan_in))
+weights, zero biases).
+
+Parameter naming follows the learner's flat buffer; `to_sonnet` /
+`from_sonnet` translate the fused duelling hidden layer to/from Sonnet's separate
+value/advantage MLP variables.
+"""
+
+from __future__ import annotations
+
+import dataclasses
+from typing import Dict, List, Sequence, Tuple
+
+import numpy as np
+
+
+def truncated_normal(rng: np.random.Generator, shape, stddev: float) -> np.ndarray:
+    """TruncatedNormal(0, stddev) cut at 2 stddev (snt.initializers.TruncatedNormal)."""
+    out = rng.standard_normal(shape)
+    bad = np.abs(out) > 2.0
+    while bad.any():
+        out[bad] = rng.standard_normal(int(bad.sum()))
+        bad = np.abs(out) > 2.0
+    return (out * stddev).astype(np.float32)
+
+
+@dataclasses.dataclass(frozen=True)
+class DQNAtariNetwork:
+    """AtariTorso + DuellingMLP(num_actions, hidden_sizes=[512]) on uint8 [84, 84, 4]."""
+
+    num_actions: int
+    obs_dtype: str = "uint8"  # uint8 frames scaled by 1/255 inside conv1, or "float32"
+    kind: str = dataclasses.field(default="nature", init=False)
+
+    def tensor_shapes(self) -> List[Tuple[str, Tuple[int, ...]]]:
+        A = self.num_actions
+        return [
+            ("atari_torso/conv2_d/w", (8, 8, 4, 32)), ("atari_torso/conv2_d/b", (32,)),
+            ("atari_torso/conv2_d_1/w", (4, 4, 32, 64)), ("atari_torso/conv2_d_1/b", (64,)),
+            ("atari_torso/conv2_d_2/w", (3, 3, 64, 64)), ("atari_torso/conv2_d_2/b", (64,)),
+            ("duelling_q_network/hidden/w", (7744, 1024)), ("duelling_q_network/hidden/b", (1024,)),
+            ("duelling_q_network/mlp/linear_1/w", (512, 1)),
+            ("duelling_q_network/mlp/linear_1/b", (1,)),
+            ("duelling_q_network/mlp_1/linear_1/w", (512, A)),
+            ("duelling_q_network/mlp_1/linear_1/b", (A,)),
+        ]
+
+    @property
+    def obs_shape(self) -> Tuple[int, ...]:
+        return (84, 84, 4)
+
+    def init(self, seed: int = 0) -> Dict[str, np.ndarray]:
+        rng = np.random.default_rng(seed)
+        out = {}
+        for name, shape in self.tensor_shapes():
+            if name.endswith("/b"):
+                out[name] = np.zeros(shape, np.float32)
+            else:
+                fan_in = int(np.prod(shape[:-1]))
+                out[name] = truncated_normal(rng, shape, 1.0 / np.sqrt(fan_in))
+        # The fused hidden layer is two Linear(7744 -> 512) layers side by side: the
+        # fan-in is 7744 for both halves, which the generic rule above already uses.
+        return out
+
+    def to_sonnet(self, params: Dict[str, np.ndarray]) -> Dict[str, np.ndarray]:
+        """Splits the fused hidden layer into Sonnet's value/advantage MLP variables."""
+        out = {k: v for k, v in params.items() if not k.startswith("duelling_q_network/hidden")}
+        w, b = params["duelling_q_network/hidden/w"], params["duelling_q_network/hidden/b"]
+        out["duelling_q_network/mlp/linear_0/w"] = w[:, :512]
+        out["duelling_q_network/mlp/linear_0/b"] = b[:512]
+        out["duelling_q_network/mlp_1/linear_0/w"] = w[:, 512:]
+        out["duelling_q_network/mlp_1/linear_0/b"] = b[512:]
+        return out
+
+    def from_sonnet(self, variables: Dict[str, np.ndarray]) -> Dict[str, np.ndarray]:
+        out = {k: v for k, v in variables.items() if "/linear_0/" not in k}
+        out["duelling_q_network/hidden/w"] = np.concatenate(
+            [variables["duelling_q_network/mlp/linear_0/w"],
+             variables["duelling_q_network/mlp_1/linear_0/w"]], axis=1)
+        out["duelling_q_network/hidden/b"] = np.concatenate(
+            [variables["duelling_q_network/mlp/linear_0/b"],
+             variables["duelling_q_network/mlp_1/linear_0/b"]])
+        return out
+
+
+@dataclasses.dataclass(frozen=True)
+class MLP:
+    """snt.Sequential([snt.Flatten(), snt.nets.MLP([*hidden, num_actions])])."""
+
+    obs_dim: int
+    hidden: Tuple[int, ...]
+    num_actions: int
+    obs_dtype: str = "float32"
+    kind: str = dataclasses.field(default="mlp", init=False)
+
+    def __init__(self, obs_dim: int, hidden: Sequence[int], num_actions: int,
+                 obs_dtype: str = "float32"):
+        object.__setattr__(self, "obs_dim", int(obs_dim))
+        object.__setattr__(self, "hidden", tuple(int(h) for h in hidden))
+        object.__setattr__(self, "num_actions", int(num_actions))
+        object.__setattr__(self, "obs_dtype", obs_dtype)
+        object.__setattr__(self, "kind", "mlp")
+
+    def tensor_shapes(self):
+        out, d = [], self.obs_dim
+        for i, h in enumerate(list(self.hidden) + [self.num_actions]):
+            out.append((f"mlp/linear_{i}/w", (d, h)))
+            out.append((f"mlp/linear_{i}/b", (h,)))
+            d = h
+        return out
+
+    @property
+    def obs_shape(self) -> Tuple[int, ...]:
+        return (self.obs_dim,)
+
+    def init(self, seed: int = 0) -> Dict[str, np.ndarray]:
+        rng = np.random.default_rng(seed)
+        out = {}
+        for name, shape in self.tensor_shapes():
+            if name.endswith("/b"):
+                out[name] = np.zeros(shape, np.float32)
+            else:
+                out[name] = truncated_normal(rng, shape, 1.0 / np.sqrt(shape[0]))
+        return out
+
+    def to_sonnet(self, params):
+        return dict(params)
+
+    def from_sonnet(self, variables):
+        return dict(variables)

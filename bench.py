@@ -1,0 +1,263 @@
+#!/usr/bin/env python3
+"""Learner throughput benchmark: sampled transitions/sec through DQN Learner.step().
+
+Workload (BASELINE.json configs[1]): Nature-CNN DQN
+(DQNAtariNetwork, 18 actions), synthetic uint8 [84, 84, 4] transitions in a 1,000,000-slot
+GPU-resident prioritized replay (alpha 0.6, beta 0.2, n-step discount 0.99^4), batch 512
+per GPU, Adam lr 1e-3, target period 100.  One "step" = prioritized sample + gather of the
+(o_tm1, a, r, d, o_t) batch + the full learner step (3 Q forwards, double-Q TD, Huber,
+f64 IS weights, backward, Adam, periodic target copy) + priority write-back — exactly the
+work of DQNLearner._step (acme/agents/tf/dqn/learning.py:112-168) plus its iterator.
+
+N > 1 (torchrun, one process per GPU): the 1M-slot replay is sharded 1/N per rank, every
+rank draws its own 512 (weak scaling, global batch 512 N), the IS-weight normaliser is
+all-reduced (MIN of probabilities) and the gradients are all-reduced (AVG) over RCCL
+before Adam, so every replica applies the identical update.
+
+Prints ONE JSON line on rank 0 (contract in the task statement / DESIGN.md §6).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "learner transitions/sec (sample+step) at batch 512, 1/2/4/8 MI355X"
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 (spec)
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+OBS_BYTES = 84 * 84 * 4
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--batch", type=int, default=512)
+    p.add_argument("--replay-size", type=int, default=1_000_000)
+    p.add_argument("--num-actions", type=int, default=18)
+    p.add_argument("--no-profile", action="store_true", help="disable the section profiler")
+    p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(batch: int, num_actions: int, seconds: float):
+    """The numpy oracle (oracle/dqn_oracle.py, float32) timed on the host cores on a bounded
+    sample: a 16,384-slot host replay with the C oracle's prioritized sum tree, batch 512,
+    as many full steps as fit in `seconds` (at least 2; the first is a warm-up)."""
+    from oracle import dqn_oracle as O
+    from tests._oracle import OracleTable
+    from acme_amd.networks import DQNAtariNetwork
+    try:
+        from threadpoolctl import threadpool_limits
+    except ImportError:  # pragma: no cover
+        threadpool_limits = None
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    ctx = threadpool_limits(threads) if threadpool_limits else None
+    rng = np.random.default_rng(0)
+    cap = 16384
+    obs = rng.integers(0, 256, (cap, 84, 84, 4), dtype=np.uint8)
+    nxt = rng.integers(0, 256, (cap, 84, 84, 4), dtype=np.uint8)
+    act = rng.integers(0, num_actions, cap).astype(np.int32)
+    rew = rng.standard_normal(cap).astype(np.float32)
+    dis = np.where(rng.random(cap) < 0.01, 0, np.float32(0.99) ** 4).astype(np.float32)
+    table = OracleTable(cap, True, 0.6, 1234)
+    table.insert(np.ones(cap))
+    net = DQNAtariNetwork(num_actions)
+    p = net.init(0)
+    state = dict(params=p, target={k: v.copy() for k, v in p.items()},
+                 m={k: np.zeros_like(v) for k, v in p.items()},
+                 v={k: np.zeros_like(v) for k, v in p.items()}, num_steps=0)
+    cfg = O.DQNConfig(num_actions=num_actions)
+
+    def one(step):
+        s = table.sample(batch, step)
+        k = s["slots"]
+        b = dict(o_tm1=obs[k], a_tm1=act[k], r_t=rew[k], d_t=dis[k], o_t=nxt[k],
+                 probabilities=s["probabilities"])
+        out, _, new_state = O.dqn_step(cfg, state, b, np.float32)
+        table.update(s["keys"], out["priorities"])
+        return new_state
+
+    state = one(0)  # warm-up (page faults, BLAS init)
+    t0 = time.perf_counter()
+    n = 0
+    while n < 2 or time.perf_counter() - t0 < seconds:
+        state = one(n + 1)
+        n += 1
+    dt = time.perf_counter() - t0
+    if ctx is not None:
+        ctx.unregister() if hasattr(ctx, "unregister") else None
+    return dict(value=round(batch * n / dt, 2), unit="transitions/s", cores=threads,
+                kind="port",
+                sample=(f"numpy float32 oracle (oracle/dqn_oracle.py) + C sum-tree oracle, "
+                        f"{n} timed steps x batch {batch} on a {cap}-slot host replay, "
+                        f"{threads} BLAS threads, {cpu_model()}"))
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist = None
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from acme_amd import _lib
+    from acme_amd.native import NativeDQN, NativeReplay
+    from acme_amd.networks import DQNAtariNetwork
+    L = _lib.lib()
+
+    B, A = args.batch, args.num_actions
+    shard = -(-args.replay_size // world)
+    t_fill = time.perf_counter()
+    replay = NativeReplay(shard, [OBS_BYTES, 4, 4, 4, OBS_BYTES], prioritized=True,
+                          priority_exponent=0.6, seed=1234 + rank, device=dev)
+    replay.fill_synthetic(shard, layout=0, num_actions=A, seed=rank)
+    learner = NativeDQN(network="nature", num_actions=A, max_batch=B, obs_dtype="uint8",
+                        discount=0.99, importance_sampling_exponent=0.2, learning_rate=1e-3,
+                        target_update_period=100, device=dev)
+    net = DQNAtariNetwork(A)
+    p0 = net.init(seed=0)  # identical on every rank
+    learner.set_params(p0, p0)
+    torch.cuda.synchronize(dev)
+    t_fill = time.perf_counter() - t_fill
+
+    info = replay.alloc_sample_info(B)
+    o_tm1 = torch.empty(B, OBS_BYTES, dtype=torch.uint8, device=dev)
+    a_tm1 = torch.empty(B, dtype=torch.int32, device=dev)
+    r_t = torch.empty(B, dtype=torch.float32, device=dev)
+    d_t = torch.empty(B, dtype=torch.float32, device=dev)
+    o_t = torch.empty(B, OBS_BYTES, dtype=torch.uint8, device=dev)
+    gmin = torch.empty(1, dtype=torch.float64, device=dev) if world > 1 else None
+    stream = torch.cuda.current_stream(dev)
+
+    def step(i):
+        replay.sample(B, i, out=info, stream=stream)
+        replay.gather(info["slots"], [o_tm1, a_tm1, r_t, d_t, o_t], stream=stream)
+        if world > 1:
+            _lib.check(L.acme_min_f64(info["probabilities"].data_ptr(), B, gmin.data_ptr(),
+                                      _lib.stream_ptr(stream)))
+            dist.all_reduce(gmin, op=dist.ReduceOp.MIN)
+        learner.forward_backward(o_tm1, a_tm1, r_t, d_t, o_t, info["probabilities"],
+                                 global_min_probability=gmin, stream=stream)
+        if world > 1:
+            dist.all_reduce(learner.grads, op=dist.ReduceOp.AVG)
+        learner.apply(stream=stream)
+        replay.update_priorities(info["keys"], learner.priorities[:B], stream=stream)
+
+    for i in range(args.warmup):
+        step(i)
+    if not args.no_profile:
+        L.acme_profile_enable(1)
+        L.acme_profile_reset()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    L.acme_profile_enable(0)
+    loss = float(learner.loss.item())
+
+    sections = []
+    for i in range(L.acme_profile_num_sections()):
+        import ctypes
+        nm, ms, cnt = ctypes.c_char_p(), ctypes.c_double(), ctypes.c_int64()
+        fl, by = ctypes.c_double(), ctypes.c_double()
+        _lib.check(L.acme_profile_query(i, ctypes.byref(nm), ctypes.byref(ms), ctypes.byref(cnt),
+                                        ctypes.byref(fl), ctypes.byref(by)))
+        if cnt.value == 0:
+            continue
+        avg_ms = ms.value / cnt.value
+        rec = dict(name=nm.value.decode(), launches=int(cnt.value), avg_us=round(1e3 * avg_ms, 2),
+                   total_ms=round(ms.value, 3))
+        if fl.value > 0:
+            tf = fl.value / cnt.value / (avg_ms * 1e-3) / 1e12
+            rec.update(bound="mfma", achieved=round(tf, 2), unit="TFLOP/s",
+                       frac=round(tf / FP32_MFMA_PEAK_TFLOPS, 4))
+        elif by.value > 0:
+            gbs = by.value / cnt.value / (avg_ms * 1e-3) / 1e9
+            rec.update(bound="hbm", achieved=round(gbs, 1), unit="GB/s",
+                       frac=round(gbs / HBM_PEAK_GBS, 4))
+        sections.append(rec)
+    sections.sort(key=lambda r: -r["total_ms"])
+
+    ms_per_step = 1e3 * elapsed / args.steps
+    value = world * B * args.steps / elapsed
+    roofline = None
+    mfma = [s for s in sections if s.get("bound") == "mfma"]
+    if mfma:
+        dom = mfma[0]
+        roofline = dict(bound="mfma", kernel=dom["name"], achieved=dom["achieved"],
+                        peak=FP32_MFMA_PEAK_TFLOPS, unit="TFLOP/s", frac=dom["frac"],
+                        traffic=None, avg_us=dom["avg_us"])
+    if rank == 0:
+        for s in sections:
+            print(f"[bench] {s['name']:16s} {s['launches']:6d} x {s['avg_us']:9.2f} us  "
+                  f"{s.get('achieved', '')} {s.get('unit', '')} frac={s.get('frac', '')}",
+                  file=sys.stderr)
+        print(f"[bench] replay fill {t_fill:.1f}s, final loss {loss:.5f}", file=sys.stderr)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(B, A, args.cpu_baseline_seconds)
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 1), "unit": "transitions/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (device-generated uint8 Atari-shape transitions, random-init "
+                    "Nature-CNN weights)",
+            "config": {"workload": "dqn_nature_cnn_prioritized_replay (BASELINE configs[1])",
+                       "global_batch": B * world, "batch_per_gpu": B,
+                       "replay_slots": args.replay_size, "replay_slots_per_gpu": shard,
+                       "obs": "uint8[84,84,4]", "num_actions": A,
+                       "sampler": "prioritized(alpha=0.6), IS beta=0.2",
+                       "parallelism": f"dp{world}"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "kernels": sections,
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -186,11 +186,25 @@ int acme_dqn_step(acme_dqn* l, const acme_transition_batch* batch,
 int acme_dqn_q_values(acme_dqn* l, const void* obs, int64_t batch, int32_t use_target,
                       float* q_out, void* stream);
 int64_t acme_dqn_num_steps(const acme_dqn* l);
+/* Device pointer + element count of an internal f32 workspace (tests / diagnostics):
+ * "x1" "x2" "x3" "hid" (online activations, 2B rows), "dzh" "dz3" "dz2" "dz1" (layer
+ * pre-activation gradients, B rows), "q_on", "q_tg", "g". */
+int acme_dqn_debug_buffer(const acme_dqn* l, const char* name, const float** out,
+                          int64_t* count);
 int acme_dqn_set_num_steps(acme_dqn* l, int64_t n);
 /* Minimum of a device f64 array (for the data-parallel IS normaliser). */
 int acme_min_f64(const double* x, int64_t n, double* out_dev, void* stream);
 
 /* ----------------------------------------------------------- elementwise ops -- */
+
+/* ------------------------------------------------------------- profiling -- */
+/* Section profiler: when enabled, every kernel section records a HIP event pair on the
+ * stream it is launched on, tagged with its algorithmic FLOPs / HBM bytes. */
+int acme_profile_enable(int32_t on);
+int acme_profile_reset(void);
+int32_t acme_profile_num_sections(void);
+int acme_profile_query(int32_t i, const char** name, double* total_ms, int64_t* count,
+                       double* flops, double* bytes);
 
 /* snt.optimizers.Adam update over a flat f32 buffer (t = 1-based step). */
 int acme_adam_update(float* params, const float* grads, float* m, float* v, int64_t n,

@@ -148,7 +148,13 @@ def nature_forward(params: Dict[str, np.ndarray], o: np.ndarray, dtype):
     return q, cache
 
 
-def nature_backward(params, cache, dq, dtype) -> Dict[str, np.ndarray]:
+def nature_backward(params, cache, dq, dtype, masks=None) -> Dict[str, np.ndarray]:
+    """Backward pass.  `masks` (optional) overrides the ReLU branch decisions (x > 0) of
+    the named activations ("hid", "x3", "x2", "x1") — used by the parity tests to check
+    the backward pass conditional on the kernel's own ReLU pattern, since fp32 and fp64
+    legitimately disagree for pre-activations within rounding of 0."""
+    masks = masks or {}
+    mask = lambda key, x: masks[key] if key in masks else (x > 0)  # noqa: E731
     g = {}
     h = cache["h"]
     hv, ha = h[:, :512], h[:, 512:]
@@ -160,11 +166,13 @@ def nature_backward(params, cache, dq, dtype) -> Dict[str, np.ndarray]:
     g["duelling_q_network/mlp/linear_1/b"] = dv.sum(0)
     g["duelling_q_network/mlp_1/linear_1/w"] = ha.T @ dadv
     g["duelling_q_network/mlp_1/linear_1/b"] = dadv.sum(0)
-    dh = np.concatenate([dv @ wv.T, dadv @ wa.T], axis=1) * (h > 0)
+    dh = np.concatenate([dv @ wv.T, dadv @ wa.T], axis=1) * mask("hid", h)
+    cache["dzh"] = dh
     g["duelling_q_network/hidden/w"] = cache["flat"].T @ dh
     g["duelling_q_network/hidden/b"] = dh.sum(0)
     dflat = dh @ params["duelling_q_network/hidden/w"].astype(dtype).T
-    dx = dflat.reshape(cache["x3"].shape) * (cache["x3"] > 0)
+    dx = dflat.reshape(cache["x3"].shape) * mask("x3", cache["x3"])
+    cache["dz3"] = dx
     for li in (2, 1, 0):
         name, s, pads = CONVS[li]
         w = params[name + "/w"].astype(dtype)
@@ -176,7 +184,8 @@ def nature_backward(params, cache, dq, dtype) -> Dict[str, np.ndarray]:
         if li > 0:
             dcols = dz @ w.reshape(-1, co).T
             xin = cache[f"x{li}"]
-            dx = _col2im(dcols, meta, kh, kw, s, pads, xin.shape) * (xin > 0)
+            dx = _col2im(dcols, meta, kh, kw, s, pads, xin.shape) * mask(f"x{li}", xin)
+            cache[f"dz{li}"] = dx
     return g
 
 
@@ -190,13 +199,15 @@ def mlp_forward(params, o, dtype, n_layers):
     return x, {"acts": acts}
 
 
-def mlp_backward(params, cache, dq, dtype, n_layers):
+def mlp_backward(params, cache, dq, dtype, n_layers, masks=None):
+    masks = masks or {}
     g, acts, dz = {}, cache["acts"], dq
     for i in reversed(range(n_layers)):
         g[f"mlp/linear_{i}/w"] = acts[i].T @ dz
         g[f"mlp/linear_{i}/b"] = dz.sum(0)
         if i > 0:
-            dz = (dz @ params[f"mlp/linear_{i}/w"].astype(dtype).T) * (acts[i] > 0)
+            m = masks.get(f"act{i - 1}", acts[i] > 0)
+            dz = (dz @ params[f"mlp/linear_{i}/w"].astype(dtype).T) * m
     return g
 
 
@@ -226,14 +237,14 @@ def forward(cfg: DQNConfig, params, o, dtype):
     return mlp_forward(params, o, dtype, len(cfg.hidden) + 1)
 
 
-def backward(cfg: DQNConfig, params, cache, dq, dtype):
+def backward(cfg: DQNConfig, params, cache, dq, dtype, masks=None):
     if cfg.network == "nature":
-        return nature_backward(params, cache, dq, dtype)
-    return mlp_backward(params, cache, dq, dtype, len(cfg.hidden) + 1)
+        return nature_backward(params, cache, dq, dtype, masks)
+    return mlp_backward(params, cache, dq, dtype, len(cfg.hidden) + 1, masks)
 
 
 def dqn_loss_and_grads(cfg: DQNConfig, params, target, batch, dtype=np.float64,
-                       global_min_probability: Optional[float] = None):
+                       global_min_probability: Optional[float] = None, masks=None):
     """Forward + backward of DQNLearner._step; returns (outputs, grads)."""
     o_tm1, a, r, d, o_t = (batch[k] for k in ("o_tm1", "a_tm1", "r_t", "d_t", "o_t"))
     probs = np.asarray(batch["probabilities"], np.float64)
@@ -260,8 +271,8 @@ def dqn_loss_and_grads(cfg: DQNConfig, params, target, batch, dtype=np.float64,
     B = len(a)
     dq = np.zeros_like(q_tm1)
     dq[bidx, a] = -(iw * np.clip(td, -delta, delta)) / B
-    grads = backward(cfg, params, cache, dq, dtype)
-    out = dict(loss=loss, td_error=td, priorities=np.abs(td).astype(np.float64), q_tm1=q_tm1,
+    grads = backward(cfg, params, cache, dq, dtype, masks)
+    out = dict(cache=cache, loss=loss, td_error=td, priorities=np.abs(td).astype(np.float64), q_tm1=q_tm1,
                q_t_value=q_t_value, q_t_selector=q_t_selector, importance_weights=iw)
     return out, grads
 
