@@ -37,12 +37,19 @@ struct Geom {
 // acme/wrappers/atari_wrapper.py:284-306) or f32 activations.
 struct InU8 {
   using T = uint8_t;
+  // float32(x / 255.0) for a byte x: reciprocal multiply + one fma residual correction,
+  // which equals the correctly rounded quotient for all 256 byte values (checked
+  // exhaustively, tests/test_oracle_cpu.py::test_u8_scaling_exact).
+  __device__ static __forceinline__ float scale(uint32_t x) {
+    const float xf = (float)x;
+    const float c = 1.0f / 255.0f;
+    const float q = xf * c;
+    return __builtin_fmaf(__builtin_fmaf(-q, 255.0f, xf), c, q);
+  }
   __device__ static __forceinline__ f32x4 load4(const uint8_t* p) {
     const uint32_t w = *reinterpret_cast<const uint32_t*>(p);
-    // float32(x / 255.0): exact for all 256 byte values via the correctly rounded
-    // f32 division (checked exhaustively, tests/test_oracle_cpu.py).
-    return f32x4{__fdiv_rn((float)(w & 0xff), 255.f), __fdiv_rn((float)((w >> 8) & 0xff), 255.f),
-                 __fdiv_rn((float)((w >> 16) & 0xff), 255.f), __fdiv_rn((float)(w >> 24), 255.f)};
+    return f32x4{scale(w & 0xff), scale((w >> 8) & 0xff), scale((w >> 16) & 0xff),
+                 scale(w >> 24)};
   }
 };
 struct InF32 {
@@ -105,10 +112,11 @@ struct ConvFwd {
 template <class G, class In>
 struct ConvWgrad {
   static constexpr int A_MODE = RCONTIG, B_MODE = RCONTIG;
+  static constexpr bool kColSum = true;  // bias gradient = column sums of dZ
   int M, N, K, k_chunk;  // M = G::K rows (kh,kw,ci), N = CO, K = batch * OPIX
   const typename In::T* x;
   const float* dz;  // [batch * OPIX][CO]
-  float* slab;      // [splits][M][N]
+  float* slab;      // [splits][M + 1][N]; row M holds the split's bias-gradient partial
   struct ARow {
     int dh, dw, ci;
     bool ok;
@@ -141,11 +149,81 @@ struct ConvWgrad {
     return *reinterpret_cast<const f32x4*>(dz + (size_t)m * G::CO + b.n);
   }
   __device__ void store(int i, int n, float v, int split) const {
-    slab[((size_t)split * M + i) * N + n] = v;
+    slab[((size_t)split * (M + 1) + i) * N + n] = v;
+  }
+  __device__ void store_colsum(int n, float v, int split) const {
+    slab[((size_t)split * (M + 1) + M) * N + n] = v;
   }
 };
 
 // ------------------------------------------------------------------ input grad
+// Stride-S input gradient by sub-pixel decomposition: input pixels are grouped by
+// parity class (PH, PW) = ((ih + PT) mod S, (iw + PL) mod S); within a class only the
+// taps kh = PH + S*jh, kw = PW + S*jw contribute, so each class is a dense implicit GEMM
+// with reduction (KH/S)*(KW/S)*CO instead of KH*KW*CO with (S^2-1)/S^2 zeros.
+template <class G, int PH, int PW>
+struct ConvDgradSub {
+  static_assert(G::KH % G::S == 0 && G::KW % G::S == 0, "kernel must be a multiple of stride");
+  static constexpr int A_MODE = KCONTIG, B_MODE = KCONTIG;
+  static constexpr int S = G::S;
+  static constexpr int RH = ((PH - G::PT) % S + S) % S;  // first ih of the class
+  static constexpr int RW = ((PW - G::PL) % S + S) % S;
+  static constexpr int NH = (G::IH - RH + S - 1) / S;    // class rows
+  static constexpr int NW = (G::IW - RW + S - 1) / S;
+  static constexpr int JH = G::KH / S, JW = G::KW / S;
+  static constexpr int KR = JH * JW * G::CO;             // reduction length
+  int M, N, K, k_chunk;  // M = batch * NH * NW, N = CI, K = KR
+  const float* dz;
+  const float* w;
+  const float* xprev;
+  float* dx;
+  struct ARow {
+    const float* base;
+    int oh0, ow0;  // (ih + PT - PH) / S, (iw + PL - PW) / S
+    bool ok;
+  };
+  struct BRow {
+    int ci;
+  };
+  __device__ static void decode(int m, int& b, int& ih, int& iw) {
+    b = m / (NH * NW);
+    const int rem = m - b * (NH * NW);
+    const int i = rem / NW, j = rem - i * NW;
+    ih = RH + S * i;
+    iw = RW + S * j;
+  }
+  __device__ ARow a_row(int m) const {
+    ARow a;
+    a.ok = m < M;
+    int b, ih, iw;
+    decode(a.ok ? m : 0, b, ih, iw);
+    a.base = dz + (size_t)b * G::OPIX * G::CO;
+    a.oh0 = (ih + G::PT - PH) / S;
+    a.ow0 = (iw + G::PL - PW) / S;
+    return a;
+  }
+  __device__ f32x4 a_load(const ARow& a, int k) const {
+    const int jh = k / (JW * G::CO), r = k - jh * (JW * G::CO);
+    const int jw = r / G::CO, co = r - jw * G::CO;
+    const int oh = a.oh0 - jh, ow = a.ow0 - jw;
+    if (!a.ok || (unsigned)oh >= (unsigned)G::OH || (unsigned)ow >= (unsigned)G::OW) return zero4();
+    return *reinterpret_cast<const f32x4*>(a.base + (oh * G::OW + ow) * G::CO + co);
+  }
+  __device__ BRow b_row(int ci) const { return BRow{ci}; }
+  __device__ f32x4 b_load(const BRow& b, int k) const {
+    if (b.ci >= N) return zero4();
+    const int jh = k / (JW * G::CO), r = k - jh * (JW * G::CO);
+    const int jw = r / G::CO, co = r - jw * G::CO;
+    const int kh = PH + S * jh, kw = PW + S * jw;
+    return *reinterpret_cast<const f32x4*>(w + ((size_t)(kh * G::KW + kw) * G::CI + b.ci) * G::CO + co);
+  }
+  __device__ void store(int m, int ci, float v, int) const {
+    int b, ih, iw;
+    decode(m, b, ih, iw);
+    const size_t idx = ((size_t)b * G::IPIX + ih * G::IW + iw) * G::CI + ci;
+    dx[idx] = xprev[idx] > 0.f ? v : 0.f;
+  }
+};
 template <class G>
 struct ConvDgrad {
   static constexpr int A_MODE = KCONTIG, B_MODE = KCONTIG;
@@ -222,6 +300,7 @@ struct DenseFwd {
   const float* bias;
   float* y;
   int act;
+  float* slab = nullptr;  // split-K: raw partial sums [splits][M][N]; finalised later
   struct ARow {
     const typename In::T* p;
   };
@@ -237,7 +316,7 @@ struct DenseFwd {
     if constexpr (sizeof(typename In::T) == 1) {
       if (VEC) return In::load4(a.p + k);
       f32x4 r;
-      for (int j = 0; j < 4; ++j) r[j] = (k + j < K) ? __fdiv_rn((float)a.p[k + j], 255.f) : 0.f;
+      for (int j = 0; j < 4; ++j) r[j] = (k + j < K) ? In::scale(a.p[k + j]) : 0.f;
       return r;
     } else {
       return load_row4<VEC>(reinterpret_cast<const float*>(a.p), k, K);
@@ -248,21 +327,29 @@ struct DenseFwd {
     if (b.n >= N || k >= K) return zero4();
     return load_row4<VEC>(w + (size_t)k * N, b.n, N);
   }
-  __device__ void store(int m, int n, float v, int) const {
+  __device__ void store(int m, int n, float v, int split) const {
+    if (slab) {
+      slab[((size_t)split * M + m) * N + n] = v;
+      return;
+    }
     v += bias[n];
     if (act == ACT_RELU) v = v > 0.f ? v : 0.f;
     y[(size_t)m * N + n] = v;
   }
 };
 
+// Weight gradient of a dense layer, single split: dW = X^T dZ written straight into the
+// gradient buffer, bias gradient = column sums of dZ (LDS colsum hook).
 template <bool VEC, class In = InF32>
 struct DenseWgrad {
   static constexpr int A_MODE = RCONTIG, B_MODE = RCONTIG;
+  static constexpr bool kColSum = true;
   int M, N, K, k_chunk;  // M = Kin, N = Nout, K = rows (batch)
   const typename In::T* x;
   int ldx;
   const float* dz;  // [batch][N]
-  float* out;       // [splits][M][N] (or the gradient buffer when splits == 1)
+  float* out;       // [M][N] weight gradient
+  float* bias_out;  // [N] bias gradient
   struct ARow {
     int i;
   };
@@ -276,7 +363,7 @@ struct DenseWgrad {
       const uint8_t* p = reinterpret_cast<const uint8_t*>(x) + (size_t)m * ldx;
       if (VEC) return In::load4(p + a.i);
       f32x4 r;
-      for (int j = 0; j < 4; ++j) r[j] = (a.i + j < M) ? __fdiv_rn((float)p[a.i + j], 255.f) : 0.f;
+      for (int j = 0; j < 4; ++j) r[j] = (a.i + j < M) ? In::scale(p[a.i + j]) : 0.f;
       return r;
     } else {
       return load_row4<VEC>(reinterpret_cast<const float*>(x) + (size_t)m * ldx, a.i, M);
@@ -287,9 +374,8 @@ struct DenseWgrad {
     if (b.n >= N || m >= K) return zero4();
     return load_row4<VEC>(dz + (size_t)m * N, b.n, N);
   }
-  __device__ void store(int i, int n, float v, int split) const {
-    out[((size_t)split * M + i) * N + n] = v;
-  }
+  __device__ void store(int i, int n, float v, int) const { out[(size_t)i * N + n] = v; }
+  __device__ void store_colsum(int n, float v, int) const { bias_out[n] = v; }
 };
 
 template <bool VEC>
@@ -321,6 +407,92 @@ struct DenseDgrad {
     const size_t idx = (size_t)m * ldx + n;
     if (xprev) v = xprev[idx] > 0.f ? v : 0.f;
     dx[idx] = v;
+  }
+};
+
+// ------------------------------------------------------------------ duelling head
+// DuellingMLP's two output layers (acme/tf/networks/duelling.py:37-57) as ONE skinny
+// GEMM over the fused hidden layer h [rows][2H]: output column a < A is the advantage
+// (weights wa on the advantage half of h), column A the value (wv on the value half).
+// The block-diagonal B operand is synthesised by the loader from the two weight
+// tensors.  Split-K partials go to a slab; duel_head_finish applies biases and
+// q = v + (adv - mean(adv)).
+struct DuelHeadFwd {
+  static constexpr int A_MODE = KCONTIG, B_MODE = RCONTIG;
+  int M, N, K, k_chunk;  // M = rows, N = A + 1, K = 2H
+  int H, A;
+  const float* h;
+  const float* wv;  // [H]
+  const float* wa;  // [H][A]
+  float* slab;      // [splits][M][A + 1]
+  struct ARow {
+    const float* p;
+  };
+  struct BRow {
+    int n;
+  };
+  __device__ ARow a_row(int m) const { return ARow{m < M ? h + (size_t)m * K : nullptr}; }
+  __device__ f32x4 a_load(const ARow& a, int k) const {
+    if (!a.p) return zero4();
+    return *reinterpret_cast<const f32x4*>(a.p + k);
+  }
+  __device__ BRow b_row(int n) const { return BRow{n}; }
+  __device__ float wt(int n, int k) const {
+    if (n < A) return k >= H ? wa[(size_t)(k - H) * A + n] : 0.f;
+    if (n == A) return k < H ? wv[k] : 0.f;
+    return 0.f;
+  }
+  __device__ f32x4 b_load(const BRow& b, int k) const {
+    return f32x4{wt(b.n, k), wt(b.n + 1, k), wt(b.n + 2, k), wt(b.n + 3, k)};
+  }
+  __device__ void store(int m, int n, float v, int split) const {
+    slab[((size_t)split * M + m) * N + n] = v;
+  }
+};
+
+// Head weight gradients: rows = hidden feature k (2H), columns = head outputs (A + 1),
+// reduction over the batch: G[k][n] = sum_b h[b][k] dq_ext[b][n] with
+// dq_ext[b][a < A] = g_b (1[a == a_b] - 1/A) (advantage, mean-subtracted) and
+// dq_ext[b][A] = g_b (value).  The block-diagonal parts are the weight gradients and the
+// column sums of dq_ext the bias gradients (colsum hook).
+struct DuelHeadWgrad {
+  static constexpr int A_MODE = RCONTIG, B_MODE = RCONTIG;
+  static constexpr bool kColSum = true;
+  int M, N, K, k_chunk;  // M = 2H, N = A + 1, K = batch
+  int A;
+  const float* h;        // [batch][2H]
+  const float* g;        // [batch]
+  const int32_t* act;    // [batch]
+  float* slab;           // [splits][M + 1][N]
+  struct ARow {
+    int i;
+  };
+  struct BRow {
+    int n;
+  };
+  __device__ ARow a_row(int i) const { return ARow{i}; }
+  __device__ f32x4 a_load(const ARow& a, int b) const {
+    if (a.i >= M) return zero4();
+    return *reinterpret_cast<const f32x4*>(h + (size_t)b * M + a.i);
+  }
+  __device__ BRow b_row(int n) const { return BRow{n}; }
+  __device__ f32x4 b_load(const BRow& r, int b) const {
+    const float gb = g[b];
+    const int ab = act[b];
+    const float inv_a = 1.f / (float)A;
+    f32x4 out;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = r.n + j;
+      out[j] = n < A ? gb * ((n == ab ? 1.f : 0.f) - inv_a) : (n == A ? gb : 0.f);
+    }
+    return out;
+  }
+  __device__ void store(int i, int n, float v, int split) const {
+    slab[((size_t)split * (M + 1) + i) * N + n] = v;
+  }
+  __device__ void store_colsum(int n, float v, int split) const {
+    slab[((size_t)split * (M + 1) + M) * N + n] = v;
   }
 };
 

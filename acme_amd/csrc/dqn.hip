@@ -76,8 +76,6 @@ struct acme_dqn {
   float *dzh = nullptr, *dz3 = nullptr, *dz2 = nullptr, *dz1 = nullptr;
   float* slab = nullptr;
   int64_t slab_floats = 0;
-  float* colsum = nullptr;
-  int64_t colsum_floats = 0;
   float* g = nullptr;  // per-sample dLoss/dq_tm1[a]
   int32_t* a_cache = nullptr;  // actions of the current batch (for the backward kernels)
   float* loss_tmp = nullptr;
@@ -146,12 +144,35 @@ inline int chunk_for(int K, int splits) {
 #define ACME_GEMM_N(name, BM, BN, WM, WN, prob, splits) \
   ACME_GEMM_F(name, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, BM, BN, WM, WN, prob, splits)
 
+// Split counts (K-splits) of the launches whose natural grid is too small to fill 256 CUs.
+constexpr int kFcFwdSplits = 4;     // [rows, 1024] x K 7744: 16x16 tiles x 4 = 1024 blocks
+constexpr int kHeadFwdSplits = 16;  // [rows, A+1] x K 1024
+constexpr int kHeadBwdSplits = 8;   // [1024, A+1] x K = batch
+constexpr int kConv1WgradSplits = 256, kConv2WgradSplits = 64, kConv3WgradSplits = 64;
+
+int64_t slab_floats_needed(int B, int A) {
+  return std::max<int64_t>({(int64_t)kConv1WgradSplits * (G1::K + 1) * G1::CO,
+                            (int64_t)kConv2WgradSplits * (G2::K + 1) * G2::CO,
+                            (int64_t)kConv3WgradSplits * (G3::K + 1) * G3::CO,
+                            (int64_t)kFcFwdSplits * 2 * B * 2 * kHidden,
+                            (int64_t)kHeadFwdSplits * 2 * B * (A + 1),
+                            (int64_t)kHeadBwdSplits * (2 * kHidden + 1) * (A + 1)});
+}
+
+int slab_reduce(const float* slab, int splits, int64_t count, float* out0, int64_t split_at,
+                float* out1, const float* bias, int ncols, int relu, const char* name,
+                hipStream_t st) {
+  ACME_PROF(name, st, 0.0, 4.0 * (double)(splits + 1) * (double)count);
+  return launch_slab_reduce(slab, splits, count, out0, split_at, out1, bias, ncols, relu, st);
+}
+
 // ---------------------------------------------------------------- Nature forward
 // rows = number of observations; first `split` rows from obs_a, the rest from obs_b.
 int nature_forward(acme_dqn* l, const float* prm, const void* obs_a, const void* obs_b,
                    int split, int rows, float* x1, float* x2, float* x3, float* hid,
                    float* q, hipStream_t st) {
   const bool u8 = l->cfg.obs_dtype == ACME_OBS_U8_SCALED;
+  const int A = l->cfg.num_actions;
   if (u8) {
     ConvFwd<G1, InU8> p;
     p.M = rows * G1::OPIX; p.N = G1::CO; p.K = G1::K; p.k_chunk = G1::K;
@@ -179,22 +200,34 @@ int nature_forward(acme_dqn* l, const float* prm, const void* obs_a, const void*
     p.bias = P(l, prm, l->t_c3b); p.y = x3;
     ACME_GEMM_N("conv3_fwd", 128, 64, 2, 2, p, 1);
   }
-  {
+  {  // Fused duelling hidden layer, split-K partials then bias + ReLU in the reduction.
     DenseFwd<true> p;
-    p.M = rows; p.N = 2 * kHidden; p.K = kFlat; p.k_chunk = kFlat;
+    p.M = rows; p.N = 2 * kHidden; p.K = kFlat; p.k_chunk = chunk_for(kFlat, kFcFwdSplits);
     p.x = x3; p.x2 = x3; p.split_b = rows; p.ldx = kFlat;
     p.w = P(l, prm, l->t_fcw); p.bias = P(l, prm, l->t_fcb); p.y = hid; p.act = ACT_RELU;
-    ACME_GEMM_N("fc_fwd", 64, 64, 2, 2, p, 1);
+    p.slab = l->slab;
+    ACME_GEMM_N("fc_fwd", 64, 64, 2, 2, p, kFcFwdSplits);
+    const int64_t cnt = (int64_t)rows * 2 * kHidden;
+    int rc = slab_reduce(l->slab, kFcFwdSplits, cnt, hid, cnt, nullptr, P(l, prm, l->t_fcb),
+                         2 * kHidden, 1, "fc_fwd_reduce", st);
+    if (rc != ACME_OK) return rc;
   }
-  ACME_PROF("head_fwd", st, 2.0 * rows * kHidden * (l->cfg.num_actions + 1), 0.0);
-  return launch_duel_head(hid, rows, kHidden, l->cfg.num_actions, P(l, prm, l->t_vw),
-                          P(l, prm, l->t_vb), P(l, prm, l->t_aw), P(l, prm, l->t_ab), q, st);
+  {  // Duelling value/advantage outputs as one skinny split-K GEMM + epilogue kernel.
+    DuelHeadFwd p;
+    p.M = rows; p.N = A + 1; p.K = 2 * kHidden; p.k_chunk = chunk_for(p.K, kHeadFwdSplits);
+    p.H = kHidden; p.A = A; p.h = hid; p.wv = P(l, prm, l->t_vw); p.wa = P(l, prm, l->t_aw);
+    p.slab = l->slab;
+    ACME_GEMM_N("head_fwd", 64, 32, 2, 1, p, kHeadFwdSplits);
+    ACME_PROF("head_fwd_finish", st, 0.0, 0.0);
+    return launch_duel_head_finish(l->slab, kHeadFwdSplits, rows, A, P(l, prm, l->t_vb),
+                                   P(l, prm, l->t_ab), q, st);
+  }
 }
 
 // ---------------------------------------------------------------- MLP forward
 template <class In>
-int mlp_layer0(acme_dqn* l, const float* prm, const Layer& L, const void* a, const void* b,
-               int split, int rows, float* y, hipStream_t st) {
+int mlp_layer(acme_dqn* l, const float* prm, const Layer& L, const void* a, const void* b,
+              int split, int rows, float* y, hipStream_t st) {
   const bool vec = L.in % 4 == 0 && L.out % 4 == 0;
   if (vec) {
     DenseFwd<true, In> p;
@@ -223,10 +256,10 @@ int mlp_forward(acme_dqn* l, const float* prm, const void* obs_a, const void* ob
     int rc;
     if (i == 0) {
       rc = l->cfg.obs_dtype == ACME_OBS_U8_SCALED
-               ? mlp_layer0<InU8>(l, prm, L, obs_a, obs_b, split, rows, y, st)
-               : mlp_layer0<InF32>(l, prm, L, obs_a, obs_b, split, rows, y, st);
+               ? mlp_layer<InU8>(l, prm, L, obs_a, obs_b, split, rows, y, st)
+               : mlp_layer<InF32>(l, prm, L, obs_a, obs_b, split, rows, y, st);
     } else {
-      rc = mlp_layer0<InF32>(l, prm, L, act[i - 1], act[i - 1], rows, rows, y, st);
+      rc = mlp_layer<InF32>(l, prm, L, act[i - 1], act[i - 1], rows, rows, y, st);
     }
     if (rc != ACME_OK) return rc;
   }
@@ -234,70 +267,74 @@ int mlp_forward(acme_dqn* l, const float* prm, const void* obs_a, const void* ob
 }
 
 // ---------------------------------------------------------------- backward helpers
-// Bias gradient = column sums of dZ [rows][n] (deterministic two-pass reduction).
-int bias_grad(acme_dqn* l, const float* dz, int64_t rows, int n, float* out, hipStream_t st) {
-  const int64_t chunks = std::min<int64_t>(ceil_div(rows, 256), l->colsum_floats / n);
-  ACME_PROF("bias_grad", st, 0.0, 4.0 * (double)rows * n);
-  return launch_colsum(dz, rows, n, (int)chunks, l->colsum, out, st);
-}
-
-int reduce_slab(const float* slab, int splits, int64_t count, float* out, hipStream_t st) {
-  ACME_PROF("slab_reduce", st, 0.0, 4.0 * (double)(splits + 1) * count);
-  return launch_slab_reduce(slab, splits, count, out, st);
-}
-
-template <class G, class In>
+// Conv weight + bias gradient: split-K over the batch pixels into [splits][K+1][CO] slabs
+// (row K = bias partial from the GEMM's colsum hook), then one deterministic reduction
+// writes dW and db.
+template <class G, class In, int BM, int BN, int WM, int WN>
 int conv_wgrad(acme_dqn* l, const typename In::T* x, const float* dz, int batch, int splits,
-               float* dw, float* db, hipStream_t st) {
+               float* dw, float* db, const char* name, const char* rname, hipStream_t st) {
   ConvWgrad<G, In> p;
   p.M = G::K; p.N = G::CO; p.K = batch * G::OPIX; p.k_chunk = chunk_for(p.K, splits);
   p.x = x; p.dz = dz; p.slab = l->slab;
-  if ((int64_t)splits * p.M * p.N > l->slab_floats) {
+  if ((int64_t)splits * (p.M + 1) * p.N > l->slab_floats) {
     set_error("slab workspace too small");
     return ACME_ERR_INVALID;
   }
-  const char* wname = G::K == 256 ? "conv1_wgrad" : (G::K == 512 ? "conv2_wgrad" : "conv3_wgrad");
-  if (G::CO == 32) {
-    ACME_GEMM_N(wname, 64, 32, 2, 1, p, splits);
-  } else {
-    ACME_GEMM_N(wname, 64, 64, 2, 2, p, splits);
-  }
-  int rc = reduce_slab(l->slab, splits, (int64_t)p.M * p.N, dw, st);
-  if (rc != ACME_OK) return rc;
-  return bias_grad(l, dz, (int64_t)batch * G::OPIX, G::CO, db, st);
+  ACME_GEMM_N(name, BM, BN, WM, WN, p, splits);
+  const int64_t count = (int64_t)(p.M + 1) * p.N;
+  return slab_reduce(l->slab, splits, count, dw, (int64_t)p.M * p.N, db, nullptr, 0, 0, rname,
+                     st);
+}
+
+template <int PH, int PW>
+int conv2_dgrad_class(acme_dqn* l, int B, hipStream_t st) {
+  using Sub = ConvDgradSub<G2, PH, PW>;
+  Sub p;
+  p.M = B * Sub::NH * Sub::NW; p.N = G2::CI; p.K = Sub::KR; p.k_chunk = Sub::KR;
+  p.dz = l->dz2; p.w = P(l, l->params, l->t_c2w); p.xprev = l->x1; p.dx = l->dz1;
+  ACME_GEMM_N("conv2_dgrad", 256, 32, 4, 1, p, 1);
+  return ACME_OK;
 }
 
 int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st) {
   const float* prm = l->params;
   float* gr = l->grads;
   const int A = l->cfg.num_actions;
-  // Head: dZ of the fused hidden layer (masked by its ReLU) and head weight grads.
   int rc;
-  {
-  ACME_PROF("head_bwd", st, 0.0, 0.0);
-  rc = launch_duel_head_backward(l->hid, l->g, l->a_cache, B, kHidden, A, P(l, prm, l->t_vw),
-                                     P(l, prm, l->t_aw), l->dzh, Pm(l, gr, l->t_vw),
-                                     Pm(l, gr, l->t_vb), Pm(l, gr, l->t_aw), Pm(l, gr, l->t_ab), st);
+  {  // Head: dZ of the fused hidden layer (masked by its ReLU).
+    ACME_PROF("head_dz", st, 0.0, 0.0);
+    rc = launch_duel_head_dz(l->hid, l->g, l->a_cache, B, kHidden, A, P(l, prm, l->t_vw),
+                             P(l, prm, l->t_aw), l->dzh, st);
+    if (rc != ACME_OK) return rc;
   }
-  if (rc != ACME_OK) return rc;
-  // FC weight grad: [7744, 1024] = x3^T dZh (reduction over the batch).
-  {
+  {  // Head weight / bias gradients: one skinny GEMM over the batch + scatter.
+    DuelHeadWgrad p;
+    p.M = 2 * kHidden; p.N = A + 1; p.K = B; p.k_chunk = chunk_for(B, kHeadBwdSplits);
+    p.A = A; p.h = l->hid; p.g = l->g; p.act = l->a_cache; p.slab = l->slab;
+    ACME_GEMM_N("head_wgrad", 64, 32, 2, 1, p, kHeadBwdSplits);
+    ACME_PROF("head_wgrad_scatter", st, 0.0, 0.0);
+    rc = launch_duel_head_grad_scatter(l->slab, kHeadBwdSplits, kHidden, A, Pm(l, gr, l->t_vw),
+                                       Pm(l, gr, l->t_vb), Pm(l, gr, l->t_aw), Pm(l, gr, l->t_ab),
+                                       st);
+    if (rc != ACME_OK) return rc;
+  }
+  {  // FC weight + bias grad: [7744, 1024] = x3^T dZh (reduction over the batch).
     DenseWgrad<true> p;
     p.M = kFlat; p.N = 2 * kHidden; p.K = B; p.k_chunk = B;
     p.x = l->x3; p.ldx = kFlat; p.dz = l->dzh; p.out = Pm(l, gr, l->t_fcw);
+    p.bias_out = Pm(l, gr, l->t_fcb);
     ACME_GEMM_N("fc_wgrad", 128, 128, 2, 2, p, 1);
   }
-  if ((rc = bias_grad(l, l->dzh, B, 2 * kHidden, Pm(l, gr, l->t_fcb), st)) != ACME_OK) return rc;
-  // FC input grad -> dZ3 (masked by conv3's ReLU).
-  {
+  {  // FC input grad -> dZ3 (masked by conv3's ReLU).
     DenseDgrad<true> p;
     p.M = B; p.N = kFlat; p.K = 2 * kHidden; p.k_chunk = p.K;
     p.dz = l->dzh; p.w = P(l, prm, l->t_fcw); p.xprev = l->x3; p.ldx = kFlat; p.dx = l->dz3;
     ACME_GEMM_N("fc_dgrad", 64, 128, 2, 2, p, 1);
   }
   // conv3
-  if ((rc = conv_wgrad<G3, InF32>(l, l->x2, l->dz3, B, 64, Pm(l, gr, l->t_c3w),
-                                  Pm(l, gr, l->t_c3b), st)) != ACME_OK)
+  if ((rc = conv_wgrad<G3, InF32, 64, 64, 2, 2>(l, l->x2, l->dz3, B, kConv3WgradSplits,
+                                                Pm(l, gr, l->t_c3w), Pm(l, gr, l->t_c3b),
+                                                "conv3_wgrad", "conv3_wgrad_reduce", st)) != ACME_OK)
     return rc;
   {
     ConvDgrad<G3> p;
@@ -306,38 +343,43 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st) {
     ACME_GEMM_N("conv3_dgrad", 128, 64, 2, 2, p, 1);
   }
   // conv2
-  if ((rc = conv_wgrad<G2, InF32>(l, l->x1, l->dz2, B, 64, Pm(l, gr, l->t_c2w),
-                                  Pm(l, gr, l->t_c2b), st)) != ACME_OK)
+  if ((rc = conv_wgrad<G2, InF32, 64, 64, 2, 2>(l, l->x1, l->dz2, B, kConv2WgradSplits,
+                                                Pm(l, gr, l->t_c2w), Pm(l, gr, l->t_c2b),
+                                                "conv2_wgrad", "conv2_wgrad_reduce", st)) != ACME_OK)
     return rc;
-  {
-    ConvDgrad<G2> p;
-    p.M = B * G2::IPIX; p.N = G2::CI; p.K = G2::KH * G2::KW * G2::CO; p.k_chunk = p.K;
-    p.dz = l->dz2; p.w = P(l, prm, l->t_c2w); p.xprev = l->x1; p.dx = l->dz1;
-    ACME_GEMM_F("conv2_dgrad", 2.0 * B * G2::OPIX * G2::CO * G2::K, 256, 32, 4, 1, p, 1);
-  }
+  // Stride-2 input gradient as four dense sub-pixel GEMMs (one per parity class).
+  if ((rc = conv2_dgrad_class<0, 0>(l, B, st)) || (rc = conv2_dgrad_class<0, 1>(l, B, st)) ||
+      (rc = conv2_dgrad_class<1, 0>(l, B, st)) || (rc = conv2_dgrad_class<1, 1>(l, B, st)))
+    return rc;
   // conv1 (no input gradient needed)
   if (l->cfg.obs_dtype == ACME_OBS_U8_SCALED) {
-    rc = conv_wgrad<G1, InU8>(l, static_cast<const uint8_t*>(o_tm1), l->dz1, B, 128,
-                              Pm(l, gr, l->t_c1w), Pm(l, gr, l->t_c1b), st);
+    rc = conv_wgrad<G1, InU8, 128, 32, 4, 1>(l, static_cast<const uint8_t*>(o_tm1), l->dz1, B,
+                                             kConv1WgradSplits, Pm(l, gr, l->t_c1w),
+                                             Pm(l, gr, l->t_c1b), "conv1_wgrad",
+                                             "conv1_wgrad_reduce", st);
   } else {
-    rc = conv_wgrad<G1, InF32>(l, static_cast<const float*>(o_tm1), l->dz1, B, 128,
-                               Pm(l, gr, l->t_c1w), Pm(l, gr, l->t_c1b), st);
+    rc = conv_wgrad<G1, InF32, 128, 32, 4, 1>(l, static_cast<const float*>(o_tm1), l->dz1, B,
+                                              kConv1WgradSplits, Pm(l, gr, l->t_c1w),
+                                              Pm(l, gr, l->t_c1b), "conv1_wgrad",
+                                              "conv1_wgrad_reduce", st);
   }
   return rc;
 }
 
 template <class In>
 int mlp_wgrad(acme_dqn* l, const Layer& L, const void* x, const float* dz, int B, float* dw,
-              hipStream_t st) {
+              float* db, hipStream_t st) {
   if (L.in % 4 == 0 && L.out % 4 == 0) {
     DenseWgrad<true, In> p;
     p.M = L.in; p.N = L.out; p.K = B; p.k_chunk = B;
     p.x = static_cast<const typename In::T*>(x); p.ldx = L.in; p.dz = dz; p.out = dw;
+    p.bias_out = db;
     ACME_GEMM_N("mlp_wgrad", 64, 64, 2, 2, p, 1);
   } else {
     DenseWgrad<false, In> p;
     p.M = L.in; p.N = L.out; p.K = B; p.k_chunk = B;
     p.x = static_cast<const typename In::T*>(x); p.ldx = L.in; p.dz = dz; p.out = dw;
+    p.bias_out = db;
     ACME_GEMM_N("mlp_wgrad", 64, 64, 2, 2, p, 1);
   }
   return ACME_OK;
@@ -355,13 +397,12 @@ int mlp_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st) {
     const float* dz = l->mlp_dz[i];
     if (i == 0) {
       rc = l->cfg.obs_dtype == ACME_OBS_U8_SCALED
-               ? mlp_wgrad<InU8>(l, L, o_tm1, dz, B, Pm(l, gr, L.w), st)
-               : mlp_wgrad<InF32>(l, L, o_tm1, dz, B, Pm(l, gr, L.w), st);
+               ? mlp_wgrad<InU8>(l, L, o_tm1, dz, B, Pm(l, gr, L.w), Pm(l, gr, L.b), st)
+               : mlp_wgrad<InF32>(l, L, o_tm1, dz, B, Pm(l, gr, L.w), Pm(l, gr, L.b), st);
     } else {
-      rc = mlp_wgrad<InF32>(l, L, l->mlp_act[i - 1], dz, B, Pm(l, gr, L.w), st);
+      rc = mlp_wgrad<InF32>(l, L, l->mlp_act[i - 1], dz, B, Pm(l, gr, L.w), Pm(l, gr, L.b), st);
     }
     if (rc != ACME_OK) return rc;
-    if ((rc = bias_grad(l, dz, B, L.out, Pm(l, gr, L.b), st)) != ACME_OK) return rc;
     if (i > 0) {
       if (L.in % 4 == 0 && L.out % 4 == 0) {
         DenseDgrad<true> p;
@@ -432,8 +473,7 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
         (rc = dev_alloc(l, &l->dz2, (int64_t)B * kFlat)) ||
         (rc = dev_alloc(l, &l->dz1, (int64_t)B * G1::OPIX * G1::CO)))
       return fail(rc);
-    l->slab_floats = std::max<int64_t>({128LL * G1::K * G1::CO, 64LL * G2::K * G2::CO,
-                                        64LL * G3::K * G3::CO});
+    l->slab_floats = slab_floats_needed(B, A);
   } else {
     ACME_CHECK_ARG(cfg->obs_dim >= 1, "obs_dim must be >= 1");
     ACME_CHECK_ARG(cfg->num_hidden >= 0 && cfg->num_hidden <= ACME_MAX_MLP_LAYERS,
@@ -465,11 +505,9 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
     }
     l->slab_floats = 1;
   }
-  l->colsum_floats = std::max<int64_t>(256LL * 1024, (int64_t)ceil_div(2LL * B * 441, 256) * 64);
   if ((rc = dev_alloc(l, &l->q_on, (int64_t)2 * B * A)) ||
       (rc = dev_alloc(l, &l->q_tg, (int64_t)B * A)) ||
       (rc = dev_alloc(l, &l->slab, l->slab_floats)) ||
-      (rc = dev_alloc(l, &l->colsum, l->colsum_floats)) ||
       (rc = dev_alloc(l, &l->g, (int64_t)B)) || (rc = dev_alloc(l, &l->a_cache, (int64_t)B)) ||
       (rc = dev_alloc(l, &l->loss_tmp, 4)) || (rc = dev_alloc(l, &l->td_tmp, (int64_t)B)) ||
       (rc = dev_alloc(l, &l->prio_tmp, (int64_t)B)))

@@ -71,6 +71,19 @@ struct OperandPlan {
   }
 };
 
+// Optional column-sum hook: problems that define `static constexpr bool kColSum = true`
+// get sum_k B[n][k] over their reduction range (bias gradients: B is the layer's dZ),
+// accumulated from the LDS-resident B tiles by the blocks of the first M tile and
+// delivered through p.store_colsum(n, value, split).
+template <class P, class = void>
+struct HasColSum {
+  static constexpr bool value = false;
+};
+template <class P>
+struct HasColSum<P, decltype(void(P::kColSum))> {
+  static constexpr bool value = P::kColSum;
+};
+
 // Problem concept (see conv.h):
 //   static constexpr int A_MODE, B_MODE;
 //   int M, N, K;            rows of A (= C rows), rows of B (= C cols), reduction length
@@ -146,6 +159,9 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_f32_kernel(const P p) {
       for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
 
   const int r = lane & 31, h = lane >> 5;
+  constexpr bool kColSum = HasColSum<P>::value;
+  const bool do_colsum = kColSum && m0 == 0 && tid < BN;
+  float colsum = 0.f;
   if (nk > 0) {
     fetch(kbeg);
     stash(0);
@@ -156,6 +172,12 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_f32_kernel(const P p) {
     if (more) fetch(kbeg + (kt + 1) * BK);
     const float* sa = smem + (kt & 1) * (BM + BN) * LDS_STRIDE;
     const float* sb = sa + BM * LDS_STRIDE;
+    if constexpr (kColSum) {
+      if (do_colsum) {
+#pragma unroll
+        for (int k = 0; k < BK; ++k) colsum += sb[tid * LDS_STRIDE + k];
+      }
+    }
 #pragma unroll
     for (int q = 0; q < BK / 8; ++q) {
       f32x4 af[MT], bf[NTL];
@@ -190,6 +212,9 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_f32_kernel(const P p) {
         const int n = n0 + wn * TN + j * 32 + r;
         if (m < p.M && n < p.N) p.store(m, n, acc[i][j][v], split);
       }
+  if constexpr (kColSum) {
+    if (do_colsum && n0 + tid < p.N) p.store_colsum(n0 + tid, colsum, split);
+  }
 }
 
 template <int BM, int BN, int WM, int WN, class P>

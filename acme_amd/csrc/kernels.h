@@ -1,4 +1,5 @@
-// Small fused kernels of the learner step (heads, losses, reductions, optimizer).
+// Small fused kernels of the learner step (head epilogues, losses, split-K reductions,
+// optimizer).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -7,17 +8,21 @@
 
 namespace acme {
 
-// DuellingMLP head (acme/tf/networks/duelling.py:40-59) on the fused hidden layer
-// h[rows][2H] (value hidden | advantage hidden):
-//   v = h_v . wv + bv;  adv_a = h_a . wa[:, a] + ba[a];  q = v + (adv - mean_a(adv)).
-int launch_duel_head(const float* h, int rows, int H, int A, const float* wv, const float* bv,
-                     const float* wa, const float* ba, float* q, hipStream_t st);
+// Finishes the duelling head GEMM (conv.h DuelHeadFwd): sums the split-K slab
+// [splits][rows][A+1], adds biases and forms q = v + (adv - mean_a(adv))
+// (acme/tf/networks/duelling.py:51-57).
+int launch_duel_head_finish(const float* slab, int splits, int rows, int A, const float* bv,
+                            const float* ba, float* q, hipStream_t st);
 
-// Backward of the duelling head for rows b < B with dq[b] = g[b] * onehot(a[b]):
-// dZ_hidden (masked by the hidden ReLU) and the head weight / bias gradients.
-int launch_duel_head_backward(const float* h, const float* g, const int32_t* a, int B, int H,
-                              int A, const float* wv, const float* wa, float* dzh, float* dwv,
-                              float* dbv, float* dwa, float* dba, hipStream_t st);
+// dZ of the fused hidden layer for rows b < B with dq[b] = g[b] * onehot(a[b]), masked by
+// the hidden ReLU.
+int launch_duel_head_dz(const float* h, const float* g, const int32_t* a, int B, int H, int A,
+                        const float* wv, const float* wa, float* dzh, hipStream_t st);
+
+// Sums the DuelHeadWgrad slab [splits][2H+1][A+1] and scatters its block-diagonal parts
+// into the head weight / bias gradients.
+int launch_duel_head_grad_scatter(const float* slab, int splits, int H, int A, float* dwv,
+                                  float* dbv, float* dwa, float* dba, hipStream_t st);
 
 // dZ of a plain linear Q head: dz[b][j] = g[b] * (j == a[b]).
 int launch_onehot_dq(const float* g, const int32_t* a, int B, int A, float* dz, hipStream_t st);
@@ -42,10 +47,11 @@ struct LossArgs {
 // (acme/agents/tf/dqn/learning.py:128-144, acme/tf/losses/huber.py:45-57).
 int launch_dqn_loss(const LossArgs& args, hipStream_t st);
 
-// out[n] = sum_rows dz[row][n] (two deterministic passes through `partial`).
-int launch_colsum(const float* dz, int64_t rows, int n, int chunks, float* partial, float* out,
-                  hipStream_t st);
-// out[i] = sum_{s < splits} slab[s][i] (fixed order).
-int launch_slab_reduce(const float* slab, int splits, int64_t count, float* out, hipStream_t st);
+// Deterministic split-K reduction: e in [0, count): v = sum_s slab[s * count + e] (fixed
+// order), optionally + bias[e % ncols] and ReLU; written to out0[e] for e < split_at and
+// to out1[e - split_at] otherwise (weights and bias gradient of one slab).
+int launch_slab_reduce(const float* slab, int splits, int64_t count, float* out0,
+                       int64_t split_at, float* out1, const float* bias, int ncols, int relu,
+                       hipStream_t st);
 
 }  // namespace acme

@@ -18,29 +18,24 @@ __device__ __forceinline__ float wave_sum(float x) {
   return x;
 }
 
-// One wave per row: lane a < A computes advantage a, lane 63 the value.
-__global__ void __launch_bounds__(256) duel_head_kernel(const float* __restrict__ h, int rows,
-                                                        int H, int A, const float* __restrict__ wv,
-                                                        const float* __restrict__ bv,
-                                                        const float* __restrict__ wa,
-                                                        const float* __restrict__ ba,
-                                                        float* __restrict__ q) {
+// Duelling head epilogue: one wave per row; lane j <= A sums the split-K partials of
+// output j (fixed split order) and adds its bias; lane A holds the value.
+__global__ void __launch_bounds__(256) duel_head_finish_kernel(const float* __restrict__ slab,
+                                                               int splits, int rows, int A,
+                                                               const float* __restrict__ bv,
+                                                               const float* __restrict__ ba,
+                                                               float* __restrict__ q) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
-  const float* hv = h + (size_t)row * 2 * H;
-  const float* ha = hv + H;
+  const int N = A + 1;
   float acc = 0.f;
-  if (lane < A) {
-    for (int k = 0; k < H; ++k) acc = fmaf(ha[k], wa[k * A + lane], acc);
-    acc += ba[lane];
-  } else if (lane == 63) {
-    for (int k = 0; k < H; ++k) acc = fmaf(hv[k], wv[k], acc);
-    acc += bv[0];
+  if (lane <= A) {
+    for (int s = 0; s < splits; ++s) acc += slab[((size_t)s * rows + row) * N + lane];
+    acc += lane < A ? ba[lane] : bv[0];
   }
-  const float v = __shfl(acc, 63, 64);
-  const float adv_sum = wave_sum(lane < A ? acc : 0.f);
-  const float mean = adv_sum / (float)A;
+  const float v = __shfl(acc, A, 64);
+  const float mean = wave_sum(lane < A ? acc : 0.f) / (float)A;
   if (lane < A) q[(size_t)row * A + lane] = v + (acc - mean);
 }
 
@@ -69,38 +64,24 @@ __global__ void duel_head_dz_kernel(const float* __restrict__ h, const float* __
   dzh[i] = h[i] > 0.f ? d : 0.f;
 }
 
-// Head weight/bias gradients: one thread per output column c.
-//   c < H               : dwv[c]     = sum_b hv[b][c] g_b
-//   H <= c < H + H*A    : dwa[k][j]  = sum_b ha[b][k] g_b (1[j==a_b] - 1/A)
-//   c == H + H*A        : dbv        = sum_b g_b
-//   next A columns      : dba[j]     = sum_b g_b (1[j==a_b] - 1/A)
-__global__ void duel_head_wgrad_kernel(const float* __restrict__ h, const float* __restrict__ g,
-                                       const int32_t* __restrict__ a, int B, int H, int A,
-                                       float* __restrict__ dwv, float* __restrict__ dbv,
-                                       float* __restrict__ dwa, float* __restrict__ dba) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  const int total = H + H * A + 1 + A;
-  if (c >= total) return;
-  const float inv_a = 1.f / (float)A;
+// Sum of the DuelHeadWgrad slab + scatter of its block-diagonal parts.
+__global__ void duel_head_grad_scatter_kernel(const float* __restrict__ slab, int splits, int H,
+                                              int A, float* __restrict__ dwv,
+                                              float* __restrict__ dbv, float* __restrict__ dwa,
+                                              float* __restrict__ dba) {
+  const int N = A + 1;
+  const int64_t count = (int64_t)(2 * H + 1) * N;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= count) return;
+  const int k = (int)(e / N), n = (int)(e - (int64_t)k * N);
+  const bool value_w = k < H && n == A, adv_w = k >= H && k < 2 * H && n < A, bias = k == 2 * H;
+  if (!(value_w || adv_w || bias)) return;
   float s = 0.f;
-  if (c < H) {
-    for (int b = 0; b < B; ++b) s = fmaf(h[(size_t)b * 2 * H + c], g[b], s);
-    dwv[c] = s;
-  } else if (c < H + H * A) {
-    const int k = (c - H) / A, j = (c - H) % A;
-    for (int b = 0; b < B; ++b) {
-      const float dadv = g[b] * ((j == a[b] ? 1.f : 0.f) - inv_a);
-      s = fmaf(h[(size_t)b * 2 * H + H + k], dadv, s);
-    }
-    dwa[(size_t)k * A + j] = s;
-  } else if (c == H + H * A) {
-    for (int b = 0; b < B; ++b) s += g[b];
-    dbv[0] = s;
-  } else {
-    const int j = c - (H + H * A + 1);
-    for (int b = 0; b < B; ++b) s += g[b] * ((j == a[b] ? 1.f : 0.f) - inv_a);
-    dba[j] = s;
-  }
+  for (int sp = 0; sp < splits; ++sp) s += slab[(size_t)sp * count + e];
+  if (value_w) dwv[k] = s;
+  else if (adv_w) dwa[(size_t)(k - H) * A + n] = s;
+  else if (n == A) dbv[0] = s;
+  else dba[n] = s;
 }
 
 __global__ void onehot_dq_kernel(const float* __restrict__ g, const int32_t* __restrict__ a,
@@ -177,42 +158,33 @@ __global__ void __launch_bounds__(kLossThreads) dqn_loss_kernel(LossArgs p) {
   }
 }
 
-__global__ void colsum_partial_kernel(const float* __restrict__ dz, int64_t rows, int n,
-                                      int64_t rows_per_chunk, float* __restrict__ partial) {
-  extern __shared__ float sm[];
-  const int chunk = blockIdx.x;
-  const int64_t r0 = (int64_t)chunk * rows_per_chunk;
-  const int64_t r1 = min(rows, r0 + rows_per_chunk);
-  const int tid = threadIdx.x;
-  if (n >= (int)blockDim.x) {
-    for (int c = tid; c < n; c += blockDim.x) {
-      float s = 0.f;
-      for (int64_t r = r0; r < r1; ++r) s += dz[r * n + c];
-      partial[(size_t)chunk * n + c] = s;
-    }
-    return;
-  }
-  const int lanes = blockDim.x / n;
-  const int col = tid % n, rl = tid / n;
+// Deterministic split-K reduction: 64 outputs x 4 split groups per 256-thread block;
+// group g sums splits g, g+4, ... (coalesced 256-B rows per wave), then the four group
+// partials are added in order.
+__global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restrict__ slab,
+                                                          int splits, int64_t count,
+                                                          float* __restrict__ out0,
+                                                          int64_t split_at,
+                                                          float* __restrict__ out1,
+                                                          const float* __restrict__ bias,
+                                                          int ncols, int relu) {
+  __shared__ float red[4][64];
+  const int o = threadIdx.x & 63, gr = threadIdx.x >> 6;
+  const int64_t e = (int64_t)blockIdx.x * 64 + o;
   float s = 0.f;
-  if (rl < lanes)
-    for (int64_t r = r0 + rl; r < r1; r += lanes) s += dz[r * n + col];
-  if (rl < lanes) sm[rl * n + col] = s;
+  if (e < count)
+    for (int sp = gr; sp < splits; sp += 4) s += slab[(size_t)sp * count + e];
+  red[gr][o] = s;
   __syncthreads();
-  if (tid < n) {
-    float t = 0.f;
-    for (int k = 0; k < lanes; ++k) t += sm[k * n + tid];
-    partial[(size_t)chunk * n + tid] = t;
+  if (gr == 0 && e < count) {
+    float v = ((red[0][o] + red[1][o]) + red[2][o]) + red[3][o];
+    if (bias) {
+      v += bias[e % ncols];
+      if (relu) v = v > 0.f ? v : 0.f;
+    }
+    if (e < split_at) out0[e] = v;
+    else out1[e - split_at] = v;
   }
-}
-
-__global__ void slab_reduce_kernel(const float* __restrict__ slab, int splits, int64_t count,
-                                   float* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= count) return;
-  float s = 0.f;
-  for (int k = 0; k < splits; ++k) s += slab[(size_t)k * count + i];
-  out[i] = s;
 }
 
 using f32x4 = __attribute__((ext_vector_type(4))) float;
@@ -266,22 +238,27 @@ __global__ void min_f64_kernel(const double* __restrict__ x, int64_t n, double* 
 
 }  // namespace
 
-int launch_duel_head(const float* h, int rows, int H, int A, const float* wv, const float* bv,
-                     const float* wa, const float* ba, float* q, hipStream_t st) {
-  duel_head_kernel<<<(unsigned)ceil_div(rows, 4), 256, 0, st>>>(h, rows, H, A, wv, bv, wa, ba, q);
+int launch_duel_head_finish(const float* slab, int splits, int rows, int A, const float* bv,
+                            const float* ba, float* q, hipStream_t st) {
+  duel_head_finish_kernel<<<(unsigned)ceil_div(rows, 4), 256, 0, st>>>(slab, splits, rows, A, bv,
+                                                                       ba, q);
   ACME_LAUNCH_CHECK();
   return ACME_OK;
 }
 
-int launch_duel_head_backward(const float* h, const float* g, const int32_t* a, int B, int H,
-                              int A, const float* wv, const float* wa, float* dzh, float* dwv,
-                              float* dbv, float* dwa, float* dba, hipStream_t st) {
+int launch_duel_head_dz(const float* h, const float* g, const int32_t* a, int B, int H, int A,
+                        const float* wv, const float* wa, float* dzh, hipStream_t st) {
   const int64_t n = (int64_t)B * 2 * H;
   duel_head_dz_kernel<<<(unsigned)ceil_div(n, 256), 256, 0, st>>>(h, g, a, B, H, A, wv, wa, dzh);
   ACME_LAUNCH_CHECK();
-  const int total = H + H * A + 1 + A;
-  duel_head_wgrad_kernel<<<(unsigned)ceil_div(total, 256), 256, 0, st>>>(h, g, a, B, H, A, dwv,
-                                                                         dbv, dwa, dba);
+  return ACME_OK;
+}
+
+int launch_duel_head_grad_scatter(const float* slab, int splits, int H, int A, float* dwv,
+                                  float* dbv, float* dwa, float* dba, hipStream_t st) {
+  const int64_t count = (int64_t)(2 * H + 1) * (A + 1);
+  duel_head_grad_scatter_kernel<<<(unsigned)ceil_div(count, 256), 256, 0, st>>>(
+      slab, splits, H, A, dwv, dbv, dwa, dba);
   ACME_LAUNCH_CHECK();
   return ACME_OK;
 }
@@ -298,18 +275,13 @@ int launch_dqn_loss(const LossArgs& args, hipStream_t st) {
   return ACME_OK;
 }
 
-int launch_colsum(const float* dz, int64_t rows, int n, int chunks, float* partial, float* out,
-                  hipStream_t st) {
-  ACME_CHECK_ARG(n >= 1 && chunks >= 1, "bad colsum shape");
-  const int64_t per = ceil_div(rows, chunks);
-  const size_t shm = n < 256 ? 256 * sizeof(float) : 0;
-  colsum_partial_kernel<<<chunks, 256, shm, st>>>(dz, rows, n, per, partial);
-  ACME_LAUNCH_CHECK();
-  return launch_slab_reduce(partial, chunks, n, out, st);
-}
-
-int launch_slab_reduce(const float* slab, int splits, int64_t count, float* out, hipStream_t st) {
-  slab_reduce_kernel<<<(unsigned)ceil_div(count, 256), 256, 0, st>>>(slab, splits, count, out);
+int launch_slab_reduce(const float* slab, int splits, int64_t count, float* out0,
+                       int64_t split_at, float* out1, const float* bias, int ncols, int relu,
+                       hipStream_t st) {
+  ACME_CHECK_ARG(splits >= 1 && count >= 1, "bad slab shape");
+  slab_reduce_kernel<<<(unsigned)ceil_div(count, 64), 256, 0, st>>>(slab, splits, count, out0,
+                                                                    split_at, out1, bias, ncols,
+                                                                    relu);
   ACME_LAUNCH_CHECK();
   return ACME_OK;
 }
