@@ -1,0 +1,139 @@
+"""N-step transition, fixed-length sequence and whole-episode adders.
+
+Semantics (pinned by the reference's golden tables, tests/golden/adder_cases.json):
+  NStepTransitionAdder  acme/adders/reverb/transition.py:119-172
+      item = (o_t, a_t, R, D, o_{t+n}[, e_t]) with, over the window s_0..s_{k-1},
+        R = r_0 + sum_{i>=1} (g^i prod_{j<i} d_j) r_i,  D = g^{k-1} prod_{j<k} d_j
+      (the agent discount g is float32); shorter windows at episode start and end.
+  SequenceAdder  acme/adders/reverb/sequence.py:30-127
+      every `period` steps once `sequence_length` steps exist, an item of the last
+      `sequence_length` steps; at episode end a zero-padded final step (+ padding).
+  EpisodeAdder  acme/adders/reverb/episode.py:31-86
+      one item per episode; raises once an episode exceeds max_sequence_length.
+"""
+
+from __future__ import annotations
+
+import copy
+from typing import Optional
+
+import numpy as np
+
+from acme_amd import specs
+from acme_amd.adders.reverb._common import (PriorityFnMapping, ReverbAdder, final_step_like,
+                                            zeros_like)
+from acme_amd.utils import tree
+
+
+class NStepTransitionAdder(ReverbAdder):
+
+    def __init__(self, client, n_step: int, discount: float,
+                 priority_fns: Optional[PriorityFnMapping] = None):
+        if n_step < 1:
+            raise ValueError(f"n_step must be >= 1, got {n_step}")
+        self._discount = np.float32(discount)
+        super().__init__(client=client, buffer_size=n_step, max_sequence_length=1,
+                         priority_fns=priority_fns)
+
+    def _transition(self):
+        head = self._buffer[0]
+        ret = copy.deepcopy(head.reward)
+        disc = copy.deepcopy(head.discount)
+        for step in list(self._buffer)[1:]:
+            disc = disc * self._discount      # agent discount enters before each reward
+            ret = ret + step.reward * disc
+            disc = disc * step.discount
+        out = (head.observation, head.action, ret, disc, self._next_observation)
+        return out + (head.extras,) if head.extras else out
+
+    def _write(self):
+        item = self._transition()
+        window = list(self._buffer) + [final_step_like(self._buffer[0], self._next_observation)]
+        self._writer.append(item)
+        self._emit(1, window)
+
+    def _write_last(self):
+        # Drain: emit the shrinking windows that end at the final observation.
+        self._buffer.popleft()
+        while self._buffer:
+            self._write()
+            self._buffer.popleft()
+
+    @classmethod
+    def signature(cls, environment_spec: specs.EnvironmentSpec, extras_spec=()):
+        sig = (environment_spec.observations, environment_spec.actions, environment_spec.rewards,
+               environment_spec.discounts, environment_spec.observations)
+        return sig + (extras_spec,) if extras_spec else sig
+
+
+class SequenceAdder(ReverbAdder):
+
+    def __init__(self, client, sequence_length: int, period: int, delta_encoded: bool = False,
+                 chunk_length: Optional[int] = None,
+                 priority_fns: Optional[PriorityFnMapping] = None,
+                 pad_end_of_episode: bool = True):
+        super().__init__(client=client, buffer_size=sequence_length,
+                         max_sequence_length=sequence_length, delta_encoded=delta_encoded,
+                         chunk_length=chunk_length, priority_fns=priority_fns)
+        self._period = period
+        self._pad = pad_end_of_episode
+        self._count = 0
+
+    def reset(self):
+        self._count = 0
+        super().reset()
+
+    def _push(self, step):
+        self._writer.append(step)
+        self._count += 1
+
+    def _write(self):
+        self._push(self._buffer[-1])
+        self._maybe_emit()
+
+    def _write_last(self):
+        closing = final_step_like(self._buffer[0], self._next_observation)
+        self._buffer.append(closing)
+        self._push(closing)
+        if self._pad:
+            L = self._max_sequence_length
+            # Pad so that the final item is full: up to L steps if fewer were written,
+            # otherwise up to the next period boundary.
+            missing = L - self._count if self._count <= L else self._period - (self._count - L)
+            zero = tree.map_structure(zeros_like, closing)
+            for _ in range(missing):
+                self._buffer.append(zero)
+                self._push(zero)
+        self._maybe_emit()
+
+    def _maybe_emit(self):
+        L = self._max_sequence_length
+        due = self._count == L or (self._count > L and (self._count - L) % self._period == 0)
+        if due:
+            steps = list(self._buffer)
+            self._emit(len(steps), steps)
+
+
+class EpisodeAdder(ReverbAdder):
+
+    def __init__(self, client, max_sequence_length: int, delta_encoded: bool = False,
+                 chunk_length: Optional[int] = None,
+                 priority_fns: Optional[PriorityFnMapping] = None):
+        super().__init__(client=client, buffer_size=max_sequence_length - 1,
+                         max_sequence_length=max_sequence_length, delta_encoded=delta_encoded,
+                         chunk_length=chunk_length, priority_fns=priority_fns)
+
+    def add(self, action, next_timestep, extras=()):
+        if len(self._buffer) == self._buffer.maxlen:
+            raise ValueError("The number of observations within the same episode exceeds "
+                             "max_sequence_length")
+        super().add(action, next_timestep, extras)
+
+    def _write(self):
+        self._writer.append(self._buffer[-1])
+
+    def _write_last(self):
+        closing = final_step_like(self._buffer[0], self._next_observation)
+        self._writer.append(closing)
+        steps = list(self._buffer) + [closing]
+        self._emit(len(steps), steps)

@@ -1,0 +1,126 @@
+"""DQNLearner — drop-in for acme/agents/tf/dqn/learning.py:35-199.
+
+Same constructor arguments and `step()` contract: one call draws a batch from the
+dataset iterator, runs the whole SGD step on the GPU (acme_dqn_step: three Q forwards,
+double-Q n-step TD, Huber, f64 IS weights, backward, snt.Adam, post-step periodic target
+copy), writes |td| priorities back to replay, increments the counter and logs.  Nothing
+synchronises the host with the device: the loss is handed to the logger as a device
+scalar and fetched only when a log line is actually emitted.
+
+`network` / `target_network` are descriptors from acme_amd.networks (the reference
+takes Sonnet modules); the target starts from its own initialisation, like the
+reference's deepcopy + create_variables (agents/tf/dqn/agent.py:127-131).
+"""
+
+from __future__ import annotations
+
+import time
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from acme_amd import core
+from acme_amd.adders import reverb as adders
+from acme_amd.native import NativeDQN
+from acme_amd.utils import counting, loggers
+
+
+class DQNLearner(core.Learner, core.Saveable):
+
+    def __init__(self, network, target_network, discount: float,
+                 importance_sampling_exponent: float, learning_rate: float,
+                 target_update_period: int, dataset, huber_loss_parameter: float = 1.0,
+                 replay_client=None, counter: Optional[counting.Counter] = None,
+                 logger: Optional[loggers.Logger] = None, checkpoint: bool = True,
+                 max_abs_reward: float = 1.0, batch_size: Optional[int] = None, seed: int = 0,
+                 device=None):
+        if huber_loss_parameter < 0:
+            raise ValueError("quadratic_linear_boundary must be >= 0.")
+        self._network = network
+        self._iterator = iter(dataset)
+        B = batch_size or getattr(dataset, "batch_size", None) or 256
+        kw = dict(network=network.kind, num_actions=network.num_actions, max_batch=B,
+                  obs_dtype=network.obs_dtype, discount=discount,
+                  importance_sampling_exponent=importance_sampling_exponent,
+                  learning_rate=learning_rate, huber_loss_parameter=huber_loss_parameter,
+                  target_update_period=target_update_period, max_abs_reward=max_abs_reward,
+                  device=device)
+        if network.kind == "mlp":
+            kw.update(obs_dim=network.obs_dim, hidden=network.hidden)
+        self._native = NativeDQN(**kw)
+        self._native.set_params(network.init(seed), target_network.init(seed + 1))
+        self._replay_client = replay_client
+        self._counter = counter or counting.Counter()
+        self._logger = logger or loggers.TerminalLogger("learner", time_delta=1.0)
+        self._timestamp = None
+        self._obs_flat = int(np.prod(network.obs_shape))
+        self._checkpoint = checkpoint
+
+    # ------------------------------------------------------------------ step
+    def _prepare(self, x: torch.Tensor, dtype) -> torch.Tensor:
+        if x.dtype != dtype:
+            x = x.to(dtype)
+        return x.contiguous()
+
+    def step(self):
+        sample = next(self._iterator)
+        o_tm1, a_tm1, r_t, d_t, o_t = sample.data[:5]
+        keys, probs = sample.info[:2]
+        B = int(a_tm1.shape[0])
+        obs_dt = torch.uint8 if self._network.obs_dtype == "uint8" else torch.float32
+        self._native.step(self._prepare(o_tm1.reshape(B, self._obs_flat), obs_dt),
+                          self._prepare(a_tm1.reshape(B), torch.int32),
+                          self._prepare(r_t.reshape(B), torch.float32),
+                          self._prepare(d_t.reshape(B), torch.float32),
+                          self._prepare(o_t.reshape(B, self._obs_flat), obs_dt),
+                          self._prepare(probs, torch.float64))
+        if self._replay_client is not None:
+            self._replay_client.update_priorities(table=adders.DEFAULT_PRIORITY_TABLE,
+                                                  keys=keys,
+                                                  priorities=self._native.priorities[:B])
+        now = time.time()
+        elapsed = now - self._timestamp if self._timestamp else 0
+        self._timestamp = now
+        result = {"loss": self._native.loss}
+        result.update(self._counter.increment(steps=1, walltime=elapsed))
+        self._logger.write(result)
+
+    # ------------------------------------------------------------------ variables
+    def q_values(self, observations, use_target: bool = False) -> np.ndarray:
+        obs_dt = torch.uint8 if self._network.obs_dtype == "uint8" else torch.float32
+        x = torch.as_tensor(np.asarray(observations)).to(self._native.device, obs_dt)
+        return self._native.q_values(x.reshape(x.shape[0], -1).contiguous(), use_target).cpu().numpy()
+
+    def get_variables(self, names: List[str]) -> List[List[np.ndarray]]:
+        # As the TF learner: one collection (the online trainable variables), names ignored.
+        sonnet = self._network.to_sonnet(self._native.get_params("params"))
+        return [[sonnet[k] for k in sorted(sonnet)]]
+
+    @property
+    def num_steps(self) -> int:
+        return self._native.num_steps
+
+    @property
+    def native(self) -> NativeDQN:
+        return self._native
+
+    @property
+    def state(self) -> Dict:
+        return self.save()
+
+    def save(self) -> Dict:
+        n = self._native
+        return {"network": n.get_params("params"), "target_network": n.get_params("target"),
+                "optimizer": {"m": n.get_params("m"), "v": n.get_params("v"),
+                              "step": n.num_steps},
+                "num_steps": n.num_steps}
+
+    def restore(self, state: Dict):
+        n = self._native
+        n.set_params(state["network"], state["target_network"])
+        for buf, src in ((n.m, state["optimizer"]["m"]), (n.v, state["optimizer"]["v"])):
+            views = n.views(buf)
+            for k, t in views.items():
+                t.copy_(torch.as_tensor(np.asarray(src[k], np.float32)).view(t.shape))
+        n.num_steps = int(state["num_steps"])

@@ -1,0 +1,147 @@
+"""make_reverb_dataset — drop-in for acme/datasets/reverb.py:36-139.
+
+The reference streams every sample through gRPC, decompresses it on a tf.data thread,
+batches on the host and copies the batch to the device.  Here a batch is drawn and
+gathered on the GPU: one sampling kernel (prioritized 64-ary sum tree or uniform) and
+one row-gather per field into device buffers, so `next(iterator)` returns a
+ReplaySample whose data are device tensors.  Buffers are double-buffered: a sample stays
+valid until the iterator is advanced twice.
+
+`server_address` may be the in-process address ('localhost:<port>'), a Server, a Table
+or a Client.  Sampling is deterministic given the table seed: draw i uses Philox
+counter block i.
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+import torch
+
+from acme_amd import replay
+from acme_amd.adders import reverb as adders
+from acme_amd.utils import tree
+
+_TORCH = {np.dtype(k): v for k, v in [
+    ("uint8", torch.uint8), ("int8", torch.int8), ("int16", torch.int16),
+    ("int32", torch.int32), ("int64", torch.int64), ("float16", torch.float16),
+    ("float32", torch.float32), ("float64", torch.float64), ("bool", torch.bool),
+    ("uint64", torch.uint64), ("uint32", torch.uint32)]}
+
+
+def _server_of(address) -> replay.Server:
+    if isinstance(address, replay.Client):
+        return address.server
+    return replay._resolve(address)  # noqa: SLF001
+
+
+class ReplayDataset:
+    """Iterable over batched ReplaySamples of one table."""
+
+    def __init__(self, table, batch_size: int, timeout: float = 60.0):
+        if batch_size is None or batch_size < 1:
+            raise ValueError("the GPU replay dataset needs a batch_size >= 1")
+        self.table = table
+        self.batch_size = int(batch_size)
+        self.timeout = timeout
+
+    def __iter__(self):
+        if isinstance(self.table, replay.QueueTable):
+            return _QueueIterator(self.table, self.batch_size, self.timeout)
+        return _TableIterator(self.table, self.batch_size, self.timeout)
+
+
+class _TableIterator:
+    def __init__(self, table: replay.Table, batch: int, timeout: float):
+        self._t = table
+        self._B = batch
+        self._timeout = timeout
+        self._slots = None
+
+    def _alloc(self):
+        native = self._t.native
+        dev = native.device
+        self._slots = []
+        for _ in range(2):
+            info = native.alloc_sample_info(self._B)
+            bufs = [torch.empty(self._B, f.row_bytes, dtype=torch.uint8, device=dev)
+                    for f in self._t.fields]
+            self._slots.append((info, bufs))
+        self._which = 0
+
+    def _typed(self, buf, f):
+        B = self._B
+        x = buf if f.nbytes == f.row_bytes else buf[:, :f.nbytes]
+        if f.dtype == np.bool_:
+            return x.view(torch.bool).reshape((B,) + f.shape)
+        return x.view(_TORCH[np.dtype(f.dtype)]).reshape((B,) + f.shape)
+
+    def __iter__(self):
+        return self
+
+    def __next__(self) -> replay.ReplaySample:
+        t = self._t
+        t.flush()
+        t.wait_for(self._B, self._timeout)
+        t.flush()
+        if self._slots is None:
+            self._alloc()
+        info, bufs = self._slots[self._which]
+        self._which ^= 1
+        native = t.native
+        native.sample(self._B, t.next_draw(), out=info)
+        native.gather(info["slots"], bufs)
+        data = tree.unflatten_as(t._structure, [self._typed(b, f)  # noqa: SLF001
+                                                for b, f in zip(bufs, t.fields)])
+        return replay.ReplaySample(
+            info=replay.SampleInfo(key=info["keys"], probability=info["probabilities"],
+                                   table_size=info["table_size"], priority=info["priorities"]),
+            data=data)
+
+
+class _QueueIterator:
+    def __init__(self, table: replay.QueueTable, batch: int, timeout: float):
+        self._t = table
+        self._B = batch
+        self._timeout = timeout
+
+    def __iter__(self):
+        return self
+
+    def __next__(self) -> replay.ReplaySample:
+        items = self._t.pop_batch(self._B, self._timeout)
+        stacked = tree.map_structure(lambda *xs: np.stack([np.asarray(x) for x in xs]), *items)
+        data = tree.map_structure(lambda x: torch.as_tensor(x).cuda(non_blocking=False), stacked)
+        ones = torch.ones(self._B, dtype=torch.float64, device="cuda")
+        info = replay.SampleInfo(key=torch.zeros(self._B, dtype=torch.uint64, device="cuda"),
+                                 probability=ones, table_size=torch.full(
+                                     (self._B,), self._t.size(), dtype=torch.int64, device="cuda"),
+                                 priority=ones)
+        return replay.ReplaySample(info=info, data=data)
+
+
+def make_reverb_dataset(server_address, environment_spec=None, batch_size: Optional[int] = None,
+                        prefetch_size: Optional[int] = None, sequence_length: Optional[int] = None,
+                        extra_spec=None, transition_adder: bool = False,
+                        table: str = adders.DEFAULT_PRIORITY_TABLE,
+                        parallel_batch_optimization: bool = True,
+                        convert_zero_size_to_none: bool = False,
+                        using_deprecated_adder: bool = False) -> ReplayDataset:
+    """Same arguments as the reference.  prefetch/parallel knobs of the tf.data pipeline
+    have no equivalent (sampling is a synchronous device kernel); the environment/extra
+    specs are only checked for consistency with the table's layout."""
+    del prefetch_size, parallel_batch_optimization, convert_zero_size_to_none
+    del using_deprecated_adder, sequence_length
+    server = _server_of(server_address)
+    if table not in server.tables:
+        raise ValueError(f"unknown table {table!r}")
+    t = server.tables[table]
+    if environment_spec is not None and transition_adder and isinstance(t, replay.Table):
+        sig = adders.NStepTransitionAdder.signature(environment_spec, extra_spec or ())
+        if t.fields is not None and len(tree.flatten(sig)) != len(t.fields):
+            raise ValueError("environment_spec does not match the table's item layout")
+    return ReplayDataset(t, batch_size)
+
+
+make_dataset = make_reverb_dataset

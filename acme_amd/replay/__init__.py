@@ -1,0 +1,382 @@
+"""In-process, GPU-resident replacement for the Reverb surface the agents use.
+
+Reference call sites (all in-process `localhost:<port>` gRPC in the reference):
+  reverb.Table(name, sampler=Prioritized(a) | Uniform(), remover=Fifo(), max_size,
+               rate_limiter=MinSize(n), signature)        acme/agents/tf/dqn/agent.py:95-101
+  reverb.Table.queue(name, max_size)                       acme/agents/tf/impala/agent.py:68-74
+  reverb.Server([tables], port=None).port                  acme/agents/tf/dqn/agent.py:102
+  reverb.Client(address).writer(...) -> append/create_item acme/adders/reverb/base.py:112-118
+  reverb.TFClient(address).update_priorities(table, keys, priorities)
+                                                           acme/agents/tf/dqn/learning.py:151-154
+  Client.mutate_priorities(table, updates)                 acme/agents/jax/dqn/learning.py:131-134
+  ReplaySample(info=SampleInfo(key, probability, table_size, priority), data)
+
+Items live in HBM (acme_amd.native.NativeReplay: one row per item per flattened field,
+64-ary sum tree for Prioritized).  Writers stage items on the host and flush them to the
+device in batches (one hipMemcpy per field per flush); a table flushes pending items
+before every sample, so a sample always sees every item created before it.
+"""
+
+from __future__ import annotations
+
+import collections
+import itertools
+import threading
+import time
+from typing import Any, Dict, List, NamedTuple, Optional, Sequence
+
+import numpy as np
+
+from acme_amd.utils import tree
+
+
+class SampleInfo(NamedTuple):
+    key: Any
+    probability: Any
+    table_size: Any
+    priority: Any
+
+
+class ReplaySample(NamedTuple):
+    info: SampleInfo
+    data: Any
+
+
+# ---------------------------------------------------------------- selectors / limiters
+class selectors:  # noqa: N801  (module-like namespace, as reverb.selectors)
+    class Prioritized(NamedTuple):
+        priority_exponent: float
+
+    class Uniform(NamedTuple):
+        pass
+
+    class Fifo(NamedTuple):
+        pass
+
+    class Lifo(NamedTuple):
+        pass
+
+
+class rate_limiters:  # noqa: N801
+    class MinSize(NamedTuple):
+        min_size_to_sample: int
+
+    class Queue(NamedTuple):
+        size: int
+
+
+# ---------------------------------------------------------------- field layout
+class _Field(NamedTuple):
+    shape: tuple
+    dtype: np.dtype
+    nbytes: int       # logical bytes per item
+    row_bytes: int    # stored bytes per item (multiple of 4)
+
+
+def _row_bytes(nbytes: int, itemsize: int) -> int:
+    align = max(4, itemsize)
+    return max(align, (nbytes + align - 1) // align * align)
+
+
+def _layout_from_item(item) -> List[_Field]:
+    out = []
+    for leaf in tree.flatten(item):
+        a = np.asarray(leaf)
+        nb = int(a.nbytes)
+        out.append(_Field(tuple(a.shape), a.dtype, nb, _row_bytes(nb, a.dtype.itemsize)))
+    return out
+
+
+def _layout_from_signature(signature) -> List[_Field]:
+    out = []
+    for s in tree.flatten(signature):
+        dt = np.dtype(s.dtype)
+        nb = int(np.prod(s.shape, dtype=np.int64)) * dt.itemsize
+        out.append(_Field(tuple(s.shape), dt, nb, _row_bytes(nb, dt.itemsize)))
+    return out
+
+
+# ---------------------------------------------------------------- table
+class Table:
+    """A named GPU replay table (Reverb Table semantics for the transition path)."""
+
+    def __init__(self, name: str, sampler, remover, max_size: int, rate_limiter=None,
+                 signature=None, seed: int = 1234, device=None, flush_every: int = 256):
+        if not isinstance(remover, (selectors.Fifo,)):
+            raise ValueError("only the Fifo remover is supported (as used by the agents)")
+        if isinstance(sampler, selectors.Prioritized):
+            self._prioritized, self._alpha = True, float(sampler.priority_exponent)
+        elif isinstance(sampler, selectors.Uniform):
+            self._prioritized, self._alpha = False, 0.0
+        else:
+            raise ValueError(f"unsupported sampler {sampler!r}")
+        self.name = name
+        self.max_size = int(max_size)
+        self._min_size = rate_limiter.min_size_to_sample if rate_limiter is not None else 1
+        self._signature = signature
+        self._structure = None
+        self._fields: Optional[List[_Field]] = None
+        self._native = None
+        self._seed = int(seed)
+        self._device = device
+        self._flush_every = int(flush_every)
+        self._pending: List[List[np.ndarray]] = []
+        self._pending_prio: List[float] = []
+        self._mu = threading.RLock()
+        self._cv = threading.Condition(self._mu)
+        self._draws = 0
+        if signature is not None:
+            self._init_layout(signature, _layout_from_signature(signature))
+
+    @classmethod
+    def queue(cls, name: str, max_size: int, signature=None):
+        return QueueTable(name, max_size, signature)
+
+    # -- layout / storage
+    def _init_layout(self, structure, fields):
+        from acme_amd.native import NativeReplay
+        self._structure = structure
+        self._fields = fields
+        self._native = NativeReplay(self.max_size, [f.row_bytes for f in fields],
+                                    prioritized=self._prioritized, priority_exponent=self._alpha,
+                                    seed=self._seed, device=self._device)
+
+    @property
+    def native(self):
+        return self._native
+
+    @property
+    def fields(self):
+        return self._fields
+
+    def size(self) -> int:
+        with self._mu:
+            n = self._native.size() if self._native is not None else 0
+            return min(self.max_size, n + len(self._pending))
+
+    def can_sample(self, num_samples: int = 1) -> bool:
+        return self.size() >= max(self._min_size, 1)
+
+    # -- inserts
+    def insert(self, item, priority: float) -> None:
+        with self._mu:
+            if self._fields is None:
+                self._init_layout(item, _layout_from_item(item))
+            leaves = tree.flatten(item)
+            if len(leaves) != len(self._fields):
+                raise ValueError(f"item has {len(leaves)} leaves, table expects "
+                                 f"{len(self._fields)}")
+            row = []
+            for leaf, f in zip(leaves, self._fields):
+                a = np.asarray(leaf, dtype=f.dtype)
+                if a.shape != f.shape:
+                    raise ValueError(f"leaf shape {a.shape} does not match table signature "
+                                     f"{f.shape}")
+                row.append(a)
+            self._pending.append(row)
+            self._pending_prio.append(float(priority))
+            if len(self._pending) >= self._flush_every:
+                self.flush()
+            self._cv.notify_all()
+
+    def flush(self) -> None:
+        with self._mu:
+            if not self._pending:
+                return
+            n = len(self._pending)
+            cols = []
+            for i, f in enumerate(self._fields):
+                buf = np.zeros((n, f.row_bytes), np.uint8)
+                for r, row in enumerate(self._pending):
+                    buf[r, :f.nbytes] = np.frombuffer(np.ascontiguousarray(row[i]).tobytes(),
+                                                      np.uint8)
+                cols.append(buf)
+            self._native.insert(cols, np.asarray(self._pending_prio, np.float64))
+            self._pending, self._pending_prio = [], []
+
+    # -- sampling
+    def wait_for(self, batch_size: int, timeout: float) -> None:
+        """Rate limiter MinSize: block until enough items exist (or time out)."""
+        deadline = time.time() + timeout
+        with self._cv:
+            while self.size() < max(self._min_size, 1):
+                left = deadline - time.time()
+                if left <= 0:
+                    raise RuntimeError(f"table '{self.name}' has {self.size()} items; "
+                                       f"MinSize({self._min_size}) not reached within {timeout}s")
+                self._cv.wait(left)
+
+    def next_draw(self) -> int:
+        with self._mu:
+            d = self._draws
+            self._draws += 1
+            return d
+
+    def update_priorities(self, keys, priorities) -> None:
+        import torch
+        with self._mu:
+            self.flush()
+            if self._native is None:
+                return
+            k = keys if isinstance(keys, torch.Tensor) else torch.as_tensor(
+                np.asarray(keys, np.uint64).view(np.int64)).view(torch.uint64)
+            p = priorities if isinstance(priorities, torch.Tensor) else torch.as_tensor(
+                np.asarray(priorities, np.float64))
+            self._native.update_priorities(k, p)
+
+
+class QueueTable:
+    """Table.queue: FIFO items consumed once (IMPALA).  Host-resident; batches are
+    stacked and moved to the device by the dataset."""
+
+    def __init__(self, name: str, max_size: int, signature=None):
+        self.name = name
+        self.max_size = int(max_size)
+        self._items: collections.deque = collections.deque()
+        self._mu = threading.Condition()
+        self._signature = signature
+
+    def size(self) -> int:
+        with self._mu:
+            return len(self._items)
+
+    def can_sample(self, num_samples: int = 1) -> bool:
+        return self.size() >= num_samples
+
+    def insert(self, item, priority: float) -> None:
+        with self._mu:
+            if len(self._items) >= self.max_size:
+                raise RuntimeError(f"queue '{self.name}' is full ({self.max_size})")
+            self._items.append(item)
+            self._mu.notify_all()
+
+    def flush(self):
+        pass
+
+    def pop_batch(self, batch_size: int, timeout: float = 60.0):
+        deadline = time.time() + timeout
+        with self._mu:
+            while len(self._items) < batch_size:
+                left = deadline - time.time()
+                if left <= 0:
+                    raise RuntimeError(f"queue '{self.name}' has {len(self._items)} items, "
+                                       f"{batch_size} requested")
+                self._mu.wait(left)
+            return [self._items.popleft() for _ in range(batch_size)]
+
+
+# ---------------------------------------------------------------- server / client
+_SERVERS: Dict[int, "Server"] = {}
+_PORTS = itertools.count(30000)
+
+
+class Server:
+    def __init__(self, tables: Sequence[Any], port: Optional[int] = None):
+        self.tables = {t.name: t for t in tables}
+        self.port = int(port) if port is not None else next(_PORTS)
+        _SERVERS[self.port] = self
+
+    def stop(self):
+        _SERVERS.pop(self.port, None)
+
+    def in_process_client(self) -> "Client":
+        return Client(self)
+
+
+def _resolve(address) -> Server:
+    if isinstance(address, Server):
+        return address
+    if isinstance(address, (Table, QueueTable)):
+        return _wrap_table(address)
+    port = int(str(address).rsplit(":", 1)[-1])
+    if port not in _SERVERS:
+        raise ValueError(f"no replay server at {address!r}")
+    return _SERVERS[port]
+
+
+def _wrap_table(table) -> Server:
+    s = Server.__new__(Server)
+    s.tables = {table.name: table}
+    s.port = -1
+    return s
+
+
+class Writer:
+    """Reverb Writer surface: append(data), create_item(table, num_timesteps, priority)."""
+
+    def __init__(self, server: Server, max_sequence_length: int):
+        self._server = server
+        self._history: collections.deque = collections.deque(maxlen=max_sequence_length)
+        self.max_sequence_length = max_sequence_length
+        self.closed = False
+
+    def append(self, data):
+        if self.closed:
+            raise RuntimeError("append on a closed writer")
+        self._history.append(data)
+
+    def create_item(self, table: str, num_timesteps: int, priority: float):
+        if self.closed:
+            raise RuntimeError("create_item on a closed writer")
+        if num_timesteps < 1 or num_timesteps > len(self._history):
+            raise ValueError(f"num_timesteps={num_timesteps} but only {len(self._history)} "
+                             "steps are available")
+        steps = list(self._history)[-num_timesteps:]
+        item = steps[0] if num_timesteps == 1 else tree.map_structure(
+            lambda *xs: np.stack([np.asarray(x) for x in xs]), *steps)
+        self._server.tables[table].insert(item, priority)
+
+    def flush(self):
+        for t in self._server.tables.values():
+            t.flush()
+
+    def close(self):
+        if not self.closed:
+            self.flush()
+            self.closed = True
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+class Client:
+    """reverb.Client / reverb.TFClient surface over the in-process server."""
+
+    def __init__(self, server_address):
+        self._server = _resolve(server_address)
+
+    @property
+    def server(self) -> Server:
+        return self._server
+
+    def writer(self, max_sequence_length: int, delta_encoded: bool = False,
+               chunk_length: Optional[int] = None) -> Writer:
+        del delta_encoded, chunk_length  # compression knobs of the gRPC path: not needed
+        return Writer(self._server, max_sequence_length)
+
+    def insert(self, data, priorities: Dict[str, float]):
+        for table, p in priorities.items():
+            self._server.tables[table].insert(data, p)
+
+    def update_priorities(self, table: str, keys, priorities):
+        """TFClient.update_priorities: device or host keys (u64) / priorities (f64)."""
+        self._server.tables[table].update_priorities(keys, priorities)
+
+    def mutate_priorities(self, table: str, updates: Optional[Dict[int, float]] = None,
+                          deletes: Optional[Sequence[int]] = None):
+        if deletes:
+            raise NotImplementedError("item deletion is not supported by the GPU table")
+        if updates:
+            keys = np.fromiter(updates.keys(), np.uint64, len(updates))
+            pr = np.fromiter(updates.values(), np.float64, len(updates))
+            self._server.tables[table].update_priorities(keys, pr)
+
+    def server_info(self):
+        return {name: dict(current_size=t.size(), max_size=t.max_size)
+                for name, t in self._server.tables.items()}
+
+
+TFClient = Client

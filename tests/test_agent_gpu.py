@@ -1,0 +1,148 @@
+"""Drop-in path on the GPU: NStepTransitionAdder -> GPU Table -> make_reverb_dataset ->
+DQNLearner.step -> update_priorities, and the DQN agent in an EnvironmentLoop
+(acme/agents/tf/dqn/agent_test.py:38-58 pattern: tiny MLP, small batch, runs)."""
+
+import numpy as np
+import pytest
+import torch
+
+from acme_amd import dm_env, replay, specs
+from acme_amd.adders import reverb as adders
+from acme_amd.datasets import make_reverb_dataset
+from acme_amd.environment_loop import EnvironmentLoop
+from acme_amd.testing import fakes
+from acme_amd.utils import loggers
+from oracle import dqn_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _spec(obs_dim=4, A=3):
+    return specs.EnvironmentSpec(observations=specs.Array((obs_dim,), np.float32),
+                                 actions=specs.DiscreteArray(A, np.int32),
+                                 rewards=specs.Array((), np.float32),
+                                 discounts=specs.BoundedArray((), np.float32, 0.0, 1.0))
+
+
+def _table(spec, prioritized=True, size=1000):
+    sampler = replay.selectors.Prioritized(0.6) if prioritized else replay.selectors.Uniform()
+    return replay.Table(adders.DEFAULT_PRIORITY_TABLE, sampler, replay.selectors.Fifo(), size,
+                        replay.rate_limiters.MinSize(1),
+                        signature=adders.NStepTransitionAdder.signature(spec))
+
+
+def test_adder_to_gpu_table_to_dataset():
+    spec = _spec()
+    table = _table(spec)
+    server = replay.Server([table])
+    client = replay.Client(f"localhost:{server.port}")
+    adder = adders.NStepTransitionAdder(client, n_step=1, discount=0.99)
+    rng = np.random.default_rng(0)
+    inserted = []
+    obs = rng.standard_normal(4).astype(np.float32)
+    adder.add_first(dm_env.restart(obs))
+    for t in range(40):
+        nxt = rng.standard_normal(4).astype(np.float32)
+        a = np.int32(t % 3)
+        r = np.float32(t)
+        ts = dm_env.termination(r, nxt) if t == 39 else dm_env.transition(r, nxt, np.float32(1.0))
+        adder.add(a, ts)
+        # n = 1: D is the environment discount (the agent discount enters only for n > 1).
+        inserted.append((obs, a, r, np.float32(0.0 if t == 39 else 1.0), nxt))
+        obs = nxt
+    ds = make_reverb_dataset(f"localhost:{server.port}", batch_size=16)
+    it = iter(ds)
+    s = next(it)
+    keys = s.info.key.cpu().numpy().view(np.int64)
+    o_tm1, a_tm1, r_t, d_t, o_t = [x.cpu().numpy() for x in s.data]
+    assert o_tm1.shape == (16, 4) and o_tm1.dtype == np.float32
+    assert a_tm1.dtype == np.int32 and r_t.shape == (16,)
+    for i, k in enumerate(keys):
+        e = inserted[k]
+        np.testing.assert_array_equal(o_tm1[i], e[0])
+        assert a_tm1[i] == e[1] and r_t[i] == e[2]
+        np.testing.assert_allclose(d_t[i], e[3], rtol=1e-6)
+        np.testing.assert_array_equal(o_t[i], e[4])
+    assert (s.info.table_size.cpu().numpy() == 40).all()
+    np.testing.assert_allclose(s.info.probability.cpu().numpy(), 1.0 / 40)  # all priority 1
+    # Priority write-back changes the sampling distribution.
+    client.update_priorities(adders.DEFAULT_PRIORITY_TABLE, s.info.key,
+                             torch.zeros(16, dtype=torch.float64, device="cuda"))
+    s2 = next(it)
+    zeroed = set(keys.tolist())
+    assert not (set(s2.info.key.cpu().numpy().view(np.int64).tolist()) & zeroed)
+
+
+def test_dqn_learner_step_through_dataset_matches_oracle():
+    from acme_amd.agents.dqn import DQNLearner
+    from acme_amd.networks import MLP
+    spec = _spec(obs_dim=8, A=4)
+    table = _table(spec)
+    server = replay.Server([table])
+    client = replay.Client(server)
+    rng = np.random.default_rng(1)
+    for i in range(300):
+        item = (rng.standard_normal(8).astype(np.float32), np.int32(rng.integers(0, 4)),
+                np.float32(rng.standard_normal()), np.float32(0.96),
+                rng.standard_normal(8).astype(np.float32))
+        table.insert(item, float(rng.uniform(0.1, 2.0)))
+    ds = make_reverb_dataset(server, batch_size=64)
+    net = MLP(8, [32, 32], 4)
+    learner = DQNLearner(net, net, discount=0.99, importance_sampling_exponent=0.2,
+                         learning_rate=1e-3, target_update_period=100, dataset=ds,
+                         replay_client=client, logger=loggers.NoOpLogger(), seed=3)
+    p0 = learner.native.get_params("params")
+    t0 = learner.native.get_params("target")
+    learner.step()
+    torch.cuda.synchronize()
+    # Re-draw the same batch from a fresh iterator of an identical table state is not
+    # possible after the priority update, so recover the batch from the learner's sample:
+    s = learner._iterator._slots[0]  # noqa: SLF001 - the buffers of draw 0
+    info, bufs = s
+    batch = dict(o_tm1=bufs[0].view(torch.float32).cpu().numpy(),
+                 a_tm1=bufs[1].view(torch.int32).cpu().numpy()[:, 0],
+                 r_t=bufs[2].view(torch.float32).cpu().numpy()[:, 0],
+                 d_t=bufs[3].view(torch.float32).cpu().numpy()[:, 0],
+                 o_t=bufs[4].view(torch.float32).cpu().numpy(),
+                 probabilities=info["probabilities"].cpu().numpy())
+    cfg = O.DQNConfig(num_actions=4, network="mlp", obs_dim=8, hidden=(32, 32))
+    out, _ = O.dqn_loss_and_grads(cfg, p0, t0, batch, np.float64)
+    np.testing.assert_allclose(learner.native.loss.item(), out["loss"], rtol=1e-5)
+    assert learner.num_steps == 1
+    var = learner.get_variables([])
+    assert len(var) == 1 and len(var[0]) == 6
+
+
+def test_dqn_agent_runs_in_environment_loop():
+    from acme_amd.agents.dqn import DQN
+    from acme_amd.networks import MLP
+    env = fakes.DiscreteEnvironment(num_actions=3, obs_shape=(5,), episode_length=10)
+    spec = specs.make_environment_spec(env)
+    agent = DQN(spec, MLP(5, [50, 50], 3), batch_size=10, samples_per_insert=2.0,
+                min_replay_size=10, checkpoint=False, logger=loggers.NoOpLogger())
+    loop = EnvironmentLoop(env, agent, logger=loggers.NoOpLogger())
+    loop.run(num_episodes=5)
+    learner = agent._learner_obj  # noqa: SLF001
+    assert learner.num_steps > 0
+    assert np.isfinite(learner.native.loss.item())
+
+
+def test_cartpole_dqn_plumbing(tmp_path):
+    """Config 1 (reference plumbing): DQN with MLP [50, 50, 2], batch 32 on CartPole."""
+    from acme_amd.agents.dqn import DQN
+    from acme_amd.environments.cartpole import CartPole
+    from acme_amd.networks import MLP
+    env = CartPole(seed=0)
+    spec = specs.make_environment_spec(env)
+    agent = DQN(spec, MLP(4, [50, 50], 2), batch_size=32, min_replay_size=100,
+                samples_per_insert=8.0, checkpoint=True, checkpoint_subpath=str(tmp_path),
+                logger=loggers.NoOpLogger())
+    EnvironmentLoop(env, agent, logger=loggers.NoOpLogger()).run(num_episodes=20)
+    learner = agent._learner_obj  # noqa: SLF001
+    assert learner.num_steps > 10
+    agent._checkpointer.save(force=True)  # noqa: SLF001
+    state = learner.save()
+    learner.native.params.zero_()
+    learner.restore(state)
+    np.testing.assert_array_equal(learner.native.get_params("params")["mlp/linear_0/w"],
+                                  state["network"]["mlp/linear_0/w"])
