@@ -34,7 +34,7 @@ class DQNLearner(core.Learner, core.Saveable):
                  replay_client=None, counter: Optional[counting.Counter] = None,
                  logger: Optional[loggers.Logger] = None, checkpoint: bool = True,
                  max_abs_reward: float = 1.0, batch_size: Optional[int] = None, seed: int = 0,
-                 device=None):
+                 device=None, data_parallel: bool = True):
         if huber_loss_parameter < 0:
             raise ValueError("quadratic_linear_boundary must be >= 0.")
         self._network = network
@@ -56,6 +56,20 @@ class DQNLearner(core.Learner, core.Saveable):
         self._timestamp = None
         self._obs_flat = int(np.prod(network.obs_shape))
         self._checkpoint = checkpoint
+        # Data parallelism (one process per GPU, torch.distributed over RCCL): each rank
+        # samples its own batch from its replay shard; the IS-weight normaliser and the
+        # gradients are reduced across ranks before Adam, so every replica applies the
+        # update of the global batch (the mean-then-apply order of the reference's only
+        # data-parallel learner, acme/agents/tf/crr/recurrent_learning.py:346-358).
+        self._dist = None
+        if data_parallel:
+            import torch.distributed as dist
+            if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+                self._dist = dist
+                for buf in (self._native.params, self._native.target):
+                    dist.broadcast(buf, src=0)
+                self._gmin = torch.empty(1, dtype=torch.float64, device=self._native.device)
+                self._avg_op = (dist.ReduceOp.AVG if dist.get_backend() == "nccl" else None)
 
     # ------------------------------------------------------------------ step
     def _prepare(self, x: torch.Tensor, dtype) -> torch.Tensor:
@@ -69,12 +83,25 @@ class DQNLearner(core.Learner, core.Saveable):
         keys, probs = sample.info[:2]
         B = int(a_tm1.shape[0])
         obs_dt = torch.uint8 if self._network.obs_dtype == "uint8" else torch.float32
-        self._native.step(self._prepare(o_tm1.reshape(B, self._obs_flat), obs_dt),
-                          self._prepare(a_tm1.reshape(B), torch.int32),
-                          self._prepare(r_t.reshape(B), torch.float32),
-                          self._prepare(d_t.reshape(B), torch.float32),
-                          self._prepare(o_t.reshape(B, self._obs_flat), obs_dt),
-                          self._prepare(probs, torch.float64))
+        batch = (self._prepare(o_tm1.reshape(B, self._obs_flat), obs_dt),
+                 self._prepare(a_tm1.reshape(B), torch.int32),
+                 self._prepare(r_t.reshape(B), torch.float32),
+                 self._prepare(d_t.reshape(B), torch.float32),
+                 self._prepare(o_t.reshape(B, self._obs_flat), obs_dt),
+                 self._prepare(probs, torch.float64))
+        if self._dist is None:
+            self._native.step(*batch)
+        else:
+            dist = self._dist
+            self._native.batch_min_probability(batch[5], self._gmin)
+            dist.all_reduce(self._gmin, op=dist.ReduceOp.MIN)
+            self._native.forward_backward(*batch, global_min_probability=self._gmin)
+            if self._avg_op is not None:  # RCCL has a native average
+                dist.all_reduce(self._native.grads, op=self._avg_op)
+            else:  # gloo: sum, then scale
+                dist.all_reduce(self._native.grads, op=dist.ReduceOp.SUM)
+                self._native.grads.mul_(1.0 / dist.get_world_size())
+            self._native.apply()
         if self._replay_client is not None:
             self._replay_client.update_priorities(table=adders.DEFAULT_PRIORITY_TABLE,
                                                   keys=keys,

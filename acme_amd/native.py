@@ -310,6 +310,11 @@ class NativeDQN:
         check(lib().acme_dqn_forward_backward(self._h, ctypes.byref(tb), ctypes.byref(out),
                                               stream_ptr(stream)), "dqn forward_backward")
 
+    def batch_min_probability(self, probabilities: torch.Tensor, out: torch.Tensor, stream=None):
+        """out[0] = min(probabilities) on the device (data-parallel IS normaliser)."""
+        check(lib().acme_min_f64(ptr(probabilities), int(probabilities.numel()), ptr(out),
+                                 stream_ptr(stream)), "min_f64")
+
     def apply(self, stream=None):
         check(lib().acme_dqn_apply(self._h, stream_ptr(stream)), "dqn apply")
 

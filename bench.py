@@ -131,48 +131,40 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    from acme_amd import _lib
-    from acme_amd.native import NativeDQN, NativeReplay
+    from acme_amd import _lib, replay, specs
+    from acme_amd.adders import reverb as adders
+    from acme_amd.agents.dqn import DQNLearner
+    from acme_amd.datasets import make_reverb_dataset
     from acme_amd.networks import DQNAtariNetwork
+    from acme_amd.utils import counting, loggers
     L = _lib.lib()
 
+    # The measured path is the drop-in one: GPU replay Table (Reverb replacement) ->
+    # make_reverb_dataset iterator -> DQNLearner.step() -> update_priorities.
     B, A = args.batch, args.num_actions
     shard = -(-args.replay_size // world)
     t_fill = time.perf_counter()
-    replay = NativeReplay(shard, [OBS_BYTES, 4, 4, 4, OBS_BYTES], prioritized=True,
-                          priority_exponent=0.6, seed=1234 + rank, device=dev)
-    replay.fill_synthetic(shard, layout=0, num_actions=A, seed=rank)
-    learner = NativeDQN(network="nature", num_actions=A, max_batch=B, obs_dtype="uint8",
-                        discount=0.99, importance_sampling_exponent=0.2, learning_rate=1e-3,
-                        target_update_period=100, device=dev)
+    env_spec = specs.EnvironmentSpec(
+        observations=specs.Array((84, 84, 4), np.uint8), actions=specs.DiscreteArray(A, np.int32),
+        rewards=specs.Array((), np.float32), discounts=specs.BoundedArray((), np.float32, 0, 1))
+    table = replay.Table(adders.DEFAULT_PRIORITY_TABLE, replay.selectors.Prioritized(0.6),
+                         replay.selectors.Fifo(), shard, replay.rate_limiters.MinSize(1),
+                         signature=adders.NStepTransitionAdder.signature(env_spec),
+                         seed=1234 + rank, device=dev)
+    assert [f.row_bytes for f in table.fields] == [OBS_BYTES, 4, 4, 4, OBS_BYTES]
+    table.native.fill_synthetic(shard, layout=0, num_actions=A, seed=rank)
+    server = replay.Server([table])
+    dataset = make_reverb_dataset(server, batch_size=B)
     net = DQNAtariNetwork(A)
-    p0 = net.init(seed=0)  # identical on every rank
-    learner.set_params(p0, p0)
+    learner = DQNLearner(net, net, discount=0.99, importance_sampling_exponent=0.2,
+                         learning_rate=1e-3, target_update_period=100, dataset=dataset,
+                         replay_client=replay.Client(server), counter=counting.Counter(),
+                         logger=loggers.NoOpLogger(), seed=0, device=dev)
     torch.cuda.synchronize(dev)
     t_fill = time.perf_counter() - t_fill
 
-    info = replay.alloc_sample_info(B)
-    o_tm1 = torch.empty(B, OBS_BYTES, dtype=torch.uint8, device=dev)
-    a_tm1 = torch.empty(B, dtype=torch.int32, device=dev)
-    r_t = torch.empty(B, dtype=torch.float32, device=dev)
-    d_t = torch.empty(B, dtype=torch.float32, device=dev)
-    o_t = torch.empty(B, OBS_BYTES, dtype=torch.uint8, device=dev)
-    gmin = torch.empty(1, dtype=torch.float64, device=dev) if world > 1 else None
-    stream = torch.cuda.current_stream(dev)
-
     def step(i):
-        replay.sample(B, i, out=info, stream=stream)
-        replay.gather(info["slots"], [o_tm1, a_tm1, r_t, d_t, o_t], stream=stream)
-        if world > 1:
-            _lib.check(L.acme_min_f64(info["probabilities"].data_ptr(), B, gmin.data_ptr(),
-                                      _lib.stream_ptr(stream)))
-            dist.all_reduce(gmin, op=dist.ReduceOp.MIN)
-        learner.forward_backward(o_tm1, a_tm1, r_t, d_t, o_t, info["probabilities"],
-                                 global_min_probability=gmin, stream=stream)
-        if world > 1:
-            dist.all_reduce(learner.grads, op=dist.ReduceOp.AVG)
-        learner.apply(stream=stream)
-        replay.update_priorities(info["keys"], learner.priorities[:B], stream=stream)
+        learner.step()
 
     for i in range(args.warmup):
         step(i)
@@ -194,7 +186,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     L.acme_profile_enable(0)
-    loss = float(learner.loss.item())
+    loss = float(learner.native.loss.item())
 
     sections = []
     for i in range(L.acme_profile_num_sections()):
