@@ -124,7 +124,7 @@ inline float* Pm(const acme_dqn* l, float* base, int t) { return base + l->tenso
 // Split-K helper: chunk size (multiple of BK) for `splits` splits of K.
 inline int chunk_for(int K, int splits) {
   int c = (int)ceil_div(K, splits);
-  return (int)ceil_div(c, gemm::BK) * gemm::BK;
+  return (int)ceil_div(c, 32) * 32;
 }
 
 #define ACME_GEMM(BM, BN, WM, WN, prob, splits)                                      \
@@ -143,9 +143,34 @@ inline int chunk_for(int K, int splits) {
   } while (0)
 #define ACME_GEMM_N(name, BM, BN, WM, WN, prob, splits) \
   ACME_GEMM_F(name, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, BM, BN, WM, WN, prob, splits)
+// Tile variant selection for tuning runs: ACME_V_<KEY>=<n> in the environment (read once
+// per key); 0 is the shipped default.
+int tune(const char* key) {
+  static std::vector<std::pair<std::string, int>> cache;
+  for (auto& kv : cache)
+    if (kv.first == key) return kv.second;
+  const char* v = getenv((std::string("ACME_V_") + key).c_str());
+  const int x = v ? atoi(v) : 0;
+  cache.emplace_back(key, x);
+  return x;
+}
+
+// Same with an explicit reduction stage depth BK (16 or 32).
+#ifndef ACME_BIG_BK
+#define ACME_BIG_BK 16
+#endif
+#define ACME_GEMM_NK(name, BM, BN, WM, WN, BKV, prob, splits)                                 \
+  do {                                                                                         \
+    ACME_PROF(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0);   \
+    hipError_t _e = launch_gemm<BM, BN, WM, WN, BKV>(prob, splits, st);                       \
+    if (_e != hipSuccess) {                                                                    \
+      set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
+      return ACME_ERR_HIP;                                                                     \
+    }                                                                                          \
+  } while (0)
 
 // Split counts (K-splits) of the launches whose natural grid is too small to fill 256 CUs.
-constexpr int kFcFwdSplits = 4;     // [rows, 1024] x K 7744: 16x16 tiles x 4 = 1024 blocks
+constexpr int kFcFwdSplits = 8;  // [rows, 1024] x K 7744: 128x128 tiles: 8x8x8 = 512 blocks (online)
 constexpr int kHeadFwdSplits = 16;  // [rows, A+1] x K 1024
 constexpr int kHeadBwdSplits = 8;   // [1024, A+1] x K = batch
 constexpr int kConv1WgradSplits = 256, kConv2WgradSplits = 64, kConv3WgradSplits = 64;
@@ -178,7 +203,12 @@ int nature_forward(acme_dqn* l, const float* prm, const void* obs_a, const void*
     p.M = rows * G1::OPIX; p.N = G1::CO; p.K = G1::K; p.k_chunk = G1::K;
     p.x = static_cast<const uint8_t*>(obs_a); p.x2 = static_cast<const uint8_t*>(obs_b);
     p.split_b = split; p.w = P(l, prm, l->t_c1w); p.bias = P(l, prm, l->t_c1b); p.y = x1;
-    ACME_GEMM_N("conv1_fwd", 256, 32, 4, 1, p, 1);
+    switch (tune("CONV1FWD")) {
+      case 1: ACME_GEMM_NK("conv1_fwd", 256, 32, 4, 1, 16, p, 1); break;
+      case 2: ACME_GEMM_NK("conv1_fwd", 256, 32, 4, 1, 32, p, 1); break;
+      case 3: ACME_GEMM_NK("conv1_fwd", 512, 32, 8, 1, 16, p, 1); break;
+      default: ACME_GEMM_NK("conv1_fwd", 128, 32, 4, 1, 16, p, 1); break;
+    }
   } else {
     ConvFwd<G1, InF32> p;
     p.M = rows * G1::OPIX; p.N = G1::CO; p.K = G1::K; p.k_chunk = G1::K;
@@ -191,24 +221,43 @@ int nature_forward(acme_dqn* l, const float* prm, const void* obs_a, const void*
     p.M = rows * G2::OPIX; p.N = G2::CO; p.K = G2::K; p.k_chunk = G2::K;
     p.x = x1; p.x2 = x1; p.split_b = rows; p.w = P(l, prm, l->t_c2w);
     p.bias = P(l, prm, l->t_c2b); p.y = x2;
-    ACME_GEMM_N("conv2_fwd", 128, 64, 2, 2, p, 1);
+    switch (tune("CONVFWD")) {
+      case 1: ACME_GEMM_NK("conv2_fwd", 256, 64, 4, 1, 16, p, 1); break;
+      case 2: ACME_GEMM_NK("conv2_fwd", 128, 64, 2, 2, 32, p, 1); break;
+      case 3: ACME_GEMM_NK("conv2_fwd", 256, 64, 4, 2, 16, p, 1); break;
+      case 4: ACME_GEMM_NK("conv2_fwd", 128, 64, 4, 1, 16, p, 1); break;
+      default: ACME_GEMM_NK("conv2_fwd", 128, 64, 2, 2, 16, p, 1); break;
+    }
   }
   {
     ConvFwd<G3, InF32> p;
     p.M = rows * G3::OPIX; p.N = G3::CO; p.K = G3::K; p.k_chunk = G3::K;
     p.x = x2; p.x2 = x2; p.split_b = rows; p.w = P(l, prm, l->t_c3w);
     p.bias = P(l, prm, l->t_c3b); p.y = x3;
-    ACME_GEMM_N("conv3_fwd", 128, 64, 2, 2, p, 1);
+    switch (tune("CONVFWD")) {
+      case 1: ACME_GEMM_NK("conv3_fwd", 256, 64, 4, 1, 16, p, 1); break;
+      case 2: ACME_GEMM_NK("conv3_fwd", 128, 64, 2, 2, 32, p, 1); break;
+      case 3: ACME_GEMM_NK("conv3_fwd", 256, 64, 4, 2, 16, p, 1); break;
+      case 4: ACME_GEMM_NK("conv3_fwd", 128, 64, 4, 1, 16, p, 1); break;
+      default: ACME_GEMM_NK("conv3_fwd", 128, 64, 2, 2, 16, p, 1); break;
+    }
   }
   {  // Fused duelling hidden layer, split-K partials then bias + ReLU in the reduction.
     DenseFwd<true> p;
-    p.M = rows; p.N = 2 * kHidden; p.K = kFlat; p.k_chunk = chunk_for(kFlat, kFcFwdSplits);
+    const int v = tune("FCFWD");
+    const int splits = v == 3 ? 4 : kFcFwdSplits;
+    p.M = rows; p.N = 2 * kHidden; p.K = kFlat; p.k_chunk = chunk_for(kFlat, splits);
     p.x = x3; p.x2 = x3; p.split_b = rows; p.ldx = kFlat;
     p.w = P(l, prm, l->t_fcw); p.bias = P(l, prm, l->t_fcb); p.y = hid; p.act = ACT_RELU;
     p.slab = l->slab;
-    ACME_GEMM_N("fc_fwd", 64, 64, 2, 2, p, kFcFwdSplits);
+    switch (v) {
+      case 1: ACME_GEMM_NK("fc_fwd", 128, 128, 2, 2, 16, p, splits); break;
+      case 2: ACME_GEMM_NK("fc_fwd", 256, 128, 4, 2, 16, p, splits); break;
+      case 4: ACME_GEMM_NK("fc_fwd", 64, 64, 2, 2, 16, p, splits); break;
+      default: ACME_GEMM_NK("fc_fwd", 128, 128, 2, 2, 32, p, splits); break;
+    }
     const int64_t cnt = (int64_t)rows * 2 * kHidden;
-    int rc = slab_reduce(l->slab, kFcFwdSplits, cnt, hid, cnt, nullptr, P(l, prm, l->t_fcb),
+    int rc = slab_reduce(l->slab, splits, cnt, hid, cnt, nullptr, P(l, prm, l->t_fcb),
                          2 * kHidden, 1, "fc_fwd_reduce", st);
     if (rc != ACME_OK) return rc;
   }
@@ -329,7 +378,11 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st) {
     DenseDgrad<true> p;
     p.M = B; p.N = kFlat; p.K = 2 * kHidden; p.k_chunk = p.K;
     p.dz = l->dzh; p.w = P(l, prm, l->t_fcw); p.xprev = l->x3; p.ldx = kFlat; p.dx = l->dz3;
-    ACME_GEMM_N("fc_dgrad", 64, 128, 2, 2, p, 1);
+    switch (tune("FCDGRAD")) {
+      case 1: ACME_GEMM_NK("fc_dgrad", 128, 128, 2, 2, 16, p, 1); break;
+      case 2: ACME_GEMM_NK("fc_dgrad", 64, 128, 1, 2, 16, p, 1); break;
+      default: ACME_GEMM_NK("fc_dgrad", 64, 128, 2, 2, 16, p, 1); break;
+    }
   }
   // conv3
   if ((rc = conv_wgrad<G3, InF32, 64, 64, 2, 2>(l, l->x2, l->dz3, B, kConv3WgradSplits,
@@ -340,7 +393,11 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st) {
     ConvDgrad<G3> p;
     p.M = B * G3::IPIX; p.N = G3::CI; p.K = G3::KH * G3::KW * G3::CO; p.k_chunk = p.K;
     p.dz = l->dz3; p.w = P(l, prm, l->t_c3w); p.xprev = l->x2; p.dx = l->dz2;
-    ACME_GEMM_N("conv3_dgrad", 128, 64, 2, 2, p, 1);
+    switch (tune("CONV3DGRAD")) {
+      case 1: ACME_GEMM_NK("conv3_dgrad", 128, 64, 4, 1, 16, p, 1); break;
+      case 2: ACME_GEMM_NK("conv3_dgrad", 256, 64, 4, 2, 16, p, 1); break;
+      default: ACME_GEMM_NK("conv3_dgrad", 128, 64, 2, 2, 16, p, 1); break;
+    }
   }
   // conv2
   if ((rc = conv_wgrad<G2, InF32, 64, 64, 2, 2>(l, l->x1, l->dz2, B, kConv2WgradSplits,

@@ -10,16 +10,22 @@
 // 1e-5 rtol, so the dense layers stay in f32.
 //
 // Tiling: 64*WM*WN threads; each wave owns a (BM/WM) x (BN/WN) output sub-tile made of
-// 32x32 MFMA tiles.  BK = 16 reduction elements per stage, two LDS stages (one barrier
-// per stage), global->register prefetch of stage k+1 overlapping the MFMAs of stage k.
+// 32x32 MFMA tiles.  BK (16 or 32) reduction elements per stage, two LDS stages (one
+// barrier per stage), global->register prefetch of stage k+1 overlapping the MFMAs of
+// stage k.
 //
-// LDS image: both operands are stored "k-contiguous", T[row][k] with a row stride of
-// 20 floats.  A lane (r = lane & 31, h = lane >> 5) fetches T[row r][8q + 4h .. +3] with
-// one ds_read_b128 and feeds the four values to four consecutive MFMAs (physical k =
-// 8q + 4h + t at MFMA step t).  A and B use the same k permutation, so the sum over k
-// is unchanged.  Stride 20 makes the ds_read_b128 lane groups hit 16 distinct 16-B bank
-// slots (conflict-free); the transposing ds_write_b32 of row-contiguous operands also
-// lands on 32 distinct banks.
+// LDS image: a lane (r = lane & 31, h = lane >> 5) fetches 4 consecutive k of its row
+// with one ds_read_b128 and feeds them to four consecutive MFMAs (physical k =
+// 8q + 4h + t at MFMA step t); A and B use the same k permutation, so the sum over k
+// is unchanged.  Two row layouts, chosen per operand by how its loader delivers data:
+//   * k-contiguous operands (loader returns 4 consecutive k, stored with ds_write_b128):
+//     unpadded rows of BK floats with the 16-B chunks XOR-swizzled by the row,
+//     chunk' = chunk ^ s(row), s = (row >> 2) & 3 (BK 16) or (row >> 1) & 7 (BK 32).
+//     Conflict-free for both the b128 stores and the b128 fragment reads (checked
+//     exhaustively against the LDS lane-group table of MI355X_MICROARCH.md).  The padded
+//     layout it replaces had 2-way store conflicts (20-35% of LDS cycles, PMC).
+//   * row-contiguous operands (loader returns 4 consecutive rows, stored with
+//     ds_write_b32): rows of BK + 4 floats, conflict-free for b32 stores and b128 reads.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -32,9 +38,6 @@ namespace gemm {
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 
-constexpr int BK = 16;
-constexpr int LDS_STRIDE = BK + 4;
-
 // Operand global-memory orientation.
 //   KCONTIG: the loader returns A[row][k .. k+3] (4 consecutive reduction elements).
 //   RCONTIG: the loader returns A[row .. row+3][k] (4 consecutive rows).
@@ -42,32 +45,48 @@ enum OperandMode { KCONTIG = 0, RCONTIG = 1 };
 
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
-// Per-thread slots of an operand tile of R rows x BK.
-template <int R, int NT, int MODE>
+template <int BK>
+__device__ __forceinline__ int kswz(int row) {
+  return BK == 16 ? ((row >> 2) & 3) : ((row >> 1) & 7);
+}
+
+// Per-thread slots and LDS image of an operand tile of R rows x BK.
+template <int R, int NT, int MODE, int BK>
 struct OperandPlan {
-  static constexpr int VECS = R * BK / 4;  // float4 vectors per tile
+  static constexpr int CH = BK / 4;                 // 16-B chunks per row
+  static constexpr int STRIDE = MODE == KCONTIG ? BK : BK + 4;
+  static constexpr int FLOATS = R * STRIDE;         // one LDS stage
+  static constexpr int VECS = R * BK / 4;           // float4 vectors per tile
   static constexpr int PER_THREAD = (VECS + NT - 1) / NT;
   static_assert(VECS % NT == 0 || VECS < NT, "tile vectors must divide evenly over the threads");
   // Thread tid owns vectors tid + i*NT; when the tile has fewer vectors than threads the
   // surplus threads own none.
   __device__ static __forceinline__ bool owns(int v) { return VECS >= NT || v < VECS; }
-  // KCONTIG: vector v -> (row v / 4, kk 4*(v % 4)).  RCONTIG: v -> (row 4*(v / BK), kk v % BK).
+  // KCONTIG: vector v -> (row v / CH, kk 4*(v % CH)).  RCONTIG: v -> (row 4*(v / BK), kk v % BK).
   __device__ static __forceinline__ int row_of(int v) {
-    return MODE == KCONTIG ? (v >> 2) : ((v / BK) << 2);
+    return MODE == KCONTIG ? (v / CH) : ((v / BK) << 2);
   }
   __device__ static __forceinline__ int kk_of(int v) {
-    return MODE == KCONTIG ? ((v & 3) << 2) : (v % BK);
+    return MODE == KCONTIG ? ((v % CH) << 2) : (v % BK);
   }
   __device__ static __forceinline__ void store(float* tile, int v, f32x4 x) {
-    const int row = row_of(v), kk = kk_of(v);
+    const int row = row_of(v);
     if (MODE == KCONTIG) {
-      *reinterpret_cast<f32x4*>(&tile[row * LDS_STRIDE + kk]) = x;
+      const int ch = (v % CH) ^ kswz<BK>(row);
+      *reinterpret_cast<f32x4*>(&tile[row * STRIDE + 4 * ch]) = x;
     } else {
-      tile[(row + 0) * LDS_STRIDE + kk] = x[0];
-      tile[(row + 1) * LDS_STRIDE + kk] = x[1];
-      tile[(row + 2) * LDS_STRIDE + kk] = x[2];
-      tile[(row + 3) * LDS_STRIDE + kk] = x[3];
+      const int kk = kk_of(v);
+      tile[(row + 0) * STRIDE + kk] = x[0];
+      tile[(row + 1) * STRIDE + kk] = x[1];
+      tile[(row + 2) * STRIDE + kk] = x[2];
+      tile[(row + 3) * STRIDE + kk] = x[3];
     }
+  }
+  // Fragment of 4 k values for row `row` (whose low 5 bits are the lane's r) and
+  // logical chunk `c` (= 2q + h).
+  __device__ static __forceinline__ f32x4 frag(const float* tile, int row, int c) {
+    const int ch = MODE == KCONTIG ? (c ^ kswz<BK>(row)) : c;
+    return *reinterpret_cast<const f32x4*>(&tile[row * STRIDE + 4 * ch]);
   }
 };
 
@@ -93,16 +112,18 @@ struct HasColSum<P, decltype(void(P::kColSum))> {
 //   void store(int m, int n, float v, int split) const;
 // The loaders must return zeros for rows >= M / N and k >= K.
 
-template <int BM, int BN, int WM, int WN, class P>
+template <int BM, int BN, int WM, int WN, int BK, class P>
 __global__ void __launch_bounds__(64 * WM * WN) gemm_f32_kernel(const P p) {
   constexpr int NT = 64 * WM * WN;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int MT = TM / 32, NTL = TN / 32;
   static_assert(TM % 32 == 0 && TN % 32 == 0, "wave tile must be a multiple of 32x32");
-  using PA = OperandPlan<BM, NT, P::A_MODE>;
-  using PB = OperandPlan<BN, NT, P::B_MODE>;
+  static_assert(BK == 16 || BK == 32, "BK must be 16 or 32");
+  using PA = OperandPlan<BM, NT, P::A_MODE, BK>;
+  using PB = OperandPlan<BN, NT, P::B_MODE, BK>;
+  constexpr int STAGE = PA::FLOATS + PB::FLOATS;
 
-  __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * LDS_STRIDE];
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -140,8 +161,8 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_f32_kernel(const P p) {
     }
   };
   auto stash = [&](int buf) {
-    float* sa = smem + buf * (BM + BN) * LDS_STRIDE;
-    float* sb = sa + BM * LDS_STRIDE;
+    float* sa = smem + buf * STAGE;
+    float* sb = sa + PA::FLOATS;
 #pragma unroll
     for (int i = 0; i < PA::PER_THREAD; ++i)
       if (PA::owns(tid + i * NT)) PA::store(sa, tid + i * NT, ra[i]);
@@ -170,25 +191,24 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_f32_kernel(const P p) {
   for (int kt = 0; kt < nk; ++kt) {
     const bool more = kt + 1 < nk;
     if (more) fetch(kbeg + (kt + 1) * BK);
-    const float* sa = smem + (kt & 1) * (BM + BN) * LDS_STRIDE;
-    const float* sb = sa + BM * LDS_STRIDE;
+    const float* sa = smem + (kt & 1) * STAGE;
+    const float* sb = sa + PA::FLOATS;
     if constexpr (kColSum) {
       if (do_colsum) {
 #pragma unroll
-        for (int k = 0; k < BK; ++k) colsum += sb[tid * LDS_STRIDE + k];
+        for (int c = 0; c < BK / 4; ++c) {
+          const f32x4 x = PB::frag(sb, tid, c);
+          colsum += (x[0] + x[1]) + (x[2] + x[3]);
+        }
       }
     }
 #pragma unroll
     for (int q = 0; q < BK / 8; ++q) {
       f32x4 af[MT], bf[NTL];
 #pragma unroll
-      for (int i = 0; i < MT; ++i)
-        af[i] = *reinterpret_cast<const f32x4*>(
-            &sa[(wm * TM + i * 32 + r) * LDS_STRIDE + 8 * q + 4 * h]);
+      for (int i = 0; i < MT; ++i) af[i] = PA::frag(sa, wm * TM + i * 32 + r, 2 * q + h);
 #pragma unroll
-      for (int j = 0; j < NTL; ++j)
-        bf[j] = *reinterpret_cast<const f32x4*>(
-            &sb[(wn * TN + j * 32 + r) * LDS_STRIDE + 8 * q + 4 * h]);
+      for (int j = 0; j < NTL; ++j) bf[j] = PB::frag(sb, wn * TN + j * 32 + r, 2 * q + h);
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -217,10 +237,10 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_f32_kernel(const P p) {
   }
 }
 
-template <int BM, int BN, int WM, int WN, class P>
+template <int BM, int BN, int WM, int WN, int BK = 16, class P>
 inline hipError_t launch_gemm(const P& p, int splits, hipStream_t st) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, P>), dim3(tiles, 1, splits),
+  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, BK, P>), dim3(tiles, 1, splits),
                      dim3(64 * WM * WN), 0, st, p);
   return hipGetLastError();
 }
