@@ -25,6 +25,9 @@ ACME_ERR_OOM = -4
 
 MAX_FIELDS = 8
 MAX_MLP_LAYERS = 8
+D4PG_MAX_LAYERS = 4
+D4PG_MAX_ACT = 16
+D4PG_MAX_ATOMS = 64
 
 c_i32, c_i64, c_u64, c_f32, c_f64, c_vp = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64,
                                           ctypes.c_float, ctypes.c_double, ctypes.c_void_p)
@@ -53,6 +56,27 @@ class TransitionBatch(ctypes.Structure):
 
 class DQNOutputs(ctypes.Structure):
     _fields_ = [("loss", c_vp), ("td_error", c_vp), ("priorities", c_vp), ("q_tm1", c_vp)]
+
+
+class D4PGConfig(ctypes.Structure):
+    _fields_ = [("obs_dim", c_i32), ("act_dim", c_i32), ("max_batch", c_i32),
+                ("num_policy_layers", c_i32), ("policy_sizes", c_i32 * D4PG_MAX_LAYERS),
+                ("num_critic_layers", c_i32), ("critic_sizes", c_i32 * D4PG_MAX_LAYERS),
+                ("num_atoms", c_i32), ("vmin", c_f32), ("vmax", c_f32),
+                ("action_min", c_f32 * D4PG_MAX_ACT), ("action_max", c_f32 * D4PG_MAX_ACT),
+                ("discount", c_f32), ("target_update_period", c_i32),
+                ("policy_learning_rate", c_f32), ("critic_learning_rate", c_f32),
+                ("adam_beta1", c_f32), ("adam_beta2", c_f32), ("adam_epsilon", c_f32),
+                ("clipping", c_i32), ("layer_norm_epsilon", c_f32)]
+
+
+class D4PGBatch(ctypes.Structure):
+    _fields_ = [("o_tm1", c_vp), ("a_tm1", c_vp), ("r_t", c_vp), ("d_t", c_vp), ("o_t", c_vp),
+                ("batch", c_i64)]
+
+
+class D4PGOutputs(ctypes.Structure):
+    _fields_ = [("critic_loss", c_vp), ("policy_loss", c_vp)]
 
 
 _SIGS = {
@@ -90,6 +114,22 @@ _SIGS = {
                                       ctypes.POINTER(c_i64)]),
     "acme_dqn_set_num_steps": (c_i32, [c_vp, c_i64]),
     "acme_min_f64": (c_i32, [c_vp, c_i64, c_vp, c_vp]),
+    "acme_d4pg_create": (c_i32, [ctypes.POINTER(D4PGConfig), ctypes.POINTER(c_vp)]),
+    "acme_d4pg_destroy": (c_i32, [c_vp]),
+    "acme_d4pg_flat_size": (c_i64, [c_vp]),
+    "acme_d4pg_policy_size": (c_i64, [c_vp]),
+    "acme_d4pg_num_tensors": (c_i32, [c_vp]),
+    "acme_d4pg_tensor_info": (c_i32, [c_vp, c_i32, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64),
+                                      ctypes.POINTER(c_i32), ctypes.POINTER(c_i64),
+                                      ctypes.POINTER(ctypes.c_char_p)]),
+    "acme_d4pg_bind": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "acme_d4pg_step": (c_i32, [c_vp, ctypes.POINTER(D4PGBatch), ctypes.POINTER(D4PGOutputs),
+                               c_vp]),
+    "acme_d4pg_policy": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp]),
+    "acme_d4pg_num_steps": (c_i64, [c_vp]),
+    "acme_d4pg_set_num_steps": (c_i32, [c_vp, c_i64]),
+    "acme_d4pg_debug_buffer": (c_i32, [c_vp, ctypes.c_char_p, ctypes.POINTER(c_vp),
+                                       ctypes.POINTER(c_i64)]),
     "acme_profile_enable": (c_i32, [c_i32]),
     "acme_profile_reset": (c_i32, []),
     "acme_profile_num_sections": (c_i32, []),

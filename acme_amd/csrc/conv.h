@@ -286,7 +286,22 @@ __device__ __forceinline__ f32x4 load_row4(const float* p, int k, int lim) {
   return r;
 }
 
-enum Act { ACT_NONE = 0, ACT_RELU = 1 };
+enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_ELU = 2, ACT_TANH = 3 };
+
+// Forward activation (tf.nn.relu / tf.nn.elu = expm1 for x < 0 / tf.tanh).
+__device__ __forceinline__ float act_fwd(int act, float v) {
+  if (act == ACT_RELU) return v > 0.f ? v : 0.f;
+  if (act == ACT_ELU) return v < 0.f ? expm1f(v) : v;
+  if (act == ACT_TANH) return tanhf(v);
+  return v;
+}
+// Gradient through an activation, from its OUTPUT y (TF's ReluGrad / EluGrad / TanhGrad).
+__device__ __forceinline__ float act_bwd(int act, float y, float g) {
+  if (act == ACT_RELU) return y > 0.f ? g : 0.f;
+  if (act == ACT_ELU) return y < 0.f ? g * (y + 1.f) : g;
+  if (act == ACT_TANH) return g * (1.f - y * y);
+  return g;
+}
 
 template <bool VEC, class In = InF32>
 struct DenseFwd {
@@ -333,8 +348,7 @@ struct DenseFwd {
       return;
     }
     v += bias[n];
-    if (act == ACT_RELU) v = v > 0.f ? v : 0.f;
-    y[(size_t)m * N + n] = v;
+    y[(size_t)m * N + n] = act_fwd(act, v);
   }
 };
 
@@ -387,6 +401,7 @@ struct DenseDgrad {
   const float* xprev;    // [rows][ldx] post-ReLU input (mask), may be null (no mask)
   int ldx;
   float* dx;             // [rows][ldx]
+  int act = ACT_RELU;    // activation that produced xprev
   struct ARow {
     const float* p;
   };
@@ -405,7 +420,7 @@ struct DenseDgrad {
   }
   __device__ void store(int m, int n, float v, int) const {
     const size_t idx = (size_t)m * ldx + n;
-    if (xprev) v = xprev[idx] > 0.f ? v : 0.f;
+    if (xprev) v = act_bwd(act, xprev[idx], v);
     dx[idx] = v;
   }
 };

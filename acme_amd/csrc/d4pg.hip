@@ -1,0 +1,1103 @@
+// D4PG learner step for MI355X: the replacement of D4PGLearner._step
+// (acme/agents/tf/d4pg/learning.py:156-247) behind the C ABI (include/acme_hip.h).
+//
+// One call = the whole step on one stream, no host synchronisation:
+//   target <- online when num_steps % period == 0 (at the start)          (:171-175)
+//   online policy on o_t (dpg actions), target policy on o_t              (:199, :206)
+//   online critic on [o_tm1, a_tm1 ; o_t, dpg_a] as ONE 2B-row pass        (:198, :207)
+//   target critic on (o_t, target actions)                                (:199)
+//   fused loss kernel: categorical L2 projection + softmax cross-entropy   (:202-203)
+//     for rows < B, d mean(q) / d logits for the dpg rows                  (:208)
+//   critic backward over 2B rows (weight gradients from the first B rows
+//     only); the LayerNorm backward of the dpg rows also forms dq/da,
+//     tf.clip_by_norm(., 1) and dloss/da = -dqda / B                      (:211-218, dpg.py)
+//   policy backward; clip_by_global_norm(40) per network; two Adams       (:221-241)
+//
+// Networks (examples/control_suite/run_d4pg.py:60-81): LayerNormMLP
+// (acme/tf/networks/continuous.py:37-68) = Linear -> LayerNorm -> tanh -> MLP(elu,
+// activate_final); policy head NearZeroInitializedLinear + TanhToSpec
+// (rescaling.py:55-74); critic head DiscreteValuedHead (distributional.py:36-67).
+//
+// Small-batch regime (B = 256, widths <= 512): the step is ~1.5 GFLOP, so it is latency
+// bound.  Dense layers go through the fp32 MFMA GEMM engine with fused bias/activation
+// epilogues and masked dgrads; the row-wise work (LayerNorm+tanh, TanhToSpec head,
+// projection loss, LayerNorm backward + dpg) are one-kernel-per-stage row kernels.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "conv.h"
+#include "gemm.h"
+#include "kernels.h"
+#include "profiler.h"
+
+using namespace acme;
+using namespace acme::conv;
+using acme::gemm::launch_gemm;
+
+namespace {
+
+constexpr int kRows = 4;      // rows per block of the LayerNorm row kernels
+constexpr int kMaxWidth = 1024;
+constexpr int kMaxIn = 64;    // obs_dim + act_dim
+constexpr int kNormBlocks = 256;
+
+struct Tensor {
+  std::string name;
+  int64_t offset = 0, numel = 0;
+  int ndim = 0;
+  int64_t shape[4] = {1, 1, 1, 1};
+};
+
+// Tensor indices of one LayerNormMLP + output layer.
+struct NetDesc {
+  int din = 0, nl = 0, nout = 0;
+  int sizes[ACME_D4PG_MAX_LAYERS] = {};
+  int w1 = -1, b1 = -1, scale = -1, offset = -1;
+  int w[ACME_D4PG_MAX_LAYERS] = {}, b[ACME_D4PG_MAX_LAYERS] = {};  // mlp linear_{i-1}, i >= 1
+  int ow = -1, ob = -1;                                            // output layer
+};
+
+// Activations of one evaluation of a network over `rows` rows.
+struct Acts {
+  float* z1 = nullptr;    // [rows][H0] first linear output (pre-LayerNorm)
+  float* mean = nullptr;  // [rows]
+  float* rstd = nullptr;  // [rows]
+  float* h[ACME_D4PG_MAX_LAYERS] = {};  // h[0] = tanh(LN(z1)), h[i] = elu(...)
+  float* out = nullptr;   // policy: actions [rows][act]; critic: logits [rows][atoms]
+  float* t = nullptr;     // policy: tanh of the head [rows][act]
+};
+
+}  // namespace
+
+struct acme_d4pg {
+  acme_d4pg_config cfg;
+  std::vector<Tensor> tensors;
+  int64_t flat = 0, policy_flat = 0;
+  float *params = nullptr, *target = nullptr, *grads = nullptr, *m = nullptr, *v = nullptr;
+  int64_t num_steps = 0;
+  NetDesc pol, cri;
+  std::vector<void*> allocs;
+  Acts pon, ptg, con, ctg;
+  float* cdz[ACME_D4PG_MAX_LAYERS] = {};  // critic pre-activation grads [2B][C_i]
+  float* pdz[ACME_D4PG_MAX_LAYERS] = {};  // policy [B][P_i]
+  float* dlogits = nullptr;               // [2B][atoms]
+  float* du = nullptr;                    // [B][act] dloss/d(policy head pre-tanh)
+  float* dqda = nullptr;                  // [B][act] clipped dq/da
+  float* values = nullptr;                // [atoms] support
+  float* act_lo = nullptr;                // [act]
+  float* act_scale = nullptr;             // [act]
+  float* lnslab = nullptr;                // LayerNorm parameter-gradient partials
+  float* ploss_part = nullptr;            // per-block dpg loss partials
+  double* norm_part = nullptr;            // [2][kNormBlocks]
+  float* norms = nullptr;                 // [2] global norms (policy, critic)
+  float* loss_tmp = nullptr;              // [2] critic / policy loss
+};
+
+namespace {
+
+int64_t align64(int64_t x) { return (x + 63) & ~int64_t(63); }
+
+int add_tensor(acme_d4pg* l, const std::string& name, std::initializer_list<int64_t> shape) {
+  Tensor t;
+  t.name = name;
+  t.ndim = (int)shape.size();
+  t.numel = 1;
+  int i = 0;
+  for (int64_t s : shape) {
+    t.shape[i++] = s;
+    t.numel *= s;
+  }
+  t.offset = l->flat;
+  l->flat = align64(l->flat + t.numel);
+  l->tensors.push_back(t);
+  return (int)l->tensors.size() - 1;
+}
+
+template <class T>
+int dev_alloc(acme_d4pg* l, T** p, int64_t count) {
+  void* q = nullptr;
+  if (hipMalloc(&q, std::max<int64_t>(count, 1) * sizeof(T)) != hipSuccess) {
+    set_error("hipMalloc of %lld bytes failed", (long long)(count * sizeof(T)));
+    return ACME_ERR_OOM;
+  }
+  l->allocs.push_back(q);
+  *p = static_cast<T*>(q);
+  return ACME_OK;
+}
+
+void add_net(acme_d4pg* l, NetDesc& d, const char* prefix, int din, int nl, const int32_t* sizes,
+             int nout, const char* head) {
+  d.din = din;
+  d.nl = nl;
+  d.nout = nout;
+  for (int i = 0; i < nl; ++i) d.sizes[i] = sizes[i];
+  const std::string p = std::string(prefix) + "/layer_norm_mlp";
+  d.w1 = add_tensor(l, p + "/linear/w", {din, sizes[0]});
+  d.b1 = add_tensor(l, p + "/linear/b", {sizes[0]});
+  d.scale = add_tensor(l, p + "/layer_norm/scale", {sizes[0]});
+  d.offset = add_tensor(l, p + "/layer_norm/offset", {sizes[0]});
+  for (int i = 1; i < nl; ++i) {
+    const std::string q = p + "/mlp/linear_" + std::to_string(i - 1);
+    d.w[i] = add_tensor(l, q + "/w", {sizes[i - 1], sizes[i]});
+    d.b[i] = add_tensor(l, q + "/b", {sizes[i]});
+  }
+  const std::string h = std::string(prefix) + "/" + head;
+  d.ow = add_tensor(l, h + "/w", {sizes[nl - 1], nout});
+  d.ob = add_tensor(l, h + "/b", {nout});
+}
+
+int alloc_acts(acme_d4pg* l, Acts& a, const NetDesc& d, int rows, bool policy) {
+  int rc;
+  if ((rc = dev_alloc(l, &a.z1, (int64_t)rows * d.sizes[0])) ||
+      (rc = dev_alloc(l, &a.mean, rows)) || (rc = dev_alloc(l, &a.rstd, rows)) ||
+      (rc = dev_alloc(l, &a.out, (int64_t)rows * d.nout)))
+    return rc;
+  for (int i = 0; i < d.nl; ++i)
+    if ((rc = dev_alloc(l, &a.h[i], (int64_t)rows * d.sizes[i]))) return rc;
+  if (policy && (rc = dev_alloc(l, &a.t, (int64_t)rows * d.nout))) return rc;
+  return ACME_OK;
+}
+
+inline const float* P(const acme_d4pg* l, const float* base, int t) {
+  return base + l->tensors[t].offset;
+}
+inline float* Pm(const acme_d4pg* l, float* base, int t) { return base + l->tensors[t].offset; }
+
+// ------------------------------------------------------------------ device helpers
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Sums N per-thread values over a 256-thread block; every thread gets the totals.
+template <int N>
+__device__ __forceinline__ void block_sum256(float (&v)[N], float (*red)[N]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = wave_sum(v[i]);
+  __syncthreads();
+  if (lane == 0)
+#pragma unroll
+    for (int i = 0; i < N; ++i) red[wave][i] = v[i];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
+}
+
+// ------------------------------------------------------------------ LayerNorm first layer
+// h = tanh(LayerNorm(concat(xa, xb) @ W + b)) for kRows rows per 256-thread block.
+// Rows < split read (xa0, xb0), the others (xa1, xb1) at row - split.
+struct LnFirstArgs {
+  const float *xa0, *xb0, *xa1, *xb1;
+  int split, rows, da, db, H;
+  const float *w, *b, *scale, *offset;
+  float eps;
+  float *z, *mean, *rstd, *h;
+};
+
+__global__ void __launch_bounds__(256) ln_first_kernel(const LnFirstArgs a) {
+  __shared__ float xs[kRows][kMaxIn];
+  __shared__ float red[4][kRows];
+  const int tid = threadIdx.x;
+  const int r0 = blockIdx.x * kRows;
+  const int din = a.da + a.db;
+  for (int i = tid; i < kRows * din; i += 256) {
+    const int r = i / din, k = i - r * din, row = r0 + r;
+    float v = 0.f;
+    if (row < a.rows) {
+      const bool second = row >= a.split;
+      const int rr = second ? row - a.split : row;
+      v = k < a.da ? (second ? a.xa1 : a.xa0)[(size_t)rr * a.da + k]
+                   : (second ? a.xb1 : a.xb0)[(size_t)rr * a.db + (k - a.da)];
+    }
+    xs[r][k] = v;
+  }
+  __syncthreads();
+  constexpr int C = kMaxWidth / 256;
+  float acc[kRows][C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const int j = tid + 256 * c;
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) acc[r][c] = 0.f;
+    if (j < a.H) {
+      for (int k = 0; k < din; ++k) {
+        const float wk = a.w[(size_t)k * a.H + j];
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) acc[r][c] = fmaf(xs[r][k], wk, acc[r][c]);
+      }
+      const float bj = a.b[j];
+#pragma unroll
+      for (int r = 0; r < kRows; ++r) acc[r][c] += bj;
+    }
+  }
+  // tf.nn.moments over the feature axis: mean, then mean of squared deviations.
+  float s[kRows];
+#pragma unroll
+  for (int r = 0; r < kRows; ++r) {
+    s[r] = 0.f;
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+      if (tid + 256 * c < a.H) s[r] += acc[r][c];
+  }
+  block_sum256<kRows>(s, red);
+  const float invH = 1.f / (float)a.H;
+  float mean[kRows], q[kRows];
+#pragma unroll
+  for (int r = 0; r < kRows; ++r) {
+    mean[r] = s[r] * invH;
+    q[r] = 0.f;
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+      if (tid + 256 * c < a.H) {
+        const float dv = acc[r][c] - mean[r];
+        q[r] = fmaf(dv, dv, q[r]);
+      }
+  }
+  block_sum256<kRows>(q, red);
+#pragma unroll
+  for (int r = 0; r < kRows; ++r) {
+    const int row = r0 + r;
+    if (row >= a.rows) continue;
+    const float rs = 1.f / sqrtf(q[r] * invH + a.eps);
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const int j = tid + 256 * c;
+      if (j >= a.H) continue;
+      const size_t idx = (size_t)row * a.H + j;
+      a.z[idx] = acc[r][c];
+      const float y = (acc[r][c] - mean[r]) * rs * a.scale[j] + a.offset[j];
+      a.h[idx] = tanhf(y);
+    }
+    if (tid == 0) {
+      a.mean[row] = mean[r];
+      a.rstd[row] = rs;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ policy head
+// One wave per row: u = h @ W + b (A <= 16 outputs), t = tanh(u),
+// a = (0.5 (t + 1)) * (max - min) + min  (TanhToSpec, rescaling.py:70-73).
+__global__ void __launch_bounds__(256) policy_head_kernel(const float* __restrict__ h,
+                                                          const float* __restrict__ w,
+                                                          const float* __restrict__ b,
+                                                          const float* __restrict__ lo,
+                                                          const float* __restrict__ scale,
+                                                          int rows, int H, int A,
+                                                          float* __restrict__ t_out,
+                                                          float* __restrict__ a_out) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float acc[ACME_D4PG_MAX_ACT];
+#pragma unroll
+  for (int j = 0; j < ACME_D4PG_MAX_ACT; ++j) acc[j] = 0.f;
+  for (int k = lane; k < H; k += 64) {
+    const float hv = h[(size_t)row * H + k];
+#pragma unroll
+    for (int j = 0; j < ACME_D4PG_MAX_ACT; ++j)
+      if (j < A) acc[j] = fmaf(hv, w[(size_t)k * A + j], acc[j]);
+  }
+  float mine = 0.f;
+#pragma unroll
+  for (int j = 0; j < ACME_D4PG_MAX_ACT; ++j) {
+    if (j >= A) break;
+    const float s = wave_sum(acc[j]);
+    if (lane == j) mine = s;
+  }
+  if (lane < A) {
+    const float t = tanhf(mine + b[lane]);
+    if (t_out) t_out[(size_t)row * A + lane] = t;
+    a_out[(size_t)row * A + lane] = (0.5f * (t + 1.f)) * scale[lane] + lo[lane];
+  }
+}
+
+// ------------------------------------------------------------------ loss
+// One 1024-thread block; wave w handles rows w, w + 16, ...; lane i = atom i.
+//   rows < B  : categorical TD loss (distributional.py:22-41) with the L2 projection
+//               written exactly as l2_project (:44-83); dlogits = (softmax - target) / B.
+//   rows >= B : dpg rows; q = sum softmax * values, dq/dlogits = (values - q) * softmax.
+__global__ void __launch_bounds__(1024) d4pg_loss_kernel(
+    const float* __restrict__ c_logits, const float* __restrict__ t_logits,
+    const float* __restrict__ r, const float* __restrict__ d, const float* __restrict__ values,
+    int B, int K, float discount, float* __restrict__ dlogits, float* __restrict__ loss_out) {
+  __shared__ float part[16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool on = lane < K;
+  const float NEG = -INFINITY;
+  const float vi = on ? values[lane] : 0.f;
+  const float vmin = values[0], vmax = values[K - 1];
+  // Support spacings of l2_project: d_pos = Zq[i+1] - Zq[i] (wrapping to vmin), d_neg =
+  // Zq[i] - Zq[i-1] (wrapping to vmax).
+  const float dpos = on ? ((lane + 1 < K ? values[lane + 1] : vmin) - vi) : 1.f;
+  const float dneg = on ? (vi - (lane > 0 ? values[lane - 1] : vmax)) : 1.f;
+  const float invB = 1.f / (float)B;
+  float lsum = 0.f;
+  for (int row = wave; row < 2 * B; row += 16) {
+    const float ql = on ? c_logits[(size_t)row * K + lane] : NEG;
+    const float m2 = wave_max(ql);
+    const float e2 = on ? expf(ql - m2) : 0.f;
+    const float s2 = wave_sum(e2);
+    const float sm = e2 / s2;
+    if (row < B) {
+      const float tl = on ? t_logits[(size_t)row * K + lane] : NEG;
+      const float mx = wave_max(tl);
+      const float e = on ? expf(tl - mx) : 0.f;
+      const float pj = e / wave_sum(e);
+      const float gd = discount * d[row];
+      const float zj = r[row] + gd * vi;
+      const float zc = fminf(fmaxf(zj, vmin), vmax);
+      float tgt = 0.f;
+      for (int j = 0; j < K; ++j) {
+        const float zcj = __shfl(zc, j, 64), pjj = __shfl(pj, j, 64);
+        const float dq = zcj - vi;
+        const float sg = dq >= 0.f ? 1.f : 0.f;
+        const float dh = (sg * dq) / dpos - ((1.f - sg) * dq) / dneg;
+        tgt += fminf(fmaxf(1.f - dh, 0.f), 1.f) * pjj;
+      }
+      const float logp = ql - m2 - logf(s2);
+      const float ce = wave_sum(on ? -tgt * logp : 0.f);
+      if (on) dlogits[(size_t)row * K + lane] = invB * (sm - tgt);
+      lsum += ce;
+    } else {
+      const float q = wave_sum(on ? sm * vi : 0.f);
+      if (on) dlogits[(size_t)row * K + lane] = (vi - q) * sm;
+    }
+  }
+  if (lane == 0) part[wave] = lsum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < 16; ++w) t += part[w];
+    *loss_out = t / (float)B;
+  }
+}
+
+// ------------------------------------------------------------------ LayerNorm backward
+// Per row (kRows rows per block): dy = dLoss/d(LayerNorm output) (tanh' already
+// applied), xhat = (z - mean) * rstd, g = dy * scale,
+//   dz = rstd * (g - mean(g) - xhat * mean(g * xhat))
+// Rows < ce_rows: dz is written in place over dy and (dy * xhat, dy) are summed into
+// per-block column partials (LayerNorm scale / offset gradients).
+// Rows >= ce_rows (the critic's dpg rows): dqda = dz @ W1[act rows]^T, clipped to norm
+// <= clip (tf.clip_by_norm; clip <= 0 disables), du = -dqda / B * 0.5 * scale_a * (1-t^2)
+// (through TanhToSpec), and 0.5 |dqda|^2 summed into ploss_part[block].
+struct LnBwdArgs {
+  float* dy;  // [rows][H], overwritten with dz for rows < ce_rows
+  const float *z, *mean, *rstd, *scale;
+  int rows, ce_rows, H;
+  float* colslab;  // [gridDim.x][2][H]
+  // dpg
+  const float* w1;  // [din][H]
+  int act_off, A;
+  float clip, invB;
+  const float *t, *act_scale;  // [B][A], [A] (policy head tanh, TanhToSpec range)
+  float *du, *dqda, *ploss_part;
+};
+
+__global__ void __launch_bounds__(256) ln_bwd_kernel(const LnBwdArgs a) {
+  constexpr int C = kMaxWidth / 256;
+  __shared__ float red[4][2 * kRows];
+  __shared__ float redq[4][kRows * ACME_D4PG_MAX_ACT];
+  __shared__ float dq_s[kRows][ACME_D4PG_MAX_ACT];
+  const int tid = threadIdx.x;
+  const int r0 = blockIdx.x * kRows;
+  const float invH = 1.f / (float)a.H;
+  float g[kRows][C], xh[kRows][C], dyv[kRows][C];
+  float s[2 * kRows];
+#pragma unroll
+  for (int r = 0; r < kRows; ++r) {
+    const int row = r0 + r;
+    const bool ok = row < a.rows;
+    const float mu = ok ? a.mean[row] : 0.f, rs = ok ? a.rstd[row] : 0.f;
+    s[2 * r] = s[2 * r + 1] = 0.f;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const int j = tid + 256 * c;
+      g[r][c] = xh[r][c] = dyv[r][c] = 0.f;
+      if (ok && j < a.H) {
+        const size_t idx = (size_t)row * a.H + j;
+        dyv[r][c] = a.dy[idx];
+        xh[r][c] = (a.z[idx] - mu) * rs;
+        g[r][c] = dyv[r][c] * a.scale[j];
+        s[2 * r] += g[r][c];
+        s[2 * r + 1] = fmaf(g[r][c], xh[r][c], s[2 * r + 1]);
+      }
+    }
+  }
+  block_sum256<2 * kRows>(s, red);
+  float cs_x[C], cs_1[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) cs_x[c] = cs_1[c] = 0.f;
+  float dqp[kRows][ACME_D4PG_MAX_ACT];
+#pragma unroll
+  for (int r = 0; r < kRows; ++r)
+#pragma unroll
+    for (int k = 0; k < ACME_D4PG_MAX_ACT; ++k) dqp[r][k] = 0.f;
+  bool any_dpg = false;
+#pragma unroll
+  for (int r = 0; r < kRows; ++r) {
+    const int row = r0 + r;
+    if (row >= a.rows) continue;
+    const float rs = a.rstd[row];
+    const float m1 = s[2 * r] * invH, m2 = s[2 * r + 1] * invH;
+    const bool ce = row < a.ce_rows;
+    any_dpg |= !ce;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const int j = tid + 256 * c;
+      if (j >= a.H) continue;
+      const float dz = rs * (g[r][c] - m1 - xh[r][c] * m2);
+      if (ce) {
+        a.dy[(size_t)row * a.H + j] = dz;
+        cs_x[c] = fmaf(dyv[r][c], xh[r][c], cs_x[c]);
+        cs_1[c] += dyv[r][c];
+      } else {
+#pragma unroll
+        for (int k = 0; k < ACME_D4PG_MAX_ACT; ++k)
+          if (k < a.A) dqp[r][k] = fmaf(dz, a.w1[(size_t)(a.act_off + k) * a.H + j], dqp[r][k]);
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const int j = tid + 256 * c;
+    if (j < a.H) {
+      a.colslab[((size_t)blockIdx.x * 2 + 0) * a.H + j] = cs_x[c];
+      a.colslab[((size_t)blockIdx.x * 2 + 1) * a.H + j] = cs_1[c];
+    }
+  }
+  if (!any_dpg) {  // uniform per block: rows are contiguous
+    if (tid == 0 && a.ploss_part) a.ploss_part[blockIdx.x] = 0.f;
+    return;
+  }
+  const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int r = 0; r < kRows; ++r)
+#pragma unroll
+    for (int k = 0; k < ACME_D4PG_MAX_ACT; ++k) {
+      if (k >= a.A) break;
+      const float v = wave_sum(dqp[r][k]);
+      if (lane == 0) redq[wave][r * ACME_D4PG_MAX_ACT + k] = v;
+    }
+  __syncthreads();
+  if (tid < kRows * ACME_D4PG_MAX_ACT) {
+    const int r = tid / ACME_D4PG_MAX_ACT, k = tid % ACME_D4PG_MAX_ACT;
+    dq_s[r][k] = ((redq[0][tid] + redq[1][tid]) + redq[2][tid]) + redq[3][tid];
+  }
+  __syncthreads();
+  if (tid < kRows) {
+    const int row = r0 + tid;
+    float pl = 0.f;
+    if (row < a.rows && row >= a.ce_rows) {
+      const int b = row - a.ce_rows;
+      float n2 = 0.f;
+      for (int k = 0; k < a.A; ++k) n2 = fmaf(dq_s[tid][k], dq_s[tid][k], n2);
+      // tf.clip_by_norm(t, c): t * c / max(|t|, c), |t| = 0 kept as is.
+      const float nrm = n2 > 0.f ? sqrtf(n2) : 0.f;
+      const float den = a.clip > 0.f ? fmaxf(nrm, a.clip) : 1.f;
+      const float cm = a.clip > 0.f ? a.clip : 1.f;
+      for (int k = 0; k < a.A; ++k) {
+        const float dq = (dq_s[tid][k] * cm) / den;
+        a.dqda[(size_t)b * a.A + k] = dq;
+        pl = fmaf(0.5f * dq, dq, pl);
+        const float tk = a.t[(size_t)b * a.A + k];
+        const float da = -dq * a.invB;
+        a.du[(size_t)b * a.A + k] = da * a.act_scale[k] * 0.5f * (1.f - tk * tk);
+      }
+    }
+    // Sum the kRows partials of this block.
+    pl += __shfl_down(pl, 2, 64);
+    pl += __shfl_down(pl, 1, 64);
+    if (tid == 0) a.ploss_part[blockIdx.x] = pl;
+  }
+}
+
+// ------------------------------------------------------------------ weight gradient of the
+// first layer: dW = concat(x0, x1)^T dZ over the batch, bias = column sums of dZ.
+struct ConcatWgrad {
+  static constexpr int A_MODE = gemm::RCONTIG, B_MODE = gemm::RCONTIG;
+  static constexpr bool kColSum = true;
+  int M, N, K, k_chunk;  // M = d0 + d1 (inputs), N = H, K = batch rows
+  const float* x0;
+  int d0;
+  const float* x1;
+  int d1;
+  const float* dz;  // [K][N]
+  float* out;       // [M][N]
+  float* bias_out;  // [N]
+  struct ARow {
+    int i;
+  };
+  struct BRow {
+    int n;
+  };
+  __device__ ARow a_row(int i) const { return ARow{i}; }
+  __device__ float x_at(int m, int f) const {
+    if (f < d0) return x0[(size_t)m * d0 + f];
+    if (f < d0 + d1) return x1[(size_t)m * d1 + (f - d0)];
+    return 0.f;
+  }
+  __device__ f32x4 a_load(const ARow& a, int m) const {
+    f32x4 r = gemm::zero4();
+    if (m >= K) return r;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = x_at(m, a.i + j);
+    return r;
+  }
+  __device__ BRow b_row(int n) const { return BRow{n}; }
+  __device__ f32x4 b_load(const BRow& b, int m) const {
+    if (b.n >= N || m >= K) return gemm::zero4();
+    return load_row4<true>(dz + (size_t)m * N, b.n, N);
+  }
+  __device__ void store(int i, int n, float v, int) const { out[(size_t)i * N + n] = v; }
+  __device__ void store_colsum(int n, float v, int) const { bias_out[n] = v; }
+};
+
+// ------------------------------------------------------------------ clip + Adam
+// Sum of squared gradients per network (policy range [0, n_pol), critic the rest), f64
+// block partials in a fixed order.
+__global__ void __launch_bounds__(256) grad_sumsq_kernel(const float* __restrict__ g,
+                                                         int64_t n4, int64_t pol4,
+                                                         double* __restrict__ part) {
+  __shared__ double red[2][4];
+  double s0 = 0.0, s1 = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const f32x4 x = reinterpret_cast<const f32x4*>(g)[i];
+    const double q = (double)x[0] * x[0] + (double)x[1] * x[1] + (double)x[2] * x[2] +
+                     (double)x[3] * x[3];
+    if (i < pol4) s0 += q;
+    else s1 += q;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s0 += __shfl_xor(s0, o, 64);
+    s1 += __shfl_xor(s1, o, 64);
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[0][wave] = s0;
+    red[1][wave] = s1;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+    part[gridDim.x + blockIdx.x] = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+  }
+}
+
+struct AdamClipArgs {
+  float *p, *m, *v;
+  const float* g;
+  int64_t n4, pol4;
+  const double* part;
+  int nparts;
+  int clipping;
+  float clip_norm;
+  float lr_pol, lr_cri, b1, omb1, b2, omb2, bc1, bc2, eps;
+  float* norms;  // [2]
+  const float* ploss_part;
+  int nploss;
+  float invB;
+  float* policy_loss;
+};
+
+__global__ void __launch_bounds__(256) adam_clip_kernel(const AdamClipArgs a) {
+  __shared__ double red[2][4];
+  __shared__ float scl[2];
+  double s0 = 0.0, s1 = 0.0;
+  for (int i = threadIdx.x; i < a.nparts; i += 256) {
+    s0 += a.part[i];
+    s1 += a.part[a.nparts + i];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s0 += __shfl_xor(s0, o, 64);
+    s1 += __shfl_xor(s1, o, 64);
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[0][wave] = s0;
+    red[1][wave] = s1;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    const int k = threadIdx.x;
+    const double ss = ((red[k][0] + red[k][1]) + red[k][2]) + red[k][3];
+    const float G = (float)sqrt(ss);
+    // tf.clip_by_global_norm: scale = clip * min(1 / G, 1 / clip).
+    float s = 1.f;
+    if (a.clipping && G > 0.f) s = a.clip_norm * fminf(1.f / G, 1.f / a.clip_norm);
+    scl[k] = s;
+    if (blockIdx.x == 0 && a.norms) a.norms[k] = G;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 64 && a.policy_loss) {
+    float t = 0.f;
+    for (int i = 0; i < a.nploss; ++i) t += a.ploss_part[i];
+    *a.policy_loss = t * a.invB;
+  }
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < a.n4; i += (int64_t)gridDim.x * 256) {
+    const bool pol = i < a.pol4;
+    const float s = pol ? scl[0] : scl[1];
+    const float lr = pol ? a.lr_pol : a.lr_cri;
+    f32x4 gg = reinterpret_cast<const f32x4*>(a.g)[i];
+    f32x4 mm = reinterpret_cast<f32x4*>(a.m)[i];
+    f32x4 vv = reinterpret_cast<f32x4*>(a.v)[i];
+    f32x4 pp = reinterpret_cast<f32x4*>(a.p)[i];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float gj = __fmul_rn(gg[j], s);
+      const float mj = __fadd_rn(__fmul_rn(a.b1, mm[j]), __fmul_rn(a.omb1, gj));
+      const float vj = __fadd_rn(__fmul_rn(a.b2, vv[j]), __fmul_rn(a.omb2, __fmul_rn(gj, gj)));
+      const float mh = __fdiv_rn(mj, a.bc1);
+      const float vh = __fdiv_rn(vj, a.bc2);
+      const float upd = __fdiv_rn(__fmul_rn(lr, mh), __fadd_rn(__fsqrt_rn(vh), a.eps));
+      mm[j] = mj;
+      vv[j] = vj;
+      pp[j] = __fsub_rn(pp[j], upd);
+    }
+    reinterpret_cast<f32x4*>(a.m)[i] = mm;
+    reinterpret_cast<f32x4*>(a.v)[i] = vv;
+    reinterpret_cast<f32x4*>(a.p)[i] = pp;
+  }
+}
+
+// ------------------------------------------------------------------ orchestration
+
+#define D4_GEMM(name, BM, BN, WM, WN, prob)                                                    \
+  do {                                                                                        \
+    ACME_PROF(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0);   \
+    hipError_t _e = launch_gemm<BM, BN, WM, WN, 16>(prob, 1, st);                              \
+    if (_e != hipSuccess) {                                                                   \
+      set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
+      return ACME_ERR_HIP;                                                                    \
+    }                                                                                         \
+  } while (0)
+
+#define D4_CHECK()                                                                            \
+  do {                                                                                        \
+    hipError_t _e = hipGetLastError();                                                        \
+    if (_e != hipSuccess) {                                                                   \
+      set_error("kernel launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
+      return ACME_ERR_HIP;                                                                    \
+    }                                                                                         \
+  } while (0)
+
+// Dense layer forward y = act(x @ W + b) over `rows` rows.
+int dense_fwd(const char* name, const float* x, int rows, int K, const float* w, const float* b,
+              int N, int act, float* y, hipStream_t st) {
+  if (K % 4 == 0 && N % 4 == 0) {
+    DenseFwd<true> p;
+    p.M = rows; p.N = N; p.K = K; p.k_chunk = K;
+    p.x = x; p.x2 = x; p.split_b = rows; p.ldx = K;
+    p.w = w; p.bias = b; p.y = y; p.act = act; p.slab = nullptr;
+    D4_GEMM(name, 32, 64, 1, 2, p);
+  } else {
+    DenseFwd<false> p;
+    p.M = rows; p.N = N; p.K = K; p.k_chunk = K;
+    p.x = x; p.x2 = x; p.split_b = rows; p.ldx = K;
+    p.w = w; p.bias = b; p.y = y; p.act = act; p.slab = nullptr;
+    D4_GEMM(name, 32, 64, 1, 2, p);
+  }
+  return ACME_OK;
+}
+
+// dX = act'(xprev) * (dZ @ W^T): dz [rows][Nout], W [Nin][Nout], xprev/dx [rows][Nin].
+int dense_dgrad(const char* name, const float* dz, int rows, int Nout, const float* w, int Nin,
+                const float* xprev, int act, float* dx, hipStream_t st) {
+  if (Nout % 4 == 0 && Nin % 4 == 0) {
+    DenseDgrad<true> p;
+    p.M = rows; p.N = Nin; p.K = Nout; p.k_chunk = Nout;
+    p.dz = dz; p.w = w; p.xprev = xprev; p.ldx = Nin; p.dx = dx; p.act = act;
+    D4_GEMM(name, 32, 64, 1, 2, p);
+  } else {
+    DenseDgrad<false> p;
+    p.M = rows; p.N = Nin; p.K = Nout; p.k_chunk = Nout;
+    p.dz = dz; p.w = w; p.xprev = xprev; p.ldx = Nin; p.dx = dx; p.act = act;
+    D4_GEMM(name, 32, 64, 1, 2, p);
+  }
+  return ACME_OK;
+}
+
+// dW = X^T dZ over `rows` rows, db = column sums of dZ.
+int dense_wgrad(const char* name, const float* x, int rows, int Nin, const float* dz, int Nout,
+                float* dw, float* db, hipStream_t st) {
+  if (Nin % 4 == 0 && Nout % 4 == 0) {
+    DenseWgrad<true> p;
+    p.M = Nin; p.N = Nout; p.K = rows; p.k_chunk = rows;
+    p.x = x; p.ldx = Nin; p.dz = dz; p.out = dw; p.bias_out = db;
+    D4_GEMM(name, 32, 64, 1, 2, p);
+  } else {
+    DenseWgrad<false> p;
+    p.M = Nin; p.N = Nout; p.K = rows; p.k_chunk = rows;
+    p.x = x; p.ldx = Nin; p.dz = dz; p.out = dw; p.bias_out = db;
+    D4_GEMM(name, 32, 64, 1, 2, p);
+  }
+  return ACME_OK;
+}
+
+// LayerNormMLP forward over rows of concat(xa, xb) (second source from row `split`).
+int lnmlp_forward(acme_d4pg* l, const NetDesc& d, const float* prm, const float* xa0,
+                  const float* xb0, const float* xa1, const float* xb1, int split, int da,
+                  int db, int rows, Acts& a, const char* tag, hipStream_t st) {
+  {
+    ACME_PROF(tag, st, 2.0 * rows * (double)(da + db) * d.sizes[0], 0.0);
+    LnFirstArgs f;
+    f.xa0 = xa0; f.xb0 = xb0; f.xa1 = xa1; f.xb1 = xb1;
+    f.split = split; f.rows = rows; f.da = da; f.db = db; f.H = d.sizes[0];
+    f.w = P(l, prm, d.w1); f.b = P(l, prm, d.b1);
+    f.scale = P(l, prm, d.scale); f.offset = P(l, prm, d.offset);
+    f.eps = l->cfg.layer_norm_epsilon;
+    f.z = a.z1; f.mean = a.mean; f.rstd = a.rstd; f.h = a.h[0];
+    ln_first_kernel<<<(unsigned)ceil_div(rows, kRows), 256, 0, st>>>(f);
+    D4_CHECK();
+  }
+  for (int i = 1; i < d.nl; ++i) {
+    int rc = dense_fwd("d4pg_mlp_fwd", a.h[i - 1], rows, d.sizes[i - 1], P(l, prm, d.w[i]),
+                       P(l, prm, d.b[i]), d.sizes[i], ACT_ELU, a.h[i], st);
+    if (rc != ACME_OK) return rc;
+  }
+  return ACME_OK;
+}
+
+int policy_forward(acme_d4pg* l, const float* prm, const float* obs, int rows, Acts& a,
+                   float* actions, hipStream_t st) {
+  const NetDesc& d = l->pol;
+  int rc = lnmlp_forward(l, d, prm, obs, nullptr, obs, nullptr, rows, l->cfg.obs_dim, 0, rows, a,
+                         "d4pg_policy_ln", st);
+  if (rc != ACME_OK) return rc;
+  ACME_PROF("d4pg_policy_head", st, 2.0 * rows * (double)d.sizes[d.nl - 1] * d.nout, 0.0);
+  policy_head_kernel<<<(unsigned)ceil_div(rows, 4), 256, 0, st>>>(
+      a.h[d.nl - 1], P(l, prm, d.ow), P(l, prm, d.ob), l->act_lo, l->act_scale, rows,
+      d.sizes[d.nl - 1], d.nout, a.t, actions);
+  D4_CHECK();
+  return ACME_OK;
+}
+
+int critic_forward(acme_d4pg* l, const float* prm, const float* o0, const float* a0,
+                   const float* o1, const float* a1, int split, int rows, Acts& a,
+                   hipStream_t st) {
+  const NetDesc& d = l->cri;
+  int rc = lnmlp_forward(l, d, prm, o0, a0, o1, a1, split, l->cfg.obs_dim, l->cfg.act_dim, rows,
+                         a, "d4pg_critic_ln", st);
+  if (rc != ACME_OK) return rc;
+  return dense_fwd("d4pg_critic_head", a.h[d.nl - 1], rows, d.sizes[d.nl - 1], P(l, prm, d.ow),
+                   P(l, prm, d.ob), d.nout, ACT_NONE, a.out, st);
+}
+
+inline int act_of_layer(int i) { return i == 0 ? ACT_TANH : ACT_ELU; }
+
+// Backward through the MLP part of a LayerNormMLP: dz[nl-1] holds the pre-activation
+// gradient of the last layer over `rows` rows; weight gradients use the first `wrows`.
+// Leaves dLoss/d(LayerNorm output) in dz[0].
+int lnmlp_backward_mlp(acme_d4pg* l, const NetDesc& d, const Acts& a, float* const* dz, int rows,
+                       int wrows, hipStream_t st) {
+  for (int i = d.nl - 1; i >= 1; --i) {
+    int rc = dense_wgrad("d4pg_mlp_wgrad", a.h[i - 1], wrows, d.sizes[i - 1], dz[i], d.sizes[i],
+                         Pm(l, l->grads, d.w[i]), Pm(l, l->grads, d.b[i]), st);
+    if (rc != ACME_OK) return rc;
+    rc = dense_dgrad("d4pg_mlp_dgrad", dz[i], rows, d.sizes[i], P(l, l->params, d.w[i]),
+                     d.sizes[i - 1], a.h[i - 1], act_of_layer(i - 1), dz[i - 1], st);
+    if (rc != ACME_OK) return rc;
+  }
+  return ACME_OK;
+}
+
+int ln_backward(acme_d4pg* l, const NetDesc& d, const Acts& a, float* dy, int rows, int ce_rows,
+                bool dpg, const float* xa, const float* xb, int da, int db, hipStream_t st) {
+  const int H = d.sizes[0];
+  const int nblk = (int)ceil_div(rows, kRows);
+  {
+    ACME_PROF("d4pg_ln_bwd", st, 0.0, 0.0);
+    LnBwdArgs b;
+    b.dy = dy; b.z = a.z1; b.mean = a.mean; b.rstd = a.rstd;
+    b.scale = P(l, l->params, d.scale);
+    b.rows = rows; b.ce_rows = ce_rows; b.H = H; b.colslab = l->lnslab;
+    b.w1 = P(l, l->params, d.w1); b.act_off = l->cfg.obs_dim; b.A = l->cfg.act_dim;
+    b.clip = l->cfg.clipping ? 1.f : 0.f; b.invB = 1.f / (float)ce_rows;
+    b.t = l->pon.t; b.act_scale = l->act_scale;
+    b.du = l->du; b.dqda = l->dqda; b.ploss_part = dpg ? l->ploss_part : nullptr;
+    ln_bwd_kernel<<<(unsigned)nblk, 256, 0, st>>>(b);
+    D4_CHECK();
+  }
+  // LayerNorm scale / offset gradients: sum the block partials [nblk][2][H].
+  int rc = launch_slab_reduce(l->lnslab, nblk, 2 * (int64_t)H, Pm(l, l->grads, d.scale), H,
+                              Pm(l, l->grads, d.offset), nullptr, 1, 0, st);
+  if (rc != ACME_OK) return rc;
+  ConcatWgrad p;
+  p.M = da + db; p.N = H; p.K = ce_rows; p.k_chunk = ce_rows;
+  p.x0 = xa; p.d0 = da; p.x1 = xb; p.d1 = db; p.dz = dy;
+  p.out = Pm(l, l->grads, d.w1); p.bias_out = Pm(l, l->grads, d.b1);
+  D4_GEMM("d4pg_first_wgrad", 32, 64, 1, 2, p);
+  return ACME_OK;
+}
+
+int d4pg_step_impl(acme_d4pg* l, const acme_d4pg_batch* bt, const acme_d4pg_outputs* out,
+                   hipStream_t st) {
+  const int B = (int)bt->batch;
+  const int od = l->cfg.obs_dim, ad = l->cfg.act_dim;
+  const NetDesc& pd = l->pol;
+  const NetDesc& cd = l->cri;
+  int rc;
+  if (l->num_steps % l->cfg.target_update_period == 0) {
+    ACME_PROF("d4pg_target_copy", st, 0.0, 2.0 * 4.0 * (double)l->flat);
+    ACME_HIP_TRY(hipMemcpyAsync(l->target, l->params, (size_t)l->flat * sizeof(float),
+                                hipMemcpyDeviceToDevice, st));
+  }
+  // Forwards.
+  if ((rc = policy_forward(l, l->params, bt->o_t, B, l->pon, l->pon.out, st)) ||
+      (rc = policy_forward(l, l->target, bt->o_t, B, l->ptg, l->ptg.out, st)) ||
+      (rc = critic_forward(l, l->params, bt->o_tm1, bt->a_tm1, bt->o_t, l->pon.out, B, 2 * B,
+                           l->con, st)) ||
+      (rc = critic_forward(l, l->target, bt->o_t, l->ptg.out, bt->o_t, l->ptg.out, B, B, l->ctg,
+                           st)))
+    return rc;
+  {
+    ACME_PROF("d4pg_loss", st, 0.0, 0.0);
+    d4pg_loss_kernel<<<1, 1024, 0, st>>>(l->con.out, l->ctg.out, bt->r_t, bt->d_t, l->values, B,
+                                         cd.nout, l->cfg.discount, l->dlogits,
+                                         out && out->critic_loss ? out->critic_loss : l->loss_tmp);
+    D4_CHECK();
+  }
+  // Critic backward: 2B rows of dgrad (CE rows + dpg rows), weight grads from the first B.
+  const int cL = cd.nl - 1;
+  if ((rc = dense_wgrad("d4pg_head_wgrad", l->con.h[cL], B, cd.sizes[cL], l->dlogits, cd.nout,
+                        Pm(l, l->grads, cd.ow), Pm(l, l->grads, cd.ob), st)) ||
+      (rc = dense_dgrad("d4pg_head_dgrad", l->dlogits, 2 * B, cd.nout, P(l, l->params, cd.ow),
+                        cd.sizes[cL], l->con.h[cL], act_of_layer(cL), l->cdz[cL], st)) ||
+      (rc = lnmlp_backward_mlp(l, cd, l->con, l->cdz, 2 * B, B, st)) ||
+      (rc = ln_backward(l, cd, l->con, l->cdz[0], 2 * B, B, true, bt->o_tm1, bt->a_tm1, od, ad,
+                        st)))
+    return rc;
+  // Policy backward from du = dloss/d(head pre-activation).
+  const int pL = pd.nl - 1;
+  if ((rc = dense_wgrad("d4pg_phead_wgrad", l->pon.h[pL], B, pd.sizes[pL], l->du, ad,
+                        Pm(l, l->grads, pd.ow), Pm(l, l->grads, pd.ob), st)) ||
+      (rc = dense_dgrad("d4pg_phead_dgrad", l->du, B, ad, P(l, l->params, pd.ow), pd.sizes[pL],
+                        l->pon.h[pL], act_of_layer(pL), l->pdz[pL], st)) ||
+      (rc = lnmlp_backward_mlp(l, pd, l->pon, l->pdz, B, B, st)) ||
+      (rc = ln_backward(l, pd, l->pon, l->pdz[0], B, B, false, bt->o_t, nullptr, od, 0, st)))
+    return rc;
+  // Global-norm clipping + Adam (t = steps taken including this one).
+  {
+    ACME_PROF("d4pg_adam", st, 0.0, 7.0 * 4.0 * (double)l->flat);
+    const int64_t n4 = l->flat / 4, pol4 = l->policy_flat / 4;
+    grad_sumsq_kernel<<<kNormBlocks, 256, 0, st>>>(l->grads, n4, pol4, l->norm_part);
+    D4_CHECK();
+    const int64_t t = l->num_steps + 1;
+    AdamClipArgs a;
+    a.p = l->params; a.m = l->m; a.v = l->v; a.g = l->grads; a.n4 = n4; a.pol4 = pol4;
+    a.part = l->norm_part; a.nparts = kNormBlocks; a.clipping = l->cfg.clipping;
+    a.clip_norm = 40.f;
+    a.lr_pol = l->cfg.policy_learning_rate; a.lr_cri = l->cfg.critic_learning_rate;
+    a.b1 = l->cfg.adam_beta1; a.omb1 = 1.f - l->cfg.adam_beta1;
+    a.b2 = l->cfg.adam_beta2; a.omb2 = 1.f - l->cfg.adam_beta2;
+    a.bc1 = 1.f - powf(l->cfg.adam_beta1, (float)t);
+    a.bc2 = 1.f - powf(l->cfg.adam_beta2, (float)t);
+    a.eps = l->cfg.adam_epsilon; a.norms = l->norms;
+    a.ploss_part = l->ploss_part; a.nploss = (int)ceil_div(2 * B, kRows); a.invB = 1.f / (float)B;
+    a.policy_loss = out && out->policy_loss ? out->policy_loss : l->loss_tmp + 1;
+    const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n4, 256), 1024);
+    adam_clip_kernel<<<grid, 256, 0, st>>>(a);
+    D4_CHECK();
+  }
+  return ACME_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int acme_d4pg_destroy(acme_d4pg* l) {
+  if (!l) return ACME_OK;
+  for (void* p : l->allocs) (void)hipFree(p);
+  delete l;
+  return ACME_OK;
+}
+
+int acme_d4pg_create(const acme_d4pg_config* cfg, acme_d4pg** out) {
+  ACME_CHECK_ARG(cfg && out, "null argument");
+  ACME_CHECK_ARG(cfg->obs_dim >= 1 && cfg->act_dim >= 1 && cfg->obs_dim + cfg->act_dim <= kMaxIn,
+                 "obs_dim + act_dim must be in [2, %d]", kMaxIn);
+  ACME_CHECK_ARG(cfg->act_dim <= ACME_D4PG_MAX_ACT, "act_dim must be <= %d", ACME_D4PG_MAX_ACT);
+  ACME_CHECK_ARG(cfg->max_batch >= 1 && cfg->max_batch <= 65536, "max_batch must be in [1, 65536]");
+  ACME_CHECK_ARG(cfg->num_atoms >= 2 && cfg->num_atoms <= ACME_D4PG_MAX_ATOMS,
+                 "num_atoms must be in [2, %d]", ACME_D4PG_MAX_ATOMS);
+  ACME_CHECK_ARG(cfg->vmax > cfg->vmin, "vmax must exceed vmin");
+  ACME_CHECK_ARG(cfg->target_update_period >= 1, "target_update_period must be >= 1");
+  for (int n : {cfg->num_policy_layers, cfg->num_critic_layers})
+    ACME_CHECK_ARG(n >= 1 && n <= ACME_D4PG_MAX_LAYERS, "layer count must be in [1, %d]",
+                   ACME_D4PG_MAX_LAYERS);
+  for (int i = 0; i < cfg->num_policy_layers; ++i)
+    ACME_CHECK_ARG(cfg->policy_sizes[i] >= 4 && cfg->policy_sizes[i] <= kMaxWidth &&
+                       cfg->policy_sizes[i] % 4 == 0,
+                   "policy layer sizes must be multiples of 4 in [4, %d]", kMaxWidth);
+  for (int i = 0; i < cfg->num_critic_layers; ++i)
+    ACME_CHECK_ARG(cfg->critic_sizes[i] >= 4 && cfg->critic_sizes[i] <= kMaxWidth &&
+                       cfg->critic_sizes[i] % 4 == 0,
+                   "critic layer sizes must be multiples of 4 in [4, %d]", kMaxWidth);
+  acme_d4pg* l = new acme_d4pg();
+  l->cfg = *cfg;
+  auto fail = [&](int code) {
+    acme_d4pg_destroy(l);
+    return code;
+  };
+  add_net(l, l->pol, "policy", cfg->obs_dim, cfg->num_policy_layers, cfg->policy_sizes,
+          cfg->act_dim, "near_zero_initialized_linear");
+  l->policy_flat = l->flat;
+  add_net(l, l->cri, "critic", cfg->obs_dim + cfg->act_dim, cfg->num_critic_layers,
+          cfg->critic_sizes, cfg->num_atoms, "discrete_valued_head/linear");
+  const int B = cfg->max_batch;
+  int rc;
+  int hmax = 0;
+  for (int i = 0; i < cfg->num_policy_layers; ++i) hmax = std::max(hmax, cfg->policy_sizes[i]);
+  for (int i = 0; i < cfg->num_critic_layers; ++i) hmax = std::max(hmax, cfg->critic_sizes[i]);
+  if ((rc = alloc_acts(l, l->pon, l->pol, B, true)) || (rc = alloc_acts(l, l->ptg, l->pol, B, true)) ||
+      (rc = alloc_acts(l, l->con, l->cri, 2 * B, false)) ||
+      (rc = alloc_acts(l, l->ctg, l->cri, B, false)))
+    return fail(rc);
+  for (int i = 0; i < l->cri.nl; ++i)
+    if ((rc = dev_alloc(l, &l->cdz[i], (int64_t)2 * B * l->cri.sizes[i]))) return fail(rc);
+  for (int i = 0; i < l->pol.nl; ++i)
+    if ((rc = dev_alloc(l, &l->pdz[i], (int64_t)B * l->pol.sizes[i]))) return fail(rc);
+  const int64_t nblk = ceil_div(2 * B, kRows);
+  if ((rc = dev_alloc(l, &l->dlogits, (int64_t)2 * B * cfg->num_atoms)) ||
+      (rc = dev_alloc(l, &l->du, (int64_t)B * cfg->act_dim)) ||
+      (rc = dev_alloc(l, &l->dqda, (int64_t)B * cfg->act_dim)) ||
+      (rc = dev_alloc(l, &l->values, cfg->num_atoms)) ||
+      (rc = dev_alloc(l, &l->act_lo, cfg->act_dim)) ||
+      (rc = dev_alloc(l, &l->act_scale, cfg->act_dim)) ||
+      (rc = dev_alloc(l, &l->lnslab, nblk * 2 * hmax)) ||
+      (rc = dev_alloc(l, &l->ploss_part, nblk)) ||
+      (rc = dev_alloc(l, &l->norm_part, 2 * kNormBlocks)) ||
+      (rc = dev_alloc(l, &l->norms, 2)) || (rc = dev_alloc(l, &l->loss_tmp, 2)))
+    return fail(rc);
+  // Support: tf.linspace(vmin, vmax, K) (computed in f64, rounded once to f32).
+  std::vector<float> vals(cfg->num_atoms), lo(cfg->act_dim), sc(cfg->act_dim);
+  const double step = ((double)cfg->vmax - (double)cfg->vmin) / (cfg->num_atoms - 1);
+  for (int i = 0; i < cfg->num_atoms; ++i) vals[i] = (float)((double)cfg->vmin + i * step);
+  for (int j = 0; j < cfg->act_dim; ++j) {
+    lo[j] = cfg->action_min[j];
+    sc[j] = cfg->action_max[j] - cfg->action_min[j];
+  }
+  if (hipMemcpy(l->values, vals.data(), vals.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(l->act_lo, lo.data(), lo.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(l->act_scale, sc.data(), sc.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+    return fail((set_error("hipMemcpy of the D4PG constants failed"), ACME_ERR_HIP));
+  *out = l;
+  return ACME_OK;
+}
+
+int64_t acme_d4pg_flat_size(const acme_d4pg* l) { return l ? l->flat : 0; }
+int64_t acme_d4pg_policy_size(const acme_d4pg* l) { return l ? l->policy_flat : 0; }
+int32_t acme_d4pg_num_tensors(const acme_d4pg* l) { return l ? (int32_t)l->tensors.size() : 0; }
+
+int acme_d4pg_tensor_info(const acme_d4pg* l, int32_t i, int64_t* offset, int64_t* numel,
+                          int32_t* ndim, int64_t* shape4, const char** name) {
+  ACME_CHECK_ARG(l, "null learner");
+  ACME_CHECK_ARG(i >= 0 && i < (int32_t)l->tensors.size(), "tensor index %d out of range", i);
+  const Tensor& t = l->tensors[i];
+  if (offset) *offset = t.offset;
+  if (numel) *numel = t.numel;
+  if (ndim) *ndim = t.ndim;
+  if (shape4)
+    for (int k = 0; k < 4; ++k) shape4[k] = t.shape[k];
+  if (name) *name = t.name.c_str();
+  return ACME_OK;
+}
+
+int acme_d4pg_bind(acme_d4pg* l, float* params, float* target, float* grads, float* adam_m,
+                   float* adam_v) {
+  ACME_CHECK_ARG(l, "null learner");
+  ACME_CHECK_ARG(params && target && grads && adam_m && adam_v, "null buffer");
+  for (const void* p : {(const void*)params, (const void*)target, (const void*)grads,
+                        (const void*)adam_m, (const void*)adam_v})
+    ACME_CHECK_ARG(((uintptr_t)p & 15) == 0, "buffers must be 16-byte aligned");
+  l->params = params;
+  l->target = target;
+  l->grads = grads;
+  l->m = adam_m;
+  l->v = adam_v;
+  return ACME_OK;
+}
+
+int acme_d4pg_step(acme_d4pg* l, const acme_d4pg_batch* batch, const acme_d4pg_outputs* out,
+                   void* stream) {
+  ACME_CHECK_ARG(l && batch, "null argument");
+  ACME_CHECK_ARG(l->params, "acme_d4pg_bind must be called first");
+  ACME_CHECK_ARG(batch->batch >= 1 && batch->batch <= l->cfg.max_batch,
+                 "batch %lld outside [1, max_batch=%d]", (long long)batch->batch,
+                 l->cfg.max_batch);
+  ACME_CHECK_ARG(batch->o_tm1 && batch->a_tm1 && batch->r_t && batch->d_t && batch->o_t,
+                 "null batch field");
+  int rc = d4pg_step_impl(l, batch, out, as_stream(stream));
+  if (rc != ACME_OK) return rc;
+  l->num_steps += 1;
+  return ACME_OK;
+}
+
+int acme_d4pg_policy(acme_d4pg* l, const float* obs, int64_t rows, int32_t use_target,
+                     float* actions, void* stream) {
+  ACME_CHECK_ARG(l && obs && actions, "null argument");
+  ACME_CHECK_ARG(l->params, "acme_d4pg_bind must be called first");
+  ACME_CHECK_ARG(rows >= 0, "negative row count");
+  hipStream_t st = as_stream(stream);
+  const int B = l->cfg.max_batch;
+  for (int64_t r0 = 0; r0 < rows; r0 += B) {
+    const int n = (int)std::min<int64_t>(B, rows - r0);
+    int rc = policy_forward(l, use_target ? l->target : l->params,
+                            obs + r0 * l->cfg.obs_dim, n, l->ptg,
+                            actions + r0 * l->cfg.act_dim, st);
+    if (rc != ACME_OK) return rc;
+  }
+  return ACME_OK;
+}
+
+int64_t acme_d4pg_num_steps(const acme_d4pg* l) { return l ? l->num_steps : 0; }
+int acme_d4pg_set_num_steps(acme_d4pg* l, int64_t n) {
+  ACME_CHECK_ARG(l && n >= 0, "bad argument");
+  l->num_steps = n;
+  return ACME_OK;
+}
+
+int acme_d4pg_debug_buffer(const acme_d4pg* l, const char* name, const float** out,
+                           int64_t* count) {
+  ACME_CHECK_ARG(l && name && out && count, "null argument");
+  const int B = l->cfg.max_batch, A = l->cfg.act_dim, K = l->cfg.num_atoms;
+  struct Item {
+    const char* n;
+    const float* p;
+    int64_t c;
+  } items[] = {
+      {"p_a", l->pon.out, (int64_t)B * A},      {"t_a", l->ptg.out, (int64_t)B * A},
+      {"c_logits", l->con.out, (int64_t)2 * B * K}, {"t_logits", l->ctg.out, (int64_t)B * K},
+      {"dlogits", l->dlogits, (int64_t)2 * B * K},  {"dqda", l->dqda, (int64_t)B * A},
+      {"du", l->du, (int64_t)B * A},             {"norms", l->norms, 2},
+      {"losses", l->loss_tmp, 2},
+  };
+  for (const Item& it : items)
+    if (strcmp(it.n, name) == 0) {
+      *out = it.p;
+      *count = it.c;
+      return ACME_OK;
+    }
+  set_error("unknown debug buffer '%s'", name);
+  return ACME_ERR_INVALID;
+}
+
+}  // extern "C"

@@ -330,3 +330,124 @@ class NativeDQN:
         check(lib().acme_dqn_q_values(self._h, ptr(obs.contiguous()), B, 1 if use_target else 0,
                                       ptr(q), stream_ptr(stream)), "dqn q_values")
         return q
+
+
+class NativeD4PG:
+    """acme_d4pg learner + its flat buffers (policy tensors first, then critic tensors)."""
+
+    def __init__(self, *, obs_dim: int, act_dim: int, max_batch: int,
+                 policy_sizes: Sequence[int] = (256, 256, 256),
+                 critic_sizes: Sequence[int] = (512, 512, 256), num_atoms: int = 51,
+                 vmin: float = -150.0, vmax: float = 150.0, action_min=None, action_max=None,
+                 discount: float = 0.99, target_update_period: int = 100,
+                 policy_learning_rate: float = 1e-4, critic_learning_rate: float = 1e-4,
+                 clipping: bool = True, adam_beta1: float = 0.9, adam_beta2: float = 0.999,
+                 adam_epsilon: float = 1e-8, layer_norm_epsilon: float = 1e-5, device=None):
+        _lib.require_gpu()
+        cfg = _lib.D4PGConfig()
+        cfg.obs_dim, cfg.act_dim, cfg.max_batch = int(obs_dim), int(act_dim), int(max_batch)
+        for n, sizes in (("policy", policy_sizes), ("critic", critic_sizes)):
+            if not 1 <= len(sizes) <= _lib.D4PG_MAX_LAYERS:
+                raise ValueError(f"{n} needs 1..{_lib.D4PG_MAX_LAYERS} layer sizes")
+        cfg.num_policy_layers = len(policy_sizes)
+        cfg.num_critic_layers = len(critic_sizes)
+        for i, s in enumerate(policy_sizes):
+            cfg.policy_sizes[i] = int(s)
+        for i, s in enumerate(critic_sizes):
+            cfg.critic_sizes[i] = int(s)
+        if act_dim > _lib.D4PG_MAX_ACT:
+            raise ValueError(f"act_dim must be <= {_lib.D4PG_MAX_ACT}")
+        lo = np.broadcast_to(np.asarray(-1.0 if action_min is None else action_min, np.float32),
+                             (act_dim,))
+        hi = np.broadcast_to(np.asarray(1.0 if action_max is None else action_max, np.float32),
+                             (act_dim,))
+        for j in range(act_dim):
+            cfg.action_min[j], cfg.action_max[j] = float(lo[j]), float(hi[j])
+        cfg.num_atoms, cfg.vmin, cfg.vmax = int(num_atoms), vmin, vmax
+        cfg.discount, cfg.target_update_period = discount, int(target_update_period)
+        cfg.policy_learning_rate, cfg.critic_learning_rate = policy_learning_rate, critic_learning_rate
+        cfg.adam_beta1, cfg.adam_beta2, cfg.adam_epsilon = adam_beta1, adam_beta2, adam_epsilon
+        cfg.clipping = 1 if clipping else 0
+        cfg.layer_norm_epsilon = layer_norm_epsilon
+        self.cfg = cfg
+        self.obs_dim, self.act_dim, self.max_batch = int(obs_dim), int(act_dim), int(max_batch)
+        self.device = torch.device(device or "cuda")
+        h = ctypes.c_void_p()
+        L = lib()
+        with torch.cuda.device(self.device):
+            check(L.acme_d4pg_create(ctypes.byref(cfg), ctypes.byref(h)), "d4pg create")
+        self._h = h
+        self.flat_size = int(L.acme_d4pg_flat_size(h))
+        self.policy_size = int(L.acme_d4pg_policy_size(h))
+        self.tensors: List[Tuple[str, int, Tuple[int, ...]]] = []
+        for i in range(L.acme_d4pg_num_tensors(h)):
+            off, numel, nd = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int32()
+            shape = (ctypes.c_int64 * 4)()
+            name = ctypes.c_char_p()
+            check(L.acme_d4pg_tensor_info(h, i, ctypes.byref(off), ctypes.byref(numel),
+                                          ctypes.byref(nd), shape, ctypes.byref(name)))
+            self.tensors.append((name.value.decode(), int(off.value),
+                                 tuple(int(shape[k]) for k in range(nd.value))))
+        d = self.device
+        z = lambda: torch.zeros(self.flat_size, dtype=torch.float32, device=d)  # noqa: E731
+        self.params, self.target, self.grads, self.m, self.v = z(), z(), z(), z(), z()
+        check(L.acme_d4pg_bind(h, ptr(self.params), ptr(self.target), ptr(self.grads),
+                               ptr(self.m), ptr(self.v)), "d4pg bind")
+        self.critic_loss = torch.zeros(1, dtype=torch.float32, device=d)
+        self.policy_loss = torch.zeros(1, dtype=torch.float32, device=d)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                lib().acme_d4pg_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    views = NativeDQN.views
+    set_params = NativeDQN.set_params
+    get_params = NativeDQN.get_params
+
+    @property
+    def num_steps(self) -> int:
+        return int(lib().acme_d4pg_num_steps(self._h))
+
+    @num_steps.setter
+    def num_steps(self, n: int) -> None:
+        check(lib().acme_d4pg_set_num_steps(self._h, int(n)))
+
+    def debug_buffer(self, name: str) -> np.ndarray:
+        p, n = ctypes.c_void_p(), ctypes.c_int64()
+        check(lib().acme_d4pg_debug_buffer(self._h, name.encode(), ctypes.byref(p),
+                                           ctypes.byref(n)))
+        return _device_array(p.value, n.value, np.float32, self.device).cpu().numpy().view(
+            np.float32).copy()
+
+    def step(self, o_tm1, a_tm1, r_t, d_t, o_t, stream=None):
+        B = int(r_t.shape[0])
+        for name, t, cols in (("o_tm1", o_tm1, self.obs_dim), ("a_tm1", a_tm1, self.act_dim),
+                              ("r_t", r_t, None), ("d_t", d_t, None), ("o_t", o_t, self.obs_dim)):
+            if not (isinstance(t, torch.Tensor) and t.is_cuda and t.is_contiguous()
+                    and t.dtype == torch.float32):
+                raise ValueError(f"{name} must be a contiguous float32 device tensor")
+            if t.shape[0] != B or (cols is not None and t.numel() != B * cols):
+                raise ValueError(f"{name} has shape {tuple(t.shape)}, expected [{B}, {cols}]")
+        b = _lib.D4PGBatch()
+        b.o_tm1, b.a_tm1, b.r_t, b.d_t, b.o_t = (ptr(o_tm1), ptr(a_tm1), ptr(r_t), ptr(d_t),
+                                                 ptr(o_t))
+        b.batch = B
+        out = _lib.D4PGOutputs()
+        out.critic_loss, out.policy_loss = ptr(self.critic_loss), ptr(self.policy_loss)
+        check(lib().acme_d4pg_step(self._h, ctypes.byref(b), ctypes.byref(out),
+                                   stream_ptr(stream)), "d4pg step")
+
+    def policy(self, obs: torch.Tensor, use_target: bool = False, stream=None) -> torch.Tensor:
+        rows = int(obs.shape[0])
+        obs = obs.reshape(rows, -1).to(self.device, torch.float32).contiguous()
+        if obs.shape[1] != self.obs_dim:
+            raise ValueError(f"observations must have {self.obs_dim} features")
+        a = torch.empty(rows, self.act_dim, dtype=torch.float32, device=self.device)
+        check(lib().acme_d4pg_policy(self._h, ptr(obs), rows, 1 if use_target else 0, ptr(a),
+                                     stream_ptr(stream)), "d4pg policy")
+        return a

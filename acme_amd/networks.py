@@ -134,3 +134,135 @@ class MLP:
 
     def from_sonnet(self, variables):
         return dict(variables)
+
+
+# ------------------------------------------------------------------ D4PG (control suite)
+
+
+def _variance_scaling_uniform(rng, shape, scale: float, fan: int) -> np.ndarray:
+    limit = np.sqrt(3.0 * scale / fan)
+    return rng.uniform(-limit, limit, shape).astype(np.float32)
+
+
+def _layer_norm_mlp_shapes(prefix: str, din: int, sizes: Sequence[int]):
+    out = [(f"{prefix}/layer_norm_mlp/linear/w", (din, sizes[0])),
+           (f"{prefix}/layer_norm_mlp/linear/b", (sizes[0],)),
+           (f"{prefix}/layer_norm_mlp/layer_norm/scale", (sizes[0],)),
+           (f"{prefix}/layer_norm_mlp/layer_norm/offset", (sizes[0],))]
+    for i in range(1, len(sizes)):
+        out += [(f"{prefix}/layer_norm_mlp/mlp/linear_{i - 1}/w", (sizes[i - 1], sizes[i])),
+                (f"{prefix}/layer_norm_mlp/mlp/linear_{i - 1}/b", (sizes[i],))]
+    return out
+
+
+def _init_layer_norm_mlp(rng, shapes, out: Dict[str, np.ndarray]) -> None:
+    # LayerNormMLP (acme/tf/networks/continuous.py:26-28, 55-65): VarianceScaling(
+    # distribution='uniform', mode='fan_out', scale=0.333) weights, zero biases, unit
+    # LayerNorm scale, zero offset.
+    for name, shape in shapes:
+        if name.endswith("/w"):
+            out[name] = _variance_scaling_uniform(rng, shape, 0.333, shape[-1])
+        elif name.endswith("/scale"):
+            out[name] = np.ones(shape, np.float32)
+        else:
+            out[name] = np.zeros(shape, np.float32)
+
+
+@dataclasses.dataclass(frozen=True)
+class LayerNormMLPPolicy:
+    """snt.Sequential([LayerNormMLP(sizes, activate_final=True),
+    NearZeroInitializedLinear(act_dim), TanhToSpec(action_spec)])
+    (examples/control_suite/run_d4pg.py:69-73)."""
+
+    obs_dim: int
+    act_dim: int
+    layer_sizes: Tuple[int, ...] = (256, 256, 256)
+    action_min: Tuple[float, ...] = ()
+    action_max: Tuple[float, ...] = ()
+
+    def __init__(self, obs_dim: int, act_dim: int, layer_sizes: Sequence[int] = (256, 256, 256),
+                 action_min=-1.0, action_max=1.0):
+        object.__setattr__(self, "obs_dim", int(obs_dim))
+        object.__setattr__(self, "act_dim", int(act_dim))
+        object.__setattr__(self, "layer_sizes", tuple(int(s) for s in layer_sizes))
+        lo = np.broadcast_to(np.asarray(action_min, np.float32), (act_dim,))
+        hi = np.broadcast_to(np.asarray(action_max, np.float32), (act_dim,))
+        object.__setattr__(self, "action_min", tuple(float(x) for x in lo))
+        object.__setattr__(self, "action_max", tuple(float(x) for x in hi))
+
+    def tensor_shapes(self):
+        s = list(self.layer_sizes)
+        return _layer_norm_mlp_shapes("policy", self.obs_dim, s) + [
+            ("policy/near_zero_initialized_linear/w", (s[-1], self.act_dim)),
+            ("policy/near_zero_initialized_linear/b", (self.act_dim,))]
+
+    def init(self, seed: int = 0) -> Dict[str, np.ndarray]:
+        rng = np.random.default_rng(seed)
+        out: Dict[str, np.ndarray] = {}
+        shapes = self.tensor_shapes()
+        _init_layer_norm_mlp(rng, shapes[:-2], out)
+        # NearZeroInitializedLinear: VarianceScaling(1e-4) = truncated normal, fan_in
+        # (continuous.py:30-35); stddev corrected for the 2-sigma truncation.
+        (wn, ws), (bn, bs) = shapes[-2:]
+        out[wn] = truncated_normal(rng, ws, np.sqrt(1e-4 / ws[0]) / 0.87962566103423978)
+        out[bn] = np.zeros(bs, np.float32)
+        return out
+
+
+@dataclasses.dataclass(frozen=True)
+class DistributionalCritic:
+    """snt.Sequential([CriticMultiplexer(), LayerNormMLP(sizes, activate_final=True),
+    DiscreteValuedHead(vmin, vmax, num_atoms)]) (examples/control_suite/run_d4pg.py:76-81)."""
+
+    obs_dim: int
+    act_dim: int
+    layer_sizes: Tuple[int, ...] = (512, 512, 256)
+    vmin: float = -150.0
+    vmax: float = 150.0
+    num_atoms: int = 51
+
+    def __init__(self, obs_dim: int, act_dim: int, layer_sizes: Sequence[int] = (512, 512, 256),
+                 vmin: float = -150.0, vmax: float = 150.0, num_atoms: int = 51):
+        object.__setattr__(self, "obs_dim", int(obs_dim))
+        object.__setattr__(self, "act_dim", int(act_dim))
+        object.__setattr__(self, "layer_sizes", tuple(int(s) for s in layer_sizes))
+        object.__setattr__(self, "vmin", float(vmin))
+        object.__setattr__(self, "vmax", float(vmax))
+        object.__setattr__(self, "num_atoms", int(num_atoms))
+
+    def tensor_shapes(self):
+        s = list(self.layer_sizes)
+        return _layer_norm_mlp_shapes("critic", self.obs_dim + self.act_dim, s) + [
+            ("critic/discrete_valued_head/linear/w", (s[-1], self.num_atoms)),
+            ("critic/discrete_valued_head/linear/b", (self.num_atoms,))]
+
+    def init(self, seed: int = 0) -> Dict[str, np.ndarray]:
+        rng = np.random.default_rng(seed)
+        out: Dict[str, np.ndarray] = {}
+        shapes = self.tensor_shapes()
+        _init_layer_norm_mlp(rng, shapes[:-2], out)
+        # DiscreteValuedHead's snt.Linear default: TruncatedNormal(1 / sqrt(fan_in)).
+        (wn, ws), (bn, bs) = shapes[-2:]
+        out[wn] = truncated_normal(rng, ws, 1.0 / np.sqrt(ws[0]))
+        out[bn] = np.zeros(bs, np.float32)
+        return out
+
+    @property
+    def values(self) -> np.ndarray:
+        step = (self.vmax - self.vmin) / (self.num_atoms - 1)
+        return (self.vmin + np.arange(self.num_atoms) * step).astype(np.float32)
+
+
+def make_d4pg_networks(obs_dim: int, action_spec, policy_layer_sizes=(256, 256, 256),
+                       critic_layer_sizes=(512, 512, 256), vmin: float = -150.0,
+                       vmax: float = 150.0, num_atoms: int = 51) -> Dict[str, object]:
+    """make_networks of examples/control_suite/run_d4pg.py:53-88 (observation network =
+    identity; tf2_utils.batch_concat of a flat observation)."""
+    act_dim = int(np.prod(action_spec.shape))
+    return {
+        "policy": LayerNormMLPPolicy(obs_dim, act_dim, policy_layer_sizes,
+                                     action_spec.minimum, action_spec.maximum),
+        "critic": DistributionalCritic(obs_dim, act_dim, critic_layer_sizes, vmin, vmax,
+                                       num_atoms),
+        "observation": "identity",
+    }

@@ -43,7 +43,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--batch", type=int, default=512)
+    p.add_argument("--workload", choices=("dqn", "d4pg"), default="dqn",
+                   help="dqn: the headline config (BASELINE configs[1]); d4pg: configs[2]")
+    p.add_argument("--batch", type=int, default=0, help="default 512 (dqn) / 256 (d4pg)")
     p.add_argument("--replay-size", type=int, default=1_000_000)
     p.add_argument("--num-actions", type=int, default=18)
     p.add_argument("--no-profile", action="store_true", help="skip the profiled pass")
@@ -119,33 +121,63 @@ def cpu_baseline(batch: int, num_actions: int, seconds: float):
                         f"{threads} BLAS threads, {cpu_model()}"))
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        dist = None
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+def d4pg_cpu_baseline(batch: int, seconds: float):
+    """The numpy D4PG oracle (oracle/d4pg_oracle.py, float32) on a bounded sample: a 16,384-
+    slot host replay drawn uniformly, batch 256, config-3 networks, as many full steps as fit
+    in `seconds` (at least 2; the first is a warm-up)."""
+    from oracle import d4pg_oracle as O
+    from acme_amd.networks import DistributionalCritic, LayerNormMLPPolicy
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    try:
+        from threadpoolctl import threadpool_limits
+        ctx = threadpool_limits(threads)
+    except ImportError:  # pragma: no cover
+        ctx = None
+    rng = np.random.default_rng(0)
+    cap = 16384
+    obs = rng.standard_normal((cap, 24)).astype(np.float32)
+    nxt = rng.standard_normal((cap, 24)).astype(np.float32)
+    act = rng.uniform(-1, 1, (cap, 6)).astype(np.float32)
+    rew = rng.uniform(0, 5, cap).astype(np.float32)
+    dis = np.where(rng.random(cap) < 0.001, 0, np.float32(0.99) ** 4).astype(np.float32)
+    cfg = O.D4PGConfig()
+    p = dict(LayerNormMLPPolicy(24, 6).init(0))
+    p.update(DistributionalCritic(24, 6).init(1))
+    z = {k: np.zeros_like(v) for k, v in p.items()}
+    state = dict(params=p, target={k: v.copy() for k, v in p.items()}, m=z, v=dict(z),
+                 num_steps=0)
 
-    from acme_amd import _lib, replay, specs
+    def one(st):
+        k = rng.integers(0, cap, batch)
+        b = dict(o_tm1=obs[k], a_tm1=act[k], r_t=rew[k], d_t=dis[k], o_t=nxt[k])
+        return O.d4pg_step(cfg, st, b, np.float32)[2]
+
+    state = one(state)
+    t0 = time.perf_counter()
+    n = 0
+    while n < 2 or time.perf_counter() - t0 < seconds:
+        state = one(state)
+        n += 1
+    dt = time.perf_counter() - t0
+    if ctx is not None and hasattr(ctx, "unregister"):
+        ctx.unregister()
+    return dict(value=round(batch * n / dt, 2), unit="transitions/s", cores=threads, kind="port",
+                sample=(f"numpy float32 oracle (oracle/d4pg_oracle.py), {n} timed steps x batch "
+                        f"{batch}, uniform draws from a {cap}-slot host replay, {threads} BLAS "
+                        f"threads, {cpu_model()}"))
+
+
+def setup_dqn(args, world, rank, dev):
+    from acme_amd import replay, specs
     from acme_amd.adders import reverb as adders
     from acme_amd.agents.dqn import DQNLearner
     from acme_amd.datasets import make_reverb_dataset
     from acme_amd.networks import DQNAtariNetwork
     from acme_amd.utils import counting, loggers
-    L = _lib.lib()
-
     # The measured path is the drop-in one: GPU replay Table (Reverb replacement) ->
     # make_reverb_dataset iterator -> DQNLearner.step() -> update_priorities.
-    B, A = args.batch, args.num_actions
+    B, A = args.batch or 512, args.num_actions
     shard = -(-args.replay_size // world)
-    t_fill = time.perf_counter()
     env_spec = specs.EnvironmentSpec(
         observations=specs.Array((84, 84, 4), np.uint8), actions=specs.DiscreteArray(A, np.int32),
         rewards=specs.Array((), np.float32), discounts=specs.BoundedArray((), np.float32, 0, 1))
@@ -162,20 +194,89 @@ def main():
                          learning_rate=1e-3, target_update_period=100, dataset=dataset,
                          replay_client=replay.Client(server), counter=counting.Counter(),
                          logger=loggers.NoOpLogger(), seed=0, device=dev)
+    meta = dict(
+        metric=METRIC, dtype="f32",
+        data="synthetic (device-generated uint8 Atari-shape transitions, random-init "
+             "Nature-CNN weights)",
+        config={"workload": "dqn_nature_cnn_prioritized_replay (BASELINE configs[1])",
+                "global_batch": B * world, "batch_per_gpu": B,
+                "replay_slots": args.replay_size, "replay_slots_per_gpu": shard,
+                "obs": "uint8[84,84,4]", "num_actions": A,
+                "sampler": "prioritized(alpha=0.6), IS beta=0.2", "parallelism": f"dp{world}"})
+    return (learner.step, B, meta, lambda: float(learner.native.loss.item()),
+            lambda: cpu_baseline(B, A, args.cpu_baseline_seconds))
+
+
+def setup_d4pg(args, world, rank, dev):
+    from acme_amd import replay, specs
+    from acme_amd.adders import reverb as adders
+    from acme_amd.agents.d4pg import D4PGLearner
+    from acme_amd.datasets import make_reverb_dataset
+    from acme_amd.networks import make_d4pg_networks
+    from acme_amd.utils import counting, loggers
+    if world > 1:
+        raise SystemExit("the D4PG workload is single-GPU (BASELINE configs[2])")
+    B = args.batch or 256
+    env_spec = specs.EnvironmentSpec(
+        observations=specs.Array((24,), np.float32),
+        actions=specs.BoundedArray((6,), np.float32, -1.0, 1.0),
+        rewards=specs.Array((), np.float32), discounts=specs.BoundedArray((), np.float32, 0, 1))
+    table = replay.Table(adders.DEFAULT_PRIORITY_TABLE, replay.selectors.Uniform(),
+                         replay.selectors.Fifo(), args.replay_size,
+                         replay.rate_limiters.MinSize(1),
+                         signature=adders.NStepTransitionAdder.signature(env_spec), seed=4321,
+                         device=dev)
+    table.native.fill_synthetic(args.replay_size, layout=1, num_actions=1, seed=rank)
+    server = replay.Server([table])
+    nets = make_d4pg_networks(24, env_spec.actions)
+    learner = D4PGLearner(nets["policy"], nets["critic"], nets["policy"], nets["critic"],
+                          discount=0.99, target_update_period=100,
+                          dataset=make_reverb_dataset(server, batch_size=B),
+                          counter=counting.Counter(), logger=loggers.NoOpLogger(), device=dev)
+    meta = dict(
+        metric="learner transitions/sec (sample+step) at batch 256, D4PG control shape",
+        dtype="f32",
+        data="synthetic (device-generated 24-dim control-shape transitions, random-init "
+             "D4PG networks)",
+        config={"workload": "d4pg_control_uniform_replay (BASELINE configs[2])",
+                "global_batch": B, "batch_per_gpu": B, "replay_slots": args.replay_size,
+                "obs": "f32[24]", "act": "f32[6]", "atoms": 51,
+                "policy": "LayerNormMLP(256,256,256)+tanh", "critic": "LayerNormMLP(512,512,256)+51",
+                "sampler": "uniform", "parallelism": "dp1"})
+    return (learner.step, B, meta, lambda: float(learner.native.critic_loss.item()),
+            lambda: d4pg_cpu_baseline(B, args.cpu_baseline_seconds))
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist = None
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from acme_amd import _lib
+    L = _lib.lib()
+    t_fill = time.perf_counter()
+    setup = {"dqn": setup_dqn, "d4pg": setup_d4pg}[args.workload]
+    step, B, meta, loss_fn, cpu_fn = setup(args, world, rank, dev)
     torch.cuda.synchronize(dev)
     t_fill = time.perf_counter() - t_fill
 
-    def step(i):
-        learner.step()
-
     for i in range(args.warmup):
-        step(i)
+        step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(args.warmup + i)
+        step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -191,10 +292,10 @@ def main():
         L.acme_profile_reset()
         L.acme_profile_enable(1)
         for i in range(args.profile_steps):
-            step(args.warmup + args.steps + i)
+            step()
         torch.cuda.synchronize(dev)
         L.acme_profile_enable(0)
-    loss = float(learner.native.loss.item())
+    loss = loss_fn()
 
     sections = []
     for i in range(L.acme_profile_num_sections()):
@@ -240,20 +341,14 @@ def main():
         print(f"[bench] replay fill {t_fill:.1f}s, final loss {loss:.5f}", file=sys.stderr)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(B, A, args.cpu_baseline_seconds)
+        cpu = cpu_fn()
     if rank == 0:
         out = {
-            "metric": METRIC, "value": round(value, 1), "unit": "transitions/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (device-generated uint8 Atari-shape transitions, random-init "
-                    "Nature-CNN weights)",
-            "config": {"workload": "dqn_nature_cnn_prioritized_replay (BASELINE configs[1])",
-                       "global_batch": B * world, "batch_per_gpu": B,
-                       "replay_slots": args.replay_size, "replay_slots_per_gpu": shard,
-                       "obs": "uint8[84,84,4]", "num_actions": A,
-                       "sampler": "prioritized(alpha=0.6), IS beta=0.2",
-                       "parallelism": f"dp{world}"},
+            "metric": meta["metric"], "value": round(value, 1), "unit": "transitions/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": meta["dtype"], "data": meta["data"],
+            "config": meta["config"],
             "roofline": roofline,
             "cpu_baseline": cpu,
             "gpu_busy_ms_per_step": None if busy is None else round(busy, 4),

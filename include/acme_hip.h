@@ -195,6 +195,79 @@ int acme_dqn_set_num_steps(acme_dqn* l, int64_t n);
 /* Minimum of a device f64 array (for the data-parallel IS normaliser). */
 int acme_min_f64(const double* x, int64_t n, double* out_dev, void* stream);
 
+/* ------------------------------------------------------------------ D4PG -- */
+/* Replaces D4PGLearner._step (acme/agents/tf/d4pg/learning.py:156-247) with the networks
+ * of examples/control_suite/run_d4pg.py:60-81: policy = LayerNormMLP(policy_sizes,
+ * activate_final) -> NearZeroInitializedLinear(act_dim) -> TanhToSpec; critic =
+ * concat(obs, action) -> LayerNormMLP(critic_sizes, activate_final) ->
+ * DiscreteValuedHead(vmin, vmax, num_atoms).  The observation network is the identity
+ * (tf2_utils.batch_concat of a flat observation). */
+#define ACME_D4PG_MAX_LAYERS 4
+#define ACME_D4PG_MAX_ACT 16
+#define ACME_D4PG_MAX_ATOMS 64
+
+typedef struct acme_d4pg acme_d4pg;
+
+typedef struct acme_d4pg_config {
+  int32_t obs_dim;              /* flat observation size (<= 64 - act_dim) */
+  int32_t act_dim;              /* <= ACME_D4PG_MAX_ACT */
+  int32_t max_batch;
+  int32_t num_policy_layers;    /* LayerNormMLP sizes, 2..ACME_D4PG_MAX_LAYERS */
+  int32_t policy_sizes[ACME_D4PG_MAX_LAYERS];
+  int32_t num_critic_layers;
+  int32_t critic_sizes[ACME_D4PG_MAX_LAYERS];
+  int32_t num_atoms;            /* <= ACME_D4PG_MAX_ATOMS */
+  float vmin, vmax;
+  float action_min[ACME_D4PG_MAX_ACT];  /* TanhToSpec bounds (spec.minimum / maximum) */
+  float action_max[ACME_D4PG_MAX_ACT];
+  float discount;
+  int32_t target_update_period;
+  float policy_learning_rate, critic_learning_rate;
+  float adam_beta1, adam_beta2, adam_epsilon;
+  int32_t clipping;             /* dqda norm clip 1.0 + global-norm clip 40 (learning.py:211-237) */
+  float layer_norm_epsilon;     /* Sonnet LayerNorm default 1e-5 */
+} acme_d4pg_config;
+
+typedef struct acme_d4pg_batch {
+  const float* o_tm1;  /* [B, obs_dim] */
+  const float* a_tm1;  /* [B, act_dim] */
+  const float* r_t;    /* [B] */
+  const float* d_t;    /* [B] */
+  const float* o_t;    /* [B, obs_dim] */
+  int64_t batch;
+} acme_d4pg_batch;
+
+typedef struct acme_d4pg_outputs {
+  float* critic_loss;  /* [1] device (optional) */
+  float* policy_loss;  /* [1] device (optional) */
+} acme_d4pg_outputs;
+
+int acme_d4pg_create(const acme_d4pg_config* cfg, acme_d4pg** out);
+int acme_d4pg_destroy(acme_d4pg* l);
+/* Flat buffers hold the policy tensors, then the critic tensors (64-float aligned). */
+int64_t acme_d4pg_flat_size(const acme_d4pg* l);
+/* Floats [0, policy_size) are the policy's (its own Adam and global-norm clip). */
+int64_t acme_d4pg_policy_size(const acme_d4pg* l);
+int32_t acme_d4pg_num_tensors(const acme_d4pg* l);
+int acme_d4pg_tensor_info(const acme_d4pg* l, int32_t i, int64_t* offset, int64_t* numel,
+                          int32_t* ndim, int64_t* shape4, const char** name);
+int acme_d4pg_bind(acme_d4pg* l, float* params, float* target, float* grads, float* adam_m,
+                   float* adam_v);
+/* One learner step: target <- online when num_steps % period == 0, num_steps += 1,
+ * critic + policy losses and gradients, global-norm clipping, two Adams. */
+int acme_d4pg_step(acme_d4pg* l, const acme_d4pg_batch* batch, const acme_d4pg_outputs* out,
+                   void* stream);
+/* Policy forward (actor / evaluation): actions [rows, act_dim]. */
+int acme_d4pg_policy(acme_d4pg* l, const float* obs, int64_t rows, int32_t use_target,
+                     float* actions, void* stream);
+int64_t acme_d4pg_num_steps(const acme_d4pg* l);
+int acme_d4pg_set_num_steps(acme_d4pg* l, int64_t n);
+/* Internal device workspaces (tests): "p_a" (dpg actions), "t_a" (target actions),
+ * "c_logits" (online critic logits, 2B rows: [q_tm1; dpg]), "t_logits", "dlogits",
+ * "dqda", "norms" (policy / critic gradient global norms before clipping). */
+int acme_d4pg_debug_buffer(const acme_d4pg* l, const char* name, const float** out,
+                           int64_t* count);
+
 /* ----------------------------------------------------------- elementwise ops -- */
 
 /* ------------------------------------------------------------- profiling -- */
