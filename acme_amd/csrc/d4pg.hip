@@ -97,6 +97,17 @@ struct acme_d4pg {
   double* norm_part = nullptr;            // [2][kNormBlocks]
   float* norms = nullptr;                 // [2] global norms (policy, critic)
   float* loss_tmp = nullptr;              // [2] critic / policy loss
+  float* ce = nullptr;                    // [B] per-row cross-entropy
+  int64_t* dev_step = nullptr;            // device mirror of num_steps (Adam t)
+  // Captured step graphs, keyed by the batch / output pointers, B and the target copy.
+  struct Graph {
+    const void* key[7];
+    int64_t B;
+    bool copy;
+    hipGraphExec_t exec;
+  };
+  std::vector<Graph> graphs;
+  hipStream_t capture = nullptr;
 };
 
 namespace {
@@ -327,64 +338,54 @@ __global__ void __launch_bounds__(256) policy_head_kernel(const float* __restric
 }
 
 // ------------------------------------------------------------------ loss
-// One 1024-thread block; wave w handles rows w, w + 16, ...; lane i = atom i.
+// One wave per row (4 rows per 256-thread block); lane i = atom i.
 //   rows < B  : categorical TD loss (distributional.py:22-41) with the L2 projection
-//               written exactly as l2_project (:44-83); dlogits = (softmax - target) / B.
+//               written exactly as l2_project (:44-83); dlogits = (softmax - target) / B,
+//               ce[row] = cross-entropy (summed into the loss by adam_clip_kernel).
 //   rows >= B : dpg rows; q = sum softmax * values, dq/dlogits = (values - q) * softmax.
-__global__ void __launch_bounds__(1024) d4pg_loss_kernel(
+__global__ void __launch_bounds__(256) d4pg_loss_kernel(
     const float* __restrict__ c_logits, const float* __restrict__ t_logits,
     const float* __restrict__ r, const float* __restrict__ d, const float* __restrict__ values,
-    int B, int K, float discount, float* __restrict__ dlogits, float* __restrict__ loss_out) {
-  __shared__ float part[16];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int B, int K, float discount, float* __restrict__ dlogits, float* __restrict__ ce_out) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= 2 * B) return;
   const bool on = lane < K;
   const float NEG = -INFINITY;
   const float vi = on ? values[lane] : 0.f;
+  const float ql = on ? c_logits[(size_t)row * K + lane] : NEG;
+  const float m2 = wave_max(ql);
+  const float e2 = on ? expf(ql - m2) : 0.f;
+  const float s2 = wave_sum(e2);
+  const float sm = e2 / s2;
+  if (row >= B) {
+    const float q = wave_sum(on ? sm * vi : 0.f);
+    if (on) dlogits[(size_t)row * K + lane] = (vi - q) * sm;
+    return;
+  }
   const float vmin = values[0], vmax = values[K - 1];
   // Support spacings of l2_project: d_pos = Zq[i+1] - Zq[i] (wrapping to vmin), d_neg =
   // Zq[i] - Zq[i-1] (wrapping to vmax).
   const float dpos = on ? ((lane + 1 < K ? values[lane + 1] : vmin) - vi) : 1.f;
   const float dneg = on ? (vi - (lane > 0 ? values[lane - 1] : vmax)) : 1.f;
-  const float invB = 1.f / (float)B;
-  float lsum = 0.f;
-  for (int row = wave; row < 2 * B; row += 16) {
-    const float ql = on ? c_logits[(size_t)row * K + lane] : NEG;
-    const float m2 = wave_max(ql);
-    const float e2 = on ? expf(ql - m2) : 0.f;
-    const float s2 = wave_sum(e2);
-    const float sm = e2 / s2;
-    if (row < B) {
-      const float tl = on ? t_logits[(size_t)row * K + lane] : NEG;
-      const float mx = wave_max(tl);
-      const float e = on ? expf(tl - mx) : 0.f;
-      const float pj = e / wave_sum(e);
-      const float gd = discount * d[row];
-      const float zj = r[row] + gd * vi;
-      const float zc = fminf(fmaxf(zj, vmin), vmax);
-      float tgt = 0.f;
-      for (int j = 0; j < K; ++j) {
-        const float zcj = __shfl(zc, j, 64), pjj = __shfl(pj, j, 64);
-        const float dq = zcj - vi;
-        const float sg = dq >= 0.f ? 1.f : 0.f;
-        const float dh = (sg * dq) / dpos - ((1.f - sg) * dq) / dneg;
-        tgt += fminf(fmaxf(1.f - dh, 0.f), 1.f) * pjj;
-      }
-      const float logp = ql - m2 - logf(s2);
-      const float ce = wave_sum(on ? -tgt * logp : 0.f);
-      if (on) dlogits[(size_t)row * K + lane] = invB * (sm - tgt);
-      lsum += ce;
-    } else {
-      const float q = wave_sum(on ? sm * vi : 0.f);
-      if (on) dlogits[(size_t)row * K + lane] = (vi - q) * sm;
-    }
+  const float tl = on ? t_logits[(size_t)row * K + lane] : NEG;
+  const float mx = wave_max(tl);
+  const float e = on ? expf(tl - mx) : 0.f;
+  const float pj = e / wave_sum(e);
+  const float gd = discount * d[row];
+  const float zc = fminf(fmaxf(r[row] + gd * vi, vmin), vmax);
+  float tgt = 0.f;
+  for (int j = 0; j < K; ++j) {
+    const float zcj = __shfl(zc, j, 64), pjj = __shfl(pj, j, 64);
+    const float dq = zcj - vi;
+    const float sg = dq >= 0.f ? 1.f : 0.f;
+    const float dh = (sg * dq) / dpos - ((1.f - sg) * dq) / dneg;
+    tgt += fminf(fmaxf(1.f - dh, 0.f), 1.f) * pjj;
   }
-  if (lane == 0) part[wave] = lsum;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float t = 0.f;
-    for (int w = 0; w < 16; ++w) t += part[w];
-    *loss_out = t / (float)B;
-  }
+  const float logp = ql - m2 - logf(s2);
+  const float ce = wave_sum(on ? -tgt * logp : 0.f);
+  if (on) dlogits[(size_t)row * K + lane] = (1.f / (float)B) * (sm - tgt);
+  if (lane == 0) ce_out[row] = ce;
 }
 
 // ------------------------------------------------------------------ LayerNorm backward
@@ -571,9 +572,13 @@ struct ConcatWgrad {
 // ------------------------------------------------------------------ clip + Adam
 // Sum of squared gradients per network (policy range [0, n_pol), critic the rest), f64
 // block partials in a fixed order.
+// Block 0 also advances the device step counter (read by adam_clip_kernel as the Adam t),
+// so a captured step graph needs no per-step host arguments.
 __global__ void __launch_bounds__(256) grad_sumsq_kernel(const float* __restrict__ g,
                                                          int64_t n4, int64_t pol4,
-                                                         double* __restrict__ part) {
+                                                         double* __restrict__ part,
+                                                         int64_t* __restrict__ dev_step) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *dev_step += 1;
   __shared__ double red[2][4];
   double s0 = 0.0, s1 = 0.0;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
@@ -608,17 +613,23 @@ struct AdamClipArgs {
   int nparts;
   int clipping;
   float clip_norm;
-  float lr_pol, lr_cri, b1, omb1, b2, omb2, bc1, bc2, eps;
+  float lr_pol, lr_cri, b1, omb1, b2, omb2, eps;
+  const int64_t* dev_step;  // Adam t (already advanced for this step)
   float* norms;  // [2]
   const float* ploss_part;
   int nploss;
   float invB;
   float* policy_loss;
+  const float* ce;  // [B] per-row cross-entropy
+  int B;
+  float* critic_loss;
 };
 
 __global__ void __launch_bounds__(256) adam_clip_kernel(const AdamClipArgs a) {
   __shared__ double red[2][4];
   __shared__ float scl[2];
+  const float tf = (float)*a.dev_step;
+  const float bc1 = 1.f - powf(a.b1, tf), bc2 = 1.f - powf(a.b2, tf);
   double s0 = 0.0, s1 = 0.0;
   for (int i = threadIdx.x; i < a.nparts; i += 256) {
     s0 += a.part[i];
@@ -650,6 +661,11 @@ __global__ void __launch_bounds__(256) adam_clip_kernel(const AdamClipArgs a) {
     for (int i = 0; i < a.nploss; ++i) t += a.ploss_part[i];
     *a.policy_loss = t * a.invB;
   }
+  if (blockIdx.x == 0 && threadIdx.x == 128 && a.critic_loss) {
+    float t = 0.f;
+    for (int i = 0; i < a.B; ++i) t += a.ce[i];
+    *a.critic_loss = t / (float)a.B;  // tf.reduce_mean
+  }
   __syncthreads();
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < a.n4; i += (int64_t)gridDim.x * 256) {
     const bool pol = i < a.pol4;
@@ -664,8 +680,8 @@ __global__ void __launch_bounds__(256) adam_clip_kernel(const AdamClipArgs a) {
       const float gj = __fmul_rn(gg[j], s);
       const float mj = __fadd_rn(__fmul_rn(a.b1, mm[j]), __fmul_rn(a.omb1, gj));
       const float vj = __fadd_rn(__fmul_rn(a.b2, vv[j]), __fmul_rn(a.omb2, __fmul_rn(gj, gj)));
-      const float mh = __fdiv_rn(mj, a.bc1);
-      const float vh = __fdiv_rn(vj, a.bc2);
+      const float mh = __fdiv_rn(mj, bc1);
+      const float vh = __fdiv_rn(vj, bc2);
       const float upd = __fdiv_rn(__fmul_rn(lr, mh), __fadd_rn(__fsqrt_rn(vh), a.eps));
       mm[j] = mj;
       vv[j] = vj;
@@ -679,10 +695,12 @@ __global__ void __launch_bounds__(256) adam_clip_kernel(const AdamClipArgs a) {
 
 // ------------------------------------------------------------------ orchestration
 
-#define D4_GEMM(name, BM, BN, WM, WN, prob)                                                    \
+// Small GEMMs: 32x32 output tiles, one wave per tile and k-group, 4 k-groups per block
+// (intra-block split-K), so a 512 x 512 x 512 layer runs 1024 waves.
+#define D4_GEMM(name, prob)                                                                   \
   do {                                                                                        \
     ACME_PROF(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0);   \
-    hipError_t _e = launch_gemm<BM, BN, WM, WN, 16>(prob, 1, st);                              \
+    hipError_t _e = launch_gemm<32, 32, 1, 1, 16, 4>(prob, 1, st);                             \
     if (_e != hipSuccess) {                                                                   \
       set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
       return ACME_ERR_HIP;                                                                    \
@@ -706,13 +724,13 @@ int dense_fwd(const char* name, const float* x, int rows, int K, const float* w,
     p.M = rows; p.N = N; p.K = K; p.k_chunk = K;
     p.x = x; p.x2 = x; p.split_b = rows; p.ldx = K;
     p.w = w; p.bias = b; p.y = y; p.act = act; p.slab = nullptr;
-    D4_GEMM(name, 32, 64, 1, 2, p);
+    D4_GEMM(name, p);
   } else {
     DenseFwd<false> p;
     p.M = rows; p.N = N; p.K = K; p.k_chunk = K;
     p.x = x; p.x2 = x; p.split_b = rows; p.ldx = K;
     p.w = w; p.bias = b; p.y = y; p.act = act; p.slab = nullptr;
-    D4_GEMM(name, 32, 64, 1, 2, p);
+    D4_GEMM(name, p);
   }
   return ACME_OK;
 }
@@ -724,12 +742,12 @@ int dense_dgrad(const char* name, const float* dz, int rows, int Nout, const flo
     DenseDgrad<true> p;
     p.M = rows; p.N = Nin; p.K = Nout; p.k_chunk = Nout;
     p.dz = dz; p.w = w; p.xprev = xprev; p.ldx = Nin; p.dx = dx; p.act = act;
-    D4_GEMM(name, 32, 64, 1, 2, p);
+    D4_GEMM(name, p);
   } else {
     DenseDgrad<false> p;
     p.M = rows; p.N = Nin; p.K = Nout; p.k_chunk = Nout;
     p.dz = dz; p.w = w; p.xprev = xprev; p.ldx = Nin; p.dx = dx; p.act = act;
-    D4_GEMM(name, 32, 64, 1, 2, p);
+    D4_GEMM(name, p);
   }
   return ACME_OK;
 }
@@ -741,12 +759,12 @@ int dense_wgrad(const char* name, const float* x, int rows, int Nin, const float
     DenseWgrad<true> p;
     p.M = Nin; p.N = Nout; p.K = rows; p.k_chunk = rows;
     p.x = x; p.ldx = Nin; p.dz = dz; p.out = dw; p.bias_out = db;
-    D4_GEMM(name, 32, 64, 1, 2, p);
+    D4_GEMM(name, p);
   } else {
     DenseWgrad<false> p;
     p.M = Nin; p.N = Nout; p.K = rows; p.k_chunk = rows;
     p.x = x; p.ldx = Nin; p.dz = dz; p.out = dw; p.bias_out = db;
-    D4_GEMM(name, 32, 64, 1, 2, p);
+    D4_GEMM(name, p);
   }
   return ACME_OK;
 }
@@ -843,18 +861,18 @@ int ln_backward(acme_d4pg* l, const NetDesc& d, const Acts& a, float* dy, int ro
   p.M = da + db; p.N = H; p.K = ce_rows; p.k_chunk = ce_rows;
   p.x0 = xa; p.d0 = da; p.x1 = xb; p.d1 = db; p.dz = dy;
   p.out = Pm(l, l->grads, d.w1); p.bias_out = Pm(l, l->grads, d.b1);
-  D4_GEMM("d4pg_first_wgrad", 32, 64, 1, 2, p);
+  D4_GEMM("d4pg_first_wgrad", p);
   return ACME_OK;
 }
 
 int d4pg_step_impl(acme_d4pg* l, const acme_d4pg_batch* bt, const acme_d4pg_outputs* out,
-                   hipStream_t st) {
+                   bool copy_target, hipStream_t st) {
   const int B = (int)bt->batch;
   const int od = l->cfg.obs_dim, ad = l->cfg.act_dim;
   const NetDesc& pd = l->pol;
   const NetDesc& cd = l->cri;
   int rc;
-  if (l->num_steps % l->cfg.target_update_period == 0) {
+  if (copy_target) {
     ACME_PROF("d4pg_target_copy", st, 0.0, 2.0 * 4.0 * (double)l->flat);
     ACME_HIP_TRY(hipMemcpyAsync(l->target, l->params, (size_t)l->flat * sizeof(float),
                                 hipMemcpyDeviceToDevice, st));
@@ -869,9 +887,9 @@ int d4pg_step_impl(acme_d4pg* l, const acme_d4pg_batch* bt, const acme_d4pg_outp
     return rc;
   {
     ACME_PROF("d4pg_loss", st, 0.0, 0.0);
-    d4pg_loss_kernel<<<1, 1024, 0, st>>>(l->con.out, l->ctg.out, bt->r_t, bt->d_t, l->values, B,
-                                         cd.nout, l->cfg.discount, l->dlogits,
-                                         out && out->critic_loss ? out->critic_loss : l->loss_tmp);
+    d4pg_loss_kernel<<<(unsigned)ceil_div(2 * B, 4), 256, 0, st>>>(
+        l->con.out, l->ctg.out, bt->r_t, bt->d_t, l->values, B, cd.nout, l->cfg.discount,
+        l->dlogits, l->ce);
     D4_CHECK();
   }
   // Critic backward: 2B rows of dgrad (CE rows + dpg rows), weight grads from the first B.
@@ -897,9 +915,9 @@ int d4pg_step_impl(acme_d4pg* l, const acme_d4pg_batch* bt, const acme_d4pg_outp
   {
     ACME_PROF("d4pg_adam", st, 0.0, 7.0 * 4.0 * (double)l->flat);
     const int64_t n4 = l->flat / 4, pol4 = l->policy_flat / 4;
-    grad_sumsq_kernel<<<kNormBlocks, 256, 0, st>>>(l->grads, n4, pol4, l->norm_part);
+    grad_sumsq_kernel<<<kNormBlocks, 256, 0, st>>>(l->grads, n4, pol4, l->norm_part,
+                                                   l->dev_step);
     D4_CHECK();
-    const int64_t t = l->num_steps + 1;
     AdamClipArgs a;
     a.p = l->params; a.m = l->m; a.v = l->v; a.g = l->grads; a.n4 = n4; a.pol4 = pol4;
     a.part = l->norm_part; a.nparts = kNormBlocks; a.clipping = l->cfg.clipping;
@@ -907,15 +925,70 @@ int d4pg_step_impl(acme_d4pg* l, const acme_d4pg_batch* bt, const acme_d4pg_outp
     a.lr_pol = l->cfg.policy_learning_rate; a.lr_cri = l->cfg.critic_learning_rate;
     a.b1 = l->cfg.adam_beta1; a.omb1 = 1.f - l->cfg.adam_beta1;
     a.b2 = l->cfg.adam_beta2; a.omb2 = 1.f - l->cfg.adam_beta2;
-    a.bc1 = 1.f - powf(l->cfg.adam_beta1, (float)t);
-    a.bc2 = 1.f - powf(l->cfg.adam_beta2, (float)t);
+    a.dev_step = l->dev_step;
     a.eps = l->cfg.adam_epsilon; a.norms = l->norms;
     a.ploss_part = l->ploss_part; a.nploss = (int)ceil_div(2 * B, kRows); a.invB = 1.f / (float)B;
     a.policy_loss = out && out->policy_loss ? out->policy_loss : l->loss_tmp + 1;
+    a.ce = l->ce; a.B = B;
+    a.critic_loss = out && out->critic_loss ? out->critic_loss : l->loss_tmp;
     const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n4, 256), 1024);
     adam_clip_kernel<<<grid, 256, 0, st>>>(a);
     D4_CHECK();
   }
+  return ACME_OK;
+}
+
+// ------------------------------------------------------------------ step graphs
+// The ~40 launches of a step are captured once per (batch pointers, outputs, B, target
+// copy) into a hipGraph on a private capture stream and replayed with one
+// hipGraphLaunch on the caller's stream: the launch cost leaves the host critical path.
+// ACME_NO_GRAPH=1 disables capture; the section profiler also bypasses it (its event
+// records belong to individual launches).
+bool graphs_enabled() {
+  static const bool on = getenv("ACME_NO_GRAPH") == nullptr;
+  return on;
+}
+
+int run_graph(acme_d4pg* l, const acme_d4pg_batch* bt, const acme_d4pg_outputs* out, bool copy,
+              hipStream_t st) {
+  const void* key[7] = {bt->o_tm1, bt->a_tm1, bt->r_t, bt->d_t, bt->o_t,
+                        out ? out->critic_loss : nullptr, out ? out->policy_loss : nullptr};
+  for (auto& g : l->graphs)
+    if (g.B == bt->batch && g.copy == copy && memcmp(g.key, key, sizeof(key)) == 0) {
+      ACME_HIP_TRY(hipGraphLaunch(g.exec, st));
+      return ACME_OK;
+    }
+  if (l->graphs.size() >= 16) {  // a caller cycling many buffers: start over
+    for (auto& g : l->graphs) (void)hipGraphExecDestroy(g.exec);
+    l->graphs.clear();
+  }
+  if (!l->capture) ACME_HIP_TRY(hipStreamCreateWithFlags(&l->capture, hipStreamNonBlocking));
+  ACME_HIP_TRY(hipStreamBeginCapture(l->capture, hipStreamCaptureModeRelaxed));
+  int rc = d4pg_step_impl(l, bt, out, copy, l->capture);
+  hipGraph_t graph = nullptr;
+  hipError_t e = hipStreamEndCapture(l->capture, &graph);
+  if (rc != ACME_OK) {
+    if (graph) (void)hipGraphDestroy(graph);
+    return rc;
+  }
+  if (e != hipSuccess) {
+    set_error("step graph capture failed: %s", hipGetErrorString(e));
+    return ACME_ERR_HIP;
+  }
+  hipGraphExec_t exec = nullptr;
+  e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(graph);
+  if (e != hipSuccess) {
+    set_error("step graph instantiation failed: %s", hipGetErrorString(e));
+    return ACME_ERR_HIP;
+  }
+  acme_d4pg::Graph g;
+  memcpy(g.key, key, sizeof(key));
+  g.B = bt->batch;
+  g.copy = copy;
+  g.exec = exec;
+  l->graphs.push_back(g);
+  ACME_HIP_TRY(hipGraphLaunch(exec, st));
   return ACME_OK;
 }
 
@@ -925,6 +998,8 @@ extern "C" {
 
 int acme_d4pg_destroy(acme_d4pg* l) {
   if (!l) return ACME_OK;
+  for (auto& g : l->graphs) (void)hipGraphExecDestroy(g.exec);
+  if (l->capture) (void)hipStreamDestroy(l->capture);
   for (void* p : l->allocs) (void)hipFree(p);
   delete l;
   return ACME_OK;
@@ -985,7 +1060,8 @@ int acme_d4pg_create(const acme_d4pg_config* cfg, acme_d4pg** out) {
       (rc = dev_alloc(l, &l->lnslab, nblk * 2 * hmax)) ||
       (rc = dev_alloc(l, &l->ploss_part, nblk)) ||
       (rc = dev_alloc(l, &l->norm_part, 2 * kNormBlocks)) ||
-      (rc = dev_alloc(l, &l->norms, 2)) || (rc = dev_alloc(l, &l->loss_tmp, 2)))
+      (rc = dev_alloc(l, &l->norms, 2)) || (rc = dev_alloc(l, &l->loss_tmp, 2)) ||
+      (rc = dev_alloc(l, &l->ce, B)) || (rc = dev_alloc(l, &l->dev_step, 1)))
     return fail(rc);
   // Support: tf.linspace(vmin, vmax, K) (computed in f64, rounded once to f32).
   std::vector<float> vals(cfg->num_atoms), lo(cfg->act_dim), sc(cfg->act_dim);
@@ -995,7 +1071,8 @@ int acme_d4pg_create(const acme_d4pg_config* cfg, acme_d4pg** out) {
     lo[j] = cfg->action_min[j];
     sc[j] = cfg->action_max[j] - cfg->action_min[j];
   }
-  if (hipMemcpy(l->values, vals.data(), vals.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+  if (hipMemset(l->dev_step, 0, sizeof(int64_t)) != hipSuccess ||
+      hipMemcpy(l->values, vals.data(), vals.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(l->act_lo, lo.data(), lo.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(l->act_scale, sc.data(), sc.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
     return fail((set_error("hipMemcpy of the D4PG constants failed"), ACME_ERR_HIP));
@@ -1045,7 +1122,14 @@ int acme_d4pg_step(acme_d4pg* l, const acme_d4pg_batch* batch, const acme_d4pg_o
                  l->cfg.max_batch);
   ACME_CHECK_ARG(batch->o_tm1 && batch->a_tm1 && batch->r_t && batch->d_t && batch->o_t,
                  "null batch field");
-  int rc = d4pg_step_impl(l, batch, out, as_stream(stream));
+  hipStream_t st = as_stream(stream);
+  const bool copy = l->num_steps % l->cfg.target_update_period == 0;
+  int rc;
+  if (graphs_enabled() && !prof::enabled()) {
+    rc = run_graph(l, batch, out, copy, st);
+  } else {
+    rc = d4pg_step_impl(l, batch, out, copy, st);
+  }
   if (rc != ACME_OK) return rc;
   l->num_steps += 1;
   return ACME_OK;
@@ -1071,6 +1155,8 @@ int acme_d4pg_policy(acme_d4pg* l, const float* obs, int64_t rows, int32_t use_t
 int64_t acme_d4pg_num_steps(const acme_d4pg* l) { return l ? l->num_steps : 0; }
 int acme_d4pg_set_num_steps(acme_d4pg* l, int64_t n) {
   ACME_CHECK_ARG(l && n >= 0, "bad argument");
+  ACME_HIP_TRY(hipDeviceSynchronize());
+  ACME_HIP_TRY(hipMemcpy(l->dev_step, &n, sizeof(n), hipMemcpyHostToDevice));
   l->num_steps = n;
   return ACME_OK;
 }

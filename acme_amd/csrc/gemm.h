@@ -112,20 +112,29 @@ struct HasColSum<P, decltype(void(P::kColSum))> {
 //   void store(int m, int n, float v, int split) const;
 // The loaders must return zeros for rows >= M / N and k >= K.
 
-template <int BM, int BN, int WM, int WN, int BK, class P>
-__global__ void __launch_bounds__(64 * WM * WN) gemm_f32_kernel(const P p) {
-  constexpr int NT = 64 * WM * WN;
+// WK > 1 splits the reduction INSIDE the block: WK groups of WM x WN waves each take a
+// contiguous share of the block's K range through their own LDS stages, and the partial
+// accumulators are summed through LDS before the epilogue.  Small GEMMs (a few hundred
+// rows, K <= 1024) use it to put 4x more waves on the same output tiles.
+template <int BM, int BN, int WM, int WN, int BK, int WK, class P>
+__global__ void __launch_bounds__(64 * WM * WN * WK) gemm_f32_kernel(const P p) {
+  constexpr int NTG = 64 * WM * WN;  // threads per k-group
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int MT = TM / 32, NTL = TN / 32;
   static_assert(TM % 32 == 0 && TN % 32 == 0, "wave tile must be a multiple of 32x32");
   static_assert(BK == 16 || BK == 32, "BK must be 16 or 32");
-  using PA = OperandPlan<BM, NT, P::A_MODE, BK>;
-  using PB = OperandPlan<BN, NT, P::B_MODE, BK>;
+  using PA = OperandPlan<BM, NTG, P::A_MODE, BK>;
+  using PB = OperandPlan<BN, NTG, P::B_MODE, BK>;
   constexpr int STAGE = PA::FLOATS + PB::FLOATS;
+  constexpr int STAGE_FLOATS = 2 * STAGE * WK;
+  constexpr int RED_FLOATS = (WK - 1) * WM * WN * MT * NTL * 16 * 64;
+  constexpr int SMEM = STAGE_FLOATS > RED_FLOATS ? STAGE_FLOATS : RED_FLOATS;
 
-  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+  __shared__ __attribute__((aligned(16))) float smem[SMEM];
 
-  const int tid = threadIdx.x;
+  const int tid_all = threadIdx.x;
+  const int grp = tid_all / NTG;
+  const int tid = tid_all - grp * NTG;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int tiles_n = (p.N + BN - 1) / BN;
@@ -133,42 +142,52 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_f32_kernel(const P p) {
   const int m0 = (tile / tiles_n) * BM;
   const int n0 = (tile % tiles_n) * BN;
   const int split = blockIdx.z;
-  const int kbeg = split * p.k_chunk;
+  int kbeg = split * p.k_chunk;
   int kend = kbeg + p.k_chunk;
   if (kend > p.K) kend = p.K;
-  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  int nk_all = nk;
+  if constexpr (WK > 1) {
+    const int per = (nk + WK - 1) / WK;  // stages per group
+    nk_all = per;
+    const int s0 = grp * per;
+    const int s1 = s0 + per < nk ? s0 + per : nk;
+    nk = s1 > s0 ? s1 - s0 : 0;
+    kbeg += s0 * BK;
+  }
+  float* my = smem + grp * 2 * STAGE;
 
   typename P::ARow arow[PA::PER_THREAD];
   typename P::BRow brow[PB::PER_THREAD];
 #pragma unroll
   for (int i = 0; i < PA::PER_THREAD; ++i)
-    arow[i] = p.a_row(m0 + (PA::owns(tid + i * NT) ? PA::row_of(tid + i * NT) : 0));
+    arow[i] = p.a_row(m0 + (PA::owns(tid + i * NTG) ? PA::row_of(tid + i * NTG) : 0));
 #pragma unroll
   for (int i = 0; i < PB::PER_THREAD; ++i)
-    brow[i] = p.b_row(n0 + (PB::owns(tid + i * NT) ? PB::row_of(tid + i * NT) : 0));
+    brow[i] = p.b_row(n0 + (PB::owns(tid + i * NTG) ? PB::row_of(tid + i * NTG) : 0));
 
   f32x4 ra[PA::PER_THREAD], rb[PB::PER_THREAD];
   auto fetch = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < PA::PER_THREAD; ++i) {
-      const int k = k0 + PA::kk_of(tid + i * NT);
-      ra[i] = (PA::owns(tid + i * NT) && k < kend) ? p.a_load(arow[i], k) : zero4();
+      const int k = k0 + PA::kk_of(tid + i * NTG);
+      ra[i] = (PA::owns(tid + i * NTG) && k < kend) ? p.a_load(arow[i], k) : zero4();
     }
 #pragma unroll
     for (int i = 0; i < PB::PER_THREAD; ++i) {
-      const int k = k0 + PB::kk_of(tid + i * NT);
-      rb[i] = (PB::owns(tid + i * NT) && k < kend) ? p.b_load(brow[i], k) : zero4();
+      const int k = k0 + PB::kk_of(tid + i * NTG);
+      rb[i] = (PB::owns(tid + i * NTG) && k < kend) ? p.b_load(brow[i], k) : zero4();
     }
   };
   auto stash = [&](int buf) {
-    float* sa = smem + buf * STAGE;
+    float* sa = my + buf * STAGE;
     float* sb = sa + PA::FLOATS;
 #pragma unroll
     for (int i = 0; i < PA::PER_THREAD; ++i)
-      if (PA::owns(tid + i * NT)) PA::store(sa, tid + i * NT, ra[i]);
+      if (PA::owns(tid + i * NTG)) PA::store(sa, tid + i * NTG, ra[i]);
 #pragma unroll
     for (int i = 0; i < PB::PER_THREAD; ++i)
-      if (PB::owns(tid + i * NT)) PB::store(sb, tid + i * NT, rb[i]);
+      if (PB::owns(tid + i * NTG)) PB::store(sb, tid + i * NTG, rb[i]);
   };
 
   f32x16 acc[MT][NTL];
@@ -186,39 +205,75 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_f32_kernel(const P p) {
   if (nk > 0) {
     fetch(kbeg);
     stash(0);
-    __syncthreads();
   }
-  for (int kt = 0; kt < nk; ++kt) {
+  __syncthreads();
+  for (int kt = 0; kt < nk_all; ++kt) {
+    const bool active = kt < nk;  // uniform per k-group
     const bool more = kt + 1 < nk;
     if (more) fetch(kbeg + (kt + 1) * BK);
-    const float* sa = smem + (kt & 1) * STAGE;
+    const float* sa = my + (kt & 1) * STAGE;
     const float* sb = sa + PA::FLOATS;
-    if constexpr (kColSum) {
-      if (do_colsum) {
+    if (active) {
+      if constexpr (kColSum) {
+        if (do_colsum) {
 #pragma unroll
-        for (int c = 0; c < BK / 4; ++c) {
-          const f32x4 x = PB::frag(sb, tid, c);
-          colsum += (x[0] + x[1]) + (x[2] + x[3]);
+          for (int c = 0; c < BK / 4; ++c) {
+            const f32x4 x = PB::frag(sb, tid, c);
+            colsum += (x[0] + x[1]) + (x[2] + x[3]);
+          }
         }
       }
-    }
 #pragma unroll
-    for (int q = 0; q < BK / 8; ++q) {
-      f32x4 af[MT], bf[NTL];
+      for (int q = 0; q < BK / 8; ++q) {
+        f32x4 af[MT], bf[NTL];
 #pragma unroll
-      for (int i = 0; i < MT; ++i) af[i] = PA::frag(sa, wm * TM + i * 32 + r, 2 * q + h);
+        for (int i = 0; i < MT; ++i) af[i] = PA::frag(sa, wm * TM + i * 32 + r, 2 * q + h);
 #pragma unroll
-      for (int j = 0; j < NTL; ++j) bf[j] = PB::frag(sb, wn * TN + j * 32 + r, 2 * q + h);
+        for (int j = 0; j < NTL; ++j) bf[j] = PB::frag(sb, wn * TN + j * 32 + r, 2 * q + h);
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+        for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int i = 0; i < MT; ++i)
+          for (int i = 0; i < MT; ++i)
 #pragma unroll
-          for (int j = 0; j < NTL; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][t], bf[j][t], acc[i][j], 0, 0, 0);
+            for (int j = 0; j < NTL; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][t], bf[j][t], acc[i][j], 0, 0, 0);
+      }
     }
     if (more) stash((kt + 1) & 1);
     __syncthreads();
+  }
+
+  if constexpr (WK > 1) {
+    // Sum the k-groups' accumulators into group 0 (fixed order: group 0 + 1 + 2 + ...).
+    constexpr int PER_WAVE = MT * NTL * 16 * 64;
+    __shared__ float cs_red[(WK - 1) * BN];
+    if (grp > 0) {
+      float* dst = smem + ((grp - 1) * WM * WN + wave) * PER_WAVE;
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NTL; ++j)
+#pragma unroll
+          for (int v = 0; v < 16; ++v) dst[((i * NTL + j) * 16 + v) * 64 + lane] = acc[i][j][v];
+      if constexpr (kColSum) {
+        if (do_colsum) cs_red[(grp - 1) * BN + tid] = colsum;
+      }
+    }
+    __syncthreads();
+    if (grp > 0) return;
+#pragma unroll
+    for (int g = 1; g < WK; ++g) {
+      const float* src = smem + ((g - 1) * WM * WN + wave) * PER_WAVE;
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NTL; ++j)
+#pragma unroll
+          for (int v = 0; v < 16; ++v) acc[i][j][v] += src[((i * NTL + j) * 16 + v) * 64 + lane];
+      if constexpr (kColSum) {
+        if (do_colsum) colsum += cs_red[(g - 1) * BN + tid];
+      }
+    }
   }
 
   // Epilogue: C/D map of the 32x32 MFMA: col = lane & 31, row = (v&3) + 8(v>>2) + 4h.
@@ -237,11 +292,11 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_f32_kernel(const P p) {
   }
 }
 
-template <int BM, int BN, int WM, int WN, int BK = 16, class P>
+template <int BM, int BN, int WM, int WN, int BK = 16, int WK = 1, class P>
 inline hipError_t launch_gemm(const P& p, int splits, hipStream_t st) {
-  const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, BK, P>), dim3(tiles, 1, splits),
-                     dim3(64 * WM * WN), 0, st, p);
+  const int tiles = ((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
+  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, BK, WK, P>), dim3(tiles, 1, splits),
+                     dim3(64 * WM * WN * WK), 0, st, p);
   return hipGetLastError();
 }
 

@@ -142,46 +142,47 @@ __global__ void sample_uniform_kernel(const double* __restrict__ raw_prio,
   if (out_prio) out_prio[j] = raw_prio[slot];
 }
 
-// Row gather for wide fields: one workgroup per (row, field); 16-B vector copies.
+// Row gather of every field in ONE launch: one workgroup per (row, field).  Rows that
+// are 16-B multiples (the 28,224-B Atari frames, 96-B control observations) move as
+// 16-B vectors with up to 8 loads in flight per thread; other rows as 4-B words or bytes.
 struct GatherArgs {
   const uint8_t* src[ACME_MAX_FIELDS];
   uint8_t* dst[ACME_MAX_FIELDS];
   int64_t bytes[ACME_MAX_FIELDS];
 };
 
-__global__ void __launch_bounds__(256) gather_wide_kernel(GatherArgs g,
-                                                          const int64_t* __restrict__ slots,
-                                                          int field0) {
-  const int f = field0 + blockIdx.y;
+__global__ void __launch_bounds__(256) gather_fields_kernel(GatherArgs g,
+                                                            const int64_t* __restrict__ slots) {
+  const int f = blockIdx.y;
   const int64_t row = blockIdx.x;
   const int64_t slot = slots[row];
-  const int64_t nvec = g.bytes[f] >> 4;
-  const uint4* __restrict__ s = reinterpret_cast<const uint4*>(g.src[f] + slot * g.bytes[f]);
-  uint4* __restrict__ d = reinterpret_cast<uint4*>(g.dst[f] + row * g.bytes[f]);
-  // Issue all loads of this thread before the stores (ILP: up to 8 in flight).
-  for (int64_t i0 = threadIdx.x; i0 < nvec; i0 += 8 * blockDim.x) {
-    uint4 r[8];
+  const int64_t nb = g.bytes[f];
+  const uint8_t* s8 = g.src[f] + slot * nb;
+  uint8_t* d8 = g.dst[f] + row * nb;
+  if ((nb & 15) == 0 && ((reinterpret_cast<uintptr_t>(d8) | reinterpret_cast<uintptr_t>(s8)) & 15) == 0) {
+    const int64_t nvec = nb >> 4;
+    const uint4* __restrict__ s = reinterpret_cast<const uint4*>(s8);
+    uint4* __restrict__ d = reinterpret_cast<uint4*>(d8);
+    for (int64_t i0 = threadIdx.x; i0 < nvec; i0 += 8 * blockDim.x) {
+      uint4 r[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int64_t i = i0 + (int64_t)k * blockDim.x;
-      if (i < nvec) r[k] = s[i];
-    }
+      for (int k = 0; k < 8; ++k) {
+        const int64_t i = i0 + (int64_t)k * blockDim.x;
+        if (i < nvec) r[k] = s[i];
+      }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int64_t i = i0 + (int64_t)k * blockDim.x;
-      if (i < nvec) d[i] = r[k];
+      for (int k = 0; k < 8; ++k) {
+        const int64_t i = i0 + (int64_t)k * blockDim.x;
+        if (i < nvec) d[i] = r[k];
+      }
     }
+  } else if ((nb & 3) == 0 && ((reinterpret_cast<uintptr_t>(d8) | reinterpret_cast<uintptr_t>(s8)) & 3) == 0) {
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(s8);
+    uint32_t* d = reinterpret_cast<uint32_t*>(d8);
+    for (int64_t i = threadIdx.x; i < (nb >> 2); i += blockDim.x) d[i] = s[i];
+  } else {
+    for (int64_t i = threadIdx.x; i < nb; i += blockDim.x) d8[i] = s8[i];
   }
-}
-
-// Narrow fields (4..15 B per row, multiples of 4): one thread per 4-byte word.
-__global__ void gather_narrow_kernel(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
-                                     const int64_t* __restrict__ slots, int64_t batch,
-                                     int64_t words) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= batch * words) return;
-  const int64_t row = i / words, w = i - row * words;
-  dst[i] = src[slots[row] * words + w];
 }
 
 // Recompute level[l] nodes from their 64 children (one wave per node).
@@ -587,27 +588,11 @@ int acme_replay_gather(acme_replay* r, const int64_t* slots, int64_t batch,
     g.dst[f] = static_cast<uint8_t*>(out_fields[f]);
     g.bytes[f] = r->cfg.field_bytes[f];
   }
-  // Wide (16-B multiple, >= 64 B) fields: one workgroup per row; consecutive wide
-  // fields with the same row size share one launch (gridDim.y = field).
   double row_bytes = 0;
   for (int k = 0; k < r->cfg.num_fields; ++k) row_bytes += (double)r->cfg.field_bytes[k];
   ACME_PROF("replay_gather", st, 0.0, 2.0 * row_bytes * (double)batch + 8.0 * (double)batch);
-  int f = 0;
-  while (f < r->cfg.num_fields) {
-    const int64_t b = g.bytes[f];
-    const bool wide = b >= 64 && b % 16 == 0 &&
-                      (reinterpret_cast<uintptr_t>(g.dst[f]) % 16) == 0;
-    if (wide) {
-      gather_wide_kernel<<<dim3((unsigned)batch, 1), 256, 0, st>>>(g, slots, f);
-    } else {
-      const int64_t words = b / 4;
-      gather_narrow_kernel<<<(unsigned)ceil_div(batch * words, 256), 256, 0, st>>>(
-          reinterpret_cast<const uint32_t*>(g.src[f]), reinterpret_cast<uint32_t*>(g.dst[f]),
-          slots, batch, words);
-    }
-    ACME_LAUNCH_CHECK();
-    ++f;
-  }
+  gather_fields_kernel<<<dim3((unsigned)batch, (unsigned)r->cfg.num_fields), 256, 0, st>>>(g, slots);
+  ACME_LAUNCH_CHECK();
   return ACME_OK;
 }
 

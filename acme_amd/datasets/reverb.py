@@ -60,6 +60,7 @@ class _TableIterator:
         self._slots = None
 
     def _alloc(self):
+        import ctypes
         native = self._t.native
         dev = native.device
         self._slots = []
@@ -67,7 +68,18 @@ class _TableIterator:
             info = native.alloc_sample_info(self._B)
             bufs = [torch.empty(self._B, f.row_bytes, dtype=torch.uint8, device=dev)
                     for f in self._t.fields]
-            self._slots.append((info, bufs))
+            data = tree.unflatten_as(self._t._structure, [self._typed(b, f)  # noqa: SLF001
+                                                          for b, f in zip(bufs, self._t.fields)])
+            sample = replay.ReplaySample(
+                info=replay.SampleInfo(key=info["keys"], probability=info["probabilities"],
+                                       table_size=info["table_size"], priority=info["priorities"]),
+                data=data)
+            # Raw device pointers for the two per-step native calls (the views above alias
+            # these buffers, so the returned sample never needs rebuilding).
+            ptrs = (ctypes.c_void_p * len(bufs))(*[b.data_ptr() for b in bufs])
+            raw = tuple(info[k].data_ptr() for k in ("slots", "keys", "probabilities",
+                                                      "table_size", "priorities"))
+            self._slots.append((raw, ptrs, sample))
         self._which = 0
 
     def _typed(self, buf, f):
@@ -81,23 +93,20 @@ class _TableIterator:
         return self
 
     def __next__(self) -> replay.ReplaySample:
+        from acme_amd._lib import check, lib, stream_ptr
         t = self._t
         t.flush()
         t.wait_for(self._B, self._timeout)
         t.flush()
         if self._slots is None:
             self._alloc()
-        info, bufs = self._slots[self._which]
+        raw, ptrs, sample = self._slots[self._which]
         self._which ^= 1
-        native = t.native
-        native.sample(self._B, t.next_draw(), out=info)
-        native.gather(info["slots"], bufs)
-        data = tree.unflatten_as(t._structure, [self._typed(b, f)  # noqa: SLF001
-                                                for b, f in zip(bufs, t.fields)])
-        return replay.ReplaySample(
-            info=replay.SampleInfo(key=info["keys"], probability=info["probabilities"],
-                                   table_size=info["table_size"], priority=info["priorities"]),
-            data=data)
+        L, h, st = lib(), t.native.handle, stream_ptr()
+        check(L.acme_replay_sample(h, self._B, t.next_draw() & 0xFFFFFFFFFFFFFFFF, *raw, st),
+              "replay sample")
+        check(L.acme_replay_gather(h, raw[0], self._B, ptrs, st), "replay gather")
+        return sample
 
 
 class _QueueIterator:

@@ -97,14 +97,11 @@ def test_dqn_learner_step_through_dataset_matches_oracle():
     torch.cuda.synchronize()
     # Re-draw the same batch from a fresh iterator of an identical table state is not
     # possible after the priority update, so recover the batch from the learner's sample:
-    s = learner._iterator._slots[0]  # noqa: SLF001 - the buffers of draw 0
-    info, bufs = s
-    batch = dict(o_tm1=bufs[0].view(torch.float32).cpu().numpy(),
-                 a_tm1=bufs[1].view(torch.int32).cpu().numpy()[:, 0],
-                 r_t=bufs[2].view(torch.float32).cpu().numpy()[:, 0],
-                 d_t=bufs[3].view(torch.float32).cpu().numpy()[:, 0],
-                 o_t=bufs[4].view(torch.float32).cpu().numpy(),
-                 probabilities=info["probabilities"].cpu().numpy())
+    _, _, sample = learner._iterator._slots[0]  # noqa: SLF001 - the buffers of draw 0
+    o1, a, r, d, o2 = sample.data
+    batch = dict(o_tm1=o1.cpu().numpy(), a_tm1=a.cpu().numpy().reshape(-1),
+                 r_t=r.cpu().numpy().reshape(-1), d_t=d.cpu().numpy().reshape(-1),
+                 o_t=o2.cpu().numpy(), probabilities=sample.info.probability.cpu().numpy())
     cfg = O.DQNConfig(num_actions=4, network="mlp", obs_dim=8, hidden=(32, 32))
     out, _ = O.dqn_loss_and_grads(cfg, p0, t0, batch, np.float64)
     np.testing.assert_allclose(learner.native.loss.item(), out["loss"], rtol=1e-5)

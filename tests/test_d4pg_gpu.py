@@ -215,3 +215,32 @@ def test_learner_dropin_path():
     assert all(k.startswith("policy/") for k in pol) and len(pol) == 10
     a = learner.policy(np.zeros((2, 24), np.float32))
     assert a.shape == (2, 6) and np.isfinite(a).all()
+
+
+def test_graph_replay_matches_eager():
+    """The captured step graph (default) and the eager launch sequence (forced by the
+    section profiler) produce bit-identical parameters, including across the target copy
+    and with the two alternating batch buffers the dataset iterator uses."""
+    from acme_amd import _lib
+    cfg = O.D4PGConfig(target_update_period=2, policy_sizes=(64, 64, 64),
+                       critic_sizes=(128, 128, 64))
+    params, target = _random_params(cfg, 11), _random_params(cfg, 12)
+    batches = [_dev(_batch(cfg, 64, 20 + i)) for i in range(2)]
+    results = []
+    for eager in (True, False):
+        n = _native(cfg, 64)
+        n.set_params(params, target)
+        _lib.lib().acme_profile_enable(1 if eager else 0)
+        try:
+            for s in range(5):
+                n.step(*batches[s % 2])
+        finally:
+            _lib.lib().acme_profile_enable(0)
+        torch.cuda.synchronize()
+        results.append((n.get_params("params"), n.get_params("target"),
+                        n.critic_loss.item(), n.policy_loss.item()))
+    (p0, t0, c0, l0), (p1, t1, c1, l1) = results
+    for k in p0:
+        np.testing.assert_array_equal(p0[k], p1[k], err_msg=k)
+        np.testing.assert_array_equal(t0[k], t1[k], err_msg=k)
+    assert c0 == c1 and l0 == l1
