@@ -79,6 +79,26 @@ class D4PGOutputs(ctypes.Structure):
     _fields_ = [("critic_loss", c_vp), ("policy_loss", c_vp)]
 
 
+IMPALA_TORSO_ATARI = 0
+IMPALA_TORSO_FLAT = 1
+
+
+class IMPALAConfig(ctypes.Structure):
+    _fields_ = [("torso", c_i32), ("obs_dim", c_i32), ("num_actions", c_i32),
+                ("max_batch", c_i32), ("max_sequence_length", c_i32), ("lstm_size", c_i32),
+                ("head_size", c_i32), ("discount", c_f32), ("entropy_cost", c_f32),
+                ("baseline_cost", c_f32), ("max_abs_reward", c_f32),
+                ("max_gradient_norm", c_f32), ("learning_rate", c_f32), ("adam_beta1", c_f32),
+                ("adam_beta2", c_f32), ("adam_epsilon", c_f32)]
+
+
+class SequenceBatch(ctypes.Structure):
+    _fields_ = [("observation", c_vp), ("prev_action", c_vp), ("prev_reward", c_vp),
+                ("action", c_vp), ("reward", c_vp), ("discount", c_vp),
+                ("behaviour_logits", c_vp), ("h0", c_vp), ("c0", c_vp),
+                ("state_stride", c_i64), ("batch", c_i64), ("sequence_length", c_i64)]
+
+
 _SIGS = {
     "acme_last_error": (ctypes.c_char_p, []),
     "acme_version": (ctypes.c_char_p, []),
@@ -114,6 +134,21 @@ _SIGS = {
                                       ctypes.POINTER(c_i64)]),
     "acme_dqn_set_num_steps": (c_i32, [c_vp, c_i64]),
     "acme_min_f64": (c_i32, [c_vp, c_i64, c_vp, c_vp]),
+    "acme_impala_create": (c_i32, [ctypes.POINTER(IMPALAConfig), ctypes.POINTER(c_vp)]),
+    "acme_impala_destroy": (c_i32, [c_vp]),
+    "acme_impala_flat_size": (c_i64, [c_vp]),
+    "acme_impala_num_tensors": (c_i32, [c_vp]),
+    "acme_impala_tensor_info": (c_i32, [c_vp, c_i32, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64),
+                                        ctypes.POINTER(c_i32), ctypes.POINTER(c_i64),
+                                        ctypes.POINTER(ctypes.c_char_p)]),
+    "acme_impala_bind": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "acme_impala_step": (c_i32, [c_vp, ctypes.POINTER(SequenceBatch), c_vp, c_vp]),
+    "acme_impala_policy_step": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
+                                        c_vp, c_vp, c_vp]),
+    "acme_impala_num_steps": (c_i64, [c_vp]),
+    "acme_impala_set_num_steps": (c_i32, [c_vp, c_i64]),
+    "acme_impala_debug_buffer": (c_i32, [c_vp, ctypes.c_char_p, ctypes.POINTER(c_vp),
+                                         ctypes.POINTER(c_i64)]),
     "acme_d4pg_create": (c_i32, [ctypes.POINTER(D4PGConfig), ctypes.POINTER(c_vp)]),
     "acme_d4pg_destroy": (c_i32, [c_vp]),
     "acme_d4pg_flat_size": (c_i64, [c_vp]),

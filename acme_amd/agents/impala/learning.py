@@ -1,0 +1,126 @@
+"""IMPALALearner — drop-in for acme/agents/tf/impala/learning.py:36-180.
+
+Same constructor (environment_spec, network, dataset, learning_rate, discount=0.99,
+entropy_cost=0., baseline_cost=1., max_abs_reward=None, max_gradient_norm=None,
+counter=None, logger=None) and `step()` contract.  One call takes a [B, T] batch of
+sequences from the dataset (Step(observation=OAR(...), action, reward, discount,
+start_of_episode, extras={'core_state': LSTMState, 'logits'})) and runs the whole step on
+the GPU (acme_impala_step): torso over all B*T frames, OAR projection, LSTM unroll from
+core_state[:, 0], policy/value head, V-trace, losses, BPTT, global-norm clip, Adam.
+"""
+
+from __future__ import annotations
+
+import time
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from acme_amd import core
+from acme_amd.native import NativeIMPALA
+from acme_amd.utils import counting, loggers
+
+
+def _state_parts(core_state):
+    if isinstance(core_state, dict):
+        return core_state["hidden"], core_state["cell"]
+    hidden, cell = core_state
+    return hidden, cell
+
+
+class IMPALALearner(core.Learner, core.Saveable):
+
+    def __init__(self, environment_spec, network, dataset, learning_rate: float,
+                 discount: float = 0.99, entropy_cost: float = 0., baseline_cost: float = 1.,
+                 max_abs_reward: Optional[float] = None,
+                 max_gradient_norm: Optional[float] = None,
+                 counter: Optional[counting.Counter] = None,
+                 logger: Optional[loggers.Logger] = None, batch_size: Optional[int] = None,
+                 sequence_length: Optional[int] = None, seed: int = 0, device=None):
+        self._env_spec = environment_spec
+        self._network = network
+        self._iterator = iter(dataset)
+        B = batch_size or getattr(dataset, "batch_size", None) or 16
+        T = sequence_length or getattr(dataset, "sequence_length", None) or 20
+        self._native = NativeIMPALA(
+            num_actions=network.num_actions, max_batch=B, max_sequence_length=T,
+            torso=network.torso, obs_dim=network.obs_dim, lstm_size=network.lstm_size,
+            head_size=network.head_size, discount=discount, entropy_cost=entropy_cost,
+            baseline_cost=baseline_cost, max_abs_reward=max_abs_reward,
+            max_gradient_norm=max_gradient_norm, learning_rate=learning_rate, device=device)
+        self._native.set_params(network.init(seed))
+        self._counter = counter or counting.Counter()
+        self._logger = logger or loggers.TerminalLogger("learner", time_delta=1.)
+        self._timestamp = None
+        m = self._native.metrics
+        self._metric_views = {"loss": m[0], "critic_loss": m[1], "entropy_loss": m[2],
+                              "policy_gradient_loss": m[3]}
+
+    def step(self):
+        sample = next(self._iterator)
+        data = sample.data
+        obs = data.observation
+        if not hasattr(obs, "observation"):
+            raise ValueError("IMPALAAtariNetwork takes OAR observations "
+                             "(wrap the environment in ObservationActionRewardWrapper)")
+        dt = torch.uint8 if self._network.torso == "atari" else torch.float32
+        c = lambda x, t: x.to(t).contiguous()  # noqa: E731
+        B, T = int(data.action.shape[0]), int(data.action.shape[1])
+        hidden, cell = _state_parts(data.extras["core_state"])
+        self._native.step(c(obs.observation.reshape((B, T, -1)) if dt == torch.float32
+                            else obs.observation, dt),
+                          c(obs.action.reshape(B, T), torch.int32),
+                          c(obs.reward.reshape(B, T), torch.float32),
+                          c(data.action.reshape(B, T), torch.int32),
+                          c(data.reward.reshape(B, T), torch.float32),
+                          c(data.discount.reshape(B, T), torch.float32),
+                          c(data.extras["logits"], torch.float32),
+                          hidden.to(torch.float32)[:, 0], cell.to(torch.float32)[:, 0])
+        now = time.time()
+        elapsed = now - self._timestamp if self._timestamp else 0
+        self._timestamp = now
+        result = dict(self._metric_views)
+        result.update(self._counter.increment(steps=1, walltime=elapsed))
+        self._logger.write(result)
+
+    def policy_step(self, observation, prev_action, prev_reward, hidden, cell):
+        """Batched network step for actors (numpy in, numpy out)."""
+        n = self._native
+        dt = torch.uint8 if self._network.torso == "atari" else torch.float32
+        dev = n.device
+        t = lambda x, d: torch.as_tensor(np.asarray(x)).to(dev, d)  # noqa: E731
+        rows = int(np.asarray(prev_action).shape[0])
+        lg, v, h, c = n.policy_step(t(observation, dt).reshape(rows, -1),
+                                    t(prev_action, torch.int32), t(prev_reward, torch.float32),
+                                    t(hidden, torch.float32), t(cell, torch.float32))
+        return lg.cpu().numpy(), v.cpu().numpy(), h.cpu().numpy(), c.cpu().numpy()
+
+    def get_variables(self, names: List[str]) -> List[Dict[str, np.ndarray]]:
+        return [self._native.get_params("params")]
+
+    @property
+    def native(self) -> NativeIMPALA:
+        return self._native
+
+    @property
+    def num_steps(self) -> int:
+        return self._native.num_steps
+
+    @property
+    def state(self) -> Dict:
+        return self.save()
+
+    def save(self) -> Dict:
+        n = self._native
+        return {"network": n.get_params("params"),
+                "optimizer": {"m": n.get_params("m"), "v": n.get_params("v")},
+                "num_steps": n.num_steps}
+
+    def restore(self, state: Dict):
+        n = self._native
+        n.set_params(state["network"])
+        for buf, src in ((n.m, state["optimizer"]["m"]), (n.v, state["optimizer"]["v"])):
+            for k, t in n.views(buf).items():
+                t.copy_(torch.as_tensor(np.asarray(src[k], np.float32)).view(t.shape))
+        n.num_steps = int(state["num_steps"])

@@ -569,130 +569,6 @@ struct ConcatWgrad {
   __device__ void store_colsum(int n, float v, int) const { bias_out[n] = v; }
 };
 
-// ------------------------------------------------------------------ clip + Adam
-// Sum of squared gradients per network (policy range [0, n_pol), critic the rest), f64
-// block partials in a fixed order.
-// Block 0 also advances the device step counter (read by adam_clip_kernel as the Adam t),
-// so a captured step graph needs no per-step host arguments.
-__global__ void __launch_bounds__(256) grad_sumsq_kernel(const float* __restrict__ g,
-                                                         int64_t n4, int64_t pol4,
-                                                         double* __restrict__ part,
-                                                         int64_t* __restrict__ dev_step) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) *dev_step += 1;
-  __shared__ double red[2][4];
-  double s0 = 0.0, s1 = 0.0;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-    const f32x4 x = reinterpret_cast<const f32x4*>(g)[i];
-    const double q = (double)x[0] * x[0] + (double)x[1] * x[1] + (double)x[2] * x[2] +
-                     (double)x[3] * x[3];
-    if (i < pol4) s0 += q;
-    else s1 += q;
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    s0 += __shfl_xor(s0, o, 64);
-    s1 += __shfl_xor(s1, o, 64);
-  }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) {
-    red[0][wave] = s0;
-    red[1][wave] = s1;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    part[blockIdx.x] = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
-    part[gridDim.x + blockIdx.x] = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
-  }
-}
-
-struct AdamClipArgs {
-  float *p, *m, *v;
-  const float* g;
-  int64_t n4, pol4;
-  const double* part;
-  int nparts;
-  int clipping;
-  float clip_norm;
-  float lr_pol, lr_cri, b1, omb1, b2, omb2, eps;
-  const int64_t* dev_step;  // Adam t (already advanced for this step)
-  float* norms;  // [2]
-  const float* ploss_part;
-  int nploss;
-  float invB;
-  float* policy_loss;
-  const float* ce;  // [B] per-row cross-entropy
-  int B;
-  float* critic_loss;
-};
-
-__global__ void __launch_bounds__(256) adam_clip_kernel(const AdamClipArgs a) {
-  __shared__ double red[2][4];
-  __shared__ float scl[2];
-  const float tf = (float)*a.dev_step;
-  const float bc1 = 1.f - powf(a.b1, tf), bc2 = 1.f - powf(a.b2, tf);
-  double s0 = 0.0, s1 = 0.0;
-  for (int i = threadIdx.x; i < a.nparts; i += 256) {
-    s0 += a.part[i];
-    s1 += a.part[a.nparts + i];
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    s0 += __shfl_xor(s0, o, 64);
-    s1 += __shfl_xor(s1, o, 64);
-  }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) {
-    red[0][wave] = s0;
-    red[1][wave] = s1;
-  }
-  __syncthreads();
-  if (threadIdx.x < 2) {
-    const int k = threadIdx.x;
-    const double ss = ((red[k][0] + red[k][1]) + red[k][2]) + red[k][3];
-    const float G = (float)sqrt(ss);
-    // tf.clip_by_global_norm: scale = clip * min(1 / G, 1 / clip).
-    float s = 1.f;
-    if (a.clipping && G > 0.f) s = a.clip_norm * fminf(1.f / G, 1.f / a.clip_norm);
-    scl[k] = s;
-    if (blockIdx.x == 0 && a.norms) a.norms[k] = G;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 64 && a.policy_loss) {
-    float t = 0.f;
-    for (int i = 0; i < a.nploss; ++i) t += a.ploss_part[i];
-    *a.policy_loss = t * a.invB;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 128 && a.critic_loss) {
-    float t = 0.f;
-    for (int i = 0; i < a.B; ++i) t += a.ce[i];
-    *a.critic_loss = t / (float)a.B;  // tf.reduce_mean
-  }
-  __syncthreads();
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < a.n4; i += (int64_t)gridDim.x * 256) {
-    const bool pol = i < a.pol4;
-    const float s = pol ? scl[0] : scl[1];
-    const float lr = pol ? a.lr_pol : a.lr_cri;
-    f32x4 gg = reinterpret_cast<const f32x4*>(a.g)[i];
-    f32x4 mm = reinterpret_cast<f32x4*>(a.m)[i];
-    f32x4 vv = reinterpret_cast<f32x4*>(a.v)[i];
-    f32x4 pp = reinterpret_cast<f32x4*>(a.p)[i];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float gj = __fmul_rn(gg[j], s);
-      const float mj = __fadd_rn(__fmul_rn(a.b1, mm[j]), __fmul_rn(a.omb1, gj));
-      const float vj = __fadd_rn(__fmul_rn(a.b2, vv[j]), __fmul_rn(a.omb2, __fmul_rn(gj, gj)));
-      const float mh = __fdiv_rn(mj, bc1);
-      const float vh = __fdiv_rn(vj, bc2);
-      const float upd = __fdiv_rn(__fmul_rn(lr, mh), __fadd_rn(__fsqrt_rn(vh), a.eps));
-      mm[j] = mj;
-      vv[j] = vj;
-      pp[j] = __fsub_rn(pp[j], upd);
-    }
-    reinterpret_cast<f32x4*>(a.m)[i] = mm;
-    reinterpret_cast<f32x4*>(a.v)[i] = vv;
-    reinterpret_cast<f32x4*>(a.p)[i] = pp;
-  }
-}
-
 // ------------------------------------------------------------------ orchestration
 
 // Small GEMMs: 32x32 output tiles, one wave per tile and k-group, 4 k-groups per block
@@ -915,25 +791,21 @@ int d4pg_step_impl(acme_d4pg* l, const acme_d4pg_batch* bt, const acme_d4pg_outp
   {
     ACME_PROF("d4pg_adam", st, 0.0, 7.0 * 4.0 * (double)l->flat);
     const int64_t n4 = l->flat / 4, pol4 = l->policy_flat / 4;
-    grad_sumsq_kernel<<<kNormBlocks, 256, 0, st>>>(l->grads, n4, pol4, l->norm_part,
-                                                   l->dev_step);
-    D4_CHECK();
-    AdamClipArgs a;
-    a.p = l->params; a.m = l->m; a.v = l->v; a.g = l->grads; a.n4 = n4; a.pol4 = pol4;
+    int rc2 = launch_grad_sumsq(l->grads, n4, pol4, l->norm_part, kNormBlocks, l->dev_step, st);
+    if (rc2 != ACME_OK) return rc2;
+    ClipAdamArgs a;
+    a.p = l->params; a.m = l->m; a.v = l->v; a.g = l->grads; a.n4 = n4; a.group0_4 = pol4;
     a.part = l->norm_part; a.nparts = kNormBlocks; a.clipping = l->cfg.clipping;
     a.clip_norm = 40.f;
-    a.lr_pol = l->cfg.policy_learning_rate; a.lr_cri = l->cfg.critic_learning_rate;
-    a.b1 = l->cfg.adam_beta1; a.omb1 = 1.f - l->cfg.adam_beta1;
-    a.b2 = l->cfg.adam_beta2; a.omb2 = 1.f - l->cfg.adam_beta2;
-    a.dev_step = l->dev_step;
-    a.eps = l->cfg.adam_epsilon; a.norms = l->norms;
-    a.ploss_part = l->ploss_part; a.nploss = (int)ceil_div(2 * B, kRows); a.invB = 1.f / (float)B;
-    a.policy_loss = out && out->policy_loss ? out->policy_loss : l->loss_tmp + 1;
-    a.ce = l->ce; a.B = B;
-    a.critic_loss = out && out->critic_loss ? out->critic_loss : l->loss_tmp;
-    const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n4, 256), 1024);
-    adam_clip_kernel<<<grid, 256, 0, st>>>(a);
-    D4_CHECK();
+    a.lr0 = l->cfg.policy_learning_rate; a.lr1 = l->cfg.critic_learning_rate;
+    a.b1 = l->cfg.adam_beta1; a.b2 = l->cfg.adam_beta2; a.eps = l->cfg.adam_epsilon;
+    a.dev_step = l->dev_step; a.norms = l->norms;
+    a.sum_a = l->ploss_part; a.n_a = (int)ceil_div(2 * B, kRows); a.div_a = (float)B;
+    a.out_a = out && out->policy_loss ? out->policy_loss : l->loss_tmp + 1;
+    a.sum_b = l->ce; a.n_b = B; a.div_b = (float)B;
+    a.out_b = out && out->critic_loss ? out->critic_loss : l->loss_tmp;
+    rc2 = launch_clip_adam(a, st);
+    if (rc2 != ACME_OK) return rc2;
   }
   return ACME_OK;
 }

@@ -27,6 +27,7 @@
 #include "gemm.h"
 #include "kernels.h"
 #include "profiler.h"
+#include "torso.h"
 
 using namespace acme;
 using namespace acme::conv;
@@ -34,11 +35,9 @@ using acme::gemm::launch_gemm;
 
 namespace {
 
-// Nature DQN torso geometry (TF SAME padding, NHWC).
-using G1 = Geom<84, 84, 4, 21, 21, 32, 8, 8, 4, 2, 2>;
-using G2 = Geom<21, 21, 32, 11, 11, 64, 4, 4, 2, 1, 1>;
-using G3 = Geom<11, 11, 64, 11, 11, 64, 3, 3, 1, 1, 1>;
-constexpr int kFlat = 11 * 11 * 64;  // 7744
+// Nature DQN torso geometry (TF SAME padding, NHWC): torso.h.
+using torso::G1;
+constexpr int kFlat = torso::kFlat;  // 7744
 constexpr int kHidden = 512;          // DuellingMLP hidden size
 constexpr int kObsBytes = 84 * 84 * 4;
 
@@ -173,13 +172,9 @@ int tune(const char* key) {
 constexpr int kFcFwdSplits = 8;  // [rows, 1024] x K 7744: 128x128 tiles: 8x8x8 = 512 blocks (online)
 constexpr int kHeadFwdSplits = 16;  // [rows, A+1] x K 1024
 constexpr int kHeadBwdSplits = 8;   // [1024, A+1] x K = batch
-constexpr int kConv1WgradSplits = 256, kConv2WgradSplits = 64, kConv3WgradSplits = 64;
 
 int64_t slab_floats_needed(int B, int A) {
-  return std::max<int64_t>({(int64_t)kConv1WgradSplits * (G1::K + 1) * G1::CO,
-                            (int64_t)kConv2WgradSplits * (G2::K + 1) * G2::CO,
-                            (int64_t)kConv3WgradSplits * (G3::K + 1) * G3::CO,
-                            (int64_t)kFcFwdSplits * 2 * B * 2 * kHidden,
+  return std::max<int64_t>({torso::wgrad_slab_floats(), (int64_t)kFcFwdSplits * 2 * B * 2 * kHidden,
                             (int64_t)kHeadFwdSplits * 2 * B * (A + 1),
                             (int64_t)kHeadBwdSplits * (2 * kHidden + 1) * (A + 1)});
 }
@@ -191,6 +186,11 @@ int slab_reduce(const float* slab, int splits, int64_t count, float* out0, int64
   return launch_slab_reduce(slab, splits, count, out0, split_at, out1, bias, ncols, relu, st);
 }
 
+torso::Weights torso_weights(const acme_dqn* l, const float* prm) {
+  return torso::Weights{P(l, prm, l->t_c1w), P(l, prm, l->t_c1b), P(l, prm, l->t_c2w),
+                        P(l, prm, l->t_c2b), P(l, prm, l->t_c3w), P(l, prm, l->t_c3b)};
+}
+
 // ---------------------------------------------------------------- Nature forward
 // rows = number of observations; first `split` rows from obs_a, the rest from obs_b.
 int nature_forward(acme_dqn* l, const float* prm, const void* obs_a, const void* obs_b,
@@ -198,50 +198,9 @@ int nature_forward(acme_dqn* l, const float* prm, const void* obs_a, const void*
                    float* q, hipStream_t st) {
   const bool u8 = l->cfg.obs_dtype == ACME_OBS_U8_SCALED;
   const int A = l->cfg.num_actions;
-  if (u8) {
-    ConvFwd<G1, InU8> p;
-    p.M = rows * G1::OPIX; p.N = G1::CO; p.K = G1::K; p.k_chunk = G1::K;
-    p.x = static_cast<const uint8_t*>(obs_a); p.x2 = static_cast<const uint8_t*>(obs_b);
-    p.split_b = split; p.w = P(l, prm, l->t_c1w); p.bias = P(l, prm, l->t_c1b); p.y = x1;
-    switch (tune("CONV1FWD")) {
-      case 1: ACME_GEMM_NK("conv1_fwd", 256, 32, 4, 1, 16, p, 1); break;
-      case 2: ACME_GEMM_NK("conv1_fwd", 256, 32, 4, 1, 32, p, 1); break;
-      case 3: ACME_GEMM_NK("conv1_fwd", 512, 32, 8, 1, 16, p, 1); break;
-      default: ACME_GEMM_NK("conv1_fwd", 128, 32, 4, 1, 16, p, 1); break;
-    }
-  } else {
-    ConvFwd<G1, InF32> p;
-    p.M = rows * G1::OPIX; p.N = G1::CO; p.K = G1::K; p.k_chunk = G1::K;
-    p.x = static_cast<const float*>(obs_a); p.x2 = static_cast<const float*>(obs_b);
-    p.split_b = split; p.w = P(l, prm, l->t_c1w); p.bias = P(l, prm, l->t_c1b); p.y = x1;
-    ACME_GEMM_N("conv1_fwd", 256, 32, 4, 1, p, 1);
-  }
-  {
-    ConvFwd<G2, InF32> p;
-    p.M = rows * G2::OPIX; p.N = G2::CO; p.K = G2::K; p.k_chunk = G2::K;
-    p.x = x1; p.x2 = x1; p.split_b = rows; p.w = P(l, prm, l->t_c2w);
-    p.bias = P(l, prm, l->t_c2b); p.y = x2;
-    switch (tune("CONVFWD")) {
-      case 1: ACME_GEMM_NK("conv2_fwd", 256, 64, 4, 1, 16, p, 1); break;
-      case 2: ACME_GEMM_NK("conv2_fwd", 128, 64, 2, 2, 32, p, 1); break;
-      case 3: ACME_GEMM_NK("conv2_fwd", 256, 64, 4, 2, 16, p, 1); break;
-      case 4: ACME_GEMM_NK("conv2_fwd", 128, 64, 4, 1, 16, p, 1); break;
-      default: ACME_GEMM_NK("conv2_fwd", 128, 64, 2, 2, 16, p, 1); break;
-    }
-  }
-  {
-    ConvFwd<G3, InF32> p;
-    p.M = rows * G3::OPIX; p.N = G3::CO; p.K = G3::K; p.k_chunk = G3::K;
-    p.x = x2; p.x2 = x2; p.split_b = rows; p.w = P(l, prm, l->t_c3w);
-    p.bias = P(l, prm, l->t_c3b); p.y = x3;
-    switch (tune("CONVFWD")) {
-      case 1: ACME_GEMM_NK("conv3_fwd", 256, 64, 4, 1, 16, p, 1); break;
-      case 2: ACME_GEMM_NK("conv3_fwd", 128, 64, 2, 2, 32, p, 1); break;
-      case 3: ACME_GEMM_NK("conv3_fwd", 256, 64, 4, 2, 16, p, 1); break;
-      case 4: ACME_GEMM_NK("conv3_fwd", 128, 64, 4, 1, 16, p, 1); break;
-      default: ACME_GEMM_NK("conv3_fwd", 128, 64, 2, 2, 16, p, 1); break;
-    }
-  }
+  int rc0 = torso::forward(torso_weights(l, prm), u8, obs_a, obs_b, split, rows,
+                           torso::Acts{x1, x2, x3}, st);
+  if (rc0 != ACME_OK) return rc0;
   {  // Fused duelling hidden layer, split-K partials then bias + ReLU in the reduction.
     DenseFwd<true> p;
     const int v = tune("FCFWD");
@@ -315,36 +274,6 @@ int mlp_forward(acme_dqn* l, const float* prm, const void* obs_a, const void* ob
   return ACME_OK;
 }
 
-// ---------------------------------------------------------------- backward helpers
-// Conv weight + bias gradient: split-K over the batch pixels into [splits][K+1][CO] slabs
-// (row K = bias partial from the GEMM's colsum hook), then one deterministic reduction
-// writes dW and db.
-template <class G, class In, int BM, int BN, int WM, int WN>
-int conv_wgrad(acme_dqn* l, const typename In::T* x, const float* dz, int batch, int splits,
-               float* dw, float* db, const char* name, const char* rname, hipStream_t st) {
-  ConvWgrad<G, In> p;
-  p.M = G::K; p.N = G::CO; p.K = batch * G::OPIX; p.k_chunk = chunk_for(p.K, splits);
-  p.x = x; p.dz = dz; p.slab = l->slab;
-  if ((int64_t)splits * (p.M + 1) * p.N > l->slab_floats) {
-    set_error("slab workspace too small");
-    return ACME_ERR_INVALID;
-  }
-  ACME_GEMM_N(name, BM, BN, WM, WN, p, splits);
-  const int64_t count = (int64_t)(p.M + 1) * p.N;
-  return slab_reduce(l->slab, splits, count, dw, (int64_t)p.M * p.N, db, nullptr, 0, 0, rname,
-                     st);
-}
-
-template <int PH, int PW>
-int conv2_dgrad_class(acme_dqn* l, int B, hipStream_t st) {
-  using Sub = ConvDgradSub<G2, PH, PW>;
-  Sub p;
-  p.M = B * Sub::NH * Sub::NW; p.N = G2::CI; p.K = Sub::KR; p.k_chunk = Sub::KR;
-  p.dz = l->dz2; p.w = P(l, l->params, l->t_c2w); p.xprev = l->x1; p.dx = l->dz1;
-  ACME_GEMM_N("conv2_dgrad", 256, 32, 4, 1, p, 1);
-  return ACME_OK;
-}
-
 int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st) {
   const float* prm = l->params;
   float* gr = l->grads;
@@ -384,43 +313,11 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st) {
       default: ACME_GEMM_NK("fc_dgrad", 64, 128, 2, 2, 16, p, 1); break;
     }
   }
-  // conv3
-  if ((rc = conv_wgrad<G3, InF32, 64, 64, 2, 2>(l, l->x2, l->dz3, B, kConv3WgradSplits,
-                                                Pm(l, gr, l->t_c3w), Pm(l, gr, l->t_c3b),
-                                                "conv3_wgrad", "conv3_wgrad_reduce", st)) != ACME_OK)
-    return rc;
-  {
-    ConvDgrad<G3> p;
-    p.M = B * G3::IPIX; p.N = G3::CI; p.K = G3::KH * G3::KW * G3::CO; p.k_chunk = p.K;
-    p.dz = l->dz3; p.w = P(l, prm, l->t_c3w); p.xprev = l->x2; p.dx = l->dz2;
-    switch (tune("CONV3DGRAD")) {
-      case 1: ACME_GEMM_NK("conv3_dgrad", 128, 64, 4, 1, 16, p, 1); break;
-      case 2: ACME_GEMM_NK("conv3_dgrad", 256, 64, 4, 2, 16, p, 1); break;
-      default: ACME_GEMM_NK("conv3_dgrad", 128, 64, 2, 2, 16, p, 1); break;
-    }
-  }
-  // conv2
-  if ((rc = conv_wgrad<G2, InF32, 64, 64, 2, 2>(l, l->x1, l->dz2, B, kConv2WgradSplits,
-                                                Pm(l, gr, l->t_c2w), Pm(l, gr, l->t_c2b),
-                                                "conv2_wgrad", "conv2_wgrad_reduce", st)) != ACME_OK)
-    return rc;
-  // Stride-2 input gradient as four dense sub-pixel GEMMs (one per parity class).
-  if ((rc = conv2_dgrad_class<0, 0>(l, B, st)) || (rc = conv2_dgrad_class<0, 1>(l, B, st)) ||
-      (rc = conv2_dgrad_class<1, 0>(l, B, st)) || (rc = conv2_dgrad_class<1, 1>(l, B, st)))
-    return rc;
-  // conv1 (no input gradient needed)
-  if (l->cfg.obs_dtype == ACME_OBS_U8_SCALED) {
-    rc = conv_wgrad<G1, InU8, 128, 32, 4, 1>(l, static_cast<const uint8_t*>(o_tm1), l->dz1, B,
-                                             kConv1WgradSplits, Pm(l, gr, l->t_c1w),
-                                             Pm(l, gr, l->t_c1b), "conv1_wgrad",
-                                             "conv1_wgrad_reduce", st);
-  } else {
-    rc = conv_wgrad<G1, InF32, 128, 32, 4, 1>(l, static_cast<const float*>(o_tm1), l->dz1, B,
-                                              kConv1WgradSplits, Pm(l, gr, l->t_c1w),
-                                              Pm(l, gr, l->t_c1b), "conv1_wgrad",
-                                              "conv1_wgrad_reduce", st);
-  }
-  return rc;
+  torso::Grads g{Pm(l, gr, l->t_c1w), Pm(l, gr, l->t_c1b), Pm(l, gr, l->t_c2w),
+                 Pm(l, gr, l->t_c2b), Pm(l, gr, l->t_c3w), Pm(l, gr, l->t_c3b)};
+  return torso::backward(torso_weights(l, prm), g, l->cfg.obs_dtype == ACME_OBS_U8_SCALED,
+                         o_tm1, B, torso::Acts{l->x1, l->x2, l->x3}, l->dz3, l->dz2, l->dz1,
+                         l->slab, st);
 }
 
 template <class In>

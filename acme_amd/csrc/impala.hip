@@ -1,0 +1,845 @@
+// IMPALA learner step for MI355X: the replacement of IMPALALearner._step
+// (acme/agents/tf/impala/learning.py:97-169) behind the C ABI (include/acme_hip.h).
+//
+// One call = the whole step on one stream, no host synchronisation.  Rows are the B*T
+// frames of the batch in the dataset's batch-major order (row = b * T + t):
+//   AtariTorso over all B*T frames (torso.h; the FLAT torso uses the observation)
+//   OAR embedding x GEMM: gx = [feat | one_hot(prev a) | tanh(prev r)] @ W_i + b, the
+//     embedding synthesised by the GEMM loader (never materialised)       (embedding.py)
+//   T launches of the LSTM cell: gates = gx_t + h_{t-1} @ W_h, (i, f, g, o), c, h
+//   head: relu(h @ W1 + b1) @ W_pv + b_pv -> logits [A], value              (atari.py:130-134)
+//   loss kernel (one wave per sequence): log-rhos, V-trace backward scan,
+//     pg / baseline / entropy losses and d loss / d(logits, value)        (learning.py:121-155)
+//   backward: head GEMMs, T launches of LSTM BPTT, W_h / W_i(+b) weight GEMMs over all
+//     rows, embedding dgrad masked by conv3's ReLU into the torso backward
+//   clip_by_global_norm(max_gradient_norm) + Adam                         (learning.py:158-160)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "conv.h"
+#include "gemm.h"
+#include "kernels.h"
+#include "profiler.h"
+#include "torso.h"
+
+using namespace acme;
+using namespace acme::conv;
+using acme::gemm::launch_gemm;
+
+namespace {
+
+constexpr int kUnits = 8;        // LSTM units per block of the cell kernels
+constexpr int kNormBlocks = 256;
+constexpr int kOarSplits = 8;    // split-K of the Atari OAR projection (K = 7744 + A + 1)
+
+struct Tensor {
+  std::string name;
+  int64_t offset = 0, numel = 0;
+  int ndim = 0;
+  int64_t shape[4] = {1, 1, 1, 1};
+};
+
+}  // namespace
+
+struct acme_impala {
+  acme_impala_config cfg;
+  std::vector<Tensor> tensors;
+  int64_t flat = 0;
+  int F = 0, D = 0, H = 0, H2 = 0, A = 0;  // features, embedding, lstm, head, actions
+  int t_c[6] = {-1, -1, -1, -1, -1, -1};   // torso w1 b1 w2 b2 w3 b3
+  int t_wi = -1, t_wh = -1, t_b = -1, t_w1 = -1, t_b1 = -1, t_wpv = -1, t_bpv = -1;
+  float *params = nullptr, *grads = nullptr, *m = nullptr, *v = nullptr;
+  int64_t num_steps = 0;
+  std::vector<void*> allocs;
+  // workspace (rows = max_batch * max_sequence_length)
+  float *x1 = nullptr, *x2 = nullptr, *x3 = nullptr, *dz1 = nullptr, *dz2 = nullptr,
+        *dz3 = nullptr;
+  float* slab = nullptr;
+  float *gx = nullptr, *gates = nullptr, *h = nullptr, *c = nullptr, *hh = nullptr, *pv = nullptr;
+  float *dpv = nullptr, *dhh = nullptr, *dh = nullptr, *dgates = nullptr, *dc = nullptr;
+  float *vs = nullptr, *pg_adv = nullptr;
+  double* norm_part = nullptr;
+  int64_t* dev_step = nullptr;
+  float* metrics_tmp = nullptr;
+  float* norms = nullptr;
+};
+
+namespace {
+
+int64_t align64(int64_t x) { return (x + 63) & ~int64_t(63); }
+
+int add_tensor(acme_impala* l, const std::string& name, std::initializer_list<int64_t> shape) {
+  Tensor t;
+  t.name = name;
+  t.ndim = (int)shape.size();
+  t.numel = 1;
+  int i = 0;
+  for (int64_t s : shape) {
+    t.shape[i++] = s;
+    t.numel *= s;
+  }
+  t.offset = l->flat;
+  l->flat = align64(l->flat + t.numel);
+  l->tensors.push_back(t);
+  return (int)l->tensors.size() - 1;
+}
+
+template <class T>
+int dev_alloc(acme_impala* l, T** p, int64_t count) {
+  void* q = nullptr;
+  if (hipMalloc(&q, std::max<int64_t>(count, 1) * sizeof(T)) != hipSuccess) {
+    set_error("hipMalloc of %lld bytes failed", (long long)(count * sizeof(T)));
+    return ACME_ERR_OOM;
+  }
+  l->allocs.push_back(q);
+  *p = static_cast<T*>(q);
+  return ACME_OK;
+}
+
+inline const float* P(const acme_impala* l, const float* base, int t) {
+  return base + l->tensors[t].offset;
+}
+inline float* Pm(const acme_impala* l, float* base, int t) { return base + l->tensors[t].offset; }
+
+__device__ __forceinline__ float sigmoidf(float x) { return 1.f / (1.f + expf(-x)); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ------------------------------------------------------------------ OAR embedding loaders
+// Embedding row m = [feat[m][0:F] | one_hot(prev_a[m], A) | tanh(prev_r[m])], D = F + A + 1.
+struct Oar {
+  const float* feat;  // [rows][F]
+  int F, A;
+  const int32_t* prev_a;
+  const float* prev_r;
+  __device__ float at(int m, int k) const {
+    if (k < F) return feat[(size_t)m * F + k];
+    k -= F;
+    if (k < A) return prev_a[m] == k ? 1.f : 0.f;
+    return k == A ? tanhf(prev_r[m]) : 0.f;
+  }
+  __device__ f32x4 four(int m, int k) const {
+    if ((F & 3) == 0 && k + 3 < F) return *reinterpret_cast<const f32x4*>(feat + (size_t)m * F + k);
+    f32x4 r;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = at(m, k + j);
+    return r;
+  }
+};
+
+// gx = emb @ W_i (+ b when not split): M = rows, N = 4H, K = D.
+struct OarFwd {
+  static constexpr int A_MODE = gemm::KCONTIG, B_MODE = gemm::RCONTIG;
+  int M, N, K, k_chunk;
+  Oar x;
+  const float* w;     // [D][4H]
+  const float* bias;  // [4H]
+  float* y;           // [rows][4H]
+  float* slab;        // split-K partials [splits][M][N] (bias added by the reduction)
+  struct ARow {
+    int m;
+  };
+  struct BRow {
+    int n;
+  };
+  __device__ ARow a_row(int m) const { return ARow{m}; }
+  __device__ f32x4 a_load(const ARow& a, int k) const {
+    if (a.m >= M || k >= K) return gemm::zero4();
+    f32x4 r = x.four(a.m, k);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (k + j >= K) r[j] = 0.f;
+    return r;
+  }
+  __device__ BRow b_row(int n) const { return BRow{n}; }
+  __device__ f32x4 b_load(const BRow& b, int k) const {
+    if (b.n >= N || k >= K) return gemm::zero4();
+    return load_row4<true>(w + (size_t)k * N, b.n, N);
+  }
+  __device__ void store(int m, int n, float v, int split) const {
+    if (slab) slab[((size_t)split * M + m) * N + n] = v;
+    else y[(size_t)m * N + n] = v + bias[n];
+  }
+};
+
+// dW_i = emb^T dgates (M = D, N = 4H, K = rows), db = column sums of dgates.
+struct OarWgrad {
+  static constexpr int A_MODE = gemm::RCONTIG, B_MODE = gemm::RCONTIG;
+  static constexpr bool kColSum = true;
+  int M, N, K, k_chunk;
+  Oar x;
+  const float* dz;  // [rows][4H]
+  float* out;
+  float* bias_out;
+  struct ARow {
+    int i;
+  };
+  struct BRow {
+    int n;
+  };
+  __device__ ARow a_row(int i) const { return ARow{i}; }
+  __device__ f32x4 a_load(const ARow& a, int m) const {
+    if (m >= K || a.i >= M) return gemm::zero4();
+    f32x4 r = x.four(m, a.i);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (a.i + j >= M) r[j] = 0.f;
+    return r;
+  }
+  __device__ BRow b_row(int n) const { return BRow{n}; }
+  __device__ f32x4 b_load(const BRow& b, int m) const {
+    if (b.n >= N || m >= K) return gemm::zero4();
+    return load_row4<true>(dz + (size_t)m * N, b.n, N);
+  }
+  __device__ void store(int i, int n, float v, int) const { out[(size_t)i * N + n] = v; }
+  __device__ void store_colsum(int n, float v, int) const { bias_out[n] = v; }
+};
+
+// dW_h = h_prev^T dgates: h_prev of row m = b*T + t is h[m - 1] (t > 0) or h0[b] (t = 0).
+struct HPrevWgrad {
+  static constexpr int A_MODE = gemm::RCONTIG, B_MODE = gemm::RCONTIG;
+  int M, N, K, k_chunk;  // M = H, N = 4H, K = rows
+  const float* h;        // [rows][H]
+  const float* h0;
+  int64_t h0_stride;
+  int T;
+  const float* dz;
+  float* out;
+  struct ARow {
+    int i;
+  };
+  struct BRow {
+    int n;
+  };
+  __device__ ARow a_row(int i) const { return ARow{i}; }
+  __device__ f32x4 a_load(const ARow& a, int m) const {
+    if (m >= K || a.i >= M) return gemm::zero4();
+    const int t = m % T;
+    const float* p = t == 0 ? h0 + (size_t)(m / T) * h0_stride : h + (size_t)(m - 1) * M;
+    return *reinterpret_cast<const f32x4*>(p + a.i);
+  }
+  __device__ BRow b_row(int n) const { return BRow{n}; }
+  __device__ f32x4 b_load(const BRow& b, int m) const {
+    if (b.n >= N || m >= K) return gemm::zero4();
+    return load_row4<true>(dz + (size_t)m * N, b.n, N);
+  }
+  __device__ void store(int i, int n, float v, int) const { out[(size_t)i * N + n] = v; }
+};
+
+// ------------------------------------------------------------------ LSTM cell kernels
+// Forward step t for all B sequences, kUnits units per block: z = gx + h_prev @ W_h
+// (gate columns q*H + u), then the snt.LSTM cell update.  h_prev row b lives at
+// hp + b * hp_stride (the core state for t = 0, the previous step's h otherwise).
+__global__ void __launch_bounds__(256) lstm_fwd_step_kernel(
+    const float* __restrict__ gx, const float* __restrict__ wh, const float* __restrict__ hp,
+    int64_t hp_stride, const float* __restrict__ cp, int64_t cp_stride, int B, int T, int t, int H,
+    float* __restrict__ gates, float* __restrict__ h_out, float* __restrict__ c_out) {
+  extern __shared__ float smem[];
+  float* hs = smem;                 // [B][H]
+  float* zs = smem + (size_t)B * H;  // [B][4 * kUnits]
+  const int u0 = blockIdx.x * kUnits;
+  for (int i = threadIdx.x; i < B * H; i += blockDim.x) {
+    const int b = i / H, k = i - b * H;
+    hs[i] = hp[(size_t)b * hp_stride + k];
+  }
+  __syncthreads();
+  constexpr int NC = 4 * kUnits;
+  for (int o = threadIdx.x; o < B * NC; o += blockDim.x) {
+    const int b = o / NC, c = o - b * NC;
+    const int col = (c / kUnits) * H + u0 + (c % kUnits);
+    const int row = b * T + t;
+    float acc = 0.f;
+    const float* hrow = hs + (size_t)b * H;
+    for (int k = 0; k < H; ++k) acc = fmaf(hrow[k], wh[(size_t)k * 4 * H + col], acc);
+    zs[o] = gx[(size_t)row * 4 * H + col] + acc;
+  }
+  __syncthreads();
+  for (int o = threadIdx.x; o < B * kUnits; o += blockDim.x) {
+    const int b = o / kUnits, u = o - b * kUnits, j = u0 + u;
+    const float* z = zs + (size_t)b * NC;
+    const float ig = sigmoidf(z[u]), fg = sigmoidf(z[kUnits + u]);
+    const float gg = tanhf(z[2 * kUnits + u]), og = sigmoidf(z[3 * kUnits + u]);
+    const float cprev = cp[(size_t)b * cp_stride + j];
+    const float cn = fg * cprev + ig * gg;
+    const float hn = og * tanhf(cn);
+    const size_t row = (size_t)b * T + t;
+    gates[row * 4 * H + j] = ig;
+    gates[row * 4 * H + H + j] = fg;
+    gates[row * 4 * H + 2 * H + j] = gg;
+    gates[row * 4 * H + 3 * H + j] = og;
+    c_out[row * H + j] = cn;
+    h_out[row * H + j] = hn;
+  }
+}
+
+// Backward step t: dh = dh_head[t] + dgates[t+1] @ W_h^T (t < T-1), dc = dc_carry +
+// dh o (1 - tanh^2 c), gate gradients (pre-activation), dc_carry <- dc f.
+__global__ void __launch_bounds__(256) lstm_bwd_step_kernel(
+    const float* __restrict__ dh_head, const float* __restrict__ wh, const float* __restrict__ gates,
+    const float* __restrict__ c_all, const float* __restrict__ c0, int64_t c0_stride,
+    float* __restrict__ dc_carry, float* __restrict__ dgates, int B, int T, int t, int H) {
+  __shared__ float part[256];
+  const int u0 = blockIdx.x * kUnits;
+  const int nout = B * kUnits;
+  for (int ob = 0; ob < nout; ob += 256) {
+    const int chunk = nout - ob < 256 ? nout - ob : 256;
+    const int ks = 256 / chunk;  // k slices per output (>= 1)
+    const int o = ob + (int)threadIdx.x % chunk, sl = (int)threadIdx.x / chunk;
+    float acc = 0.f;
+    if (t + 1 < T && sl < ks) {
+      const int b = o / kUnits, j = u0 + o % kUnits;
+      const float* dn = dgates + ((size_t)b * T + t + 1) * 4 * H;
+      const float* w = wh + (size_t)j * 4 * H;
+      for (int k = sl; k < 4 * H; k += ks) acc = fmaf(dn[k], w[k], acc);
+    }
+    if (sl < ks) part[threadIdx.x] = acc;
+    __syncthreads();
+    if ((int)threadIdx.x < chunk) {
+      float dhn = 0.f;
+      for (int s2 = 0; s2 < ks; ++s2) dhn += part[s2 * chunk + threadIdx.x];
+      const int b = o / kUnits, j = u0 + o % kUnits;
+      const size_t row = (size_t)b * T + t;
+      const float* g = gates + row * 4 * H;
+      const float ig = g[j], fg = g[H + j], gg = g[2 * H + j], og = g[3 * H + j];
+      const float cn = c_all[row * H + j];
+      const float cprev = t > 0 ? c_all[(row - 1) * H + j] : c0[(size_t)b * c0_stride + j];
+      const float tc = tanhf(cn);
+      const float dh = dh_head[row * H + j] + dhn;
+      const float dc = dc_carry[(size_t)b * H + j] + dh * og * (1.f - tc * tc);
+      float* dg = dgates + row * 4 * H;
+      dg[j] = dc * gg * ig * (1.f - ig);
+      dg[H + j] = dc * cprev * fg * (1.f - fg);
+      dg[2 * H + j] = dc * ig * (1.f - gg * gg);
+      dg[3 * H + j] = dh * tc * og * (1.f - og);
+      dc_carry[(size_t)b * H + j] = dc * fg;
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------ loss
+// One wave per sequence b (lane = action): for t < T-1 log pi, log mu, log rho, entropy;
+// V-trace backward scan (trfl.vtrace_from_importance_weights, rho_bar = c_bar = 1);
+// losses and d loss / d [logits | value] written into dpv rows b*T + t (zero at t = T-1).
+struct LossArgs {
+  const float* pv;  // [rows][A + 1]
+  const int32_t* action;
+  const float *reward, *discount, *mu;
+  int B, T, A;
+  float gamma, entropy_cost, baseline_cost, max_abs_reward;
+  float* dpv;
+  float *vs, *pg_adv;  // [(T-1) * B] time-major
+  float* metrics;      // [4]
+};
+
+__global__ void __launch_bounds__(1024) impala_loss_kernel(const LossArgs a) {
+  __shared__ float red[16][3];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int A = a.A, T = a.T, W = A + 1;
+  const bool on = lane < A;
+  const float invN = 1.f / (float)((T - 1) * a.B);
+  float s_pg = 0.f, s_cr = 0.f, s_en = 0.f;
+  for (int b = wave; b < a.B; b += nw) {
+    // Pass 1 (forward in t): per-step quantities kept in the lane owning step t (T <= 64).
+    float my_lrho = 0.f, my_lpa = 0.f, my_ent = 0.f, my_r = 0.f, my_g = 0.f, my_v = 0.f;
+    for (int t = 0; t < T; ++t) {
+      const size_t row = (size_t)b * T + t;
+      const float v = a.pv[row * W + A];
+      if (lane == t) my_v = v;
+      if (t == T - 1) break;
+      const float l = on ? a.pv[row * W + lane] : -INFINITY;
+      const float m = wave_max(l);
+      const float e = on ? expf(l - m) : 0.f;
+      const float s = wave_sum(e);
+      const float logp = l - m - logf(s);
+      const float mu = on ? a.mu[row * A + lane] : -INFINITY;
+      const float mm = wave_max(mu);
+      const float me = on ? expf(mu - mm) : 0.f;
+      const float logmu = mu - mm - logf(wave_sum(me));
+      const int act = a.action[row];
+      const float lpa = __shfl(logp, act, 64), lma = __shfl(logmu, act, 64);
+      const float ent = -wave_sum(on ? (e / s) * logp : 0.f);
+      if (lane == t) {
+        my_lrho = lpa - lma;
+        my_lpa = lpa;
+        my_ent = ent;
+        float r = a.reward[row];
+        r = fminf(fmaxf(r, -a.max_abs_reward), a.max_abs_reward);
+        my_r = r;
+        my_g = a.gamma * a.discount[row];
+      }
+    }
+    // Pass 2: V-trace backward scan, serial in lane 0 over values gathered by shuffles.
+    const float boot = __shfl(my_v, T - 1, 64);
+    float acc = 0.f, vs_next = boot, my_vs = 0.f, my_adv = 0.f;
+    for (int t = T - 2; t >= 0; --t) {
+      const float lrho = __shfl(my_lrho, t, 64), r = __shfl(my_r, t, 64);
+      const float g = __shfl(my_g, t, 64), v = __shfl(my_v, t, 64);
+      const float v1 = __shfl(my_v, t + 1, 64);
+      const float rho = expf(lrho);
+      const float cr = fminf(1.f, rho);
+      const float delta = cr * (r + g * v1 - v);
+      acc = delta + g * cr * acc;
+      const float vs = acc + v;
+      const float adv = cr * (r + g * vs_next - v);
+      vs_next = vs;
+      if (lane == t) {
+        my_vs = vs;
+        my_adv = adv;
+      }
+    }
+    // Pass 3: losses and gradients.
+    for (int t = 0; t < T; ++t) {
+      const size_t row = (size_t)b * T + t;
+      if (t == T - 1) {
+        if (lane < W) a.dpv[row * W + lane] = 0.f;
+        continue;
+      }
+      const float vs = __shfl(my_vs, t, 64), adv = __shfl(my_adv, t, 64);
+      const float v = __shfl(my_v, t, 64), ent = __shfl(my_ent, t, 64);
+      const float lpa = __shfl(my_lpa, t, 64);
+      const float l = on ? a.pv[row * W + lane] : -INFINITY;
+      const float m = wave_max(l);
+      const float e = on ? expf(l - m) : 0.f;
+      const float s = wave_sum(e);
+      const float logp = l - m - logf(s);
+      const float pi = e / s;
+      const int act = a.action[row];
+      if (on) {
+        const float oh = lane == act ? 1.f : 0.f;
+        a.dpv[row * W + lane] =
+            (-(oh - pi) * adv + a.entropy_cost * pi * (logp + ent)) * invN;
+      }
+      if (lane == A) a.dpv[row * W + A] = a.baseline_cost * (-2.f) * (vs - v) * invN;
+      if (lane == 0) {
+        s_pg += -lpa * adv;
+        s_cr += (vs - v) * (vs - v);
+        s_en += -ent;
+        a.vs[(size_t)t * a.B + b] = vs;
+        a.pg_adv[(size_t)t * a.B + b] = adv;
+      }
+    }
+  }
+  if (lane == 0) {
+    red[wave][0] = s_pg;
+    red[wave][1] = s_cr;
+    red[wave][2] = s_en;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float pg = 0.f, cr = 0.f, en = 0.f;
+    for (int w = 0; w < nw; ++w) {
+      pg += red[w][0];
+      cr += red[w][1];
+      en += red[w][2];
+    }
+    pg *= invN;
+    cr *= invN;
+    en *= invN;
+    a.metrics[0] = pg + a.baseline_cost * cr + a.entropy_cost * en;
+    a.metrics[1] = cr;
+    a.metrics[2] = en;
+    a.metrics[3] = pg;
+  }
+}
+
+// ------------------------------------------------------------------ orchestration
+
+#define IM_GEMM(name, BM, BN, WM, WN, WK, prob, splits)                                         \
+  do {                                                                                         \
+    ACME_PROF(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0);    \
+    hipError_t _e = launch_gemm<BM, BN, WM, WN, 16, WK>(prob, splits, st);                      \
+    if (_e != hipSuccess) {                                                                    \
+      set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__);  \
+      return ACME_ERR_HIP;                                                                     \
+    }                                                                                          \
+  } while (0)
+
+#define IM_CHECK()                                                                             \
+  do {                                                                                         \
+    hipError_t _e = hipGetLastError();                                                         \
+    if (_e != hipSuccess) {                                                                    \
+      set_error("kernel launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
+      return ACME_ERR_HIP;                                                                     \
+    }                                                                                          \
+  } while (0)
+
+inline int chunk_for(int K, int splits) {
+  int c = (int)ceil_div(K, splits);
+  return (int)ceil_div(c, 32) * 32;
+}
+
+bool atari(const acme_impala* l) { return l->cfg.torso == ACME_IMPALA_TORSO_ATARI; }
+
+torso::Weights torso_w(const acme_impala* l) {
+  return torso::Weights{P(l, l->params, l->t_c[0]), P(l, l->params, l->t_c[1]),
+                        P(l, l->params, l->t_c[2]), P(l, l->params, l->t_c[3]),
+                        P(l, l->params, l->t_c[4]), P(l, l->params, l->t_c[5])};
+}
+
+// Network forward over rows = B*T frames: features, OAR projection, T LSTM steps, head.
+int network_forward(acme_impala* l, const void* obs, const int32_t* prev_a, const float* prev_r,
+                    const float* h0, const float* c0, int64_t state_stride, int B, int T,
+                    hipStream_t st) {
+  const int rows = B * T, H = l->H, A = l->A;
+  const float* feat;
+  if (atari(l)) {
+    int rc = torso::forward(torso_w(l), true, obs, obs, rows, rows,
+                            torso::Acts{l->x1, l->x2, l->x3}, st);
+    if (rc != ACME_OK) return rc;
+    feat = l->x3;
+  } else {
+    feat = static_cast<const float*>(obs);
+  }
+  {
+    OarFwd p;
+    p.M = rows; p.N = 4 * H; p.K = l->D;
+    p.x = Oar{feat, l->F, A, prev_a, prev_r};
+    p.w = P(l, l->params, l->t_wi); p.bias = P(l, l->params, l->t_b); p.y = l->gx;
+    if (atari(l)) {
+      p.k_chunk = chunk_for(p.K, kOarSplits);
+      p.slab = l->slab;
+      IM_GEMM("impala_oar_fwd", 64, 64, 2, 2, 1, p, kOarSplits);
+      ACME_PROF("impala_oar_reduce", st, 0.0, 4.0 * (kOarSplits + 1) * (double)rows * 4 * H);
+      int rc = launch_slab_reduce(l->slab, kOarSplits, (int64_t)rows * 4 * H, l->gx,
+                                  (int64_t)rows * 4 * H, nullptr, P(l, l->params, l->t_b), 4 * H,
+                                  0, st);
+      if (rc != ACME_OK) return rc;
+    } else {
+      p.k_chunk = p.K;
+      p.slab = nullptr;
+      IM_GEMM("impala_oar_fwd", 32, 32, 1, 1, 4, p, 1);
+    }
+  }
+  {
+    ACME_PROF("impala_lstm_fwd", st, 2.0 * rows * (double)H * 4 * H, 0.0);
+    const size_t smem = ((size_t)B * H + (size_t)B * 4 * kUnits) * sizeof(float);
+    for (int t = 0; t < T; ++t) {
+      const float* hp = t == 0 ? h0 : l->h + (size_t)(t - 1) * H;
+      const float* cp = t == 0 ? c0 : l->c + (size_t)(t - 1) * H;
+      const int64_t hs = t == 0 ? state_stride : (int64_t)T * H;
+      lstm_fwd_step_kernel<<<H / kUnits, 256, smem, st>>>(l->gx, P(l, l->params, l->t_wh), hp, hs,
+                                                          cp, hs, B, T, t, H, l->gates, l->h,
+                                                          l->c);
+      IM_CHECK();
+    }
+  }
+  {
+    DenseFwd<true> p;
+    p.M = rows; p.N = l->H2; p.K = H; p.k_chunk = H;
+    p.x = l->h; p.x2 = l->h; p.split_b = rows; p.ldx = H;
+    p.w = P(l, l->params, l->t_w1); p.bias = P(l, l->params, l->t_b1); p.y = l->hh;
+    p.act = ACT_RELU; p.slab = nullptr;
+    IM_GEMM("impala_head_fwd", 32, 32, 1, 1, 4, p, 1);
+  }
+  {
+    DenseFwd<false> p;
+    p.M = rows; p.N = A + 1; p.K = l->H2; p.k_chunk = l->H2;
+    p.x = l->hh; p.x2 = l->hh; p.split_b = rows; p.ldx = l->H2;
+    p.w = P(l, l->params, l->t_wpv); p.bias = P(l, l->params, l->t_bpv); p.y = l->pv;
+    p.act = ACT_NONE; p.slab = nullptr;
+    IM_GEMM("impala_pv_fwd", 32, 32, 1, 1, 4, p, 1);
+  }
+  return ACME_OK;
+}
+
+int impala_step_impl(acme_impala* l, const acme_sequence_batch* bt, float* metrics,
+                     hipStream_t st) {
+  const int B = (int)bt->batch, T = (int)bt->sequence_length, rows = B * T;
+  const int H = l->H, A = l->A;
+  int rc = network_forward(l, bt->observation, bt->prev_action, bt->prev_reward, bt->h0, bt->c0,
+                           bt->state_stride, B, T, st);
+  if (rc != ACME_OK) return rc;
+  {
+    ACME_PROF("impala_loss", st, 0.0, 0.0);
+    LossArgs a;
+    a.pv = l->pv; a.action = bt->action; a.reward = bt->reward; a.discount = bt->discount;
+    a.mu = bt->behaviour_logits; a.B = B; a.T = T; a.A = A;
+    a.gamma = l->cfg.discount; a.entropy_cost = l->cfg.entropy_cost;
+    a.baseline_cost = l->cfg.baseline_cost; a.max_abs_reward = l->cfg.max_abs_reward;
+    a.dpv = l->dpv; a.vs = l->vs; a.pg_adv = l->pg_adv;
+    a.metrics = metrics ? metrics : l->metrics_tmp;
+    impala_loss_kernel<<<1, 64 * std::min(B, 16), 0, st>>>(a);
+    IM_CHECK();
+  }
+  float* gr = l->grads;
+  {  // policy/value head
+    DenseWgrad<false> w;
+    w.M = l->H2; w.N = A + 1; w.K = rows; w.k_chunk = rows;
+    w.x = l->hh; w.ldx = l->H2; w.dz = l->dpv; w.out = Pm(l, gr, l->t_wpv);
+    w.bias_out = Pm(l, gr, l->t_bpv);
+    IM_GEMM("impala_pv_wgrad", 32, 32, 1, 1, 4, w, 1);
+    DenseDgrad<false> d;
+    d.M = rows; d.N = l->H2; d.K = A + 1; d.k_chunk = A + 1;
+    d.dz = l->dpv; d.w = P(l, l->params, l->t_wpv); d.xprev = l->hh; d.ldx = l->H2; d.dx = l->dhh;
+    d.act = ACT_RELU;
+    IM_GEMM("impala_pv_dgrad", 32, 32, 1, 1, 4, d, 1);
+  }
+  {  // Linear(256) after the LSTM
+    DenseWgrad<true> w;
+    w.M = H; w.N = l->H2; w.K = rows; w.k_chunk = rows;
+    w.x = l->h; w.ldx = H; w.dz = l->dhh; w.out = Pm(l, gr, l->t_w1); w.bias_out = Pm(l, gr, l->t_b1);
+    IM_GEMM("impala_head_wgrad", 32, 32, 1, 1, 4, w, 1);
+    DenseDgrad<true> d;
+    d.M = rows; d.N = H; d.K = l->H2; d.k_chunk = l->H2;
+    d.dz = l->dhh; d.w = P(l, l->params, l->t_w1); d.xprev = nullptr; d.ldx = H; d.dx = l->dh;
+    IM_GEMM("impala_head_dgrad", 32, 32, 1, 1, 4, d, 1);
+  }
+  {  // BPTT
+    ACME_PROF("impala_lstm_bwd", st, 2.0 * rows * (double)H * 4 * H, 0.0);
+    ACME_HIP_TRY(hipMemsetAsync(l->dc, 0, (size_t)B * H * sizeof(float), st));
+    for (int t = T - 1; t >= 0; --t) {
+      lstm_bwd_step_kernel<<<H / kUnits, 256, 0, st>>>(l->dh, P(l, l->params, l->t_wh), l->gates,
+                                                       l->c, bt->c0, bt->state_stride, l->dc,
+                                                       l->dgates, B, T, t, H);
+      IM_CHECK();
+    }
+  }
+  {  // LSTM weights: W_h over h_prev, W_i (+ b via colsum) over the OAR embedding
+    HPrevWgrad w;
+    w.M = H; w.N = 4 * H; w.K = rows; w.k_chunk = rows;
+    w.h = l->h; w.h0 = bt->h0; w.h0_stride = bt->state_stride; w.T = T; w.dz = l->dgates;
+    w.out = Pm(l, gr, l->t_wh);
+    IM_GEMM("impala_wh_wgrad", 32, 32, 1, 1, 4, w, 1);
+    const float* feat = atari(l) ? l->x3 : static_cast<const float*>(bt->observation);
+    OarWgrad o;
+    o.M = l->D; o.N = 4 * H; o.K = rows; o.k_chunk = rows;
+    o.x = Oar{feat, l->F, A, bt->prev_action, bt->prev_reward};
+    o.dz = l->dgates; o.out = Pm(l, gr, l->t_wi); o.bias_out = Pm(l, gr, l->t_b);
+    if (atari(l)) IM_GEMM("impala_wi_wgrad", 128, 128, 2, 2, 1, o, 1);
+    else IM_GEMM("impala_wi_wgrad", 32, 32, 1, 1, 4, o, 1);
+  }
+  if (atari(l)) {  // embedding features -> conv3 dZ -> torso backward
+    DenseDgrad<true> d;
+    d.M = rows; d.N = l->F; d.K = 4 * H; d.k_chunk = 4 * H;
+    d.dz = l->dgates; d.w = P(l, l->params, l->t_wi); d.xprev = l->x3; d.ldx = l->F;
+    d.dx = l->dz3; d.act = ACT_RELU;
+    IM_GEMM("impala_feat_dgrad", 64, 128, 2, 2, 1, d, 1);
+    torso::Grads g{Pm(l, gr, l->t_c[0]), Pm(l, gr, l->t_c[1]), Pm(l, gr, l->t_c[2]),
+                   Pm(l, gr, l->t_c[3]), Pm(l, gr, l->t_c[4]), Pm(l, gr, l->t_c[5])};
+    rc = torso::backward(torso_w(l), g, true, bt->observation, rows,
+                         torso::Acts{l->x1, l->x2, l->x3}, l->dz3, l->dz2, l->dz1, l->slab, st);
+    if (rc != ACME_OK) return rc;
+  }
+  {
+    ACME_PROF("impala_adam", st, 0.0, 7.0 * 4.0 * (double)l->flat);
+    const int64_t n4 = l->flat / 4;
+    rc = launch_grad_sumsq(gr, n4, n4, l->norm_part, kNormBlocks, l->dev_step, st);
+    if (rc != ACME_OK) return rc;
+    ClipAdamArgs a;
+    a.p = l->params; a.m = l->m; a.v = l->v; a.g = gr; a.n4 = n4; a.group0_4 = n4;
+    a.part = l->norm_part; a.nparts = kNormBlocks; a.clipping = 1;
+    a.clip_norm = l->cfg.max_gradient_norm;
+    a.lr0 = a.lr1 = l->cfg.learning_rate;
+    a.b1 = l->cfg.adam_beta1; a.b2 = l->cfg.adam_beta2; a.eps = l->cfg.adam_epsilon;
+    a.dev_step = l->dev_step; a.norms = l->norms;
+    rc = launch_clip_adam(a, st);
+    if (rc != ACME_OK) return rc;
+  }
+  return ACME_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int acme_impala_destroy(acme_impala* l) {
+  if (!l) return ACME_OK;
+  for (void* p : l->allocs) (void)hipFree(p);
+  delete l;
+  return ACME_OK;
+}
+
+int acme_impala_create(const acme_impala_config* cfg, acme_impala** out) {
+  ACME_CHECK_ARG(cfg && out, "null argument");
+  ACME_CHECK_ARG(cfg->torso == ACME_IMPALA_TORSO_ATARI || cfg->torso == ACME_IMPALA_TORSO_FLAT,
+                 "unknown torso %d", cfg->torso);
+  ACME_CHECK_ARG(cfg->torso == ACME_IMPALA_TORSO_ATARI || cfg->obs_dim >= 1,
+                 "obs_dim must be >= 1 for the flat torso");
+  ACME_CHECK_ARG(cfg->num_actions >= 1 && cfg->num_actions <= 63, "num_actions must be in [1, 63]");
+  ACME_CHECK_ARG(cfg->max_batch >= 1 && cfg->max_batch <= 1024, "max_batch must be in [1, 1024]");
+  ACME_CHECK_ARG(cfg->max_sequence_length >= 2 && cfg->max_sequence_length <= 64,
+                 "max_sequence_length must be in [2, 64]");
+  ACME_CHECK_ARG(cfg->lstm_size >= 8 && cfg->lstm_size % 8 == 0,
+                 "lstm_size must be a positive multiple of 8");
+  ACME_CHECK_ARG((int64_t)cfg->max_batch * (cfg->lstm_size + 4 * kUnits) <= 16384,
+                 "max_batch * (lstm_size + 32) must be <= 16384 (LSTM cell LDS)");
+  ACME_CHECK_ARG(cfg->head_size >= 4 && cfg->head_size % 4 == 0,
+                 "head_size must be a positive multiple of 4");
+  acme_impala* l = new acme_impala();
+  l->cfg = *cfg;
+  auto fail = [&](int code) {
+    acme_impala_destroy(l);
+    return code;
+  };
+  l->A = cfg->num_actions;
+  l->H = cfg->lstm_size;
+  l->H2 = cfg->head_size;
+  l->F = cfg->torso == ACME_IMPALA_TORSO_ATARI ? torso::kFlat : cfg->obs_dim;
+  l->D = l->F + l->A + 1;
+  const std::string pre = "impala_atari_network/";
+  if (cfg->torso == ACME_IMPALA_TORSO_ATARI) {
+    l->t_c[0] = add_tensor(l, pre + "atari_torso/conv2_d/w", {8, 8, 4, 32});
+    l->t_c[1] = add_tensor(l, pre + "atari_torso/conv2_d/b", {32});
+    l->t_c[2] = add_tensor(l, pre + "atari_torso/conv2_d_1/w", {4, 4, 32, 64});
+    l->t_c[3] = add_tensor(l, pre + "atari_torso/conv2_d_1/b", {64});
+    l->t_c[4] = add_tensor(l, pre + "atari_torso/conv2_d_2/w", {3, 3, 64, 64});
+    l->t_c[5] = add_tensor(l, pre + "atari_torso/conv2_d_2/b", {64});
+  }
+  const int H = l->H, A = l->A, H2 = l->H2;
+  l->t_wi = add_tensor(l, pre + "lstm/w_i", {l->D, 4 * H});
+  l->t_wh = add_tensor(l, pre + "lstm/w_h", {H, 4 * H});
+  l->t_b = add_tensor(l, pre + "lstm/b", {4 * H});
+  l->t_w1 = add_tensor(l, pre + "linear/w", {H, H2});
+  l->t_b1 = add_tensor(l, pre + "linear/b", {H2});
+  l->t_wpv = add_tensor(l, pre + "policy_value/w", {H2, A + 1});
+  l->t_bpv = add_tensor(l, pre + "policy_value/b", {A + 1});
+  const int64_t R = (int64_t)cfg->max_batch * cfg->max_sequence_length;
+  const int B = cfg->max_batch;
+  int rc;
+  int64_t slab = 1;
+  if (cfg->torso == ACME_IMPALA_TORSO_ATARI) {
+    slab = std::max<int64_t>(torso::wgrad_slab_floats(), (int64_t)kOarSplits * R * 4 * H);
+    if ((rc = dev_alloc(l, &l->x1, R * torso::kX1)) || (rc = dev_alloc(l, &l->x2, R * torso::kFlat)) ||
+        (rc = dev_alloc(l, &l->x3, R * torso::kFlat)) || (rc = dev_alloc(l, &l->dz1, R * torso::kX1)) ||
+        (rc = dev_alloc(l, &l->dz2, R * torso::kFlat)) || (rc = dev_alloc(l, &l->dz3, R * torso::kFlat)))
+      return fail(rc);
+  }
+  if ((rc = dev_alloc(l, &l->slab, slab)) || (rc = dev_alloc(l, &l->gx, R * 4 * H)) ||
+      (rc = dev_alloc(l, &l->gates, R * 4 * H)) || (rc = dev_alloc(l, &l->h, R * H)) ||
+      (rc = dev_alloc(l, &l->c, R * H)) || (rc = dev_alloc(l, &l->hh, R * H2)) ||
+      (rc = dev_alloc(l, &l->pv, R * (A + 1))) || (rc = dev_alloc(l, &l->dpv, R * (A + 1))) ||
+      (rc = dev_alloc(l, &l->dhh, R * H2)) || (rc = dev_alloc(l, &l->dh, R * H)) ||
+      (rc = dev_alloc(l, &l->dgates, R * 4 * H)) || (rc = dev_alloc(l, &l->dc, (int64_t)B * H)) ||
+      (rc = dev_alloc(l, &l->vs, R)) || (rc = dev_alloc(l, &l->pg_adv, R)) ||
+      (rc = dev_alloc(l, &l->norm_part, 2 * kNormBlocks)) || (rc = dev_alloc(l, &l->dev_step, 1)) ||
+      (rc = dev_alloc(l, &l->metrics_tmp, 4)) || (rc = dev_alloc(l, &l->norms, 2)))
+    return fail(rc);
+  if (hipMemset(l->dev_step, 0, sizeof(int64_t)) != hipSuccess)
+    return fail((set_error("hipMemset failed"), ACME_ERR_HIP));
+  *out = l;
+  return ACME_OK;
+}
+
+int64_t acme_impala_flat_size(const acme_impala* l) { return l ? l->flat : 0; }
+int32_t acme_impala_num_tensors(const acme_impala* l) { return l ? (int32_t)l->tensors.size() : 0; }
+
+int acme_impala_tensor_info(const acme_impala* l, int32_t i, int64_t* offset, int64_t* numel,
+                            int32_t* ndim, int64_t* shape4, const char** name) {
+  ACME_CHECK_ARG(l, "null learner");
+  ACME_CHECK_ARG(i >= 0 && i < (int32_t)l->tensors.size(), "tensor index %d out of range", i);
+  const Tensor& t = l->tensors[i];
+  if (offset) *offset = t.offset;
+  if (numel) *numel = t.numel;
+  if (ndim) *ndim = t.ndim;
+  if (shape4)
+    for (int k = 0; k < 4; ++k) shape4[k] = t.shape[k];
+  if (name) *name = t.name.c_str();
+  return ACME_OK;
+}
+
+int acme_impala_bind(acme_impala* l, float* params, float* grads, float* adam_m, float* adam_v) {
+  ACME_CHECK_ARG(l, "null learner");
+  ACME_CHECK_ARG(params && grads && adam_m && adam_v, "null buffer");
+  l->params = params;
+  l->grads = grads;
+  l->m = adam_m;
+  l->v = adam_v;
+  return ACME_OK;
+}
+
+int acme_impala_step(acme_impala* l, const acme_sequence_batch* b, float* metrics, void* stream) {
+  ACME_CHECK_ARG(l && b, "null argument");
+  ACME_CHECK_ARG(l->params, "acme_impala_bind must be called first");
+  ACME_CHECK_ARG(b->batch >= 1 && b->batch <= l->cfg.max_batch, "batch %lld outside [1, %d]",
+                 (long long)b->batch, l->cfg.max_batch);
+  ACME_CHECK_ARG(b->sequence_length >= 2 && b->sequence_length <= l->cfg.max_sequence_length,
+                 "sequence_length %lld outside [2, %d]", (long long)b->sequence_length,
+                 l->cfg.max_sequence_length);
+  ACME_CHECK_ARG(b->observation && b->prev_action && b->prev_reward && b->action && b->reward &&
+                     b->discount && b->behaviour_logits && b->h0 && b->c0,
+                 "null batch field");
+  ACME_CHECK_ARG(b->state_stride >= l->H && b->state_stride % 4 == 0 &&
+                     ((uintptr_t)b->h0 & 15) == 0,
+                 "core state rows must be 16-byte aligned with state_stride >= lstm_size");
+  int rc = impala_step_impl(l, b, metrics, as_stream(stream));
+  if (rc != ACME_OK) return rc;
+  l->num_steps += 1;
+  return ACME_OK;
+}
+
+int acme_impala_policy_step(acme_impala* l, const void* obs, const int32_t* prev_action,
+                            const float* prev_reward, const float* h, const float* c,
+                            int64_t rows, float* logits, float* values, float* h_out,
+                            float* c_out, void* stream) {
+  ACME_CHECK_ARG(l && obs && prev_action && prev_reward && h && c, "null argument");
+  ACME_CHECK_ARG(l->params, "acme_impala_bind must be called first");
+  ACME_CHECK_ARG(rows >= 1 && rows <= l->cfg.max_batch,
+                 "rows must be in [1, max_batch=%d]", l->cfg.max_batch);
+  hipStream_t st = as_stream(stream);
+  const int H = l->H, A = l->A;
+  int rc = network_forward(l, obs, prev_action, prev_reward, h, c, H, (int)rows, 1, st);
+  if (rc != ACME_OK) return rc;
+  // Outputs are rows of the T = 1 unroll.
+  if (logits)
+    ACME_HIP_TRY(hipMemcpy2DAsync(logits, A * sizeof(float), l->pv, (A + 1) * sizeof(float),
+                                  A * sizeof(float), rows, hipMemcpyDeviceToDevice, st));
+  if (values)
+    ACME_HIP_TRY(hipMemcpy2DAsync(values, sizeof(float), l->pv + A, (A + 1) * sizeof(float),
+                                  sizeof(float), rows, hipMemcpyDeviceToDevice, st));
+  if (h_out)
+    ACME_HIP_TRY(hipMemcpyAsync(h_out, l->h, rows * H * sizeof(float), hipMemcpyDeviceToDevice, st));
+  if (c_out)
+    ACME_HIP_TRY(hipMemcpyAsync(c_out, l->c, rows * H * sizeof(float), hipMemcpyDeviceToDevice, st));
+  return ACME_OK;
+}
+
+int64_t acme_impala_num_steps(const acme_impala* l) { return l ? l->num_steps : 0; }
+
+int acme_impala_set_num_steps(acme_impala* l, int64_t n) {
+  ACME_CHECK_ARG(l && n >= 0, "bad argument");
+  ACME_HIP_TRY(hipDeviceSynchronize());
+  ACME_HIP_TRY(hipMemcpy(l->dev_step, &n, sizeof(n), hipMemcpyHostToDevice));
+  l->num_steps = n;
+  return ACME_OK;
+}
+
+int acme_impala_debug_buffer(const acme_impala* l, const char* name, const float** out,
+                             int64_t* count) {
+  ACME_CHECK_ARG(l && name && out && count, "null argument");
+  const int64_t R = (int64_t)l->cfg.max_batch * l->cfg.max_sequence_length;
+  struct Item {
+    const char* n;
+    const float* p;
+    int64_t c;
+  } items[] = {
+      {"pv", l->pv, R * (l->A + 1)}, {"vs", l->vs, R},        {"pg_adv", l->pg_adv, R},
+      {"h", l->h, R * l->H},         {"c", l->c, R * l->H},   {"dpv", l->dpv, R * (l->A + 1)},
+      {"dgates", l->dgates, R * 4 * l->H}, {"grad_norm", l->norms, 1},
+  };
+  for (const Item& it : items)
+    if (strcmp(it.n, name) == 0) {
+      *out = it.p;
+      *count = it.c;
+      return ACME_OK;
+    }
+  set_error("unknown debug buffer '%s'", name);
+  return ACME_ERR_INVALID;
+}
+
+}  // extern "C"

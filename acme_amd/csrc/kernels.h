@@ -54,4 +54,36 @@ int launch_slab_reduce(const float* slab, int splits, int64_t count, float* out0
                        int64_t split_at, float* out1, const float* bias, int ncols, int relu,
                        hipStream_t st);
 
+// Gradient global norms of two parameter groups ([0, group0_4) and [group0_4, n4) in
+// float4 units): f64 partial sums of squares per block into part[2][nparts], fixed order.
+// Block 0 also advances *dev_step (the Adam t read by launch_clip_adam), so a captured
+// step graph needs no per-step host argument.
+int launch_grad_sumsq(const float* g, int64_t n4, int64_t group0_4, double* part, int nparts,
+                      int64_t* dev_step, hipStream_t st);
+
+// tf.clip_by_global_norm per group (scale = clip * min(1/G, 1/clip) when clipping) then
+// snt.Adam with t = *dev_step and a per-group learning rate.  Optionally block 0 also
+// reduces two per-row loss buffers: *out_x = sum(sum_x[0:n_x]) / div_x.
+struct ClipAdamArgs {
+  float *p = nullptr, *m = nullptr, *v = nullptr;
+  const float* g = nullptr;
+  int64_t n4 = 0, group0_4 = 0;
+  const double* part = nullptr;
+  int nparts = 0;
+  int clipping = 0;
+  float clip_norm = 1e10f;
+  float lr0 = 0.f, lr1 = 0.f, b1 = 0.9f, b2 = 0.999f, eps = 1e-8f;
+  const int64_t* dev_step = nullptr;
+  float* norms = nullptr;  // [2] (optional)
+  const float* sum_a = nullptr;
+  int n_a = 0;
+  float div_a = 1.f;
+  float* out_a = nullptr;
+  const float* sum_b = nullptr;
+  int n_b = 0;
+  float div_b = 1.f;
+  float* out_b = nullptr;
+};
+int launch_clip_adam(const ClipAdamArgs& a, hipStream_t st);
+
 }  // namespace acme

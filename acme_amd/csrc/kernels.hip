@@ -221,6 +221,105 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p,
   }
 }
 
+
+__global__ void __launch_bounds__(256) grad_sumsq_kernel(const float* __restrict__ g, int64_t n4,
+                                                         int64_t pol4, double* __restrict__ part,
+                                                         int64_t* __restrict__ dev_step) {
+  if (blockIdx.x == 0 && threadIdx.x == 0 && dev_step) *dev_step += 1;
+  __shared__ double red[2][4];
+  double s0 = 0.0, s1 = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const f32x4 x = reinterpret_cast<const f32x4*>(g)[i];
+    const double q = (double)x[0] * x[0] + (double)x[1] * x[1] + (double)x[2] * x[2] +
+                     (double)x[3] * x[3];
+    if (i < pol4) s0 += q;
+    else s1 += q;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s0 += __shfl_xor(s0, o, 64);
+    s1 += __shfl_xor(s1, o, 64);
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[0][wave] = s0;
+    red[1][wave] = s1;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+    part[gridDim.x + blockIdx.x] = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+  }
+}
+
+__global__ void __launch_bounds__(256) clip_adam_kernel(const ClipAdamArgs a) {
+  __shared__ double red[2][4];
+  __shared__ float scl[2];
+  const float tf = (float)*a.dev_step;
+  const float bc1 = 1.f - powf(a.b1, tf), bc2 = 1.f - powf(a.b2, tf);
+  const float omb1 = 1.f - a.b1, omb2 = 1.f - a.b2;
+  double s0 = 0.0, s1 = 0.0;
+  for (int i = threadIdx.x; i < a.nparts; i += 256) {
+    s0 += a.part[i];
+    s1 += a.part[a.nparts + i];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s0 += __shfl_xor(s0, o, 64);
+    s1 += __shfl_xor(s1, o, 64);
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[0][wave] = s0;
+    red[1][wave] = s1;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    const int k = threadIdx.x;
+    const double ss = ((red[k][0] + red[k][1]) + red[k][2]) + red[k][3];
+    const float G = (float)sqrt(ss);
+    float s = 1.f;
+    if (a.clipping && G > 0.f) s = a.clip_norm * fminf(1.f / G, 1.f / a.clip_norm);
+    scl[k] = s;
+    if (blockIdx.x == 0 && a.norms) a.norms[k] = G;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 64 && a.out_a) {
+    float t = 0.f;
+    for (int i = 0; i < a.n_a; ++i) t += a.sum_a[i];
+    *a.out_a = t / a.div_a;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 128 && a.out_b) {
+    float t = 0.f;
+    for (int i = 0; i < a.n_b; ++i) t += a.sum_b[i];
+    *a.out_b = t / a.div_b;
+  }
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < a.n4; i += (int64_t)gridDim.x * 256) {
+    const bool g0 = i < a.group0_4;
+    const float s = g0 ? scl[0] : scl[1];
+    const float lr = g0 ? a.lr0 : a.lr1;
+    f32x4 gg = reinterpret_cast<const f32x4*>(a.g)[i];
+    f32x4 mm = reinterpret_cast<f32x4*>(a.m)[i];
+    f32x4 vv = reinterpret_cast<f32x4*>(a.v)[i];
+    f32x4 pp = reinterpret_cast<f32x4*>(a.p)[i];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float gj = __fmul_rn(gg[j], s);
+      const float mj = __fadd_rn(__fmul_rn(a.b1, mm[j]), __fmul_rn(omb1, gj));
+      const float vj = __fadd_rn(__fmul_rn(a.b2, vv[j]), __fmul_rn(omb2, __fmul_rn(gj, gj)));
+      const float mh = __fdiv_rn(mj, bc1);
+      const float vh = __fdiv_rn(vj, bc2);
+      const float upd = __fdiv_rn(__fmul_rn(lr, mh), __fadd_rn(__fsqrt_rn(vh), a.eps));
+      mm[j] = mj;
+      vv[j] = vj;
+      pp[j] = __fsub_rn(pp[j], upd);
+    }
+    reinterpret_cast<f32x4*>(a.m)[i] = mm;
+    reinterpret_cast<f32x4*>(a.v)[i] = vv;
+    reinterpret_cast<f32x4*>(a.p)[i] = pp;
+  }
+}
+
 __global__ void min_f64_kernel(const double* __restrict__ x, int64_t n, double* out) {
   __shared__ double red[16];
   double m = INFINITY;
@@ -282,6 +381,22 @@ int launch_slab_reduce(const float* slab, int splits, int64_t count, float* out0
   slab_reduce_kernel<<<(unsigned)ceil_div(count, 64), 256, 0, st>>>(slab, splits, count, out0,
                                                                     split_at, out1, bias, ncols,
                                                                     relu);
+  ACME_LAUNCH_CHECK();
+  return ACME_OK;
+}
+
+int launch_grad_sumsq(const float* g, int64_t n4, int64_t group0_4, double* part, int nparts,
+                      int64_t* dev_step, hipStream_t st) {
+  ACME_CHECK_ARG(g && part && nparts >= 1, "bad argument");
+  grad_sumsq_kernel<<<(unsigned)nparts, 256, 0, st>>>(g, n4, group0_4, part, dev_step);
+  ACME_LAUNCH_CHECK();
+  return ACME_OK;
+}
+
+int launch_clip_adam(const ClipAdamArgs& a, hipStream_t st) {
+  ACME_CHECK_ARG(a.p && a.m && a.v && a.g && a.part && a.dev_step, "bad argument");
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(a.n4, 256), 1024);
+  clip_adam_kernel<<<std::max(grid, 1u), 256, 0, st>>>(a);
   ACME_LAUNCH_CHECK();
   return ACME_OK;
 }

@@ -1,0 +1,49 @@
+// AtariTorso (acme/tf/networks/atari.py:36-50: Conv2D(32, 8, 4) -> ReLU -> Conv2D(64, 4, 2)
+// -> ReLU -> Conv2D(64, 3, 1) -> ReLU -> Flatten, Sonnet SAME padding, NHWC) as implicit-GEMM
+// MFMA launches, shared by the DQN learner (DQNAtariNetwork) and the IMPALA learner
+// (IMPALAAtariNetwork's OAR embedding torso).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "conv.h"
+
+namespace acme {
+namespace torso {
+
+using G1 = conv::Geom<84, 84, 4, 21, 21, 32, 8, 8, 4, 2, 2>;
+using G2 = conv::Geom<21, 21, 32, 11, 11, 64, 4, 4, 2, 1, 1>;
+using G3 = conv::Geom<11, 11, 64, 11, 11, 64, 3, 3, 1, 1, 1>;
+constexpr int kFlat = 11 * 11 * 64;  // 7744 features per frame
+constexpr int kObsBytes = 84 * 84 * 4;
+constexpr int kX1 = G1::OPIX * G1::CO;  // conv1 output floats per frame (14112)
+
+struct Weights {
+  const float *w1, *b1, *w2, *b2, *w3, *b3;
+};
+struct Grads {
+  float *w1, *b1, *w2, *b2, *w3, *b3;
+};
+// Post-ReLU activations, [rows][...] NHWC: x1 [rows][kX1], x2 / x3 [rows][kFlat].
+struct Acts {
+  float *x1, *x2, *x3;
+};
+
+// Floats of split-K workspace the weight-gradient launches need.
+int64_t wgrad_slab_floats();
+
+// Forward over `rows` frames; frames [0, split) come from obs_a, the rest from obs_b
+// (uint8 scaled by 1/255 inside conv1 when u8, else float32).
+int forward(const Weights& w, bool u8, const void* obs_a, const void* obs_b, int split, int rows,
+            const Acts& a, hipStream_t st);
+
+// Backward over `rows` frames from dz3 = dLoss/d(conv3 pre-activation) [rows][kFlat]
+// (already masked by conv3's ReLU).  dz2 [rows][kFlat] and dz1 [rows][kX1] are scratch;
+// slab holds at least wgrad_slab_floats() floats.  No input gradient for the frames.
+int backward(const Weights& w, const Grads& g, bool u8, const void* obs, int rows, const Acts& a,
+             const float* dz3, float* dz2, float* dz1, float* slab, hipStream_t st);
+
+}  // namespace torso
+}  // namespace acme

@@ -1,0 +1,137 @@
+// AtariTorso forward / backward launches (see torso.h).  Tile shapes come from the
+// round-1 A/B sweep on MI355X (profiles/r01): 128x32 (4 waves 4x1) for conv1's 32 output
+// channels, 128x64 (2x2) for conv2/conv3 forward, split-K weight gradients reduced by one
+// deterministic slab pass, and the stride-2 conv2 input gradient as four sub-pixel GEMMs.
+#include "torso.h"
+
+#include <algorithm>
+
+#include "common.h"
+#include "gemm.h"
+#include "kernels.h"
+#include "profiler.h"
+
+namespace acme {
+namespace torso {
+
+using namespace acme::conv;
+using acme::gemm::launch_gemm;
+
+namespace {
+
+constexpr int kConv1WgradSplits = 256, kConv2WgradSplits = 64, kConv3WgradSplits = 64;
+
+inline int chunk_for(int K, int splits) {
+  int c = (int)ceil_div(K, splits);
+  return (int)ceil_div(c, 32) * 32;
+}
+
+#define TORSO_GEMM(name, BM, BN, WM, WN, prob, splits)                                        \
+  do {                                                                                        \
+    ACME_PROF(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0);   \
+    hipError_t _e = launch_gemm<BM, BN, WM, WN, 16>(prob, splits, st);                         \
+    if (_e != hipSuccess) {                                                                   \
+      set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
+      return ACME_ERR_HIP;                                                                    \
+    }                                                                                         \
+  } while (0)
+
+// Conv weight + bias gradient: split-K over the batch pixels into [splits][K+1][CO] slabs
+// (row K = bias partial from the GEMM's colsum hook), then one deterministic reduction
+// writes dW and db.
+template <class G, class In, int BM, int BN, int WM, int WN>
+int conv_wgrad(const typename In::T* x, const float* dz, int rows, int splits, float* slab,
+               float* dw, float* db, const char* name, const char* rname, hipStream_t st) {
+  ConvWgrad<G, In> p;
+  p.M = G::K; p.N = G::CO; p.K = rows * G::OPIX; p.k_chunk = chunk_for(p.K, splits);
+  p.x = x; p.dz = dz; p.slab = slab;
+  TORSO_GEMM(name, BM, BN, WM, WN, p, splits);
+  const int64_t count = (int64_t)(p.M + 1) * p.N;
+  ACME_PROF(rname, st, 0.0, 4.0 * (double)(splits + 1) * (double)count);
+  return launch_slab_reduce(slab, splits, count, dw, (int64_t)p.M * p.N, db, nullptr, 0, 0, st);
+}
+
+template <int PH, int PW>
+int conv2_dgrad_class(const float* w2, const float* x1, const float* dz2, float* dz1, int rows,
+                      hipStream_t st) {
+  using Sub = ConvDgradSub<G2, PH, PW>;
+  Sub p;
+  p.M = rows * Sub::NH * Sub::NW; p.N = G2::CI; p.K = Sub::KR; p.k_chunk = Sub::KR;
+  p.dz = dz2; p.w = w2; p.xprev = x1; p.dx = dz1;
+  TORSO_GEMM("conv2_dgrad", 256, 32, 4, 1, p, 1);
+  return ACME_OK;
+}
+
+}  // namespace
+
+int64_t wgrad_slab_floats() {
+  return std::max<int64_t>({(int64_t)kConv1WgradSplits * (G1::K + 1) * G1::CO,
+                            (int64_t)kConv2WgradSplits * (G2::K + 1) * G2::CO,
+                            (int64_t)kConv3WgradSplits * (G3::K + 1) * G3::CO});
+}
+
+int forward(const Weights& w, bool u8, const void* obs_a, const void* obs_b, int split, int rows,
+            const Acts& a, hipStream_t st) {
+  if (u8) {
+    ConvFwd<G1, InU8> p;
+    p.M = rows * G1::OPIX; p.N = G1::CO; p.K = G1::K; p.k_chunk = G1::K;
+    p.x = static_cast<const uint8_t*>(obs_a); p.x2 = static_cast<const uint8_t*>(obs_b);
+    p.split_b = split; p.w = w.w1; p.bias = w.b1; p.y = a.x1;
+    TORSO_GEMM("conv1_fwd", 128, 32, 4, 1, p, 1);
+  } else {
+    ConvFwd<G1, InF32> p;
+    p.M = rows * G1::OPIX; p.N = G1::CO; p.K = G1::K; p.k_chunk = G1::K;
+    p.x = static_cast<const float*>(obs_a); p.x2 = static_cast<const float*>(obs_b);
+    p.split_b = split; p.w = w.w1; p.bias = w.b1; p.y = a.x1;
+    TORSO_GEMM("conv1_fwd", 128, 32, 4, 1, p, 1);
+  }
+  {
+    ConvFwd<G2, InF32> p;
+    p.M = rows * G2::OPIX; p.N = G2::CO; p.K = G2::K; p.k_chunk = G2::K;
+    p.x = a.x1; p.x2 = a.x1; p.split_b = rows; p.w = w.w2; p.bias = w.b2; p.y = a.x2;
+    TORSO_GEMM("conv2_fwd", 128, 64, 2, 2, p, 1);
+  }
+  {
+    ConvFwd<G3, InF32> p;
+    p.M = rows * G3::OPIX; p.N = G3::CO; p.K = G3::K; p.k_chunk = G3::K;
+    p.x = a.x2; p.x2 = a.x2; p.split_b = rows; p.w = w.w3; p.bias = w.b3; p.y = a.x3;
+    TORSO_GEMM("conv3_fwd", 128, 64, 2, 2, p, 1);
+  }
+  return ACME_OK;
+}
+
+int backward(const Weights& w, const Grads& g, bool u8, const void* obs, int rows, const Acts& a,
+             const float* dz3, float* dz2, float* dz1, float* slab, hipStream_t st) {
+  int rc;
+  // conv3
+  if ((rc = conv_wgrad<G3, InF32, 64, 64, 2, 2>(a.x2, dz3, rows, kConv3WgradSplits, slab, g.w3,
+                                                g.b3, "conv3_wgrad", "conv3_wgrad_reduce", st)))
+    return rc;
+  {
+    ConvDgrad<G3> p;
+    p.M = rows * G3::IPIX; p.N = G3::CI; p.K = G3::KH * G3::KW * G3::CO; p.k_chunk = p.K;
+    p.dz = dz3; p.w = w.w3; p.xprev = a.x2; p.dx = dz2;
+    TORSO_GEMM("conv3_dgrad", 128, 64, 2, 2, p, 1);
+  }
+  // conv2
+  if ((rc = conv_wgrad<G2, InF32, 64, 64, 2, 2>(a.x1, dz2, rows, kConv2WgradSplits, slab, g.w2,
+                                                g.b2, "conv2_wgrad", "conv2_wgrad_reduce", st)))
+    return rc;
+  // Stride-2 input gradient as four dense sub-pixel GEMMs (one per parity class).
+  if ((rc = conv2_dgrad_class<0, 0>(w.w2, a.x1, dz2, dz1, rows, st)) ||
+      (rc = conv2_dgrad_class<0, 1>(w.w2, a.x1, dz2, dz1, rows, st)) ||
+      (rc = conv2_dgrad_class<1, 0>(w.w2, a.x1, dz2, dz1, rows, st)) ||
+      (rc = conv2_dgrad_class<1, 1>(w.w2, a.x1, dz2, dz1, rows, st)))
+    return rc;
+  // conv1 (no input gradient needed)
+  if (u8)
+    return conv_wgrad<G1, InU8, 128, 32, 4, 1>(static_cast<const uint8_t*>(obs), dz1, rows,
+                                               kConv1WgradSplits, slab, g.w1, g.b1,
+                                               "conv1_wgrad", "conv1_wgrad_reduce", st);
+  return conv_wgrad<G1, InF32, 128, 32, 4, 1>(static_cast<const float*>(obs), dz1, rows,
+                                              kConv1WgradSplits, slab, g.w1, g.b1, "conv1_wgrad",
+                                              "conv1_wgrad_reduce", st);
+}
+
+}  // namespace torso
+}  // namespace acme

@@ -451,3 +451,127 @@ class NativeD4PG:
         check(lib().acme_d4pg_policy(self._h, ptr(obs), rows, 1 if use_target else 0, ptr(a),
                                      stream_ptr(stream)), "d4pg policy")
         return a
+
+
+class NativeIMPALA:
+    """acme_impala learner + its flat buffers (no target network)."""
+
+    def __init__(self, *, num_actions: int, max_batch: int, max_sequence_length: int,
+                 torso: str = "atari", obs_dim: int = 0, lstm_size: int = 256,
+                 head_size: int = 256, discount: float = 0.99, entropy_cost: float = 0.0,
+                 baseline_cost: float = 1.0, max_abs_reward: Optional[float] = None,
+                 max_gradient_norm: Optional[float] = None, learning_rate: float = 1e-3,
+                 adam_beta1: float = 0.9, adam_beta2: float = 0.999, adam_epsilon: float = 1e-8,
+                 device=None):
+        _lib.require_gpu()
+        cfg = _lib.IMPALAConfig()
+        cfg.torso = _lib.IMPALA_TORSO_ATARI if torso == "atari" else _lib.IMPALA_TORSO_FLAT
+        cfg.obs_dim, cfg.num_actions = int(obs_dim), int(num_actions)
+        cfg.max_batch, cfg.max_sequence_length = int(max_batch), int(max_sequence_length)
+        cfg.lstm_size, cfg.head_size = int(lstm_size), int(head_size)
+        cfg.discount, cfg.entropy_cost, cfg.baseline_cost = discount, entropy_cost, baseline_cost
+        # learning.py:67-71: None -> no reward clipping, gradient norm 1e10.
+        cfg.max_abs_reward = float("inf") if max_abs_reward is None else max_abs_reward
+        cfg.max_gradient_norm = 1e10 if max_gradient_norm is None else max_gradient_norm
+        cfg.learning_rate = learning_rate
+        cfg.adam_beta1, cfg.adam_beta2, cfg.adam_epsilon = adam_beta1, adam_beta2, adam_epsilon
+        self.cfg = cfg
+        self.torso, self.obs_dim = torso, int(obs_dim)
+        self.num_actions, self.lstm_size = int(num_actions), int(lstm_size)
+        self.max_batch, self.max_sequence_length = int(max_batch), int(max_sequence_length)
+        self.device = torch.device(device or "cuda")
+        h = ctypes.c_void_p()
+        L = lib()
+        with torch.cuda.device(self.device):
+            check(L.acme_impala_create(ctypes.byref(cfg), ctypes.byref(h)), "impala create")
+        self._h = h
+        self.flat_size = int(L.acme_impala_flat_size(h))
+        self.tensors: List[Tuple[str, int, Tuple[int, ...]]] = []
+        for i in range(L.acme_impala_num_tensors(h)):
+            off, numel, nd = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int32()
+            shape = (ctypes.c_int64 * 4)()
+            name = ctypes.c_char_p()
+            check(L.acme_impala_tensor_info(h, i, ctypes.byref(off), ctypes.byref(numel),
+                                            ctypes.byref(nd), shape, ctypes.byref(name)))
+            self.tensors.append((name.value.decode(), int(off.value),
+                                 tuple(int(shape[k]) for k in range(nd.value))))
+        z = lambda: torch.zeros(self.flat_size, dtype=torch.float32, device=self.device)  # noqa
+        self.params, self.grads, self.m, self.v = z(), z(), z(), z()
+        check(L.acme_impala_bind(h, ptr(self.params), ptr(self.grads), ptr(self.m),
+                                 ptr(self.v)), "impala bind")
+        self.metrics = torch.zeros(4, dtype=torch.float32, device=self.device)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                lib().acme_impala_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    views = NativeDQN.views
+    get_params = NativeDQN.get_params
+
+    def set_params(self, params: Dict[str, np.ndarray]) -> None:
+        for name, t in self.views(self.params).items():
+            t.copy_(torch.as_tensor(np.asarray(params[name], np.float32)).view(t.shape))
+
+    @property
+    def num_steps(self) -> int:
+        return int(lib().acme_impala_num_steps(self._h))
+
+    @num_steps.setter
+    def num_steps(self, n: int) -> None:
+        check(lib().acme_impala_set_num_steps(self._h, int(n)))
+
+    def debug_buffer(self, name: str) -> np.ndarray:
+        p, n = ctypes.c_void_p(), ctypes.c_int64()
+        check(lib().acme_impala_debug_buffer(self._h, name.encode(), ctypes.byref(p),
+                                             ctypes.byref(n)))
+        return _device_array(p.value, n.value, np.float32, self.device).cpu().numpy().view(
+            np.float32).copy()
+
+    def step(self, observation, prev_action, prev_reward, action, reward, discount,
+             behaviour_logits, h0, c0, stream=None):
+        """Batch-major [B, T, ...] device tensors; h0 / c0 are [B, H] views (any row stride
+        that is a multiple of 4 floats, e.g. core_state[:, 0] of a [B, T, H] tensor)."""
+        B, T = int(action.shape[0]), int(action.shape[1])
+        want = torch.uint8 if self.torso == "atari" else torch.float32
+        checks = (("observation", observation, want), ("prev_action", prev_action, torch.int32),
+                  ("prev_reward", prev_reward, torch.float32), ("action", action, torch.int32),
+                  ("reward", reward, torch.float32), ("discount", discount, torch.float32),
+                  ("behaviour_logits", behaviour_logits, torch.float32))
+        for name, t, dt in checks:
+            if not (isinstance(t, torch.Tensor) and t.is_cuda and t.is_contiguous()
+                    and t.dtype == dt):
+                raise ValueError(f"{name} must be a contiguous {dt} device tensor")
+            if tuple(t.shape[:2]) != (B, T):
+                raise ValueError(f"{name} has shape {tuple(t.shape)}, expected [{B}, {T}, ...]")
+        for name, t in (("h0", h0), ("c0", c0)):
+            if t.dtype != torch.float32 or t.shape != (B, self.lstm_size) or t.stride(1) != 1:
+                raise ValueError(f"{name} must be float32 [{B}, {self.lstm_size}] with unit "
+                                 "inner stride")
+        if h0.stride(0) != c0.stride(0):
+            raise ValueError("h0 and c0 must share a row stride")
+        b = _lib.SequenceBatch()
+        b.observation, b.prev_action, b.prev_reward = ptr(observation), ptr(prev_action), ptr(prev_reward)
+        b.action, b.reward, b.discount = ptr(action), ptr(reward), ptr(discount)
+        b.behaviour_logits, b.h0, b.c0 = ptr(behaviour_logits), ptr(h0), ptr(c0)
+        b.state_stride, b.batch, b.sequence_length = int(h0.stride(0)), B, T
+        check(lib().acme_impala_step(self._h, ctypes.byref(b), ptr(self.metrics),
+                                     stream_ptr(stream)), "impala step")
+
+    def policy_step(self, obs, prev_action, prev_reward, h, c, stream=None):
+        """One network step for `rows` actors; returns (logits, values, h, c)."""
+        rows = int(prev_action.shape[0])
+        A, H = self.num_actions, self.lstm_size
+        out = [torch.empty(rows, A, dtype=torch.float32, device=self.device),
+               torch.empty(rows, dtype=torch.float32, device=self.device),
+               torch.empty(rows, H, dtype=torch.float32, device=self.device),
+               torch.empty(rows, H, dtype=torch.float32, device=self.device)]
+        check(lib().acme_impala_policy_step(
+            self._h, ptr(obs.contiguous()), ptr(prev_action.contiguous()),
+            ptr(prev_reward.contiguous()), ptr(h.contiguous()), ptr(c.contiguous()), rows,
+            *[ptr(o) for o in out], stream_ptr(stream)), "impala policy_step")
+        return tuple(out)

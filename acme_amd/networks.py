@@ -15,7 +15,7 @@ value/advantage MLP variables.
 from __future__ import annotations
 
 import dataclasses
-from typing import Dict, List, Sequence, Tuple
+from typing import Dict, List, NamedTuple, Sequence, Tuple
 
 import numpy as np
 
@@ -266,3 +266,75 @@ def make_d4pg_networks(obs_dim: int, action_spec, policy_layer_sizes=(256, 256, 
                                        num_atoms),
         "observation": "identity",
     }
+
+
+# ------------------------------------------------------------------ IMPALA (Atari)
+
+
+class LSTMState(NamedTuple):
+    """snt.LSTMState: the core state carried by the IMPALA actor and stored in extras."""
+    hidden: np.ndarray
+    cell: np.ndarray
+
+
+@dataclasses.dataclass(frozen=True)
+class IMPALAAtariNetwork:
+    """IMPALAAtariNetwork (acme/tf/networks/atari.py:115-144): OAREmbedding(AtariTorso) ->
+    snt.LSTM(lstm_size) -> Linear(head_size) -> ReLU -> PolicyValueHead(num_actions).
+    torso="flat" replaces the AtariTorso by the identity over a float observation vector
+    of obs_dim features (small configurations and tests)."""
+
+    num_actions: int
+    lstm_size: int = 256
+    head_size: int = 256
+    torso: str = "atari"
+    obs_dim: int = 0
+
+    @property
+    def feat(self) -> int:
+        return 7744 if self.torso == "atari" else self.obs_dim
+
+    @property
+    def obs_dtype(self) -> str:
+        return "uint8" if self.torso == "atari" else "float32"
+
+    def tensor_shapes(self):
+        H, H2, A = self.lstm_size, self.head_size, self.num_actions
+        pre = "impala_atari_network"
+        out = []
+        if self.torso == "atari":
+            out += [(f"{pre}/atari_torso/conv2_d/w", (8, 8, 4, 32)),
+                    (f"{pre}/atari_torso/conv2_d/b", (32,)),
+                    (f"{pre}/atari_torso/conv2_d_1/w", (4, 4, 32, 64)),
+                    (f"{pre}/atari_torso/conv2_d_1/b", (64,)),
+                    (f"{pre}/atari_torso/conv2_d_2/w", (3, 3, 64, 64)),
+                    (f"{pre}/atari_torso/conv2_d_2/b", (64,))]
+        D = self.feat + A + 1
+        out += [(f"{pre}/lstm/w_i", (D, 4 * H)), (f"{pre}/lstm/w_h", (H, 4 * H)),
+                (f"{pre}/lstm/b", (4 * H,)), (f"{pre}/linear/w", (H, H2)),
+                (f"{pre}/linear/b", (H2,)), (f"{pre}/policy_value/w", (H2, A + 1)),
+                (f"{pre}/policy_value/b", (A + 1,))]
+        return out
+
+    def init(self, seed: int = 0) -> Dict[str, np.ndarray]:
+        """Sonnet defaults: conv / linear TruncatedNormal(1/sqrt(fan_in)), zero biases;
+        snt.LSTM w_i ~ TruncatedNormal(1/sqrt(input)), w_h ~ TruncatedNormal(1/sqrt(H)),
+        bias zero with forget_bias 1.0 folded into the forget-gate slice."""
+        rng = np.random.default_rng(seed)
+        out = {}
+        H = self.lstm_size
+        for name, shape in self.tensor_shapes():
+            if name.endswith("lstm/b"):
+                b = np.zeros(shape, np.float32)
+                b[H:2 * H] = 1.0
+                out[name] = b
+            elif name.endswith("/b"):
+                out[name] = np.zeros(shape, np.float32)
+            else:
+                fan_in = int(np.prod(shape[:-1]))
+                out[name] = truncated_normal(rng, shape, 1.0 / np.sqrt(fan_in))
+        return out
+
+    def initial_state(self, batch_size: int) -> LSTMState:
+        z = np.zeros((batch_size, self.lstm_size), np.float32)
+        return LSTMState(z, z.copy())

@@ -1,0 +1,63 @@
+"""ObservationActionRewardWrapper — drop-in for
+acme/wrappers/observation_action_reward.py:27-83: observations become
+OAR(observation, previous action, previous reward), the input of IMPALAAtariNetwork's
+OAR embedding (acme/tf/networks/embedding.py:26-45)."""
+
+from __future__ import annotations
+
+from typing import Any, NamedTuple
+
+import numpy as np
+
+from acme_amd import dm_env, specs
+
+
+class OAR(NamedTuple):
+    observation: Any
+    action: Any
+    reward: Any
+
+
+class ObservationActionRewardWrapper:
+    def __init__(self, environment):
+        self._environment = environment
+        self._prev_action = None
+        self._prev_reward = None
+
+    def reset(self) -> dm_env.TimeStep:
+        ts = self._environment.reset()
+        self._prev_action = np.zeros((), self._environment.action_spec().dtype)
+        self._prev_reward = np.zeros((), self._environment.reward_spec().dtype)
+        return ts._replace(observation=OAR(ts.observation, self._prev_action, self._prev_reward))
+
+    def step(self, action) -> dm_env.TimeStep:
+        ts = self._environment.step(action)
+        self._prev_action = np.asarray(action, self._environment.action_spec().dtype)
+        self._prev_reward = np.asarray(ts.reward if ts.reward is not None else 0,
+                                       self._environment.reward_spec().dtype)
+        return ts._replace(observation=OAR(ts.observation, self._prev_action, self._prev_reward))
+
+    def observation_spec(self):
+        return OAR(observation=self._environment.observation_spec(),
+                   action=self._environment.action_spec(),
+                   reward=self._environment.reward_spec())
+
+    def action_spec(self):
+        return self._environment.action_spec()
+
+    def reward_spec(self):
+        return self._environment.reward_spec()
+
+    def discount_spec(self):
+        return self._environment.discount_spec()
+
+    def close(self):
+        close = getattr(self._environment, "close", None)
+        if close:
+            close()
+
+    def __getattr__(self, name):
+        return getattr(self._environment, name)
+
+
+del specs  # imported for the type vocabulary only

@@ -268,6 +268,71 @@ int acme_d4pg_set_num_steps(acme_d4pg* l, int64_t n);
 int acme_d4pg_debug_buffer(const acme_d4pg* l, const char* name, const float** out,
                            int64_t* count);
 
+/* ---------------------------------------------------------------- IMPALA -- */
+/* Replaces IMPALALearner._step (acme/agents/tf/impala/learning.py:97-169) with
+ * IMPALAAtariNetwork (acme/tf/networks/atari.py:115-144): OAREmbedding(AtariTorso) ->
+ * snt.LSTM(lstm_size) -> Linear(head_size) -> ReLU -> PolicyValueHead(num_actions).
+ * The policy and value layers are one fused [head_size, A + 1] tensor (column A = value). */
+#define ACME_IMPALA_TORSO_ATARI 0 /* uint8 [84, 84, 4] frames, scaled 1/255 inside conv1 */
+#define ACME_IMPALA_TORSO_FLAT 1  /* float [obs_dim] vector used as the torso output */
+
+typedef struct acme_impala acme_impala;
+
+typedef struct acme_impala_config {
+  int32_t torso;
+  int32_t obs_dim;              /* FLAT torso only */
+  int32_t num_actions;          /* <= 63 */
+  int32_t max_batch;            /* sequences per step (B) */
+  int32_t max_sequence_length;  /* T */
+  int32_t lstm_size;            /* multiple of 8, max_batch * (lstm_size + 32) <= 16384 */
+  int32_t head_size;            /* multiple of 4 */
+  float discount, entropy_cost, baseline_cost;
+  float max_abs_reward;         /* INFINITY = no reward clipping (learning.py:70-71) */
+  float max_gradient_norm;      /* 1e10 = effectively none (learning.py:72-73) */
+  float learning_rate, adam_beta1, adam_beta2, adam_epsilon;
+} acme_impala_config;
+
+/* One batch of sequences, batch-major [B, T, ...] as the dataset yields them. */
+typedef struct acme_sequence_batch {
+  const void* observation;      /* [B, T, 84, 84, 4] u8 or [B, T, obs_dim] f32 */
+  const int32_t* prev_action;   /* [B, T] OAR observation: previous action */
+  const float* prev_reward;     /* [B, T] OAR observation: previous reward */
+  const int32_t* action;        /* [B, T] */
+  const float* reward;          /* [B, T] */
+  const float* discount;        /* [B, T] */
+  const float* behaviour_logits;/* [B, T, A] extras['logits'] */
+  const float* h0;              /* core_state hidden at t = 0: row b at h0 + b * state_stride */
+  const float* c0;              /* core_state cell at t = 0 */
+  int64_t state_stride;         /* floats between consecutive rows of h0 / c0 */
+  int64_t batch;                /* B <= max_batch */
+  int64_t sequence_length;      /* T, 2 <= T <= max_sequence_length */
+} acme_sequence_batch;
+
+int acme_impala_create(const acme_impala_config* cfg, acme_impala** out);
+int acme_impala_destroy(acme_impala* l);
+int64_t acme_impala_flat_size(const acme_impala* l);
+int32_t acme_impala_num_tensors(const acme_impala* l);
+int acme_impala_tensor_info(const acme_impala* l, int32_t i, int64_t* offset, int64_t* numel,
+                            int32_t* ndim, int64_t* shape4, const char** name);
+int acme_impala_bind(acme_impala* l, float* params, float* grads, float* adam_m, float* adam_v);
+/* One SGD step; metrics (device, optional) = [loss, critic_loss, entropy_loss,
+ * policy_gradient_loss] as logged by learning.py:162-167. */
+int acme_impala_step(acme_impala* l, const acme_sequence_batch* batch, float* metrics,
+                     void* stream);
+/* One network step for `rows` independent actors (IMPALAActor.select_action): inputs
+ * obs [rows, ...], prev_action / prev_reward [rows], state h / c [rows, lstm_size];
+ * outputs logits [rows, A], values [rows], next state h_out / c_out. */
+int acme_impala_policy_step(acme_impala* l, const void* obs, const int32_t* prev_action,
+                            const float* prev_reward, const float* h, const float* c,
+                            int64_t rows, float* logits, float* values, float* h_out,
+                            float* c_out, void* stream);
+int64_t acme_impala_num_steps(const acme_impala* l);
+int acme_impala_set_num_steps(acme_impala* l, int64_t n);
+/* "logits" "values" [B*T] batch-major rows, "vs" "pg_adv" [(T-1)*B] time-major,
+ * "h" [B*T, H], "dpv" [B*T, A+1], "grad_norm" [1]. */
+int acme_impala_debug_buffer(const acme_impala* l, const char* name, const float** out,
+                             int64_t* count);
+
 /* ----------------------------------------------------------- elementwise ops -- */
 
 /* ------------------------------------------------------------- profiling -- */

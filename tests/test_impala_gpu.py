@@ -1,0 +1,152 @@
+"""HIP IMPALA learner step vs the numpy oracle (oracle/impala_oracle.py, float64).
+
+Reference: IMPALALearner._step (acme/agents/tf/impala/learning.py:97-169).
+Tolerances (fp32 kernels against an fp64 restatement):
+  losses / logits / values / vs / pg advantages: rtol 1e-5 (+ 2e-6 of the tensor's scale)
+  gradients: per tensor |g - g_ref| <= 1e-4 |g_ref| + 2e-5 max|g_ref|; the Atari torso's
+      conv gradients (ReLU branch decisions at fp32 rounding of 0 can differ) by relative
+      Frobenius error <= 1e-4
+  Adam-updated params: every element within 2 lr, 99% within 1e-5 relative.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import impala_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _native(cfg, B, T, **kw):
+    from acme_amd.native import NativeIMPALA
+    return NativeIMPALA(num_actions=cfg.num_actions, max_batch=B, max_sequence_length=T,
+                        torso=cfg.torso, obs_dim=cfg.obs_dim, lstm_size=cfg.lstm_size,
+                        head_size=cfg.head_size, discount=cfg.discount,
+                        entropy_cost=cfg.entropy_cost, baseline_cost=cfg.baseline_cost,
+                        learning_rate=cfg.learning_rate, **kw)
+
+
+def _params(cfg, seed):
+    rng = np.random.default_rng(seed)
+    out = {}
+    for n, s in O.tensor_shapes(cfg):
+        fan = np.prod(s[:-1]) if len(s) > 1 else s[0]
+        out[n] = (rng.standard_normal(s) / np.sqrt(fan)).astype(np.float32)
+        if n.endswith("/b"):
+            out[n] = (0.1 * rng.standard_normal(s)).astype(np.float32)
+    return out
+
+
+def _batch(cfg, B, T, seed):
+    rng = np.random.default_rng(seed)
+    A, H = cfg.num_actions, cfg.lstm_size
+    if cfg.torso == "atari":
+        obs = rng.integers(0, 256, (B, T, 84, 84, 4), dtype=np.uint8)
+    else:
+        obs = rng.standard_normal((B, T, cfg.obs_dim)).astype(np.float32)
+    state = (0.5 * rng.standard_normal((B, T, 2, H))).astype(np.float32)
+    return dict(obs=obs, prev_action=rng.integers(0, A, (B, T)).astype(np.int32),
+                prev_reward=rng.standard_normal((B, T)).astype(np.float32),
+                action=rng.integers(0, A, (B, T)).astype(np.int32),
+                reward=(2 * rng.standard_normal((B, T))).astype(np.float32),
+                discount=np.where(rng.random((B, T)) < 0.1, 0.0, 1.0).astype(np.float32),
+                behaviour_logits=rng.standard_normal((B, T, A)).astype(np.float32),
+                state=state, h0=state[:, 0, 0].copy(), c0=state[:, 0, 1].copy())
+
+
+def _run(n, b):
+    d = lambda k: torch.as_tensor(b[k]).cuda().contiguous()  # noqa: E731
+    st = torch.as_tensor(b["state"]).cuda()
+    # core_state[:, 0] views of a [B, T, 2, H] extras tensor: row stride T * 2 * H.
+    n.step(d("obs"), d("prev_action"), d("prev_reward"), d("action"), d("reward"),
+           d("discount"), d("behaviour_logits"), st[:, 0, 0], st[:, 0, 1])
+    torch.cuda.synchronize()
+
+
+def _close(got, ref, rtol=1e-5, floor=2e-6, name=""):
+    ref = np.asarray(ref, np.float64)
+    got = np.asarray(got, np.float64).reshape(ref.shape)
+    scale = max(float(np.abs(ref).max()), 1e-30)
+    np.testing.assert_allclose(got, ref, rtol=rtol, atol=floor * scale, err_msg=name)
+
+
+def _check_grads(n, g_ref, frob_only=()):
+    g = n.get_params("grads")
+    for name, ref in g_ref.items():
+        got = g[name].reshape(ref.shape).astype(np.float64)
+        if any(name.startswith(p) for p in frob_only):
+            rel = np.linalg.norm(got - ref) / max(np.linalg.norm(ref), 1e-30)
+            assert rel <= 1e-4, (name, rel)
+            continue
+        scale = np.abs(ref).max()
+        err = np.abs(got - ref)
+        assert (err <= 1e-4 * np.abs(ref) + 2e-5 * scale + 1e-30).all(), \
+            (name, float(err.max()), float(scale))
+
+
+def _check_params(got, ref, lr):
+    for k, r in ref.items():
+        gk = got[k].reshape(r.shape).astype(np.float64)
+        err = np.abs(gk - r)
+        assert err.max() <= 2 * lr + 1e-6, (k, float(err.max()))
+        assert np.mean(err <= 1e-5 * np.abs(r) + 1e-7) >= 0.99, k
+
+
+def _compare(cfg, n, params, b, frob_only=()):
+    z = {k: np.zeros_like(v) for k, v in params.items()}
+    ref, raw, st = O.impala_step(cfg, dict(params=params, m=z, v=dict(z), num_steps=0), b)
+    B, T = b["action"].shape
+    A = cfg.num_actions
+    m = n.metrics.cpu().numpy()
+    _close(m[0], ref["loss"], name="loss")
+    _close(m[1], ref["critic_loss"], name="critic_loss")
+    _close(m[2], ref["entropy_loss"], name="entropy_loss")
+    _close(m[3], ref["policy_gradient_loss"], name="pg_loss")
+    pv = n.debug_buffer("pv")[:B * T * (A + 1)].reshape(B, T, A + 1)
+    _close(pv[..., :A], ref["logits"], name="logits")
+    _close(pv[..., A], ref["values"], name="values")
+    _close(n.debug_buffer("vs")[:(T - 1) * B].reshape(T - 1, B), ref["vs"], name="vs")
+    _close(n.debug_buffer("pg_adv")[:(T - 1) * B].reshape(T - 1, B), ref["pg_advantages"],
+           name="pg_adv")
+    _check_grads(n, raw, frob_only)
+    _check_params(n.get_params("params"), st["params"], cfg.learning_rate)
+
+
+@pytest.mark.parametrize("B,T,H", [(4, 6, 16), (16, 20, 256), (3, 2, 8)])
+def test_flat_torso_step_matches_oracle(B, T, H):
+    cfg = O.IMPALAConfig(num_actions=5, torso="flat", obs_dim=12, lstm_size=H,
+                         head_size=max(H // 2, 4) // 4 * 4, entropy_cost=0.01, baseline_cost=0.5)
+    n = _native(cfg, B, T)
+    params = _params(cfg, 1)
+    n.set_params(params)
+    b = _batch(cfg, B, T, 2)
+    _run(n, b)
+    _compare(cfg, n, params, b)
+
+
+def test_atari_torso_step_matches_oracle():
+    """IMPALAAtariNetwork at full width (LSTM 256, head 256, 18 actions) on B=2, T=5."""
+    cfg = O.IMPALAConfig(num_actions=18, torso="atari", entropy_cost=0.01, baseline_cost=0.5)
+    n = _native(cfg, 2, 5)
+    params = _params(cfg, 3)
+    n.set_params(params)
+    b = _batch(cfg, 2, 5, 4)
+    _run(n, b)
+    _compare(cfg, n, params, b, frob_only=(f"{O.PREFIX}/atari_torso",))
+
+
+def test_policy_step_matches_unroll():
+    cfg = O.IMPALAConfig(num_actions=6, torso="flat", obs_dim=10, lstm_size=32, head_size=16)
+    n = _native(cfg, 8, 4)
+    params = _params(cfg, 5)
+    n.set_params(params)
+    b = _batch(cfg, 8, 2, 6)
+    logits, values, cache = O.forward(cfg, params, b, np.float64)
+    d = lambda x: torch.as_tensor(np.ascontiguousarray(x)).cuda()  # noqa: E731
+    lg, v, h, c = n.policy_step(d(b["obs"][:, 0]), d(b["prev_action"][:, 0]),
+                                d(b["prev_reward"][:, 0]), d(b["h0"]), d(b["c0"]))
+    _close(lg.cpu().numpy(), logits[:, 0], name="logits")
+    _close(v.cpu().numpy(), values[:, 0], name="values")
+    _close(h.cpu().numpy(), cache["hs"][:, 0], name="h")
+    _close(c.cpu().numpy(), cache["cs"][:, 0], name="c")
