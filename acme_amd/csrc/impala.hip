@@ -63,7 +63,7 @@ struct acme_impala {
   float* slab = nullptr;
   float *gx = nullptr, *gates = nullptr, *h = nullptr, *c = nullptr, *hh = nullptr, *pv = nullptr;
   float *dpv = nullptr, *dhh = nullptr, *dh = nullptr, *dgates = nullptr, *dc = nullptr;
-  float *vs = nullptr, *pg_adv = nullptr;
+  float *vs = nullptr, *pg_adv = nullptr, *lrho = nullptr, *lpa = nullptr, *ent = nullptr;
   double* norm_part = nullptr;
   int64_t* dev_step = nullptr;
   float* metrics_tmp = nullptr;
@@ -242,39 +242,81 @@ struct HPrevWgrad {
 };
 
 // ------------------------------------------------------------------ LSTM cell kernels
-// Forward step t for all B sequences, kUnits units per block: z = gx + h_prev @ W_h
-// (gate columns q*H + u), then the snt.LSTM cell update.  h_prev row b lives at
-// hp + b * hp_stride (the core state for t = 0, the previous step's h otherwise).
+// kUnits units per block (4 * kUnits = 32 gate columns q * H + u).  The recurrent
+// mat-vecs are spread over 256 threads as 32 columns (or units) x 8 (or 32) k-slices with
+// 16 batch rows per pass in registers, so every W_h element read feeds 16 FMAs and the
+// k-slices are summed once through LDS.
+constexpr int kRowChunk = 16;
+
+// Forward step t for all B sequences: z = gx + h_prev @ W_h, then the snt.LSTM cell
+// update.  h_prev row b lives at hp + b * hp_stride (the core state for t = 0, the
+// previous step's h otherwise).  kFwdUnits units per block (16 gate columns); the
+// block's W_h columns are staged through LDS in k-chunks with float4 loads.
+constexpr int kFwdUnits = 4;
+
 __global__ void __launch_bounds__(256) lstm_fwd_step_kernel(
     const float* __restrict__ gx, const float* __restrict__ wh, const float* __restrict__ hp,
     int64_t hp_stride, const float* __restrict__ cp, int64_t cp_stride, int B, int T, int t, int H,
     float* __restrict__ gates, float* __restrict__ h_out, float* __restrict__ c_out) {
-  extern __shared__ float smem[];
-  float* hs = smem;                 // [B][H]
-  float* zs = smem + (size_t)B * H;  // [B][4 * kUnits]
-  const int u0 = blockIdx.x * kUnits;
-  for (int i = threadIdx.x; i < B * H; i += blockDim.x) {
-    const int b = i / H, k = i - b * H;
-    hs[i] = hp[(size_t)b * hp_stride + k];
+  constexpr int NC = 4 * kFwdUnits;    // gate columns per block (4 segments of kFwdUnits)
+  constexpr int KS = 256 / NC;         // k-slices
+  static_assert(kRowChunk * NC == 256, "one reduction output per thread");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* hs = smem;                            // [B][H]
+  float* ws = hs + (size_t)B * H;              // [H][NC]
+  float* red = ws + (size_t)H * NC;            // [KS][kRowChunk][NC]
+  float* zs = red + KS * kRowChunk * NC;       // [B][NC]
+  const int u0 = blockIdx.x * kFwdUnits;
+  // Every global load of the step is issued up front (the cell state this thread updates,
+  // h_prev, the block's W_h columns as float4 segments), so the step pays one latency.
+  const bool cell_thread = (int)threadIdx.x < B * kFwdUnits;  // B <= 64 for one pass
+  const float cprev_pre = cell_thread ? cp[(size_t)(threadIdx.x / kFwdUnits) * cp_stride + u0 +
+                                           threadIdx.x % kFwdUnits]
+                                      : 0.f;
+  for (int e = threadIdx.x; e < B * H / 4; e += blockDim.x) {
+    const int b = e / (H / 4), k = 4 * (e % (H / 4));
+    *reinterpret_cast<f32x4*>(hs + (size_t)b * H + k) =
+        *reinterpret_cast<const f32x4*>(hp + (size_t)b * hp_stride + k);
+  }
+  for (int e = threadIdx.x; e < H * 4; e += blockDim.x) {
+    const int k = e / 4, q = e % 4;
+    *reinterpret_cast<f32x4*>(ws + (size_t)k * NC + q * kFwdUnits) =
+        *reinterpret_cast<const f32x4*>(wh + (size_t)k * 4 * H + q * H + u0);
   }
   __syncthreads();
-  constexpr int NC = 4 * kUnits;
-  for (int o = threadIdx.x; o < B * NC; o += blockDim.x) {
-    const int b = o / NC, c = o - b * NC;
-    const int col = (c / kUnits) * H + u0 + (c % kUnits);
-    const int row = b * T + t;
-    float acc = 0.f;
-    const float* hrow = hs + (size_t)b * H;
-    for (int k = 0; k < H; ++k) acc = fmaf(hrow[k], wh[(size_t)k * 4 * H + col], acc);
-    zs[o] = gx[(size_t)row * 4 * H + col] + acc;
+  const int c = threadIdx.x % NC, sl = threadIdx.x / NC;
+  for (int b0 = 0; b0 < B; b0 += kRowChunk) {
+    // The gx term of this thread's reduction output, loaded before the mat-vec.
+    const int oi = threadIdx.x / NC, occ = threadIdx.x % NC, ob = b0 + oi;
+    const float gxv = ob < B ? gx[((size_t)ob * T + t) * 4 * H + (occ / kFwdUnits) * H + u0 +
+                                  (occ % kFwdUnits)]
+                             : 0.f;
+    float acc[kRowChunk];
+#pragma unroll
+    for (int i = 0; i < kRowChunk; ++i) acc[i] = 0.f;
+    for (int k = sl; k < H; k += KS) {
+      const float w = ws[k * NC + c];
+#pragma unroll
+      for (int i = 0; i < kRowChunk; ++i)
+        if (b0 + i < B) acc[i] = fmaf(hs[(size_t)(b0 + i) * H + k], w, acc[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < kRowChunk; ++i) red[(sl * kRowChunk + i) * NC + c] = acc[i];
+    __syncthreads();
+    if (ob < B) {  // 256 threads = kRowChunk rows x NC columns
+      float z = 0.f;
+      for (int s2 = 0; s2 < KS; ++s2) z += red[(s2 * kRowChunk + oi) * NC + occ];
+      zs[ob * NC + occ] = gxv + z;
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  for (int o = threadIdx.x; o < B * kUnits; o += blockDim.x) {
-    const int b = o / kUnits, u = o - b * kUnits, j = u0 + u;
+  for (int o = threadIdx.x; o < B * kFwdUnits; o += blockDim.x) {
+    const int b = o / kFwdUnits, u = o - b * kFwdUnits, j = u0 + u;
     const float* z = zs + (size_t)b * NC;
-    const float ig = sigmoidf(z[u]), fg = sigmoidf(z[kUnits + u]);
-    const float gg = tanhf(z[2 * kUnits + u]), og = sigmoidf(z[3 * kUnits + u]);
-    const float cprev = cp[(size_t)b * cp_stride + j];
+    const float ig = sigmoidf(z[u]), fg = sigmoidf(z[kFwdUnits + u]);
+    const float gg = tanhf(z[2 * kFwdUnits + u]), og = sigmoidf(z[3 * kFwdUnits + u]);
+    const float cprev = o == (int)threadIdx.x && cell_thread ? cprev_pre
+                                                             : cp[(size_t)b * cp_stride + j];
     const float cn = fg * cprev + ig * gg;
     const float hn = og * tanhf(cn);
     const size_t row = (size_t)b * T + t;
@@ -287,167 +329,179 @@ __global__ void __launch_bounds__(256) lstm_fwd_step_kernel(
   }
 }
 
+size_t lstm_fwd_smem(int B, int H) {
+  constexpr int NC = 4 * kFwdUnits;
+  return ((size_t)B * H + (size_t)H * NC + (size_t)(256 / NC) * kRowChunk * NC +
+          (size_t)B * NC) * sizeof(float);
+}
+
 // Backward step t: dh = dh_head[t] + dgates[t+1] @ W_h^T (t < T-1), dc = dc_carry +
 // dh o (1 - tanh^2 c), gate gradients (pre-activation), dc_carry <- dc f.
 __global__ void __launch_bounds__(256) lstm_bwd_step_kernel(
     const float* __restrict__ dh_head, const float* __restrict__ wh, const float* __restrict__ gates,
     const float* __restrict__ c_all, const float* __restrict__ c0, int64_t c0_stride,
     float* __restrict__ dc_carry, float* __restrict__ dgates, int B, int T, int t, int H) {
-  __shared__ float part[256];
+  constexpr int KS = 256 / kUnits;  // 32 k-slices: consecutive threads read consecutive k
+  constexpr int KC = 256;           // k-chunk staged in LDS per pass
+  __shared__ float red[kUnits][kRowChunk][KS + 1];
+  __shared__ __attribute__((aligned(16))) float ds[kRowChunk][KC];
   const int u0 = blockIdx.x * kUnits;
-  const int nout = B * kUnits;
-  for (int ob = 0; ob < nout; ob += 256) {
-    const int chunk = nout - ob < 256 ? nout - ob : 256;
-    const int ks = 256 / chunk;  // k slices per output (>= 1)
-    const int o = ob + (int)threadIdx.x % chunk, sl = (int)threadIdx.x / chunk;
-    float acc = 0.f;
-    if (t + 1 < T && sl < ks) {
-      const int b = o / kUnits, j = u0 + o % kUnits;
-      const float* dn = dgates + ((size_t)b * T + t + 1) * 4 * H;
-      const float* w = wh + (size_t)j * 4 * H;
-      for (int k = sl; k < 4 * H; k += ks) acc = fmaf(dn[k], w[k], acc);
+  const int sl = threadIdx.x % KS, u = threadIdx.x / KS;
+  const float* w = wh + (size_t)(u0 + u) * 4 * H;
+  for (int b0 = 0; b0 < B; b0 += kRowChunk) {
+    float acc[kRowChunk];
+#pragma unroll
+    for (int i = 0; i < kRowChunk; ++i) acc[i] = 0.f;
+    if (t + 1 < T) {
+      for (int kc = 0; kc < 4 * H; kc += KC) {
+        // Stage dgates[t+1][b0 .. b0+15][kc .. kc+255] with float4 loads (4 per thread,
+        // all in flight) and this thread's 8 W_h values, then compute from LDS.
+        float wv[KC / KS];
+#pragma unroll
+        for (int j = 0; j < KC / KS; ++j) {
+          const int k = kc + sl + KS * j;
+          wv[j] = k < 4 * H ? w[k] : 0.f;
+        }
+        f32x4 v4[kRowChunk * KC / 4 / 256];
+#pragma unroll
+        for (int q = 0; q < kRowChunk * KC / 4 / 256; ++q) {
+          const int e = (int)threadIdx.x + 256 * q;  // float4 index in the chunk
+          const int i = e / (KC / 4), k = kc + 4 * (e % (KC / 4));
+          v4[q] = (b0 + i < B && k < 4 * H)
+                      ? *reinterpret_cast<const f32x4*>(dgates + ((size_t)(b0 + i) * T + t + 1) * 4 * H + k)
+                      : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        __syncthreads();  // previous chunk fully consumed
+#pragma unroll
+        for (int q = 0; q < kRowChunk * KC / 4 / 256; ++q) {
+          const int e = (int)threadIdx.x + 256 * q;
+          *reinterpret_cast<f32x4*>(&ds[e / (KC / 4)][4 * (e % (KC / 4))]) = v4[q];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < KC / KS; ++j) {
+          const int k = sl + KS * j;
+#pragma unroll
+          for (int i = 0; i < kRowChunk; ++i) acc[i] = fmaf(ds[i][k], wv[j], acc[i]);
+        }
+      }
     }
-    if (sl < ks) part[threadIdx.x] = acc;
+#pragma unroll
+    for (int i = 0; i < kRowChunk; ++i) red[u][i][sl] = acc[i];
     __syncthreads();
-    if ((int)threadIdx.x < chunk) {
-      float dhn = 0.f;
-      for (int s2 = 0; s2 < ks; ++s2) dhn += part[s2 * chunk + threadIdx.x];
-      const int b = o / kUnits, j = u0 + o % kUnits;
-      const size_t row = (size_t)b * T + t;
-      const float* g = gates + row * 4 * H;
-      const float ig = g[j], fg = g[H + j], gg = g[2 * H + j], og = g[3 * H + j];
-      const float cn = c_all[row * H + j];
-      const float cprev = t > 0 ? c_all[(row - 1) * H + j] : c0[(size_t)b * c0_stride + j];
-      const float tc = tanhf(cn);
-      const float dh = dh_head[row * H + j] + dhn;
-      const float dc = dc_carry[(size_t)b * H + j] + dh * og * (1.f - tc * tc);
-      float* dg = dgates + row * 4 * H;
-      dg[j] = dc * gg * ig * (1.f - ig);
-      dg[H + j] = dc * cprev * fg * (1.f - fg);
-      dg[2 * H + j] = dc * ig * (1.f - gg * gg);
-      dg[3 * H + j] = dh * tc * og * (1.f - og);
-      dc_carry[(size_t)b * H + j] = dc * fg;
+    if ((int)threadIdx.x < kUnits * kRowChunk) {
+      const int uu = threadIdx.x / kRowChunk, i = threadIdx.x % kRowChunk, b = b0 + i;
+      if (b < B) {
+        float dhn = 0.f;
+        for (int s2 = 0; s2 < KS; ++s2) dhn += red[uu][i][s2];
+        const int j = u0 + uu;
+        const size_t row = (size_t)b * T + t;
+        const float* g = gates + row * 4 * H;
+        const float ig = g[j], fg = g[H + j], gg = g[2 * H + j], og = g[3 * H + j];
+        const float cn = c_all[row * H + j];
+        const float cprev = t > 0 ? c_all[(row - 1) * H + j] : c0[(size_t)b * c0_stride + j];
+        const float tc = tanhf(cn);
+        const float dh = dh_head[row * H + j] + dhn;
+        const float dc = dc_carry[(size_t)b * H + j] + dh * og * (1.f - tc * tc);
+        float* dg = dgates + row * 4 * H;
+        dg[j] = dc * gg * ig * (1.f - ig);
+        dg[H + j] = dc * cprev * fg * (1.f - fg);
+        dg[2 * H + j] = dc * ig * (1.f - gg * gg);
+        dg[3 * H + j] = dh * tc * og * (1.f - og);
+        dc_carry[(size_t)b * H + j] = dc * fg;
+      }
     }
     __syncthreads();
   }
 }
 
 // ------------------------------------------------------------------ loss
-// One wave per sequence b (lane = action): for t < T-1 log pi, log mu, log rho, entropy;
-// V-trace backward scan (trfl.vtrace_from_importance_weights, rho_bar = c_bar = 1);
-// losses and d loss / d [logits | value] written into dpv rows b*T + t (zero at t = T-1).
+// Three launches over the B*T rows (row = b * T + t, t < T-1 carry the losses):
+//   rowstats (one wave per row, lane = action): log pi, log mu -> log rho, log pi(a),
+//     entropy H(pi)
+//   vtrace (one thread per sequence): trfl.vtrace_from_importance_weights backward scan
+//     (rho_bar = c_bar = 1) -> vs, pg advantages; the four logged means
+//   grads (one wave per row): d loss / d logits = (-(onehot - pi) adv + c_e pi (log pi
+//     + H)) / N, d loss / d value = -2 c_b (vs - v) / N; zero at t = T-1
 struct LossArgs {
   const float* pv;  // [rows][A + 1]
   const int32_t* action;
   const float *reward, *discount, *mu;
   int B, T, A;
   float gamma, entropy_cost, baseline_cost, max_abs_reward;
+  float* lrho;   // [rows] scratch
+  float* lpa;    // [rows]
+  float* ent;    // [rows]
   float* dpv;
   float *vs, *pg_adv;  // [(T-1) * B] time-major
   float* metrics;      // [4]
 };
 
-__global__ void __launch_bounds__(1024) impala_loss_kernel(const LossArgs a) {
-  __shared__ float red[16][3];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int A = a.A, T = a.T, W = A + 1;
+__global__ void __launch_bounds__(256) impala_rowstats_kernel(const LossArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.B * a.T || row % a.T == a.T - 1) return;
+  const int A = a.A, W = A + 1;
   const bool on = lane < A;
-  const float invN = 1.f / (float)((T - 1) * a.B);
+  const float l = on ? a.pv[(size_t)row * W + lane] : -INFINITY;
+  const float m = wave_max(l);
+  const float e = on ? expf(l - m) : 0.f;
+  const float s = wave_sum(e);
+  const float logp = l - m - logf(s);
+  const float mu = on ? a.mu[(size_t)row * A + lane] : -INFINITY;
+  const float mm = wave_max(mu);
+  const float me = on ? expf(mu - mm) : 0.f;
+  const float logmu = mu - mm - logf(wave_sum(me));
+  const int act = a.action[row];
+  const float lpa = __shfl(logp, act, 64), lma = __shfl(logmu, act, 64);
+  const float ent = -wave_sum(on ? (e / s) * logp : 0.f);
+  if (lane == 0) {
+    a.lrho[row] = lpa - lma;
+    a.lpa[row] = lpa;
+    a.ent[row] = ent;
+  }
+}
+
+__global__ void __launch_bounds__(64) impala_vtrace_kernel(const LossArgs a) {
+  __shared__ float red[64][3];
+  const int b = threadIdx.x;
+  const int T = a.T, W = a.A + 1;
   float s_pg = 0.f, s_cr = 0.f, s_en = 0.f;
-  for (int b = wave; b < a.B; b += nw) {
-    // Pass 1 (forward in t): per-step quantities kept in the lane owning step t (T <= 64).
-    float my_lrho = 0.f, my_lpa = 0.f, my_ent = 0.f, my_r = 0.f, my_g = 0.f, my_v = 0.f;
-    for (int t = 0; t < T; ++t) {
-      const size_t row = (size_t)b * T + t;
-      const float v = a.pv[row * W + A];
-      if (lane == t) my_v = v;
-      if (t == T - 1) break;
-      const float l = on ? a.pv[row * W + lane] : -INFINITY;
-      const float m = wave_max(l);
-      const float e = on ? expf(l - m) : 0.f;
-      const float s = wave_sum(e);
-      const float logp = l - m - logf(s);
-      const float mu = on ? a.mu[row * A + lane] : -INFINITY;
-      const float mm = wave_max(mu);
-      const float me = on ? expf(mu - mm) : 0.f;
-      const float logmu = mu - mm - logf(wave_sum(me));
-      const int act = a.action[row];
-      const float lpa = __shfl(logp, act, 64), lma = __shfl(logmu, act, 64);
-      const float ent = -wave_sum(on ? (e / s) * logp : 0.f);
-      if (lane == t) {
-        my_lrho = lpa - lma;
-        my_lpa = lpa;
-        my_ent = ent;
-        float r = a.reward[row];
-        r = fminf(fmaxf(r, -a.max_abs_reward), a.max_abs_reward);
-        my_r = r;
-        my_g = a.gamma * a.discount[row];
-      }
-    }
-    // Pass 2: V-trace backward scan, serial in lane 0 over values gathered by shuffles.
-    const float boot = __shfl(my_v, T - 1, 64);
-    float acc = 0.f, vs_next = boot, my_vs = 0.f, my_adv = 0.f;
+  for (int bb = b; bb < a.B; bb += 64) {
+    const size_t base = (size_t)bb * T;
+    const float boot = a.pv[(base + T - 1) * W + a.A];
+    float acc = 0.f, vs_next = boot, v1 = boot;
     for (int t = T - 2; t >= 0; --t) {
-      const float lrho = __shfl(my_lrho, t, 64), r = __shfl(my_r, t, 64);
-      const float g = __shfl(my_g, t, 64), v = __shfl(my_v, t, 64);
-      const float v1 = __shfl(my_v, t + 1, 64);
-      const float rho = expf(lrho);
-      const float cr = fminf(1.f, rho);
-      const float delta = cr * (r + g * v1 - v);
-      acc = delta + g * cr * acc;
+      const size_t row = base + t;
+      const float v = a.pv[row * W + a.A];
+      float r = a.reward[row];
+      r = fminf(fmaxf(r, -a.max_abs_reward), a.max_abs_reward);
+      const float g = a.gamma * a.discount[row];
+      const float cr = fminf(1.f, expf(a.lrho[row]));
+      acc = cr * (r + g * v1 - v) + g * cr * acc;
       const float vs = acc + v;
       const float adv = cr * (r + g * vs_next - v);
+      a.vs[(size_t)t * a.B + bb] = vs;
+      a.pg_adv[(size_t)t * a.B + bb] = adv;
+      s_pg += -a.lpa[row] * adv;
+      s_cr += (vs - v) * (vs - v);
+      s_en += -a.ent[row];
       vs_next = vs;
-      if (lane == t) {
-        my_vs = vs;
-        my_adv = adv;
-      }
-    }
-    // Pass 3: losses and gradients.
-    for (int t = 0; t < T; ++t) {
-      const size_t row = (size_t)b * T + t;
-      if (t == T - 1) {
-        if (lane < W) a.dpv[row * W + lane] = 0.f;
-        continue;
-      }
-      const float vs = __shfl(my_vs, t, 64), adv = __shfl(my_adv, t, 64);
-      const float v = __shfl(my_v, t, 64), ent = __shfl(my_ent, t, 64);
-      const float lpa = __shfl(my_lpa, t, 64);
-      const float l = on ? a.pv[row * W + lane] : -INFINITY;
-      const float m = wave_max(l);
-      const float e = on ? expf(l - m) : 0.f;
-      const float s = wave_sum(e);
-      const float logp = l - m - logf(s);
-      const float pi = e / s;
-      const int act = a.action[row];
-      if (on) {
-        const float oh = lane == act ? 1.f : 0.f;
-        a.dpv[row * W + lane] =
-            (-(oh - pi) * adv + a.entropy_cost * pi * (logp + ent)) * invN;
-      }
-      if (lane == A) a.dpv[row * W + A] = a.baseline_cost * (-2.f) * (vs - v) * invN;
-      if (lane == 0) {
-        s_pg += -lpa * adv;
-        s_cr += (vs - v) * (vs - v);
-        s_en += -ent;
-        a.vs[(size_t)t * a.B + b] = vs;
-        a.pg_adv[(size_t)t * a.B + b] = adv;
-      }
+      v1 = v;
     }
   }
-  if (lane == 0) {
-    red[wave][0] = s_pg;
-    red[wave][1] = s_cr;
-    red[wave][2] = s_en;
-  }
+  red[b][0] = s_pg;
+  red[b][1] = s_cr;
+  red[b][2] = s_en;
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (b == 0) {
     float pg = 0.f, cr = 0.f, en = 0.f;
-    for (int w = 0; w < nw; ++w) {
-      pg += red[w][0];
-      cr += red[w][1];
-      en += red[w][2];
+    for (int i = 0; i < 64; ++i) {
+      pg += red[i][0];
+      cr += red[i][1];
+      en += red[i][2];
     }
+    const float invN = 1.f / (float)((T - 1) * a.B);
     pg *= invN;
     cr *= invN;
     en *= invN;
@@ -455,6 +509,36 @@ __global__ void __launch_bounds__(1024) impala_loss_kernel(const LossArgs a) {
     a.metrics[1] = cr;
     a.metrics[2] = en;
     a.metrics[3] = pg;
+  }
+}
+
+__global__ void __launch_bounds__(256) impala_loss_grad_kernel(const LossArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.B * a.T) return;
+  const int A = a.A, W = A + 1, T = a.T;
+  const int b = row / T, t = row - b * T;
+  if (t == T - 1) {
+    if (lane < W) a.dpv[(size_t)row * W + lane] = 0.f;
+    return;
+  }
+  const float invN = 1.f / (float)((T - 1) * a.B);
+  const bool on = lane < A;
+  const float l = on ? a.pv[(size_t)row * W + lane] : -INFINITY;
+  const float m = wave_max(l);
+  const float e = on ? expf(l - m) : 0.f;
+  const float s = wave_sum(e);
+  const float logp = l - m - logf(s);
+  const float pi = e / s;
+  const float adv = a.pg_adv[(size_t)t * a.B + b], vs = a.vs[(size_t)t * a.B + b];
+  const float ent = a.ent[row];
+  if (on) {
+    const float oh = lane == a.action[row] ? 1.f : 0.f;
+    a.dpv[(size_t)row * W + lane] = (-(oh - pi) * adv + a.entropy_cost * pi * (logp + ent)) * invN;
+  }
+  if (lane == A) {
+    const float v = a.pv[(size_t)row * W + A];
+    a.dpv[(size_t)row * W + A] = a.baseline_cost * (-2.f) * (vs - v) * invN;
   }
 }
 
@@ -528,12 +612,12 @@ int network_forward(acme_impala* l, const void* obs, const int32_t* prev_a, cons
   }
   {
     ACME_PROF("impala_lstm_fwd", st, 2.0 * rows * (double)H * 4 * H, 0.0);
-    const size_t smem = ((size_t)B * H + (size_t)B * 4 * kUnits) * sizeof(float);
+    const size_t smem = lstm_fwd_smem(B, H);
     for (int t = 0; t < T; ++t) {
       const float* hp = t == 0 ? h0 : l->h + (size_t)(t - 1) * H;
       const float* cp = t == 0 ? c0 : l->c + (size_t)(t - 1) * H;
       const int64_t hs = t == 0 ? state_stride : (int64_t)T * H;
-      lstm_fwd_step_kernel<<<H / kUnits, 256, smem, st>>>(l->gx, P(l, l->params, l->t_wh), hp, hs,
+      lstm_fwd_step_kernel<<<H / kFwdUnits, 256, smem, st>>>(l->gx, P(l, l->params, l->t_wh), hp, hs,
                                                           cp, hs, B, T, t, H, l->gates, l->h,
                                                           l->c);
       IM_CHECK();
@@ -573,8 +657,14 @@ int impala_step_impl(acme_impala* l, const acme_sequence_batch* bt, float* metri
     a.gamma = l->cfg.discount; a.entropy_cost = l->cfg.entropy_cost;
     a.baseline_cost = l->cfg.baseline_cost; a.max_abs_reward = l->cfg.max_abs_reward;
     a.dpv = l->dpv; a.vs = l->vs; a.pg_adv = l->pg_adv;
+    a.lrho = l->lrho; a.lpa = l->lpa; a.ent = l->ent;
     a.metrics = metrics ? metrics : l->metrics_tmp;
-    impala_loss_kernel<<<1, 64 * std::min(B, 16), 0, st>>>(a);
+    const unsigned rb = (unsigned)ceil_div(rows, 4);
+    impala_rowstats_kernel<<<rb, 256, 0, st>>>(a);
+    IM_CHECK();
+    impala_vtrace_kernel<<<1, 64, 0, st>>>(a);
+    IM_CHECK();
+    impala_loss_grad_kernel<<<rb, 256, 0, st>>>(a);
     IM_CHECK();
   }
   float* gr = l->grads;
@@ -677,8 +767,8 @@ int acme_impala_create(const acme_impala_config* cfg, acme_impala** out) {
                  "max_sequence_length must be in [2, 64]");
   ACME_CHECK_ARG(cfg->lstm_size >= 8 && cfg->lstm_size % 8 == 0,
                  "lstm_size must be a positive multiple of 8");
-  ACME_CHECK_ARG((int64_t)cfg->max_batch * (cfg->lstm_size + 4 * kUnits) <= 16384,
-                 "max_batch * (lstm_size + 32) must be <= 16384 (LSTM cell LDS)");
+  ACME_CHECK_ARG(lstm_fwd_smem(cfg->max_batch, cfg->lstm_size) <= 65536,
+                 "max_batch * lstm_size + 16 * lstm_size must stay within 64 KB of LDS");
   ACME_CHECK_ARG(cfg->head_size >= 4 && cfg->head_size % 4 == 0,
                  "head_size must be a positive multiple of 4");
   acme_impala* l = new acme_impala();
@@ -727,6 +817,8 @@ int acme_impala_create(const acme_impala_config* cfg, acme_impala** out) {
       (rc = dev_alloc(l, &l->dhh, R * H2)) || (rc = dev_alloc(l, &l->dh, R * H)) ||
       (rc = dev_alloc(l, &l->dgates, R * 4 * H)) || (rc = dev_alloc(l, &l->dc, (int64_t)B * H)) ||
       (rc = dev_alloc(l, &l->vs, R)) || (rc = dev_alloc(l, &l->pg_adv, R)) ||
+      (rc = dev_alloc(l, &l->lrho, R)) || (rc = dev_alloc(l, &l->lpa, R)) ||
+      (rc = dev_alloc(l, &l->ent, R)) ||
       (rc = dev_alloc(l, &l->norm_part, 2 * kNormBlocks)) || (rc = dev_alloc(l, &l->dev_step, 1)) ||
       (rc = dev_alloc(l, &l->metrics_tmp, 4)) || (rc = dev_alloc(l, &l->norms, 2)))
     return fail(rc);

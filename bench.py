@@ -43,8 +43,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--workload", choices=("dqn", "d4pg"), default="dqn",
-                   help="dqn: the headline config (BASELINE configs[1]); d4pg: configs[2]")
+    p.add_argument("--workload", choices=("dqn", "d4pg", "impala"), default="dqn",
+                   help="dqn: the headline config (BASELINE configs[1]); d4pg: configs[2]; "
+                        "impala: configs[3] (learner side)")
     p.add_argument("--batch", type=int, default=0, help="default 512 (dqn) / 256 (d4pg)")
     p.add_argument("--replay-size", type=int, default=1_000_000)
     p.add_argument("--num-actions", type=int, default=18)
@@ -247,6 +248,90 @@ def setup_d4pg(args, world, rank, dev):
             lambda: d4pg_cpu_baseline(B, args.cpu_baseline_seconds))
 
 
+def impala_cpu_baseline(B: int, T: int, seconds: float):
+    """The numpy IMPALA oracle (oracle/impala_oracle.py, float32) on a bounded sample: the
+    same B x T Atari sequences, as many full learner steps as fit in `seconds` (at least 2;
+    the first is a warm-up)."""
+    from oracle import impala_oracle as O
+    from acme_amd.networks import IMPALAAtariNetwork
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    try:
+        from threadpoolctl import threadpool_limits
+        ctx = threadpool_limits(threads)
+    except ImportError:  # pragma: no cover
+        ctx = None
+    rng = np.random.default_rng(0)
+    A, H = 18, 256
+    batch = dict(obs=rng.integers(0, 256, (B, T, 84, 84, 4), dtype=np.uint8),
+                 prev_action=rng.integers(0, A, (B, T)).astype(np.int32),
+                 prev_reward=rng.standard_normal((B, T)).astype(np.float32),
+                 action=rng.integers(0, A, (B, T)).astype(np.int32),
+                 reward=rng.standard_normal((B, T)).astype(np.float32),
+                 discount=np.full((B, T), 0.99, np.float32),
+                 behaviour_logits=rng.standard_normal((B, T, A)).astype(np.float32),
+                 h0=np.zeros((B, H), np.float32), c0=np.zeros((B, H), np.float32))
+    cfg = O.IMPALAConfig(num_actions=A)
+    p = IMPALAAtariNetwork(A).init(0)
+    z = {k: np.zeros_like(v) for k, v in p.items()}
+    state = dict(params=p, m=z, v=dict(z), num_steps=0)
+    state = O.impala_step(cfg, state, batch, np.float32)[2]
+    t0 = time.perf_counter()
+    n = 0
+    while n < 2 or time.perf_counter() - t0 < seconds:
+        state = O.impala_step(cfg, state, batch, np.float32)[2]
+        n += 1
+    dt = time.perf_counter() - t0
+    if ctx is not None and hasattr(ctx, "unregister"):
+        ctx.unregister()
+    return dict(value=round(B * T * n / dt, 2), unit="frames/s", cores=threads, kind="port",
+                sample=(f"numpy float32 oracle (oracle/impala_oracle.py), {n} timed steps of "
+                        f"B={B} x T={T} Atari sequences, {threads} BLAS threads, {cpu_model()}"))
+
+
+def setup_impala(args, world, rank, dev):
+    """BASELINE configs[3]: IMPALAAtariNetwork (LSTM 256, 18 actions), batch 16 sequences
+    of T = 20 frames.  The queue is a device-resident pool of 4 batches of synthetic
+    sequences (what 64 actors would have enqueued); each step consumes the next batch."""
+    from acme_amd.native import NativeIMPALA
+    from acme_amd.networks import IMPALAAtariNetwork
+    if world > 1:
+        raise SystemExit("the IMPALA workload is single-GPU (BASELINE configs[3])")
+    B, T, A, H = args.batch or 16, 20, 18, 256
+    pool = 4
+    g = torch.Generator(device=dev).manual_seed(rank)
+    obs = torch.randint(0, 256, (pool, B, T, 84, 84, 4), dtype=torch.uint8, device=dev, generator=g)
+    ia = lambda: torch.randint(0, A, (pool, B, T), dtype=torch.int32, device=dev, generator=g)  # noqa
+    fl = lambda *s: torch.randn(*s, device=dev, generator=g)  # noqa
+    prev_a, act = ia(), ia()
+    prev_r, rew = fl(pool, B, T), fl(pool, B, T)
+    disc = torch.where(torch.rand(pool, B, T, device=dev, generator=g) < 0.01, 0.0, 0.99)
+    mu = fl(pool, B, T, A)
+    state = 0.1 * fl(pool, B, T, 2, H)
+    net = IMPALAAtariNetwork(A)
+    n = NativeIMPALA(num_actions=A, max_batch=B, max_sequence_length=T, lstm_size=H,
+                     head_size=256, entropy_cost=0.01, baseline_cost=0.5, learning_rate=1e-3,
+                     device=dev)
+    n.set_params(net.init(0))
+    it = [0]
+
+    def step():
+        i = it[0] % pool
+        it[0] += 1
+        n.step(obs[i], prev_a[i], prev_r[i], act[i], rew[i], disc[i], mu[i], state[i][:, 0, 0],
+               state[i][:, 0, 1])
+
+    meta = dict(
+        metric="learner frames/sec (B=16 sequences x T=20) IMPALA Atari, 1 MI355X",
+        unit="frames/s", dtype="f32",
+        data="synthetic (device-generated uint8 Atari sequences in a device-resident queue "
+             "pool, random-init IMPALAAtariNetwork)",
+        config={"workload": "impala_atari_lstm_vtrace (BASELINE configs[3])",
+                "batch_sequences": B, "sequence_length": T, "frames_per_step": B * T,
+                "obs": "uint8[84,84,4]", "num_actions": A, "lstm": H, "parallelism": "dp1"})
+    return (step, B * T, meta, lambda: float(n.metrics[0].item()),
+            lambda: impala_cpu_baseline(B, T, args.cpu_baseline_seconds))
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -264,7 +349,7 @@ def main():
     from acme_amd import _lib
     L = _lib.lib()
     t_fill = time.perf_counter()
-    setup = {"dqn": setup_dqn, "d4pg": setup_d4pg}[args.workload]
+    setup = {"dqn": setup_dqn, "d4pg": setup_d4pg, "impala": setup_impala}[args.workload]
     step, B, meta, loss_fn, cpu_fn = setup(args, world, rank, dev)
     torch.cuda.synchronize(dev)
     t_fill = time.perf_counter() - t_fill
@@ -344,7 +429,8 @@ def main():
         cpu = cpu_fn()
     if rank == 0:
         out = {
-            "metric": meta["metric"], "value": round(value, 1), "unit": "transitions/s",
+            "metric": meta["metric"], "value": round(value, 1),
+            "unit": meta.get("unit", "transitions/s"),
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": meta["dtype"], "data": meta["data"],

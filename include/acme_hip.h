@@ -284,7 +284,7 @@ typedef struct acme_impala_config {
   int32_t num_actions;          /* <= 63 */
   int32_t max_batch;            /* sequences per step (B) */
   int32_t max_sequence_length;  /* T */
-  int32_t lstm_size;            /* multiple of 8, max_batch * (lstm_size + 32) <= 16384 */
+  int32_t lstm_size;            /* multiple of 8, max_batch * (lstm_size + 32) <= 12288 */
   int32_t head_size;            /* multiple of 4 */
   float discount, entropy_cost, baseline_cost;
   float max_abs_reward;         /* INFINITY = no reward clipping (learning.py:70-71) */
