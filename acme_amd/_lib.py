@@ -23,6 +23,9 @@ ACME_ERR_HIP = -2
 ACME_ERR_EMPTY = -3
 ACME_ERR_OOM = -4
 
+MATMUL_F32 = 0
+MATMUL_X6 = 1
+
 MAX_FIELDS = 8
 MAX_MLP_LAYERS = 8
 D4PG_MAX_LAYERS = 4
@@ -103,6 +106,9 @@ _SIGS = {
     "acme_last_error": (ctypes.c_char_p, []),
     "acme_version": (ctypes.c_char_p, []),
     "acme_target_arch": (ctypes.c_char_p, []),
+    "acme_set_matmul_engine": (c_i32, [c_i32]),
+    "acme_matmul_engine": (c_i32, []),
+    "acme_dense_forward": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp]),
     "acme_replay_create": (c_i32, [ctypes.POINTER(ReplayConfig), ctypes.POINTER(c_vp)]),
     "acme_replay_destroy": (c_i32, [c_vp]),
     "acme_replay_insert": (c_i32, [c_vp, ctypes.POINTER(c_vp), c_i64, c_vp, c_i32, c_vp, c_vp]),

@@ -14,9 +14,33 @@ void set_error(const char* fmt, ...) {
   va_end(ap);
 }
 
+namespace gemm {
+
+// Matmul engine: 1 = three-plane bf16 MFMA (gemm_x6.h, f32-equivalent), 0 = f32 MFMA
+// (gemm.h).  Initialised from ACME_MATMUL ("f32" or "x6"), default x6.
+static int g_engine = -1;
+
+bool use_x6() {
+  if (g_engine < 0) {
+    const char* e = getenv("ACME_MATMUL");
+    g_engine = (e && strcmp(e, "f32") == 0) ? ACME_MATMUL_F32 : ACME_MATMUL_X6;
+  }
+  return g_engine == ACME_MATMUL_X6;
+}
+
+}  // namespace gemm
 }  // namespace acme
 
 extern "C" {
+
+int acme_set_matmul_engine(int32_t engine) {
+  ACME_CHECK_ARG(engine == ACME_MATMUL_F32 || engine == ACME_MATMUL_X6, "unknown matmul engine %d",
+                 engine);
+  acme::gemm::g_engine = engine;
+  return ACME_OK;
+}
+
+int32_t acme_matmul_engine(void) { return acme::gemm::use_x6() ? ACME_MATMUL_X6 : ACME_MATMUL_F32; }
 
 const char* acme_last_error(void) { return acme::g_last_error; }
 

@@ -63,6 +63,7 @@ struct InF32 {
 template <class G, class In>
 struct ConvFwd {
   static constexpr int A_MODE = KCONTIG, B_MODE = RCONTIG;
+  static constexpr bool kX6 = true;  // narrow weight operand (gemm_x6.h)
   int M, N, K, k_chunk;
   const typename In::T* x;   // rows [0, split_b) of the batch
   const typename In::T* x2;  // rows [split_b, batch) (may alias x)
@@ -224,6 +225,94 @@ struct ConvDgradSub {
     dx[idx] = xprev[idx] > 0.f ? v : 0.f;
   }
 };
+// All S*S parity classes of the sub-pixel input gradient in ONE launch: blockIdx.z is
+// the class (the GEMM engines call for_z(z) per block, and z is not a K split), so the
+// four class GEMMs share one grid and the CUs hold several blocks at a time.
+template <class G>
+struct ConvDgradSubZ {
+  static_assert(G::KH % G::S == 0 && G::KW % G::S == 0, "kernel must be a multiple of stride");
+  static constexpr int A_MODE = KCONTIG, B_MODE = KCONTIG;
+  static constexpr bool kZClass = true;
+  static constexpr int S = G::S;
+  static constexpr int JH = G::KH / S, JW = G::KW / S;
+  static constexpr int KR = JH * JW * G::CO;
+  int M, N, K, k_chunk;  // M = rows of the largest class (grid), N = CI, K = KR
+  int batch;
+  const float* dz;
+  const float* w;
+  const float* xprev;
+  float* dx;
+  int ph = 0, pw = 0, rh = 0, rw = 0, nh = 1, nw = 1, mc = 0;  // set by for_z
+  __device__ ConvDgradSubZ for_z(int z) const {
+    ConvDgradSubZ q = *this;
+    q.ph = z / S;
+    q.pw = z % S;
+    q.rh = ((q.ph - G::PT) % S + S) % S;
+    q.rw = ((q.pw - G::PL) % S + S) % S;
+    q.nh = (G::IH - q.rh + S - 1) / S;
+    q.nw = (G::IW - q.rw + S - 1) / S;
+    q.mc = batch * q.nh * q.nw;
+    return q;
+  }
+  static int max_rows(int batch) {
+    int best = 0;
+    for (int ph = 0; ph < S; ++ph)
+      for (int pw = 0; pw < S; ++pw) {
+        const int rh = ((ph - G::PT) % S + S) % S, rw = ((pw - G::PL) % S + S) % S;
+        const int n = batch * ((G::IH - rh + S - 1) / S) * ((G::IW - rw + S - 1) / S);
+        best = n > best ? n : best;
+      }
+    return best;
+  }
+  struct ARow {
+    const float* base;
+    int oh0, ow0;
+    bool ok;
+  };
+  struct BRow {
+    int ci;
+  };
+  __device__ void decode(int m, int& b, int& ih, int& iw) const {
+    b = m / (nh * nw);
+    const int rem = m - b * (nh * nw);
+    const int i = rem / nw, j = rem - i * nw;
+    ih = rh + S * i;
+    iw = rw + S * j;
+  }
+  __device__ ARow a_row(int m) const {
+    ARow a;
+    a.ok = m < mc;
+    int b, ih, iw;
+    decode(a.ok ? m : 0, b, ih, iw);
+    a.base = dz + (size_t)b * G::OPIX * G::CO;
+    a.oh0 = (ih + G::PT - ph) / S;
+    a.ow0 = (iw + G::PL - pw) / S;
+    return a;
+  }
+  __device__ f32x4 a_load(const ARow& a, int k) const {
+    const int jh = k / (JW * G::CO), r = k - jh * (JW * G::CO);
+    const int jw = r / G::CO, co = r - jw * G::CO;
+    const int oh = a.oh0 - jh, ow = a.ow0 - jw;
+    if (!a.ok || (unsigned)oh >= (unsigned)G::OH || (unsigned)ow >= (unsigned)G::OW) return zero4();
+    return *reinterpret_cast<const f32x4*>(a.base + (oh * G::OW + ow) * G::CO + co);
+  }
+  __device__ BRow b_row(int ci) const { return BRow{ci}; }
+  __device__ f32x4 b_load(const BRow& b, int k) const {
+    if (b.ci >= N) return zero4();
+    const int jh = k / (JW * G::CO), r = k - jh * (JW * G::CO);
+    const int jw = r / G::CO, co = r - jw * G::CO;
+    const int kh = ph + S * jh, kw = pw + S * jw;
+    return *reinterpret_cast<const f32x4*>(w + ((size_t)(kh * G::KW + kw) * G::CI + b.ci) * G::CO + co);
+  }
+  __device__ void store(int m, int ci, float v, int) const {
+    if (m >= mc) return;
+    int b, ih, iw;
+    decode(m, b, ih, iw);
+    const size_t idx = ((size_t)b * G::IPIX + ih * G::IW + iw) * G::CI + ci;
+    dx[idx] = xprev[idx] > 0.f ? v : 0.f;
+  }
+};
+
 template <class G>
 struct ConvDgrad {
   static constexpr int A_MODE = KCONTIG, B_MODE = KCONTIG;
@@ -306,6 +395,7 @@ __device__ __forceinline__ float act_bwd(int act, float y, float g) {
 template <bool VEC, class In = InF32>
 struct DenseFwd {
   static constexpr int A_MODE = KCONTIG, B_MODE = RCONTIG;
+  static constexpr bool kX6 = true;
   int M, N, K, k_chunk;
   const typename In::T* x;
   const typename In::T* x2;

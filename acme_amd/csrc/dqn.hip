@@ -25,6 +25,7 @@
 #include "common.h"
 #include "conv.h"
 #include "gemm.h"
+#include "gemm_x6.h"
 #include "kernels.h"
 #include "profiler.h"
 #include "torso.h"
@@ -128,7 +129,7 @@ inline int chunk_for(int K, int splits) {
 
 #define ACME_GEMM(BM, BN, WM, WN, prob, splits)                                      \
   do {                                                                               \
-    hipError_t _e = launch_gemm<BM, BN, WM, WN>(prob, splits, st);                  \
+    hipError_t _e = gemm::launch_matmul<BM, BN, WM, WN>(prob, splits, st);          \
     if (_e != hipSuccess) {                                                          \
       set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
       return ACME_ERR_HIP;                                                           \
@@ -161,7 +162,7 @@ int tune(const char* key) {
 #define ACME_GEMM_NK(name, BM, BN, WM, WN, BKV, prob, splits)                                 \
   do {                                                                                         \
     ACME_PROF(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0);   \
-    hipError_t _e = launch_gemm<BM, BN, WM, WN, BKV>(prob, splits, st);                       \
+    hipError_t _e = gemm::launch_matmul<BM, BN, WM, WN, BKV>(prob, splits, st);               \
     if (_e != hipSuccess) {                                                                    \
       set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
       return ACME_ERR_HIP;                                                                     \

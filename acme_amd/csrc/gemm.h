@@ -103,6 +103,22 @@ struct HasColSum<P, decltype(void(P::kColSum))> {
   static constexpr bool value = P::kColSum;
 };
 
+// Optional z-class hook: problems with `static constexpr bool kZClass = true` use
+// blockIdx.z to select a sub-problem (p.for_z(z)) instead of a K split.
+template <class P, class = void>
+struct HasZClass {
+  static constexpr bool value = false;
+};
+template <class P>
+struct HasZClass<P, decltype(void(P::kZClass))> {
+  static constexpr bool value = P::kZClass;
+};
+template <class P>
+__device__ __forceinline__ P z_select(const P& p) {
+  if constexpr (HasZClass<P>::value) return p.for_z(blockIdx.z);
+  else return p;
+}
+
 // Problem concept (see conv.h):
 //   static constexpr int A_MODE, B_MODE;
 //   int M, N, K;            rows of A (= C rows), rows of B (= C cols), reduction length
@@ -117,7 +133,8 @@ struct HasColSum<P, decltype(void(P::kColSum))> {
 // accumulators are summed through LDS before the epilogue.  Small GEMMs (a few hundred
 // rows, K <= 1024) use it to put 4x more waves on the same output tiles.
 template <int BM, int BN, int WM, int WN, int BK, int WK, class P>
-__global__ void __launch_bounds__(64 * WM * WN * WK) gemm_f32_kernel(const P p) {
+__global__ void __launch_bounds__(64 * WM * WN * WK) gemm_f32_kernel(const P p_in) {
+  const P p = z_select(p_in);
   constexpr int NTG = 64 * WM * WN;  // threads per k-group
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int MT = TM / 32, NTL = TN / 32;
@@ -141,7 +158,7 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) gemm_f32_kernel(const P p) 
   const int tile = blockIdx.x;
   const int m0 = (tile / tiles_n) * BM;
   const int n0 = (tile % tiles_n) * BN;
-  const int split = blockIdx.z;
+  const int split = HasZClass<P>::value ? 0 : blockIdx.z;
   int kbeg = split * p.k_chunk;
   int kend = kbeg + p.k_chunk;
   if (kend > p.K) kend = p.K;

@@ -24,6 +24,7 @@
 #include "common.h"
 #include "conv.h"
 #include "gemm.h"
+#include "gemm_x6.h"
 #include "kernels.h"
 #include "profiler.h"
 #include "torso.h"
@@ -547,7 +548,7 @@ __global__ void __launch_bounds__(256) impala_loss_grad_kernel(const LossArgs a)
 #define IM_GEMM(name, BM, BN, WM, WN, WK, prob, splits)                                         \
   do {                                                                                         \
     ACME_PROF(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0);    \
-    hipError_t _e = launch_gemm<BM, BN, WM, WN, 16, WK>(prob, splits, st);                      \
+    hipError_t _e = gemm::launch_matmul<BM, BN, WM, WN, 16, WK>(prob, splits, st);              \
     if (_e != hipSuccess) {                                                                    \
       set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__);  \
       return ACME_ERR_HIP;                                                                     \

@@ -2,6 +2,9 @@
 // column sums, split-K slab reductions, snt.Adam.
 #include "kernels.h"
 
+#include "conv.h"
+#include "gemm_x6.h"
+
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -418,6 +421,26 @@ int acme_adam_update(float* params, const float* grads, float* m, float* v, int6
   acme::adam_kernel<<<grid, 256, 0, acme::as_stream(stream)>>>(params, grads, m, v, n4, lr, beta1,
                                                                 omb1, beta2, omb2, bc1, bc2, eps);
   ACME_LAUNCH_CHECK();
+  return ACME_OK;
+}
+
+int acme_dense_forward(const float* x, int64_t rows, int64_t in, const float* w, const float* b,
+                       int64_t out, int32_t act, float* y, void* stream) {
+  ACME_CHECK_ARG(x && w && b && y, "null buffer");
+  ACME_CHECK_ARG(rows >= 1 && rows < (1 << 30) && in >= 4 && in % 4 == 0 && out >= 4 &&
+                     out % 4 == 0 && in < (1 << 30) && out < (1 << 30),
+                 "bad dense shape [%lld x %lld] -> %lld", (long long)rows, (long long)in,
+                 (long long)out);
+  ACME_CHECK_ARG(act >= 0 && act <= 3, "unknown activation %d", act);
+  acme::conv::DenseFwd<true> p;
+  p.M = (int)rows; p.N = (int)out; p.K = (int)in; p.k_chunk = (int)in;
+  p.x = x; p.x2 = x; p.split_b = (int)rows; p.ldx = (int)in;
+  p.w = w; p.bias = b; p.y = y; p.act = act; p.slab = nullptr;
+  hipError_t e = acme::gemm::launch_matmul<128, 128, 2, 2>(p, 1, acme::as_stream(stream));
+  if (e != hipSuccess) {
+    acme::set_error("dense launch failed: %s", hipGetErrorString(e));
+    return ACME_ERR_HIP;
+  }
   return ACME_OK;
 }
 

@@ -8,6 +8,7 @@
 
 #include "common.h"
 #include "gemm.h"
+#include "gemm_x6.h"
 #include "kernels.h"
 #include "profiler.h"
 
@@ -27,9 +28,12 @@ inline int chunk_for(int K, int splits) {
 }
 
 #define TORSO_GEMM(name, BM, BN, WM, WN, prob, splits)                                        \
+  TORSO_GEMM_F(name, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, BM, BN, WM, \
+               WN, prob, splits)
+#define TORSO_GEMM_F(name, flops, BM, BN, WM, WN, prob, splits)                               \
   do {                                                                                        \
-    ACME_PROF(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0);   \
-    hipError_t _e = launch_gemm<BM, BN, WM, WN, 16>(prob, splits, st);                         \
+    ACME_PROF(name, st, flops, 0.0);                                                          \
+    hipError_t _e = gemm::launch_matmul<BM, BN, WM, WN, 16>(prob, splits, st);                 \
     if (_e != hipSuccess) {                                                                   \
       set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
       return ACME_ERR_HIP;                                                                    \
@@ -49,17 +53,6 @@ int conv_wgrad(const typename In::T* x, const float* dz, int rows, int splits, f
   const int64_t count = (int64_t)(p.M + 1) * p.N;
   ACME_PROF(rname, st, 0.0, 4.0 * (double)(splits + 1) * (double)count);
   return launch_slab_reduce(slab, splits, count, dw, (int64_t)p.M * p.N, db, nullptr, 0, 0, st);
-}
-
-template <int PH, int PW>
-int conv2_dgrad_class(const float* w2, const float* x1, const float* dz2, float* dz1, int rows,
-                      hipStream_t st) {
-  using Sub = ConvDgradSub<G2, PH, PW>;
-  Sub p;
-  p.M = rows * Sub::NH * Sub::NW; p.N = G2::CI; p.K = Sub::KR; p.k_chunk = Sub::KR;
-  p.dz = dz2; p.w = w2; p.xprev = x1; p.dx = dz1;
-  TORSO_GEMM("conv2_dgrad", 256, 32, 4, 1, p, 1);
-  return ACME_OK;
 }
 
 }  // namespace
@@ -117,12 +110,15 @@ int backward(const Weights& w, const Grads& g, bool u8, const void* obs, int row
   if ((rc = conv_wgrad<G2, InF32, 64, 64, 2, 2>(a.x1, dz2, rows, kConv2WgradSplits, slab, g.w2,
                                                 g.b2, "conv2_wgrad", "conv2_wgrad_reduce", st)))
     return rc;
-  // Stride-2 input gradient as four dense sub-pixel GEMMs (one per parity class).
-  if ((rc = conv2_dgrad_class<0, 0>(w.w2, a.x1, dz2, dz1, rows, st)) ||
-      (rc = conv2_dgrad_class<0, 1>(w.w2, a.x1, dz2, dz1, rows, st)) ||
-      (rc = conv2_dgrad_class<1, 0>(w.w2, a.x1, dz2, dz1, rows, st)) ||
-      (rc = conv2_dgrad_class<1, 1>(w.w2, a.x1, dz2, dz1, rows, st)))
-    return rc;
+  {  // Stride-2 input gradient: the four sub-pixel parity classes as one launch (z = class).
+    ConvDgradSubZ<G2> p;
+    p.M = ConvDgradSubZ<G2>::max_rows(rows); p.N = G2::CI; p.K = ConvDgradSubZ<G2>::KR;
+    p.k_chunk = p.K; p.batch = rows;
+    p.dz = dz2; p.w = w.w2; p.xprev = a.x1; p.dx = dz1;
+    // Useful FLOPs: every input pixel once, K = KR per class.
+    TORSO_GEMM_F("conv2_dgrad", 2.0 * rows * G2::IPIX * G2::CI * (double)p.K, 256, 32, 4, 1, p,
+                 G2::S * G2::S);
+  }
   // conv1 (no input gradient needed)
   if (u8)
     return conv_wgrad<G1, InU8, 128, 32, 4, 1>(static_cast<const uint8_t*>(obs), dz1, rows,

@@ -50,6 +50,20 @@ const char* acme_version(void);
 /* Name of the GPU the library was built for ("gfx950"). */
 const char* acme_target_arch(void);
 
+/* Matmul engine of the learners' dense layers (process-wide; default from the
+ * ACME_MATMUL environment variable, "x6" unless it says "f32"):
+ *   ACME_MATMUL_X6  f32 operands split exactly into three bf16 planes, six bf16 MFMAs
+ *                   per 16-deep k step, f32 accumulation: f32-equivalent error
+ *                   (csrc/gemm_x6.h), 2.7x the MFMA rate of
+ *   ACME_MATMUL_F32 v_mfma_f32_32x32x2_f32 (exact f32 products, csrc/gemm.h). */
+enum { ACME_MATMUL_F32 = 0, ACME_MATMUL_X6 = 1 };
+int acme_set_matmul_engine(int32_t engine);
+int32_t acme_matmul_engine(void);
+/* One dense layer on the current engine: y[rows, out] = act(x[rows, in] @ w[in, out] + b)
+ * (act: 0 none, 1 relu, 2 elu, 3 tanh); in and out multiples of 4.  Device pointers. */
+int acme_dense_forward(const float* x, int64_t rows, int64_t in, const float* w, const float* b,
+                       int64_t out, int32_t act, float* y, void* stream);
+
 /* ------------------------------------------------------------------ replay -- */
 
 #define ACME_MAX_FIELDS 8
