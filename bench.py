@@ -332,6 +332,23 @@ def setup_impala(args, world, rank, dev):
             lambda: impala_cpu_baseline(B, T, args.cpu_baseline_seconds))
 
 
+def pmc_traffic(workload: str, section: str):
+    """HBM bytes per launch of `section` from the newest committed PMC summary
+    (profiles/<round>/pmc_traffic_<workload>.json, written by tools/pmc_traffic.py from
+    separate rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench); (None, None) if absent."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"pmc_traffic_{workload}.json")))
+    for path in reversed(paths):
+        try:
+            with open(path) as f:
+                k = json.load(f)["kernels"].get(section)
+        except (OSError, ValueError, KeyError):
+            continue
+        if k:
+            return int(k["bytes"]), os.path.relpath(path, ROOT)
+    return None, None
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -415,9 +432,11 @@ def main():
     mfma = [s for s in sections if s.get("bound") == "mfma"]
     if mfma:
         dom = mfma[0]
+        traffic, src = pmc_traffic(args.workload, dom["name"])
         roofline = dict(bound="mfma", kernel=dom["name"], achieved=dom["achieved"],
                         peak=FP32_MFMA_PEAK_TFLOPS, unit="TFLOP/s", frac=dom["frac"],
-                        traffic=None, avg_us=dom["avg_us"])
+                        traffic=traffic, traffic_unit="bytes/launch", traffic_source=src,
+                        avg_us=dom["avg_us"])
     if rank == 0:
         for s in sections:
             print(f"[bench] {s['name']:16s} {s['launches']:6d} x {s['avg_us']:9.2f} us  "

@@ -1,0 +1,104 @@
+#!/usr/bin/env python3
+"""Per-kernel HBM traffic from rocprofv3 PMC passes (FETCH_SIZE and WRITE_SIZE collected
+in SEPARATE passes with --kernel-trace only, MI355X_MICROARCH.md § HBM):
+
+  bytes_read  = 2 x FETCH_SIZE x 1024   (FETCH_SIZE is in KB and, on gfx950, reports half
+                                        the bytes of wide 16-B-per-lane reads)
+  bytes_write = WRITE_SIZE x 1024       (exact for 16-B-per-lane stores and float atomics;
+                                        narrower stores are uncalibrated)
+
+averaged per launch and keyed by the library's profiler section names (the names bench.py
+reports), so bench.py can put the dominant kernel's measured traffic next to its
+algorithmic bytes.  Usage:
+    tools/pmc_traffic.py <workload> <fetch_dir> <write_dir> <out.json>
+"""
+import collections
+import csv
+import glob
+import json
+import re
+import sys
+
+# kernel symbol pattern -> profiler section name (first match wins), per workload
+SECTIONS_D4PG = [
+    (r"DenseFwd<true.*|gemm_\w+_kernel<32, 32, 1, 1, 16, 4, acme::conv::DenseFwd<true", "d4pg_mlp_fwd"),
+    (r"gemm_\w+_kernel<32, 32, 1, 1, 16, 4, acme::conv::DenseDgrad<true", "d4pg_mlp_dgrad"),
+    (r"gemm_\w+_kernel<32, 32, 1, 1, 16, 4, acme::conv::DenseWgrad<true", "d4pg_mlp_wgrad"),
+    (r"ln_bwd_kernel", "d4pg_ln_bwd"),
+    (r"ln_first_kernel", "d4pg_ln_first"),
+    (r"clip_adam_kernel", "d4pg_adam"),
+]
+SECTIONS_IMPALA = [
+    (r"DenseDgrad<true", "impala_feat_dgrad"),
+    (r"OarFwd", "impala_oar_fwd"),
+    (r"OarWgrad", "impala_wi_wgrad"),
+    (r"lstm_fwd_step", "impala_lstm_fwd_step"),
+    (r"lstm_bwd_step", "impala_lstm_bwd_step"),
+    (r"clip_adam_kernel", "impala_adam"),
+    (r"ConvFwd<acme::conv::Geom<84,", "conv1_fwd"),
+    (r"ConvFwd<acme::conv::Geom<21,", "conv2_fwd"),
+    (r"ConvFwd<acme::conv::Geom<11,", "conv3_fwd"),
+    (r"ConvWgrad<acme::conv::Geom<84,", "conv1_wgrad"),
+    (r"ConvWgrad<acme::conv::Geom<21,", "conv2_wgrad"),
+    (r"ConvWgrad<acme::conv::Geom<11,", "conv3_wgrad"),
+    (r"ConvDgradSub", "conv2_dgrad"),
+    (r"ConvDgrad<", "conv3_dgrad"),
+]
+SECTIONS = [
+    (r"gemm_\w+_kernel<128, 128, 2, 2,.*DenseFwd<true", "fc_fwd"),
+    (r"ConvFwd<acme::conv::Geom<84,", "conv1_fwd"),
+    (r"ConvFwd<acme::conv::Geom<21,", "conv2_fwd"),
+    (r"ConvFwd<acme::conv::Geom<11,", "conv3_fwd"),
+    (r"DenseWgrad<true", "fc_wgrad"),
+    (r"DenseDgrad<true", "fc_dgrad"),
+    (r"ConvWgrad<acme::conv::Geom<84,", "conv1_wgrad"),
+    (r"ConvWgrad<acme::conv::Geom<21,", "conv2_wgrad"),
+    (r"ConvWgrad<acme::conv::Geom<11,", "conv3_wgrad"),
+    (r"ConvDgradSub", "conv2_dgrad"),
+    (r"ConvDgrad<", "conv3_dgrad"),
+    (r"(?<!clip_)adam_kernel", "adam"),
+    (r"gather_fields_kernel", "replay_gather"),
+]
+TABLES = {"dqn": SECTIONS, "d4pg": SECTIONS_D4PG, "impala": SECTIONS_IMPALA}
+TABLE = SECTIONS
+
+
+def section(name):
+    for pat, sec in TABLE:
+        if re.search(pat, name):
+            return sec
+    return None
+
+
+def per_launch(d, counter):
+    vals = collections.defaultdict(list)
+    for path in glob.glob(f"{d}/*counter_collection.csv"):
+        for r in csv.DictReader(open(path)):
+            if r["Counter_Name"] != counter:
+                continue
+            sec = section(r["Kernel_Name"])
+            if sec:
+                vals[sec].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in vals.items()}
+
+
+def main():
+    global TABLE
+    workload, fetch_dir, write_dir, out = sys.argv[1:5]
+    TABLE = TABLES[workload]
+    f = per_launch(fetch_dir, "FETCH_SIZE")
+    w = per_launch(write_dir, "WRITE_SIZE")
+    res = {}
+    for sec in sorted(set(f) | set(w)):
+        rd = 2.0 * 1024.0 * f.get(sec, 0.0)
+        wr = 1024.0 * w.get(sec, 0.0)
+        res[sec] = {"read_bytes": round(rd), "write_bytes": round(wr), "bytes": round(rd + wr)}
+    json.dump({"method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes; "
+                         "read = 2 x FETCH_SIZE KB (gfx950 half-count of 16-B reads), write = "
+                         "WRITE_SIZE KB; per launch", "kernels": res}, open(out, "w"), indent=1)
+    for k, v in res.items():
+        print(f"{k:22s} {v['bytes'] / 1e6:10.1f} MB/launch")
+
+
+if __name__ == "__main__":
+    main()
