@@ -132,6 +132,9 @@ _SIGS = {
     "acme_dqn_forward_backward": (c_i32, [c_vp, ctypes.POINTER(TransitionBatch),
                                           ctypes.POINTER(DQNOutputs), c_vp]),
     "acme_dqn_apply": (c_i32, [c_vp, c_vp]),
+    "acme_dqn_forward_backward_stage": (c_i32, [c_vp, ctypes.POINTER(TransitionBatch),
+                                                ctypes.POINTER(DQNOutputs), c_i32, c_vp]),
+    "acme_dqn_grad_split": (c_i32, [c_vp, ctypes.POINTER(c_i64)]),
     "acme_dqn_step": (c_i32, [c_vp, ctypes.POINTER(TransitionBatch), ctypes.POINTER(DQNOutputs),
                               c_vp]),
     "acme_dqn_q_values": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp]),

@@ -69,6 +69,7 @@ class DQNLearner(core.Learner, core.Saveable):
                 for buf in (self._native.params, self._native.target):
                     dist.broadcast(buf, src=0)
                 self._gmin = torch.empty(1, dtype=torch.float64, device=self._native.device)
+                self._grad_split = self._native.grad_split
                 self._avg_op = (dist.ReduceOp.AVG if dist.get_backend() == "nccl" else None)
 
     # ------------------------------------------------------------------ step
@@ -92,16 +93,25 @@ class DQNLearner(core.Learner, core.Saveable):
         if self._dist is None:
             self._native.step(*batch)
         else:
+            # Gradient all-reduce in two buckets overlapped with the backward pass: the dense
+            # layers' gradients (the buffer's tail, ~99% of the bytes) are reduced on the
+            # collective stream while the torso backward runs on the compute stream.
             dist = self._dist
-            self._native.batch_min_probability(batch[5], self._gmin)
+            n = self._native
+            n.batch_min_probability(batch[5], self._gmin)
             dist.all_reduce(self._gmin, op=dist.ReduceOp.MIN)
-            self._native.forward_backward(*batch, global_min_probability=self._gmin)
-            if self._avg_op is not None:  # RCCL has a native average
-                dist.all_reduce(self._native.grads, op=self._avg_op)
-            else:  # gloo: sum, then scale
-                dist.all_reduce(self._native.grads, op=dist.ReduceOp.SUM)
-                self._native.grads.mul_(1.0 / dist.get_world_size())
-            self._native.apply()
+            n.forward_backward_stage(0, *batch, global_min_probability=self._gmin)
+            split = self._grad_split
+            tail, head = n.grads[split:], n.grads[:split]
+            op = self._avg_op if self._avg_op is not None else dist.ReduceOp.SUM
+            work = dist.all_reduce(tail, op=op, async_op=True)
+            n.forward_backward_stage(1, *batch, global_min_probability=self._gmin)
+            if split > 0:
+                dist.all_reduce(head, op=op)
+            work.wait()
+            if self._avg_op is None:  # gloo: sum, then scale
+                n.grads.mul_(1.0 / dist.get_world_size())
+            n.apply()
         if self._replay_client is not None:
             self._replay_client.update_priorities(table=adders.DEFAULT_PRIORITY_TABLE,
                                                   keys=keys,

@@ -314,11 +314,7 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st) {
       default: ACME_GEMM_NK("fc_dgrad", 64, 128, 2, 2, 16, p, 1); break;
     }
   }
-  torso::Grads g{Pm(l, gr, l->t_c1w), Pm(l, gr, l->t_c1b), Pm(l, gr, l->t_c2w),
-                 Pm(l, gr, l->t_c2b), Pm(l, gr, l->t_c3w), Pm(l, gr, l->t_c3b)};
-  return torso::backward(torso_weights(l, prm), g, l->cfg.obs_dtype == ACME_OBS_U8_SCALED,
-                         o_tm1, B, torso::Acts{l->x1, l->x2, l->x3}, l->dz3, l->dz2, l->dz1,
-                         l->slab, st);
+  return ACME_OK;  // the torso backward is stage 1 (acme_dqn_forward_backward_stage)
 }
 
 template <class In>
@@ -561,9 +557,10 @@ int acme_dqn_q_values(acme_dqn* l, const void* obs, int64_t batch, int32_t use_t
   return mlp_forward(l, prm, obs, obs, B, B, l->mlp_tact, q_out, st);
 }
 
-int acme_dqn_forward_backward(acme_dqn* l, const acme_transition_batch* batch,
-                              const acme_dqn_outputs* out, void* stream) {
+int acme_dqn_forward_backward_stage(acme_dqn* l, const acme_transition_batch* batch,
+                                    const acme_dqn_outputs* out, int32_t stage, void* stream) {
   ACME_CHECK_ARG(l && batch && l->params, "null argument or unbound learner");
+  ACME_CHECK_ARG(stage == 0 || stage == 1, "stage must be 0 or 1");
   ACME_CHECK_ARG(batch->o_tm1 && batch->a_tm1 && batch->r_t && batch->d_t && batch->o_t &&
                      batch->probabilities,
                  "transition batch has null fields");
@@ -571,12 +568,22 @@ int acme_dqn_forward_backward(acme_dqn* l, const acme_transition_batch* batch,
                  "batch %lld outside [1, max_batch=%d]", (long long)batch->batch, l->cfg.max_batch);
   hipStream_t st = as_stream(stream);
   const int B = (int)batch->batch;
+  const bool nature = l->cfg.network == ACME_NET_NATURE_DQN;
+  if (stage == 1) {
+    // Torso weight gradients (the flat buffer's head, [0, grad_split)).  Every gradient
+    // element is written by its kernel (no accumulation), so nothing is cleared.
+    if (!nature) return ACME_OK;
+    torso::Grads g{Pm(l, l->grads, l->t_c1w), Pm(l, l->grads, l->t_c1b), Pm(l, l->grads, l->t_c2w),
+                   Pm(l, l->grads, l->t_c2b), Pm(l, l->grads, l->t_c3w), Pm(l, l->grads, l->t_c3b)};
+    return torso::backward(torso_weights(l, l->params), g,
+                           l->cfg.obs_dtype == ACME_OBS_U8_SCALED, batch->o_tm1, B,
+                           torso::Acts{l->x1, l->x2, l->x3}, l->dz3, l->dz2, l->dz1, l->slab, st);
+  }
   const int A = l->cfg.num_actions;
   int rc;
-  ACME_HIP_TRY(hipMemsetAsync(l->grads, 0, l->flat * sizeof(float), st));
   // Forward: online on [o_tm1; o_t] (q_tm1 rows 0..B-1, q_t_selector rows B..2B-1),
   // target on o_t (q_t_value).
-  if (l->cfg.network == ACME_NET_NATURE_DQN) {
+  if (nature) {
     if ((rc = nature_forward(l, l->params, batch->o_tm1, batch->o_t, B, 2 * B, l->x1, l->x2, l->x3,
                              l->hid, l->q_on, st)) != ACME_OK)
       return rc;
@@ -620,8 +627,20 @@ int acme_dqn_forward_backward(acme_dqn* l, const acme_transition_batch* batch,
   if (out && out->q_tm1)
     ACME_HIP_TRY(hipMemcpyAsync(out->q_tm1, l->q_on, (size_t)B * A * sizeof(float),
                                 hipMemcpyDeviceToDevice, st));
-  return l->cfg.network == ACME_NET_NATURE_DQN ? nature_backward(l, batch->o_tm1, B, st)
-                                               : mlp_backward(l, batch->o_tm1, B, st);
+  return nature ? nature_backward(l, batch->o_tm1, B, st) : mlp_backward(l, batch->o_tm1, B, st);
+}
+
+int acme_dqn_forward_backward(acme_dqn* l, const acme_transition_batch* batch,
+                              const acme_dqn_outputs* out, void* stream) {
+  int rc = acme_dqn_forward_backward_stage(l, batch, out, 0, stream);
+  if (rc != ACME_OK) return rc;
+  return acme_dqn_forward_backward_stage(l, batch, out, 1, stream);
+}
+
+int acme_dqn_grad_split(const acme_dqn* l, int64_t* split) {
+  ACME_CHECK_ARG(l && split, "null argument");
+  *split = l->cfg.network == ACME_NET_NATURE_DQN ? l->tensors[l->t_fcw].offset : 0;
+  return ACME_OK;
 }
 
 int acme_dqn_apply(acme_dqn* l, void* stream) {

@@ -310,6 +310,22 @@ class NativeDQN:
         check(lib().acme_dqn_forward_backward(self._h, ctypes.byref(tb), ctypes.byref(out),
                                               stream_ptr(stream)), "dqn forward_backward")
 
+    def forward_backward_stage(self, stage: int, *batch, global_min_probability=None,
+                               q_tm1=None, stream=None):
+        """Stage 0: forwards, loss, head/dense backward (grads[grad_split:]); stage 1: torso
+        backward (grads[:grad_split])."""
+        tb = self._batch(*batch, global_min_probability=global_min_probability)
+        out = self._outputs(q_tm1)
+        check(lib().acme_dqn_forward_backward_stage(self._h, ctypes.byref(tb), ctypes.byref(out),
+                                                    int(stage), stream_ptr(stream)),
+              f"dqn forward_backward stage {stage}")
+
+    @property
+    def grad_split(self) -> int:
+        s = ctypes.c_int64()
+        check(lib().acme_dqn_grad_split(self._h, ctypes.byref(s)))
+        return int(s.value)
+
     def batch_min_probability(self, probabilities: torch.Tensor, out: torch.Tensor, stream=None):
         """out[0] = min(probabilities) on the device (data-parallel IS normaliser)."""
         check(lib().acme_min_f64(ptr(probabilities), int(probabilities.numel()), ptr(out),

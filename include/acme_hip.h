@@ -190,6 +190,13 @@ typedef struct acme_dqn_outputs {
 /* Forward + backward: fills grads (flat) and outputs.  Does not touch params. */
 int acme_dqn_forward_backward(acme_dqn* l, const acme_transition_batch* batch,
                               const acme_dqn_outputs* out, void* stream);
+/* The same work in two stages, for data parallelism that overlaps the gradient
+ * all-reduce with the rest of the backward pass: stage 0 = forwards, loss, head and
+ * dense-layer backward (writes grads[grad_split:]); stage 1 = torso backward (writes
+ * grads[:grad_split]; a no-op for MLP networks, whose grad_split is 0). */
+int acme_dqn_forward_backward_stage(acme_dqn* l, const acme_transition_batch* batch,
+                                    const acme_dqn_outputs* out, int32_t stage, void* stream);
+int acme_dqn_grad_split(const acme_dqn* l, int64_t* split);
 /* Adam on (params, grads), then target <- params when num_steps % period == 0, then
  * num_steps += 1 (acme/agents/tf/dqn/learning.py:147-161). */
 int acme_dqn_apply(acme_dqn* l, void* stream);
