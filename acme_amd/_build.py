@@ -20,7 +20,7 @@ ARCH = os.environ.get("ACME_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", CSRC, "-I", INCLUDE,
-          "-Wall", "-Wno-unused-result"]
+          "-Wall", "-Wno-unused-result"] + os.environ.get("ACME_EXTRA_CFLAGS", "").split()
 
 
 def _sources():

@@ -129,6 +129,7 @@ _SIGS = {
                                      ctypes.POINTER(c_i32), ctypes.POINTER(c_i64),
                                      ctypes.POINTER(ctypes.c_char_p)]),
     "acme_dqn_bind": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "acme_dqn_params_changed": (c_i32, [c_vp]),
     "acme_dqn_forward_backward": (c_i32, [c_vp, ctypes.POINTER(TransitionBatch),
                                           ctypes.POINTER(DQNOutputs), c_vp]),
     "acme_dqn_apply": (c_i32, [c_vp, c_vp]),

@@ -68,6 +68,7 @@ class DQNLearner(core.Learner, core.Saveable):
                 self._dist = dist
                 for buf in (self._native.params, self._native.target):
                     dist.broadcast(buf, src=0)
+                self._native.params_changed()
                 self._gmin = torch.empty(1, dtype=torch.float64, device=self._native.device)
                 self._grad_split = self._native.grad_split
                 self._avg_op = (dist.ReduceOp.AVG if dist.get_backend() == "nccl" else None)
@@ -160,4 +161,5 @@ class DQNLearner(core.Learner, core.Saveable):
             views = n.views(buf)
             for k, t in views.items():
                 t.copy_(torch.as_tensor(np.asarray(src[k], np.float32)).view(t.shape))
+        n.params_changed()
         n.num_steps = int(state["num_steps"])

@@ -19,6 +19,10 @@ namespace acme {
 
 void set_error(const char* fmt, ...);
 
+// Tile / schedule variant for tuning runs: ACME_V_<KEY>=<n> in the environment (read once
+// per key); 0 is the shipped default.
+int tune_variant(const char* key);
+
 #define ACME_HIP_TRY(expr)                                                   \
   do {                                                                       \
     hipError_t _e = (expr);                                                  \

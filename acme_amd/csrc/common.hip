@@ -2,6 +2,10 @@
 #include "common.h"
 
 #include <cstring>
+#include <mutex>
+#include <string>
+#include <utility>
+#include <vector>
 
 namespace acme {
 
@@ -12,6 +16,18 @@ void set_error(const char* fmt, ...) {
   va_start(ap, fmt);
   vsnprintf(g_last_error, sizeof(g_last_error), fmt, ap);
   va_end(ap);
+}
+
+int tune_variant(const char* key) {
+  static std::mutex mu;
+  static std::vector<std::pair<std::string, int>> cache;
+  std::lock_guard<std::mutex> lock(mu);
+  for (auto& kv : cache)
+    if (kv.first == key) return kv.second;
+  const char* v = getenv((std::string("ACME_V_") + key).c_str());
+  const int x = v ? atoi(v) : 0;
+  cache.emplace_back(key, x);
+  return x;
 }
 
 namespace gemm {

@@ -24,7 +24,9 @@
 
 #include "common.h"
 #include "conv.h"
+#include "conv_p3.h"
 #include "gemm.h"
+#include "gemm_p3.h"
 #include "gemm_x6.h"
 #include "kernels.h"
 #include "profiler.h"
@@ -81,6 +83,14 @@ struct acme_dqn {
   float* loss_tmp = nullptr;
   float* td_tmp = nullptr;
   double* prio_tmp = nullptr;
+  // Plane path (gemm_p3.h; Nature network on uint8 frames, x6 engine): exact bf16 planes
+  // of the parameters / target parameters ([3][flat]) and of every GEMM operand.
+  bool p3_capable = false;
+  bool planes_stale = true;  // parameter planes need a refresh from the f32 buffers
+  bool last_p3 = false;      // the last forward/backward ran the plane path
+  uint16_t *wpl = nullptr, *tpl = nullptr;
+  uint16_t* frames = nullptr;  // bf16 copies of [o_tm1; o_t] (2B frames)
+  torso::Plane x1p{}, x2p{}, x3p{}, t1p{}, t2p{}, t3p{}, dzhp{}, dz3p{}, dz2p{}, dz1p{};
 };
 
 namespace {
@@ -116,10 +126,36 @@ int dev_alloc(acme_dqn* l, T** p, int64_t count) {
   return ACME_OK;
 }
 
+int plane_alloc(acme_dqn* l, torso::Plane* x, int64_t count) {
+  const int64_t stride = align64(count);
+  uint16_t* p = nullptr;
+  int rc = dev_alloc(l, &p, 3 * stride);
+  if (rc != ACME_OK) return rc;
+  *x = torso::Plane{p, stride};
+  return ACME_OK;
+}
+
 inline const float* P(const acme_dqn* l, const float* base, int t) {
   return base + l->tensors[t].offset;
 }
 inline float* Pm(const acme_dqn* l, float* base, int t) { return base + l->tensors[t].offset; }
+// Plane view of parameter tensor t in a [3][flat] parameter-plane buffer.
+inline torso::Plane WP(const acme_dqn* l, uint16_t* base, int t) {
+  return torso::Plane{base + l->tensors[t].offset, l->flat};
+}
+inline CPlanes CP(const torso::Plane& x) { return CPlanes{x.p, x.stride}; }
+inline gemm::PlaneSrc SRC(const torso::Plane& x, int64_t elems) {
+  return gemm::PlaneSrc{x.p, x.stride, (int32_t)(2 * elems)};
+}
+// bf16 frames of obs_a (rows [0, split)) and obs_b (the rest) into l->frames.
+int convert_frames(acme_dqn* l, const void* obs_a, const void* obs_b, int split, int rows,
+                   hipStream_t st) {
+  ACME_PROF("frames_bf16", st, 0.0, 3.0 * (double)rows * kObsBytes);
+  return launch_frames_bf16(static_cast<const uint8_t*>(obs_a), static_cast<const uint8_t*>(obs_b),
+                            split, rows, kObsBytes, l->frames, st);
+}
+inline Planes PP(const torso::Plane& x) { return Planes{x.p, x.stride}; }
+bool use_p3(const acme_dqn* l) { return l->p3_capable && gemm::use_x6(); }
 
 // Split-K helper: chunk size (multiple of BK) for `splits` splits of K.
 inline int chunk_for(int K, int splits) {
@@ -143,17 +179,7 @@ inline int chunk_for(int K, int splits) {
   } while (0)
 #define ACME_GEMM_N(name, BM, BN, WM, WN, prob, splits) \
   ACME_GEMM_F(name, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, BM, BN, WM, WN, prob, splits)
-// Tile variant selection for tuning runs: ACME_V_<KEY>=<n> in the environment (read once
-// per key); 0 is the shipped default.
-int tune(const char* key) {
-  static std::vector<std::pair<std::string, int>> cache;
-  for (auto& kv : cache)
-    if (kv.first == key) return kv.second;
-  const char* v = getenv((std::string("ACME_V_") + key).c_str());
-  const int x = v ? atoi(v) : 0;
-  cache.emplace_back(key, x);
-  return x;
-}
+int tune(const char* key) { return tune_variant(key); }
 
 // Same with an explicit reduction stage depth BK (16 or 32).
 #ifndef ACME_BIG_BK
@@ -163,6 +189,16 @@ int tune(const char* key) {
   do {                                                                                         \
     ACME_PROF(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0);   \
     hipError_t _e = gemm::launch_matmul<BM, BN, WM, WN, BKV>(prob, splits, st);               \
+    if (_e != hipSuccess) {                                                                    \
+      set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
+      return ACME_ERR_HIP;                                                                     \
+    }                                                                                          \
+  } while (0)
+
+#define ACME_P3_GEMM(name, BM, BN, WM, WN, BKV, prob, splits)                                \
+  do {                                                                                         \
+    ACME_PROF(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0);   \
+    hipError_t _e = gemm::launch_gemm_p3<BM, BN, WM, WN, BKV>(prob, splits, st);              \
     if (_e != hipSuccess) {                                                                    \
       set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
       return ACME_ERR_HIP;                                                                     \
@@ -192,13 +228,26 @@ torso::Weights torso_weights(const acme_dqn* l, const float* prm) {
                         P(l, prm, l->t_c2b), P(l, prm, l->t_c3w), P(l, prm, l->t_c3b)};
 }
 
+// Duelling value/advantage outputs as one skinny split-K GEMM + epilogue kernel.
+int head_forward(acme_dqn* l, const float* prm, int rows, const float* hid, float* q,
+                 hipStream_t st) {
+  const int A = l->cfg.num_actions;
+  DuelHeadFwd p;
+  p.M = rows; p.N = A + 1; p.K = 2 * kHidden; p.k_chunk = chunk_for(p.K, kHeadFwdSplits);
+  p.H = kHidden; p.A = A; p.h = hid; p.wv = P(l, prm, l->t_vw); p.wa = P(l, prm, l->t_aw);
+  p.slab = l->slab;
+  ACME_GEMM_N("head_fwd", 64, 32, 2, 1, p, kHeadFwdSplits);
+  ACME_PROF("head_fwd_finish", st, 0.0, 0.0);
+  return launch_duel_head_finish(l->slab, kHeadFwdSplits, rows, A, P(l, prm, l->t_vb),
+                                 P(l, prm, l->t_ab), q, st);
+}
+
 // ---------------------------------------------------------------- Nature forward
 // rows = number of observations; first `split` rows from obs_a, the rest from obs_b.
 int nature_forward(acme_dqn* l, const float* prm, const void* obs_a, const void* obs_b,
                    int split, int rows, float* x1, float* x2, float* x3, float* hid,
                    float* q, hipStream_t st) {
   const bool u8 = l->cfg.obs_dtype == ACME_OBS_U8_SCALED;
-  const int A = l->cfg.num_actions;
   int rc0 = torso::forward(torso_weights(l, prm), u8, obs_a, obs_b, split, rows,
                            torso::Acts{x1, x2, x3}, st);
   if (rc0 != ACME_OK) return rc0;
@@ -221,16 +270,35 @@ int nature_forward(acme_dqn* l, const float* prm, const void* obs_a, const void*
                          2 * kHidden, 1, "fc_fwd_reduce", st);
     if (rc != ACME_OK) return rc;
   }
-  {  // Duelling value/advantage outputs as one skinny split-K GEMM + epilogue kernel.
-    DuelHeadFwd p;
-    p.M = rows; p.N = A + 1; p.K = 2 * kHidden; p.k_chunk = chunk_for(p.K, kHeadFwdSplits);
-    p.H = kHidden; p.A = A; p.h = hid; p.wv = P(l, prm, l->t_vw); p.wa = P(l, prm, l->t_aw);
-    p.slab = l->slab;
-    ACME_GEMM_N("head_fwd", 64, 32, 2, 1, p, kHeadFwdSplits);
-    ACME_PROF("head_fwd_finish", st, 0.0, 0.0);
-    return launch_duel_head_finish(l->slab, kHeadFwdSplits, rows, A, P(l, prm, l->t_vb),
-                                   P(l, prm, l->t_ab), q, st);
+  return head_forward(l, prm, rows, hid, q, st);
+}
+
+// Nature forward on the plane path: torso and the fused hidden layer read exact bf16
+// planes (gemm_p3.h); `wpl` are the planes of `prm`.
+int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const uint16_t* frames,
+                      int rows, const torso::Plane& x1, const torso::Plane& x2,
+                      const torso::Plane& x3, float* hid, float* q, hipStream_t st) {
+  torso::PWeights w{WP(l, wpl, l->t_c1w), WP(l, wpl, l->t_c2w), WP(l, wpl, l->t_c3w),
+                    P(l, prm, l->t_c1b), P(l, prm, l->t_c2b), P(l, prm, l->t_c3b)};
+  int rc = torso::forward_p3(w, frames, rows, torso::PActs{x1, x2, x3}, st);
+  if (rc != ACME_OK) return rc;
+  {
+    P3DenseFwd p;
+    const int splits = kFcFwdSplits;
+    p.M = rows; p.N = 2 * kHidden; p.K = kFlat; p.k_chunk = chunk_for(kFlat, splits);
+    p.a_src = SRC(x3, (int64_t)rows * kFlat); p.ldx = kFlat;
+    p.b_src = SRC(WP(l, wpl, l->t_fcw), (int64_t)kFlat * 2 * kHidden); p.slab = l->slab;
+    switch (tune("P3FCF")) {
+      case 1: ACME_P3_GEMM("fc_fwd", 128, 128, 2, 2, 16, p, splits); break;
+      case 2: ACME_P3_GEMM("fc_fwd", 256, 128, 4, 2, 16, p, splits); break;
+      default: ACME_P3_GEMM("fc_fwd", 128, 128, 2, 2, 32, p, splits); break;
+    }
+    const int64_t cnt = (int64_t)rows * 2 * kHidden;
+    rc = slab_reduce(l->slab, splits, cnt, hid, cnt, nullptr, P(l, prm, l->t_fcb), 2 * kHidden, 1,
+                     "fc_fwd_reduce", st);
+    if (rc != ACME_OK) return rc;
   }
+  return head_forward(l, prm, rows, hid, q, st);
 }
 
 // ---------------------------------------------------------------- MLP forward
@@ -279,11 +347,13 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st) {
   const float* prm = l->params;
   float* gr = l->grads;
   const int A = l->cfg.num_actions;
+  const bool p3 = use_p3(l);
   int rc;
   {  // Head: dZ of the fused hidden layer (masked by its ReLU).
     ACME_PROF("head_dz", st, 0.0, 0.0);
     rc = launch_duel_head_dz(l->hid, l->g, l->a_cache, B, kHidden, A, P(l, prm, l->t_vw),
-                             P(l, prm, l->t_aw), l->dzh, st);
+                             P(l, prm, l->t_aw), l->dzh, st, p3 ? l->dzhp.p : nullptr,
+                             l->dzhp.stride);
     if (rc != ACME_OK) return rc;
   }
   {  // Head weight / bias gradients: one skinny GEMM over the batch + scatter.
@@ -296,6 +366,32 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st) {
                                        Pm(l, gr, l->t_vb), Pm(l, gr, l->t_aw), Pm(l, gr, l->t_ab),
                                        st);
     if (rc != ACME_OK) return rc;
+  }
+  if (p3) {
+    {  // FC weight + bias grad: [7744, 1024] = x3^T dZh (reduction over the batch).
+      P3DenseWgrad p;
+      p.M = kFlat; p.N = 2 * kHidden; p.K = B; p.k_chunk = B;
+      p.a_src = SRC(l->x3p, (int64_t)B * kFlat); p.ldx = kFlat;
+      p.b_src = SRC(l->dzhp, (int64_t)B * 2 * kHidden); p.out = Pm(l, gr, l->t_fcw);
+      p.bias_out = Pm(l, gr, l->t_fcb);
+      switch (tune("P3FCW")) {
+        case 1: ACME_P3_GEMM("fc_wgrad", 128, 128, 2, 2, 32, p, 1); break;
+        default: ACME_P3_GEMM("fc_wgrad", 128, 128, 2, 2, 16, p, 1); break;
+      }
+    }
+    {  // FC input grad -> dZ3 planes (masked by conv3's ReLU).
+      P3DenseDgrad p;
+      p.M = B; p.N = kFlat; p.K = 2 * kHidden; p.k_chunk = p.K;
+      p.a_src = SRC(l->dzhp, (int64_t)B * 2 * kHidden);
+      p.b_src = SRC(WP(l, l->wpl, l->t_fcw), (int64_t)kFlat * 2 * kHidden); p.xprev = CP(l->x3p);
+      p.ldx = kFlat; p.dx = PP(l->dz3p);
+      switch (tune("P3FCD")) {
+        case 1: ACME_P3_GEMM("fc_dgrad", 64, 128, 2, 2, 32, p, 1); break;
+        case 2: ACME_P3_GEMM("fc_dgrad", 64, 128, 2, 2, 16, p, 1); break;
+        default: ACME_P3_GEMM("fc_dgrad", 128, 128, 2, 2, 32, p, 1); break;
+      }
+    }
+    return ACME_OK;
   }
   {  // FC weight + bias grad: [7744, 1024] = x3^T dZh (reduction over the batch).
     DenseWgrad<true> p;
@@ -373,6 +469,15 @@ int mlp_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st) {
   return ACME_OK;
 }
 
+// Refreshes the parameter planes from the f32 parameter buffers.
+int sync_planes(acme_dqn* l, hipStream_t st) {
+  if (!l->p3_capable || !l->planes_stale) return ACME_OK;
+  int rc = launch_split_planes(l->params, l->flat, l->wpl, l->flat, st);
+  if (rc == ACME_OK) rc = launch_split_planes(l->target, l->flat, l->tpl, l->flat, st);
+  if (rc == ACME_OK) l->planes_stale = false;
+  return rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -425,6 +530,24 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
         (rc = dev_alloc(l, &l->dz1, (int64_t)B * G1::OPIX * G1::CO)))
       return fail(rc);
     l->slab_floats = slab_floats_needed(B, A);
+    if (cfg->obs_dtype == ACME_OBS_U8_SCALED) {
+      l->p3_capable = true;
+      const int64_t fl = l->flat;
+      if ((rc = dev_alloc(l, &l->wpl, 3 * fl)) || (rc = dev_alloc(l, &l->tpl, 3 * fl)) ||
+          (rc = dev_alloc(l, &l->frames, (int64_t)R2 * kObsBytes)) ||
+          (rc = plane_alloc(l, &l->x1p, (int64_t)R2 * torso::kX1)) ||
+          (rc = plane_alloc(l, &l->x2p, (int64_t)R2 * kFlat)) ||
+          (rc = plane_alloc(l, &l->x3p, (int64_t)R2 * kFlat)) ||
+          (rc = plane_alloc(l, &l->t1p, (int64_t)B * torso::kX1)) ||
+          (rc = plane_alloc(l, &l->t2p, (int64_t)B * kFlat)) ||
+          (rc = plane_alloc(l, &l->t3p, (int64_t)B * kFlat)) ||
+          (rc = plane_alloc(l, &l->dzhp, (int64_t)B * 2 * kHidden)) ||
+          (rc = plane_alloc(l, &l->dz3p, (int64_t)B * kFlat)) ||
+          (rc = plane_alloc(l, &l->dz2p, (int64_t)B * kFlat)) ||
+          (rc = plane_alloc(l, &l->dz1p, (int64_t)B * torso::kX1)))
+        return fail(rc);
+      l->slab_floats = std::max(l->slab_floats, torso::wgrad_slab_floats_p3());
+    }
   } else {
     ACME_CHECK_ARG(cfg->obs_dim >= 1, "obs_dim must be >= 1");
     ACME_CHECK_ARG(cfg->num_hidden >= 0 && cfg->num_hidden <= ACME_MAX_MLP_LAYERS,
@@ -502,6 +625,13 @@ int acme_dqn_bind(acme_dqn* l, float* params, float* target, float* grads, float
   l->grads = grads;
   l->m = adam_m;
   l->v = adam_v;
+  l->planes_stale = true;
+  return ACME_OK;
+}
+
+int acme_dqn_params_changed(acme_dqn* l) {
+  ACME_CHECK_ARG(l, "null learner");
+  l->planes_stale = true;
   return ACME_OK;
 }
 
@@ -528,6 +658,19 @@ int acme_dqn_debug_buffer(const acme_dqn* l, const char* name, const float** out
              {"q_tg", l->q_tg, B * l->cfg.num_actions}, {"g", l->g, B}};
   for (auto& e : tab)
     if (e.p && std::strcmp(e.n, name) == 0) {
+      if (l->last_p3) {  // the plane path keeps these tensors as planes: join into f32
+        struct {
+          const char* n;
+          torso::Plane pl;
+        } ptab[] = {{"x1", l->x1p},   {"x2", l->x2p},   {"x3", l->x3p},  {"dzh", l->dzhp},
+                    {"dz3", l->dz3p}, {"dz2", l->dz2p}, {"dz1", l->dz1p}};
+        for (auto& q : ptab)
+          if (std::strcmp(q.n, name) == 0) {
+            int rc = launch_join_planes(q.pl.p, q.pl.stride, e.c, const_cast<float*>(e.p), 0);
+            if (rc != ACME_OK) return rc;
+            ACME_HIP_TRY(hipDeviceSynchronize());
+          }
+      }
       *out = e.p;
       *count = e.c;
       return ACME_OK;
@@ -552,6 +695,13 @@ int acme_dqn_q_values(acme_dqn* l, const void* obs, int64_t batch, int32_t use_t
   hipStream_t st = as_stream(stream);
   const float* prm = use_target ? l->target : l->params;
   const int B = (int)batch;
+  if (l->cfg.network == ACME_NET_NATURE_DQN && use_p3(l)) {
+    int rc = sync_planes(l, st);
+    if (rc == ACME_OK) rc = convert_frames(l, obs, obs, B, B, st);
+    if (rc != ACME_OK) return rc;
+    return nature_forward_p3(l, prm, use_target ? l->tpl : l->wpl, l->frames, B, l->t1p, l->t2p,
+                             l->t3p, l->thid, q_out, st);
+  }
   if (l->cfg.network == ACME_NET_NATURE_DQN)
     return nature_forward(l, prm, obs, obs, B, B, l->t1, l->t2, l->t3, l->thid, q_out, st);
   return mlp_forward(l, prm, obs, obs, B, B, l->mlp_tact, q_out, st);
@@ -573,6 +723,17 @@ int acme_dqn_forward_backward_stage(acme_dqn* l, const acme_transition_batch* ba
     // Torso weight gradients (the flat buffer's head, [0, grad_split)).  Every gradient
     // element is written by its kernel (no accumulation), so nothing is cleared.
     if (!nature) return ACME_OK;
+    if (use_p3(l)) {
+      torso::Grads g{Pm(l, l->grads, l->t_c1w), Pm(l, l->grads, l->t_c1b),
+                     Pm(l, l->grads, l->t_c2w), Pm(l, l->grads, l->t_c2b),
+                     Pm(l, l->grads, l->t_c3w), Pm(l, l->grads, l->t_c3b)};
+      torso::PWeights w{WP(l, l->wpl, l->t_c1w), WP(l, l->wpl, l->t_c2w),
+                        WP(l, l->wpl, l->t_c3w), P(l, l->params, l->t_c1b),
+                        P(l, l->params, l->t_c2b), P(l, l->params, l->t_c3b)};
+      return torso::backward_p3(w, g, l->frames, B,
+                                torso::PActs{l->x1p, l->x2p, l->x3p}, l->dz3p, l->dz2p, l->dz1p,
+                                l->slab, st);
+    }
     torso::Grads g{Pm(l, l->grads, l->t_c1w), Pm(l, l->grads, l->t_c1b), Pm(l, l->grads, l->t_c2w),
                    Pm(l, l->grads, l->t_c2b), Pm(l, l->grads, l->t_c3w), Pm(l, l->grads, l->t_c3b)};
     return torso::backward(torso_weights(l, l->params), g,
@@ -583,7 +744,17 @@ int acme_dqn_forward_backward_stage(acme_dqn* l, const acme_transition_batch* ba
   int rc;
   // Forward: online on [o_tm1; o_t] (q_tm1 rows 0..B-1, q_t_selector rows B..2B-1),
   // target on o_t (q_t_value).
-  if (nature) {
+  l->last_p3 = nature && use_p3(l);
+  if (l->last_p3) {
+    if ((rc = sync_planes(l, st)) != ACME_OK) return rc;
+    if ((rc = convert_frames(l, batch->o_tm1, batch->o_t, B, 2 * B, st)) != ACME_OK) return rc;
+    if ((rc = nature_forward_p3(l, l->params, l->wpl, l->frames, 2 * B, l->x1p, l->x2p, l->x3p,
+                                l->hid, l->q_on, st)) != ACME_OK)
+      return rc;
+    if ((rc = nature_forward_p3(l, l->target, l->tpl, l->frames + (size_t)B * kObsBytes, B,
+                                l->t1p, l->t2p, l->t3p, l->thid, l->q_tg, st)) != ACME_OK)
+      return rc;
+  } else if (nature) {
     if ((rc = nature_forward(l, l->params, batch->o_tm1, batch->o_t, B, 2 * B, l->x1, l->x2, l->x3,
                              l->hid, l->q_on, st)) != ACME_OK)
       return rc;
@@ -648,13 +819,18 @@ int acme_dqn_apply(acme_dqn* l, void* stream) {
   hipStream_t st = as_stream(stream);
   const int64_t t = l->num_steps + 1;  // snt.Adam increments its step before the update
   ACME_PROF("adam", st, 0.0, 28.0 * (double)l->logical);
-  int rc = acme_adam_update(l->params, l->grads, l->m, l->v, l->flat, l->cfg.learning_rate,
-                            l->cfg.adam_beta1, l->cfg.adam_beta2, l->cfg.adam_epsilon, t, stream);
+  // The parameter planes (plane path) are refreshed by the same pass.
+  int rc = launch_adam(l->params, l->grads, l->m, l->v, l->flat, l->cfg.learning_rate,
+                       l->cfg.adam_beta1, l->cfg.adam_beta2, l->cfg.adam_epsilon, t,
+                       l->p3_capable ? l->wpl : nullptr, l->flat, st);
   if (rc != ACME_OK) return rc;
   if (l->num_steps % l->cfg.target_update_period == 0) {
     ACME_PROF("target_copy", st, 0.0, 8.0 * (double)l->logical);
     ACME_HIP_TRY(hipMemcpyAsync(l->target, l->params, l->flat * sizeof(float),
                                 hipMemcpyDeviceToDevice, st));
+    if (l->p3_capable)
+      ACME_HIP_TRY(hipMemcpyAsync(l->tpl, l->wpl, 3 * l->flat * sizeof(uint16_t),
+                                  hipMemcpyDeviceToDevice, st));
   }
   l->num_steps += 1;
   return ACME_OK;

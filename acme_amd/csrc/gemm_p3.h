@@ -1,0 +1,463 @@
+// Plane-operand GEMM engine (gfx950 / CDNA4): f32 GEMMs whose operands are ALREADY
+// stored in HBM as exact bf16 planes, so the main loop is plain bf16 MFMA work.
+//
+// An f32 tensor x is kept as three bf16 arrays h, m, l with x = h + m + l exactly
+// (h = bf16(x), m = bf16(x - h), l = bf16(x - h - m); 8 + 8 + 8 significant bits), written
+// once by the kernel that produces x (a GEMM epilogue, the Adam update, a reduction).
+// The product a b is then the six bf16 MFMA terms of gemm_x6.h (hh, hm, mh, hl, lh, mm;
+// the dropped ml, lm, ll are below f32's unit roundoff).  An operand that is exactly a
+// bf16 value (the uint8 Atari frames: integers 0..255) is ONE plane, and its products
+// take 3 MFMAs instead of 6.  Compared with gemm_x6.h, which splits f32 operands while
+// staging every tile (5-6 VALU per element, redone for every block that reads it), the
+// split runs once per element and the staging path is 16-byte loads and stores.
+//
+// Operand modes (of the operand's HBM layout; gemm.h KCONTIG / RCONTIG):
+//   KCONTIG: a load unit is 8 consecutive k of one row  -> LDS [row][k], fragment =
+//            ds_read_b128 (16-B chunks XOR-swizzled by row, conflict-free).
+//   RCONTIG: a load unit is 8 consecutive rows at one k  -> LDS [k][row], fragment =
+//            2 x ds_read_b64_tr_b16 (the hardware transpose read); 32-row segments of a
+//            k-row are XOR-swizzled by k so the four k-rows a 32-lane half reads fall
+//            in four different 64-byte bank windows (conflict-free).
+//
+// Problem concept (conv_p3.h):
+//   static constexpr int A_MODE, B_MODE, A_PLANES, B_PLANES;   (planes 1 or 3)
+//   int M, N, K, k_chunk;
+//   PlaneSrc a_src, b_src;   the operands' plane buffers (read through buffer descriptors)
+//   ARow a_row(int row) const;  uint32_t a_off(const ARow&, int k0, int kk) const;
+//   BRow b_row(int row) const;  uint32_t b_off(const BRow&, int k0, int kk) const;
+//     byte offset (within every plane) of the 16-byte unit at reduction index k0 + kk:
+//     KCONTIG: k .. k+7 of `row`; RCONTIG: rows row .. row+7 at k; kOOB for a unit of
+//     zeros (padding).  k0 is the stage's first k (a multiple of BK, wave-uniform, so the
+//     loaders' k0 arithmetic stays scalar) and kk the unit's offset in the stage.
+//   void store(int m, int n, float v, int split) const;
+//   optional kColSum (+ store_colsum): sum_k B[n][k], computed by one extra MFMA per B
+//   plane against an all-ones A fragment in the blocks of the first row tile;
+//   optional kZClass (+ for_z): blockIdx.z selects a sub-problem.
+// Loads are raw buffer loads: an out-of-range offset returns zeros, so padding and the
+// reduction tail cost no branches.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <type_traits>
+
+#include "gemm.h"
+#include "gemm_x6.h"
+
+namespace acme {
+namespace gemm {
+
+using u32x4 = __attribute__((ext_vector_type(4))) uint32_t;
+using i16x4 = __attribute__((ext_vector_type(4))) short;
+
+__device__ __forceinline__ u32x4 zero_u4() { return u32x4{0u, 0u, 0u, 0u}; }
+
+// Byte offset of a unit of zeros: beyond every plane's descriptor range.
+constexpr uint32_t kOOB = 0x80000000u;
+
+// An operand's plane buffers: plane i at p + i * stride (elements), `bytes` readable
+// bytes per plane (the descriptor range; < 2^31).
+struct PlaneSrc {
+  const uint16_t* p;
+  int64_t stride;
+  int32_t bytes;
+};
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const PlaneSrc& s, int pl) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(s.p + pl * s.stride), (short)0,
+                                           s.bytes, 0x00020000);
+}
+
+// Exact three-way split of an f32 value (bf16 bit patterns).
+__device__ __forceinline__ void split3_bits(float x, uint16_t& h, uint16_t& m, uint16_t& l) {
+  const __bf16 hb = (__bf16)x;
+  const float r = x - (float)hb;
+  const __bf16 mb = (__bf16)r;
+  const __bf16 lb = (__bf16)(r - (float)mb);
+  h = __builtin_bit_cast(uint16_t, hb);
+  m = __builtin_bit_cast(uint16_t, mb);
+  l = __builtin_bit_cast(uint16_t, lb);
+}
+__device__ __forceinline__ float bf16_bits_to_f32(uint16_t b) {
+  return __builtin_bit_cast(float, (uint32_t)b << 16);
+}
+
+// A plane tensor: plane i of element e at p[i * stride + e].
+struct Planes {
+  uint16_t* p;
+  int64_t stride;
+  __device__ __forceinline__ void put(int64_t e, float x) const {
+    uint16_t h, m, l;
+    split3_bits(x, h, m, l);
+    p[e] = h;
+    p[stride + e] = m;
+    p[2 * stride + e] = l;
+  }
+};
+struct CPlanes {
+  const uint16_t* p;
+  int64_t stride;
+  __device__ __forceinline__ u32x4 ld8(int64_t e, int plane) const {
+    return *reinterpret_cast<const u32x4*>(p + plane * stride + e);
+  }
+  // x > 0 of a value whose planes are stored (ReLU masks: h = bf16(x) has x's sign and
+  // is zero only for |x| below bf16's subnormal range).
+  __device__ __forceinline__ bool positive(int64_t e) const {
+    const uint16_t h = p[e];
+    return h != 0 && (h & 0x8000) == 0;
+  }
+  __device__ __forceinline__ float value(int64_t e) const {
+    return (bf16_bits_to_f32(p[e]) + bf16_bits_to_f32(p[stride + e])) +
+           bf16_bits_to_f32(p[2 * stride + e]);
+  }
+};
+
+// Optional vector epilogue: problems with `static constexpr bool kStore8 = true` receive
+// 8 consecutive columns of one row, p.store8(m, n, v[8], split) with n % 8 == 0 (their N
+// must be a multiple of 8).
+template <class P, class = void>
+struct HasStore8 {
+  static constexpr bool value = false;
+};
+template <class P>
+struct HasStore8<P, decltype(void(P::kStore8))> {
+  static constexpr bool value = P::kStore8;
+};
+
+template <int BK>
+__device__ __forceinline__ int p3_kswz(int row) {
+  return BK == 16 ? ((row >> 3) & 1) : ((row >> 2) & 3);
+}
+template <int R>
+__device__ __forceinline__ int p3_rswz(int k) {
+  return R >= 128 ? (k & 3) : (R == 64 ? ((k >> 1) & 1) : 0);
+}
+
+template <int R, int NT, int MODE, int NPL, int BK>
+struct PlanP3 {
+  static_assert(R % 32 == 0, "operand tile rows must be a multiple of 32");
+  static constexpr int PLANE = R * BK * 2;  // bytes of one plane per stage
+  static constexpr int BYTES = NPL * PLANE;
+  static constexpr int CPR = BK / 8;        // KCONTIG: 16-B chunks per row
+  static constexpr int OPK = R / 8;         // RCONTIG: row octets per k
+  static constexpr int UNITS = MODE == KCONTIG ? R * CPR : OPK * BK;
+  static constexpr int PER_THREAD = (UNITS + NT - 1) / NT;
+  static_assert(UNITS % NT == 0 || UNITS < NT, "tile units must divide evenly over the threads");
+  __device__ static __forceinline__ bool owns(int u) { return UNITS >= NT || u < UNITS; }
+  __device__ static __forceinline__ int row_of(int u) {
+    return MODE == KCONTIG ? u / CPR : 8 * (u % OPK);
+  }
+  __device__ static __forceinline__ int kk_of(int u) {
+    return MODE == KCONTIG ? 8 * (u % CPR) : u / OPK;
+  }
+  __device__ static __forceinline__ int offset(int u) {
+    if constexpr (MODE == KCONTIG) {
+      const int row = u / CPR;
+      return row * (2 * BK) + 16 * ((u % CPR) ^ p3_kswz<BK>(row));
+    } else {
+      const int k = u / OPK, row = 8 * (u % OPK);
+      return k * (2 * R) + 2 * (row ^ (p3_rswz<R>(k) << 5));
+    }
+  }
+  // MFMA operand of rows rb .. rb+31 (rb a multiple of 32), k step s (16 k).
+  __device__ static __forceinline__ bf16x8 frag(const uint8_t* tile, int plane, int rb, int s,
+                                                int lane) {
+    const uint8_t* t = tile + plane * PLANE;
+    if constexpr (MODE == KCONTIG) {
+      const int row = rb + (lane & 31);
+      const int c = 2 * s + (lane >> 5);
+      return *reinterpret_cast<const bf16x8*>(t + row * (2 * BK) + 16 * (c ^ p3_kswz<BK>(row)));
+    } else {
+      const int h = lane >> 5, g = (lane >> 4) & 1, q = (lane >> 2) & 3, pp = lane & 3;
+      const int row = rb + 16 * g + 4 * pp;
+      const int k0 = 16 * s + 8 * h + q;
+      const int k1 = k0 + 4;
+      typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+      const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_i16x4*)(t + k0 * (2 * R) + 2 * (row ^ (p3_rswz<R>(k0) << 5))));
+      const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_i16x4*)(t + k1 * (2 * R) + 2 * (row ^ (p3_rswz<R>(k1) << 5))));
+      const __attribute__((ext_vector_type(8))) short v{lo[0], lo[1], lo[2], lo[3],
+                                                        hi[0], hi[1], hi[2], hi[3]};
+      return __builtin_bit_cast(bf16x8, v);
+    }
+  }
+};
+
+template <int BM, int BN, int WM, int WN, int BK, bool DEEP, class P>
+__global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in) {
+  const P p = z_select(p_in);
+  constexpr int NT = 64 * WM * WN;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int MT = TM / 32, NTL = TN / 32;
+  constexpr int NPA = P::A_PLANES, NPB = P::B_PLANES;
+  static_assert(TM % 32 == 0 && TN % 32 == 0, "wave tile must be a multiple of 32x32");
+  static_assert(BK == 16 || BK == 32, "BK must be 16 or 32");
+  static_assert((NPA == 1 || NPA == 3) && (NPB == 1 || NPB == 3), "1 or 3 planes per operand");
+  using PA = PlanP3<BM, NT, P::A_MODE, NPA, BK>;
+  using PB = PlanP3<BN, NT, P::B_MODE, NPB, BK>;
+  constexpr int STAGE = PA::BYTES + PB::BYTES;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int tiles_n = (p.N + BN - 1) / BN;
+  const int tile = blockIdx.x;
+  const int m0 = (tile / tiles_n) * BM;
+  const int n0 = (tile % tiles_n) * BN;
+  const int split = HasZClass<P>::value ? 0 : blockIdx.z;
+  const int kbeg = split * p.k_chunk;
+  int kend = kbeg + p.k_chunk;
+  if (kend > p.K) kend = p.K;
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+
+  typename P::ARow arow[PA::PER_THREAD];
+  typename P::BRow brow[PB::PER_THREAD];
+#pragma unroll
+  for (int i = 0; i < PA::PER_THREAD; ++i)
+    arow[i] = p.a_row(m0 + (PA::owns(tid + i * NT) ? PA::row_of(tid + i * NT) : 0));
+#pragma unroll
+  for (int i = 0; i < PB::PER_THREAD; ++i)
+    brow[i] = p.b_row(n0 + (PB::owns(tid + i * NT) ? PB::row_of(tid + i * NT) : 0));
+
+  __amdgpu_buffer_rsrc_t srcA[NPA], srcB[NPB];
+#pragma unroll
+  for (int pl = 0; pl < NPA; ++pl) srcA[pl] = plane_rsrc(p.a_src, pl);
+#pragma unroll
+  for (int pl = 0; pl < NPB; ++pl) srcB[pl] = plane_rsrc(p.b_src, pl);
+  // Register sets for the global -> LDS staging: with DEEP, stage j is fetched into set
+  // j & 1 two stages ahead of its compute, so a load has a whole iteration (compute,
+  // stash, barrier, compute) to land; otherwise one set, fetched one stage ahead.
+  constexpr int SETS = DEEP ? 2 : 1;
+  u32x4 ra[SETS][PA::PER_THREAD][NPA], rb[SETS][PB::PER_THREAD][NPB];
+  auto fetch = [&](auto S, int k0) {
+    constexpr int set = decltype(S)::value;
+#pragma unroll
+    for (int i = 0; i < PA::PER_THREAD; ++i) {
+      const int u = tid + i * NT;
+      const int kk = PA::kk_of(u);
+      const uint32_t off = (PA::owns(u) && k0 + kk < kend) ? p.a_off(arow[i], k0, kk) : kOOB;
+#pragma unroll
+      for (int pl = 0; pl < NPA; ++pl)
+        ra[set][i][pl] =
+            __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srcA[pl], off, 0, 0));
+    }
+#pragma unroll
+    for (int i = 0; i < PB::PER_THREAD; ++i) {
+      const int u = tid + i * NT;
+      const int kk = PB::kk_of(u);
+      const uint32_t off = (PB::owns(u) && k0 + kk < kend) ? p.b_off(brow[i], k0, kk) : kOOB;
+#pragma unroll
+      for (int pl = 0; pl < NPB; ++pl)
+        rb[set][i][pl] =
+            __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srcB[pl], off, 0, 0));
+    }
+  };
+  auto stash = [&](auto S, int buf) {
+    constexpr int set = decltype(S)::value;
+    uint8_t* sa = smem + buf * STAGE;
+    uint8_t* sb = sa + PA::BYTES;
+#pragma unroll
+    for (int i = 0; i < PA::PER_THREAD; ++i) {
+      const int u = tid + i * NT;
+      if (!PA::owns(u)) continue;
+      const int off = PA::offset(u);
+#pragma unroll
+      for (int pl = 0; pl < NPA; ++pl)
+        *reinterpret_cast<u32x4*>(sa + pl * PA::PLANE + off) = ra[set][i][pl];
+    }
+#pragma unroll
+    for (int i = 0; i < PB::PER_THREAD; ++i) {
+      const int u = tid + i * NT;
+      if (!PB::owns(u)) continue;
+      const int off = PB::offset(u);
+#pragma unroll
+      for (int pl = 0; pl < NPB; ++pl)
+        *reinterpret_cast<u32x4*>(sb + pl * PB::PLANE + off) = rb[set][i][pl];
+    }
+  };
+
+  f32x16 acc[MT][NTL];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NTL; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
+
+  constexpr bool kColSum = HasColSum<P>::value;
+  const bool do_colsum = kColSum && m0 == 0 && wm == 0;
+  f32x16 cs[kColSum ? NTL : 1];
+#pragma unroll
+  for (int j = 0; j < (kColSum ? NTL : 1); ++j)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) cs[j][v] = 0.f;
+  const bf16x8 ones{(__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f,
+                    (__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f};
+
+  auto compute = [&](int buf) {
+    const uint8_t* sa = smem + buf * STAGE;
+    const uint8_t* sb = sa + PA::BYTES;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      bf16x8 fa[MT][NPA], fb[NTL][NPB];
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int pl = 0; pl < NPA; ++pl) fa[i][pl] = PA::frag(sa, pl, wm * TM + i * 32, s, lane);
+#pragma unroll
+      for (int j = 0; j < NTL; ++j)
+#pragma unroll
+        for (int pl = 0; pl < NPB; ++pl) fb[j][pl] = PB::frag(sb, pl, wn * TN + j * 32, s, lane);
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NTL; ++j) {
+          // Smallest terms first: (1,1), (2,0), (0,2), (1,0), (0,1), (0,0).
+          if constexpr (NPA == 3 && NPB == 3) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], acc[i][j], 0, 0, 0);
+          } else if constexpr (NPA == 3) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], acc[i][j], 0, 0, 0);
+          } else if constexpr (NPB == 3) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], acc[i][j], 0, 0, 0);
+          }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], acc[i][j], 0, 0, 0);
+        }
+      if constexpr (kColSum) {
+        if (do_colsum) {
+#pragma unroll
+          for (int j = 0; j < NTL; ++j)
+#pragma unroll
+            for (int pl = NPB - 1; pl >= 0; --pl)
+              cs[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fb[j][pl], cs[j], 0, 0, 0);
+        }
+      }
+    }
+  };
+
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  if constexpr (DEEP) {
+    if (nk > 0) {
+      fetch(S0{}, kbeg);
+      stash(S0{}, 0);
+    }
+    if (nk > 1) fetch(S1{}, kbeg + BK);
+    __syncthreads();
+    // Iteration kt: LDS buffer kt & 1 holds stage kt, register set (kt + 1) & 1 holds
+    // stage kt + 1; stage kt + 2 is fetched into set kt & 1.
+    auto iter = [&](auto S, int kt) {
+      constexpr int set = decltype(S)::value;
+      using Other = std::integral_constant<int, set ^ 1>;
+      if (kt + 2 < nk) fetch(S, kbeg + (kt + 2) * BK);
+      compute(set);
+      if (kt + 1 < nk) stash(Other{}, set ^ 1);
+      __syncthreads();
+    };
+    int kt = 0;
+    for (; kt + 1 < nk; kt += 2) {
+      iter(S0{}, kt);
+      iter(S1{}, kt + 1);
+    }
+    if (kt < nk) iter(S0{}, kt);
+  } else {
+    if (nk > 0) {
+      fetch(S0{}, kbeg);
+      stash(S0{}, 0);
+    }
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool more = kt + 1 < nk;
+      if (more) fetch(S0{}, kbeg + (kt + 1) * BK);
+      compute(kt & 1);
+      if (more) stash(S0{}, (kt + 1) & 1);
+      __syncthreads();
+    }
+  }
+
+  // Epilogue.  C/D map of the 32x32 MFMA: col = lane & 31, row = (v&3) + 8(v>>2) + 4h.
+  const int r = lane & 31, h = lane >> 5;
+  if constexpr (HasStore8<P>::value) {
+    // Row-major restage through LDS, one 32-row block of the wave's tile at a time, so
+    // each lane finishes 8 consecutive columns of one row (one decode per 8 outputs,
+    // 16-byte plane / 32-byte f32 stores).
+    constexpr int PITCH = TN + 4;
+    float* cw = reinterpret_cast<float*>(smem) + wave * 32 * PITCH;
+    constexpr int CHUNKS = 32 * TN / 8;
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+#pragma unroll
+      for (int j = 0; j < NTL; ++j)
+#pragma unroll
+        for (int v = 0; v < 16; ++v)
+          cw[((v & 3) + 8 * (v >> 2) + 4 * h) * PITCH + j * 32 + r] = acc[i][j][v];
+      __syncthreads();
+#pragma unroll
+      for (int c = lane; c < CHUNKS; c += 64) {
+        const int row = c / (TN / 8), col = 8 * (c % (TN / 8));
+        const int m = m0 + wm * TM + i * 32 + row;
+        const int n = n0 + wn * TN + col;
+        const f32x4 lo = *reinterpret_cast<const f32x4*>(cw + row * PITCH + col);
+        const f32x4 hi = *reinterpret_cast<const f32x4*>(cw + row * PITCH + col + 4);
+        const float v8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        if (m < p.M && n < p.N) p.store8(m, n, v8, split);
+      }
+      __syncthreads();
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NTL; ++j)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int m = m0 + wm * TM + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+          const int n = n0 + wn * TN + j * 32 + r;
+          if (m < p.M && n < p.N) p.store(m, n, acc[i][j][v], split);
+        }
+  }
+  if constexpr (kColSum) {
+    if (do_colsum && h == 0) {
+#pragma unroll
+      for (int j = 0; j < NTL; ++j) {
+        const int n = n0 + wn * TN + j * 32 + r;
+        if (n < p.N) p.store_colsum(n, cs[j][0], split);
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int BK, bool DEEP = true, class P>
+inline hipError_t launch_gemm_p3(const P& p, int splits, hipStream_t st) {
+  constexpr int NT = 64 * WM * WN;
+  using PA = PlanP3<BM, NT, P::A_MODE, P::A_PLANES, BK>;
+  using PB = PlanP3<BN, NT, P::B_MODE, P::B_PLANES, BK>;
+  constexpr int STAGES_BYTES = 2 * (PA::BYTES + PB::BYTES);
+  constexpr int EPI_BYTES = HasStore8<P>::value ? WM * WN * 32 * (BN / WN + 4) * 4 : 0;
+  constexpr int LDS = STAGES_BYTES > EPI_BYTES ? STAGES_BYTES : EPI_BYTES;
+  static_assert(LDS <= 160 * 1024, "two stages must fit the 160-KiB LDS of a CU");
+  if constexpr (LDS > 65536) {
+    static bool attr_set = false;
+    if (!attr_set) {
+      hipError_t e = hipFuncSetAttribute(
+          reinterpret_cast<const void*>(&gemm_p3_kernel<BM, BN, WM, WN, BK, DEEP, P>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+      if (e != hipSuccess) return e;
+      attr_set = true;
+    }
+  }
+  const int tiles = ((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
+  hipLaunchKernelGGL((gemm_p3_kernel<BM, BN, WM, WN, BK, DEEP, P>), dim3(tiles, 1, splits), dim3(NT),
+                     LDS, st, p);
+  return hipGetLastError();
+}
+
+}  // namespace gemm
+}  // namespace acme

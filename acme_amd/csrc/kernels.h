@@ -16,8 +16,11 @@ int launch_duel_head_finish(const float* slab, int splits, int rows, int A, cons
 
 // dZ of the fused hidden layer for rows b < B with dq[b] = g[b] * onehot(a[b]), masked by
 // the hidden ReLU.
+// With `planes` non-null the result is written as exact bf16 planes (gemm_p3.h Planes,
+// plane stride `pstride` elements) instead of f32 to dzh.
 int launch_duel_head_dz(const float* h, const float* g, const int32_t* a, int B, int H, int A,
-                        const float* wv, const float* wa, float* dzh, hipStream_t st);
+                        const float* wv, const float* wa, float* dzh, hipStream_t st,
+                        uint16_t* planes = nullptr, int64_t pstride = 0);
 
 // Sums the DuelHeadWgrad slab [splits][2H+1][A+1] and scatters its block-diagonal parts
 // into the head weight / bias gradients.
@@ -85,5 +88,21 @@ struct ClipAdamArgs {
   float* out_b = nullptr;
 };
 int launch_clip_adam(const ClipAdamArgs& a, hipStream_t st);
+
+// snt.Adam over n (multiple of 4) floats at step t (acme_adam_update); with `planes`
+// non-null the updated parameters are also written as exact bf16 planes (stride pstride).
+int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,
+                float b2, float eps, int64_t t, uint16_t* planes, int64_t pstride, hipStream_t st);
+
+// Exact three-plane split of n floats (n multiple of 4): planes[i * pstride + e].
+int launch_split_planes(const float* x, int64_t n, uint16_t* planes, int64_t pstride,
+                        hipStream_t st);
+// uint8 frames -> exact bf16 (one plane): out[f][e] = bf16(frame f byte e) for rows frames
+// of `frame_bytes` (multiple of 8), frames [0, split) from a and the rest from b.
+int launch_frames_bf16(const uint8_t* a, const uint8_t* b, int split, int rows, int frame_bytes,
+                       uint16_t* out, hipStream_t st);
+// Inverse (h + m + l in f32) for n elements.
+int launch_join_planes(const uint16_t* planes, int64_t pstride, int64_t n, float* x,
+                       hipStream_t st);
 
 }  // namespace acme

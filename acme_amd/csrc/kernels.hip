@@ -3,6 +3,7 @@
 #include "kernels.h"
 
 #include "conv.h"
+#include "gemm_p3.h"
 #include "gemm_x6.h"
 
 #include <hip/hip_runtime.h>
@@ -46,7 +47,8 @@ __global__ void __launch_bounds__(256) duel_head_finish_kernel(const float* __re
 __global__ void duel_head_dz_kernel(const float* __restrict__ h, const float* __restrict__ g,
                                     const int32_t* __restrict__ a, int B, int H, int A,
                                     const float* __restrict__ wv, const float* __restrict__ wa,
-                                    float* __restrict__ dzh) {
+                                    float* __restrict__ dzh, uint16_t* __restrict__ planes,
+                                    int64_t pstride) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (int64_t)B * 2 * H) return;
   const int b = (int)(i / (2 * H));
@@ -64,7 +66,9 @@ __global__ void duel_head_dz_kernel(const float* __restrict__ h, const float* __
     for (int j = 0; j < A; ++j) s = fmaf(gb * ((j == ab ? 1.f : 0.f) - inv_a), row[j], s);
     d = s;
   }
-  dzh[i] = h[i] > 0.f ? d : 0.f;
+  const float z = h[i] > 0.f ? d : 0.f;
+  if (planes) gemm::Planes{planes, pstride}.put(i, z);
+  else dzh[i] = z;
 }
 
 // Sum of the DuelHeadWgrad slab + scatter of its block-diagonal parts.
@@ -192,6 +196,20 @@ __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restric
 
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 
+// Planes of 4 consecutive floats (element 4i .. 4i+3), 8-byte stores per plane.
+__device__ __forceinline__ void store_planes4(uint16_t* planes, int64_t pstride, int64_t i,
+                                              const f32x4 x) {
+  uint16_t h[4], m[4], l[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) gemm::split3_bits(x[j], h[j], m[j], l[j]);
+  auto pack = [](const uint16_t* q) {
+    return uint2{(uint32_t)q[0] | ((uint32_t)q[1] << 16), (uint32_t)q[2] | ((uint32_t)q[3] << 16)};
+  };
+  reinterpret_cast<uint2*>(planes)[i] = pack(h);
+  reinterpret_cast<uint2*>(planes + pstride)[i] = pack(m);
+  reinterpret_cast<uint2*>(planes + 2 * pstride)[i] = pack(l);
+}
+
 // snt.optimizers.Adam (Kingma & Ba Algorithm 1 form):
 //   m = b1 m + (1-b1) g;  v = b2 v + (1-b2) g g
 //   p -= lr * (m / (1 - b1^t)) / (sqrt(v / (1 - b2^t)) + eps)
@@ -200,7 +218,8 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p,
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    int64_t n4, float lr, float b1, float omb1,
                                                    float b2, float omb2, float bc1, float bc2,
-                                                   float eps) {
+                                                   float eps, uint16_t* __restrict__ planes,
+                                                   int64_t pstride) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (int64_t)gridDim.x * blockDim.x) {
     f32x4 gg = reinterpret_cast<const f32x4*>(g)[i];
@@ -221,7 +240,43 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p,
     reinterpret_cast<f32x4*>(m)[i] = mm;
     reinterpret_cast<f32x4*>(v)[i] = vv;
     reinterpret_cast<f32x4*>(p)[i] = pp;
+    if (planes) store_planes4(planes, pstride, i, pp);
   }
+}
+
+__global__ void __launch_bounds__(256) split_planes_kernel(const float* __restrict__ x, int64_t n4,
+                                                           uint16_t* __restrict__ planes,
+                                                           int64_t pstride) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x)
+    store_planes4(planes, pstride, i, reinterpret_cast<const f32x4*>(x)[i]);
+}
+
+__global__ void __launch_bounds__(256) frames_bf16_kernel(const uint8_t* __restrict__ a,
+                                                          const uint8_t* __restrict__ b,
+                                                          int64_t split8, int64_t n8,
+                                                          uint16_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint2 w = i < split8 ? reinterpret_cast<const uint2*>(a)[i]
+                               : reinterpret_cast<const uint2*>(b)[i - split8];
+    // bf16(byte) is the upper half of float(byte) (exact: 8 significant bits).
+    auto cvt = [](uint32_t x, int s) { return __builtin_bit_cast(uint32_t, (float)((x >> s) & 0xff)); };
+    const uint32_t o0 = (cvt(w.x, 0) >> 16) | (cvt(w.x, 8) & 0xffff0000u);
+    const uint32_t o1 = (cvt(w.x, 16) >> 16) | (cvt(w.x, 24) & 0xffff0000u);
+    const uint32_t o2 = (cvt(w.y, 0) >> 16) | (cvt(w.y, 8) & 0xffff0000u);
+    const uint32_t o3 = (cvt(w.y, 16) >> 16) | (cvt(w.y, 24) & 0xffff0000u);
+    reinterpret_cast<uint4*>(out)[i] = uint4{o0, o1, o2, o3};
+  }
+}
+
+__global__ void __launch_bounds__(256) join_planes_kernel(const uint16_t* __restrict__ planes,
+                                                          int64_t pstride, int64_t n,
+                                                          float* __restrict__ x) {
+  const gemm::CPlanes c{planes, pstride};
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    x[i] = c.value(i);
 }
 
 
@@ -349,9 +404,11 @@ int launch_duel_head_finish(const float* slab, int splits, int rows, int A, cons
 }
 
 int launch_duel_head_dz(const float* h, const float* g, const int32_t* a, int B, int H, int A,
-                        const float* wv, const float* wa, float* dzh, hipStream_t st) {
+                        const float* wv, const float* wa, float* dzh, hipStream_t st,
+                        uint16_t* planes, int64_t pstride) {
   const int64_t n = (int64_t)B * 2 * H;
-  duel_head_dz_kernel<<<(unsigned)ceil_div(n, 256), 256, 0, st>>>(h, g, a, B, H, A, wv, wa, dzh);
+  duel_head_dz_kernel<<<(unsigned)ceil_div(n, 256), 256, 0, st>>>(h, g, a, B, H, A, wv, wa, dzh,
+                                                                   planes, pstride);
   ACME_LAUNCH_CHECK();
   return ACME_OK;
 }
@@ -396,6 +453,53 @@ int launch_grad_sumsq(const float* g, int64_t n4, int64_t group0_4, double* part
   return ACME_OK;
 }
 
+int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,
+                float b2, float eps, int64_t t, uint16_t* planes, int64_t pstride, hipStream_t st) {
+  ACME_CHECK_ARG(p && g && m && v, "null buffer");
+  ACME_CHECK_ARG(n % 4 == 0, "adam buffer length must be a multiple of 4");
+  ACME_CHECK_ARG(pstride % 4 == 0, "plane stride must be a multiple of 4");
+  ACME_CHECK_ARG(t >= 1, "adam step must be >= 1");
+  const float bc1 = 1.f - powf(b1, (float)t);
+  const float bc2 = 1.f - powf(b2, (float)t);
+  const int64_t n4 = n / 4;
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n4, 256), 2048);
+  adam_kernel<<<std::max(grid, 1u), 256, 0, st>>>(p, g, m, v, n4, lr, b1, 1.f - b1, b2, 1.f - b2,
+                                                  bc1, bc2, eps, planes, pstride);
+  ACME_LAUNCH_CHECK();
+  return ACME_OK;
+}
+
+int launch_split_planes(const float* x, int64_t n, uint16_t* planes, int64_t pstride,
+                        hipStream_t st) {
+  ACME_CHECK_ARG(n % 4 == 0 && pstride % 4 == 0, "plane split needs multiples of 4");
+  const int64_t n4 = n / 4;
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n4, 256), 2048);
+  split_planes_kernel<<<std::max(grid, 1u), 256, 0, st>>>(x, n4, planes, pstride);
+  ACME_LAUNCH_CHECK();
+  return ACME_OK;
+}
+
+int launch_frames_bf16(const uint8_t* a, const uint8_t* b, int split, int rows, int frame_bytes,
+                       uint16_t* out, hipStream_t st) {
+  ACME_CHECK_ARG(frame_bytes % 8 == 0, "frame bytes must be a multiple of 8");
+  ACME_CHECK_ARG(reinterpret_cast<uintptr_t>(a) % 8 == 0 && reinterpret_cast<uintptr_t>(b) % 8 == 0,
+                 "uint8 frame buffers must be 8-byte aligned");
+  const int64_t per = frame_bytes / 8;
+  const int64_t n8 = per * rows;
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n8, 256), 8192);
+  frames_bf16_kernel<<<std::max(grid, 1u), 256, 0, st>>>(a, b, per * split, n8, out);
+  ACME_LAUNCH_CHECK();
+  return ACME_OK;
+}
+
+int launch_join_planes(const uint16_t* planes, int64_t pstride, int64_t n, float* x,
+                       hipStream_t st) {
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n, 256), 4096);
+  join_planes_kernel<<<std::max(grid, 1u), 256, 0, st>>>(planes, pstride, n, x);
+  ACME_LAUNCH_CHECK();
+  return ACME_OK;
+}
+
 int launch_clip_adam(const ClipAdamArgs& a, hipStream_t st) {
   ACME_CHECK_ARG(a.p && a.m && a.v && a.g && a.part && a.dev_step, "bad argument");
   const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(a.n4, 256), 1024);
@@ -413,15 +517,8 @@ int acme_adam_update(float* params, const float* grads, float* m, float* v, int6
   ACME_CHECK_ARG(params && grads && m && v, "null buffer");
   ACME_CHECK_ARG(n % 4 == 0, "adam buffer length must be a multiple of 4");
   ACME_CHECK_ARG(t >= 1, "adam step must be >= 1");
-  const float omb1 = 1.f - beta1, omb2 = 1.f - beta2;
-  const float bc1 = 1.f - powf(beta1, (float)t);
-  const float bc2 = 1.f - powf(beta2, (float)t);
-  const int64_t n4 = n / 4;
-  const unsigned grid = (unsigned)std::min<int64_t>(acme::ceil_div(n4, 256), 2048);
-  acme::adam_kernel<<<grid, 256, 0, acme::as_stream(stream)>>>(params, grads, m, v, n4, lr, beta1,
-                                                                omb1, beta2, omb2, bc1, bc2, eps);
-  ACME_LAUNCH_CHECK();
-  return ACME_OK;
+  return acme::launch_adam(params, grads, m, v, n, lr, beta1, beta2, eps, t, nullptr, 0,
+                           acme::as_stream(stream));
 }
 
 int acme_dense_forward(const float* x, int64_t rows, int64_t in, const float* w, const float* b,

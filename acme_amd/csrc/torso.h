@@ -45,5 +45,27 @@ int forward(const Weights& w, bool u8, const void* obs_a, const void* obs_b, int
 int backward(const Weights& w, const Grads& g, bool u8, const void* obs, int rows, const Acts& a,
              const float* dz3, float* dz2, float* dz1, float* slab, hipStream_t st);
 
+// ---- Plane path (gemm_p3.h engine, uint8 frames): activations, gradients and weights
+// as exact three-plane bf16 tensors (Plane::p[i * stride + e] = plane i of element e).
+struct Plane {
+  uint16_t* p;
+  int64_t stride;
+};
+struct PWeights {
+  Plane w1, w2, w3;  // views into the flat parameter planes
+  const float *b1, *b2, *b3;
+};
+struct PActs {
+  Plane x1, x2, x3;
+};
+int64_t wgrad_slab_floats_p3();
+// frames: bf16 copies of the uint8 frames [rows][84*84*4] (launch_frames_bf16).
+int forward_p3(const PWeights& w, const uint16_t* frames, int rows, const PActs& a,
+               hipStream_t st);
+// dz3: conv3's dZ planes [rows][kFlat] (masked); dz2 / dz1 plane scratch.
+int backward_p3(const PWeights& w, const Grads& g, const uint16_t* frames, int rows,
+                const PActs& a, const Plane& dz3, const Plane& dz2, const Plane& dz1, float* slab,
+                hipStream_t st);
+
 }  // namespace torso
 }  // namespace acme

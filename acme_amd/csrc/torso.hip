@@ -7,7 +7,9 @@
 #include <algorithm>
 
 #include "common.h"
+#include "conv_p3.h"
 #include "gemm.h"
+#include "gemm_p3.h"
 #include "gemm_x6.h"
 #include "kernels.h"
 #include "profiler.h"
@@ -127,6 +129,147 @@ int backward(const Weights& w, const Grads& g, bool u8, const void* obs, int row
   return conv_wgrad<G1, InF32, 128, 32, 4, 1>(static_cast<const float*>(obs), dz1, rows,
                                               kConv1WgradSplits, slab, g.w1, g.b1, "conv1_wgrad",
                                               "conv1_wgrad_reduce", st);
+}
+
+// ---------------------------------------------------------------- plane path
+namespace {
+
+constexpr int kP3Conv1WgradSplits = 256, kP3Conv2WgradSplits = 64, kP3Conv3WgradSplits = 64;
+
+#define P3_GEMM_F(name, flops, BM, BN, WM, WN, BK, prob, splits)                             \
+  do {                                                                                        \
+    ACME_PROF(name, st, flops, 0.0);                                                          \
+    hipError_t _e = gemm::launch_gemm_p3<BM, BN, WM, WN, BK>(prob, splits, st);               \
+    if (_e != hipSuccess) {                                                                   \
+      set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
+      return ACME_ERR_HIP;                                                                    \
+    }                                                                                         \
+  } while (0)
+#define P3_GEMM(name, BM, BN, WM, WN, BK, prob, splits)                                      \
+  P3_GEMM_F(name, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, BM, BN, WM, \
+            WN, BK, prob, splits)
+
+inline CPlanes cp(const Plane& x) { return CPlanes{x.p, x.stride}; }
+inline Planes pl(const Plane& x) { return Planes{x.p, x.stride}; }
+// Operand source over the first `elems` elements of each plane.
+inline PlaneSrc src(const Plane& x, int64_t elems) {
+  return PlaneSrc{x.p, x.stride, (int32_t)(2 * elems)};
+}
+inline PlaneSrc frames_src(const uint16_t* f, int rows) {
+  return PlaneSrc{f, 0, (int32_t)(2 * (int64_t)rows * G1::IPIX * G1::CI)};
+}
+
+template <class P>
+int p3_wgrad_reduce(const P& p, int splits, float* slab, float* dw, float* db, const char* rname,
+                    hipStream_t st) {
+  const int64_t count = (int64_t)(p.M + 1) * p.N;
+  ACME_PROF(rname, st, 0.0, 4.0 * (double)(splits + 1) * (double)count);
+  return launch_slab_reduce(slab, splits, count, dw, (int64_t)p.M * p.N, db, nullptr, 0, 0, st);
+}
+
+}  // namespace
+
+int64_t wgrad_slab_floats_p3() {
+  return std::max<int64_t>({(int64_t)kP3Conv1WgradSplits * (G1::K + 1) * G1::CO,
+                            (int64_t)kP3Conv2WgradSplits * (G2::K + 1) * G2::CO,
+                            (int64_t)kP3Conv3WgradSplits * (G3::K + 1) * G3::CO});
+}
+
+int forward_p3(const PWeights& w, const uint16_t* frames, int rows, const PActs& a,
+               hipStream_t st) {
+  {
+    P3ConvFwd<G1, 1> p;
+    p.M = rows * G1::OPIX; p.N = G1::CO; p.K = G1::K; p.k_chunk = G1::K;
+    p.a_src = frames_src(frames, rows); p.b_src = src(w.w1, G1::K * G1::CO);
+    p.bias = w.b1; p.y = pl(a.x1);
+    switch (tune_variant("P3C1F")) {
+      case 1: P3_GEMM("conv1_fwd", 128, 32, 4, 1, 32, p, 1); break;
+      case 2: P3_GEMM("conv1_fwd", 256, 32, 4, 1, 32, p, 1); break;
+      default: P3_GEMM("conv1_fwd", 256, 32, 4, 1, 16, p, 1); break;
+    }
+  }
+  {
+    P3ConvFwd<G2, 3> p;
+    p.M = rows * G2::OPIX; p.N = G2::CO; p.K = G2::K; p.k_chunk = G2::K;
+    p.a_src = src(a.x1, (int64_t)rows * kX1); p.b_src = src(w.w2, G2::K * G2::CO);
+    p.bias = w.b2; p.y = pl(a.x2);
+    switch (tune_variant("P3C2F")) {
+      case 1: P3_GEMM("conv2_fwd", 128, 64, 2, 2, 16, p, 1); break;
+      case 2: P3_GEMM("conv2_fwd", 256, 64, 4, 1, 32, p, 1); break;
+      default: P3_GEMM("conv2_fwd", 128, 64, 2, 2, 32, p, 1); break;
+    }
+  }
+  {
+    P3ConvFwd<G3, 3> p;
+    p.M = rows * G3::OPIX; p.N = G3::CO; p.K = G3::K; p.k_chunk = G3::K;
+    p.a_src = src(a.x2, (int64_t)rows * kFlat); p.b_src = src(w.w3, G3::K * G3::CO);
+    p.bias = w.b3; p.y = pl(a.x3);
+    switch (tune_variant("P3C3F")) {
+      case 1: P3_GEMM("conv3_fwd", 128, 64, 2, 2, 16, p, 1); break;
+      case 2: P3_GEMM("conv3_fwd", 256, 64, 4, 1, 32, p, 1); break;
+      default: P3_GEMM("conv3_fwd", 128, 64, 2, 2, 32, p, 1); break;
+    }
+  }
+  return ACME_OK;
+}
+
+int backward_p3(const PWeights& w, const Grads& g, const uint16_t* frames, int rows,
+                const PActs& a, const Plane& dz3, const Plane& dz2, const Plane& dz1, float* slab,
+                hipStream_t st) {
+  int rc;
+  {  // conv3 weight + bias gradient
+    P3ConvWgrad<G3, 3> p;
+    p.M = G3::K; p.N = G3::CO; p.K = rows * G3::OPIX;
+    p.k_chunk = chunk_for(p.K, kP3Conv3WgradSplits);
+    p.a_src = src(a.x2, (int64_t)rows * kFlat); p.b_src = src(dz3, (int64_t)rows * kFlat);
+    p.slab = slab;
+    P3_GEMM("conv3_wgrad", 128, 64, 2, 2, 32, p, kP3Conv3WgradSplits);
+    if ((rc = p3_wgrad_reduce(p, kP3Conv3WgradSplits, slab, g.w3, g.b3, "conv3_wgrad_reduce", st)))
+      return rc;
+  }
+  {
+    P3ConvDgrad<G3> p;
+    p.M = rows * G3::IPIX; p.N = G3::CI; p.K = G3::KH * G3::KW * G3::CO; p.k_chunk = p.K;
+    p.a_src = src(dz3, (int64_t)rows * kFlat); p.b_src = src(w.w3, G3::K * G3::CO);
+    p.xprev = cp(a.x2); p.dx = pl(dz2);
+    switch (tune_variant("P3C3D")) {
+      case 1: P3_GEMM("conv3_dgrad", 128, 64, 2, 2, 16, p, 1); break;
+      case 2: P3_GEMM("conv3_dgrad", 256, 64, 4, 1, 32, p, 1); break;
+      default: P3_GEMM("conv3_dgrad", 128, 64, 2, 2, 32, p, 1); break;
+    }
+  }
+  {  // conv2
+    P3ConvWgrad<G2, 3> p;
+    p.M = G2::K; p.N = G2::CO; p.K = rows * G2::OPIX;
+    p.k_chunk = chunk_for(p.K, kP3Conv2WgradSplits);
+    p.a_src = src(a.x1, (int64_t)rows * kX1); p.b_src = src(dz2, (int64_t)rows * kFlat);
+    p.slab = slab;
+    P3_GEMM("conv2_wgrad", 128, 64, 2, 2, 32, p, kP3Conv2WgradSplits);
+    if ((rc = p3_wgrad_reduce(p, kP3Conv2WgradSplits, slab, g.w2, g.b2, "conv2_wgrad_reduce", st)))
+      return rc;
+  }
+  {  // stride-2 input gradient, four sub-pixel classes in one launch
+    P3ConvDgradSubZ<G2> p;
+    p.M = P3ConvDgradSubZ<G2>::max_rows(rows); p.N = G2::CI; p.K = P3ConvDgradSubZ<G2>::KR;
+    p.k_chunk = p.K; p.batch = rows;
+    p.a_src = src(dz2, (int64_t)rows * kFlat); p.b_src = src(w.w2, G2::K * G2::CO);
+    p.xprev = cp(a.x1); p.dx = pl(dz1);
+    const double fl = 2.0 * rows * G2::IPIX * G2::CI * (double)p.K;
+    switch (tune_variant("P3C2D")) {
+      case 1: P3_GEMM_F("conv2_dgrad", fl, 256, 32, 4, 1, 32, p, G2::S * G2::S); break;
+      case 2: P3_GEMM_F("conv2_dgrad", fl, 256, 32, 4, 1, 16, p, G2::S * G2::S); break;
+      default: P3_GEMM_F("conv2_dgrad", fl, 128, 32, 4, 1, 32, p, G2::S * G2::S); break;
+    }
+  }
+  {  // conv1 (no input gradient)
+    P3ConvWgrad<G1, 1> p;
+    p.M = G1::K; p.N = G1::CO; p.K = rows * G1::OPIX;
+    p.k_chunk = chunk_for(p.K, kP3Conv1WgradSplits);
+    p.a_src = frames_src(frames, rows); p.b_src = src(dz1, (int64_t)rows * kX1);
+    p.slab = slab;
+    P3_GEMM("conv1_wgrad", 256, 32, 4, 1, 32, p, kP3Conv1WgradSplits);
+    return p3_wgrad_reduce(p, kP3Conv1WgradSplits, slab, g.w1, g.b1, "conv1_wgrad_reduce", st);
+  }
 }
 
 }  // namespace torso

@@ -254,6 +254,12 @@ class NativeDQN:
             v = self.views(flat)
             for name, t in v.items():
                 t.copy_(torch.as_tensor(np.asarray(src[name], np.float32)).view(t.shape))
+        self.params_changed()
+
+    def params_changed(self) -> None:
+        """Tells the learner its params / target buffers were written from outside (its
+        derived bf16 parameter planes are rebuilt before the next use)."""
+        check(lib().acme_dqn_params_changed(self._h), "dqn params_changed")
 
     def get_params(self, which: str = "params") -> Dict[str, np.ndarray]:
         flat = getattr(self, which)
@@ -424,6 +430,9 @@ class NativeD4PG:
     views = NativeDQN.views
     set_params = NativeDQN.set_params
     get_params = NativeDQN.get_params
+
+    def params_changed(self) -> None:  # the D4PG step reads the f32 buffers directly
+        pass
 
     @property
     def num_steps(self) -> int:

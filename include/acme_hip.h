@@ -166,6 +166,11 @@ int acme_dqn_tensor_info(const acme_dqn* l, int32_t i, int64_t* offset, int64_t*
  * target params, gradients, Adam first/second moments. */
 int acme_dqn_bind(acme_dqn* l, float* params, float* target, float* grads, float* adam_m,
                   float* adam_v);
+/* Declares that the caller wrote the bound params / target buffers directly (restore,
+ * broadcast, initialisation): the learner's derived copies of them (the exact bf16
+ * parameter planes of the uint8 Nature path) are rebuilt before the next use.  The
+ * learner's own updates (step / apply) need no call. */
+int acme_dqn_params_changed(acme_dqn* l);
 
 typedef struct acme_transition_batch {
   const void* o_tm1;   /* [B, obs...]  u8 or f32 */
