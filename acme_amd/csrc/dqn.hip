@@ -205,6 +205,16 @@ int tune(const char* key) { return tune_variant(key); }
     }                                                                                          \
   } while (0)
 
+#define ACME_P3G_GEMM(name, BM, BN, WM, WN, BKV, ST, prob, splits)                            \
+  do {                                                                                         \
+    ACME_PROF(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0);   \
+    hipError_t _e = gemm::launch_gemm_p3g<BM, BN, WM, WN, BKV, ST>(prob, splits, st);         \
+    if (_e != hipSuccess) {                                                                    \
+      set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
+      return ACME_ERR_HIP;                                                                     \
+    }                                                                                          \
+  } while (0)
+
 // Split counts (K-splits) of the launches whose natural grid is too small to fill 256 CUs.
 constexpr int kFcFwdSplits = 8;  // [rows, 1024] x K 7744: 128x128 tiles: 8x8x8 = 512 blocks (online)
 constexpr int kHeadFwdSplits = 16;  // [rows, A+1] x K 1024
@@ -291,14 +301,16 @@ int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const uint16
     switch (tune("P3FCF")) {
       case 1: ACME_P3_GEMM("fc_fwd", 128, 128, 2, 2, 16, p, splits); break;
       case 2: ACME_P3_GEMM("fc_fwd", 256, 128, 4, 2, 16, p, splits); break;
+      case 3: ACME_P3G_GEMM("fc_fwd", 128, 128, 2, 2, 16, 3, p, splits); break;
+      case 4: ACME_P3G_GEMM("fc_fwd", 128, 128, 2, 2, 32, 3, p, splits); break;
+      case 5: ACME_P3G_GEMM("fc_fwd", 128, 128, 2, 2, 16, 4, p, splits); break;
       default: ACME_P3_GEMM("fc_fwd", 128, 128, 2, 2, 32, p, splits); break;
     }
-    const int64_t cnt = (int64_t)rows * 2 * kHidden;
-    rc = slab_reduce(l->slab, splits, cnt, hid, cnt, nullptr, P(l, prm, l->t_fcb), 2 * kHidden, 1,
-                     "fc_fwd_reduce", st);
-    if (rc != ACME_OK) return rc;
+    ACME_PROF("fc_head_fwd", st, 0.0, 4.0 * (double)rows * 2 * kHidden * (splits + 1));
+    return launch_fc_head_forward(l->slab, splits, rows, kHidden, P(l, prm, l->t_fcb),
+                                  P(l, prm, l->t_vw), P(l, prm, l->t_vb), P(l, prm, l->t_aw),
+                                  P(l, prm, l->t_ab), l->cfg.num_actions, hid, q, st);
   }
-  return head_forward(l, prm, rows, hid, q, st);
 }
 
 // ---------------------------------------------------------------- MLP forward
@@ -351,9 +363,10 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st) {
   int rc;
   {  // Head: dZ of the fused hidden layer (masked by its ReLU).
     ACME_PROF("head_dz", st, 0.0, 0.0);
-    rc = launch_duel_head_dz(l->hid, l->g, l->a_cache, B, kHidden, A, P(l, prm, l->t_vw),
-                             P(l, prm, l->t_aw), l->dzh, st, p3 ? l->dzhp.p : nullptr,
-                             l->dzhp.stride);
+    rc = p3 ? launch_head_dz_planes(l->hid, l->g, l->a_cache, B, kHidden, A, P(l, prm, l->t_vw),
+                                    P(l, prm, l->t_aw), l->dzhp.p, l->dzhp.stride, st)
+            : launch_duel_head_dz(l->hid, l->g, l->a_cache, B, kHidden, A, P(l, prm, l->t_vw),
+                                  P(l, prm, l->t_aw), l->dzh, st);
     if (rc != ACME_OK) return rc;
   }
   {  // Head weight / bias gradients: one skinny GEMM over the batch + scatter.
@@ -376,6 +389,8 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st) {
       p.bias_out = Pm(l, gr, l->t_fcb);
       switch (tune("P3FCW")) {
         case 1: ACME_P3_GEMM("fc_wgrad", 128, 128, 2, 2, 32, p, 1); break;
+        case 3: ACME_P3G_GEMM("fc_wgrad", 128, 128, 2, 2, 16, 3, p, 1); break;
+        case 4: ACME_P3G_GEMM("fc_wgrad", 128, 128, 2, 2, 32, 3, p, 1); break;
         default: ACME_P3_GEMM("fc_wgrad", 128, 128, 2, 2, 16, p, 1); break;
       }
     }
@@ -388,7 +403,9 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st) {
       switch (tune("P3FCD")) {
         case 1: ACME_P3_GEMM("fc_dgrad", 64, 128, 2, 2, 32, p, 1); break;
         case 2: ACME_P3_GEMM("fc_dgrad", 64, 128, 2, 2, 16, p, 1); break;
-        default: ACME_P3_GEMM("fc_dgrad", 128, 128, 2, 2, 32, p, 1); break;
+        case 3: ACME_P3G_GEMM("fc_dgrad", 128, 128, 2, 2, 16, 3, p, 1); break;
+        case 4: ACME_P3_GEMM("fc_dgrad", 128, 128, 2, 2, 32, p, 1); break;
+        default: ACME_P3G_GEMM("fc_dgrad", 128, 128, 2, 2, 32, 3, p, 1); break;
       }
     }
     return ACME_OK;

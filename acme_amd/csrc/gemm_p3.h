@@ -159,6 +159,19 @@ struct PlanP3 {
       return k * (2 * R) + 2 * (row ^ (p3_rswz<R>(k) << 5));
     }
   }
+  // LDS-DMA view: the image is unit-linear (slot u at byte 16 u), so DMA block b (64
+  // slots, one per lane) lands in 1 KiB at 1024 b, and the swizzle is applied by choosing
+  // which logical unit each slot's lane fetches.
+  static constexpr int BLOCKS = UNITS / 64;
+  static_assert(UNITS % 64 == 0, "tile units must fill whole 64-lane DMA blocks");
+  __device__ static __forceinline__ int slot_row(int u) {
+    if constexpr (MODE == KCONTIG) return u / CPR;
+    else return 8 * ((u % OPK) ^ (p3_rswz<R>(u / OPK) << 2));
+  }
+  __device__ static __forceinline__ int slot_kk(int u) {
+    if constexpr (MODE == KCONTIG) return 8 * ((u % CPR) ^ p3_kswz<BK>(u / CPR));
+    else return u / OPK;
+  }
   // MFMA operand of rows rb .. rb+31 (rb a multiple of 32), k step s (16 k).
   __device__ static __forceinline__ bf16x8 frag(const uint8_t* tile, int plane, int rb, int s,
                                                 int lane) {
@@ -184,19 +197,145 @@ struct PlanP3 {
   }
 };
 
-template <int BM, int BN, int WM, int WN, int BK, bool DEEP, class P>
-__global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in) {
-  const P p = z_select(p_in);
-  constexpr int NT = 64 * WM * WN;
-  constexpr int TM = BM / WM, TN = BN / WN;
-  constexpr int MT = TM / 32, NTL = TN / 32;
-  constexpr int NPA = P::A_PLANES, NPB = P::B_PLANES;
+// Shared MFMA core of the plane kernels: one LDS stage's fragments and MFMAs, and the
+// epilogue.
+template <int BM, int BN, int WM, int WN, int BK, class P>
+struct P3Core {
+  static constexpr int NT = 64 * WM * WN;
+  static constexpr int TM = BM / WM, TN = BN / WN;
+  static constexpr int MT = TM / 32, NTL = TN / 32;
+  static constexpr int NPA = P::A_PLANES, NPB = P::B_PLANES;
   static_assert(TM % 32 == 0 && TN % 32 == 0, "wave tile must be a multiple of 32x32");
   static_assert(BK == 16 || BK == 32, "BK must be 16 or 32");
   static_assert((NPA == 1 || NPA == 3) && (NPB == 1 || NPB == 3), "1 or 3 planes per operand");
   using PA = PlanP3<BM, NT, P::A_MODE, NPA, BK>;
   using PB = PlanP3<BN, NT, P::B_MODE, NPB, BK>;
-  constexpr int STAGE = PA::BYTES + PB::BYTES;
+  static constexpr int STAGE = PA::BYTES + PB::BYTES;
+  static constexpr bool kColSum = HasColSum<P>::value;
+  static constexpr int NCS = kColSum ? NTL : 1;
+  static constexpr int EPI_BYTES = HasStore8<P>::value ? WM * WN * 32 * (TN + 4) * 4 : 0;
+
+  __device__ static __forceinline__ void mma(const uint8_t* sa, const uint8_t* sb, int wm, int wn,
+                                             int lane, f32x16 (&acc)[MT][NTL], f32x16 (&cs)[NCS],
+                                             bool do_colsum) {
+    const bf16x8 ones{(__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f,
+                      (__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f};
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      bf16x8 fa[MT][NPA], fb[NTL][NPB];
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int pl = 0; pl < NPA; ++pl) fa[i][pl] = PA::frag(sa, pl, wm * TM + i * 32, s, lane);
+#pragma unroll
+      for (int j = 0; j < NTL; ++j)
+#pragma unroll
+        for (int pl = 0; pl < NPB; ++pl) fb[j][pl] = PB::frag(sb, pl, wn * TN + j * 32, s, lane);
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NTL; ++j) {
+          // Smallest terms first: (1,1), (2,0), (0,2), (1,0), (0,1), (0,0).
+          if constexpr (NPA == 3 && NPB == 3) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], acc[i][j], 0, 0, 0);
+          } else if constexpr (NPA == 3) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], acc[i][j], 0, 0, 0);
+          } else if constexpr (NPB == 3) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], acc[i][j], 0, 0, 0);
+          }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], acc[i][j], 0, 0, 0);
+        }
+      if constexpr (kColSum) {
+        if (do_colsum) {
+#pragma unroll
+          for (int j = 0; j < NTL; ++j)
+#pragma unroll
+            for (int pl = NPB - 1; pl >= 0; --pl)
+              cs[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fb[j][pl], cs[j], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // Epilogue.  C/D map of the 32x32 MFMA: col = lane & 31, row = (v&3) + 8(v>>2) + 4h.
+  // The LDS is free (every stage consumed) when this runs; it contains barriers, so all
+  // waves of the block call it.
+  __device__ static __forceinline__ void epilogue(const P& p, uint8_t* smem, int m0, int n0,
+                                                  int wave, int wm, int wn, int lane, int split,
+                                                  f32x16 (&acc)[MT][NTL], f32x16 (&cs)[NCS],
+                                                  bool do_colsum) {
+    const int r = lane & 31, h = lane >> 5;
+    if constexpr (HasStore8<P>::value) {
+      // Row-major restage through LDS, one 32-row block of the wave's tile at a time, so
+      // each lane finishes 8 consecutive columns of one row (one decode per 8 outputs,
+      // 16-byte plane / 32-byte f32 stores).
+      constexpr int PITCH = TN + 4;
+      float* cw = reinterpret_cast<float*>(smem) + wave * 32 * PITCH;
+      constexpr int CHUNKS = 32 * TN / 8;
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+#pragma unroll
+        for (int j = 0; j < NTL; ++j)
+#pragma unroll
+          for (int v = 0; v < 16; ++v)
+            cw[((v & 3) + 8 * (v >> 2) + 4 * h) * PITCH + j * 32 + r] = acc[i][j][v];
+        __syncthreads();
+#pragma unroll
+        for (int c = lane; c < CHUNKS; c += 64) {
+          const int row = c / (TN / 8), col = 8 * (c % (TN / 8));
+          const int m = m0 + wm * TM + i * 32 + row;
+          const int n = n0 + wn * TN + col;
+          const f32x4 lo = *reinterpret_cast<const f32x4*>(cw + row * PITCH + col);
+          const f32x4 hi = *reinterpret_cast<const f32x4*>(cw + row * PITCH + col + 4);
+          const float v8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          if (m < p.M && n < p.N) p.store8(m, n, v8, split);
+        }
+        __syncthreads();
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NTL; ++j)
+#pragma unroll
+          for (int v = 0; v < 16; ++v) {
+            const int m = m0 + wm * TM + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+            const int n = n0 + wn * TN + j * 32 + r;
+            if (m < p.M && n < p.N) p.store(m, n, acc[i][j][v], split);
+          }
+    }
+    if constexpr (kColSum) {
+      if (do_colsum && h == 0) {
+#pragma unroll
+        for (int j = 0; j < NTL; ++j) {
+          const int n = n0 + wn * TN + j * 32 + r;
+          if (n < p.N) p.store_colsum(n, cs[j][0], split);
+        }
+      }
+    }
+  }
+};
+
+#ifndef P3_EARLY_STASH
+#define P3_EARLY_STASH 1
+#endif
+
+// Register-staged kernel: global -> VGPR -> LDS, two LDS stages; with DEEP two register
+// sets so a stage's loads are issued two stages before its compute.
+template <int BM, int BN, int WM, int WN, int BK, bool DEEP, class P>
+__global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in) {
+  constexpr bool EARLY_STASH = P3_EARLY_STASH;
+  using C = P3Core<BM, BN, WM, WN, BK, P>;
+  using PA = typename C::PA;
+  using PB = typename C::PB;
+  constexpr int NT = C::NT, NPA = C::NPA, NPB = C::NPB, STAGE = C::STAGE;
+  const P p = z_select(p_in);
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
   const int tid = threadIdx.x;
@@ -226,9 +365,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in) {
   for (int pl = 0; pl < NPA; ++pl) srcA[pl] = plane_rsrc(p.a_src, pl);
 #pragma unroll
   for (int pl = 0; pl < NPB; ++pl) srcB[pl] = plane_rsrc(p.b_src, pl);
-  // Register sets for the global -> LDS staging: with DEEP, stage j is fetched into set
-  // j & 1 two stages ahead of its compute, so a load has a whole iteration (compute,
-  // stash, barrier, compute) to land; otherwise one set, fetched one stage ahead.
+
   constexpr int SETS = DEEP ? 2 : 1;
   u32x4 ra[SETS][PA::PER_THREAD][NPA], rb[SETS][PB::PER_THREAD][NPB];
   auto fetch = [&](auto S, int k0) {
@@ -278,68 +415,22 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in) {
     }
   };
 
-  f32x16 acc[MT][NTL];
+  f32x16 acc[C::MT][C::NTL];
+  f32x16 cs[C::NCS];
 #pragma unroll
-  for (int i = 0; i < MT; ++i)
+  for (int i = 0; i < C::MT; ++i)
 #pragma unroll
-    for (int j = 0; j < NTL; ++j)
+    for (int j = 0; j < C::NTL; ++j)
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
-
-  constexpr bool kColSum = HasColSum<P>::value;
-  const bool do_colsum = kColSum && m0 == 0 && wm == 0;
-  f32x16 cs[kColSum ? NTL : 1];
 #pragma unroll
-  for (int j = 0; j < (kColSum ? NTL : 1); ++j)
+  for (int j = 0; j < C::NCS; ++j)
 #pragma unroll
     for (int v = 0; v < 16; ++v) cs[j][v] = 0.f;
-  const bf16x8 ones{(__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f,
-                    (__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f};
-
+  const bool do_colsum = C::kColSum && m0 == 0 && wm == 0;
   auto compute = [&](int buf) {
     const uint8_t* sa = smem + buf * STAGE;
-    const uint8_t* sb = sa + PA::BYTES;
-#pragma unroll
-    for (int s = 0; s < BK / 16; ++s) {
-      bf16x8 fa[MT][NPA], fb[NTL][NPB];
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int pl = 0; pl < NPA; ++pl) fa[i][pl] = PA::frag(sa, pl, wm * TM + i * 32, s, lane);
-#pragma unroll
-      for (int j = 0; j < NTL; ++j)
-#pragma unroll
-        for (int pl = 0; pl < NPB; ++pl) fb[j][pl] = PB::frag(sb, pl, wn * TN + j * 32, s, lane);
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NTL; ++j) {
-          // Smallest terms first: (1,1), (2,0), (0,2), (1,0), (0,1), (0,0).
-          if constexpr (NPA == 3 && NPB == 3) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], acc[i][j], 0, 0, 0);
-          } else if constexpr (NPA == 3) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], acc[i][j], 0, 0, 0);
-          } else if constexpr (NPB == 3) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], acc[i][j], 0, 0, 0);
-          }
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], acc[i][j], 0, 0, 0);
-        }
-      if constexpr (kColSum) {
-        if (do_colsum) {
-#pragma unroll
-          for (int j = 0; j < NTL; ++j)
-#pragma unroll
-            for (int pl = NPB - 1; pl >= 0; --pl)
-              cs[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fb[j][pl], cs[j], 0, 0, 0);
-        }
-      }
-    }
+    C::mma(sa, sa + PA::BYTES, wm, wn, lane, acc, cs, do_colsum);
   };
 
   using S0 = std::integral_constant<int, 0>;
@@ -352,13 +443,22 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in) {
     if (nk > 1) fetch(S1{}, kbeg + BK);
     __syncthreads();
     // Iteration kt: LDS buffer kt & 1 holds stage kt, register set (kt + 1) & 1 holds
-    // stage kt + 1; stage kt + 2 is fetched into set kt & 1.
+    // stage kt + 1 (loaded during iteration kt - 1); stage kt + 2 is fetched into set
+    // kt & 1.  Stage kt + 1 is stashed BEFORE the MFMAs of stage kt (its buffer was last
+    // read in iteration kt - 1, before the barrier), so the LDS stores overlap the MFMAs and
+    // the barrier waits only for the compute.
     auto iter = [&](auto S, int kt) {
       constexpr int set = decltype(S)::value;
       using Other = std::integral_constant<int, set ^ 1>;
-      if (kt + 2 < nk) fetch(S, kbeg + (kt + 2) * BK);
-      compute(set);
-      if (kt + 1 < nk) stash(Other{}, set ^ 1);
+      if constexpr (EARLY_STASH) {
+        if (kt + 1 < nk) stash(Other{}, set ^ 1);
+        if (kt + 2 < nk) fetch(S, kbeg + (kt + 2) * BK);
+        compute(set);
+      } else {
+        if (kt + 2 < nk) fetch(S, kbeg + (kt + 2) * BK);
+        compute(set);
+        if (kt + 1 < nk) stash(Other{}, set ^ 1);
+      }
       __syncthreads();
     };
     int kt = 0;
@@ -381,81 +481,171 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in) {
       __syncthreads();
     }
   }
+  C::epilogue(p, smem, m0, n0, wave, wm, wn, lane, split, acc, cs, do_colsum);
+}
 
-  // Epilogue.  C/D map of the 32x32 MFMA: col = lane & 31, row = (v&3) + 8(v>>2) + 4h.
-  const int r = lane & 31, h = lane >> 5;
-  if constexpr (HasStore8<P>::value) {
-    // Row-major restage through LDS, one 32-row block of the wave's tile at a time, so
-    // each lane finishes 8 consecutive columns of one row (one decode per 8 outputs,
-    // 16-byte plane / 32-byte f32 stores).
-    constexpr int PITCH = TN + 4;
-    float* cw = reinterpret_cast<float*>(smem) + wave * 32 * PITCH;
-    constexpr int CHUNKS = 32 * TN / 8;
+// LDS-DMA kernel: every operand unit goes HBM -> LDS by buffer_load ... lds (no VGPR
+// staging), through a ring of STAGES LDS buffers with STAGES - 1 stages in flight.  Each
+// wave issues the same number of DMA instructions per stage (surplus lanes of a short
+// operand fetch zeros into a scratch KiB), so one counted vmcnt per iteration retires the
+// stage about to be read; one raw s_barrier per iteration publishes it and frees the
+// buffer the next DMA overwrites.
+template <int BM, int BN, int WM, int WN, int BK, int STAGES, class P>
+__global__ void __launch_bounds__(64 * WM * WN) gemm_p3g_kernel(const P p_in) {
+  // Device pass only: hipcc does not emit this template's host launch stub when the host
+  // pass instantiates the body (the LDS-DMA builtins), so the host sees an empty kernel.
+#if defined(__HIP_DEVICE_COMPILE__)
+  using C = P3Core<BM, BN, WM, WN, BK, P>;
+  using PA = typename C::PA;
+  using PB = typename C::PB;
+  constexpr int NW = WM * WN, NPA = C::NPA, NPB = C::NPB, STAGE = C::STAGE;
+  constexpr int PWA = (PA::BLOCKS + NW - 1) / NW, PWB = (PB::BLOCKS + NW - 1) / NW;
+  constexpr int D = PWA * NPA + PWB * NPB;  // DMA instructions per wave per stage
+  static_assert(STAGES >= 2 && STAGES <= 4, "2..4 LDS stages");
+  static_assert((STAGES - 2) * D <= 63, "vmcnt range");
+  const P p = z_select(p_in);
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* scratch = smem + STAGES * STAGE;  // 1 KiB sink of surplus DMA lanes
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int tiles_n = (p.N + BN - 1) / BN;
+  const int tile = blockIdx.x;
+  const int m0 = (tile / tiles_n) * BM;
+  const int n0 = (tile % tiles_n) * BN;
+  const int split = HasZClass<P>::value ? 0 : blockIdx.z;
+  const int kbeg = split * p.k_chunk;
+  int kend = kbeg + p.k_chunk;
+  if (kend > p.K) kend = p.K;
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+
+  // The unit each lane fetches for each of its wave's DMA blocks.
+  typename P::ARow arow[PWA];
+  typename P::BRow brow[PWB];
+  int akk[PWA], bkk[PWB];
 #pragma unroll
-    for (int i = 0; i < MT; ++i) {
-#pragma unroll
-      for (int j = 0; j < NTL; ++j)
-#pragma unroll
-        for (int v = 0; v < 16; ++v)
-          cw[((v & 3) + 8 * (v >> 2) + 4 * h) * PITCH + j * 32 + r] = acc[i][j][v];
-      __syncthreads();
-#pragma unroll
-      for (int c = lane; c < CHUNKS; c += 64) {
-        const int row = c / (TN / 8), col = 8 * (c % (TN / 8));
-        const int m = m0 + wm * TM + i * 32 + row;
-        const int n = n0 + wn * TN + col;
-        const f32x4 lo = *reinterpret_cast<const f32x4*>(cw + row * PITCH + col);
-        const f32x4 hi = *reinterpret_cast<const f32x4*>(cw + row * PITCH + col + 4);
-        const float v8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        if (m < p.M && n < p.N) p.store8(m, n, v8, split);
-      }
-      __syncthreads();
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int j = 0; j < NTL; ++j)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const int m = m0 + wm * TM + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-          const int n = n0 + wn * TN + j * 32 + r;
-          if (m < p.M && n < p.N) p.store(m, n, acc[i][j][v], split);
-        }
+  for (int j = 0; j < PWA; ++j) {
+    const int b = wave + NW * j;
+    const int u = 64 * (b < PA::BLOCKS ? b : 0) + lane;
+    arow[j] = p.a_row(m0 + PA::slot_row(u));
+    akk[j] = PA::slot_kk(u);
   }
-  if constexpr (kColSum) {
-    if (do_colsum && h == 0) {
 #pragma unroll
-      for (int j = 0; j < NTL; ++j) {
-        const int n = n0 + wn * TN + j * 32 + r;
-        if (n < p.N) p.store_colsum(n, cs[j][0], split);
-      }
-    }
+  for (int j = 0; j < PWB; ++j) {
+    const int b = wave + NW * j;
+    const int u = 64 * (b < PB::BLOCKS ? b : 0) + lane;
+    brow[j] = p.b_row(n0 + PB::slot_row(u));
+    bkk[j] = PB::slot_kk(u);
   }
+  __amdgpu_buffer_rsrc_t srcA[NPA], srcB[NPB];
+#pragma unroll
+  for (int pl = 0; pl < NPA; ++pl) srcA[pl] = plane_rsrc(p.a_src, pl);
+#pragma unroll
+  for (int pl = 0; pl < NPB; ++pl) srcB[pl] = plane_rsrc(p.b_src, pl);
+
+  typedef __attribute__((address_space(3))) void lds_void;
+  // DMA of stage `st` (k0 = kbeg + st * BK) into LDS buffer `buf`; stages past the end
+  // fetch zeros (uniform instruction counts keep the vmcnt arithmetic exact).
+  auto issue = [&](int st, int buf) {
+    const int k0 = kbeg + st * BK;
+    uint8_t* sa = smem + buf * STAGE;
+    uint8_t* sb = sa + PA::BYTES;
+#pragma unroll
+    for (int j = 0; j < PWA; ++j) {
+      const int b = wave + NW * j;
+      const bool real = b < PA::BLOCKS;
+      const uint32_t off = (real && k0 + akk[j] < kend) ? p.a_off(arow[j], k0, akk[j]) : kOOB;
+#pragma unroll
+      for (int pl = 0; pl < NPA; ++pl)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            srcA[pl], (lds_void*)(real ? sa + pl * PA::PLANE + 1024 * b : scratch), 16, off, 0, 0,
+            0);
+    }
+#pragma unroll
+    for (int j = 0; j < PWB; ++j) {
+      const int b = wave + NW * j;
+      const bool real = b < PB::BLOCKS;
+      const uint32_t off = (real && k0 + bkk[j] < kend) ? p.b_off(brow[j], k0, bkk[j]) : kOOB;
+#pragma unroll
+      for (int pl = 0; pl < NPB; ++pl)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            srcB[pl], (lds_void*)(real ? sb + pl * PB::PLANE + 1024 * b : scratch), 16, off, 0, 0,
+            0);
+    }
+  };
+
+  f32x16 acc[C::MT][C::NTL];
+  f32x16 cs[C::NCS];
+#pragma unroll
+  for (int i = 0; i < C::MT; ++i)
+#pragma unroll
+    for (int j = 0; j < C::NTL; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
+#pragma unroll
+  for (int j = 0; j < C::NCS; ++j)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) cs[j][v] = 0.f;
+  const bool do_colsum = C::kColSum && m0 == 0 && wm == 0;
+
+  // s_waitcnt immediates (gfx9 encoding): vmcnt(n) alone, and vmcnt(0) + lgkmcnt(0).
+  constexpr int kWaitStage = (((STAGES - 2) * D) & 15) | ((((STAGES - 2) * D) >> 4) << 14) |
+                             (0x7 << 4) | (0xF << 8);
+#pragma unroll
+  for (int st = 0; st < STAGES - 1; ++st) issue(st, st);
+  int buf = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    __builtin_amdgcn_s_waitcnt(kWaitStage);  // this wave's DMA of stage kt has landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();            // ... and every wave's; buffer kt-1 is free
+    asm volatile("" ::: "memory");
+    const int nb = buf == 0 ? STAGES - 1 : buf - 1;  // (kt + STAGES - 1) % STAGES
+    issue(kt + STAGES - 1, nb);
+    const uint8_t* sa = smem + buf * STAGE;
+    C::mma(sa, sa + PA::BYTES, wm, wn, lane, acc, cs, do_colsum);
+    buf = buf == STAGES - 1 ? 0 : buf + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  C::epilogue(p, smem, m0, n0, wave, wm, wn, lane, split, acc, cs, do_colsum);
+#endif
+}
+
+template <class Kern>
+inline hipError_t p3_set_lds(Kern* k, int lds) {
+  if (lds <= 65536) return hipSuccess;
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                             hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 }
 
 template <int BM, int BN, int WM, int WN, int BK, bool DEEP = true, class P>
 inline hipError_t launch_gemm_p3(const P& p, int splits, hipStream_t st) {
-  constexpr int NT = 64 * WM * WN;
-  using PA = PlanP3<BM, NT, P::A_MODE, P::A_PLANES, BK>;
-  using PB = PlanP3<BN, NT, P::B_MODE, P::B_PLANES, BK>;
-  constexpr int STAGES_BYTES = 2 * (PA::BYTES + PB::BYTES);
-  constexpr int EPI_BYTES = HasStore8<P>::value ? WM * WN * 32 * (BN / WN + 4) * 4 : 0;
-  constexpr int LDS = STAGES_BYTES > EPI_BYTES ? STAGES_BYTES : EPI_BYTES;
+  using C = P3Core<BM, BN, WM, WN, BK, P>;
+  constexpr int STAGES_BYTES = 2 * C::STAGE;
+  constexpr int LDS = STAGES_BYTES > C::EPI_BYTES ? STAGES_BYTES : C::EPI_BYTES;
   static_assert(LDS <= 160 * 1024, "two stages must fit the 160-KiB LDS of a CU");
-  if constexpr (LDS > 65536) {
-    static bool attr_set = false;
-    if (!attr_set) {
-      hipError_t e = hipFuncSetAttribute(
-          reinterpret_cast<const void*>(&gemm_p3_kernel<BM, BN, WM, WN, BK, DEEP, P>),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-      if (e != hipSuccess) return e;
-      attr_set = true;
-    }
-  }
+  static hipError_t attr = p3_set_lds(&gemm_p3_kernel<BM, BN, WM, WN, BK, DEEP, P>, LDS);
+  if (attr != hipSuccess) return attr;
   const int tiles = ((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
-  hipLaunchKernelGGL((gemm_p3_kernel<BM, BN, WM, WN, BK, DEEP, P>), dim3(tiles, 1, splits), dim3(NT),
-                     LDS, st, p);
+  hipLaunchKernelGGL((gemm_p3_kernel<BM, BN, WM, WN, BK, DEEP, P>), dim3(tiles, 1, splits),
+                     dim3(C::NT), LDS, st, p);
+  return hipGetLastError();
+}
+
+// LDS-DMA variant (gemm_p3g_kernel) with STAGES buffers.
+template <int BM, int BN, int WM, int WN, int BK, int STAGES, class P>
+inline hipError_t launch_gemm_p3g(const P& p, int splits, hipStream_t st) {
+  using C = P3Core<BM, BN, WM, WN, BK, P>;
+  constexpr int RING = STAGES * C::STAGE + 1024;
+  constexpr int LDS = RING > C::EPI_BYTES ? RING : C::EPI_BYTES;
+  static_assert(LDS <= 160 * 1024, "the stage ring must fit the 160-KiB LDS of a CU");
+  static hipError_t attr = p3_set_lds(&gemm_p3g_kernel<BM, BN, WM, WN, BK, STAGES, P>, LDS);
+  if (attr != hipSuccess) return attr;
+  const int tiles = ((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
+  hipLaunchKernelGGL((gemm_p3g_kernel<BM, BN, WM, WN, BK, STAGES, P>), dim3(tiles, 1, splits),
+                     dim3(C::NT), LDS, st, p);
   return hipGetLastError();
 }
 

@@ -22,6 +22,17 @@ int launch_duel_head_dz(const float* h, const float* g, const int32_t* a, int B,
                         const float* wv, const float* wa, float* dzh, hipStream_t st,
                         uint16_t* planes = nullptr, int64_t pstride = 0);
 
+// Fused DQN head forward: hid = relu(sum_s slab[s] + fcb) ([rows][2H], written) and the
+// duelling q = v + adv - mean(adv) from it (replaces the slab reduction + DuelHeadFwd +
+// duel_head_finish of the f32 path).
+int launch_fc_head_forward(const float* slab, int splits, int rows, int H, const float* fcb,
+                           const float* wv, const float* bv, const float* wa, const float* ba,
+                           int A, float* hid, float* q, hipStream_t st);
+// launch_duel_head_dz writing planes, 8 units per thread.
+int launch_head_dz_planes(const float* h, const float* g, const int32_t* a, int B, int H, int A,
+                          const float* wv, const float* wa, uint16_t* planes, int64_t pstride,
+                          hipStream_t st);
+
 // Sums the DuelHeadWgrad slab [splits][2H+1][A+1] and scatters its block-diagonal parts
 // into the head weight / bias gradients.
 int launch_duel_head_grad_scatter(const float* slab, int splits, int H, int A, float* dwv,

@@ -213,6 +213,182 @@ __device__ __forceinline__ void store_planes4(uint16_t* planes, int64_t pstride,
 // snt.optimizers.Adam (Kingma & Ba Algorithm 1 form):
 //   m = b1 m + (1-b1) g;  v = b2 v + (1-b2) g g
 //   p -= lr * (m / (1 - b1^t)) / (sqrt(v / (1 - b2^t)) + eps)
+// Vectorised deterministic split-K reduction (count, split_at, ncols multiples of 4):
+// 16 float4 columns x 16 split groups per 256-thread block; group g sums splits g, g+16,
+// ... in order, then the groups are added in order.
+__global__ void __launch_bounds__(256) slab_reduce4_kernel(const float* __restrict__ slab,
+                                                           int splits, int64_t count4,
+                                                           float* __restrict__ out0,
+                                                           int64_t split_at4,
+                                                           float* __restrict__ out1,
+                                                           const float* __restrict__ bias,
+                                                           int ncols, int relu) {
+  __shared__ f32x4 red[16][16];
+  const int c = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int64_t e = (int64_t)blockIdx.x * 16 + c;
+  const f32x4* s4 = reinterpret_cast<const f32x4*>(slab);
+  f32x4 acc{0.f, 0.f, 0.f, 0.f};
+  if (e < count4)
+    for (int sp = g; sp < splits; sp += 16) acc += s4[(size_t)sp * count4 + e];
+  red[g][c] = acc;
+  __syncthreads();
+  if (g == 0 && e < count4) {
+    f32x4 v = red[0][c];
+#pragma unroll
+    for (int q = 1; q < 16; ++q) v += red[q][c];
+    if (bias) {
+      const int col = (int)((e * 4) % ncols);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[j] += bias[col + j];
+        if (relu) v[j] = v[j] > 0.f ? v[j] : 0.f;
+      }
+    }
+    if (e < split_at4) reinterpret_cast<f32x4*>(out0)[e] = v;
+    else reinterpret_cast<f32x4*>(out1)[e - split_at4] = v;
+  }
+}
+
+// Fused hidden-layer finish + duelling head (DQN forward): per row, hid = relu(sum of the
+// split-K slab + bias) (written out for the backward), then
+// q = v + adv - mean(adv) with v = hid[:H] . wv + bv, adv_j = hid[H:] . wa[:, j] + ba_j
+// (acme/tf/networks/duelling.py:51-57).  4 rows per 256-thread block: the advantage
+// weights are staged once per block in LDS, each wave finishes one row with lane-parallel
+// partial dot products and a fixed shuffle tree (deterministic).
+constexpr int kHeadRows = 4;
+constexpr int kHeadChunk = 8;  // advantage outputs per accumulation pass
+template <int SPL>
+__global__ void __launch_bounds__(256) fc_head_forward_kernel(
+    const float* __restrict__ slab, int splits, int rows, int H, const float* __restrict__ fcb,
+    const float* __restrict__ wv, const float* __restrict__ bv, const float* __restrict__ wa,
+    const float* __restrict__ ba, int A, float* __restrict__ hid, float* __restrict__ q) {
+  extern __shared__ float sh[];  // [kHeadRows][2H] hid | [H][A] wa | [kHeadRows][A + 1] dots
+  float* swa = sh + kHeadRows * 2 * H;
+  float* dots = swa + H * A;
+  const int r0 = blockIdx.x * kHeadRows;
+  const int n4 = 2 * H / 4;
+  const int64_t count4 = (int64_t)rows * n4;
+  const f32x4* s4 = reinterpret_cast<const f32x4*>(slab);
+  for (int t = threadIdx.x; t < H * A; t += 256) swa[t] = wa[t];
+  for (int t = threadIdx.x; t < kHeadRows * n4; t += 256) {
+    const int rr = t / n4, c4 = t - rr * n4;
+    const int row = r0 + rr;
+    if (row >= rows) continue;
+    const int64_t e = (int64_t)row * n4 + c4;
+    f32x4 v;
+    if constexpr (SPL > 0) {
+      f32x4 part[SPL];
+#pragma unroll
+      for (int sp = 0; sp < SPL; ++sp) part[sp] = s4[(size_t)sp * count4 + e];
+      v = part[0];
+#pragma unroll
+      for (int sp = 1; sp < SPL; ++sp) v += part[sp];
+    } else {
+      v = s4[e];
+      for (int sp = 1; sp < splits; ++sp) v += s4[(size_t)sp * count4 + e];
+    }
+    const f32x4 b = reinterpret_cast<const f32x4*>(fcb)[c4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const float x = v[jj] + b[jj];
+      v[jj] = x > 0.f ? x : 0.f;
+    }
+    reinterpret_cast<f32x4*>(hid)[e] = v;
+    reinterpret_cast<f32x4*>(sh + rr * 2 * H)[c4] = v;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  auto wave_sum = [](float x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+    return x;
+  };
+  for (int rr = wave; rr < kHeadRows; rr += 4) {
+    const float* h = sh + rr * 2 * H;
+    float av = 0.f;
+    for (int k = lane; k < H; k += 64) av = fmaf(h[k], wv[k], av);
+    av = wave_sum(av);
+    if (lane == 0) dots[rr * (A + 1) + A] = av + bv[0];
+    for (int j0 = 0; j0 < A; j0 += kHeadChunk) {
+      float acc[kHeadChunk];
+#pragma unroll
+      for (int jj = 0; jj < kHeadChunk; ++jj) acc[jj] = 0.f;
+      for (int k = lane; k < H; k += 64) {
+        const float x = h[H + k];
+        const float* w = swa + k * A + j0;
+#pragma unroll
+        for (int jj = 0; jj < kHeadChunk; ++jj)
+          if (j0 + jj < A) acc[jj] = fmaf(x, w[jj], acc[jj]);
+      }
+#pragma unroll
+      for (int jj = 0; jj < kHeadChunk; ++jj) {
+        const float d = wave_sum(acc[jj]);
+        if (lane == 0 && j0 + jj < A) dots[rr * (A + 1) + j0 + jj] = d + ba[j0 + jj];
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < kHeadRows) {
+    const int rr = threadIdx.x, row = r0 + rr;
+    if (row < rows) {
+      const float* d = dots + rr * (A + 1);
+      float mean = 0.f;
+      for (int jj = 0; jj < A; ++jj) mean += d[jj];
+      mean /= (float)A;
+      for (int jj = 0; jj < A; ++jj) q[(size_t)row * A + jj] = d[A] + (d[jj] - mean);
+    }
+  }
+}
+
+// dZ of the fused hidden layer as planes, 8 consecutive units per thread:
+// k < H: g_b wv[k];  k >= H: g_b (wa[k-H][a_b] - mean_j wa[k-H][j]); masked by hid > 0.
+__global__ void __launch_bounds__(256) head_dz_planes_kernel(
+    const float* __restrict__ h, const float* __restrict__ g, const int32_t* __restrict__ a,
+    int B, int H, int A, const float* __restrict__ wv, const float* __restrict__ wa,
+    uint16_t* __restrict__ planes, int64_t pstride) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int per = 2 * H / 8;
+  if (t >= (int64_t)B * per) return;
+  const int b = (int)(t / per), k0 = 8 * (int)(t - (int64_t)b * per);
+  const float gb = g[b];
+  const int ab = a[b];
+  const float inv_a = 1.f / (float)A;
+  const float* hr = h + (size_t)b * 2 * H + k0;
+  const f32x4 h0 = reinterpret_cast<const f32x4*>(hr)[0], h1 = reinterpret_cast<const f32x4*>(hr)[1];
+  const float hv[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+  float d[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = k0 + j;
+    float v;
+    if (k < H) {
+      v = gb * wv[k];
+    } else {
+      // dadv_i = g_b (1[i == a_b] - 1/A);  dh_k = sum_i dadv_i wa[k][i] (fixed order).
+      const float* row = wa + (size_t)(k - H) * A;
+      float s = 0.f;
+#pragma unroll 6
+      for (int i = 0; i < A; ++i) s = fmaf(gb * ((i == ab ? 1.f : 0.f) - inv_a), row[i], s);
+      v = s;
+    }
+    d[j] = hv[j] > 0.f ? v : 0.f;
+  }
+  uint32_t ph[4], pm[4], pl[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    uint16_t x0, y0, z0, x1, y1, z1;
+    gemm::split3_bits(d[2 * j], x0, y0, z0);
+    gemm::split3_bits(d[2 * j + 1], x1, y1, z1);
+    ph[j] = x0 | ((uint32_t)x1 << 16);
+    pm[j] = y0 | ((uint32_t)y1 << 16);
+    pl[j] = z0 | ((uint32_t)z1 << 16);
+  }
+  const int64_t e = (int64_t)b * 2 * H + k0;
+  *reinterpret_cast<uint4*>(planes + e) = uint4{ph[0], ph[1], ph[2], ph[3]};
+  *reinterpret_cast<uint4*>(planes + pstride + e) = uint4{pm[0], pm[1], pm[2], pm[3]};
+  *reinterpret_cast<uint4*>(planes + 2 * pstride + e) = uint4{pl[0], pl[1], pl[2], pl[3]};
+}
+
 __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p,
                                                    const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
@@ -434,10 +610,49 @@ int launch_dqn_loss(const LossArgs& args, hipStream_t st) {
   return ACME_OK;
 }
 
+int launch_fc_head_forward(const float* slab, int splits, int rows, int H, const float* fcb,
+                           const float* wv, const float* bv, const float* wa, const float* ba,
+                           int A, float* hid, float* q, hipStream_t st) {
+  ACME_CHECK_ARG(H % 2 == 0 && A >= 1 && splits >= 1 && rows >= 1, "bad head shape");
+  const size_t shmem = sizeof(float) * (kHeadRows * 2 * H + (size_t)H * A + kHeadRows * (A + 1));
+  ACME_CHECK_ARG(shmem <= 65536, "head too large for the fused head kernel");
+  const unsigned grid = (unsigned)ceil_div(rows, kHeadRows);
+  if (splits == 8)
+    fc_head_forward_kernel<8><<<grid, 256, shmem, st>>>(slab, splits, rows, H, fcb, wv, bv, wa, ba,
+                                                         A, hid, q);
+  else
+    fc_head_forward_kernel<0><<<grid, 256, shmem, st>>>(slab, splits, rows, H, fcb, wv, bv, wa, ba,
+                                                         A, hid, q);
+  ACME_LAUNCH_CHECK();
+  return ACME_OK;
+}
+
+int launch_head_dz_planes(const float* h, const float* g, const int32_t* a, int B, int H, int A,
+                          const float* wv, const float* wa, uint16_t* planes, int64_t pstride,
+                          hipStream_t st) {
+  ACME_CHECK_ARG((2 * H) % 8 == 0 && pstride % 8 == 0, "bad head_dz shape");
+  const int64_t n = (int64_t)B * (2 * H / 8);
+  head_dz_planes_kernel<<<(unsigned)ceil_div(n, 256), 256, 0, st>>>(h, g, a, B, H, A, wv, wa,
+                                                                    planes, pstride);
+  ACME_LAUNCH_CHECK();
+  return ACME_OK;
+}
+
 int launch_slab_reduce(const float* slab, int splits, int64_t count, float* out0,
                        int64_t split_at, float* out1, const float* bias, int ncols, int relu,
                        hipStream_t st) {
   ACME_CHECK_ARG(splits >= 1 && count >= 1, "bad slab shape");
+  const bool vec = count % 4 == 0 && split_at % 4 == 0 && (!bias || ncols % 4 == 0) &&
+                   reinterpret_cast<uintptr_t>(slab) % 16 == 0 &&
+                   reinterpret_cast<uintptr_t>(out0) % 16 == 0 &&
+                   (split_at >= count || reinterpret_cast<uintptr_t>(out1) % 16 == 0);
+  if (vec) {
+    const int64_t count4 = count / 4;
+    slab_reduce4_kernel<<<(unsigned)ceil_div(count4, 16), 256, 0, st>>>(
+        slab, splits, count4, out0, split_at / 4, out1, bias, ncols, relu);
+    ACME_LAUNCH_CHECK();
+    return ACME_OK;
+  }
   slab_reduce_kernel<<<(unsigned)ceil_div(count, 64), 256, 0, st>>>(slab, splits, count, out0,
                                                                     split_at, out1, bias, ncols,
                                                                     relu);

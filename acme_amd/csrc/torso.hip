@@ -145,6 +145,15 @@ constexpr int kP3Conv1WgradSplits = 256, kP3Conv2WgradSplits = 64, kP3Conv3Wgrad
       return ACME_ERR_HIP;                                                                    \
     }                                                                                         \
   } while (0)
+#define P3G_GEMM(name, BM, BN, WM, WN, BK, ST, prob, splits)                                 \
+  do {                                                                                        \
+    ACME_PROF(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0);  \
+    hipError_t _e = gemm::launch_gemm_p3g<BM, BN, WM, WN, BK, ST>(prob, splits, st);         \
+    if (_e != hipSuccess) {                                                                   \
+      set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
+      return ACME_ERR_HIP;                                                                    \
+    }                                                                                         \
+  } while (0)
 #define P3_GEMM(name, BM, BN, WM, WN, BK, prob, splits)                                      \
   P3_GEMM_F(name, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, BM, BN, WM, \
             WN, BK, prob, splits)
@@ -185,6 +194,8 @@ int forward_p3(const PWeights& w, const uint16_t* frames, int rows, const PActs&
     switch (tune_variant("P3C1F")) {
       case 1: P3_GEMM("conv1_fwd", 128, 32, 4, 1, 32, p, 1); break;
       case 2: P3_GEMM("conv1_fwd", 256, 32, 4, 1, 32, p, 1); break;
+      case 3: P3G_GEMM("conv1_fwd", 256, 32, 4, 1, 16, 3, p, 1); break;
+      case 4: P3G_GEMM("conv1_fwd", 256, 32, 4, 1, 32, 3, p, 1); break;
       default: P3_GEMM("conv1_fwd", 256, 32, 4, 1, 16, p, 1); break;
     }
   }
@@ -196,6 +207,8 @@ int forward_p3(const PWeights& w, const uint16_t* frames, int rows, const PActs&
     switch (tune_variant("P3C2F")) {
       case 1: P3_GEMM("conv2_fwd", 128, 64, 2, 2, 16, p, 1); break;
       case 2: P3_GEMM("conv2_fwd", 256, 64, 4, 1, 32, p, 1); break;
+      case 3: P3G_GEMM("conv2_fwd", 128, 64, 2, 2, 32, 3, p, 1); break;
+      case 4: P3G_GEMM("conv2_fwd", 128, 64, 2, 2, 16, 4, p, 1); break;
       default: P3_GEMM("conv2_fwd", 128, 64, 2, 2, 32, p, 1); break;
     }
   }
@@ -207,6 +220,8 @@ int forward_p3(const PWeights& w, const uint16_t* frames, int rows, const PActs&
     switch (tune_variant("P3C3F")) {
       case 1: P3_GEMM("conv3_fwd", 128, 64, 2, 2, 16, p, 1); break;
       case 2: P3_GEMM("conv3_fwd", 256, 64, 4, 1, 32, p, 1); break;
+      case 3: P3G_GEMM("conv3_fwd", 128, 64, 2, 2, 32, 3, p, 1); break;
+      case 4: P3G_GEMM("conv3_fwd", 128, 64, 2, 2, 16, 4, p, 1); break;
       default: P3_GEMM("conv3_fwd", 128, 64, 2, 2, 32, p, 1); break;
     }
   }
@@ -223,7 +238,8 @@ int backward_p3(const PWeights& w, const Grads& g, const uint16_t* frames, int r
     p.k_chunk = chunk_for(p.K, kP3Conv3WgradSplits);
     p.a_src = src(a.x2, (int64_t)rows * kFlat); p.b_src = src(dz3, (int64_t)rows * kFlat);
     p.slab = slab;
-    P3_GEMM("conv3_wgrad", 128, 64, 2, 2, 32, p, kP3Conv3WgradSplits);
+    if (tune_variant("P3C3W") == 1) P3G_GEMM("conv3_wgrad", 128, 64, 2, 2, 32, 3, p, kP3Conv3WgradSplits);
+    else P3_GEMM("conv3_wgrad", 128, 64, 2, 2, 32, p, kP3Conv3WgradSplits);
     if ((rc = p3_wgrad_reduce(p, kP3Conv3WgradSplits, slab, g.w3, g.b3, "conv3_wgrad_reduce", st)))
       return rc;
   }
@@ -235,6 +251,7 @@ int backward_p3(const PWeights& w, const Grads& g, const uint16_t* frames, int r
     switch (tune_variant("P3C3D")) {
       case 1: P3_GEMM("conv3_dgrad", 128, 64, 2, 2, 16, p, 1); break;
       case 2: P3_GEMM("conv3_dgrad", 256, 64, 4, 1, 32, p, 1); break;
+      case 3: P3G_GEMM("conv3_dgrad", 128, 64, 2, 2, 32, 3, p, 1); break;
       default: P3_GEMM("conv3_dgrad", 128, 64, 2, 2, 32, p, 1); break;
     }
   }
@@ -244,7 +261,8 @@ int backward_p3(const PWeights& w, const Grads& g, const uint16_t* frames, int r
     p.k_chunk = chunk_for(p.K, kP3Conv2WgradSplits);
     p.a_src = src(a.x1, (int64_t)rows * kX1); p.b_src = src(dz2, (int64_t)rows * kFlat);
     p.slab = slab;
-    P3_GEMM("conv2_wgrad", 128, 64, 2, 2, 32, p, kP3Conv2WgradSplits);
+    if (tune_variant("P3C2W") == 1) P3G_GEMM("conv2_wgrad", 128, 64, 2, 2, 32, 3, p, kP3Conv2WgradSplits);
+    else P3_GEMM("conv2_wgrad", 128, 64, 2, 2, 32, p, kP3Conv2WgradSplits);
     if ((rc = p3_wgrad_reduce(p, kP3Conv2WgradSplits, slab, g.w2, g.b2, "conv2_wgrad_reduce", st)))
       return rc;
   }
@@ -258,6 +276,12 @@ int backward_p3(const PWeights& w, const Grads& g, const uint16_t* frames, int r
     switch (tune_variant("P3C2D")) {
       case 1: P3_GEMM_F("conv2_dgrad", fl, 256, 32, 4, 1, 32, p, G2::S * G2::S); break;
       case 2: P3_GEMM_F("conv2_dgrad", fl, 256, 32, 4, 1, 16, p, G2::S * G2::S); break;
+      case 3: {
+        ACME_PROF("conv2_dgrad", st, fl, 0.0);
+        hipError_t e = gemm::launch_gemm_p3g<128, 32, 4, 1, 32, 3>(p, G2::S * G2::S, st);
+        if (e != hipSuccess) return (set_error("gemm launch failed: %s", hipGetErrorString(e)), ACME_ERR_HIP);
+        break;
+      }
       default: P3_GEMM_F("conv2_dgrad", fl, 128, 32, 4, 1, 32, p, G2::S * G2::S); break;
     }
   }
@@ -267,7 +291,8 @@ int backward_p3(const PWeights& w, const Grads& g, const uint16_t* frames, int r
     p.k_chunk = chunk_for(p.K, kP3Conv1WgradSplits);
     p.a_src = frames_src(frames, rows); p.b_src = src(dz1, (int64_t)rows * kX1);
     p.slab = slab;
-    P3_GEMM("conv1_wgrad", 256, 32, 4, 1, 32, p, kP3Conv1WgradSplits);
+    if (tune_variant("P3C1W") == 1) P3G_GEMM("conv1_wgrad", 256, 32, 4, 1, 32, 3, p, kP3Conv1WgradSplits);
+    else P3_GEMM("conv1_wgrad", 256, 32, 4, 1, 32, p, kP3Conv1WgradSplits);
     return p3_wgrad_reduce(p, kP3Conv1WgradSplits, slab, g.w1, g.b1, "conv1_wgrad_reduce", st);
   }
 }
