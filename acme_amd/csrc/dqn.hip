@@ -217,11 +217,12 @@ int tune(const char* key) { return tune_variant(key); }
 
 // Split counts (K-splits) of the launches whose natural grid is too small to fill 256 CUs.
 constexpr int kFcFwdSplits = 8;  // [rows, 1024] x K 7744: 128x128 tiles: 8x8x8 = 512 blocks (online)
+constexpr int kFcFwdMaxSplits = 32;  // slab capacity for the plane path's split choices
 constexpr int kHeadFwdSplits = 16;  // [rows, A+1] x K 1024
 constexpr int kHeadBwdSplits = 8;   // [1024, A+1] x K = batch
 
 int64_t slab_floats_needed(int B, int A) {
-  return std::max<int64_t>({torso::wgrad_slab_floats(), (int64_t)kFcFwdSplits * 2 * B * 2 * kHidden,
+  return std::max<int64_t>({torso::wgrad_slab_floats(), (int64_t)kFcFwdMaxSplits * 2 * B * 2 * kHidden,
                             (int64_t)kHeadFwdSplits * 2 * B * (A + 1),
                             (int64_t)kHeadBwdSplits * (2 * kHidden + 1) * (A + 1)});
 }
@@ -294,16 +295,23 @@ int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const uint16
   if (rc != ACME_OK) return rc;
   {
     P3DenseFwd p;
-    const int splits = kFcFwdSplits;
+    // Split-K: about one round of blocks (128x128 tiles, one block per CU at BK 32).
+    const int sv = tune("P3FCS");
+    const int fv = tune("P3FCF");
+    int splits = sv > 0 && sv <= kFcFwdMaxSplits ? sv : (rows > 512 ? 4 : kFcFwdSplits);
+    if (sv <= 0 && fv == 6) splits = rows > 512 ? 8 : 16;   // 256x128 tiles
+    if (sv <= 0 && fv == 7) splits = rows > 512 ? 16 : 32;  // 256x256 tiles
     p.M = rows; p.N = 2 * kHidden; p.K = kFlat; p.k_chunk = chunk_for(kFlat, splits);
     p.a_src = SRC(x3, (int64_t)rows * kFlat); p.ldx = kFlat;
     p.b_src = SRC(WP(l, wpl, l->t_fcw), (int64_t)kFlat * 2 * kHidden); p.slab = l->slab;
-    switch (tune("P3FCF")) {
+    switch (fv) {
       case 1: ACME_P3_GEMM("fc_fwd", 128, 128, 2, 2, 16, p, splits); break;
       case 2: ACME_P3_GEMM("fc_fwd", 256, 128, 4, 2, 16, p, splits); break;
       case 3: ACME_P3G_GEMM("fc_fwd", 128, 128, 2, 2, 16, 3, p, splits); break;
       case 4: ACME_P3G_GEMM("fc_fwd", 128, 128, 2, 2, 32, 3, p, splits); break;
       case 5: ACME_P3G_GEMM("fc_fwd", 128, 128, 2, 2, 16, 4, p, splits); break;
+      case 6: ACME_P3_GEMM("fc_fwd", 256, 128, 4, 2, 16, p, splits); break;
+      case 7: ACME_P3_GEMM("fc_fwd", 256, 256, 4, 2, 16, p, splits); break;
       default: ACME_P3_GEMM("fc_fwd", 128, 128, 2, 2, 32, p, splits); break;
     }
     ACME_PROF("fc_head_fwd", st, 0.0, 4.0 * (double)rows * 2 * kHidden * (splits + 1));

@@ -45,8 +45,46 @@
 #include "gemm.h"
 #include "gemm_x6.h"
 
+#ifndef P3_EXP
+#define P3_EXP 0  // bottleneck experiments: 1 no global loads, 2 no LDS fragment reads, 3 no MFMA,
+                  // 4 no loads and no LDS stores, 5 = 4 without the per-stage barrier
+#endif
+
 namespace acme {
 namespace gemm {
+
+// XCD-aware block placement.  Blocks are dealt round-robin over the 8 XCDs (block b and
+// b + 8 share one L2; MI355X_MICROARCH.md, Workgroup dispatch), so the flat block id is
+// remapped (bijectively) to give each XCD one contiguous range of the logical order, in
+// which consecutive tiles share an operand panel: K-splits outermost (a split's A and B
+// slabs stay in one L2), then tiles with the LARGER operand's panel index slowest.
+struct BlockPlace {
+  int m0, n0, z;
+};
+template <int BM, int BN>
+__device__ __forceinline__ BlockPlace place_block(int M, int N, int n_major) {
+  const int tiles = gridDim.x;
+  const int total = tiles * gridDim.z;
+  const int orig = blockIdx.x + tiles * blockIdx.z;
+  const int xcd = orig & 7, q = total >> 3, r = total & 7;
+  const int L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int z = L / tiles, t = L - z * tiles;
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+  int mt, nt;
+  if (n_major) {
+    nt = t / tiles_m;
+    mt = t - nt * tiles_m;
+  } else {
+    mt = t / tiles_n;
+    nt = t - mt * tiles_n;
+  }
+  return BlockPlace{mt * BM, nt * BN, z};
+}
+template <class P>
+__device__ __forceinline__ P z_select_at(const P& p, int z) {
+  if constexpr (HasZClass<P>::value) return p.for_z(z);
+  else return p;
+}
 
 using u32x4 = __attribute__((ext_vector_type(4))) uint32_t;
 using i16x4 = __attribute__((ext_vector_type(4))) short;
@@ -226,11 +264,22 @@ struct P3Core {
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
-        for (int pl = 0; pl < NPA; ++pl) fa[i][pl] = PA::frag(sa, pl, wm * TM + i * 32, s, lane);
+        for (int pl = 0; pl < NPA; ++pl)
+          fa[i][pl] = P3_EXP == 2 ? ones : PA::frag(sa, pl, wm * TM + i * 32, s, lane);
 #pragma unroll
       for (int j = 0; j < NTL; ++j)
 #pragma unroll
-        for (int pl = 0; pl < NPB; ++pl) fb[j][pl] = PB::frag(sb, pl, wn * TN + j * 32, s, lane);
+        for (int pl = 0; pl < NPB; ++pl)
+          fb[j][pl] = P3_EXP == 2 ? ones : PB::frag(sb, pl, wn * TN + j * 32, s, lane);
+      if constexpr (P3_EXP == 3) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int j = 0; j < NTL; ++j)
+            acc[i][j][0] += (float)fa[i][0][0] + (float)fb[j][0][0] + (float)fa[i][NPA - 1][1] +
+                            (float)fb[j][NPB - 1][1];
+        continue;
+      }
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -329,23 +378,21 @@ struct P3Core {
 // Register-staged kernel: global -> VGPR -> LDS, two LDS stages; with DEEP two register
 // sets so a stage's loads are issued two stages before its compute.
 template <int BM, int BN, int WM, int WN, int BK, bool DEEP, class P>
-__global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in) {
+__global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in, int n_major) {
   constexpr bool EARLY_STASH = P3_EARLY_STASH;
   using C = P3Core<BM, BN, WM, WN, BK, P>;
   using PA = typename C::PA;
   using PB = typename C::PB;
   constexpr int NT = C::NT, NPA = C::NPA, NPB = C::NPB, STAGE = C::STAGE;
-  const P p = z_select(p_in);
+  const BlockPlace bp = place_block<BM, BN>(p_in.M, p_in.N, n_major);
+  const P p = z_select_at(p_in, bp.z);
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  const int tiles_n = (p.N + BN - 1) / BN;
-  const int tile = blockIdx.x;
-  const int m0 = (tile / tiles_n) * BM;
-  const int n0 = (tile % tiles_n) * BN;
-  const int split = HasZClass<P>::value ? 0 : blockIdx.z;
+  const int m0 = bp.m0, n0 = bp.n0;
+  const int split = HasZClass<P>::value ? 0 : bp.z;
   const int kbeg = split * p.k_chunk;
   int kend = kbeg + p.k_chunk;
   if (kend > p.K) kend = p.K;
@@ -377,8 +424,8 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in) {
       const uint32_t off = (PA::owns(u) && k0 + kk < kend) ? p.a_off(arow[i], k0, kk) : kOOB;
 #pragma unroll
       for (int pl = 0; pl < NPA; ++pl)
-        ra[set][i][pl] =
-            __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srcA[pl], off, 0, 0));
+        ra[set][i][pl] = (P3_EXP == 1 || P3_EXP >= 4) ? u32x4{off, (uint32_t)k0, 1u, 2u}
+                                     : __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srcA[pl], off, 0, 0));
     }
 #pragma unroll
     for (int i = 0; i < PB::PER_THREAD; ++i) {
@@ -387,12 +434,13 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in) {
       const uint32_t off = (PB::owns(u) && k0 + kk < kend) ? p.b_off(brow[i], k0, kk) : kOOB;
 #pragma unroll
       for (int pl = 0; pl < NPB; ++pl)
-        rb[set][i][pl] =
-            __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srcB[pl], off, 0, 0));
+        rb[set][i][pl] = (P3_EXP == 1 || P3_EXP >= 4) ? u32x4{off, (uint32_t)k0, 1u, 2u}
+                                     : __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srcB[pl], off, 0, 0));
     }
   };
   auto stash = [&](auto S, int buf) {
     constexpr int set = decltype(S)::value;
+    if constexpr (P3_EXP >= 4) return;
     uint8_t* sa = smem + buf * STAGE;
     uint8_t* sb = sa + PA::BYTES;
 #pragma unroll
@@ -459,7 +507,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in) {
         compute(set);
         if (kt + 1 < nk) stash(Other{}, set ^ 1);
       }
-      __syncthreads();
+      if constexpr (P3_EXP != 5) __syncthreads();
     };
     int kt = 0;
     for (; kt + 1 < nk; kt += 2) {
@@ -491,7 +539,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in) {
 // stage about to be read; one raw s_barrier per iteration publishes it and frees the
 // buffer the next DMA overwrites.
 template <int BM, int BN, int WM, int WN, int BK, int STAGES, class P>
-__global__ void __launch_bounds__(64 * WM * WN) gemm_p3g_kernel(const P p_in) {
+__global__ void __launch_bounds__(64 * WM * WN) gemm_p3g_kernel(const P p_in, int n_major) {
   // Device pass only: hipcc does not emit this template's host launch stub when the host
   // pass instantiates the body (the LDS-DMA builtins), so the host sees an empty kernel.
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -503,18 +551,16 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3g_kernel(const P p_in) {
   constexpr int D = PWA * NPA + PWB * NPB;  // DMA instructions per wave per stage
   static_assert(STAGES >= 2 && STAGES <= 4, "2..4 LDS stages");
   static_assert((STAGES - 2) * D <= 63, "vmcnt range");
-  const P p = z_select(p_in);
+  const BlockPlace bp = place_block<BM, BN>(p_in.M, p_in.N, n_major);
+  const P p = z_select_at(p_in, bp.z);
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* scratch = smem + STAGES * STAGE;  // 1 KiB sink of surplus DMA lanes
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
-  const int tiles_n = (p.N + BN - 1) / BN;
-  const int tile = blockIdx.x;
-  const int m0 = (tile / tiles_n) * BM;
-  const int n0 = (tile % tiles_n) * BN;
-  const int split = HasZClass<P>::value ? 0 : blockIdx.z;
+  const int m0 = bp.m0, n0 = bp.n0;
+  const int split = HasZClass<P>::value ? 0 : bp.z;
   const int kbeg = split * p.k_chunk;
   int kend = kbeg + p.k_chunk;
   if (kend > p.K) kend = p.K;
@@ -613,6 +659,12 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3g_kernel(const P p_in) {
 #endif
 }
 
+// Tile order: B's panels slowest when B is the larger operand (N * planes > M * planes).
+template <class P>
+inline int p3_n_major(const P& p) {
+  return (int64_t)p.N * P::B_PLANES > (int64_t)p.M * P::A_PLANES ? 1 : 0;
+}
+
 template <class Kern>
 inline hipError_t p3_set_lds(Kern* k, int lds) {
   if (lds <= 65536) return hipSuccess;
@@ -630,7 +682,7 @@ inline hipError_t launch_gemm_p3(const P& p, int splits, hipStream_t st) {
   if (attr != hipSuccess) return attr;
   const int tiles = ((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
   hipLaunchKernelGGL((gemm_p3_kernel<BM, BN, WM, WN, BK, DEEP, P>), dim3(tiles, 1, splits),
-                     dim3(C::NT), LDS, st, p);
+                     dim3(C::NT), LDS, st, p, p3_n_major(p));
   return hipGetLastError();
 }
 
@@ -645,7 +697,7 @@ inline hipError_t launch_gemm_p3g(const P& p, int splits, hipStream_t st) {
   if (attr != hipSuccess) return attr;
   const int tiles = ((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
   hipLaunchKernelGGL((gemm_p3g_kernel<BM, BN, WM, WN, BK, STAGES, P>), dim3(tiles, 1, splits),
-                     dim3(C::NT), LDS, st, p);
+                     dim3(C::NT), LDS, st, p, p3_n_major(p));
   return hipGetLastError();
 }
 

@@ -257,11 +257,12 @@ __global__ void __launch_bounds__(256) slab_reduce4_kernel(const float* __restri
 // partial dot products and a fixed shuffle tree (deterministic).
 constexpr int kHeadRows = 4;
 constexpr int kHeadChunk = 8;  // advantage outputs per accumulation pass
-template <int SPL>
+template <int SPL, int HC>
 __global__ void __launch_bounds__(256) fc_head_forward_kernel(
-    const float* __restrict__ slab, int splits, int rows, int H, const float* __restrict__ fcb,
+    const float* __restrict__ slab, int splits, int rows, int H_, const float* __restrict__ fcb,
     const float* __restrict__ wv, const float* __restrict__ bv, const float* __restrict__ wa,
     const float* __restrict__ ba, int A, float* __restrict__ hid, float* __restrict__ q) {
+  const int H = HC > 0 ? HC : H_;  // compile-time hidden width when HC > 0
   extern __shared__ float sh[];  // [kHeadRows][2H] hid | [H][A] wa | [kHeadRows][A + 1] dots
   float* swa = sh + kHeadRows * 2 * H;
   float* dots = swa + H * A;
@@ -269,7 +270,15 @@ __global__ void __launch_bounds__(256) fc_head_forward_kernel(
   const int n4 = 2 * H / 4;
   const int64_t count4 = (int64_t)rows * n4;
   const f32x4* s4 = reinterpret_cast<const f32x4*>(slab);
-  for (int t = threadIdx.x; t < H * A; t += 256) swa[t] = wa[t];
+  if ((H * A) % 4 == 0) {
+    const int n = H * A / 4;
+#pragma unroll 4
+    for (int t = threadIdx.x; t < n; t += 256)
+      reinterpret_cast<f32x4*>(swa)[t] = reinterpret_cast<const f32x4*>(wa)[t];
+  } else {
+    for (int t = threadIdx.x; t < H * A; t += 256) swa[t] = wa[t];
+  }
+#pragma unroll
   for (int t = threadIdx.x; t < kHeadRows * n4; t += 256) {
     const int rr = t / n4, c4 = t - rr * n4;
     const int row = r0 + rr;
@@ -617,12 +626,16 @@ int launch_fc_head_forward(const float* slab, int splits, int rows, int H, const
   const size_t shmem = sizeof(float) * (kHeadRows * 2 * H + (size_t)H * A + kHeadRows * (A + 1));
   ACME_CHECK_ARG(shmem <= 65536, "head too large for the fused head kernel");
   const unsigned grid = (unsigned)ceil_div(rows, kHeadRows);
-  if (splits == 8)
-    fc_head_forward_kernel<8><<<grid, 256, shmem, st>>>(slab, splits, rows, H, fcb, wv, bv, wa, ba,
-                                                         A, hid, q);
+  const bool wa16 = reinterpret_cast<uintptr_t>(wa) % 16 == 0;
+  if (H == 512 && wa16 && splits == 8)
+    fc_head_forward_kernel<8, 512><<<grid, 256, shmem, st>>>(slab, splits, rows, H, fcb, wv, bv, wa,
+                                                              ba, A, hid, q);
+  else if (H == 512 && wa16 && splits == 4)
+    fc_head_forward_kernel<4, 512><<<grid, 256, shmem, st>>>(slab, splits, rows, H, fcb, wv, bv, wa,
+                                                              ba, A, hid, q);
   else
-    fc_head_forward_kernel<0><<<grid, 256, shmem, st>>>(slab, splits, rows, H, fcb, wv, bv, wa, ba,
-                                                         A, hid, q);
+    fc_head_forward_kernel<0, 0><<<grid, 256, shmem, st>>>(slab, splits, rows, H, fcb, wv, bv, wa,
+                                                            ba, A, hid, q);
   ACME_LAUNCH_CHECK();
   return ACME_OK;
 }

@@ -134,7 +134,14 @@ int backward(const Weights& w, const Grads& g, bool u8, const void* obs, int row
 // ---------------------------------------------------------------- plane path
 namespace {
 
-constexpr int kP3Conv1WgradSplits = 256, kP3Conv2WgradSplits = 64, kP3Conv3WgradSplits = 64;
+// Weight-gradient K splits (defaults; ACME_V_P3C<i>WS overrides up to the cap that sizes the
+// slab).
+constexpr int kP3Conv1WgradSplits = 512, kP3Conv2WgradSplits = 128, kP3Conv3WgradSplits = 128;
+constexpr int kP3MaxWgradSplits = 512;
+int wsplits(const char* key, int def) {
+  const int v = tune_variant(key);
+  return v > 0 && v <= kP3MaxWgradSplits ? v : def;
+}
 
 #define P3_GEMM_F(name, flops, BM, BN, WM, WN, BK, prob, splits)                             \
   do {                                                                                        \
@@ -179,9 +186,9 @@ int p3_wgrad_reduce(const P& p, int splits, float* slab, float* dw, float* db, c
 }  // namespace
 
 int64_t wgrad_slab_floats_p3() {
-  return std::max<int64_t>({(int64_t)kP3Conv1WgradSplits * (G1::K + 1) * G1::CO,
-                            (int64_t)kP3Conv2WgradSplits * (G2::K + 1) * G2::CO,
-                            (int64_t)kP3Conv3WgradSplits * (G3::K + 1) * G3::CO});
+  return std::max<int64_t>({(int64_t)kP3MaxWgradSplits * (G1::K + 1) * G1::CO,
+                            (int64_t)kP3MaxWgradSplits * (G2::K + 1) * G2::CO,
+                            (int64_t)kP3MaxWgradSplits * (G3::K + 1) * G3::CO});
 }
 
 int forward_p3(const PWeights& w, const uint16_t* frames, int rows, const PActs& a,
@@ -235,12 +242,13 @@ int backward_p3(const PWeights& w, const Grads& g, const uint16_t* frames, int r
   {  // conv3 weight + bias gradient
     P3ConvWgrad<G3, 3> p;
     p.M = G3::K; p.N = G3::CO; p.K = rows * G3::OPIX;
-    p.k_chunk = chunk_for(p.K, kP3Conv3WgradSplits);
+    const int splits = wsplits("P3C3WS", kP3Conv3WgradSplits);
+    p.k_chunk = chunk_for(p.K, splits);
     p.a_src = src(a.x2, (int64_t)rows * kFlat); p.b_src = src(dz3, (int64_t)rows * kFlat);
     p.slab = slab;
-    if (tune_variant("P3C3W") == 1) P3G_GEMM("conv3_wgrad", 128, 64, 2, 2, 32, 3, p, kP3Conv3WgradSplits);
-    else P3_GEMM("conv3_wgrad", 128, 64, 2, 2, 32, p, kP3Conv3WgradSplits);
-    if ((rc = p3_wgrad_reduce(p, kP3Conv3WgradSplits, slab, g.w3, g.b3, "conv3_wgrad_reduce", st)))
+    if (tune_variant("P3C3W") == 1) P3G_GEMM("conv3_wgrad", 128, 64, 2, 2, 32, 3, p, splits);
+    else P3_GEMM("conv3_wgrad", 128, 64, 2, 2, 32, p, splits);
+    if ((rc = p3_wgrad_reduce(p, splits, slab, g.w3, g.b3, "conv3_wgrad_reduce", st)))
       return rc;
   }
   {
@@ -258,12 +266,13 @@ int backward_p3(const PWeights& w, const Grads& g, const uint16_t* frames, int r
   {  // conv2
     P3ConvWgrad<G2, 3> p;
     p.M = G2::K; p.N = G2::CO; p.K = rows * G2::OPIX;
-    p.k_chunk = chunk_for(p.K, kP3Conv2WgradSplits);
+    const int splits = wsplits("P3C2WS", kP3Conv2WgradSplits);
+    p.k_chunk = chunk_for(p.K, splits);
     p.a_src = src(a.x1, (int64_t)rows * kX1); p.b_src = src(dz2, (int64_t)rows * kFlat);
     p.slab = slab;
-    if (tune_variant("P3C2W") == 1) P3G_GEMM("conv2_wgrad", 128, 64, 2, 2, 32, 3, p, kP3Conv2WgradSplits);
-    else P3_GEMM("conv2_wgrad", 128, 64, 2, 2, 32, p, kP3Conv2WgradSplits);
-    if ((rc = p3_wgrad_reduce(p, kP3Conv2WgradSplits, slab, g.w2, g.b2, "conv2_wgrad_reduce", st)))
+    if (tune_variant("P3C2W") == 1) P3G_GEMM("conv2_wgrad", 128, 64, 2, 2, 32, 3, p, splits);
+    else P3_GEMM("conv2_wgrad", 128, 64, 2, 2, 32, p, splits);
+    if ((rc = p3_wgrad_reduce(p, splits, slab, g.w2, g.b2, "conv2_wgrad_reduce", st)))
       return rc;
   }
   {  // stride-2 input gradient, four sub-pixel classes in one launch
@@ -288,12 +297,13 @@ int backward_p3(const PWeights& w, const Grads& g, const uint16_t* frames, int r
   {  // conv1 (no input gradient)
     P3ConvWgrad<G1, 1> p;
     p.M = G1::K; p.N = G1::CO; p.K = rows * G1::OPIX;
-    p.k_chunk = chunk_for(p.K, kP3Conv1WgradSplits);
+    const int splits = wsplits("P3C1WS", kP3Conv1WgradSplits);
+    p.k_chunk = chunk_for(p.K, splits);
     p.a_src = frames_src(frames, rows); p.b_src = src(dz1, (int64_t)rows * kX1);
     p.slab = slab;
-    if (tune_variant("P3C1W") == 1) P3G_GEMM("conv1_wgrad", 256, 32, 4, 1, 32, 3, p, kP3Conv1WgradSplits);
-    else P3_GEMM("conv1_wgrad", 256, 32, 4, 1, 32, p, kP3Conv1WgradSplits);
-    return p3_wgrad_reduce(p, kP3Conv1WgradSplits, slab, g.w1, g.b1, "conv1_wgrad_reduce", st);
+    if (tune_variant("P3C1W") == 1) P3G_GEMM("conv1_wgrad", 256, 32, 4, 1, 32, 3, p, splits);
+    else P3_GEMM("conv1_wgrad", 256, 32, 4, 1, 32, p, splits);
+    return p3_wgrad_reduce(p, splits, slab, g.w1, g.b1, "conv1_wgrad_reduce", st);
   }
 }
 
