@@ -178,6 +178,7 @@ _SIGS = {
     "acme_profile_enable": (c_i32, [c_i32]),
     "acme_profile_reset": (c_i32, []),
     "acme_profile_num_sections": (c_i32, []),
+    "acme_profile_query_peak": (c_i32, [c_i32, ctypes.POINTER(c_f64)]),
     "acme_profile_query": (c_i32, [c_i32, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(c_f64),
                                    ctypes.POINTER(c_i64), ctypes.POINTER(c_f64),
                                    ctypes.POINTER(c_f64)]),

@@ -575,7 +575,7 @@ struct ConcatWgrad {
 // (intra-block split-K), so a 512 x 512 x 512 layer runs 1024 waves.
 #define D4_GEMM(name, prob)                                                                   \
   do {                                                                                        \
-    ACME_PROF(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0);   \
+    ACME_PROF_PEAK(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0, 157.3);       \
     hipError_t _e = launch_gemm<32, 32, 1, 1, 16, 4>(prob, 1, st);                             \
     if (_e != hipSuccess) {                                                                   \
       set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \

@@ -174,7 +174,8 @@ inline int chunk_for(int K, int splits) {
 // Profiled launch: `flops` = algorithmic FLOPs of the launch (2 * useful MACs).
 #define ACME_GEMM_F(name, flops, BM, BN, WM, WN, prob, splits) \
   do {                                                          \
-    ACME_PROF(name, st, (double)(flops), 0.0);                  \
+    ACME_PROF_PEAK(name, st, (double)(flops), 0.0,              \
+                   (gemm::matmul_peak_tflops<1, decltype(prob)>())); \
     ACME_GEMM(BM, BN, WM, WN, prob, splits);                    \
   } while (0)
 #define ACME_GEMM_N(name, BM, BN, WM, WN, prob, splits) \
@@ -187,7 +188,8 @@ int tune(const char* key) { return tune_variant(key); }
 #endif
 #define ACME_GEMM_NK(name, BM, BN, WM, WN, BKV, prob, splits)                                 \
   do {                                                                                         \
-    ACME_PROF(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0);   \
+    ACME_PROF_PEAK(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0, \
+                   (gemm::matmul_peak_tflops<1, decltype(prob)>()));                             \
     hipError_t _e = gemm::launch_matmul<BM, BN, WM, WN, BKV>(prob, splits, st);               \
     if (_e != hipSuccess) {                                                                    \
       set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
@@ -197,7 +199,8 @@ int tune(const char* key) { return tune_variant(key); }
 
 #define ACME_P3_GEMM(name, BM, BN, WM, WN, BKV, prob, splits)                                \
   do {                                                                                         \
-    ACME_PROF(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0);   \
+    ACME_PROF_PEAK(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0, \
+                   gemm::p3_peak_tflops<decltype(prob)>());                                    \
     hipError_t _e = gemm::launch_gemm_p3<BM, BN, WM, WN, BKV>(prob, splits, st);              \
     if (_e != hipSuccess) {                                                                    \
       set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
@@ -207,7 +210,8 @@ int tune(const char* key) { return tune_variant(key); }
 
 #define ACME_P3G_GEMM(name, BM, BN, WM, WN, BKV, ST, prob, splits)                            \
   do {                                                                                         \
-    ACME_PROF(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0);   \
+    ACME_PROF_PEAK(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0, \
+                   gemm::p3_peak_tflops<decltype(prob)>());                                    \
     hipError_t _e = gemm::launch_gemm_p3g<BM, BN, WM, WN, BKV, ST>(prob, splits, st);         \
     if (_e != hipSuccess) {                                                                    \
       set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \

@@ -499,8 +499,11 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in, int
       constexpr int set = decltype(S)::value;
       using Other = std::integral_constant<int, set ^ 1>;
       if constexpr (EARLY_STASH) {
-        if (kt + 1 < nk) stash(Other{}, set ^ 1);
-        if (kt + 2 < nk) fetch(S, kbeg + (kt + 2) * BK);
+        // Branch-free body (one basic block, so the scheduler can spread the LDS stores
+        // and loads among the MFMAs): past the end, fetch reads zeros (offsets beyond kend
+        // are kOOB) and stash fills a buffer that is never read.
+        stash(Other{}, set ^ 1);
+        fetch(S, kbeg + (kt + 2) * BK);
         compute(set);
       } else {
         if (kt + 2 < nk) fetch(S, kbeg + (kt + 2) * BK);
@@ -663,6 +666,13 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3g_kernel(const P p_in, in
 template <class P>
 inline int p3_n_major(const P& p) {
   return (int64_t)p.N * P::B_PLANES > (int64_t)p.M * P::A_PLANES ? 1 : 0;
+}
+
+// TFLOP/s ceiling of a plane GEMM in algorithmic (f32) FLOPs: bf16 dense MFMA peak over
+// the MFMA terms per product (6 for three-plane x three-plane, 3 with a one-plane operand).
+template <class P>
+constexpr double p3_peak_tflops() {
+  return 2500.0 / (P::A_PLANES * P::B_PLANES == 9 ? 6.0 : (P::A_PLANES * P::B_PLANES == 3 ? 3.0 : 1.0));
 }
 
 template <class Kern>

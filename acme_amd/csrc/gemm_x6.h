@@ -302,6 +302,17 @@ constexpr bool x6_eligible() {
   return P::A_MODE == KCONTIG && (P::B_MODE == KCONTIG || X6OptIn<P>::value);
 }
 
+// TFLOP/s ceiling of the engine launch_matmul picks for P (profiler roofline): the x6
+// engine runs six bf16 MFMA terms per f32 product (bf16 dense peak / 6), the f32 engine
+// v_mfma_f32_32x32x2_f32.
+template <int WK = 1, class P>
+inline double matmul_peak_tflops() {
+  if constexpr (WK == 1 && x6_eligible<P>()) {
+    if (use_x6()) return 2500.0 / 6.0;
+  }
+  return 157.3;
+}
+
 // The engine a learner launch uses: x6 for eligible problems unless ACME_MATMUL=f32 / the
 // C API chose f32.
 template <int BM, int BN, int WM, int WN, int BK = 16, int WK = 1, class P>

@@ -547,7 +547,8 @@ __global__ void __launch_bounds__(256) impala_loss_grad_kernel(const LossArgs a)
 
 #define IM_GEMM(name, BM, BN, WM, WN, WK, prob, splits)                                         \
   do {                                                                                         \
-    ACME_PROF(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0);    \
+    ACME_PROF_PEAK(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0,  \
+                   (gemm::matmul_peak_tflops<WK, decltype(prob)>()));                             \
     hipError_t _e = gemm::launch_matmul<BM, BN, WM, WN, 16, WK>(prob, splits, st);              \
     if (_e != hipSuccess) {                                                                    \
       set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__);  \

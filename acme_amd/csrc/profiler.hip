@@ -24,7 +24,7 @@ struct Rec {
 
 struct Section {
   std::string name;
-  double ms = 0, flops = 0, bytes = 0;
+  double ms = 0, flops = 0, bytes = 0, peak = 0;
   int64_t count = 0;
 };
 
@@ -68,7 +68,7 @@ void drain() {
 
 bool enabled() { return g_enabled; }
 
-int begin(const char* name, hipStream_t st, double flops, double bytes) {
+int begin(const char* name, hipStream_t st, double flops, double bytes, double peak) {
   std::lock_guard<std::mutex> lk(g_mu);
   auto it = g_index.find(name);
   int sec;
@@ -79,6 +79,7 @@ int begin(const char* name, hipStream_t st, double flops, double bytes) {
   } else {
     sec = it->second;
   }
+  if (peak > 0) g_sections[sec].peak = peak;
   if (g_open.size() > 100000 && g_open.back().closed) drain();  // bound the backlog
   Rec r{sec, get_event(), get_event(), flops, bytes, false};
   (void)hipEventRecord(r.a, st);
@@ -128,6 +129,13 @@ int acme_profile_query(int32_t i, const char** name, double* total_ms, int64_t* 
   if (count) *count = s.count;
   if (flops) *flops = s.flops;
   if (bytes) *bytes = s.bytes;
+  return ACME_OK;
+}
+
+int acme_profile_query_peak(int32_t i, double* peak_tflops) {
+  std::lock_guard<std::mutex> lk(acme::prof::g_mu);
+  ACME_CHECK_ARG(i >= 0 && i < (int32_t)acme::prof::g_sections.size(), "section out of range");
+  if (peak_tflops) *peak_tflops = acme::prof::g_sections[i].peak;
   return ACME_OK;
 }
 

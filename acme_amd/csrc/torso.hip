@@ -34,7 +34,7 @@ inline int chunk_for(int K, int splits) {
                WN, prob, splits)
 #define TORSO_GEMM_F(name, flops, BM, BN, WM, WN, prob, splits)                               \
   do {                                                                                        \
-    ACME_PROF(name, st, flops, 0.0);                                                          \
+    ACME_PROF_PEAK(name, st, flops, 0.0, (gemm::matmul_peak_tflops<1, decltype(prob)>()));      \
     hipError_t _e = gemm::launch_matmul<BM, BN, WM, WN, 16>(prob, splits, st);                 \
     if (_e != hipSuccess) {                                                                   \
       set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
@@ -145,7 +145,7 @@ int wsplits(const char* key, int def) {
 
 #define P3_GEMM_F(name, flops, BM, BN, WM, WN, BK, prob, splits)                             \
   do {                                                                                        \
-    ACME_PROF(name, st, flops, 0.0);                                                          \
+    ACME_PROF_PEAK(name, st, flops, 0.0, gemm::p3_peak_tflops<decltype(prob)>());             \
     hipError_t _e = gemm::launch_gemm_p3<BM, BN, WM, WN, BK>(prob, splits, st);               \
     if (_e != hipSuccess) {                                                                   \
       set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
@@ -154,7 +154,8 @@ int wsplits(const char* key, int def) {
   } while (0)
 #define P3G_GEMM(name, BM, BN, WM, WN, BK, ST, prob, splits)                                 \
   do {                                                                                        \
-    ACME_PROF(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0);  \
+    ACME_PROF_PEAK(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0, \
+                   gemm::p3_peak_tflops<decltype(prob)>());                                   \
     hipError_t _e = gemm::launch_gemm_p3g<BM, BN, WM, WN, BK, ST>(prob, splits, st);         \
     if (_e != hipSuccess) {                                                                   \
       set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
@@ -286,7 +287,7 @@ int backward_p3(const PWeights& w, const Grads& g, const uint16_t* frames, int r
       case 1: P3_GEMM_F("conv2_dgrad", fl, 256, 32, 4, 1, 32, p, G2::S * G2::S); break;
       case 2: P3_GEMM_F("conv2_dgrad", fl, 256, 32, 4, 1, 16, p, G2::S * G2::S); break;
       case 3: {
-        ACME_PROF("conv2_dgrad", st, fl, 0.0);
+        ACME_PROF_PEAK("conv2_dgrad", st, fl, 0.0, gemm::p3_peak_tflops<decltype(p)>());
         hipError_t e = gemm::launch_gemm_p3g<128, 32, 4, 1, 32, 3>(p, G2::S * G2::S, st);
         if (e != hipSuccess) return (set_error("gemm launch failed: %s", hipGetErrorString(e)), ACME_ERR_HIP);
         break;

@@ -412,9 +412,14 @@ def main():
         rec = dict(name=nm.value.decode(), launches=int(cnt.value), avg_us=round(1e3 * avg_ms, 2),
                    total_ms=round(ms.value, 3))
         if fl.value > 0:
+            # Peak of the arithmetic path the section ran on (f32 MFMA, or the exact
+            # bf16-plane engines at bf16 dense peak / MFMA terms per product).
+            pk = ctypes.c_double()
+            _lib.check(L.acme_profile_query_peak(i, ctypes.byref(pk)))
+            peak = pk.value if pk.value > 0 else FP32_MFMA_PEAK_TFLOPS
             tf = fl.value / cnt.value / (avg_ms * 1e-3) / 1e12
-            rec.update(bound="mfma", achieved=round(tf, 2), unit="TFLOP/s",
-                       frac=round(tf / FP32_MFMA_PEAK_TFLOPS, 4))
+            rec.update(bound="mfma", achieved=round(tf, 2), unit="TFLOP/s", peak=round(peak, 1),
+                       frac=round(tf / peak, 4))
         elif by.value > 0:
             gbs = by.value / cnt.value / (avg_ms * 1e-3) / 1e9
             rec.update(bound="hbm", achieved=round(gbs, 1), unit="GB/s",
@@ -434,13 +439,14 @@ def main():
         dom = mfma[0]
         traffic, src = pmc_traffic(args.workload, dom["name"])
         roofline = dict(bound="mfma", kernel=dom["name"], achieved=dom["achieved"],
-                        peak=FP32_MFMA_PEAK_TFLOPS, unit="TFLOP/s", frac=dom["frac"],
+                        peak=dom["peak"], unit="TFLOP/s", frac=dom["frac"],
                         traffic=traffic, traffic_unit="bytes/launch", traffic_source=src,
                         avg_us=dom["avg_us"])
     if rank == 0:
         for s in sections:
             print(f"[bench] {s['name']:16s} {s['launches']:6d} x {s['avg_us']:9.2f} us  "
-                  f"{s.get('achieved', '')} {s.get('unit', '')} frac={s.get('frac', '')}",
+                  f"{s.get('achieved', '')} {s.get('unit', '')} (peak {s.get('peak', '-')}) "
+                  f"frac={s.get('frac', '')}",
                   file=sys.stderr)
         print(f"[bench] replay fill {t_fill:.1f}s, final loss {loss:.5f}", file=sys.stderr)
     cpu = None

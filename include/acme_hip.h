@@ -369,6 +369,10 @@ int acme_profile_reset(void);
 int32_t acme_profile_num_sections(void);
 int acme_profile_query(int32_t i, const char** name, double* total_ms, int64_t* count,
                        double* flops, double* bytes);
+/* TFLOP/s ceiling of the arithmetic path section i runs on (f32 MFMA 157.3; the exact
+ * bf16-plane engines 2500 / MFMA terms per product: 416.7 for six terms, 833.3 for three);
+ * 0 for non-GEMM sections. */
+int acme_profile_query_peak(int32_t i, double* peak_tflops);
 
 /* snt.optimizers.Adam update over a flat f32 buffer (t = 1-based step). */
 int acme_adam_update(float* params, const float* grads, float* m, float* v, int64_t n,

@@ -45,6 +45,12 @@ SECTIONS_IMPALA = [
     (r"ConvDgrad<", "conv3_dgrad"),
 ]
 SECTIONS = [
+    (r"P3DenseFwd", "fc_fwd"),
+    (r"P3DenseWgrad", "fc_wgrad"),
+    (r"P3DenseDgrad", "fc_dgrad"),
+    (r"fc_head_forward_kernel", "fc_head_fwd"),
+    (r"frames_bf16_kernel", "frames_bf16"),
+    (r"head_dz_planes_kernel", "head_dz"),
     (r"gemm_\w+_kernel<128, 128, 2, 2,.*DenseFwd<true", "fc_fwd"),
     (r"ConvFwd<acme::conv::Geom<84,", "conv1_fwd"),
     (r"ConvFwd<acme::conv::Geom<21,", "conv2_fwd"),
