@@ -253,13 +253,19 @@ struct P3Core {
   static constexpr int NCS = kColSum ? NTL : 1;
   static constexpr int EPI_BYTES = HasStore8<P>::value ? WM * WN * 32 * (TN + 4) * 4 : 0;
 
+  struct NoHook {
+    __device__ void operator()(int) const {}
+  };
+  // hook(g) runs after MFMA group g = i * NTL + j of step S0 (the interleaving point for
+  // the next stage's LDS stores).
+  template <int S0 = 0, int S1 = BK / 16, class Hook = NoHook>
   __device__ static __forceinline__ void mma(const uint8_t* sa, const uint8_t* sb, int wm, int wn,
                                              int lane, f32x16 (&acc)[MT][NTL], f32x16 (&cs)[NCS],
-                                             bool do_colsum) {
+                                             bool do_colsum, const Hook& hook = Hook()) {
     const bf16x8 ones{(__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f,
                       (__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f};
 #pragma unroll
-    for (int s = 0; s < BK / 16; ++s) {
+    for (int s = S0; s < S1; ++s) {
       bf16x8 fa[MT][NPA], fb[NTL][NPB];
 #pragma unroll
       for (int i = 0; i < MT; ++i)
@@ -299,6 +305,7 @@ struct P3Core {
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], acc[i][j], 0, 0, 0);
           }
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], acc[i][j], 0, 0, 0);
+          if (s == S0) hook(i * NTL + j);
         }
       if constexpr (kColSum) {
         if (do_colsum) {
@@ -371,6 +378,12 @@ struct P3Core {
   }
 };
 
+#ifndef P3_SPLIT
+#define P3_SPLIT 1  // 1: LDS stores between the two k16 steps of a BK-32 stage (measured +7% fc_fwd)
+#endif
+#ifndef P3_SCHED
+#define P3_SCHED 0
+#endif
 #ifndef P3_EARLY_STASH
 #define P3_EARLY_STASH 1
 #endif
@@ -463,6 +476,26 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in, int
     }
   };
 
+  // One LDS store of the stash (k < WR: A units first, then B), for interleaving.
+  constexpr int WR = PA::PER_THREAD * NPA + PB::PER_THREAD * NPB;
+  auto stash_one = [&](auto S, int buf, int k) {
+    constexpr int set = decltype(S)::value;
+    uint8_t* sa = smem + buf * STAGE;
+    uint8_t* sb = sa + PA::BYTES;
+    if (k < PA::PER_THREAD * NPA) {
+      const int i = k / NPA, pl = k % NPA;
+      const int u = tid + i * NT;
+      if (PA::owns(u))
+        *reinterpret_cast<u32x4*>(sa + pl * PA::PLANE + PA::offset(u)) = ra[set][i][pl];
+    } else {
+      const int kb = k - PA::PER_THREAD * NPA;
+      const int i = kb / NPB, pl = kb % NPB;
+      const int u = tid + i * NT;
+      if (PB::owns(u))
+        *reinterpret_cast<u32x4*>(sb + pl * PB::PLANE + PB::offset(u)) = rb[set][i][pl];
+    }
+  };
+
   f32x16 acc[C::MT][C::NTL];
   f32x16 cs[C::NCS];
 #pragma unroll
@@ -502,9 +535,52 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in, int
         // Branch-free body (one basic block, so the scheduler can spread the LDS stores
         // and loads among the MFMAs): past the end, fetch reads zeros (offsets beyond kend
         // are kOOB) and stash fills a buffer that is never read.
-        stash(Other{}, set ^ 1);
-        fetch(S, kbeg + (kt + 2) * BK);
-        compute(set);
+        if constexpr (P3_SPLIT && BK == 32) {
+          // First k16 step's MFMAs, then the LDS stores of stage kt + 1 and the loads of
+          // stage kt + 2, then the second step: the stores overlap MFMAs already queued.
+          const uint8_t* sa = smem + set * STAGE;
+          if constexpr (P3_SPLIT == 2) {
+            // Stores interleaved among the first step's MFMA groups (source order).
+            constexpr int G = C::MT * C::NTL;
+            auto hook = [&](int g) {
+#pragma unroll
+              for (int k = g * WR / G; k < (g + 1) * WR / G; ++k) stash_one(Other{}, set ^ 1, k);
+            };
+            C::template mma<0, 1>(sa, sa + PA::BYTES, wm, wn, lane, acc, cs, do_colsum, hook);
+          } else {
+            C::template mma<0, 1>(sa, sa + PA::BYTES, wm, wn, lane, acc, cs, do_colsum);
+            stash(Other{}, set ^ 1);
+          }
+          fetch(S, kbeg + (kt + 2) * BK);
+          C::template mma<1, 2>(sa, sa + PA::BYTES, wm, wn, lane, acc, cs, do_colsum);
+        } else {
+          stash(Other{}, set ^ 1);
+          fetch(S, kbeg + (kt + 2) * BK);
+          compute(set);
+        }
+        if constexpr (P3_SCHED) {
+          // Issue order for the scheduler: the first k16 step's fragment reads, then each
+          // MFMA followed by at most one LDS store, one global load and (for the next k16
+          // step) fragment reads, so the stores and loads ride in the MFMAs' issue gaps
+          // instead of delaying the first MFMA.
+          constexpr int RD = C::MT * NPA * (P::A_MODE == KCONTIG ? 1 : 2) +
+                             C::NTL * NPB * (P::B_MODE == KCONTIG ? 1 : 2);
+          constexpr int TERMS = NPA * NPB == 9 ? 6 : (NPA * NPB == 3 ? 3 : 1);
+          constexpr int MF = C::MT * C::NTL * TERMS;
+          constexpr int WR = PA::PER_THREAD * NPA + PB::PER_THREAD * NPB;
+          constexpr int STEPS = BK / 16;
+          __builtin_amdgcn_sched_group_barrier(0x100, RD, 0);
+#pragma unroll
+          for (int st = 0; st < STEPS; ++st) {
+#pragma unroll
+            for (int m = 0; m < MF; ++m) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+              if (st == 0 && m < WR) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+              if (st == 0 && m < WR) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+              if (st + 1 < STEPS && m >= MF - RD) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
+          }
+        }
       } else {
         if (kt + 2 < nk) fetch(S, kbeg + (kt + 2) * BK);
         compute(set);

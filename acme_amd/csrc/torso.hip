@@ -204,6 +204,8 @@ int forward_p3(const PWeights& w, const uint16_t* frames, int rows, const PActs&
       case 2: P3_GEMM("conv1_fwd", 256, 32, 4, 1, 32, p, 1); break;
       case 3: P3G_GEMM("conv1_fwd", 256, 32, 4, 1, 16, 3, p, 1); break;
       case 4: P3G_GEMM("conv1_fwd", 256, 32, 4, 1, 32, 3, p, 1); break;
+      case 5: P3_GEMM("conv1_fwd", 512, 32, 4, 1, 16, p, 1); break;
+      case 6: P3_GEMM("conv1_fwd", 512, 32, 4, 1, 32, p, 1); break;
       default: P3_GEMM("conv1_fwd", 256, 32, 4, 1, 16, p, 1); break;
     }
   }
@@ -286,6 +288,8 @@ int backward_p3(const PWeights& w, const Grads& g, const uint16_t* frames, int r
     switch (tune_variant("P3C2D")) {
       case 1: P3_GEMM_F("conv2_dgrad", fl, 256, 32, 4, 1, 32, p, G2::S * G2::S); break;
       case 2: P3_GEMM_F("conv2_dgrad", fl, 256, 32, 4, 1, 16, p, G2::S * G2::S); break;
+      case 4: P3_GEMM_F("conv2_dgrad", fl, 512, 32, 4, 1, 16, p, G2::S * G2::S); break;
+      case 5: P3_GEMM_F("conv2_dgrad", fl, 256, 32, 2, 1, 32, p, G2::S * G2::S); break;
       case 3: {
         ACME_PROF_PEAK("conv2_dgrad", st, fl, 0.0, gemm::p3_peak_tflops<decltype(p)>());
         hipError_t e = gemm::launch_gemm_p3g<128, 32, 4, 1, 32, 3>(p, G2::S * G2::S, st);
@@ -302,8 +306,11 @@ int backward_p3(const PWeights& w, const Grads& g, const uint16_t* frames, int r
     p.k_chunk = chunk_for(p.K, splits);
     p.a_src = frames_src(frames, rows); p.b_src = src(dz1, (int64_t)rows * kX1);
     p.slab = slab;
-    if (tune_variant("P3C1W") == 1) P3G_GEMM("conv1_wgrad", 256, 32, 4, 1, 32, 3, p, splits);
-    else P3_GEMM("conv1_wgrad", 256, 32, 4, 1, 32, p, splits);
+    switch (tune_variant("P3C1W")) {
+      case 1: P3G_GEMM("conv1_wgrad", 256, 32, 4, 1, 32, 3, p, splits); break;
+      case 2: P3_GEMM("conv1_wgrad", 256, 32, 2, 1, 32, p, splits); break;
+      default: P3_GEMM("conv1_wgrad", 256, 32, 4, 1, 32, p, splits); break;
+    }
     return p3_wgrad_reduce(p, splits, slab, g.w1, g.b1, "conv1_wgrad_reduce", st);
   }
 }
