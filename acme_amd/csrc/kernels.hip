@@ -257,15 +257,20 @@ __global__ void __launch_bounds__(256) slab_reduce4_kernel(const float* __restri
 // partial dot products and a fixed shuffle tree (deterministic).
 constexpr int kHeadRows = 4;
 constexpr int kHeadChunk = 8;  // advantage outputs per accumulation pass
+#ifndef HEAD_EXP
+#define HEAD_EXP 0  // experiments: 1 skip the dot products, 2 skip the slab sum
+#endif
 template <int SPL, int HC>
 __global__ void __launch_bounds__(256) fc_head_forward_kernel(
     const float* __restrict__ slab, int splits, int rows, int H_, const float* __restrict__ fcb,
     const float* __restrict__ wv, const float* __restrict__ bv, const float* __restrict__ wa,
     const float* __restrict__ ba, int A, float* __restrict__ hid, float* __restrict__ q) {
   const int H = HC > 0 ? HC : H_;  // compile-time hidden width when HC > 0
-  extern __shared__ float sh[];  // [kHeadRows][2H] hid | [H][A] wa | [kHeadRows][A + 1] dots
+  // [kHeadRows][2H] hid | [H][A] wa | [H] wv | [kHeadRows][A + 1] dots | 4 x [8][64] partials
+  extern __shared__ float sh[];
   float* swa = sh + kHeadRows * 2 * H;
-  float* dots = swa + H * A;
+  float* swv = swa + H * A;
+  float* dots = swv + H;
   const int r0 = blockIdx.x * kHeadRows;
   const int n4 = 2 * H / 4;
   const int64_t count4 = (int64_t)rows * n4;
@@ -278,6 +283,7 @@ __global__ void __launch_bounds__(256) fc_head_forward_kernel(
   } else {
     for (int t = threadIdx.x; t < H * A; t += 256) swa[t] = wa[t];
   }
+  for (int t = threadIdx.x; t < H; t += 256) swv[t] = wv[t];
 #pragma unroll
   for (int t = threadIdx.x; t < kHeadRows * n4; t += 256) {
     const int rr = t / n4, c4 = t - rr * n4;
@@ -285,7 +291,9 @@ __global__ void __launch_bounds__(256) fc_head_forward_kernel(
     if (row >= rows) continue;
     const int64_t e = (int64_t)row * n4 + c4;
     f32x4 v;
-    if constexpr (SPL > 0) {
+    if constexpr (HEAD_EXP == 2) {
+      v = s4[e];
+    } else if constexpr (SPL > 0) {
       f32x4 part[SPL];
 #pragma unroll
       for (int sp = 0; sp < SPL; ++sp) part[sp] = s4[(size_t)sp * count4 + e];
@@ -307,33 +315,53 @@ __global__ void __launch_bounds__(256) fc_head_forward_kernel(
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  auto wave_sum = [](float x) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
-    return x;
-  };
+  // Outputs o = 0..A (o < A: advantage o, o == A: value), kHeadChunk at a time: each lane
+  // accumulates its strided k-slice, the 64 partials go through a per-wave LDS row, and
+  // lane jj sums output jj's row in a fixed order (no cross-lane shuffle chains).
+  float* red = dots + kHeadRows * (A + 1) + wave * kHeadChunk * 64;
+  float* zero = dots + kHeadRows * (A + 1) + 4 * kHeadChunk * 64;  // one zero word
+  if (threadIdx.x == 0) zero[0] = 0.f;
+  __syncthreads();
   for (int rr = wave; rr < kHeadRows; rr += 4) {
+    if constexpr (HEAD_EXP == 1) break;
     const float* h = sh + rr * 2 * H;
-    float av = 0.f;
-    for (int k = lane; k < H; k += 64) av = fmaf(h[k], wv[k], av);
-    av = wave_sum(av);
-    if (lane == 0) dots[rr * (A + 1) + A] = av + bv[0];
-    for (int j0 = 0; j0 < A; j0 += kHeadChunk) {
+    for (int o0 = 0; o0 <= A; o0 += kHeadChunk) {
+      // Per-output weight column (uniform): advantage o -> wa[:, o] (stride A) over
+      // hid[H:]; value -> wv (stride 1) over hid[:H]; past the end -> a zero word.
+      const float* wp[kHeadChunk];
+      int ws[kHeadChunk], hoff[kHeadChunk];
+#pragma unroll
+      for (int jj = 0; jj < kHeadChunk; ++jj) {
+        const int o = o0 + jj;
+        wp[jj] = o < A ? swa + o : (o == A ? swv : zero);
+        ws[jj] = o < A ? A : (o == A ? 1 : 0);
+        hoff[jj] = o < A ? H : 0;
+      }
       float acc[kHeadChunk];
 #pragma unroll
       for (int jj = 0; jj < kHeadChunk; ++jj) acc[jj] = 0.f;
+#pragma unroll 8
       for (int k = lane; k < H; k += 64) {
-        const float x = h[H + k];
-        const float* w = swa + k * A + j0;
 #pragma unroll
         for (int jj = 0; jj < kHeadChunk; ++jj)
-          if (j0 + jj < A) acc[jj] = fmaf(x, w[jj], acc[jj]);
+          acc[jj] = fmaf(h[hoff[jj] + k], wp[jj][k * ws[jj]], acc[jj]);
       }
 #pragma unroll
-      for (int jj = 0; jj < kHeadChunk; ++jj) {
-        const float d = wave_sum(acc[jj]);
-        if (lane == 0 && j0 + jj < A) dots[rr * (A + 1) + j0 + jj] = d + ba[j0 + jj];
+      for (int jj = 0; jj < kHeadChunk; ++jj) red[jj * 64 + lane] = acc[jj];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (lane < kHeadChunk && o0 + lane <= A) {
+        const f32x4* r4 = reinterpret_cast<const f32x4*>(red + lane * 64);
+        f32x4 t = r4[0];
+#pragma unroll
+        for (int q = 1; q < 16; ++q) t += r4[q];
+        const int o = o0 + lane;
+        dots[rr * (A + 1) + o] = ((t[0] + t[1]) + (t[2] + t[3])) + (o == A ? bv[0] : ba[o]);
       }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   }
   __syncthreads();
@@ -623,7 +651,9 @@ int launch_fc_head_forward(const float* slab, int splits, int rows, int H, const
                            const float* wv, const float* bv, const float* wa, const float* ba,
                            int A, float* hid, float* q, hipStream_t st) {
   ACME_CHECK_ARG(H % 2 == 0 && A >= 1 && splits >= 1 && rows >= 1, "bad head shape");
-  const size_t shmem = sizeof(float) * (kHeadRows * 2 * H + (size_t)H * A + kHeadRows * (A + 1));
+  const size_t shmem =
+      sizeof(float) * (kHeadRows * 2 * H + (size_t)H * A + H + kHeadRows * (A + 1) +
+                       4 * kHeadChunk * 64 + 4);
   ACME_CHECK_ARG(shmem <= 65536, "head too large for the fused head kernel");
   const unsigned grid = (unsigned)ceil_div(rows, kHeadRows);
   const bool wa16 = reinterpret_cast<uintptr_t>(wa) % 16 == 0;
