@@ -90,6 +90,12 @@ struct acme_dqn {
   bool last_p3 = false;      // the last forward/backward ran the plane path
   uint16_t *wpl = nullptr, *tpl = nullptr;
   uint16_t* frames = nullptr;  // bf16 copies of [o_tm1; o_t] (2B frames)
+  // Second stream of the plane path: the target forward runs beside the online forward,
+  // and weight gradients beside input gradients (fork / join by events on the caller's
+  // stream; side_slab is its split-K scratch).
+  hipStream_t side = nullptr;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  float* side_slab = nullptr;
   torso::Plane x1p{}, x2p{}, x3p{}, t1p{}, t2p{}, t3p{}, dzhp{}, dz3p{}, dz2p{}, dz1p{};
 };
 
@@ -156,6 +162,9 @@ int convert_frames(acme_dqn* l, const void* obs_a, const void* obs_b, int split,
 }
 inline Planes PP(const torso::Plane& x) { return Planes{x.p, x.stride}; }
 bool use_p3(const acme_dqn* l) { return l->p3_capable && gemm::use_x6(); }
+// The side stream is used unless the section profiler is on: profiled passes run every
+// kernel alone on one stream, so their per-kernel durations are uncontended.
+hipStream_t side_stream(const acme_dqn* l) { return prof::enabled() ? nullptr : l->side; }
 
 // Split-K helper: chunk size (multiple of BK) for `splits` splits of K.
 inline int chunk_for(int K, int splits) {
@@ -208,6 +217,16 @@ int tune(const char* key) { return tune_variant(key); }
     }                                                                                          \
   } while (0)
 
+#define ACME_P3P_GEMM(name, BM, BN, WM, WN, prob, splits)                                    \
+  do {                                                                                        \
+    ACME_PROF_PEAK(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0, \
+                   gemm::p3_peak_tflops<decltype(prob)>());                                   \
+    hipError_t _e = gemm::launch_gemm_p3p<BM, BN, WM, WN>(prob, splits, st);                  \
+    if (_e != hipSuccess) {                                                                   \
+      set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
+      return ACME_ERR_HIP;                                                                    \
+    }                                                                                         \
+  } while (0)
 #define ACME_P3G_GEMM(name, BM, BN, WM, WN, BKV, ST, prob, splits)                            \
   do {                                                                                         \
     ACME_PROF_PEAK(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0, \
@@ -292,7 +311,9 @@ int nature_forward(acme_dqn* l, const float* prm, const void* obs_a, const void*
 // planes (gemm_p3.h); `wpl` are the planes of `prm`.
 int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const uint16_t* frames,
                       int rows, const torso::Plane& x1, const torso::Plane& x2,
-                      const torso::Plane& x3, float* hid, float* q, hipStream_t st) {
+                      const torso::Plane& x3, float* hid, float* q, hipStream_t st,
+                      float* slab = nullptr) {
+  if (!slab) slab = l->slab;
   torso::PWeights w{WP(l, wpl, l->t_c1w), WP(l, wpl, l->t_c2w), WP(l, wpl, l->t_c3w),
                     P(l, prm, l->t_c1b), P(l, prm, l->t_c2b), P(l, prm, l->t_c3b)};
   int rc = torso::forward_p3(w, frames, rows, torso::PActs{x1, x2, x3}, st);
@@ -307,7 +328,7 @@ int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const uint16
     if (sv <= 0 && fv == 7) splits = rows > 512 ? 16 : 32;  // 256x256 tiles
     p.M = rows; p.N = 2 * kHidden; p.K = kFlat; p.k_chunk = chunk_for(kFlat, splits);
     p.a_src = SRC(x3, (int64_t)rows * kFlat); p.ldx = kFlat;
-    p.b_src = SRC(WP(l, wpl, l->t_fcw), (int64_t)kFlat * 2 * kHidden); p.slab = l->slab;
+    p.b_src = SRC(WP(l, wpl, l->t_fcw), (int64_t)kFlat * 2 * kHidden); p.slab = slab;
     switch (fv) {
       case 1: ACME_P3_GEMM("fc_fwd", 128, 128, 2, 2, 16, p, splits); break;
       case 2: ACME_P3_GEMM("fc_fwd", 256, 128, 4, 2, 16, p, splits); break;
@@ -316,10 +337,11 @@ int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const uint16
       case 5: ACME_P3G_GEMM("fc_fwd", 128, 128, 2, 2, 16, 4, p, splits); break;
       case 6: ACME_P3_GEMM("fc_fwd", 256, 128, 4, 2, 16, p, splits); break;
       case 7: ACME_P3_GEMM("fc_fwd", 256, 256, 4, 2, 16, p, splits); break;
+      case 8: ACME_P3P_GEMM("fc_fwd", 128, 128, 2, 2, p, splits); break;
       default: ACME_P3_GEMM("fc_fwd", 128, 128, 2, 2, 32, p, splits); break;
     }
     ACME_PROF("fc_head_fwd", st, 0.0, 4.0 * (double)rows * 2 * kHidden * (splits + 1));
-    return launch_fc_head_forward(l->slab, splits, rows, kHidden, P(l, prm, l->t_fcb),
+    return launch_fc_head_forward(slab, splits, rows, kHidden, P(l, prm, l->t_fcb),
                                   P(l, prm, l->t_vw), P(l, prm, l->t_vb), P(l, prm, l->t_aw),
                                   P(l, prm, l->t_ab), l->cfg.num_actions, hid, q, st);
   }
@@ -367,7 +389,8 @@ int mlp_forward(acme_dqn* l, const float* prm, const void* obs_a, const void* ob
   return ACME_OK;
 }
 
-int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st) {
+int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st_main) {
+  hipStream_t st = st_main;
   const float* prm = l->params;
   float* gr = l->grads;
   const int A = l->cfg.num_actions;
@@ -381,13 +404,21 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st) {
                                   P(l, prm, l->t_aw), l->dzh, st);
     if (rc != ACME_OK) return rc;
   }
+  // Weight gradients (head, then FC) on the side stream beside the FC input gradient.
+  const bool fork = p3 && side_stream(l);
+  float* hslab = fork ? l->side_slab : l->slab;
+  if (fork) {
+    ACME_HIP_TRY(hipEventRecord(l->ev[2], st_main));
+    ACME_HIP_TRY(hipStreamWaitEvent(l->side, l->ev[2], 0));
+    st = l->side;
+  }
   {  // Head weight / bias gradients: one skinny GEMM over the batch + scatter.
     DuelHeadWgrad p;
     p.M = 2 * kHidden; p.N = A + 1; p.K = B; p.k_chunk = chunk_for(B, kHeadBwdSplits);
-    p.A = A; p.h = l->hid; p.g = l->g; p.act = l->a_cache; p.slab = l->slab;
+    p.A = A; p.h = l->hid; p.g = l->g; p.act = l->a_cache; p.slab = hslab;
     ACME_GEMM_N("head_wgrad", 64, 32, 2, 1, p, kHeadBwdSplits);
     ACME_PROF("head_wgrad_scatter", st, 0.0, 0.0);
-    rc = launch_duel_head_grad_scatter(l->slab, kHeadBwdSplits, kHidden, A, Pm(l, gr, l->t_vw),
+    rc = launch_duel_head_grad_scatter(hslab, kHeadBwdSplits, kHidden, A, Pm(l, gr, l->t_vw),
                                        Pm(l, gr, l->t_vb), Pm(l, gr, l->t_aw), Pm(l, gr, l->t_ab),
                                        st);
     if (rc != ACME_OK) return rc;
@@ -403,8 +434,13 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st) {
         case 1: ACME_P3_GEMM("fc_wgrad", 128, 128, 2, 2, 32, p, 1); break;
         case 3: ACME_P3G_GEMM("fc_wgrad", 128, 128, 2, 2, 16, 3, p, 1); break;
         case 4: ACME_P3G_GEMM("fc_wgrad", 128, 128, 2, 2, 32, 3, p, 1); break;
+        case 8: ACME_P3P_GEMM("fc_wgrad", 128, 128, 2, 2, p, 1); break;
         default: ACME_P3_GEMM("fc_wgrad", 128, 128, 2, 2, 16, p, 1); break;
       }
+    }
+    if (fork) {
+      ACME_HIP_TRY(hipEventRecord(l->ev[3], l->side));
+      st = st_main;
     }
     {  // FC input grad -> dZ3 planes (masked by conv3's ReLU).
       P3DenseDgrad p;
@@ -417,9 +453,12 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st) {
         case 2: ACME_P3_GEMM("fc_dgrad", 64, 128, 2, 2, 16, p, 1); break;
         case 3: ACME_P3G_GEMM("fc_dgrad", 128, 128, 2, 2, 16, 3, p, 1); break;
         case 4: ACME_P3_GEMM("fc_dgrad", 128, 128, 2, 2, 32, p, 1); break;
+        case 8: ACME_P3P_GEMM("fc_dgrad", 128, 128, 2, 2, p, 1); break;
+        case 9: ACME_P3P_GEMM("fc_dgrad", 64, 128, 2, 2, p, 1); break;
         default: ACME_P3G_GEMM("fc_dgrad", 128, 128, 2, 2, 32, 3, p, 1); break;
       }
     }
+    if (fork) ACME_HIP_TRY(hipStreamWaitEvent(st_main, l->ev[3], 0));  // join
     return ACME_OK;
   }
   {  // FC weight + bias grad: [7744, 1024] = x3^T dZh (reduction over the batch).
@@ -576,6 +615,14 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
           (rc = plane_alloc(l, &l->dz1p, (int64_t)B * torso::kX1)))
         return fail(rc);
       l->slab_floats = std::max(l->slab_floats, torso::wgrad_slab_floats_p3());
+      if (tune("SIDE") != 1) {  // ACME_V_SIDE=1: single stream
+        hipError_t e = hipStreamCreateWithFlags(&l->side, hipStreamNonBlocking);
+        for (auto& ev : l->ev)
+          if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (e != hipSuccess)
+          return fail((set_error("side stream: %s", hipGetErrorString(e)), ACME_ERR_HIP));
+        if ((rc = dev_alloc(l, &l->side_slab, l->slab_floats))) return fail(rc);
+      }
     }
   } else {
     ACME_CHECK_ARG(cfg->obs_dim >= 1, "obs_dim must be >= 1");
@@ -623,6 +670,9 @@ int acme_dqn_destroy(acme_dqn* l) {
   if (!l) return ACME_OK;
   (void)hipDeviceSynchronize();
   for (void* p : l->allocs) (void)hipFree(p);
+  for (auto& e : l->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (l->side) (void)hipStreamDestroy(l->side);
   delete l;
   return ACME_OK;
 }
@@ -759,9 +809,15 @@ int acme_dqn_forward_backward_stage(acme_dqn* l, const acme_transition_batch* ba
       torso::PWeights w{WP(l, l->wpl, l->t_c1w), WP(l, l->wpl, l->t_c2w),
                         WP(l, l->wpl, l->t_c3w), P(l, l->params, l->t_c1b),
                         P(l, l->params, l->t_c2b), P(l, l->params, l->t_c3b)};
+      torso::Side sd;
+      if (side_stream(l)) {
+        sd.side = l->side;
+        sd.slab = l->side_slab;
+        for (int i = 0; i < 3; ++i) sd.e[i] = l->ev[i];
+      }
       return torso::backward_p3(w, g, l->frames, B,
                                 torso::PActs{l->x1p, l->x2p, l->x3p}, l->dz3p, l->dz2p, l->dz1p,
-                                l->slab, st);
+                                l->slab, st, sd);
     }
     torso::Grads g{Pm(l, l->grads, l->t_c1w), Pm(l, l->grads, l->t_c1b), Pm(l, l->grads, l->t_c2w),
                    Pm(l, l->grads, l->t_c2b), Pm(l, l->grads, l->t_c3w), Pm(l, l->grads, l->t_c3b)};
@@ -777,12 +833,23 @@ int acme_dqn_forward_backward_stage(acme_dqn* l, const acme_transition_batch* ba
   if (l->last_p3) {
     if ((rc = sync_planes(l, st)) != ACME_OK) return rc;
     if ((rc = convert_frames(l, batch->o_tm1, batch->o_t, B, 2 * B, st)) != ACME_OK) return rc;
+    // Target forward (q_t_value) on the side stream, beside the online forward.
+    hipStream_t tst = st;
+    hipStream_t side = side_stream(l);
+    if (side) {
+      ACME_HIP_TRY(hipEventRecord(l->ev[0], st));
+      ACME_HIP_TRY(hipStreamWaitEvent(side, l->ev[0], 0));
+      tst = side;
+    }
+    if ((rc = nature_forward_p3(l, l->target, l->tpl, l->frames + (size_t)B * kObsBytes, B,
+                                l->t1p, l->t2p, l->t3p, l->thid, l->q_tg, tst,
+                                side ? l->side_slab : l->slab)) != ACME_OK)
+      return rc;
+    if (side) ACME_HIP_TRY(hipEventRecord(l->ev[1], side));
     if ((rc = nature_forward_p3(l, l->params, l->wpl, l->frames, 2 * B, l->x1p, l->x2p, l->x3p,
                                 l->hid, l->q_on, st)) != ACME_OK)
       return rc;
-    if ((rc = nature_forward_p3(l, l->target, l->tpl, l->frames + (size_t)B * kObsBytes, B,
-                                l->t1p, l->t2p, l->t3p, l->thid, l->q_tg, st)) != ACME_OK)
-      return rc;
+    if (side) ACME_HIP_TRY(hipStreamWaitEvent(st, l->ev[1], 0));
   } else if (nature) {
     if ((rc = nature_forward(l, l->params, batch->o_tm1, batch->o_t, B, 2 * B, l->x1, l->x2, l->x3,
                              l->hid, l->q_on, st)) != ACME_OK)

@@ -247,6 +247,74 @@ __global__ void prio_reset_kernel(const int64_t* __restrict__ slots,
   winner[slots[j]] = -1;
 }
 
+// update_priorities in ONE launch.  Updates are partitioned over the workgroups by their
+// ancestor at level h = nlevels - 2 (owner = slot >> 6h, workgroup owner % gridDim.x), so
+// every update of a slot, and every touched node of levels 1..h, belongs to exactly one
+// workgroup: it elects the last valid update per slot in LDS (largest j wins, Reverb's
+// in-order application), writes raw priority and leaf p^alpha, and rescans its nodes of
+// levels 1..h with barriers between levels.  The top level (children written by many
+// workgroups) is rescanned by a second one-workgroup launch: a device-wide "last
+// workgroup" hand-off needs agent-scope fences, which on the multi-XCD part write back and
+// invalidate L2 and measured slower than the launch they replace.
+constexpr int kFusedUpdateMax = 4096;
+constexpr int kFusedUpdateBlocks = 256;
+struct FusedUpdateArgs {
+  const uint64_t* upd_keys;
+  const double* prios;
+  int n;
+  int64_t capacity;
+  const uint64_t* keys;
+  double alpha;
+  double* raw_prio;
+  double* level[8];
+  int nlevels;
+};
+__global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs a) {
+  __shared__ int s_j[kFusedUpdateMax];
+  __shared__ int64_t s_slot[kFusedUpdateMax];
+  __shared__ int s_len;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int h = a.nlevels >= 2 ? a.nlevels - 2 : 0;
+  if (tid == 0) s_len = 0;
+  __syncthreads();
+  for (int j = tid; j < a.n; j += nt) {  // this workgroup's updates (valid keys only)
+    const uint64_t k = a.upd_keys[j];
+    const int64_t slot = (int64_t)(k % (uint64_t)a.capacity);
+    if ((int)((slot >> (6 * h)) % G) != bid) continue;
+    if (a.keys[slot] != k) continue;  // evicted since it was sampled: ignored
+    const int e = atomicAdd(&s_len, 1);
+    s_j[e] = j;
+    s_slot[e] = slot;
+  }
+  __syncthreads();
+  const int len = s_len;
+  for (int e = tid; e < len; e += nt) {  // last update of each slot wins
+    const int64_t slot = s_slot[e];
+    const int j = s_j[e];
+    bool win = true;
+    for (int f = 0; f < len; ++f)
+      if (s_slot[f] == slot && s_j[f] > j) win = false;
+    if (win) {
+      const double p = a.prios[j];
+      a.raw_prio[slot] = p;
+      a.level[0][slot] = det_pow_priority(p, a.alpha);
+    }
+  }
+  __syncthreads();
+  for (int l = 1; l <= h; ++l) {  // this workgroup's ancestors, one wave per node
+    for (int e = wave; e < len; e += nw) {
+      const int64_t node = s_slot[e] >> (6 * l);
+      const double s = wave_scan64(a.level[l - 1][node * 64 + lane]);
+      if (lane == 63) a.level[l][node] = s;
+    }
+    __syncthreads();
+  }
+}
+
+
+
 __global__ void fill_i32_kernel(int32_t* p, int64_t n, int32_t v) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = v;
@@ -620,6 +688,22 @@ int acme_replay_update_priorities(acme_replay* r, const uint64_t* keys, const do
   const double alpha =
       r->cfg.sampler == ACME_SAMPLER_PRIORITIZED ? r->cfg.priority_exponent : 0.0;
   ACME_PROF("replay_update", st, 0.0, (double)n * (16.0 + 8.0 * 3 + 512.0 * (r->nlevels - 1)));
+  if (n <= kFusedUpdateMax && tune_variant("UPD") != 1) {
+    FusedUpdateArgs a;
+    a.upd_keys = keys; a.prios = prios; a.n = (int)n; a.capacity = r->cfg.capacity;
+    a.keys = r->keys; a.alpha = alpha; a.raw_prio = r->raw_prio; a.nlevels = r->nlevels;
+    for (int l = 0; l < 8; ++l) a.level[l] = r->levels[l];
+    prio_update_fused_kernel<<<kFusedUpdateBlocks, 256, 0, st>>>(a);
+    ACME_LAUNCH_CHECK();
+    if (r->nlevels >= 2) {  // the top level, over all its entries that have children
+      const int top = r->nlevels - 1;
+      const int64_t nodes = r->level_size[top - 1] / 64;
+      level_update_kernel<<<(unsigned)ceil_div(nodes, 4), 256, 0, st>>>(
+          r->levels[top - 1], r->levels[top], 0, nodes, nullptr, nullptr, 0);
+      ACME_LAUNCH_CHECK();
+    }
+    return ACME_OK;
+  }
   prio_resolve_kernel<<<g, 256, 0, st>>>(keys, n, r->keys, r->cfg.capacity, t_slots, t_valid,
                                          r->winner);
   ACME_LAUNCH_CHECK();

@@ -62,10 +62,18 @@ int64_t wgrad_slab_floats_p3();
 // frames: bf16 copies of the uint8 frames [rows][84*84*4] (launch_frames_bf16).
 int forward_p3(const PWeights& w, const uint16_t* frames, int rows, const PActs& a,
                hipStream_t st);
+// Optional second stream for the weight gradients: conv3 / conv2 weight gradients run on
+// `side` (with their own split-K slab) beside the input gradients on the main stream;
+// events e[0..2] are scratch (hipEventDisableTiming).  side == nullptr: one stream.
+struct Side {
+  hipStream_t side = nullptr;
+  float* slab = nullptr;
+  hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+};
 // dz3: conv3's dZ planes [rows][kFlat] (masked); dz2 / dz1 plane scratch.
 int backward_p3(const PWeights& w, const Grads& g, const uint16_t* frames, int rows,
                 const PActs& a, const Plane& dz3, const Plane& dz2, const Plane& dz1, float* slab,
-                hipStream_t st);
+                hipStream_t st, const Side& side = Side());
 
 }  // namespace torso
 }  // namespace acme

@@ -10,6 +10,7 @@
 #include "conv_p3.h"
 #include "gemm.h"
 #include "gemm_p3.h"
+#include "gemm_p3d.h"
 #include "gemm_x6.h"
 #include "kernels.h"
 #include "profiler.h"
@@ -162,6 +163,30 @@ int wsplits(const char* key, int def) {
       return ACME_ERR_HIP;                                                                    \
     }                                                                                         \
   } while (0)
+#define P3D_GEMM_F(name, flops, BN, MT, NW, BK, prob, z)                                     \
+  do {                                                                                        \
+    ACME_PROF_PEAK(name, st, flops, 0.0, gemm::p3_peak_tflops<decltype(prob)>());             \
+    hipError_t _e = gemm::launch_gemm_p3d<BN, MT, NW, BK>(prob, z, st);                       \
+    if (_e != hipSuccess) {                                                                   \
+      set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
+      return ACME_ERR_HIP;                                                                    \
+    }                                                                                         \
+  } while (0)
+#define P3D_GEMM(name, BN, MT, NW, BK, prob)                                                 \
+  P3D_GEMM_F(name, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, BN, MT, NW, \
+             BK, prob, 1)
+#define P3P_GEMM_F(name, flops, BM, BN, WM, WN, prob, splits)                                \
+  do {                                                                                        \
+    ACME_PROF_PEAK(name, st, flops, 0.0, gemm::p3_peak_tflops<decltype(prob)>());             \
+    hipError_t _e = gemm::launch_gemm_p3p<BM, BN, WM, WN>(prob, splits, st);                  \
+    if (_e != hipSuccess) {                                                                   \
+      set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
+      return ACME_ERR_HIP;                                                                    \
+    }                                                                                         \
+  } while (0)
+#define P3P_GEMM(name, BM, BN, WM, WN, prob, splits)                                         \
+  P3P_GEMM_F(name, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, BM, BN, WM, \
+             WN, prob, splits)
 #define P3_GEMM(name, BM, BN, WM, WN, BK, prob, splits)                                      \
   P3_GEMM_F(name, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, BM, BN, WM, \
             WN, BK, prob, splits)
@@ -206,7 +231,13 @@ int forward_p3(const PWeights& w, const uint16_t* frames, int rows, const PActs&
       case 4: P3G_GEMM("conv1_fwd", 256, 32, 4, 1, 32, 3, p, 1); break;
       case 5: P3_GEMM("conv1_fwd", 512, 32, 4, 1, 16, p, 1); break;
       case 6: P3_GEMM("conv1_fwd", 512, 32, 4, 1, 32, p, 1); break;
-      default: P3_GEMM("conv1_fwd", 256, 32, 4, 1, 16, p, 1); break;
+      case 7: P3D_GEMM("conv1_fwd", 32, 2, 4, 32, p); break;
+      case 8: P3D_GEMM("conv1_fwd", 32, 4, 4, 32, p); break;
+      case 9: P3D_GEMM("conv1_fwd", 32, 1, 4, 32, p); break;
+      case 10: P3P_GEMM("conv1_fwd", 256, 32, 4, 1, p, 1); break;
+      case 11: P3P_GEMM("conv1_fwd", 128, 32, 4, 1, p, 1); break;
+      case 12: P3_GEMM("conv1_fwd", 256, 32, 4, 1, 16, p, 1); break;
+      default: P3D_GEMM("conv1_fwd", 32, 2, 4, 32, p); break;  // direct A (gemm_p3d.h)
     }
   }
   {
@@ -219,6 +250,13 @@ int forward_p3(const PWeights& w, const uint16_t* frames, int rows, const PActs&
       case 2: P3_GEMM("conv2_fwd", 256, 64, 4, 1, 32, p, 1); break;
       case 3: P3G_GEMM("conv2_fwd", 128, 64, 2, 2, 32, 3, p, 1); break;
       case 4: P3G_GEMM("conv2_fwd", 128, 64, 2, 2, 16, 4, p, 1); break;
+      case 5: P3D_GEMM("conv2_fwd", 64, 2, 4, 32, p); break;
+      case 6: P3D_GEMM("conv2_fwd", 64, 1, 4, 32, p); break;
+      case 7: P3D_GEMM("conv2_fwd", 64, 4, 4, 32, p); break;
+      case 8: P3D_GEMM("conv2_fwd", 64, 2, 2, 32, p); break;
+      case 9: P3P_GEMM("conv2_fwd", 128, 64, 2, 2, p, 1); break;
+      case 10: P3P_GEMM("conv2_fwd", 256, 64, 4, 1, p, 1); break;
+      case 11: P3P_GEMM("conv2_fwd", 128, 64, 4, 1, p, 1); break;
       default: P3_GEMM("conv2_fwd", 128, 64, 2, 2, 32, p, 1); break;
     }
   }
@@ -232,6 +270,13 @@ int forward_p3(const PWeights& w, const uint16_t* frames, int rows, const PActs&
       case 2: P3_GEMM("conv3_fwd", 256, 64, 4, 1, 32, p, 1); break;
       case 3: P3G_GEMM("conv3_fwd", 128, 64, 2, 2, 32, 3, p, 1); break;
       case 4: P3G_GEMM("conv3_fwd", 128, 64, 2, 2, 16, 4, p, 1); break;
+      case 5: P3D_GEMM("conv3_fwd", 64, 2, 4, 32, p); break;
+      case 6: P3D_GEMM("conv3_fwd", 64, 1, 4, 32, p); break;
+      case 7: P3D_GEMM("conv3_fwd", 64, 4, 4, 32, p); break;
+      case 8: P3D_GEMM("conv3_fwd", 64, 2, 2, 32, p); break;
+      case 9: P3P_GEMM("conv3_fwd", 128, 64, 2, 2, p, 1); break;
+      case 10: P3P_GEMM("conv3_fwd", 256, 64, 4, 1, p, 1); break;
+      case 11: P3P_GEMM("conv3_fwd", 128, 64, 4, 1, p, 1); break;
       default: P3_GEMM("conv3_fwd", 128, 64, 2, 2, 32, p, 1); break;
     }
   }
@@ -240,20 +285,31 @@ int forward_p3(const PWeights& w, const uint16_t* frames, int rows, const PActs&
 
 int backward_p3(const PWeights& w, const Grads& g, const uint16_t* frames, int rows,
                 const PActs& a, const Plane& dz3, const Plane& dz2, const Plane& dz1, float* slab,
-                hipStream_t st) {
+                hipStream_t st_main, const Side& sd) {
   int rc;
+  // Weight gradients of conv3 and conv2 go to the side stream (when given): each only
+  // waits for its layer's dZ, and runs beside the next input gradient on the main stream.
+  const bool fork = sd.side != nullptr;
+  hipStream_t st = fork ? sd.side : st_main;
+  float* wslab = fork ? sd.slab : slab;
+  if (fork) {
+    ACME_HIP_TRY(hipEventRecord(sd.e[0], st_main));
+    ACME_HIP_TRY(hipStreamWaitEvent(sd.side, sd.e[0], 0));
+  }
   {  // conv3 weight + bias gradient
     P3ConvWgrad<G3, 3> p;
     p.M = G3::K; p.N = G3::CO; p.K = rows * G3::OPIX;
     const int splits = wsplits("P3C3WS", kP3Conv3WgradSplits);
     p.k_chunk = chunk_for(p.K, splits);
     p.a_src = src(a.x2, (int64_t)rows * kFlat); p.b_src = src(dz3, (int64_t)rows * kFlat);
-    p.slab = slab;
-    if (tune_variant("P3C3W") == 1) P3G_GEMM("conv3_wgrad", 128, 64, 2, 2, 32, 3, p, splits);
+    p.slab = wslab;
+    if (tune_variant("P3C3W") == 9) P3P_GEMM("conv3_wgrad", 128, 64, 2, 2, p, splits);
+    else if (tune_variant("P3C3W") == 1) P3G_GEMM("conv3_wgrad", 128, 64, 2, 2, 32, 3, p, splits);
     else P3_GEMM("conv3_wgrad", 128, 64, 2, 2, 32, p, splits);
-    if ((rc = p3_wgrad_reduce(p, splits, slab, g.w3, g.b3, "conv3_wgrad_reduce", st)))
+    if ((rc = p3_wgrad_reduce(p, splits, wslab, g.w3, g.b3, "conv3_wgrad_reduce", st)))
       return rc;
   }
+  st = st_main;
   {
     P3ConvDgrad<G3> p;
     p.M = rows * G3::IPIX; p.N = G3::CI; p.K = G3::KH * G3::KW * G3::CO; p.k_chunk = p.K;
@@ -263,8 +319,17 @@ int backward_p3(const PWeights& w, const Grads& g, const uint16_t* frames, int r
       case 1: P3_GEMM("conv3_dgrad", 128, 64, 2, 2, 16, p, 1); break;
       case 2: P3_GEMM("conv3_dgrad", 256, 64, 4, 1, 32, p, 1); break;
       case 3: P3G_GEMM("conv3_dgrad", 128, 64, 2, 2, 32, 3, p, 1); break;
+      case 4: P3D_GEMM("conv3_dgrad", 64, 2, 4, 32, p); break;
+      case 5: P3D_GEMM("conv3_dgrad", 64, 1, 4, 32, p); break;
+      case 9: P3P_GEMM("conv3_dgrad", 128, 64, 2, 2, p, 1); break;
+      case 10: P3P_GEMM("conv3_dgrad", 256, 64, 4, 1, p, 1); break;
       default: P3_GEMM("conv3_dgrad", 128, 64, 2, 2, 32, p, 1); break;
     }
+  }
+  if (fork) {
+    ACME_HIP_TRY(hipEventRecord(sd.e[1], st_main));
+    ACME_HIP_TRY(hipStreamWaitEvent(sd.side, sd.e[1], 0));
+    st = sd.side;
   }
   {  // conv2
     P3ConvWgrad<G2, 3> p;
@@ -272,12 +337,15 @@ int backward_p3(const PWeights& w, const Grads& g, const uint16_t* frames, int r
     const int splits = wsplits("P3C2WS", kP3Conv2WgradSplits);
     p.k_chunk = chunk_for(p.K, splits);
     p.a_src = src(a.x1, (int64_t)rows * kX1); p.b_src = src(dz2, (int64_t)rows * kFlat);
-    p.slab = slab;
-    if (tune_variant("P3C2W") == 1) P3G_GEMM("conv2_wgrad", 128, 64, 2, 2, 32, 3, p, splits);
+    p.slab = wslab;
+    if (tune_variant("P3C2W") == 9) P3P_GEMM("conv2_wgrad", 128, 64, 2, 2, p, splits);
+    else if (tune_variant("P3C2W") == 1) P3G_GEMM("conv2_wgrad", 128, 64, 2, 2, 32, 3, p, splits);
     else P3_GEMM("conv2_wgrad", 128, 64, 2, 2, 32, p, splits);
-    if ((rc = p3_wgrad_reduce(p, splits, slab, g.w2, g.b2, "conv2_wgrad_reduce", st)))
+    if ((rc = p3_wgrad_reduce(p, splits, wslab, g.w2, g.b2, "conv2_wgrad_reduce", st)))
       return rc;
+    if (fork) ACME_HIP_TRY(hipEventRecord(sd.e[2], sd.side));
   }
+  st = st_main;
   {  // stride-2 input gradient, four sub-pixel classes in one launch
     P3ConvDgradSubZ<G2> p;
     p.M = P3ConvDgradSubZ<G2>::max_rows(rows); p.N = G2::CI; p.K = P3ConvDgradSubZ<G2>::KR;
@@ -290,6 +358,11 @@ int backward_p3(const PWeights& w, const Grads& g, const uint16_t* frames, int r
       case 2: P3_GEMM_F("conv2_dgrad", fl, 256, 32, 4, 1, 16, p, G2::S * G2::S); break;
       case 4: P3_GEMM_F("conv2_dgrad", fl, 512, 32, 4, 1, 16, p, G2::S * G2::S); break;
       case 5: P3_GEMM_F("conv2_dgrad", fl, 256, 32, 2, 1, 32, p, G2::S * G2::S); break;
+      case 6: P3D_GEMM_F("conv2_dgrad", fl, 32, 2, 4, 32, p, G2::S * G2::S); break;
+      case 7: P3D_GEMM_F("conv2_dgrad", fl, 32, 4, 4, 32, p, G2::S * G2::S); break;
+      case 8: P3D_GEMM_F("conv2_dgrad", fl, 32, 1, 4, 32, p, G2::S * G2::S); break;
+      case 9: P3P_GEMM_F("conv2_dgrad", fl, 128, 32, 4, 1, p, G2::S * G2::S); break;
+      case 10: P3P_GEMM_F("conv2_dgrad", fl, 256, 32, 4, 1, p, G2::S * G2::S); break;
       case 3: {
         ACME_PROF_PEAK("conv2_dgrad", st, fl, 0.0, gemm::p3_peak_tflops<decltype(p)>());
         hipError_t e = gemm::launch_gemm_p3g<128, 32, 4, 1, 32, 3>(p, G2::S * G2::S, st);
@@ -309,10 +382,14 @@ int backward_p3(const PWeights& w, const Grads& g, const uint16_t* frames, int r
     switch (tune_variant("P3C1W")) {
       case 1: P3G_GEMM("conv1_wgrad", 256, 32, 4, 1, 32, 3, p, splits); break;
       case 2: P3_GEMM("conv1_wgrad", 256, 32, 2, 1, 32, p, splits); break;
+      case 9: P3P_GEMM("conv1_wgrad", 256, 32, 4, 1, p, splits); break;
       default: P3_GEMM("conv1_wgrad", 256, 32, 4, 1, 32, p, splits); break;
     }
-    return p3_wgrad_reduce(p, splits, slab, g.w1, g.b1, "conv1_wgrad_reduce", st);
+    if ((rc = p3_wgrad_reduce(p, splits, slab, g.w1, g.b1, "conv1_wgrad_reduce", st)))
+      return rc;
   }
+  if (fork) ACME_HIP_TRY(hipStreamWaitEvent(st_main, sd.e[2], 0));  // join
+  return ACME_OK;
 }
 
 }  // namespace torso
