@@ -389,7 +389,11 @@ int mlp_forward(acme_dqn* l, const float* prm, const void* obs_a, const void* ob
   return ACME_OK;
 }
 
-int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st_main) {
+// join_dense: the caller's stream waits for the side stream's dense weight gradients
+// before returning (stage 0 of a data-parallel step all-reduces them next); otherwise the
+// torso backward's final join covers them.
+int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st_main,
+                    bool join_dense) {
   hipStream_t st = st_main;
   const float* prm = l->params;
   float* gr = l->grads;
@@ -458,7 +462,7 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st_main) 
         default: ACME_P3G_GEMM("fc_dgrad", 128, 128, 2, 2, 32, 3, p, 1); break;
       }
     }
-    if (fork) ACME_HIP_TRY(hipStreamWaitEvent(st_main, l->ev[3], 0));  // join
+    if (fork && join_dense) ACME_HIP_TRY(hipStreamWaitEvent(st_main, l->ev[3], 0));
     return ACME_OK;
   }
   {  // FC weight + bias grad: [7744, 1024] = x3^T dZh (reduction over the batch).
@@ -786,8 +790,18 @@ int acme_dqn_q_values(acme_dqn* l, const void* obs, int64_t batch, int32_t use_t
   return mlp_forward(l, prm, obs, obs, B, B, l->mlp_tact, q_out, st);
 }
 
+static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batch,
+                                  const acme_dqn_outputs* out, int32_t stage, void* stream,
+                                  bool join_dense);
+
 int acme_dqn_forward_backward_stage(acme_dqn* l, const acme_transition_batch* batch,
                                     const acme_dqn_outputs* out, int32_t stage, void* stream) {
+  return forward_backward_stage(l, batch, out, stage, stream, true);
+}
+
+static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batch,
+                                  const acme_dqn_outputs* out, int32_t stage, void* stream,
+                                  bool join_dense) {
   ACME_CHECK_ARG(l && batch && l->params, "null argument or unbound learner");
   ACME_CHECK_ARG(stage == 0 || stage == 1, "stage must be 0 or 1");
   ACME_CHECK_ARG(batch->o_tm1 && batch->a_tm1 && batch->r_t && batch->d_t && batch->o_t &&
@@ -894,14 +908,15 @@ int acme_dqn_forward_backward_stage(acme_dqn* l, const acme_transition_batch* ba
   if (out && out->q_tm1)
     ACME_HIP_TRY(hipMemcpyAsync(out->q_tm1, l->q_on, (size_t)B * A * sizeof(float),
                                 hipMemcpyDeviceToDevice, st));
-  return nature ? nature_backward(l, batch->o_tm1, B, st) : mlp_backward(l, batch->o_tm1, B, st);
+  return nature ? nature_backward(l, batch->o_tm1, B, st, join_dense)
+                : mlp_backward(l, batch->o_tm1, B, st);
 }
 
 int acme_dqn_forward_backward(acme_dqn* l, const acme_transition_batch* batch,
                               const acme_dqn_outputs* out, void* stream) {
-  int rc = acme_dqn_forward_backward_stage(l, batch, out, 0, stream);
+  int rc = forward_backward_stage(l, batch, out, 0, stream, false);
   if (rc != ACME_OK) return rc;
-  return acme_dqn_forward_backward_stage(l, batch, out, 1, stream);
+  return forward_backward_stage(l, batch, out, 1, stream, false);
 }
 
 int acme_dqn_grad_split(const acme_dqn* l, int64_t* split) {

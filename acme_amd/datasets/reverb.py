@@ -4,8 +4,15 @@ The reference streams every sample through gRPC, decompresses it on a tf.data th
 batches on the host and copies the batch to the device.  Here a batch is drawn and
 gathered on the GPU: one sampling kernel (prioritized 64-ary sum tree or uniform) and
 one row-gather per field into device buffers, so `next(iterator)` returns a
-ReplaySample whose data are device tensors.  Buffers are double-buffered: a sample stays
-valid until the iterator is advanced twice.
+ReplaySample whose data are device tensors.  A sample stays valid until the iterator is
+advanced twice.
+
+`prefetch_size` keeps the reference's tf.data prefetch (datasets/reverb.py:136-137; the
+DQN agent asks for 4, agents/tf/dqn/agent.py:50): with P > 0 the sample and gather of batch
+k + P are issued on the dataset's own stream when batch k is handed out, ordered after
+every kernel already queued on the caller's stream (so they see the priority updates of
+steps < k, like Reverb's prefetched samples), and the caller's stream waits only for the
+batch it receives.  The draw order, and so every sampled index, is deterministic.
 
 `server_address` may be the in-process address ('localhost:<port>'), a Server, a Table
 or a Client.  Sampling is deterministic given the table seed: draw i uses Philox
@@ -39,32 +46,42 @@ def _server_of(address) -> replay.Server:
 class ReplayDataset:
     """Iterable over batched ReplaySamples of one table."""
 
-    def __init__(self, table, batch_size: int, timeout: float = 60.0):
+    def __init__(self, table, batch_size: int, timeout: float = 60.0, prefetch: int = 0):
         if batch_size is None or batch_size < 1:
             raise ValueError("the GPU replay dataset needs a batch_size >= 1")
+        if prefetch < 0:
+            raise ValueError("prefetch_size must be >= 0")
         self.table = table
         self.batch_size = int(batch_size)
         self.timeout = timeout
+        self.prefetch = int(prefetch)
 
     def __iter__(self):
         if isinstance(self.table, replay.QueueTable):
             return _QueueIterator(self.table, self.batch_size, self.timeout)
-        return _TableIterator(self.table, self.batch_size, self.timeout)
+        return _TableIterator(self.table, self.batch_size, self.timeout, self.prefetch)
 
 
 class _TableIterator:
-    def __init__(self, table: replay.Table, batch: int, timeout: float):
+    def __init__(self, table: replay.Table, batch: int, timeout: float, prefetch: int = 0):
         self._t = table
         self._B = batch
         self._timeout = timeout
+        self._P = prefetch
         self._slots = None
+        self._queue = []  # (slot index, ready event) of batches issued ahead
 
     def _alloc(self):
         import ctypes
         native = self._t.native
         dev = native.device
         self._slots = []
-        for _ in range(2):
+        if self._P > 0:
+            self._stream = torch.cuda.Stream(device=dev)
+            self._issued = torch.cuda.Event()
+            self._ready = [torch.cuda.Event() for _ in range(self._P + 2)]
+            self._next_slot = 0
+        for _ in range(self._P + 2 if self._P > 0 else 2):
             info = native.alloc_sample_info(self._B)
             bufs = [torch.empty(self._B, f.row_bytes, dtype=torch.uint8, device=dev)
                     for f in self._t.fields]
@@ -100,13 +117,34 @@ class _TableIterator:
         t.flush()
         if self._slots is None:
             self._alloc()
-        raw, ptrs, sample = self._slots[self._which]
-        self._which ^= 1
-        L, h, st = lib(), t.native.handle, stream_ptr()
-        check(L.acme_replay_sample(h, self._B, t.next_draw() & 0xFFFFFFFFFFFFFFFF, *raw, st),
-              "replay sample")
-        check(L.acme_replay_gather(h, raw[0], self._B, ptrs, st), "replay gather")
-        return sample
+        L, h = lib(), t.native.handle
+        if self._P == 0:
+            raw, ptrs, sample = self._slots[self._which]
+            self._which ^= 1
+            st = stream_ptr()
+            check(L.acme_replay_sample(h, self._B, t.next_draw() & 0xFFFFFFFFFFFFFFFF, *raw, st),
+                  "replay sample")
+            check(L.acme_replay_gather(h, raw[0], self._B, ptrs, st), "replay gather")
+            return sample
+        # Prefetch: order the dataset stream after everything queued so far on the caller's
+        # stream (inserts, earlier learner steps and their priority updates), top the queue
+        # up to P + 1 batches, hand out the oldest.
+        main = torch.cuda.current_stream(self._t.native.device)
+        self._issued.record(main)
+        self._stream.wait_event(self._issued)
+        st = stream_ptr(self._stream)
+        while len(self._queue) < self._P + 1:
+            i = self._next_slot
+            self._next_slot = (i + 1) % (self._P + 2)
+            raw, ptrs, _ = self._slots[i]
+            check(L.acme_replay_sample(h, self._B, t.next_draw() & 0xFFFFFFFFFFFFFFFF, *raw, st),
+                  "replay sample")
+            check(L.acme_replay_gather(h, raw[0], self._B, ptrs, st), "replay gather")
+            self._ready[i].record(self._stream)
+            self._queue.append(i)
+        i = self._queue.pop(0)
+        main.wait_event(self._ready[i])
+        return self._slots[i][2]
 
 
 class _QueueIterator:
@@ -137,10 +175,11 @@ def make_reverb_dataset(server_address, environment_spec=None, batch_size: Optio
                         parallel_batch_optimization: bool = True,
                         convert_zero_size_to_none: bool = False,
                         using_deprecated_adder: bool = False) -> ReplayDataset:
-    """Same arguments as the reference.  prefetch/parallel knobs of the tf.data pipeline
-    have no equivalent (sampling is a synchronous device kernel); the environment/extra
-    specs are only checked for consistency with the table's layout."""
-    del prefetch_size, parallel_batch_optimization, convert_zero_size_to_none
+    """Same arguments as the reference.  `prefetch_size` issues that many batches ahead on
+    the dataset's stream (module docstring); the parallel-batch knob of the tf.data pipeline
+    has no equivalent; the environment/extra specs are only checked for consistency with
+    the table's layout."""
+    del parallel_batch_optimization, convert_zero_size_to_none
     del using_deprecated_adder, sequence_length
     server = _server_of(server_address)
     if table not in server.tables:
@@ -150,7 +189,7 @@ def make_reverb_dataset(server_address, environment_spec=None, batch_size: Optio
         sig = adders.NStepTransitionAdder.signature(environment_spec, extra_spec or ())
         if t.fields is not None and len(tree.flatten(sig)) != len(t.fields):
             raise ValueError("environment_spec does not match the table's item layout")
-    return ReplayDataset(t, batch_size)
+    return ReplayDataset(t, batch_size, prefetch=prefetch_size or 0)
 
 
 make_dataset = make_reverb_dataset

@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--batch", type=int, default=0, help="default 512 (dqn) / 256 (d4pg)")
     p.add_argument("--replay-size", type=int, default=1_000_000)
     p.add_argument("--num-actions", type=int, default=18)
+    p.add_argument("--prefetch", type=int, default=4,
+                   help="dataset prefetch_size (DQN; the reference DQN agent's default is 4)")
     p.add_argument("--no-profile", action="store_true", help="skip the profiled pass")
     p.add_argument("--profile-steps", type=int, default=50,
                    help="steps of the separate, untimed section-profiler pass")
@@ -189,7 +191,9 @@ def setup_dqn(args, world, rank, dev):
     assert [f.row_bytes for f in table.fields] == [OBS_BYTES, 4, 4, 4, OBS_BYTES]
     table.native.fill_synthetic(shard, layout=0, num_actions=A, seed=rank)
     server = replay.Server([table])
-    dataset = make_reverb_dataset(server, batch_size=B)
+    # prefetch_size as the reference DQN agent (agents/tf/dqn/agent.py:50): batch k+4 is
+    # sampled and gathered on the dataset's stream while step k runs.
+    dataset = make_reverb_dataset(server, batch_size=B, prefetch_size=args.prefetch)
     net = DQNAtariNetwork(A)
     learner = DQNLearner(net, net, discount=0.99, importance_sampling_exponent=0.2,
                          learning_rate=1e-3, target_update_period=100, dataset=dataset,
@@ -203,7 +207,8 @@ def setup_dqn(args, world, rank, dev):
                 "global_batch": B * world, "batch_per_gpu": B,
                 "replay_slots": args.replay_size, "replay_slots_per_gpu": shard,
                 "obs": "uint8[84,84,4]", "num_actions": A,
-                "sampler": "prioritized(alpha=0.6), IS beta=0.2", "parallelism": f"dp{world}"})
+                "sampler": "prioritized(alpha=0.6), IS beta=0.2", "prefetch_size": args.prefetch,
+                "parallelism": f"dp{world}"})
     return (learner.step, B, meta, lambda: float(learner.native.loss.item()),
             lambda: cpu_baseline(B, A, args.cpu_baseline_seconds))
 

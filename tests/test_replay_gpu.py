@@ -145,3 +145,66 @@ def test_synthetic_fill_atari_layout():
     f = np.float32(0.99)
     assert set(np.unique(d)).issubset({0.0, ((f * f) * f) * f})
     assert (s["probabilities"].cpu().numpy() == 1.0 / 2048).all()
+
+
+@pytest.mark.parametrize("n_upd", [512, 4096, 5000])
+def test_priority_updates_deep_tree(n_upd):
+    """Four-level tree (the 1M-slot shape): the one-launch update (n <= 4096) and the
+    multi-launch path (n > 4096) both match the oracle bit for bit."""
+    rng = np.random.default_rng(n_upd)
+    cap = 300_000
+    r = _native(cap, [4], True)
+    o = OracleTable(cap, True, 0.6, 1234)
+    pr = rng.uniform(0.1, 2.0, cap + 1000)
+    r.insert([np.zeros((cap + 1000, 1), np.int32)], pr)
+    o.insert(pr)
+    for it in range(3):
+        keys = rng.integers(1000, cap + 1000, n_upd).astype(np.uint64)
+        keys[:16] = keys[16]          # duplicates: the last one wins
+        keys[17] = 3                  # evicted key: ignored
+        newp = rng.uniform(0.0, 3.0, n_upd)
+        r.update_priorities(torch.as_tensor(keys.view(np.int64)).cuda().view(torch.uint64),
+                            torch.as_tensor(newp).cuda())
+        o.update(keys, newp)
+        np.testing.assert_array_equal(r.debug_state()["leaves"], o.leaves()[:cap])
+        _cmp_sample(r, o, 512, 200 + it)
+
+
+@pytest.mark.parametrize("prefetch", [0, 1, 4])
+def test_prefetched_dataset_draw_order(prefetch):
+    """make_reverb_dataset(prefetch_size=P): batch k is drawn (Philox counter k) after the
+    priority updates of steps < k - P and before the later ones, as Reverb's prefetched
+    samples; replayed exactly by the oracle in that order."""
+    from acme_amd import replay, specs
+    from acme_amd.adders import reverb as adders
+    from acme_amd.datasets import make_reverb_dataset
+    cap, B = 5000, 64
+    env_spec = specs.EnvironmentSpec(
+        observations=specs.Array((24,), np.float32),
+        actions=specs.BoundedArray((6,), np.float32, -1.0, 1.0),
+        rewards=specs.Array((), np.float32), discounts=specs.BoundedArray((), np.float32, 0, 1))
+    table = replay.Table(adders.DEFAULT_PRIORITY_TABLE, replay.selectors.Prioritized(0.6),
+                         replay.selectors.Fifo(), cap, replay.rate_limiters.MinSize(1),
+                         signature=adders.NStepTransitionAdder.signature(env_spec), seed=1234,
+                         device=torch.device("cuda"))
+    table.native.fill_synthetic(cap, layout=1, num_actions=1, seed=0)
+    server = replay.Server([table])
+    client = replay.Client(server)
+    it = iter(make_reverb_dataset(server, batch_size=B, prefetch_size=prefetch))
+    o = OracleTable(cap, True, 0.6, 1234)
+    o.insert(np.ones(cap))
+    rng = np.random.default_rng(prefetch)
+    issued, expect = 0, {}
+    for k in range(8):
+        s = next(it)
+        while issued <= k + prefetch:
+            expect[issued] = o.sample(B, issued)
+            issued += 1
+        keys = s.info.key.cpu().numpy().view(np.uint64)
+        np.testing.assert_array_equal(keys, expect[k]["keys"])
+        np.testing.assert_array_equal(s.info.probability.cpu().numpy(),
+                                      expect[k]["probabilities"])
+        newp = rng.uniform(0.0, 3.0, B)
+        client.update_priorities(adders.DEFAULT_PRIORITY_TABLE, s.info.key,
+                                 torch.as_tensor(newp).cuda())
+        o.update(keys, newp)
