@@ -179,3 +179,29 @@ def test_full_step_trajectory_matches_oracle():
             np.testing.assert_allclose(got[k], state["params"][k], rtol=1e-5, atol=1e-3 + 1e-6)
             frac = np.mean(np.abs(got[k] - state["params"][k]) <= 1e-5 * np.abs(state["params"][k]) + 1e-6)
             assert frac > 0.98, (k, frac)
+
+
+def test_fused_step_equals_staged_step_bitwise():
+    """acme_dqn_step (dense Adam on the side stream beside the torso backward, one join)
+    and forward_backward + apply (single ordering) give bit-identical parameters, Adam
+    moments, target and planes over steps that include a target copy."""
+    from acme_amd.networks import DQNAtariNetwork
+    net = DQNAtariNetwork(18)
+    B = 32
+    p0, t0 = net.init(1), net.init(2)
+    a = _learner(net, B, target_update_period=2)
+    b = _learner(net, B, target_update_period=2)
+    a.set_params(p0, t0)
+    b.set_params(p0, t0)
+    rng = np.random.default_rng(11)
+    for _ in range(3):
+        dev = _dev(_batch(rng, B, (84, 84, 4), 18))
+        a.step(*dev)
+        b.forward_backward(*dev)
+        b.apply()
+        torch.cuda.synchronize()
+        for buf in ("params", "target", "m", "v"):
+            ga, gb = a.get_params(buf), b.get_params(buf)
+            for k in ga:
+                np.testing.assert_array_equal(ga[k], gb[k], err_msg=f"{buf}/{k}")
+        assert a.loss.item() == b.loss.item()
