@@ -104,6 +104,7 @@ class SequenceBatch(ctypes.Structure):
 
 _SIGS = {
     "acme_last_error": (ctypes.c_char_p, []),
+    "acme_tune_set": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32]),
     "acme_version": (ctypes.c_char_p, []),
     "acme_target_arch": (ctypes.c_char_p, []),
     "acme_set_matmul_engine": (c_i32, [c_i32]),

@@ -22,6 +22,7 @@ void set_error(const char* fmt, ...);
 // Tile / schedule variant for tuning runs: ACME_V_<KEY>=<n> in the environment (read once
 // per key); 0 is the shipped default.
 int tune_variant(const char* key);
+void tune_set(const char* key, int value);
 
 #define ACME_HIP_TRY(expr)                                                   \
   do {                                                                       \

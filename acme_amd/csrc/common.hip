@@ -18,16 +18,29 @@ void set_error(const char* fmt, ...) {
   va_end(ap);
 }
 
+namespace {
+std::mutex g_tune_mu;
+std::vector<std::pair<std::string, int>> g_tune;  // key -> value (env, or acme_tune_set)
+}  // namespace
+
 int tune_variant(const char* key) {
-  static std::mutex mu;
-  static std::vector<std::pair<std::string, int>> cache;
-  std::lock_guard<std::mutex> lock(mu);
-  for (auto& kv : cache)
+  std::lock_guard<std::mutex> lock(g_tune_mu);
+  for (auto& kv : g_tune)
     if (kv.first == key) return kv.second;
   const char* v = getenv((std::string("ACME_V_") + key).c_str());
   const int x = v ? atoi(v) : 0;
-  cache.emplace_back(key, x);
+  g_tune.emplace_back(key, x);
   return x;
+}
+
+void tune_set(const char* key, int value) {
+  std::lock_guard<std::mutex> lock(g_tune_mu);
+  for (auto& kv : g_tune)
+    if (kv.first == key) {
+      kv.second = value;
+      return;
+    }
+  g_tune.emplace_back(key, value);
 }
 
 namespace gemm {
@@ -59,6 +72,12 @@ int acme_set_matmul_engine(int32_t engine) {
 int32_t acme_matmul_engine(void) { return acme::gemm::use_x6() ? ACME_MATMUL_X6 : ACME_MATMUL_F32; }
 
 const char* acme_last_error(void) { return acme::g_last_error; }
+
+int acme_tune_set(const char* key, int32_t value) {
+  ACME_CHECK_ARG(key, "null key");
+  acme::tune_set(key, value);
+  return ACME_OK;
+}
 
 const char* acme_version(void) { return "acme_amd 0.1.0 (" __DATE__ " " __TIME__ ")"; }
 

@@ -90,6 +90,10 @@ struct acme_dqn {
   bool last_p3 = false;      // the last forward/backward ran the plane path
   uint16_t *wpl = nullptr, *tpl = nullptr;
   uint16_t* frames = nullptr;  // bf16 copies of [o_tm1; o_t] (2B frames)
+  // conv1's input of the current step: l->frames (bf16 copy), or with ACME_V_U8F=2 the
+  // batch's own uint8 frames when o_t directly follows o_tm1 in memory (the GPU dataset
+  // allocates them so).
+  torso::Frames cur_frames{nullptr, false};
   // Second stream of the plane path: the target forward runs beside the online forward,
   // and weight gradients beside input gradients (fork / join by events on the caller's
   // stream; side_slab is its split-K scratch).
@@ -309,7 +313,7 @@ int nature_forward(acme_dqn* l, const float* prm, const void* obs_a, const void*
 
 // Nature forward on the plane path: torso and the fused hidden layer read exact bf16
 // planes (gemm_p3.h); `wpl` are the planes of `prm`.
-int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const uint16_t* frames,
+int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const torso::Frames& frames,
                       int rows, const torso::Plane& x1, const torso::Plane& x2,
                       const torso::Plane& x3, float* hid, float* q, hipStream_t st,
                       float* slab = nullptr) {
@@ -782,7 +786,8 @@ int acme_dqn_q_values(acme_dqn* l, const void* obs, int64_t batch, int32_t use_t
     int rc = sync_planes(l, st);
     if (rc == ACME_OK) rc = convert_frames(l, obs, obs, B, B, st);
     if (rc != ACME_OK) return rc;
-    return nature_forward_p3(l, prm, use_target ? l->tpl : l->wpl, l->frames, B, l->t1p, l->t2p,
+    return nature_forward_p3(l, prm, use_target ? l->tpl : l->wpl, torso::Frames{l->frames, false},
+                             B, l->t1p, l->t2p,
                              l->t3p, l->thid, q_out, st);
   }
   if (l->cfg.network == ACME_NET_NATURE_DQN)
@@ -829,7 +834,7 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
         sd.slab = l->side_slab;
         for (int i = 0; i < 3; ++i) sd.e[i] = l->ev[i];
       }
-      return torso::backward_p3(w, g, l->frames, B,
+      return torso::backward_p3(w, g, l->cur_frames, B,
                                 torso::PActs{l->x1p, l->x2p, l->x3p}, l->dz3p, l->dz2p, l->dz1p,
                                 l->slab, st, sd);
     }
@@ -846,7 +851,16 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
   l->last_p3 = nature && use_p3(l);
   if (l->last_p3) {
     if ((rc = sync_planes(l, st)) != ACME_OK) return rc;
-    if ((rc = convert_frames(l, batch->o_tm1, batch->o_t, B, 2 * B, st)) != ACME_OK) return rc;
+    const uint8_t* o1 = static_cast<const uint8_t*>(batch->o_tm1);
+    // ACME_V_U8F=2: conv1 reads the batch's uint8 frames directly when o_t follows o_tm1.
+    // Faster on one stream (no conversion pass), but measured ~20 us per step slower than
+    // the bf16 copy once the target forward runs on the side stream, so not the default.
+    if (batch->o_t == o1 + (size_t)B * kObsBytes && tune("U8F") == 2) {
+      l->cur_frames = torso::Frames{o1, true};
+    } else {
+      if ((rc = convert_frames(l, batch->o_tm1, batch->o_t, B, 2 * B, st)) != ACME_OK) return rc;
+      l->cur_frames = torso::Frames{l->frames, false};
+    }
     // Target forward (q_t_value) on the side stream, beside the online forward.
     hipStream_t tst = st;
     hipStream_t side = side_stream(l);
@@ -855,12 +869,12 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
       ACME_HIP_TRY(hipStreamWaitEvent(side, l->ev[0], 0));
       tst = side;
     }
-    if ((rc = nature_forward_p3(l, l->target, l->tpl, l->frames + (size_t)B * kObsBytes, B,
+    if ((rc = nature_forward_p3(l, l->target, l->tpl, l->cur_frames.rows_from(B), B,
                                 l->t1p, l->t2p, l->t3p, l->thid, l->q_tg, tst,
                                 side ? l->side_slab : l->slab)) != ACME_OK)
       return rc;
     if (side) ACME_HIP_TRY(hipEventRecord(l->ev[1], side));
-    if ((rc = nature_forward_p3(l, l->params, l->wpl, l->frames, 2 * B, l->x1p, l->x2p, l->x3p,
+    if ((rc = nature_forward_p3(l, l->params, l->wpl, l->cur_frames, 2 * B, l->x1p, l->x2p, l->x3p,
                                 l->hid, l->q_on, st)) != ACME_OK)
       return rc;
     if (side) ACME_HIP_TRY(hipStreamWaitEvent(st, l->ev[1], 0));

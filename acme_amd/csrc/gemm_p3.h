@@ -162,6 +162,33 @@ struct HasStore8<P, decltype(void(P::kStore8))> {
   static constexpr bool value = P::kStore8;
 };
 
+// Optional uint8 A operand: problems with `static constexpr bool kAU8 = true` (one plane)
+// keep A as the raw uint8 frames; the loaders' offsets still count bf16 bytes (2 * element),
+// and the kernel loads the unit's 8 bytes and widens them to the 8 exact bf16 values
+// (integers 0..255), so no converted copy of the frames exists.
+template <class P, class = void>
+struct HasAU8 {
+  static constexpr bool value = false;
+};
+template <class P>
+struct HasAU8<P, decltype(void(P::kAU8))> {
+  static constexpr bool value = P::kAU8;
+};
+// bf16 bit pattern of byte i of w: the upper half of float(byte) (exact).
+__device__ __forceinline__ uint32_t u8pair_bf16(uint32_t w, int i) {
+  const uint32_t a = __builtin_bit_cast(uint32_t, (float)((w >> (8 * i)) & 0xffu));
+  const uint32_t b = __builtin_bit_cast(uint32_t, (float)((w >> (8 * i + 8)) & 0xffu));
+  return (a >> 16) | (b & 0xffff0000u);
+}
+// 16-byte unit (8 bf16) of a uint8 operand at bf16-byte offset `off` (kOOB -> zeros).
+__device__ __forceinline__ u32x4 load_u8_unit(__amdgpu_buffer_rsrc_t rsrc, uint32_t off) {
+  const uint32_t o8 = (off >> 1) | (off & 0x80000000u);
+  typedef __attribute__((ext_vector_type(2))) int i32x2;
+  const i32x2 w = __builtin_amdgcn_raw_buffer_load_b64(rsrc, o8, 0, 0);
+  const uint32_t lo = (uint32_t)w[0], hi = (uint32_t)w[1];
+  return u32x4{u8pair_bf16(lo, 0), u8pair_bf16(lo, 2), u8pair_bf16(hi, 0), u8pair_bf16(hi, 2)};
+}
+
 template <int BK>
 __device__ __forceinline__ int p3_kswz(int row) {
   return BK == 16 ? ((row >> 3) & 1) : ((row >> 2) & 3);
@@ -436,9 +463,13 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in, int
       const int kk = PA::kk_of(u);
       const uint32_t off = (PA::owns(u) && k0 + kk < kend) ? p.a_off(arow[i], k0, kk) : kOOB;
 #pragma unroll
-      for (int pl = 0; pl < NPA; ++pl)
-        ra[set][i][pl] = (P3_EXP == 1 || P3_EXP >= 4) ? u32x4{off, (uint32_t)k0, 1u, 2u}
+      for (int pl = 0; pl < NPA; ++pl) {
+        if constexpr (HasAU8<P>::value)
+          ra[set][i][pl] = load_u8_unit(srcA[pl], off);
+        else
+          ra[set][i][pl] = (P3_EXP == 1 || P3_EXP >= 4) ? u32x4{off, (uint32_t)k0, 1u, 2u}
                                      : __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srcA[pl], off, 0, 0));
+      }
     }
 #pragma unroll
     for (int i = 0; i < PB::PER_THREAD; ++i) {

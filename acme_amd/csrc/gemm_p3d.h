@@ -77,9 +77,13 @@ __global__ void __launch_bounds__(64 * NW) gemm_p3d_kernel(const P p_in) {
         const int kk = 16 * s + kl;
         const uint32_t off = k0 + kk < kend ? p.a_off(arow[i], k0, kk) : kOOB;
 #pragma unroll
-        for (int pl = 0; pl < NPA; ++pl)
-          fa[set][s][i][pl] = __builtin_bit_cast(
-              bf16x8, __builtin_amdgcn_raw_buffer_load_b128(srcA[pl], off, 0, 0));
+        for (int pl = 0; pl < NPA; ++pl) {
+          if constexpr (HasAU8<P>::value)
+            fa[set][s][i][pl] = __builtin_bit_cast(bf16x8, load_u8_unit(srcA[pl], off));
+          else
+            fa[set][s][i][pl] = __builtin_bit_cast(
+                bf16x8, __builtin_amdgcn_raw_buffer_load_b128(srcA[pl], off, 0, 0));
+        }
       }
   };
   auto fetch_b = [&](auto S, int k0) {

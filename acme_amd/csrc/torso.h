@@ -59,8 +59,18 @@ struct PActs {
   Plane x1, x2, x3;
 };
 int64_t wgrad_slab_floats_p3();
+// conv1's input: the uint8 frames themselves (u8, read by the kernels as one exact bf16
+// plane, gemm_p3.h kAU8) or their bf16 copy (launch_frames_bf16); rows of 84*84*4.
+struct Frames {
+  const void* p;
+  bool u8;
+  Frames rows_from(int r) const {
+    const size_t off = (size_t)r * kObsBytes * (u8 ? 1 : 2);
+    return Frames{static_cast<const uint8_t*>(p) + off, u8};
+  }
+};
 // frames: bf16 copies of the uint8 frames [rows][84*84*4] (launch_frames_bf16).
-int forward_p3(const PWeights& w, const uint16_t* frames, int rows, const PActs& a,
+int forward_p3(const PWeights& w, const Frames& frames, int rows, const PActs& a,
                hipStream_t st);
 // Optional second stream for the weight gradients: conv3 / conv2 weight gradients run on
 // `side` (with their own split-K slab) beside the input gradients on the main stream;
@@ -71,7 +81,7 @@ struct Side {
   hipEvent_t e[3] = {nullptr, nullptr, nullptr};
 };
 // dz3: conv3's dZ planes [rows][kFlat] (masked); dz2 / dz1 plane scratch.
-int backward_p3(const PWeights& w, const Grads& g, const uint16_t* frames, int rows,
+int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int rows,
                 const PActs& a, const Plane& dz3, const Plane& dz2, const Plane& dz1, float* slab,
                 hipStream_t st, const Side& side = Side());
 

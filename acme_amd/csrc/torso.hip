@@ -197,8 +197,9 @@ inline Planes pl(const Plane& x) { return Planes{x.p, x.stride}; }
 inline PlaneSrc src(const Plane& x, int64_t elems) {
   return PlaneSrc{x.p, x.stride, (int32_t)(2 * elems)};
 }
-inline PlaneSrc frames_src(const uint16_t* f, int rows) {
-  return PlaneSrc{f, 0, (int32_t)(2 * (int64_t)rows * G1::IPIX * G1::CI)};
+inline PlaneSrc frames_src(const Frames& f, int rows) {
+  return PlaneSrc{static_cast<const uint16_t*>(f.p), 0,
+                  (int32_t)((f.u8 ? 1 : 2) * (int64_t)rows * G1::IPIX * G1::CI)};
 }
 
 template <class P>
@@ -217,9 +218,15 @@ int64_t wgrad_slab_floats_p3() {
                             (int64_t)kP3MaxWgradSplits * (G3::K + 1) * G3::CO});
 }
 
-int forward_p3(const PWeights& w, const uint16_t* frames, int rows, const PActs& a,
+int forward_p3(const PWeights& w, const Frames& frames, int rows, const PActs& a,
                hipStream_t st) {
-  {
+  if (frames.u8) {  // conv1 straight from the uint8 frames
+    P3ConvFwd<G1, 1, true> p;
+    p.M = rows * G1::OPIX; p.N = G1::CO; p.K = G1::K; p.k_chunk = G1::K;
+    p.a_src = frames_src(frames, rows); p.b_src = src(w.w1, G1::K * G1::CO);
+    p.bias = w.b1; p.y = pl(a.x1);
+    P3D_GEMM("conv1_fwd", 32, 2, 4, 32, p);
+  } else {
     P3ConvFwd<G1, 1> p;
     p.M = rows * G1::OPIX; p.N = G1::CO; p.K = G1::K; p.k_chunk = G1::K;
     p.a_src = frames_src(frames, rows); p.b_src = src(w.w1, G1::K * G1::CO);
@@ -283,7 +290,7 @@ int forward_p3(const PWeights& w, const uint16_t* frames, int rows, const PActs&
   return ACME_OK;
 }
 
-int backward_p3(const PWeights& w, const Grads& g, const uint16_t* frames, int rows,
+int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int rows,
                 const PActs& a, const Plane& dz3, const Plane& dz2, const Plane& dz1, float* slab,
                 hipStream_t st_main, const Side& sd) {
   int rc;
@@ -372,7 +379,17 @@ int backward_p3(const PWeights& w, const Grads& g, const uint16_t* frames, int r
       default: P3_GEMM_F("conv2_dgrad", fl, 128, 32, 4, 1, 32, p, G2::S * G2::S); break;
     }
   }
-  {  // conv1 (no input gradient)
+  if (frames.u8) {  // conv1 (no input gradient), straight from the uint8 frames
+    P3ConvWgrad<G1, 1, true> p;
+    p.M = G1::K; p.N = G1::CO; p.K = rows * G1::OPIX;
+    const int splits = wsplits("P3C1WS", kP3Conv1WgradSplits);
+    p.k_chunk = chunk_for(p.K, splits);
+    p.a_src = frames_src(frames, rows); p.b_src = src(dz1, (int64_t)rows * kX1);
+    p.slab = slab;
+    P3_GEMM("conv1_wgrad", 256, 32, 4, 1, 32, p, splits);
+    if ((rc = p3_wgrad_reduce(p, splits, slab, g.w1, g.b1, "conv1_wgrad_reduce", st)))
+      return rc;
+  } else {  // conv1 (no input gradient)
     P3ConvWgrad<G1, 1> p;
     p.M = G1::K; p.N = G1::CO; p.K = rows * G1::OPIX;
     const int splits = wsplits("P3C1WS", kP3Conv1WgradSplits);

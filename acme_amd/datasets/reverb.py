@@ -83,8 +83,18 @@ class _TableIterator:
             self._next_slot = 0
         for _ in range(self._P + 2 if self._P > 0 else 2):
             info = native.alloc_sample_info(self._B)
-            bufs = [torch.empty(self._B, f.row_bytes, dtype=torch.uint8, device=dev)
-                    for f in self._t.fields]
+            fields = self._t.fields
+            bufs = [None] * len(fields)
+            # Transition items (o_tm1, a_tm1, r_t, d_t, o_t, ...): the two observations share
+            # one [2, B, row] allocation, so o_t directly follows o_tm1 and the DQN learner
+            # reads both as one frame array without a packing copy.
+            if (len(fields) >= 5 and fields[0].row_bytes == fields[4].row_bytes
+                    and fields[0].dtype == fields[4].dtype and fields[0].shape == fields[4].shape):
+                pair = torch.empty(2, self._B, fields[0].row_bytes, dtype=torch.uint8, device=dev)
+                bufs[0], bufs[4] = pair[0], pair[1]
+            bufs = [b if b is not None else
+                    torch.empty(self._B, f.row_bytes, dtype=torch.uint8, device=dev)
+                    for b, f in zip(bufs, fields)]
             data = tree.unflatten_as(self._t._structure, [self._typed(b, f)  # noqa: SLF001
                                                           for b, f in zip(bufs, self._t.fields)])
             sample = replay.ReplaySample(

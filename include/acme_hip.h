@@ -45,6 +45,11 @@ typedef enum acme_status {
 } acme_status;
 
 const char* acme_last_error(void);
+
+/* Tuning / experiment switch `key` (the ACME_V_<key> environment variable, read once per
+ * process) set to `value` for the rest of the process; 0 restores the default.  Not part
+ * of the reference interface: kernel-variant selection for tests and sweeps. */
+int acme_tune_set(const char* key, int32_t value);
 /* Library version string (build id). */
 const char* acme_version(void);
 /* Name of the GPU the library was built for ("gfx950"). */

@@ -205,3 +205,33 @@ def test_fused_step_equals_staged_step_bitwise():
             for k in ga:
                 np.testing.assert_array_equal(ga[k], gb[k], err_msg=f"{buf}/{k}")
         assert a.loss.item() == b.loss.item()
+
+
+def test_adjacent_uint8_frames_path_bitwise():
+    """When o_t directly follows o_tm1 in memory (the GPU dataset's layout) conv1 reads the
+    uint8 frames themselves (no bf16 copy); results are bit-identical to the copy path."""
+    from acme_amd.networks import DQNAtariNetwork
+    from acme_amd._lib import lib
+    lib().acme_tune_set(b"U8F", 2)
+    net = DQNAtariNetwork(18)
+    B = 24
+    p0, t0 = net.init(3), net.init(4)
+    a = _learner(net, B)
+    b = _learner(net, B)
+    a.set_params(p0, t0)
+    b.set_params(p0, t0)
+    rng = np.random.default_rng(5)
+    for _ in range(2):
+        dev = _dev(_batch(rng, B, (84, 84, 4), 18))
+        pair = torch.empty(2, B, 84 * 84 * 4, dtype=torch.uint8, device="cuda")
+        pair[0].copy_(dev[0].reshape(B, -1))
+        pair[1].copy_(dev[4].reshape(B, -1))
+        a.step(pair[0], *dev[1:4], pair[1], dev[5])
+        b.step(dev[0].reshape(B, -1).clone(), *dev[1:4], dev[4].reshape(B, -1).clone(), dev[5])
+        torch.cuda.synchronize()
+        assert a.loss.item() == b.loss.item()
+        for buf in ("params", "m", "v"):
+            ga, gb = a.get_params(buf), b.get_params(buf)
+            for k in ga:
+                np.testing.assert_array_equal(ga[k], gb[k], err_msg=f"{buf}/{k}")
+    lib().acme_tune_set(b"U8F", 0)
