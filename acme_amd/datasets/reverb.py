@@ -106,7 +106,9 @@ class _TableIterator:
             ptrs = (ctypes.c_void_p * len(bufs))(*[b.data_ptr() for b in bufs])
             raw = tuple(info[k].data_ptr() for k in ("slots", "keys", "probabilities",
                                                       "table_size", "priorities"))
-            self._slots.append((raw, ptrs, sample))
+            # `info` and `bufs` own the device memory behind `raw` / `ptrs` (the sampled
+            # slots have no other reference): keep them alive with the slot set.
+            self._slots.append((raw, ptrs, sample, info, bufs))
         self._which = 0
 
     def _typed(self, buf, f):
@@ -119,6 +121,13 @@ class _TableIterator:
     def __iter__(self):
         return self
 
+    def _gather(self, L, h, slots, ptrs, st):
+        from acme_amd._lib import check
+        if isinstance(self._t, replay.FrameTable):  # stacks rebuilt from stored frames
+            self._t.gather_into(slots, self._B, ptrs, st)
+        else:
+            check(L.acme_replay_gather(h, slots, self._B, ptrs, st), "replay gather")
+
     def __next__(self) -> replay.ReplaySample:
         from acme_amd._lib import check, lib, stream_ptr
         t = self._t
@@ -129,12 +138,12 @@ class _TableIterator:
             self._alloc()
         L, h = lib(), t.native.handle
         if self._P == 0:
-            raw, ptrs, sample = self._slots[self._which]
+            raw, ptrs, sample = self._slots[self._which][:3]
             self._which ^= 1
             st = stream_ptr()
             check(L.acme_replay_sample(h, self._B, t.next_draw() & 0xFFFFFFFFFFFFFFFF, *raw, st),
                   "replay sample")
-            check(L.acme_replay_gather(h, raw[0], self._B, ptrs, st), "replay gather")
+            self._gather(L, h, raw[0], ptrs, st)
             return sample
         # Prefetch: order the dataset stream after everything queued so far on the caller's
         # stream (inserts, earlier learner steps and their priority updates), top the queue
@@ -146,10 +155,10 @@ class _TableIterator:
         while len(self._queue) < self._P + 1:
             i = self._next_slot
             self._next_slot = (i + 1) % (self._P + 2)
-            raw, ptrs, _ = self._slots[i]
+            raw, ptrs = self._slots[i][:2]
             check(L.acme_replay_sample(h, self._B, t.next_draw() & 0xFFFFFFFFFFFFFFFF, *raw, st),
                   "replay sample")
-            check(L.acme_replay_gather(h, raw[0], self._B, ptrs, st), "replay gather")
+            self._gather(L, h, raw[0], ptrs, st)
             self._ready[i].record(self._stream)
             self._queue.append(i)
         i = self._queue.pop(0)

@@ -225,6 +225,11 @@ class Table:
             self._native.update_priorities(k, p)
 
 
+from acme_amd.replay.frame_table import _make_frame_table  # noqa: E402
+
+FrameTable = _make_frame_table(Table, _Field, _layout_from_signature)
+
+
 class QueueTable:
     """Table.queue: FIFO items consumed once (IMPALA).  Host-resident; batches are
     stacked and moved to the device by the dataset."""

@@ -117,6 +117,15 @@ int acme_replay_sample(acme_replay* r, int64_t batch, uint64_t step_counter,
 int acme_replay_gather(acme_replay* r, const int64_t* slots, int64_t batch,
                        void* const* out_fields, void* stream);
 
+/* Frame-deduplicated observations: rebuild `batch` stacked
+ * observations out[b] = stack(frames[idx[b][0..stack-1]], axis=-1) (uint8 HWC, as
+ * acme/wrappers/frame_stacking.py:78-83 builds them) from a device frame ring
+ * frames[num_frames][frame_bytes]; idx is int32 [batch][stack] on the device.  Replaces the
+ * whole-stack storage of adders/reverb/transition.py:147-152 (replay/FrameTable). */
+int acme_frames_expand(const uint8_t* frames, int64_t num_frames, int64_t frame_bytes,
+                       int32_t stack, const int32_t* idx, int64_t batch, uint8_t* out,
+                       void* stream);
+
 /* Set priorities of the items identified by device arrays keys/priorities.  Keys no
  * longer in the table are ignored; for repeated keys the last one wins (Reverb
  * applies updates in order). */

@@ -97,7 +97,7 @@ def test_dqn_learner_step_through_dataset_matches_oracle():
     torch.cuda.synchronize()
     # Re-draw the same batch from a fresh iterator of an identical table state is not
     # possible after the priority update, so recover the batch from the learner's sample:
-    _, _, sample = learner._iterator._slots[0]  # noqa: SLF001 - the buffers of draw 0
+    sample = learner._iterator._slots[0][2]  # noqa: SLF001 - the buffers of draw 0
     o1, a, r, d, o2 = sample.data
     batch = dict(o_tm1=o1.cpu().numpy(), a_tm1=a.cpu().numpy().reshape(-1),
                  r_t=r.cpu().numpy().reshape(-1), d_t=d.cpu().numpy().reshape(-1),

@@ -1,0 +1,116 @@
+"""FrameTable: frame-deduplicated Atari replay.
+
+The same Atari-shaped episodes (FrameStacker semantics, acme/wrappers/frame_stacking.py:
+78-83: zero-padded np.stack(last 4 frames, axis=-1)) go through the unchanged
+NStepTransitionAdder into a Table and into a FrameTable with the same seed; the two datasets
+must return bit-identical ReplaySamples (keys, probabilities, every observation byte),
+including after FIFO eviction and frame-ring recycling, while the FrameTable stores about
+one frame per environment step instead of 2 x 4 per transition."""
+
+import numpy as np
+import pytest
+import torch
+
+from acme_amd import dm_env, replay, specs
+from acme_amd.adders import reverb as adders
+from acme_amd.datasets import make_reverb_dataset
+
+pytestmark = pytest.mark.gpu
+
+H = W = 84
+S = 4
+
+
+def _spec():
+    return specs.EnvironmentSpec(observations=specs.Array((H, W, S), np.uint8),
+                                 actions=specs.DiscreteArray(18, np.int32),
+                                 rewards=specs.Array((), np.float32),
+                                 discounts=specs.BoundedArray((), np.float32, 0.0, 1.0))
+
+
+def _episodes(rng, n_episodes, length):
+    for _ in range(n_episodes):
+        stack = [np.zeros((H, W), np.uint8)] * (S - 1)
+        frames = []
+        for t in range(length + 1):
+            f = rng.integers(0, 256, (H, W), dtype=np.uint8)
+            if t % 7 == 3:
+                f = frames[-1]  # a repeated frame (static screen) dedups too
+            frames.append(f)
+            stack = (stack + [f])[-S:]
+            yield t, length, np.stack(stack, axis=-1)
+
+
+def _fill(tables, rng, n_episodes, length):
+    clients = []
+    for t in tables:
+        server = replay.Server([t])
+        clients.append((server, adders.NStepTransitionAdder(replay.Client(server), n_step=3,
+                                                            discount=0.99)))
+    for t, L, obs in _episodes(rng, n_episodes, length):
+        for _, adder in clients:
+            if t == 0:
+                adder.add_first(dm_env.restart(obs))
+            else:
+                r = np.float32(t)
+                ts = (dm_env.termination(r, obs) if t == L else
+                      dm_env.transition(r, obs, np.float32(1.0)))
+                adder.add(np.int32(t % 18), ts)
+    return [s for s, _ in clients]
+
+
+@pytest.mark.parametrize("capacity,max_frames", [(500, None), (120, 200)])
+def test_frame_table_samples_bit_identical(capacity, max_frames):
+    spec = _spec()
+    sig = adders.NStepTransitionAdder.signature(spec)
+    mk = dict(name=adders.DEFAULT_PRIORITY_TABLE, sampler=replay.selectors.Prioritized(0.6),
+              remover=replay.selectors.Fifo(), max_size=capacity,
+              rate_limiter=replay.rate_limiters.MinSize(1), signature=sig, seed=77)
+    plain = replay.Table(**mk)
+    ft = replay.FrameTable(**mk, max_frames=max_frames)
+    s_plain, s_ft = _fill([plain, ft], np.random.default_rng(0), n_episodes=6, length=40)
+    assert plain.size() == ft.size() > 0
+    # ~ one new frame per env step (+ none for repeated frames), vs 8 per transition
+    assert ft.frames_stored <= 6 * 41
+    assert ft.stored_bytes_per_item < 64
+    it_a = iter(make_reverb_dataset(s_plain, batch_size=64, prefetch_size=2))
+    it_b = iter(make_reverb_dataset(s_ft, batch_size=64, prefetch_size=2))
+    rng = np.random.default_rng(1)
+    for _ in range(4):
+        a, b = next(it_a), next(it_b)
+        torch.cuda.synchronize()
+        for x, y in zip(a.info, b.info):
+            np.testing.assert_array_equal(x.cpu().numpy(), y.cpu().numpy())
+        for x, y in zip(a.data, b.data):
+            assert x.dtype == y.dtype and x.shape == y.shape
+            np.testing.assert_array_equal(x.cpu().numpy(), y.cpu().numpy())
+        newp = torch.as_tensor(rng.uniform(0.1, 2.0, 64)).cuda()
+        for srv, smp in ((s_plain, a), (s_ft, b)):
+            replay.Client(srv).update_priorities(adders.DEFAULT_PRIORITY_TABLE, smp.info.key,
+                                                 newp)
+
+
+def test_frame_table_too_small_ring_raises():
+    spec = _spec()
+    sig = adders.NStepTransitionAdder.signature(spec)
+    ft = replay.FrameTable(adders.DEFAULT_PRIORITY_TABLE, replay.selectors.Uniform(),
+                           replay.selectors.Fifo(), 100, replay.rate_limiters.MinSize(1),
+                           signature=sig, max_frames=20)
+    with pytest.raises(ValueError, match="max_frames"):
+        _fill([ft], np.random.default_rng(2), n_episodes=2, length=40)
+
+
+def test_frames_expand_matches_numpy():
+    from acme_amd._lib import check, lib
+    rng = np.random.default_rng(3)
+    F, px, B = 37, 84 * 84, 9
+    frames = torch.as_tensor(rng.integers(0, 256, (F, px), dtype=np.uint8)).cuda()
+    for stack in (4, 3):
+        idx = rng.integers(0, F, (B, stack)).astype(np.int32)
+        out = torch.empty(B, px * stack, dtype=torch.uint8, device="cuda")
+        check(lib().acme_frames_expand(frames.data_ptr(), F, px, stack,
+                                       torch.as_tensor(idx).cuda().data_ptr(), B, out.data_ptr(),
+                                       0), "expand")
+        torch.cuda.synchronize()
+        ref = np.stack([frames.cpu().numpy()[idx[:, s]] for s in range(stack)], axis=-1)
+        np.testing.assert_array_equal(out.cpu().numpy(), ref.reshape(B, -1))
