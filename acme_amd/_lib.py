@@ -116,6 +116,8 @@ _SIGS = {
     "acme_replay_fill_synthetic": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_u64, c_vp]),
     "acme_replay_sample": (c_i32, [c_vp, c_i64, c_u64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "acme_replay_gather": (c_i32, [c_vp, c_vp, c_i64, ctypes.POINTER(c_vp), c_vp]),
+    "acme_r2d2_priorities": (c_i32, [c_vp, c_i32, c_i32, ctypes.c_double, c_vp, c_vp]),
+    "acme_r2d2_importance_weights": (c_i32, [c_vp, c_i32, c_i64, ctypes.c_double, c_vp, c_vp]),
     "acme_frames_expand": (c_i32, [c_vp, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp, c_vp]),
     "acme_replay_update_priorities": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp]),
     "acme_replay_size": (c_i64, [c_vp]),

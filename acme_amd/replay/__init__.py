@@ -125,6 +125,7 @@ class Table:
         self._mu = threading.RLock()
         self._cv = threading.Condition(self._mu)
         self._draws = 0
+        self._seq_len: Optional[int] = None
         if signature is not None:
             self._init_layout(signature, _layout_from_signature(signature))
 
@@ -166,6 +167,7 @@ class Table:
             if len(leaves) != len(self._fields):
                 raise ValueError(f"item has {len(leaves)} leaves, table expects "
                                  f"{len(self._fields)}")
+            self._maybe_sequence_layout(leaves)
             row = []
             for leaf, f in zip(leaves, self._fields):
                 a = np.asarray(leaf, dtype=f.dtype)
@@ -178,6 +180,32 @@ class Table:
             if len(self._pending) >= self._flush_every:
                 self.flush()
             self._cv.notify_all()
+
+    def _maybe_sequence_layout(self, leaves) -> None:
+        """Sequence items (SequenceAdder, R2D2): Reverb signatures are per timestep
+        (adders/reverb/base.py:179-206) and the table stores T-step items.  The first item
+        whose every leaf is [T] + the signature's shape fixes the stored layout to T steps."""
+        if self._seq_len is not None or self._pending or self._native.size() > 0:
+            return
+        shapes = [np.shape(x) for x in leaves]
+        if all(s == f.shape for s, f in zip(shapes, self._fields)):
+            self._seq_len = 0
+            return
+        T = shapes[0][0] if shapes[0] else None
+        if T is None or not all(len(s) == len(f.shape) + 1 and s[0] == T and s[1:] == f.shape
+                                for s, f in zip(shapes, self._fields)):
+            return  # a genuine mismatch: reported by the caller's shape check
+        self._seq_len = int(T)
+        seq = [_Field((T,) + f.shape, f.dtype, T * f.nbytes, _row_bytes(T * f.nbytes,
+                                                                      f.dtype.itemsize))
+               for f in self._fields]
+        self._native = None
+        self._init_layout(self._structure, seq)
+
+    @property
+    def sequence_length(self) -> Optional[int]:
+        """Steps per item for sequence tables (None until the first item, 0 if not)."""
+        return self._seq_len
 
     def flush(self) -> None:
         with self._mu:

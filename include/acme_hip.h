@@ -126,6 +126,17 @@ int acme_frames_expand(const uint8_t* frames, int64_t num_frames, int64_t frame_
                        int32_t stack, const int32_t* idx, int64_t batch, uint8_t* out,
                        void* stream);
 
+/* R2D2 prioritized sequence replay, device arrays:
+ * priorities out[b] = (f64)(eta * max_t |errors[t][b]| + (1 - eta) * mean_t |errors[t][b]|)
+ *   in f32, errors [T][B] (acme/agents/tf/r2d2/learning.py:230-236, written back at :196-199);
+ * importance weights out[b] = (f32)((1 / (N p_b))^beta / max_b (1 / (N p_b))^beta) in f64,
+ *   N = max_replay_size (learning.py:178-183; the [T, B] weights are this, per sequence). */
+int acme_r2d2_priorities(const float* errors, int32_t T, int32_t B, double eta, double* out,
+                         void* stream);
+int acme_r2d2_importance_weights(const double* probabilities, int32_t B,
+                                 int64_t max_replay_size, double beta, float* out,
+                                 void* stream);
+
 /* Set priorities of the items identified by device arrays keys/priorities.  Keys no
  * longer in the table are ignored; for repeated keys the last one wins (Reverb
  * applies updates in order). */
