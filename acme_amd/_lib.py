@@ -246,3 +246,19 @@ def stream_ptr(stream=None) -> int:
 
 def ptr(t) -> int:
     return 0 if t is None else int(t.data_ptr())
+
+
+_PROFILING = False
+
+
+def set_profiling(on: bool) -> None:
+    """Turns the library's section profiler on/off (acme_profile_enable).  While it is on,
+    Python-side producers (the prefetching dataset) also issue on the caller's stream, so
+    every profiled kernel runs alone."""
+    global _PROFILING
+    check(lib().acme_profile_enable(1 if on else 0), "profile enable")
+    _PROFILING = bool(on)
+
+
+def profiling() -> bool:
+    return _PROFILING

@@ -148,10 +148,14 @@ class _TableIterator:
         # Prefetch: order the dataset stream after everything queued so far on the caller's
         # stream (inserts, earlier learner steps and their priority updates), top the queue
         # up to P + 1 batches, hand out the oldest.
+        from acme_amd._lib import profiling
         main = torch.cuda.current_stream(self._t.native.device)
+        # Under the section profiler the batches are issued on the caller's stream, so no
+        # profiled kernel shares the GPU with a prefetch (same draws, same order).
+        side = main if profiling() else self._stream
         self._issued.record(main)
-        self._stream.wait_event(self._issued)
-        st = stream_ptr(self._stream)
+        side.wait_event(self._issued)
+        st = stream_ptr(side)
         while len(self._queue) < self._P + 1:
             i = self._next_slot
             self._next_slot = (i + 1) % (self._P + 2)
@@ -159,7 +163,7 @@ class _TableIterator:
             check(L.acme_replay_sample(h, self._B, t.next_draw() & 0xFFFFFFFFFFFFFFFF, *raw, st),
                   "replay sample")
             self._gather(L, h, raw[0], ptrs, st)
-            self._ready[i].record(self._stream)
+            self._ready[i].record(side)
             self._queue.append(i)
         i = self._queue.pop(0)
         main.wait_event(self._ready[i])

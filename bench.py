@@ -396,12 +396,13 @@ def main():
     # (HIP event pairs on the launch stream), so its event records stay out of the timed
     # region above.
     if not args.no_profile and args.profile_steps > 0:
+        torch.cuda.synchronize(dev)  # prefetched batches land before profiling starts
         L.acme_profile_reset()
-        L.acme_profile_enable(1)
+        _lib.set_profiling(True)
         for i in range(args.profile_steps):
             step()
         torch.cuda.synchronize(dev)
-        L.acme_profile_enable(0)
+        _lib.set_profiling(False)
     loss = loss_fn()
 
     sections = []

@@ -78,7 +78,7 @@ def section(name):
 
 def per_launch(d, counter):
     vals = collections.defaultdict(list)
-    for path in glob.glob(f"{d}/*counter_collection.csv"):
+    for path in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(path)):
             if r["Counter_Name"] != counter:
                 continue
