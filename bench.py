@@ -359,10 +359,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # One rank per GPU.  More ranks than visible GPUs (a rehearsal on a one-GPU box) share
+    # devices round-robin; ACME_DIST_BACKEND=gloo selects gloo for such a rehearsal, since
+    # RCCL rejects two ranks on one device.  The driver's runs use RCCL ("nccl").
+    ngpu = torch.cuda.device_count()
+    local = local % max(ngpu, 1)
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("ACME_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         dist = None
     dev = torch.device("cuda", local)
