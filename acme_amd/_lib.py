@@ -15,7 +15,8 @@ import threading
 import torch  # noqa: F401  (must load the HIP runtime before libacme_hip.so)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libacme_hip.so")
+# ACME_LIB_PATH: an alternative build (experiments); the in-tree library by default.
+LIB_PATH = os.environ.get("ACME_LIB_PATH") or os.path.join(_HERE, "libacme_hip.so")
 
 ACME_OK = 0
 ACME_ERR_INVALID = -1
