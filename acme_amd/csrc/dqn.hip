@@ -27,6 +27,7 @@
 #include "conv_p3.h"
 #include "gemm.h"
 #include "gemm_p3.h"
+#include "gemm_p3d.h"
 #include "gemm_x6.h"
 #include "kernels.h"
 #include "profiler.h"
@@ -210,6 +211,18 @@ int tune(const char* key) { return tune_variant(key); }
     }                                                                                          \
   } while (0)
 
+// Direct-A plane GEMM (gemm_p3d.h): BN-column panels, NW waves of 32 * MT rows each.
+#define ACME_P3D_GEMM(name, BN, MT, NW, BKV, prob, splits)                                    \
+  do {                                                                                        \
+    ACME_PROF_PEAK(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0, \
+                   gemm::p3_peak_tflops<decltype(prob)>());                                   \
+    hipError_t _e = gemm::launch_gemm_p3d<BN, MT, NW, BKV>(prob, splits, st);                 \
+    if (_e != hipSuccess) {                                                                   \
+      set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
+      return ACME_ERR_HIP;                                                                    \
+    }                                                                                         \
+  } while (0)
+
 #define ACME_P3_GEMM(name, BM, BN, WM, WN, BKV, prob, splits)                                \
   do {                                                                                         \
     ACME_PROF_PEAK(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0, \
@@ -342,6 +355,10 @@ int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const torso:
       case 6: ACME_P3_GEMM("fc_fwd", 256, 128, 4, 2, 16, p, splits); break;
       case 7: ACME_P3_GEMM("fc_fwd", 256, 256, 4, 2, 16, p, splits); break;
       case 8: ACME_P3P_GEMM("fc_fwd", 128, 128, 2, 2, p, splits); break;
+      case 9: ACME_P3D_GEMM("fc_fwd", 128, 1, 4, 32, p, splits); break;
+      case 10: ACME_P3D_GEMM("fc_fwd", 128, 2, 4, 32, p, splits); break;
+      case 11: ACME_P3D_GEMM("fc_fwd", 64, 1, 4, 32, p, splits); break;
+      case 12: ACME_P3D_GEMM("fc_fwd", 128, 1, 8, 32, p, splits); break;
       default: ACME_P3_GEMM("fc_fwd", 128, 128, 2, 2, 32, p, splits); break;
     }
     ACME_PROF("fc_head_fwd", st, 0.0, 4.0 * (double)rows * 2 * kHidden * (splits + 1));
@@ -463,6 +480,8 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st_main,
         case 4: ACME_P3_GEMM("fc_dgrad", 128, 128, 2, 2, 32, p, 1); break;
         case 8: ACME_P3P_GEMM("fc_dgrad", 128, 128, 2, 2, p, 1); break;
         case 9: ACME_P3P_GEMM("fc_dgrad", 64, 128, 2, 2, p, 1); break;
+        case 10: ACME_P3D_GEMM("fc_dgrad", 128, 1, 4, 32, p, 1); break;
+        case 11: ACME_P3D_GEMM("fc_dgrad", 128, 2, 4, 32, p, 1); break;
         default: ACME_P3G_GEMM("fc_dgrad", 128, 128, 2, 2, 32, 3, p, 1); break;
       }
     }

@@ -1,5 +1,8 @@
-// Direct-operand plane GEMM (gfx950): for the Nature-CNN convolutions, whose N (output or
-// input channels, 32 or 64) fits one block, so every A element is used by exactly ONE wave.
+// Direct-operand plane GEMM (gfx950): the block's waves are stacked along M (WN = 1), so
+// every A element of the block's N panel (<= 128 columns) is used by exactly ONE wave.
+// Written for the Nature-CNN convolutions (N = 32 or 64 channels: one panel); wider
+// problems (the fused dense layer) tile N in 128-column panels and may split K
+// (blockIdx.z, p.k_chunk per split, as gemm_p3_kernel).
 //
 // gemm_p3.h stages both operands through LDS.  With N <= 64 the A tile dominates the
 // staging traffic: (BM + BN) * BK * 6 bytes of ds_write_b128 per stage against BM * BN * BK
@@ -31,7 +34,7 @@ struct P3DCfg {
 };
 
 template <int BN_, int MT, int NW, int BK, class P>
-__global__ void __launch_bounds__(64 * NW) gemm_p3d_kernel(const P p_in) {
+__global__ void __launch_bounds__(64 * NW) gemm_p3d_kernel(const P p_in, int n_major) {
   static_assert(P::A_MODE == KCONTIG, "direct A fragments need k-contiguous A units");
   using Cfg = P3DCfg<BN_, MT, NW, BK, P>;
   using C = typename Cfg::Core;
@@ -39,16 +42,19 @@ __global__ void __launch_bounds__(64 * NW) gemm_p3d_kernel(const P p_in) {
   constexpr int BN = Cfg::BN, BM = Cfg::BM;
   constexpr int NT = 64 * NW, NPA = P::A_PLANES, NPB = P::B_PLANES, NTL = BN / 32;
   constexpr int KS = BK / 16;  // k16 steps per stage
-  static_assert(BN % 32 == 0 && BN <= 64, "N must be one 32- or 64-column panel");
-  const BlockPlace bp = place_block<BM, BN>(p_in.M, BN, 0);
+  static_assert(BN % 32 == 0 && BN <= 128, "N panel of 32, 64, 96 or 128 columns");
+  const BlockPlace bp = place_block<BM, BN>(p_in.M, p_in.N, n_major);
   const P p = z_select_at(p_in, bp.z);
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int m0 = bp.m0;
-  const int kbeg = 0, kend = p.K;
-  const int nk = (kend + BK - 1) / BK;
+  const int m0 = bp.m0, n0 = bp.n0;
+  // blockIdx.z: the problem's class (kZClass) or its K split.
+  const int split = HasZClass<P>::value ? 0 : bp.z;
+  const int kbeg = split * p.k_chunk;
+  const int kend = kbeg + p.k_chunk < p.K ? kbeg + p.k_chunk : p.K;
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
 
   // This lane's A rows (one per 32-row block of the wave's tile) and k offset in a step.
   typename P::ARow arow[MT];
@@ -58,7 +64,7 @@ __global__ void __launch_bounds__(64 * NW) gemm_p3d_kernel(const P p_in) {
   typename P::BRow brow[PB::PER_THREAD];
 #pragma unroll
   for (int i = 0; i < PB::PER_THREAD; ++i)
-    brow[i] = p.b_row(PB::owns(tid + i * NT) ? PB::row_of(tid + i * NT) : 0);
+    brow[i] = p.b_row(n0 + (PB::owns(tid + i * NT) ? PB::row_of(tid + i * NT) : 0));
 
   __amdgpu_buffer_rsrc_t srcA[NPA], srcB[NPB];
 #pragma unroll
@@ -186,19 +192,19 @@ __global__ void __launch_bounds__(64 * NW) gemm_p3d_kernel(const P p_in) {
   if (kt < nk) iter(S0{}, kt);
 
   f32x16 cs[C::NCS];
-  C::epilogue(p, smem, m0, 0, wave, wave, 0, lane, 0, acc, cs, false);
+  C::epilogue(p, smem, m0, n0, wave, wave, 0, lane, split, acc, cs, false);
 }
 
+// z: the number of classes of a kZClass problem, else of K splits (p.k_chunk each).
 template <int BN, int MT, int NW, int BK, class P>
-inline hipError_t launch_gemm_p3d(const P& p, int zclasses, hipStream_t st) {
+inline hipError_t launch_gemm_p3d(const P& p, int z, hipStream_t st) {
   using Cfg = P3DCfg<BN, MT, NW, BK, P>;
   static_assert(Cfg::LDS <= 160 * 1024, "LDS");
   static hipError_t attr = p3_set_lds(&gemm_p3d_kernel<BN, MT, NW, BK, P>, Cfg::LDS);
   if (attr != hipSuccess) return attr;
-  if (p.N > Cfg::BN) return hipErrorInvalidValue;
-  const int tiles = (p.M + Cfg::BM - 1) / Cfg::BM;
-  hipLaunchKernelGGL((gemm_p3d_kernel<BN, MT, NW, BK, P>), dim3(tiles, 1, zclasses), dim3(64 * NW),
-                     Cfg::LDS, st, p);
+  const int tiles = ((p.N + Cfg::BN - 1) / Cfg::BN) * ((p.M + Cfg::BM - 1) / Cfg::BM);
+  hipLaunchKernelGGL((gemm_p3d_kernel<BN, MT, NW, BK, P>), dim3(tiles, 1, z), dim3(64 * NW),
+                     Cfg::LDS, st, p, p3_n_major(p));
   return hipGetLastError();
 }
 

@@ -118,6 +118,24 @@ def test_forward_backward_matches_oracle(netname, B):
     _check_grads(d.get_params("grads"), grads)
 
 
+@pytest.mark.parametrize("variants", [
+    {"P3FCF": 9}, {"P3FCF": 10}, {"P3FCF": 11}, {"P3FCF": 12}, {"P3FCD": 10}, {"P3FCD": 11},
+    {"P3C2F": 12}, {"P3C2F": 13}, {"P3C3F": 12}, {"P3C3F": 13}, {"P3C3F": 14}, {"P3C3F": 15},
+    {"P3C3F": 16}, {"P3C3D": 13}, {"P3C3D": 14}, {"P3C3D": 16}])
+def test_kernel_variants_match_oracle(variants):
+    """The plane engine's alternative kernels (acme_tune_set switches: direct-A dense layers,
+    image-resident convolutions; B = 37 leaves partial tiles and a half-filled two-frame
+    block) against the oracle, as test_forward_backward_matches_oracle."""
+    from acme_amd._lib import lib
+    for k, v in variants.items():
+        lib().acme_tune_set(k.encode(), v)
+    try:
+        test_forward_backward_matches_oracle("nature", 37)
+    finally:
+        for k in variants:
+            lib().acme_tune_set(k.encode(), 0)
+
+
 def test_adam_and_target_copy_cadence():
     from acme_amd.networks import MLP
     net = MLP(4, [50, 50], 2)
