@@ -411,6 +411,10 @@ struct P3Core {
 #ifndef P3_SCHED
 #define P3_SCHED 0
 #endif
+#ifndef P3_FETCH_FIRST
+#define P3_FETCH_FIRST 0  // 1: stage kt+2 loads issued at the top of iteration kt (see iter);
+                          // measured slower (fc_fwd 64 -> 75 us), kept as an experiment switch
+#endif
 #ifndef P3_EARLY_STASH
 #define P3_EARLY_STASH 1
 #endif
@@ -578,11 +582,19 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in, int
               for (int k = g * WR / G; k < (g + 1) * WR / G; ++k) stash_one(Other{}, set ^ 1, k);
             };
             C::template mma<0, 1>(sa, sa + PA::BYTES, wm, wn, lane, acc, cs, do_colsum, hook);
+          } else if constexpr (P3_FETCH_FIRST) {
+            // The global loads of stage kt + 2 first (their registers were stashed in
+            // iteration kt - 1), fenced so the scheduler cannot sink them behind the MFMAs:
+            // they get two whole iterations to land before their stash.
+            fetch(S, kbeg + (kt + 2) * BK);
+            __builtin_amdgcn_sched_barrier(0);
+            C::template mma<0, 1>(sa, sa + PA::BYTES, wm, wn, lane, acc, cs, do_colsum);
+            stash(Other{}, set ^ 1);
           } else {
             C::template mma<0, 1>(sa, sa + PA::BYTES, wm, wn, lane, acc, cs, do_colsum);
             stash(Other{}, set ^ 1);
           }
-          fetch(S, kbeg + (kt + 2) * BK);
+          if constexpr (!P3_FETCH_FIRST || P3_SPLIT == 2) fetch(S, kbeg + (kt + 2) * BK);
           C::template mma<1, 2>(sa, sa + PA::BYTES, wm, wn, lane, acc, cs, do_colsum);
         } else {
           stash(Other{}, set ^ 1);

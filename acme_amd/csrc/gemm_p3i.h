@@ -1,22 +1,24 @@
 // Image-resident implicit-GEMM convolution on exact bf16 planes (gfx950).
 //
 // gemm_p3.h reads a convolution's A operand as im2col rows: every input pixel is fetched
-// KH*KW/S^2 times (4x for conv2, 9x for conv3) and every fetch goes global -> VGPR -> LDS,
-// so the A tile's LDS stores (ds_write_b128 ~79 B/clk/CU, MI355X_MICROARCH.md §LDS) and its
-// duplicated L2 reads bound conv2/conv3 (29-34% of the plane-engine ceiling).  Here a block
-// owns FPB whole frames: their input image, all three planes, is loaded into LDS ONCE (each
-// HBM byte once, each LDS byte stored once), and the MFMA A fragments are read from it
-// directly, with the tap offset applied per lane (padding taps read a zero unit).  Only the
-// weight panel B (K x BN) streams through the two-stage register-staged LDS ring of
-// gemm_p3d.h.  Per 32-k stage a wave issues MT * 2 * 3 ds_read_b128 for A and its NTL B
-// fragments per k16 step, against MT * NTL * 2 * 6 MFMAs.
+// KH*KW/S^2 times (4x for conv1 / conv2, 9x for conv3) and every fetch goes global -> VGPR
+// -> LDS (or, in gemm_p3d.h, global -> VGPR as short per-lane row segments), so the A
+// tile's LDS stores (ds_write_b128 ~79 B/clk/CU, MI355X_MICROARCH.md §LDS) or its TA
+// issue bound the convolutions (15-34% of the plane-engine ceiling).  Here a block owns
+// FPB whole frames: their input image, every plane, is loaded into LDS ONCE (each HBM
+// byte once, each LDS byte stored once), and the MFMA A fragments are read from it
+// directly, with the tap offset applied per lane (padding taps read a zero unit).  Only
+// the weight panel B (K x BN) streams through the two-stage register-staged LDS ring of
+// gemm_p3d.h.
 //
-// LDS image layout, per plane: pixel q = (frame * H + ih) * W + col, col = iw (stride 1)
-// or, for stride 2, the even columns then the odd ones (consecutive output columns, i.e.
-// the consecutive rows of an MFMA fragment, read consecutive pixels); the 16-B channel
-// chunk c of pixel q sits at chunk c ^ ((q >> SWZ) & (CPX - 1)), CPX chunks per pixel, so
-// 16 consecutive pixels' reads of one chunk fall in 16 distinct 4-bank groups (a
-// conflict-free ds_read_b128 lane group).  A zero unit follows each plane's image.
+// A geometry GI says where each 16-B unit (8 consecutive k of one GEMM row) lives:
+//   UNITS            16-B HBM units per frame (frames contiguous in HBM);
+//   IMG              LDS bytes of one frame's image (one plane);
+//   fill(f, u)       LDS byte offset of HBM unit u of the block's frame f;
+//   Lane lane(f, pp, ok)         per-lane state of output pixel pp of frame f;
+//   Stage stage(lane, k0)        per 32-k stage (k0 a multiple of 32);
+//   int unit(stage, lane, k0, s, h)  byte offset of the lane's unit in k16 step s (lane
+//                                    half h), or -1 for padding (the zero unit).
 #pragma once
 
 #include "gemm_p3.h"
@@ -24,11 +26,17 @@
 namespace acme {
 namespace gemm {
 
-// Image and tap geometry of a convolution GEMM over conv.h's Geom G.  Forward (DGRAD =
-// false): the image is the layer input X [IH][IW][CI], GEMM rows are (frame, oh, ow), tap
-// (kh, kw) reads (oh*S - PT + kh, ow*S - PL + kw).  Stride-1 input gradient (DGRAD = true):
-// the image is dZ [OH][OW][CO], rows are (frame, ih, iw), tap (kh, kw) reads
-// (ih + PT - kh, iw + PL - kw).  K is ordered (kh, kw, channel) in both, as conv_p3.h.
+// Channel-chunk images (conv2 / conv3 forward, stride-1 input gradient) over conv.h's Geom
+// G.  Forward (DGRAD = false): the image is the layer input X [IH][IW][CI], GEMM rows are
+// (frame, oh, ow), tap (kh, kw) reads (oh*S - PT + kh, ow*S - PL + kw).  Input gradient
+// (DGRAD = true, stride 1): the image is dZ [OH][OW][CO], rows are (frame, ih, iw), tap
+// (kh, kw) reads (ih + PT - kh, iw + PL - kw).  K is ordered (kh, kw, channel), as
+// conv_p3.h; C is 32 or 64, so a 32-k stage stays within one tap.
+// LDS layout, per plane: pixel q = (frame * H + ih) * W + col, col = iw (stride 1) or, for
+// stride 2, the even columns then the odd ones (consecutive output columns, i.e. the
+// consecutive rows of an MFMA fragment, read consecutive pixels); the 16-B channel chunk c
+// of pixel q sits at chunk c ^ ((q >> SWZ) & (CPX - 1)), CPX chunks per pixel, so 16
+// consecutive pixels' reads of one chunk fall in 16 distinct 4-bank groups.
 template <class G, bool DGRAD>
 struct ImgGeom {
   static constexpr int H = DGRAD ? G::OH : G::IH, W = DGRAD ? G::OW : G::IW;
@@ -40,18 +48,86 @@ struct ImgGeom {
   static constexpr int CPX = C / 8;         // 16-B chunks per pixel
   static constexpr int HALF = (W + 1) / 2;  // stride 2: even columns first
   static constexpr int SWZ = CPX == 8 ? 1 : 2;
+  static constexpr int UNITS = IPIX * CPX, IMG = IPIX * 2 * C;
   static_assert(!DGRAD || G::S == 1, "strided input gradients are not image-resident");
   static_assert(C == 32 || C == 64, "a 32-k stage must stay within one tap");
   static_assert(S == 1 || S == 2, "stride 1 or 2");
   __device__ static __forceinline__ int dh(int kh) { return DGRAD ? G::PT - kh : kh - G::PT; }
   __device__ static __forceinline__ int dw(int kw) { return DGRAD ? G::PL - kw : kw - G::PL; }
-  // LDS pixel index of (fr, ih, iw) among the block's frames.
   __device__ static __forceinline__ int pix(int fr, int ih, int iw) {
     return (fr * H + ih) * W + (S == 1 ? iw : (iw & 1) * HALF + (iw >> 1));
   }
   __device__ static __forceinline__ int swz(int q) { return (q >> SWZ) & (CPX - 1); }
-  // Byte offset, within a plane, of chunk c of LDS pixel q.
-  __device__ static __forceinline__ int addr(int q, int c) { return q * (2 * C) + 16 * (c ^ swz(q)); }
+  __device__ static __forceinline__ int fill(int f, int u) {
+    const int px = u / CPX, c = u - px * CPX;
+    const int ih = px / W, iw = px - ih * W;
+    const int q = pix(f, ih, iw);
+    return q * (2 * C) + 16 * (c ^ swz(q));
+  }
+  struct Lane {
+    int f, ih, iw;
+    bool ok;
+  };
+  __device__ static __forceinline__ Lane lane(int f, int pp, bool ok) {
+    const int oh = pp / OW, ow = pp - oh * OW;
+    return Lane{f, oh * S, ow * S, ok};
+  }
+  struct Stage {
+    int base, x;  // pixel byte base (-1: padding), chunk swizzle
+  };
+  __device__ static __forceinline__ Stage stage(const Lane& l, int k0) {
+    const int tap = k0 / C;  // wave-uniform
+    const int kh = tap / KW, kw = tap - kh * KW;
+    const int ih = l.ih + dh(kh), iw = l.iw + dw(kw);
+    const bool in = l.ok && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+    const int q = pix(l.f, ih, iw);
+    return Stage{in ? q * (2 * C) : -1, swz(q)};
+  }
+  __device__ static __forceinline__ int unit(const Stage& st, const Lane&, int k0, int s, int h) {
+    const int c = ((k0 % C) >> 3) + 2 * s + h;
+    return st.base >= 0 ? st.base + 16 * (c ^ st.x) : -1;
+  }
+};
+
+// Pixel-pair images for a 4-channel input (conv1 over the bf16 frames, one plane): a 16-B
+// unit is two horizontally adjacent pixels x 4 channels, which is exactly the 8 k of one
+// MFMA lane (k = (kh, kw, c): kw even, kw + 1).  A 32-k stage is one kernel row kh
+// (KW * CI = 32).  LDS layout: unit (ih, pw) (pw = iw / 2) at (frame * IH + ih) * PAIRS +
+// col, col = the even pairs then the odd ones, so stride-S output columns read consecutive
+// units (conflict-free ds_read_b128 lane groups).
+template <class G>
+struct ImgGeomPairs {
+  static constexpr int H = G::IH, W = G::IW;
+  static constexpr int OW = G::OW, OPIX = G::OPIX;
+  static constexpr int PAIRS = W / 2, HALF = (PAIRS + 1) / 2;
+  static constexpr int UNITS = H * PAIRS, IMG = UNITS * 16;
+  static_assert(G::CI == 4 && G::KW * G::CI == 32, "4 channels, one kernel row per stage");
+  static_assert(W % 2 == 0 && G::S % 2 == 0 && G::PL % 2 == 0, "pairs never straddle the border");
+  __device__ static __forceinline__ int col(int pw) { return (pw & 1) * HALF + (pw >> 1); }
+  __device__ static __forceinline__ int fill(int f, int u) {
+    const int ih = u / PAIRS, pw = u - ih * PAIRS;
+    return ((f * H + ih) * PAIRS + col(pw)) * 16;
+  }
+  struct Lane {
+    int f, ih, iw;
+    bool ok;
+  };
+  __device__ static __forceinline__ Lane lane(int f, int pp, bool ok) {
+    const int oh = pp / OW, ow = pp - oh * OW;
+    return Lane{f, oh * G::S - G::PT, ow * G::S - G::PL, ok};
+  }
+  struct Stage {
+    int base;  // image row byte base (-1: padding row)
+  };
+  __device__ static __forceinline__ Stage stage(const Lane& l, int k0) {
+    const int ih = l.ih + k0 / 32;
+    const bool in = l.ok && (unsigned)ih < (unsigned)H;
+    return Stage{in ? (l.f * H + ih) * PAIRS * 16 : -1};
+  }
+  __device__ static __forceinline__ int unit(const Stage& st, const Lane& l, int, int s, int h) {
+    const int iw = l.iw + 4 * s + 2 * h;  // kw = (16 s + 8 h) / 4
+    return st.base >= 0 && (unsigned)iw < (unsigned)W ? st.base + col(iw >> 1) * 16 : -1;
+  }
 };
 
 template <class GI, int FPB, int BN, int WM, int WN, int MT, class P>
@@ -64,8 +140,9 @@ struct P3ICfg {
   static_assert(TN % 32 == 0, "wave panel of whole 32-column MFMA tiles");
   using Core = P3Core<BM, BN, WM, WN, BK, P>;
   using PB = typename Core::PB;
-  static constexpr int PLANE = FPB * GI::IPIX * 2 * GI::C + 16;  // + the zero unit
-  static constexpr int IMG = 3 * PLANE;
+  static constexpr int NPA = P::A_PLANES;
+  static constexpr int PLANE = FPB * GI::IMG + 16;  // + the zero unit
+  static constexpr int IMG = NPA * PLANE;
   static constexpr int STAGE_B = PB::BYTES;
   static constexpr int MAIN = IMG + 2 * STAGE_B;
   static constexpr int LDS = MAIN > Core::EPI_BYTES ? MAIN : Core::EPI_BYTES;
@@ -77,9 +154,9 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
   using C = typename Cfg::Core;
   using PB = typename Cfg::PB;
   constexpr int NT = Cfg::NT, NTL = Cfg::NTL, TN = Cfg::TN, BK = Cfg::BK, KS = Cfg::KS;
-  constexpr int PLANE = Cfg::PLANE;
-  static_assert(P::A_MODE == KCONTIG && P::A_PLANES == 3 && P::B_PLANES == 3,
-                "three-plane operands, k-contiguous A");
+  constexpr int PLANE = Cfg::PLANE, NPA = Cfg::NPA;
+  static_assert(P::A_MODE == KCONTIG && (NPA == 1 || NPA == 3) && P::B_PLANES == 3,
+                "k-contiguous A (one or three planes), three-plane B");
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
   const int tid = threadIdx.x;
@@ -136,21 +213,21 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
 
   // ---- A: the block's frames, each 16-B unit of each plane loaded and stored once.
   {
-    constexpr int UNITS = FPB * GI::IPIX * GI::CPX;
+    constexpr int UNITS = FPB * GI::UNITS;
     constexpr int PER = (UNITS + NT - 1) / NT;
-    __amdgpu_buffer_rsrc_t srcA[3];
+    __amdgpu_buffer_rsrc_t srcA[NPA];
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl) srcA[pl] = plane_rsrc(p.a_src, pl);
-    u32x4 v[PER][3];
+    for (int pl = 0; pl < NPA; ++pl) srcA[pl] = plane_rsrc(p.a_src, pl);
+    u32x4 v[PER][NPA];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const int u = tid + j * NT;
-      const int f = u / (GI::IPIX * GI::CPX);
+      const int f = u / GI::UNITS;
       const bool ok = u < UNITS && f < nf;
-      // Units are HBM-linear over the block's frames: byte (f0 * IPIX * CPX + u) * 16.
-      const uint32_t off = ok ? (uint32_t)(((int64_t)f0 * GI::IPIX * GI::CPX + u) * 16) : kOOB;
+      // Units are HBM-linear over the block's frames: byte (f0 * UNITS + u) * 16.
+      const uint32_t off = ok ? (uint32_t)(((int64_t)f0 * GI::UNITS + u) * 16) : kOOB;
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
+      for (int pl = 0; pl < NPA; ++pl)
         v[j][pl] =
             __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srcA[pl], off, 0, 0));
     }
@@ -158,31 +235,24 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
     for (int j = 0; j < PER; ++j) {
       const int u = tid + j * NT;
       if (UNITS % NT == 0 || u < UNITS) {
-        const int f = u / (GI::IPIX * GI::CPX);
-        const int r = u - f * (GI::IPIX * GI::CPX);
-        const int px = r / GI::CPX, c = r - px * GI::CPX;
-        const int ih = px / GI::W, iw = px - ih * GI::W;
-        const int a = GI::addr(GI::pix(f, ih, iw), c);
+        const int f = u / GI::UNITS;
+        const int a = GI::fill(f, u - f * GI::UNITS);
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<u32x4*>(smem + pl * PLANE + a) = v[j][pl];
+        for (int pl = 0; pl < NPA; ++pl)
+          *reinterpret_cast<u32x4*>(smem + pl * PLANE + a) = v[j][pl];
       }
     }
-    if (tid < 3) *reinterpret_cast<u32x4*>(smem + tid * PLANE + PLANE - 16) = zero_u4();
+    if (tid < NPA) *reinterpret_cast<u32x4*>(smem + tid * PLANE + PLANE - 16) = zero_u4();
   }
   stash_b(S0{}, 0);
 
   // ---- This lane's GEMM rows (one per 32-row block of the wave's tile).
-  int ihs[MT], iws[MT], frs[MT];
-  bool rok[MT];
+  typename GI::Lane ln[MT];
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
     const int lr = wm * 32 * MT + i * 32 + (lane & 31);
-    const int f = lr / GI::OPIX, pp = lr - f * GI::OPIX;
-    const int oh = pp / GI::OW, ow = pp - oh * GI::OW;
-    rok[i] = lr < rows;
-    ihs[i] = oh * GI::S;
-    iws[i] = ow * GI::S;
-    frs[i] = f;
+    const int f = lr / GI::OPIX;
+    ln[i] = GI::lane(f, lr - f * GI::OPIX, lr < rows);
   }
   __syncthreads();
 
@@ -196,19 +266,9 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
 
   auto compute = [&](int k0, int buf) {
     const uint8_t* sb = smem + Cfg::IMG + buf * Cfg::STAGE_B;
-    const int tap = k0 / GI::C;  // wave-uniform: a stage never crosses a tap
-    const int kh = tap / GI::KW, kw = tap - kh * GI::KW;
-    const int dh = GI::dh(kh), dw = GI::dw(kw);
-    const int cb = (k0 - tap * GI::C) >> 3;
-    int qb[MT], qs[MT];  // this stage's pixel byte base (-1: padding) and chunk swizzle
+    typename GI::Stage sg[MT];
 #pragma unroll
-    for (int i = 0; i < MT; ++i) {
-      const int ih = ihs[i] + dh, iw = iws[i] + dw;
-      const bool in = rok[i] && (unsigned)ih < (unsigned)GI::H && (unsigned)iw < (unsigned)GI::W;
-      const int q = GI::pix(frs[i], ih, iw);
-      qb[i] = in ? q * (2 * GI::C) : -1;
-      qs[i] = GI::swz(q);
-    }
+    for (int i = 0; i < MT; ++i) sg[i] = GI::stage(ln[i], k0);
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       bf16x8 fb[NTL][3];
@@ -216,22 +276,27 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
       for (int j = 0; j < NTL; ++j)
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl) fb[j][pl] = PB::frag(sb, pl, wn * TN + j * 32, s, lane);
-      const int c = cb + 2 * s + (lane >> 5);
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
-        const int a = qb[i] >= 0 ? qb[i] + 16 * (c ^ qs[i]) : PLANE - 16;
-        bf16x8 fa[3];
+        const int u = GI::unit(sg[i], ln[i], k0, s, lane >> 5);
+        const int a = u >= 0 ? u : PLANE - 16;
+        bf16x8 fa[NPA];
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
+        for (int pl = 0; pl < NPA; ++pl)
           fa[pl] = *reinterpret_cast<const bf16x8*>(smem + pl * PLANE + a);
 #pragma unroll
         for (int j = 0; j < NTL; ++j) {
           // Smallest terms first, as gemm_p3.h.
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[j][1], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[j][0], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[j][2], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[j][0], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[j][1], acc[i][j], 0, 0, 0);
+          if constexpr (NPA == 3) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[j][1], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[j][0], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[j][2], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[j][0], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[j][1], acc[i][j], 0, 0, 0);
+          } else {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[j][2], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[j][1], acc[i][j], 0, 0, 0);
+          }
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[j][0], acc[i][j], 0, 0, 0);
         }
       }
