@@ -89,24 +89,27 @@ struct ImgGeom {
   }
 };
 
-// Pixel-pair images for a 4-channel input (conv1 over the bf16 frames, one plane): a 16-B
-// unit is two horizontally adjacent pixels x 4 channels, which is exactly the 8 k of one
-// MFMA lane (k = (kh, kw, c): kw even, kw + 1).  A 32-k stage is one kernel row kh
-// (KW * CI = 32).  LDS layout: unit (ih, pw) (pw = iw / 2) at (frame * IH + ih) * PAIRS +
-// col, col = the even pairs then the odd ones, so stride-S output columns read consecutive
-// units (conflict-free ds_read_b128 lane groups).
-template <class G>
+// Pixel-pair images for a 4-channel input (conv1 over the frames, one plane): a unit is two
+// horizontally adjacent pixels x 4 channels, which is exactly the 8 k of one MFMA lane
+// (k = (kh, kw, c): kw even, kw + 1) -- 16 B of the bf16 frame copy, or (U8) the 8 raw
+// uint8 bytes, widened to exact bf16 in registers after the LDS read.  A 32-k stage is one
+// kernel row kh (KW * CI = 32).  LDS layout: unit (ih, pw) (pw = iw / 2) at (frame * IH +
+// ih) * PAIRS + col, col = the even pairs then the odd ones, so stride-S output columns
+// read consecutive units (conflict-free ds_read_b128 / ds_read_b64 lane groups).
+template <class G, bool U8_ = false>
 struct ImgGeomPairs {
+  static constexpr bool U8 = U8_;
+  static constexpr int UNIT = U8 ? 8 : 16;  // bytes per unit, in HBM and in LDS
   static constexpr int H = G::IH, W = G::IW;
   static constexpr int OW = G::OW, OPIX = G::OPIX;
   static constexpr int PAIRS = W / 2, HALF = (PAIRS + 1) / 2;
-  static constexpr int UNITS = H * PAIRS, IMG = UNITS * 16;
+  static constexpr int UNITS = H * PAIRS, IMG = UNITS * UNIT;
   static_assert(G::CI == 4 && G::KW * G::CI == 32, "4 channels, one kernel row per stage");
   static_assert(W % 2 == 0 && G::S % 2 == 0 && G::PL % 2 == 0, "pairs never straddle the border");
   __device__ static __forceinline__ int col(int pw) { return (pw & 1) * HALF + (pw >> 1); }
   __device__ static __forceinline__ int fill(int f, int u) {
     const int ih = u / PAIRS, pw = u - ih * PAIRS;
-    return ((f * H + ih) * PAIRS + col(pw)) * 16;
+    return ((f * H + ih) * PAIRS + col(pw)) * UNIT;
   }
   struct Lane {
     int f, ih, iw;
@@ -122,12 +125,24 @@ struct ImgGeomPairs {
   __device__ static __forceinline__ Stage stage(const Lane& l, int k0) {
     const int ih = l.ih + k0 / 32;
     const bool in = l.ok && (unsigned)ih < (unsigned)H;
-    return Stage{in ? (l.f * H + ih) * PAIRS * 16 : -1};
+    return Stage{in ? (l.f * H + ih) * PAIRS * UNIT : -1};
   }
   __device__ static __forceinline__ int unit(const Stage& st, const Lane& l, int, int s, int h) {
     const int iw = l.iw + 4 * s + 2 * h;  // kw = (16 s + 8 h) / 4
-    return st.base >= 0 && (unsigned)iw < (unsigned)W ? st.base + col(iw >> 1) * 16 : -1;
+    return st.base >= 0 && (unsigned)iw < (unsigned)W ? st.base + col(iw >> 1) * UNIT : -1;
   }
+};
+
+// Unit size and element type of a geometry (16-B bf16 units unless it says otherwise).
+template <class GI, class = void>
+struct ImgUnit {
+  static constexpr int BYTES = 16;
+  static constexpr bool U8 = false;
+};
+template <class GI>
+struct ImgUnit<GI, decltype(void(GI::UNIT))> {
+  static constexpr int BYTES = GI::UNIT;
+  static constexpr bool U8 = GI::U8;
 };
 
 template <class GI, int FPB, int BN, int WM, int WN, int MT, class P>
@@ -211,25 +226,31 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
   fetch_b(S0{}, 0);
   fetch_b(S1{}, BK);
 
-  // ---- A: the block's frames, each 16-B unit of each plane loaded and stored once.
+  // ---- A: the block's frames, each unit of each plane loaded and stored once.
+  constexpr int UB = ImgUnit<GI>::BYTES;
+  using u32x2 = __attribute__((ext_vector_type(2))) uint32_t;
+  using UT = std::conditional_t<UB == 8, u32x2, u32x4>;
   {
     constexpr int UNITS = FPB * GI::UNITS;
     constexpr int PER = (UNITS + NT - 1) / NT;
     __amdgpu_buffer_rsrc_t srcA[NPA];
 #pragma unroll
     for (int pl = 0; pl < NPA; ++pl) srcA[pl] = plane_rsrc(p.a_src, pl);
-    u32x4 v[PER][NPA];
+    UT v[PER][NPA];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const int u = tid + j * NT;
       const int f = u / GI::UNITS;
       const bool ok = u < UNITS && f < nf;
-      // Units are HBM-linear over the block's frames: byte (f0 * UNITS + u) * 16.
-      const uint32_t off = ok ? (uint32_t)(((int64_t)f0 * GI::UNITS + u) * 16) : kOOB;
+      // Units are HBM-linear over the block's frames: byte (f0 * UNITS + u) * UB.
+      const uint32_t off = ok ? (uint32_t)(((int64_t)f0 * GI::UNITS + u) * UB) : kOOB;
 #pragma unroll
-      for (int pl = 0; pl < NPA; ++pl)
-        v[j][pl] =
-            __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srcA[pl], off, 0, 0));
+      for (int pl = 0; pl < NPA; ++pl) {
+        if constexpr (UB == 8)
+          v[j][pl] = __builtin_bit_cast(UT, __builtin_amdgcn_raw_buffer_load_b64(srcA[pl], off, 0, 0));
+        else
+          v[j][pl] = __builtin_bit_cast(UT, __builtin_amdgcn_raw_buffer_load_b128(srcA[pl], off, 0, 0));
+      }
     }
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
@@ -238,8 +259,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
         const int f = u / GI::UNITS;
         const int a = GI::fill(f, u - f * GI::UNITS);
 #pragma unroll
-        for (int pl = 0; pl < NPA; ++pl)
-          *reinterpret_cast<u32x4*>(smem + pl * PLANE + a) = v[j][pl];
+        for (int pl = 0; pl < NPA; ++pl) *reinterpret_cast<UT*>(smem + pl * PLANE + a) = v[j][pl];
       }
     }
     if (tid < NPA) *reinterpret_cast<u32x4*>(smem + tid * PLANE + PLANE - 16) = zero_u4();
@@ -281,9 +301,15 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
         const int u = GI::unit(sg[i], ln[i], k0, s, lane >> 5);
         const int a = u >= 0 ? u : PLANE - 16;
         bf16x8 fa[NPA];
+        if constexpr (ImgUnit<GI>::U8) {  // 8 uint8 values -> 8 exact bf16 (gemm_p3.h kAU8)
+          const u32x2 w = *reinterpret_cast<const u32x2*>(smem + a);
+          fa[0] = __builtin_bit_cast(bf16x8, u32x4{u8pair_bf16(w[0], 0), u8pair_bf16(w[0], 2),
+                                                   u8pair_bf16(w[1], 0), u8pair_bf16(w[1], 2)});
+        } else {
 #pragma unroll
-        for (int pl = 0; pl < NPA; ++pl)
-          fa[pl] = *reinterpret_cast<const bf16x8*>(smem + pl * PLANE + a);
+          for (int pl = 0; pl < NPA; ++pl)
+            fa[pl] = *reinterpret_cast<const bf16x8*>(smem + pl * PLANE + a);
+        }
 #pragma unroll
         for (int j = 0; j < NTL; ++j) {
           // Smallest terms first, as gemm_p3.h.

@@ -194,6 +194,7 @@ int wsplits(const char* key, int def) {
 // Image-resident convolution (gemm_p3i.h): FPB frames per block, WM x WN waves of 32*MT
 // rows; `frames` images.
 using I1F = gemm::ImgGeomPairs<G1>;
+using I1U = gemm::ImgGeomPairs<G1, true>;
 using I2F = gemm::ImgGeom<G2, false>;
 using I3F = gemm::ImgGeom<G3, false>;
 using I3D = gemm::ImgGeom<G3, true>;
@@ -242,7 +243,12 @@ int forward_p3(const PWeights& w, const Frames& frames, int rows, const PActs& a
     p.M = rows * G1::OPIX; p.N = G1::CO; p.K = G1::K; p.k_chunk = G1::K;
     p.a_src = frames_src(frames, rows); p.b_src = src(w.w1, G1::K * G1::CO);
     p.bias = w.b1; p.y = pl(a.x1);
-    P3D_GEMM("conv1_fwd", 32, 2, 4, 32, p);
+    switch (tune_variant("P3C1U")) {
+      case 7: P3D_GEMM("conv1_fwd", 32, 2, 4, 32, p); break;  // direct A from HBM
+      case 14: P3I_GEMM("conv1_fwd", I1U, 1, 32, 14, 1, 1, p, rows); break;
+      // Image-resident uint8 frames (28 KB of LDS per frame).
+      default: P3I_GEMM("conv1_fwd", I1U, 1, 32, 7, 1, 2, p, rows); break;
+    }
   } else {
     P3ConvFwd<G1, 1> p;
     p.M = rows * G1::OPIX; p.N = G1::CO; p.K = G1::K; p.k_chunk = G1::K;

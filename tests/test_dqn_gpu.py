@@ -226,12 +226,16 @@ def test_fused_step_equals_staged_step_bitwise():
         assert a.loss.item() == b.loss.item()
 
 
-def test_adjacent_uint8_frames_path_bitwise():
+@pytest.mark.parametrize("u8_kernel", [0, 7, 14])
+def test_adjacent_uint8_frames_path_bitwise(u8_kernel):
     """When o_t directly follows o_tm1 in memory (the GPU dataset's layout) conv1 reads the
-    uint8 frames themselves (no bf16 copy); results are bit-identical to the copy path."""
+    uint8 frames themselves (no bf16 copy); results are bit-identical to the copy path
+    (image-resident uint8 kernel by default, 7: direct-A loads, 14: 14-wave image blocks)."""
     from acme_amd.networks import DQNAtariNetwork
     from acme_amd._lib import lib
     lib().acme_tune_set(b"U8F", 2)
+    lib().acme_tune_set(b"P3C1U", u8_kernel)
+    lib().acme_tune_set(b"P3C1F", 0 if u8_kernel != 7 else 7)
     net = DQNAtariNetwork(18)
     B = 24
     p0, t0 = net.init(3), net.init(4)
@@ -254,3 +258,5 @@ def test_adjacent_uint8_frames_path_bitwise():
             for k in ga:
                 np.testing.assert_array_equal(ga[k], gb[k], err_msg=f"{buf}/{k}")
     lib().acme_tune_set(b"U8F", 0)
+    lib().acme_tune_set(b"P3C1U", 0)
+    lib().acme_tune_set(b"P3C1F", 0)
