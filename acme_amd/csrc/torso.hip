@@ -332,13 +332,14 @@ int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int row
   // Weight gradients of conv3 and conv2 go to the side stream (when given): each only
   // waits for its layer's dZ, and runs beside the next input gradient on the main stream.
   const bool fork = sd.side != nullptr;
+  // Two forks (default): conv3_wgrad beside conv3_dgrad, conv2_wgrad beside conv2_dgrad.
+  // ACME_V_BWF=1: one fork after conv3_dgrad (both weight gradients beside conv2_dgrad +
+  // conv1_wgrad) saves an event record on the main stream (~7 us of main-stream idle each,
+  // rocprofv3 trace) but measured 0.754 -> 0.767 ms per step: the lost overlap costs more.
+  const bool two_forks = fork && tune_variant("BWF") != 1;
   hipStream_t st = fork ? sd.side : st_main;
   float* wslab = fork ? sd.slab : slab;
-  if (fork) {
-    ACME_HIP_TRY(hipEventRecord(sd.e[0], st_main));
-    ACME_HIP_TRY(hipStreamWaitEvent(sd.side, sd.e[0], 0));
-  }
-  {  // conv3 weight + bias gradient
+  auto conv3_wgrad = [&](hipStream_t st) -> int {  // conv3 weight + bias gradient
     P3ConvWgrad<G3, 3> p;
     p.M = G3::K; p.N = G3::CO; p.K = rows * G3::OPIX;
     const int splits = wsplits("P3C3WS", kP3Conv3WgradSplits);
@@ -348,8 +349,14 @@ int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int row
     if (tune_variant("P3C3W") == 9) P3P_GEMM("conv3_wgrad", 128, 64, 2, 2, p, splits);
     else if (tune_variant("P3C3W") == 1) P3G_GEMM("conv3_wgrad", 128, 64, 2, 2, 32, 3, p, splits);
     else P3_GEMM("conv3_wgrad", 128, 64, 2, 2, 32, p, splits);
-    if ((rc = p3_wgrad_reduce(p, splits, wslab, g.w3, g.b3, "conv3_wgrad_reduce", st)))
-      return rc;
+    return p3_wgrad_reduce(p, splits, wslab, g.w3, g.b3, "conv3_wgrad_reduce", st);
+  };
+  if (two_forks) {
+    ACME_HIP_TRY(hipEventRecord(sd.e[0], st_main));
+    ACME_HIP_TRY(hipStreamWaitEvent(sd.side, sd.e[0], 0));
+    if ((rc = conv3_wgrad(sd.side))) return rc;
+  } else if (!fork) {
+    if ((rc = conv3_wgrad(st_main))) return rc;
   }
   st = st_main;
   {
@@ -377,6 +384,7 @@ int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int row
     ACME_HIP_TRY(hipEventRecord(sd.e[1], st_main));
     ACME_HIP_TRY(hipStreamWaitEvent(sd.side, sd.e[1], 0));
     st = sd.side;
+    if (!two_forks && (rc = conv3_wgrad(sd.side))) return rc;
   }
   {  // conv2
     P3ConvWgrad<G2, 3> p;
