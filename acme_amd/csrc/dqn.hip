@@ -341,7 +341,7 @@ int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const torso:
     const int sv = tune("P3FCS");
     const int fv = tune("P3FCF");
     int splits = sv > 0 && sv <= kFcFwdMaxSplits ? sv : (rows > 512 ? 4 : kFcFwdSplits);
-    if (sv <= 0 && fv == 6) splits = rows > 512 ? 8 : 16;   // 256x128 tiles
+    if (sv <= 0 && (fv == 6 || fv == 13 || fv == 14)) splits = rows > 512 ? 8 : 16;  // 256x128
     if (sv <= 0 && fv == 7) splits = rows > 512 ? 16 : 32;  // 256x256 tiles
     p.M = rows; p.N = 2 * kHidden; p.K = kFlat; p.k_chunk = chunk_for(kFlat, splits);
     p.a_src = SRC(x3, (int64_t)rows * kFlat); p.ldx = kFlat;
@@ -359,6 +359,8 @@ int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const torso:
       case 10: ACME_P3D_GEMM("fc_fwd", 128, 2, 4, 32, p, splits); break;
       case 11: ACME_P3D_GEMM("fc_fwd", 64, 1, 4, 32, p, splits); break;
       case 12: ACME_P3D_GEMM("fc_fwd", 128, 1, 8, 32, p, splits); break;
+      case 13: ACME_P3_GEMM("fc_fwd", 256, 128, 4, 2, 32, p, splits); break;
+      case 14: ACME_P3_GEMM("fc_fwd", 128, 256, 2, 4, 32, p, splits); break;
       default: ACME_P3_GEMM("fc_fwd", 128, 128, 2, 2, 32, p, splits); break;
     }
     ACME_PROF("fc_head_fwd", st, 0.0, 4.0 * (double)rows * 2 * kHidden * (splits + 1));
