@@ -102,6 +102,10 @@ struct acme_dqn {
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   float* side_slab = nullptr;
   torso::Plane x1p{}, x2p{}, x3p{}, t1p{}, t2p{}, t3p{}, dzhp{}, dz3p{}, dz2p{}, dz1p{};
+  // Plane path: the loss is launched together with the head dZ (launch_dqn_loss_head_dz)
+  // by the backward; forward_backward_stage leaves its arguments here.
+  LossArgs pending_la{};
+  bool loss_pending = false;
 };
 
 namespace {
@@ -423,7 +427,13 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st_main,
   const int A = l->cfg.num_actions;
   const bool p3 = use_p3(l);
   int rc;
-  {  // Head: dZ of the fused hidden layer (masked by its ReLU).
+  if (p3 && l->loss_pending) {  // the loss and the head dZ planes, one launch
+    l->loss_pending = false;
+    ACME_PROF("loss_head_dz", st, 0.0, 0.0);
+    rc = launch_dqn_loss_head_dz(l->pending_la, l->hid, kHidden, P(l, prm, l->t_vw),
+                                 P(l, prm, l->t_aw), l->dzhp.p, l->dzhp.stride, st);
+    if (rc != ACME_OK) return rc;
+  } else {  // Head: dZ of the fused hidden layer (masked by its ReLU).
     ACME_PROF("head_dz", st, 0.0, 0.0);
     rc = p3 ? launch_head_dz_planes(l->hid, l->g, l->a_cache, B, kHidden, A, P(l, prm, l->t_vw),
                                     P(l, prm, l->t_aw), l->dzhp.p, l->dzhp.stride, st)
@@ -936,7 +946,10 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
   la.prio = prio;
   la.g = l->g;
   la.a_cache = l->a_cache;
-  {
+  if (l->last_p3 && tune("LHDZ") != 1) {  // fused with the head dZ (nature_backward)
+    l->pending_la = la;
+    l->loss_pending = true;
+  } else {
     ACME_PROF("loss", st, 0.0, 0.0);
     if ((rc = launch_dqn_loss(la, st)) != ACME_OK) return rc;
   }

@@ -60,6 +60,10 @@ struct LossArgs {
 // trfl.double_qlearning + losses.huber + importance weighting + mean
 // (acme/agents/tf/dqn/learning.py:128-144, acme/tf/losses/huber.py:45-57).
 int launch_dqn_loss(const LossArgs& args, hipStream_t st);
+// The loss fused with the duelling head's dZ planes (as launch_head_dz_planes, from the
+// hidden activations h [B][2H]): one launch, the same bits as the two kernels.
+int launch_dqn_loss_head_dz(const LossArgs& args, const float* h, int H, const float* wv,
+                            const float* wa, uint16_t* planes, int64_t pstride, hipStream_t st);
 
 // Deterministic split-K reduction: e in [0, count): v = sum_s slab[s * count + e] (fixed
 // order), optionally + bias[e % ncols] and ReLU; written to out0[e] for e < split_at and

@@ -101,6 +101,41 @@ __global__ void onehot_dq_kernel(const float* __restrict__ g, const int32_t* __r
 
 constexpr int kLossThreads = 1024;
 
+// One transition of the loss: reward clip, discount, double-Q target, TD, Huber, f64
+// importance weight; shared by the loss kernel and the fused loss + head dZ kernel so both
+// produce the same bits.
+struct LossRow {
+  float g, td, hub_w;
+};
+__device__ __forceinline__ LossRow loss_row(const LossArgs& p, int b, double wmax) {
+  const int B = p.B, A = p.A;
+  const float* qt = p.q_on + (size_t)b * A;
+  const float* qs = p.q_on + (size_t)(B + b) * A;
+  const float* qv = p.q_tg + (size_t)b * A;
+  int best = 0;  // tf.argmax: first maximal index
+  float bq = qs[0];
+  for (int j = 1; j < A; ++j)
+    if (qs[j] > bq) {
+      bq = qs[j];
+      best = j;
+    }
+  float r = p.r[b];
+  r = fminf(fmaxf(r, -p.max_abs_reward), p.max_abs_reward);
+  const float dg = __fmul_rn(p.d[b], p.discount);
+  const float target = __fadd_rn(r, __fmul_rn(dg, qv[best]));
+  const int ab = p.a[b];
+  const float td = __fsub_rn(target, qt[ab]);
+  const float ax = fabsf(td);
+  const float quad = fminf(ax, p.delta);
+  const float lin = ax - quad;
+  const float hub = __fadd_rn(__fmul_rn(0.5f, __fmul_rn(quad, quad)), __fmul_rn(p.delta, lin));
+  const double w = pow(1.0 / p.probs[b], (double)p.beta) / wmax;
+  const float wf = (float)w;
+  const float dtd = fminf(fmaxf(td, -p.delta), p.delta);  // d huber / d td
+  const float inv_b = 1.f / (float)B;
+  return LossRow{-(inv_b * wf * dtd), td, hub * wf};
+}
+
 __global__ void __launch_bounds__(kLossThreads) dqn_loss_kernel(LossArgs p) {
   __shared__ double red[kLossThreads / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -122,37 +157,14 @@ __global__ void __launch_bounds__(kLossThreads) dqn_loss_kernel(LossArgs p) {
   pmin = p.global_min_prob ? *p.global_min_prob : red[0];
   __syncthreads();
   const double wmax = pow(1.0 / pmin, (double)p.beta);
-  const float inv_b = 1.f / (float)B;
   double lsum = 0.0;
   for (int b = tid; b < B; b += blockDim.x) {
-    const float* qt = p.q_on + (size_t)b * A;
-    const float* qs = p.q_on + (size_t)(B + b) * A;
-    const float* qv = p.q_tg + (size_t)b * A;
-    int best = 0;  // tf.argmax: first maximal index
-    float bq = qs[0];
-    for (int j = 1; j < A; ++j)
-      if (qs[j] > bq) {
-        bq = qs[j];
-        best = j;
-      }
-    float r = p.r[b];
-    r = fminf(fmaxf(r, -p.max_abs_reward), p.max_abs_reward);
-    const float dg = __fmul_rn(p.d[b], p.discount);
-    const float target = __fadd_rn(r, __fmul_rn(dg, qv[best]));
-    const int ab = p.a[b];
-    const float td = __fsub_rn(target, qt[ab]);
-    const float ax = fabsf(td);
-    const float quad = fminf(ax, p.delta);
-    const float lin = ax - quad;
-    const float hub = __fadd_rn(__fmul_rn(0.5f, __fmul_rn(quad, quad)), __fmul_rn(p.delta, lin));
-    const double w = pow(1.0 / p.probs[b], (double)p.beta) / wmax;
-    const float wf = (float)w;
-    lsum += (double)(hub * wf);
-    const float dtd = fminf(fmaxf(td, -p.delta), p.delta);  // d huber / d td
-    p.g[b] = -(inv_b * wf * dtd);
-    p.td[b] = td;
-    p.prio[b] = (double)ax;
-    p.a_cache[b] = ab;
+    const LossRow row = loss_row(p, b, wmax);
+    lsum += (double)row.hub_w;
+    p.g[b] = row.g;
+    p.td[b] = row.td;
+    p.prio[b] = (double)fabsf(row.td);
+    p.a_cache[b] = p.a[b];
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) lsum += __shfl_xor(lsum, o, 64);
@@ -375,6 +387,91 @@ __global__ void __launch_bounds__(256) fc_head_forward_kernel(
       for (int jj = 0; jj < A; ++jj) q[(size_t)row * A + jj] = d[A] + (d[jj] - mean);
     }
   }
+}
+
+// Loss + head dZ in one launch (plane path).  Blocks [0, nb) each write the dZ planes of
+// 256 / (2H / 8) rows (8 units per thread, as head_dz_planes_kernel), recomputing g_b of
+// their rows with loss_row (the loss kernel's bits); the last block is the loss kernel
+// (loss, TD errors, priorities, g and the action cache of every row).  Saves the loss
+// launch and its dependency on the critical path.
+__global__ void __launch_bounds__(256) dqn_loss_head_dz_kernel(
+    LossArgs p, const float* __restrict__ h, int H, const float* __restrict__ wv,
+    const float* __restrict__ wa, uint16_t* __restrict__ planes, int64_t pstride) {
+  __shared__ double red[4];
+  __shared__ float gs[8];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int B = p.B, A = p.A;
+  // Importance-weight normaliser: max_b (1/p_b)^beta = (1/min_b p_b)^beta.
+  double pmin = INFINITY;
+  for (int b = tid; b < B; b += 256) pmin = fmin(pmin, p.probs[b]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) pmin = fmin(pmin, __shfl_xor(pmin, o, 64));
+  if (lane == 0) red[wave] = pmin;
+  __syncthreads();
+  pmin = fmin(fmin(red[0], red[1]), fmin(red[2], red[3]));
+  if (p.global_min_prob) pmin = *p.global_min_prob;
+  const double wmax = pow(1.0 / pmin, (double)p.beta);
+  if (blockIdx.x == gridDim.x - 1) {
+    __syncthreads();  // red is reused below
+    double lsum = 0.0;
+    for (int b = tid; b < B; b += 256) {
+      const LossRow row = loss_row(p, b, wmax);
+      lsum += (double)row.hub_w;
+      p.g[b] = row.g;
+      p.td[b] = row.td;
+      p.prio[b] = (double)fabsf(row.td);
+      p.a_cache[b] = p.a[b];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) lsum += __shfl_xor(lsum, o, 64);
+    if (lane == 0) red[wave] = lsum;
+    __syncthreads();
+    if (tid == 0) p.loss[0] = (float)((((red[0] + red[1]) + red[2]) + red[3]) / (double)B);
+    return;
+  }
+  const int per = 2 * H / 8;  // threads per row (divides 256: launch_dqn_loss_head_dz)
+  const int b0 = (int)((int64_t)blockIdx.x * 256 / per);
+  if (tid < 256 / per && b0 + tid < B) gs[tid] = loss_row(p, b0 + tid, wmax).g;
+  __syncthreads();
+  const int64_t t = (int64_t)blockIdx.x * 256 + tid;
+  if (t >= (int64_t)B * per) return;
+  const int b = (int)(t / per), k0 = 8 * (int)(t - (int64_t)b * per);
+  const float gb = gs[b - b0];
+  const int ab = p.a[b];
+  const float inv_a = 1.f / (float)A;
+  const float* hr = h + (size_t)b * 2 * H + k0;
+  const f32x4 h0 = reinterpret_cast<const f32x4*>(hr)[0], h1 = reinterpret_cast<const f32x4*>(hr)[1];
+  const float hv[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+  float d[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = k0 + j;
+    float v;
+    if (k < H) {
+      v = gb * wv[k];
+    } else {
+      const float* row = wa + (size_t)(k - H) * A;
+      float s = 0.f;
+#pragma unroll 6
+      for (int i = 0; i < A; ++i) s = fmaf(gb * ((i == ab ? 1.f : 0.f) - inv_a), row[i], s);
+      v = s;
+    }
+    d[j] = hv[j] > 0.f ? v : 0.f;
+  }
+  uint32_t ph[4], pm[4], pl[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    uint16_t x0, y0, z0, x1, y1, z1;
+    gemm::split3_bits(d[2 * j], x0, y0, z0);
+    gemm::split3_bits(d[2 * j + 1], x1, y1, z1);
+    ph[j] = x0 | ((uint32_t)x1 << 16);
+    pm[j] = y0 | ((uint32_t)y1 << 16);
+    pl[j] = z0 | ((uint32_t)z1 << 16);
+  }
+  const int64_t e = (int64_t)b * 2 * H + k0;
+  *reinterpret_cast<uint4*>(planes + e) = uint4{ph[0], ph[1], ph[2], ph[3]};
+  *reinterpret_cast<uint4*>(planes + pstride + e) = uint4{pm[0], pm[1], pm[2], pm[3]};
+  *reinterpret_cast<uint4*>(planes + 2 * pstride + e) = uint4{pl[0], pl[1], pl[2], pl[3]};
 }
 
 // dZ of the fused hidden layer as planes, 8 consecutive units per thread:
@@ -666,6 +763,17 @@ int launch_fc_head_forward(const float* slab, int splits, int rows, int H, const
   else
     fc_head_forward_kernel<0, 0><<<grid, 256, shmem, st>>>(slab, splits, rows, H, fcb, wv, bv, wa,
                                                             ba, A, hid, q);
+  ACME_LAUNCH_CHECK();
+  return ACME_OK;
+}
+
+int launch_dqn_loss_head_dz(const LossArgs& args, const float* h, int H, const float* wv,
+                            const float* wa, uint16_t* planes, int64_t pstride, hipStream_t st) {
+  ACME_CHECK_ARG(args.B >= 1 && args.A >= 1 && h && wv && wa && planes, "bad loss / head dZ args");
+  const int per = 2 * H / 8;
+  ACME_CHECK_ARG(H % 4 == 0 && per >= 32 && 256 % per == 0, "hidden size %d: 2H/8 must divide 256", H);
+  const int64_t nb = ceil_div((int64_t)args.B * per, 256);
+  dqn_loss_head_dz_kernel<<<(unsigned)(nb + 1), 256, 0, st>>>(args, h, H, wv, wa, planes, pstride);
   ACME_LAUNCH_CHECK();
   return ACME_OK;
 }
