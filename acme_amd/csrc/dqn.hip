@@ -365,6 +365,8 @@ int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const torso:
       case 12: ACME_P3D_GEMM("fc_fwd", 128, 1, 8, 32, p, splits); break;
       case 13: ACME_P3_GEMM("fc_fwd", 256, 128, 4, 2, 32, p, splits); break;
       case 14: ACME_P3_GEMM("fc_fwd", 128, 256, 2, 4, 32, p, splits); break;
+      case 15: ACME_P3_GEMM("fc_fwd", 128, 128, 2, 4, 32, p, splits); break;
+      case 16: ACME_P3_GEMM("fc_fwd", 128, 128, 4, 2, 32, p, splits); break;
       default: ACME_P3_GEMM("fc_fwd", 128, 128, 2, 2, 32, p, splits); break;
     }
     ACME_PROF("fc_head_fwd", st, 0.0, 4.0 * (double)rows * 2 * kHidden * (splits + 1));
@@ -883,29 +885,43 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
   if (l->last_p3) {
     if ((rc = sync_planes(l, st)) != ACME_OK) return rc;
     const uint8_t* o1 = static_cast<const uint8_t*>(batch->o_tm1);
-    // ACME_V_U8F=2: conv1 reads the batch's uint8 frames directly when o_t follows o_tm1.
-    // Faster on one stream (no conversion pass), but measured ~20 us per step slower than
-    // the bf16 copy once the target forward runs on the side stream, so not the default.
-    if (batch->o_t == o1 + (size_t)B * kObsBytes && tune("U8F") == 2) {
-      l->cur_frames = torso::Frames{o1, true};
-    } else {
-      if ((rc = convert_frames(l, batch->o_tm1, batch->o_t, B, 2 * B, st)) != ACME_OK) return rc;
-      l->cur_frames = torso::Frames{l->frames, false};
-    }
-    // Target forward (q_t_value) on the side stream, beside the online forward.
     hipStream_t tst = st;
     hipStream_t side = side_stream(l);
+    // conv1's input.  Default: a bf16 copy of [o_tm1; o_t] on the main stream for everything.
+    // When o_t directly follows o_tm1 (the GPU dataset's layout): ACME_V_U8F=2 reads the
+    // batch's uint8 frames everywhere (no copy); ACME_V_U8F=3 reads them in both forwards
+    // and makes the weight gradient's bf16 copy of o_tm1 only, on the side stream ahead of
+    // the target forward.  Both measured slower beside the side stream (0.746 -> 0.750 ms
+    // per step for 3): the uint8 image kernel is slower there than the bf16 one.
+    const bool adjacent = batch->o_t == o1 + (size_t)B * kObsBytes;
+    const int u8f = tune("U8F");
+    torso::Frames fwd_frames{l->frames, false};
+    bool convert_on_side = false;
+    if (adjacent && u8f == 2) {
+      fwd_frames = l->cur_frames = torso::Frames{o1, true};
+    } else if (adjacent && u8f == 3 && side) {
+      fwd_frames = torso::Frames{o1, true};
+      l->cur_frames = torso::Frames{l->frames, false};
+      convert_on_side = true;
+    } else {
+      if ((rc = convert_frames(l, batch->o_tm1, batch->o_t, B, 2 * B, st)) != ACME_OK) return rc;
+      l->cur_frames = fwd_frames;
+    }
+    // Target forward (q_t_value) on the side stream, beside the online forward.
     if (side) {
       ACME_HIP_TRY(hipEventRecord(l->ev[0], st));
       ACME_HIP_TRY(hipStreamWaitEvent(side, l->ev[0], 0));
       tst = side;
     }
-    if ((rc = nature_forward_p3(l, l->target, l->tpl, l->cur_frames.rows_from(B), B,
+    if (convert_on_side &&
+        (rc = convert_frames(l, batch->o_tm1, batch->o_tm1, B, B, side)) != ACME_OK)
+      return rc;
+    if ((rc = nature_forward_p3(l, l->target, l->tpl, fwd_frames.rows_from(B), B,
                                 l->t1p, l->t2p, l->t3p, l->thid, l->q_tg, tst,
                                 side ? l->side_slab : l->slab)) != ACME_OK)
       return rc;
     if (side) ACME_HIP_TRY(hipEventRecord(l->ev[1], side));
-    if ((rc = nature_forward_p3(l, l->params, l->wpl, l->cur_frames, 2 * B, l->x1p, l->x2p, l->x3p,
+    if ((rc = nature_forward_p3(l, l->params, l->wpl, fwd_frames, 2 * B, l->x1p, l->x2p, l->x3p,
                                 l->hid, l->q_on, st)) != ACME_OK)
       return rc;
     if (side) ACME_HIP_TRY(hipStreamWaitEvent(st, l->ev[1], 0));

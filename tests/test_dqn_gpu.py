@@ -226,14 +226,16 @@ def test_fused_step_equals_staged_step_bitwise():
         assert a.loss.item() == b.loss.item()
 
 
-@pytest.mark.parametrize("u8_kernel", [0, 7, 14])
-def test_adjacent_uint8_frames_path_bitwise(u8_kernel):
-    """When o_t directly follows o_tm1 in memory (the GPU dataset's layout) conv1 reads the
-    uint8 frames themselves (no bf16 copy); results are bit-identical to the copy path
-    (image-resident uint8 kernel by default, 7: direct-A loads, 14: 14-wave image blocks)."""
+@pytest.mark.parametrize("u8f,u8_kernel", [(3, 0), (2, 0), (2, 7), (2, 14)])
+def test_adjacent_uint8_frames_path_bitwise(u8f, u8_kernel):
+    """When o_t directly follows o_tm1 in memory (the GPU dataset's layout) conv1's forwards
+    read the uint8 frames themselves (U8F=3: the weight gradient's bf16 copy of o_tm1 is
+    made on the side stream; U8F=2: no copy at all); results are bit-identical to the copy
+    path of non-adjacent batches (image-resident uint8 kernel by default, 7: direct-A
+    loads, 14: 14-wave image blocks)."""
     from acme_amd.networks import DQNAtariNetwork
     from acme_amd._lib import lib
-    lib().acme_tune_set(b"U8F", 2)
+    lib().acme_tune_set(b"U8F", u8f)
     lib().acme_tune_set(b"P3C1U", u8_kernel)
     lib().acme_tune_set(b"P3C1F", 0 if u8_kernel != 7 else 7)
     net = DQNAtariNetwork(18)
