@@ -267,7 +267,10 @@ __global__ void __launch_bounds__(256) slab_reduce4_kernel(const float* __restri
 // (acme/tf/networks/duelling.py:51-57).  4 rows per 256-thread block: the advantage
 // weights are staged once per block in LDS, each wave finishes one row with lane-parallel
 // partial dot products and a fixed shuffle tree (deterministic).
-constexpr int kHeadRows = 4;
+#ifndef ACME_HEAD_ROWS
+#define ACME_HEAD_ROWS 4
+#endif
+constexpr int kHeadRows = ACME_HEAD_ROWS;
 constexpr int kHeadChunk = 8;  // advantage outputs per accumulation pass
 #ifndef HEAD_EXP
 #define HEAD_EXP 0  // experiments: 1 skip the dot products, 2 skip the slab sum
