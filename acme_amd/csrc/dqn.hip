@@ -639,7 +639,10 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
         (rc = dev_alloc(l, &l->dz1, (int64_t)B * G1::OPIX * G1::CO)))
       return fail(rc);
     l->slab_floats = slab_floats_needed(B, A);
-    if (cfg->obs_dtype == ACME_OBS_U8_SCALED) {
+    // The plane kernels address each operand plane through a buffer descriptor with a
+    // 31-bit byte range: the bf16 frame copy of [o_tm1; o_t] (2B x 56,448 B) bounds the batch
+    // (B <= 19,000); larger batches run the f32 / x6 engines.
+    if (cfg->obs_dtype == ACME_OBS_U8_SCALED && (int64_t)R2 * kObsBytes * 2 < (int64_t)INT32_MAX) {
       l->p3_capable = true;
       const int64_t fl = l->flat;
       if ((rc = dev_alloc(l, &l->wpl, 3 * fl)) || (rc = dev_alloc(l, &l->tpl, 3 * fl)) ||
