@@ -536,6 +536,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p,
                                                    float b2, float omb2, float bc1, float bc2,
                                                    float eps, uint16_t* __restrict__ planes,
                                                    int64_t pstride) {
+#pragma unroll 2
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (int64_t)gridDim.x * blockDim.x) {
     f32x4 gg = reinterpret_cast<const f32x4*>(g)[i];
@@ -834,7 +835,8 @@ int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float l
   const float bc1 = 1.f - powf(b1, (float)t);
   const float bc2 = 1.f - powf(b2, (float)t);
   const int64_t n4 = n / 4;
-  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n4, 256), 2048);
+  const int gcap = tune_variant("ADAMG") > 0 ? tune_variant("ADAMG") : 8192;  // 47.7 -> 45.2 us vs 2048
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n4, 256), gcap);
   adam_kernel<<<std::max(grid, 1u), 256, 0, st>>>(p, g, m, v, n4, lr, b1, 1.f - b1, b2, 1.f - b2,
                                                   bc1, bc2, eps, planes, pstride);
   ACME_LAUNCH_CHECK();
