@@ -96,10 +96,13 @@ struct ImgGeom {
 // kernel row kh (KW * CI = 32).  LDS layout: unit (ih, pw) (pw = iw / 2) at (frame * IH +
 // ih) * PAIRS + col, col = the even pairs then the odd ones, so stride-S output columns
 // read consecutive units (conflict-free ds_read_b128 / ds_read_b64 lane groups).
-template <class G, bool U8_ = false>
+// SRC 0: the bf16 frame copy; 1: the raw uint8 frames, kept as uint8 in LDS (widened per
+// fragment read); 2: the raw uint8 frames, widened to bf16 once while filling the image.
+template <class G, int SRC = 0>
 struct ImgGeomPairs {
-  static constexpr bool U8 = U8_;
-  static constexpr int UNIT = U8 ? 8 : 16;  // bytes per unit, in HBM and in LDS
+  static constexpr bool U8 = SRC == 1;            // fragments widened after the LDS read
+  static constexpr int UNIT = SRC == 1 ? 8 : 16;  // LDS bytes per unit
+  static constexpr int HBM_UNIT = SRC == 0 ? 16 : 8;
   static constexpr int H = G::IH, W = G::IW;
   static constexpr int OW = G::OW, OPIX = G::OPIX;
   static constexpr int PAIRS = W / 2, HALF = (PAIRS + 1) / 2;
@@ -138,11 +141,13 @@ template <class GI, class = void>
 struct ImgUnit {
   static constexpr int BYTES = 16;
   static constexpr bool U8 = false;
+  static constexpr bool WIDEN = false;
 };
 template <class GI>
 struct ImgUnit<GI, decltype(void(GI::UNIT))> {
-  static constexpr int BYTES = GI::UNIT;
+  static constexpr int BYTES = GI::HBM_UNIT;  // HBM bytes per unit
   static constexpr bool U8 = GI::U8;
+  static constexpr bool WIDEN = GI::HBM_UNIT == 8 && GI::UNIT == 16;  // uint8 -> bf16 at fill
 };
 
 template <class GI, int FPB, int BN, int WM, int WN, int MT, class P>
@@ -258,8 +263,15 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
       if (UNITS % NT == 0 || u < UNITS) {
         const int f = u / GI::UNITS;
         const int a = GI::fill(f, u - f * GI::UNITS);
+        if constexpr (ImgUnit<GI>::WIDEN) {  // 8 uint8 values -> 8 exact bf16, stored once
+          const UT w = v[j][0];
+          *reinterpret_cast<u32x4*>(smem + a) =
+              u32x4{u8pair_bf16(w[0], 0), u8pair_bf16(w[0], 2), u8pair_bf16(w[1], 0),
+                    u8pair_bf16(w[1], 2)};
+        } else {
 #pragma unroll
-        for (int pl = 0; pl < NPA; ++pl) *reinterpret_cast<UT*>(smem + pl * PLANE + a) = v[j][pl];
+          for (int pl = 0; pl < NPA; ++pl) *reinterpret_cast<UT*>(smem + pl * PLANE + a) = v[j][pl];
+        }
       }
     }
     if (tid < NPA) *reinterpret_cast<u32x4*>(smem + tid * PLANE + PLANE - 16) = zero_u4();

@@ -195,7 +195,8 @@ int wsplits(const char* key, int def) {
 // Image-resident convolution (gemm_p3i.h): FPB frames per block, WM x WN waves of 32*MT
 // rows; `frames` images.
 using I1F = gemm::ImgGeomPairs<G1>;
-using I1U = gemm::ImgGeomPairs<G1, true>;
+using I1U = gemm::ImgGeomPairs<G1, 1>;
+using I1W = gemm::ImgGeomPairs<G1, 2>;
 using I2F = gemm::ImgGeom<G2, false>;
 using I3F = gemm::ImgGeom<G3, false>;
 using I3D = gemm::ImgGeom<G3, true>;
@@ -247,8 +248,9 @@ int forward_p3(const PWeights& w, const Frames& frames, int rows, const PActs& a
     switch (tune_variant("P3C1U")) {
       case 7: P3D_GEMM("conv1_fwd", 32, 2, 4, 32, p); break;  // direct A from HBM
       case 14: P3I_GEMM("conv1_fwd", I1U, 1, 32, 14, 1, 1, p, rows); break;
-      // Image-resident uint8 frames (28 KB of LDS per frame).
-      default: P3I_GEMM("conv1_fwd", I1U, 1, 32, 7, 1, 2, p, rows); break;
+      case 15: P3I_GEMM("conv1_fwd", I1U, 1, 32, 7, 1, 2, p, rows); break;  // uint8 in LDS
+      // Image-resident frames: uint8 from HBM, widened to bf16 once while filling the LDS.
+      default: P3I_GEMM("conv1_fwd", I1W, 1, 32, 7, 1, 2, p, rows); break;
     }
   } else {
     P3ConvFwd<G1, 1> p;

@@ -226,7 +226,7 @@ def test_fused_step_equals_staged_step_bitwise():
         assert a.loss.item() == b.loss.item()
 
 
-@pytest.mark.parametrize("u8f,u8_kernel", [(3, 0), (2, 0), (2, 7), (2, 14)])
+@pytest.mark.parametrize("u8f,u8_kernel", [(3, 0), (2, 0), (2, 7), (2, 14), (2, 15)])
 def test_adjacent_uint8_frames_path_bitwise(u8f, u8_kernel):
     """When o_t directly follows o_tm1 in memory (the GPU dataset's layout) conv1's forwards
     read the uint8 frames themselves (U8F=3: the weight gradient's bf16 copy of o_tm1 is
