@@ -18,31 +18,34 @@
 namespace acme {
 namespace gemm {
 
-template <class G>
+template <class G, int FPB = 1>
 struct P3SCfg {
   using P = conv::P3ConvDgradSubZ<G>;
   static constexpr int S = G::S, CLASSES = G::S * G::S;
-  static constexpr int MT = 2, NW = 2 * CLASSES, NT = 64 * NW, BK = 32, KS = 2;
+  static constexpr int MT = 2, NW = 2 * CLASSES * FPB, NT = 64 * NW, BK = 32, KS = 2;
   static constexpr int BN = 32;                                // N = CI
   static constexpr int H = G::OH, W = G::OW, C = G::CO;        // the dZ image
   static constexpr int CPX = C / 8;
-  static constexpr int PLANE = H * W * 2 * C + 16;             // + the zero unit
+  static constexpr int FRAME = H * W * 2 * C;                  // one frame's image, one plane
+  static constexpr int PLANE = FPB * FRAME + 16;               // + the zero unit
   static constexpr int IMG = 3 * PLANE;
-  using PB = PlanP3<BN, NT, KCONTIG, 3, BK>;                   // one class's B stage
+  using PB = PlanP3<BN, 64 * 2 * CLASSES, KCONTIG, 3, BK>;     // one class's B stage
   static constexpr int STAGE_B = CLASSES * PB::BYTES;
   static constexpr int MAIN = IMG + 2 * STAGE_B;
   static constexpr int EPI = NW * 32 * (BN + 4) * 4;
   static constexpr int LDS = MAIN > EPI ? MAIN : EPI;
   using Core = P3Core<2 * 32 * MT, BN, 2, 1, BK, P>;           // a class's 2 waves x 64 rows
   static_assert(G::CI == BN && C == 64 && CPX == 8, "conv2 geometry (CI 32, CO 64)");
-  static_assert(PB::UNITS * CLASSES == NT, "one B unit per thread per plane");
+  static constexpr int BT = PB::UNITS * CLASSES;               // B loader threads
+  static_assert(BT == 64 * 2 * CLASSES, "one B unit per loader thread per plane");
   static_assert(P::KR % BK == 0 && (P::KR / BK) % 2 == 0, "whole, even stage count");
   __device__ static __forceinline__ int swz(int q) { return (q >> 1) & (CPX - 1); }
 };
 
-template <class G>
-__global__ void __launch_bounds__(P3SCfg<G>::NT) gemm_p3s_kernel(const conv::P3ConvDgradSubZ<G> p_in) {
-  using Cfg = P3SCfg<G>;
+template <class G, int FPB>
+__global__ void __launch_bounds__(64 * 2 * G::S * G::S * FPB) gemm_p3s_kernel(
+    const conv::P3ConvDgradSubZ<G> p_in, int frames) {
+  using Cfg = P3SCfg<G, FPB>;
   using PB = typename Cfg::PB;
   using C = typename Cfg::Core;
   using P = conv::P3ConvDgradSubZ<G>;
@@ -51,16 +54,19 @@ __global__ void __launch_bounds__(P3SCfg<G>::NT) gemm_p3s_kernel(const conv::P3C
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int f = blockIdx.x;  // the frame
-  const int z = wave >> 1, half = wave & 1;  // this wave's class and its half of the rows
+  const int fi = wave / (2 * Cfg::CLASSES);  // this wave's frame in the block
+  const int f = blockIdx.x * FPB + fi;
+  const int z = (wave >> 1) % Cfg::CLASSES, half = wave & 1;  // its class, half of the rows
+  const uint8_t* img = smem + fi * Cfg::FRAME;
   P pz = p_in.for_z(z);
   const int nhw = pz.nh * pz.nw;
   const int m0 = f * nhw;
   pz.M = m0 + nhw < pz.M ? m0 + nhw : pz.M;  // this frame's rows of the class only
   const int nk = P::KR / BK;
 
-  // ---- B: thread tid loads unit tid % 128 of class tid / 128's panel (three planes).
-  const int bz = tid / PB::UNITS, bu = tid - bz * PB::UNITS;
+  // ---- B: loader thread tid loads unit tid % 128 of class tid / 128's panel (3 planes).
+  const bool bload = tid < Cfg::BT;
+  const int bz = bload ? tid / PB::UNITS : 0, bu = tid - bz * PB::UNITS;
   const P pb = p_in.for_z(bz);
   const typename P::BRow brow = pb.b_row(PB::row_of(bu));
   __amdgpu_buffer_rsrc_t srcB[3];
@@ -69,7 +75,7 @@ __global__ void __launch_bounds__(P3SCfg<G>::NT) gemm_p3s_kernel(const conv::P3C
   u32x4 rb[2][3];
   auto fetch_b = [&](auto S_, int k0) {
     constexpr int set = decltype(S_)::value;
-    const uint32_t off = k0 < P::KR ? pb.b_off(brow, k0, PB::kk_of(bu)) : kOOB;
+    const uint32_t off = bload && k0 < P::KR ? pb.b_off(brow, k0, PB::kk_of(bu)) : kOOB;
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl)
       rb[set][pl] =
@@ -78,6 +84,7 @@ __global__ void __launch_bounds__(P3SCfg<G>::NT) gemm_p3s_kernel(const conv::P3C
   auto stash_b = [&](auto S_, int buf) {
     constexpr int set = decltype(S_)::value;
     uint8_t* sb = smem + Cfg::IMG + buf * Cfg::STAGE_B + bz * PB::BYTES;
+    if (!bload) return;
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl)
       *reinterpret_cast<u32x4*>(sb + pl * PB::PLANE + PB::offset(bu)) = rb[set][pl];
@@ -87,9 +94,9 @@ __global__ void __launch_bounds__(P3SCfg<G>::NT) gemm_p3s_kernel(const conv::P3C
   fetch_b(S0{}, 0);
   fetch_b(S1{}, BK);
 
-  // ---- A: the frame's dZ image, each 16-B unit of each plane once.
+  // ---- A: the block's dZ images, each 16-B unit of each plane once.
   {
-    constexpr int UNITS = H * W * CPX;
+    constexpr int UNITS = FPB * H * W * CPX;
     constexpr int PER = (UNITS + NT - 1) / NT;
     __amdgpu_buffer_rsrc_t srcA[3];
 #pragma unroll
@@ -98,7 +105,8 @@ __global__ void __launch_bounds__(P3SCfg<G>::NT) gemm_p3s_kernel(const conv::P3C
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const int u = tid + j * NT;
-      const uint32_t off = u < UNITS ? (uint32_t)(((int64_t)f * UNITS + u) * 16) : kOOB;
+      const bool ok = u < UNITS && blockIdx.x * FPB + u / (H * W * CPX) < frames;
+      const uint32_t off = ok ? (uint32_t)(((int64_t)blockIdx.x * UNITS + u) * 16) : kOOB;
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl)
         v[j][pl] =
@@ -108,8 +116,9 @@ __global__ void __launch_bounds__(P3SCfg<G>::NT) gemm_p3s_kernel(const conv::P3C
     for (int j = 0; j < PER; ++j) {
       const int u = tid + j * NT;
       if (u < UNITS) {
-        const int q = u / CPX, c = u - q * CPX;
-        const int a = q * (2 * Cfg::C) + 16 * (c ^ Cfg::swz(q));
+        const int fu = u / (H * W * CPX), uu = u - fu * (H * W * CPX);
+        const int q = uu / CPX, c = uu - q * CPX;
+        const int a = fu * Cfg::FRAME + q * (2 * Cfg::C) + 16 * (c ^ Cfg::swz(q));
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<u32x4*>(smem + pl * PLANE + a) = v[j][pl];
       }
@@ -124,7 +133,7 @@ __global__ void __launch_bounds__(P3SCfg<G>::NT) gemm_p3s_kernel(const conv::P3C
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
     const int lr = half * 32 * MT + i * 32 + (lane & 31);
-    rok[i] = lr < nhw;
+    rok[i] = lr < nhw && f < frames;
     const int ii = rok[i] ? lr / pz.nw : 0, jj = rok[i] ? lr - ii * pz.nw : 0;
     oh0[i] = (pz.rh + Cfg::S * ii + G::PT - pz.ph) / Cfg::S;
     ow0[i] = (pz.rw + Cfg::S * jj + G::PL - pz.pw) / Cfg::S;
@@ -159,11 +168,11 @@ __global__ void __launch_bounds__(P3SCfg<G>::NT) gemm_p3s_kernel(const conv::P3C
       const int c = cb + 2 * s + (lane >> 5);
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
-        const int a = qb[i] >= 0 ? qb[i] + 16 * (c ^ qs[i]) : PLANE - 16;
+        const uint8_t* a = qb[i] >= 0 ? img + qb[i] + 16 * (c ^ qs[i]) : smem + PLANE - 16;
         bf16x8 fa[3];
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl)
-          fa[pl] = *reinterpret_cast<const bf16x8*>(smem + pl * PLANE + a);
+          fa[pl] = *reinterpret_cast<const bf16x8*>(a + pl * PLANE);
         // Smallest terms first, as gemm_p3.h.
         acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1], acc[i][0], 0, 0, 0);
         acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0], acc[i][0], 0, 0, 0);
@@ -192,14 +201,15 @@ __global__ void __launch_bounds__(P3SCfg<G>::NT) gemm_p3s_kernel(const conv::P3C
   C::epilogue(pz, smem, m0, 0, wave, half, 0, lane, 0, acc, cs, false);
 }
 
-template <class G>
+template <class G, int FPB = 1>
 inline hipError_t launch_gemm_p3s(const conv::P3ConvDgradSubZ<G>& p, int frames, hipStream_t st) {
-  using Cfg = P3SCfg<G>;
-  static_assert(Cfg::LDS <= 160 * 1024, "dZ image + two four-class B stages must fit the LDS");
-  static hipError_t attr = p3_set_lds(&gemm_p3s_kernel<G>, Cfg::LDS);
+  using Cfg = P3SCfg<G, FPB>;
+  static_assert(Cfg::LDS <= 160 * 1024, "dZ images + two four-class B stages must fit the LDS");
+  static hipError_t attr = p3_set_lds(&gemm_p3s_kernel<G, FPB>, Cfg::LDS);
   if (attr != hipSuccess) return attr;
   if (p.N > Cfg::BN || p.batch != frames || frames < 1) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(gemm_p3s_kernel<G>, dim3(frames), dim3(Cfg::NT), Cfg::LDS, st, p);
+  hipLaunchKernelGGL((gemm_p3s_kernel<G, FPB>), dim3((frames + FPB - 1) / FPB), dim3(Cfg::NT),
+                     Cfg::LDS, st, p, frames);
   return hipGetLastError();
 }
 

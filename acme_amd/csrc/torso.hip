@@ -421,6 +421,12 @@ int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int row
       case 8: P3D_GEMM_F("conv2_dgrad", fl, 32, 1, 4, 32, p, G2::S * G2::S); break;
       case 9: P3P_GEMM_F("conv2_dgrad", fl, 128, 32, 4, 1, p, G2::S * G2::S); break;
       case 10: P3P_GEMM_F("conv2_dgrad", fl, 256, 32, 4, 1, p, G2::S * G2::S); break;
+      case 12: {  // image-resident dZ, two frames per block (16 waves)
+        ACME_PROF_PEAK("conv2_dgrad", st, fl, 0.0, gemm::p3_peak_tflops<decltype(p)>());
+        hipError_t e = gemm::launch_gemm_p3s<G2, 2>(p, rows, st);
+        if (e != hipSuccess) return (set_error("gemm launch failed: %s", hipGetErrorString(e)), ACME_ERR_HIP);
+        break;
+      }
       case 11: {  // image-resident dZ, four classes per block (gemm_p3s.h)
         ACME_PROF_PEAK("conv2_dgrad", st, fl, 0.0, gemm::p3_peak_tflops<decltype(p)>());
         hipError_t e = gemm::launch_gemm_p3s<G2>(p, rows, st);
@@ -434,9 +440,10 @@ int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int row
         break;
       }
       case 16: P3_GEMM_F("conv2_dgrad", fl, 128, 32, 4, 1, 32, p, G2::S * G2::S); break;
-      default: {  // image-resident dZ, four classes per block: 57.7 -> 38.0 us vs case 16
+      default: {  // image-resident dZ, two frames x four classes per block (16 waves):
+                  // 57.7 us (case 16) -> 38.0 (case 11, one frame) -> 34.7 us
         ACME_PROF_PEAK("conv2_dgrad", st, fl, 0.0, gemm::p3_peak_tflops<decltype(p)>());
-        hipError_t e = gemm::launch_gemm_p3s<G2>(p, rows, st);
+        hipError_t e = gemm::launch_gemm_p3s<G2, 2>(p, rows, st);
         if (e != hipSuccess) return (set_error("gemm launch failed: %s", hipGetErrorString(e)), ACME_ERR_HIP);
         break;
       }
