@@ -321,6 +321,7 @@ int forward_p3(const PWeights& w, const Frames& frames, int rows, const PActs& a
       case 14: P3I_GEMM("conv3_fwd", I3F, 1, 64, 4, 2, 1, p, rows); break;
       case 15: P3I_GEMM("conv3_fwd", I3F, 2, 64, 4, 1, 2, p, rows); break;
       case 16: P3_GEMM("conv3_fwd", 128, 64, 2, 2, 32, p, 1); break;
+      case 17: P3I_GEMM("conv3_fwd", I3F, 2, 64, 8, 2, 1, p, rows); break;
       // Image-resident, 4 x 2 waves (measured 50.1 -> 43.5 us vs the 128x64 im2col engine).
       default: P3I_GEMM("conv3_fwd", I3F, 1, 64, 4, 2, 1, p, rows); break;
     }
@@ -379,8 +380,9 @@ int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int row
       case 13: P3I_GEMM("conv3_dgrad", I3D, 2, 64, 8, 1, 1, p, rows); break;
       case 14: P3I_GEMM("conv3_dgrad", I3D, 1, 64, 4, 2, 1, p, rows); break;
       case 16: P3_GEMM("conv3_dgrad", 128, 64, 2, 2, 32, p, 1); break;
-      // Image-resident dZ (measured 37.4 -> 32.6 us vs the 128x64 gather engine).
-      default: P3I_GEMM("conv3_dgrad", I3D, 1, 64, 4, 1, 1, p, rows); break;
+      // Image-resident dZ, two frames x 8 x 2 waves: 37.4 us (case 16) -> 32.6 (case 12) ->
+      // 31.2 us.
+      default: P3I_GEMM("conv3_dgrad", I3D, 2, 64, 8, 2, 1, p, rows); break;
     }
   }
   if (fork) {
