@@ -333,11 +333,11 @@ int nature_forward(acme_dqn* l, const float* prm, const void* obs_a, const void*
 int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const torso::Frames& frames,
                       int rows, const torso::Plane& x1, const torso::Plane& x2,
                       const torso::Plane& x3, float* hid, float* q, hipStream_t st,
-                      float* slab = nullptr) {
+                      float* slab = nullptr, int keep_x1 = -1) {
   if (!slab) slab = l->slab;
   torso::PWeights w{WP(l, wpl, l->t_c1w), WP(l, wpl, l->t_c2w), WP(l, wpl, l->t_c3w),
                     P(l, prm, l->t_c1b), P(l, prm, l->t_c2b), P(l, prm, l->t_c3b)};
-  int rc = torso::forward_p3(w, frames, rows, torso::PActs{x1, x2, x3}, st);
+  int rc = torso::forward_p3(w, frames, rows, torso::PActs{x1, x2, x3}, st, keep_x1);
   if (rc != ACME_OK) return rc;
   {
     P3DenseFwd p;
@@ -921,11 +921,11 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
       return rc;
     if ((rc = nature_forward_p3(l, l->target, l->tpl, fwd_frames.rows_from(B), B,
                                 l->t1p, l->t2p, l->t3p, l->thid, l->q_tg, tst,
-                                side ? l->side_slab : l->slab)) != ACME_OK)
+                                side ? l->side_slab : l->slab, 0)) != ACME_OK)
       return rc;
     if (side) ACME_HIP_TRY(hipEventRecord(l->ev[1], side));
     if ((rc = nature_forward_p3(l, l->params, l->wpl, fwd_frames, 2 * B, l->x1p, l->x2p, l->x3p,
-                                l->hid, l->q_on, st)) != ACME_OK)
+                                l->hid, l->q_on, st, nullptr, B)) != ACME_OK)
       return rc;
     if (side) ACME_HIP_TRY(hipStreamWaitEvent(st, l->ev[1], 0));
   } else if (nature) {

@@ -70,8 +70,11 @@ struct Frames {
   }
 };
 // frames: bf16 copies of the uint8 frames [rows][84*84*4] (launch_frames_bf16).
+// keep_x1: frames [0, keep_x1) get their conv1 output x1 in HBM (the backward reads it);
+// -1: all.  With the fused conv1 -> conv2 kernel (ACME_V_C12=1) the other frames' x1 only
+// lives in LDS.
 int forward_p3(const PWeights& w, const Frames& frames, int rows, const PActs& a,
-               hipStream_t st);
+               hipStream_t st, int keep_x1 = -1);
 // Optional second stream for the weight gradients: conv3 / conv2 weight gradients run on
 // `side` (with their own split-K slab) beside the input gradients on the main stream;
 // events e[0..2] are scratch (hipEventDisableTiming).  side == nullptr: one stream.

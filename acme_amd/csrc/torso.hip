@@ -13,6 +13,7 @@
 #include "gemm_p3d.h"
 #include "gemm_p3i.h"
 #include "gemm_p3s.h"
+#include "gemm_p3c12.h"
 #include "gemm_x6.h"
 #include "kernels.h"
 #include "profiler.h"
@@ -239,8 +240,28 @@ int64_t wgrad_slab_floats_p3() {
 }
 
 int forward_p3(const PWeights& w, const Frames& frames, int rows, const PActs& a,
-               hipStream_t st) {
-  if (frames.u8) {  // conv1 straight from the uint8 frames
+               hipStream_t st, int keep_x1) {
+  // Fused conv1 -> conv2 (gemm_p3c12.h; 81 us vs 34.8 + 50.3 us alone, but one 150-KB
+  // block per CU shares the GPU badly with the other stream).  ACME_V_C12: default the target
+  // forward (keep_x1 == 0, on the side stream) only, measured 0.716 -> 0.713 ms per step;
+  // 1 every forward (0.726 -> 0.733); 2 the online forward only (0.716 -> 0.725); 4 off.
+  const int c12 = tune_variant("C12");
+  const bool fused = !frames.u8 && (c12 == 1 || (c12 == 2 && keep_x1 != 0) ||
+                                    ((c12 == 0 || c12 == 3) && keep_x1 == 0));
+  if (fused) {
+    P3ConvFwd<G1, 1> p1;
+    p1.M = rows * G1::OPIX; p1.N = G1::CO; p1.K = G1::K; p1.k_chunk = G1::K;
+    p1.a_src = frames_src(frames, rows); p1.b_src = src(w.w1, G1::K * G1::CO);
+    p1.bias = w.b1; p1.y = pl(a.x1);
+    P3ConvFwd<G2, 3> p2;
+    p2.M = rows * G2::OPIX; p2.N = G2::CO; p2.K = G2::K; p2.k_chunk = G2::K;
+    p2.a_src = src(a.x1, (int64_t)rows * kX1); p2.b_src = src(w.w2, G2::K * G2::CO);
+    p2.bias = w.b2; p2.y = pl(a.x2);
+    const double fl = 2.0 * p1.M * p1.N * (double)p1.K + 2.0 * p2.M * p2.N * (double)p2.K;
+    ACME_PROF_PEAK("conv12_fwd", st, fl, 0.0, gemm::p3_peak_tflops<decltype(p2)>());
+    hipError_t e = gemm::launch_gemm_p3c12(p1, p2, rows, keep_x1 < 0 ? rows : keep_x1, st);
+    if (e != hipSuccess) return (set_error("gemm launch failed: %s", hipGetErrorString(e)), ACME_ERR_HIP);
+  } else if (frames.u8) {  // conv1 straight from the uint8 frames
     P3ConvFwd<G1, 1, true> p;
     p.M = rows * G1::OPIX; p.N = G1::CO; p.K = G1::K; p.k_chunk = G1::K;
     p.a_src = frames_src(frames, rows); p.b_src = src(w.w1, G1::K * G1::CO);
@@ -277,7 +298,7 @@ int forward_p3(const PWeights& w, const Frames& frames, int rows, const PActs& a
       default: P3I_GEMM("conv1_fwd", I1F, 1, 32, 7, 1, 2, p, rows); break;
     }
   }
-  {
+  if (!fused) {
     P3ConvFwd<G2, 3> p;
     p.M = rows * G2::OPIX; p.N = G2::CO; p.K = G2::K; p.k_chunk = G2::K;
     p.a_src = src(a.x1, (int64_t)rows * kX1); p.b_src = src(w.w2, G2::K * G2::CO);
