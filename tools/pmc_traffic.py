@@ -51,6 +51,8 @@ SECTIONS = [
     (r"fc_head_forward_kernel", "fc_head_fwd"),
     (r"frames_bf16_kernel", "frames_bf16"),
     (r"head_dz_planes_kernel", "head_dz"),
+    (r"dqn_loss_head_dz_kernel", "loss_head_dz"),
+    (r"gemm_p3c12_kernel", "conv12_fwd"),
     (r"gemm_\w+_kernel<128, 128, 2, 2,.*DenseFwd<true", "fc_fwd"),
     (r"ConvFwd<acme::conv::Geom<84,", "conv1_fwd"),
     (r"ConvFwd<acme::conv::Geom<21,", "conv2_fwd"),
