@@ -14,6 +14,7 @@
 #include "gemm_p3i.h"
 #include "gemm_p3s.h"
 #include "gemm_p3c12.h"
+#include "gemm_p3w.h"
 #include "gemm_x6.h"
 #include "kernels.h"
 #include "profiler.h"
@@ -371,6 +372,14 @@ int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int row
     p.k_chunk = chunk_for(p.K, splits);
     p.a_src = src(a.x2, (int64_t)rows * kFlat); p.b_src = src(dz3, (int64_t)rows * kFlat);
     p.slab = wslab;
+    if (tune_variant("P3C3W") == 12) {  // image-resident, one wave per tap (gemm_p3w.h)
+      const int fs = (rows + 1) / 2;
+      ACME_PROF_PEAK("conv3_wgrad", st, 2.0 * (double)p.M * (double)p.N * (double)p.K, 0.0,
+                     gemm::p3_peak_tflops<decltype(p)>());
+      hipError_t e = gemm::launch_gemm_p3w<G3, 2>(p, rows, st);
+      if (e != hipSuccess) return (set_error("gemm launch failed: %s", hipGetErrorString(e)), ACME_ERR_HIP);
+      return p3_wgrad_reduce(p, fs, wslab, g.w3, g.b3, "conv3_wgrad_reduce", st);
+    }
     if (tune_variant("P3C3W") == 9) P3P_GEMM("conv3_wgrad", 128, 64, 2, 2, p, splits);
     else if (tune_variant("P3C3W") == 1) P3G_GEMM("conv3_wgrad", 128, 64, 2, 2, 32, 3, p, splits);
     else P3_GEMM("conv3_wgrad", 128, 64, 2, 2, 32, p, splits);
