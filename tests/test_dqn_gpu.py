@@ -93,8 +93,8 @@ NETS = {
 }
 
 
-@pytest.mark.parametrize("netname,B", [("nature", 4), ("nature", 37), ("cartpole_mlp", 32),
-                                       ("mlp_vec", 100)])
+@pytest.mark.parametrize("netname,B", [("nature", 1), ("nature", 4), ("nature", 37),
+                                       ("cartpole_mlp", 32), ("mlp_vec", 100)])
 def test_forward_backward_matches_oracle(netname, B):
     net = NETS[netname]()
     rng = np.random.default_rng(B)
