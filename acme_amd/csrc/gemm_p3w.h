@@ -41,27 +41,6 @@ struct P3WCfg {
   __device__ static __forceinline__ int chunk(int q, int c) { return c ^ (((q >> 1) & 1) << 2); }
 };
 
-// Transposed fragment of a [pixel][64-channel] image: rows rb..rb+31 (channels), the 16
-// pixels of k16 step s; pix(k) gives the LDS pixel (or -1 for a zero row) of step pixel k.
-template <class Cfg, class PixFn>
-__device__ __forceinline__ bf16x8 frag_tr(const uint8_t* img, const uint8_t* zero, int rb,
-                                          int lane, const PixFn& pix) {
-  const int h = lane >> 5, g = (lane >> 4) & 1, qq = (lane >> 2) & 3, pp = lane & 3;
-  const int row = rb + 16 * g + 4 * pp;
-  auto addr = [&](int k) -> const uint8_t* {
-    const int q = pix(k);
-    if (q < 0) return zero;
-    return img + q * 128 + 16 * Cfg::chunk(q, row >> 3) + 2 * (row & 7);
-  };
-  typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
-  const int k0 = 8 * h + qq;
-  const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)addr(k0));
-  const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)addr(k0 + 4));
-  const __attribute__((ext_vector_type(8))) short v{lo[0], lo[1], lo[2], lo[3],
-                                                    hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, v);
-}
-
 template <class G, int FPB>
 __global__ void __launch_bounds__(64 * G::KH * G::KW) gemm_p3w_kernel(
     const conv::P3ConvWgrad<G, 3> p, int frames) {
@@ -144,47 +123,68 @@ __global__ void __launch_bounds__(64 * G::KH * G::KW) gemm_p3w_kernel(
       }
       __syncthreads();
     }
-    // ---- 8 k16 steps over the frame's output pixels.
-#pragma unroll 2
-    for (int s = 0; s < Cfg::STEPS; ++s) {
-      const int pb = 16 * s;
-      auto xpix = [&](int k) {  // X pixel of output pixel pb + k under this tap
-        const int pz = pb + k;
-        const int oh = pz / G::OW, ow = pz - oh * G::OW;
-        const int ih = oh + dh, iw = ow + dw;
-        return pz < Cfg::PIX && (unsigned)ih < (unsigned)G::IH && (unsigned)iw < (unsigned)G::IW
-                   ? ih * G::IW + iw : -1;
+    // ---- 8 k16 steps over the frame's output pixels.  A lane's transpose reads touch
+    // step pixels k0 = 8h + qq and k0 + 4 (as PlanP3's row-contiguous fragments) and
+    // channels 16g + 4pp (+ 32 for the second row block): the pixel arithmetic is done
+    // once per step, the chunk arithmetic once per lane.
+    {
+      const int h = lane >> 5, g = (lane >> 4) & 1, qq = (lane >> 2) & 3, pp = lane & 3;
+      const int cbase = 2 * g + (pp >> 1), cbyte = 8 * (pp & 1);
+      typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+      auto rd = [&](const uint8_t* img, const uint8_t* zero, int q, int i) -> i16x4 {
+        const uint8_t* a =
+            q < 0 ? zero : img + q * 128 + 16 * Cfg::chunk(q, 4 * i + cbase) + cbyte;
+        return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)a);
       };
-      auto dpix = [&](int k) { return pb + k < Cfg::PIX ? pb + k : -1; };
-      bf16x8 fa[2][3], fb[2][3];
+#pragma unroll 2
+      for (int s = 0; s < Cfg::STEPS; ++s) {
+        int qx[2], qd[2];
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) {
-        const uint8_t* xi = smem + Cfg::X0 + pl * Cfg::XPL;
-        const uint8_t* di = smem + Cfg::D0 + pl * Cfg::DPL;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          fa[i][pl] = frag_tr<Cfg>(xi, xi + Cfg::IMG, 32 * i, lane, xpix);
-          fb[i][pl] = frag_tr<Cfg>(di, di + Cfg::DZ, 32 * i, lane, dpix);
+        for (int t = 0; t < 2; ++t) {
+          const int pz = 16 * s + 8 * h + qq + 4 * t;
+          const int oh = pz / G::OW, ow = pz - oh * G::OW;
+          const int ih = oh + dh, iw = ow + dw;
+          const bool in = pz < Cfg::PIX;
+          qx[t] = in && (unsigned)ih < (unsigned)G::IH && (unsigned)iw < (unsigned)G::IW
+                      ? ih * G::IW + iw : -1;
+          qd[t] = in ? pz : -1;
         }
-      }
+        bf16x8 fa[2][3], fb[2][3];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+        for (int pl = 0; pl < 3; ++pl) {
+          const uint8_t* xi = smem + Cfg::X0 + pl * Cfg::XPL;
+          const uint8_t* di = smem + Cfg::D0 + pl * Cfg::DPL;
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          // Smallest terms first, as gemm_p3.h.
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], acc[i][j], 0, 0, 0);
+          for (int i = 0; i < 2; ++i) {
+            const i16x4 xl = rd(xi, xi + Cfg::IMG, qx[0], i), xh = rd(xi, xi + Cfg::IMG, qx[1], i);
+            const i16x4 dl = rd(di, di + Cfg::DZ, qd[0], i), dhh = rd(di, di + Cfg::DZ, qd[1], i);
+            const __attribute__((ext_vector_type(8))) short vx{xl[0], xl[1], xl[2], xl[3],
+                                                               xh[0], xh[1], xh[2], xh[3]};
+            const __attribute__((ext_vector_type(8))) short vd{dl[0], dl[1], dl[2], dl[3],
+                                                               dhh[0], dhh[1], dhh[2], dhh[3]};
+            fa[i][pl] = __builtin_bit_cast(bf16x8, vx);
+            fb[i][pl] = __builtin_bit_cast(bf16x8, vd);
+          }
         }
-      if (colsum) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int pl = 2; pl >= 0; --pl)
-            cs[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fb[j][pl], cs[j], 0, 0, 0);
+          for (int j = 0; j < 2; ++j) {
+            // Smallest terms first, as gemm_p3.h.
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], acc[i][j], 0, 0, 0);
+          }
+        if (colsum) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int pl = 2; pl >= 0; --pl)
+              cs[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fb[j][pl], cs[j], 0, 0, 0);
+        }
       }
     }
   }
