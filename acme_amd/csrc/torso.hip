@@ -295,6 +295,7 @@ int forward_p3(const PWeights& w, const Frames& frames, int rows, const PActs& a
       case 13: P3I_GEMM("conv1_fwd", I1F, 1, 32, 7, 1, 2, p, rows); break;
       case 14: P3I_GEMM("conv1_fwd", I1F, 1, 32, 14, 1, 1, p, rows); break;
       case 15: P3I_GEMM("conv1_fwd", I1F, 1, 32, 4, 1, 4, p, rows); break;
+      case 16: P3I_GEMM("conv1_fwd", I1F, 2, 32, 14, 1, 2, p, rows); break;
       // Image-resident frames (gemm_p3i.h pixel pairs): 39.6 -> 33.7 us vs direct A (case 7).
       default: P3I_GEMM("conv1_fwd", I1F, 1, 32, 7, 1, 2, p, rows); break;
     }

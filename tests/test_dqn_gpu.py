@@ -123,7 +123,7 @@ def test_forward_backward_matches_oracle(netname, B):
     {"P3C2F": 12}, {"P3C2F": 13}, {"P3C3F": 12}, {"P3C3F": 13}, {"P3C3F": 14}, {"P3C3F": 15},
     {"P3C3F": 16}, {"P3C3D": 13}, {"P3C3D": 14}, {"P3C3D": 16},
     {"P3C1F": 13}, {"P3C1F": 14}, {"P3C1F": 15}, {"P3C2D": 11}, {"P3C2D": 12}, {"P3C2D": 16},
-    {"P3C3F": 17}, {"P3C3D": 12}, {"C12": 1}, {"C12": 4}, {"P3C3W": 12}])
+    {"P3C3F": 17}, {"P3C3D": 12}, {"C12": 1}, {"C12": 4}, {"P3C3W": 12}, {"P3C1F": 16}])
 def test_kernel_variants_match_oracle(variants):
     """The plane engine's alternative kernels (acme_tune_set switches: direct-A dense layers,
     image-resident convolutions; B = 37 leaves partial tiles and a half-filled two-frame
