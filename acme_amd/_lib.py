@@ -125,6 +125,9 @@ _SIGS = {
     "acme_replay_capacity": (c_i64, [c_vp]),
     "acme_replay_debug_leaves": (c_i32, [c_vp, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp),
                                          ctypes.POINTER(c_vp)]),
+    "acme_replay_storage": (c_i32, [c_vp, c_i32, ctypes.POINTER(c_vp)]),
+    "acme_replay_inserted": (c_i64, [c_vp]),
+    "acme_replay_restore": (c_i32, [c_vp, c_i64, c_vp]),
     "acme_dqn_create": (c_i32, [ctypes.POINTER(DQNConfig), ctypes.POINTER(c_vp)]),
     "acme_dqn_destroy": (c_i32, [c_vp]),
     "acme_dqn_num_params": (c_i64, [c_vp]),

@@ -977,6 +977,12 @@ int acme_d4pg_bind(acme_d4pg* l, float* params, float* target, float* grads, flo
   for (const void* p : {(const void*)params, (const void*)target, (const void*)grads,
                         (const void*)adam_m, (const void*)adam_v})
     ACME_CHECK_ARG(((uintptr_t)p & 15) == 0, "buffers must be 16-byte aligned");
+  // Captured graphs bake in the bound buffers: a re-bind invalidates them.
+  if (!l->graphs.empty()) {
+    ACME_HIP_TRY(hipDeviceSynchronize());
+    for (auto& g : l->graphs) (void)hipGraphExecDestroy(g.exec);
+    l->graphs.clear();
+  }
   l->params = params;
   l->target = target;
   l->grads = grads;

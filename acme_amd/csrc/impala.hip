@@ -925,9 +925,11 @@ int acme_impala_debug_buffer(const acme_impala* l, const char* name, const float
       {"pv", l->pv, R * (l->A + 1)}, {"vs", l->vs, R},        {"pg_adv", l->pg_adv, R},
       {"h", l->h, R * l->H},         {"c", l->c, R * l->H},   {"dpv", l->dpv, R * (l->A + 1)},
       {"dgates", l->dgates, R * 4 * l->H}, {"grad_norm", l->norms, 1},
+      {"hh", l->hh, R * l->H2},      {"x1", l->x1, l->x1 ? R * torso::kX1 : 0},
+      {"x2", l->x2, l->x2 ? R * torso::kFlat : 0}, {"x3", l->x3, l->x3 ? R * torso::kFlat : 0},
   };
   for (const Item& it : items)
-    if (strcmp(it.n, name) == 0) {
+    if (it.p && strcmp(it.n, name) == 0) {
       *out = it.p;
       *count = it.c;
       return ACME_OK;

@@ -392,6 +392,14 @@ __global__ void fill_scalars_kernel(int32_t* __restrict__ action, float* __restr
   leaves[slot] = 1.0;
 }
 
+// Checkpoint restore: leaves from the restored raw priorities (zero past the live range).
+__global__ void restore_leaves_kernel(const double* __restrict__ raw, double* __restrict__ leaves,
+                                      int64_t live, int64_t n, int prioritized, double alpha) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  leaves[i] = i < live ? (prioritized ? det_pow_priority(raw[i], alpha) : 1.0) : 0.0;
+}
+
 // Recompute all internal levels over the slot range touched by an insert.
 int refresh_range(acme_replay* r, int64_t first_key, int64_t n, hipStream_t st) {
   const int64_t C = r->cfg.capacity;
@@ -502,6 +510,36 @@ int acme_replay_debug_leaves(const acme_replay* r, const double** leaf_values,
   if (leaf_values) *leaf_values = r->levels[0];
   if (raw_priorities) *raw_priorities = r->raw_prio;
   if (keys) *keys = r->keys;
+  return ACME_OK;
+}
+
+int acme_replay_storage(const acme_replay* r, int32_t field, void** out) {
+  ACME_CHECK_ARG(r && out, "null argument");
+  ACME_CHECK_ARG(field >= 0 && field < r->cfg.num_fields, "field %d out of range", field);
+  *out = r->fields[field];
+  return ACME_OK;
+}
+
+int64_t acme_replay_inserted(const acme_replay* r) { return r ? r->inserted : 0; }
+
+int acme_replay_restore(acme_replay* r, int64_t inserted, void* stream) {
+  ACME_CHECK_ARG(r, "null replay");
+  ACME_CHECK_ARG(inserted >= 0, "negative insert count");
+  std::lock_guard<std::mutex> lock(r->mu);
+  hipStream_t st = as_stream(stream);
+  const int64_t C = r->cfg.capacity, live = std::min(inserted, C);
+  const int64_t n = r->level_size[0];
+  restore_leaves_kernel<<<(unsigned)ceil_div(n, 256), 256, 0, st>>>(
+      r->raw_prio, r->levels[0], live, n, r->cfg.sampler == ACME_SAMPLER_PRIORITIZED,
+      r->cfg.priority_exponent);
+  ACME_LAUNCH_CHECK();
+  for (int l = 1; l < r->nlevels; ++l) {  // every node of every level
+    const int64_t count = r->level_size[l - 1] / 64;
+    level_update_kernel<<<(unsigned)ceil_div(count, 4), 256, 0, st>>>(
+        r->levels[l - 1], r->levels[l], 0, count, nullptr, nullptr, 0);
+    ACME_LAUNCH_CHECK();
+  }
+  r->inserted = inserted;
   return ACME_OK;
 }
 

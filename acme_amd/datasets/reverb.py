@@ -12,7 +12,10 @@ DQN agent asks for 4, agents/tf/dqn/agent.py:50): with P > 0 the sample and gath
 k + P are issued on the dataset's own stream when batch k is handed out, ordered after
 every kernel already queued on the caller's stream (so they see the priority updates of
 steps < k, like Reverb's prefetched samples), and the caller's stream waits only for the
-batch it receives.  The draw order, and so every sampled index, is deterministic.
+batch it receives.  Writers of the table (priority updates, inserts) in turn order the
+caller's stream after the last issued prefetch (Table._after_readers), so a queued draw
+never overlaps a tree update or a slot overwrite.  The draw order, and so every sampled
+index, is deterministic.
 
 `server_address` may be the in-process address ('localhost:<port>'), a Server, a Table
 or a Client.  Sampling is deterministic given the table seed: draw i uses Philox
@@ -165,6 +168,7 @@ class _TableIterator:
             self._gather(L, h, raw[0], ptrs, st)
             self._ready[i].record(side)
             self._queue.append(i)
+            t.set_reader_event(self._ready[i])
         i = self._queue.pop(0)
         # A batch issued P steps ago has normally landed: ordering the caller's stream
         # after a completed event is a no-op, and skipping the wait saves its queue-side

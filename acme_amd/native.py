@@ -129,6 +129,51 @@ class NativeReplay:
                                                   int(keys.numel()), stream_ptr(stream)),
               "update_priorities")
 
+    def export_state(self) -> Dict[str, np.ndarray]:
+        """Host copy of the live table (checkpoints): field rows, keys and raw priorities of
+        slots [0, size), the insert counter.  Leaves and tree levels are derived data."""
+        L = lib()
+        n = self.size()
+        torch.cuda.synchronize(self.device)
+        out = {"inserted": np.int64(L.acme_replay_inserted(self._h))}
+        for f, b in enumerate(self.field_bytes):
+            p = ctypes.c_void_p()
+            check(L.acme_replay_storage(self._h, f, ctypes.byref(p)))
+            out[f"field_{f}"] = _device_array(p.value, n * b, np.uint8, self.device).cpu() \
+                .numpy().reshape(n, b).copy()
+        lv, rp, ks = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        check(L.acme_replay_debug_leaves(self._h, ctypes.byref(lv), ctypes.byref(rp),
+                                         ctypes.byref(ks)))
+        out["raw_priorities"] = _device_array(rp.value, n, np.float64, self.device).cpu() \
+            .numpy().view(np.float64).copy()
+        out["keys"] = _device_array(ks.value, n, np.uint64, self.device).cpu().numpy() \
+            .view(np.uint64).copy()
+        return out
+
+    def import_state(self, state: Dict[str, np.ndarray]) -> None:
+        """Inverse of export_state (same capacity and field layout): writes rows, keys and
+        raw priorities, then rebuilds leaves and levels on the device."""
+        L = lib()
+        keys = np.asarray(state["keys"], np.uint64)
+        n = len(keys)
+        if n > self.capacity:
+            raise ValueError(f"state holds {n} items, table capacity is {self.capacity}")
+        torch.cuda.synchronize(self.device)
+        for f, b in enumerate(self.field_bytes):
+            rows = np.ascontiguousarray(state[f"field_{f}"], np.uint8)
+            if rows.shape != (n, b):
+                raise ValueError(f"field {f}: state rows {rows.shape}, table expects {(n, b)}")
+            p = ctypes.c_void_p()
+            check(L.acme_replay_storage(self._h, f, ctypes.byref(p)))
+            _memcpy_htod(p.value, rows)
+        lv, rp, ks = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        check(L.acme_replay_debug_leaves(self._h, ctypes.byref(lv), ctypes.byref(rp),
+                                         ctypes.byref(ks)))
+        _memcpy_htod(rp.value, np.asarray(state["raw_priorities"], np.float64))
+        _memcpy_htod(ks.value, keys)
+        check(L.acme_replay_restore(self._h, int(state["inserted"]), None), "replay restore")
+        torch.cuda.synchronize(self.device)
+
     def debug_state(self) -> Dict[str, np.ndarray]:
         """Host copies of leaf weights / raw priorities / keys (tests)."""
         lv, rp, ks = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
@@ -155,15 +200,26 @@ def _device_array(address: int, count: int, dtype, device) -> torch.Tensor:
 _hip = None
 
 
-def _memcpy_dtod(dst: int, src: int, nbytes: int) -> None:
+def _hip_memcpy(dst: int, src: int, nbytes: int, kind: int) -> None:
     global _hip
     if _hip is None:
         _hip = ctypes.CDLL("libamdhip64.so.7")
         _hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
         _hip.hipMemcpy.restype = ctypes.c_int
-    rc = _hip.hipMemcpy(ctypes.c_void_p(dst), ctypes.c_void_p(src), ctypes.c_size_t(nbytes), 3)
+    rc = _hip.hipMemcpy(ctypes.c_void_p(dst), ctypes.c_void_p(src), ctypes.c_size_t(nbytes), kind)
     if rc != 0:
         raise RuntimeError(f"hipMemcpy failed ({rc})")
+
+
+def _memcpy_dtod(dst: int, src: int, nbytes: int) -> None:
+    _hip_memcpy(dst, src, nbytes, 3)
+
+
+def _memcpy_htod(dst: int, host: np.ndarray) -> None:
+    """Synchronous host -> device copy of a numpy array to a raw device address."""
+    a = np.ascontiguousarray(host)
+    if a.nbytes:
+        _hip_memcpy(dst, a.ctypes.data, a.nbytes, 1)
 
 
 NET_NATURE = 0

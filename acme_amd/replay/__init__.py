@@ -126,6 +126,10 @@ class Table:
         self._cv = threading.Condition(self._mu)
         self._draws = 0
         self._seq_len: Optional[int] = None
+        # The last sample/gather a prefetching dataset issued on its own stream: writers
+        # (priority updates, inserts) order the caller's stream after it, so a queued draw
+        # never reads a half-updated tree or a slot being overwritten.
+        self._reader_event = None
         if signature is not None:
             self._init_layout(signature, _layout_from_signature(signature))
 
@@ -207,10 +211,23 @@ class Table:
         """Steps per item for sequence tables (None until the first item, 0 if not)."""
         return self._seq_len
 
+    def set_reader_event(self, event) -> None:
+        """Called by a prefetching dataset after it issues device reads of this table."""
+        self._reader_event = event
+
+    def _after_readers(self) -> None:
+        """Orders the current stream after the last issued prefetch read (a no-op when it
+        has already completed, which is the steady state: a batch is issued P steps ahead)."""
+        ev = self._reader_event
+        if ev is not None and not ev.query():
+            import torch
+            torch.cuda.current_stream(self._native.device).wait_event(ev)
+
     def flush(self) -> None:
         with self._mu:
             if not self._pending:
                 return
+            self._after_readers()
             n = len(self._pending)
             cols = []
             for i, f in enumerate(self._fields):
@@ -221,6 +238,29 @@ class Table:
                 cols.append(buf)
             self._native.insert(cols, np.asarray(self._pending_prio, np.float64))
             self._pending, self._pending_prio = [], []
+
+    # -- checkpointing (optional replay state; core.Saveable interface)
+    def save(self) -> Dict[str, Any]:
+        """The live items, their keys and raw priorities, the insert and draw counters (a
+        1M-slot Atari table is ~56 GB: include a table in a Checkpointer only on purpose)."""
+        with self._mu:
+            self.flush()
+            if self._native is None:
+                return {"draws": np.int64(self._draws)}
+            state = self._native.export_state()
+            state["draws"] = np.int64(self._draws)
+            return state
+
+    def restore(self, state: Dict[str, Any]) -> None:
+        with self._mu:
+            self._pending, self._pending_prio = [], []
+            if "keys" in state:
+                if self._native is None:
+                    raise ValueError("restore needs the table layout (construct the table "
+                                     "with its signature)")
+                self._after_readers()
+                self._native.import_state(state)
+            self._draws = int(state["draws"])
 
     # -- sampling
     def wait_for(self, batch_size: int, timeout: float) -> None:
@@ -250,6 +290,7 @@ class Table:
                 np.asarray(keys, np.uint64).view(np.int64)).view(torch.uint64)
             p = priorities if isinstance(priorities, torch.Tensor) else torch.as_tensor(
                 np.asarray(priorities, np.float64))
+            self._after_readers()
             self._native.update_priorities(k, p)
 
 

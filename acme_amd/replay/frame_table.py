@@ -52,6 +52,11 @@ def _make_frame_table(Table, _Field, _layout_from_signature):
                     raise ValueError(f"field {i} is not a uint8 [H, W, S] stack")
             self._H, self._W, self._S = shape
             self._px = self._H * self._W
+            if (self._px * self._S) % 4:
+                # Dataset rows are padded to 4 bytes (_row_bytes) while the expand kernel
+                # writes packed H*W*S rows: only unpadded stacks are supported.
+                raise ValueError(f"stacked fields need H*W*S to be a multiple of 4, got "
+                                 f"{self._H}x{self._W}x{self._S}")
             inner = [(_Field((self._S,), np.dtype(np.int32), 4 * self._S, 4 * self._S)
                       if i in self._stacked else f) for i, f in enumerate(outer)]
             super().__init__(name, sampler, remover, max_size, rate_limiter, signature=None,
@@ -120,26 +125,46 @@ def _make_frame_table(Table, _Field, _layout_from_signature):
                 if len(leaves) != len(self._outer_fields):
                     raise ValueError(f"item has {len(leaves)} leaves, table expects "
                                      f"{len(self._outer_fields)}")
-                # The item about to be inserted evicts the oldest one when the table is full.
-                if len(self._live_min) >= self.max_size:
-                    old = self._live_min.popleft()
-                    if self._live_mono and self._live_mono[0] == old:
-                        self._live_mono.popleft()
-                floor = self._live_mono[0] if self._live_mono else 1 << 62
-                out, used = list(leaves), []
                 for i in self._stacked:
-                    a = np.asarray(leaves[i], np.uint8)
-                    if a.shape != (self._H, self._W, self._S):
-                        raise ValueError(f"leaf shape {a.shape} does not match table "
-                                         f"signature {(self._H, self._W, self._S)}")
-                    idx = np.empty(self._S, np.int32)
-                    for s in range(self._S):
-                        pos, g = self._frame_index(np.ascontiguousarray(a[..., s]),
-                                                   min(floor, *(used or [1 << 62])))
-                        idx[s] = pos
-                        if g is not None:
-                            used.append(g)
-                    out[i] = idx
+                    if np.shape(leaves[i]) != (self._H, self._W, self._S):
+                        raise ValueError(f"leaf shape {np.shape(leaves[i])} does not match "
+                                         f"table signature {(self._H, self._W, self._S)}")
+                # The item about to be inserted evicts the oldest one when the table is full.
+                # Everything below is undone if a frame cannot be placed (max_frames too
+                # small), so a failed insert leaves the bookkeeping as it was.
+                evicted = mono_evicted = None
+                if len(self._live_min) >= self.max_size:
+                    evicted = self._live_min.popleft()
+                    if self._live_mono and self._live_mono[0] == evicted:
+                        mono_evicted = self._live_mono.popleft()
+                floor = self._live_mono[0] if self._live_mono else 1 << 62
+                g0, npend = self._g, len(self._pending_frames)
+                out, used = list(leaves), []
+                try:
+                    for i in self._stacked:
+                        a = np.asarray(leaves[i], np.uint8)
+                        idx = np.empty(self._S, np.int32)
+                        for s in range(self._S):
+                            pos, g = self._frame_index(np.ascontiguousarray(a[..., s]),
+                                                       min(floor, *(used or [1 << 62])))
+                            idx[s] = pos
+                            if g is not None:
+                                used.append(g)
+                        out[i] = idx
+                except ValueError:
+                    self._g = g0
+                    del self._pending_frames[npend:]
+                    for h in list(self._recent):
+                        kept = [e for e in self._recent[h] if e[0] < g0]
+                        if kept:
+                            self._recent[h] = kept
+                        else:
+                            del self._recent[h]
+                    if mono_evicted is not None:
+                        self._live_mono.appendleft(mono_evicted)
+                    if evicted is not None:
+                        self._live_min.appendleft(evicted)
+                    raise
                 m = min(used) if used else 1 << 62
                 self._live_min.append(m)
                 while self._live_mono and self._live_mono[-1] > m:
@@ -151,6 +176,7 @@ def _make_frame_table(Table, _Field, _layout_from_signature):
             with self._mu:
                 if self._pending_frames:
                     import torch
+                    self._after_readers()  # a queued expand may still read these positions
                     pos = torch.as_tensor([p for p, _ in self._pending_frames], dtype=torch.int64)
                     data = np.frombuffer(bytearray(b"".join(b for _, b in self._pending_frames)),
                                          np.uint8).reshape(-1, self._px)

@@ -149,6 +149,16 @@ int64_t acme_replay_capacity(const acme_replay* r);
 int acme_replay_debug_leaves(const acme_replay* r, const double** leaf_values,
                              const double** raw_priorities, const uint64_t** keys);
 
+/* Table state for checkpoints (optional replay state of acme/tf/savers.py's Checkpointer,
+ * SURVEY §8(f) row 2).  acme_replay_storage: device pointer of field f's [capacity, bytes]
+ * rows; acme_replay_inserted: items ever inserted (the next key).  acme_replay_restore:
+ * after the caller wrote field rows, keys and raw priorities (device pointers from
+ * acme_replay_storage / acme_replay_debug_leaves), sets the insert counter and rebuilds the
+ * leaves (p^alpha) and every level of the sum tree on `stream`. */
+int acme_replay_storage(const acme_replay* r, int32_t field, void** out);
+int64_t acme_replay_inserted(const acme_replay* r);
+int acme_replay_restore(acme_replay* r, int64_t inserted, void* stream);
+
 /* -------------------------------------------------------------------- DQN -- */
 
 enum { ACME_NET_NATURE_DQN = 0, ACME_NET_MLP = 1 };

@@ -166,7 +166,9 @@ def vtrace(log_rhos, discounts, rewards, values, bootstrap):
     return vs, pg_adv
 
 
-def loss_and_grads(cfg: IMPALAConfig, p, batch, dtype=np.float64):
+def loss_and_grads(cfg: IMPALAConfig, p, batch, dtype=np.float64, masks=None):
+    """masks: optional ReLU patterns {"x1", "x2", "x3", "hh"} that replace (x > 0) in the
+    backward pass (a kernel's own branch decisions, for kink-conditioned comparisons)."""
     f = dtype
     B, T = batch["action"].shape
     A, H = cfg.num_actions, cfg.lstm_size
@@ -202,7 +204,7 @@ def loss_and_grads(cfg: IMPALAConfig, p, batch, dtype=np.float64):
     dlogits[:-1], dvalues[:-1] = dlg, dv
     dpv = np.concatenate([np.swapaxes(dlogits, 0, 1).reshape(B * T, A),
                           np.swapaxes(dvalues, 0, 1).reshape(B * T, 1)], axis=1)
-    grads = backward(cfg, p, batch, cache, dpv, f)
+    grads = backward(cfg, p, batch, cache, dpv, f, masks)
     out = dict(loss=loss, critic_loss=critic.mean(), entropy_loss=(-ent).mean(),
                policy_gradient_loss=pg.mean(), logits=logits, values=values, vs=vs,
                pg_advantages=pg_adv, log_rhos=log_rhos, dpv=dpv, hs=cache["hs"],
@@ -210,14 +212,20 @@ def loss_and_grads(cfg: IMPALAConfig, p, batch, dtype=np.float64):
     return out, grads
 
 
-def backward(cfg: IMPALAConfig, p, batch, cache, dpv, f):
+def backward(cfg: IMPALAConfig, p, batch, cache, dpv, f, masks=None):
     B, T = batch["action"].shape
     H = cfg.lstm_size
     g = {}
     hh = cache["hh"]
+
+    def relu_mask(name, x):
+        if masks is not None and name in masks:
+            return masks[name].reshape(x.shape)
+        return x > 0
+
     g[f"{PREFIX}/policy_value/w"] = hh.T @ dpv
     g[f"{PREFIX}/policy_value/b"] = dpv.sum(0)
-    dhh = (dpv @ p[f"{PREFIX}/policy_value/w"].astype(f).T) * (hh > 0)
+    dhh = (dpv @ p[f"{PREFIX}/policy_value/w"].astype(f).T) * relu_mask("hh", hh)
     hflat = cache["hs"].reshape(B * T, H)
     g[f"{PREFIX}/linear/w"] = hflat.T @ dhh
     g[f"{PREFIX}/linear/b"] = dhh.sum(0)
@@ -251,7 +259,7 @@ def backward(cfg: IMPALAConfig, p, batch, cache, dpv, f):
     g[f"{PREFIX}/lstm/b"] = dgf.sum(0)
     if cfg.torso == "atari":
         dfeat = dgf @ p[f"{PREFIX}/lstm/w_i"].astype(f)[:cfg.feat].T
-        dx = dfeat.reshape(cache["x3"].shape) * (cache["x3"] > 0)
+        dx = dfeat.reshape(cache["x3"].shape) * relu_mask("x3", cache["x3"])
         for li in (2, 1, 0):
             name = _torso_names()[li]
             _, s, pads = CONVS[li]
@@ -264,7 +272,7 @@ def backward(cfg: IMPALAConfig, p, batch, cache, dpv, f):
             if li > 0:
                 dcols = dz @ w.reshape(-1, co).T
                 xin = cache[f"x{li}"]
-                dx = _col2im(dcols, meta, kh, kw, s, pads, xin.shape) * (xin > 0)
+                dx = _col2im(dcols, meta, kh, kw, s, pads, xin.shape) * relu_mask(f"x{li}", xin)
     return g
 
 
@@ -274,9 +282,9 @@ def clip_by_global_norm(grads, clip, f):
     return {k: (x * f(scale)).astype(f) for k, x in grads.items()}, G
 
 
-def impala_step(cfg: IMPALAConfig, state: dict, batch: dict, dtype=np.float64):
+def impala_step(cfg: IMPALAConfig, state: dict, batch: dict, dtype=np.float64, masks=None):
     """One learner step. state = {params, m, v, num_steps}."""
-    out, raw = loss_and_grads(cfg, state["params"], batch, dtype)
+    out, raw = loss_and_grads(cfg, state["params"], batch, dtype, masks)
     grads, out["grad_norm"] = clip_by_global_norm(raw, cfg.max_gradient_norm, dtype)
     t = state["num_steps"] + 1
     new_p, new_m, new_v = {}, {}, {}

@@ -94,6 +94,7 @@ NETS = {
 
 
 @pytest.mark.parametrize("netname,B", [("nature", 1), ("nature", 4), ("nature", 37),
+                                       ("nature", 200), ("nature", 512),
                                        ("cartpole_mlp", 32), ("mlp_vec", 100)])
 def test_forward_backward_matches_oracle(netname, B):
     net = NETS[netname]()
