@@ -114,9 +114,15 @@ _SIGS = {
     "acme_replay_create": (c_i32, [ctypes.POINTER(ReplayConfig), ctypes.POINTER(c_vp)]),
     "acme_replay_destroy": (c_i32, [c_vp]),
     "acme_replay_insert": (c_i32, [c_vp, ctypes.POINTER(c_vp), c_i64, c_vp, c_i32, c_vp, c_vp]),
+    "acme_replay_stage_capacity": (c_i64, [c_vp]),
+    "acme_replay_stage": (c_i32, [c_vp, c_i64, ctypes.POINTER(c_vp)]),
+    "acme_replay_commit": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "acme_replay_sync_inserts": (c_i32, [c_vp]),
     "acme_replay_fill_synthetic": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_u64, c_vp]),
     "acme_replay_sample": (c_i32, [c_vp, c_i64, c_u64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "acme_replay_gather": (c_i32, [c_vp, c_vp, c_i64, ctypes.POINTER(c_vp), c_vp]),
+    "acme_replay_sample_gather": (c_i32, [c_vp, c_i64, c_u64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                          ctypes.POINTER(c_vp), c_vp]),
     "acme_r2d2_priorities": (c_i32, [c_vp, c_i32, c_i32, ctypes.c_double, c_vp, c_vp]),
     "acme_r2d2_importance_weights": (c_i32, [c_vp, c_i32, c_i64, ctypes.c_double, c_vp, c_vp]),
     "acme_frames_expand": (c_i32, [c_vp, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp, c_vp]),

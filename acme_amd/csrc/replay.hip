@@ -33,6 +33,26 @@
 
 using namespace acme;
 
+// Host inserts (the actor side, adders/reverb/transition.py:119-165 -> one item per env
+// step) go through a ring of pinned staging chunks and the table's own non-blocking side
+// stream: the caller's thread packs items into a pinned chunk (or writes them there
+// directly, acme_replay_stage), acme_replay_commit issues the H2D copies and the tree
+// refresh on the side stream and returns without waiting.  A chunk is reused only after
+// its copies completed (its event), so the host blocks only when PCIe falls 4 chunks behind.
+//
+// Ordering (no per-step event cost on the learner stream):
+//  * every device operation on a caller stream (sample, gather, update_priorities, ...)
+//    first waits on the latest insert's event if that stream has not yet waited for it, so
+//    a sample sees every committed item;
+//  * the streams those operations ran on are remembered; a commit records an event on each
+//    of them (and on the committing caller's stream) and makes the side stream wait, so an
+//    insert never overwrites a slot an earlier-issued gather still reads, nor rescans the
+//    tree concurrently with an earlier priority update.
+// Streams passed to a table must stay alive while the table does (torch streams do).
+constexpr int kStageChunks = 4;
+constexpr int64_t kStageBytes = 32ll << 20;  // per chunk
+constexpr int kMaxReaders = 8;
+
 struct acme_replay {
   acme_replay_config cfg;
   int nlevels = 0;
@@ -47,6 +67,26 @@ struct acme_replay {
   uint8_t* fields[ACME_MAX_FIELDS] = {};
   int64_t inserted = 0;  // total items ever inserted (host side; = next key)
   std::mutex mu;
+  // Insert path.
+  hipStream_t side = nullptr;
+  hipEvent_t insert_event = nullptr;  // recorded on `side` after each commit
+  uint64_t insert_seq = 0;            // commits so far
+  int64_t stage_items = 0;            // items per staging chunk
+  int64_t stage_off[ACME_MAX_FIELDS + 3] = {};  // field rows, then keys, raw prio, leaves
+  uint8_t* stage[kStageChunks] = {};
+  hipEvent_t stage_done[kStageChunks] = {};
+  bool stage_used[kStageChunks] = {};
+  int stage_next = 0;
+  int staged = -1;  // chunk handed out by acme_replay_stage, not yet committed
+  int64_t staged_n = 0;
+  struct Reader {
+    hipStream_t s;
+    hipEvent_t ev;
+    uint64_t waited;  // insert_seq this stream last waited for
+    bool dirty;       // has table work issued since the last commit
+  } readers[kMaxReaders] = {};
+  int nreaders = 0;
+  std::mutex order_mu;
 };
 
 namespace {
@@ -427,6 +467,185 @@ int refresh_range(acme_replay* r, int64_t first_key, int64_t n, hipStream_t st) 
   return ACME_OK;
 }
 
+// Records `st` as a stream that touched the table; the slot is created on first use.  With
+// every slot taken, the oldest stream's work so far is fenced into the side stream now and
+// its slot reused (a correct, slightly earlier fence).
+int reader_slot(acme_replay* r, hipStream_t st, acme_replay::Reader** out) {
+  for (int i = 0; i < r->nreaders; ++i)
+    if (r->readers[i].s == st) {
+      *out = &r->readers[i];
+      return ACME_OK;
+    }
+  acme_replay::Reader* rd;
+  if (r->nreaders < kMaxReaders) {
+    rd = &r->readers[r->nreaders++];
+    ACME_HIP_TRY(hipEventCreateWithFlags(&rd->ev, hipEventDisableTiming));
+  } else {
+    rd = &r->readers[0];
+    if (rd->dirty) {
+      ACME_HIP_TRY(hipEventRecord(rd->ev, rd->s));
+      ACME_HIP_TRY(hipStreamWaitEvent(r->side, rd->ev, 0));
+    }
+    const hipEvent_t ev = rd->ev;
+    std::memmove(&r->readers[0], &r->readers[1], sizeof(acme_replay::Reader) * (kMaxReaders - 1));
+    rd = &r->readers[kMaxReaders - 1];
+    rd->ev = ev;
+  }
+  rd->s = st;
+  rd->waited = 0;
+  rd->dirty = false;
+  *out = rd;
+  return ACME_OK;
+}
+
+// Prologue of every device operation on a caller stream: wait for the latest committed
+// insert (once per stream per commit) and remember the stream for the next commit.
+// size_out (optional): the table size this operation may use (items whose copies it waits for).
+int order_after_inserts(acme_replay* r, hipStream_t st, int64_t* size_out = nullptr) {
+  std::lock_guard<std::mutex> lock(r->order_mu);
+  if (size_out) *size_out = std::min(r->inserted, r->cfg.capacity);
+  if (!r->side) return ACME_OK;  // no host insert has run yet
+  acme_replay::Reader* rd;
+  int rc = reader_slot(r, st, &rd);
+  if (rc != ACME_OK) return rc;
+  if (rd->waited < r->insert_seq) {
+    ACME_HIP_TRY(hipStreamWaitEvent(st, r->insert_event, 0));
+    rd->waited = r->insert_seq;
+  }
+  rd->dirty = true;
+  return ACME_OK;
+}
+
+// Side stream, staging chunks and events, created on the first host insert.
+int ensure_insert_path(acme_replay* r) {
+  if (r->side) return ACME_OK;
+  int64_t item = 0;
+  for (int f = 0; f < r->cfg.num_fields; ++f) item += (r->cfg.field_bytes[f] + 255) / 256 * 256;
+  item += 3 * 8;
+  int64_t n = std::max<int64_t>(1, kStageBytes / std::max<int64_t>(item, 1));
+  n = std::min(n, r->cfg.capacity);
+  int64_t off = 0;
+  for (int f = 0; f < r->cfg.num_fields; ++f) {
+    r->stage_off[f] = off;
+    off += (n * r->cfg.field_bytes[f] + 255) / 256 * 256;
+  }
+  for (int k = 0; k < 3; ++k) {
+    r->stage_off[ACME_MAX_FIELDS + k] = off;
+    off += (n * 8 + 255) / 256 * 256;
+  }
+  for (int c = 0; c < kStageChunks; ++c) {
+    if (hipHostMalloc(reinterpret_cast<void**>(&r->stage[c]), off, hipHostMallocDefault) !=
+        hipSuccess) {
+      set_error("hipHostMalloc of a %lld-byte insert staging chunk failed", (long long)off);
+      return ACME_ERR_OOM;
+    }
+    ACME_HIP_TRY(hipEventCreateWithFlags(&r->stage_done[c], hipEventDisableTiming));
+  }
+  ACME_HIP_TRY(hipEventCreateWithFlags(&r->insert_event, hipEventDisableTiming));
+  r->stage_items = n;
+  ACME_HIP_TRY(hipStreamCreateWithFlags(&r->side, hipStreamNonBlocking));
+  return ACME_OK;
+}
+
+// Next staging chunk, once the copies that last used it have completed.
+int acquire_chunk(acme_replay* r, int* out) {
+  const int c = r->stage_next;
+  r->stage_next = (c + 1) % kStageChunks;
+  if (r->stage_used[c]) ACME_HIP_TRY(hipEventSynchronize(r->stage_done[c]));
+  *out = c;
+  return ACME_OK;
+}
+
+// Issues the n <= stage_items items staged in chunk c: keys, raw priorities and leaf
+// weights into the chunk, the side stream fenced after `after` and every stream that
+// touched the table, H2D copies in at most two ring segments, the tree refresh, events.
+//
+// dev (optional): device rows of the n items; then the copies run on `after` itself (the
+// caller's stream, which owns those buffers) instead of the side stream.  skip: keys
+// consumed before these items (an over-capacity insert).
+int commit_chunk(acme_replay* r, int c, int64_t n, const double* priorities, uint64_t* out_keys,
+                 hipStream_t after, const void* const* dev = nullptr, int64_t skip = 0) {
+  const int64_t C = r->cfg.capacity;
+  const int64_t first_key = r->inserted + skip;
+  uint8_t* base = r->stage[c];
+  uint64_t* hkeys = reinterpret_cast<uint64_t*>(base + r->stage_off[ACME_MAX_FIELDS]);
+  double* hprio = reinterpret_cast<double*>(base + r->stage_off[ACME_MAX_FIELDS + 1]);
+  double* hleaf = reinterpret_cast<double*>(base + r->stage_off[ACME_MAX_FIELDS + 2]);
+  for (int64_t i = 0; i < n; ++i) {
+    const double p = priorities ? priorities[i] : 1.0;
+    if (!(p >= 0.0)) {
+      set_error("priority %g at item %lld must be >= 0", p, (long long)i);
+      return ACME_ERR_INVALID;
+    }
+    hkeys[i] = (uint64_t)(first_key + i);
+    hprio[i] = p;
+    hleaf[i] = r->cfg.sampler == ACME_SAMPLER_PRIORITIZED
+                   ? det_pow_priority(p, r->cfg.priority_exponent)
+                   : 1.0;
+  }
+  if (out_keys) std::memcpy(out_keys, hkeys, n * sizeof(uint64_t));
+  {
+    std::lock_guard<std::mutex> lock(r->order_mu);
+    acme_replay::Reader* rd;
+    int rc = reader_slot(r, after, &rd);
+    if (rc != ACME_OK) return rc;
+    hipStream_t st = dev ? after : r->side;
+    if (dev) {  // the caller's stream first catches up with earlier host inserts
+      if (rd->waited < r->insert_seq) ACME_HIP_TRY(hipStreamWaitEvent(st, r->insert_event, 0));
+    } else {
+      rd->dirty = true;  // the committing caller's own earlier work (e.g. frame uploads)
+    }
+    for (int i = 0; i < r->nreaders; ++i) {
+      acme_replay::Reader& x = r->readers[i];
+      if (!x.dirty || x.s == st) continue;
+      ACME_HIP_TRY(hipEventRecord(x.ev, x.s));
+      ACME_HIP_TRY(hipStreamWaitEvent(st, x.ev, 0));
+      x.dirty = false;
+    }
+  }
+  hipStream_t st = dev ? after : r->side;
+  int64_t done = 0;
+  while (done < n) {
+    const int64_t slot = (first_key + done) % C;
+    const int64_t len = std::min(n - done, C - slot);
+    for (int f = 0; f < r->cfg.num_fields; ++f) {
+      const int64_t b = r->cfg.field_bytes[f];
+      if (dev)
+        ACME_HIP_TRY(hipMemcpyAsync(r->fields[f] + slot * b,
+                                    static_cast<const uint8_t*>(dev[f]) + done * b, len * b,
+                                    hipMemcpyDeviceToDevice, st));
+      else
+        ACME_HIP_TRY(hipMemcpyAsync(r->fields[f] + slot * b, base + r->stage_off[f] + done * b,
+                                    len * b, hipMemcpyHostToDevice, st));
+    }
+    ACME_HIP_TRY(hipMemcpyAsync(r->keys + slot, hkeys + done, len * sizeof(uint64_t),
+                                hipMemcpyHostToDevice, st));
+    ACME_HIP_TRY(hipMemcpyAsync(r->raw_prio + slot, hprio + done, len * sizeof(double),
+                                hipMemcpyHostToDevice, st));
+    ACME_HIP_TRY(hipMemcpyAsync(r->levels[0] + slot, hleaf + done, len * sizeof(double),
+                                hipMemcpyHostToDevice, st));
+    done += len;
+  }
+  int rc = refresh_range(r, first_key, n, st);
+  if (rc != ACME_OK) return rc;
+  ACME_HIP_TRY(hipEventRecord(r->stage_done[c], st));
+  r->stage_used[c] = true;
+  {
+    std::lock_guard<std::mutex> lock(r->order_mu);
+    ACME_HIP_TRY(hipEventRecord(r->insert_event, st));
+    r->insert_seq += 1;
+    r->inserted += skip + n;
+    if (dev) {  // the caller's stream is ordered after this insert already
+      acme_replay::Reader* rd;
+      int rc2 = reader_slot(r, st, &rd);
+      if (rc2 != ACME_OK) return rc2;
+      rd->waited = r->insert_seq;
+      rd->dirty = true;
+    }
+  }
+  return ACME_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -493,6 +712,13 @@ int acme_replay_destroy(acme_replay* r) {
   if (r->upd_valid) (void)hipFree(r->upd_valid);
   for (int f = 0; f < ACME_MAX_FIELDS; ++f)
     if (r->fields[f]) (void)hipFree(r->fields[f]);
+  for (int c = 0; c < kStageChunks; ++c) {
+    if (r->stage[c]) (void)hipHostFree(r->stage[c]);
+    if (r->stage_done[c]) (void)hipEventDestroy(r->stage_done[c]);
+  }
+  for (int i = 0; i < r->nreaders; ++i) (void)hipEventDestroy(r->readers[i].ev);
+  if (r->insert_event) (void)hipEventDestroy(r->insert_event);
+  if (r->side) (void)hipStreamDestroy(r->side);
   delete r;
   return ACME_OK;
 }
@@ -527,6 +753,8 @@ int acme_replay_restore(acme_replay* r, int64_t inserted, void* stream) {
   ACME_CHECK_ARG(inserted >= 0, "negative insert count");
   std::lock_guard<std::mutex> lock(r->mu);
   hipStream_t st = as_stream(stream);
+  int rc = order_after_inserts(r, st);
+  if (rc != ACME_OK) return rc;
   const int64_t C = r->cfg.capacity, live = std::min(inserted, C);
   const int64_t n = r->level_size[0];
   restore_leaves_kernel<<<(unsigned)ceil_div(n, 256), 256, 0, st>>>(
@@ -539,7 +767,54 @@ int acme_replay_restore(acme_replay* r, int64_t inserted, void* stream) {
         r->levels[l - 1], r->levels[l], 0, count, nullptr, nullptr, 0);
     ACME_LAUNCH_CHECK();
   }
+  std::lock_guard<std::mutex> olock(r->order_mu);
   r->inserted = inserted;
+  return ACME_OK;
+}
+
+int64_t acme_replay_stage_capacity(acme_replay* r) {
+  if (!r) return 0;
+  std::lock_guard<std::mutex> lock(r->mu);
+  if (ensure_insert_path(r) != ACME_OK) return 0;
+  return r->stage_items;
+}
+
+int acme_replay_stage(acme_replay* r, int64_t n, void** field_ptrs) {
+  ACME_CHECK_ARG(r && field_ptrs, "null argument");
+  std::lock_guard<std::mutex> lock(r->mu);
+  int rc = ensure_insert_path(r);
+  if (rc != ACME_OK) return rc;
+  ACME_CHECK_ARG(n >= 1 && n <= r->stage_items, "stage: n = %lld must be in [1, %lld]",
+                 (long long)n, (long long)r->stage_items);
+  ACME_CHECK_ARG(r->staged < 0, "stage: the previously staged chunk was not committed");
+  int c;
+  rc = acquire_chunk(r, &c);
+  if (rc != ACME_OK) return rc;
+  for (int f = 0; f < r->cfg.num_fields; ++f) field_ptrs[f] = r->stage[c] + r->stage_off[f];
+  r->staged = c;
+  r->staged_n = n;
+  return ACME_OK;
+}
+
+int acme_replay_commit(acme_replay* r, int64_t n, const double* priorities, uint64_t* out_keys,
+                       void* stream) {
+  ACME_CHECK_ARG(r, "null replay");
+  std::lock_guard<std::mutex> lock(r->mu);
+  ACME_CHECK_ARG(r->staged >= 0, "commit without a staged chunk");
+  ACME_CHECK_ARG(n >= 0 && n <= r->staged_n, "commit: n = %lld exceeds the %lld staged items",
+                 (long long)n, (long long)r->staged_n);
+  const int c = r->staged;
+  r->staged = -1;
+  if (n == 0) {
+    r->stage_used[c] = false;
+    return ACME_OK;
+  }
+  return commit_chunk(r, c, n, priorities, out_keys, as_stream(stream));
+}
+
+int acme_replay_sync_inserts(acme_replay* r) {
+  ACME_CHECK_ARG(r, "null replay");
+  if (r->side) ACME_HIP_TRY(hipStreamSynchronize(r->side));
   return ACME_OK;
 }
 
@@ -549,51 +824,40 @@ int acme_replay_insert(acme_replay* r, const void* const* fields, int64_t n,
   ACME_CHECK_ARG(r && (n == 0 || fields), "null argument");
   ACME_CHECK_ARG(n >= 0, "negative item count");
   if (n == 0) return ACME_OK;
+  for (int64_t i = 0; priorities && i < n; ++i)
+    ACME_CHECK_ARG(priorities[i] >= 0.0, "priority %g at item %lld must be >= 0", priorities[i],
+                   (long long)i);
   std::lock_guard<std::mutex> lock(r->mu);
+  int rc = ensure_insert_path(r);
+  if (rc != ACME_OK) return rc;
+  ACME_CHECK_ARG(r->staged < 0, "insert while a staged chunk is uncommitted");
   hipStream_t st = as_stream(stream);
   const int64_t C = r->cfg.capacity;
-  const int64_t first_key = r->inserted;
-  // Host-side metadata: keys, raw priorities, leaf weights (same det_pow code as device).
-  std::vector<uint64_t> hkeys(n);
-  std::vector<double> hprio(n), hleaf(n);
-  for (int64_t i = 0; i < n; ++i) {
-    hkeys[i] = (uint64_t)(first_key + i);
-    const double p = priorities ? priorities[i] : 1.0;
-    if (!(p >= 0.0)) {
-      set_error("priority %g at item %lld must be >= 0", p, (long long)i);
-      return ACME_ERR_INVALID;
-    }
-    hprio[i] = p;
-    hleaf[i] = r->cfg.sampler == ACME_SAMPLER_PRIORITIZED
-                   ? det_pow_priority(p, r->cfg.priority_exponent)
-                   : 1.0;
-  }
-  if (out_keys) std::memcpy(out_keys, hkeys.data(), n * sizeof(uint64_t));
-  // Only the last C items survive an over-capacity insert.
-  int64_t skip = n > C ? n - C : 0;
-  int64_t done = skip;
-  const hipMemcpyKind kind = src_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
-  while (done < n) {
-    const int64_t slot = (first_key + done) % C;
-    const int64_t len = std::min(n - done, C - slot);
+  // Only the last C items of an over-capacity insert survive: the first `skip` consume
+  // their keys (reported in out_keys) but never land.
+  const int64_t skip = n > C ? n - C : 0;
+  if (out_keys)
+    for (int64_t i = 0; i < skip; ++i) out_keys[i] = (uint64_t)(r->inserted + i);
+  int64_t pending_skip = skip;
+  for (int64_t done = skip; done < n;) {
+    const int64_t len = std::min(n - done, r->stage_items);
+    int c;
+    rc = acquire_chunk(r, &c);
+    if (rc != ACME_OK) return rc;
+    const void* dev[ACME_MAX_FIELDS] = {};
     for (int f = 0; f < r->cfg.num_fields; ++f) {
       const int64_t b = r->cfg.field_bytes[f];
       const uint8_t* src = static_cast<const uint8_t*>(fields[f]) + done * b;
-      ACME_HIP_TRY(hipMemcpyAsync(r->fields[f] + slot * b, src, len * b, kind, st));
+      if (src_on_device) dev[f] = src;  // HBM rows: copied on the caller's stream
+      else std::memcpy(r->stage[c] + r->stage_off[f], src, len * b);  // pack into pinned
     }
-    ACME_HIP_TRY(hipMemcpyAsync(r->keys + slot, hkeys.data() + done, len * sizeof(uint64_t),
-                                hipMemcpyHostToDevice, st));
-    ACME_HIP_TRY(hipMemcpyAsync(r->raw_prio + slot, hprio.data() + done, len * sizeof(double),
-                                hipMemcpyHostToDevice, st));
-    ACME_HIP_TRY(hipMemcpyAsync(r->levels[0] + slot, hleaf.data() + done, len * sizeof(double),
-                                hipMemcpyHostToDevice, st));
+    rc = commit_chunk(r, c, len, priorities ? priorities + done : nullptr,
+                      out_keys ? out_keys + done : nullptr, st,
+                      src_on_device ? dev : nullptr, pending_skip);
+    if (rc != ACME_OK) return rc;
+    pending_skip = 0;
     done += len;
   }
-  int rc = refresh_range(r, first_key, n, st);
-  if (rc != ACME_OK) return rc;
-  // The host vectors above are pageable: make sure the copies have consumed them.
-  ACME_HIP_TRY(hipStreamSynchronize(st));
-  r->inserted += n;
   return ACME_OK;
 }
 
@@ -610,6 +874,8 @@ int acme_replay_fill_synthetic(acme_replay* r, int64_t n, int32_t layout, int32_
   if (n == 0) return ACME_OK;
   std::lock_guard<std::mutex> lock(r->mu);
   hipStream_t st = as_stream(stream);
+  int rc0 = order_after_inserts(r, st);
+  if (rc0 != ACME_OK) return rc0;
   const int64_t C = r->cfg.capacity;
   const int64_t first_key = r->inserted;
   int64_t skip = n > C ? n - C : 0;
@@ -651,6 +917,7 @@ int acme_replay_fill_synthetic(acme_replay* r, int64_t n, int32_t layout, int32_
   }
   int rc = refresh_range(r, k0, cnt, st);
   if (rc != ACME_OK) return rc;
+  std::lock_guard<std::mutex> olock(r->order_mu);
   r->inserted += n;
   return ACME_OK;
 }
@@ -660,12 +927,14 @@ int acme_replay_sample(acme_replay* r, int64_t batch, uint64_t step_counter, int
                        double* priorities, void* stream) {
   ACME_CHECK_ARG(r && slots, "null argument");
   ACME_CHECK_ARG(batch > 0 && batch <= (int64_t(1) << 31), "batch must be in [1, 2^31]");
-  const int64_t size = acme_replay_size(r);
+  hipStream_t st = as_stream(stream);
+  int64_t size = 0;
+  int rc = order_after_inserts(r, st, &size);
+  if (rc != ACME_OK) return rc;
   if (size <= 0) {
     set_error("cannot sample from an empty table (rate limiter MinSize(1))");
     return ACME_ERR_EMPTY;
   }
-  hipStream_t st = as_stream(stream);
   ACME_PROF("replay_sample", st, 0.0, (double)batch * (r->cfg.sampler == ACME_SAMPLER_PRIORITIZED ? 512.0 * r->nlevels + 40.0 : 48.0));
   if (r->cfg.sampler == ACME_SAMPLER_PRIORITIZED) {
     TreeView tv;
@@ -688,6 +957,8 @@ int acme_replay_gather(acme_replay* r, const int64_t* slots, int64_t batch,
   ACME_CHECK_ARG(r && slots && out_fields, "null argument");
   ACME_CHECK_ARG(batch > 0 && batch < (int64_t(1) << 31), "bad batch");
   hipStream_t st = as_stream(stream);
+  int rc = order_after_inserts(r, st);
+  if (rc != ACME_OK) return rc;
   GatherArgs g = {};
   for (int f = 0; f < r->cfg.num_fields; ++f) {
     g.src[f] = r->fields[f];
@@ -702,6 +973,18 @@ int acme_replay_gather(acme_replay* r, const int64_t* slots, int64_t batch,
   return ACME_OK;
 }
 
+int acme_replay_sample_gather(acme_replay* r, int64_t batch, uint64_t step_counter,
+                              int64_t* slots, uint64_t* keys, double* probabilities,
+                              int64_t* table_size, double* priorities, void* const* out_fields,
+                              void* stream) {
+  ACME_CHECK_ARG(r, "null replay");
+  std::lock_guard<std::mutex> lock(r->mu);  // no insert commits between the two launches
+  int rc = acme_replay_sample(r, batch, step_counter, slots, keys, probabilities, table_size,
+                              priorities, stream);
+  if (rc != ACME_OK) return rc;
+  return acme_replay_gather(r, slots, batch, out_fields, stream);
+}
+
 int acme_replay_update_priorities(acme_replay* r, const uint64_t* keys, const double* prios,
                                   int64_t n, void* stream) {
   ACME_CHECK_ARG(r && (n == 0 || (keys && prios)), "null argument");
@@ -709,6 +992,8 @@ int acme_replay_update_priorities(acme_replay* r, const uint64_t* keys, const do
   if (n == 0) return ACME_OK;
   hipStream_t st = as_stream(stream);
   std::lock_guard<std::mutex> lock(r->mu);
+  int rc = order_after_inserts(r, st);
+  if (rc != ACME_OK) return rc;
   // Scratch for resolved slots / validity (grown on demand; growth drains the device).
   if (n > r->upd_cap) {
     if (r->upd_slots) {

@@ -12,10 +12,12 @@ DQN agent asks for 4, agents/tf/dqn/agent.py:50): with P > 0 the sample and gath
 k + P are issued on the dataset's own stream when batch k is handed out, ordered after
 every kernel already queued on the caller's stream (so they see the priority updates of
 steps < k, like Reverb's prefetched samples), and the caller's stream waits only for the
-batch it receives.  Writers of the table (priority updates, inserts) in turn order the
-caller's stream after the last issued prefetch (Table._after_readers), so a queued draw
-never overlaps a tree update or a slot overwrite.  The draw order, and so every sampled
-index, is deterministic.
+batch it receives.  Priority updates in turn order the caller's stream after the last
+issued prefetch (Table._after_readers), and host inserts are ordered after every stream
+that has read the table (inside the native table, csrc/replay.hip), so a queued draw never
+overlaps a tree update or a slot overwrite; a draw and its row gather are one unit with
+respect to inserts (acme_replay_sample_gather).  The draw order, and so every sampled
+index, is deterministic for a given interleaving of inserts.
 
 `server_address` may be the in-process address ('localhost:<port>'), a Server, a Table
 or a Client.  Sampling is deterministic given the table seed: draw i uses Philox
@@ -124,12 +126,19 @@ class _TableIterator:
     def __iter__(self):
         return self
 
-    def _gather(self, L, h, slots, ptrs, st):
+    def _draw(self, L, h, raw, ptrs, st):
+        """Sample + gather of one batch as a unit: no insert lands between the draw and the
+        row copy (actor threads may be inserting), so each row is that of its reported key."""
         from acme_amd._lib import check
-        if isinstance(self._t, replay.FrameTable):  # stacks rebuilt from stored frames
-            self._t.gather_into(slots, self._B, ptrs, st)
+        t = self._t
+        step = t.next_draw() & 0xFFFFFFFFFFFFFFFF
+        if isinstance(t, replay.FrameTable):  # stacks rebuilt from stored frames
+            with t._mu:  # noqa: SLF001  (inserts commit under the table lock)
+                check(L.acme_replay_sample(h, self._B, step, *raw, st), "replay sample")
+                t.gather_into(raw[0], self._B, ptrs, st)
         else:
-            check(L.acme_replay_gather(h, slots, self._B, ptrs, st), "replay gather")
+            check(L.acme_replay_sample_gather(h, self._B, step, *raw, ptrs, st),
+                  "replay sample")
 
     def __next__(self) -> replay.ReplaySample:
         from acme_amd._lib import check, lib, stream_ptr
@@ -143,10 +152,7 @@ class _TableIterator:
         if self._P == 0:
             raw, ptrs, sample = self._slots[self._which][:3]
             self._which ^= 1
-            st = stream_ptr()
-            check(L.acme_replay_sample(h, self._B, t.next_draw() & 0xFFFFFFFFFFFFFFFF, *raw, st),
-                  "replay sample")
-            self._gather(L, h, raw[0], ptrs, st)
+            self._draw(L, h, raw, ptrs, stream_ptr())
             return sample
         # Prefetch: order the dataset stream after everything queued so far on the caller's
         # stream (inserts, earlier learner steps and their priority updates), top the queue
@@ -163,9 +169,7 @@ class _TableIterator:
             i = self._next_slot
             self._next_slot = (i + 1) % (self._P + 2)
             raw, ptrs = self._slots[i][:2]
-            check(L.acme_replay_sample(h, self._B, t.next_draw() & 0xFFFFFFFFFFFFFFFF, *raw, st),
-                  "replay sample")
-            self._gather(L, h, raw[0], ptrs, st)
+            self._draw(L, h, raw, ptrs, st)
             self._ready[i].record(side)
             self._queue.append(i)
             t.set_reader_event(self._ready[i])

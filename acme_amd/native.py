@@ -93,6 +93,36 @@ class NativeReplay:
               "replay insert")
         return keys
 
+    def stage_capacity(self) -> int:
+        """Items per pinned staging chunk (acme_replay_stage_capacity)."""
+        n = int(lib().acme_replay_stage_capacity(self._h))
+        if n <= 0:
+            check(_lib.ACME_ERR_HIP, "replay staging")
+        return n
+
+    def stage(self, n: int) -> List[np.ndarray]:
+        """Pinned host rows for n items: one writable uint8 [n, field_bytes[f]] array per
+        field (valid until the matching commit)."""
+        ptrs = (ctypes.c_void_p * len(self.field_bytes))()
+        check(lib().acme_replay_stage(self._h, int(n), ptrs), "replay stage")
+        return [np.ctypeslib.as_array((ctypes.c_uint8 * (n * b)).from_address(ptrs[i]))
+                .reshape(n, b) for i, b in enumerate(self.field_bytes)]
+
+    def commit(self, n: int, priorities: Optional[np.ndarray] = None, stream=None) -> np.ndarray:
+        """Issues the first n staged items (side-stream H2D, no host wait); returns keys."""
+        keys = np.empty(n, np.uint64)
+        pr = None
+        if priorities is not None:
+            pr = np.ascontiguousarray(priorities, np.float64)
+            if pr.shape != (n,):
+                raise ValueError("priorities must have shape [n]")
+        check(lib().acme_replay_commit(self._h, int(n), None if pr is None else pr.ctypes.data,
+                                       keys.ctypes.data, stream_ptr(stream)), "replay commit")
+        return keys
+
+    def sync_inserts(self) -> None:
+        check(lib().acme_replay_sync_inserts(self._h), "replay sync_inserts")
+
     def fill_synthetic(self, n: int, layout: int, num_actions: int = 18, seed: int = 0,
                        stream=None) -> None:
         check(lib().acme_replay_fill_synthetic(self._h, int(n), int(layout), int(num_actions),

@@ -224,19 +224,26 @@ class Table:
             torch.cuda.current_stream(self._native.device).wait_event(ev)
 
     def flush(self) -> None:
+        """Writes the pending items straight into the table's pinned staging chunks and
+        commits them: hipMemcpyAsync on the table's side stream, no host wait.  The native
+        table orders the copies after every stream that has read it (a queued prefetch
+        gather never sees a slot overwritten under it) and every later sample after them."""
         with self._mu:
             if not self._pending:
                 return
-            self._after_readers()
-            n = len(self._pending)
-            cols = []
-            for i, f in enumerate(self._fields):
-                buf = np.zeros((n, f.row_bytes), np.uint8)
-                for r, row in enumerate(self._pending):
-                    buf[r, :f.nbytes] = np.frombuffer(np.ascontiguousarray(row[i]).tobytes(),
-                                                      np.uint8)
-                cols.append(buf)
-            self._native.insert(cols, np.asarray(self._pending_prio, np.float64))
+            nat = self._native
+            cap = nat.stage_capacity()
+            prio = np.asarray(self._pending_prio, np.float64)
+            for s in range(0, len(self._pending), cap):
+                rows = self._pending[s:s + cap]
+                bufs = nat.stage(len(rows))
+                for i, f in enumerate(self._fields):
+                    b = bufs[i]
+                    for r, row in enumerate(rows):
+                        b[r, :f.nbytes] = np.ascontiguousarray(row[i]).reshape(-1).view(np.uint8)
+                    if f.row_bytes > f.nbytes:
+                        b[:, f.nbytes:] = 0
+                nat.commit(len(rows), prio[s:s + cap])
             self._pending, self._pending_prio = [], []
 
     # -- checkpointing (optional replay state; core.Saveable interface)

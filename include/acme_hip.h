@@ -23,9 +23,10 @@
  *                       three Q forwards, double-Q n-step TD, Huber, f64 IS weights,
  *                       backward, snt.Adam, post-step periodic target copy.
  *
- * Threading: one learner stream; acme_replay_insert may be called from actor threads
- * (internal mutex).  Ordering between an insert's side stream and the sampling stream
- * is the caller's (the Python Table records an event after each insert flush).
+ * Threading: one learner stream; acme_replay_insert / _stage / _commit may be called from
+ * actor threads (internal mutex).  Host inserts run on the table's own side stream; the
+ * table orders them against every stream that samples, gathers or updates priorities
+ * (see acme_replay_insert), with no per-step event on the learner stream.
  */
 #ifndef ACME_HIP_H_
 #define ACME_HIP_H_
@@ -89,13 +90,30 @@ typedef struct acme_replay acme_replay;
 int acme_replay_create(const acme_replay_config* cfg, acme_replay** out);
 int acme_replay_destroy(acme_replay* r);
 
-/* Insert n items.  fields[f] points at n * field_bytes[f] contiguous bytes, on the
- * host (pinned for true asynchrony) when src_on_device == 0, else on the device.
- * priorities: n raw priorities (host).  out_keys (host, optional): the keys assigned.
- * Items go to ring slots (insert_count + i) % capacity (Fifo remover). */
+/* Insert n items (replaces Writer.append + create_item, adders/reverb/transition.py:119-165,
+ * one item per environment step; Reverb's insert RPC).  fields[f] points at
+ * n * field_bytes[f] contiguous bytes, on the host when src_on_device == 0, else on the
+ * device.  priorities: n raw priorities (host, NULL = 1.0).  out_keys (host, optional): the
+ * keys assigned.  Items go to ring slots (insert_count + i) % capacity (Fifo remover).
+ * Host rows are packed into the table's pinned staging ring and copied by hipMemcpyAsync
+ * on the table's own side stream; the call returns without waiting for the copies.  The
+ * insert is ordered after the work already issued on `stream` and on every stream that has
+ * used the table; every later sample / gather / update_priorities (any stream) is ordered
+ * after it.  Device rows are copied on `stream` itself. */
 int acme_replay_insert(acme_replay* r, const void* const* fields, int64_t n,
                        const double* priorities, int32_t src_on_device,
                        uint64_t* out_keys, void* stream);
+
+/* Zero-copy form of the host insert: acme_replay_stage hands out pinned host pointers
+ * field_ptrs[f] with room for n <= acme_replay_stage_capacity(r) items (blocking only while
+ * that staging chunk's previous copies are in flight); the caller writes the rows there
+ * and acme_replay_commit(r, m <= n, ...) issues them exactly as acme_replay_insert does. */
+int64_t acme_replay_stage_capacity(acme_replay* r);
+int acme_replay_stage(acme_replay* r, int64_t n, void** field_ptrs);
+int acme_replay_commit(acme_replay* r, int64_t n, const double* priorities, uint64_t* out_keys,
+                       void* stream);
+/* Host wait for every issued insert (tests, checkpoints, shutdown). */
+int acme_replay_sync_inserts(acme_replay* r);
 
 /* Fill n items with synthetic data generated on the device (benchmark/test helper,
  * no host traffic).  layout: 0 = DQN Atari transition (o_tm1 u8, a i32, r f32, d f32,
@@ -116,6 +134,14 @@ int acme_replay_sample(acme_replay* r, int64_t batch, uint64_t step_counter,
  * (batch * field_bytes[f] bytes each). */
 int acme_replay_gather(acme_replay* r, const int64_t* slots, int64_t batch,
                        void* const* out_fields, void* stream);
+
+/* acme_replay_sample then acme_replay_gather as one unit: no insert is committed between
+ * the draw and the row copy, so every gathered row is the row of the key reported for it
+ * even while actor threads insert (the two separate calls leave that to the caller). */
+int acme_replay_sample_gather(acme_replay* r, int64_t batch, uint64_t step_counter,
+                              int64_t* slots, uint64_t* keys, double* probabilities,
+                              int64_t* table_size, double* priorities, void* const* out_fields,
+                              void* stream);
 
 /* Frame-deduplicated observations: rebuild `batch` stacked
  * observations out[b] = stack(frames[idx[b][0..stack-1]], axis=-1) (uint8 HWC, as
