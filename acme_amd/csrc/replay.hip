@@ -24,7 +24,9 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <condition_variable>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "common.h"
@@ -79,6 +81,8 @@ struct acme_replay {
   int stage_next = 0;
   int staged = -1;  // chunk handed out by acme_replay_stage, not yet committed
   int64_t staged_n = 0;
+  std::thread::id staged_by;         // the thread that must commit it
+  std::condition_variable stage_cv;  // other threads wait here for the commit
   struct Reader {
     hipStream_t s;
     hipEvent_t ev;
@@ -781,18 +785,23 @@ int64_t acme_replay_stage_capacity(acme_replay* r) {
 
 int acme_replay_stage(acme_replay* r, int64_t n, void** field_ptrs) {
   ACME_CHECK_ARG(r && field_ptrs, "null argument");
-  std::lock_guard<std::mutex> lock(r->mu);
+  std::unique_lock<std::mutex> lock(r->mu);
   int rc = ensure_insert_path(r);
   if (rc != ACME_OK) return rc;
   ACME_CHECK_ARG(n >= 1 && n <= r->stage_items, "stage: n = %lld must be in [1, %lld]",
                  (long long)n, (long long)r->stage_items);
-  ACME_CHECK_ARG(r->staged < 0, "stage: the previously staged chunk was not committed");
+  const std::thread::id me = std::this_thread::get_id();
+  ACME_CHECK_ARG(r->staged < 0 || r->staged_by != me,
+                 "stage: this thread's previously staged chunk was not committed");
+  // Another writer thread's chunk is outstanding: wait for its commit.
+  r->stage_cv.wait(lock, [r] { return r->staged < 0; });
   int c;
   rc = acquire_chunk(r, &c);
   if (rc != ACME_OK) return rc;
   for (int f = 0; f < r->cfg.num_fields; ++f) field_ptrs[f] = r->stage[c] + r->stage_off[f];
   r->staged = c;
   r->staged_n = n;
+  r->staged_by = me;
   return ACME_OK;
 }
 
@@ -800,15 +809,14 @@ int acme_replay_commit(acme_replay* r, int64_t n, const double* priorities, uint
                        void* stream) {
   ACME_CHECK_ARG(r, "null replay");
   std::lock_guard<std::mutex> lock(r->mu);
-  ACME_CHECK_ARG(r->staged >= 0, "commit without a staged chunk");
+  ACME_CHECK_ARG(r->staged >= 0 && r->staged_by == std::this_thread::get_id(),
+                 "commit without a chunk staged by this thread");
   ACME_CHECK_ARG(n >= 0 && n <= r->staged_n, "commit: n = %lld exceeds the %lld staged items",
                  (long long)n, (long long)r->staged_n);
   const int c = r->staged;
   r->staged = -1;
-  if (n == 0) {
-    r->stage_used[c] = false;
-    return ACME_OK;
-  }
+  r->stage_cv.notify_all();
+  if (n == 0) return ACME_OK;  // the chunk's last copies (if any) are still tracked
   return commit_chunk(r, c, n, priorities, out_keys, as_stream(stream));
 }
 
@@ -827,10 +835,12 @@ int acme_replay_insert(acme_replay* r, const void* const* fields, int64_t n,
   for (int64_t i = 0; priorities && i < n; ++i)
     ACME_CHECK_ARG(priorities[i] >= 0.0, "priority %g at item %lld must be >= 0", priorities[i],
                    (long long)i);
-  std::lock_guard<std::mutex> lock(r->mu);
+  std::unique_lock<std::mutex> lock(r->mu);
   int rc = ensure_insert_path(r);
   if (rc != ACME_OK) return rc;
-  ACME_CHECK_ARG(r->staged < 0, "insert while a staged chunk is uncommitted");
+  ACME_CHECK_ARG(r->staged < 0 || r->staged_by != std::this_thread::get_id(),
+                 "insert while this thread's staged chunk is uncommitted");
+  r->stage_cv.wait(lock, [r] { return r->staged < 0; });
   hipStream_t st = as_stream(stream);
   const int64_t C = r->cfg.capacity;
   // Only the last C items of an over-capacity insert survive: the first `skip` consume

@@ -43,9 +43,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--workload", choices=("dqn", "d4pg", "impala"), default="dqn",
+    p.add_argument("--workload", choices=("dqn", "d4pg", "impala", "insert"), default="dqn",
                    help="dqn: the headline config (BASELINE configs[1]); d4pg: configs[2]; "
-                        "impala: configs[3] (learner side)")
+                        "impala: configs[3] (learner side); insert: host inserts into the "
+                        "configs[1] table while its learner steps")
     p.add_argument("--batch", type=int, default=0, help="default 512 (dqn) / 256 (d4pg)")
     p.add_argument("--replay-size", type=int, default=1_000_000)
     p.add_argument("--num-actions", type=int, default=18)
@@ -209,8 +210,132 @@ def setup_dqn(args, world, rank, dev):
                 "obs": "uint8[84,84,4]", "num_actions": A,
                 "sampler": "prioritized(alpha=0.6), IS beta=0.2", "prefetch_size": args.prefetch,
                 "parallelism": f"dp{world}"})
+    meta["_table"] = table
     return (learner.step, B, meta, lambda: float(learner.native.loss.item()),
             lambda: cpu_baseline(B, A, args.cpu_baseline_seconds))
+
+
+def insert_bench(args, dev):
+    """Actor-side insert path (north star: pinned hipMemcpyAsync on a side stream) into the
+    1M-slot table of the headline config while the DQN learner steps.  Three measurements:
+    learner steps alone; the same steps with a host thread inserting through the adder-facing
+    Table.insert (one item per call, as Writer.create_item; flushes of 256 items into the
+    pinned staging ring); and with a host thread committing whole staged chunks (the
+    native stage/commit path, bulk).  Inserts/s counts items whose commit returned inside
+    the timed window of learner steps."""
+    import threading
+    step, B, meta, _, _ = setup_dqn(args, 1, 0, dev)
+    table = meta["_table"]
+    nat = table.native
+    rng = np.random.default_rng(0)
+    pool = 512
+    obs = rng.integers(0, 256, (pool, 84, 84, 4), dtype=np.uint8)
+    items = [(obs[i], np.int32(i % 18), np.float32(0.5), np.float32(0.99 ** 4),
+              obs[(i + 5) % pool]) for i in range(pool)]
+    rows = [obs.reshape(pool, -1), np.arange(pool, dtype=np.int32).view(np.uint8).reshape(pool, 4),
+            np.full(pool, 0.5, np.float32).view(np.uint8).reshape(pool, 4),
+            np.full(pool, 0.99 ** 4, np.float32).view(np.uint8).reshape(pool, 4),
+            np.roll(obs.reshape(pool, -1), -5, axis=0)]
+
+    done = [0]
+
+    def timed_steps(n):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(n):
+            step()
+            done[0] += 1
+        torch.cuda.synchronize(dev)
+        return time.perf_counter() - t0
+
+    def with_inserter(body):
+        count, stop = [0], threading.Event()
+
+        def run():
+            while not stop.is_set():
+                count[0] += body()
+        th = threading.Thread(target=run, daemon=True)
+        th.start()
+        try:
+            time.sleep(0.2)  # the inserter reaches its steady state
+            c0 = count[0]
+            dt = timed_steps(args.steps)
+            c1 = count[0]
+        finally:
+            stop.set()
+            th.join()
+        nat.sync_inserts()
+        return dt, (c1 - c0) / dt
+
+    def adder_body(n=64):
+        for i in range(n):
+            table.insert(items[(done[0] + i) % pool], 1.0)
+        return n
+
+    # The reference agent's ratio: one insert per samples_per_insert = 32 sampled items
+    # (agents/tf/dqn/agent.py:52, agents/agent.py:45-89), i.e. B / 32 items per step.
+    per_step = B // 32
+    issued = [0]
+
+    def paced_adder_body():
+        if issued[0] >= (done[0] + 1) * per_step:
+            time.sleep(50e-6)
+            return 0
+        issued[0] += adder_body(per_step)
+        return per_step
+
+    chunk = min(nat.stage_capacity(), pool)
+
+    def bulk_body():
+        bufs = nat.stage(chunk)
+        for b, src in zip(bufs, rows):
+            np.copyto(b, src[:chunk])
+        nat.commit(chunk, None)
+        return chunk
+
+    for _ in range(args.warmup):
+        step()
+    t_alone = timed_steps(args.steps)
+    issued[0] = done[0] * per_step
+    t_paced, r_paced = with_inserter(paced_adder_body)
+    t_bulk, r_bulk = with_inserter(bulk_body)
+    t0 = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t0 < 1.0:
+        n += adder_body()
+    table.flush()
+    r_adder = n / (time.perf_counter() - t0)
+    # Bulk inserts with no learner running: the host + PCIe ceiling of the path.
+    t0 = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t0 < 2.0:
+        n += bulk_body()
+    nat.sync_inserts()
+    r_solo = n / (time.perf_counter() - t0)
+    item_bytes = sum(f.row_bytes for f in table.fields)
+    out = {
+        "metric": "host->HBM inserts/s into the 1M-slot prioritized table (pinned staging ring, "
+                  "side-stream hipMemcpyAsync) while the DQN learner steps",
+        "value": round(r_bulk, 1), "unit": "items/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "higher_is_better": True, "vs_baseline": None,
+        "dtype": "u8", "data": "synthetic uint8 Atari transitions (56,460 B per item)",
+        "config": {"workload": "dqn_insert (BASELINE configs[1] table + learner)",
+                   "item_bytes": item_bytes, "staging_chunk_items": nat.stage_capacity(),
+                   "batch": B},
+        "inserts": {
+            "bulk_items_per_s_concurrent": round(r_bulk, 1),
+            "bulk_items_per_s_alone": round(r_solo, 1),
+            "bulk_GB_per_s_alone": round(r_solo * item_bytes / 1e9, 2),
+            "adder_items_per_s_alone": round(r_adder, 1),
+            "adder_items_per_s_paced": round(r_paced, 1),
+            "learner_ms_per_step_alone": round(1e3 * t_alone / args.steps, 4),
+            "learner_ms_per_step_with_paced_adder_inserts": round(1e3 * t_paced / args.steps, 4),
+            "learner_ms_per_step_with_bulk_inserts": round(1e3 * t_bulk / args.steps, 4),
+            "reference_rate_needed_items_per_s": round(
+                B / 32.0 / (t_alone / args.steps), 1),  # samples_per_insert = 32
+        },
+    }
+    print(json.dumps(out))
 
 
 def setup_d4pg(args, world, rank, dev):
@@ -354,9 +479,28 @@ def pmc_traffic(workload: str, section: str):
     return None, None
 
 
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` run without a launcher: start N ranks with torch.distributed.run
+    (one process per GPU, rendezvous on 127.0.0.1) as a child process, before this process
+    touches the GPU, and return its exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world:
+        if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+            sys.exit(spawn_ranks(args.gpus))
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # One rank per GPU.  More ranks than visible GPUs (a rehearsal on a one-GPU box) share
@@ -379,6 +523,11 @@ def main():
 
     from acme_amd import _lib
     L = _lib.lib()
+    if args.workload == "insert":
+        if world > 1:
+            raise SystemExit("the insert workload is single-GPU")
+        insert_bench(args, dev)
+        return
     t_fill = time.perf_counter()
     setup = {"dqn": setup_dqn, "d4pg": setup_d4pg, "impala": setup_impala}[args.workload]
     step, B, meta, loss_fn, cpu_fn = setup(args, world, rank, dev)
