@@ -24,6 +24,9 @@ ACME_ERR_HIP = -2
 ACME_ERR_EMPTY = -3
 ACME_ERR_OOM = -4
 
+SEMANTICS_TF = 0
+SEMANTICS_JAX = 1
+
 MATMUL_F32 = 0
 MATMUL_X6 = 1
 
@@ -50,7 +53,7 @@ class DQNConfig(ctypes.Structure):
                 ("importance_sampling_exponent", c_f32), ("learning_rate", c_f32),
                 ("huber_loss_parameter", c_f32), ("adam_beta1", c_f32), ("adam_beta2", c_f32),
                 ("adam_epsilon", c_f32), ("target_update_period", c_i32),
-                ("max_abs_reward", c_f32)]
+                ("max_abs_reward", c_f32), ("semantics", c_i32)]
 
 
 class TransitionBatch(ctypes.Structure):
@@ -93,7 +96,7 @@ class IMPALAConfig(ctypes.Structure):
                 ("head_size", c_i32), ("discount", c_f32), ("entropy_cost", c_f32),
                 ("baseline_cost", c_f32), ("max_abs_reward", c_f32),
                 ("max_gradient_norm", c_f32), ("learning_rate", c_f32), ("adam_beta1", c_f32),
-                ("adam_beta2", c_f32), ("adam_epsilon", c_f32)]
+                ("adam_beta2", c_f32), ("adam_epsilon", c_f32), ("semantics", c_i32)]
 
 
 class SequenceBatch(ctypes.Structure):

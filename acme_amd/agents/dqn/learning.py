@@ -34,7 +34,8 @@ class DQNLearner(core.Learner, core.Saveable):
                  replay_client=None, counter: Optional[counting.Counter] = None,
                  logger: Optional[loggers.Logger] = None, checkpoint: bool = True,
                  max_abs_reward: float = 1.0, batch_size: Optional[int] = None, seed: int = 0,
-                 device=None, data_parallel: bool = True):
+                 device=None, data_parallel: bool = True, semantics: str = "tf",
+                 target_seed: Optional[int] = None, adam=None):
         if huber_loss_parameter < 0:
             raise ValueError("quadratic_linear_boundary must be >= 0.")
         self._network = network
@@ -45,17 +46,21 @@ class DQNLearner(core.Learner, core.Saveable):
                   importance_sampling_exponent=importance_sampling_exponent,
                   learning_rate=learning_rate, huber_loss_parameter=huber_loss_parameter,
                   target_update_period=target_update_period, max_abs_reward=max_abs_reward,
-                  device=device)
+                  semantics=semantics, device=device)
+        if adam is not None:
+            kw.update(adam_beta1=adam.beta1, adam_beta2=adam.beta2, adam_epsilon=adam.epsilon)
         if network.kind == "mlp":
             kw.update(obs_dim=network.obs_dim, hidden=network.hidden)
         self._native = NativeDQN(**kw)
-        self._native.set_params(network.init(seed), target_network.init(seed + 1))
+        self._native.set_params(network.init(seed), target_network.init(
+            seed + 1 if target_seed is None else target_seed))
         self._replay_client = replay_client
         self._counter = counter or counting.Counter()
         self._logger = logger or loggers.TerminalLogger("learner", time_delta=1.0)
         self._timestamp = None
         self._obs_flat = int(np.prod(network.obs_shape))
         self._checkpoint = checkpoint
+        self._log_loss = True
         # Data parallelism (one process per GPU, torch.distributed over RCCL): each rank
         # samples its own batch from its replay shard; the IS-weight normaliser and the
         # gradients are reduced across ranks before Adam, so every replica applies the
@@ -120,7 +125,7 @@ class DQNLearner(core.Learner, core.Saveable):
         now = time.time()
         elapsed = now - self._timestamp if self._timestamp else 0
         self._timestamp = now
-        result = {"loss": self._native.loss}
+        result = {"loss": self._native.loss} if self._log_loss else {}
         result.update(self._counter.increment(steps=1, walltime=elapsed))
         self._logger.write(result)
 

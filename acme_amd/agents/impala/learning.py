@@ -37,7 +37,8 @@ class IMPALALearner(core.Learner, core.Saveable):
                  max_gradient_norm: Optional[float] = None,
                  counter: Optional[counting.Counter] = None,
                  logger: Optional[loggers.Logger] = None, batch_size: Optional[int] = None,
-                 sequence_length: Optional[int] = None, seed: int = 0, device=None):
+                 sequence_length: Optional[int] = None, seed: int = 0, device=None,
+                 semantics: str = "tf", adam=None):
         self._env_spec = environment_spec
         self._network = network
         self._iterator = iter(dataset)
@@ -48,7 +49,9 @@ class IMPALALearner(core.Learner, core.Saveable):
             torso=network.torso, obs_dim=network.obs_dim, lstm_size=network.lstm_size,
             head_size=network.head_size, discount=discount, entropy_cost=entropy_cost,
             baseline_cost=baseline_cost, max_abs_reward=max_abs_reward,
-            max_gradient_norm=max_gradient_norm, learning_rate=learning_rate, device=device)
+            max_gradient_norm=max_gradient_norm, learning_rate=learning_rate, semantics=semantics,
+            device=device, **({} if adam is None else dict(
+                adam_beta1=adam.beta1, adam_beta2=adam.beta2, adam_epsilon=adam.epsilon)))
         self._native.set_params(network.init(seed))
         self._counter = counter or counting.Counter()
         self._logger = logger or loggers.TerminalLogger("learner", time_delta=1.)

@@ -601,6 +601,8 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
                  "unknown observation dtype %d", cfg->obs_dtype);
   ACME_CHECK_ARG(cfg->huber_loss_parameter >= 0.f, "quadratic_linear_boundary must be >= 0.");
   ACME_CHECK_ARG(cfg->target_update_period >= 1, "target_update_period must be >= 1");
+  ACME_CHECK_ARG(cfg->semantics == ACME_SEMANTICS_TF || cfg->semantics == ACME_SEMANTICS_JAX,
+                 "unknown learner semantics %d", cfg->semantics);
   acme_dqn* l = new acme_dqn();
   l->cfg = *cfg;
   const int A = cfg->num_actions;
@@ -960,6 +962,7 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
   la.beta = l->cfg.importance_sampling_exponent;
   la.delta = l->cfg.huber_loss_parameter;
   la.max_abs_reward = l->cfg.max_abs_reward;
+  la.jax = l->cfg.semantics == ACME_SEMANTICS_JAX;
   la.loss = loss;
   la.td = td;
   la.prio = prio;
@@ -995,14 +998,18 @@ int acme_dqn_grad_split(const acme_dqn* l, int64_t* split) {
 int acme_dqn_apply(acme_dqn* l, void* stream) {
   ACME_CHECK_ARG(l && l->params, "unbound learner");
   hipStream_t st = as_stream(stream);
-  const int64_t t = l->num_steps + 1;  // snt.Adam increments its step before the update
+  const int64_t t = l->num_steps + 1;  // snt.Adam / optix.adam count this step first
+  const bool jax = l->cfg.semantics == ACME_SEMANTICS_JAX;
   ACME_PROF("adam", st, 0.0, 28.0 * (double)l->logical);
   // The parameter planes (plane path) are refreshed by the same pass.
   int rc = launch_adam(l->params, l->grads, l->m, l->v, l->flat, l->cfg.learning_rate,
                        l->cfg.adam_beta1, l->cfg.adam_beta2, l->cfg.adam_epsilon, t,
-                       l->p3_capable ? l->wpl : nullptr, l->flat, st);
+                       l->p3_capable ? l->wpl : nullptr, l->flat, st, jax ? 1 : 0);
   if (rc != ACME_OK) return rc;
-  if (l->num_steps % l->cfg.target_update_period == 0) {
+  // TF: copy when num_steps % period == 0, then num_steps += 1 (tf/dqn/learning.py:157-161);
+  // JAX: steps + 1 first, copy when that is a multiple of the period (jax/dqn/learning.py:114-119).
+  const int64_t copy_at = jax ? l->num_steps + 1 : l->num_steps;
+  if (copy_at % l->cfg.target_update_period == 0) {
     ACME_PROF("target_copy", st, 0.0, 8.0 * (double)l->logical);
     ACME_HIP_TRY(hipMemcpyAsync(l->target, l->params, l->flat * sizeof(float),
                                 hipMemcpyDeviceToDevice, st));

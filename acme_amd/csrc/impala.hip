@@ -737,6 +737,7 @@ int impala_step_impl(acme_impala* l, const acme_sequence_batch* bt, float* metri
     a.p = l->params; a.m = l->m; a.v = l->v; a.g = gr; a.n4 = n4; a.group0_4 = n4;
     a.part = l->norm_part; a.nparts = kNormBlocks; a.clipping = 1;
     a.clip_norm = l->cfg.max_gradient_norm;
+    a.optix = l->cfg.semantics == ACME_SEMANTICS_JAX;
     a.lr0 = a.lr1 = l->cfg.learning_rate;
     a.b1 = l->cfg.adam_beta1; a.b2 = l->cfg.adam_beta2; a.eps = l->cfg.adam_epsilon;
     a.dev_step = l->dev_step; a.norms = l->norms;
@@ -764,6 +765,8 @@ int acme_impala_create(const acme_impala_config* cfg, acme_impala** out) {
   ACME_CHECK_ARG(cfg->torso == ACME_IMPALA_TORSO_ATARI || cfg->obs_dim >= 1,
                  "obs_dim must be >= 1 for the flat torso");
   ACME_CHECK_ARG(cfg->num_actions >= 1 && cfg->num_actions <= 63, "num_actions must be in [1, 63]");
+  ACME_CHECK_ARG(cfg->semantics == ACME_SEMANTICS_TF || cfg->semantics == ACME_SEMANTICS_JAX,
+                 "unknown learner semantics %d", cfg->semantics);
   ACME_CHECK_ARG(cfg->max_batch >= 1 && cfg->max_batch <= 1024, "max_batch must be in [1, 1024]");
   ACME_CHECK_ARG(cfg->max_sequence_length >= 2 && cfg->max_sequence_length <= 64,
                  "max_sequence_length must be in [2, 64]");

@@ -51,6 +51,7 @@ struct LossArgs {
   const double* global_min_prob;  // optional
   int B, A;
   float discount, beta, delta, max_abs_reward;
+  int jax;        // JAX DQNLearner: f32 importance weights (agents/jax/dqn/learning.py:94-96)
   float* loss;    // [1]
   float* td;      // [B]
   double* prio;   // [B]
@@ -90,6 +91,9 @@ struct ClipAdamArgs {
   int nparts = 0;
   int clipping = 0;
   float clip_norm = 1e10f;
+  // optix.chain(clip_by_global_norm, adam) (agents/jax/impala/agent.py:98-101): g * (c / G)
+  // only when G >= c, and the optix Adam update lr * (m_hat / (sqrt(v_hat) + eps)).
+  int optix = 0;
   float lr0 = 0.f, lr1 = 0.f, b1 = 0.9f, b2 = 0.999f, eps = 1e-8f;
   const int64_t* dev_step = nullptr;
   float* norms = nullptr;  // [2] (optional)
@@ -106,8 +110,10 @@ int launch_clip_adam(const ClipAdamArgs& a, hipStream_t st);
 
 // snt.Adam over n (multiple of 4) floats at step t (acme_adam_update); with `planes`
 // non-null the updated parameters are also written as exact bf16 planes (stride pstride).
+// optix != 0: optix.adam's rounding order, p + (-lr) * (m_hat / (sqrt(v_hat) + eps)).
 int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,
-                float b2, float eps, int64_t t, uint16_t* planes, int64_t pstride, hipStream_t st);
+                float b2, float eps, int64_t t, uint16_t* planes, int64_t pstride, hipStream_t st,
+                int optix = 0);
 
 // Exact three-plane split of n floats (n multiple of 4): planes[i * pstride + e].
 int launch_split_planes(const float* x, int64_t n, uint16_t* planes, int64_t pstride,

@@ -129,8 +129,12 @@ __device__ __forceinline__ LossRow loss_row(const LossArgs& p, int b, double wma
   const float quad = fminf(ax, p.delta);
   const float lin = ax - quad;
   const float hub = __fadd_rn(__fmul_rn(0.5f, __fmul_rn(quad, quad)), __fmul_rn(p.delta, lin));
-  const double w = pow(1.0 / p.probs[b], (double)p.beta) / wmax;
-  const float wf = (float)w;
+  float wf;
+  if (p.jax) {  // ((1 / probs).astype(f32) ** beta) / max, all in f32 (jax/dqn/learning.py:94-96)
+    wf = __fdiv_rn(powf((float)(1.0 / p.probs[b]), p.beta), (float)wmax);
+  } else {      // f64 weights cast at the multiply (tf/dqn/learning.py:138-143)
+    wf = (float)(pow(1.0 / p.probs[b], (double)p.beta) / wmax);
+  }
   const float dtd = fminf(fmaxf(td, -p.delta), p.delta);  // d huber / d td
   const float inv_b = 1.f / (float)B;
   return LossRow{-(inv_b * wf * dtd), td, hub * wf};
@@ -156,7 +160,8 @@ __global__ void __launch_bounds__(kLossThreads) dqn_loss_kernel(LossArgs p) {
   __syncthreads();
   pmin = p.global_min_prob ? *p.global_min_prob : red[0];
   __syncthreads();
-  const double wmax = pow(1.0 / pmin, (double)p.beta);
+  const double wmax = p.jax ? (double)powf((float)(1.0 / pmin), p.beta)
+                            : pow(1.0 / pmin, (double)p.beta);
   double lsum = 0.0;
   for (int b = tid; b < B; b += blockDim.x) {
     const LossRow row = loss_row(p, b, wmax);
@@ -416,7 +421,8 @@ __global__ void __launch_bounds__(256) dqn_loss_head_dz_kernel(
   __syncthreads();
   pmin = fmin(fmin(red[0], red[1]), fmin(red[2], red[3]));
   if (p.global_min_prob) pmin = *p.global_min_prob;
-  const double wmax = pow(1.0 / pmin, (double)p.beta);
+  const double wmax = p.jax ? (double)powf((float)(1.0 / pmin), p.beta)
+                            : pow(1.0 / pmin, (double)p.beta);
   if (blockIdx.x == gridDim.x - 1) {
     __syncthreads();  // red is reused below
     double lsum = 0.0;
@@ -535,7 +541,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p,
                                                    int64_t n4, float lr, float b1, float omb1,
                                                    float b2, float omb2, float bc1, float bc2,
                                                    float eps, uint16_t* __restrict__ planes,
-                                                   int64_t pstride) {
+                                                   int64_t pstride, int optix) {
 #pragma unroll 2
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -549,7 +555,8 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p,
       const float vj = __fadd_rn(__fmul_rn(b2, vv[j]), __fmul_rn(omb2, __fmul_rn(gg[j], gg[j])));
       const float mh = __fdiv_rn(mj, bc1);
       const float vh = __fdiv_rn(vj, bc2);
-      const float upd = __fdiv_rn(__fmul_rn(lr, mh), __fadd_rn(__fsqrt_rn(vh), eps));
+      const float den = __fadd_rn(__fsqrt_rn(vh), eps);
+      const float upd = optix ? __fmul_rn(lr, __fdiv_rn(mh, den)) : __fdiv_rn(__fmul_rn(lr, mh), den);
       mm[j] = mj;
       vv[j] = vj;
       pp[j] = __fsub_rn(pp[j], upd);
@@ -629,7 +636,7 @@ __global__ void __launch_bounds__(256) grad_sumsq_kernel(const float* __restrict
 
 __global__ void __launch_bounds__(256) clip_adam_kernel(const ClipAdamArgs a) {
   __shared__ double red[2][4];
-  __shared__ float scl[2];
+  __shared__ float scl[4];
   const float tf = (float)*a.dev_step;
   const float bc1 = 1.f - powf(a.b1, tf), bc2 = 1.f - powf(a.b2, tf);
   const float omb1 = 1.f - a.b1, omb2 = 1.f - a.b2;
@@ -654,8 +661,13 @@ __global__ void __launch_bounds__(256) clip_adam_kernel(const ClipAdamArgs a) {
     const double ss = ((red[k][0] + red[k][1]) + red[k][2]) + red[k][3];
     const float G = (float)sqrt(ss);
     float s = 1.f;
-    if (a.clipping && G > 0.f) s = a.clip_norm * fminf(1.f / G, 1.f / a.clip_norm);
+    if (a.optix) {  // optix.clip_by_global_norm: (t / G) * c when G >= c
+      if (a.clipping && !(G < a.clip_norm)) s = -1.f;  // marks "divide by G, times c"
+    } else if (a.clipping && G > 0.f) {  // tf.clip_by_global_norm
+      s = a.clip_norm * fminf(1.f / G, 1.f / a.clip_norm);
+    }
     scl[k] = s;
+    scl[2 + k] = G;
     if (blockIdx.x == 0 && a.norms) a.norms[k] = G;
   }
   if (blockIdx.x == 0 && threadIdx.x == 64 && a.out_a) {
@@ -672,6 +684,7 @@ __global__ void __launch_bounds__(256) clip_adam_kernel(const ClipAdamArgs a) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < a.n4; i += (int64_t)gridDim.x * 256) {
     const bool g0 = i < a.group0_4;
     const float s = g0 ? scl[0] : scl[1];
+    const float G = g0 ? scl[2] : scl[3];
     const float lr = g0 ? a.lr0 : a.lr1;
     f32x4 gg = reinterpret_cast<const f32x4*>(a.g)[i];
     f32x4 mm = reinterpret_cast<f32x4*>(a.m)[i];
@@ -679,12 +692,13 @@ __global__ void __launch_bounds__(256) clip_adam_kernel(const ClipAdamArgs a) {
     f32x4 pp = reinterpret_cast<f32x4*>(a.p)[i];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float gj = __fmul_rn(gg[j], s);
+      const float gj = s < 0.f ? __fmul_rn(__fdiv_rn(gg[j], G), a.clip_norm) : __fmul_rn(gg[j], s);
       const float mj = __fadd_rn(__fmul_rn(a.b1, mm[j]), __fmul_rn(omb1, gj));
       const float vj = __fadd_rn(__fmul_rn(a.b2, vv[j]), __fmul_rn(omb2, __fmul_rn(gj, gj)));
       const float mh = __fdiv_rn(mj, bc1);
       const float vh = __fdiv_rn(vj, bc2);
-      const float upd = __fdiv_rn(__fmul_rn(lr, mh), __fadd_rn(__fsqrt_rn(vh), a.eps));
+      const float den = __fadd_rn(__fsqrt_rn(vh), a.eps);
+      const float upd = a.optix ? __fmul_rn(lr, __fdiv_rn(mh, den)) : __fdiv_rn(__fmul_rn(lr, mh), den);
       mm[j] = mj;
       vv[j] = vj;
       pp[j] = __fsub_rn(pp[j], upd);
@@ -827,7 +841,8 @@ int launch_grad_sumsq(const float* g, int64_t n4, int64_t group0_4, double* part
 }
 
 int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,
-                float b2, float eps, int64_t t, uint16_t* planes, int64_t pstride, hipStream_t st) {
+                float b2, float eps, int64_t t, uint16_t* planes, int64_t pstride, hipStream_t st,
+                int optix) {
   ACME_CHECK_ARG(p && g && m && v, "null buffer");
   ACME_CHECK_ARG(n % 4 == 0, "adam buffer length must be a multiple of 4");
   ACME_CHECK_ARG(pstride % 4 == 0, "plane stride must be a multiple of 4");
@@ -838,7 +853,7 @@ int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float l
   const int gcap = tune_variant("ADAMG") > 0 ? tune_variant("ADAMG") : 8192;  // 47.7 -> 45.2 us vs 2048
   const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n4, 256), gcap);
   adam_kernel<<<std::max(grid, 1u), 256, 0, st>>>(p, g, m, v, n4, lr, b1, 1.f - b1, b2, 1.f - b2,
-                                                  bc1, bc2, eps, planes, pstride);
+                                                  bc1, bc2, eps, planes, pstride, optix);
   ACME_LAUNCH_CHECK();
   return ACME_OK;
 }

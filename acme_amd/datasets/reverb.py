@@ -123,6 +123,10 @@ class _TableIterator:
             return x.view(torch.bool).reshape((B,) + f.shape)
         return x.view(_TORCH[np.dtype(f.dtype)]).reshape((B,) + f.shape)
 
+    @property
+    def batch_size(self) -> int:
+        return self._B
+
     def __iter__(self):
         return self
 
@@ -187,6 +191,10 @@ class _QueueIterator:
         self._t = table
         self._B = batch
         self._timeout = timeout
+
+    @property
+    def batch_size(self) -> int:
+        return self._B
 
     def __iter__(self):
         return self

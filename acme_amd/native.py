@@ -266,8 +266,12 @@ class NativeDQN:
                  importance_sampling_exponent: float = 0.2, learning_rate: float = 1e-3,
                  huber_loss_parameter: float = 1.0, target_update_period: int = 100,
                  max_abs_reward: float = 1.0, adam_beta1: float = 0.9, adam_beta2: float = 0.999,
-                 adam_epsilon: float = 1e-8, device=None):
+                 adam_epsilon: float = 1e-8, semantics: str = "tf", device=None):
+        """semantics: "tf" restates acme/agents/tf/dqn/learning.py, "jax" the JAX learner
+        (acme/agents/jax/dqn/learning.py: f32 IS weights, steps+1 target cadence, optix.adam)."""
         _lib.require_gpu()
+        if semantics not in ("tf", "jax"):
+            raise ValueError(f"semantics must be 'tf' or 'jax', got {semantics!r}")
         if huber_loss_parameter < 0:
             raise ValueError("quadratic_linear_boundary must be >= 0.")
         cfg = _lib.DQNConfig()
@@ -288,7 +292,9 @@ class NativeDQN:
         cfg.adam_beta1, cfg.adam_beta2, cfg.adam_epsilon = adam_beta1, adam_beta2, adam_epsilon
         cfg.target_update_period = int(target_update_period)
         cfg.max_abs_reward = max_abs_reward
+        cfg.semantics = _lib.SEMANTICS_JAX if semantics == "jax" else _lib.SEMANTICS_TF
         self.cfg = cfg
+        self.semantics = semantics
         self.network = network
         self.num_actions = int(num_actions)
         self.max_batch = int(max_batch)
@@ -573,8 +579,12 @@ class NativeIMPALA:
                  baseline_cost: float = 1.0, max_abs_reward: Optional[float] = None,
                  max_gradient_norm: Optional[float] = None, learning_rate: float = 1e-3,
                  adam_beta1: float = 0.9, adam_beta2: float = 0.999, adam_epsilon: float = 1e-8,
-                 device=None):
+                 semantics: str = "tf", device=None):
+        """semantics: "tf" (acme/agents/tf/impala) or "jax" (acme/agents/jax/impala: the
+        optix.chain(clip_by_global_norm, adam) update; max_gradient_norm None = inf)."""
         _lib.require_gpu()
+        if semantics not in ("tf", "jax"):
+            raise ValueError(f"semantics must be 'tf' or 'jax', got {semantics!r}")
         cfg = _lib.IMPALAConfig()
         cfg.torso = _lib.IMPALA_TORSO_ATARI if torso == "atari" else _lib.IMPALA_TORSO_FLAT
         cfg.obs_dim, cfg.num_actions = int(obs_dim), int(num_actions)
@@ -583,7 +593,9 @@ class NativeIMPALA:
         cfg.discount, cfg.entropy_cost, cfg.baseline_cost = discount, entropy_cost, baseline_cost
         # learning.py:67-71: None -> no reward clipping, gradient norm 1e10.
         cfg.max_abs_reward = float("inf") if max_abs_reward is None else max_abs_reward
-        cfg.max_gradient_norm = 1e10 if max_gradient_norm is None else max_gradient_norm
+        cfg.max_gradient_norm = ((float("inf") if semantics == "jax" else 1e10)
+                                 if max_gradient_norm is None else max_gradient_norm)
+        cfg.semantics = _lib.SEMANTICS_JAX if semantics == "jax" else _lib.SEMANTICS_TF
         cfg.learning_rate = learning_rate
         cfg.adam_beta1, cfg.adam_beta2, cfg.adam_epsilon = adam_beta1, adam_beta2, adam_epsilon
         self.cfg = cfg

@@ -188,6 +188,15 @@ int acme_replay_restore(acme_replay* r, int64_t inserted, void* stream);
 /* -------------------------------------------------------------------- DQN -- */
 
 enum { ACME_NET_NATURE_DQN = 0, ACME_NET_MLP = 1 };
+/* Which reference learner a config restates:
+ *   ACME_SEMANTICS_TF   acme/agents/tf/{dqn,impala}/learning.py (snt.Adam, f64 IS weights,
+ *                       post-step target copy when num_steps % period == 0);
+ *   ACME_SEMANTICS_JAX  acme/agents/jax/{dqn,impala}/learning.py: DQN importance weights in
+ *                       f32 before ** beta (dqn/learning.py:94-96), target copy when
+ *                       (steps + 1) % period == 0 (:114-119, jax/utils.py:148-154), optix.adam's
+ *                       update order; IMPALA optix.chain(clip_by_global_norm, adam)
+ *                       (impala/agent.py:98-101). */
+enum { ACME_SEMANTICS_TF = 0, ACME_SEMANTICS_JAX = 1 };
 enum { ACME_OBS_U8_SCALED = 0, ACME_OBS_F32 = 1 };
 
 #define ACME_MAX_MLP_LAYERS 8
@@ -209,6 +218,7 @@ typedef struct acme_dqn_config {
   float adam_beta1, adam_beta2, adam_epsilon;
   int32_t target_update_period;
   float max_abs_reward;      /* reward clip (TF DQN clips to [-1, 1])               */
+  int32_t semantics;         /* ACME_SEMANTICS_TF (default) or ACME_SEMANTICS_JAX    */
 } acme_dqn_config;
 
 typedef struct acme_dqn acme_dqn;
@@ -377,6 +387,7 @@ typedef struct acme_impala_config {
   float max_abs_reward;         /* INFINITY = no reward clipping (learning.py:70-71) */
   float max_gradient_norm;      /* 1e10 = effectively none (learning.py:72-73) */
   float learning_rate, adam_beta1, adam_beta2, adam_epsilon;
+  int32_t semantics;            /* ACME_SEMANTICS_TF (default) or ACME_SEMANTICS_JAX */
 } acme_impala_config;
 
 /* One batch of sequences, batch-major [B, T, ...] as the dataset yields them. */

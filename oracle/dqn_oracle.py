@@ -229,6 +229,11 @@ class DQNConfig:
     adam_beta1: float = 0.9
     adam_beta2: float = 0.999
     adam_epsilon: float = 1e-8
+    # "tf": acme/agents/tf/dqn/learning.py (the primary oracle); "jax":
+    # acme/agents/jax/dqn/learning.py:74-178 — importance weights cast to f32 before ** beta
+    # (:94-96), target copy when (steps + 1) % period == 0 (:114-119 with
+    # jax/utils.py:148-154), optix.adam (agents/jax/dqn/agent.py:110).
+    semantics: str = "tf"
 
 
 def forward(cfg: DQNConfig, params, o, dtype):
@@ -261,12 +266,21 @@ def dqn_loss_and_grads(cfg: DQNConfig, params, target, batch, dtype=np.float64,
     ax = np.abs(td)
     quad = np.minimum(ax, delta)
     hub = 0.5 * quad ** 2 + delta * (ax - quad)
-    iw = (1.0 / probs) ** np.float64(cfg.importance_sampling_exponent)
-    if global_min_probability is not None:
-        wmax = (1.0 / global_min_probability) ** np.float64(cfg.importance_sampling_exponent)
-    else:
-        wmax = iw.max()
-    iw = (iw / wmax).astype(np.float32).astype(dtype)
+    if cfg.semantics == "jax":  # jax/dqn/learning.py:94-96, all in f32
+        beta32 = np.float32(cfg.importance_sampling_exponent)
+        iw32 = (1.0 / probs).astype(np.float32) ** beta32
+        if global_min_probability is not None:
+            wmax32 = np.float32(1.0 / global_min_probability) ** beta32
+        else:
+            wmax32 = iw32.max()
+        iw = (iw32 / wmax32).astype(dtype)
+    else:  # tf/dqn/learning.py:138-143: f64, cast to f32 at the multiply
+        iw = (1.0 / probs) ** np.float64(cfg.importance_sampling_exponent)
+        if global_min_probability is not None:
+            wmax = (1.0 / global_min_probability) ** np.float64(cfg.importance_sampling_exponent)
+        else:
+            wmax = iw.max()
+        iw = (iw / wmax).astype(np.float32).astype(dtype)
     loss = np.mean(hub * iw)
     B = len(a)
     dq = np.zeros_like(q_tm1)
@@ -277,8 +291,9 @@ def dqn_loss_and_grads(cfg: DQNConfig, params, target, batch, dtype=np.float64,
     return out, grads
 
 
-def adam_update(p, g, m, v, t, lr, b1=0.9, b2=0.999, eps=1e-8):
-    """snt.optimizers.Adam in float32, op order of the product kernel."""
+def adam_update(p, g, m, v, t, lr, b1=0.9, b2=0.999, eps=1e-8, optix=False):
+    """snt.optimizers.Adam in float32, op order of the product kernel.  optix=True: the
+    optix.adam form (scale_by_adam then scale(-lr)), update = lr * (m_hat / (sqrt(v_hat) + eps))."""
     f = np.float32
     p, g, m, v = (np.asarray(x, f) for x in (p, g, m, v))
     b1, b2, lr, eps = f(b1), f(b2), f(lr), f(eps)
@@ -286,7 +301,10 @@ def adam_update(p, g, m, v, t, lr, b1=0.9, b2=0.999, eps=1e-8):
     v = b2 * v + (f(1) - b2) * (g * g)
     bc1 = f(1) - np.power(b1, f(t))
     bc2 = f(1) - np.power(b2, f(t))
-    upd = (lr * (m / bc1)) / (np.sqrt(v / bc2) + eps)
+    if optix:
+        upd = lr * ((m / bc1) / (np.sqrt(v / bc2) + eps))
+    else:
+        upd = (lr * (m / bc1)) / (np.sqrt(v / bc2) + eps)
     return p - upd, m, v
 
 
@@ -298,9 +316,10 @@ def dqn_step(cfg: DQNConfig, state: dict, batch: dict, dtype=np.float64):
     for k in state["params"]:
         new_p[k], new_m[k], new_v[k] = adam_update(
             state["params"][k], grads[k], state["m"][k], state["v"][k], t, cfg.learning_rate,
-            cfg.adam_beta1, cfg.adam_beta2, cfg.adam_epsilon)
+            cfg.adam_beta1, cfg.adam_beta2, cfg.adam_epsilon, optix=cfg.semantics == "jax")
     target = state["target"]
-    if state["num_steps"] % cfg.target_update_period == 0:
+    copy_at = state["num_steps"] + (1 if cfg.semantics == "jax" else 0)
+    if copy_at % cfg.target_update_period == 0:
         target = {k: v.copy() for k, v in new_p.items()}
     new_state = dict(params=new_p, target=target, m=new_m, v=new_v,
                      num_steps=state["num_steps"] + 1)

@@ -58,6 +58,13 @@ class IMPALAConfig:
     max_abs_reward: float = float("inf")
     max_gradient_norm: float = 1e10
     learning_rate: float = 1e-3
+    # "tf": agents/tf/impala/learning.py; "jax": agents/jax/impala/learning.py:66-136 with the
+    # agent's optix.chain(clip_by_global_norm(max_gradient_norm), adam(lr))
+    # (agents/jax/impala/agent.py:98-101).  The rlax losses (categorical IS ratios,
+    # vtrace_td_error_and_advantage with lambda 1 and rho / pg-rho clips 1, policy_gradient_loss,
+    # entropy_loss, per-sequence means averaged by vmap + mean) equal the TF ones here: every
+    # sequence has T - 1 terms, so the mean of per-sequence means is the [T - 1, B] mean.
+    semantics: str = "tf"
 
     @property
     def feat(self) -> int:
@@ -276,8 +283,14 @@ def backward(cfg: IMPALAConfig, p, batch, cache, dpv, f, masks=None):
     return g
 
 
-def clip_by_global_norm(grads, clip, f):
+def clip_by_global_norm(grads, clip, f, optix=False):
+    """tf.clip_by_global_norm: g * c * min(1 / G, 1 / c).  optix=True: optix's
+    clip_by_global_norm, g unchanged when G < c, else (g / G) * c."""
     G = np.sqrt(sum(float(np.sum(np.square(x.astype(np.float64)))) for x in grads.values()))
+    if optix:
+        if G < clip:
+            return {k: x.astype(f) for k, x in grads.items()}, G
+        return {k: ((x / f(G)) * f(clip)).astype(f) for k, x in grads.items()}, G
     scale = f(clip) * min(f(1.0) / f(G), f(1.0) / f(clip)) if G > 0 else f(1.0)
     return {k: (x * f(scale)).astype(f) for k, x in grads.items()}, G
 
@@ -285,10 +298,12 @@ def clip_by_global_norm(grads, clip, f):
 def impala_step(cfg: IMPALAConfig, state: dict, batch: dict, dtype=np.float64, masks=None):
     """One learner step. state = {params, m, v, num_steps}."""
     out, raw = loss_and_grads(cfg, state["params"], batch, dtype, masks)
-    grads, out["grad_norm"] = clip_by_global_norm(raw, cfg.max_gradient_norm, dtype)
+    jax = cfg.semantics == "jax"
+    grads, out["grad_norm"] = clip_by_global_norm(raw, cfg.max_gradient_norm, dtype, optix=jax)
     t = state["num_steps"] + 1
     new_p, new_m, new_v = {}, {}, {}
     for k in state["params"]:
         new_p[k], new_m[k], new_v[k] = adam_update(state["params"][k], grads[k], state["m"][k],
-                                                   state["v"][k], t, cfg.learning_rate)
+                                                   state["v"][k], t, cfg.learning_rate,
+                                                   optix=jax)
     return out, raw, dict(params=new_p, m=new_m, v=new_v, num_steps=t)
