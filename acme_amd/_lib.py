@@ -58,7 +58,8 @@ class DQNConfig(ctypes.Structure):
 
 class TransitionBatch(ctypes.Structure):
     _fields_ = [("o_tm1", c_vp), ("a_tm1", c_vp), ("r_t", c_vp), ("d_t", c_vp), ("o_t", c_vp),
-                ("probabilities", c_vp), ("batch", c_i64), ("global_min_probability", c_vp)]
+                ("probabilities", c_vp), ("batch", c_i64), ("global_min_probability", c_vp),
+                ("mean_over", c_i64)]
 
 
 class DQNOutputs(ctypes.Structure):
@@ -124,6 +125,9 @@ _SIGS = {
     "acme_replay_fill_synthetic": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_u64, c_vp]),
     "acme_replay_sample": (c_i32, [c_vp, c_i64, c_u64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "acme_replay_gather": (c_i32, [c_vp, c_vp, c_i64, ctypes.POINTER(c_vp), c_vp]),
+    "acme_replay_total": (c_i32, [c_vp, c_vp, c_vp]),
+    "acme_replay_sample_share": (c_i32, [c_vp, c_i64, c_u64, c_f64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                         ctypes.POINTER(c_vp), c_vp]),
     "acme_replay_sample_gather": (c_i32, [c_vp, c_i64, c_u64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                           ctypes.POINTER(c_vp), c_vp]),
     "acme_r2d2_priorities": (c_i32, [c_vp, c_i32, c_i32, ctypes.c_double, c_vp, c_vp]),

@@ -958,6 +958,7 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
   la.global_min_prob = batch->global_min_probability;
   la.B = B;
   la.A = A;
+  la.mean_over = batch->mean_over > 0 ? (int)batch->mean_over : B;
   la.discount = l->cfg.discount;
   la.beta = l->cfg.importance_sampling_exponent;
   la.delta = l->cfg.huber_loss_parameter;

@@ -50,6 +50,7 @@ struct LossArgs {
   const double* probs;
   const double* global_min_prob;  // optional
   int B, A;
+  int mean_over;  // the loss / gradient mean's denominator (B, or the global share, DP)
   float discount, beta, delta, max_abs_reward;
   int jax;        // JAX DQNLearner: f32 importance weights (agents/jax/dqn/learning.py:94-96)
   float* loss;    // [1]

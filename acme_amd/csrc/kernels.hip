@@ -136,7 +136,7 @@ __device__ __forceinline__ LossRow loss_row(const LossArgs& p, int b, double wma
     wf = (float)(pow(1.0 / p.probs[b], (double)p.beta) / wmax);
   }
   const float dtd = fminf(fmaxf(td, -p.delta), p.delta);  // d huber / d td
-  const float inv_b = 1.f / (float)B;
+  const float inv_b = 1.f / (float)p.mean_over;
   return LossRow{-(inv_b * wf * dtd), td, hub * wf};
 }
 
@@ -178,7 +178,7 @@ __global__ void __launch_bounds__(kLossThreads) dqn_loss_kernel(LossArgs p) {
   if (tid == 0) {
     double s = 0.0;
     for (int w = 0; w < nw; ++w) s += red[w];
-    p.loss[0] = (float)(s / (double)B);
+    p.loss[0] = (float)(s / (double)p.mean_over);
   }
 }
 
@@ -438,7 +438,7 @@ __global__ void __launch_bounds__(256) dqn_loss_head_dz_kernel(
     for (int o = 32; o > 0; o >>= 1) lsum += __shfl_xor(lsum, o, 64);
     if (lane == 0) red[wave] = lsum;
     __syncthreads();
-    if (tid == 0) p.loss[0] = (float)((((red[0] + red[1]) + red[2]) + red[3]) / (double)B);
+    if (tid == 0) p.loss[0] = (float)((((red[0] + red[1]) + red[2]) + red[3]) / (double)p.mean_over);
     return;
   }
   const int per = 2 * H / 8;  // threads per row (divides 256: launch_dqn_loss_head_dz)

@@ -125,8 +125,9 @@ struct TreeView {
 
 __global__ void __launch_bounds__(256) sample_prioritized_kernel(
     TreeView tree, const double* __restrict__ raw_prio, const uint64_t* __restrict__ keys,
-    int64_t batch, int64_t size, uint64_t seed, uint64_t step, int64_t* out_slots,
-    uint64_t* out_keys, double* out_probs, int64_t* out_size, double* out_prio) {
+    int64_t batch, int64_t size, uint64_t seed, uint64_t step, double prob_scale,
+    int64_t* out_slots, uint64_t* out_keys, double* out_probs, int64_t* out_size,
+    double* out_prio) {
   const int lane = threadIdx.x & 63;
   const int64_t j = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (j >= batch) return;  // wave-uniform
@@ -159,6 +160,7 @@ __global__ void __launch_bounds__(256) sample_prioritized_kernel(
     slot = node;
     prob = leaf_value / total;
   }
+  prob *= prob_scale;  // 1 (exact) unless this table is one shard of a global draw
   if (lane == 0) {
     out_slots[j] = slot;
     if (out_keys) out_keys[j] = keys[slot];
@@ -171,7 +173,7 @@ __global__ void __launch_bounds__(256) sample_prioritized_kernel(
 __global__ void sample_uniform_kernel(const double* __restrict__ raw_prio,
                                       const uint64_t* __restrict__ keys, int64_t batch,
                                       int64_t size, uint64_t seed, uint64_t step,
-                                      int64_t* out_slots, uint64_t* out_keys,
+                                      double prob_scale, int64_t* out_slots, uint64_t* out_keys,
                                       double* out_probs, int64_t* out_size,
                                       double* out_prio) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -181,9 +183,22 @@ __global__ void sample_uniform_kernel(const double* __restrict__ raw_prio,
   if (slot >= size) slot = size - 1;
   out_slots[j] = slot;
   if (out_keys) out_keys[j] = keys[slot];
-  if (out_probs) out_probs[j] = 1.0 / (double)size;
+  if (out_probs) out_probs[j] = (1.0 / (double)size) * prob_scale;
   if (out_size) out_size[j] = size;
   if (out_prio) out_prio[j] = raw_prio[slot];
+}
+
+// Sampling mass of the table (one wave): the prioritized root total with the sampler's own
+// scan (same bits as `total` in sample_prioritized_kernel), or the item count (uniform).
+__global__ void total_kernel(const double* __restrict__ top, int prioritized, int64_t size,
+                             double* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  if (!prioritized) {
+    if (lane == 0) *out = (double)size;
+    return;
+  }
+  const double s = wave_scan64(top[lane]);
+  if (lane == 63) *out = s;
 }
 
 // Row gather of every field in ONE launch: one workgroup per (row, field).  Rows that
@@ -932,9 +947,45 @@ int acme_replay_fill_synthetic(acme_replay* r, int64_t n, int32_t layout, int32_
   return ACME_OK;
 }
 
+static int sample_impl(acme_replay* r, int64_t batch, uint64_t step_counter, double prob_scale,
+                       int64_t* slots, uint64_t* keys, double* probabilities,
+                       int64_t* table_size, double* priorities, void* stream);
+
 int acme_replay_sample(acme_replay* r, int64_t batch, uint64_t step_counter, int64_t* slots,
                        uint64_t* keys, double* probabilities, int64_t* table_size,
                        double* priorities, void* stream) {
+  return sample_impl(r, batch, step_counter, 1.0, slots, keys, probabilities, table_size,
+                     priorities, stream);
+}
+
+int acme_replay_total(acme_replay* r, double* out, void* stream) {
+  ACME_CHECK_ARG(r && out, "null argument");
+  hipStream_t st = as_stream(stream);
+  int64_t size = 0;
+  int rc = order_after_inserts(r, st, &size);
+  if (rc != ACME_OK) return rc;
+  total_kernel<<<1, 64, 0, st>>>(r->levels[r->nlevels - 1],
+                                 r->cfg.sampler == ACME_SAMPLER_PRIORITIZED, size, out);
+  ACME_LAUNCH_CHECK();
+  return ACME_OK;
+}
+
+int acme_replay_sample_share(acme_replay* r, int64_t batch, uint64_t step_counter,
+                             double prob_scale, int64_t* slots, uint64_t* keys,
+                             double* probabilities, int64_t* table_size, double* priorities,
+                             void* const* out_fields, void* stream) {
+  ACME_CHECK_ARG(r, "null replay");
+  ACME_CHECK_ARG(prob_scale > 0.0 && prob_scale <= 1.0, "prob_scale must be in (0, 1]");
+  std::lock_guard<std::mutex> lock(r->mu);  // no insert commits between draw and gather
+  int rc = sample_impl(r, batch, step_counter, prob_scale, slots, keys, probabilities,
+                       table_size, priorities, stream);
+  if (rc != ACME_OK || !out_fields) return rc;
+  return acme_replay_gather(r, slots, batch, out_fields, stream);
+}
+
+static int sample_impl(acme_replay* r, int64_t batch, uint64_t step_counter, double prob_scale,
+                       int64_t* slots, uint64_t* keys, double* probabilities,
+                       int64_t* table_size, double* priorities, void* stream) {
   ACME_CHECK_ARG(r && slots, "null argument");
   ACME_CHECK_ARG(batch > 0 && batch <= (int64_t(1) << 31), "batch must be in [1, 2^31]");
   hipStream_t st = as_stream(stream);
@@ -951,11 +1002,11 @@ int acme_replay_sample(acme_replay* r, int64_t batch, uint64_t step_counter, int
     for (int l = 0; l < 8; ++l) tv.level[l] = r->levels[l];
     tv.nlevels = r->nlevels;
     sample_prioritized_kernel<<<(unsigned)ceil_div(batch, 4), 256, 0, st>>>(
-        tv, r->raw_prio, r->keys, batch, size, r->cfg.seed, step_counter, slots, keys,
-        probabilities, table_size, priorities);
+        tv, r->raw_prio, r->keys, batch, size, r->cfg.seed, step_counter, prob_scale, slots,
+        keys, probabilities, table_size, priorities);
   } else {
     sample_uniform_kernel<<<(unsigned)ceil_div(batch, 256), 256, 0, st>>>(
-        r->raw_prio, r->keys, batch, size, r->cfg.seed, step_counter, slots, keys,
+        r->raw_prio, r->keys, batch, size, r->cfg.seed, step_counter, prob_scale, slots, keys,
         probabilities, table_size, priorities);
   }
   ACME_LAUNCH_CHECK();

@@ -33,6 +33,8 @@ import torch
 
 from acme_amd import replay
 from acme_amd.adders import reverb as adders
+from acme_amd.replay.sharding import LAG as _LAG
+from acme_amd.replay.sharding import allocate_shares
 from acme_amd.utils import tree
 
 _TORCH = {np.dtype(k): v for k, v in [
@@ -48,10 +50,24 @@ def _server_of(address) -> replay.Server:
     return replay._resolve(address)  # noqa: SLF001
 
 
-class ReplayDataset:
-    """Iterable over batched ReplaySamples of one table."""
+def _data_parallel():
+    """(world, rank) of an initialised torch.distributed group with more than one rank."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return dist.get_world_size(), dist.get_rank()
+    return None
 
-    def __init__(self, table, batch_size: int, timeout: float = 60.0, prefetch: int = 0):
+
+class ReplayDataset:
+    """Iterable over batched ReplaySamples of one table.
+
+    global_sampling (default: on when torch.distributed runs more than one rank): the table
+    is this rank's shard of a global replay; each batch is this rank's share of a global draw
+    of world * batch_size items (acme_amd.replay.sharding), so it holds a varying number of
+    items (at most 2 * batch_size) whose probabilities are their global marginals."""
+
+    def __init__(self, table, batch_size: int, timeout: float = 60.0, prefetch: int = 0,
+                 global_sampling: Optional[bool] = None):
         if batch_size is None or batch_size < 1:
             raise ValueError("the GPU replay dataset needs a batch_size >= 1")
         if prefetch < 0:
@@ -60,21 +76,36 @@ class ReplayDataset:
         self.batch_size = int(batch_size)
         self.timeout = timeout
         self.prefetch = int(prefetch)
+        self.global_sampling = global_sampling
 
     def __iter__(self):
         if isinstance(self.table, replay.QueueTable):
             return _QueueIterator(self.table, self.batch_size, self.timeout)
-        return _TableIterator(self.table, self.batch_size, self.timeout, self.prefetch)
+        dp = _data_parallel()
+        shard = dp if (self.global_sampling if self.global_sampling is not None
+                       else dp is not None) else None
+        if shard is None and self.global_sampling:
+            raise ValueError("global_sampling needs an initialised torch.distributed group")
+        return _TableIterator(self.table, self.batch_size, self.timeout, self.prefetch, shard)
 
 
 class _TableIterator:
-    def __init__(self, table: replay.Table, batch: int, timeout: float, prefetch: int = 0):
+    def __init__(self, table: replay.Table, batch: int, timeout: float, prefetch: int = 0,
+                 shard=None):
         self._t = table
         self._B = batch
         self._timeout = timeout
         self._P = prefetch
         self._slots = None
         self._queue = []  # (slot index, ready event) of batches issued ahead
+        # Global-probability sampling over shards: (world, rank), buffers for shares of up to
+        # 2 B items, the mass snapshots by draw index, the share of each buffer slot.
+        self._shard = shard
+        self._rows = 2 * batch if shard is not None else batch
+        self._snaps = {}
+        self._share = {}
+        if shard is not None and isinstance(table, replay.FrameTable):
+            raise ValueError("global sampling over FrameTable shards is not supported")
 
     def _alloc(self):
         import ctypes
@@ -86,8 +117,16 @@ class _TableIterator:
             self._issued = torch.cuda.Event()
             self._ready = [torch.cuda.Event() for _ in range(self._P + 2)]
             self._next_slot = 0
+        if self._shard is not None:
+            import torch.distributed as dist
+            world = self._shard[0]
+            self._dist = dist
+            self._snap_ring = [(torch.zeros(world, dtype=torch.float64, device=dev),
+                                torch.zeros(world, dtype=torch.float64).pin_memory(),
+                                torch.cuda.Event()) for _ in range(self._P + 2 + 2 * _LAG)]
+            self._snap_next = 0
         for _ in range(self._P + 2 if self._P > 0 else 2):
-            info = native.alloc_sample_info(self._B)
+            info = native.alloc_sample_info(self._rows)
             fields = self._t.fields
             bufs = [None] * len(fields)
             # Transition items (o_tm1, a_tm1, r_t, d_t, o_t, ...): the two observations share
@@ -95,10 +134,11 @@ class _TableIterator:
             # reads both as one frame array without a packing copy.
             if (len(fields) >= 5 and fields[0].row_bytes == fields[4].row_bytes
                     and fields[0].dtype == fields[4].dtype and fields[0].shape == fields[4].shape):
-                pair = torch.empty(2, self._B, fields[0].row_bytes, dtype=torch.uint8, device=dev)
+                pair = torch.empty(2, self._rows, fields[0].row_bytes, dtype=torch.uint8,
+                                   device=dev)
                 bufs[0], bufs[4] = pair[0], pair[1]
             bufs = [b if b is not None else
-                    torch.empty(self._B, f.row_bytes, dtype=torch.uint8, device=dev)
+                    torch.empty(self._rows, f.row_bytes, dtype=torch.uint8, device=dev)
                     for b, f in zip(bufs, fields)]
             data = tree.unflatten_as(self._t._structure, [self._typed(b, f)  # noqa: SLF001
                                                           for b, f in zip(bufs, self._t.fields)])
@@ -116,9 +156,9 @@ class _TableIterator:
             self._slots.append((raw, ptrs, sample, info, bufs))
         self._which = 0
 
-    def _typed(self, buf, f):
-        B = self._B
-        x = buf if f.nbytes == f.row_bytes else buf[:, :f.nbytes]
+    def _typed(self, buf, f, rows=None):
+        B = self._rows if rows is None else rows
+        x = buf[:B] if f.nbytes == f.row_bytes else buf[:B, :f.nbytes]
         if f.dtype == np.bool_:
             return x.view(torch.bool).reshape((B,) + f.shape)
         return x.view(_TORCH[np.dtype(f.dtype)]).reshape((B,) + f.shape)
@@ -130,12 +170,19 @@ class _TableIterator:
     def __iter__(self):
         return self
 
-    def _draw(self, L, h, raw, ptrs, st):
+    def _draw(self, L, h, raw, ptrs, st, stream=None):
         """Sample + gather of one batch as a unit: no insert lands between the draw and the
-        row copy (actor threads may be inserting), so each row is that of its reported key."""
+        row copy (actor threads may be inserting), so each row is that of its reported key.
+        Returns the number of items drawn."""
         from acme_amd._lib import check
         t = self._t
         step = t.next_draw() & 0xFFFFFFFFFFFFFFFF
+        if self._shard is not None:
+            n, scale = self._shares(step)
+            check(L.acme_replay_sample_share(h, n, step, scale, *raw, ptrs, st),
+                  "replay sample")
+            self._snapshot(L, h, step, st, stream)
+            return n
         if isinstance(t, replay.FrameTable):  # stacks rebuilt from stored frames
             with t._mu:  # noqa: SLF001  (inserts commit under the table lock)
                 check(L.acme_replay_sample(h, self._B, step, *raw, st), "replay sample")
@@ -143,6 +190,49 @@ class _TableIterator:
         else:
             check(L.acme_replay_sample_gather(h, self._B, step, *raw, ptrs, st),
                   "replay sample")
+        return self._B
+
+    # -- global-probability sampling over shards (acme_amd.replay.sharding)
+    def _shares(self, step: int):
+        """(this rank's share n_r, probability scale n_r / (N B)) of draw `step`, from the
+        mass snapshot taken after draw step - LAG (equal shares before the first one)."""
+        world, rank = self._shard
+        NB = world * self._B
+        snap = self._snaps.pop(step - _LAG, None)
+        if snap is None:
+            n = self._B
+        else:
+            host, ev = snap
+            ev.synchronize()  # issued LAG draws ago: normally long complete
+            n = allocate_shares(host.tolist(), NB, cap=self._rows)[rank]
+        return n, n / NB
+
+    def _snapshot(self, L, h, step: int, st: int, stream) -> None:
+        from acme_amd._lib import check
+        world, rank = self._shard
+        dev_vec, host, ev = self._snap_ring[self._snap_next]
+        self._snap_next = (self._snap_next + 1) % len(self._snap_ring)
+        s = stream if stream is not None else torch.cuda.current_stream(self._t.native.device)
+        with torch.cuda.stream(s):
+            dev_vec.zero_()
+            check(L.acme_replay_total(h, dev_vec[rank:].data_ptr(), st), "replay total")
+            self._dist.all_reduce(dev_vec)  # SUM of one-hot masses: exact, identical on ranks
+            host.copy_(dev_vec, non_blocking=True)
+            ev.record(s)
+        self._snaps[step] = (host, ev)
+
+    def _sample_view(self, i: int, n: int) -> replay.ReplaySample:
+        """The first n rows of buffer slot i as a ReplaySample (shard draws vary in size)."""
+        raw, ptrs, sample, info, bufs = self._slots[i]
+        if n == self._rows:
+            return sample
+        data = tree.unflatten_as(self._t._structure, [self._typed(b, f, n)  # noqa: SLF001
+                                                      for b, f in zip(bufs, self._t.fields)])
+        return replay.ReplaySample(
+            info=replay.SampleInfo(key=info["keys"][:n], probability=info["probabilities"][:n],
+                                   table_size=info["table_size"][:n],
+                                   priority=info["priorities"][:n]),
+            data=data)
 
     def __next__(self) -> replay.ReplaySample:
         from acme_amd._lib import check, lib, stream_ptr
@@ -154,10 +244,11 @@ class _TableIterator:
             self._alloc()
         L, h = lib(), t.native.handle
         if self._P == 0:
-            raw, ptrs, sample = self._slots[self._which][:3]
+            i = self._which
+            raw, ptrs = self._slots[i][:2]
             self._which ^= 1
-            self._draw(L, h, raw, ptrs, stream_ptr())
-            return sample
+            n = self._draw(L, h, raw, ptrs, stream_ptr())
+            return self._sample_view(i, n)
         # Prefetch: order the dataset stream after everything queued so far on the caller's
         # stream (inserts, earlier learner steps and their priority updates), top the queue
         # up to P + 1 batches, hand out the oldest.
@@ -173,7 +264,7 @@ class _TableIterator:
             i = self._next_slot
             self._next_slot = (i + 1) % (self._P + 2)
             raw, ptrs = self._slots[i][:2]
-            self._draw(L, h, raw, ptrs, st)
+            self._share[i] = self._draw(L, h, raw, ptrs, st, side)
             self._ready[i].record(side)
             self._queue.append(i)
             t.set_reader_event(self._ready[i])
@@ -183,7 +274,7 @@ class _TableIterator:
         # cost (each event wait / record on a stream leaves ~7 us before the next kernel).
         if not self._ready[i].query():
             main.wait_event(self._ready[i])
-        return self._slots[i][2]
+        return self._sample_view(i, self._share[i])
 
 
 class _QueueIterator:
@@ -217,7 +308,8 @@ def make_reverb_dataset(server_address, environment_spec=None, batch_size: Optio
                         table: str = adders.DEFAULT_PRIORITY_TABLE,
                         parallel_batch_optimization: bool = True,
                         convert_zero_size_to_none: bool = False,
-                        using_deprecated_adder: bool = False) -> ReplayDataset:
+                        using_deprecated_adder: bool = False,
+                        global_sampling: Optional[bool] = None) -> ReplayDataset:
     """Same arguments as the reference.  `prefetch_size` issues that many batches ahead on
     the dataset's stream (module docstring); the parallel-batch knob of the tf.data pipeline
     has no equivalent; the environment/extra specs are only checked for consistency with
@@ -232,7 +324,8 @@ def make_reverb_dataset(server_address, environment_spec=None, batch_size: Optio
         sig = adders.NStepTransitionAdder.signature(environment_spec, extra_spec or ())
         if t.fields is not None and len(tree.flatten(sig)) != len(t.fields):
             raise ValueError("environment_spec does not match the table's item layout")
-    return ReplayDataset(t, batch_size, prefetch=prefetch_size or 0)
+    return ReplayDataset(t, batch_size, prefetch=prefetch_size or 0,
+                         global_sampling=global_sampling)
 
 
 make_dataset = make_reverb_dataset

@@ -373,8 +373,11 @@ class NativeDQN:
             np.float32).copy()
 
     # --------------------------------------------------------------- step
-    def _batch(self, o_tm1, a_tm1, r_t, d_t, o_t, probabilities, global_min_probability=None):
+    def _batch(self, o_tm1, a_tm1, r_t, d_t, o_t, probabilities, global_min_probability=None,
+               mean_over=None):
         B = int(a_tm1.shape[0])
+        if B < 1 or B > self.max_batch:
+            raise ValueError(f"batch of {B} rows: the learner takes 1..{self.max_batch}")
         for name, t in (("o_tm1", o_tm1), ("a_tm1", a_tm1), ("r_t", r_t), ("d_t", d_t),
                         ("o_t", o_t), ("probabilities", probabilities)):
             if not (isinstance(t, torch.Tensor) and t.is_cuda and t.is_contiguous()):
@@ -394,6 +397,7 @@ class NativeDQN:
         tb.probabilities = ptr(probabilities)
         tb.batch = B
         tb.global_min_probability = ptr(global_min_probability)
+        tb.mean_over = int(mean_over or 0)
         return tb
 
     def _outputs(self, q_tm1=None):
@@ -409,10 +413,12 @@ class NativeDQN:
                                               stream_ptr(stream)), "dqn forward_backward")
 
     def forward_backward_stage(self, stage: int, *batch, global_min_probability=None,
-                               q_tm1=None, stream=None):
+                               q_tm1=None, stream=None, mean_over=None):
         """Stage 0: forwards, loss, head/dense backward (grads[grad_split:]); stage 1: torso
-        backward (grads[:grad_split])."""
-        tb = self._batch(*batch, global_min_probability=global_min_probability)
+        backward (grads[:grad_split]).  mean_over: the batch mean's denominator (default
+        the batch; a data-parallel share passes the nominal per-rank batch)."""
+        tb = self._batch(*batch, global_min_probability=global_min_probability,
+                         mean_over=mean_over)
         out = self._outputs(q_tm1)
         check(lib().acme_dqn_forward_backward_stage(self._h, ctypes.byref(tb), ctypes.byref(out),
                                                     int(stage), stream_ptr(stream)),

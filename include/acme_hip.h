@@ -143,6 +143,21 @@ int acme_replay_sample_gather(acme_replay* r, int64_t batch, uint64_t step_count
                               int64_t* table_size, double* priorities, void* const* out_fields,
                               void* stream);
 
+/* Data-parallel global-probability sampling: one table per rank holds a
+ * shard of the global replay.  acme_replay_total writes the shard's sampling mass S_r
+ * (sum of p^alpha, or the item count for Uniform) to out[0] on the device; the ranks
+ * all-gather the masses, allocate the global batch N * B in proportion (n_r / (N B) =
+ * S_r / S), and each draws its share n_r from its own shard with
+ * acme_replay_sample_share(prob_scale = n_r / (N B)), which reports
+ * probability = prob_scale * p^alpha / S_r — the item's marginal probability of being
+ * drawn by the global draw, p^alpha / S_global when the shares are proportional — and, when
+ * out_fields is non-NULL, gathers the rows as acme_replay_sample_gather does. */
+int acme_replay_total(acme_replay* r, double* out, void* stream);
+int acme_replay_sample_share(acme_replay* r, int64_t batch, uint64_t step_counter,
+                             double prob_scale, int64_t* slots, uint64_t* keys,
+                             double* probabilities, int64_t* table_size, double* priorities,
+                             void* const* out_fields, void* stream);
+
 /* Frame-deduplicated observations: rebuild `batch` stacked
  * observations out[b] = stack(frames[idx[b][0..stack-1]], axis=-1) (uint8 HWC, as
  * acme/wrappers/frame_stacking.py:78-83 builds them) from a device frame ring
@@ -254,6 +269,11 @@ typedef struct acme_transition_batch {
   /* If non-NULL: the minimum probability over the GLOBAL batch (data-parallel),
    * else the local batch minimum is used for the IS-weight max. */
   const double* global_min_probability;
+  /* Denominator of the batch mean (loss and its gradient): 0 = batch.  A data-parallel
+   * rank holding a share of a global batch of N * mean_over rows passes the nominal
+   * per-rank batch, so that the all-reduce mean of the ranks' gradients is the global
+   * batch's mean whatever the shares. */
+  int64_t mean_over;
 } acme_transition_batch;
 
 typedef struct acme_dqn_outputs {

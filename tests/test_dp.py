@@ -144,3 +144,157 @@ def test_dp_learner_matches_global_batch_gpu():
     # to within lr on elements whose gradient is at the rounding floor.
     np.testing.assert_allclose(res[0], got, rtol=1e-5, atol=1e-3 + 1e-6)
     assert np.mean(np.abs(res[0] - got) <= 1e-5 * np.abs(got) + 1e-6) > 0.98
+
+
+# ------------------------------------------------------------ global-probability sharding
+
+def test_allocate_shares_proportional_and_deterministic():
+    from acme_amd.replay.sharding import allocate_shares
+    assert allocate_shares([1.0, 1.0], 64) == [32, 32]
+    assert allocate_shares([1.0, 3.0], 64) == [16, 48]
+    s = allocate_shares([0.2, 0.5, 0.3001], 100)
+    assert sum(s) == 100 and s == [20, 50, 30]
+    rng = np.random.default_rng(0)
+    for _ in range(200):
+        tot = rng.uniform(0.0, 10.0, 8) ** 3
+        n = int(rng.integers(8, 5000))
+        s = allocate_shares(tot, n, cap=2 * -(-n // 8) + 8)
+        assert sum(s) == n and min(s) >= 1
+        q = n * tot / tot.sum()
+        slack = 1.0 + np.sum(q < 1.0)  # the one-draw minimum moves a draw per tiny shard
+        assert (np.abs(np.array(s) - q) < slack + 1e-9).all() or max(s) == 2 * -(-n // 8) + 8
+        assert s == allocate_shares(list(tot), n, cap=2 * -(-n // 8) + 8)
+    # a shard with almost no mass still draws one item; the cap moves the excess elsewhere
+    assert allocate_shares([1e-12, 1.0], 10) == [1, 9]
+    assert allocate_shares([1.0, 100.0], 10, cap=6) == [4, 6]
+    with pytest.raises(RuntimeError):
+        allocate_shares([0.0, 0.0], 10)
+
+
+def _shard_item(rank, key):
+    x = np.sin(np.arange(1, 7, dtype=np.float64) * (key + 1) * (rank + 1.7)).astype(np.float32)
+    return (x, np.int32((key + rank) % 3), np.float32(np.cos(key * 0.37 + rank)),
+            np.float32(0.96 if key % 11 else 0.0), (x * 0.5 + 0.25).astype(np.float32))
+
+
+def _shard_priorities(rank, n):
+    rng = np.random.default_rng(100 + rank)
+    return rng.uniform(0.5, 1.5, n) * (1.0 if rank == 0 else 4.0)
+
+
+SHARD_CAP, SHARD_B, SHARD_STEPS = 400, 32, 5
+
+
+def _sharded_worker(rank, world, port, prefetch, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from acme_amd import replay, specs
+    from acme_amd.adders import reverb as adders
+    from acme_amd.agents.dqn import DQNLearner
+    from acme_amd.datasets import make_reverb_dataset
+    from acme_amd.networks import MLP
+    from acme_amd.utils import loggers
+    spec = specs.EnvironmentSpec(
+        observations=specs.Array((6,), np.float32), actions=specs.DiscreteArray(3, np.int32),
+        rewards=specs.Array((), np.float32), discounts=specs.BoundedArray((), np.float32, 0, 1))
+    table = replay.Table(adders.DEFAULT_PRIORITY_TABLE, replay.selectors.Prioritized(0.6),
+                         replay.selectors.Fifo(), SHARD_CAP, replay.rate_limiters.MinSize(1),
+                         signature=adders.NStepTransitionAdder.signature(spec), seed=100 + rank,
+                         device=torch.device("cuda", 0))
+    for k, p in enumerate(_shard_priorities(rank, SHARD_CAP)):
+        table.insert(_shard_item(rank, k), float(p))
+    table.flush()
+    server = replay.Server([table])
+    ds = make_reverb_dataset(server, batch_size=SHARD_B, prefetch_size=prefetch)
+    records = []
+
+    class _Rec:
+        def __init__(self, it):
+            self.it = it
+            self.batch_size = SHARD_B
+
+        def __iter__(self):
+            return self
+
+        def __next__(self):
+            s = next(self.it)
+            records.append((s.info.key.cpu().numpy().view(np.uint64).copy(),
+                            s.info.probability.cpu().numpy().copy()))
+            return s
+
+    net = MLP(6, [16, 16], 3)
+    learner = DQNLearner(net, net, 0.99, 0.2, 1e-3, 100, _Rec(iter(ds)),
+                         logger=loggers.NoOpLogger(), seed=0)
+    for _ in range(SHARD_STEPS):
+        learner.step()
+    torch.cuda.synchronize()
+    q.put((rank, records, learner.native.params.cpu().numpy()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prefetch", [0, 2])
+def test_sharded_global_sampling_gpu(prefetch):
+    """Two ranks, each a 400-slot shard (rank 1's priorities 4x rank 0's): every draw is
+    bit-identical to the oracle's global draw (shares from the mass snapshot LAG draws
+    earlier, each shard's own Philox stream, probability = share scale x p^a / S_r = the
+    global marginal); the replicas' parameters after five steps equal a single learner
+    stepping on the union batch with those probabilities, averaged over N * B."""
+    from acme_amd.native import NativeDQN
+    from acme_amd.networks import MLP
+    from acme_amd.replay.sharding import LAG, allocate_shares
+    from tests._oracle import OracleTable
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, prefetch, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, recs, params = q.get(timeout=300)
+        res[r] = (recs, params)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    np.testing.assert_array_equal(res[0][1], res[1][1])  # replicas identical
+    orc = []
+    for r in range(world):
+        o = OracleTable(SHARD_CAP, True, 0.6, 100 + r)
+        o.insert(_shard_priorities(r, SHARD_CAP))
+        orc.append(o)
+    NB = world * SHARD_B
+    totals = [o.total() for o in orc]
+    shares_seen = []
+    for k in range(SHARD_STEPS):
+        shares = ([SHARD_B] * world if k < LAG
+                  else allocate_shares(totals, NB, cap=2 * SHARD_B))
+        shares_seen.append(shares)
+        for r in range(world):
+            keys, probs = res[r][0][k]
+            ref = orc[r].sample(shares[r], k)
+            np.testing.assert_array_equal(keys, ref["keys"], err_msg=f"step {k} rank {r}")
+            np.testing.assert_array_equal(probs, ref["probabilities"] * (shares[r] / NB))
+    assert shares_seen[-1][1] > 2 * shares_seen[-1][0]  # rank 1 holds ~4x the mass
+    # Marginals: share_r / NB * p^a / S_r == p^a / S up to the integer rounding of shares.
+    S = sum(totals)
+    keys, probs = res[1][0][-1]
+    lv = orc[1].leaves()[keys.astype(np.int64)]
+    np.testing.assert_allclose(probs, lv / S, rtol=2.0 / shares_seen[-1][1])
+    # One learner on the union batches, mean over N * B.
+    net = MLP(6, [16, 16], 3)
+    d = NativeDQN(network="mlp", num_actions=3, max_batch=2 * NB, obs_dtype="float32",
+                  obs_dim=6, hidden=(16, 16), discount=0.99, importance_sampling_exponent=0.2,
+                  learning_rate=1e-3, target_update_period=100)
+    d.set_params(net.init(0), net.init(1))
+    for k in range(SHARD_STEPS):
+        items = [_shard_item(r, int(key)) for r in range(world) for key in res[r][0][k][0]]
+        cols = [np.stack([it[c] for it in items]) for c in range(5)]
+        probs = np.concatenate([res[r][0][k][1] for r in range(world)])
+        dev = [torch.as_tensor(x).cuda().contiguous() for x in cols + [probs]]
+        d.step(*dev)
+    got = d.params.cpu().numpy()
+    np.testing.assert_allclose(res[0][1], got, rtol=1e-5, atol=1e-3 + 1e-6)
+    assert np.mean(np.abs(res[0][1] - got) <= 1e-5 * np.abs(got) + 1e-6) > 0.98
