@@ -244,6 +244,126 @@ __global__ void __launch_bounds__(256) gather_fields_kernel(GatherArgs g,
   }
 }
 
+// Row gather as wave-sized pieces.  A piece is what one wave-instruction moves: 64 lanes x
+// 16 B = 1 KiB of ONE row of one field (pieces never cross rows, so the row, its slot and
+// the field are wave-uniform scalars).  Rows of at least 1 KiB (the 28,224-B Atari frames:
+// 28 pieces, the last one 576 B) are split into pieces, field-major then row then piece;
+// each wave takes K consecutive pieces, issues all K loads, then the K stores, and strides
+// over the rest.  Smaller rows (a, r, d) are copied 64 rows per wave by 4-B words after the
+// big fields.  Source rows are read once, so they are loaded non-temporal.
+struct PieceArgs {
+  const uint8_t* src[ACME_MAX_FIELDS];
+  uint8_t* dst[ACME_MAX_FIELDS];
+  int32_t bytes[ACME_MAX_FIELDS];
+  int32_t ppr[ACME_MAX_FIELDS];    // pieces per row of a big field (0: small field)
+  int32_t first[ACME_MAX_FIELDS + 1];  // first piece of each big field; first[nbig] = total
+  int32_t big[ACME_MAX_FIELDS];    // field indices of the big fields, then the small ones
+  int32_t nbig, nsmall;
+};
+
+using vu4 = __attribute__((ext_vector_type(4))) uint32_t;
+
+template <int K>
+__global__ void __launch_bounds__(256) gather_pieces_kernel(PieceArgs args,
+                                                            const int64_t* __restrict__ slots,
+                                                            int32_t batch) {
+  __shared__ PieceArgs a;  // LDS copy of the tables (see gather_row_kernel)
+  if (threadIdx.x == 0) a = args;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int32_t nwaves = gridDim.x * 4;
+  const int32_t total = a.first[a.nbig];
+  for (int32_t p0 = wave * K; p0 < total; p0 += nwaves * K) {
+    vu4 v[K];
+    uint8_t* dst[K];
+    bool ok[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int32_t p = p0 + k;
+      ok[k] = false;
+      dst[k] = nullptr;
+      if (p >= total) continue;
+      int i = 0;
+      while (i + 1 < a.nbig && p >= a.first[i + 1]) ++i;
+      const int f = a.big[i];
+      const int32_t local = p - a.first[i];
+      const int32_t r = local / a.ppr[i];
+      const int32_t q = local - r * a.ppr[i];
+      const int32_t off = q * 1024 + lane * 16;
+      ok[k] = off < a.bytes[f];
+      const int64_t slot = slots[r];
+      const vu4* s = reinterpret_cast<const vu4*>(a.src[f] + slot * a.bytes[f] + off);
+      dst[k] = a.dst[f] + (int64_t)r * a.bytes[f] + off;
+      if (ok[k]) v[k] = __builtin_nontemporal_load(s);
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if (ok[k]) *reinterpret_cast<vu4*>(dst[k]) = v[k];
+  }
+  // Small fields: wave w copies rows [64 w', 64 w' + 64) of small field s, 4 B per step.
+  const int32_t per = (batch + 63) / 64;
+  for (int32_t w = wave; w < a.nsmall * per; w += nwaves) {
+    const int f = a.big[a.nbig + w / per];
+    const int32_t r = (w % per) * 64 + lane;
+    if (r >= batch) continue;
+    const int64_t slot = slots[r];
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(a.src[f] + slot * a.bytes[f]);
+    uint32_t* d = reinterpret_cast<uint32_t*>(a.dst[f] + (int64_t)r * a.bytes[f]);
+    for (int j = 0; j < a.bytes[f] / 4; ++j) d[j] = s[j];
+  }
+}
+
+// The transition layout (two equal big rows o_tm1 / o_t, small a / r / d): one workgroup per
+// sampled row moves both big rows (2 x nvec 16-B chunks, up to MAXC per thread, all loads
+// issued before the first store) and the small rows.  Every address comes from kernel
+// arguments and the row's slot, so the loads are global loads with nothing between them
+// that waits on memory.
+struct SmallFields {
+  const uint8_t* src[ACME_MAX_FIELDS];
+  uint8_t* dst[ACME_MAX_FIELDS];
+  int32_t words[ACME_MAX_FIELDS];
+  int32_t n;
+};
+
+template <int T, int MAXC, bool NT>
+__global__ void __launch_bounds__(T) gather_pair_kernel(const uint8_t* __restrict__ s0,
+                                                        const uint8_t* __restrict__ s1,
+                                                        uint8_t* __restrict__ d0,
+                                                        uint8_t* __restrict__ d1, int32_t nvec,
+                                                        SmallFields sm,
+                                                        const int64_t* __restrict__ slots) {
+  const int64_t r = blockIdx.x;
+  const int64_t slot = slots[r];
+  const int64_t rb = (int64_t)nvec * 16;
+  const vu4* a0 = reinterpret_cast<const vu4*>(s0 + slot * rb);
+  const vu4* a1 = reinterpret_cast<const vu4*>(s1 + slot * rb);
+  vu4* b0 = reinterpret_cast<vu4*>(d0 + r * rb);
+  vu4* b1 = reinterpret_cast<vu4*>(d1 + r * rb);
+  vu4 v[MAXC];
+#pragma unroll
+  for (int k = 0; k < MAXC; ++k) {
+    // Unconditional loads (a lane past the end re-reads the last chunk): a load under a
+    // branch gets a full vmcnt(0) wait at the join, which would serialise the row.
+    const int32_t c = min(threadIdx.x + k * T, 2 * nvec - 1);
+    const vu4* p = c < nvec ? a0 + c : a1 + (c - nvec);
+    v[k] = NT ? __builtin_nontemporal_load(p) : *p;
+  }
+#pragma unroll
+  for (int k = 0; k < MAXC; ++k) {
+    const int32_t c = threadIdx.x + k * T;
+    vu4* p = c < nvec ? b0 + c : b1 + (c - nvec);
+    if (c < 2 * nvec) *p = v[k];
+  }
+#pragma unroll
+  for (int q = 0; q < ACME_MAX_FIELDS; ++q) {
+    if (q >= sm.n) break;
+    for (int w = threadIdx.x; w < sm.words[q]; w += T)
+      reinterpret_cast<uint32_t*>(sm.dst[q] + r * 4 * sm.words[q])[w] =
+          reinterpret_cast<const uint32_t*>(sm.src[q] + slot * 4 * sm.words[q])[w];
+  }
+}
+
 // Recompute level[l] nodes from their 64 children (one wave per node).
 // Mode A: contiguous node range [node_begin, node_begin + count).
 // Mode B: node = slots[j] >> (6 l) for j < count (duplicates recompute identically).
@@ -1029,6 +1149,70 @@ int acme_replay_gather(acme_replay* r, const int64_t* slots, int64_t batch,
   double row_bytes = 0;
   for (int k = 0; k < r->cfg.num_fields; ++k) row_bytes += (double)r->cfg.field_bytes[k];
   ACME_PROF("replay_gather", st, 0.0, 2.0 * row_bytes * (double)batch + 8.0 * (double)batch);
+  // Pieces path: every field a multiple of 4 B (always: acme_replay_create checks it) and
+  // 16-B aligned rows and buffers for the big fields.
+  bool pieces = tune_variant("GATH") != 1;
+  PieceArgs pa = {};
+  int64_t total = 0;
+  for (int f = 0; f < r->cfg.num_fields && pieces; ++f) {
+    const int64_t nb = r->cfg.field_bytes[f];
+    if (nb < 1024) continue;
+    pieces = nb % 16 == 0 && reinterpret_cast<uintptr_t>(g.dst[f]) % 16 == 0;
+    pa.big[pa.nbig] = f;
+    pa.ppr[pa.nbig] = (int32_t)ceil_div(nb, 1024);
+    pa.first[pa.nbig] = (int32_t)total;
+    total += (int64_t)pa.ppr[pa.nbig] * batch;
+    pa.nbig++;
+  }
+  pieces = pieces && total < (int64_t(1) << 30) && pa.nbig > 0;
+  const int gv = tune_variant("GATH");
+  // Transition layout: exactly two big fields of equal bytes, the rest small.
+  if (pieces && pa.nbig == 2 && r->cfg.field_bytes[pa.big[0]] == r->cfg.field_bytes[pa.big[1]] &&
+      gv == 0) {
+    const int f0 = pa.big[0], f1 = pa.big[1];
+    const int32_t nvec = (int32_t)(r->cfg.field_bytes[f0] / 16);
+    SmallFields sm = {};
+    for (int f = 0; f < r->cfg.num_fields; ++f)
+      if (f != f0 && f != f1) {
+        sm.src[sm.n] = g.src[f];
+        sm.dst[sm.n] = g.dst[f];
+        sm.words[sm.n] = (int32_t)(r->cfg.field_bytes[f] / 4);
+        sm.n++;
+      }
+    const unsigned gb = (unsigned)batch;
+    bool done = true;
+    // Measured (tools/gather_bench.py, 1M-slot Atari table, B = 512): 256 threads x 14
+    // chunks 12.05 us (4.80 TB/s), 1024 x 4 12.17 us, 512 x 7 12.45 us; plain loads instead
+    // of non-temporal 12.85 us; the contiguous copy of the same bytes 11.2 us.
+    if (2 * nvec <= 256 * 14)
+      gather_pair_kernel<256, 14, true><<<gb, 256, 0, st>>>(g.src[f0], g.src[f1], g.dst[f0],
+                                                             g.dst[f1], nvec, sm, slots);
+    else if (2 * nvec <= 1024 * 16)
+      gather_pair_kernel<1024, 16, true><<<gb, 1024, 0, st>>>(g.src[f0], g.src[f1], g.dst[f0],
+                                                               g.dst[f1], nvec, sm, slots);
+    else
+      done = false;
+    if (done) {
+      ACME_LAUNCH_CHECK();
+      return ACME_OK;
+    }
+  }
+  if (pieces && gv != 1) {
+    pa.first[pa.nbig] = (int32_t)total;
+    for (int f = 0; f < r->cfg.num_fields; ++f) {
+      pa.src[f] = g.src[f];
+      pa.dst[f] = g.dst[f];
+      pa.bytes[f] = (int32_t)r->cfg.field_bytes[f];
+      if (r->cfg.field_bytes[f] < 1024) pa.big[pa.nbig + pa.nsmall++] = f;
+    }
+    constexpr int K = 8;
+    const int gcap = tune_variant("GATHG") > 0 ? tune_variant("GATHG") : 2048;
+    const int64_t waves = std::max(ceil_div(total, K), (int64_t)pa.nsmall * ceil_div(batch, 64));
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(waves, 4), gcap));
+    gather_pieces_kernel<K><<<grid, 256, 0, st>>>(pa, slots, (int32_t)batch);
+    ACME_LAUNCH_CHECK();
+    return ACME_OK;
+  }
   gather_fields_kernel<<<dim3((unsigned)batch, (unsigned)r->cfg.num_fields), 256, 0, st>>>(g, slots);
   ACME_LAUNCH_CHECK();
   return ACME_OK;

@@ -208,3 +208,31 @@ def test_prefetched_dataset_draw_order(prefetch):
         client.update_priorities(adders.DEFAULT_PRIORITY_TABLE, s.info.key,
                                  torch.as_tensor(newp).cuda())
         o.update(keys, newp)
+
+
+@pytest.mark.parametrize("fields", [[28224, 4, 4, 4, 28224], [28224, 4, 4], [2048, 1040, 8],
+                                    [96, 24, 4, 4, 96], [1024, 4, 1024], [3072, 12, 3072]])
+def test_gather_kernels_bit_identical(fields):
+    """The gather kernels (acme_tune_set GATH: 0 = transition pair / pieces default, 1 =
+    row-per-workgroup, 2 = wave pieces) copy exactly the sampled rows."""
+    from acme_amd._lib import lib
+    rng = np.random.default_rng(len(fields) * 31 + fields[0])
+    cap, n, B = 700, 900, 333
+    data = [rng.integers(0, 256, (n, b), dtype=np.uint8) for b in fields]
+    r = _native(cap, fields, True)
+    r.insert(data, rng.uniform(0.1, 2.0, n))
+    s = r.sample(B, 4)
+    keys = s["keys"].cpu().numpy().view(np.int64)
+    outs = {}
+    for gv in (0, 1, 2):
+        lib().acme_tune_set(b"GATH", gv)
+        try:
+            o = [torch.full((B, b), 7, dtype=torch.uint8, device="cuda") for b in fields]
+            r.gather(s["slots"], o)
+            outs[gv] = [x.cpu().numpy() for x in o]
+        finally:
+            lib().acme_tune_set(b"GATH", 0)
+    for f, b in enumerate(fields):
+        np.testing.assert_array_equal(outs[0][f], data[f][keys])
+        np.testing.assert_array_equal(outs[1][f], outs[0][f])
+        np.testing.assert_array_equal(outs[2][f], outs[0][f])
