@@ -23,6 +23,8 @@ void set_error(const char* fmt, ...);
 // per key); 0 is the shipped default.
 int tune_variant(const char* key);
 void tune_set(const char* key, int value);
+// Incremented by every tune_set: cached launch plans (captured graphs) keyed on it.
+int tune_generation();
 
 #define ACME_HIP_TRY(expr)                                                   \
   do {                                                                       \

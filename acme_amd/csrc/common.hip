@@ -21,7 +21,13 @@ void set_error(const char* fmt, ...) {
 namespace {
 std::mutex g_tune_mu;
 std::vector<std::pair<std::string, int>> g_tune;  // key -> value (env, or acme_tune_set)
+int g_tune_gen = 0;
 }  // namespace
+
+int tune_generation() {
+  std::lock_guard<std::mutex> lock(g_tune_mu);
+  return g_tune_gen;
+}
 
 int tune_variant(const char* key) {
   std::lock_guard<std::mutex> lock(g_tune_mu);
@@ -35,6 +41,7 @@ int tune_variant(const char* key) {
 
 void tune_set(const char* key, int value) {
   std::lock_guard<std::mutex> lock(g_tune_mu);
+  ++g_tune_gen;
   for (auto& kv : g_tune)
     if (kv.first == key) {
       kv.second = value;

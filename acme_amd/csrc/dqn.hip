@@ -106,6 +106,21 @@ struct acme_dqn {
   // by the backward; forward_backward_stage leaves its arguments here.
   LossArgs pending_la{};
   bool loss_pending = false;
+  // Adam's step count on the device for captured step graphs (a replay reads it); valid
+  // (equal to num_steps) while dev_steps_synced.
+  int64_t* dev_steps = nullptr;
+  bool dev_steps_synced = true;
+  // Captured steps (acme_dqn_step on the plane path), keyed by the batch / output pointers,
+  // B, the mean denominator and whether the step copies the target.
+  struct Graph {
+    const void* key[11];
+    int64_t B, mean_over;
+    bool copy;
+    int tune_gen;
+    hipGraphExec_t exec;
+  };
+  std::vector<Graph> graphs;
+  hipStream_t capture = nullptr;
 };
 
 namespace {
@@ -706,8 +721,11 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
       (rc = dev_alloc(l, &l->slab, l->slab_floats)) ||
       (rc = dev_alloc(l, &l->g, (int64_t)B)) || (rc = dev_alloc(l, &l->a_cache, (int64_t)B)) ||
       (rc = dev_alloc(l, &l->loss_tmp, 4)) || (rc = dev_alloc(l, &l->td_tmp, (int64_t)B)) ||
-      (rc = dev_alloc(l, &l->prio_tmp, (int64_t)B)))
+      (rc = dev_alloc(l, &l->prio_tmp, (int64_t)B)) || (rc = dev_alloc(l, &l->dev_steps, 1)))
     return fail(rc);
+  if (hipMemset(l->dev_steps, 0, sizeof(int64_t)) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess)
+    return fail((set_error("step counter init failed"), ACME_ERR_HIP));
   *out = l;
   return ACME_OK;
 }
@@ -715,6 +733,8 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
 int acme_dqn_destroy(acme_dqn* l) {
   if (!l) return ACME_OK;
   (void)hipDeviceSynchronize();
+  for (auto& g : l->graphs) (void)hipGraphExecDestroy(g.exec);
+  if (l->capture) (void)hipStreamDestroy(l->capture);
   for (void* p : l->allocs) (void)hipFree(p);
   for (auto& e : l->ev)
     if (e) (void)hipEventDestroy(e);
@@ -751,6 +771,12 @@ int acme_dqn_bind(acme_dqn* l, float* params, float* target, float* grads, float
   l->m = adam_m;
   l->v = adam_v;
   l->planes_stale = true;
+  // Captured graphs bake in the bound buffers: a re-bind invalidates them.
+  if (!l->graphs.empty()) {
+    ACME_HIP_TRY(hipDeviceSynchronize());
+    for (auto& g : l->graphs) (void)hipGraphExecDestroy(g.exec);
+    l->graphs.clear();
+  }
   return ACME_OK;
 }
 
@@ -763,7 +789,10 @@ int acme_dqn_params_changed(acme_dqn* l) {
 int64_t acme_dqn_num_steps(const acme_dqn* l) { return l ? l->num_steps : 0; }
 int acme_dqn_set_num_steps(acme_dqn* l, int64_t n) {
   ACME_CHECK_ARG(l && n >= 0, "bad argument");
+  ACME_HIP_TRY(hipDeviceSynchronize());
+  ACME_HIP_TRY(hipMemcpy(l->dev_steps, &n, sizeof(int64_t), hipMemcpyHostToDevice));
   l->num_steps = n;
+  l->dev_steps_synced = true;
   return ACME_OK;
 }
 
@@ -996,21 +1025,20 @@ int acme_dqn_grad_split(const acme_dqn* l, int64_t* split) {
   return ACME_OK;
 }
 
-int acme_dqn_apply(acme_dqn* l, void* stream) {
-  ACME_CHECK_ARG(l && l->params, "unbound learner");
-  hipStream_t st = as_stream(stream);
-  const int64_t t = l->num_steps + 1;  // snt.Adam / optix.adam count this step first
+// Adam (+ the parameter planes) and the periodic target copy; `copy` decided by the host.
+// graph: the step count is read from (and advanced on) the device, for a captured step.
+static int apply_impl(acme_dqn* l, bool copy, hipStream_t st, bool graph = false) {
   const bool jax = l->cfg.semantics == ACME_SEMANTICS_JAX;
   ACME_PROF("adam", st, 0.0, 28.0 * (double)l->logical);
-  // The parameter planes (plane path) are refreshed by the same pass.
+  // The parameter planes (plane path) are refreshed by the same pass.  t = num_steps + 1
+  // (snt.Adam / optix.adam count this step first).
   int rc = launch_adam(l->params, l->grads, l->m, l->v, l->flat, l->cfg.learning_rate,
-                       l->cfg.adam_beta1, l->cfg.adam_beta2, l->cfg.adam_epsilon, t,
-                       l->p3_capable ? l->wpl : nullptr, l->flat, st, jax ? 1 : 0);
+                       l->cfg.adam_beta1, l->cfg.adam_beta2, l->cfg.adam_epsilon,
+                       l->num_steps + 1, l->p3_capable ? l->wpl : nullptr, l->flat, st,
+                       jax ? 1 : 0, graph ? l->dev_steps : nullptr);
   if (rc != ACME_OK) return rc;
-  // TF: copy when num_steps % period == 0, then num_steps += 1 (tf/dqn/learning.py:157-161);
-  // JAX: steps + 1 first, copy when that is a multiple of the period (jax/dqn/learning.py:114-119).
-  const int64_t copy_at = jax ? l->num_steps + 1 : l->num_steps;
-  if (copy_at % l->cfg.target_update_period == 0) {
+  if (!graph) l->dev_steps_synced = false;
+  if (copy) {
     ACME_PROF("target_copy", st, 0.0, 8.0 * (double)l->logical);
     ACME_HIP_TRY(hipMemcpyAsync(l->target, l->params, l->flat * sizeof(float),
                                 hipMemcpyDeviceToDevice, st));
@@ -1018,15 +1046,119 @@ int acme_dqn_apply(acme_dqn* l, void* stream) {
       ACME_HIP_TRY(hipMemcpyAsync(l->tpl, l->wpl, 3 * l->flat * sizeof(uint16_t),
                                   hipMemcpyDeviceToDevice, st));
   }
+  return ACME_OK;
+}
+
+// TF: copy when num_steps % period == 0, then num_steps += 1 (tf/dqn/learning.py:157-161);
+// JAX: steps + 1 first, copy when that is a multiple of the period (jax/dqn/learning.py:114-119).
+static bool copies_target(const acme_dqn* l) {
+  const int64_t at = l->cfg.semantics == ACME_SEMANTICS_JAX ? l->num_steps + 1 : l->num_steps;
+  return at % l->cfg.target_update_period == 0;
+}
+
+int acme_dqn_apply(acme_dqn* l, void* stream) {
+  ACME_CHECK_ARG(l && l->params, "unbound learner");
+  int rc = apply_impl(l, copies_target(l), as_stream(stream));
+  if (rc != ACME_OK) return rc;
   l->num_steps += 1;
+  return ACME_OK;
+}
+
+// ------------------------------------------------------------------ step graphs
+// A plane-path step is ~40 launches on two streams joined by events; each event record or
+// wait on the caller's queue leaves it idle for several microseconds before its next kernel
+// (DESIGN §4.1).  The step is captured once per (batch / output pointers, B, mean
+// denominator, target copy) on a private stream — the side stream's fork / join become graph
+// edges — and replayed with one hipGraphLaunch on the caller's stream.  Measured slower
+// than the eager two-stream step (0.744 vs 0.725 ms per step at B = 512: in the eager trace
+// the GPU idles only 29 us per step, the rest is the two streams' kernels contending), so it
+// is opt-in: ACME_V_DQNGRAPH=2.  The section profiler bypasses it.
+static bool dqn_graphs_enabled() {
+  return tune("DQNGRAPH") == 2 && !prof::enabled();
+}
+
+static int step_impl(acme_dqn* l, const acme_transition_batch* batch, const acme_dqn_outputs* out,
+                     bool copy, hipStream_t st, bool graph = false) {
+  int rc = forward_backward_stage(l, batch, out, 0, st, false);
+  if (rc == ACME_OK) rc = forward_backward_stage(l, batch, out, 1, st, false);
+  if (rc == ACME_OK) rc = apply_impl(l, copy, st, graph);
+  return rc;
+}
+
+static int run_step_graph(acme_dqn* l, const acme_transition_batch* b, const acme_dqn_outputs* out,
+                          bool copy, hipStream_t st) {
+  const void* key[11] = {b->o_tm1, b->a_tm1, b->r_t, b->d_t, b->o_t, b->probabilities,
+                         b->global_min_probability, out ? out->loss : nullptr,
+                         out ? out->td_error : nullptr, out ? out->priorities : nullptr,
+                         out ? out->q_tm1 : nullptr};
+  for (auto& g : l->graphs)
+    if (g.B == b->batch && g.mean_over == b->mean_over && g.copy == copy &&
+        g.tune_gen == tune_generation() && memcmp(g.key, key, sizeof(key)) == 0) {
+      ACME_HIP_TRY(hipGraphLaunch(g.exec, st));
+      return ACME_OK;
+    }
+  if (l->graphs.size() >= 32) {  // a caller cycling many buffers: start over
+    ACME_HIP_TRY(hipStreamSynchronize(st));
+    for (auto& g : l->graphs) (void)hipGraphExecDestroy(g.exec);
+    l->graphs.clear();
+  }
+  if (!l->capture) ACME_HIP_TRY(hipStreamCreateWithFlags(&l->capture, hipStreamNonBlocking));
+  ACME_HIP_TRY(hipStreamBeginCapture(l->capture, hipStreamCaptureModeRelaxed));
+  int rc = step_impl(l, b, out, copy, l->capture, true);
+  hipGraph_t graph = nullptr;
+  hipError_t e = hipStreamEndCapture(l->capture, &graph);
+  if (rc != ACME_OK) {
+    if (graph) (void)hipGraphDestroy(graph);
+    return rc;
+  }
+  if (e != hipSuccess) {
+    set_error("step graph capture failed: %s", hipGetErrorString(e));
+    return ACME_ERR_HIP;
+  }
+  hipGraphExec_t exec = nullptr;
+  e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(graph);
+  if (e != hipSuccess) {
+    set_error("step graph instantiation failed: %s", hipGetErrorString(e));
+    return ACME_ERR_HIP;
+  }
+  acme_dqn::Graph g;
+  memcpy(g.key, key, sizeof(key));
+  g.B = b->batch;
+  g.mean_over = b->mean_over;
+  g.copy = copy;
+  g.tune_gen = tune_generation();
+  g.exec = exec;
+  l->graphs.push_back(g);
+  ACME_HIP_TRY(hipGraphLaunch(exec, st));
   return ACME_OK;
 }
 
 int acme_dqn_step(acme_dqn* l, const acme_transition_batch* batch, const acme_dqn_outputs* out,
                   void* stream) {
-  int rc = acme_dqn_forward_backward(l, batch, out, stream);
+  ACME_CHECK_ARG(l && batch && l->params, "null argument or unbound learner");
+  hipStream_t st = as_stream(stream);
+  const bool copy = copies_target(l);
+  int rc;
+  if (l->cfg.network == ACME_NET_NATURE_DQN && use_p3(l) && dqn_graphs_enabled()) {
+    ACME_CHECK_ARG(batch->batch >= 1 && batch->batch <= l->cfg.max_batch,
+                   "batch %lld outside [1, max_batch=%d]", (long long)batch->batch,
+                   l->cfg.max_batch);
+    // Parameter planes written from outside are refreshed eagerly, so no graph contains
+    // that conditional launch; so is the device step count after eager steps.
+    if ((rc = sync_planes(l, st)) != ACME_OK) return rc;
+    if (!l->dev_steps_synced) {
+      ACME_HIP_TRY(hipStreamSynchronize(st));
+      ACME_HIP_TRY(hipMemcpy(l->dev_steps, &l->num_steps, sizeof(int64_t), hipMemcpyHostToDevice));
+      l->dev_steps_synced = true;
+    }
+    rc = run_step_graph(l, batch, out, copy, st);
+  } else {
+    rc = step_impl(l, batch, out, copy, st);
+  }
   if (rc != ACME_OK) return rc;
-  return acme_dqn_apply(l, stream);
+  l->num_steps += 1;
+  return ACME_OK;
 }
 
 }  // extern "C"

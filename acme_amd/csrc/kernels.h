@@ -112,9 +112,12 @@ int launch_clip_adam(const ClipAdamArgs& a, hipStream_t st);
 // snt.Adam over n (multiple of 4) floats at step t (acme_adam_update); with `planes`
 // non-null the updated parameters are also written as exact bf16 planes (stride pstride).
 // optix != 0: optix.adam's rounding order, p + (-lr) * (m_hat / (sqrt(v_hat) + eps)).
+// dev_steps (optional): the step count lives on the device (t = *dev_steps + 1, bias
+// corrections computed by the kernel, the count incremented by a one-thread launch after
+// it), so a captured step graph replays correctly; `t` is then ignored.
 int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,
                 float b2, float eps, int64_t t, uint16_t* planes, int64_t pstride, hipStream_t st,
-                int optix = 0);
+                int optix = 0, int64_t* dev_steps = nullptr);
 
 // Exact three-plane split of n floats (n multiple of 4): planes[i * pstride + e].
 int launch_split_planes(const float* x, int64_t n, uint16_t* planes, int64_t pstride,

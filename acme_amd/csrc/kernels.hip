@@ -541,7 +541,13 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p,
                                                    int64_t n4, float lr, float b1, float omb1,
                                                    float b2, float omb2, float bc1, float bc2,
                                                    float eps, uint16_t* __restrict__ planes,
-                                                   int64_t pstride, int optix) {
+                                                   int64_t pstride, int optix,
+                                                   const int64_t* __restrict__ dev_steps) {
+  if (dev_steps) {  // device-side step count (graph replay): same expressions as the host's
+    const float tf = (float)(*dev_steps + 1);
+    bc1 = 1.f - powf(b1, tf);
+    bc2 = 1.f - powf(b2, tf);
+  }
 #pragma unroll 2
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -567,6 +573,8 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p,
     if (planes) store_planes4(planes, pstride, i, pp);
   }
 }
+
+__global__ void count_step_kernel(int64_t* c) { *c += 1; }
 
 __global__ void __launch_bounds__(256) split_planes_kernel(const float* __restrict__ x, int64_t n4,
                                                            uint16_t* __restrict__ planes,
@@ -842,19 +850,23 @@ int launch_grad_sumsq(const float* g, int64_t n4, int64_t group0_4, double* part
 
 int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,
                 float b2, float eps, int64_t t, uint16_t* planes, int64_t pstride, hipStream_t st,
-                int optix) {
+                int optix, int64_t* dev_steps) {
   ACME_CHECK_ARG(p && g && m && v, "null buffer");
   ACME_CHECK_ARG(n % 4 == 0, "adam buffer length must be a multiple of 4");
   ACME_CHECK_ARG(pstride % 4 == 0, "plane stride must be a multiple of 4");
-  ACME_CHECK_ARG(t >= 1, "adam step must be >= 1");
-  const float bc1 = 1.f - powf(b1, (float)t);
-  const float bc2 = 1.f - powf(b2, (float)t);
+  ACME_CHECK_ARG(t >= 1 || dev_steps, "adam step must be >= 1");
+  const float bc1 = dev_steps ? 0.f : 1.f - powf(b1, (float)t);
+  const float bc2 = dev_steps ? 0.f : 1.f - powf(b2, (float)t);
   const int64_t n4 = n / 4;
   const int gcap = tune_variant("ADAMG") > 0 ? tune_variant("ADAMG") : 8192;  // 47.7 -> 45.2 us vs 2048
   const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n4, 256), gcap);
   adam_kernel<<<std::max(grid, 1u), 256, 0, st>>>(p, g, m, v, n4, lr, b1, 1.f - b1, b2, 1.f - b2,
-                                                  bc1, bc2, eps, planes, pstride, optix);
+                                                  bc1, bc2, eps, planes, pstride, optix, dev_steps);
   ACME_LAUNCH_CHECK();
+  if (dev_steps) {
+    count_step_kernel<<<1, 1, 0, st>>>(dev_steps);
+    ACME_LAUNCH_CHECK();
+  }
   return ACME_OK;
 }
 
