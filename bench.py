@@ -72,57 +72,61 @@ def cpu_model() -> str:
 
 
 def cpu_baseline(batch: int, num_actions: int, seconds: float):
-    """The numpy oracle (oracle/dqn_oracle.py, float32) timed on the host cores on a bounded
-    sample: a 16,384-slot host replay with the C oracle's prioritized sum tree, batch 512,
-    as many full steps as fit in `seconds` (at least 2; the first is a warm-up)."""
-    from oracle import dqn_oracle as O
+    """SURVEY §8(d)'s CPU baseline: the build's float32 torch-CPU restatement of the TF
+    DQN step (oracle/dqn_torch.py: F.conv2d + autograd + Sonnet Adam) fed by the C oracle's
+    prioritized sum tree over 1,000,000 slots (draw, gather, step, priority write-back),
+    timed on the host cores: all of them (torch.set_num_threads), then one thread.  The
+    frames of the 1M slots would be 56 GB of host memory, so slot s reads frame pair
+    s mod 16,384 of a host pool (the tree, draws and priorities are the full 1M-slot ones).
+    Bounded sample: as many steps as fit in `seconds` for all threads (at least 2 after one
+    warm-up step) and in `seconds` / 2 for one thread (at least 1)."""
+    from oracle.dqn_torch import TorchDQN
     from tests._oracle import OracleTable
     from acme_amd.networks import DQNAtariNetwork
-    try:
-        from threadpoolctl import threadpool_limits
-    except ImportError:  # pragma: no cover
-        threadpool_limits = None
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
-    ctx = threadpool_limits(threads) if threadpool_limits else None
     rng = np.random.default_rng(0)
-    cap = 16384
-    obs = rng.integers(0, 256, (cap, 84, 84, 4), dtype=np.uint8)
-    nxt = rng.integers(0, 256, (cap, 84, 84, 4), dtype=np.uint8)
-    act = rng.integers(0, num_actions, cap).astype(np.int32)
-    rew = rng.standard_normal(cap).astype(np.float32)
-    dis = np.where(rng.random(cap) < 0.01, 0, np.float32(0.99) ** 4).astype(np.float32)
+    pool, cap = 16384, 1_000_000
+    obs = torch.from_numpy(rng.integers(0, 256, (pool, 84, 84, 4), dtype=np.uint8))
+    nxt = torch.from_numpy(rng.integers(0, 256, (pool, 84, 84, 4), dtype=np.uint8))
+    act = torch.from_numpy(rng.integers(0, num_actions, pool).astype(np.int32))
+    rew = torch.from_numpy(rng.standard_normal(pool).astype(np.float32))
+    dis = torch.from_numpy(np.where(rng.random(pool) < 0.01, 0,
+                                    np.float32(0.99) ** 4).astype(np.float32))
     table = OracleTable(cap, True, 0.6, 1234)
     table.insert(np.ones(cap))
-    net = DQNAtariNetwork(num_actions)
-    p = net.init(0)
-    state = dict(params=p, target={k: v.copy() for k, v in p.items()},
-                 m={k: np.zeros_like(v) for k, v in p.items()},
-                 v={k: np.zeros_like(v) for k, v in p.items()}, num_steps=0)
-    cfg = O.DQNConfig(num_actions=num_actions)
+    learner = TorchDQN(DQNAtariNetwork(num_actions).init(0), num_actions)
+    draw = [0]
 
-    def one(step):
-        s = table.sample(batch, step)
-        k = s["slots"]
-        b = dict(o_tm1=obs[k], a_tm1=act[k], r_t=rew[k], d_t=dis[k], o_t=nxt[k],
-                 probabilities=s["probabilities"])
-        out, _, new_state = O.dqn_step(cfg, state, b, np.float32)
-        table.update(s["keys"], out["priorities"])
-        return new_state
+    def one():
+        s = table.sample(batch, draw[0])
+        draw[0] += 1
+        k = torch.from_numpy(s["slots"] % pool)
+        _, prio = learner.step(obs[k], act[k], rew[k], dis[k], nxt[k], s["probabilities"])
+        table.update(s["keys"], prio)
 
-    state = one(0)  # warm-up (page faults, BLAS init)
-    t0 = time.perf_counter()
-    n = 0
-    while n < 2 or time.perf_counter() - t0 < seconds:
-        state = one(n + 1)
-        n += 1
-    dt = time.perf_counter() - t0
-    if ctx is not None:
-        ctx.unregister() if hasattr(ctx, "unregister") else None
-    return dict(value=round(batch * n / dt, 2), unit="transitions/s", cores=threads,
-                kind="port",
-                sample=(f"numpy float32 oracle (oracle/dqn_oracle.py) + C sum-tree oracle, "
-                        f"{n} timed steps x batch {batch} on a {cap}-slot host replay, "
-                        f"{threads} BLAS threads, {cpu_model()}"))
+    def timed(threads, budget, least):
+        torch.set_num_threads(threads)
+        one()  # warm-up (page faults, oneDNN primitive creation)
+        t0 = time.perf_counter()
+        n = 0
+        while n < least or time.perf_counter() - t0 < budget:
+            one()
+            n += 1
+        return batch * n / (time.perf_counter() - t0), n
+
+    cores = len(os.sched_getaffinity(0))
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or cores
+    prev = torch.get_num_threads()
+    try:
+        v_all, n_all = timed(threads, seconds, 2)
+        v_one, n_one = timed(1, seconds / 2, 1)
+    finally:
+        torch.set_num_threads(prev)
+    return dict(value=round(v_all, 2), unit="transitions/s", cores=threads, kind="port",
+                value_1thread=round(v_one, 2),
+                sample=(f"float32 torch-CPU restatement of the TF DQN step (oracle/dqn_torch.py) "
+                        f"+ C sum-tree oracle over 1,000,000 slots (frames from a {pool}-slot "
+                        f"host pool), batch {batch}: {n_all} timed steps on {threads} threads, "
+                        f"{n_one} on 1 thread; {cpu_model()}, {cores} cores visible"))
 
 
 def d4pg_cpu_baseline(batch: int, seconds: float):
