@@ -123,14 +123,12 @@ struct TreeView {
   int nlevels;
 };
 
-__global__ void __launch_bounds__(256) sample_prioritized_kernel(
-    TreeView tree, const double* __restrict__ raw_prio, const uint64_t* __restrict__ keys,
-    int64_t batch, int64_t size, uint64_t seed, uint64_t step, double prob_scale,
-    int64_t* out_slots, uint64_t* out_keys, double* out_probs, int64_t* out_size,
-    double* out_prio) {
+// Draw j of a prioritized sample by one wave (every lane returns the same slot and
+// probability): the descent the oracle restates (oracle/replay_oracle.c).
+__device__ __forceinline__ void draw_prioritized(const TreeView& tree, int64_t size,
+                                                 uint64_t seed, uint64_t step, int64_t j,
+                                                 int64_t* slot_out, double* prob_out) {
   const int lane = threadIdx.x & 63;
-  const int64_t j = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (j >= batch) return;  // wave-uniform
   const double u = sample_uniform(seed, step, (uint32_t)j);
 
   int64_t node = 0;
@@ -160,6 +158,21 @@ __global__ void __launch_bounds__(256) sample_prioritized_kernel(
     slot = node;
     prob = leaf_value / total;
   }
+  *slot_out = slot;
+  *prob_out = prob;
+}
+
+__global__ void __launch_bounds__(256) sample_prioritized_kernel(
+    TreeView tree, const double* __restrict__ raw_prio, const uint64_t* __restrict__ keys,
+    int64_t batch, int64_t size, uint64_t seed, uint64_t step, double prob_scale,
+    int64_t* out_slots, uint64_t* out_keys, double* out_probs, int64_t* out_size,
+    double* out_prio) {
+  const int lane = threadIdx.x & 63;
+  const int64_t j = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (j >= batch) return;  // wave-uniform
+  int64_t slot;
+  double prob;
+  draw_prioritized(tree, size, seed, step, j, &slot, &prob);
   prob *= prob_scale;  // 1 (exact) unless this table is one shard of a global draw
   if (lane == 0) {
     out_slots[j] = slot;
@@ -348,6 +361,69 @@ __global__ void __launch_bounds__(T) gather_pair_kernel(const uint8_t* __restric
     const int32_t c = min(threadIdx.x + k * T, 2 * nvec - 1);
     const vu4* p = c < nvec ? a0 + c : a1 + (c - nvec);
     v[k] = NT ? __builtin_nontemporal_load(p) : *p;
+  }
+#pragma unroll
+  for (int k = 0; k < MAXC; ++k) {
+    const int32_t c = threadIdx.x + k * T;
+    vu4* p = c < nvec ? b0 + c : b1 + (c - nvec);
+    if (c < 2 * nvec) *p = v[k];
+  }
+#pragma unroll
+  for (int q = 0; q < ACME_MAX_FIELDS; ++q) {
+    if (q >= sm.n) break;
+    for (int w = threadIdx.x; w < sm.words[q]; w += T)
+      reinterpret_cast<uint32_t*>(sm.dst[q] + r * 4 * sm.words[q])[w] =
+          reinterpret_cast<const uint32_t*>(sm.src[q] + slot * 4 * sm.words[q])[w];
+  }
+}
+
+// Sample + gather fused for the transition layout: workgroup j's first wave draws item j
+// (prioritized descent or uniform, the same arithmetic as the sampling kernels) and writes
+// the sample record; then the workgroup copies the item's rows as gather_pair_kernel does.
+// One launch instead of two, and no slot round trip through memory.
+template <bool PRIO, int T, int MAXC>
+__global__ void __launch_bounds__(T) sample_gather_pair_kernel(
+    TreeView tree, const double* __restrict__ raw_prio, const uint64_t* __restrict__ keys,
+    int64_t size, uint64_t seed, uint64_t step, double prob_scale, int64_t* out_slots,
+    uint64_t* out_keys, double* out_probs, int64_t* out_size, double* out_prio,
+    const uint8_t* __restrict__ s0, const uint8_t* __restrict__ s1, uint8_t* __restrict__ d0,
+    uint8_t* __restrict__ d1, int32_t nvec, SmallFields sm) {
+  __shared__ int64_t s_slot;
+  const int64_t r = blockIdx.x;
+  if (threadIdx.x < 64) {
+    int64_t slot;
+    double prob;
+    if (PRIO) {
+      draw_prioritized(tree, size, seed, step, r, &slot, &prob);
+    } else {
+      const double u = sample_uniform(seed, step, (uint32_t)r);
+      slot = (int64_t)(u * (double)size);
+      if (slot >= size) slot = size - 1;
+      prob = 1.0 / (double)size;
+    }
+    prob *= prob_scale;
+    if (threadIdx.x == 0) {
+      out_slots[r] = slot;
+      if (out_keys) out_keys[r] = keys[slot];
+      if (out_probs) out_probs[r] = prob;
+      if (out_size) out_size[r] = size;
+      if (out_prio) out_prio[r] = raw_prio[slot];
+      s_slot = slot;
+    }
+  }
+  __syncthreads();
+  const int64_t slot = s_slot;
+  const int64_t rb = (int64_t)nvec * 16;
+  const vu4* a0 = reinterpret_cast<const vu4*>(s0 + slot * rb);
+  const vu4* a1 = reinterpret_cast<const vu4*>(s1 + slot * rb);
+  vu4* b0 = reinterpret_cast<vu4*>(d0 + r * rb);
+  vu4* b1 = reinterpret_cast<vu4*>(d1 + r * rb);
+  vu4 v[MAXC];
+#pragma unroll
+  for (int k = 0; k < MAXC; ++k) {
+    const int32_t c = min(threadIdx.x + k * T, 2 * nvec - 1);
+    const vu4* p = c < nvec ? a0 + c : a1 + (c - nvec);
+    v[k] = __builtin_nontemporal_load(p);
   }
 #pragma unroll
   for (int k = 0; k < MAXC; ++k) {
@@ -1070,6 +1146,10 @@ int acme_replay_fill_synthetic(acme_replay* r, int64_t n, int32_t layout, int32_
 static int sample_impl(acme_replay* r, int64_t batch, uint64_t step_counter, double prob_scale,
                        int64_t* slots, uint64_t* keys, double* probabilities,
                        int64_t* table_size, double* priorities, void* stream);
+static int sample_gather_impl(acme_replay* r, int64_t batch, uint64_t step_counter,
+                              double prob_scale, int64_t* slots, uint64_t* keys,
+                              double* probabilities, int64_t* table_size, double* priorities,
+                              void* const* out_fields, void* stream);
 
 int acme_replay_sample(acme_replay* r, int64_t batch, uint64_t step_counter, int64_t* slots,
                        uint64_t* keys, double* probabilities, int64_t* table_size,
@@ -1097,10 +1177,11 @@ int acme_replay_sample_share(acme_replay* r, int64_t batch, uint64_t step_counte
   ACME_CHECK_ARG(r, "null replay");
   ACME_CHECK_ARG(prob_scale > 0.0 && prob_scale <= 1.0, "prob_scale must be in (0, 1]");
   std::lock_guard<std::mutex> lock(r->mu);  // no insert commits between draw and gather
-  int rc = sample_impl(r, batch, step_counter, prob_scale, slots, keys, probabilities,
+  if (!out_fields)
+    return sample_impl(r, batch, step_counter, prob_scale, slots, keys, probabilities,
                        table_size, priorities, stream);
-  if (rc != ACME_OK || !out_fields) return rc;
-  return acme_replay_gather(r, slots, batch, out_fields, stream);
+  return sample_gather_impl(r, batch, step_counter, prob_scale, slots, keys, probabilities,
+                            table_size, priorities, out_fields, stream);
 }
 
 static int sample_impl(acme_replay* r, int64_t batch, uint64_t step_counter, double prob_scale,
@@ -1131,6 +1212,85 @@ static int sample_impl(acme_replay* r, int64_t batch, uint64_t step_counter, dou
   }
   ACME_LAUNCH_CHECK();
   return ACME_OK;
+}
+
+// The transition layout (two big fields of equal bytes, multiples of 16, 16-B aligned
+// destinations; every other field below 1 KiB): its big fields and the small ones.
+static bool pair_layout(const acme_replay* r, void* const* out_fields, int* f0, int* f1,
+                        SmallFields* sm) {
+  int big[ACME_MAX_FIELDS], nbig = 0;
+  for (int f = 0; f < r->cfg.num_fields; ++f)
+    if (r->cfg.field_bytes[f] >= 1024) big[nbig++] = f;
+  if (nbig != 2) return false;
+  const int64_t nb = r->cfg.field_bytes[big[0]];
+  if (nb != r->cfg.field_bytes[big[1]] || nb % 16 != 0 || nb / 16 > 1024 * 16) return false;
+  for (int i = 0; i < 2; ++i)
+    if (reinterpret_cast<uintptr_t>(out_fields[big[i]]) % 16 != 0) return false;
+  *f0 = big[0];
+  *f1 = big[1];
+  *sm = SmallFields{};
+  for (int f = 0; f < r->cfg.num_fields; ++f)
+    if (f != big[0] && f != big[1]) {
+      sm->src[sm->n] = r->fields[f];
+      sm->dst[sm->n] = static_cast<uint8_t*>(out_fields[f]);
+      sm->words[sm->n] = (int32_t)(r->cfg.field_bytes[f] / 4);
+      sm->n++;
+    }
+  return true;
+}
+
+// Sample + gather as a unit (the caller holds r->mu): one fused launch for the transition
+// layout, else the sampling kernel then the gather.
+static int sample_gather_impl(acme_replay* r, int64_t batch, uint64_t step_counter,
+                              double prob_scale, int64_t* slots, uint64_t* keys,
+                              double* probabilities, int64_t* table_size, double* priorities,
+                              void* const* out_fields, void* stream) {
+  ACME_CHECK_ARG(slots && out_fields, "null argument");
+  ACME_CHECK_ARG(batch > 0 && batch < (int64_t(1) << 31), "bad batch");
+  int f0, f1;
+  SmallFields sm;
+  if (tune_variant("SGF") != 1 && tune_variant("GATH") == 0 &&
+      pair_layout(r, out_fields, &f0, &f1, &sm)) {
+    hipStream_t st = as_stream(stream);
+    int64_t size = 0;
+    int rc = order_after_inserts(r, st, &size);
+    if (rc != ACME_OK) return rc;
+    if (size <= 0) {
+      set_error("cannot sample from an empty table (rate limiter MinSize(1))");
+      return ACME_ERR_EMPTY;
+    }
+    double row_bytes = 0;
+    for (int k = 0; k < r->cfg.num_fields; ++k) row_bytes += (double)r->cfg.field_bytes[k];
+    const bool prio = r->cfg.sampler == ACME_SAMPLER_PRIORITIZED;
+    ACME_PROF("replay_sample_gather", st, 0.0,
+              (double)batch * (2.0 * row_bytes + 40.0 + (prio ? 512.0 * r->nlevels : 0.0)));
+    TreeView tv;
+    for (int l = 0; l < 8; ++l) tv.level[l] = r->levels[l];
+    tv.nlevels = r->nlevels;
+    const int32_t nvec = (int32_t)(r->cfg.field_bytes[f0] / 16);
+    const unsigned gb = (unsigned)batch;
+    const uint8_t *s0 = r->fields[f0], *s1 = r->fields[f1];
+    uint8_t* d0 = static_cast<uint8_t*>(out_fields[f0]);
+    uint8_t* d1 = static_cast<uint8_t*>(out_fields[f1]);
+#define ACME_SGP(PRIO, T, MAXC)                                                                 \
+  sample_gather_pair_kernel<PRIO, T, MAXC><<<gb, T, 0, st>>>(                                   \
+      tv, r->raw_prio, r->keys, size, r->cfg.seed, step_counter, prob_scale, slots, keys,       \
+      probabilities, table_size, priorities, s0, s1, d0, d1, nvec, sm)
+    if (2 * nvec <= 256 * 14) {
+      if (prio) ACME_SGP(true, 256, 14);
+      else ACME_SGP(false, 256, 14);
+    } else {
+      if (prio) ACME_SGP(true, 1024, 32);
+      else ACME_SGP(false, 1024, 32);
+    }
+#undef ACME_SGP
+    ACME_LAUNCH_CHECK();
+    return ACME_OK;
+  }
+  int rc = sample_impl(r, batch, step_counter, prob_scale, slots, keys, probabilities,
+                       table_size, priorities, stream);
+  if (rc != ACME_OK) return rc;
+  return acme_replay_gather(r, slots, batch, out_fields, stream);
 }
 
 int acme_replay_gather(acme_replay* r, const int64_t* slots, int64_t batch,
@@ -1223,11 +1383,9 @@ int acme_replay_sample_gather(acme_replay* r, int64_t batch, uint64_t step_count
                               int64_t* table_size, double* priorities, void* const* out_fields,
                               void* stream) {
   ACME_CHECK_ARG(r, "null replay");
-  std::lock_guard<std::mutex> lock(r->mu);  // no insert commits between the two launches
-  int rc = acme_replay_sample(r, batch, step_counter, slots, keys, probabilities, table_size,
-                              priorities, stream);
-  if (rc != ACME_OK) return rc;
-  return acme_replay_gather(r, slots, batch, out_fields, stream);
+  std::lock_guard<std::mutex> lock(r->mu);  // no insert commits between draw and gather
+  return sample_gather_impl(r, batch, step_counter, 1.0, slots, keys, probabilities, table_size,
+                            priorities, out_fields, stream);
 }
 
 int acme_replay_update_priorities(acme_replay* r, const uint64_t* keys, const double* prios,

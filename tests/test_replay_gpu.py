@@ -236,3 +236,44 @@ def test_gather_kernels_bit_identical(fields):
         np.testing.assert_array_equal(outs[0][f], data[f][keys])
         np.testing.assert_array_equal(outs[1][f], outs[0][f])
         np.testing.assert_array_equal(outs[2][f], outs[0][f])
+
+
+@pytest.mark.parametrize("prioritized", [True, False])
+@pytest.mark.parametrize("fields", [[28224, 4, 4, 4, 28224], [2048, 4, 2048]])
+def test_fused_sample_gather_matches_two_launches(prioritized, fields):
+    """acme_replay_sample_gather's fused kernel (the transition layout: draw + row copy in
+    one workgroup) against the sampling kernel + gather (SGF=1) and the oracle's draw."""
+    import ctypes
+    from acme_amd._lib import lib
+    rng = np.random.default_rng(5)
+    cap, n, B = 3000, 3500, 257
+    data = [rng.integers(0, 256, (n, b), dtype=np.uint8) for b in fields]
+    pr = rng.uniform(0.0, 2.0, n)
+    r = _native(cap, fields, prioritized)
+    r.insert(data, pr)
+    o = OracleTable(cap, prioritized, 0.6, 1234)
+    o.insert(pr)
+    L = lib()
+    res = {}
+    for sgf in (0, 1):
+        L.acme_tune_set(b"SGF", sgf)
+        try:
+            info = r.alloc_sample_info(B)
+            outs = [torch.zeros(B, b, dtype=torch.uint8, device="cuda") for b in fields]
+            ptrs = (ctypes.c_void_p * len(outs))(*[x.data_ptr() for x in outs])
+            raw = [info[k].data_ptr() for k in ("slots", "keys", "probabilities", "table_size",
+                                                  "priorities")]
+            assert L.acme_replay_sample_gather(r.handle, B, 77, *raw, ptrs, None) == 0
+            torch.cuda.synchronize()
+            res[sgf] = ({k: v.cpu().numpy() for k, v in info.items()},
+                        [x.cpu().numpy() for x in outs])
+        finally:
+            L.acme_tune_set(b"SGF", 0)
+    ref = o.sample(B, 77)
+    for k in ("slots", "probabilities", "table_size", "priorities"):
+        np.testing.assert_array_equal(res[0][0][k], ref[k])
+        np.testing.assert_array_equal(res[1][0][k], ref[k])
+    keys = res[0][0]["keys"].view(np.int64)
+    for f in range(len(fields)):
+        np.testing.assert_array_equal(res[0][1][f], data[f][keys])
+        np.testing.assert_array_equal(res[1][1][f], res[0][1][f])

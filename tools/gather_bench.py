@@ -71,6 +71,30 @@ def main():
         us = run(v)
         res[name] = dict(us=round(us, 2), TBps=round(algo / us / 1e6, 3))
         print(f"{name:24s} {us:8.2f} us  {algo / us / 1e6:6.3f} TB/s", flush=True)
+    # Sample + gather: the two launches (SGF=1) and the fused kernel (default), fresh draws.
+    keys_b = torch.empty(B, dtype=torch.int64, device="cuda")
+    h = r.handle
+    import ctypes
+    ptrs = (ctypes.c_void_p * len(outs))(*[o.data_ptr() for o in outs])
+    info = r.alloc_sample_info(B)
+    raw = [info[k].data_ptr() for k in ("slots", "keys", "probabilities", "table_size",
+                                          "priorities")]
+    for name, sgf in (("sample+gather (2 launches)", 1), ("sample+gather (fused)", 0)):
+        L.acme_tune_set(b"SGF", sgf)
+        for s in range(4):
+            L.acme_replay_sample_gather(h, B, s, *raw, ptrs, None)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for s in range(4 * n_draws):
+            L.acme_replay_sample_gather(h, B, 1000 + s, *raw, ptrs, None)
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / (4 * n_draws)
+        res[name] = dict(us=round(us, 2), TBps=round(algo / us / 1e6, 3))
+        print(f"{name:24s} {us:8.2f} us  {algo / us / 1e6:6.3f} TB/s", flush=True)
+    L.acme_tune_set(b"SGF", 0)
+    del keys_b
     # The same bytes as a contiguous device copy (torch copy_ of a [2, B, 28224] block).
     src = torch.empty(n_draws, 2 * B * 28224, dtype=torch.uint8, device="cuda")
     dst = torch.empty(2 * B * 28224, dtype=torch.uint8, device="cuda")

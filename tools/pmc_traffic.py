@@ -65,7 +65,9 @@ SECTIONS = [
     (r"ConvDgradSub", "conv2_dgrad"),
     (r"ConvDgrad<", "conv3_dgrad"),
     (r"(?<!clip_)adam_kernel", "adam"),
-    (r"gather_fields_kernel", "replay_gather"),
+    (r"gather_fields_kernel|gather_pair_kernel|gather_pieces_kernel", "replay_gather"),
+    (r"sample_prioritized_kernel", "replay_sample"),
+    (r"prio_update_fused_kernel", "replay_update"),
 ]
 TABLES = {"dqn": SECTIONS, "d4pg": SECTIONS_D4PG, "impala": SECTIONS_IMPALA}
 TABLE = SECTIONS
