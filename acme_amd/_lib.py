@@ -30,7 +30,7 @@ SEMANTICS_JAX = 1
 MATMUL_F32 = 0
 MATMUL_X6 = 1
 
-MAX_FIELDS = 8
+MAX_FIELDS = 16
 MAX_MLP_LAYERS = 8
 D4PG_MAX_LAYERS = 4
 D4PG_MAX_ACT = 16

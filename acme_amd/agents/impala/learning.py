@@ -99,6 +99,35 @@ class IMPALALearner(core.Learner, core.Saveable):
                                     t(hidden, torch.float32), t(cell, torch.float32))
         return lg.cpu().numpy(), v.cpu().numpy(), h.cpu().numpy(), c.cpu().numpy()
 
+    def actor_policy(self, max_rows: int = 16):
+        """A policy_step for actor threads that does not share the learner's workspace: a
+        second native network bound to the learner's parameter buffer, on its own stream
+        (actor inference overlaps learner steps; the actors read the parameters current when
+        their step runs, as a VariableClient refreshed every step would)."""
+        n = self._native
+        net = NativeIMPALA(num_actions=n.num_actions, max_batch=int(max_rows),
+                           max_sequence_length=2, torso=n.torso, obs_dim=n.obs_dim,
+                           lstm_size=n.lstm_size, head_size=self._network.head_size,
+                           device=n.device, shared_params=n.params)
+        stream = torch.cuda.Stream(device=n.device)
+        dt = torch.uint8 if self._network.torso == "atari" else torch.float32
+        dev = n.device
+
+        def step(observation, prev_action, prev_reward, hidden, cell):
+            t = lambda x, d: torch.as_tensor(np.asarray(x)).to(dev, d, non_blocking=True)  # noqa
+            rows = int(np.asarray(prev_action).shape[0])
+            with torch.cuda.stream(stream):
+                lg, v, h, c = net.policy_step(t(observation, dt).reshape(rows, -1),
+                                              t(prev_action, torch.int32),
+                                              t(prev_reward, torch.float32),
+                                              t(hidden, torch.float32), t(cell, torch.float32),
+                                              stream=stream)
+                out = [x.cpu().numpy() for x in (lg, v, h, c)]
+            return tuple(out)
+
+        step.native = net  # keeps the network alive with the closure
+        return step
+
     def get_variables(self, names: List[str]) -> List[Dict[str, np.ndarray]]:
         return [self._native.get_params("params")]
 

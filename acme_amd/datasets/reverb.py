@@ -277,29 +277,34 @@ class _TableIterator:
         return self._sample_view(i, self._share[i])
 
 
-class _QueueIterator:
+class _QueueIterator(_TableIterator):
+    """Batches of a QueueTable: each next() consumes the next B items (FIFO, once) and
+    gathers their rows from the HBM ring on the GPU (keys = insertion indices, probability
+    and priority 1, table_size = items still queued)."""
+
     def __init__(self, table: replay.QueueTable, batch: int, timeout: float):
-        self._t = table
-        self._B = batch
-        self._timeout = timeout
-
-    @property
-    def batch_size(self) -> int:
-        return self._B
-
-    def __iter__(self):
-        return self
+        super().__init__(table, batch, timeout, prefetch=0, shard=None)
 
     def __next__(self) -> replay.ReplaySample:
-        items = self._t.pop_batch(self._B, self._timeout)
-        stacked = tree.map_structure(lambda *xs: np.stack([np.asarray(x) for x in xs]), *items)
-        data = tree.map_structure(lambda x: torch.as_tensor(x).cuda(non_blocking=False), stacked)
-        ones = torch.ones(self._B, dtype=torch.float64, device="cuda")
-        info = replay.SampleInfo(key=torch.zeros(self._B, dtype=torch.uint64, device="cuda"),
-                                 probability=ones, table_size=torch.full(
-                                     (self._B,), self._t.size(), dtype=torch.int64, device="cuda"),
-                                 priority=ones)
-        return replay.ReplaySample(info=info, data=data)
+        from acme_amd._lib import check, lib, stream_ptr
+        t = self._t
+        first = t.pop_slots(self._B, self._timeout)
+        if self._slots is None:
+            self._alloc()
+        i = self._which
+        self._which ^= 1
+        raw, ptrs, sample, info, _ = self._slots[i]
+        dev = t.native.device
+        idx = torch.arange(first, first + self._B, dtype=torch.int64, device=dev)
+        info["keys"].copy_(idx.view(torch.uint64) if idx.dtype == torch.int64 else idx)
+        info["probabilities"].fill_(1.0)
+        info["priorities"].fill_(1.0)
+        info["table_size"].fill_(t.size())
+        slots = idx % t.max_size
+        check(lib().acme_replay_gather(t.native.handle, slots.data_ptr(), self._B, ptrs,
+                                       stream_ptr()), "queue gather")
+        self._keep = slots  # the launch reads it on the stream
+        return sample
 
 
 def make_reverb_dataset(server_address, environment_spec=None, batch_size: Optional[int] = None,

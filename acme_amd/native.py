@@ -585,9 +585,11 @@ class NativeIMPALA:
                  baseline_cost: float = 1.0, max_abs_reward: Optional[float] = None,
                  max_gradient_norm: Optional[float] = None, learning_rate: float = 1e-3,
                  adam_beta1: float = 0.9, adam_beta2: float = 0.999, adam_epsilon: float = 1e-8,
-                 semantics: str = "tf", device=None):
+                 semantics: str = "tf", device=None, shared_params: Optional[torch.Tensor] = None):
         """semantics: "tf" (acme/agents/tf/impala) or "jax" (acme/agents/jax/impala: the
-        optix.chain(clip_by_global_norm, adam) update; max_gradient_norm None = inf)."""
+        optix.chain(clip_by_global_norm, adam) update; max_gradient_norm None = inf).
+        shared_params: bind another instance's parameter buffer (an actor-side network with
+        its own workspace, reading the learner's current parameters)."""
         _lib.require_gpu()
         if semantics not in ("tf", "jax"):
             raise ValueError(f"semantics must be 'tf' or 'jax', got {semantics!r}")
@@ -625,7 +627,13 @@ class NativeIMPALA:
             self.tensors.append((name.value.decode(), int(off.value),
                                  tuple(int(shape[k]) for k in range(nd.value))))
         z = lambda: torch.zeros(self.flat_size, dtype=torch.float32, device=self.device)  # noqa
-        self.params, self.grads, self.m, self.v = z(), z(), z(), z()
+        if shared_params is not None:
+            if shared_params.numel() != self.flat_size or not shared_params.is_cuda:
+                raise ValueError("shared_params must be a device buffer of the same layout")
+            self.params = shared_params
+        else:
+            self.params = z()
+        self.grads, self.m, self.v = z(), z(), z()
         check(L.acme_impala_bind(h, ptr(self.params), ptr(self.grads), ptr(self.m),
                                  ptr(self.v)), "impala bind")
         self.metrics = torch.zeros(4, dtype=torch.float32, device=self.device)

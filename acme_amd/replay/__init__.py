@@ -4,6 +4,7 @@ Reference call sites (all in-process `localhost:<port>` gRPC in the reference):
   reverb.Table(name, sampler=Prioritized(a) | Uniform(), remover=Fifo(), max_size,
                rate_limiter=MinSize(n), signature)        acme/agents/tf/dqn/agent.py:95-101
   reverb.Table.queue(name, max_size)                       acme/agents/tf/impala/agent.py:68-74
+                                                           (device FIFO, QueueTable)
   reverb.Server([tables], port=None).port                  acme/agents/tf/dqn/agent.py:102
   reverb.Client(address).writer(...) -> append/create_item acme/adders/reverb/base.py:112-118
   reverb.TFClient(address).update_priorities(table, keys, priorities)
@@ -12,9 +13,10 @@ Reference call sites (all in-process `localhost:<port>` gRPC in the reference):
   ReplaySample(info=SampleInfo(key, probability, table_size, priority), data)
 
 Items live in HBM (acme_amd.native.NativeReplay: one row per item per flattened field,
-64-ary sum tree for Prioritized).  Writers stage items on the host and flush them to the
-device in batches (one hipMemcpy per field per flush); a table flushes pending items
-before every sample, so a sample always sees every item created before it.
+64-ary sum tree for Prioritized).  Writers stage items on the host and flush them in
+batches straight into the table's pinned staging ring (side-stream hipMemcpyAsync, no
+host wait); a table flushes pending items before every sample, so a sample always sees
+every item created before it.
 """
 
 from __future__ import annotations
@@ -134,8 +136,8 @@ class Table:
             self._init_layout(signature, _layout_from_signature(signature))
 
     @classmethod
-    def queue(cls, name: str, max_size: int, signature=None):
-        return QueueTable(name, max_size, signature)
+    def queue(cls, name: str, max_size: int, signature=None, device=None):
+        return QueueTable(name, max_size, signature, device=device)
 
     # -- layout / storage
     def _init_layout(self, structure, fields):
@@ -306,44 +308,69 @@ from acme_amd.replay.frame_table import _make_frame_table  # noqa: E402
 FrameTable = _make_frame_table(Table, _Field, _layout_from_signature)
 
 
-class QueueTable:
-    """Table.queue: FIFO items consumed once (IMPALA).  Host-resident; batches are
-    stacked and moved to the device by the dataset."""
+class QueueTable(Table):
+    """Table.queue (acme/agents/tf/impala/agent.py:68-74): a FIFO whose items are consumed
+    once, device-resident.  Items (SequenceAdder sequences) go through the same pinned
+    staging ring and side-stream copies as Table inserts, into an HBM ring of max_size
+    slots; `pop_slots(B)` hands the next B items to the dataset, which gathers them on the
+    GPU (rows of consecutive ring slots).  Reverb's Queue rate limiter blocks a writer while
+    the queue is full and a reader while it holds fewer than the batch; so do insert() and
+    pop_slots() (with a timeout).  An item's slot is reused only after its gather: the
+    native table orders every insert after the streams that read it."""
 
-    def __init__(self, name: str, max_size: int, signature=None):
-        self.name = name
-        self.max_size = int(max_size)
-        self._items: collections.deque = collections.deque()
-        self._mu = threading.Condition()
-        self._signature = signature
+    def __init__(self, name: str, max_size: int, signature=None, device=None,
+                 flush_every: int = 16, timeout: float = 60.0):
+        super().__init__(name, selectors.Uniform(), selectors.Fifo(), max_size, None,
+                         signature=signature, device=device, flush_every=flush_every)
+        self._accepted = 0   # items insert() took (pending or flushed)
+        self._consumed = 0   # items handed to readers
+        self._timeout = float(timeout)
 
     def size(self) -> int:
         with self._mu:
-            return len(self._items)
+            return self._accepted - self._consumed
 
     def can_sample(self, num_samples: int = 1) -> bool:
         return self.size() >= num_samples
 
     def insert(self, item, priority: float) -> None:
-        with self._mu:
-            if len(self._items) >= self.max_size:
-                raise RuntimeError(f"queue '{self.name}' is full ({self.max_size})")
-            self._items.append(item)
-            self._mu.notify_all()
-
-    def flush(self):
-        pass
-
-    def pop_batch(self, batch_size: int, timeout: float = 60.0):
-        deadline = time.time() + timeout
-        with self._mu:
-            while len(self._items) < batch_size:
+        deadline = time.time() + self._timeout
+        with self._cv:
+            while self._accepted - self._consumed >= self.max_size:
+                self.flush()
                 left = deadline - time.time()
                 if left <= 0:
-                    raise RuntimeError(f"queue '{self.name}' has {len(self._items)} items, "
+                    raise RuntimeError(f"queue '{self.name}' stayed full ({self.max_size} items) "
+                                       f"for {self._timeout}s")
+                self._cv.wait(left)
+            super().insert(item, priority)
+            self._accepted += 1
+
+    def pop_slots(self, batch_size: int, timeout: Optional[float] = None) -> int:
+        """Blocks until `batch_size` items are queued, flushes them to the device and
+        consumes them; returns the insertion index of the first one (its ring slot is that
+        index modulo max_size, the next ones follow)."""
+        if batch_size > self.max_size:
+            raise ValueError(f"batch {batch_size} exceeds the queue capacity {self.max_size}")
+        deadline = time.time() + (self._timeout if timeout is None else timeout)
+        with self._cv:
+            while self._accepted - self._consumed < batch_size:
+                left = deadline - time.time()
+                if left <= 0:
+                    raise RuntimeError(f"queue '{self.name}' has {self.size()} items, "
                                        f"{batch_size} requested")
-                self._mu.wait(left)
-            return [self._items.popleft() for _ in range(batch_size)]
+                self._cv.wait(left)
+            self.flush()
+            first = self._consumed
+            self._consumed += batch_size
+            self._cv.notify_all()
+            return first
+
+    def pop_batch(self, batch_size: int, timeout: float = 60.0):
+        raise NotImplementedError("the device queue is read through make_reverb_dataset")
+
+    def update_priorities(self, keys, priorities) -> None:
+        pass  # queue items carry no priorities (Reverb ignores updates of consumed items)
 
 
 # ---------------------------------------------------------------- server / client

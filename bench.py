@@ -43,10 +43,13 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--workload", choices=("dqn", "d4pg", "impala", "insert"), default="dqn",
+    p.add_argument("--workload", choices=("dqn", "d4pg", "impala", "impala_actors", "insert"),
+                   default="dqn",
                    help="dqn: the headline config (BASELINE configs[1]); d4pg: configs[2]; "
-                        "impala: configs[3] (learner side); insert: host inserts into the "
-                        "configs[1] table while its learner steps")
+                        "impala: configs[3] (learner side); impala_actors: configs[3] end to "
+                        "end (--actors host actor threads feeding the device queue); insert: "
+                        "host inserts into the configs[1] table while its learner steps")
+    p.add_argument("--actors", type=int, default=64, help="impala_actors: actor threads")
     p.add_argument("--batch", type=int, default=0, help="default 512 (dqn) / 256 (d4pg)")
     p.add_argument("--replay-size", type=int, default=1_000_000)
     p.add_argument("--num-actions", type=int, default=18)
@@ -466,6 +469,83 @@ def setup_impala(args, world, rank, dev):
             lambda: impala_cpu_baseline(B, T, args.cpu_baseline_seconds))
 
 
+def impala_actors_bench(args, dev):
+    """BASELINE configs[3] end to end: `--actors` host threads, each an Atari-shaped
+    environment (acme_amd.environments.AtariLike), an IMPALAActor and a SequenceAdder
+    (T = 20, period 20) writing into the device queue table; their policy calls are batched
+    into GPU network steps on the learner's current parameters (agents/impala/actors.py);
+    the learner (B = 16 sequences) steps whenever the queue holds a batch
+    (agents/tf/impala/agent.py:117-120).  Reports learned frames/s (B x T per learner step)
+    over `--steps` learner steps after `--warmup`, and the actors' environment steps/s."""
+    from acme_amd import replay, specs
+    from acme_amd.adders import reverb as adders
+    from acme_amd.agents.impala import IMPALALearner
+    from acme_amd.agents.impala.actors import ActorPool, BatchedPolicy
+    from acme_amd.datasets import make_reverb_dataset
+    from acme_amd.environments.atari_like import AtariLike
+    from acme_amd.networks import IMPALAAtariNetwork, LSTMState
+    from acme_amd.utils import loggers
+    from acme_amd.wrappers import ObservationActionRewardWrapper
+    B, T, A, H = args.batch or 16, 20, 18, 256
+    env0 = ObservationActionRewardWrapper(AtariLike(seed=0))
+    spec = specs.make_environment_spec(env0)
+    extra = {"core_state": LSTMState(specs.Array((H,), np.float32), specs.Array((H,), np.float32)),
+             "logits": specs.Array((A,), np.float32)}
+    queue = replay.Table.queue(adders.DEFAULT_PRIORITY_TABLE, max_size=4 * B * 8,
+                               signature=adders.SequenceAdder.signature(spec, extras_spec=extra),
+                               device=dev)
+    server = replay.Server([queue])
+    net = IMPALAAtariNetwork(A)
+    learner = IMPALALearner(spec, net, make_reverb_dataset(server, batch_size=B,
+                                                           sequence_length=T),
+                            learning_rate=1e-3, entropy_cost=0.01, baseline_cost=0.5,
+                            logger=loggers.NoOpLogger(), batch_size=B, sequence_length=T,
+                            device=dev)
+    policy = BatchedPolicy(learner.actor_policy(max_rows=16), max_rows=16)
+    pool = ActorPool(lambda i: ObservationActionRewardWrapper(AtariLike(seed=1 + i)),
+                     lambda i: adders.SequenceAdder(replay.Client(server), sequence_length=T,
+                                                    period=T),
+                     policy, net.initial_state, num_actors=args.actors)
+    pool.start()
+    try:
+        def learn(n):
+            done = 0
+            while done < n:
+                if pool.errors:
+                    raise pool.errors[0]
+                if queue.can_sample(B):
+                    learner.step()
+                    done += 1
+                else:
+                    time.sleep(0.0005)
+        learn(args.warmup)
+        torch.cuda.synchronize(dev)
+        s0, t0 = pool.env_steps, time.perf_counter()
+        learn(args.steps)
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+        env_rate = (pool.env_steps - s0) / dt
+    finally:
+        pool.stop(timeout=5)
+        policy.close()
+    out = {
+        "metric": "IMPALA learned frames/sec (B=16 x T=20 per step) with host actors feeding "
+                  "the device queue, 1 MI355X",
+        "value": round(B * T * args.steps / dt, 1), "unit": "frames/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic Atari-shaped environment (acme_amd.environments.AtariLike), "
+                "random-init IMPALAAtariNetwork",
+        "config": {"workload": "impala_actor_learner (BASELINE configs[3])", "actors": args.actors,
+                   "batch_sequences": B, "sequence_length": T, "sequence_period": T,
+                   "obs": "uint8[84,84,4]", "num_actions": A, "lstm": H},
+        "actors": {"env_steps_per_s": round(env_rate, 1),
+                   "policy_batches": policy.batches,
+                   "mean_policy_rows": round(policy.rows / max(policy.batches, 1), 2)},
+    }
+    print(json.dumps(out))
+
+
 def pmc_traffic(workload: str, section: str):
     """HBM bytes per launch of `section` from the newest committed PMC summary
     (profiles/<round>/pmc_traffic_<workload>.json, written by tools/pmc_traffic.py from
@@ -527,10 +607,10 @@ def main():
 
     from acme_amd import _lib
     L = _lib.lib()
-    if args.workload == "insert":
+    if args.workload in ("insert", "impala_actors"):
         if world > 1:
-            raise SystemExit("the insert workload is single-GPU")
-        insert_bench(args, dev)
+            raise SystemExit(f"the {args.workload} workload is single-GPU")
+        (insert_bench if args.workload == "insert" else impala_actors_bench)(args, dev)
         return
     t_fill = time.perf_counter()
     setup = {"dqn": setup_dqn, "d4pg": setup_d4pg, "impala": setup_impala}[args.workload]

@@ -72,7 +72,7 @@ int acme_dense_forward(const float* x, int64_t rows, int64_t in, const float* w,
 
 /* ------------------------------------------------------------------ replay -- */
 
-#define ACME_MAX_FIELDS 8
+#define ACME_MAX_FIELDS 16
 
 enum { ACME_SAMPLER_UNIFORM = 0, ACME_SAMPLER_PRIORITIZED = 1 };
 

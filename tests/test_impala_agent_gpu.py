@@ -87,3 +87,52 @@ def test_impala_agent_runs_in_environment_loop():
     learner = agent._learner  # noqa: SLF001
     assert learner.num_steps >= 1
     assert np.isfinite(learner.native.metrics.cpu().numpy()).all()
+
+
+def test_actor_pool_feeds_device_queue_learner():
+    """BASELINE configs[3] shape end to end at small scale: 6 actor threads (Atari-shaped
+    environments, IMPALAActor, SequenceAdder) with batched GPU policy steps on the learner's
+    parameters feed the device queue; the learner steps whenever a batch is queued."""
+    import time
+    from acme_amd import datasets, replay
+    from acme_amd.adders import reverb as adders
+    from acme_amd.agents.impala import IMPALALearner
+    from acme_amd.agents.impala.actors import ActorPool, BatchedPolicy
+    from acme_amd.environments.atari_like import AtariLike
+    from acme_amd.networks import IMPALAAtariNetwork, LSTMState
+    A, H, T, B = 18, 32, 5, 4
+    env = ObservationActionRewardWrapper(AtariLike(seed=0, min_length=7, max_length=30))
+    spec = specs.make_environment_spec(env)
+    extra = {"core_state": LSTMState(specs.Array((H,), np.float32), specs.Array((H,), np.float32)),
+             "logits": specs.Array((A,), np.float32)}
+    queue = replay.Table.queue(adders.DEFAULT_PRIORITY_TABLE, 16,
+                               signature=adders.SequenceAdder.signature(spec, extras_spec=extra))
+    server = replay.Server([queue])
+    net = IMPALAAtariNetwork(A, lstm_size=H, head_size=16)
+    learner = IMPALALearner(spec, net, datasets.make_reverb_dataset(server, batch_size=B,
+                                                                    sequence_length=T),
+                            learning_rate=1e-3, entropy_cost=0.01, baseline_cost=0.5,
+                            logger=loggers.NoOpLogger(), batch_size=B, sequence_length=T)
+    policy = BatchedPolicy(learner.actor_policy(max_rows=4), max_rows=4)
+    pool = ActorPool(lambda i: ObservationActionRewardWrapper(
+                         AtariLike(seed=10 + i, min_length=7, max_length=30)),
+                     lambda i: adders.SequenceAdder(replay.Client(server), sequence_length=T,
+                                                    period=T),
+                     policy, net.initial_state, num_actors=6)
+    pool.start()
+    try:
+        deadline = time.time() + 120
+        while learner.num_steps < 5 and time.time() < deadline:
+            assert not pool.errors, pool.errors
+            if queue.can_sample(B):
+                learner.step()
+            else:
+                time.sleep(0.001)
+    finally:
+        pool.stop(timeout=10)
+        policy.close()
+    torch.cuda.synchronize()
+    assert learner.num_steps >= 5
+    assert pool.env_steps >= 5 * B * T
+    assert policy.batches > 0 and policy.rows >= pool.env_steps
+    assert np.isfinite(learner.native.metrics.cpu().numpy()).all()
