@@ -69,6 +69,10 @@ struct acme_impala {
   int64_t* dev_step = nullptr;
   float* metrics_tmp = nullptr;
   float* norms = nullptr;
+  // Persistent LSTM forward: h_t exchange granules [2][B * H] (8 B: epoch tag | value bits)
+  // and the spin-timeout word, zeroed before every launch.
+  unsigned long long* xg = nullptr;
+  unsigned* tmo = nullptr;
 };
 
 namespace {
@@ -318,8 +322,8 @@ __global__ void __launch_bounds__(256) lstm_fwd_step_kernel(
     const float gg = tanhf(z[2 * kFwdUnits + u]), og = sigmoidf(z[3 * kFwdUnits + u]);
     const float cprev = o == (int)threadIdx.x && cell_thread ? cprev_pre
                                                              : cp[(size_t)b * cp_stride + j];
-    const float cn = fg * cprev + ig * gg;
-    const float hn = og * tanhf(cn);
+    const float cn = __fadd_rn(__fmul_rn(fg, cprev), __fmul_rn(ig, gg));  // no contraction:
+    const float hn = __fmul_rn(og, tanhf(cn));  // the persistent kernel computes the same bits
     const size_t row = (size_t)b * T + t;
     gates[row * 4 * H + j] = ig;
     gates[row * 4 * H + H + j] = fg;
@@ -327,6 +331,150 @@ __global__ void __launch_bounds__(256) lstm_fwd_step_kernel(
     gates[row * 4 * H + 3 * H + j] = og;
     c_out[row * H + j] = cn;
     h_out[row * H + j] = hn;
+  }
+}
+
+// ---------------------------------------------------------------- persistent forward
+// All T steps in ONE launch: H / kFwdUnits workgroups (co-resident: a cooperative launch),
+// each keeping its W_h columns in LDS for the whole unroll and its cells' c in registers.
+// Step t needs every unit's h_{t-1}: each workgroup publishes its h_t values as 8-byte
+// granules {tag = t + 1, value} with agent-scope relaxed atomic stores (write-through), and
+// one wave of every workgroup sweeps all B * H granules of step t - 1 (relaxed agent-scope
+// atomic loads) until every tag matches, then the workgroup computes.  The data is its own
+// flag (cdna_hip_programming.md Guideline 16, R2), the two granule buffers alternate by
+// step parity, and a workgroup cannot publish step t + 1 before every workgroup published
+// step t, so a buffer is only rewritten after all its readers are done.  Spins are
+// bounded: a timeout writes a code to `tmo` and every workgroup leaves the kernel.
+using gu64 = __attribute__((address_space(1))) unsigned long long;
+using gu32 = __attribute__((address_space(1))) unsigned;
+constexpr unsigned kSpinLimit = 1u << 22;
+
+__device__ __forceinline__ void put_granule(unsigned long long* g, unsigned tag, float v) {
+  __hip_atomic_store((gu64*)(g),
+                     ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One wave: copies the n granules of g (tag `tag`) into dst as floats; false on timeout.
+__device__ bool sweep_into(const unsigned long long* g, int n, unsigned tag, float* dst,
+                           unsigned* tmo) {
+  const int lane = threadIdx.x & 63;
+  constexpr int CH = 16;  // granules per lane per pass
+  for (int base = 0; base < n; base += 64 * CH) {
+    unsigned long long v[CH];
+    for (unsigned spins = 0;; ++spins) {
+      bool ok = true;
+#pragma unroll
+      for (int k = 0; k < CH; ++k) {
+        const int i = base + k * 64 + lane;
+        v[k] = i < n ? __hip_atomic_load((const gu64*)(g + i), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT)
+                     : ((unsigned long long)tag << 32);
+        ok &= (unsigned)(v[k] >> 32) == tag;
+      }
+      if (__all(ok)) break;
+      if (spins >= kSpinLimit) {
+        if (lane == 0)
+          __hip_atomic_store((gu32*)(tmo), 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+      const int i = base + k * 64 + lane;
+      if (i < n) dst[i] = __uint_as_float((unsigned)v[k]);
+    }
+  }
+  return true;
+}
+
+__global__ void __launch_bounds__(256) lstm_fwd_persistent_kernel(
+    const float* __restrict__ gx, const float* __restrict__ wh, const float* __restrict__ h0,
+    int64_t h0_stride, const float* __restrict__ c0, int64_t c0_stride, int B, int T, int H,
+    float* __restrict__ gates, float* __restrict__ h_out, float* __restrict__ c_out,
+    unsigned long long* xg, unsigned* tmo) {
+  constexpr int NC = 4 * kFwdUnits;
+  constexpr int KS = 256 / NC;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* hs = smem;                            // [B][H]
+  float* ws = hs + (size_t)B * H;              // [H][NC]
+  float* red = ws + (size_t)H * NC;            // [KS][kRowChunk][NC]
+  float* zs = red + KS * kRowChunk * NC;       // [B][NC]
+  __shared__ int s_fail;
+  const int u0 = blockIdx.x * kFwdUnits;
+  const int BH = B * H;
+  if (threadIdx.x == 0) s_fail = 0;
+  for (int e = threadIdx.x; e < H * 4; e += blockDim.x) {  // W_h columns, once
+    const int k = e / 4, q = e % 4;
+    *reinterpret_cast<f32x4*>(ws + (size_t)k * NC + q * kFwdUnits) =
+        *reinterpret_cast<const f32x4*>(wh + (size_t)k * 4 * H + q * H + u0);
+  }
+  const bool cell_thread = (int)threadIdx.x < B * kFwdUnits;
+  const int cb = threadIdx.x / kFwdUnits, cu = threadIdx.x % kFwdUnits;
+  float creg = cell_thread ? c0[(size_t)cb * c0_stride + u0 + cu] : 0.f;
+  const int c = threadIdx.x % NC, sl = threadIdx.x / NC;
+  for (int t = 0; t < T; ++t) {
+    if (t == 0) {
+      for (int e = threadIdx.x; e < BH / 4; e += blockDim.x) {
+        const int b = e / (H / 4), k = 4 * (e % (H / 4));
+        *reinterpret_cast<f32x4*>(hs + (size_t)b * H + k) =
+            *reinterpret_cast<const f32x4*>(h0 + (size_t)b * h0_stride + k);
+      }
+    } else {
+      // Every wave sweeps its quarter of the granules (one pass of 16 per lane at B*H = 4096).
+      const int wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+      const int per = (BH + nw - 1) / nw, lo = wv * per;
+      const int cnt = lo < BH ? min(per, BH - lo) : 0;
+      if (!sweep_into(xg + (size_t)((t - 1) & 1) * BH + lo, cnt, (unsigned)t, hs + lo, tmo) &&
+          (threadIdx.x & 63) == 0)
+        s_fail = 1;
+    }
+    __syncthreads();
+    if (s_fail) return;  // every workgroup leaves on a timeout (its sweep fails too)
+    for (int b0 = 0; b0 < B; b0 += kRowChunk) {
+      const int oi = threadIdx.x / NC, occ = threadIdx.x % NC, ob = b0 + oi;
+      const float gxv = ob < B ? gx[((size_t)ob * T + t) * 4 * H + (occ / kFwdUnits) * H + u0 +
+                                    (occ % kFwdUnits)]
+                               : 0.f;
+      float acc[kRowChunk];
+#pragma unroll
+      for (int i = 0; i < kRowChunk; ++i) acc[i] = 0.f;
+      for (int k = sl; k < H; k += KS) {
+        const float w = ws[k * NC + c];
+#pragma unroll
+        for (int i = 0; i < kRowChunk; ++i)
+          if (b0 + i < B) acc[i] = fmaf(hs[(size_t)(b0 + i) * H + k], w, acc[i]);
+      }
+#pragma unroll
+      for (int i = 0; i < kRowChunk; ++i) red[(sl * kRowChunk + i) * NC + c] = acc[i];
+      __syncthreads();
+      if (ob < B) {
+        float z = 0.f;
+        for (int s2 = 0; s2 < KS; ++s2) z += red[(s2 * kRowChunk + oi) * NC + occ];
+        zs[ob * NC + occ] = gxv + z;
+      }
+      __syncthreads();
+    }
+    if (cell_thread) {
+      const float* z = zs + (size_t)cb * NC;
+      const float ig = sigmoidf(z[cu]), fg = sigmoidf(z[kFwdUnits + cu]);
+      const float gg = tanhf(z[2 * kFwdUnits + cu]), og = sigmoidf(z[3 * kFwdUnits + cu]);
+      const float cn = __fadd_rn(__fmul_rn(fg, creg), __fmul_rn(ig, gg));
+      const float hn = __fmul_rn(og, tanhf(cn));
+      creg = cn;
+      const int j = u0 + cu;
+      const size_t row = (size_t)cb * T + t;
+      gates[row * 4 * H + j] = ig;
+      gates[row * 4 * H + H + j] = fg;
+      gates[row * 4 * H + 2 * H + j] = gg;
+      gates[row * 4 * H + 3 * H + j] = og;
+      c_out[row * H + j] = cn;
+      h_out[row * H + j] = hn;
+      if (t + 1 < T) put_granule(xg + (size_t)(t & 1) * BH + (size_t)cb * H + j, (unsigned)(t + 1), hn);
+    }
+    __syncthreads();  // hs / zs are rewritten by the next step
   }
 }
 
@@ -615,6 +763,23 @@ int network_forward(acme_impala* l, const void* obs, const int32_t* prev_a, cons
   {
     ACME_PROF("impala_lstm_fwd", st, 2.0 * rows * (double)H * 4 * H, 0.0);
     const size_t smem = lstm_fwd_smem(B, H);
+    if (T > 1 && tune_variant("LSTMP") == 2 && l->xg) {
+      // One cooperative launch for the whole unroll (lstm_fwd_persistent_kernel).  Opt-in:
+      // measured 328-352 us for T = 20 at B = 16, H = 256 against 20 x 16 us of per-step
+      // launches: a step is bound by its dependent phases (the h_{t-1} exchange or load,
+      // the k-sliced reduction, the cell update), not by the launch.
+      ACME_HIP_TRY(hipMemsetAsync(l->xg, 0, (size_t)2 * B * H * sizeof(unsigned long long), st));
+      const float* wh = P(l, l->params, l->t_wh);
+      float *g = l->gates, *ho = l->h, *co = l->c;
+      unsigned long long* xg = l->xg;
+      unsigned* tmo = l->tmo;
+      int Bv = B, Tv = T, Hv = H;
+      int64_t hs0 = state_stride, cs0 = state_stride;
+      const float* gxp = l->gx;
+      void* args[] = {&gxp, &wh, &h0, &hs0, &c0, &cs0, &Bv, &Tv, &Hv, &g, &ho, &co, &xg, &tmo};
+      ACME_HIP_TRY(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(lstm_fwd_persistent_kernel),
+                                              dim3(H / kFwdUnits), dim3(256), args, smem, st));
+    } else
     for (int t = 0; t < T; ++t) {
       const float* hp = t == 0 ? h0 : l->h + (size_t)(t - 1) * H;
       const float* cp = t == 0 ? c0 : l->c + (size_t)(t - 1) * H;
@@ -825,9 +990,11 @@ int acme_impala_create(const acme_impala_config* cfg, acme_impala** out) {
       (rc = dev_alloc(l, &l->lrho, R)) || (rc = dev_alloc(l, &l->lpa, R)) ||
       (rc = dev_alloc(l, &l->ent, R)) ||
       (rc = dev_alloc(l, &l->norm_part, 2 * kNormBlocks)) || (rc = dev_alloc(l, &l->dev_step, 1)) ||
-      (rc = dev_alloc(l, &l->metrics_tmp, 4)) || (rc = dev_alloc(l, &l->norms, 2)))
+      (rc = dev_alloc(l, &l->metrics_tmp, 4)) || (rc = dev_alloc(l, &l->norms, 2)) ||
+      (rc = dev_alloc(l, &l->xg, (int64_t)2 * B * H)) || (rc = dev_alloc(l, &l->tmo, 4)))
     return fail(rc);
-  if (hipMemset(l->dev_step, 0, sizeof(int64_t)) != hipSuccess)
+  if (hipMemset(l->dev_step, 0, sizeof(int64_t)) != hipSuccess ||
+      hipMemset(l->tmo, 0, 4 * sizeof(unsigned)) != hipSuccess)
     return fail((set_error("hipMemset failed"), ACME_ERR_HIP));
   *out = l;
   return ACME_OK;
@@ -928,6 +1095,7 @@ int acme_impala_debug_buffer(const acme_impala* l, const char* name, const float
       {"pv", l->pv, R * (l->A + 1)}, {"vs", l->vs, R},        {"pg_adv", l->pg_adv, R},
       {"h", l->h, R * l->H},         {"c", l->c, R * l->H},   {"dpv", l->dpv, R * (l->A + 1)},
       {"dgates", l->dgates, R * 4 * l->H}, {"grad_norm", l->norms, 1},
+      {"lstm_timeout", reinterpret_cast<const float*>(l->tmo), 1},
       {"hh", l->hh, R * l->H2},      {"x1", l->x1, l->x1 ? R * torso::kX1 : 0},
       {"x2", l->x2, l->x2 ? R * torso::kFlat : 0}, {"x3", l->x3, l->x3 ? R * torso::kFlat : 0},
   };

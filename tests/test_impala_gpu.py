@@ -173,3 +173,36 @@ def test_policy_step_matches_unroll():
     _close(v.cpu().numpy(), values[:, 0], name="values")
     _close(h.cpu().numpy(), cache["hs"][:, 0], name="h")
     _close(c.cpu().numpy(), cache["cs"][:, 0], name="c")
+
+
+@pytest.mark.parametrize("B,T,H,torso", [(16, 20, 256, "flat"), (3, 7, 64, "flat"),
+                                         (16, 20, 256, "atari")])
+def test_persistent_lstm_forward_bitwise(B, T, H, torso):
+    """The one-launch LSTM unroll (lstm_fwd_persistent_kernel: W_h resident in LDS across
+    the T steps, h_t exchanged between workgroups as tagged granules) against the
+    per-step launches (the default; ACME_V_LSTMP=2 selects the persistent kernel): h, c,
+    gate gradients and losses equal to fp32
+    rounding (the two kernels' instruction selection differs in the last bit), no spin
+    timeout.  Both are checked against the f64 oracle by the tests above."""
+    from acme_amd._lib import lib
+    cfg = O.IMPALAConfig(num_actions=18 if torso == "atari" else 5, torso=torso, obs_dim=12,
+                         lstm_size=H, head_size=64, entropy_cost=0.01, baseline_cost=0.5)
+    params = _params(cfg, 5)
+    b = _batch(cfg, B, T, 6)
+    res = {}
+    for v in (2, 0):
+        lib().acme_tune_set(b"LSTMP", v)
+        try:
+            n = _native(cfg, B, T)
+            n.set_params(params)
+            _run(n, b)
+            res[v] = {k: n.debug_buffer(k) for k in ("h", "c", "dgates", "pv")}
+            res[v]["metrics"] = n.metrics.cpu().numpy()
+            res[v]["tmo"] = n.debug_buffer("lstm_timeout")[:1].view(np.uint32)
+        finally:
+            lib().acme_tune_set(b"LSTMP", 0)
+    assert res[2]["tmo"][0] == 0
+    for k in ("h", "c", "dgates", "pv", "metrics"):
+        scale = float(np.abs(res[0][k]).max())
+        np.testing.assert_allclose(res[2][k], res[0][k], rtol=1e-5, atol=1e-6 * scale,
+                                   err_msg=k)
