@@ -69,12 +69,10 @@ __device__ __forceinline__ void relu_mask8(const CPlanes& x, int64_t e, V8& v) {
 }
 
 // ------------------------------------------------------------------ forward
-// NPA = 1: frames (uint8 values; U8: the raw uint8 frames, else their bf16 copy), result
-// scaled by 1/255; NPA = 3: f32 planes.
-template <class G, int NPA, bool U8 = false>
+// NPA = 1: frames (the bf16 copy of the uint8 values), result scaled by 1/255; NPA = 3:
+// f32 planes.
+template <class G, int NPA>
 struct P3ConvFwd {
-  static_assert(!U8 || NPA == 1, "uint8 operands are one plane");
-  static constexpr bool kAU8 = U8;
   static_assert(G::CI % 8 == 0 || (G::CI == 4 && G::KW % 2 == 0 && G::S % 2 == 0 &&
                                    G::PL % 2 == 0),
                 "8-k units need 8 channels, or 4-channel pixel pairs that never straddle "
@@ -140,10 +138,8 @@ struct P3ConvFwd {
 };
 
 // ------------------------------------------------------------------ weight grad
-template <class G, int NPA, bool U8 = false>
+template <class G, int NPA>
 struct P3ConvWgrad {
-  static_assert(!U8 || NPA == 1, "uint8 operands are one plane");
-  static constexpr bool kAU8 = U8;
   static_assert(G::CI % 8 == 0 || (G::CI == 4 && G::KW % 2 == 0 && G::S % 2 == 0 &&
                                    G::PL % 2 == 0),
                 "see P3ConvFwd");

@@ -27,7 +27,6 @@
 #include "conv_p3.h"
 #include "gemm.h"
 #include "gemm_p3.h"
-#include "gemm_p3d.h"
 #include "gemm_x6.h"
 #include "kernels.h"
 #include "profiler.h"
@@ -91,10 +90,8 @@ struct acme_dqn {
   bool last_p3 = false;      // the last forward/backward ran the plane path
   uint16_t *wpl = nullptr, *tpl = nullptr;
   uint16_t* frames = nullptr;  // bf16 copies of [o_tm1; o_t] (2B frames)
-  // conv1's input of the current step: l->frames (bf16 copy), or with ACME_V_U8F=2 the
-  // batch's own uint8 frames when o_t directly follows o_tm1 in memory (the GPU dataset
-  // allocates them so).
-  torso::Frames cur_frames{nullptr, false};
+  // conv1's input of the current step (l->frames, the bf16 copy).
+  torso::Frames cur_frames{nullptr};
   // Second stream of the plane path: the target forward runs beside the online forward,
   // and weight gradients beside input gradients (fork / join by events on the caller's
   // stream; side_slab is its split-K scratch).
@@ -230,18 +227,6 @@ int tune(const char* key) { return tune_variant(key); }
     }                                                                                          \
   } while (0)
 
-// Direct-A plane GEMM (gemm_p3d.h): BN-column panels, NW waves of 32 * MT rows each.
-#define ACME_P3D_GEMM(name, BN, MT, NW, BKV, prob, splits)                                    \
-  do {                                                                                        \
-    ACME_PROF_PEAK(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0, \
-                   gemm::p3_peak_tflops<decltype(prob)>());                                   \
-    hipError_t _e = gemm::launch_gemm_p3d<BN, MT, NW, BKV>(prob, splits, st);                 \
-    if (_e != hipSuccess) {                                                                   \
-      set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
-      return ACME_ERR_HIP;                                                                    \
-    }                                                                                         \
-  } while (0)
-
 #define ACME_P3_GEMM(name, BM, BN, WM, WN, BKV, prob, splits)                                \
   do {                                                                                         \
     ACME_PROF_PEAK(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0, \
@@ -253,16 +238,6 @@ int tune(const char* key) { return tune_variant(key); }
     }                                                                                          \
   } while (0)
 
-#define ACME_P3P_GEMM(name, BM, BN, WM, WN, prob, splits)                                    \
-  do {                                                                                        \
-    ACME_PROF_PEAK(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0, \
-                   gemm::p3_peak_tflops<decltype(prob)>());                                   \
-    hipError_t _e = gemm::launch_gemm_p3p<BM, BN, WM, WN>(prob, splits, st);                  \
-    if (_e != hipSuccess) {                                                                   \
-      set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
-      return ACME_ERR_HIP;                                                                    \
-    }                                                                                         \
-  } while (0)
 #define ACME_P3G_GEMM(name, BM, BN, WM, WN, BKV, ST, prob, splits)                            \
   do {                                                                                         \
     ACME_PROF_PEAK(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0, \
@@ -276,12 +251,11 @@ int tune(const char* key) { return tune_variant(key); }
 
 // Split counts (K-splits) of the launches whose natural grid is too small to fill 256 CUs.
 constexpr int kFcFwdSplits = 8;  // [rows, 1024] x K 7744: 128x128 tiles: 8x8x8 = 512 blocks (online)
-constexpr int kFcFwdMaxSplits = 32;  // slab capacity for the plane path's split choices
 constexpr int kHeadFwdSplits = 16;  // [rows, A+1] x K 1024
 constexpr int kHeadBwdSplits = 8;   // [1024, A+1] x K = batch
 
 int64_t slab_floats_needed(int B, int A) {
-  return std::max<int64_t>({torso::wgrad_slab_floats(), (int64_t)kFcFwdMaxSplits * 2 * B * 2 * kHidden,
+  return std::max<int64_t>({torso::wgrad_slab_floats(), (int64_t)kFcFwdSplits * 2 * B * 2 * kHidden,
                             (int64_t)kHeadFwdSplits * 2 * B * (A + 1),
                             (int64_t)kHeadBwdSplits * (2 * kHidden + 1) * (A + 1)});
 }
@@ -323,18 +297,12 @@ int nature_forward(acme_dqn* l, const float* prm, const void* obs_a, const void*
   if (rc0 != ACME_OK) return rc0;
   {  // Fused duelling hidden layer, split-K partials then bias + ReLU in the reduction.
     DenseFwd<true> p;
-    const int v = tune("FCFWD");
-    const int splits = v == 3 ? 4 : kFcFwdSplits;
+    const int splits = kFcFwdSplits;
     p.M = rows; p.N = 2 * kHidden; p.K = kFlat; p.k_chunk = chunk_for(kFlat, splits);
     p.x = x3; p.x2 = x3; p.split_b = rows; p.ldx = kFlat;
     p.w = P(l, prm, l->t_fcw); p.bias = P(l, prm, l->t_fcb); p.y = hid; p.act = ACT_RELU;
     p.slab = l->slab;
-    switch (v) {
-      case 1: ACME_GEMM_NK("fc_fwd", 128, 128, 2, 2, 16, p, splits); break;
-      case 2: ACME_GEMM_NK("fc_fwd", 256, 128, 4, 2, 16, p, splits); break;
-      case 4: ACME_GEMM_NK("fc_fwd", 64, 64, 2, 2, 16, p, splits); break;
-      default: ACME_GEMM_NK("fc_fwd", 128, 128, 2, 2, 32, p, splits); break;
-    }
+    ACME_GEMM_NK("fc_fwd", 128, 128, 2, 2, 32, p, splits);
     const int64_t cnt = (int64_t)rows * 2 * kHidden;
     int rc = slab_reduce(l->slab, splits, cnt, hid, cnt, nullptr, P(l, prm, l->t_fcb),
                          2 * kHidden, 1, "fc_fwd_reduce", st);
@@ -357,33 +325,11 @@ int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const torso:
   {
     P3DenseFwd p;
     // Split-K: about one round of blocks (128x128 tiles, one block per CU at BK 32).
-    const int sv = tune("P3FCS");
-    const int fv = tune("P3FCF");
-    int splits = sv > 0 && sv <= kFcFwdMaxSplits ? sv : (rows > 512 ? 4 : kFcFwdSplits);
-    if (sv <= 0 && (fv == 6 || fv == 13 || fv == 14)) splits = rows > 512 ? 8 : 16;  // 256x128
-    if (sv <= 0 && fv == 7) splits = rows > 512 ? 16 : 32;  // 256x256 tiles
+    const int splits = rows > 512 ? 4 : kFcFwdSplits;
     p.M = rows; p.N = 2 * kHidden; p.K = kFlat; p.k_chunk = chunk_for(kFlat, splits);
     p.a_src = SRC(x3, (int64_t)rows * kFlat); p.ldx = kFlat;
     p.b_src = SRC(WP(l, wpl, l->t_fcw), (int64_t)kFlat * 2 * kHidden); p.slab = slab;
-    switch (fv) {
-      case 1: ACME_P3_GEMM("fc_fwd", 128, 128, 2, 2, 16, p, splits); break;
-      case 2: ACME_P3_GEMM("fc_fwd", 256, 128, 4, 2, 16, p, splits); break;
-      case 3: ACME_P3G_GEMM("fc_fwd", 128, 128, 2, 2, 16, 3, p, splits); break;
-      case 4: ACME_P3G_GEMM("fc_fwd", 128, 128, 2, 2, 32, 3, p, splits); break;
-      case 5: ACME_P3G_GEMM("fc_fwd", 128, 128, 2, 2, 16, 4, p, splits); break;
-      case 6: ACME_P3_GEMM("fc_fwd", 256, 128, 4, 2, 16, p, splits); break;
-      case 7: ACME_P3_GEMM("fc_fwd", 256, 256, 4, 2, 16, p, splits); break;
-      case 8: ACME_P3P_GEMM("fc_fwd", 128, 128, 2, 2, p, splits); break;
-      case 9: ACME_P3D_GEMM("fc_fwd", 128, 1, 4, 32, p, splits); break;
-      case 10: ACME_P3D_GEMM("fc_fwd", 128, 2, 4, 32, p, splits); break;
-      case 11: ACME_P3D_GEMM("fc_fwd", 64, 1, 4, 32, p, splits); break;
-      case 12: ACME_P3D_GEMM("fc_fwd", 128, 1, 8, 32, p, splits); break;
-      case 13: ACME_P3_GEMM("fc_fwd", 256, 128, 4, 2, 32, p, splits); break;
-      case 14: ACME_P3_GEMM("fc_fwd", 128, 256, 2, 4, 32, p, splits); break;
-      case 15: ACME_P3_GEMM("fc_fwd", 128, 128, 2, 4, 32, p, splits); break;
-      case 16: ACME_P3_GEMM("fc_fwd", 128, 128, 4, 2, 32, p, splits); break;
-      default: ACME_P3_GEMM("fc_fwd", 128, 128, 2, 2, 32, p, splits); break;
-    }
+    ACME_P3_GEMM("fc_fwd", 128, 128, 2, 2, 32, p, splits);
     ACME_PROF("fc_head_fwd", st, 0.0, 4.0 * (double)rows * 2 * kHidden * (splits + 1));
     return launch_fc_head_forward(slab, splits, rows, kHidden, P(l, prm, l->t_fcb),
                                   P(l, prm, l->t_vw), P(l, prm, l->t_vb), P(l, prm, l->t_aw),
@@ -484,13 +430,7 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st_main,
       p.a_src = SRC(l->x3p, (int64_t)B * kFlat); p.ldx = kFlat;
       p.b_src = SRC(l->dzhp, (int64_t)B * 2 * kHidden); p.out = Pm(l, gr, l->t_fcw);
       p.bias_out = Pm(l, gr, l->t_fcb);
-      switch (tune("P3FCW")) {
-        case 1: ACME_P3_GEMM("fc_wgrad", 128, 128, 2, 2, 32, p, 1); break;
-        case 3: ACME_P3G_GEMM("fc_wgrad", 128, 128, 2, 2, 16, 3, p, 1); break;
-        case 4: ACME_P3G_GEMM("fc_wgrad", 128, 128, 2, 2, 32, 3, p, 1); break;
-        case 8: ACME_P3P_GEMM("fc_wgrad", 128, 128, 2, 2, p, 1); break;
-        default: ACME_P3_GEMM("fc_wgrad", 128, 128, 2, 2, 16, p, 1); break;
-      }
+      ACME_P3_GEMM("fc_wgrad", 128, 128, 2, 2, 16, p, 1);
     }
     if (fork) {
       ACME_HIP_TRY(hipEventRecord(l->ev[3], l->side));
@@ -502,17 +442,8 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st_main,
       p.a_src = SRC(l->dzhp, (int64_t)B * 2 * kHidden);
       p.b_src = SRC(WP(l, l->wpl, l->t_fcw), (int64_t)kFlat * 2 * kHidden); p.xprev = CP(l->x3p);
       p.ldx = kFlat; p.dx = PP(l->dz3p);
-      switch (tune("P3FCD")) {
-        case 1: ACME_P3_GEMM("fc_dgrad", 64, 128, 2, 2, 32, p, 1); break;
-        case 2: ACME_P3_GEMM("fc_dgrad", 64, 128, 2, 2, 16, p, 1); break;
-        case 3: ACME_P3G_GEMM("fc_dgrad", 128, 128, 2, 2, 16, 3, p, 1); break;
-        case 4: ACME_P3_GEMM("fc_dgrad", 128, 128, 2, 2, 32, p, 1); break;
-        case 8: ACME_P3P_GEMM("fc_dgrad", 128, 128, 2, 2, p, 1); break;
-        case 9: ACME_P3P_GEMM("fc_dgrad", 64, 128, 2, 2, p, 1); break;
-        case 10: ACME_P3D_GEMM("fc_dgrad", 128, 1, 4, 32, p, 1); break;
-        case 11: ACME_P3D_GEMM("fc_dgrad", 128, 2, 4, 32, p, 1); break;
-        default: ACME_P3G_GEMM("fc_dgrad", 128, 128, 2, 2, 32, 3, p, 1); break;
-      }
+      // LDS-DMA staging (gemm_p3.h P3G) measured fastest for this shape.
+      ACME_P3G_GEMM("fc_dgrad", 128, 128, 2, 2, 32, 3, p, 1);
     }
     if (fork && join_dense) ACME_HIP_TRY(hipStreamWaitEvent(st_main, l->ev[3], 0));
     return ACME_OK;
@@ -528,11 +459,7 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st_main,
     DenseDgrad<true> p;
     p.M = B; p.N = kFlat; p.K = 2 * kHidden; p.k_chunk = p.K;
     p.dz = l->dzh; p.w = P(l, prm, l->t_fcw); p.xprev = l->x3; p.ldx = kFlat; p.dx = l->dz3;
-    switch (tune("FCDGRAD")) {
-      case 1: ACME_GEMM_NK("fc_dgrad", 128, 128, 2, 2, 16, p, 1); break;
-      case 2: ACME_GEMM_NK("fc_dgrad", 64, 128, 1, 2, 16, p, 1); break;
-      default: ACME_GEMM_NK("fc_dgrad", 64, 128, 2, 2, 16, p, 1); break;
-    }
+    ACME_GEMM_NK("fc_dgrad", 64, 128, 2, 2, 16, p, 1);
   }
   return ACME_OK;  // the torso backward is stage 1 (acme_dqn_forward_backward_stage)
 }
@@ -853,7 +780,7 @@ int acme_dqn_q_values(acme_dqn* l, const void* obs, int64_t batch, int32_t use_t
     int rc = sync_planes(l, st);
     if (rc == ACME_OK) rc = convert_frames(l, obs, obs, B, B, st);
     if (rc != ACME_OK) return rc;
-    return nature_forward_p3(l, prm, use_target ? l->tpl : l->wpl, torso::Frames{l->frames, false},
+    return nature_forward_p3(l, prm, use_target ? l->tpl : l->wpl, torso::Frames{l->frames},
                              B, l->t1p, l->t2p,
                              l->t3p, l->thid, q_out, st);
   }
@@ -918,38 +845,20 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
   l->last_p3 = nature && use_p3(l);
   if (l->last_p3) {
     if ((rc = sync_planes(l, st)) != ACME_OK) return rc;
-    const uint8_t* o1 = static_cast<const uint8_t*>(batch->o_tm1);
     hipStream_t tst = st;
     hipStream_t side = side_stream(l);
-    // conv1's input.  Default: a bf16 copy of [o_tm1; o_t] on the main stream for everything.
-    // When o_t directly follows o_tm1 (the GPU dataset's layout): ACME_V_U8F=2 reads the
-    // batch's uint8 frames everywhere (no copy); ACME_V_U8F=3 reads them in both forwards
-    // and makes the weight gradient's bf16 copy of o_tm1 only, on the side stream ahead of
-    // the target forward.  Both measured slower beside the side stream (0.746 -> 0.750 ms
-    // per step for 3): the uint8 image kernel is slower there than the bf16 one.
-    const bool adjacent = batch->o_t == o1 + (size_t)B * kObsBytes;
-    const int u8f = tune("U8F");
-    torso::Frames fwd_frames{l->frames, false};
-    bool convert_on_side = false;
-    if (adjacent && u8f == 2) {
-      fwd_frames = l->cur_frames = torso::Frames{o1, true};
-    } else if (adjacent && u8f == 3 && side) {
-      fwd_frames = torso::Frames{o1, true};
-      l->cur_frames = torso::Frames{l->frames, false};
-      convert_on_side = true;
-    } else {
-      if ((rc = convert_frames(l, batch->o_tm1, batch->o_t, B, 2 * B, st)) != ACME_OK) return rc;
-      l->cur_frames = fwd_frames;
-    }
+    // conv1's input: a bf16 copy of [o_tm1; o_t] on the main stream for everything.  (Reading
+    // the batch's uint8 frames in the kernels instead measured slower beside the side stream,
+    // 0.746 -> 0.750 ms per step: the uint8 image kernel is slower there than the bf16 one.)
+    if ((rc = convert_frames(l, batch->o_tm1, batch->o_t, B, 2 * B, st)) != ACME_OK) return rc;
+    const torso::Frames fwd_frames{l->frames};
+    l->cur_frames = fwd_frames;
     // Target forward (q_t_value) on the side stream, beside the online forward.
     if (side) {
       ACME_HIP_TRY(hipEventRecord(l->ev[0], st));
       ACME_HIP_TRY(hipStreamWaitEvent(side, l->ev[0], 0));
       tst = side;
     }
-    if (convert_on_side &&
-        (rc = convert_frames(l, batch->o_tm1, batch->o_tm1, B, B, side)) != ACME_OK)
-      return rc;
     if ((rc = nature_forward_p3(l, l->target, l->tpl, fwd_frames.rows_from(B), B,
                                 l->t1p, l->t2p, l->t3p, l->thid, l->q_tg, tst,
                                 side ? l->side_slab : l->slab, 0)) != ACME_OK)
@@ -998,7 +907,7 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
   la.prio = prio;
   la.g = l->g;
   la.a_cache = l->a_cache;
-  if (l->last_p3 && tune("LHDZ") != 1) {  // fused with the head dZ (nature_backward)
+  if (l->last_p3) {  // fused with the head dZ (nature_backward)
     l->pending_la = la;
     l->loss_pending = true;
   } else {

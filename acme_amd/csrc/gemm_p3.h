@@ -162,33 +162,6 @@ struct HasStore8<P, decltype(void(P::kStore8))> {
   static constexpr bool value = P::kStore8;
 };
 
-// Optional uint8 A operand: problems with `static constexpr bool kAU8 = true` (one plane)
-// keep A as the raw uint8 frames; the loaders' offsets still count bf16 bytes (2 * element),
-// and the kernel loads the unit's 8 bytes and widens them to the 8 exact bf16 values
-// (integers 0..255), so no converted copy of the frames exists.
-template <class P, class = void>
-struct HasAU8 {
-  static constexpr bool value = false;
-};
-template <class P>
-struct HasAU8<P, decltype(void(P::kAU8))> {
-  static constexpr bool value = P::kAU8;
-};
-// bf16 bit pattern of byte i of w: the upper half of float(byte) (exact).
-__device__ __forceinline__ uint32_t u8pair_bf16(uint32_t w, int i) {
-  const uint32_t a = __builtin_bit_cast(uint32_t, (float)((w >> (8 * i)) & 0xffu));
-  const uint32_t b = __builtin_bit_cast(uint32_t, (float)((w >> (8 * i + 8)) & 0xffu));
-  return (a >> 16) | (b & 0xffff0000u);
-}
-// 16-byte unit (8 bf16) of a uint8 operand at bf16-byte offset `off` (kOOB -> zeros).
-__device__ __forceinline__ u32x4 load_u8_unit(__amdgpu_buffer_rsrc_t rsrc, uint32_t off) {
-  const uint32_t o8 = (off >> 1) | (off & 0x80000000u);
-  typedef __attribute__((ext_vector_type(2))) int i32x2;
-  const i32x2 w = __builtin_amdgcn_raw_buffer_load_b64(rsrc, o8, 0, 0);
-  const uint32_t lo = (uint32_t)w[0], hi = (uint32_t)w[1];
-  return u32x4{u8pair_bf16(lo, 0), u8pair_bf16(lo, 2), u8pair_bf16(hi, 0), u8pair_bf16(hi, 2)};
-}
-
 template <int BK>
 __device__ __forceinline__ int p3_kswz(int row) {
   return BK == 16 ? ((row >> 3) & 1) : ((row >> 2) & 3);
@@ -468,10 +441,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in, int
       const uint32_t off = (PA::owns(u) && k0 + kk < kend) ? p.a_off(arow[i], k0, kk) : kOOB;
 #pragma unroll
       for (int pl = 0; pl < NPA; ++pl) {
-        if constexpr (HasAU8<P>::value)
-          ra[set][i][pl] = load_u8_unit(srcA[pl], off);
-        else
-          ra[set][i][pl] = (P3_EXP == 1 || P3_EXP >= 4) ? u32x4{off, (uint32_t)k0, 1u, 2u}
+        ra[set][i][pl] = (P3_EXP == 1 || P3_EXP >= 4) ? u32x4{off, (uint32_t)k0, 1u, 2u}
                                      : __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srcA[pl], off, 0, 0));
       }
     }
@@ -781,192 +751,6 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3g_kernel(const P p_in, in
 #endif
 }
 
-// Fragment-pipelined variant of gemm_p3_kernel (BK = 32: two k16 steps per stage).  The
-// plain kernel reads each step's fragments from LDS and then waits for them before its
-// first MFMA, exposing the LDS latency once per k16 step (the compiler does not carry
-// fragment reads across steps or across the stage barrier).  Here the fragments are double
-// buffered: step 1's reads are issued before step 0's MFMAs, and the NEXT stage's step-0
-// reads right after the stage barrier, before step 1's MFMAs, so every read is covered
-// by a full step of MFMAs.  Per iteration (stage kt in LDS buffer kt & 1):
-//   read F1 <- (kt, step 1); MFMA(F0); stash stage kt+1 -> other buffer; fetch stage kt+2;
-//   barrier; read F0 <- (kt+1, step 0); MFMA(F1).
-template <int BM, int BN, int WM, int WN, class P>
-__global__ void __launch_bounds__(64 * WM * WN) gemm_p3p_kernel(const P p_in, int n_major) {
-  constexpr int BK = 32;
-  using C = P3Core<BM, BN, WM, WN, BK, P>;
-  using PA = typename C::PA;
-  using PB = typename C::PB;
-  constexpr int NT = C::NT, NPA = C::NPA, NPB = C::NPB, STAGE = C::STAGE;
-  constexpr int MT = C::MT, NTL = C::NTL, TM = C::TM, TN = C::TN;
-  const BlockPlace bp = place_block<BM, BN>(p_in.M, p_in.N, n_major);
-  const P p = z_select_at(p_in, bp.z);
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN;
-  const int m0 = bp.m0, n0 = bp.n0;
-  const int split = HasZClass<P>::value ? 0 : bp.z;
-  const int kbeg = split * p.k_chunk;
-  int kend = kbeg + p.k_chunk;
-  if (kend > p.K) kend = p.K;
-  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-
-  typename P::ARow arow[PA::PER_THREAD];
-  typename P::BRow brow[PB::PER_THREAD];
-#pragma unroll
-  for (int i = 0; i < PA::PER_THREAD; ++i)
-    arow[i] = p.a_row(m0 + (PA::owns(tid + i * NT) ? PA::row_of(tid + i * NT) : 0));
-#pragma unroll
-  for (int i = 0; i < PB::PER_THREAD; ++i)
-    brow[i] = p.b_row(n0 + (PB::owns(tid + i * NT) ? PB::row_of(tid + i * NT) : 0));
-  __amdgpu_buffer_rsrc_t srcA[NPA], srcB[NPB];
-#pragma unroll
-  for (int pl = 0; pl < NPA; ++pl) srcA[pl] = plane_rsrc(p.a_src, pl);
-#pragma unroll
-  for (int pl = 0; pl < NPB; ++pl) srcB[pl] = plane_rsrc(p.b_src, pl);
-
-  u32x4 ra[2][PA::PER_THREAD][NPA], rb[2][PB::PER_THREAD][NPB];
-  auto fetch = [&](auto S, int k0) {
-    constexpr int set = decltype(S)::value;
-#pragma unroll
-    for (int i = 0; i < PA::PER_THREAD; ++i) {
-      const int u = tid + i * NT;
-      const int kk = PA::kk_of(u);
-      const uint32_t off = (PA::owns(u) && k0 + kk < kend) ? p.a_off(arow[i], k0, kk) : kOOB;
-#pragma unroll
-      for (int pl = 0; pl < NPA; ++pl)
-        ra[set][i][pl] =
-            __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srcA[pl], off, 0, 0));
-    }
-#pragma unroll
-    for (int i = 0; i < PB::PER_THREAD; ++i) {
-      const int u = tid + i * NT;
-      const int kk = PB::kk_of(u);
-      const uint32_t off = (PB::owns(u) && k0 + kk < kend) ? p.b_off(brow[i], k0, kk) : kOOB;
-#pragma unroll
-      for (int pl = 0; pl < NPB; ++pl)
-        rb[set][i][pl] =
-            __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srcB[pl], off, 0, 0));
-    }
-  };
-  auto stash = [&](auto S, int buf) {
-    constexpr int set = decltype(S)::value;
-    uint8_t* sa = smem + buf * STAGE;
-    uint8_t* sb = sa + PA::BYTES;
-#pragma unroll
-    for (int i = 0; i < PA::PER_THREAD; ++i) {
-      const int u = tid + i * NT;
-      if (!PA::owns(u)) continue;
-      const int off = PA::offset(u);
-#pragma unroll
-      for (int pl = 0; pl < NPA; ++pl)
-        *reinterpret_cast<u32x4*>(sa + pl * PA::PLANE + off) = ra[set][i][pl];
-    }
-#pragma unroll
-    for (int i = 0; i < PB::PER_THREAD; ++i) {
-      const int u = tid + i * NT;
-      if (!PB::owns(u)) continue;
-      const int off = PB::offset(u);
-#pragma unroll
-      for (int pl = 0; pl < NPB; ++pl)
-        *reinterpret_cast<u32x4*>(sb + pl * PB::PLANE + off) = rb[set][i][pl];
-    }
-  };
-
-  f32x16 acc[MT][NTL];
-  f32x16 cs[C::NCS];
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int j = 0; j < NTL; ++j)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
-#pragma unroll
-  for (int j = 0; j < C::NCS; ++j)
-#pragma unroll
-    for (int v = 0; v < 16; ++v) cs[j][v] = 0.f;
-  const bool do_colsum = C::kColSum && m0 == 0 && wm == 0;
-
-  bf16x8 fa[2][MT][NPA], fb[2][NTL][NPB];
-  auto rd = [&](auto F, int buf, int s) {
-    constexpr int f = decltype(F)::value;
-    const uint8_t* sa = smem + buf * STAGE;
-    const uint8_t* sb = sa + PA::BYTES;
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int pl = 0; pl < NPA; ++pl) fa[f][i][pl] = PA::frag(sa, pl, wm * TM + i * 32, s, lane);
-#pragma unroll
-    for (int j = 0; j < NTL; ++j)
-#pragma unroll
-      for (int pl = 0; pl < NPB; ++pl) fb[f][j][pl] = PB::frag(sb, pl, wn * TN + j * 32, s, lane);
-  };
-  const bf16x8 ones{(__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f,
-                    (__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f};
-  auto mm = [&](auto F) {
-    constexpr int f = decltype(F)::value;
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int j = 0; j < NTL; ++j) {
-        const bf16x8(&a)[NPA] = fa[f][i];
-        const bf16x8(&b)[NPB] = fb[f][j];
-        if constexpr (NPA == 3 && NPB == 3) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc[i][j], 0, 0, 0);
-        } else if constexpr (NPA == 3) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc[i][j], 0, 0, 0);
-        } else if constexpr (NPB == 3) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc[i][j], 0, 0, 0);
-        }
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc[i][j], 0, 0, 0);
-      }
-    if constexpr (C::kColSum) {
-      if (do_colsum) {
-#pragma unroll
-        for (int j = 0; j < NTL; ++j)
-#pragma unroll
-          for (int pl = NPB - 1; pl >= 0; --pl)
-            cs[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fb[f][j][pl], cs[j], 0, 0, 0);
-      }
-    }
-  };
-
-  using S0 = std::integral_constant<int, 0>;
-  using S1 = std::integral_constant<int, 1>;
-  fetch(S0{}, kbeg);
-  stash(S0{}, 0);
-  fetch(S1{}, kbeg + BK);
-  __syncthreads();
-  rd(S0{}, 0, 0);
-  auto iter = [&](auto S, int kt) {
-    constexpr int set = decltype(S)::value;
-    using Other = std::integral_constant<int, set ^ 1>;
-    rd(S1{}, set, 1);
-    mm(S0{});
-    stash(Other{}, set ^ 1);
-    fetch(S, kbeg + (kt + 2) * BK);
-    __syncthreads();
-    rd(S0{}, set ^ 1, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    mm(S1{});
-  };
-  int kt = 0;
-  for (; kt + 1 < nk; kt += 2) {
-    iter(S0{}, kt);
-    iter(S1{}, kt + 1);
-  }
-  if (kt < nk) iter(S0{}, kt);
-  __syncthreads();
-  C::epilogue(p, smem, m0, n0, wave, wm, wn, lane, split, acc, cs, do_colsum);
-}
-
 // Tile order: B's panels slowest when B is the larger operand (N * planes > M * planes).
 template <class P>
 inline int p3_n_major(const P& p) {
@@ -1013,20 +797,6 @@ inline hipError_t launch_gemm_p3g(const P& p, int splits, hipStream_t st) {
   const int tiles = ((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
   hipLaunchKernelGGL((gemm_p3g_kernel<BM, BN, WM, WN, BK, STAGES, P>), dim3(tiles, 1, splits),
                      dim3(C::NT), LDS, st, p, p3_n_major(p));
-  return hipGetLastError();
-}
-
-template <int BM, int BN, int WM, int WN, class P>
-inline hipError_t launch_gemm_p3p(const P& p, int splits, hipStream_t st) {
-  using C = P3Core<BM, BN, WM, WN, 32, P>;
-  constexpr int STAGES_BYTES = 2 * C::STAGE;
-  constexpr int LDS = STAGES_BYTES > C::EPI_BYTES ? STAGES_BYTES : C::EPI_BYTES;
-  static_assert(LDS <= 160 * 1024, "two stages must fit the 160-KiB LDS of a CU");
-  static hipError_t attr = p3_set_lds(&gemm_p3p_kernel<BM, BN, WM, WN, P>, LDS);
-  if (attr != hipSuccess) return attr;
-  const int tiles = ((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
-  hipLaunchKernelGGL((gemm_p3p_kernel<BM, BN, WM, WN, P>), dim3(tiles, 1, splits), dim3(C::NT),
-                     LDS, st, p, p3_n_major(p));
   return hipGetLastError();
 }
 

@@ -2,14 +2,13 @@
 //
 // gemm_p3.h reads a convolution's A operand as im2col rows: every input pixel is fetched
 // KH*KW/S^2 times (4x for conv1 / conv2, 9x for conv3) and every fetch goes global -> VGPR
-// -> LDS (or, in gemm_p3d.h, global -> VGPR as short per-lane row segments), so the A
+// -> LDS, so the A
 // tile's LDS stores (ds_write_b128 ~79 B/clk/CU, MI355X_MICROARCH.md §LDS) or its TA
 // issue bound the convolutions (15-34% of the plane-engine ceiling).  Here a block owns
 // FPB whole frames: their input image, every plane, is loaded into LDS ONCE (each HBM
 // byte once, each LDS byte stored once), and the MFMA A fragments are read from it
 // directly, with the tap offset applied per lane (padding taps read a zero unit).  Only
-// the weight panel B (K x BN) streams through the two-stage register-staged LDS ring of
-// gemm_p3d.h.
+// the weight panel B (K x BN) streams through a two-stage register-staged LDS ring.
 //
 // A geometry GI says where each 16-B unit (8 consecutive k of one GEMM row) lives:
 //   UNITS            16-B HBM units per frame (frames contiguous in HBM);
@@ -91,18 +90,13 @@ struct ImgGeom {
 
 // Pixel-pair images for a 4-channel input (conv1 over the frames, one plane): a unit is two
 // horizontally adjacent pixels x 4 channels, which is exactly the 8 k of one MFMA lane
-// (k = (kh, kw, c): kw even, kw + 1) -- 16 B of the bf16 frame copy, or (U8) the 8 raw
-// uint8 bytes, widened to exact bf16 in registers after the LDS read.  A 32-k stage is one
+// (k = (kh, kw, c): kw even, kw + 1) -- 16 B of the bf16 frame copy.  A 32-k stage is one
 // kernel row kh (KW * CI = 32).  LDS layout: unit (ih, pw) (pw = iw / 2) at (frame * IH +
 // ih) * PAIRS + col, col = the even pairs then the odd ones, so stride-S output columns
-// read consecutive units (conflict-free ds_read_b128 / ds_read_b64 lane groups).
-// SRC 0: the bf16 frame copy; 1: the raw uint8 frames, kept as uint8 in LDS (widened per
-// fragment read); 2: the raw uint8 frames, widened to bf16 once while filling the image.
-template <class G, int SRC = 0>
+// read consecutive units (conflict-free ds_read_b128 lane groups).
+template <class G>
 struct ImgGeomPairs {
-  static constexpr bool U8 = SRC == 1;            // fragments widened after the LDS read
-  static constexpr int UNIT = SRC == 1 ? 8 : 16;  // LDS bytes per unit
-  static constexpr int HBM_UNIT = SRC == 0 ? 16 : 8;
+  static constexpr int UNIT = 16;  // LDS bytes per unit
   static constexpr int H = G::IH, W = G::IW;
   static constexpr int OW = G::OW, OPIX = G::OPIX;
   static constexpr int PAIRS = W / 2, HALF = (PAIRS + 1) / 2;
@@ -134,20 +128,6 @@ struct ImgGeomPairs {
     const int iw = l.iw + 4 * s + 2 * h;  // kw = (16 s + 8 h) / 4
     return st.base >= 0 && (unsigned)iw < (unsigned)W ? st.base + col(iw >> 1) * UNIT : -1;
   }
-};
-
-// Unit size and element type of a geometry (16-B bf16 units unless it says otherwise).
-template <class GI, class = void>
-struct ImgUnit {
-  static constexpr int BYTES = 16;
-  static constexpr bool U8 = false;
-  static constexpr bool WIDEN = false;
-};
-template <class GI>
-struct ImgUnit<GI, decltype(void(GI::UNIT))> {
-  static constexpr int BYTES = GI::HBM_UNIT;  // HBM bytes per unit
-  static constexpr bool U8 = GI::U8;
-  static constexpr bool WIDEN = GI::HBM_UNIT == 8 && GI::UNIT == 16;  // uint8 -> bf16 at fill
 };
 
 template <class GI, int FPB, int BN, int WM, int WN, int MT, class P>
@@ -190,7 +170,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
   p.M = m0 + rows < p_in.M ? m0 + rows : p_in.M;  // the epilogue writes this block's rows only
   const int nk = p.K / BK;
 
-  // ---- B: the weight panel, register-staged double buffer (gemm_p3d.h).
+  // ---- B: the weight panel, register-staged double buffer.
   typename P::BRow brow[PB::PER_THREAD];
 #pragma unroll
   for (int i = 0; i < PB::PER_THREAD; ++i)
@@ -232,9 +212,8 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
   fetch_b(S1{}, BK);
 
   // ---- A: the block's frames, each unit of each plane loaded and stored once.
-  constexpr int UB = ImgUnit<GI>::BYTES;
-  using u32x2 = __attribute__((ext_vector_type(2))) uint32_t;
-  using UT = std::conditional_t<UB == 8, u32x2, u32x4>;
+  constexpr int UB = 16;  // bytes per unit
+  using UT = u32x4;
   {
     constexpr int UNITS = FPB * GI::UNITS;
     constexpr int PER = (UNITS + NT - 1) / NT;
@@ -251,10 +230,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
       const uint32_t off = ok ? (uint32_t)(((int64_t)f0 * GI::UNITS + u) * UB) : kOOB;
 #pragma unroll
       for (int pl = 0; pl < NPA; ++pl) {
-        if constexpr (UB == 8)
-          v[j][pl] = __builtin_bit_cast(UT, __builtin_amdgcn_raw_buffer_load_b64(srcA[pl], off, 0, 0));
-        else
-          v[j][pl] = __builtin_bit_cast(UT, __builtin_amdgcn_raw_buffer_load_b128(srcA[pl], off, 0, 0));
+        v[j][pl] = __builtin_bit_cast(UT, __builtin_amdgcn_raw_buffer_load_b128(srcA[pl], off, 0, 0));
       }
     }
 #pragma unroll
@@ -263,15 +239,8 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
       if (UNITS % NT == 0 || u < UNITS) {
         const int f = u / GI::UNITS;
         const int a = GI::fill(f, u - f * GI::UNITS);
-        if constexpr (ImgUnit<GI>::WIDEN) {  // 8 uint8 values -> 8 exact bf16, stored once
-          const UT w = v[j][0];
-          *reinterpret_cast<u32x4*>(smem + a) =
-              u32x4{u8pair_bf16(w[0], 0), u8pair_bf16(w[0], 2), u8pair_bf16(w[1], 0),
-                    u8pair_bf16(w[1], 2)};
-        } else {
 #pragma unroll
-          for (int pl = 0; pl < NPA; ++pl) *reinterpret_cast<UT*>(smem + pl * PLANE + a) = v[j][pl];
-        }
+        for (int pl = 0; pl < NPA; ++pl) *reinterpret_cast<UT*>(smem + pl * PLANE + a) = v[j][pl];
       }
     }
     if (tid < NPA) *reinterpret_cast<u32x4*>(smem + tid * PLANE + PLANE - 16) = zero_u4();
@@ -313,15 +282,9 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
         const int u = GI::unit(sg[i], ln[i], k0, s, lane >> 5);
         const int a = u >= 0 ? u : PLANE - 16;
         bf16x8 fa[NPA];
-        if constexpr (ImgUnit<GI>::U8) {  // 8 uint8 values -> 8 exact bf16 (gemm_p3.h kAU8)
-          const u32x2 w = *reinterpret_cast<const u32x2*>(smem + a);
-          fa[0] = __builtin_bit_cast(bf16x8, u32x4{u8pair_bf16(w[0], 0), u8pair_bf16(w[0], 2),
-                                                   u8pair_bf16(w[1], 0), u8pair_bf16(w[1], 2)});
-        } else {
 #pragma unroll
-          for (int pl = 0; pl < NPA; ++pl)
-            fa[pl] = *reinterpret_cast<const bf16x8*>(smem + pl * PLANE + a);
-        }
+        for (int pl = 0; pl < NPA; ++pl)
+          fa[pl] = *reinterpret_cast<const bf16x8*>(smem + pl * PLANE + a);
 #pragma unroll
         for (int j = 0; j < NTL; ++j) {
           // Smallest terms first, as gemm_p3.h.

@@ -59,20 +59,17 @@ struct PActs {
   Plane x1, x2, x3;
 };
 int64_t wgrad_slab_floats_p3();
-// conv1's input: the uint8 frames themselves (u8, read by the kernels as one exact bf16
-// plane, gemm_p3.h kAU8) or their bf16 copy (launch_frames_bf16); rows of 84*84*4.
+// conv1's input: the bf16 copy of the uint8 frames (launch_frames_bf16), rows of 84*84*4.
 struct Frames {
   const void* p;
-  bool u8;
   Frames rows_from(int r) const {
-    const size_t off = (size_t)r * kObsBytes * (u8 ? 1 : 2);
-    return Frames{static_cast<const uint8_t*>(p) + off, u8};
+    return Frames{static_cast<const uint8_t*>(p) + (size_t)r * kObsBytes * 2};
   }
 };
 // frames: bf16 copies of the uint8 frames [rows][84*84*4] (launch_frames_bf16).
 // keep_x1: frames [0, keep_x1) get their conv1 output x1 in HBM (the backward reads it);
-// -1: all.  With the fused conv1 -> conv2 kernel (ACME_V_C12=1) the other frames' x1 only
-// lives in LDS.
+// -1: all.  With the fused conv1 -> conv2 kernel (gemm_p3c12.h, used when
+// keep_x1 == 0) x1 only lives in LDS.
 int forward_p3(const PWeights& w, const Frames& frames, int rows, const PActs& a,
                hipStream_t st, int keep_x1 = -1);
 // Optional second stream for the weight gradients: conv3 / conv2 weight gradients run on

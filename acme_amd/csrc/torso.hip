@@ -10,11 +10,9 @@
 #include "conv_p3.h"
 #include "gemm.h"
 #include "gemm_p3.h"
-#include "gemm_p3d.h"
 #include "gemm_p3i.h"
 #include "gemm_p3s.h"
 #include "gemm_p3c12.h"
-#include "gemm_p3w.h"
 #include "gemm_x6.h"
 #include "kernels.h"
 #include "profiler.h"
@@ -139,14 +137,9 @@ int backward(const Weights& w, const Grads& g, bool u8, const void* obs, int row
 // ---------------------------------------------------------------- plane path
 namespace {
 
-// Weight-gradient K splits (defaults; ACME_V_P3C<i>WS overrides up to the cap that sizes the
-// slab).
+// Weight-gradient K splits; kP3MaxWgradSplits sizes the slab.
 constexpr int kP3Conv1WgradSplits = 512, kP3Conv2WgradSplits = 128, kP3Conv3WgradSplits = 128;
 constexpr int kP3MaxWgradSplits = 512;
-int wsplits(const char* key, int def) {
-  const int v = tune_variant(key);
-  return v > 0 && v <= kP3MaxWgradSplits ? v : def;
-}
 
 #define P3_GEMM_F(name, flops, BM, BN, WM, WN, BK, prob, splits)                             \
   do {                                                                                        \
@@ -157,49 +150,12 @@ int wsplits(const char* key, int def) {
       return ACME_ERR_HIP;                                                                    \
     }                                                                                         \
   } while (0)
-#define P3G_GEMM(name, BM, BN, WM, WN, BK, ST, prob, splits)                                 \
-  do {                                                                                        \
-    ACME_PROF_PEAK(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0, \
-                   gemm::p3_peak_tflops<decltype(prob)>());                                   \
-    hipError_t _e = gemm::launch_gemm_p3g<BM, BN, WM, WN, BK, ST>(prob, splits, st);         \
-    if (_e != hipSuccess) {                                                                   \
-      set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
-      return ACME_ERR_HIP;                                                                    \
-    }                                                                                         \
-  } while (0)
-#define P3D_GEMM_F(name, flops, BN, MT, NW, BK, prob, z)                                     \
-  do {                                                                                        \
-    ACME_PROF_PEAK(name, st, flops, 0.0, gemm::p3_peak_tflops<decltype(prob)>());             \
-    hipError_t _e = gemm::launch_gemm_p3d<BN, MT, NW, BK>(prob, z, st);                       \
-    if (_e != hipSuccess) {                                                                   \
-      set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
-      return ACME_ERR_HIP;                                                                    \
-    }                                                                                         \
-  } while (0)
-#define P3D_GEMM(name, BN, MT, NW, BK, prob)                                                 \
-  P3D_GEMM_F(name, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, BN, MT, NW, \
-             BK, prob, 1)
-#define P3P_GEMM_F(name, flops, BM, BN, WM, WN, prob, splits)                                \
-  do {                                                                                        \
-    ACME_PROF_PEAK(name, st, flops, 0.0, gemm::p3_peak_tflops<decltype(prob)>());             \
-    hipError_t _e = gemm::launch_gemm_p3p<BM, BN, WM, WN>(prob, splits, st);                  \
-    if (_e != hipSuccess) {                                                                   \
-      set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
-      return ACME_ERR_HIP;                                                                    \
-    }                                                                                         \
-  } while (0)
-#define P3P_GEMM(name, BM, BN, WM, WN, prob, splits)                                         \
-  P3P_GEMM_F(name, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, BM, BN, WM, \
-             WN, prob, splits)
 #define P3_GEMM(name, BM, BN, WM, WN, BK, prob, splits)                                      \
   P3_GEMM_F(name, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, BM, BN, WM, \
             WN, BK, prob, splits)
 // Image-resident convolution (gemm_p3i.h): FPB frames per block, WM x WN waves of 32*MT
 // rows; `frames` images.
 using I1F = gemm::ImgGeomPairs<G1>;
-using I1U = gemm::ImgGeomPairs<G1, 1>;
-using I1W = gemm::ImgGeomPairs<G1, 2>;
-using I2F = gemm::ImgGeom<G2, false>;
 using I3F = gemm::ImgGeom<G3, false>;
 using I3D = gemm::ImgGeom<G3, true>;
 #define P3I_GEMM(name, GI, FPB, BN, WM, WN, MT, prob, frames)                                 \
@@ -221,7 +177,7 @@ inline PlaneSrc src(const Plane& x, int64_t elems) {
 }
 inline PlaneSrc frames_src(const Frames& f, int rows) {
   return PlaneSrc{static_cast<const uint16_t*>(f.p), 0,
-                  (int32_t)((f.u8 ? 1 : 2) * (int64_t)rows * G1::IPIX * G1::CI)};
+                  (int32_t)(2 * (int64_t)rows * G1::IPIX * G1::CI)};
 }
 
 template <class P>
@@ -243,12 +199,10 @@ int64_t wgrad_slab_floats_p3() {
 int forward_p3(const PWeights& w, const Frames& frames, int rows, const PActs& a,
                hipStream_t st, int keep_x1) {
   // Fused conv1 -> conv2 (gemm_p3c12.h; 81 us vs 34.8 + 50.3 us alone, but one 150-KB
-  // block per CU shares the GPU badly with the other stream).  ACME_V_C12: default the target
-  // forward (keep_x1 == 0, on the side stream) only, measured 0.716 -> 0.713 ms per step;
-  // 1 every forward (0.726 -> 0.733); 2 the online forward only (0.716 -> 0.725); 4 off.
-  const int c12 = tune_variant("C12");
-  const bool fused = !frames.u8 && (c12 == 1 || (c12 == 2 && keep_x1 != 0) ||
-                                    ((c12 == 0 || c12 == 3) && keep_x1 == 0));
+  // block per CU shares the GPU badly with the other stream): the target forward only
+  // (keep_x1 == 0, on the side stream), measured 0.716 -> 0.713 ms per step; fusing every
+  // forward measured 0.733, the online forward only 0.725.
+  const bool fused = keep_x1 == 0;
   if (fused) {
     P3ConvFwd<G1, 1> p1;
     p1.M = rows * G1::OPIX; p1.N = G1::CO; p1.K = G1::K; p1.k_chunk = G1::K;
@@ -262,92 +216,29 @@ int forward_p3(const PWeights& w, const Frames& frames, int rows, const PActs& a
     ACME_PROF_PEAK("conv12_fwd", st, fl, 0.0, gemm::p3_peak_tflops<decltype(p2)>());
     hipError_t e = gemm::launch_gemm_p3c12(p1, p2, rows, keep_x1 < 0 ? rows : keep_x1, st);
     if (e != hipSuccess) return (set_error("gemm launch failed: %s", hipGetErrorString(e)), ACME_ERR_HIP);
-  } else if (frames.u8) {  // conv1 straight from the uint8 frames
-    P3ConvFwd<G1, 1, true> p;
-    p.M = rows * G1::OPIX; p.N = G1::CO; p.K = G1::K; p.k_chunk = G1::K;
-    p.a_src = frames_src(frames, rows); p.b_src = src(w.w1, G1::K * G1::CO);
-    p.bias = w.b1; p.y = pl(a.x1);
-    switch (tune_variant("P3C1U")) {
-      case 7: P3D_GEMM("conv1_fwd", 32, 2, 4, 32, p); break;  // direct A from HBM
-      case 14: P3I_GEMM("conv1_fwd", I1U, 1, 32, 14, 1, 1, p, rows); break;
-      case 15: P3I_GEMM("conv1_fwd", I1U, 1, 32, 7, 1, 2, p, rows); break;  // uint8 in LDS
-      // Image-resident frames: uint8 from HBM, widened to bf16 once while filling the LDS.
-      default: P3I_GEMM("conv1_fwd", I1W, 1, 32, 7, 1, 2, p, rows); break;
-    }
   } else {
     P3ConvFwd<G1, 1> p;
     p.M = rows * G1::OPIX; p.N = G1::CO; p.K = G1::K; p.k_chunk = G1::K;
     p.a_src = frames_src(frames, rows); p.b_src = src(w.w1, G1::K * G1::CO);
     p.bias = w.b1; p.y = pl(a.x1);
-    switch (tune_variant("P3C1F")) {
-      case 1: P3_GEMM("conv1_fwd", 128, 32, 4, 1, 32, p, 1); break;
-      case 2: P3_GEMM("conv1_fwd", 256, 32, 4, 1, 32, p, 1); break;
-      case 3: P3G_GEMM("conv1_fwd", 256, 32, 4, 1, 16, 3, p, 1); break;
-      case 4: P3G_GEMM("conv1_fwd", 256, 32, 4, 1, 32, 3, p, 1); break;
-      case 5: P3_GEMM("conv1_fwd", 512, 32, 4, 1, 16, p, 1); break;
-      case 6: P3_GEMM("conv1_fwd", 512, 32, 4, 1, 32, p, 1); break;
-      case 7: P3D_GEMM("conv1_fwd", 32, 2, 4, 32, p); break;
-      case 8: P3D_GEMM("conv1_fwd", 32, 4, 4, 32, p); break;
-      case 9: P3D_GEMM("conv1_fwd", 32, 1, 4, 32, p); break;
-      case 10: P3P_GEMM("conv1_fwd", 256, 32, 4, 1, p, 1); break;
-      case 11: P3P_GEMM("conv1_fwd", 128, 32, 4, 1, p, 1); break;
-      case 12: P3_GEMM("conv1_fwd", 256, 32, 4, 1, 16, p, 1); break;
-      case 13: P3I_GEMM("conv1_fwd", I1F, 1, 32, 7, 1, 2, p, rows); break;
-      case 14: P3I_GEMM("conv1_fwd", I1F, 1, 32, 14, 1, 1, p, rows); break;
-      case 15: P3I_GEMM("conv1_fwd", I1F, 1, 32, 4, 1, 4, p, rows); break;
-      case 16: P3I_GEMM("conv1_fwd", I1F, 2, 32, 14, 1, 2, p, rows); break;
-      // Image-resident frames (gemm_p3i.h pixel pairs): 39.6 -> 33.7 us vs direct A (case 7).
-      default: P3I_GEMM("conv1_fwd", I1F, 1, 32, 7, 1, 2, p, rows); break;
-    }
+    // Image-resident frames (gemm_p3i.h pixel pairs): 39.6 -> 33.7 us vs the best im2col
+    // tiling.
+    P3I_GEMM("conv1_fwd", I1F, 1, 32, 7, 1, 2, p, rows);
   }
   if (!fused) {
     P3ConvFwd<G2, 3> p;
     p.M = rows * G2::OPIX; p.N = G2::CO; p.K = G2::K; p.k_chunk = G2::K;
     p.a_src = src(a.x1, (int64_t)rows * kX1); p.b_src = src(w.w2, G2::K * G2::CO);
     p.bias = w.b2; p.y = pl(a.x2);
-    switch (tune_variant("P3C2F")) {
-      case 1: P3_GEMM("conv2_fwd", 128, 64, 2, 2, 16, p, 1); break;
-      case 2: P3_GEMM("conv2_fwd", 256, 64, 4, 1, 32, p, 1); break;
-      case 3: P3G_GEMM("conv2_fwd", 128, 64, 2, 2, 32, 3, p, 1); break;
-      case 4: P3G_GEMM("conv2_fwd", 128, 64, 2, 2, 16, 4, p, 1); break;
-      case 5: P3D_GEMM("conv2_fwd", 64, 2, 4, 32, p); break;
-      case 6: P3D_GEMM("conv2_fwd", 64, 1, 4, 32, p); break;
-      case 7: P3D_GEMM("conv2_fwd", 64, 4, 4, 32, p); break;
-      case 8: P3D_GEMM("conv2_fwd", 64, 2, 2, 32, p); break;
-      case 9: P3P_GEMM("conv2_fwd", 128, 64, 2, 2, p, 1); break;
-      case 10: P3P_GEMM("conv2_fwd", 256, 64, 4, 1, p, 1); break;
-      case 11: P3P_GEMM("conv2_fwd", 128, 64, 4, 1, p, 1); break;
-      case 12: P3I_GEMM("conv2_fwd", I2F, 1, 64, 4, 1, 1, p, rows); break;
-      case 13: P3I_GEMM("conv2_fwd", I2F, 1, 64, 4, 2, 1, p, rows); break;
-      default: P3_GEMM("conv2_fwd", 128, 64, 2, 2, 32, p, 1); break;
-    }
+    P3_GEMM("conv2_fwd", 128, 64, 2, 2, 32, p, 1);
   }
   {
     P3ConvFwd<G3, 3> p;
     p.M = rows * G3::OPIX; p.N = G3::CO; p.K = G3::K; p.k_chunk = G3::K;
     p.a_src = src(a.x2, (int64_t)rows * kFlat); p.b_src = src(w.w3, G3::K * G3::CO);
     p.bias = w.b3; p.y = pl(a.x3);
-    switch (tune_variant("P3C3F")) {
-      case 1: P3_GEMM("conv3_fwd", 128, 64, 2, 2, 16, p, 1); break;
-      case 2: P3_GEMM("conv3_fwd", 256, 64, 4, 1, 32, p, 1); break;
-      case 3: P3G_GEMM("conv3_fwd", 128, 64, 2, 2, 32, 3, p, 1); break;
-      case 4: P3G_GEMM("conv3_fwd", 128, 64, 2, 2, 16, 4, p, 1); break;
-      case 5: P3D_GEMM("conv3_fwd", 64, 2, 4, 32, p); break;
-      case 6: P3D_GEMM("conv3_fwd", 64, 1, 4, 32, p); break;
-      case 7: P3D_GEMM("conv3_fwd", 64, 4, 4, 32, p); break;
-      case 8: P3D_GEMM("conv3_fwd", 64, 2, 2, 32, p); break;
-      case 9: P3P_GEMM("conv3_fwd", 128, 64, 2, 2, p, 1); break;
-      case 10: P3P_GEMM("conv3_fwd", 256, 64, 4, 1, p, 1); break;
-      case 11: P3P_GEMM("conv3_fwd", 128, 64, 4, 1, p, 1); break;
-      case 12: P3I_GEMM("conv3_fwd", I3F, 1, 64, 4, 1, 1, p, rows); break;
-      case 13: P3I_GEMM("conv3_fwd", I3F, 2, 64, 8, 1, 1, p, rows); break;
-      case 14: P3I_GEMM("conv3_fwd", I3F, 1, 64, 4, 2, 1, p, rows); break;
-      case 15: P3I_GEMM("conv3_fwd", I3F, 2, 64, 4, 1, 2, p, rows); break;
-      case 16: P3_GEMM("conv3_fwd", 128, 64, 2, 2, 32, p, 1); break;
-      case 17: P3I_GEMM("conv3_fwd", I3F, 2, 64, 8, 2, 1, p, rows); break;
-      // Image-resident, 4 x 2 waves (measured 50.1 -> 43.5 us vs the 128x64 im2col engine).
-      default: P3I_GEMM("conv3_fwd", I3F, 1, 64, 4, 2, 1, p, rows); break;
-    }
+    // Image-resident, 4 x 2 waves (measured 50.1 -> 43.5 us vs the 128x64 im2col engine).
+    P3I_GEMM("conv3_fwd", I3F, 1, 64, 4, 2, 1, p, rows);
   }
   return ACME_OK;
 }
@@ -357,41 +248,26 @@ int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int row
                 hipStream_t st_main, const Side& sd) {
   int rc;
   // Weight gradients of conv3 and conv2 go to the side stream (when given): each only
-  // waits for its layer's dZ, and runs beside the next input gradient on the main stream.
+  // waits for its layer's dZ, and runs beside the next input gradient on the main stream
+  // (two forks; one fork after conv3_dgrad saved an event record but measured 0.754 ->
+  // 0.767 ms per step: the lost overlap costs more).
   const bool fork = sd.side != nullptr;
-  // Two forks (default): conv3_wgrad beside conv3_dgrad, conv2_wgrad beside conv2_dgrad.
-  // ACME_V_BWF=1: one fork after conv3_dgrad (both weight gradients beside conv2_dgrad +
-  // conv1_wgrad) saves an event record on the main stream (~7 us of main-stream idle each,
-  // rocprofv3 trace) but measured 0.754 -> 0.767 ms per step: the lost overlap costs more.
-  const bool two_forks = fork && tune_variant("BWF") != 1;
   hipStream_t st = fork ? sd.side : st_main;
   float* wslab = fork ? sd.slab : slab;
-  auto conv3_wgrad = [&](hipStream_t st) -> int {  // conv3 weight + bias gradient
+  {  // conv3 weight + bias gradient
+    if (fork) {
+      ACME_HIP_TRY(hipEventRecord(sd.e[0], st_main));
+      ACME_HIP_TRY(hipStreamWaitEvent(sd.side, sd.e[0], 0));
+    }
     P3ConvWgrad<G3, 3> p;
     p.M = G3::K; p.N = G3::CO; p.K = rows * G3::OPIX;
-    const int splits = wsplits("P3C3WS", kP3Conv3WgradSplits);
+    const int splits = kP3Conv3WgradSplits;
     p.k_chunk = chunk_for(p.K, splits);
     p.a_src = src(a.x2, (int64_t)rows * kFlat); p.b_src = src(dz3, (int64_t)rows * kFlat);
     p.slab = wslab;
-    if (tune_variant("P3C3W") == 12) {  // image-resident, one wave per tap (gemm_p3w.h)
-      const int fs = (rows + 1) / 2;
-      ACME_PROF_PEAK("conv3_wgrad", st, 2.0 * (double)p.M * (double)p.N * (double)p.K, 0.0,
-                     gemm::p3_peak_tflops<decltype(p)>());
-      hipError_t e = gemm::launch_gemm_p3w<G3, 2>(p, rows, st);
-      if (e != hipSuccess) return (set_error("gemm launch failed: %s", hipGetErrorString(e)), ACME_ERR_HIP);
-      return p3_wgrad_reduce(p, fs, wslab, g.w3, g.b3, "conv3_wgrad_reduce", st);
-    }
-    if (tune_variant("P3C3W") == 9) P3P_GEMM("conv3_wgrad", 128, 64, 2, 2, p, splits);
-    else if (tune_variant("P3C3W") == 1) P3G_GEMM("conv3_wgrad", 128, 64, 2, 2, 32, 3, p, splits);
-    else P3_GEMM("conv3_wgrad", 128, 64, 2, 2, 32, p, splits);
-    return p3_wgrad_reduce(p, splits, wslab, g.w3, g.b3, "conv3_wgrad_reduce", st);
-  };
-  if (two_forks) {
-    ACME_HIP_TRY(hipEventRecord(sd.e[0], st_main));
-    ACME_HIP_TRY(hipStreamWaitEvent(sd.side, sd.e[0], 0));
-    if ((rc = conv3_wgrad(sd.side))) return rc;
-  } else if (!fork) {
-    if ((rc = conv3_wgrad(st_main))) return rc;
+    P3_GEMM("conv3_wgrad", 128, 64, 2, 2, 32, p, splits);
+    if ((rc = p3_wgrad_reduce(p, splits, wslab, g.w3, g.b3, "conv3_wgrad_reduce", st)))
+      return rc;
   }
   st = st_main;
   {
@@ -399,39 +275,22 @@ int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int row
     p.M = rows * G3::IPIX; p.N = G3::CI; p.K = G3::KH * G3::KW * G3::CO; p.k_chunk = p.K;
     p.a_src = src(dz3, (int64_t)rows * kFlat); p.b_src = src(w.w3, G3::K * G3::CO);
     p.xprev = cp(a.x2); p.dx = pl(dz2);
-    switch (tune_variant("P3C3D")) {
-      case 1: P3_GEMM("conv3_dgrad", 128, 64, 2, 2, 16, p, 1); break;
-      case 2: P3_GEMM("conv3_dgrad", 256, 64, 4, 1, 32, p, 1); break;
-      case 3: P3G_GEMM("conv3_dgrad", 128, 64, 2, 2, 32, 3, p, 1); break;
-      case 4: P3D_GEMM("conv3_dgrad", 64, 2, 4, 32, p); break;
-      case 5: P3D_GEMM("conv3_dgrad", 64, 1, 4, 32, p); break;
-      case 9: P3P_GEMM("conv3_dgrad", 128, 64, 2, 2, p, 1); break;
-      case 10: P3P_GEMM("conv3_dgrad", 256, 64, 4, 1, p, 1); break;
-      case 12: P3I_GEMM("conv3_dgrad", I3D, 1, 64, 4, 1, 1, p, rows); break;
-      case 13: P3I_GEMM("conv3_dgrad", I3D, 2, 64, 8, 1, 1, p, rows); break;
-      case 14: P3I_GEMM("conv3_dgrad", I3D, 1, 64, 4, 2, 1, p, rows); break;
-      case 16: P3_GEMM("conv3_dgrad", 128, 64, 2, 2, 32, p, 1); break;
-      // Image-resident dZ, two frames x 8 x 2 waves: 37.4 us (case 16) -> 32.6 (case 12) ->
-      // 31.2 us.
-      default: P3I_GEMM("conv3_dgrad", I3D, 2, 64, 8, 2, 1, p, rows); break;
-    }
+    // Image-resident dZ, two frames x 8 x 2 waves: 37.4 us (128x64 im2col) -> 31.2 us.
+    P3I_GEMM("conv3_dgrad", I3D, 2, 64, 8, 2, 1, p, rows);
   }
   if (fork) {
     ACME_HIP_TRY(hipEventRecord(sd.e[1], st_main));
     ACME_HIP_TRY(hipStreamWaitEvent(sd.side, sd.e[1], 0));
     st = sd.side;
-    if (!two_forks && (rc = conv3_wgrad(sd.side))) return rc;
   }
   {  // conv2
     P3ConvWgrad<G2, 3> p;
     p.M = G2::K; p.N = G2::CO; p.K = rows * G2::OPIX;
-    const int splits = wsplits("P3C2WS", kP3Conv2WgradSplits);
+    const int splits = kP3Conv2WgradSplits;
     p.k_chunk = chunk_for(p.K, splits);
     p.a_src = src(a.x1, (int64_t)rows * kX1); p.b_src = src(dz2, (int64_t)rows * kFlat);
     p.slab = wslab;
-    if (tune_variant("P3C2W") == 9) P3P_GEMM("conv2_wgrad", 128, 64, 2, 2, p, splits);
-    else if (tune_variant("P3C2W") == 1) P3G_GEMM("conv2_wgrad", 128, 64, 2, 2, 32, 3, p, splits);
-    else P3_GEMM("conv2_wgrad", 128, 64, 2, 2, 32, p, splits);
+    P3_GEMM("conv2_wgrad", 128, 64, 2, 2, 32, p, splits);
     if ((rc = p3_wgrad_reduce(p, splits, wslab, g.w2, g.b2, "conv2_wgrad_reduce", st)))
       return rc;
     if (fork) ACME_HIP_TRY(hipEventRecord(sd.e[2], sd.side));
@@ -443,68 +302,21 @@ int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int row
     p.k_chunk = p.K; p.batch = rows;
     p.a_src = src(dz2, (int64_t)rows * kFlat); p.b_src = src(w.w2, G2::K * G2::CO);
     p.xprev = cp(a.x1); p.dx = pl(dz1);
+    // Image-resident dZ, two frames x four classes per block (16 waves, gemm_p3s.h):
+    // 57.7 us (128x32 im2col) -> 38.0 (one frame per block) -> 34.7 us.
     const double fl = 2.0 * rows * G2::IPIX * G2::CI * (double)p.K;
-    switch (tune_variant("P3C2D")) {
-      case 1: P3_GEMM_F("conv2_dgrad", fl, 256, 32, 4, 1, 32, p, G2::S * G2::S); break;
-      case 2: P3_GEMM_F("conv2_dgrad", fl, 256, 32, 4, 1, 16, p, G2::S * G2::S); break;
-      case 4: P3_GEMM_F("conv2_dgrad", fl, 512, 32, 4, 1, 16, p, G2::S * G2::S); break;
-      case 5: P3_GEMM_F("conv2_dgrad", fl, 256, 32, 2, 1, 32, p, G2::S * G2::S); break;
-      case 6: P3D_GEMM_F("conv2_dgrad", fl, 32, 2, 4, 32, p, G2::S * G2::S); break;
-      case 7: P3D_GEMM_F("conv2_dgrad", fl, 32, 4, 4, 32, p, G2::S * G2::S); break;
-      case 8: P3D_GEMM_F("conv2_dgrad", fl, 32, 1, 4, 32, p, G2::S * G2::S); break;
-      case 9: P3P_GEMM_F("conv2_dgrad", fl, 128, 32, 4, 1, p, G2::S * G2::S); break;
-      case 10: P3P_GEMM_F("conv2_dgrad", fl, 256, 32, 4, 1, p, G2::S * G2::S); break;
-      case 12: {  // image-resident dZ, two frames per block (16 waves)
-        ACME_PROF_PEAK("conv2_dgrad", st, fl, 0.0, gemm::p3_peak_tflops<decltype(p)>());
-        hipError_t e = gemm::launch_gemm_p3s<G2, 2>(p, rows, st);
-        if (e != hipSuccess) return (set_error("gemm launch failed: %s", hipGetErrorString(e)), ACME_ERR_HIP);
-        break;
-      }
-      case 11: {  // image-resident dZ, four classes per block (gemm_p3s.h)
-        ACME_PROF_PEAK("conv2_dgrad", st, fl, 0.0, gemm::p3_peak_tflops<decltype(p)>());
-        hipError_t e = gemm::launch_gemm_p3s<G2>(p, rows, st);
-        if (e != hipSuccess) return (set_error("gemm launch failed: %s", hipGetErrorString(e)), ACME_ERR_HIP);
-        break;
-      }
-      case 3: {
-        ACME_PROF_PEAK("conv2_dgrad", st, fl, 0.0, gemm::p3_peak_tflops<decltype(p)>());
-        hipError_t e = gemm::launch_gemm_p3g<128, 32, 4, 1, 32, 3>(p, G2::S * G2::S, st);
-        if (e != hipSuccess) return (set_error("gemm launch failed: %s", hipGetErrorString(e)), ACME_ERR_HIP);
-        break;
-      }
-      case 16: P3_GEMM_F("conv2_dgrad", fl, 128, 32, 4, 1, 32, p, G2::S * G2::S); break;
-      default: {  // image-resident dZ, two frames x four classes per block (16 waves):
-                  // 57.7 us (case 16) -> 38.0 (case 11, one frame) -> 34.7 us
-        ACME_PROF_PEAK("conv2_dgrad", st, fl, 0.0, gemm::p3_peak_tflops<decltype(p)>());
-        hipError_t e = gemm::launch_gemm_p3s<G2, 2>(p, rows, st);
-        if (e != hipSuccess) return (set_error("gemm launch failed: %s", hipGetErrorString(e)), ACME_ERR_HIP);
-        break;
-      }
-    }
+    ACME_PROF_PEAK("conv2_dgrad", st, fl, 0.0, gemm::p3_peak_tflops<decltype(p)>());
+    hipError_t e = gemm::launch_gemm_p3s<G2, 2>(p, rows, st);
+    if (e != hipSuccess) return (set_error("gemm launch failed: %s", hipGetErrorString(e)), ACME_ERR_HIP);
   }
-  if (frames.u8) {  // conv1 (no input gradient), straight from the uint8 frames
-    P3ConvWgrad<G1, 1, true> p;
+  {  // conv1 (no input gradient)
+    P3ConvWgrad<G1, 1> p;
     p.M = G1::K; p.N = G1::CO; p.K = rows * G1::OPIX;
-    const int splits = wsplits("P3C1WS", kP3Conv1WgradSplits);
+    const int splits = kP3Conv1WgradSplits;
     p.k_chunk = chunk_for(p.K, splits);
     p.a_src = frames_src(frames, rows); p.b_src = src(dz1, (int64_t)rows * kX1);
     p.slab = slab;
     P3_GEMM("conv1_wgrad", 256, 32, 4, 1, 32, p, splits);
-    if ((rc = p3_wgrad_reduce(p, splits, slab, g.w1, g.b1, "conv1_wgrad_reduce", st)))
-      return rc;
-  } else {  // conv1 (no input gradient)
-    P3ConvWgrad<G1, 1> p;
-    p.M = G1::K; p.N = G1::CO; p.K = rows * G1::OPIX;
-    const int splits = wsplits("P3C1WS", kP3Conv1WgradSplits);
-    p.k_chunk = chunk_for(p.K, splits);
-    p.a_src = frames_src(frames, rows); p.b_src = src(dz1, (int64_t)rows * kX1);
-    p.slab = slab;
-    switch (tune_variant("P3C1W")) {
-      case 1: P3G_GEMM("conv1_wgrad", 256, 32, 4, 1, 32, 3, p, splits); break;
-      case 2: P3_GEMM("conv1_wgrad", 256, 32, 2, 1, 32, p, splits); break;
-      case 9: P3P_GEMM("conv1_wgrad", 256, 32, 4, 1, p, splits); break;
-      default: P3_GEMM("conv1_wgrad", 256, 32, 4, 1, 32, p, splits); break;
-    }
     if ((rc = p3_wgrad_reduce(p, splits, slab, g.w1, g.b1, "conv1_wgrad_reduce", st)))
       return rc;
   }
