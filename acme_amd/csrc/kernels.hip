@@ -400,6 +400,93 @@ __global__ void __launch_bounds__(256) fc_head_forward_kernel(
   }
 }
 
+// The same for the Nature head (2H = 1024 hidden units, compile-time A): thread t owns hidden
+// columns [4t, 4t + 4) of the block's R rows, so the split-K sum, bias and ReLU land in its
+// registers and the row's dot products start from them (t < 128: the value half against
+// wv; t >= 128: the advantage half against its 4 rows of wa, A float4 loads issued with the
+// slab loads).  Per-thread partials go through LDS and each output is summed by one wave in
+// a fixed order (lane pairs, then a shuffle tree), so the result is deterministic.  One
+// wait for every global load of the block; R = 2 rows per block puts two blocks on most CUs.
+template <int SPL, int A, int R>
+__global__ void __launch_bounds__(256) fc_head1024_kernel(
+    const float* __restrict__ slab, int rows, const float* __restrict__ fcb,
+    const float* __restrict__ wv, const float* __restrict__ bv, const float* __restrict__ wa,
+    const float* __restrict__ ba, float* __restrict__ hid, float* __restrict__ q) {
+  constexpr int N4 = 256, HALF = 128;
+  __shared__ float part[R][A + 1][HALF];
+  __shared__ float dots[R][A + 1];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int r0 = blockIdx.x * R;
+  const int64_t count4 = (int64_t)rows * N4;
+  const f32x4* s4 = reinterpret_cast<const f32x4*>(slab);
+  f32x4 sp[R][SPL];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int row = r0 + r < rows ? r0 + r : rows - 1;  // a clamped duplicate, never stored
+    const int64_t e = (int64_t)row * N4 + t;
+#pragma unroll
+    for (int k = 0; k < SPL; ++k) sp[r][k] = s4[(size_t)k * count4 + e];
+  }
+  const bool adv = t >= HALF;
+  const int c = adv ? t - HALF : t;  // this thread's 4 hidden units within its half
+  f32x4 w[A];
+  if (adv) {
+    const f32x4* wa4 = reinterpret_cast<const f32x4*>(wa) + (size_t)c * A;  // wa rows 4c .. 4c+3
+#pragma unroll
+    for (int i = 0; i < A; ++i) w[i] = wa4[i];
+  } else {
+    w[0] = reinterpret_cast<const f32x4*>(wv)[c];
+  }
+  const f32x4 b = reinterpret_cast<const f32x4*>(fcb)[t];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    f32x4 v = sp[r][0];
+#pragma unroll
+    for (int k = 1; k < SPL; ++k) v += sp[r][k];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const float x = v[jj] + b[jj];
+      v[jj] = x > 0.f ? x : 0.f;
+    }
+    if (r0 + r < rows) reinterpret_cast<f32x4*>(hid)[(int64_t)(r0 + r) * N4 + t] = v;
+    if (adv) {
+      const float* wf = reinterpret_cast<const float*>(w);  // [4][A], compile-time indices
+#pragma unroll
+      for (int o = 0; o < A; ++o) {
+        float acc = v[0] * wf[o];
+        acc = fmaf(v[1], wf[A + o], acc);
+        acc = fmaf(v[2], wf[2 * A + o], acc);
+        acc = fmaf(v[3], wf[3 * A + o], acc);
+        part[r][o][c] = acc;
+      }
+    } else {
+      float acc = v[0] * w[0][0];
+      acc = fmaf(v[1], w[0][1], acc);
+      acc = fmaf(v[2], w[0][2], acc);
+      acc = fmaf(v[3], w[0][3], acc);
+      part[r][A][c] = acc;
+    }
+  }
+  __syncthreads();
+  for (int j = wave; j < R * (A + 1); j += 4) {
+    const int r = j / (A + 1), o = j - r * (A + 1);
+    float x = part[r][o][2 * lane] + part[r][o][2 * lane + 1];
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d, 64);
+    if (lane == 0) dots[r][o] = x + (o == A ? bv[0] : ba[o]);
+  }
+  __syncthreads();
+  if (t < R * A) {
+    const int r = t / A, jj = t - r * A, row = r0 + r;
+    if (row < rows) {
+      float mean = 0.f;
+      for (int k = 0; k < A; ++k) mean += dots[r][k];
+      mean /= (float)A;
+      q[(size_t)row * A + jj] = dots[r][A] + (dots[r][jj] - mean);
+    }
+  }
+}
+
 // Loss + head dZ in one launch (plane path).  Blocks [0, nb) each write the dZ planes of
 // 256 / (2H / 8) rows (8 units per thread, as head_dz_planes_kernel), recomputing g_b of
 // their rows with loss_row (the loss kernel's bits); the last block is the loss kernel
@@ -781,8 +868,19 @@ int launch_fc_head_forward(const float* slab, int splits, int rows, int H, const
       sizeof(float) * (kHeadRows * 2 * H + (size_t)H * A + H + kHeadRows * (A + 1) +
                        4 * kHeadChunk * 64 + 4);
   ACME_CHECK_ARG(shmem <= 65536, "head too large for the fused head kernel");
+  const bool wa16 = reinterpret_cast<uintptr_t>(wa) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(wv) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(fcb) % 16 == 0;
+  if (H == 512 && A == 18 && wa16 && (splits == 4 || splits == 8) && tune_variant("HEAD") != 1) {
+    const unsigned g2 = (unsigned)ceil_div(rows, 2);
+    if (splits == 8)
+      fc_head1024_kernel<8, 18, 2><<<g2, 256, 0, st>>>(slab, rows, fcb, wv, bv, wa, ba, hid, q);
+    else
+      fc_head1024_kernel<4, 18, 2><<<g2, 256, 0, st>>>(slab, rows, fcb, wv, bv, wa, ba, hid, q);
+    ACME_LAUNCH_CHECK();
+    return ACME_OK;
+  }
   const unsigned grid = (unsigned)ceil_div(rows, kHeadRows);
-  const bool wa16 = reinterpret_cast<uintptr_t>(wa) % 16 == 0;
   if (H == 512 && wa16 && splits == 8)
     fc_head_forward_kernel<8, 512><<<grid, 256, shmem, st>>>(slab, splits, rows, H, fcb, wv, bv, wa,
                                                               ba, A, hid, q);

@@ -88,13 +88,15 @@ def _relu_masks(d, net, batch, params, B):
 
 NETS = {
     "nature": lambda: __import__("acme_amd.networks", fromlist=["x"]).DQNAtariNetwork(18),
+    # A != 18 takes the generic head kernel (fc_head_forward_kernel) instead of the Nature one.
+    "nature_a6": lambda: __import__("acme_amd.networks", fromlist=["x"]).DQNAtariNetwork(6),
     "cartpole_mlp": lambda: __import__("acme_amd.networks", fromlist=["x"]).MLP(4, [50, 50], 2),
     "mlp_vec": lambda: __import__("acme_amd.networks", fromlist=["x"]).MLP(24, [64, 32], 6),
 }
 
 
 @pytest.mark.parametrize("netname,B", [("nature", 1), ("nature", 4), ("nature", 37),
-                                       ("nature", 200), ("nature", 512),
+                                       ("nature", 200), ("nature", 512), ("nature_a6", 37),
                                        ("cartpole_mlp", 32), ("mlp_vec", 100)])
 def test_forward_backward_matches_oracle(netname, B):
     net = NETS[netname]()
