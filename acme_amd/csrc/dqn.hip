@@ -238,6 +238,17 @@ int tune(const char* key) { return tune_variant(key); }
     }                                                                                          \
   } while (0)
 
+// Warp-specialised plane GEMM (gemm_p3ws_kernel: producer and consumer waves).
+#define ACME_P3WS_GEMM(name, BM, BN, WM, WN, BKV, prob, splits, PIPE)                        \
+  do {                                                                                         \
+    ACME_PROF_PEAK(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0, \
+                   gemm::p3_peak_tflops<decltype(prob)>());                                    \
+    hipError_t _e = gemm::launch_gemm_p3ws<BM, BN, WM, WN, BKV, PIPE>(prob, splits, st);      \
+    if (_e != hipSuccess) {                                                                    \
+      set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
+      return ACME_ERR_HIP;                                                                     \
+    }                                                                                          \
+  } while (0)
 #define ACME_P3G_GEMM(name, BM, BN, WM, WN, BKV, ST, prob, splits)                            \
   do {                                                                                         \
     ACME_PROF_PEAK(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0, \
@@ -329,7 +340,10 @@ int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const torso:
     p.M = rows; p.N = 2 * kHidden; p.K = kFlat; p.k_chunk = chunk_for(kFlat, splits);
     p.a_src = SRC(x3, (int64_t)rows * kFlat); p.ldx = kFlat;
     p.b_src = SRC(WP(l, wpl, l->t_fcw), (int64_t)kFlat * 2 * kHidden); p.slab = slab;
-    ACME_P3_GEMM("fc_fwd", 128, 128, 2, 2, 32, p, splits);
+    // Producer / consumer waves with fragment reads one k16 step ahead (gemm_p3ws_kernel):
+    // 65.2 -> 60.5 us against the single-role kernel, the same bits.
+    if (tune("WSN") == 1) ACME_P3_GEMM("fc_fwd", 128, 128, 2, 2, 32, p, splits);  // tests
+    else ACME_P3WS_GEMM("fc_fwd", 128, 128, 2, 2, 32, p, splits, true);
     ACME_PROF("fc_head_fwd", st, 0.0, 4.0 * (double)rows * 2 * kHidden * (splits + 1));
     return launch_fc_head_forward(slab, splits, rows, kHidden, P(l, prm, l->t_fcb),
                                   P(l, prm, l->t_vw), P(l, prm, l->t_vb), P(l, prm, l->t_aw),
@@ -443,7 +457,10 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st_main,
       p.b_src = SRC(WP(l, l->wpl, l->t_fcw), (int64_t)kFlat * 2 * kHidden); p.xprev = CP(l->x3p);
       p.ldx = kFlat; p.dx = PP(l->dz3p);
       // LDS-DMA staging (gemm_p3.h P3G) measured fastest for this shape.
-      ACME_P3G_GEMM("fc_dgrad", 128, 128, 2, 2, 32, 3, p, 1);
+      // Producer / consumer waves (gemm_p3ws_kernel): 51.4 -> 47.3 us against the LDS-DMA
+      // ring, the same bits.
+      if (tune("WSN") == 1) ACME_P3G_GEMM("fc_dgrad", 128, 128, 2, 2, 32, 3, p, 1);  // tests
+      else ACME_P3WS_GEMM("fc_dgrad", 128, 128, 2, 2, 32, p, 1, true);
     }
     if (fork && join_dense) ACME_HIP_TRY(hipStreamWaitEvent(st_main, l->ev[3], 0));
     return ACME_OK;

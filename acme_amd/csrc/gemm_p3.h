@@ -319,6 +319,57 @@ struct P3Core {
     }
   }
 
+  // The two halves of mma() for one k16 step, for callers that software-pipeline the
+  // fragment reads (same terms in the same order, so the same bits).
+  using FragA = bf16x8[MT][NPA];
+  using FragB = bf16x8[NTL][NPB];
+  __device__ static __forceinline__ void read_frags(const uint8_t* sa, const uint8_t* sb, int wm,
+                                                    int wn, int s, int lane, FragA& fa,
+                                                    FragB& fb) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int pl = 0; pl < NPA; ++pl) fa[i][pl] = PA::frag(sa, pl, wm * TM + i * 32, s, lane);
+#pragma unroll
+    for (int j = 0; j < NTL; ++j)
+#pragma unroll
+      for (int pl = 0; pl < NPB; ++pl) fb[j][pl] = PB::frag(sb, pl, wn * TN + j * 32, s, lane);
+  }
+  __device__ static __forceinline__ void mfma_frags(const FragA& fa, const FragB& fb,
+                                                    f32x16 (&acc)[MT][NTL], f32x16 (&cs)[NCS],
+                                                    bool do_colsum) {
+    const bf16x8 ones{(__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f,
+                      (__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f};
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NTL; ++j) {
+        if constexpr (NPA == 3 && NPB == 3) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], acc[i][j], 0, 0, 0);
+        } else if constexpr (NPA == 3) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], acc[i][j], 0, 0, 0);
+        } else if constexpr (NPB == 3) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], acc[i][j], 0, 0, 0);
+        }
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], acc[i][j], 0, 0, 0);
+      }
+    if constexpr (kColSum) {
+      if (do_colsum) {
+#pragma unroll
+        for (int j = 0; j < NTL; ++j)
+#pragma unroll
+          for (int pl = NPB - 1; pl >= 0; --pl)
+            cs[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fb[j][pl], cs[j], 0, 0, 0);
+      }
+    }
+  }
+
   // Epilogue.  C/D map of the 32x32 MFMA: col = lane & 31, row = (v&3) + 8(v>>2) + 4h.
   // The LDS is free (every stage consumed) when this runs; it contains barriers, so all
   // waves of the block call it.
@@ -751,6 +802,192 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3g_kernel(const P p_in, in
 #endif
 }
 
+// Warp-specialised kernel: WM x WN consumer waves (fragment reads + MFMAs only, the same
+// P3Core::mma as gemm_p3_kernel, so the same bits) and as many producer waves (global ->
+// VGPR -> LDS only), two waves per SIMD, so one wave's staging instructions issue in the
+// other's MFMA gaps instead of in its own instruction stream.  Ring of 3 LDS stages and two
+// producer register sets: in iteration kt the consumers read stage kt (buffer kt % 3) while
+// the producers store stage kt + 2 (loaded two iterations earlier) into buffer (kt + 2) % 3,
+// last read in iteration kt - 1, and issue the loads of stage kt + 4; one barrier per
+// iteration.  Stages past the end load zeros into buffers that are never read.
+template <int BM, int BN, int WM, int WN, int BK, bool PIPE, class P>
+__global__ void __launch_bounds__(128 * WM * WN) gemm_p3ws_kernel(const P p_in, int n_major) {
+  using C = P3Core<BM, BN, WM, WN, BK, P>;
+  using PA = typename C::PA;
+  using PB = typename C::PB;
+  constexpr int NT = C::NT, NPA = C::NPA, NPB = C::NPB, STAGE = C::STAGE;
+  constexpr int RING = 3;
+  const BlockPlace bp = place_block<BM, BN>(p_in.M, p_in.N, n_major);
+  const P p = z_select_at(p_in, bp.z);
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+
+  const int tid = threadIdx.x;
+  const bool producer = __builtin_amdgcn_readfirstlane(tid) >= NT;
+  const int lane = tid & 63;
+  const int m0 = bp.m0, n0 = bp.n0;
+  const int split = HasZClass<P>::value ? 0 : bp.z;
+  const int kbeg = split * p.k_chunk;
+  int kend = kbeg + p.k_chunk;
+  if (kend > p.K) kend = p.K;
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+
+  if (producer) {
+    const int pt = tid - NT;
+    typename P::ARow arow[PA::PER_THREAD];
+    typename P::BRow brow[PB::PER_THREAD];
+#pragma unroll
+    for (int i = 0; i < PA::PER_THREAD; ++i)
+      arow[i] = p.a_row(m0 + (PA::owns(pt + i * NT) ? PA::row_of(pt + i * NT) : 0));
+#pragma unroll
+    for (int i = 0; i < PB::PER_THREAD; ++i)
+      brow[i] = p.b_row(n0 + (PB::owns(pt + i * NT) ? PB::row_of(pt + i * NT) : 0));
+    __amdgpu_buffer_rsrc_t srcA[NPA], srcB[NPB];
+#pragma unroll
+    for (int pl = 0; pl < NPA; ++pl) srcA[pl] = plane_rsrc(p.a_src, pl);
+#pragma unroll
+    for (int pl = 0; pl < NPB; ++pl) srcB[pl] = plane_rsrc(p.b_src, pl);
+    u32x4 ra[2][PA::PER_THREAD][NPA], rb[2][PB::PER_THREAD][NPB];
+    auto fetch = [&](auto S, int st) {
+      constexpr int set = decltype(S)::value;
+      const int k0 = kbeg + st * BK;
+#pragma unroll
+      for (int i = 0; i < PA::PER_THREAD; ++i) {
+        const int u = pt + i * NT;
+        const int kk = PA::kk_of(u);
+        const uint32_t off = (PA::owns(u) && k0 + kk < kend) ? p.a_off(arow[i], k0, kk) : kOOB;
+#pragma unroll
+        for (int pl = 0; pl < NPA; ++pl)
+          ra[set][i][pl] =
+              __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srcA[pl], off, 0, 0));
+      }
+#pragma unroll
+      for (int i = 0; i < PB::PER_THREAD; ++i) {
+        const int u = pt + i * NT;
+        const int kk = PB::kk_of(u);
+        const uint32_t off = (PB::owns(u) && k0 + kk < kend) ? p.b_off(brow[i], k0, kk) : kOOB;
+#pragma unroll
+        for (int pl = 0; pl < NPB; ++pl)
+          rb[set][i][pl] =
+              __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srcB[pl], off, 0, 0));
+      }
+    };
+    auto stash = [&](auto S, int buf) {
+      constexpr int set = decltype(S)::value;
+      uint8_t* sa = smem + buf * STAGE;
+      uint8_t* sb = sa + PA::BYTES;
+#pragma unroll
+      for (int i = 0; i < PA::PER_THREAD; ++i) {
+        const int u = pt + i * NT;
+        if (!PA::owns(u)) continue;
+#pragma unroll
+        for (int pl = 0; pl < NPA; ++pl)
+          *reinterpret_cast<u32x4*>(sa + pl * PA::PLANE + PA::offset(u)) = ra[set][i][pl];
+      }
+#pragma unroll
+      for (int i = 0; i < PB::PER_THREAD; ++i) {
+        const int u = pt + i * NT;
+        if (!PB::owns(u)) continue;
+#pragma unroll
+        for (int pl = 0; pl < NPB; ++pl)
+          *reinterpret_cast<u32x4*>(sb + pl * PB::PLANE + PB::offset(u)) = rb[set][i][pl];
+      }
+    };
+#ifndef WS_EXP
+#define WS_EXP 0  // bottleneck experiments: 1 producers idle, 2 consumers idle
+#endif
+    if constexpr (WS_EXP == 1) {
+      __syncthreads();
+      for (int kt = 0; kt < nk; ++kt) __syncthreads();
+      if constexpr (HasStore8<P>::value)
+        for (int i = 0; i < C::MT; ++i) {
+          __syncthreads();
+          __syncthreads();
+        }
+      return;
+    }
+    fetch(S0{}, 0);
+    fetch(S1{}, 1);
+    stash(S0{}, 0);
+    fetch(S0{}, 2);
+    stash(S1{}, 1);
+    fetch(S1{}, 3);
+    __syncthreads();
+    // Iteration kt: stage kt + 2 sits in set kt % 2 (loaded in iteration kt - 2, or the
+    // prologue); store it to buffer (kt + 2) % 3, then load stage kt + 4 into that set.
+    // (Three sets, loads three iterations ahead, measured the same.)
+    int wbuf = 2;
+    auto iter = [&](auto S, int kt) {
+      stash(S, wbuf);
+      fetch(S, kt + 4);
+      wbuf = wbuf == RING - 1 ? 0 : wbuf + 1;
+      __syncthreads();
+    };
+    int kt = 0;
+    for (; kt + 1 < nk; kt += 2) {
+      iter(S0{}, kt);
+      iter(S1{}, kt + 1);
+    }
+    if (kt < nk) iter(S0{}, kt);
+    // The consumers' epilogue barriers.
+    if constexpr (HasStore8<P>::value) {
+#pragma unroll
+      for (int i = 0; i < C::MT; ++i) {
+        __syncthreads();
+        __syncthreads();
+      }
+    }
+    return;
+  }
+
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  f32x16 acc[C::MT][C::NTL];
+  f32x16 cs[C::NCS];
+#pragma unroll
+  for (int i = 0; i < C::MT; ++i)
+#pragma unroll
+    for (int j = 0; j < C::NTL; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
+#pragma unroll
+  for (int j = 0; j < C::NCS; ++j)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) cs[j][v] = 0.f;
+  const bool do_colsum = C::kColSum && m0 == 0 && wm == 0;
+  __syncthreads();
+  int rbuf = 0;
+  if constexpr (WS_EXP == 2) {
+    for (int kt = 0; kt < nk; ++kt) __syncthreads();
+  } else if constexpr (PIPE && BK == 32) {
+    // Fragment reads one k16 step ahead: step 1 of stage kt is read before step 0's
+    // MFMAs, and step 0 of stage kt + 1 (published by the previous barrier) before step
+    // 1's, so no MFMA waits on the LDS latency of its own reads.
+    typename C::FragA fa0, fa1;
+    typename C::FragB fb0, fb1;
+    if (nk > 0) C::read_frags(smem, smem + PA::BYTES, wm, wn, 0, lane, fa0, fb0);
+    for (int kt = 0; kt < nk; ++kt) {
+      const uint8_t* sa = smem + rbuf * STAGE;
+      rbuf = rbuf == RING - 1 ? 0 : rbuf + 1;
+      const uint8_t* na = smem + rbuf * STAGE;
+      C::read_frags(sa, sa + PA::BYTES, wm, wn, 1, lane, fa1, fb1);
+      C::mfma_frags(fa0, fb0, acc, cs, do_colsum);
+      C::read_frags(na, na + PA::BYTES, wm, wn, 0, lane, fa0, fb0);
+      C::mfma_frags(fa1, fb1, acc, cs, do_colsum);
+      __syncthreads();
+    }
+  } else {
+    for (int kt = 0; kt < nk; ++kt) {
+      const uint8_t* sa = smem + rbuf * STAGE;
+      C::mma(sa, sa + PA::BYTES, wm, wn, lane, acc, cs, do_colsum);
+      rbuf = rbuf == RING - 1 ? 0 : rbuf + 1;
+      __syncthreads();
+    }
+  }
+  C::epilogue(p, smem, m0, n0, wave, wm, wn, lane, split, acc, cs, do_colsum);
+}
+
 // Tile order: B's panels slowest when B is the larger operand (N * planes > M * planes).
 template <class P>
 inline int p3_n_major(const P& p) {
@@ -782,6 +1019,21 @@ inline hipError_t launch_gemm_p3(const P& p, int splits, hipStream_t st) {
   const int tiles = ((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
   hipLaunchKernelGGL((gemm_p3_kernel<BM, BN, WM, WN, BK, DEEP, P>), dim3(tiles, 1, splits),
                      dim3(C::NT), LDS, st, p, p3_n_major(p));
+  return hipGetLastError();
+}
+
+// Warp-specialised variant (gemm_p3ws_kernel): 2 x WM x WN waves, a ring of 3 stages.
+template <int BM, int BN, int WM, int WN, int BK, bool PIPE = false, class P>
+inline hipError_t launch_gemm_p3ws(const P& p, int splits, hipStream_t st) {
+  using C = P3Core<BM, BN, WM, WN, BK, P>;
+  constexpr int RING_BYTES = 3 * C::STAGE;
+  constexpr int LDS = RING_BYTES > C::EPI_BYTES ? RING_BYTES : C::EPI_BYTES;
+  static_assert(LDS <= 160 * 1024, "three stages must fit the 160-KiB LDS of a CU");
+  static hipError_t attr = p3_set_lds(&gemm_p3ws_kernel<BM, BN, WM, WN, BK, PIPE, P>, LDS);
+  if (attr != hipSuccess) return attr;
+  const int tiles = ((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
+  hipLaunchKernelGGL((gemm_p3ws_kernel<BM, BN, WM, WN, BK, PIPE, P>), dim3(tiles, 1, splits),
+                     dim3(2 * C::NT), LDS, st, p, p3_n_major(p));
   return hipGetLastError();
 }
 

@@ -150,6 +150,17 @@ constexpr int kP3MaxWgradSplits = 512;
       return ACME_ERR_HIP;                                                                    \
     }                                                                                         \
   } while (0)
+// Warp-specialised form (gemm_p3ws_kernel, fragment reads one k16 step ahead; BK = 32).
+#define P3WS_GEMM(name, BM, BN, WM, WN, prob, splits)                                        \
+  do {                                                                                        \
+    ACME_PROF_PEAK(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0, \
+                   gemm::p3_peak_tflops<decltype(prob)>());                                   \
+    hipError_t _e = gemm::launch_gemm_p3ws<BM, BN, WM, WN, 32, true>(prob, splits, st);      \
+    if (_e != hipSuccess) {                                                                   \
+      set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
+      return ACME_ERR_HIP;                                                                    \
+    }                                                                                         \
+  } while (0)
 #define P3_GEMM(name, BM, BN, WM, WN, BK, prob, splits)                                      \
   P3_GEMM_F(name, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, BM, BN, WM, \
             WN, BK, prob, splits)
@@ -316,7 +327,9 @@ int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int row
     p.k_chunk = chunk_for(p.K, splits);
     p.a_src = frames_src(frames, rows); p.b_src = src(dz1, (int64_t)rows * kX1);
     p.slab = slab;
-    P3_GEMM("conv1_wgrad", 256, 32, 4, 1, 32, p, splits);
+    // Producer / consumer waves (gemm_p3ws_kernel): 28.5 -> 25.0 us, the same bits.
+    if (tune_variant("WSN") == 1) P3_GEMM("conv1_wgrad", 256, 32, 4, 1, 32, p, splits);
+    else P3WS_GEMM("conv1_wgrad", 256, 32, 4, 1, p, splits);
     if ((rc = p3_wgrad_reduce(p, splits, slab, g.w1, g.b1, "conv1_wgrad_reduce", st)))
       return rc;
   }

@@ -152,6 +152,40 @@ def test_single_stream_schedule_bitwise():
         lib().acme_tune_set(b"SIDE", 0)
 
 
+def test_warp_specialised_gemms_bitwise():
+    """fc_fwd, fc_dgrad and conv1_wgrad run on gemm_p3ws_kernel (producer / consumer waves,
+    fragment reads one k16 step ahead): the consumers execute
+    the same fragment reads and MFMAs over the same stages as the single-role kernels
+    (ACME_V_WSN=1), so the step is bit-identical (B = 37: partial tiles; B = 512: the
+    bench's grids)."""
+    from acme_amd._lib import lib
+    from acme_amd.networks import DQNAtariNetwork
+    net = DQNAtariNetwork(18)
+    for B in (37, 512):
+        p0, t0 = net.init(3), net.init(4)
+        a = _learner(net, B)
+        b = _learner(net, B)
+        a.set_params(p0, t0)
+        b.set_params(p0, t0)
+        rng = np.random.default_rng(B)
+        try:
+            for _ in range(2):
+                dev = _dev(_batch(rng, B, (84, 84, 4), 18))
+                lib().acme_tune_set(b"WSN", 1)
+                a.step(*dev)
+                lib().acme_tune_set(b"WSN", 0)
+                b.step(*dev)
+                lib().acme_tune_set(b"WSN", 0)
+                torch.cuda.synchronize()
+                assert a.loss.item() == b.loss.item(), B
+                for buf in ("grads", "params", "m", "v"):
+                    ga, gb = a.get_params(buf), b.get_params(buf)
+                    for k in ga:
+                        np.testing.assert_array_equal(ga[k], gb[k], err_msg=f"B={B} {buf}/{k}")
+        finally:
+            lib().acme_tune_set(b"WSN", 0)
+
+
 def test_adam_and_target_copy_cadence():
     from acme_amd.networks import MLP
     net = MLP(4, [50, 50], 2)
