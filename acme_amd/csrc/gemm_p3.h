@@ -812,11 +812,11 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3g_kernel(const P p_in, in
 // iteration.  Stages past the end load zeros into buffers that are never read.
 template <int BM, int BN, int WM, int WN, int BK, bool PIPE, class P>
 __global__ void __launch_bounds__(128 * WM * WN) gemm_p3ws_kernel(const P p_in, int n_major) {
+  constexpr int RING = 3;  // (two stages, two blocks per CU, measured slower on the step)
   using C = P3Core<BM, BN, WM, WN, BK, P>;
   using PA = typename C::PA;
   using PB = typename C::PB;
   constexpr int NT = C::NT, NPA = C::NPA, NPB = C::NPB, STAGE = C::STAGE;
-  constexpr int RING = 3;
   const BlockPlace bp = place_block<BM, BN>(p_in.M, p_in.N, n_major);
   const P p = z_select_at(p_in, bp.z);
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];

@@ -241,7 +241,12 @@ int forward_p3(const PWeights& w, const Frames& frames, int rows, const PActs& a
     p.M = rows * G2::OPIX; p.N = G2::CO; p.K = G2::K; p.k_chunk = G2::K;
     p.a_src = src(a.x1, (int64_t)rows * kX1); p.b_src = src(w.w2, G2::K * G2::CO);
     p.bias = w.b2; p.y = pl(a.x2);
-    P3_GEMM("conv2_fwd", 128, 64, 2, 2, 32, p, 1);
+    // Producer / consumer waves (gemm_p3ws_kernel).  Alone this launch is slower (62 -> 69 us:
+    // one 512-thread block per CU instead of two 256-thread ones), but beside the target
+    // forward on the other stream the step is faster: 0.723 -> 0.700 ms (3 alternating runs
+    // each, one box).  tune WSN=1: the single-role kernel (same bits; tests).
+    if (tune_variant("WSN") == 1) P3_GEMM("conv2_fwd", 128, 64, 2, 2, 32, p, 1);
+    else P3WS_GEMM("conv2_fwd", 128, 64, 2, 2, p, 1);
   }
   {
     P3ConvFwd<G3, 3> p;

@@ -153,7 +153,7 @@ def test_single_stream_schedule_bitwise():
 
 
 def test_warp_specialised_gemms_bitwise():
-    """fc_fwd, fc_dgrad and conv1_wgrad run on gemm_p3ws_kernel (producer / consumer waves,
+    """fc_fwd, fc_dgrad, conv2_fwd and conv1_wgrad run on gemm_p3ws_kernel (producer / consumer waves,
     fragment reads one k16 step ahead): the consumers execute
     the same fragment reads and MFMAs over the same stages as the single-role kernels
     (ACME_V_WSN=1), so the step is bit-identical (B = 37: partial tiles; B = 512: the

@@ -1,4 +1,4 @@
-# Same-box A/B of the warp-specialised plane GEMMs (fc_fwd, fc_dgrad, conv1_wgrad) against
+# Same-box A/B of the warp-specialised plane GEMMs (fc_fwd, fc_dgrad, conv2_fwd, conv1_wgrad) against
 # the single-role kernels (ACME_V_WSN=1): alternating bench runs with section profiles;
 # prints step time and the affected kernels.  Run under gpurun.
 set -e
