@@ -48,7 +48,7 @@ SECTIONS = [
     (r"P3DenseFwd", "fc_fwd"),
     (r"P3DenseWgrad", "fc_wgrad"),
     (r"P3DenseDgrad", "fc_dgrad"),
-    (r"fc_head_forward_kernel", "fc_head_fwd"),
+    (r"fc_head_forward_kernel|fc_head1024_kernel", "fc_head_fwd"),
     (r"frames_bf16_kernel", "frames_bf16"),
     (r"head_dz_planes_kernel", "head_dz"),
     (r"dqn_loss_head_dz_kernel", "loss_head_dz"),
@@ -65,6 +65,7 @@ SECTIONS = [
     (r"ConvDgradSub", "conv2_dgrad"),
     (r"ConvDgrad<", "conv3_dgrad"),
     (r"(?<!clip_)adam_kernel", "adam"),
+    (r"sample_gather_pair_kernel", "replay_sample_gather"),
     (r"gather_fields_kernel|gather_pair_kernel|gather_pieces_kernel", "replay_gather"),
     (r"sample_prioritized_kernel", "replay_sample"),
     (r"prio_update_fused_kernel", "replay_update"),
