@@ -9,6 +9,11 @@ requests of all actors and runs them as one GPU network step (acme_impala_policy
 the learner's current parameters, in chunks of the learner's max batch).  The actors see
 the learner's latest parameters at every step (the reference's VariableClient refreshes
 every `update_period` steps; a fresher policy is the limit of that).
+
+VectorActorPool runs the same per-environment actor semantics with K environments per host
+thread and one policy call per K steps: a thread per actor pays two GIL hand-offs per
+environment step (request, reply), which caps the thread pool at ~3k steps/s whatever the
+environment costs.
 """
 
 from __future__ import annotations
@@ -20,6 +25,7 @@ from typing import Callable, List, Optional
 import numpy as np
 
 from acme_amd.agents.impala.acting import IMPALAActor
+from acme_amd.networks import LSTMState
 
 
 class BatchedPolicy:
@@ -142,6 +148,111 @@ class ActorPool:
     def start(self) -> None:
         self._threads = [threading.Thread(target=self._run, args=(i,), daemon=True)
                          for i in range(self._n)]
+        for t in self._threads:
+            t.start()
+
+    def stop(self, timeout: Optional[float] = 30.0) -> None:
+        self._stop.set()
+        for t in self._threads:
+            t.join(timeout)
+
+
+class VectorActor:
+    """K environments stepped by one host thread with one batched policy call per step:
+    per environment exactly IMPALAActor's behaviour (acme/agents/tf/impala/acting.py:
+    a ~ Categorical(logits) of the step, the LSTM state carried across steps and reset at
+    episode starts, {'logits', 'core_state'} of the step handed to the adder as extras)."""
+
+    def __init__(self, envs: List[object], adders: List[object], policy_step: Callable,
+                 initial_state: Callable, seed: int = 0, max_rows: Optional[int] = None):
+        self._envs = envs
+        self._rows = int(max_rows) if max_rows else len(envs)  # rows per policy call
+        self._adders = adders
+        self._policy = policy_step
+        self._K = len(envs)
+        self._rng = np.random.default_rng(seed)
+        s0 = initial_state(1)
+        self._h0, self._c0 = s0.hidden[0].copy(), s0.cell[0].copy()
+        st = initial_state(self._K)
+        self._h, self._c = st.hidden.copy(), st.cell.copy()
+        self._ts = [None] * self._K
+        self.steps = 0
+
+    def start(self) -> None:
+        for i, (env, adder) in enumerate(zip(self._envs, self._adders)):
+            ts = env.reset()
+            adder.add_first(ts)
+            self._ts[i] = ts
+            self._h[i], self._c[i] = self._h0, self._c0
+
+    def step(self) -> None:
+        K, ts = self._K, self._ts
+        obs = np.stack([t.observation.observation for t in ts])
+        prev_a = np.array([t.observation.action for t in ts], np.int32)
+        prev_r = np.array([t.observation.reward for t in ts], np.float32)
+        if self._rows >= K:
+            logits, _, h, c = self._policy(obs, prev_a, prev_r, self._h, self._c)
+        else:
+            parts = [self._policy(obs[j:j + self._rows], prev_a[j:j + self._rows],
+                                  prev_r[j:j + self._rows], self._h[j:j + self._rows],
+                                  self._c[j:j + self._rows]) for j in range(0, K, self._rows)]
+            logits, h, c = (np.concatenate([q[k] for q in parts]) for k in (0, 2, 3))
+        z = logits - logits.max(axis=1, keepdims=True)
+        p = np.exp(z)
+        cdf = np.cumsum(p, axis=1)
+        u = self._rng.random(K) * cdf[:, -1]
+        actions = np.minimum((cdf < u[:, None]).sum(axis=1), logits.shape[1] - 1).astype(np.int32)
+        prev_h, prev_c = self._h, self._c
+        self._h, self._c = np.array(h, np.float32), np.array(c, np.float32)
+        for i in range(K):
+            a = actions[i]
+            nt = self._envs[i].step(a)
+            self._adders[i].add(a, nt, {"logits": logits[i],
+                                        "core_state": LSTMState(prev_h[i], prev_c[i])})
+            if nt.last():
+                nt = self._envs[i].reset()
+                self._adders[i].add_first(nt)
+                self._h[i], self._c[i] = self._h0, self._c0
+            ts[i] = nt
+        self.steps += K
+
+
+class VectorActorPool:
+    """`num_actors` environments over `threads` host threads (VectorActor each); each thread
+    calls its own policy (make_policy(t): e.g. learner.actor_policy(max_rows), one network
+    and stream per thread) on at most `max_rows` environments at a time.  start() / stop();
+    env_steps counts every environment step."""
+
+    def __init__(self, make_env: Callable[[int], object], make_adder: Callable[[int], object],
+                 make_policy: Callable[[int], Callable], initial_state: Callable,
+                 num_actors: int = 64, threads: int = 2, seed: int = 0,
+                 max_rows: Optional[int] = None):
+        self._stop = threading.Event()
+        self._threads: List[threading.Thread] = []
+        self.errors: List[BaseException] = []
+        threads = max(1, min(int(threads), int(num_actors)))
+        split = np.array_split(np.arange(int(num_actors)), threads)
+        self._actors = [VectorActor([make_env(int(i)) for i in ids],
+                                    [make_adder(int(i)) for i in ids], make_policy(t),
+                                    initial_state, seed=seed + t, max_rows=max_rows)
+                        for t, ids in enumerate(split)]
+
+    @property
+    def env_steps(self) -> int:
+        return sum(a.steps for a in self._actors)
+
+    def _run(self, actor: VectorActor) -> None:
+        try:
+            actor.start()
+            while not self._stop.is_set():
+                actor.step()
+        except BaseException as e:  # noqa: BLE001
+            if not self._stop.is_set():
+                self.errors.append(e)
+
+    def start(self) -> None:
+        self._threads = [threading.Thread(target=self._run, args=(a,), daemon=True)
+                         for a in self._actors]
         for t in self._threads:
             t.start()
 

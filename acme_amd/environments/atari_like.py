@@ -5,11 +5,10 @@ actors feeding one GPU learner).  The ALE is not installed here, so this stands 
 axis, 18 discrete actions, clipped rewards in {-1, 0, 1}, episodes of a random length.
 Frames are cheap deterministic functions of (seed, episode, step, action) — a scrolling
 band pattern plus per-step noise rows — so an actor's host cost is dominated by what the
-reference's actors also pay per step (policy call, adder), not by frame synthesis."""
+reference's actors also pay per step (policy call, adder), not by frame synthesis (about
+20 us per step)."""
 
 from __future__ import annotations
-
-import collections
 
 import numpy as np
 
@@ -18,47 +17,68 @@ from acme_amd import dm_env, specs
 
 class AtariLike(dm_env.Environment):
 
+    _NOISE = 4096  # noise rows drawn per refill of an environment's pool
+
     def __init__(self, seed: int = 0, num_actions: int = 18, min_length: int = 200,
                  max_length: int = 1000, stack: int = 4):
         self._rng = np.random.default_rng(seed)
         self._A = int(num_actions)
         self._lengths = (int(min_length), int(max_length))
         self._stack = int(stack)
-        self._frames = collections.deque(maxlen=self._stack)
         base = np.arange(84, dtype=np.int32)
-        self._pattern = ((base[:, None] * 3 + base[None, :] * 5) % 256).astype(np.uint8)
+        pattern = ((base[:, None] * 3 + base[None, :] * 5) % 256).astype(np.uint8)
+        # Two copies side by side: the pattern scrolled by `pos` is a view (no np.roll).
+        self._wide = np.concatenate([pattern, pattern], axis=1)
+        self._obs = np.zeros((84, 84, self._stack), np.uint8)
         self._t = 0
         self._len = 0
         self._pos = 0
+        self._refill()
 
-    def _frame(self) -> np.ndarray:
-        f = np.roll(self._pattern, self._pos, axis=1)
-        rows = self._rng.integers(0, 84, 4)
-        f[rows] = self._rng.integers(0, 256, (4, 84), dtype=np.uint8)
-        return f
+    def _refill(self) -> None:
+        # Noise rows, row indices and reward draws, consumed in order (deterministic by seed).
+        self._noise = self._rng.integers(0, 256, (self._NOISE, 4, 84), dtype=np.uint8)
+        self._rows = self._rng.integers(0, 84, (self._NOISE, 4))
+        self._u = self._rng.random(self._NOISE)
+        self._k = 0
 
-    def _observation(self) -> np.ndarray:
-        return np.stack(list(self._frames), axis=-1)
+    def _next_frame(self) -> None:
+        """Shifts the stack by one frame and writes the new frame into the last slot: the
+        scrolled band pattern with 4 noise rows.  With 4 frames a pixel's stack is one
+        little-endian uint32 (frame i in byte i), so the shift is `>> 8` and the new frame
+        goes into the top byte."""
+        if self._k == self._NOISE:
+            self._refill()
+        f = self._wide[:, 84 - self._pos:168 - self._pos].copy()
+        f[self._rows[self._k]] = self._noise[self._k]
+        if self._stack == 4:
+            w = (self._obs.view(np.uint32)[..., 0] >> 8) | (f.astype(np.uint32) << 24)
+            self._obs = w.view(np.uint8).reshape(84, 84, 4)
+        else:
+            obs = np.empty_like(self._obs)
+            obs[:, :, :-1] = self._obs[:, :, 1:]
+            obs[:, :, -1] = f
+            self._obs = obs
 
     def reset(self) -> dm_env.TimeStep:
         self._t = 0
         self._len = int(self._rng.integers(*self._lengths))
         self._pos = int(self._rng.integers(0, 84))
-        self._frames.clear()
-        for _ in range(self._stack - 1):
-            self._frames.append(np.zeros((84, 84), np.uint8))  # zero padding at the start
-        self._frames.append(self._frame())
-        return dm_env.restart(self._observation())
+        self._obs = np.zeros((84, 84, self._stack), np.uint8)  # zero padding at the start
+        self._next_frame()
+        self._k += 1
+        return dm_env.restart(self._obs)
 
     def step(self, action) -> dm_env.TimeStep:
         self._t += 1
         self._pos = (self._pos + int(action) - self._A // 2) % 84
-        self._frames.append(self._frame())
-        u = self._rng.random()
+        self._next_frame()
+        u = self._u[self._k]
+        self._k += 1
         reward = np.float32(1.0 if u < 0.02 else (-1.0 if u > 0.99 else 0.0))
         if self._t >= self._len:
-            return dm_env.termination(reward, self._observation())
-        return dm_env.transition(reward, self._observation())
+            return dm_env.termination(reward, self._obs)
+        return dm_env.transition(reward, self._obs)
 
     def observation_spec(self):
         return specs.Array((84, 84, self._stack), np.uint8, name="observation")

@@ -23,18 +23,21 @@ class ObservationActionRewardWrapper:
         self._environment = environment
         self._prev_action = None
         self._prev_reward = None
+        # The wrapped environment's specs are fixed; their dtypes are looked up once.
+        self._action_dtype = environment.action_spec().dtype
+        self._reward_dtype = environment.reward_spec().dtype
 
     def reset(self) -> dm_env.TimeStep:
         ts = self._environment.reset()
-        self._prev_action = np.zeros((), self._environment.action_spec().dtype)
-        self._prev_reward = np.zeros((), self._environment.reward_spec().dtype)
+        self._prev_action = np.zeros((), self._action_dtype)
+        self._prev_reward = np.zeros((), self._reward_dtype)
         return ts._replace(observation=OAR(ts.observation, self._prev_action, self._prev_reward))
 
     def step(self, action) -> dm_env.TimeStep:
         ts = self._environment.step(action)
-        self._prev_action = np.asarray(action, self._environment.action_spec().dtype)
+        self._prev_action = np.asarray(action, self._action_dtype)
         self._prev_reward = np.asarray(ts.reward if ts.reward is not None else 0,
-                                       self._environment.reward_spec().dtype)
+                                       self._reward_dtype)
         return ts._replace(observation=OAR(ts.observation, self._prev_action, self._prev_reward))
 
     def observation_spec(self):

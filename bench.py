@@ -49,7 +49,10 @@ def parse():
                         "impala: configs[3] (learner side); impala_actors: configs[3] end to "
                         "end (--actors host actor threads feeding the device queue); insert: "
                         "host inserts into the configs[1] table while its learner steps")
-    p.add_argument("--actors", type=int, default=64, help="impala_actors: actor threads")
+    p.add_argument("--actors", type=int, default=64, help="impala_actors: environments / actors")
+    p.add_argument("--actor-threads", type=int, default=2,
+                   help="impala_actors: host threads stepping the environments in batches "
+                        "(VectorActorPool); 0 = one thread per actor (ActorPool)")
     p.add_argument("--batch", type=int, default=0, help="default 512 (dqn) / 256 (d4pg)")
     p.add_argument("--replay-size", type=int, default=1_000_000)
     p.add_argument("--num-actions", type=int, default=18)
@@ -480,7 +483,7 @@ def impala_actors_bench(args, dev):
     from acme_amd import replay, specs
     from acme_amd.adders import reverb as adders
     from acme_amd.agents.impala import IMPALALearner
-    from acme_amd.agents.impala.actors import ActorPool, BatchedPolicy
+    from acme_amd.agents.impala.actors import ActorPool, BatchedPolicy, VectorActorPool
     from acme_amd.datasets import make_reverb_dataset
     from acme_amd.environments.atari_like import AtariLike
     from acme_amd.networks import IMPALAAtariNetwork, LSTMState
@@ -501,11 +504,19 @@ def impala_actors_bench(args, dev):
                             learning_rate=1e-3, entropy_cost=0.01, baseline_cost=0.5,
                             logger=loggers.NoOpLogger(), batch_size=B, sequence_length=T,
                             device=dev)
-    policy = BatchedPolicy(learner.actor_policy(max_rows=16), max_rows=16)
-    pool = ActorPool(lambda i: ObservationActionRewardWrapper(AtariLike(seed=1 + i)),
-                     lambda i: adders.SequenceAdder(replay.Client(server), sequence_length=T,
-                                                    period=T),
-                     policy, net.initial_state, num_actors=args.actors)
+    make_env = lambda i: ObservationActionRewardWrapper(AtariLike(seed=1 + i))  # noqa: E731
+    make_adder = lambda i: adders.SequenceAdder(replay.Client(server), sequence_length=T,  # noqa: E731
+                                                period=T)
+    if args.actor_threads > 0:  # K environments per host thread, one policy call per K steps
+        th = args.actor_threads
+        per = min(-(-args.actors // th), 16)  # the native policy's batch limit (LDS) at LSTM 256
+        policy = None
+        pool = VectorActorPool(make_env, make_adder, lambda t: learner.actor_policy(max_rows=per),
+                               net.initial_state, num_actors=args.actors, threads=th,
+                               max_rows=per)
+    else:  # one host thread per actor (IMPALAActor), policy calls batched by a server thread
+        policy = BatchedPolicy(learner.actor_policy(max_rows=16), max_rows=16)
+        pool = ActorPool(make_env, make_adder, policy, net.initial_state, num_actors=args.actors)
     pool.start()
     try:
         def learn(n):
@@ -527,7 +538,8 @@ def impala_actors_bench(args, dev):
         env_rate = (pool.env_steps - s0) / dt
     finally:
         pool.stop(timeout=5)
-        policy.close()
+        if policy is not None:
+            policy.close()
     out = {
         "metric": "IMPALA learned frames/sec (B=16 x T=20 per step) with host actors feeding "
                   "the device queue, 1 MI355X",
@@ -540,8 +552,11 @@ def impala_actors_bench(args, dev):
                    "batch_sequences": B, "sequence_length": T, "sequence_period": T,
                    "obs": "uint8[84,84,4]", "num_actions": A, "lstm": H},
         "actors": {"env_steps_per_s": round(env_rate, 1),
-                   "policy_batches": policy.batches,
-                   "mean_policy_rows": round(policy.rows / max(policy.batches, 1), 2)},
+                   "host_threads": args.actor_threads if policy is None else args.actors,
+                   "policy_batches": policy.batches if policy else None,
+                   "mean_policy_rows": (round(policy.rows / max(policy.batches, 1), 2)
+                                        if policy else min(-(-args.actors // args.actor_threads),
+                                                           16))},
     }
     print(json.dumps(out))
 

@@ -136,3 +136,50 @@ def test_actor_pool_feeds_device_queue_learner():
     assert pool.env_steps >= 5 * B * T
     assert policy.batches > 0 and policy.rows >= pool.env_steps
     assert np.isfinite(learner.native.metrics.cpu().numpy()).all()
+
+
+def test_vector_actor_pool_feeds_device_queue_learner():
+    """The same with VectorActorPool: 2 host threads x 3 environments, one policy call per
+    thread step on the learner's parameters (chunks of 2 rows), into the device queue."""
+    import time
+    from acme_amd import datasets, replay
+    from acme_amd.adders import reverb as adders
+    from acme_amd.agents.impala import IMPALALearner
+    from acme_amd.agents.impala.actors import VectorActorPool
+    from acme_amd.environments.atari_like import AtariLike
+    from acme_amd.networks import IMPALAAtariNetwork, LSTMState
+    A, H, T, B = 18, 32, 5, 4
+    env = ObservationActionRewardWrapper(AtariLike(seed=0, min_length=7, max_length=30))
+    spec = specs.make_environment_spec(env)
+    extra = {"core_state": LSTMState(specs.Array((H,), np.float32), specs.Array((H,), np.float32)),
+             "logits": specs.Array((A,), np.float32)}
+    queue = replay.Table.queue(adders.DEFAULT_PRIORITY_TABLE, 16,
+                               signature=adders.SequenceAdder.signature(spec, extras_spec=extra))
+    server = replay.Server([queue])
+    net = IMPALAAtariNetwork(A, lstm_size=H, head_size=16)
+    learner = IMPALALearner(spec, net, datasets.make_reverb_dataset(server, batch_size=B,
+                                                                    sequence_length=T),
+                            learning_rate=1e-3, entropy_cost=0.01, baseline_cost=0.5,
+                            logger=loggers.NoOpLogger(), batch_size=B, sequence_length=T)
+    pool = VectorActorPool(lambda i: ObservationActionRewardWrapper(
+                               AtariLike(seed=10 + i, min_length=7, max_length=30)),
+                           lambda i: adders.SequenceAdder(replay.Client(server), sequence_length=T,
+                                                          period=T),
+                           lambda t: learner.actor_policy(max_rows=2), net.initial_state,
+                           num_actors=6, threads=2, max_rows=2)
+    pool.start()
+    try:
+        deadline = time.time() + 120
+        while learner.num_steps < 5 and time.time() < deadline:
+            assert not pool.errors, pool.errors
+            if queue.can_sample(B):
+                learner.step()
+            else:
+                time.sleep(0.001)
+    finally:
+        pool.stop(timeout=10)
+    torch.cuda.synchronize()
+    assert not pool.errors, pool.errors
+    assert learner.num_steps >= 5
+    assert pool.env_steps >= 5 * B * T
+    assert np.isfinite(learner.native.metrics.cpu().numpy()).all()
