@@ -59,7 +59,7 @@ class DQNConfig(ctypes.Structure):
 class TransitionBatch(ctypes.Structure):
     _fields_ = [("o_tm1", c_vp), ("a_tm1", c_vp), ("r_t", c_vp), ("d_t", c_vp), ("o_t", c_vp),
                 ("probabilities", c_vp), ("batch", c_i64), ("global_min_probability", c_vp),
-                ("mean_over", c_i64)]
+                ("mean_over", c_i64), ("obs_bf16", c_vp)]
 
 
 class DQNOutputs(ctypes.Structure):
@@ -130,6 +130,8 @@ _SIGS = {
                                          ctypes.POINTER(c_vp), c_vp]),
     "acme_replay_sample_gather": (c_i32, [c_vp, c_i64, c_u64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                           ctypes.POINTER(c_vp), c_vp]),
+    "acme_replay_sample_gather_frames": (c_i32, [c_vp, c_i64, c_u64, c_vp, c_vp, c_vp, c_vp,
+                                                 c_vp, ctypes.POINTER(c_vp), c_vp, c_vp]),
     "acme_r2d2_priorities": (c_i32, [c_vp, c_i32, c_i32, ctypes.c_double, c_vp, c_vp]),
     "acme_r2d2_importance_weights": (c_i32, [c_vp, c_i32, c_i64, ctypes.c_double, c_vp, c_vp]),
     "acme_frames_expand": (c_i32, [c_vp, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp, c_vp]),

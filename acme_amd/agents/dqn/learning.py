@@ -104,7 +104,13 @@ class DQNLearner(core.Learner, core.Saveable):
                  self._prepare(o_t.reshape(B, self._obs_flat), obs_dt),
                  self._prepare(probs, torch.float64))
         if self._dist is None:
-            self._native.step(*batch)
+            # The dataset's fused gather also wrote the exact bf16 copy of [o_tm1; o_t]
+            # (uint8 tables): the learner then skips its own conversion (same bits).
+            fb = getattr(self._iterator, "last_frames_bf16", None)
+            if fb is not None and (obs_dt != torch.uint8 or tuple(fb.shape) != (2 * B,
+                                                                                self._obs_flat)):
+                fb = None
+            self._native.step(*batch, obs_bf16=fb)
         else:
             # Gradient all-reduce in two buckets overlapped with the backward pass: the dense
             # layers' gradients (the buffer's tail, ~99% of the bytes) are reduced on the

@@ -868,8 +868,12 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
     // conv1's input: a bf16 copy of [o_tm1; o_t] on the main stream for everything.  (Reading
     // the batch's uint8 frames in the kernels instead measured slower beside the side stream,
     // 0.746 -> 0.750 ms per step: the uint8 image kernel is slower there than the bf16 one.)
-    if ((rc = convert_frames(l, batch->o_tm1, batch->o_t, B, 2 * B, st)) != ACME_OK) return rc;
-    const torso::Frames fwd_frames{l->frames};
+    if (!batch->obs_bf16 &&
+        (rc = convert_frames(l, batch->o_tm1, batch->o_t, B, 2 * B, st)) != ACME_OK)
+      return rc;
+    // The dataset's fused gather may hand over the bf16 copy (acme_replay_sample_gather_frames).
+    const torso::Frames fwd_frames{batch->obs_bf16 ? static_cast<const void*>(batch->obs_bf16)
+                                                   : static_cast<const void*>(l->frames)};
     l->cur_frames = fwd_frames;
     // Target forward (q_t_value) on the side stream, beside the online forward.
     if (side) {

@@ -26,6 +26,7 @@ counter block i.
 
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import numpy as np
@@ -104,6 +105,11 @@ class _TableIterator:
         self._rows = 2 * batch if shard is not None else batch
         self._snaps = {}
         self._share = {}
+        # The exact bf16 copy of [o_tm1; o_t] written by the fused sample + gather (uint8
+        # transition tables): per buffer slot, or None; `last_frames_bf16` is the copy of
+        # the batch handed out last (the DQN learner then skips its own conversion).
+        self._fb = []
+        self.last_frames_bf16 = None
         if shard is not None and isinstance(table, replay.FrameTable):
             raise ValueError("global sampling over FrameTable shards is not supported")
 
@@ -154,7 +160,21 @@ class _TableIterator:
             # `info` and `bufs` own the device memory behind `raw` / `ptrs` (the sampled
             # slots have no other reference): keep them alive with the slot set.
             self._slots.append((raw, ptrs, sample, info, bufs))
+            self._fb.append(torch.empty(2 * self._rows, fields[0].row_bytes, dtype=torch.int16,
+                                        device=dev) if self._bf16_frames() else None)
         self._which = 0
+
+    def _bf16_frames(self) -> bool:
+        """The fused kernel's bf16 copy applies to uint8 transition tables whose only large
+        fields are the two observations (fields 0 and 4), on one table (no shards)."""
+        if self._shard is not None or isinstance(self._t, (replay.FrameTable, replay.QueueTable)):
+            return False
+        if os.environ.get("ACME_DATASET_BF16", "1") == "0":  # A/B switch: learner converts
+            return False
+        f = self._t.fields
+        big = [i for i, x in enumerate(f) if x.row_bytes >= 1024]
+        return (big == [0, 4] and f[0].dtype == np.uint8 and f[0].row_bytes == f[4].row_bytes
+                and f[0].row_bytes % 16 == 0)
 
     def _typed(self, buf, f, rows=None):
         B = self._rows if rows is None else rows
@@ -170,7 +190,7 @@ class _TableIterator:
     def __iter__(self):
         return self
 
-    def _draw(self, L, h, raw, ptrs, st, stream=None):
+    def _draw(self, L, h, raw, ptrs, st, stream=None, fb=None):
         """Sample + gather of one batch as a unit: no insert lands between the draw and the
         row copy (actor threads may be inserting), so each row is that of its reported key.
         Returns the number of items drawn."""
@@ -187,6 +207,9 @@ class _TableIterator:
             with t._mu:  # noqa: SLF001  (inserts commit under the table lock)
                 check(L.acme_replay_sample(h, self._B, step, *raw, st), "replay sample")
                 t.gather_into(raw[0], self._B, ptrs, st)
+        elif fb is not None:
+            check(L.acme_replay_sample_gather_frames(h, self._B, step, *raw, ptrs, fb.data_ptr(),
+                                                     st), "replay sample")
         else:
             check(L.acme_replay_sample_gather(h, self._B, step, *raw, ptrs, st),
                   "replay sample")
@@ -247,7 +270,8 @@ class _TableIterator:
             i = self._which
             raw, ptrs = self._slots[i][:2]
             self._which ^= 1
-            n = self._draw(L, h, raw, ptrs, stream_ptr())
+            n = self._draw(L, h, raw, ptrs, stream_ptr(), fb=self._fb[i])
+            self.last_frames_bf16 = self._fb[i]
             return self._sample_view(i, n)
         # Prefetch: order the dataset stream after everything queued so far on the caller's
         # stream (inserts, earlier learner steps and their priority updates), top the queue
@@ -264,7 +288,7 @@ class _TableIterator:
             i = self._next_slot
             self._next_slot = (i + 1) % (self._P + 2)
             raw, ptrs = self._slots[i][:2]
-            self._share[i] = self._draw(L, h, raw, ptrs, st, side)
+            self._share[i] = self._draw(L, h, raw, ptrs, st, side, fb=self._fb[i])
             self._ready[i].record(side)
             self._queue.append(i)
             t.set_reader_event(self._ready[i])
@@ -274,6 +298,7 @@ class _TableIterator:
         # cost (each event wait / record on a stream leaves ~7 us before the next kernel).
         if not self._ready[i].query():
             main.wait_event(self._ready[i])
+        self.last_frames_bf16 = self._fb[i]
         return self._sample_view(i, self._share[i])
 
 

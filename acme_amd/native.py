@@ -374,7 +374,7 @@ class NativeDQN:
 
     # --------------------------------------------------------------- step
     def _batch(self, o_tm1, a_tm1, r_t, d_t, o_t, probabilities, global_min_probability=None,
-               mean_over=None):
+               mean_over=None, obs_bf16=None):
         B = int(a_tm1.shape[0])
         if B < 1 or B > self.max_batch:
             raise ValueError(f"batch of {B} rows: the learner takes 1..{self.max_batch}")
@@ -398,6 +398,13 @@ class NativeDQN:
         tb.batch = B
         tb.global_min_probability = ptr(global_min_probability)
         tb.mean_over = int(mean_over or 0)
+        if obs_bf16 is not None:  # [2B, obs] bf16 bits of [o_tm1; o_t] (the dataset's copy)
+            if not (isinstance(obs_bf16, torch.Tensor) and obs_bf16.is_cuda and
+                    obs_bf16.dtype in (torch.int16, torch.uint16, torch.bfloat16) and
+                    obs_bf16.is_contiguous() and obs_bf16.shape[0] >= 2 * B and
+                    obs_bf16[0].numel() == o_tm1[0].numel()):
+                raise ValueError("obs_bf16 must be a contiguous [2B, obs] 16-bit device tensor")
+            tb.obs_bf16 = ptr(obs_bf16)
         return tb
 
     def _outputs(self, q_tm1=None):
@@ -438,8 +445,8 @@ class NativeDQN:
     def apply(self, stream=None):
         check(lib().acme_dqn_apply(self._h, stream_ptr(stream)), "dqn apply")
 
-    def step(self, *batch, q_tm1=None, stream=None):
-        tb = self._batch(*batch)
+    def step(self, *batch, q_tm1=None, stream=None, obs_bf16=None):
+        tb = self._batch(*batch, obs_bf16=obs_bf16)
         out = self._outputs(q_tm1)
         check(lib().acme_dqn_step(self._h, ctypes.byref(tb), ctypes.byref(out),
                                   stream_ptr(stream)), "dqn step")

@@ -143,6 +143,17 @@ int acme_replay_sample_gather(acme_replay* r, int64_t batch, uint64_t step_count
                               int64_t* table_size, double* priorities, void* const* out_fields,
                               void* stream);
 
+/* acme_replay_sample_gather for the transition layout (two equal uint8 fields, e.g. o_tm1 /
+ * o_t) that also writes the exact bf16 copy of both fields that the DQN plane path reads
+ * (frames_bf16: [2 * batch][field_bytes] u16, rows [0, batch) the first field, [batch,
+ * 2 * batch) the second; 16-B aligned), in the same launch; pass it to the learner as
+ * acme_transition_batch.obs_bf16.  Errors for other layouts. */
+int acme_replay_sample_gather_frames(acme_replay* r, int64_t batch, uint64_t step_counter,
+                                     int64_t* slots, uint64_t* keys, double* probabilities,
+                                     int64_t* table_size, double* priorities,
+                                     void* const* out_fields, uint16_t* frames_bf16,
+                                     void* stream);
+
 /* Data-parallel global-probability sampling: one table per rank holds a
  * shard of the global replay.  acme_replay_total writes the shard's sampling mass S_r
  * (sum of p^alpha, or the item count for Uniform) to out[0] on the device; the ranks
@@ -274,6 +285,10 @@ typedef struct acme_transition_batch {
    * per-rank batch, so that the all-reduce mean of the ranks' gradients is the global
    * batch's mean whatever the shares. */
   int64_t mean_over;
+  /* Optional (uint8 Nature network): the exact bf16 copy of [o_tm1; o_t], [2B][obs bytes]
+   * u16, as acme_replay_sample_gather_frames writes it; the learner then skips its own
+   * conversion (same bits).  NULL: the learner converts. */
+  const uint16_t* obs_bf16;
 } acme_transition_batch;
 
 typedef struct acme_dqn_outputs {
