@@ -140,7 +140,18 @@ class DQNLearner(core.Learner, core.Saveable):
         now = time.time()
         elapsed = now - self._timestamp if self._timestamp else 0
         self._timestamp = now
-        result = {"loss": self._native.loss} if self._log_loss else {}
+        loss = self._native.loss
+        if (self._dist is not None and self._log_loss
+                and not isinstance(self._logger, loggers.NoOpLogger)):
+            # The logged loss is the global batch's (SURVEY §8(e) collective 3): each rank's
+            # loss is its share's sum over the nominal per-rank batch, so the mean over ranks.
+            loss = loss.clone()
+            if self._avg_op is not None:
+                self._dist.all_reduce(loss, op=self._avg_op)
+            else:
+                self._dist.all_reduce(loss)
+                loss.mul_(1.0 / self._dist.get_world_size())
+        result = {"loss": loss} if self._log_loss else {}
         result.update(self._counter.increment(steps=1, walltime=elapsed))
         self._logger.write(result)
 

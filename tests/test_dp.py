@@ -104,12 +104,14 @@ def _gpu_worker(rank, world, port, q):
             while True:
                 yield replay.ReplaySample(info=info, data=data)
 
-    learner = DQNLearner(net, net, 0.99, 0.2, 1e-3, 100, _Fixed(), logger=loggers.NoOpLogger(),
+    log = loggers.InMemoryLogger()
+    learner = DQNLearner(net, net, 0.99, 0.2, 1e-3, 100, _Fixed(), logger=log,
                          seed=rank)  # different seeds: the broadcast must equalise them
     for _ in range(3):
         learner.step()
     torch.cuda.synchronize()
-    q.put((rank, learner.native.params.cpu().numpy()))
+    q.put((rank, (learner.native.params.cpu().numpy(),
+                  [float(np.asarray(r["loss"])) for r in log.data])))
     dist.destroy_process_group()
 
 
@@ -127,7 +129,10 @@ def test_dp_learner_matches_global_batch_gpu():
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
+    losses = {r: res[r][1] for r in res}
+    res = {r: res[r][0] for r in res}
     np.testing.assert_array_equal(res[0], res[1])  # replicas identical
+    assert losses[0] == losses[1]  # the logged loss is the global batch's on every rank
     # Single process, global batch 64, same initial params (rank 0's seed).
     net = MLP(6, [16, 16], 3)
     d = NativeDQN(network="mlp", num_actions=3, max_batch=64, obs_dtype="float32", obs_dim=6,
@@ -137,8 +142,12 @@ def test_dp_learner_matches_global_batch_gpu():
     batch = _global_batch(np.random.default_rng(7), 64, 6, 3)
     dev = [torch.as_tensor(batch[k]).cuda() for k in
            ("o_tm1", "a_tm1", "r_t", "d_t", "o_t", "probabilities")]
+    ref_losses = []
     for _ in range(3):
         d.step(*dev)
+        ref_losses.append(d.loss.item())
+    # The logged loss: mean over ranks of the shard sums over 32 = the 64-row mean.
+    np.testing.assert_allclose(losses[0], ref_losses, rtol=1e-5)
     got = d.params.cpu().numpy()
     # fp32 sums over 32 + 32 rows vs 64 rows differ in order: Adam-normalised steps agree
     # to within lr on elements whose gradient is at the rounding floor.
