@@ -128,6 +128,8 @@ _SIGS = {
     "acme_replay_total": (c_i32, [c_vp, c_vp, c_vp]),
     "acme_replay_sample_share": (c_i32, [c_vp, c_i64, c_u64, c_f64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                          ctypes.POINTER(c_vp), c_vp]),
+    "acme_replay_sample_share_frames": (c_i32, [c_vp, c_i64, c_u64, c_f64, c_vp, c_vp, c_vp, c_vp,
+                                                c_vp, ctypes.POINTER(c_vp), c_vp, c_vp]),
     "acme_replay_sample_gather": (c_i32, [c_vp, c_i64, c_u64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                           ctypes.POINTER(c_vp), c_vp]),
     "acme_replay_sample_gather_frames": (c_i32, [c_vp, c_i64, c_u64, c_vp, c_vp, c_vp, c_vp,

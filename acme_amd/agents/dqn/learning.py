@@ -103,13 +103,14 @@ class DQNLearner(core.Learner, core.Saveable):
                  self._prepare(d_t.reshape(B), torch.float32),
                  self._prepare(o_t.reshape(B, self._obs_flat), obs_dt),
                  self._prepare(probs, torch.float64))
+        # The dataset's fused gather also wrote the exact bf16 copy of [o_tm1; o_t] (uint8
+        # tables; rows [0, B) and [B, 2B) of its buffer): the learner then skips its own
+        # conversion (same bits).
+        fb = getattr(self._iterator, "last_frames_bf16", None)
+        if fb is not None:
+            fb = (fb[:2 * B] if obs_dt == torch.uint8 and fb.shape[0] >= 2 * B
+                  and fb.shape[1] == self._obs_flat else None)
         if self._dist is None:
-            # The dataset's fused gather also wrote the exact bf16 copy of [o_tm1; o_t]
-            # (uint8 tables): the learner then skips its own conversion (same bits).
-            fb = getattr(self._iterator, "last_frames_bf16", None)
-            if fb is not None and (obs_dt != torch.uint8 or tuple(fb.shape) != (2 * B,
-                                                                                self._obs_flat)):
-                fb = None
             self._native.step(*batch, obs_bf16=fb)
         else:
             # Gradient all-reduce in two buckets overlapped with the backward pass: the dense
@@ -120,7 +121,7 @@ class DQNLearner(core.Learner, core.Saveable):
             n.batch_min_probability(batch[5], self._gmin)
             dist.all_reduce(self._gmin, op=dist.ReduceOp.MIN)
             n.forward_backward_stage(0, *batch, global_min_probability=self._gmin,
-                                     mean_over=self._B)
+                                     mean_over=self._B, obs_bf16=fb)
             split = self._grad_split
             tail, head = n.grads[split:], n.grads[:split]
             op = self._avg_op if self._avg_op is not None else dist.ReduceOp.SUM

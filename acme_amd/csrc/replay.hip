@@ -1210,6 +1210,18 @@ int acme_replay_sample_share(acme_replay* r, int64_t batch, uint64_t step_counte
                             table_size, priorities, out_fields, stream);
 }
 
+int acme_replay_sample_share_frames(acme_replay* r, int64_t batch, uint64_t step_counter,
+                                    double prob_scale, int64_t* slots, uint64_t* keys,
+                                    double* probabilities, int64_t* table_size,
+                                    double* priorities, void* const* out_fields,
+                                    uint16_t* frames_bf16, void* stream) {
+  ACME_CHECK_ARG(r && out_fields && frames_bf16, "null argument");
+  ACME_CHECK_ARG(prob_scale > 0.0 && prob_scale <= 1.0, "prob_scale must be in (0, 1]");
+  std::lock_guard<std::mutex> lock(r->mu);
+  return sample_gather_impl(r, batch, step_counter, prob_scale, slots, keys, probabilities,
+                            table_size, priorities, out_fields, stream, frames_bf16);
+}
+
 static int sample_impl(acme_replay* r, int64_t batch, uint64_t step_counter, double prob_scale,
                        int64_t* slots, uint64_t* keys, double* probabilities,
                        int64_t* table_size, double* priorities, void* stream) {

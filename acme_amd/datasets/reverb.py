@@ -166,8 +166,8 @@ class _TableIterator:
 
     def _bf16_frames(self) -> bool:
         """The fused kernel's bf16 copy applies to uint8 transition tables whose only large
-        fields are the two observations (fields 0 and 4), on one table (no shards)."""
-        if self._shard is not None or isinstance(self._t, (replay.FrameTable, replay.QueueTable)):
+        fields are the two observations (fields 0 and 4); a shard's copy holds its share."""
+        if isinstance(self._t, (replay.FrameTable, replay.QueueTable)):
             return False
         if os.environ.get("ACME_DATASET_BF16", "1") == "0":  # A/B switch: learner converts
             return False
@@ -199,8 +199,12 @@ class _TableIterator:
         step = t.next_draw() & 0xFFFFFFFFFFFFFFFF
         if self._shard is not None:
             n, scale = self._shares(step)
-            check(L.acme_replay_sample_share(h, n, step, scale, *raw, ptrs, st),
-                  "replay sample")
+            if fb is not None:
+                check(L.acme_replay_sample_share_frames(h, n, step, scale, *raw, ptrs,
+                                                        fb.data_ptr(), st), "replay sample")
+            else:
+                check(L.acme_replay_sample_share(h, n, step, scale, *raw, ptrs, st),
+                      "replay sample")
             self._snapshot(L, h, step, st, stream)
             return n
         if isinstance(t, replay.FrameTable):  # stacks rebuilt from stored frames

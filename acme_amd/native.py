@@ -420,12 +420,12 @@ class NativeDQN:
                                               stream_ptr(stream)), "dqn forward_backward")
 
     def forward_backward_stage(self, stage: int, *batch, global_min_probability=None,
-                               q_tm1=None, stream=None, mean_over=None):
+                               q_tm1=None, stream=None, mean_over=None, obs_bf16=None):
         """Stage 0: forwards, loss, head/dense backward (grads[grad_split:]); stage 1: torso
         backward (grads[:grad_split]).  mean_over: the batch mean's denominator (default
         the batch; a data-parallel share passes the nominal per-rank batch)."""
         tb = self._batch(*batch, global_min_probability=global_min_probability,
-                         mean_over=mean_over)
+                         mean_over=mean_over, obs_bf16=obs_bf16)
         out = self._outputs(q_tm1)
         check(lib().acme_dqn_forward_backward_stage(self._h, ctypes.byref(tb), ctypes.byref(out),
                                                     int(stage), stream_ptr(stream)),

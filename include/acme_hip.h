@@ -168,6 +168,13 @@ int acme_replay_sample_share(acme_replay* r, int64_t batch, uint64_t step_counte
                              double prob_scale, int64_t* slots, uint64_t* keys,
                              double* probabilities, int64_t* table_size, double* priorities,
                              void* const* out_fields, void* stream);
+/* acme_replay_sample_share with the gather and the bf16 frame copy of
+ * acme_replay_sample_gather_frames (rows [0, batch) / [batch, 2 * batch) of frames_bf16). */
+int acme_replay_sample_share_frames(acme_replay* r, int64_t batch, uint64_t step_counter,
+                                    double prob_scale, int64_t* slots, uint64_t* keys,
+                                    double* probabilities, int64_t* table_size,
+                                    double* priorities, void* const* out_fields,
+                                    uint16_t* frames_bf16, void* stream);
 
 /* Frame-deduplicated observations: rebuild `batch` stacked
  * observations out[b] = stack(frames[idx[b][0..stack-1]], axis=-1) (uint8 HWC, as

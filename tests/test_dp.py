@@ -307,3 +307,72 @@ def test_sharded_global_sampling_gpu(prefetch):
     got = d.params.cpu().numpy()
     np.testing.assert_allclose(res[0][1], got, rtol=1e-5, atol=1e-3 + 1e-6)
     assert np.mean(np.abs(res[0][1] - got) <= 1e-5 * np.abs(got) + 1e-6) > 0.98
+
+
+def _nature_dp_worker(rank, world, port, q):
+    """One rank of a Nature-CNN DP learner on a uint8 shard, run twice from the same state:
+    with the dataset's fused bf16 frame copy (acme_replay_sample_share_frames) and with the
+    learner converting the frames itself (ACME_DATASET_BF16=0)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from acme_amd import replay, specs
+    from acme_amd.adders import reverb as adders
+    from acme_amd.agents.dqn import DQNLearner
+    from acme_amd.datasets import make_reverb_dataset
+    from acme_amd.networks import DQNAtariNetwork
+    from acme_amd.utils import loggers
+    spec = specs.EnvironmentSpec(
+        observations=specs.Array((84, 84, 4), np.uint8), actions=specs.DiscreteArray(6, np.int32),
+        rewards=specs.Array((), np.float32), discounts=specs.BoundedArray((), np.float32, 0, 1))
+    rng = np.random.default_rng(50 + rank)
+    items = [(rng.integers(0, 256, (84, 84, 4), dtype=np.uint8), np.int32(k % 6),
+              np.float32(rng.normal()), np.float32(0.96 if k % 7 else 0.0),
+              rng.integers(0, 256, (84, 84, 4), dtype=np.uint8)) for k in range(48)]
+    prios = rng.uniform(0.5, 1.5, 48) * (1.0 if rank == 0 else 3.0)
+    out, copies = [], []
+    for flag in ("1", "0"):
+        os.environ["ACME_DATASET_BF16"] = flag
+        table = replay.Table(adders.DEFAULT_PRIORITY_TABLE, replay.selectors.Prioritized(0.6),
+                             replay.selectors.Fifo(), 48, replay.rate_limiters.MinSize(1),
+                             signature=adders.NStepTransitionAdder.signature(spec),
+                             seed=300 + rank, device=torch.device("cuda", 0))
+        for it, p in zip(items, prios):
+            table.insert(it, float(p))
+        table.flush()
+        server = replay.Server([table])
+        ds = make_reverb_dataset(server, batch_size=8, prefetch_size=2)
+        net = DQNAtariNetwork(6)
+        learner = DQNLearner(net, net, 0.99, 0.2, 1e-3, 100, ds, logger=loggers.NoOpLogger(),
+                             seed=0)
+        for _ in range(4):
+            learner.step()
+        torch.cuda.synchronize()
+        copies.append(getattr(learner._iterator, "last_frames_bf16", None) is not None)
+        out.append((learner.native.params.cpu().numpy(), learner.native.loss.item()))
+    os.environ.pop("ACME_DATASET_BF16")
+    q.put((rank, out, copies))
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_dp_nature_bf16_frame_copy_gpu():
+    """Sharded uint8 tables: the fused sample + gather + bf16 copy of each rank's share feeds
+    the DP learner's forward (rows [0, n) and [n, 2n) of the copy for a share of n rows);
+    the steps are bit-identical to the learner's own conversion, and replicas agree."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_nature_dp_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (out, copies)) for r, out, copies in (q.get(timeout=300) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for r in range(world):
+        (with_copy, loss_a), (without, loss_b) = res[r][0]
+        assert res[r][1] == [True, False]
+        np.testing.assert_array_equal(with_copy, without, err_msg=f"rank {r}")
+        assert loss_a == loss_b
+    np.testing.assert_array_equal(res[0][0][0][0], res[1][0][0][0])
