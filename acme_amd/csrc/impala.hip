@@ -23,7 +23,9 @@
 
 #include "common.h"
 #include "conv.h"
+#include "conv_p3.h"
 #include "gemm.h"
+#include "gemm_p3.h"
 #include "gemm_x6.h"
 #include "kernels.h"
 #include "profiler.h"
@@ -38,6 +40,8 @@ namespace {
 constexpr int kUnits = 8;        // LSTM units per block of the cell kernels
 constexpr int kNormBlocks = 256;
 constexpr int kOarSplits = 8;    // split-K of the Atari OAR projection (K = 7744 + A + 1)
+constexpr int kOarSplitsP3 = 8;  // split-K of the plane-engine OAR projection (K = 7744)
+constexpr int kP3MinRows = 64;   // learner steps of at least this many frames use the planes
 
 struct Tensor {
   std::string name;
@@ -73,6 +77,17 @@ struct acme_impala {
   // and the spin-timeout word, zeroed before every launch.
   unsigned long long* xg = nullptr;
   unsigned* tmo = nullptr;
+  // Plane path of the Atari learner step (the DQN kernels: exact three-plane bf16 MFMA):
+  // parameter planes of the torso + W_i prefix of the flat buffer, refreshed at the start
+  // of every plane step; bf16 frames; activation / gradient planes; its own split-K slab.
+  bool p3_capable = false;
+  int64_t p3_prefix = 0;  // floats of the flat buffer split into planes (torso + W_i)
+  uint16_t* wpl = nullptr;
+  uint16_t* frames = nullptr;
+  torso::Plane x1p{}, x2p{}, x3p{}, dz1p{}, dz2p{}, dz3p{}, dgp{};
+  float* pslab = nullptr;
+  bool last_p3 = false;  // the last learner step ran the plane path (debug buffers join planes)
+  int64_t last_rows = 0;
 };
 
 namespace {
@@ -720,6 +735,105 @@ inline int chunk_for(int K, int splits) {
 
 bool atari(const acme_impala* l) { return l->cfg.torso == ACME_IMPALA_TORSO_ATARI; }
 
+// ---- plane path helpers
+#define IM_P3_GEMM(name, BM, BN, WM, WN, BKV, prob, splits)                                    \
+  do {                                                                                         \
+    ACME_PROF_PEAK(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0, \
+                   gemm::p3_peak_tflops<decltype(prob)>());                                    \
+    hipError_t _e = gemm::launch_gemm_p3<BM, BN, WM, WN, BKV>(prob, splits, st);              \
+    if (_e != hipSuccess) {                                                                    \
+      set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
+      return ACME_ERR_HIP;                                                                     \
+    }                                                                                          \
+  } while (0)
+#define IM_P3WS_GEMM(name, BM, BN, WM, WN, BKV, prob, splits)                                  \
+  do {                                                                                         \
+    ACME_PROF_PEAK(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0, \
+                   gemm::p3_peak_tflops<decltype(prob)>());                                    \
+    hipError_t _e = gemm::launch_gemm_p3ws<BM, BN, WM, WN, BKV, true>(prob, splits, st);      \
+    if (_e != hipSuccess) {                                                                    \
+      set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
+      return ACME_ERR_HIP;                                                                     \
+    }                                                                                          \
+  } while (0)
+
+// Plane view of parameter tensor t in the [3][flat] parameter planes.
+torso::Plane WP(const acme_impala* l, int t) {
+  return torso::Plane{l->wpl + l->tensors[t].offset, l->flat};
+}
+gemm::PlaneSrc SRC(const torso::Plane& x, int64_t elems) {
+  return gemm::PlaneSrc{x.p, x.stride, (int32_t)(2 * elems)};
+}
+torso::PWeights torso_pw(const acme_impala* l) {
+  return torso::PWeights{WP(l, l->t_c[0]), WP(l, l->t_c[2]), WP(l, l->t_c[4]),
+                         P(l, l->params, l->t_c[1]), P(l, l->params, l->t_c[3]),
+                         P(l, l->params, l->t_c[5])};
+}
+// The plane path runs the learner steps of the Atari torso with enough frames to fill the
+// GEMMs (ACME_V_IMP3=1: the f32 engine throughout, for tests and A/B).
+bool use_p3(const acme_impala* l, int rows) {
+  return l->p3_capable && rows >= kP3MinRows && tune_variant("IMP3") != 1;
+}
+
+// gx = OAR(emb) @ W_i + b from the plane GEMM's split-K partials of feat @ W_i[0:F]: the
+// one-hot(prev a) row of W_i, tanh(prev r) times its last row and the bias are added here
+// (the embedding's last A + 1 columns), one thread per (row, 4 gate columns).
+__global__ void __launch_bounds__(256) oar_finish_kernel(const float* __restrict__ slab,
+                                                         int splits, int rows, int N,
+                                                         const float* __restrict__ wi_tail,
+                                                         const float* __restrict__ bias,
+                                                         const int32_t* __restrict__ prev_a,
+                                                         const float* __restrict__ prev_r, int A,
+                                                         float* __restrict__ gx) {
+  const int n4 = N / 4;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)rows * n4) return;
+  const int m = (int)(i / n4), c = (int)(i - (int64_t)m * n4);
+  const int64_t cnt = (int64_t)rows * N;
+  f32x4 v = reinterpret_cast<const f32x4*>(slab)[i];
+  for (int s = 1; s < splits; ++s) v += reinterpret_cast<const f32x4*>(slab + s * cnt)[i];
+  const int a = prev_a[m];
+  const float tr = tanhf(prev_r[m]);
+  const f32x4 wa = reinterpret_cast<const f32x4*>(wi_tail + (size_t)a * N)[c];
+  const f32x4 wr = reinterpret_cast<const f32x4*>(wi_tail + (size_t)A * N)[c];
+  const f32x4 b = reinterpret_cast<const f32x4*>(bias)[c];
+  f32x4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = ((v[j] + wa[j]) + tr * wr[j]) + b[j];
+  reinterpret_cast<f32x4*>(gx)[i] = o;
+}
+
+// The last A + 1 rows of dW_i (the one-hot and tanh(prev r) embedding columns):
+// dW[F + j][n] = sum over rows with prev_a == j of dgates[m][n], dW[F + A][n] = sum of
+// tanh(prev_r[m]) dgates[m][n].  Block (n / 64, j): lane = column, wave w takes rows
+// m = w (mod 4); the four wave partials are summed in a fixed order through LDS.
+__global__ void __launch_bounds__(256) oar_wgrad_tail_kernel(const float* __restrict__ dg,
+                                                             int rows, int N,
+                                                             const int32_t* __restrict__ prev_a,
+                                                             const float* __restrict__ prev_r,
+                                                             int A, float* __restrict__ dw_tail) {
+  __shared__ float part[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + lane, j = blockIdx.y;
+  float acc = 0.f;
+  if (n < N) {
+    if (j < A) {
+#pragma unroll 4
+      for (int m = wave; m < rows; m += 4) {
+        const float g = dg[(size_t)m * N + n];
+        acc += prev_a[m] == j ? g : 0.f;
+      }
+    } else {
+#pragma unroll 4
+      for (int m = wave; m < rows; m += 4) acc = fmaf(tanhf(prev_r[m]), dg[(size_t)m * N + n], acc);
+    }
+  }
+  part[wave][lane] = acc;
+  __syncthreads();
+  if (wave == 0 && n < N)
+    dw_tail[(size_t)j * N + n] = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+}
+
 torso::Weights torso_w(const acme_impala* l) {
   return torso::Weights{P(l, l->params, l->t_c[0]), P(l, l->params, l->t_c[1]),
                         P(l, l->params, l->t_c[2]), P(l, l->params, l->t_c[3]),
@@ -729,10 +843,42 @@ torso::Weights torso_w(const acme_impala* l) {
 // Network forward over rows = B*T frames: features, OAR projection, T LSTM steps, head.
 int network_forward(acme_impala* l, const void* obs, const int32_t* prev_a, const float* prev_r,
                     const float* h0, const float* c0, int64_t state_stride, int B, int T,
-                    hipStream_t st) {
+                    hipStream_t st, bool p3 = false) {
   const int rows = B * T, H = l->H, A = l->A;
   const float* feat;
-  if (atari(l)) {
+  if (p3) {
+    // Parameter planes of the torso + W_i (the only plane operands), the bf16 frames,
+    // the plane torso, then feat @ W_i[0:F] on the plane engine and the embedding tail.
+    int rc;
+    {
+      ACME_PROF("impala_planes", st, 0.0, 10.0 * (double)l->p3_prefix);
+      rc = launch_split_planes(l->params, l->p3_prefix, l->wpl, l->flat, st);
+      if (rc != ACME_OK) return rc;
+    }
+    {
+      ACME_PROF("impala_frames_bf16", st, 0.0, 3.0 * (double)rows * torso::kObsBytes);
+      rc = launch_frames_bf16(static_cast<const uint8_t*>(obs), static_cast<const uint8_t*>(obs),
+                              rows, rows, torso::kObsBytes, l->frames, st);
+      if (rc != ACME_OK) return rc;
+    }
+    rc = torso::forward_p3(torso_pw(l), torso::Frames{l->frames}, rows,
+                           torso::PActs{l->x1p, l->x2p, l->x3p}, st);
+    if (rc != ACME_OK) return rc;
+    const int F = l->F, N = 4 * H;
+    P3DenseFwd p;
+    p.M = rows; p.N = N; p.K = F; p.k_chunk = chunk_for(F, kOarSplitsP3);
+    p.a_src = SRC(l->x3p, (int64_t)rows * F); p.ldx = F;
+    p.b_src = SRC(WP(l, l->t_wi), (int64_t)F * N); p.slab = l->pslab;
+    IM_P3WS_GEMM("impala_oar_fwd", 128, 128, 2, 2, 32, p, kOarSplitsP3);
+    {
+      ACME_PROF("impala_oar_reduce", st, 0.0, 4.0 * (kOarSplitsP3 + 1) * (double)rows * N);
+      const int64_t n4 = (int64_t)rows * N / 4;
+      oar_finish_kernel<<<(unsigned)ceil_div(n4, 256), 256, 0, st>>>(
+          l->pslab, kOarSplitsP3, rows, N, P(l, l->params, l->t_wi) + (size_t)F * N,
+          P(l, l->params, l->t_b), prev_a, prev_r, A, l->gx);
+      IM_CHECK();
+    }
+  } else if (atari(l)) {
     int rc = torso::forward(torso_w(l), true, obs, obs, rows, rows,
                             torso::Acts{l->x1, l->x2, l->x3}, st);
     if (rc != ACME_OK) return rc;
@@ -740,7 +886,7 @@ int network_forward(acme_impala* l, const void* obs, const int32_t* prev_a, cons
   } else {
     feat = static_cast<const float*>(obs);
   }
-  {
+  if (!p3) {
     OarFwd p;
     p.M = rows; p.N = 4 * H; p.K = l->D;
     p.x = Oar{feat, l->F, A, prev_a, prev_r};
@@ -813,8 +959,11 @@ int impala_step_impl(acme_impala* l, const acme_sequence_batch* bt, float* metri
                      hipStream_t st) {
   const int B = (int)bt->batch, T = (int)bt->sequence_length, rows = B * T;
   const int H = l->H, A = l->A;
+  const bool p3 = atari(l) && use_p3(l, rows);
+  l->last_p3 = p3;
+  l->last_rows = rows;
   int rc = network_forward(l, bt->observation, bt->prev_action, bt->prev_reward, bt->h0, bt->c0,
-                           bt->state_stride, B, T, st);
+                           bt->state_stride, B, T, st, p3);
   if (rc != ACME_OK) return rc;
   {
     ACME_PROF("impala_loss", st, 0.0, 0.0);
@@ -873,6 +1022,45 @@ int impala_step_impl(acme_impala* l, const acme_sequence_batch* bt, float* metri
     w.h = l->h; w.h0 = bt->h0; w.h0_stride = bt->state_stride; w.T = T; w.dz = l->dgates;
     w.out = Pm(l, gr, l->t_wh);
     IM_GEMM("impala_wh_wgrad", 32, 32, 1, 1, 4, w, 1);
+  }
+  if (p3) {  // W_i, b and the embedding gradient on the plane engine, then the plane torso
+    const int F = l->F, N = 4 * H;
+    {
+      ACME_PROF("impala_dgates_planes", st, 0.0, 10.0 * (double)rows * N);
+      rc = launch_split_planes(l->dgates, (int64_t)rows * N, l->dgp.p, l->dgp.stride, st);
+      if (rc != ACME_OK) return rc;
+    }
+    {
+      P3DenseWgrad p;
+      p.M = F; p.N = N; p.K = rows; p.k_chunk = rows;
+      p.a_src = SRC(l->x3p, (int64_t)rows * F); p.ldx = F;
+      p.b_src = SRC(l->dgp, (int64_t)rows * N); p.out = Pm(l, gr, l->t_wi);
+      p.bias_out = Pm(l, gr, l->t_b);
+      IM_P3_GEMM("impala_wi_wgrad", 128, 128, 2, 2, 16, p, 1);
+    }
+    {
+      ACME_PROF("impala_wi_wgrad_tail", st, 0.0, 4.0 * (double)rows * N);
+      oar_wgrad_tail_kernel<<<dim3((unsigned)ceil_div(N, 64), (unsigned)(A + 1)), 256, 0, st>>>(
+          l->dgates, rows, N, bt->prev_action, bt->prev_reward, A,
+          Pm(l, gr, l->t_wi) + (size_t)F * N);
+      IM_CHECK();
+    }
+    {
+      P3DenseDgrad p;
+      p.M = rows; p.N = F; p.K = N; p.k_chunk = N;
+      p.a_src = SRC(l->dgp, (int64_t)rows * N);
+      p.b_src = SRC(WP(l, l->t_wi), (int64_t)F * N);
+      p.xprev = CPlanes{l->x3p.p, l->x3p.stride}; p.ldx = F;
+      p.dx = Planes{l->dz3p.p, l->dz3p.stride};
+      IM_P3WS_GEMM("impala_feat_dgrad", 128, 128, 2, 2, 32, p, 1);
+    }
+    torso::Grads g{Pm(l, gr, l->t_c[0]), Pm(l, gr, l->t_c[1]), Pm(l, gr, l->t_c[2]),
+                   Pm(l, gr, l->t_c[3]), Pm(l, gr, l->t_c[4]), Pm(l, gr, l->t_c[5])};
+    rc = torso::backward_p3(torso_pw(l), g, torso::Frames{l->frames}, rows,
+                            torso::PActs{l->x1p, l->x2p, l->x3p}, l->dz3p, l->dz2p, l->dz1p,
+                            l->pslab, st);
+    if (rc != ACME_OK) return rc;
+  } else {
     const float* feat = atari(l) ? l->x3 : static_cast<const float*>(bt->observation);
     OarWgrad o;
     o.M = l->D; o.N = 4 * H; o.K = rows; o.k_chunk = rows;
@@ -881,7 +1069,7 @@ int impala_step_impl(acme_impala* l, const acme_sequence_batch* bt, float* metri
     if (atari(l)) IM_GEMM("impala_wi_wgrad", 128, 128, 2, 2, 1, o, 1);
     else IM_GEMM("impala_wi_wgrad", 32, 32, 1, 1, 4, o, 1);
   }
-  if (atari(l)) {  // embedding features -> conv3 dZ -> torso backward
+  if (!p3 && atari(l)) {  // embedding features -> conv3 dZ -> torso backward
     DenseDgrad<true> d;
     d.M = rows; d.N = l->F; d.K = 4 * H; d.k_chunk = 4 * H;
     d.dz = l->dgates; d.w = P(l, l->params, l->t_wi); d.xprev = l->x3; d.ldx = l->F;
@@ -993,6 +1181,29 @@ int acme_impala_create(const acme_impala_config* cfg, acme_impala** out) {
       (rc = dev_alloc(l, &l->metrics_tmp, 4)) || (rc = dev_alloc(l, &l->norms, 2)) ||
       (rc = dev_alloc(l, &l->xg, (int64_t)2 * B * H)) || (rc = dev_alloc(l, &l->tmo, 4)))
     return fail(rc);
+  // Plane path (Atari torso): each operand plane is addressed through a 31-bit byte range,
+  // so the bf16 frames of one step bound it (R < 38,000 frames); larger unrolls stay f32.
+  if (cfg->torso == ACME_IMPALA_TORSO_ATARI && R * torso::kObsBytes * 2 < (int64_t)INT32_MAX &&
+      R >= kP3MinRows) {
+    l->p3_capable = true;
+    l->p3_prefix = align64(l->tensors[l->t_wi].offset + l->tensors[l->t_wi].numel);
+    auto plane = [&](torso::Plane* x, int64_t count) {
+      const int64_t stride = align64(count);
+      uint16_t* q = nullptr;
+      int r = dev_alloc(l, &q, 3 * stride);
+      *x = torso::Plane{q, stride};
+      return r;
+    };
+    if ((rc = dev_alloc(l, &l->wpl, 3 * l->flat)) ||
+        (rc = dev_alloc(l, &l->frames, R * torso::kObsBytes)) ||
+        (rc = plane(&l->x1p, R * torso::kX1)) || (rc = plane(&l->x2p, R * torso::kFlat)) ||
+        (rc = plane(&l->x3p, R * torso::kFlat)) || (rc = plane(&l->dz1p, R * torso::kX1)) ||
+        (rc = plane(&l->dz2p, R * torso::kFlat)) || (rc = plane(&l->dz3p, R * torso::kFlat)) ||
+        (rc = plane(&l->dgp, R * 4 * H)) ||
+        (rc = dev_alloc(l, &l->pslab, std::max<int64_t>(torso::wgrad_slab_floats_p3(),
+                                                        (int64_t)kOarSplitsP3 * R * 4 * H))))
+      return fail(rc);
+  }
   if (hipMemset(l->dev_step, 0, sizeof(int64_t)) != hipSuccess ||
       hipMemset(l->tmo, 0, 4 * sizeof(unsigned)) != hipSuccess)
     return fail((set_error("hipMemset failed"), ACME_ERR_HIP));
@@ -1101,6 +1312,22 @@ int acme_impala_debug_buffer(const acme_impala* l, const char* name, const float
   };
   for (const Item& it : items)
     if (it.p && strcmp(it.n, name) == 0) {
+      if (l->last_p3) {  // the plane path keeps the torso activations as planes: join them
+        const struct {
+          const char* n;
+          torso::Plane pl;
+          int64_t per_row;
+        } ptab[] = {{"x1", l->x1p, torso::kX1}, {"x2", l->x2p, torso::kFlat},
+                    {"x3", l->x3p, torso::kFlat}};
+        for (const auto& q : ptab)
+          if (strcmp(q.n, name) == 0) {
+            ACME_HIP_TRY(hipDeviceSynchronize());
+            int rc = launch_join_planes(q.pl.p, q.pl.stride, l->last_rows * q.per_row,
+                                        const_cast<float*>(it.p), 0);
+            if (rc != ACME_OK) return rc;
+            ACME_HIP_TRY(hipDeviceSynchronize());
+          }
+      }
       *out = it.p;
       *count = it.c;
       return ACME_OK;

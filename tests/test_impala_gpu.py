@@ -146,16 +146,23 @@ def test_flat_torso_step_matches_oracle(B, T, H):
     _compare(cfg, n, params, b)
 
 
-@pytest.mark.parametrize("B,T", [(2, 5), (16, 20)])
-def test_atari_torso_step_matches_oracle(B, T):
+@pytest.mark.parametrize("B,T,f32", [(2, 5, False), (16, 20, False), (16, 20, True)])
+def test_atari_torso_step_matches_oracle(B, T, f32):
     """IMPALAAtariNetwork at full width (LSTM 256, head 256, 18 actions); (16, 20) is the
-    configs[3] learner batch (agents/tf/impala/agent.py:50, 20-step rollouts)."""
+    configs[3] learner batch (agents/tf/impala/agent.py:50, 20-step rollouts).  Steps of at
+    least 64 frames run the torso and the W_i projection / gradients on the exact plane
+    engine (the DQN kernels); f32: the f32 engine throughout (ACME_V_IMP3=1)."""
+    from acme_amd._lib import lib
     cfg = O.IMPALAConfig(num_actions=18, torso="atari", entropy_cost=0.01, baseline_cost=0.5)
     n = _native(cfg, B, T)
     params = _params(cfg, 3)
     n.set_params(params)
     b = _batch(cfg, B, T, 4)
-    _run(n, b)
+    lib().acme_tune_set(b"IMP3", 1 if f32 else 0)
+    try:
+        _run(n, b)
+    finally:
+        lib().acme_tune_set(b"IMP3", 0)
     _compare(cfg, n, params, b)
 
 
