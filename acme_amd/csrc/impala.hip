@@ -273,6 +273,7 @@ constexpr int kRowChunk = 16;
 // previous step's h otherwise).  kFwdUnits units per block (16 gate columns); the
 // block's W_h columns are staged through LDS in k-chunks with float4 loads.
 constexpr int kFwdUnits = 4;
+constexpr int kFwdPre = 4;  // float4 loads per thread of h_prev / W_h issued up front
 
 __global__ void __launch_bounds__(256) lstm_fwd_step_kernel(
     const float* __restrict__ gx, const float* __restrict__ wh, const float* __restrict__ hp,
@@ -293,24 +294,64 @@ __global__ void __launch_bounds__(256) lstm_fwd_step_kernel(
   const float cprev_pre = cell_thread ? cp[(size_t)(threadIdx.x / kFwdUnits) * cp_stride + u0 +
                                            threadIdx.x % kFwdUnits]
                                       : 0.f;
-  for (int e = threadIdx.x; e < B * H / 4; e += blockDim.x) {
-    const int b = e / (H / 4), k = 4 * (e % (H / 4));
-    *reinterpret_cast<f32x4*>(hs + (size_t)b * H + k) =
-        *reinterpret_cast<const f32x4*>(hp + (size_t)b * hp_stride + k);
-  }
-  for (int e = threadIdx.x; e < H * 4; e += blockDim.x) {
-    const int k = e / 4, q = e % 4;
-    *reinterpret_cast<f32x4*>(ws + (size_t)k * NC + q * kFwdUnits) =
-        *reinterpret_cast<const f32x4*>(wh + (size_t)k * 4 * H + q * H + u0);
+  const int oi = threadIdx.x / NC, occ = threadIdx.x % NC;
+  auto gx_at = [&](int ob) {
+    return ob < B ? gx[((size_t)ob * T + t) * 4 * H + (occ / kFwdUnits) * H + u0 +
+                       (occ % kFwdUnits)]
+                  : 0.f;
+  };
+  const float gx0 = gx_at(oi);  // the first pass's gx term, in flight with the staging
+  const int nh4 = B * H / 4, nw4 = H * 4;
+  if (nh4 <= 256 * kFwdPre && nw4 <= 256 * kFwdPre) {
+    // Up to kFwdPre float4 of h_prev and of W_h per thread: every load issued (clamped
+    // addresses, no branches around them) before the first LDS store, one latency.
+    f32x4 hv[kFwdPre], wv[kFwdPre];
+#pragma unroll
+    for (int q = 0; q < kFwdPre; ++q) {
+      const int e = min((int)threadIdx.x + 256 * q, nh4 - 1);
+      const int b = e / (H / 4), k = 4 * (e % (H / 4));
+      hv[q] = *reinterpret_cast<const f32x4*>(hp + (size_t)b * hp_stride + k);
+    }
+#pragma unroll
+    for (int q = 0; q < kFwdPre; ++q) {
+      const int e = min((int)threadIdx.x + 256 * q, nw4 - 1);
+      const int k = e / 4, g = e % 4;
+      wv[q] = *reinterpret_cast<const f32x4*>(wh + (size_t)k * 4 * H + g * H + u0);
+    }
+#pragma unroll
+    for (int q = 0; q < kFwdPre; ++q) {
+      const int e = (int)threadIdx.x + 256 * q;
+      if (e < nh4) {
+        const int b = e / (H / 4), k = 4 * (e % (H / 4));
+        *reinterpret_cast<f32x4*>(hs + (size_t)b * H + k) = hv[q];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kFwdPre; ++q) {
+      const int e = (int)threadIdx.x + 256 * q;
+      if (e < nw4) {
+        const int k = e / 4, g = e % 4;
+        *reinterpret_cast<f32x4*>(ws + (size_t)k * NC + g * kFwdUnits) = wv[q];
+      }
+    }
+  } else {
+    for (int e = threadIdx.x; e < nh4; e += blockDim.x) {
+      const int b = e / (H / 4), k = 4 * (e % (H / 4));
+      *reinterpret_cast<f32x4*>(hs + (size_t)b * H + k) =
+          *reinterpret_cast<const f32x4*>(hp + (size_t)b * hp_stride + k);
+    }
+    for (int e = threadIdx.x; e < nw4; e += blockDim.x) {
+      const int k = e / 4, g = e % 4;
+      *reinterpret_cast<f32x4*>(ws + (size_t)k * NC + g * kFwdUnits) =
+          *reinterpret_cast<const f32x4*>(wh + (size_t)k * 4 * H + g * H + u0);
+    }
   }
   __syncthreads();
   const int c = threadIdx.x % NC, sl = threadIdx.x / NC;
   for (int b0 = 0; b0 < B; b0 += kRowChunk) {
-    // The gx term of this thread's reduction output, loaded before the mat-vec.
-    const int oi = threadIdx.x / NC, occ = threadIdx.x % NC, ob = b0 + oi;
-    const float gxv = ob < B ? gx[((size_t)ob * T + t) * 4 * H + (occ / kFwdUnits) * H + u0 +
-                                  (occ % kFwdUnits)]
-                             : 0.f;
+    // The gx term of this thread's reduction output.
+    const int ob = b0 + oi;
+    const float gxv = b0 == 0 ? gx0 : gx_at(ob);
     float acc[kRowChunk];
 #pragma unroll
     for (int i = 0; i < kRowChunk; ++i) acc[i] = 0.f;
