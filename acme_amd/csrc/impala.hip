@@ -355,11 +355,15 @@ __global__ void __launch_bounds__(256) lstm_fwd_step_kernel(
     float acc[kRowChunk];
 #pragma unroll
     for (int i = 0; i < kRowChunk; ++i) acc[i] = 0.f;
+    // Rows past B read row B - 1 (clamped, no branch around the LDS reads: a branch per
+    // row serialised every read behind its own wait); their sums are never stored.
+    int roff[kRowChunk];
+#pragma unroll
+    for (int i = 0; i < kRowChunk; ++i) roff[i] = min(b0 + i, B - 1) * H;
     for (int k = sl; k < H; k += KS) {
       const float w = ws[k * NC + c];
 #pragma unroll
-      for (int i = 0; i < kRowChunk; ++i)
-        if (b0 + i < B) acc[i] = fmaf(hs[(size_t)(b0 + i) * H + k], w, acc[i]);
+      for (int i = 0; i < kRowChunk; ++i) acc[i] = fmaf(hs[roff[i] + k], w, acc[i]);
     }
 #pragma unroll
     for (int i = 0; i < kRowChunk; ++i) red[(sl * kRowChunk + i) * NC + c] = acc[i];
@@ -497,11 +501,13 @@ __global__ void __launch_bounds__(256) lstm_fwd_persistent_kernel(
       float acc[kRowChunk];
 #pragma unroll
       for (int i = 0; i < kRowChunk; ++i) acc[i] = 0.f;
+      int roff[kRowChunk];  // clamped rows, as lstm_fwd_step_kernel
+#pragma unroll
+      for (int i = 0; i < kRowChunk; ++i) roff[i] = min(b0 + i, B - 1) * H;
       for (int k = sl; k < H; k += KS) {
         const float w = ws[k * NC + c];
 #pragma unroll
-        for (int i = 0; i < kRowChunk; ++i)
-          if (b0 + i < B) acc[i] = fmaf(hs[(size_t)(b0 + i) * H + k], w, acc[i]);
+        for (int i = 0; i < kRowChunk; ++i) acc[i] = fmaf(hs[roff[i] + k], w, acc[i]);
       }
 #pragma unroll
       for (int i = 0; i < kRowChunk; ++i) red[(sl * kRowChunk + i) * NC + c] = acc[i];
@@ -553,42 +559,78 @@ __global__ void __launch_bounds__(256) lstm_bwd_step_kernel(
   const int u0 = blockIdx.x * kUnits;
   const int sl = threadIdx.x % KS, u = threadIdx.x / KS;
   const float* w = wh + (size_t)(u0 + u) * 4 * H;
+  // The cell-gradient operands of this thread's (unit, row) in the first row pass, loaded
+  // before the mat-vec so that their latency overlaps it (clamped addresses, used only by
+  // the threads and rows that own them).
+  struct CellIn {
+    float ig, fg, gg, og, cn, cprev, dh, dc;
+  };
+  auto cell_in = [&](int b0) {
+    const int uu = threadIdx.x / kRowChunk, i = threadIdx.x % kRowChunk;
+    const int b = min(b0 + i, B - 1), j = u0 + min(uu, kUnits - 1);
+    const size_t row = (size_t)b * T + t;
+    const float* g = gates + row * 4 * H;
+    CellIn x;
+    x.ig = g[j]; x.fg = g[H + j]; x.gg = g[2 * H + j]; x.og = g[3 * H + j];
+    x.cn = c_all[row * H + j];
+    x.cprev = t > 0 ? c_all[(row - 1) * H + j] : c0[(size_t)b * c0_stride + j];
+    x.dh = dh_head[row * H + j];
+    x.dc = dc_carry[(size_t)b * H + j];
+    return x;
+  };
+  const CellIn first = cell_in(0);
   for (int b0 = 0; b0 < B; b0 += kRowChunk) {
     float acc[kRowChunk];
 #pragma unroll
     for (int i = 0; i < kRowChunk; ++i) acc[i] = 0.f;
     if (t + 1 < T) {
-      for (int kc = 0; kc < 4 * H; kc += KC) {
-        // Stage dgates[t+1][b0 .. b0+15][kc .. kc+255] with float4 loads (4 per thread,
-        // all in flight) and this thread's 8 W_h values, then compute from LDS.
-        float wv[KC / KS];
+      // Stage dgates[t+1][b0 .. b0+15][kc .. kc+255] with float4 loads (4 per thread) and
+      // this thread's 8 W_h values; chunk kc + KC is loaded into registers before chunk kc
+      // is computed from LDS, so one load latency is exposed per step instead of one per
+      // chunk.  Loads past B or 4H read clamped addresses and are replaced by zeros
+      // (selects, not branches around the loads).
+      constexpr int NQ = kRowChunk * KC / 4 / 256;
+      float wv[KC / KS], wn[KC / KS];
+      f32x4 v4[NQ], vn[NQ];
+      auto load = [&](int kc, float (&wr)[KC / KS], f32x4 (&vr)[NQ]) {
 #pragma unroll
         for (int j = 0; j < KC / KS; ++j) {
           const int k = kc + sl + KS * j;
-          wv[j] = k < 4 * H ? w[k] : 0.f;
+          const float x = w[min(k, 4 * H - 1)];
+          wr[j] = k < 4 * H ? x : 0.f;
         }
-        f32x4 v4[kRowChunk * KC / 4 / 256];
 #pragma unroll
-        for (int q = 0; q < kRowChunk * KC / 4 / 256; ++q) {
+        for (int q = 0; q < NQ; ++q) {
           const int e = (int)threadIdx.x + 256 * q;  // float4 index in the chunk
           const int i = e / (KC / 4), k = kc + 4 * (e % (KC / 4));
-          v4[q] = (b0 + i < B && k < 4 * H)
-                      ? *reinterpret_cast<const f32x4*>(dgates + ((size_t)(b0 + i) * T + t + 1) * 4 * H + k)
-                      : f32x4{0.f, 0.f, 0.f, 0.f};
+          const bool ok = b0 + i < B && k < 4 * H;
+          const f32x4 x = *reinterpret_cast<const f32x4*>(
+              dgates + ((size_t)min(b0 + i, B - 1) * T + t + 1) * 4 * H + min(k, 4 * H - 4));
+          vr[q] = ok ? x : f32x4{0.f, 0.f, 0.f, 0.f};
         }
+      };
+      load(0, wv, v4);
+      for (int kc = 0; kc < 4 * H; kc += KC) {
         __syncthreads();  // previous chunk fully consumed
 #pragma unroll
-        for (int q = 0; q < kRowChunk * KC / 4 / 256; ++q) {
+        for (int q = 0; q < NQ; ++q) {
           const int e = (int)threadIdx.x + 256 * q;
           *reinterpret_cast<f32x4*>(&ds[e / (KC / 4)][4 * (e % (KC / 4))]) = v4[q];
         }
         __syncthreads();
+        // The next chunk (the last one again at the end: no branch around the loads, whose
+        // join would wait for them before the compute below).
+        load(kc + KC < 4 * H ? kc + KC : kc, wn, vn);
 #pragma unroll
         for (int j = 0; j < KC / KS; ++j) {
           const int k = sl + KS * j;
 #pragma unroll
           for (int i = 0; i < kRowChunk; ++i) acc[i] = fmaf(ds[i][k], wv[j], acc[i]);
         }
+#pragma unroll
+        for (int j = 0; j < KC / KS; ++j) wv[j] = wn[j];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) v4[q] = vn[q];
       }
     }
 #pragma unroll
@@ -601,13 +643,12 @@ __global__ void __launch_bounds__(256) lstm_bwd_step_kernel(
         for (int s2 = 0; s2 < KS; ++s2) dhn += red[uu][i][s2];
         const int j = u0 + uu;
         const size_t row = (size_t)b * T + t;
-        const float* g = gates + row * 4 * H;
-        const float ig = g[j], fg = g[H + j], gg = g[2 * H + j], og = g[3 * H + j];
-        const float cn = c_all[row * H + j];
-        const float cprev = t > 0 ? c_all[(row - 1) * H + j] : c0[(size_t)b * c0_stride + j];
+        const CellIn x = b0 == 0 ? first : cell_in(b0);
+        const float ig = x.ig, fg = x.fg, gg = x.gg, og = x.og;
+        const float cn = x.cn, cprev = x.cprev;
         const float tc = tanhf(cn);
-        const float dh = dh_head[row * H + j] + dhn;
-        const float dc = dc_carry[(size_t)b * H + j] + dh * og * (1.f - tc * tc);
+        const float dh = x.dh + dhn;
+        const float dc = x.dc + dh * og * (1.f - tc * tc);
         float* dg = dgates + row * 4 * H;
         dg[j] = dc * gg * ig * (1.f - ig);
         dg[H + j] = dc * cprev * fg * (1.f - fg);
