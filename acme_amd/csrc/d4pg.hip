@@ -420,24 +420,40 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const LnBwdArgs a) {
   const float invH = 1.f / (float)a.H;
   float g[kRows][C], xh[kRows][C], dyv[kRows][C];
   float s[2 * kRows];
+  // Every load of the block is issued before the first use: clamped addresses and selects
+  // instead of branches around the loads (a branch per load serialises them).  Invalid
+  // entries contribute exact zeros to the sums.
+  const int last = a.rows - 1;
+  const bool has_dpg = r0 + kRows - 1 >= a.ce_rows && r0 < a.rows;  // uniform per block
+  float w1v[C][ACME_D4PG_MAX_ACT];
+  if (has_dpg) {
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int k = 0; k < ACME_D4PG_MAX_ACT; ++k)
+        w1v[c][k] = a.w1[(size_t)(a.act_off + min(k, a.A - 1)) * a.H + min(tid + 256 * c, a.H - 1)];
+  }
+  float sc[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) sc[c] = a.scale[min(tid + 256 * c, a.H - 1)];
 #pragma unroll
   for (int r = 0; r < kRows; ++r) {
     const int row = r0 + r;
     const bool ok = row < a.rows;
-    const float mu = ok ? a.mean[row] : 0.f, rs = ok ? a.rstd[row] : 0.f;
+    const float mu0 = a.mean[min(row, last)], rs0 = a.rstd[min(row, last)];
+    const float mu = ok ? mu0 : 0.f, rs = ok ? rs0 : 0.f;
     s[2 * r] = s[2 * r + 1] = 0.f;
 #pragma unroll
     for (int c = 0; c < C; ++c) {
       const int j = tid + 256 * c;
-      g[r][c] = xh[r][c] = dyv[r][c] = 0.f;
-      if (ok && j < a.H) {
-        const size_t idx = (size_t)row * a.H + j;
-        dyv[r][c] = a.dy[idx];
-        xh[r][c] = (a.z[idx] - mu) * rs;
-        g[r][c] = dyv[r][c] * a.scale[j];
-        s[2 * r] += g[r][c];
-        s[2 * r + 1] = fmaf(g[r][c], xh[r][c], s[2 * r + 1]);
-      }
+      const bool v = ok && j < a.H;
+      const size_t idx = (size_t)min(row, last) * a.H + min(j, a.H - 1);
+      const float dy = a.dy[idx], z = a.z[idx];
+      dyv[r][c] = v ? dy : 0.f;
+      xh[r][c] = v ? (z - mu) * rs : 0.f;
+      g[r][c] = v ? dy * sc[c] : 0.f;
+      s[2 * r] += g[r][c];
+      s[2 * r + 1] = fmaf(g[r][c], xh[r][c], s[2 * r + 1]);
     }
   }
   block_sum256<2 * kRows>(s, red);
@@ -470,7 +486,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const LnBwdArgs a) {
       } else {
 #pragma unroll
         for (int k = 0; k < ACME_D4PG_MAX_ACT; ++k)
-          if (k < a.A) dqp[r][k] = fmaf(dz, a.w1[(size_t)(a.act_off + k) * a.H + j], dqp[r][k]);
+          dqp[r][k] = k < a.A ? fmaf(dz, w1v[c][k], dqp[r][k]) : dqp[r][k];
       }
     }
   }
