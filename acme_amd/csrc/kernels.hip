@@ -487,6 +487,39 @@ __global__ void __launch_bounds__(256) fc_head1024_kernel(
   }
 }
 
+// dZ of 8 consecutive hidden units k0 .. k0 + 7 of one row (all in the value half or all in
+// the advantage half: H % 8 == 0): k < H: g_b wv[k]; k >= H: dadv_i = g_b (1[i == a_b] -
+// 1/A), dh_k = sum_i dadv_i wa[k][i] in order i = 0 .. A-1; masked by hid > 0.  The eight
+// sums advance together, so each step over i issues eight independent loads (one branch per
+// thread, outside the loads).
+__device__ __forceinline__ void head_dz8(int k0, int H, int A, float gb, int ab, float inv_a,
+                                         const float* __restrict__ wv,
+                                         const float* __restrict__ wa, const float (&hv)[8],
+                                         float (&d)[8]) {
+  float v[8];
+  if (k0 < H) {
+    const f32x4 w0 = reinterpret_cast<const f32x4*>(wv + k0)[0];
+    const f32x4 w1 = reinterpret_cast<const f32x4*>(wv + k0)[1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[j] = gb * w0[j];
+      v[4 + j] = gb * w1[j];
+    }
+  } else {
+    const float* rows = wa + (size_t)(k0 - H) * A;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = 0.f;
+#pragma unroll 6
+    for (int i = 0; i < A; ++i) {
+      const float c = gb * ((i == ab ? 1.f : 0.f) - inv_a);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = fmaf(c, rows[(size_t)j * A + i], v[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) d[j] = hv[j] > 0.f ? v[j] : 0.f;
+}
+
 // Loss + head dZ in one launch (plane path).  Blocks [0, nb) each write the dZ planes of
 // 256 / (2H / 8) rows (8 units per thread, as head_dz_planes_kernel), recomputing g_b of
 // their rows with loss_row (the loss kernel's bits); the last block is the loss kernel
@@ -542,21 +575,7 @@ __global__ void __launch_bounds__(256) dqn_loss_head_dz_kernel(
   const f32x4 h0 = reinterpret_cast<const f32x4*>(hr)[0], h1 = reinterpret_cast<const f32x4*>(hr)[1];
   const float hv[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
   float d[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int k = k0 + j;
-    float v;
-    if (k < H) {
-      v = gb * wv[k];
-    } else {
-      const float* row = wa + (size_t)(k - H) * A;
-      float s = 0.f;
-#pragma unroll 6
-      for (int i = 0; i < A; ++i) s = fmaf(gb * ((i == ab ? 1.f : 0.f) - inv_a), row[i], s);
-      v = s;
-    }
-    d[j] = hv[j] > 0.f ? v : 0.f;
-  }
+  head_dz8(k0, H, A, gb, ab, inv_a, wv, wa, hv, d);
   uint32_t ph[4], pm[4], pl[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -590,22 +609,7 @@ __global__ void __launch_bounds__(256) head_dz_planes_kernel(
   const f32x4 h0 = reinterpret_cast<const f32x4*>(hr)[0], h1 = reinterpret_cast<const f32x4*>(hr)[1];
   const float hv[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
   float d[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int k = k0 + j;
-    float v;
-    if (k < H) {
-      v = gb * wv[k];
-    } else {
-      // dadv_i = g_b (1[i == a_b] - 1/A);  dh_k = sum_i dadv_i wa[k][i] (fixed order).
-      const float* row = wa + (size_t)(k - H) * A;
-      float s = 0.f;
-#pragma unroll 6
-      for (int i = 0; i < A; ++i) s = fmaf(gb * ((i == ab ? 1.f : 0.f) - inv_a), row[i], s);
-      v = s;
-    }
-    d[j] = hv[j] > 0.f ? v : 0.f;
-  }
+  head_dz8(k0, H, A, gb, ab, inv_a, wv, wa, hv, d);
   uint32_t ph[4], pm[4], pl[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -898,7 +902,8 @@ int launch_dqn_loss_head_dz(const LossArgs& args, const float* h, int H, const f
                             const float* wa, uint16_t* planes, int64_t pstride, hipStream_t st) {
   ACME_CHECK_ARG(args.B >= 1 && args.A >= 1 && h && wv && wa && planes, "bad loss / head dZ args");
   const int per = 2 * H / 8;
-  ACME_CHECK_ARG(H % 4 == 0 && per >= 32 && 256 % per == 0, "hidden size %d: 2H/8 must divide 256", H);
+  ACME_CHECK_ARG(H % 8 == 0 && per >= 32 && 256 % per == 0, "hidden size %d: 2H/8 must divide 256", H);
+  ACME_CHECK_ARG(reinterpret_cast<uintptr_t>(wv) % 16 == 0, "wv must be 16-byte aligned");
   const int64_t nb = ceil_div((int64_t)args.B * per, 256);
   dqn_loss_head_dz_kernel<<<(unsigned)(nb + 1), 256, 0, st>>>(args, h, H, wv, wa, planes, pstride);
   ACME_LAUNCH_CHECK();
@@ -908,7 +913,8 @@ int launch_dqn_loss_head_dz(const LossArgs& args, const float* h, int H, const f
 int launch_head_dz_planes(const float* h, const float* g, const int32_t* a, int B, int H, int A,
                           const float* wv, const float* wa, uint16_t* planes, int64_t pstride,
                           hipStream_t st) {
-  ACME_CHECK_ARG((2 * H) % 8 == 0 && pstride % 8 == 0, "bad head_dz shape");
+  ACME_CHECK_ARG(H % 8 == 0 && pstride % 8 == 0 && reinterpret_cast<uintptr_t>(wv) % 16 == 0,
+                 "bad head_dz shape");
   const int64_t n = (int64_t)B * (2 * H / 8);
   head_dz_planes_kernel<<<(unsigned)ceil_div(n, 256), 256, 0, st>>>(h, g, a, B, H, A, wv, wa,
                                                                     planes, pstride);
