@@ -118,9 +118,13 @@ class DQNLearner(core.Learner, core.Saveable):
             # collective stream while the torso backward runs on the compute stream.
             dist = self._dist
             n = self._native
+            # The IS normaliser's all-reduce (8 bytes) runs beside the forwards: only the
+            # loss (stage 3) reads it.
             n.batch_min_probability(batch[5], self._gmin)
-            dist.all_reduce(self._gmin, op=dist.ReduceOp.MIN)
-            n.forward_backward_stage(0, *batch, global_min_probability=self._gmin,
+            work_min = dist.all_reduce(self._gmin, op=dist.ReduceOp.MIN, async_op=True)
+            n.forward_backward_stage(2, *batch, mean_over=self._B, obs_bf16=fb)
+            work_min.wait()
+            n.forward_backward_stage(3, *batch, global_min_probability=self._gmin,
                                      mean_over=self._B, obs_bf16=fb)
             split = self._grad_split
             tail, head = n.grads[split:], n.grads[:split]

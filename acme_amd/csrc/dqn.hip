@@ -89,6 +89,7 @@ struct acme_dqn {
   bool planes_stale = true;  // parameter planes need a refresh from the f32 buffers
   bool last_p3 = false;      // the last forward/backward ran the plane path
   uint16_t *wpl = nullptr, *tpl = nullptr;
+  int64_t fwd_batch = 0;  // rows of the last stage-2 forward awaiting its stage 3
   uint16_t* frames = nullptr;  // bf16 copies of [o_tm1; o_t] (2B frames)
   // conv1's input of the current step (l->frames, the bf16 copy).
   torso::Frames cur_frames{nullptr};
@@ -816,11 +817,14 @@ int acme_dqn_forward_backward_stage(acme_dqn* l, const acme_transition_batch* ba
   return forward_backward_stage(l, batch, out, stage, stream, true);
 }
 
+static int loss_and_dense_backward(acme_dqn* l, const acme_transition_batch* batch,
+                                   const acme_dqn_outputs* out, hipStream_t st, bool join_dense);
+
 static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batch,
                                   const acme_dqn_outputs* out, int32_t stage, void* stream,
                                   bool join_dense) {
   ACME_CHECK_ARG(l && batch && l->params, "null argument or unbound learner");
-  ACME_CHECK_ARG(stage == 0 || stage == 1, "stage must be 0 or 1");
+  ACME_CHECK_ARG(stage >= 0 && stage <= 3, "stage must be 0, 1, 2 or 3");
   ACME_CHECK_ARG(batch->o_tm1 && batch->a_tm1 && batch->r_t && batch->d_t && batch->o_t &&
                      batch->probabilities,
                  "transition batch has null fields");
@@ -858,6 +862,13 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
   }
   const int A = l->cfg.num_actions;
   int rc;
+  // Stage 0 = stage 2 (the forwards) + stage 3 (loss and the dense backward); a
+  // data-parallel rank splits them to run the IS-normaliser all-reduce beside the forwards.
+  if (stage == 3) {
+    ACME_CHECK_ARG(l->fwd_batch == (int64_t)B, "stage 3 needs the stage-2 forward of this batch");
+    l->fwd_batch = 0;
+    return loss_and_dense_backward(l, batch, out, st, join_dense);
+  }
   // Forward: online on [o_tm1; o_t] (q_tm1 rows 0..B-1, q_t_selector rows B..2B-1),
   // target on o_t (q_t_value).
   l->last_p3 = nature && use_p3(l);
@@ -905,6 +916,20 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
         ACME_OK)
       return rc;
   }
+  if (stage == 2) {
+    l->fwd_batch = B;
+    return ACME_OK;
+  }
+  return loss_and_dense_backward(l, batch, out, st, join_dense);
+}
+
+// Loss (fused into the head dZ on the plane path) and the dense layers' backward, after
+// the forwards of the same batch.
+static int loss_and_dense_backward(acme_dqn* l, const acme_transition_batch* batch,
+                                   const acme_dqn_outputs* out, hipStream_t st, bool join_dense) {
+  const int B = (int)batch->batch, A = l->cfg.num_actions;
+  const bool nature = l->cfg.network == ACME_NET_NATURE_DQN;
+  int rc;
   float* loss = out && out->loss ? out->loss : l->loss_tmp;
   float* td = out && out->td_error ? out->td_error : l->td_tmp;
   double* prio = out && out->priorities ? out->priorities : l->prio_tmp;

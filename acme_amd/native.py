@@ -422,7 +422,8 @@ class NativeDQN:
     def forward_backward_stage(self, stage: int, *batch, global_min_probability=None,
                                q_tm1=None, stream=None, mean_over=None, obs_bf16=None):
         """Stage 0: forwards, loss, head/dense backward (grads[grad_split:]); stage 1: torso
-        backward (grads[:grad_split]).  mean_over: the batch mean's denominator (default
+        backward (grads[:grad_split]).  Stage 0 may be issued as stage 2 (forwards) then
+        stage 3 (loss and dense backward; global_min_probability is read from here on).  mean_over: the batch mean's denominator (default
         the batch; a data-parallel share passes the nominal per-rank batch)."""
         tb = self._batch(*batch, global_min_probability=global_min_probability,
                          mean_over=mean_over, obs_bf16=obs_bf16)

@@ -311,7 +311,9 @@ int acme_dqn_forward_backward(acme_dqn* l, const acme_transition_batch* batch,
 /* The same work in two stages, for data parallelism that overlaps the gradient
  * all-reduce with the rest of the backward pass: stage 0 = forwards, loss, head and
  * dense-layer backward (writes grads[grad_split:]); stage 1 = torso backward (writes
- * grads[:grad_split]; a no-op for MLP networks, whose grad_split is 0). */
+ * grads[:grad_split]; a no-op for MLP networks, whose grad_split is 0).  Stage 0 may itself
+ * be issued as stage 2 (the forwards) then stage 3 (loss, head and dense backward, the same
+ * batch), so that batch->global_min_probability is only read from stage 3 on. */
 int acme_dqn_forward_backward_stage(acme_dqn* l, const acme_transition_batch* batch,
                                     const acme_dqn_outputs* out, int32_t stage, void* stream);
 int acme_dqn_grad_split(const acme_dqn* l, int64_t* split);
