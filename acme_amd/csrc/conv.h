@@ -446,6 +446,15 @@ struct DenseFwd {
     v += bias[n];
     y[(size_t)m * N + n] = act_fwd(act, v);
   }
+  // Prefetched epilogue (gemm.h HasPreStore): the bias of every output loaded up front
+  // (bias is required, also with a slab, where it is loaded and not used).
+  static constexpr bool kPreStore = true;
+  __device__ float pre(int, int n) const { return bias[n]; }
+  __device__ float finish(float v, float b) const { return slab ? v : act_fwd(act, v + b); }
+  __device__ void put(int m, int n, float v, int split) const {
+    if (slab) slab[((size_t)split * M + m) * N + n] = v;
+    else y[(size_t)m * N + n] = v;
+  }
 };
 
 // Weight gradient of a dense layer, single split: dW = X^T dZ written straight into the
@@ -525,6 +534,14 @@ struct DenseDgrad {
     if (xprev) v = act_bwd(act, xprev[idx], v);
     dx[idx] = v;
   }
+  // Prefetched epilogue (gemm.h HasPreStore): the masks loaded up front (from dx when
+  // there is no mask: a valid address whose value is not used).
+  static constexpr bool kPreStore = true;
+  __device__ float pre(int m, int n) const {
+    return (xprev ? xprev : static_cast<const float*>(dx))[(size_t)m * ldx + n];
+  }
+  __device__ float finish(float v, float xp) const { return xprev ? act_bwd(act, xp, v) : v; }
+  __device__ void put(int m, int n, float v, int) const { dx[(size_t)m * ldx + n] = v; }
 };
 
 // ------------------------------------------------------------------ duelling head

@@ -103,6 +103,21 @@ struct HasColSum<P, decltype(void(P::kColSum))> {
   static constexpr bool value = P::kColSum;
 };
 
+// Optional prefetched-epilogue hook: problems with `static constexpr bool kPreStore = true`
+// supply p.pre(m, n), a value loaded for every output of the tile (clamped indices, no
+// branch around the load), p.finish(v, pre) (arithmetic only) and p.put(m, n, value, split).
+// The epilogue loads all of a lane's pre values, finishes every output, then stores: a load
+// inside a per-element store (a bias, a ReLU mask) is otherwise waited for element by
+// element, and behind the stores already issued (vmcnt counts both).
+template <class P, class = void>
+struct HasPreStore {
+  static constexpr bool value = false;
+};
+template <class P>
+struct HasPreStore<P, decltype(void(P::kPreStore))> {
+  static constexpr bool value = P::kPreStore;
+};
+
 // Optional z-class hook: problems with `static constexpr bool kZClass = true` use
 // blockIdx.z to select a sub-problem (p.for_z(z)) instead of a K split.
 template <class P, class = void>
@@ -294,16 +309,46 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) gemm_f32_kernel(const P p_i
   }
 
   // Epilogue: C/D map of the 32x32 MFMA: col = lane & 31, row = (v&3) + 8(v>>2) + 4h.
+  if constexpr (HasPreStore<P>::value) {
+    float pre[MT][NTL][16];
 #pragma unroll
-  for (int i = 0; i < MT; ++i)
+    for (int i = 0; i < MT; ++i)
 #pragma unroll
-    for (int j = 0; j < NTL; ++j)
+      for (int j = 0; j < NTL; ++j)
 #pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int m = m0 + wm * TM + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-        const int n = n0 + wn * TN + j * 32 + r;
-        if (m < p.M && n < p.N) p.store(m, n, acc[i][j][v], split);
-      }
+        for (int v = 0; v < 16; ++v) {
+          const int m = m0 + wm * TM + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+          const int n = n0 + wn * TN + j * 32 + r;
+          pre[i][j][v] = p.pre(m < p.M ? m : p.M - 1, n < p.N ? n : p.N - 1);
+        }
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NTL; ++j)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) pre[i][j][v] = p.finish(acc[i][j][v], pre[i][j][v]);
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NTL; ++j)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int m = m0 + wm * TM + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+          const int n = n0 + wn * TN + j * 32 + r;
+          if (m < p.M && n < p.N) p.put(m, n, pre[i][j][v], split);
+        }
+  } else {
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NTL; ++j)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int m = m0 + wm * TM + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+          const int n = n0 + wn * TN + j * 32 + r;
+          if (m < p.M && n < p.N) p.store(m, n, acc[i][j][v], split);
+        }
+  }
   if constexpr (kColSum) {
     if (do_colsum && n0 + tid < p.N) p.store_colsum(n0 + tid, colsum, split);
   }
