@@ -118,6 +118,53 @@ struct HasPreStore<P, decltype(void(P::kPreStore))> {
   static constexpr bool value = P::kPreStore;
 };
 
+// Epilogue of the f32 / x6 engines: C/D map of the 32x32 MFMA, col = lane & 31,
+// row = (v&3) + 8(v>>2) + 4h, for the wave tile at (mb, nb).
+template <int MT, int NTL, class P>
+__device__ __forceinline__ void store_tile(const P& p, const f32x16 (&acc)[MT][NTL], int mb,
+                                           int nb, int h, int r, int split) {
+  if constexpr (HasPreStore<P>::value) {
+    float pre[MT][NTL][16];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NTL; ++j)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int m = mb + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+          const int n = nb + j * 32 + r;
+          pre[i][j][v] = p.pre(m < p.M ? m : p.M - 1, n < p.N ? n : p.N - 1);
+        }
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NTL; ++j)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) pre[i][j][v] = p.finish(acc[i][j][v], pre[i][j][v]);
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NTL; ++j)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int m = mb + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+          const int n = nb + j * 32 + r;
+          if (m < p.M && n < p.N) p.put(m, n, pre[i][j][v], split);
+        }
+  } else {
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NTL; ++j)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int m = mb + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+          const int n = nb + j * 32 + r;
+          if (m < p.M && n < p.N) p.store(m, n, acc[i][j][v], split);
+        }
+  }
+}
+
 // Optional z-class hook: problems with `static constexpr bool kZClass = true` use
 // blockIdx.z to select a sub-problem (p.for_z(z)) instead of a K split.
 template <class P, class = void>
@@ -308,47 +355,7 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) gemm_f32_kernel(const P p_i
     }
   }
 
-  // Epilogue: C/D map of the 32x32 MFMA: col = lane & 31, row = (v&3) + 8(v>>2) + 4h.
-  if constexpr (HasPreStore<P>::value) {
-    float pre[MT][NTL][16];
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int j = 0; j < NTL; ++j)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const int m = m0 + wm * TM + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-          const int n = n0 + wn * TN + j * 32 + r;
-          pre[i][j][v] = p.pre(m < p.M ? m : p.M - 1, n < p.N ? n : p.N - 1);
-        }
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int j = 0; j < NTL; ++j)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) pre[i][j][v] = p.finish(acc[i][j][v], pre[i][j][v]);
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int j = 0; j < NTL; ++j)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const int m = m0 + wm * TM + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-          const int n = n0 + wn * TN + j * 32 + r;
-          if (m < p.M && n < p.N) p.put(m, n, pre[i][j][v], split);
-        }
-  } else {
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int j = 0; j < NTL; ++j)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const int m = m0 + wm * TM + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-          const int n = n0 + wn * TN + j * 32 + r;
-          if (m < p.M && n < p.N) p.store(m, n, acc[i][j][v], split);
-        }
-  }
+  store_tile<MT, NTL>(p, acc, m0 + wm * TM, n0 + wn * TN, h, r, split);
   if constexpr (kColSum) {
     if (do_colsum && n0 + tid < p.N) p.store_colsum(n0 + tid, colsum, split);
   }

@@ -257,17 +257,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_x6_kernel(const P p_in) {
     __syncthreads();
   }
 
-  // Epilogue: C/D map of the 32x32 MFMA: col = lane & 31, row = (v&3) + 8(v>>2) + 4h.
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int j = 0; j < NTL; ++j)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int m = m0 + wm * TM + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-        const int n = n0 + wn * TN + j * 32 + r;
-        if (m < p.M && n < p.N) p.store(m, n, acc[i][j][v], split);
-      }
+  store_tile<MT, NTL>(p, acc, m0 + wm * TM, n0 + wn * TN, h, r, split);
   if constexpr (kColSum) {
     if (do_colsum && n0 + tid < p.N) p.store_colsum(n0 + tid, colsum, split);
   }
