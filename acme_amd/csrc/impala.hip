@@ -985,7 +985,7 @@ int network_forward(acme_impala* l, const void* obs, const int32_t* prev_a, cons
     } else {
       p.k_chunk = p.K;
       p.slab = nullptr;
-      IM_GEMM("impala_oar_fwd", 32, 32, 1, 1, 4, p, 1);
+      IM_GEMM("impala_oar_fwd", 32, 32, 1, 1, 8, p, 1);
     }
   }
   {
@@ -1024,7 +1024,7 @@ int network_forward(acme_impala* l, const void* obs, const int32_t* prev_a, cons
     p.x = l->h; p.x2 = l->h; p.split_b = rows; p.ldx = H;
     p.w = P(l, l->params, l->t_w1); p.bias = P(l, l->params, l->t_b1); p.y = l->hh;
     p.act = ACT_RELU; p.slab = nullptr;
-    IM_GEMM("impala_head_fwd", 32, 32, 1, 1, 4, p, 1);
+    IM_GEMM("impala_head_fwd", 32, 32, 1, 1, 8, p, 1);
   }
   {
     DenseFwd<false> p;
@@ -1032,7 +1032,7 @@ int network_forward(acme_impala* l, const void* obs, const int32_t* prev_a, cons
     p.x = l->hh; p.x2 = l->hh; p.split_b = rows; p.ldx = l->H2;
     p.w = P(l, l->params, l->t_wpv); p.bias = P(l, l->params, l->t_bpv); p.y = l->pv;
     p.act = ACT_NONE; p.slab = nullptr;
-    IM_GEMM("impala_pv_fwd", 32, 32, 1, 1, 4, p, 1);
+    IM_GEMM("impala_pv_fwd", 32, 32, 1, 1, 8, p, 1);
   }
   return ACME_OK;
 }
@@ -1071,22 +1071,22 @@ int impala_step_impl(acme_impala* l, const acme_sequence_batch* bt, float* metri
     w.M = l->H2; w.N = A + 1; w.K = rows; w.k_chunk = rows;
     w.x = l->hh; w.ldx = l->H2; w.dz = l->dpv; w.out = Pm(l, gr, l->t_wpv);
     w.bias_out = Pm(l, gr, l->t_bpv);
-    IM_GEMM("impala_pv_wgrad", 32, 32, 1, 1, 4, w, 1);
+    IM_GEMM("impala_pv_wgrad", 32, 32, 1, 1, 8, w, 1);
     DenseDgrad<false> d;
     d.M = rows; d.N = l->H2; d.K = A + 1; d.k_chunk = A + 1;
     d.dz = l->dpv; d.w = P(l, l->params, l->t_wpv); d.xprev = l->hh; d.ldx = l->H2; d.dx = l->dhh;
     d.act = ACT_RELU;
-    IM_GEMM("impala_pv_dgrad", 32, 32, 1, 1, 4, d, 1);
+    IM_GEMM("impala_pv_dgrad", 32, 32, 1, 1, 8, d, 1);
   }
   {  // Linear(256) after the LSTM
     DenseWgrad<true> w;
     w.M = H; w.N = l->H2; w.K = rows; w.k_chunk = rows;
     w.x = l->h; w.ldx = H; w.dz = l->dhh; w.out = Pm(l, gr, l->t_w1); w.bias_out = Pm(l, gr, l->t_b1);
-    IM_GEMM("impala_head_wgrad", 32, 32, 1, 1, 4, w, 1);
+    IM_GEMM("impala_head_wgrad", 32, 32, 1, 1, 8, w, 1);
     DenseDgrad<true> d;
     d.M = rows; d.N = H; d.K = l->H2; d.k_chunk = l->H2;
     d.dz = l->dhh; d.w = P(l, l->params, l->t_w1); d.xprev = nullptr; d.ldx = H; d.dx = l->dh;
-    IM_GEMM("impala_head_dgrad", 32, 32, 1, 1, 4, d, 1);
+    IM_GEMM("impala_head_dgrad", 32, 32, 1, 1, 8, d, 1);
   }
   {  // BPTT
     ACME_PROF("impala_lstm_bwd", st, 2.0 * rows * (double)H * 4 * H, 0.0);
@@ -1103,7 +1103,7 @@ int impala_step_impl(acme_impala* l, const acme_sequence_batch* bt, float* metri
     w.M = H; w.N = 4 * H; w.K = rows; w.k_chunk = rows;
     w.h = l->h; w.h0 = bt->h0; w.h0_stride = bt->state_stride; w.T = T; w.dz = l->dgates;
     w.out = Pm(l, gr, l->t_wh);
-    IM_GEMM("impala_wh_wgrad", 32, 32, 1, 1, 4, w, 1);
+    IM_GEMM("impala_wh_wgrad", 32, 32, 1, 1, 8, w, 1);
   }
   if (p3) {  // W_i, b and the embedding gradient on the plane engine, then the plane torso
     const int F = l->F, N = 4 * H;
@@ -1149,7 +1149,7 @@ int impala_step_impl(acme_impala* l, const acme_sequence_batch* bt, float* metri
     o.x = Oar{feat, l->F, A, bt->prev_action, bt->prev_reward};
     o.dz = l->dgates; o.out = Pm(l, gr, l->t_wi); o.bias_out = Pm(l, gr, l->t_b);
     if (atari(l)) IM_GEMM("impala_wi_wgrad", 128, 128, 2, 2, 1, o, 1);
-    else IM_GEMM("impala_wi_wgrad", 32, 32, 1, 1, 4, o, 1);
+    else IM_GEMM("impala_wi_wgrad", 32, 32, 1, 1, 8, o, 1);
   }
   if (!p3 && atari(l)) {  // embedding features -> conv3 dZ -> torso backward
     DenseDgrad<true> d;
