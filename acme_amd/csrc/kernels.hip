@@ -112,28 +112,46 @@ __device__ __forceinline__ LossRow loss_row(const LossArgs& p, int b, double wma
   const float* qt = p.q_on + (size_t)b * A;
   const float* qs = p.q_on + (size_t)(B + b) * A;
   const float* qv = p.q_tg + (size_t)b * A;
-  int best = 0;  // tf.argmax: first maximal index
-  float bq = qs[0];
-  for (int j = 1; j < A; ++j)
-    if (qs[j] > bq) {
-      bq = qs[j];
-      best = j;
-    }
-  float r = p.r[b];
-  r = fminf(fmaxf(r, -p.max_abs_reward), p.max_abs_reward);
-  const float dg = __fmul_rn(p.d[b], p.discount);
-  const float target = __fadd_rn(r, __fmul_rn(dg, qv[best]));
+  // The row's scalars first (and q_tm1[a], which depends only on a), so their latency
+  // overlaps the argmax's loads.
   const int ab = p.a[b];
-  const float td = __fsub_rn(target, qt[ab]);
+  float r = p.r[b];
+  const float dgv = p.d[b];
+  const double prob = p.probs[b];
+  const float qa = qt[ab];
+  // tf.argmax: first maximal index.  The selector row is read 8 entries at a time, all 8
+  // loads issued before the compares (clamped addresses): one latency per 8 actions
+  // instead of one per action.
+  int best = 0;
+  float bq = 0.f;
+  for (int j0 = 0; j0 < A; j0 += 8) {
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = qs[min(j0 + k, A - 1)];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int j = j0 + k;
+      if (j == 0) {
+        bq = v[k];
+      } else if (j < A && v[k] > bq) {
+        bq = v[k];
+        best = j;
+      }
+    }
+  }
+  r = fminf(fmaxf(r, -p.max_abs_reward), p.max_abs_reward);
+  const float dg = __fmul_rn(dgv, p.discount);
+  const float target = __fadd_rn(r, __fmul_rn(dg, qv[best]));
+  const float td = __fsub_rn(target, qa);
   const float ax = fabsf(td);
   const float quad = fminf(ax, p.delta);
   const float lin = ax - quad;
   const float hub = __fadd_rn(__fmul_rn(0.5f, __fmul_rn(quad, quad)), __fmul_rn(p.delta, lin));
   float wf;
   if (p.jax) {  // ((1 / probs).astype(f32) ** beta) / max, all in f32 (jax/dqn/learning.py:94-96)
-    wf = __fdiv_rn(powf((float)(1.0 / p.probs[b]), p.beta), (float)wmax);
+    wf = __fdiv_rn(powf((float)(1.0 / prob), p.beta), (float)wmax);
   } else {      // f64 weights cast at the multiply (tf/dqn/learning.py:138-143)
-    wf = (float)(pow(1.0 / p.probs[b], (double)p.beta) / wmax);
+    wf = (float)(pow(1.0 / prob, (double)p.beta) / wmax);
   }
   const float dtd = fminf(fmaxf(td, -p.delta), p.delta);  // d huber / d td
   const float inv_b = 1.f / (float)p.mean_over;
