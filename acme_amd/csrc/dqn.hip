@@ -104,6 +104,7 @@ struct acme_dqn {
   // by the backward; forward_backward_stage leaves its arguments here.
   LossArgs pending_la{};
   bool loss_pending = false;
+  double* loss_part = nullptr;  // per-block loss partials of the fused loss + head dZ
   // Adam's step count on the device for captured step graphs (a replay reads it); valid
   // (equal to num_steps) while dev_steps_synced.
   int64_t* dev_steps = nullptr;
@@ -405,10 +406,15 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st_main,
   const int A = l->cfg.num_actions;
   const bool p3 = use_p3(l);
   int rc;
+  // The fused kernel leaves the batch loss as per-block partials; their sum is the side
+  // stream's first launch (off the critical path).
+  bool loss_sum = false;
+  const LossArgs la = l->pending_la;
   if (p3 && l->loss_pending) {  // the loss and the head dZ planes, one launch
     l->loss_pending = false;
+    loss_sum = la.loss_part != nullptr;
     ACME_PROF("loss_head_dz", st, 0.0, 0.0);
-    rc = launch_dqn_loss_head_dz(l->pending_la, l->hid, kHidden, P(l, prm, l->t_vw),
+    rc = launch_dqn_loss_head_dz(la, l->hid, kHidden, P(l, prm, l->t_vw),
                                  P(l, prm, l->t_aw), l->dzhp.p, l->dzhp.stride, st);
     if (rc != ACME_OK) return rc;
   } else {  // Head: dZ of the fused hidden layer (masked by its ReLU).
@@ -426,6 +432,12 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st_main,
     ACME_HIP_TRY(hipEventRecord(l->ev[2], st_main));
     ACME_HIP_TRY(hipStreamWaitEvent(l->side, l->ev[2], 0));
     st = l->side;
+  }
+  if (loss_sum) {
+    ACME_PROF("loss_sum", st, 0.0, 0.0);
+    rc = launch_dqn_loss_sum(la.loss_part, dqn_loss_head_dz_blocks(B, kHidden), la.mean_over,
+                             la.loss, st);
+    if (rc != ACME_OK) return rc;
   }
   {  // Head weight / bias gradients: one skinny GEMM over the batch + scatter.
     DuelHeadWgrad p;
@@ -617,6 +629,7 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
           (rc = plane_alloc(l, &l->t2p, (int64_t)B * kFlat)) ||
           (rc = plane_alloc(l, &l->t3p, (int64_t)B * kFlat)) ||
           (rc = plane_alloc(l, &l->dzhp, (int64_t)B * 2 * kHidden)) ||
+          (rc = dev_alloc(l, &l->loss_part, dqn_loss_head_dz_blocks(B, kHidden))) ||
           (rc = plane_alloc(l, &l->dz3p, (int64_t)B * kFlat)) ||
           (rc = plane_alloc(l, &l->dz2p, (int64_t)B * kFlat)) ||
           (rc = plane_alloc(l, &l->dz1p, (int64_t)B * torso::kX1)))
@@ -955,6 +968,7 @@ static int loss_and_dense_backward(acme_dqn* l, const acme_transition_batch* bat
   la.g = l->g;
   la.a_cache = l->a_cache;
   if (l->last_p3) {  // fused with the head dZ (nature_backward)
+    la.loss_part = l->loss_part;
     l->pending_la = la;
     l->loss_pending = true;
   } else {

@@ -58,6 +58,10 @@ struct LossArgs {
   double* prio;   // [B]
   float* g;       // [B] dLoss / dq_tm1[b][a_b]
   int32_t* a_cache;
+  // launch_dqn_loss_head_dz only (optional): every block writes the f64 sum of its rows'
+  // weighted Huber losses here and no block reduces the batch; launch_dqn_loss_sum then
+  // forms the loss (off the critical path, e.g. on the side stream).
+  double* loss_part = nullptr;
 };
 // trfl.double_qlearning + losses.huber + importance weighting + mean
 // (acme/agents/tf/dqn/learning.py:128-144, acme/tf/losses/huber.py:45-57).
@@ -66,6 +70,10 @@ int launch_dqn_loss(const LossArgs& args, hipStream_t st);
 // hidden activations h [B][2H]): one launch, the same bits as the two kernels.
 int launch_dqn_loss_head_dz(const LossArgs& args, const float* h, int H, const float* wv,
                             const float* wa, uint16_t* planes, int64_t pstride, hipStream_t st);
+// Blocks of launch_dqn_loss_head_dz for a batch of B rows (the loss_part entries written).
+int64_t dqn_loss_head_dz_blocks(int B, int H);
+// loss[0] = (sum of the n partials, in order) / mean_over.
+int launch_dqn_loss_sum(const double* part, int64_t n, int mean_over, float* loss, hipStream_t st);
 
 // Deterministic split-K reduction: e in [0, count): v = sum_s slab[s * count + e] (fixed
 // order), optionally + bias[e % ncols] and ReLU; written to out0[e] for e < split_at and

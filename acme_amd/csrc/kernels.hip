@@ -561,7 +561,7 @@ __global__ void __launch_bounds__(256) dqn_loss_head_dz_kernel(
   if (p.global_min_prob) pmin = *p.global_min_prob;
   const double wmax = p.jax ? (double)powf((float)(1.0 / pmin), p.beta)
                             : pow(1.0 / pmin, (double)p.beta);
-  if (blockIdx.x == gridDim.x - 1) {
+  if (!p.loss_part && blockIdx.x == gridDim.x - 1) {
     __syncthreads();  // red is reused below
     double lsum = 0.0;
     for (int b = tid; b < B; b += 256) {
@@ -581,7 +581,33 @@ __global__ void __launch_bounds__(256) dqn_loss_head_dz_kernel(
   }
   const int per = 2 * H / 8;  // threads per row (divides 256: launch_dqn_loss_head_dz)
   const int b0 = (int)((int64_t)blockIdx.x * 256 / per);
-  if (tid < 256 / per && b0 + tid < B) gs[tid] = loss_row(p, b0 + tid, wmax).g;
+  if (p.loss_part) {
+    // This block's rows own their loss outputs (as the loss block does for every row) and
+    // the block's f64 loss partial, summed in row order.
+    __shared__ double hs[8];
+    if (tid < 256 / per) {
+      const int b = b0 + tid;
+      double hw = 0.0;
+      if (b < B) {
+        const LossRow row = loss_row(p, b, wmax);
+        gs[tid] = row.g;
+        hw = (double)row.hub_w;
+        p.g[b] = row.g;
+        p.td[b] = row.td;
+        p.prio[b] = (double)fabsf(row.td);
+        p.a_cache[b] = p.a[b];
+      }
+      hs[tid] = hw;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double sum = 0.0;
+      for (int i = 0; i < 256 / per; ++i) sum += hs[i];
+      p.loss_part[blockIdx.x] = sum;
+    }
+  } else if (tid < 256 / per && b0 + tid < B) {
+    gs[tid] = loss_row(p, b0 + tid, wmax).g;
+  }
   __syncthreads();
   const int64_t t = (int64_t)blockIdx.x * 256 + tid;
   if (t >= (int64_t)B * per) return;
@@ -916,6 +942,29 @@ int launch_fc_head_forward(const float* slab, int splits, int rows, int H, const
   return ACME_OK;
 }
 
+int64_t dqn_loss_head_dz_blocks(int B, int H) { return ceil_div((int64_t)B * (2 * H / 8), 256); }
+
+__global__ void __launch_bounds__(256) dqn_loss_sum_kernel(const double* __restrict__ part,
+                                                           int64_t n, int mean_over,
+                                                           float* __restrict__ loss) {
+  __shared__ double red[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  double s = 0.0;
+  for (int64_t i = tid; i < n; i += 256) s += part[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0) red[wave] = s;
+  __syncthreads();
+  if (tid == 0) loss[0] = (float)((((red[0] + red[1]) + red[2]) + red[3]) / (double)mean_over);
+}
+
+int launch_dqn_loss_sum(const double* part, int64_t n, int mean_over, float* loss, hipStream_t st) {
+  ACME_CHECK_ARG(part && loss && n >= 1 && mean_over >= 1, "bad loss sum args");
+  dqn_loss_sum_kernel<<<1, 256, 0, st>>>(part, n, mean_over, loss);
+  ACME_LAUNCH_CHECK();
+  return ACME_OK;
+}
+
 int launch_dqn_loss_head_dz(const LossArgs& args, const float* h, int H, const float* wv,
                             const float* wa, uint16_t* planes, int64_t pstride, hipStream_t st) {
   ACME_CHECK_ARG(args.B >= 1 && args.A >= 1 && h && wv && wa && planes, "bad loss / head dZ args");
@@ -923,7 +972,8 @@ int launch_dqn_loss_head_dz(const LossArgs& args, const float* h, int H, const f
   ACME_CHECK_ARG(H % 8 == 0 && per >= 32 && 256 % per == 0, "hidden size %d: 2H/8 must divide 256", H);
   ACME_CHECK_ARG(reinterpret_cast<uintptr_t>(wv) % 16 == 0, "wv must be 16-byte aligned");
   const int64_t nb = ceil_div((int64_t)args.B * per, 256);
-  dqn_loss_head_dz_kernel<<<(unsigned)(nb + 1), 256, 0, st>>>(args, h, H, wv, wa, planes, pstride);
+  dqn_loss_head_dz_kernel<<<(unsigned)(args.loss_part ? nb : nb + 1), 256, 0, st>>>(
+      args, h, H, wv, wa, planes, pstride);
   ACME_LAUNCH_CHECK();
   return ACME_OK;
 }
