@@ -424,7 +424,7 @@ __global__ void __launch_bounds__(256) fc_head_forward_kernel(
 // wv; t >= 128: the advantage half against its 4 rows of wa, A float4 loads issued with the
 // slab loads).  Per-thread partials go through LDS and each output is summed by one wave in
 // a fixed order (lane pairs, then a shuffle tree), so the result is deterministic.  One
-// wait for every global load of the block; R = 2 rows per block puts two blocks on most CUs.
+// wait for every global load of the block.  Launched with R = 1 row per block.
 template <int SPL, int A, int R>
 __global__ void __launch_bounds__(256) fc_head1024_kernel(
     const float* __restrict__ slab, int rows, const float* __restrict__ fcb,
@@ -670,6 +670,7 @@ __global__ void __launch_bounds__(256) head_dz_planes_kernel(
   *reinterpret_cast<uint4*>(planes + 2 * pstride + e) = uint4{pl[0], pl[1], pl[2], pl[3]};
 }
 
+template <bool PNT>
 __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p,
                                                    const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
@@ -686,10 +687,14 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p,
 #pragma unroll 2
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (int64_t)gridDim.x * blockDim.x) {
-    f32x4 gg = reinterpret_cast<const f32x4*>(g)[i];
-    f32x4 mm = reinterpret_cast<f32x4*>(m)[i];
-    f32x4 vv = reinterpret_cast<f32x4*>(v)[i];
-    f32x4 pp = reinterpret_cast<f32x4*>(p)[i];
+    // The gradient and the moments are streamed (read once, written once per step) with
+    // non-temporal accesses, so they bypass the caches the next step's forwards read the
+    // parameter planes through.
+    f32x4 gg = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(g) + i);
+    f32x4 mm = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(m) + i);
+    f32x4 vv = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(v) + i);
+    f32x4 pp = PNT ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p) + i)
+                   : reinterpret_cast<f32x4*>(p)[i];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float mj = __fadd_rn(__fmul_rn(b1, mm[j]), __fmul_rn(omb1, gg[j]));
@@ -702,9 +707,10 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p,
       vv[j] = vj;
       pp[j] = __fsub_rn(pp[j], upd);
     }
-    reinterpret_cast<f32x4*>(m)[i] = mm;
-    reinterpret_cast<f32x4*>(v)[i] = vv;
-    reinterpret_cast<f32x4*>(p)[i] = pp;
+    __builtin_nontemporal_store(mm, reinterpret_cast<f32x4*>(m) + i);
+    __builtin_nontemporal_store(vv, reinterpret_cast<f32x4*>(v) + i);
+    if (PNT) __builtin_nontemporal_store(pp, reinterpret_cast<f32x4*>(p) + i);
+    else reinterpret_cast<f32x4*>(p)[i] = pp;
     if (planes) store_planes4(planes, pstride, i, pp);
   }
 }
@@ -920,11 +926,11 @@ int launch_fc_head_forward(const float* slab, int splits, int rows, int H, const
                     reinterpret_cast<uintptr_t>(wv) % 16 == 0 &&
                     reinterpret_cast<uintptr_t>(fcb) % 16 == 0;
   if (H == 512 && A == 18 && wa16 && (splits == 4 || splits == 8) && tune_variant("HEAD") != 1) {
-    const unsigned g2 = (unsigned)ceil_div(rows, 2);
+    // One row per block (2 rows: 12.7 us, 4 rows: 16.3 us, 1 row: 11.4 us per launch).
     if (splits == 8)
-      fc_head1024_kernel<8, 18, 2><<<g2, 256, 0, st>>>(slab, rows, fcb, wv, bv, wa, ba, hid, q);
+      fc_head1024_kernel<8, 18, 1><<<rows, 256, 0, st>>>(slab, rows, fcb, wv, bv, wa, ba, hid, q);
     else
-      fc_head1024_kernel<4, 18, 2><<<g2, 256, 0, st>>>(slab, rows, fcb, wv, bv, wa, ba, hid, q);
+      fc_head1024_kernel<4, 18, 1><<<rows, 256, 0, st>>>(slab, rows, fcb, wv, bv, wa, ba, hid, q);
     ACME_LAUNCH_CHECK();
     return ACME_OK;
   }
@@ -1032,8 +1038,17 @@ int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float l
   const int64_t n4 = n / 4;
   const int gcap = tune_variant("ADAMG") > 0 ? tune_variant("ADAMG") : 8192;  // 47.7 -> 45.2 us vs 2048
   const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n4, 256), gcap);
-  adam_kernel<<<std::max(grid, 1u), 256, 0, st>>>(p, g, m, v, n4, lr, b1, 1.f - b1, b2, 1.f - b2,
-                                                  bc1, bc2, eps, planes, pstride, optix, dev_steps);
+  // Non-temporal gradient / moment traffic: 45.8 -> 45.1 us, and the next step's forwards
+  // (which read the parameter planes) ~1 us faster each; step 0.689 -> 0.681 ms with the
+  // one-row head blocks (three alternating pairs on one box).
+  if (tune_variant("ADAMP") == 1)
+    adam_kernel<true><<<std::max(grid, 1u), 256, 0, st>>>(p, g, m, v, n4, lr, b1, 1.f - b1, b2,
+                                                          1.f - b2, bc1, bc2, eps, planes, pstride,
+                                                          optix, dev_steps);
+  else
+    adam_kernel<false><<<std::max(grid, 1u), 256, 0, st>>>(p, g, m, v, n4, lr, b1, 1.f - b1, b2,
+                                                           1.f - b2, bc1, bc2, eps, planes, pstride,
+                                                           optix, dev_steps);
   ACME_LAUNCH_CHECK();
   if (dev_steps) {
     count_step_kernel<<<1, 1, 0, st>>>(dev_steps);
