@@ -670,7 +670,6 @@ __global__ void __launch_bounds__(256) head_dz_planes_kernel(
   *reinterpret_cast<uint4*>(planes + 2 * pstride + e) = uint4{pl[0], pl[1], pl[2], pl[3]};
 }
 
-template <bool PNT>
 __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p,
                                                    const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
@@ -693,8 +692,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p,
     f32x4 gg = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(g) + i);
     f32x4 mm = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(m) + i);
     f32x4 vv = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(v) + i);
-    f32x4 pp = PNT ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p) + i)
-                   : reinterpret_cast<f32x4*>(p)[i];
+    f32x4 pp = reinterpret_cast<f32x4*>(p)[i];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float mj = __fadd_rn(__fmul_rn(b1, mm[j]), __fmul_rn(omb1, gg[j]));
@@ -709,8 +707,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p,
     }
     __builtin_nontemporal_store(mm, reinterpret_cast<f32x4*>(m) + i);
     __builtin_nontemporal_store(vv, reinterpret_cast<f32x4*>(v) + i);
-    if (PNT) __builtin_nontemporal_store(pp, reinterpret_cast<f32x4*>(p) + i);
-    else reinterpret_cast<f32x4*>(p)[i] = pp;
+    reinterpret_cast<f32x4*>(p)[i] = pp;
     if (planes) store_planes4(planes, pstride, i, pp);
   }
 }
@@ -1041,14 +1038,9 @@ int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float l
   // Non-temporal gradient / moment traffic: 45.8 -> 45.1 us, and the next step's forwards
   // (which read the parameter planes) ~1 us faster each; step 0.689 -> 0.681 ms with the
   // one-row head blocks (three alternating pairs on one box).
-  if (tune_variant("ADAMP") == 1)
-    adam_kernel<true><<<std::max(grid, 1u), 256, 0, st>>>(p, g, m, v, n4, lr, b1, 1.f - b1, b2,
-                                                          1.f - b2, bc1, bc2, eps, planes, pstride,
-                                                          optix, dev_steps);
-  else
-    adam_kernel<false><<<std::max(grid, 1u), 256, 0, st>>>(p, g, m, v, n4, lr, b1, 1.f - b1, b2,
-                                                           1.f - b2, bc1, bc2, eps, planes, pstride,
-                                                           optix, dev_steps);
+  adam_kernel<<<std::max(grid, 1u), 256, 0, st>>>(p, g, m, v, n4, lr, b1, 1.f - b1, b2,
+                                                  1.f - b2, bc1, bc2, eps, planes, pstride,
+                                                  optix, dev_steps);
   ACME_LAUNCH_CHECK();
   if (dev_steps) {
     count_step_kernel<<<1, 1, 0, st>>>(dev_steps);
