@@ -15,5 +15,5 @@ for v in $V; do
   env $(envs $v) timeout -k 10 150 python3 bench.py --no-cpu-baseline --steps 100 --warmup 20 > gpurun_out/ab/prof_${v}.json 2>/dev/null
   python3 -c "
 import json;d=json.load(open('gpurun_out/ab/prof_${v}.json'))
-print('$v', {k['name']:k['avg_us'] for k in d['kernels'] if k['name'] in ('fc_head_fwd','adam','fc_fwd','conv1_fwd','conv12_fwd')})"
+print('$v', {k['name']:k['avg_us'] for k in d['kernels'] if k['name'].endswith('_reduce') or k['name'] in ('fc_head_fwd','adam')})"
 done
