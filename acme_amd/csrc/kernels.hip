@@ -550,6 +550,16 @@ __global__ void __launch_bounds__(256) dqn_loss_head_dz_kernel(
   __shared__ float gs[8];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int B = p.B, A = p.A;
+  // This thread's dZ operands (hidden units and action) are loaded first, at a clamped
+  // index (the loss block's threads load a duplicate they never use), so their latency
+  // overlaps the normaliser and loss below instead of following them.
+  const int per = 2 * H / 8;  // threads per row (divides 256: launch_dqn_loss_head_dz)
+  const int64_t t = (int64_t)blockIdx.x * 256 + tid;
+  const int64_t tc = t < (int64_t)B * per ? t : (int64_t)B * per - 1;
+  const int b = (int)(tc / per), k0 = 8 * (int)(tc - (int64_t)b * per);
+  const float* hr = h + (size_t)b * 2 * H + k0;
+  const f32x4 h0 = reinterpret_cast<const f32x4*>(hr)[0], h1 = reinterpret_cast<const f32x4*>(hr)[1];
+  const int ab = p.a[b];
   // Importance-weight normaliser: max_b (1/p_b)^beta = (1/min_b p_b)^beta.
   double pmin = INFINITY;
   for (int b = tid; b < B; b += 256) pmin = fmin(pmin, p.probs[b]);
@@ -579,7 +589,6 @@ __global__ void __launch_bounds__(256) dqn_loss_head_dz_kernel(
     if (tid == 0) p.loss[0] = (float)((((red[0] + red[1]) + red[2]) + red[3]) / (double)p.mean_over);
     return;
   }
-  const int per = 2 * H / 8;  // threads per row (divides 256: launch_dqn_loss_head_dz)
   const int b0 = (int)((int64_t)blockIdx.x * 256 / per);
   if (p.loss_part) {
     // This block's rows own their loss outputs (as the loss block does for every row) and
@@ -609,14 +618,9 @@ __global__ void __launch_bounds__(256) dqn_loss_head_dz_kernel(
     gs[tid] = loss_row(p, b0 + tid, wmax).g;
   }
   __syncthreads();
-  const int64_t t = (int64_t)blockIdx.x * 256 + tid;
   if (t >= (int64_t)B * per) return;
-  const int b = (int)(t / per), k0 = 8 * (int)(t - (int64_t)b * per);
   const float gb = gs[b - b0];
-  const int ab = p.a[b];
   const float inv_a = 1.f / (float)A;
-  const float* hr = h + (size_t)b * 2 * H + k0;
-  const f32x4 h0 = reinterpret_cast<const f32x4*>(hr)[0], h1 = reinterpret_cast<const f32x4*>(hr)[1];
   const float hv[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
   float d[8];
   head_dz8(k0, H, A, gb, ab, inv_a, wv, wa, hv, d);
