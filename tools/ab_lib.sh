@@ -1,3 +1,7 @@
+# A/B of two builds of the library on the DQN step: the current acme_amd/libacme_hip.so
+# ("new") against acme_amd/libacme_hip_old.so ("old", built beforehand from the baseline
+# commit), selected through ACME_LIB_PATH; alternating step-time runs, then one profiled run
+# each.  Run under gpurun; delete libacme_hip_old.so afterwards.
 set -e
 mkdir -p gpurun_out/ab
 for i in 1 2 3; do
