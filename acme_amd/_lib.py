@@ -59,7 +59,7 @@ class DQNConfig(ctypes.Structure):
 class TransitionBatch(ctypes.Structure):
     _fields_ = [("o_tm1", c_vp), ("a_tm1", c_vp), ("r_t", c_vp), ("d_t", c_vp), ("o_t", c_vp),
                 ("probabilities", c_vp), ("batch", c_i64), ("global_min_probability", c_vp),
-                ("mean_over", c_i64), ("obs_bf16", c_vp)]
+                ("mean_over", c_i64), ("obs_f16", c_vp)]
 
 
 class DQNOutputs(ctypes.Structure):
@@ -155,6 +155,9 @@ _SIGS = {
                                      ctypes.POINTER(ctypes.c_char_p)]),
     "acme_dqn_bind": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "acme_dqn_params_changed": (c_i32, [c_vp]),
+    "acme_dqn_plane_overflow": (c_i32, [c_vp, ctypes.POINTER(c_i32), c_i32]),
+    "acme_dqn_scale_state": (c_i32, [c_vp, c_vp, c_i32, ctypes.POINTER(c_i32)]),
+    "acme_dqn_set_scale_state": (c_i32, [c_vp, c_vp, c_i32]),
     "acme_dqn_forward_backward": (c_i32, [c_vp, ctypes.POINTER(TransitionBatch),
                                           ctypes.POINTER(DQNOutputs), c_vp]),
     "acme_dqn_apply": (c_i32, [c_vp, c_vp]),
@@ -178,6 +181,7 @@ _SIGS = {
                                         ctypes.POINTER(ctypes.c_char_p)]),
     "acme_impala_bind": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp]),
     "acme_impala_step": (c_i32, [c_vp, ctypes.POINTER(SequenceBatch), c_vp, c_vp]),
+    "acme_impala_plane_overflow": (c_i32, [c_vp, ctypes.POINTER(c_i32), c_i32]),
     "acme_impala_policy_step": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
                                         c_vp, c_vp, c_vp]),
     "acme_impala_num_steps": (c_i64, [c_vp]),

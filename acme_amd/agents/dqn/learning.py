@@ -103,15 +103,15 @@ class DQNLearner(core.Learner, core.Saveable):
                  self._prepare(d_t.reshape(B), torch.float32),
                  self._prepare(o_t.reshape(B, self._obs_flat), obs_dt),
                  self._prepare(probs, torch.float64))
-        # The dataset's fused gather also wrote the exact bf16 copy of [o_tm1; o_t] (uint8
+        # The dataset's fused gather also wrote the exact f16 copy of [o_tm1; o_t] (uint8
         # tables; rows [0, B) and [B, 2B) of its buffer): the learner then skips its own
         # conversion (same bits).
-        fb = getattr(self._iterator, "last_frames_bf16", None)
+        fb = getattr(self._iterator, "last_frames_f16", None)
         if fb is not None:
             fb = (fb[:2 * B] if obs_dt == torch.uint8 and fb.shape[0] >= 2 * B
                   and fb.shape[1] == self._obs_flat else None)
         if self._dist is None:
-            self._native.step(*batch, obs_bf16=fb)
+            self._native.step(*batch, obs_f16=fb)
         else:
             # Gradient all-reduce in two buckets overlapped with the backward pass: the dense
             # layers' gradients (the buffer's tail, ~99% of the bytes) are reduced on the
@@ -122,10 +122,10 @@ class DQNLearner(core.Learner, core.Saveable):
             # loss (stage 3) reads it.
             n.batch_min_probability(batch[5], self._gmin)
             work_min = dist.all_reduce(self._gmin, op=dist.ReduceOp.MIN, async_op=True)
-            n.forward_backward_stage(2, *batch, mean_over=self._B, obs_bf16=fb)
+            n.forward_backward_stage(2, *batch, mean_over=self._B, obs_f16=fb)
             work_min.wait()
             n.forward_backward_stage(3, *batch, global_min_probability=self._gmin,
-                                     mean_over=self._B, obs_bf16=fb)
+                                     mean_over=self._B, obs_f16=fb)
             split = self._grad_split
             tail, head = n.grads[split:], n.grads[:split]
             op = self._avg_op if self._avg_op is not None else dist.ReduceOp.SUM
@@ -188,7 +188,10 @@ class DQNLearner(core.Learner, core.Saveable):
         return {"network": n.get_params("params"), "target_network": n.get_params("target"),
                 "optimizer": {"m": n.get_params("m"), "v": n.get_params("v"),
                               "step": n.num_steps},
-                "num_steps": n.num_steps}
+                "num_steps": n.num_steps,
+                # f16 plane scales (csrc/gemm_p3.h): restoring them keeps a resumed run
+                # bit-identical to an uninterrupted one.
+                "plane_scales": n.scale_state()}
 
     def restore(self, state: Dict):
         n = self._native
@@ -198,4 +201,6 @@ class DQNLearner(core.Learner, core.Saveable):
             for k, t in views.items():
                 t.copy_(torch.as_tensor(np.asarray(src[k], np.float32)).view(t.shape))
         n.params_changed()
+        if "plane_scales" in state:
+            n.set_scale_state(state["plane_scales"])
         n.num_steps = int(state["num_steps"])

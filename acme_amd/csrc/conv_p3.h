@@ -3,9 +3,10 @@
 // Same layers, conventions and TF SAME padding as conv.h (NHWC activations, HWIO
 // weights, dZ = gradient w.r.t. a layer's pre-activation); the difference is storage:
 // every f32 activation / gradient / weight operand is read from, and every activation /
-// gradient result written to, exact three-plane bf16 form (gemm_p3.h), and the uint8
-// Atari frames are read as ONE exact bf16 plane (integers 0..255, converted once per
-// step by launch_frames_bf16) with the 1/255 scale applied to the f32 result
+// gradient result written to, scaled two-plane f16 form (gemm_p3.h; results are multiplied
+// by the operands' read scales), and the uint8 Atari frames are read as ONE exact f16 plane
+// (integers 0..255, converted once per step by launch_frames_f16 or the replay's fused
+// gather) with the 1/255 scale applied to the f32 result
 // (acme/wrappers/atari_wrapper.py:284-306 scales the frame before the first convolution;
 // the scale commutes with the sum up to f32 rounding of the result).
 //
@@ -35,28 +36,35 @@ __device__ __forceinline__ uint32_t boff(int64_t elem) { return (uint32_t)(2 * e
 
 using V8 = float[8];
 
-// Planes of 8 consecutive values at element e (16-B aligned): three 16-byte stores.
-__device__ __forceinline__ void put8(const Planes& y, int64_t e, const V8& v) {
-  uint32_t h[4], m[4], l[4];
+// The two planes of 8 scaled values (v[j] * w) as packed f16 pairs; returns max |v|.
+__device__ __forceinline__ float split8(const V8& v, float w, uint32_t (&h)[4], uint32_t (&l)[4]) {
+  float mx = 0.f;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    uint16_t h0, m0, l0, h1, m1, l1;
-    gemm::split3_bits(v[2 * j], h0, m0, l0);
-    gemm::split3_bits(v[2 * j + 1], h1, m1, l1);
+    uint16_t h0, l0, h1, l1;
+    gemm::split2_bits(v[2 * j] * w, h0, l0);
+    gemm::split2_bits(v[2 * j + 1] * w, h1, l1);
     h[j] = (uint32_t)h0 | ((uint32_t)h1 << 16);
-    m[j] = (uint32_t)m0 | ((uint32_t)m1 << 16);
     l[j] = (uint32_t)l0 | ((uint32_t)l1 << 16);
+    mx = fmaxf(mx, fmaxf(fabsf(v[2 * j]), fabsf(v[2 * j + 1])));
   }
+  return mx;
+}
+// Planes of 8 consecutive values at element e (16-B aligned): two 16-byte stores; returns
+// max |v| (the tensor's amax).
+__device__ __forceinline__ float put8(const Planes& y, int64_t e, const V8& v) {
+  uint32_t h[4], l[4];
+  const float mx = split8(v, y.w(), h, l);
   *reinterpret_cast<uint4*>(y.p + e) = uint4{h[0], h[1], h[2], h[3]};
-  *reinterpret_cast<uint4*>(y.p + y.stride + e) = uint4{m[0], m[1], m[2], m[3]};
-  *reinterpret_cast<uint4*>(y.p + 2 * y.stride + e) = uint4{l[0], l[1], l[2], l[3]};
+  *reinterpret_cast<uint4*>(y.p + y.stride + e) = uint4{l[0], l[1], l[2], l[3]};
+  return mx;
 }
 // 8 f32 values at p (32-B aligned).
 __device__ __forceinline__ void st8(float* p, const V8& v) {
   *reinterpret_cast<float4*>(p) = float4{v[0], v[1], v[2], v[3]};
   *reinterpret_cast<float4*>(p + 4) = float4{v[4], v[5], v[6], v[7]};
 }
-// ReLU mask of 8 stored activations (their bf16 h plane; x > 0 <=> h > 0): dz where x > 0.
+// ReLU mask of 8 stored activations (their f16 h plane; x > 0 <=> h > 0): dz where x > 0.
 __device__ __forceinline__ void relu_mask8(const CPlanes& x, int64_t e, V8& v) {
   const uint4 w = *reinterpret_cast<const uint4*>(x.p + e);
   const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
@@ -69,7 +77,7 @@ __device__ __forceinline__ void relu_mask8(const CPlanes& x, int64_t e, V8& v) {
 }
 
 // ------------------------------------------------------------------ forward
-// NPA = 1: frames (the bf16 copy of the uint8 values), result scaled by 1/255; NPA = 3:
+// NPA = 1: frames (the f16 copy of the uint8 values), result scaled by 1/255; NPA = 2:
 // f32 planes.
 template <class G, int NPA>
 struct P3ConvFwd {
@@ -80,12 +88,14 @@ struct P3ConvFwd {
   static_assert((G::KW * G::CI) % 32 == 0, "a filter-tap row must hold whole 32-k stages");
   static_assert(G::CO % 8 == 0, "output channels must be a multiple of 8");
   static constexpr int A_MODE = gemm::KCONTIG, B_MODE = gemm::RCONTIG;
-  static constexpr int A_PLANES = NPA, B_PLANES = 3;
+  static constexpr int A_PLANES = NPA, B_PLANES = gemm::kPlanes;
+  static constexpr bool kAmax = true;
   int M, N, K, k_chunk;  // M = frames * OPIX, N = CO, K = KH*KW*CI
   PlaneSrc a_src;        // [frames][IH][IW][CI]
   PlaneSrc b_src;        // W [K][CO]
   const float* bias;
   Planes y;              // [frames][OH][OW][CO]
+  __device__ gemm::PScale* amax_sc() const { return y.sc; }
   struct ARow {
     int pix;  // element offset of (frame, ih0, iw0)
     int ih0, iw0;
@@ -119,21 +129,21 @@ struct P3ConvFwd {
     return b.n < N ? boff((int64_t)(k0 + kk) * G::CO + b.n) : kOOB;
   }
   static constexpr bool kStore8 = true;
-  __device__ void store8(int m, int n, const V8& acc, int) const {
-    V8 v;
+  // relu(acc r (/ 255) + b): the activation of 8 outputs (r = the operands' read scales).
+  __device__ void act8(int n, const V8& acc, V8& v) const {
+    const float rs = gemm::result_scale(a_src, b_src);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float x = acc[j];
+      float x = acc[j] * rs;
       if constexpr (NPA == 1) x = x / 255.0f;
       x += bias[n + j];
       v[j] = x > 0.f ? x : 0.f;
     }
-    put8(y, (int64_t)m * G::CO + n, v);
   }
-  __device__ void store(int m, int n, float v, int) const {
-    if constexpr (NPA == 1) v = v / 255.0f;
-    v += bias[n];
-    y.put((int64_t)m * G::CO + n, v > 0.f ? v : 0.f);
+  __device__ float store8(int m, int n, const V8& acc, int) const {
+    V8 v;
+    act8(n, acc, v);
+    return put8(y, (int64_t)m * G::CO + n, v);
   }
 };
 
@@ -145,7 +155,7 @@ struct P3ConvWgrad {
                 "see P3ConvFwd");
   static_assert(G::OPIX >= 32, "a 32-k stage must span at most two frames");
   static constexpr int A_MODE = gemm::RCONTIG, B_MODE = gemm::RCONTIG;
-  static constexpr int A_PLANES = NPA, B_PLANES = 3;
+  static constexpr int A_PLANES = NPA, B_PLANES = gemm::kPlanes;
   static constexpr bool kColSum = true;  // bias gradient = column sums of dZ
   int M, N, K, k_chunk;  // M = G::K rows (kh,kw,ci), N = CO, K = frames * OPIX
   PlaneSrc a_src;        // X [frames][IH][IW][CI]
@@ -185,18 +195,16 @@ struct P3ConvWgrad {
     return b.n < N ? boff((int64_t)(k0 + kk) * G::CO + b.n) : kOOB;
   }
   static constexpr bool kStore8 = true;
-  __device__ void store8(int i, int n, const V8& acc, int split) const {
+  __device__ float store8(int i, int n, const V8& acc, int split) const {
+    const float rs = gemm::result_scale(a_src, b_src);
     V8 v;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = NPA == 1 ? acc[j] / 255.0f : acc[j];
+    for (int j = 0; j < 8; ++j) v[j] = NPA == 1 ? (acc[j] * rs) / 255.0f : acc[j] * rs;
     st8(slab + ((size_t)split * (M + 1) + i) * N + n, v);
-  }
-  __device__ void store(int i, int n, float v, int split) const {
-    if constexpr (NPA == 1) v = v / 255.0f;
-    slab[((size_t)split * (M + 1) + i) * N + n] = v;
+    return 0.f;
   }
   __device__ void store_colsum(int n, float v, int split) const {
-    slab[((size_t)split * (M + 1) + M) * N + n] = v;
+    slab[((size_t)split * (M + 1) + M) * N + n] = v * gemm::read_scale(b_src.sc);
   }
 };
 
@@ -207,12 +215,14 @@ struct P3ConvDgrad {
   static_assert(G::S == 1, "strided input gradients use P3ConvDgradSubZ");
   static_assert(G::CO % 32 == 0 && G::CI % 8 == 0, "channel counts");
   static constexpr int A_MODE = gemm::KCONTIG, B_MODE = gemm::KCONTIG;
-  static constexpr int A_PLANES = 3, B_PLANES = 3;
+  static constexpr int A_PLANES = gemm::kPlanes, B_PLANES = gemm::kPlanes;
+  static constexpr bool kAmax = true;
   int M, N, K, k_chunk;  // M = frames * IPIX, N = CI, K = KH*KW*CO
   PlaneSrc a_src;        // dZ [frames][OH][OW][CO]
   PlaneSrc b_src;        // W [KH][KW][CI][CO]
   CPlanes xprev;         // [frames][IH][IW][CI] post-ReLU activations of the previous layer
   Planes dx;             // [frames][IH][IW][CI] = dZ of the previous layer
+  __device__ gemm::PScale* amax_sc() const { return dx.sc; }
   struct ARow {
     int pix;  // element offset of (frame, th0, tw0) in dZ
     int th0, tw0;
@@ -250,17 +260,14 @@ struct P3ConvDgrad {
     return b.ci < N ? boff(((kh * G::KW + kw) * G::CI + b.ci) * G::CO + co) : kOOB;
   }
   static constexpr bool kStore8 = true;
-  __device__ void store8(int m, int ci, const V8& acc, int) const {
+  __device__ float store8(int m, int ci, const V8& acc, int) const {
     const int64_t idx = (int64_t)m * G::CI + ci;
+    const float rs = gemm::result_scale(a_src, b_src);
     V8 v;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = acc[j];
+    for (int j = 0; j < 8; ++j) v[j] = acc[j] * rs;
     relu_mask8(xprev, idx, v);
-    put8(dx, idx, v);
-  }
-  __device__ void store(int m, int ci, float v, int) const {
-    const int64_t idx = (int64_t)m * G::CI + ci;
-    dx.put(idx, xprev.positive(idx) ? v : 0.f);
+    return put8(dx, idx, v);
   }
 };
 
@@ -271,8 +278,9 @@ struct P3ConvDgradSubZ {
   static_assert(G::KH % G::S == 0 && G::KW % G::S == 0, "kernel must be a multiple of stride");
   static_assert(G::CO % 32 == 0 && G::CI % 8 == 0, "channel counts");
   static constexpr int A_MODE = gemm::KCONTIG, B_MODE = gemm::KCONTIG;
-  static constexpr int A_PLANES = 3, B_PLANES = 3;
+  static constexpr int A_PLANES = gemm::kPlanes, B_PLANES = gemm::kPlanes;
   static constexpr bool kZClass = true;
+  static constexpr bool kAmax = true;
   static constexpr int S = G::S;
   static constexpr int JH = G::KH / S, JW = G::KW / S;
   static constexpr int KR = JH * JW * G::CO;
@@ -282,6 +290,7 @@ struct P3ConvDgradSubZ {
   CPlanes xprev;
   Planes dx;
   int ph = 0, pw = 0, rh = 0, rw = 0, nh = 1, nw = 1, mc = 0;  // set by for_z
+  __device__ gemm::PScale* amax_sc() const { return dx.sc; }
   __device__ P3ConvDgradSubZ for_z(int z) const {
     P3ConvDgradSubZ q = *this;
     q.ph = z / S;
@@ -338,23 +347,17 @@ struct P3ConvDgradSubZ {
     return b.ci < N ? boff(((kh * G::KW + kw) * G::CI + b.ci) * G::CO + co) : kOOB;
   }
   static constexpr bool kStore8 = true;
-  __device__ void store8(int m, int ci, const V8& acc, int) const {
-    if (m >= mc) return;
+  __device__ float store8(int m, int ci, const V8& acc, int) const {
+    if (m >= mc) return 0.f;
     int b, ih, iw;
     decode(m, b, ih, iw);
     const int64_t idx = ((int64_t)b * G::IPIX + ih * G::IW + iw) * G::CI + ci;
+    const float rs = gemm::result_scale(a_src, b_src);
     V8 v;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = acc[j];
+    for (int j = 0; j < 8; ++j) v[j] = acc[j] * rs;
     relu_mask8(xprev, idx, v);
-    put8(dx, idx, v);
-  }
-  __device__ void store(int m, int ci, float v, int) const {
-    if (m >= mc) return;
-    int b, ih, iw;
-    decode(m, b, ih, iw);
-    const int64_t idx = ((int64_t)b * G::IPIX + ih * G::IW + iw) * G::CI + ci;
-    dx.put(idx, xprev.positive(idx) ? v : 0.f);
+    return put8(dx, idx, v);
   }
 };
 
@@ -362,12 +365,13 @@ struct P3ConvDgradSubZ {
 // Y = X W (+ bias, act in the split-K reduction): X [rows][ldx] planes, W [K][N] planes.
 struct P3DenseFwd {
   static constexpr int A_MODE = gemm::KCONTIG, B_MODE = gemm::RCONTIG;
-  static constexpr int A_PLANES = 3, B_PLANES = 3;
+  static constexpr int A_PLANES = gemm::kPlanes, B_PLANES = gemm::kPlanes;
   int M, N, K, k_chunk;
   PlaneSrc a_src;  // X
   int ldx;
   PlaneSrc b_src;  // W
-  float* slab;     // [splits][M][N] raw partial sums (finalised by the slab reduction)
+  float* slab;     // [splits][M][N] partial sums (already read-scaled; finalised by the
+                   // slab reduction)
   struct ARow {
     int off;
     bool ok;
@@ -384,18 +388,20 @@ struct P3DenseFwd {
     return b.n < N ? boff((int64_t)(k0 + kk) * N + b.n) : kOOB;
   }
   static constexpr bool kStore8 = true;
-  __device__ void store8(int m, int n, const V8& v, int split) const {
+  __device__ float store8(int m, int n, const V8& acc, int split) const {
+    const float rs = gemm::result_scale(a_src, b_src);
+    V8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = acc[j] * rs;
     st8(slab + ((size_t)split * M + m) * N + n, v);
-  }
-  __device__ void store(int m, int n, float v, int split) const {
-    slab[((size_t)split * M + m) * N + n] = v;
+    return 0.f;
   }
 };
 
 // dW = X^T dZ (reduction over the batch), db = column sums of dZ.
 struct P3DenseWgrad {
   static constexpr int A_MODE = gemm::RCONTIG, B_MODE = gemm::RCONTIG;
-  static constexpr int A_PLANES = 3, B_PLANES = 3;
+  static constexpr int A_PLANES = gemm::kPlanes, B_PLANES = gemm::kPlanes;
   static constexpr bool kColSum = true;
   int M, N, K, k_chunk;  // M = Kin, N = Nout, K = rows (batch)
   PlaneSrc a_src;        // X [rows][ldx]
@@ -418,22 +424,32 @@ struct P3DenseWgrad {
     return b.n < N ? boff((int64_t)(k0 + kk) * N + b.n) : kOOB;
   }
   static constexpr bool kStore8 = true;
-  __device__ void store8(int i, int n, const V8& v, int) const { st8(out + (size_t)i * N + n, v); }
-  __device__ void store(int i, int n, float v, int) const { out[(size_t)i * N + n] = v; }
-  __device__ void store_colsum(int n, float v, int) const { bias_out[n] = v; }
+  __device__ float store8(int i, int n, const V8& acc, int) const {
+    const float rs = gemm::result_scale(a_src, b_src);
+    V8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = acc[j] * rs;
+    st8(out + (size_t)i * N + n, v);
+    return 0.f;
+  }
+  __device__ void store_colsum(int n, float v, int) const {
+    bias_out[n] = v * gemm::read_scale(b_src.sc);
+  }
 };
 
 // dX = dZ W^T masked by the previous layer's ReLU: dZ [rows][K] planes, W [N][K] planes
 // (the layer's [Kin][Nout] weight: Nout = K is contiguous).
 struct P3DenseDgrad {
   static constexpr int A_MODE = gemm::KCONTIG, B_MODE = gemm::KCONTIG;
-  static constexpr int A_PLANES = 3, B_PLANES = 3;
+  static constexpr int A_PLANES = gemm::kPlanes, B_PLANES = gemm::kPlanes;
+  static constexpr bool kAmax = true;
   int M, N, K, k_chunk;  // M = rows, N = Kin, K = Nout
   PlaneSrc a_src;        // dZ
   PlaneSrc b_src;        // W
   CPlanes xprev;         // [rows][ldx]
   int ldx;
   Planes dx;             // [rows][ldx]
+  __device__ gemm::PScale* amax_sc() const { return dx.sc; }
   struct ARow {
     int off;
     bool ok;
@@ -450,17 +466,14 @@ struct P3DenseDgrad {
     return b.n < N ? boff((int64_t)b.n * K + k0 + kk) : kOOB;
   }
   static constexpr bool kStore8 = true;
-  __device__ void store8(int m, int n, const V8& acc, int) const {
+  __device__ float store8(int m, int n, const V8& acc, int) const {
     const int64_t idx = (int64_t)m * ldx + n;
+    const float rs = gemm::result_scale(a_src, b_src);
     V8 v;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = acc[j];
+    for (int j = 0; j < 8; ++j) v[j] = acc[j] * rs;
     relu_mask8(xprev, idx, v);
-    put8(dx, idx, v);
-  }
-  __device__ void store(int m, int n, float v, int) const {
-    const int64_t idx = (int64_t)m * ldx + n;
-    dx.put(idx, xprev.positive(idx) ? v : 0.f);
+    return put8(dx, idx, v);
   }
 };
 

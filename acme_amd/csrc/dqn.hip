@@ -83,15 +83,20 @@ struct acme_dqn {
   float* loss_tmp = nullptr;
   float* td_tmp = nullptr;
   double* prio_tmp = nullptr;
-  // Plane path (gemm_p3.h; Nature network on uint8 frames, x6 engine): exact bf16 planes
-  // of the parameters / target parameters ([3][flat]) and of every GEMM operand.
+  // Plane path (gemm_p3.h; Nature network on uint8 frames): scaled two-plane f16 copies of
+  // the parameters / target parameters ([2][flat]) and of every GEMM operand.
   bool p3_capable = false;
   bool planes_stale = true;  // parameter planes need a refresh from the f32 buffers
   bool last_p3 = false;      // the last forward/backward ran the plane path
   uint16_t *wpl = nullptr, *tpl = nullptr;
+  // Scale records of the plane tensors (kScale* below) and the sticky overflow flag.
+  gemm::PScale* scales = nullptr;
+  int* overflow = nullptr;
+  bool scales_ok = false;    // the activation / gradient scales are calibrated
+  bool calibrating = false;
   int64_t fwd_batch = 0;  // rows of the last stage-2 forward awaiting its stage 3
-  uint16_t* frames = nullptr;  // bf16 copies of [o_tm1; o_t] (2B frames)
-  // conv1's input of the current step (l->frames, the bf16 copy).
+  uint16_t* frames = nullptr;  // f16 copies of [o_tm1; o_t] (2B frames)
+  // conv1's input of the current step (l->frames, the f16 copy).
   torso::Frames cur_frames{nullptr};
   // Second stream of the plane path: the target forward runs beside the online forward,
   // and weight gradients beside input gradients (fork / join by events on the caller's
@@ -105,26 +110,20 @@ struct acme_dqn {
   LossArgs pending_la{};
   bool loss_pending = false;
   double* loss_part = nullptr;  // per-block loss partials of the fused loss + head dZ
-  // Adam's step count on the device for captured step graphs (a replay reads it); valid
-  // (equal to num_steps) while dev_steps_synced.
-  int64_t* dev_steps = nullptr;
-  bool dev_steps_synced = true;
-  // Captured steps (acme_dqn_step on the plane path), keyed by the batch / output pointers,
-  // B, the mean denominator and whether the step copies the target.
-  struct Graph {
-    const void* key[11];
-    int64_t B, mean_over;
-    bool copy;
-    int tune_gen;
-    hipGraphExec_t exec;
-  };
-  std::vector<Graph> graphs;
-  hipStream_t capture = nullptr;
 };
 
 namespace {
 
 int64_t align64(int64_t x) { return (x + 63) & ~int64_t(63); }
+
+// Scale records (gemm_p3.h PScale) of the plane tensors: the transient activations and
+// gradients of one step first, then the two persistent parameter-plane buffers.
+enum {
+  kScX1, kScX2, kScX3, kScT1, kScT2, kScT3, kScDzh, kScDz3, kScDz2, kScDz1,
+  kScTransient,
+  kScParams = kScTransient, kScTarget,
+  kScCount
+};
 
 int add_tensor(acme_dqn* l, const char* name, std::initializer_list<int64_t> shape) {
   Tensor t;
@@ -155,12 +154,12 @@ int dev_alloc(acme_dqn* l, T** p, int64_t count) {
   return ACME_OK;
 }
 
-int plane_alloc(acme_dqn* l, torso::Plane* x, int64_t count) {
+int plane_alloc(acme_dqn* l, torso::Plane* x, int64_t count, int rec) {
   const int64_t stride = align64(count);
   uint16_t* p = nullptr;
-  int rc = dev_alloc(l, &p, 3 * stride);
+  int rc = dev_alloc(l, &p, gemm::kPlanes * stride);
   if (rc != ACME_OK) return rc;
-  *x = torso::Plane{p, stride};
+  *x = torso::Plane{p, stride, l->scales + rec};
   return ACME_OK;
 }
 
@@ -168,22 +167,24 @@ inline const float* P(const acme_dqn* l, const float* base, int t) {
   return base + l->tensors[t].offset;
 }
 inline float* Pm(const acme_dqn* l, float* base, int t) { return base + l->tensors[t].offset; }
-// Plane view of parameter tensor t in a [3][flat] parameter-plane buffer.
+// Plane view of parameter tensor t in a [2][flat] parameter-plane buffer (wpl or tpl, whose
+// scale records are kScParams / kScTarget).
 inline torso::Plane WP(const acme_dqn* l, uint16_t* base, int t) {
-  return torso::Plane{base + l->tensors[t].offset, l->flat};
+  return torso::Plane{base + l->tensors[t].offset, l->flat,
+                      l->scales + (base == l->tpl ? kScTarget : kScParams)};
 }
-inline CPlanes CP(const torso::Plane& x) { return CPlanes{x.p, x.stride}; }
+inline CPlanes CP(const torso::Plane& x) { return CPlanes{x.p, x.stride, x.sc}; }
 inline gemm::PlaneSrc SRC(const torso::Plane& x, int64_t elems) {
-  return gemm::PlaneSrc{x.p, x.stride, (int32_t)(2 * elems)};
+  return gemm::PlaneSrc{x.p, x.stride, (int32_t)(2 * elems), x.sc};
 }
-// bf16 frames of obs_a (rows [0, split)) and obs_b (the rest) into l->frames.
+// f16 frames of obs_a (rows [0, split)) and obs_b (the rest) into l->frames.
 int convert_frames(acme_dqn* l, const void* obs_a, const void* obs_b, int split, int rows,
                    hipStream_t st) {
-  ACME_PROF("frames_bf16", st, 0.0, 3.0 * (double)rows * kObsBytes);
-  return launch_frames_bf16(static_cast<const uint8_t*>(obs_a), static_cast<const uint8_t*>(obs_b),
-                            split, rows, kObsBytes, l->frames, st);
+  ACME_PROF("frames_f16", st, 0.0, 3.0 * (double)rows * kObsBytes);
+  return launch_frames_f16(static_cast<const uint8_t*>(obs_a), static_cast<const uint8_t*>(obs_b),
+                           split, rows, kObsBytes, l->frames, st);
 }
-inline Planes PP(const torso::Plane& x) { return Planes{x.p, x.stride}; }
+inline Planes PP(const torso::Plane& x) { return Planes{x.p, x.stride, x.sc}; }
 bool use_p3(const acme_dqn* l) { return l->p3_capable && gemm::use_x6(); }
 // The side stream is used unless the section profiler is on: profiled passes run every
 // kernel alone on one stream, so their per-kernel durations are uncontended.
@@ -324,8 +325,8 @@ int nature_forward(acme_dqn* l, const float* prm, const void* obs_a, const void*
   return head_forward(l, prm, rows, hid, q, st);
 }
 
-// Nature forward on the plane path: torso and the fused hidden layer read exact bf16
-// planes (gemm_p3.h); `wpl` are the planes of `prm`.
+// Nature forward on the plane path: torso and the fused hidden layer read f16 planes
+// (gemm_p3.h); `wpl` are the planes of `prm`.
 int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const torso::Frames& frames,
                       int rows, const torso::Plane& x1, const torso::Plane& x2,
                       const torso::Plane& x3, float* hid, float* q, hipStream_t st,
@@ -415,12 +416,12 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st_main,
     loss_sum = la.loss_part != nullptr;
     ACME_PROF("loss_head_dz", st, 0.0, 0.0);
     rc = launch_dqn_loss_head_dz(la, l->hid, kHidden, P(l, prm, l->t_vw),
-                                 P(l, prm, l->t_aw), l->dzhp.p, l->dzhp.stride, st);
+                                 P(l, prm, l->t_aw), l->dzhp.p, l->dzhp.stride, l->dzhp.sc, st);
     if (rc != ACME_OK) return rc;
   } else {  // Head: dZ of the fused hidden layer (masked by its ReLU).
     ACME_PROF("head_dz", st, 0.0, 0.0);
     rc = p3 ? launch_head_dz_planes(l->hid, l->g, l->a_cache, B, kHidden, A, P(l, prm, l->t_vw),
-                                    P(l, prm, l->t_aw), l->dzhp.p, l->dzhp.stride, st)
+                                    P(l, prm, l->t_aw), l->dzhp.p, l->dzhp.stride, l->dzhp.sc, st)
             : launch_duel_head_dz(l->hid, l->g, l->a_cache, B, kHidden, A, P(l, prm, l->t_vw),
                                   P(l, prm, l->t_aw), l->dzh, st);
     if (rc != ACME_OK) return rc;
@@ -551,13 +552,29 @@ int mlp_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st) {
   return ACME_OK;
 }
 
-// Refreshes the parameter planes from the f32 parameter buffers.
+// Refreshes the parameter planes from the f32 parameter buffers, each at a scale that suits
+// its max (the current one when it does: after acme_dqn_set_scale_state the planes are the
+// bits the checkpointed run's Adam wrote).
 int sync_planes(acme_dqn* l, hipStream_t st) {
   if (!l->p3_capable || !l->planes_stale) return ACME_OK;
-  int rc = launch_split_planes(l->params, l->flat, l->wpl, l->flat, st);
-  if (rc == ACME_OK) rc = launch_split_planes(l->target, l->flat, l->tpl, l->flat, st);
+  int rc = launch_split_planes(l->params, l->flat, l->wpl, l->flat, l->scales + kScParams, st,
+                               l->overflow, 1);
+  if (rc == ACME_OK)
+    rc = launch_split_planes(l->target, l->flat, l->tpl, l->flat, l->scales + kScTarget, st,
+                             l->overflow, 1);
   if (rc == ACME_OK) l->planes_stale = false;
   return rc;
+}
+
+// Initial scale records: w = r = wi = 1, amax slots 0.
+int reset_scales(acme_dqn* l) {
+  std::vector<gemm::PScale> init(kScCount);
+  std::memset(init.data(), 0, init.size() * sizeof(gemm::PScale));
+  for (auto& r : init) r.w = r.r = r.wi = r.rl = 1.f;
+  ACME_HIP_TRY(hipMemcpy(l->scales, init.data(), init.size() * sizeof(gemm::PScale),
+                         hipMemcpyHostToDevice));
+  ACME_HIP_TRY(hipMemset(l->overflow, 0, sizeof(int)));
+  return ACME_OK;
 }
 
 }  // namespace
@@ -620,19 +637,22 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
     if (cfg->obs_dtype == ACME_OBS_U8_SCALED && (int64_t)R2 * kObsBytes * 2 < (int64_t)INT32_MAX) {
       l->p3_capable = true;
       const int64_t fl = l->flat;
-      if ((rc = dev_alloc(l, &l->wpl, 3 * fl)) || (rc = dev_alloc(l, &l->tpl, 3 * fl)) ||
+      if ((rc = dev_alloc(l, &l->scales, kScCount)) || (rc = dev_alloc(l, &l->overflow, 1)) ||
+          (rc = reset_scales(l)) ||
+          (rc = dev_alloc(l, &l->wpl, gemm::kPlanes * fl)) ||
+          (rc = dev_alloc(l, &l->tpl, gemm::kPlanes * fl)) ||
           (rc = dev_alloc(l, &l->frames, (int64_t)R2 * kObsBytes)) ||
-          (rc = plane_alloc(l, &l->x1p, (int64_t)R2 * torso::kX1)) ||
-          (rc = plane_alloc(l, &l->x2p, (int64_t)R2 * kFlat)) ||
-          (rc = plane_alloc(l, &l->x3p, (int64_t)R2 * kFlat)) ||
-          (rc = plane_alloc(l, &l->t1p, (int64_t)B * torso::kX1)) ||
-          (rc = plane_alloc(l, &l->t2p, (int64_t)B * kFlat)) ||
-          (rc = plane_alloc(l, &l->t3p, (int64_t)B * kFlat)) ||
-          (rc = plane_alloc(l, &l->dzhp, (int64_t)B * 2 * kHidden)) ||
+          (rc = plane_alloc(l, &l->x1p, (int64_t)R2 * torso::kX1, kScX1)) ||
+          (rc = plane_alloc(l, &l->x2p, (int64_t)R2 * kFlat, kScX2)) ||
+          (rc = plane_alloc(l, &l->x3p, (int64_t)R2 * kFlat, kScX3)) ||
+          (rc = plane_alloc(l, &l->t1p, (int64_t)B * torso::kX1, kScT1)) ||
+          (rc = plane_alloc(l, &l->t2p, (int64_t)B * kFlat, kScT2)) ||
+          (rc = plane_alloc(l, &l->t3p, (int64_t)B * kFlat, kScT3)) ||
+          (rc = plane_alloc(l, &l->dzhp, (int64_t)B * 2 * kHidden, kScDzh)) ||
           (rc = dev_alloc(l, &l->loss_part, dqn_loss_head_dz_blocks(B, kHidden))) ||
-          (rc = plane_alloc(l, &l->dz3p, (int64_t)B * kFlat)) ||
-          (rc = plane_alloc(l, &l->dz2p, (int64_t)B * kFlat)) ||
-          (rc = plane_alloc(l, &l->dz1p, (int64_t)B * torso::kX1)))
+          (rc = plane_alloc(l, &l->dz3p, (int64_t)B * kFlat, kScDz3)) ||
+          (rc = plane_alloc(l, &l->dz2p, (int64_t)B * kFlat, kScDz2)) ||
+          (rc = plane_alloc(l, &l->dz1p, (int64_t)B * torso::kX1, kScDz1)))
         return fail(rc);
       l->slab_floats = std::max(l->slab_floats, torso::wgrad_slab_floats_p3());
       if (tune("SIDE") != 1) {  // ACME_V_SIDE=1: single stream
@@ -680,11 +700,10 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
       (rc = dev_alloc(l, &l->slab, l->slab_floats)) ||
       (rc = dev_alloc(l, &l->g, (int64_t)B)) || (rc = dev_alloc(l, &l->a_cache, (int64_t)B)) ||
       (rc = dev_alloc(l, &l->loss_tmp, 4)) || (rc = dev_alloc(l, &l->td_tmp, (int64_t)B)) ||
-      (rc = dev_alloc(l, &l->prio_tmp, (int64_t)B)) || (rc = dev_alloc(l, &l->dev_steps, 1)))
+      (rc = dev_alloc(l, &l->prio_tmp, (int64_t)B)))
     return fail(rc);
-  if (hipMemset(l->dev_steps, 0, sizeof(int64_t)) != hipSuccess ||
-      hipDeviceSynchronize() != hipSuccess)
-    return fail((set_error("step counter init failed"), ACME_ERR_HIP));
+  if (hipDeviceSynchronize() != hipSuccess)
+    return fail((set_error("learner init failed"), ACME_ERR_HIP));
   *out = l;
   return ACME_OK;
 }
@@ -692,8 +711,6 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
 int acme_dqn_destroy(acme_dqn* l) {
   if (!l) return ACME_OK;
   (void)hipDeviceSynchronize();
-  for (auto& g : l->graphs) (void)hipGraphExecDestroy(g.exec);
-  if (l->capture) (void)hipStreamDestroy(l->capture);
   for (void* p : l->allocs) (void)hipFree(p);
   for (auto& e : l->ev)
     if (e) (void)hipEventDestroy(e);
@@ -730,28 +747,61 @@ int acme_dqn_bind(acme_dqn* l, float* params, float* target, float* grads, float
   l->m = adam_m;
   l->v = adam_v;
   l->planes_stale = true;
-  // Captured graphs bake in the bound buffers: a re-bind invalidates them.
-  if (!l->graphs.empty()) {
-    ACME_HIP_TRY(hipDeviceSynchronize());
-    for (auto& g : l->graphs) (void)hipGraphExecDestroy(g.exec);
-    l->graphs.clear();
-  }
+  l->scales_ok = false;
   return ACME_OK;
 }
 
 int acme_dqn_params_changed(acme_dqn* l) {
   ACME_CHECK_ARG(l, "null learner");
   l->planes_stale = true;
+  l->scales_ok = false;  // new parameters: recalibrate (unless a scale state is restored)
+  return ACME_OK;
+}
+
+// Scale state = (w, r, wi, rl) of every record, host floats.
+int acme_dqn_scale_state(const acme_dqn* l, float* out, int32_t capacity, int32_t* count) {
+  ACME_CHECK_ARG(l && count, "null argument");
+  *count = l->scales ? 4 * kScCount : 0;
+  if (!l->scales || !out) return ACME_OK;
+  ACME_CHECK_ARG(capacity >= 4 * kScCount, "scale state needs %d floats", 4 * kScCount);
+  ACME_HIP_TRY(hipDeviceSynchronize());
+  for (int i = 0; i < kScCount; ++i)
+    ACME_HIP_TRY(hipMemcpy(out + 4 * i, l->scales + i, 4 * sizeof(float), hipMemcpyDeviceToHost));
+  return ACME_OK;
+}
+
+int acme_dqn_set_scale_state(acme_dqn* l, const float* in, int32_t count) {
+  ACME_CHECK_ARG(l && in, "null argument");
+  ACME_CHECK_ARG(l->scales && count == 4 * kScCount, "scale state of %d floats expected, got %d",
+                 l->scales ? 4 * kScCount : 0, count);
+  for (int i = 0; i < 4 * kScCount; ++i) {
+    int e;
+    const float m = std::frexp(in[i], &e);
+    ACME_CHECK_ARG(m == 0.5f, "scale state entries must be powers of two");
+  }
+  ACME_HIP_TRY(hipDeviceSynchronize());
+  for (int i = 0; i < kScCount; ++i)
+    ACME_HIP_TRY(hipMemcpy(l->scales + i, in + 4 * i, 4 * sizeof(float), hipMemcpyHostToDevice));
+  l->scales_ok = true;
+  return ACME_OK;
+}
+
+int acme_dqn_plane_overflow(acme_dqn* l, int32_t* overflow, int32_t reset) {
+  ACME_CHECK_ARG(l && overflow, "null argument");
+  *overflow = 0;
+  if (!l->overflow) return ACME_OK;
+  ACME_HIP_TRY(hipDeviceSynchronize());
+  int v = 0;
+  ACME_HIP_TRY(hipMemcpy(&v, l->overflow, sizeof(int), hipMemcpyDeviceToHost));
+  *overflow = v != 0;
+  if (reset) ACME_HIP_TRY(hipMemset(l->overflow, 0, sizeof(int)));
   return ACME_OK;
 }
 
 int64_t acme_dqn_num_steps(const acme_dqn* l) { return l ? l->num_steps : 0; }
 int acme_dqn_set_num_steps(acme_dqn* l, int64_t n) {
   ACME_CHECK_ARG(l && n >= 0, "bad argument");
-  ACME_HIP_TRY(hipDeviceSynchronize());
-  ACME_HIP_TRY(hipMemcpy(l->dev_steps, &n, sizeof(int64_t), hipMemcpyHostToDevice));
   l->num_steps = n;
-  l->dev_steps_synced = true;
   return ACME_OK;
 }
 
@@ -779,7 +829,8 @@ int acme_dqn_debug_buffer(const acme_dqn* l, const char* name, const float** out
                     {"dz3", l->dz3p}, {"dz2", l->dz2p}, {"dz1", l->dz1p}};
         for (auto& q : ptab)
           if (std::strcmp(q.n, name) == 0) {
-            int rc = launch_join_planes(q.pl.p, q.pl.stride, e.c, const_cast<float*>(e.p), 0);
+            int rc = launch_join_planes(q.pl.p, q.pl.stride, e.c, const_cast<float*>(e.p),
+                                        q.pl.sc, 0);
             if (rc != ACME_OK) return rc;
             ACME_HIP_TRY(hipDeviceSynchronize());
           }
@@ -811,10 +862,14 @@ int acme_dqn_q_values(acme_dqn* l, const void* obs, int64_t batch, int32_t use_t
   if (l->cfg.network == ACME_NET_NATURE_DQN && use_p3(l)) {
     int rc = sync_planes(l, st);
     if (rc == ACME_OK) rc = convert_frames(l, obs, obs, B, B, st);
-    if (rc != ACME_OK) return rc;
-    return nature_forward_p3(l, prm, use_target ? l->tpl : l->wpl, torso::Frames{l->frames},
-                             B, l->t1p, l->t2p,
-                             l->t3p, l->thid, q_out, st);
+    // Uncalibrated scales: one forward to measure the activations, then the real one.
+    for (int pass = l->scales_ok ? 1 : 0; pass < 2 && rc == ACME_OK; ++pass) {
+      rc = nature_forward_p3(l, prm, use_target ? l->tpl : l->wpl, torso::Frames{l->frames}, B,
+                             l->t1p, l->t2p, l->t3p, l->thid, q_out, st);
+      if (rc == ACME_OK && pass == 0)
+        rc = launch_plane_rescale(l->scales, kScTransient, kScTransient, -1, -1, l->overflow, st);
+    }
+    return rc;
   }
   if (l->cfg.network == ACME_NET_NATURE_DQN)
     return nature_forward(l, prm, obs, obs, B, B, l->t1, l->t2, l->t3, l->thid, q_out, st);
@@ -832,6 +887,32 @@ int acme_dqn_forward_backward_stage(acme_dqn* l, const acme_transition_batch* ba
 
 static int loss_and_dense_backward(acme_dqn* l, const acme_transition_batch* batch,
                                    const acme_dqn_outputs* out, hipStream_t st, bool join_dense);
+
+// Activation / gradient scales for new parameters (gemm_p3.h): two passes of the step's
+// forward, loss and backward on this batch (local IS normaliser, outputs to scratch; no
+// Adam, no target copy), each followed by a rescale of the transient records.  The first
+// pass runs at the current scales (1 after creation), whose maxima are measured before the
+// split and so are accurate even where that pass's planes lose precision; the second
+// refines them.  Writes nothing the real step does not overwrite.
+static int calibrate_scales(acme_dqn* l, const acme_transition_batch* batch, hipStream_t st) {
+  acme_transition_batch cb = *batch;
+  cb.global_min_probability = nullptr;
+  l->calibrating = true;
+  int rc = ACME_OK;
+  for (int pass = 0; pass < 2 && rc == ACME_OK; ++pass) {
+    rc = forward_backward_stage(l, &cb, nullptr, 2, st, false);
+    if (rc == ACME_OK) rc = forward_backward_stage(l, &cb, nullptr, 3, st, false);
+    if (rc == ACME_OK) rc = forward_backward_stage(l, &cb, nullptr, 1, st, false);
+    if (rc == ACME_OK)
+      rc = launch_plane_rescale(l->scales, kScTransient, kScTransient, -1, -1, l->overflow, st);
+  }
+  l->calibrating = false;
+  if (rc != ACME_OK) return rc;
+  // Overflows at the initial scales are expected and corrected by the passes.
+  ACME_HIP_TRY(hipMemsetAsync(l->overflow, 0, sizeof(int), st));
+  l->scales_ok = true;
+  return ACME_OK;
+}
 
 static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batch,
                                   const acme_dqn_outputs* out, int32_t stage, void* stream,
@@ -887,16 +968,19 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
   l->last_p3 = nature && use_p3(l);
   if (l->last_p3) {
     if ((rc = sync_planes(l, st)) != ACME_OK) return rc;
+    if (!l->scales_ok && !l->calibrating && (rc = calibrate_scales(l, batch, st)) != ACME_OK)
+      return rc;
+    l->last_p3 = true;
     hipStream_t tst = st;
     hipStream_t side = side_stream(l);
-    // conv1's input: a bf16 copy of [o_tm1; o_t] on the main stream for everything.  (Reading
+    // conv1's input: an f16 copy of [o_tm1; o_t] on the main stream for everything.  (Reading
     // the batch's uint8 frames in the kernels instead measured slower beside the side stream,
-    // 0.746 -> 0.750 ms per step: the uint8 image kernel is slower there than the bf16 one.)
-    if (!batch->obs_bf16 &&
+    // 0.746 -> 0.750 ms per step: the uint8 image kernel is slower there than the 16-bit one.)
+    if (!batch->obs_f16 &&
         (rc = convert_frames(l, batch->o_tm1, batch->o_t, B, 2 * B, st)) != ACME_OK)
       return rc;
-    // The dataset's fused gather may hand over the bf16 copy (acme_replay_sample_gather_frames).
-    const torso::Frames fwd_frames{batch->obs_bf16 ? static_cast<const void*>(batch->obs_bf16)
+    // The dataset's fused gather may hand over the f16 copy (acme_replay_sample_gather_frames).
+    const torso::Frames fwd_frames{batch->obs_f16 ? static_cast<const void*>(batch->obs_f16)
                                                    : static_cast<const void*>(l->frames)};
     l->cur_frames = fwd_frames;
     // Target forward (q_t_value) on the side stream, beside the online forward.
@@ -996,8 +1080,7 @@ int acme_dqn_grad_split(const acme_dqn* l, int64_t* split) {
 }
 
 // Adam (+ the parameter planes) and the periodic target copy; `copy` decided by the host.
-// graph: the step count is read from (and advanced on) the device, for a captured step.
-static int apply_impl(acme_dqn* l, bool copy, hipStream_t st, bool graph = false) {
+static int apply_impl(acme_dqn* l, bool copy, hipStream_t st) {
   const bool jax = l->cfg.semantics == ACME_SEMANTICS_JAX;
   ACME_PROF("adam", st, 0.0, 28.0 * (double)l->logical);
   // The parameter planes (plane path) are refreshed by the same pass.  t = num_steps + 1
@@ -1005,18 +1088,25 @@ static int apply_impl(acme_dqn* l, bool copy, hipStream_t st, bool graph = false
   int rc = launch_adam(l->params, l->grads, l->m, l->v, l->flat, l->cfg.learning_rate,
                        l->cfg.adam_beta1, l->cfg.adam_beta2, l->cfg.adam_epsilon,
                        l->num_steps + 1, l->p3_capable ? l->wpl : nullptr, l->flat, st,
-                       jax ? 1 : 0, graph ? l->dev_steps : nullptr);
+                       jax ? 1 : 0, nullptr,
+                       l->p3_capable ? l->scales + kScParams : nullptr);
   if (rc != ACME_OK) return rc;
-  if (!graph) l->dev_steps_synced = false;
   if (copy) {
     ACME_PROF("target_copy", st, 0.0, 8.0 * (double)l->logical);
     ACME_HIP_TRY(hipMemcpyAsync(l->target, l->params, l->flat * sizeof(float),
                                 hipMemcpyDeviceToDevice, st));
     if (l->p3_capable)
-      ACME_HIP_TRY(hipMemcpyAsync(l->tpl, l->wpl, 3 * l->flat * sizeof(uint16_t),
+      ACME_HIP_TRY(hipMemcpyAsync(l->tpl, l->wpl, gemm::kPlanes * l->flat * sizeof(uint16_t),
                                   hipMemcpyDeviceToDevice, st));
   }
-  return ACME_OK;
+  if (l->p3_capable) {
+    // Next step's scales from this step's maxima; the target planes copied from the
+    // parameter planes take their scale.
+    ACME_PROF("plane_rescale", st, 0.0, 0.0);
+    rc = launch_plane_rescale(l->scales, kScTransient, kScCount, copy ? kScParams : -1,
+                              copy ? kScTarget : -1, l->overflow, st);
+  }
+  return rc;
 }
 
 // TF: copy when num_steps % period == 0, then num_steps += 1 (tf/dqn/learning.py:157-161);
@@ -1034,98 +1124,18 @@ int acme_dqn_apply(acme_dqn* l, void* stream) {
   return ACME_OK;
 }
 
-// ------------------------------------------------------------------ step graphs
-// A plane-path step is ~40 launches on two streams joined by events; each event record or
-// wait on the caller's queue leaves it idle for several microseconds before its next kernel
-// (DESIGN §4.1).  The step is captured once per (batch / output pointers, B, mean
-// denominator, target copy) on a private stream — the side stream's fork / join become graph
-// edges — and replayed with one hipGraphLaunch on the caller's stream.  Measured slower
-// than the eager two-stream step (0.744 vs 0.725 ms per step at B = 512: in the eager trace
-// the GPU idles only 29 us per step, the rest is the two streams' kernels contending), so it
-// is opt-in: ACME_V_DQNGRAPH=2.  The section profiler bypasses it.
-static bool dqn_graphs_enabled() {
-  return tune("DQNGRAPH") == 2 && !prof::enabled();
-}
-
 static int step_impl(acme_dqn* l, const acme_transition_batch* batch, const acme_dqn_outputs* out,
-                     bool copy, hipStream_t st, bool graph = false) {
+                     bool copy, hipStream_t st) {
   int rc = forward_backward_stage(l, batch, out, 0, st, false);
   if (rc == ACME_OK) rc = forward_backward_stage(l, batch, out, 1, st, false);
-  if (rc == ACME_OK) rc = apply_impl(l, copy, st, graph);
+  if (rc == ACME_OK) rc = apply_impl(l, copy, st);
   return rc;
-}
-
-static int run_step_graph(acme_dqn* l, const acme_transition_batch* b, const acme_dqn_outputs* out,
-                          bool copy, hipStream_t st) {
-  const void* key[11] = {b->o_tm1, b->a_tm1, b->r_t, b->d_t, b->o_t, b->probabilities,
-                         b->global_min_probability, out ? out->loss : nullptr,
-                         out ? out->td_error : nullptr, out ? out->priorities : nullptr,
-                         out ? out->q_tm1 : nullptr};
-  for (auto& g : l->graphs)
-    if (g.B == b->batch && g.mean_over == b->mean_over && g.copy == copy &&
-        g.tune_gen == tune_generation() && memcmp(g.key, key, sizeof(key)) == 0) {
-      ACME_HIP_TRY(hipGraphLaunch(g.exec, st));
-      return ACME_OK;
-    }
-  if (l->graphs.size() >= 32) {  // a caller cycling many buffers: start over
-    ACME_HIP_TRY(hipStreamSynchronize(st));
-    for (auto& g : l->graphs) (void)hipGraphExecDestroy(g.exec);
-    l->graphs.clear();
-  }
-  if (!l->capture) ACME_HIP_TRY(hipStreamCreateWithFlags(&l->capture, hipStreamNonBlocking));
-  ACME_HIP_TRY(hipStreamBeginCapture(l->capture, hipStreamCaptureModeRelaxed));
-  int rc = step_impl(l, b, out, copy, l->capture, true);
-  hipGraph_t graph = nullptr;
-  hipError_t e = hipStreamEndCapture(l->capture, &graph);
-  if (rc != ACME_OK) {
-    if (graph) (void)hipGraphDestroy(graph);
-    return rc;
-  }
-  if (e != hipSuccess) {
-    set_error("step graph capture failed: %s", hipGetErrorString(e));
-    return ACME_ERR_HIP;
-  }
-  hipGraphExec_t exec = nullptr;
-  e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-  (void)hipGraphDestroy(graph);
-  if (e != hipSuccess) {
-    set_error("step graph instantiation failed: %s", hipGetErrorString(e));
-    return ACME_ERR_HIP;
-  }
-  acme_dqn::Graph g;
-  memcpy(g.key, key, sizeof(key));
-  g.B = b->batch;
-  g.mean_over = b->mean_over;
-  g.copy = copy;
-  g.tune_gen = tune_generation();
-  g.exec = exec;
-  l->graphs.push_back(g);
-  ACME_HIP_TRY(hipGraphLaunch(exec, st));
-  return ACME_OK;
 }
 
 int acme_dqn_step(acme_dqn* l, const acme_transition_batch* batch, const acme_dqn_outputs* out,
                   void* stream) {
   ACME_CHECK_ARG(l && batch && l->params, "null argument or unbound learner");
-  hipStream_t st = as_stream(stream);
-  const bool copy = copies_target(l);
-  int rc;
-  if (l->cfg.network == ACME_NET_NATURE_DQN && use_p3(l) && dqn_graphs_enabled()) {
-    ACME_CHECK_ARG(batch->batch >= 1 && batch->batch <= l->cfg.max_batch,
-                   "batch %lld outside [1, max_batch=%d]", (long long)batch->batch,
-                   l->cfg.max_batch);
-    // Parameter planes written from outside are refreshed eagerly, so no graph contains
-    // that conditional launch; so is the device step count after eager steps.
-    if ((rc = sync_planes(l, st)) != ACME_OK) return rc;
-    if (!l->dev_steps_synced) {
-      ACME_HIP_TRY(hipStreamSynchronize(st));
-      ACME_HIP_TRY(hipMemcpy(l->dev_steps, &l->num_steps, sizeof(int64_t), hipMemcpyHostToDevice));
-      l->dev_steps_synced = true;
-    }
-    rc = run_step_graph(l, batch, out, copy, st);
-  } else {
-    rc = step_impl(l, batch, out, copy, st);
-  }
+  const int rc = step_impl(l, batch, out, copies_target(l), as_stream(stream));
   if (rc != ACME_OK) return rc;
   l->num_steps += 1;
   return ACME_OK;

@@ -1,15 +1,21 @@
 // Plane-operand GEMM engine (gfx950 / CDNA4): f32 GEMMs whose operands are ALREADY
-// stored in HBM as exact bf16 planes, so the main loop is plain bf16 MFMA work.
+// stored in HBM as exact-to-f32-rounding f16 planes, so the main loop is plain f16 MFMA work.
 //
-// An f32 tensor x is kept as three bf16 arrays h, m, l with x = h + m + l exactly
-// (h = bf16(x), m = bf16(x - h), l = bf16(x - h - m); 8 + 8 + 8 significant bits), written
-// once by the kernel that produces x (a GEMM epilogue, the Adam update, a reduction).
-// The product a b is then the six bf16 MFMA terms of gemm_x6.h (hh, hm, mh, hl, lh, mm;
-// the dropped ml, lm, ll are below f32's unit roundoff).  An operand that is exactly a
-// bf16 value (the uint8 Atari frames: integers 0..255) is ONE plane, and its products
-// take 3 MFMAs instead of 6.  Compared with gemm_x6.h, which splits f32 operands while
-// staging every tile (5-6 VALU per element, redone for every block that reads it), the
-// split runs once per element and the staging path is 16-byte loads and stores.
+// An f32 tensor x is kept as two f16 arrays h, l of its scaled value y = x * w:
+// h = f16(y), l = f16(y - h) (11 + 11 significant bits, each rounding to nearest, so
+// |y - h - l| <= 2^-24 |y|: the representation error of an f32 rounding).  w is a power of
+// two chosen per tensor (PScale) so that the tensor's largest element sits at 2^7..2^8,
+// 2^8 below f16's overflow; every element within 2^-10 of the maximum then keeps the full
+// 2^-24 relative precision and smaller ones an absolute error <= 2^-33 max|x| (f16
+// subnormals), far below an f32 dot product's own rounding error.  Scaling by a power of
+// two commutes with every rounding, so the results do not depend on w.
+// The product a b is the three f16 MFMA terms hl, lh, hh (smallest first, f32
+// accumulation; the dropped ll is <= 2^-22 |ab| before rounding and below the f32
+// accumulation's own error), and the consumer multiplies its f32 result by
+// 1 / (w_a w_b) (exact).  An operand that is exactly an f16 value (the uint8 Atari frames:
+// integers 0..255) is ONE unscaled plane and its products take 2 MFMAs.  The planes are
+// written once per element by the kernel that produces x (a GEMM epilogue, the Adam
+// update, the head dZ kernel), which also records max|x| for the next step's scale.
 //
 // Operand modes (of the operand's HBM layout; gemm.h KCONTIG / RCONTIG):
 //   KCONTIG: a load unit is 8 consecutive k of one row  -> LDS [row][k], fragment =
@@ -20,16 +26,21 @@
 //            in four different 64-byte bank windows (conflict-free).
 //
 // Problem concept (conv_p3.h):
-//   static constexpr int A_MODE, B_MODE, A_PLANES, B_PLANES;   (planes 1 or 3)
+//   static constexpr int A_MODE, B_MODE, A_PLANES, B_PLANES;   (planes 1 or 2)
 //   int M, N, K, k_chunk;
 //   PlaneSrc a_src, b_src;   the operands' plane buffers (read through buffer descriptors)
+//                            and their scale records (the result is multiplied by both r)
 //   ARow a_row(int row) const;  uint32_t a_off(const ARow&, int k0, int kk) const;
 //   BRow b_row(int row) const;  uint32_t b_off(const BRow&, int k0, int kk) const;
 //     byte offset (within every plane) of the 16-byte unit at reduction index k0 + kk:
 //     KCONTIG: k .. k+7 of `row`; RCONTIG: rows row .. row+7 at k; kOOB for a unit of
 //     zeros (padding).  k0 is the stage's first k (a multiple of BK, wave-uniform, so the
 //     loaders' k0 arithmetic stays scalar) and kk the unit's offset in the stage.
-//   void store(int m, int n, float v, int split) const;
+//   float store8(int m, int n, const float (&v)[8], int split) const;  8 consecutive
+//     columns of one row (N a multiple of 8); returns max |value stored| of a plane output
+//     (0 otherwise);
+//   optional kAmax (+ PScale* amax_sc() const): the output's scale record, whose amax the
+//   epilogue raises to the block's maximum;
 //   optional kColSum (+ store_colsum): sum_k B[n][k], computed by one extra MFMA per B
 //   plane against an all-ones A fragment in the blocks of the first row tile;
 //   optional kZClass (+ for_z): blockIdx.z selects a sub-problem.
@@ -88,66 +99,143 @@ __device__ __forceinline__ P z_select_at(const P& p, int z) {
 
 using u32x4 = __attribute__((ext_vector_type(4))) uint32_t;
 using i16x4 = __attribute__((ext_vector_type(4))) short;
+using f16x8 = __attribute__((ext_vector_type(8))) _Float16;
 
 __device__ __forceinline__ u32x4 zero_u4() { return u32x4{0u, 0u, 0u, 0u}; }
 
 // Byte offset of a unit of zeros: beyond every plane's descriptor range.
 constexpr uint32_t kOOB = 0x80000000u;
 
+// Planes of a full f32 operand (a one-plane operand is an exact f16 value, unscaled).
+constexpr int kPlanes = 2;
+
+// Scale record of a plane tensor (device memory; the learners own arrays of them).
+//   w    producers store the planes of x * w (a power of two);
+//   r    consumers multiply their f32 results by r: 1 / the w the stored planes carry;
+//   wi   1 / w (a copy of the planes takes it as its r);
+//   rl   the r of the planes stored now, after a rescale moved r to the next step's scale
+//        (host-side joins of a transient tensor between steps: debug buffers);
+//   slot max |x| written since the last rescale, spread over kAmaxSlots words on separate
+//        128-B lines (f32 bits; atomicMax as an unsigned: one address took ~12 ns per wave's
+//        atomic, 7,168 of them serialised added 87 us to conv1_fwd); the rescale reduces them.
+constexpr int kAmaxSlots = 64;
+struct PScale {
+  float w, r, wi, rl;
+  uint32_t pad1[28];
+  struct Slot {
+    uint32_t v;
+    uint32_t pad[31];
+  } slot[kAmaxSlots];
+};
+static_assert(sizeof(PScale) == 128 * (1 + kAmaxSlots), "one 128-B line per amax slot");
+__device__ __forceinline__ float read_scale(const PScale* s) { return s ? s->r : 1.f; }
+
 // An operand's plane buffers: plane i at p + i * stride (elements), `bytes` readable
-// bytes per plane (the descriptor range; < 2^31).
+// bytes per plane (the descriptor range; < 2^31), and its scale record (null: unscaled).
 struct PlaneSrc {
   const uint16_t* p;
   int64_t stride;
   int32_t bytes;
+  const PScale* sc = nullptr;
 };
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const PlaneSrc& s, int pl) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(s.p + pl * s.stride), (short)0,
                                            s.bytes, 0x00020000);
 }
+// The factor a consumer applies to its f32 accumulators: 1 / (w_a w_b).
+__device__ __forceinline__ float result_scale(const PlaneSrc& a, const PlaneSrc& b) {
+  return read_scale(a.sc) * read_scale(b.sc);
+}
 
-// Exact three-way split of an f32 value (bf16 bit patterns).
-__device__ __forceinline__ void split3_bits(float x, uint16_t& h, uint16_t& m, uint16_t& l) {
-  const __bf16 hb = (__bf16)x;
-  const float r = x - (float)hb;
-  const __bf16 mb = (__bf16)r;
-  const __bf16 lb = (__bf16)(r - (float)mb);
+// Two-way split of a scaled f32 value y (f16 bit patterns): h = f16(y), l = f16(y - h)
+// (y - h is exact in f32).  |y| >= 65520 overflows h (caught by the rescale's check).
+__device__ __forceinline__ void split2_bits(float y, uint16_t& h, uint16_t& l) {
+  const _Float16 hb = (_Float16)y;
+  const _Float16 lb = (_Float16)(y - (float)hb);
   h = __builtin_bit_cast(uint16_t, hb);
-  m = __builtin_bit_cast(uint16_t, mb);
   l = __builtin_bit_cast(uint16_t, lb);
 }
-__device__ __forceinline__ float bf16_bits_to_f32(uint16_t b) {
-  return __builtin_bit_cast(float, (uint32_t)b << 16);
+__device__ __forceinline__ float f16_bits_to_f32(uint16_t b) {
+  return (float)__builtin_bit_cast(_Float16, b);
+}
+// Exact f16 of a byte (integers 0..255 have 8 significant bits).
+__device__ __forceinline__ uint32_t f16_of_byte(uint32_t x, int sh) {
+  return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)(uint16_t)((x >> sh) & 0xffu));
+}
+// Two packed f16 of bytes sh and sh + 8 of x.
+__device__ __forceinline__ uint32_t f16x2_of_bytes(uint32_t x, int sh) {
+  return f16_of_byte(x, sh) | (f16_of_byte(x, sh + 8) << 16);
 }
 
-// A plane tensor: plane i of element e at p[i * stride + e].
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// Raises one of sc's amax slots (chosen by the wave's position in the grid) to the wave's
+// maximum of v (v >= 0, or NaN); every lane of the wave calls.
+__device__ __forceinline__ void amax_commit(PScale* sc, float v) {
+  v = wave_max(v);
+  const int wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (sc && (threadIdx.x & 63) == 0 && v != 0.f)
+    atomicMax(&sc->slot[wid & (kAmaxSlots - 1)].v, __builtin_bit_cast(uint32_t, v));
+}
+
+// A plane tensor: plane i of element e at p[i * stride + e], written as x * sc->w.
 struct Planes {
   uint16_t* p;
   int64_t stride;
-  __device__ __forceinline__ void put(int64_t e, float x) const {
-    uint16_t h, m, l;
-    split3_bits(x, h, m, l);
+  PScale* sc;
+  __device__ __forceinline__ float w() const { return sc->w; }
+  // Stores x; returns |x| (the caller's amax).
+  __device__ __forceinline__ float put(int64_t e, float x) const {
+    uint16_t h, l;
+    split2_bits(x * w(), h, l);
     p[e] = h;
-    p[stride + e] = m;
-    p[2 * stride + e] = l;
+    p[stride + e] = l;
+    return fabsf(x);
   }
 };
 struct CPlanes {
   const uint16_t* p;
   int64_t stride;
-  __device__ __forceinline__ u32x4 ld8(int64_t e, int plane) const {
-    return *reinterpret_cast<const u32x4*>(p + plane * stride + e);
-  }
-  // x > 0 of a value whose planes are stored (ReLU masks: h = bf16(x) has x's sign and
-  // is zero only for |x| below bf16's subnormal range).
+  const PScale* sc;
+  // x > 0 of a value whose planes are stored (ReLU masks: h = f16(x w) has x's sign and
+  // is zero only for x w below half of f16's smallest subnormal, i.e. x < 2^-33 max|x|).
   __device__ __forceinline__ bool positive(int64_t e) const {
     const uint16_t h = p[e];
     return h != 0 && (h & 0x8000) == 0;
   }
+  // The stored value (between steps: at the scale the planes were written with).
   __device__ __forceinline__ float value(int64_t e) const {
-    return (bf16_bits_to_f32(p[e]) + bf16_bits_to_f32(p[stride + e])) +
-           bf16_bits_to_f32(p[2 * stride + e]);
+    return (f16_bits_to_f32(p[e]) + f16_bits_to_f32(p[stride + e])) * (sc ? sc->rl : 1.f);
   }
+};
+
+// The MFMA terms of one 32x32x16 product of an NPA-plane A fragment and an NPB-plane B
+// fragment, smallest first: (1,0), (0,1), (0,0).
+template <int NPA, int NPB>
+__device__ __forceinline__ void p3_terms(const f16x8 (&fa)[NPA], const f16x8 (&fb)[NPB],
+                                         f32x16& acc) {
+  static_assert((NPA == 1 || NPA == 2) && (NPB == 1 || NPB == 2), "1 or 2 planes per operand");
+  if constexpr (NPA == 2) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[1], fb[0], acc, 0, 0, 0);
+  if constexpr (NPB == 2) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[0], fb[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[0], fb[0], acc, 0, 0, 0);
+}
+template <int NPA, int NPB>
+constexpr int p3_nterms() {
+  return 1 + (NPA == 2 ? 1 : 0) + (NPB == 2 ? 1 : 0);
+}
+
+// Problems with `static constexpr bool kAmax = true` write a plane output whose scale
+// record amax_sc() collects max |x|.
+template <class P, class = void>
+struct HasAmax {
+  static constexpr bool value = false;
+};
+template <class P>
+struct HasAmax<P, decltype(void(P::kAmax))> {
+  static constexpr bool value = P::kAmax;
 };
 
 // Optional vector epilogue: problems with `static constexpr bool kStore8 = true` receive
@@ -161,6 +249,11 @@ template <class P>
 struct HasStore8<P, decltype(void(P::kStore8))> {
   static constexpr bool value = P::kStore8;
 };
+
+__device__ __forceinline__ f16x8 ones16() {
+  const _Float16 o = (_Float16)1.f;
+  return f16x8{o, o, o, o, o, o, o, o};
+}
 
 template <int BK>
 __device__ __forceinline__ int p3_kswz(int row) {
@@ -211,13 +304,13 @@ struct PlanP3 {
     else return u / OPK;
   }
   // MFMA operand of rows rb .. rb+31 (rb a multiple of 32), k step s (16 k).
-  __device__ static __forceinline__ bf16x8 frag(const uint8_t* tile, int plane, int rb, int s,
-                                                int lane) {
+  __device__ static __forceinline__ f16x8 frag(const uint8_t* tile, int plane, int rb, int s,
+                                               int lane) {
     const uint8_t* t = tile + plane * PLANE;
     if constexpr (MODE == KCONTIG) {
       const int row = rb + (lane & 31);
       const int c = 2 * s + (lane >> 5);
-      return *reinterpret_cast<const bf16x8*>(t + row * (2 * BK) + 16 * (c ^ p3_kswz<BK>(row)));
+      return *reinterpret_cast<const f16x8*>(t + row * (2 * BK) + 16 * (c ^ p3_kswz<BK>(row)));
     } else {
       const int h = lane >> 5, g = (lane >> 4) & 1, q = (lane >> 2) & 3, pp = lane & 3;
       const int row = rb + 16 * g + 4 * pp;
@@ -230,7 +323,7 @@ struct PlanP3 {
           (lds_i16x4*)(t + k1 * (2 * R) + 2 * (row ^ (p3_rswz<R>(k1) << 5))));
       const __attribute__((ext_vector_type(8))) short v{lo[0], lo[1], lo[2], lo[3],
                                                         hi[0], hi[1], hi[2], hi[3]};
-      return __builtin_bit_cast(bf16x8, v);
+      return __builtin_bit_cast(f16x8, v);
     }
   }
 };
@@ -245,7 +338,7 @@ struct P3Core {
   static constexpr int NPA = P::A_PLANES, NPB = P::B_PLANES;
   static_assert(TM % 32 == 0 && TN % 32 == 0, "wave tile must be a multiple of 32x32");
   static_assert(BK == 16 || BK == 32, "BK must be 16 or 32");
-  static_assert((NPA == 1 || NPA == 3) && (NPB == 1 || NPB == 3), "1 or 3 planes per operand");
+  static_assert((NPA == 1 || NPA == 2) && (NPB == 1 || NPB == 2), "1 or 2 planes per operand");
   using PA = PlanP3<BM, NT, P::A_MODE, NPA, BK>;
   using PB = PlanP3<BN, NT, P::B_MODE, NPB, BK>;
   static constexpr int STAGE = PA::BYTES + PB::BYTES;
@@ -262,21 +355,19 @@ struct P3Core {
   __device__ static __forceinline__ void mma(const uint8_t* sa, const uint8_t* sb, int wm, int wn,
                                              int lane, f32x16 (&acc)[MT][NTL], f32x16 (&cs)[NCS],
                                              bool do_colsum, const Hook& hook = Hook()) {
-    const bf16x8 ones{(__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f,
-                      (__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f};
 #pragma unroll
     for (int s = S0; s < S1; ++s) {
-      bf16x8 fa[MT][NPA], fb[NTL][NPB];
+      f16x8 fa[MT][NPA], fb[NTL][NPB];
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int pl = 0; pl < NPA; ++pl)
-          fa[i][pl] = P3_EXP == 2 ? ones : PA::frag(sa, pl, wm * TM + i * 32, s, lane);
+          fa[i][pl] = P3_EXP == 2 ? ones16() : PA::frag(sa, pl, wm * TM + i * 32, s, lane);
 #pragma unroll
       for (int j = 0; j < NTL; ++j)
 #pragma unroll
         for (int pl = 0; pl < NPB; ++pl)
-          fb[j][pl] = P3_EXP == 2 ? ones : PB::frag(sb, pl, wn * TN + j * 32, s, lane);
+          fb[j][pl] = P3_EXP == 2 ? ones16() : PB::frag(sb, pl, wn * TN + j * 32, s, lane);
       if constexpr (P3_EXP == 3) {
 #pragma unroll
         for (int i = 0; i < MT; ++i)
@@ -290,21 +381,7 @@ struct P3Core {
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NTL; ++j) {
-          // Smallest terms first: (1,1), (2,0), (0,2), (1,0), (0,1), (0,0).
-          if constexpr (NPA == 3 && NPB == 3) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], acc[i][j], 0, 0, 0);
-          } else if constexpr (NPA == 3) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], acc[i][j], 0, 0, 0);
-          } else if constexpr (NPB == 3) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], acc[i][j], 0, 0, 0);
-          }
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], acc[i][j], 0, 0, 0);
+          p3_terms<NPA, NPB>(fa[i], fb[j], acc[i][j]);
           if (s == S0) hook(i * NTL + j);
         }
       if constexpr (kColSum) {
@@ -313,7 +390,7 @@ struct P3Core {
           for (int j = 0; j < NTL; ++j)
 #pragma unroll
             for (int pl = NPB - 1; pl >= 0; --pl)
-              cs[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fb[j][pl], cs[j], 0, 0, 0);
+              cs[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ones16(), fb[j][pl], cs[j], 0, 0, 0);
         }
       }
     }
@@ -321,8 +398,8 @@ struct P3Core {
 
   // The two halves of mma() for one k16 step, for callers that software-pipeline the
   // fragment reads (same terms in the same order, so the same bits).
-  using FragA = bf16x8[MT][NPA];
-  using FragB = bf16x8[NTL][NPB];
+  using FragA = f16x8[MT][NPA];
+  using FragB = f16x8[NTL][NPB];
   __device__ static __forceinline__ void read_frags(const uint8_t* sa, const uint8_t* sb, int wm,
                                                     int wn, int s, int lane, FragA& fa,
                                                     FragB& fb) {
@@ -338,34 +415,17 @@ struct P3Core {
   __device__ static __forceinline__ void mfma_frags(const FragA& fa, const FragB& fb,
                                                     f32x16 (&acc)[MT][NTL], f32x16 (&cs)[NCS],
                                                     bool do_colsum) {
-    const bf16x8 ones{(__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f,
-                      (__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f};
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
-      for (int j = 0; j < NTL; ++j) {
-        if constexpr (NPA == 3 && NPB == 3) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], acc[i][j], 0, 0, 0);
-        } else if constexpr (NPA == 3) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], acc[i][j], 0, 0, 0);
-        } else if constexpr (NPB == 3) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], acc[i][j], 0, 0, 0);
-        }
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], acc[i][j], 0, 0, 0);
-      }
+      for (int j = 0; j < NTL; ++j) p3_terms<NPA, NPB>(fa[i], fb[j], acc[i][j]);
     if constexpr (kColSum) {
       if (do_colsum) {
 #pragma unroll
         for (int j = 0; j < NTL; ++j)
 #pragma unroll
           for (int pl = NPB - 1; pl >= 0; --pl)
-            cs[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fb[j][pl], cs[j], 0, 0, 0);
+            cs[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ones16(), fb[j][pl], cs[j], 0, 0, 0);
       }
     }
   }
@@ -377,46 +437,36 @@ struct P3Core {
                                                   int wave, int wm, int wn, int lane, int split,
                                                   f32x16 (&acc)[MT][NTL], f32x16 (&cs)[NCS],
                                                   bool do_colsum) {
+    static_assert(HasStore8<P>::value, "plane problems store 8 columns at a time");
     const int r = lane & 31, h = lane >> 5;
-    if constexpr (HasStore8<P>::value) {
-      // Row-major restage through LDS, one 32-row block of the wave's tile at a time, so
-      // each lane finishes 8 consecutive columns of one row (one decode per 8 outputs,
-      // 16-byte plane / 32-byte f32 stores).
-      constexpr int PITCH = TN + 4;
-      float* cw = reinterpret_cast<float*>(smem) + wave * 32 * PITCH;
-      constexpr int CHUNKS = 32 * TN / 8;
+    // Row-major restage through LDS, one 32-row block of the wave's tile at a time, so
+    // each lane finishes 8 consecutive columns of one row (one decode per 8 outputs,
+    // 16-byte plane / 32-byte f32 stores).
+    constexpr int PITCH = TN + 4;
+    float* cw = reinterpret_cast<float*>(smem) + wave * 32 * PITCH;
+    constexpr int CHUNKS = 32 * TN / 8;
+    float amx = 0.f;
 #pragma unroll
-      for (int i = 0; i < MT; ++i) {
+    for (int i = 0; i < MT; ++i) {
 #pragma unroll
-        for (int j = 0; j < NTL; ++j)
+      for (int j = 0; j < NTL; ++j)
 #pragma unroll
-          for (int v = 0; v < 16; ++v)
-            cw[((v & 3) + 8 * (v >> 2) + 4 * h) * PITCH + j * 32 + r] = acc[i][j][v];
-        __syncthreads();
+        for (int v = 0; v < 16; ++v)
+          cw[((v & 3) + 8 * (v >> 2) + 4 * h) * PITCH + j * 32 + r] = acc[i][j][v];
+      __syncthreads();
 #pragma unroll
-        for (int c = lane; c < CHUNKS; c += 64) {
-          const int row = c / (TN / 8), col = 8 * (c % (TN / 8));
-          const int m = m0 + wm * TM + i * 32 + row;
-          const int n = n0 + wn * TN + col;
-          const f32x4 lo = *reinterpret_cast<const f32x4*>(cw + row * PITCH + col);
-          const f32x4 hi = *reinterpret_cast<const f32x4*>(cw + row * PITCH + col + 4);
-          const float v8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          if (m < p.M && n < p.N) p.store8(m, n, v8, split);
-        }
-        __syncthreads();
+      for (int c = lane; c < CHUNKS; c += 64) {
+        const int row = c / (TN / 8), col = 8 * (c % (TN / 8));
+        const int m = m0 + wm * TM + i * 32 + row;
+        const int n = n0 + wn * TN + col;
+        const f32x4 lo = *reinterpret_cast<const f32x4*>(cw + row * PITCH + col);
+        const f32x4 hi = *reinterpret_cast<const f32x4*>(cw + row * PITCH + col + 4);
+        const float v8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        if (m < p.M && n < p.N) amx = fmaxf(amx, p.store8(m, n, v8, split));
       }
-    } else {
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NTL; ++j)
-#pragma unroll
-          for (int v = 0; v < 16; ++v) {
-            const int m = m0 + wm * TM + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-            const int n = n0 + wn * TN + j * 32 + r;
-            if (m < p.M && n < p.N) p.store(m, n, acc[i][j][v], split);
-          }
+      __syncthreads();
     }
+    if constexpr (HasAmax<P>::value) amax_commit(p.amax_sc(), amx);
     if constexpr (kColSum) {
       if (do_colsum && h == 0) {
 #pragma unroll
@@ -629,7 +679,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in, int
           // instead of delaying the first MFMA.
           constexpr int RD = C::MT * NPA * (P::A_MODE == KCONTIG ? 1 : 2) +
                              C::NTL * NPB * (P::B_MODE == KCONTIG ? 1 : 2);
-          constexpr int TERMS = NPA * NPB == 9 ? 6 : (NPA * NPB == 3 ? 3 : 1);
+          constexpr int TERMS = p3_nterms<NPA, NPB>();
           constexpr int MF = C::MT * C::NTL * TERMS;
           constexpr int WR = PA::PER_THREAD * NPA + PB::PER_THREAD * NPB;
           constexpr int STEPS = BK / 16;
@@ -994,11 +1044,12 @@ inline int p3_n_major(const P& p) {
   return (int64_t)p.N * P::B_PLANES > (int64_t)p.M * P::A_PLANES ? 1 : 0;
 }
 
-// TFLOP/s ceiling of a plane GEMM in algorithmic (f32) FLOPs: bf16 dense MFMA peak over
-// the MFMA terms per product (6 for three-plane x three-plane, 3 with a one-plane operand).
+// TFLOP/s ceiling of a plane GEMM in algorithmic (f32) FLOPs: the f16 dense MFMA peak
+// (= bf16's, 2.5 PF) over the MFMA terms per product (3 for two planes x two planes, 2
+// with a one-plane operand).
 template <class P>
 constexpr double p3_peak_tflops() {
-  return 2500.0 / (P::A_PLANES * P::B_PLANES == 9 ? 6.0 : (P::A_PLANES * P::B_PLANES == 3 ? 3.0 : 1.0));
+  return 2500.0 / (double)p3_nterms<P::A_PLANES, P::B_PLANES>();
 }
 
 template <class Kern>

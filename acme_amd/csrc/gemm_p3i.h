@@ -1,4 +1,4 @@
-// Image-resident implicit-GEMM convolution on exact bf16 planes (gfx950).
+// Image-resident implicit-GEMM convolution on f16 operand planes (gfx950).
 //
 // gemm_p3.h reads a convolution's A operand as im2col rows: every input pixel is fetched
 // KH*KW/S^2 times (4x for conv1 / conv2, 9x for conv3) and every fetch goes global -> VGPR
@@ -90,7 +90,7 @@ struct ImgGeom {
 
 // Pixel-pair images for a 4-channel input (conv1 over the frames, one plane): a unit is two
 // horizontally adjacent pixels x 4 channels, which is exactly the 8 k of one MFMA lane
-// (k = (kh, kw, c): kw even, kw + 1) -- 16 B of the bf16 frame copy.  A 32-k stage is one
+// (k = (kh, kw, c): kw even, kw + 1) -- 16 B of the f16 frame copy.  A 32-k stage is one
 // kernel row kh (KW * CI = 32).  LDS layout: unit (ih, pw) (pw = iw / 2) at (frame * IH +
 // ih) * PAIRS + col, col = the even pairs then the odd ones, so stride-S output columns
 // read consecutive units (conflict-free ds_read_b128 lane groups).
@@ -155,8 +155,9 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
   using PB = typename Cfg::PB;
   constexpr int NT = Cfg::NT, NTL = Cfg::NTL, TN = Cfg::TN, BK = Cfg::BK, KS = Cfg::KS;
   constexpr int PLANE = Cfg::PLANE, NPA = Cfg::NPA;
-  static_assert(P::A_MODE == KCONTIG && (NPA == 1 || NPA == 3) && P::B_PLANES == 3,
-                "k-contiguous A (one or three planes), three-plane B");
+  constexpr int NPB = kPlanes;
+  static_assert(P::A_MODE == KCONTIG && (NPA == 1 || NPA == kPlanes) && P::B_PLANES == NPB,
+                "k-contiguous A (one or two planes), two-plane B");
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
   const int tid = threadIdx.x;
@@ -175,10 +176,10 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
 #pragma unroll
   for (int i = 0; i < PB::PER_THREAD; ++i)
     brow[i] = p.b_row(PB::owns(tid + i * NT) ? PB::row_of(tid + i * NT) : 0);
-  __amdgpu_buffer_rsrc_t srcB[3];
+  __amdgpu_buffer_rsrc_t srcB[NPB];
 #pragma unroll
-  for (int pl = 0; pl < 3; ++pl) srcB[pl] = plane_rsrc(p.b_src, pl);
-  u32x4 rb[2][PB::PER_THREAD][3];
+  for (int pl = 0; pl < NPB; ++pl) srcB[pl] = plane_rsrc(p.b_src, pl);
+  u32x4 rb[2][PB::PER_THREAD][NPB];
   auto fetch_b = [&](auto S, int k0) {
     constexpr int set = decltype(S)::value;
 #pragma unroll
@@ -187,7 +188,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
       const int kk = PB::kk_of(u);
       const uint32_t off = (PB::owns(u) && k0 + kk < p.K) ? p.b_off(brow[i], k0, kk) : kOOB;
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
+      for (int pl = 0; pl < NPB; ++pl)
         rb[set][i][pl] =
             __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srcB[pl], off, 0, 0));
     }
@@ -201,7 +202,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
       if (!PB::owns(u)) continue;
       const int off = PB::offset(u);
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
+      for (int pl = 0; pl < NPB; ++pl)
         *reinterpret_cast<u32x4*>(sb + pl * PB::PLANE + off) = rb[set][i][pl];
     }
   };
@@ -272,34 +273,21 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
     for (int i = 0; i < MT; ++i) sg[i] = GI::stage(ln[i], k0);
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      bf16x8 fb[NTL][3];
+      f16x8 fb[NTL][NPB];
 #pragma unroll
       for (int j = 0; j < NTL; ++j)
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) fb[j][pl] = PB::frag(sb, pl, wn * TN + j * 32, s, lane);
+        for (int pl = 0; pl < NPB; ++pl) fb[j][pl] = PB::frag(sb, pl, wn * TN + j * 32, s, lane);
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
         const int u = GI::unit(sg[i], ln[i], k0, s, lane >> 5);
         const int a = u >= 0 ? u : PLANE - 16;
-        bf16x8 fa[NPA];
+        f16x8 fa[NPA];
 #pragma unroll
         for (int pl = 0; pl < NPA; ++pl)
-          fa[pl] = *reinterpret_cast<const bf16x8*>(smem + pl * PLANE + a);
+          fa[pl] = *reinterpret_cast<const f16x8*>(smem + pl * PLANE + a);
 #pragma unroll
-        for (int j = 0; j < NTL; ++j) {
-          // Smallest terms first, as gemm_p3.h.
-          if constexpr (NPA == 3) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[j][1], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[j][0], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[j][2], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[j][0], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[j][1], acc[i][j], 0, 0, 0);
-          } else {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[j][2], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[j][1], acc[i][j], 0, 0, 0);
-          }
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[j][0], acc[i][j], 0, 0, 0);
-        }
+        for (int j = 0; j < NTL; ++j) p3_terms<NPA, NPB>(fa, fb[j], acc[i][j]);
       }
     }
   };

@@ -4,8 +4,8 @@
 // output pixel (each a stride-1 correlation with a 2x2 sub-kernel, K = 2*2*CO = 256) and
 // gemm_p3.h runs the classes as blockIdx.z: every class gathers its dZ rows from HBM / L2
 // again (PMC: 169 MB per launch against 81 MB of distinct bytes) and each block computes
-// only 8 k-stages.  Here one block owns one frame: the frame's dZ image (OH x OW x CO, all
-// three planes, XOR-swizzled 16-B chunks as gemm_p3i.h) is loaded into LDS once, and the
+// only 8 k-stages.  Here one block owns one frame: the frame's dZ image (OH x OW x CO, both
+// planes, XOR-swizzled 16-B chunks as gemm_p3i.h) is loaded into LDS once, and the
 // four classes are computed from it at once -- waves 2z and 2z + 1 own class z's rows (at
 // most 128: 64 each, MT = 2) -- with the four classes' weight panels streamed together
 // through the two-stage register-staged ring (one 16-B unit per thread per plane).  The
@@ -28,8 +28,9 @@ struct P3SCfg {
   static constexpr int CPX = C / 8;
   static constexpr int FRAME = H * W * 2 * C;                  // one frame's image, one plane
   static constexpr int PLANE = FPB * FRAME + 16;               // + the zero unit
-  static constexpr int IMG = 3 * PLANE;
-  using PB = PlanP3<BN, 64 * 2 * CLASSES, KCONTIG, 3, BK>;     // one class's B stage
+  static constexpr int NP = kPlanes;
+  static constexpr int IMG = NP * PLANE;
+  using PB = PlanP3<BN, 64 * 2 * CLASSES, KCONTIG, NP, BK>;    // one class's B stage
   static constexpr int STAGE_B = CLASSES * PB::BYTES;
   static constexpr int MAIN = IMG + 2 * STAGE_B;
   static constexpr int EPI = NW * 32 * (BN + 4) * 4;
@@ -50,7 +51,7 @@ __global__ void __launch_bounds__(64 * 2 * G::S * G::S * FPB) gemm_p3s_kernel(
   using C = typename Cfg::Core;
   using P = conv::P3ConvDgradSubZ<G>;
   constexpr int NT = Cfg::NT, BK = Cfg::BK, KS = Cfg::KS, MT = Cfg::MT, PLANE = Cfg::PLANE;
-  constexpr int W = Cfg::W, H = Cfg::H, CPX = Cfg::CPX;
+  constexpr int W = Cfg::W, H = Cfg::H, CPX = Cfg::CPX, NP = Cfg::NP;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -64,20 +65,20 @@ __global__ void __launch_bounds__(64 * 2 * G::S * G::S * FPB) gemm_p3s_kernel(
   pz.M = m0 + nhw < pz.M ? m0 + nhw : pz.M;  // this frame's rows of the class only
   const int nk = P::KR / BK;
 
-  // ---- B: loader thread tid loads unit tid % 128 of class tid / 128's panel (3 planes).
+  // ---- B: loader thread tid loads unit tid % 128 of class tid / 128's panel (each plane).
   const bool bload = tid < Cfg::BT;
   const int bz = bload ? tid / PB::UNITS : 0, bu = tid - bz * PB::UNITS;
   const P pb = p_in.for_z(bz);
   const typename P::BRow brow = pb.b_row(PB::row_of(bu));
-  __amdgpu_buffer_rsrc_t srcB[3];
+  __amdgpu_buffer_rsrc_t srcB[NP];
 #pragma unroll
-  for (int pl = 0; pl < 3; ++pl) srcB[pl] = plane_rsrc(p_in.b_src, pl);
-  u32x4 rb[2][3];
+  for (int pl = 0; pl < NP; ++pl) srcB[pl] = plane_rsrc(p_in.b_src, pl);
+  u32x4 rb[2][NP];
   auto fetch_b = [&](auto S_, int k0) {
     constexpr int set = decltype(S_)::value;
     const uint32_t off = bload && k0 < P::KR ? pb.b_off(brow, k0, PB::kk_of(bu)) : kOOB;
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl)
+    for (int pl = 0; pl < NP; ++pl)
       rb[set][pl] =
           __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srcB[pl], off, 0, 0));
   };
@@ -86,7 +87,7 @@ __global__ void __launch_bounds__(64 * 2 * G::S * G::S * FPB) gemm_p3s_kernel(
     uint8_t* sb = smem + Cfg::IMG + buf * Cfg::STAGE_B + bz * PB::BYTES;
     if (!bload) return;
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl)
+    for (int pl = 0; pl < NP; ++pl)
       *reinterpret_cast<u32x4*>(sb + pl * PB::PLANE + PB::offset(bu)) = rb[set][pl];
   };
   using S0 = std::integral_constant<int, 0>;
@@ -98,17 +99,17 @@ __global__ void __launch_bounds__(64 * 2 * G::S * G::S * FPB) gemm_p3s_kernel(
   {
     constexpr int UNITS = FPB * H * W * CPX;
     constexpr int PER = (UNITS + NT - 1) / NT;
-    __amdgpu_buffer_rsrc_t srcA[3];
+    __amdgpu_buffer_rsrc_t srcA[NP];
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl) srcA[pl] = plane_rsrc(p_in.a_src, pl);
-    u32x4 v[PER][3];
+    for (int pl = 0; pl < NP; ++pl) srcA[pl] = plane_rsrc(p_in.a_src, pl);
+    u32x4 v[PER][NP];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const int u = tid + j * NT;
       const bool ok = u < UNITS && blockIdx.x * FPB + u / (H * W * CPX) < frames;
       const uint32_t off = ok ? (uint32_t)(((int64_t)blockIdx.x * UNITS + u) * 16) : kOOB;
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
+      for (int pl = 0; pl < NP; ++pl)
         v[j][pl] =
             __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srcA[pl], off, 0, 0));
     }
@@ -120,10 +121,10 @@ __global__ void __launch_bounds__(64 * 2 * G::S * G::S * FPB) gemm_p3s_kernel(
         const int q = uu / CPX, c = uu - q * CPX;
         const int a = fu * Cfg::FRAME + q * (2 * Cfg::C) + 16 * (c ^ Cfg::swz(q));
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<u32x4*>(smem + pl * PLANE + a) = v[j][pl];
+        for (int pl = 0; pl < NP; ++pl) *reinterpret_cast<u32x4*>(smem + pl * PLANE + a) = v[j][pl];
       }
     }
-    if (tid < 3) *reinterpret_cast<u32x4*>(smem + tid * PLANE + PLANE - 16) = zero_u4();
+    if (tid < NP) *reinterpret_cast<u32x4*>(smem + tid * PLANE + PLANE - 16) = zero_u4();
   }
   stash_b(S0{}, 0);
 
@@ -162,24 +163,18 @@ __global__ void __launch_bounds__(64 * 2 * G::S * G::S * FPB) gemm_p3s_kernel(
     }
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      bf16x8 fb[3];
+      f16x8 fb[NP];
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) fb[pl] = PB::frag(sb, pl, 0, s, lane);
+      for (int pl = 0; pl < NP; ++pl) fb[pl] = PB::frag(sb, pl, 0, s, lane);
       const int c = cb + 2 * s + (lane >> 5);
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
         const uint8_t* a = qb[i] >= 0 ? img + qb[i] + 16 * (c ^ qs[i]) : smem + PLANE - 16;
-        bf16x8 fa[3];
+        f16x8 fa[NP];
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
-          fa[pl] = *reinterpret_cast<const bf16x8*>(a + pl * PLANE);
-        // Smallest terms first, as gemm_p3.h.
-        acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1], acc[i][0], 0, 0, 0);
-        acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0], acc[i][0], 0, 0, 0);
-        acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[2], acc[i][0], 0, 0, 0);
-        acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[0], acc[i][0], 0, 0, 0);
-        acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[1], acc[i][0], 0, 0, 0);
-        acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0], acc[i][0], 0, 0, 0);
+        for (int pl = 0; pl < NP; ++pl)
+          fa[pl] = *reinterpret_cast<const f16x8*>(a + pl * PLANE);
+        p3_terms<NP, NP>(fa, fb, acc[i][0]);
       }
     }
   };

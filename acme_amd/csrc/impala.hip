@@ -77,14 +77,20 @@ struct acme_impala {
   // and the spin-timeout word, zeroed before every launch.
   unsigned long long* xg = nullptr;
   unsigned* tmo = nullptr;
-  // Plane path of the Atari learner step (the DQN kernels: exact three-plane bf16 MFMA):
+  // Plane path of the Atari learner step (the DQN kernels: scaled two-plane f16 MFMA):
   // parameter planes of the torso + W_i prefix of the flat buffer, refreshed at the start
-  // of every plane step; bf16 frames; activation / gradient planes; its own split-K slab.
+  // of every plane step; f16 frames; activation / gradient planes; its own split-K slab.
   bool p3_capable = false;
   int64_t p3_prefix = 0;  // floats of the flat buffer split into planes (torso + W_i)
   uint16_t* wpl = nullptr;
   uint16_t* frames = nullptr;
   torso::Plane x1p{}, x2p{}, x3p{}, dz1p{}, dz2p{}, dz3p{}, dgp{};
+  // Scale records (gemm_p3.h PScale): the transient torso activations / gradients first
+  // (rescaled at the end of every plane step), then the parameter and dgates planes (set
+  // from their exact maxima by every split); sticky overflow flag.
+  gemm::PScale* scales = nullptr;
+  int* overflow = nullptr;
+  bool scales_ok = false;
   float* pslab = nullptr;
   bool last_p3 = false;  // the last learner step ran the plane path (debug buffers join planes)
   int64_t last_rows = 0;
@@ -93,6 +99,9 @@ struct acme_impala {
 namespace {
 
 int64_t align64(int64_t x) { return (x + 63) & ~int64_t(63); }
+
+enum { kScX1, kScX2, kScX3, kScDz3, kScDz2, kScDz1, kScTransient, kScParams = kScTransient,
+       kScDgates, kScCount };
 
 int add_tensor(acme_impala* l, const std::string& name, std::initializer_list<int64_t> shape) {
   Tensor t;
@@ -839,12 +848,12 @@ bool atari(const acme_impala* l) { return l->cfg.torso == ACME_IMPALA_TORSO_ATAR
     }                                                                                          \
   } while (0)
 
-// Plane view of parameter tensor t in the [3][flat] parameter planes.
+// Plane view of parameter tensor t in the [2][flat] parameter planes.
 torso::Plane WP(const acme_impala* l, int t) {
-  return torso::Plane{l->wpl + l->tensors[t].offset, l->flat};
+  return torso::Plane{l->wpl + l->tensors[t].offset, l->flat, l->scales + kScParams};
 }
 gemm::PlaneSrc SRC(const torso::Plane& x, int64_t elems) {
-  return gemm::PlaneSrc{x.p, x.stride, (int32_t)(2 * elems)};
+  return gemm::PlaneSrc{x.p, x.stride, (int32_t)(2 * elems), x.sc};
 }
 torso::PWeights torso_pw(const acme_impala* l) {
   return torso::PWeights{WP(l, l->t_c[0]), WP(l, l->t_c[2]), WP(l, l->t_c[4]),
@@ -929,17 +938,18 @@ int network_forward(acme_impala* l, const void* obs, const int32_t* prev_a, cons
   const int rows = B * T, H = l->H, A = l->A;
   const float* feat;
   if (p3) {
-    // Parameter planes of the torso + W_i (the only plane operands), the bf16 frames,
+    // Parameter planes of the torso + W_i (the only plane operands), the f16 frames,
     // the plane torso, then feat @ W_i[0:F] on the plane engine and the embedding tail.
     int rc;
     {
       ACME_PROF("impala_planes", st, 0.0, 10.0 * (double)l->p3_prefix);
-      rc = launch_split_planes(l->params, l->p3_prefix, l->wpl, l->flat, st);
+      rc = launch_split_planes(l->params, l->p3_prefix, l->wpl, l->flat, l->scales + kScParams,
+                               st, l->overflow);
       if (rc != ACME_OK) return rc;
     }
     {
-      ACME_PROF("impala_frames_bf16", st, 0.0, 3.0 * (double)rows * torso::kObsBytes);
-      rc = launch_frames_bf16(static_cast<const uint8_t*>(obs), static_cast<const uint8_t*>(obs),
+      ACME_PROF("impala_frames_f16", st, 0.0, 3.0 * (double)rows * torso::kObsBytes);
+      rc = launch_frames_f16(static_cast<const uint8_t*>(obs), static_cast<const uint8_t*>(obs),
                               rows, rows, torso::kObsBytes, l->frames, st);
       if (rc != ACME_OK) return rc;
     }
@@ -1037,8 +1047,9 @@ int network_forward(acme_impala* l, const void* obs, const int32_t* prev_a, cons
   return ACME_OK;
 }
 
+// apply = false: the forward, loss and backward only (the plane-scale calibration passes).
 int impala_step_impl(acme_impala* l, const acme_sequence_batch* bt, float* metrics,
-                     hipStream_t st) {
+                     hipStream_t st, bool apply = true) {
   const int B = (int)bt->batch, T = (int)bt->sequence_length, rows = B * T;
   const int H = l->H, A = l->A;
   const bool p3 = atari(l) && use_p3(l, rows);
@@ -1109,7 +1120,8 @@ int impala_step_impl(acme_impala* l, const acme_sequence_batch* bt, float* metri
     const int F = l->F, N = 4 * H;
     {
       ACME_PROF("impala_dgates_planes", st, 0.0, 10.0 * (double)rows * N);
-      rc = launch_split_planes(l->dgates, (int64_t)rows * N, l->dgp.p, l->dgp.stride, st);
+      rc = launch_split_planes(l->dgates, (int64_t)rows * N, l->dgp.p, l->dgp.stride, l->dgp.sc,
+                               st, l->overflow);
       if (rc != ACME_OK) return rc;
     }
     {
@@ -1132,8 +1144,8 @@ int impala_step_impl(acme_impala* l, const acme_sequence_batch* bt, float* metri
       p.M = rows; p.N = F; p.K = N; p.k_chunk = N;
       p.a_src = SRC(l->dgp, (int64_t)rows * N);
       p.b_src = SRC(WP(l, l->t_wi), (int64_t)F * N);
-      p.xprev = CPlanes{l->x3p.p, l->x3p.stride}; p.ldx = F;
-      p.dx = Planes{l->dz3p.p, l->dz3p.stride};
+      p.xprev = CPlanes{l->x3p.p, l->x3p.stride, l->x3p.sc}; p.ldx = F;
+      p.dx = Planes{l->dz3p.p, l->dz3p.stride, l->dz3p.sc};
       IM_P3WS_GEMM("impala_feat_dgrad", 128, 128, 2, 2, 32, p, 1);
     }
     torso::Grads g{Pm(l, gr, l->t_c[0]), Pm(l, gr, l->t_c[1]), Pm(l, gr, l->t_c[2]),
@@ -1141,6 +1153,9 @@ int impala_step_impl(acme_impala* l, const acme_sequence_batch* bt, float* metri
     rc = torso::backward_p3(torso_pw(l), g, torso::Frames{l->frames}, rows,
                             torso::PActs{l->x1p, l->x2p, l->x3p}, l->dz3p, l->dz2p, l->dz1p,
                             l->pslab, st);
+    if (rc != ACME_OK) return rc;
+    // The next plane step's activation / gradient scales from this step's maxima.
+    rc = launch_plane_rescale(l->scales, kScTransient, kScTransient, -1, -1, l->overflow, st);
     if (rc != ACME_OK) return rc;
   } else {
     const float* feat = atari(l) ? l->x3 : static_cast<const float*>(bt->observation);
@@ -1163,6 +1178,7 @@ int impala_step_impl(acme_impala* l, const acme_sequence_batch* bt, float* metri
                          torso::Acts{l->x1, l->x2, l->x3}, l->dz3, l->dz2, l->dz1, l->slab, st);
     if (rc != ACME_OK) return rc;
   }
+  if (!apply) return ACME_OK;
   {
     ACME_PROF("impala_adam", st, 0.0, 7.0 * 4.0 * (double)l->flat);
     const int64_t n4 = l->flat / 4;
@@ -1264,24 +1280,36 @@ int acme_impala_create(const acme_impala_config* cfg, acme_impala** out) {
       (rc = dev_alloc(l, &l->xg, (int64_t)2 * B * H)) || (rc = dev_alloc(l, &l->tmo, 4)))
     return fail(rc);
   // Plane path (Atari torso): each operand plane is addressed through a 31-bit byte range,
-  // so the bf16 frames of one step bound it (R < 38,000 frames); larger unrolls stay f32.
+  // so the f16 frames of one step bound it (R < 38,000 frames); larger unrolls stay f32.
   if (cfg->torso == ACME_IMPALA_TORSO_ATARI && R * torso::kObsBytes * 2 < (int64_t)INT32_MAX &&
       R >= kP3MinRows) {
     l->p3_capable = true;
     l->p3_prefix = align64(l->tensors[l->t_wi].offset + l->tensors[l->t_wi].numel);
-    auto plane = [&](torso::Plane* x, int64_t count) {
+    if ((rc = dev_alloc(l, &l->scales, kScCount)) || (rc = dev_alloc(l, &l->overflow, 1)))
+      return fail(rc);
+    std::vector<gemm::PScale> init(kScCount);
+    std::memset(init.data(), 0, init.size() * sizeof(gemm::PScale));
+    for (auto& r : init) r.w = r.r = r.wi = r.rl = 1.f;
+    if (hipMemcpy(l->scales, init.data(), init.size() * sizeof(gemm::PScale),
+                  hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(l->overflow, 0, sizeof(int)) != hipSuccess)
+      return fail((set_error("scale record init failed"), ACME_ERR_HIP));
+    auto plane = [&](torso::Plane* x, int64_t count, int rec) {
       const int64_t stride = align64(count);
       uint16_t* q = nullptr;
-      int r = dev_alloc(l, &q, 3 * stride);
-      *x = torso::Plane{q, stride};
+      int r = dev_alloc(l, &q, gemm::kPlanes * stride);
+      *x = torso::Plane{q, stride, l->scales + rec};
       return r;
     };
-    if ((rc = dev_alloc(l, &l->wpl, 3 * l->flat)) ||
+    if ((rc = dev_alloc(l, &l->wpl, gemm::kPlanes * l->flat)) ||
         (rc = dev_alloc(l, &l->frames, R * torso::kObsBytes)) ||
-        (rc = plane(&l->x1p, R * torso::kX1)) || (rc = plane(&l->x2p, R * torso::kFlat)) ||
-        (rc = plane(&l->x3p, R * torso::kFlat)) || (rc = plane(&l->dz1p, R * torso::kX1)) ||
-        (rc = plane(&l->dz2p, R * torso::kFlat)) || (rc = plane(&l->dz3p, R * torso::kFlat)) ||
-        (rc = plane(&l->dgp, R * 4 * H)) ||
+        (rc = plane(&l->x1p, R * torso::kX1, kScX1)) ||
+        (rc = plane(&l->x2p, R * torso::kFlat, kScX2)) ||
+        (rc = plane(&l->x3p, R * torso::kFlat, kScX3)) ||
+        (rc = plane(&l->dz1p, R * torso::kX1, kScDz1)) ||
+        (rc = plane(&l->dz2p, R * torso::kFlat, kScDz2)) ||
+        (rc = plane(&l->dz3p, R * torso::kFlat, kScDz3)) ||
+        (rc = plane(&l->dgp, R * 4 * H, kScDgates)) ||
         (rc = dev_alloc(l, &l->pslab, std::max<int64_t>(torso::wgrad_slab_floats_p3(),
                                                         (int64_t)kOarSplitsP3 * R * 4 * H))))
       return fail(rc);
@@ -1317,6 +1345,7 @@ int acme_impala_bind(acme_impala* l, float* params, float* grads, float* adam_m,
   l->grads = grads;
   l->m = adam_m;
   l->v = adam_v;
+  l->scales_ok = false;
   return ACME_OK;
 }
 
@@ -1334,9 +1363,33 @@ int acme_impala_step(acme_impala* l, const acme_sequence_batch* b, float* metric
   ACME_CHECK_ARG(b->state_stride >= l->H && b->state_stride % 4 == 0 &&
                      ((uintptr_t)b->h0 & 15) == 0,
                  "core state rows must be 16-byte aligned with state_stride >= lstm_size");
-  int rc = impala_step_impl(l, b, metrics, as_stream(stream));
+  hipStream_t st = as_stream(stream);
+  int rc = ACME_OK;
+  if (atari(l) && use_p3(l, (int)(b->batch * b->sequence_length)) && !l->scales_ok) {
+    // Plane scales for newly bound parameters: two forward + backward passes without the
+    // update (the first at the current scales, whose maxima are measured before the split;
+    // each ends with the rescale), then the step.  Overflows at the initial scales are
+    // expected and cleared.
+    for (int pass = 0; pass < 2 && rc == ACME_OK; ++pass) rc = impala_step_impl(l, b, nullptr, st, false);
+    if (rc != ACME_OK) return rc;
+    ACME_HIP_TRY(hipMemsetAsync(l->overflow, 0, sizeof(int), st));
+    l->scales_ok = true;
+  }
+  rc = impala_step_impl(l, b, metrics, st);
   if (rc != ACME_OK) return rc;
   l->num_steps += 1;
+  return ACME_OK;
+}
+
+int acme_impala_plane_overflow(acme_impala* l, int32_t* overflow, int32_t reset) {
+  ACME_CHECK_ARG(l && overflow, "null argument");
+  *overflow = 0;
+  if (!l->overflow) return ACME_OK;
+  ACME_HIP_TRY(hipDeviceSynchronize());
+  int v = 0;
+  ACME_HIP_TRY(hipMemcpy(&v, l->overflow, sizeof(int), hipMemcpyDeviceToHost));
+  *overflow = v != 0;
+  if (reset) ACME_HIP_TRY(hipMemset(l->overflow, 0, sizeof(int)));
   return ACME_OK;
 }
 
@@ -1405,7 +1458,7 @@ int acme_impala_debug_buffer(const acme_impala* l, const char* name, const float
           if (strcmp(q.n, name) == 0) {
             ACME_HIP_TRY(hipDeviceSynchronize());
             int rc = launch_join_planes(q.pl.p, q.pl.stride, l->last_rows * q.per_row,
-                                        const_cast<float*>(it.p), 0);
+                                        const_cast<float*>(it.p), q.pl.sc, 0);
             if (rc != ACME_OK) return rc;
             ACME_HIP_TRY(hipDeviceSynchronize());
           }

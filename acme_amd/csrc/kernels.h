@@ -7,6 +7,9 @@
 #include <cstdint>
 
 namespace acme {
+namespace gemm {
+struct PScale;  // gemm_p3.h: the scale record of a plane tensor
+}
 
 // Finishes the duelling head GEMM (conv.h DuelHeadFwd): sums the split-K slab
 // [splits][rows][A+1], adds biases and forms q = v + (adv - mean_a(adv))
@@ -16,11 +19,12 @@ int launch_duel_head_finish(const float* slab, int splits, int rows, int A, cons
 
 // dZ of the fused hidden layer for rows b < B with dq[b] = g[b] * onehot(a[b]), masked by
 // the hidden ReLU.
-// With `planes` non-null the result is written as exact bf16 planes (gemm_p3.h Planes,
-// plane stride `pstride` elements) instead of f32 to dzh.
+// With `planes` non-null the result is written as scaled f16 planes (gemm_p3.h Planes,
+// plane stride `pstride` elements, scale record sc) instead of f32 to dzh.
 int launch_duel_head_dz(const float* h, const float* g, const int32_t* a, int B, int H, int A,
                         const float* wv, const float* wa, float* dzh, hipStream_t st,
-                        uint16_t* planes = nullptr, int64_t pstride = 0);
+                        uint16_t* planes = nullptr, int64_t pstride = 0,
+                        gemm::PScale* sc = nullptr);
 
 // Fused DQN head forward: hid = relu(sum_s slab[s] + fcb) ([rows][2H], written) and the
 // duelling q = v + adv - mean(adv) from it (replaces the slab reduction + DuelHeadFwd +
@@ -31,7 +35,7 @@ int launch_fc_head_forward(const float* slab, int splits, int rows, int H, const
 // launch_duel_head_dz writing planes, 8 units per thread.
 int launch_head_dz_planes(const float* h, const float* g, const int32_t* a, int B, int H, int A,
                           const float* wv, const float* wa, uint16_t* planes, int64_t pstride,
-                          hipStream_t st);
+                          gemm::PScale* sc, hipStream_t st);
 
 // Sums the DuelHeadWgrad slab [splits][2H+1][A+1] and scatters its block-diagonal parts
 // into the head weight / bias gradients.
@@ -69,7 +73,8 @@ int launch_dqn_loss(const LossArgs& args, hipStream_t st);
 // The loss fused with the duelling head's dZ planes (as launch_head_dz_planes, from the
 // hidden activations h [B][2H]): one launch, the same bits as the two kernels.
 int launch_dqn_loss_head_dz(const LossArgs& args, const float* h, int H, const float* wv,
-                            const float* wa, uint16_t* planes, int64_t pstride, hipStream_t st);
+                            const float* wa, uint16_t* planes, int64_t pstride, gemm::PScale* sc,
+                            hipStream_t st);
 // Blocks of launch_dqn_loss_head_dz for a batch of B rows (the loss_part entries written).
 int64_t dqn_loss_head_dz_blocks(int B, int H);
 // loss[0] = (sum of the n partials, in order) / mean_over.
@@ -118,24 +123,33 @@ struct ClipAdamArgs {
 int launch_clip_adam(const ClipAdamArgs& a, hipStream_t st);
 
 // snt.Adam over n (multiple of 4) floats at step t (acme_adam_update); with `planes`
-// non-null the updated parameters are also written as exact bf16 planes (stride pstride).
+// non-null the updated parameters are also written as f16 planes (stride pstride) at the
+// scale record psc's w, whose amax the pass raises.
 // optix != 0: optix.adam's rounding order, p + (-lr) * (m_hat / (sqrt(v_hat) + eps)).
 // dev_steps (optional): the step count lives on the device (t = *dev_steps + 1, bias
 // corrections computed by the kernel, the count incremented by a one-thread launch after
 // it), so a captured step graph replays correctly; `t` is then ignored.
 int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,
                 float b2, float eps, int64_t t, uint16_t* planes, int64_t pstride, hipStream_t st,
-                int optix = 0, int64_t* dev_steps = nullptr);
+                int optix = 0, int64_t* dev_steps = nullptr, gemm::PScale* psc = nullptr);
 
-// Exact three-plane split of n floats (n multiple of 4): planes[i * pstride + e].
+// Two-plane split of n floats (n multiple of 4): planes[i * pstride + e], at the scale of
+// max |x| (sets the record sc: w, r = wi = 1 / w; overflow |= 1 on a non-finite x).
+// keep_scale: a record whose current read scale suits max |x| keeps it (checkpoint restore).
 int launch_split_planes(const float* x, int64_t n, uint16_t* planes, int64_t pstride,
-                        hipStream_t st);
-// uint8 frames -> exact bf16 (one plane): out[f][e] = bf16(frame f byte e) for rows frames
+                        gemm::PScale* sc, hipStream_t st, int* overflow = nullptr,
+                        int keep_scale = 0);
+// End-of-step rescale of a record array (kernels.hip plane_rescale_kernel): records
+// [0, n_transient) transient, [n_transient, n) persistent; copy_to >= 0 took a plane copy of
+// copy_from's latest write.
+int launch_plane_rescale(gemm::PScale* recs, int n_transient, int n, int copy_from, int copy_to,
+                         int* overflow, hipStream_t st);
+// uint8 frames -> exact f16 (one plane): out[f][e] = f16(frame f byte e) for rows frames
 // of `frame_bytes` (multiple of 8), frames [0, split) from a and the rest from b.
-int launch_frames_bf16(const uint8_t* a, const uint8_t* b, int split, int rows, int frame_bytes,
-                       uint16_t* out, hipStream_t st);
-// Inverse (h + m + l in f32) for n elements.
+int launch_frames_f16(const uint8_t* a, const uint8_t* b, int split, int rows, int frame_bytes,
+                      uint16_t* out, hipStream_t st);
+// Inverse ((h + l) r in f32) for n elements.
 int launch_join_planes(const uint16_t* planes, int64_t pstride, int64_t n, float* x,
-                       hipStream_t st);
+                       const gemm::PScale* sc, hipStream_t st);
 
 }  // namespace acme

@@ -48,9 +48,9 @@ __global__ void duel_head_dz_kernel(const float* __restrict__ h, const float* __
                                     const int32_t* __restrict__ a, int B, int H, int A,
                                     const float* __restrict__ wv, const float* __restrict__ wa,
                                     float* __restrict__ dzh, uint16_t* __restrict__ planes,
-                                    int64_t pstride) {
+                                    int64_t pstride, gemm::PScale* sc) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (int64_t)B * 2 * H) return;
+  if (i >= (int64_t)B * 2 * H) return;  // (the plane path uses head_dz_planes_kernel)
   const int b = (int)(i / (2 * H));
   const int k = (int)(i - (int64_t)b * 2 * H);
   const float gb = g[b];
@@ -67,7 +67,7 @@ __global__ void duel_head_dz_kernel(const float* __restrict__ h, const float* __
     d = s;
   }
   const float z = h[i] > 0.f ? d : 0.f;
-  if (planes) gemm::Planes{planes, pstride}.put(i, z);
+  if (planes) gemm::Planes{planes, pstride, sc}.put(i, z);
   else dzh[i] = z;
 }
 
@@ -231,18 +231,23 @@ __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restric
 
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 
-// Planes of 4 consecutive floats (element 4i .. 4i+3), 8-byte stores per plane.
-__device__ __forceinline__ void store_planes4(uint16_t* planes, int64_t pstride, int64_t i,
-                                              const f32x4 x) {
-  uint16_t h[4], m[4], l[4];
+// Planes of 4 consecutive floats (element 4i .. 4i+3) scaled by w, 8-byte stores per
+// plane; returns max |x|.
+__device__ __forceinline__ float store_planes4(uint16_t* planes, int64_t pstride, int64_t i,
+                                               const f32x4 x, float w) {
+  uint16_t h[4], l[4];
+  float mx = 0.f;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) gemm::split3_bits(x[j], h[j], m[j], l[j]);
+  for (int j = 0; j < 4; ++j) {
+    gemm::split2_bits(x[j] * w, h[j], l[j]);
+    mx = fmaxf(mx, fabsf(x[j]));
+  }
   auto pack = [](const uint16_t* q) {
     return uint2{(uint32_t)q[0] | ((uint32_t)q[1] << 16), (uint32_t)q[2] | ((uint32_t)q[3] << 16)};
   };
   reinterpret_cast<uint2*>(planes)[i] = pack(h);
-  reinterpret_cast<uint2*>(planes + pstride)[i] = pack(m);
-  reinterpret_cast<uint2*>(planes + 2 * pstride)[i] = pack(l);
+  reinterpret_cast<uint2*>(planes + pstride)[i] = pack(l);
+  return mx;
 }
 
 // snt.optimizers.Adam (Kingma & Ba Algorithm 1 form):
@@ -538,6 +543,25 @@ __device__ __forceinline__ void head_dz8(int k0, int H, int A, float gb, int ab,
   for (int j = 0; j < 8; ++j) d[j] = hv[j] > 0.f ? v[j] : 0.f;
 }
 
+// Planes of 8 consecutive values at element e scaled by w (16-B stores); returns max |d|.
+__device__ __forceinline__ float store_planes8(uint16_t* planes, int64_t pstride, int64_t e,
+                                              const float (&d)[8], float w) {
+  uint32_t ph[4], pl[4];
+  float mx = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    uint16_t x0, y0, x1, y1;
+    gemm::split2_bits(d[2 * j] * w, x0, y0);
+    gemm::split2_bits(d[2 * j + 1] * w, x1, y1);
+    ph[j] = x0 | ((uint32_t)x1 << 16);
+    pl[j] = y0 | ((uint32_t)y1 << 16);
+    mx = fmaxf(mx, fmaxf(fabsf(d[2 * j]), fabsf(d[2 * j + 1])));
+  }
+  *reinterpret_cast<uint4*>(planes + e) = uint4{ph[0], ph[1], ph[2], ph[3]};
+  *reinterpret_cast<uint4*>(planes + pstride + e) = uint4{pl[0], pl[1], pl[2], pl[3]};
+  return mx;
+}
+
 // Loss + head dZ in one launch (plane path).  Blocks [0, nb) each write the dZ planes of
 // 256 / (2H / 8) rows (8 units per thread, as head_dz_planes_kernel), recomputing g_b of
 // their rows with loss_row (the loss kernel's bits); the last block is the loss kernel
@@ -545,7 +569,8 @@ __device__ __forceinline__ void head_dz8(int k0, int H, int A, float gb, int ab,
 // launch and its dependency on the critical path.
 __global__ void __launch_bounds__(256) dqn_loss_head_dz_kernel(
     LossArgs p, const float* __restrict__ h, int H, const float* __restrict__ wv,
-    const float* __restrict__ wa, uint16_t* __restrict__ planes, int64_t pstride) {
+    const float* __restrict__ wa, uint16_t* __restrict__ planes, int64_t pstride,
+    gemm::PScale* __restrict__ sc) {
   __shared__ double red[4];
   __shared__ float gs[8];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -618,26 +643,15 @@ __global__ void __launch_bounds__(256) dqn_loss_head_dz_kernel(
     gs[tid] = loss_row(p, b0 + tid, wmax).g;
   }
   __syncthreads();
-  if (t >= (int64_t)B * per) return;
-  const float gb = gs[b - b0];
+  const bool live = t < (int64_t)B * per;
+  const float gb = gs[live ? b - b0 : 0];
   const float inv_a = 1.f / (float)A;
   const float hv[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
   float d[8];
   head_dz8(k0, H, A, gb, ab, inv_a, wv, wa, hv, d);
-  uint32_t ph[4], pm[4], pl[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    uint16_t x0, y0, z0, x1, y1, z1;
-    gemm::split3_bits(d[2 * j], x0, y0, z0);
-    gemm::split3_bits(d[2 * j + 1], x1, y1, z1);
-    ph[j] = x0 | ((uint32_t)x1 << 16);
-    pm[j] = y0 | ((uint32_t)y1 << 16);
-    pl[j] = z0 | ((uint32_t)z1 << 16);
-  }
-  const int64_t e = (int64_t)b * 2 * H + k0;
-  *reinterpret_cast<uint4*>(planes + e) = uint4{ph[0], ph[1], ph[2], ph[3]};
-  *reinterpret_cast<uint4*>(planes + pstride + e) = uint4{pm[0], pm[1], pm[2], pm[3]};
-  *reinterpret_cast<uint4*>(planes + 2 * pstride + e) = uint4{pl[0], pl[1], pl[2], pl[3]};
+  float mx = 0.f;
+  if (live) mx = store_planes8(planes, pstride, (int64_t)b * 2 * H + k0, d, sc->w);
+  gemm::amax_commit(sc, mx);
 }
 
 // dZ of the fused hidden layer as planes, 8 consecutive units per thread:
@@ -645,10 +659,11 @@ __global__ void __launch_bounds__(256) dqn_loss_head_dz_kernel(
 __global__ void __launch_bounds__(256) head_dz_planes_kernel(
     const float* __restrict__ h, const float* __restrict__ g, const int32_t* __restrict__ a,
     int B, int H, int A, const float* __restrict__ wv, const float* __restrict__ wa,
-    uint16_t* __restrict__ planes, int64_t pstride) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    uint16_t* __restrict__ planes, int64_t pstride, gemm::PScale* __restrict__ sc) {
   const int per = 2 * H / 8;
-  if (t >= (int64_t)B * per) return;
+  const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool live = t0 < (int64_t)B * per;
+  const int64_t t = live ? t0 : (int64_t)B * per - 1;  // clamped: every lane reaches the amax
   const int b = (int)(t / per), k0 = 8 * (int)(t - (int64_t)b * per);
   const float gb = g[b];
   const int ab = a[b];
@@ -658,20 +673,9 @@ __global__ void __launch_bounds__(256) head_dz_planes_kernel(
   const float hv[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
   float d[8];
   head_dz8(k0, H, A, gb, ab, inv_a, wv, wa, hv, d);
-  uint32_t ph[4], pm[4], pl[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    uint16_t x0, y0, z0, x1, y1, z1;
-    gemm::split3_bits(d[2 * j], x0, y0, z0);
-    gemm::split3_bits(d[2 * j + 1], x1, y1, z1);
-    ph[j] = x0 | ((uint32_t)x1 << 16);
-    pm[j] = y0 | ((uint32_t)y1 << 16);
-    pl[j] = z0 | ((uint32_t)z1 << 16);
-  }
-  const int64_t e = (int64_t)b * 2 * H + k0;
-  *reinterpret_cast<uint4*>(planes + e) = uint4{ph[0], ph[1], ph[2], ph[3]};
-  *reinterpret_cast<uint4*>(planes + pstride + e) = uint4{pm[0], pm[1], pm[2], pm[3]};
-  *reinterpret_cast<uint4*>(planes + 2 * pstride + e) = uint4{pl[0], pl[1], pl[2], pl[3]};
+  float mx = 0.f;
+  if (live) mx = store_planes8(planes, pstride, (int64_t)b * 2 * H + k0, d, sc->w);
+  gemm::amax_commit(sc, mx);
 }
 
 __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p,
@@ -680,13 +684,16 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p,
                                                    int64_t n4, float lr, float b1, float omb1,
                                                    float b2, float omb2, float bc1, float bc2,
                                                    float eps, uint16_t* __restrict__ planes,
-                                                   int64_t pstride, int optix,
+                                                   int64_t pstride, gemm::PScale* __restrict__ psc,
+                                                   int optix,
                                                    const int64_t* __restrict__ dev_steps) {
   if (dev_steps) {  // device-side step count (graph replay): same expressions as the host's
     const float tf = (float)(*dev_steps + 1);
     bc1 = 1.f - powf(b1, tf);
     bc2 = 1.f - powf(b2, tf);
   }
+  const float pw = planes ? psc->w : 0.f;
+  float amx = 0.f;
 #pragma unroll 2
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -712,42 +719,131 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p,
     __builtin_nontemporal_store(mm, reinterpret_cast<f32x4*>(m) + i);
     __builtin_nontemporal_store(vv, reinterpret_cast<f32x4*>(v) + i);
     reinterpret_cast<f32x4*>(p)[i] = pp;
-    if (planes) store_planes4(planes, pstride, i, pp);
+    if (planes) amx = fmaxf(amx, store_planes4(planes, pstride, i, pp, pw));
+  }
+  if (planes) {  // one amax atomic per block
+    __shared__ float bm[4];
+    amx = gemm::wave_max(amx);
+    if ((threadIdx.x & 63) == 0) bm[threadIdx.x >> 6] = amx;
+    __syncthreads();
+    if (threadIdx.x < 64)
+      gemm::amax_commit(psc, threadIdx.x < 4 ? bm[threadIdx.x] : 0.f);
   }
 }
 
 __global__ void count_step_kernel(int64_t* c) { *c += 1; }
 
+// Planes of x at the scale record's read scale (1 / r, set or kept by
+// plane_scale_set_kernel; exact for a power of two); no amax.
 __global__ void __launch_bounds__(256) split_planes_kernel(const float* __restrict__ x, int64_t n4,
                                                            uint16_t* __restrict__ planes,
-                                                           int64_t pstride) {
+                                                           int64_t pstride,
+                                                           const gemm::PScale* __restrict__ sc) {
+  const float w = 1.f / sc->r;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (int64_t)gridDim.x * blockDim.x)
-    store_planes4(planes, pstride, i, reinterpret_cast<const f32x4*>(x)[i]);
+    store_planes4(planes, pstride, i, reinterpret_cast<const f32x4*>(x)[i], w);
 }
 
-__global__ void __launch_bounds__(256) frames_bf16_kernel(const uint8_t* __restrict__ a,
-                                                          const uint8_t* __restrict__ b,
-                                                          int64_t split8, int64_t n8,
-                                                          uint16_t* __restrict__ out) {
+// max |x| into sc->amax (which is 0 between rescales).
+__global__ void __launch_bounds__(256) amax_kernel(const float* __restrict__ x, int64_t n4,
+                                                   gemm::PScale* __restrict__ sc) {
+  float mx = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const f32x4 v = reinterpret_cast<const f32x4*>(x)[i];
+    mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+  }
+  gemm::amax_commit(sc, mx);
+}
+
+// The power of two w that puts a (> 0, finite) at 2^7 <= a w < 2^8 (gemm_p3.h); exponent
+// clamped so w and 1 / w stay normal f32.
+__device__ __forceinline__ int scale_exp(float a) {
+  int k;
+  (void)frexpf(a, &k);  // a = m 2^k, m in [0.5, 1)
+  const int e = 8 - k;
+  return e < -100 ? -100 : (e > 100 ? 100 : e);
+}
+
+// The record's amax (max over its slots, read by every lane of one wave) and its slots
+// cleared.  Non-negative floats order as their bits; NaN above infinity.
+__device__ __forceinline__ float take_amax(gemm::PScale* sc, int lane) {
+  uint32_t a = sc->slot[lane].v;
+  sc->slot[lane].v = 0u;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) a = max(a, (uint32_t)__shfl_xor((int)a, o, 64));
+  return __builtin_bit_cast(float, a);
+}
+
+// Sets a record for planes about to be written at 1 / r from the amax just collected (one
+// wave), slots cleared.  keep != 0: a record whose read scale r already suits the data
+// (2^4 <= amax / r < 2^12, e.g. restored from a checkpoint together with the parameters it
+// was written for) is left as it is, so the rewritten planes are the bits its writer
+// produced and the next write uses the restored w; otherwise w from the amax (1 if it is
+// 0) and r = wi = 1 / w.
+__global__ void __launch_bounds__(64) plane_scale_set_kernel(gemm::PScale* __restrict__ sc,
+                                                             int* __restrict__ overflow,
+                                                             int keep) {
+  const float a = take_amax(sc, threadIdx.x);
+  if (threadIdx.x != 0) return;
+  if (!(a <= 3.0e38f) && overflow) atomicOr(overflow, 1);  // NaN / infinite input
+  const float y = a / sc->r;
+  if (keep && a > 0.f && y >= 16.f && y < 4096.f) return;
+  const int e = a > 0.f && a <= 3.0e38f ? scale_exp(a) : 0;
+  sc->w = ldexpf(1.f, e);
+  sc->r = sc->wi = sc->rl = ldexpf(1.f, -e);
+}
+
+// End-of-step rescale of n records (one wave each; blockDim.x = 64 n).  Records [0, nt)
+// are transient (written and read within a step: the next step writes and reads at the new
+// scale), [nt, n) persistent (parameter planes, read in the step after the one that wrote
+// them: their r becomes the wi their writer used, then w moves).  copy_to >= 0: record
+// copy_to received a plane copy of record copy_from's latest write (r = its wi).  A record
+// whose amax is 0 keeps its scale.  overflow |= 1 when a write exceeded f16's range
+// (amax w >= 65520) or was not finite.
+__global__ void __launch_bounds__(1024) plane_rescale_kernel(gemm::PScale* __restrict__ s, int nt,
+                                                             int n, int copy_from, int copy_to,
+                                                             int* __restrict__ overflow) {
+  const int i = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (threadIdx.x == 0 && copy_to >= 0) s[copy_to].r = s[copy_to].rl = s[copy_from].wi;
+  __syncthreads();
+  if (i >= n) return;
+  gemm::PScale* rec = s + i;
+  const float a = take_amax(rec, lane);
+  if (lane != 0 || a == 0.f) return;
+  if (!(a * rec->w < 65520.f)) atomicOr(overflow, 1);
+  const bool finite = a <= 3.0e38f;
+  if (i >= nt) rec->r = rec->wi;
+  rec->rl = rec->r;  // the planes stored now
+  const int e = finite ? scale_exp(a) : 0;
+  const float w = finite ? ldexpf(1.f, e) : rec->w * 0x1p-16f;
+  const float wi = finite ? ldexpf(1.f, -e) : rec->wi * 0x1p16f;
+  rec->w = w;
+  rec->wi = wi;
+  if (i < nt) rec->r = wi;
+}
+
+__global__ void __launch_bounds__(256) frames_f16_kernel(const uint8_t* __restrict__ a,
+                                                         const uint8_t* __restrict__ b,
+                                                         int64_t split8, int64_t n8,
+                                                         uint16_t* __restrict__ out) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8;
        i += (int64_t)gridDim.x * blockDim.x) {
     const uint2 w = i < split8 ? reinterpret_cast<const uint2*>(a)[i]
                                : reinterpret_cast<const uint2*>(b)[i - split8];
-    // bf16(byte) is the upper half of float(byte) (exact: 8 significant bits).
-    auto cvt = [](uint32_t x, int s) { return __builtin_bit_cast(uint32_t, (float)((x >> s) & 0xff)); };
-    const uint32_t o0 = (cvt(w.x, 0) >> 16) | (cvt(w.x, 8) & 0xffff0000u);
-    const uint32_t o1 = (cvt(w.x, 16) >> 16) | (cvt(w.x, 24) & 0xffff0000u);
-    const uint32_t o2 = (cvt(w.y, 0) >> 16) | (cvt(w.y, 8) & 0xffff0000u);
-    const uint32_t o3 = (cvt(w.y, 16) >> 16) | (cvt(w.y, 24) & 0xffff0000u);
-    reinterpret_cast<uint4*>(out)[i] = uint4{o0, o1, o2, o3};
+    // f16(byte) is exact (8 significant bits).
+    reinterpret_cast<uint4*>(out)[i] =
+        uint4{gemm::f16x2_of_bytes(w.x, 0), gemm::f16x2_of_bytes(w.x, 16),
+              gemm::f16x2_of_bytes(w.y, 0), gemm::f16x2_of_bytes(w.y, 16)};
   }
 }
 
 __global__ void __launch_bounds__(256) join_planes_kernel(const uint16_t* __restrict__ planes,
                                                           int64_t pstride, int64_t n,
-                                                          float* __restrict__ x) {
-  const gemm::CPlanes c{planes, pstride};
+                                                          float* __restrict__ x,
+                                                          const gemm::PScale* __restrict__ sc) {
+  const gemm::CPlanes c{planes, pstride, sc};
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
     x[i] = c.value(i);
@@ -886,10 +982,11 @@ int launch_duel_head_finish(const float* slab, int splits, int rows, int A, cons
 
 int launch_duel_head_dz(const float* h, const float* g, const int32_t* a, int B, int H, int A,
                         const float* wv, const float* wa, float* dzh, hipStream_t st,
-                        uint16_t* planes, int64_t pstride) {
+                        uint16_t* planes, int64_t pstride, gemm::PScale* sc) {
+  ACME_CHECK_ARG(!planes || sc, "planes need a scale record");
   const int64_t n = (int64_t)B * 2 * H;
   duel_head_dz_kernel<<<(unsigned)ceil_div(n, 256), 256, 0, st>>>(h, g, a, B, H, A, wv, wa, dzh,
-                                                                   planes, pstride);
+                                                                   planes, pstride, sc);
   ACME_LAUNCH_CHECK();
   return ACME_OK;
 }
@@ -973,26 +1070,28 @@ int launch_dqn_loss_sum(const double* part, int64_t n, int mean_over, float* los
 }
 
 int launch_dqn_loss_head_dz(const LossArgs& args, const float* h, int H, const float* wv,
-                            const float* wa, uint16_t* planes, int64_t pstride, hipStream_t st) {
-  ACME_CHECK_ARG(args.B >= 1 && args.A >= 1 && h && wv && wa && planes, "bad loss / head dZ args");
+                            const float* wa, uint16_t* planes, int64_t pstride, gemm::PScale* sc,
+                            hipStream_t st) {
+  ACME_CHECK_ARG(args.B >= 1 && args.A >= 1 && h && wv && wa && planes && sc,
+                 "bad loss / head dZ args");
   const int per = 2 * H / 8;
   ACME_CHECK_ARG(H % 8 == 0 && per >= 32 && 256 % per == 0, "hidden size %d: 2H/8 must divide 256", H);
   ACME_CHECK_ARG(reinterpret_cast<uintptr_t>(wv) % 16 == 0, "wv must be 16-byte aligned");
   const int64_t nb = ceil_div((int64_t)args.B * per, 256);
   dqn_loss_head_dz_kernel<<<(unsigned)(args.loss_part ? nb : nb + 1), 256, 0, st>>>(
-      args, h, H, wv, wa, planes, pstride);
+      args, h, H, wv, wa, planes, pstride, sc);
   ACME_LAUNCH_CHECK();
   return ACME_OK;
 }
 
 int launch_head_dz_planes(const float* h, const float* g, const int32_t* a, int B, int H, int A,
                           const float* wv, const float* wa, uint16_t* planes, int64_t pstride,
-                          hipStream_t st) {
-  ACME_CHECK_ARG(H % 8 == 0 && pstride % 8 == 0 && reinterpret_cast<uintptr_t>(wv) % 16 == 0,
+                          gemm::PScale* sc, hipStream_t st) {
+  ACME_CHECK_ARG(H % 8 == 0 && pstride % 8 == 0 && reinterpret_cast<uintptr_t>(wv) % 16 == 0 && sc,
                  "bad head_dz shape");
   const int64_t n = (int64_t)B * (2 * H / 8);
   head_dz_planes_kernel<<<(unsigned)ceil_div(n, 256), 256, 0, st>>>(h, g, a, B, H, A, wv, wa,
-                                                                    planes, pstride);
+                                                                    planes, pstride, sc);
   ACME_LAUNCH_CHECK();
   return ACME_OK;
 }
@@ -1029,8 +1128,9 @@ int launch_grad_sumsq(const float* g, int64_t n4, int64_t group0_4, double* part
 
 int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,
                 float b2, float eps, int64_t t, uint16_t* planes, int64_t pstride, hipStream_t st,
-                int optix, int64_t* dev_steps) {
+                int optix, int64_t* dev_steps, gemm::PScale* psc) {
   ACME_CHECK_ARG(p && g && m && v, "null buffer");
+  ACME_CHECK_ARG(!planes || psc, "parameter planes need a scale record");
   ACME_CHECK_ARG(n % 4 == 0, "adam buffer length must be a multiple of 4");
   ACME_CHECK_ARG(pstride % 4 == 0, "plane stride must be a multiple of 4");
   ACME_CHECK_ARG(t >= 1 || dev_steps, "adam step must be >= 1");
@@ -1044,7 +1144,7 @@ int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float l
   // one-row head blocks (three alternating pairs on one box).
   adam_kernel<<<std::max(grid, 1u), 256, 0, st>>>(p, g, m, v, n4, lr, b1, 1.f - b1, b2,
                                                   1.f - b2, bc1, bc2, eps, planes, pstride,
-                                                  optix, dev_steps);
+                                                  psc, optix, dev_steps);
   ACME_LAUNCH_CHECK();
   if (dev_steps) {
     count_step_kernel<<<1, 1, 0, st>>>(dev_steps);
@@ -1054,32 +1154,47 @@ int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float l
 }
 
 int launch_split_planes(const float* x, int64_t n, uint16_t* planes, int64_t pstride,
-                        hipStream_t st) {
-  ACME_CHECK_ARG(n % 4 == 0 && pstride % 4 == 0, "plane split needs multiples of 4");
+                        gemm::PScale* sc, hipStream_t st, int* overflow, int keep_scale) {
+  ACME_CHECK_ARG(n % 4 == 0 && pstride % 4 == 0 && sc, "plane split needs multiples of 4");
   const int64_t n4 = n / 4;
   const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n4, 256), 2048);
-  split_planes_kernel<<<std::max(grid, 1u), 256, 0, st>>>(x, n4, planes, pstride);
+  amax_kernel<<<std::max(grid, 1u), 256, 0, st>>>(x, n4, sc);
+  ACME_LAUNCH_CHECK();
+  plane_scale_set_kernel<<<1, 64, 0, st>>>(sc, overflow, keep_scale);
+  ACME_LAUNCH_CHECK();
+  split_planes_kernel<<<std::max(grid, 1u), 256, 0, st>>>(x, n4, planes, pstride, sc);
   ACME_LAUNCH_CHECK();
   return ACME_OK;
 }
 
-int launch_frames_bf16(const uint8_t* a, const uint8_t* b, int split, int rows, int frame_bytes,
-                       uint16_t* out, hipStream_t st) {
+int launch_plane_rescale(gemm::PScale* recs, int n_transient, int n, int copy_from, int copy_to,
+                         int* overflow, hipStream_t st) {
+  ACME_CHECK_ARG(recs && overflow && n >= 1 && n <= 16 && n_transient >= 0 && n_transient <= n,
+                 "bad rescale arguments");
+  ACME_CHECK_ARG(copy_to < 16 && copy_from < 16, "bad rescale copy");
+  plane_rescale_kernel<<<1, (unsigned)(64 * n), 0, st>>>(recs, n_transient, n, copy_from, copy_to,
+                                                         overflow);
+  ACME_LAUNCH_CHECK();
+  return ACME_OK;
+}
+
+int launch_frames_f16(const uint8_t* a, const uint8_t* b, int split, int rows, int frame_bytes,
+                      uint16_t* out, hipStream_t st) {
   ACME_CHECK_ARG(frame_bytes % 8 == 0, "frame bytes must be a multiple of 8");
   ACME_CHECK_ARG(reinterpret_cast<uintptr_t>(a) % 8 == 0 && reinterpret_cast<uintptr_t>(b) % 8 == 0,
                  "uint8 frame buffers must be 8-byte aligned");
   const int64_t per = frame_bytes / 8;
   const int64_t n8 = per * rows;
   const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n8, 256), 8192);
-  frames_bf16_kernel<<<std::max(grid, 1u), 256, 0, st>>>(a, b, per * split, n8, out);
+  frames_f16_kernel<<<std::max(grid, 1u), 256, 0, st>>>(a, b, per * split, n8, out);
   ACME_LAUNCH_CHECK();
   return ACME_OK;
 }
 
 int launch_join_planes(const uint16_t* planes, int64_t pstride, int64_t n, float* x,
-                       hipStream_t st) {
+                       const gemm::PScale* sc, hipStream_t st) {
   const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n, 256), 4096);
-  join_planes_kernel<<<std::max(grid, 1u), 256, 0, st>>>(planes, pstride, n, x);
+  join_planes_kernel<<<std::max(grid, 1u), 256, 0, st>>>(planes, pstride, n, x, sc);
   ACME_LAUNCH_CHECK();
   return ACME_OK;
 }

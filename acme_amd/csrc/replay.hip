@@ -431,7 +431,7 @@ __global__ void __launch_bounds__(T) sample_gather_pair_kernel(
     vu4* p = c < nvec ? b0 + c : b1 + (c - nvec);
     if (c < 2 * nvec) *p = v[k];
   }
-  if (fb) {  // the learner's exact bf16 copy of both frames: rows [0, B) o_tm1, [B, 2B) o_t
+  if (fb) {  // the learner's exact f16 copy of both frames: rows [0, B) o_tm1, [B, 2B) o_t
     const int64_t B = gridDim.x;
 #pragma unroll
     for (int k = 0; k < MAXC; ++k) {
@@ -440,17 +440,17 @@ __global__ void __launch_bounds__(T) sample_gather_pair_kernel(
       const int64_t row = c < nvec ? r : B + r;
       const int32_t cc = c < nvec ? c : c - nvec;
       vu4* q = reinterpret_cast<vu4*>(fb + (row * nvec + cc) * 16);
-      // bf16(byte) is the upper half of float(byte) (exact: 8 significant bits).
+      // f16(byte) is exact (8 significant bits).
       auto cvt = [](uint32_t x, int sh) {
-        return __builtin_bit_cast(uint32_t, (float)((x >> sh) & 0xffu));
+        return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)(uint16_t)((x >> sh) & 0xffu));
       };
       vu4 lo, hi;
 #pragma unroll
       for (int w = 0; w < 2; ++w) {
-        lo[2 * w] = (cvt(v[k][w], 0) >> 16) | (cvt(v[k][w], 8) & 0xffff0000u);
-        lo[2 * w + 1] = (cvt(v[k][w], 16) >> 16) | (cvt(v[k][w], 24) & 0xffff0000u);
-        hi[2 * w] = (cvt(v[k][w + 2], 0) >> 16) | (cvt(v[k][w + 2], 8) & 0xffff0000u);
-        hi[2 * w + 1] = (cvt(v[k][w + 2], 16) >> 16) | (cvt(v[k][w + 2], 24) & 0xffff0000u);
+        lo[2 * w] = cvt(v[k][w], 0) | (cvt(v[k][w], 8) << 16);
+        lo[2 * w + 1] = cvt(v[k][w], 16) | (cvt(v[k][w], 24) << 16);
+        hi[2 * w] = cvt(v[k][w + 2], 0) | (cvt(v[k][w + 2], 8) << 16);
+        hi[2 * w + 1] = cvt(v[k][w + 2], 16) | (cvt(v[k][w + 2], 24) << 16);
       }
       q[0] = lo;
       q[1] = hi;
@@ -1175,7 +1175,7 @@ static int sample_gather_impl(acme_replay* r, int64_t batch, uint64_t step_count
                               double prob_scale, int64_t* slots, uint64_t* keys,
                               double* probabilities, int64_t* table_size, double* priorities,
                               void* const* out_fields, void* stream,
-                              uint16_t* frames_bf16 = nullptr);
+                              uint16_t* frames_f16 = nullptr);
 
 int acme_replay_sample(acme_replay* r, int64_t batch, uint64_t step_counter, int64_t* slots,
                        uint64_t* keys, double* probabilities, int64_t* table_size,
@@ -1214,12 +1214,12 @@ int acme_replay_sample_share_frames(acme_replay* r, int64_t batch, uint64_t step
                                     double prob_scale, int64_t* slots, uint64_t* keys,
                                     double* probabilities, int64_t* table_size,
                                     double* priorities, void* const* out_fields,
-                                    uint16_t* frames_bf16, void* stream) {
-  ACME_CHECK_ARG(r && out_fields && frames_bf16, "null argument");
+                                    uint16_t* frames_f16, void* stream) {
+  ACME_CHECK_ARG(r && out_fields && frames_f16, "null argument");
   ACME_CHECK_ARG(prob_scale > 0.0 && prob_scale <= 1.0, "prob_scale must be in (0, 1]");
   std::lock_guard<std::mutex> lock(r->mu);
   return sample_gather_impl(r, batch, step_counter, prob_scale, slots, keys, probabilities,
-                            table_size, priorities, out_fields, stream, frames_bf16);
+                            table_size, priorities, out_fields, stream, frames_f16);
 }
 
 static int sample_impl(acme_replay* r, int64_t batch, uint64_t step_counter, double prob_scale,
@@ -1283,16 +1283,16 @@ static int sample_gather_impl(acme_replay* r, int64_t batch, uint64_t step_count
                               double prob_scale, int64_t* slots, uint64_t* keys,
                               double* probabilities, int64_t* table_size, double* priorities,
                               void* const* out_fields, void* stream,
-                              uint16_t* frames_bf16) {
+                              uint16_t* frames_f16) {
   ACME_CHECK_ARG(slots && out_fields, "null argument");
   ACME_CHECK_ARG(batch > 0 && batch < (int64_t(1) << 31), "bad batch");
   int f0, f1;
   SmallFields sm;
   const bool pair = pair_layout(r, out_fields, &f0, &f1, &sm);
-  ACME_CHECK_ARG(!frames_bf16 || (pair && reinterpret_cast<uintptr_t>(frames_bf16) % 16 == 0),
+  ACME_CHECK_ARG(!frames_f16 || (pair && reinterpret_cast<uintptr_t>(frames_f16) % 16 == 0),
                  "a bf16 frame copy needs the transition layout (two equal big fields) and a "
                  "16-byte aligned buffer");
-  if (frames_bf16 || (tune_variant("SGF") != 1 && tune_variant("GATH") == 0 && pair)) {
+  if (frames_f16 || (tune_variant("SGF") != 1 && tune_variant("GATH") == 0 && pair)) {
     hipStream_t st = as_stream(stream);
     int64_t size = 0;
     int rc = order_after_inserts(r, st, &size);
@@ -1306,7 +1306,7 @@ static int sample_gather_impl(acme_replay* r, int64_t batch, uint64_t step_count
     const bool prio = r->cfg.sampler == ACME_SAMPLER_PRIORITIZED;
     ACME_PROF("replay_sample_gather", st, 0.0,
               (double)batch * (2.0 * row_bytes + 40.0 + (prio ? 512.0 * r->nlevels : 0.0) +
-                               (frames_bf16 ? 4.0 * (double)r->cfg.field_bytes[f0] : 0.0)));
+                               (frames_f16 ? 4.0 * (double)r->cfg.field_bytes[f0] : 0.0)));
     TreeView tv;
     for (int l = 0; l < 8; ++l) tv.level[l] = r->levels[l];
     tv.nlevels = r->nlevels;
@@ -1318,7 +1318,7 @@ static int sample_gather_impl(acme_replay* r, int64_t batch, uint64_t step_count
 #define ACME_SGP(PRIO, T, MAXC)                                                                 \
   sample_gather_pair_kernel<PRIO, T, MAXC><<<gb, T, 0, st>>>(                                   \
       tv, r->raw_prio, r->keys, size, r->cfg.seed, step_counter, prob_scale, slots, keys,       \
-      probabilities, table_size, priorities, s0, s1, d0, d1, nvec, sm, frames_bf16)
+      probabilities, table_size, priorities, s0, s1, d0, d1, nvec, sm, frames_f16)
     if (2 * nvec <= 256 * 14) {
       if (prio) ACME_SGP(true, 256, 14);
       else ACME_SGP(false, 256, 14);
@@ -1434,12 +1434,12 @@ int acme_replay_sample_gather(acme_replay* r, int64_t batch, uint64_t step_count
 int acme_replay_sample_gather_frames(acme_replay* r, int64_t batch, uint64_t step_counter,
                                      int64_t* slots, uint64_t* keys, double* probabilities,
                                      int64_t* table_size, double* priorities,
-                                     void* const* out_fields, uint16_t* frames_bf16,
+                                     void* const* out_fields, uint16_t* frames_f16,
                                      void* stream) {
-  ACME_CHECK_ARG(r && frames_bf16, "null argument");
+  ACME_CHECK_ARG(r && frames_f16, "null argument");
   std::lock_guard<std::mutex> lock(r->mu);
   return sample_gather_impl(r, batch, step_counter, 1.0, slots, keys, probabilities, table_size,
-                            priorities, out_fields, stream, frames_bf16);
+                            priorities, out_fields, stream, frames_f16);
 }
 
 int acme_replay_update_priorities(acme_replay* r, const uint64_t* keys, const double* prios,

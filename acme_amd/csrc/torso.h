@@ -11,6 +11,9 @@
 #include "conv.h"
 
 namespace acme {
+namespace gemm {
+struct PScale;  // gemm_p3.h
+}
 namespace torso {
 
 using G1 = conv::Geom<84, 84, 4, 21, 21, 32, 8, 8, 4, 2, 2>;
@@ -46,10 +49,12 @@ int backward(const Weights& w, const Grads& g, bool u8, const void* obs, int row
              const float* dz3, float* dz2, float* dz1, float* slab, hipStream_t st);
 
 // ---- Plane path (gemm_p3.h engine, uint8 frames): activations, gradients and weights
-// as exact three-plane bf16 tensors (Plane::p[i * stride + e] = plane i of element e).
+// as scaled two-plane f16 tensors (Plane::p[i * stride + e] = plane i of element e; sc =
+// the tensor's scale record).
 struct Plane {
   uint16_t* p;
   int64_t stride;
+  gemm::PScale* sc;
 };
 struct PWeights {
   Plane w1, w2, w3;  // views into the flat parameter planes
@@ -59,14 +64,14 @@ struct PActs {
   Plane x1, x2, x3;
 };
 int64_t wgrad_slab_floats_p3();
-// conv1's input: the bf16 copy of the uint8 frames (launch_frames_bf16), rows of 84*84*4.
+// conv1's input: the f16 copy of the uint8 frames (launch_frames_f16), rows of 84*84*4.
 struct Frames {
   const void* p;
   Frames rows_from(int r) const {
     return Frames{static_cast<const uint8_t*>(p) + (size_t)r * kObsBytes * 2};
   }
 };
-// frames: bf16 copies of the uint8 frames [rows][84*84*4] (launch_frames_bf16).
+// frames: f16 copies of the uint8 frames [rows][84*84*4] (launch_frames_f16).
 // keep_x1: frames [0, keep_x1) get their conv1 output x1 in HBM (the backward reads it);
 // -1: all.  With the fused conv1 -> conv2 kernel (gemm_p3c12.h, used when
 // keep_x1 == 0) x1 only lives in LDS.

@@ -180,11 +180,11 @@ using I3D = gemm::ImgGeom<G3, true>;
     }                                                                                         \
   } while (0)
 
-inline CPlanes cp(const Plane& x) { return CPlanes{x.p, x.stride}; }
-inline Planes pl(const Plane& x) { return Planes{x.p, x.stride}; }
+inline CPlanes cp(const Plane& x) { return CPlanes{x.p, x.stride, x.sc}; }
+inline Planes pl(const Plane& x) { return Planes{x.p, x.stride, x.sc}; }
 // Operand source over the first `elems` elements of each plane.
 inline PlaneSrc src(const Plane& x, int64_t elems) {
-  return PlaneSrc{x.p, x.stride, (int32_t)(2 * elems)};
+  return PlaneSrc{x.p, x.stride, (int32_t)(2 * elems), x.sc};
 }
 inline PlaneSrc frames_src(const Frames& f, int rows) {
   return PlaneSrc{static_cast<const uint16_t*>(f.p), 0,
@@ -219,7 +219,7 @@ int forward_p3(const PWeights& w, const Frames& frames, int rows, const PActs& a
     p1.M = rows * G1::OPIX; p1.N = G1::CO; p1.K = G1::K; p1.k_chunk = G1::K;
     p1.a_src = frames_src(frames, rows); p1.b_src = src(w.w1, G1::K * G1::CO);
     p1.bias = w.b1; p1.y = pl(a.x1);
-    P3ConvFwd<G2, 3> p2;
+    P3ConvFwd<G2, gemm::kPlanes> p2;
     p2.M = rows * G2::OPIX; p2.N = G2::CO; p2.K = G2::K; p2.k_chunk = G2::K;
     p2.a_src = src(a.x1, (int64_t)rows * kX1); p2.b_src = src(w.w2, G2::K * G2::CO);
     p2.bias = w.b2; p2.y = pl(a.x2);
@@ -237,7 +237,7 @@ int forward_p3(const PWeights& w, const Frames& frames, int rows, const PActs& a
     P3I_GEMM("conv1_fwd", I1F, 1, 32, 7, 1, 2, p, rows);
   }
   if (!fused) {
-    P3ConvFwd<G2, 3> p;
+    P3ConvFwd<G2, gemm::kPlanes> p;
     p.M = rows * G2::OPIX; p.N = G2::CO; p.K = G2::K; p.k_chunk = G2::K;
     p.a_src = src(a.x1, (int64_t)rows * kX1); p.b_src = src(w.w2, G2::K * G2::CO);
     p.bias = w.b2; p.y = pl(a.x2);
@@ -249,7 +249,7 @@ int forward_p3(const PWeights& w, const Frames& frames, int rows, const PActs& a
     else P3WS_GEMM("conv2_fwd", 128, 64, 2, 2, p, 1);
   }
   {
-    P3ConvFwd<G3, 3> p;
+    P3ConvFwd<G3, gemm::kPlanes> p;
     p.M = rows * G3::OPIX; p.N = G3::CO; p.K = G3::K; p.k_chunk = G3::K;
     p.a_src = src(a.x2, (int64_t)rows * kFlat); p.b_src = src(w.w3, G3::K * G3::CO);
     p.bias = w.b3; p.y = pl(a.x3);
@@ -275,7 +275,7 @@ int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int row
       ACME_HIP_TRY(hipEventRecord(sd.e[0], st_main));
       ACME_HIP_TRY(hipStreamWaitEvent(sd.side, sd.e[0], 0));
     }
-    P3ConvWgrad<G3, 3> p;
+    P3ConvWgrad<G3, gemm::kPlanes> p;
     p.M = G3::K; p.N = G3::CO; p.K = rows * G3::OPIX;
     const int splits = kP3Conv3WgradSplits;
     p.k_chunk = chunk_for(p.K, splits);
@@ -300,7 +300,7 @@ int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int row
     st = sd.side;
   }
   {  // conv2
-    P3ConvWgrad<G2, 3> p;
+    P3ConvWgrad<G2, gemm::kPlanes> p;
     p.M = G2::K; p.N = G2::CO; p.K = rows * G2::OPIX;
     const int splits = kP3Conv2WgradSplits;
     p.k_chunk = chunk_for(p.K, splits);

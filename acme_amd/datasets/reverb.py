@@ -105,11 +105,11 @@ class _TableIterator:
         self._rows = 2 * batch if shard is not None else batch
         self._snaps = {}
         self._share = {}
-        # The exact bf16 copy of [o_tm1; o_t] written by the fused sample + gather (uint8
-        # transition tables): per buffer slot, or None; `last_frames_bf16` is the copy of
+        # The exact f16 copy of [o_tm1; o_t] written by the fused sample + gather (uint8
+        # transition tables): per buffer slot, or None; `last_frames_f16` is the copy of
         # the batch handed out last (the DQN learner then skips its own conversion).
         self._fb = []
-        self.last_frames_bf16 = None
+        self.last_frames_f16 = None
         if shard is not None and isinstance(table, replay.FrameTable):
             raise ValueError("global sampling over FrameTable shards is not supported")
 
@@ -161,11 +161,11 @@ class _TableIterator:
             # slots have no other reference): keep them alive with the slot set.
             self._slots.append((raw, ptrs, sample, info, bufs))
             self._fb.append(torch.empty(2 * self._rows, fields[0].row_bytes, dtype=torch.int16,
-                                        device=dev) if self._bf16_frames() else None)
+                                        device=dev) if self._f16_frames() else None)
         self._which = 0
 
-    def _bf16_frames(self) -> bool:
-        """The fused kernel's bf16 copy applies to uint8 transition tables whose only large
+    def _f16_frames(self) -> bool:
+        """The fused kernel's f16 copy applies to uint8 transition tables whose only large
         fields are the two observations (fields 0 and 4); a shard's copy holds its share."""
         if isinstance(self._t, (replay.FrameTable, replay.QueueTable)):
             return False
@@ -275,7 +275,7 @@ class _TableIterator:
             raw, ptrs = self._slots[i][:2]
             self._which ^= 1
             n = self._draw(L, h, raw, ptrs, stream_ptr(), fb=self._fb[i])
-            self.last_frames_bf16 = self._fb[i]
+            self.last_frames_f16 = self._fb[i]
             return self._sample_view(i, n)
         # Prefetch: order the dataset stream after everything queued so far on the caller's
         # stream (inserts, earlier learner steps and their priority updates), top the queue
@@ -302,7 +302,7 @@ class _TableIterator:
         # cost (each event wait / record on a stream leaves ~7 us before the next kernel).
         if not self._ready[i].query():
             main.wait_event(self._ready[i])
-        self.last_frames_bf16 = self._fb[i]
+        self.last_frames_f16 = self._fb[i]
         return self._sample_view(i, self._share[i])
 
 
@@ -317,22 +317,27 @@ class _QueueIterator(_TableIterator):
     def __next__(self) -> replay.ReplaySample:
         from acme_amd._lib import check, lib, stream_ptr
         t = self._t
-        first = t.pop_slots(self._B, self._timeout)
         if self._slots is None:
+            t.wait_for(1, self._timeout)  # the first item fixes the layout the slots need
             self._alloc()
         i = self._which
         self._which ^= 1
         raw, ptrs, sample, info, _ = self._slots[i]
-        dev = t.native.device
-        idx = torch.arange(first, first + self._B, dtype=torch.int64, device=dev)
-        info["keys"].copy_(idx.view(torch.uint64) if idx.dtype == torch.int64 else idx)
-        info["probabilities"].fill_(1.0)
-        info["priorities"].fill_(1.0)
-        info["table_size"].fill_(t.size())
-        slots = idx % t.max_size
-        check(lib().acme_replay_gather(t.native.handle, slots.data_ptr(), self._B, ptrs,
-                                       stream_ptr()), "queue gather")
-        self._keep = slots  # the launch reads it on the stream
+
+        def read(first: int) -> None:
+            # Issued under the table lock, before pop_slots frees the slots to writers.
+            dev = t.native.device
+            idx = torch.arange(first, first + self._B, dtype=torch.int64, device=dev)
+            info["keys"].copy_(idx.view(torch.uint64))
+            info["probabilities"].fill_(1.0)
+            info["priorities"].fill_(1.0)
+            info["table_size"].fill_(t.size() - self._B)
+            slots = idx % t.max_size
+            check(lib().acme_replay_gather(t.native.handle, slots.data_ptr(), self._B, ptrs,
+                                           stream_ptr()), "queue gather")
+            self._keep = slots  # the launch reads it on the stream
+
+        t.pop_slots(self._B, self._timeout, read=read)
         return sample
 
 

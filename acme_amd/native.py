@@ -350,8 +350,32 @@ class NativeDQN:
 
     def params_changed(self) -> None:
         """Tells the learner its params / target buffers were written from outside (its
-        derived bf16 parameter planes are rebuilt before the next use)."""
+        derived f16 parameter planes are rebuilt before the next use)."""
         check(lib().acme_dqn_params_changed(self._h), "dqn params_changed")
+
+    def scale_state(self) -> np.ndarray:
+        """The plane scales (learner state for checkpoints; empty without the plane path)."""
+        n = ctypes.c_int32(0)
+        check(lib().acme_dqn_scale_state(self._h, None, 0, ctypes.byref(n)), "dqn scale_state")
+        out = np.zeros(n.value, np.float32)
+        if n.value:
+            check(lib().acme_dqn_scale_state(self._h, out.ctypes.data, n.value, ctypes.byref(n)),
+                  "dqn scale_state")
+        return out
+
+    def set_scale_state(self, state) -> None:
+        """Restores scale_state() (after params_changed): resumed steps are bit-identical."""
+        a = np.ascontiguousarray(np.asarray(state, np.float32))
+        if a.size:
+            check(lib().acme_dqn_set_scale_state(self._h, a.ctypes.data, a.size),
+                  "dqn set_scale_state")
+
+    def plane_overflow(self, reset: bool = False) -> bool:
+        """True if a plane tensor of the uint8 Nature path exceeded f16's range at its scale
+        since the last reset (synchronises the device; acme_dqn_plane_overflow)."""
+        v = ctypes.c_int32(0)
+        check(lib().acme_dqn_plane_overflow(self._h, ctypes.byref(v), int(reset)), "dqn plane_overflow")
+        return bool(v.value)
 
     def get_params(self, which: str = "params") -> Dict[str, np.ndarray]:
         flat = getattr(self, which)
@@ -374,7 +398,7 @@ class NativeDQN:
 
     # --------------------------------------------------------------- step
     def _batch(self, o_tm1, a_tm1, r_t, d_t, o_t, probabilities, global_min_probability=None,
-               mean_over=None, obs_bf16=None):
+               mean_over=None, obs_f16=None):
         B = int(a_tm1.shape[0])
         if B < 1 or B > self.max_batch:
             raise ValueError(f"batch of {B} rows: the learner takes 1..{self.max_batch}")
@@ -398,13 +422,13 @@ class NativeDQN:
         tb.batch = B
         tb.global_min_probability = ptr(global_min_probability)
         tb.mean_over = int(mean_over or 0)
-        if obs_bf16 is not None:  # [2B, obs] bf16 bits of [o_tm1; o_t] (the dataset's copy)
-            if not (isinstance(obs_bf16, torch.Tensor) and obs_bf16.is_cuda and
-                    obs_bf16.dtype in (torch.int16, torch.uint16, torch.bfloat16) and
-                    obs_bf16.is_contiguous() and obs_bf16.shape[0] >= 2 * B and
-                    obs_bf16[0].numel() == o_tm1[0].numel()):
-                raise ValueError("obs_bf16 must be a contiguous [2B, obs] 16-bit device tensor")
-            tb.obs_bf16 = ptr(obs_bf16)
+        if obs_f16 is not None:  # [2B, obs] f16 bits of [o_tm1; o_t] (the dataset's copy)
+            if not (isinstance(obs_f16, torch.Tensor) and obs_f16.is_cuda and
+                    obs_f16.dtype in (torch.int16, torch.uint16, torch.float16) and
+                    obs_f16.is_contiguous() and obs_f16.shape[0] >= 2 * B and
+                    obs_f16[0].numel() == o_tm1[0].numel()):
+                raise ValueError("obs_f16 must be a contiguous [2B, obs] 16-bit device tensor")
+            tb.obs_f16 = ptr(obs_f16)
         return tb
 
     def _outputs(self, q_tm1=None):
@@ -420,13 +444,13 @@ class NativeDQN:
                                               stream_ptr(stream)), "dqn forward_backward")
 
     def forward_backward_stage(self, stage: int, *batch, global_min_probability=None,
-                               q_tm1=None, stream=None, mean_over=None, obs_bf16=None):
+                               q_tm1=None, stream=None, mean_over=None, obs_f16=None):
         """Stage 0: forwards, loss, head/dense backward (grads[grad_split:]); stage 1: torso
         backward (grads[:grad_split]).  Stage 0 may be issued as stage 2 (forwards) then
         stage 3 (loss and dense backward; global_min_probability is read from here on).  mean_over: the batch mean's denominator (default
         the batch; a data-parallel share passes the nominal per-rank batch)."""
         tb = self._batch(*batch, global_min_probability=global_min_probability,
-                         mean_over=mean_over, obs_bf16=obs_bf16)
+                         mean_over=mean_over, obs_f16=obs_f16)
         out = self._outputs(q_tm1)
         check(lib().acme_dqn_forward_backward_stage(self._h, ctypes.byref(tb), ctypes.byref(out),
                                                     int(stage), stream_ptr(stream)),
@@ -446,8 +470,8 @@ class NativeDQN:
     def apply(self, stream=None):
         check(lib().acme_dqn_apply(self._h, stream_ptr(stream)), "dqn apply")
 
-    def step(self, *batch, q_tm1=None, stream=None, obs_bf16=None):
-        tb = self._batch(*batch, obs_bf16=obs_bf16)
+    def step(self, *batch, q_tm1=None, stream=None, obs_f16=None):
+        tb = self._batch(*batch, obs_f16=obs_f16)
         out = self._outputs(q_tm1)
         check(lib().acme_dqn_step(self._h, ctypes.byref(tb), ctypes.byref(out),
                                   stream_ptr(stream)), "dqn step")
@@ -676,6 +700,13 @@ class NativeIMPALA:
                                              ctypes.byref(n)))
         return _device_array(p.value, n.value, np.float32, self.device).cpu().numpy().view(
             np.float32).copy()
+
+    def plane_overflow(self, reset: bool = False) -> bool:
+        """As NativeDQN.plane_overflow, for the Atari torso's plane path."""
+        v = ctypes.c_int32(0)
+        check(lib().acme_impala_plane_overflow(self._h, ctypes.byref(v), int(reset)),
+              "impala plane_overflow")
+        return bool(v.value)
 
     def step(self, observation, prev_action, prev_reward, action, reward, discount,
              behaviour_logits, h0, c0, stream=None):

@@ -346,10 +346,15 @@ class QueueTable(Table):
             super().insert(item, priority)
             self._accepted += 1
 
-    def pop_slots(self, batch_size: int, timeout: Optional[float] = None) -> int:
+    def pop_slots(self, batch_size: int, timeout: Optional[float] = None,
+                  read=None) -> int:
         """Blocks until `batch_size` items are queued, flushes them to the device and
         consumes them; returns the insertion index of the first one (its ring slot is that
-        index modulo max_size, the next ones follow)."""
+        index modulo max_size, the next ones follow).  `read(first)` issues the device reads
+        of those slots: it runs under the table lock BEFORE the slots are released to
+        writers, so the native table orders any later insert into them after the reads (a
+        writer blocked on a full queue cannot overwrite a slot whose gather is not yet on a
+        stream)."""
         if batch_size > self.max_size:
             raise ValueError(f"batch {batch_size} exceeds the queue capacity {self.max_size}")
         deadline = time.time() + (self._timeout if timeout is None else timeout)
@@ -362,12 +367,25 @@ class QueueTable(Table):
                 self._cv.wait(left)
             self.flush()
             first = self._consumed
+            if read is not None:
+                read(first)
             self._consumed += batch_size
             self._cv.notify_all()
             return first
 
     def pop_batch(self, batch_size: int, timeout: float = 60.0):
         raise NotImplementedError("the device queue is read through make_reverb_dataset")
+
+    # A queue's items are consumed once and its counters live beside the ring: the plain
+    # Table export would restore a ring the counters do not describe.  The reference's
+    # IMPALA agent checkpoints the learner only (agents/tf/impala/agent.py), never its queue.
+    def save(self) -> Dict[str, Any]:
+        raise NotImplementedError(f"queue table '{self.name}' is not checkpointable "
+                                  f"(its items are consumed once; checkpoint the learner)")
+
+    def restore(self, state: Dict[str, Any]) -> None:
+        raise NotImplementedError(f"queue table '{self.name}' is not checkpointable "
+                                  f"(its items are consumed once; checkpoint the learner)")
 
     def update_priorities(self, keys, priorities) -> None:
         pass  # queue items carry no priorities (Reverb ignores updates of consumed items)

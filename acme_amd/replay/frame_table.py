@@ -185,6 +185,38 @@ def _make_frame_table(Table, _Field, _layout_from_signature):
                     self._pending_frames = []
                 super().flush()
 
+        # -- checkpointing: the base table's items (ring positions) plus the frame ring and the
+        # bookkeeping that decides when a ring position may be recycled.  The dedup window
+        # is a cache: a restored table starts it empty (a repeated frame may be stored
+        # twice; the samples are the same).
+        def save(self):
+            with self._mu:
+                state = super().save()  # flushes the pending frames too
+                state["frames"] = self._frames.cpu().numpy()
+                state["frames_stored"] = np.int64(self._g)
+                state["live_min"] = np.asarray(self._live_min, np.int64)
+                state["live_mono"] = np.asarray(self._live_mono, np.int64)
+                return state
+
+        def restore(self, state) -> None:
+            import torch
+            with self._mu:
+                if "frames" not in state:
+                    raise ValueError(f"FrameTable '{self.name}': the checkpoint holds no "
+                                     f"frame ring (saved by a plain Table?)")
+                frames = np.asarray(state["frames"], np.uint8)
+                if frames.shape != tuple(self._frames.shape):
+                    raise ValueError(f"FrameTable '{self.name}': checkpoint frame ring "
+                                     f"{frames.shape} != {tuple(self._frames.shape)}")
+                super().restore(state)
+                self._after_readers()
+                self._frames.copy_(torch.as_tensor(frames).to(self._frames.device))
+                self._g = int(state["frames_stored"])
+                self._live_min = collections.deque(int(x) for x in state["live_min"])
+                self._live_mono = collections.deque(int(x) for x in state["live_mono"])
+                self._recent = collections.OrderedDict()
+                self._pending_frames = []
+
         def gather_into(self, slots_ptr: int, batch: int, out_ptrs, stream: int) -> None:
             """Gather the sampled items into the dataset's (expanded) field buffers."""
             import ctypes

@@ -676,7 +676,7 @@ def main():
                    total_ms=round(ms.value, 3))
         if fl.value > 0:
             # Peak of the arithmetic path the section ran on (f32 MFMA, or the exact
-            # bf16-plane engines at bf16 dense peak / MFMA terms per product).
+            # f16-plane engine at the f16 dense peak / MFMA terms per product).
             pk = ctypes.c_double()
             _lib.check(L.acme_profile_query_peak(i, ctypes.byref(pk)))
             peak = pk.value if pk.value > 0 else FP32_MFMA_PEAK_TFLOPS

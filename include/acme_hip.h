@@ -144,14 +144,14 @@ int acme_replay_sample_gather(acme_replay* r, int64_t batch, uint64_t step_count
                               void* stream);
 
 /* acme_replay_sample_gather for the transition layout (two equal uint8 fields, e.g. o_tm1 /
- * o_t) that also writes the exact bf16 copy of both fields that the DQN plane path reads
- * (frames_bf16: [2 * batch][field_bytes] u16, rows [0, batch) the first field, [batch,
+ * o_t) that also writes the exact f16 copy of both fields that the DQN plane path reads
+ * (frames_f16: [2 * batch][field_bytes] u16, rows [0, batch) the first field, [batch,
  * 2 * batch) the second; 16-B aligned), in the same launch; pass it to the learner as
- * acme_transition_batch.obs_bf16.  Errors for other layouts. */
+ * acme_transition_batch.obs_f16.  Errors for other layouts. */
 int acme_replay_sample_gather_frames(acme_replay* r, int64_t batch, uint64_t step_counter,
                                      int64_t* slots, uint64_t* keys, double* probabilities,
                                      int64_t* table_size, double* priorities,
-                                     void* const* out_fields, uint16_t* frames_bf16,
+                                     void* const* out_fields, uint16_t* frames_f16,
                                      void* stream);
 
 /* Data-parallel global-probability sampling: one table per rank holds a
@@ -168,13 +168,13 @@ int acme_replay_sample_share(acme_replay* r, int64_t batch, uint64_t step_counte
                              double prob_scale, int64_t* slots, uint64_t* keys,
                              double* probabilities, int64_t* table_size, double* priorities,
                              void* const* out_fields, void* stream);
-/* acme_replay_sample_share with the gather and the bf16 frame copy of
- * acme_replay_sample_gather_frames (rows [0, batch) / [batch, 2 * batch) of frames_bf16). */
+/* acme_replay_sample_share with the gather and the f16 frame copy of
+ * acme_replay_sample_gather_frames (rows [0, batch) / [batch, 2 * batch) of frames_f16). */
 int acme_replay_sample_share_frames(acme_replay* r, int64_t batch, uint64_t step_counter,
                                     double prob_scale, int64_t* slots, uint64_t* keys,
                                     double* probabilities, int64_t* table_size,
                                     double* priorities, void* const* out_fields,
-                                    uint16_t* frames_bf16, void* stream);
+                                    uint16_t* frames_f16, void* stream);
 
 /* Frame-deduplicated observations: rebuild `batch` stacked
  * observations out[b] = stack(frames[idx[b][0..stack-1]], axis=-1) (uint8 HWC, as
@@ -271,10 +271,22 @@ int acme_dqn_tensor_info(const acme_dqn* l, int32_t i, int64_t* offset, int64_t*
 int acme_dqn_bind(acme_dqn* l, float* params, float* target, float* grads, float* adam_m,
                   float* adam_v);
 /* Declares that the caller wrote the bound params / target buffers directly (restore,
- * broadcast, initialisation): the learner's derived copies of them (the exact bf16
- * parameter planes of the uint8 Nature path) are rebuilt before the next use.  The
- * learner's own updates (step / apply) need no call. */
+ * broadcast, initialisation): the learner's derived copies of them (the scaled f16
+ * parameter planes of the uint8 Nature path) are rebuilt, and the activation / gradient
+ * plane scales recalibrated, before the next use.  The learner's own updates (step /
+ * apply) need no call. */
 int acme_dqn_params_changed(acme_dqn* l);
+/* Plane-range check of the uint8 Nature path (synchronises the device): *overflow = 1 if
+ * some plane tensor written since the last reset exceeded f16's range at its scale (its
+ * maximum grew more than 2^8-fold within one step; the results of that step are then not
+ * exact), else 0.  reset != 0 clears the flag. */
+int acme_dqn_plane_overflow(acme_dqn* l, int32_t* overflow, int32_t reset);
+/* The plane scales (powers of two) as learner state for checkpoints: acme_dqn_scale_state
+ * writes *count floats to out (when out is non-NULL and capacity suffices);
+ * acme_dqn_set_scale_state restores them after acme_dqn_params_changed, so the resumed
+ * steps are bit-identical to the uninterrupted run instead of recalibrating. */
+int acme_dqn_scale_state(const acme_dqn* l, float* out, int32_t capacity, int32_t* count);
+int acme_dqn_set_scale_state(acme_dqn* l, const float* in, int32_t count);
 
 typedef struct acme_transition_batch {
   const void* o_tm1;   /* [B, obs...]  u8 or f32 */
@@ -292,10 +304,10 @@ typedef struct acme_transition_batch {
    * per-rank batch, so that the all-reduce mean of the ranks' gradients is the global
    * batch's mean whatever the shares. */
   int64_t mean_over;
-  /* Optional (uint8 Nature network): the exact bf16 copy of [o_tm1; o_t], [2B][obs bytes]
+  /* Optional (uint8 Nature network): the exact f16 copy of [o_tm1; o_t], [2B][obs bytes]
    * u16, as acme_replay_sample_gather_frames writes it; the learner then skips its own
    * conversion (same bits).  NULL: the learner converts. */
-  const uint16_t* obs_bf16;
+  const uint16_t* obs_f16;
 } acme_transition_batch;
 
 typedef struct acme_dqn_outputs {
@@ -461,6 +473,8 @@ int acme_impala_bind(acme_impala* l, float* params, float* grads, float* adam_m,
  * policy_gradient_loss] as logged by learning.py:162-167. */
 int acme_impala_step(acme_impala* l, const acme_sequence_batch* batch, float* metrics,
                      void* stream);
+/* Plane-range check of the Atari plane path (as acme_dqn_plane_overflow). */
+int acme_impala_plane_overflow(acme_impala* l, int32_t* overflow, int32_t reset);
 /* One network step for `rows` independent actors (IMPALAActor.select_action): inputs
  * obs [rows, ...], prev_action / prev_reward [rows], state h / c [rows, lstm_size];
  * outputs logits [rows, A], values [rows], next state h_out / c_out. */
@@ -486,7 +500,7 @@ int32_t acme_profile_num_sections(void);
 int acme_profile_query(int32_t i, const char** name, double* total_ms, int64_t* count,
                        double* flops, double* bytes);
 /* TFLOP/s ceiling of the arithmetic path section i runs on (f32 MFMA 157.3; the exact
- * bf16-plane engines 2500 / MFMA terms per product: 416.7 for six terms, 833.3 for three);
+ * plane engines 2500 / MFMA terms per product: 833.3 for three terms, 1250 for two);
  * 0 for non-GEMM sections. */
 int acme_profile_query_peak(int32_t i, double* peak_tflops);
 

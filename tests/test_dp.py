@@ -311,7 +311,7 @@ def test_sharded_global_sampling_gpu(prefetch):
 
 def _nature_dp_worker(rank, world, port, q):
     """One rank of a Nature-CNN DP learner on a uint8 shard, run twice from the same state:
-    with the dataset's fused bf16 frame copy (acme_replay_sample_share_frames) and with the
+    with the dataset's fused f16 frame copy (acme_replay_sample_share_frames) and with the
     learner converting the frames itself (ACME_DATASET_BF16=0)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
@@ -348,7 +348,7 @@ def _nature_dp_worker(rank, world, port, q):
         for _ in range(4):
             learner.step()
         torch.cuda.synchronize()
-        copies.append(getattr(learner._iterator, "last_frames_bf16", None) is not None)
+        copies.append(getattr(learner._iterator, "last_frames_f16", None) is not None)
         out.append((learner.native.params.cpu().numpy(), learner.native.loss.item()))
     os.environ.pop("ACME_DATASET_BF16")
     q.put((rank, out, copies))
@@ -356,8 +356,8 @@ def _nature_dp_worker(rank, world, port, q):
 
 
 @pytest.mark.gpu
-def test_dp_nature_bf16_frame_copy_gpu():
-    """Sharded uint8 tables: the fused sample + gather + bf16 copy of each rank's share feeds
+def test_dp_nature_f16_frame_copy_gpu():
+    """Sharded uint8 tables: the fused sample + gather + f16 copy of each rank's share feeds
     the DP learner's forward (rows [0, n) and [n, 2n) of the copy for a share of n rows);
     the steps are bit-identical to the learner's own conversion, and replicas agree."""
     world, port = 2, _free_port()

@@ -275,48 +275,6 @@ def test_fused_step_equals_staged_step_bitwise():
         assert a.loss.item() == b.loss.item()
 
 
-def test_captured_step_graph_matches_eager():
-    """The opt-in captured step (ACME_V_DQNGRAPH=2: one hipGraph per batch buffers / target
-    copy, Adam's step count on the device) against an eager step from the same state, five
-    steps with target copies, the graph replayed from two sets of batch buffers and after an
-    eager step: loss and gradients bit-identical, Adam within its bias-correction rounding
-    (device vs host powf: rtol 1e-6, atol lr x 1e-6), the same target-copy cadence."""
-    from acme_amd._lib import lib
-    from acme_amd.networks import DQNAtariNetwork
-    net = DQNAtariNetwork(18)
-    B = 32
-    p0, t0 = net.init(3), net.init(4)
-    a = _learner(net, B, target_update_period=2)
-    b = _learner(net, B, target_update_period=2)
-    a.set_params(p0, t0)
-    rng = np.random.default_rng(12)
-    bufs = [_dev(_batch(rng, B, (84, 84, 4), 18)) for _ in range(2)]
-    try:
-        for i in range(5):
-            for w in ("params", "target", "m", "v"):  # b starts from a's state
-                getattr(b, w).copy_(getattr(a, w))
-            b.params_changed()
-            b.num_steps = a.num_steps
-            dev = bufs[i % 2]
-            lib().acme_tune_set(b"DQNGRAPH", 0 if i == 3 else 2)  # step 3 eager on both
-            a.step(*dev)
-            lib().acme_tune_set(b"DQNGRAPH", 0)
-            b.step(*dev)
-            torch.cuda.synchronize()
-            assert a.loss.item() == b.loss.item(), i
-            ga, gb = a.get_params("grads"), b.get_params("grads")
-            for k in ga:
-                np.testing.assert_array_equal(ga[k], gb[k], err_msg=f"step {i} grads/{k}")
-            for buf in ("params", "target", "m", "v"):
-                ga, gb = a.get_params(buf), b.get_params(buf)
-                for k in ga:
-                    np.testing.assert_allclose(ga[k], gb[k], rtol=1e-6, atol=1e-9,
-                                               err_msg=f"step {i} {buf}/{k}")
-            assert a.num_steps == b.num_steps == i + 1
-    finally:
-        lib().acme_tune_set(b"DQNGRAPH", 0)
-
-
 def test_adjacent_frames_layout_bitwise():
     """The GPU dataset hands o_t directly after o_tm1 in one allocation; the step on that
     layout is bit-identical to the step on separate buffers."""

@@ -114,3 +114,36 @@ def test_frames_expand_matches_numpy():
         torch.cuda.synchronize()
         ref = np.stack([frames.cpu().numpy()[idx[:, s]] for s in range(stack)], axis=-1)
         np.testing.assert_array_equal(out.cpu().numpy(), ref.reshape(B, -1))
+
+
+def test_frame_table_checkpoint_round_trip():
+    """save() / restore() carry the frame ring and its recycling bookkeeping: a restored
+    FrameTable samples the same bytes as the original, and both keep accepting the same
+    episodes (through ring recycling) with identical samples afterwards."""
+    spec = _spec()
+    sig = adders.NStepTransitionAdder.signature(spec)
+    mk = dict(name=adders.DEFAULT_PRIORITY_TABLE, sampler=replay.selectors.Prioritized(0.6),
+              remover=replay.selectors.Fifo(), max_size=120,
+              rate_limiter=replay.rate_limiters.MinSize(1), signature=sig, seed=5)
+    a = replay.FrameTable(**mk, max_frames=200)
+    _fill([a], np.random.default_rng(4), n_episodes=3, length=40)
+    state = a.save()
+    b = replay.FrameTable(**mk, max_frames=200)
+    b.restore(state)
+    assert b.size() == a.size() and b.frames_stored == a.frames_stored
+    for t in (a, b):  # more episodes: the ring recycles positions saved in the checkpoint
+        _fill([t], np.random.default_rng(6), n_episodes=2, length=40)
+    its = [iter(make_reverb_dataset(replay.Server([t]), batch_size=32)) for t in (a, b)]
+    for _ in range(3):
+        x, y = next(its[0]), next(its[1])
+        torch.cuda.synchronize()
+        for u, v in zip(list(x.info) + list(x.data), list(y.info) + list(y.data)):
+            np.testing.assert_array_equal(u.cpu().numpy(), v.cpu().numpy())
+
+
+def test_queue_table_refuses_checkpoint():
+    q = replay.Table.queue("queue", 8)
+    with pytest.raises(NotImplementedError, match="not checkpointable"):
+        q.save()
+    with pytest.raises(NotImplementedError, match="not checkpointable"):
+        q.restore({})

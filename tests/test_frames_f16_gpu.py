@@ -1,5 +1,5 @@
-"""The fused sample + gather's bf16 frame copy (acme_replay_sample_gather_frames) and the
-DQN learner reading it (acme_transition_batch.obs_bf16): the copy is bf16(byte) of exactly
+"""The fused sample + gather's f16 frame copy (acme_replay_sample_gather_frames) and the
+DQN learner reading it (acme_transition_batch.obs_f16): the copy is f16(byte) of exactly
 the gathered o_tm1 / o_t rows, and a learner step on it is bit-identical to the step that
 converts the uint8 batch itself (the dataset -> DQNLearner path of the bench)."""
 
@@ -14,12 +14,12 @@ from tests.test_replay_gpu import _native
 pytestmark = pytest.mark.gpu
 
 
-def _bf16_of(u8: np.ndarray) -> np.ndarray:
-    return (u8.astype(np.float32).view(np.uint32) >> 16).astype(np.uint16)
+def _f16_of(u8: np.ndarray) -> np.ndarray:
+    return u8.astype(np.float16).view(np.uint16)
 
 
 @pytest.mark.parametrize("prioritized", [True, False])
-def test_sample_gather_frames_writes_exact_bf16(prioritized):
+def test_sample_gather_frames_writes_exact_f16(prioritized):
     from acme_amd._lib import lib
     rng = np.random.default_rng(2)
     fields = [28224, 4, 4, 4, 28224]
@@ -42,8 +42,8 @@ def test_sample_gather_frames_writes_exact_bf16(prioritized):
     np.testing.assert_array_equal(o_tm1, data[0][keys])
     np.testing.assert_array_equal(o_t, data[4][keys])
     got = fb.cpu().numpy().view(np.uint16)
-    np.testing.assert_array_equal(got[:B], _bf16_of(o_tm1))
-    np.testing.assert_array_equal(got[B:], _bf16_of(o_t))
+    np.testing.assert_array_equal(got[:B], _f16_of(o_tm1))
+    np.testing.assert_array_equal(got[B:], _f16_of(o_t))
     # Other layouts are refused.
     r2 = _native(cap, [64, 4], prioritized)
     r2.insert([rng.integers(0, 256, (10, 64), dtype=np.uint8),
@@ -57,7 +57,7 @@ def test_sample_gather_frames_writes_exact_bf16(prioritized):
                                               None) != 0
 
 
-def test_learner_step_on_dataset_bf16_frames_bitwise():
+def test_learner_step_on_dataset_f16_frames_bitwise():
     from acme_amd.native import NativeDQN
     from acme_amd.networks import DQNAtariNetwork
     net = DQNAtariNetwork(18)
@@ -78,7 +78,7 @@ def test_learner_step_on_dataset_bf16_frames_bitwise():
         fb = torch.cat([o1, o2]).to(torch.float32).view(torch.int32).bitwise_right_shift(16) \
             .to(torch.int16).contiguous()
         a.step(o1, act, rew, dis, o2, pr)
-        b.step(o1, act, rew, dis, o2, pr, obs_bf16=fb)
+        b.step(o1, act, rew, dis, o2, pr, obs_f16=fb)
         torch.cuda.synchronize()
         assert a.loss.item() == b.loss.item()
         for buf in ("params", "m", "v", "grads"):

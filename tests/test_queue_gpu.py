@@ -1,0 +1,63 @@
+"""Table.queue under contention: writer threads blocked on a full queue
+resume the moment the reader consumes a batch.  The reader's gather of the consumed ring
+slots must be on a stream before those slots are released, or a resumed writer's insert
+lands in a slot whose gather has not run yet and the batch carries newer rows than its
+keys.  Every gathered item is checked against its key (the item's insertion index, which
+the writers encode into its payload)."""
+
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from acme_amd import replay
+from acme_amd.datasets import make_reverb_dataset
+
+pytestmark = pytest.mark.gpu
+
+PAYLOAD = 32768  # bytes per item: a gather long enough to race a resumed writer's copy
+
+
+def _item(k: int):
+    p = np.full(PAYLOAD, k % 251, np.uint8)
+    p[:4] = np.frombuffer(np.int32(k).tobytes(), np.uint8)
+    return {"index": np.int32(k), "payload": p}
+
+
+def test_queue_gather_matches_keys_with_writers_blocked_on_full_queue():
+    B, cap, writers, per_writer = 4, 8, 3, 160
+    q = replay.Table.queue("queue", cap)
+    server = replay.Server([q])
+    order = {}  # insertion index -> the item's k
+
+    def write(w: int):
+        for j in range(per_writer):
+            k = w * 100000 + j
+            # The queue's lock (re-entrant; released while insert() waits on a full queue)
+            # makes "insert, then read the insertion index" atomic against other writers,
+            # and the reader cannot consume the item before it is recorded.
+            with q._cv:  # noqa: SLF001
+                q.insert(_item(k), 1.0)
+                order[q._accepted - 1] = k  # noqa: SLF001
+
+    threads = [threading.Thread(target=write, args=(w,), daemon=True) for w in range(writers)]
+    for t in threads:
+        t.start()
+    it = iter(make_reverb_dataset(server, batch_size=B))
+    seen = 0
+    for _ in range(writers * per_writer // B):
+        s = next(it)
+        torch.cuda.synchronize()
+        keys = s.info.key.cpu().numpy().view(np.int64)
+        idx = s.data["index"].cpu().numpy()
+        pay = s.data["payload"].cpu().numpy()
+        expect = np.asarray([order[i] for i in keys])
+        np.testing.assert_array_equal(keys, np.arange(seen, seen + B))
+        np.testing.assert_array_equal(idx, expect)
+        np.testing.assert_array_equal(pay[:, 4:], np.repeat((expect % 251)[:, None], PAYLOAD - 4,
+                                                            axis=1).astype(np.uint8))
+        seen += B
+    for t in threads:
+        t.join(timeout=30)
+    assert q.size() == 0

@@ -49,7 +49,7 @@ SECTIONS = [
     (r"P3DenseWgrad", "fc_wgrad"),
     (r"P3DenseDgrad", "fc_dgrad"),
     (r"fc_head_forward_kernel|fc_head1024_kernel", "fc_head_fwd"),
-    (r"frames_bf16_kernel", "frames_bf16"),
+    (r"frames_f16_kernel", "frames_f16"),
     (r"head_dz_planes_kernel", "head_dz"),
     (r"dqn_loss_head_dz_kernel", "loss_head_dz"),
     (r"gemm_p3c12_kernel", "conv12_fwd"),
