@@ -35,7 +35,8 @@ class DQNLearner(core.Learner, core.Saveable):
                  logger: Optional[loggers.Logger] = None, checkpoint: bool = True,
                  max_abs_reward: float = 1.0, batch_size: Optional[int] = None, seed: int = 0,
                  device=None, data_parallel: bool = True, semantics: str = "tf",
-                 target_seed: Optional[int] = None, adam=None):
+                 target_seed: Optional[int] = None, adam=None,
+                 reduce_logged_loss: bool = True):
         if huber_loss_parameter < 0:
             raise ValueError("quadratic_linear_boundary must be >= 0.")
         self._network = network
@@ -68,6 +69,11 @@ class DQNLearner(core.Learner, core.Saveable):
         self._obs_flat = int(np.prod(network.obs_shape))
         self._checkpoint = checkpoint
         self._log_loss = True
+        # Data parallel: whether the logged loss is all-reduced to the global batch's.  Every
+        # rank must make the same choice (a collective issued on some ranks only would pair
+        # with a different collective on the others), so it is a constructor argument, never
+        # derived from per-rank state such as the logger type.
+        self._reduce_loss = bool(reduce_logged_loss)
         # Data parallelism (one process per GPU, torch.distributed over RCCL): each rank
         # samples its own batch from its replay shard; the IS-weight normaliser and the
         # gradients are reduced across ranks before Adam, so every replica applies the
@@ -146,8 +152,7 @@ class DQNLearner(core.Learner, core.Saveable):
         elapsed = now - self._timestamp if self._timestamp else 0
         self._timestamp = now
         loss = self._native.loss
-        if (self._dist is not None and self._log_loss
-                and not isinstance(self._logger, loggers.NoOpLogger)):
+        if self._dist is not None and self._log_loss and self._reduce_loss:
             # The logged loss is the global batch's (SURVEY §8(e) collective 3): each rank's
             # loss is its share's sum over the nominal per-rank batch, so the mean over ranks.
             loss = loss.clone()

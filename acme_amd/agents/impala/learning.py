@@ -11,6 +11,7 @@ core_state[:, 0], policy/value head, V-trace, losses, BPTT, global-norm clip, Ad
 
 from __future__ import annotations
 
+import threading
 import time
 from typing import Dict, List, Optional
 
@@ -59,6 +60,8 @@ class IMPALALearner(core.Learner, core.Saveable):
         m = self._native.metrics
         self._metric_views = {"loss": m[0], "critic_loss": m[1], "entropy_loss": m[2],
                               "policy_gradient_loss": m[3]}
+        # Parameter snapshots for actor networks (actor_policy): allocated on first use.
+        self._snap = None
 
     def step(self):
         sample = next(self._iterator)
@@ -80,6 +83,8 @@ class IMPALALearner(core.Learner, core.Saveable):
                           c(data.discount.reshape(B, T), torch.float32),
                           c(data.extras["logits"], torch.float32),
                           hidden.to(torch.float32)[:, 0], cell.to(torch.float32)[:, 0])
+        if self._snap is not None:
+            self._publish_snapshot()
         now = time.time()
         elapsed = now - self._timestamp if self._timestamp else 0
         self._timestamp = now
@@ -99,16 +104,48 @@ class IMPALALearner(core.Learner, core.Saveable):
                                     t(hidden, torch.float32), t(cell, torch.float32))
         return lg.cpu().numpy(), v.cpu().numpy(), h.cpu().numpy(), c.cpu().numpy()
 
-    def actor_policy(self, max_rows: int = 16):
-        """A policy_step for actor threads that does not share the learner's workspace: a
-        second native network bound to the learner's parameter buffer, on its own stream
-        (actor inference overlaps learner steps; the actors read the parameters current when
-        their step runs, as a VariableClient refreshed every step would)."""
+    # -- actor-side parameter snapshots (the reference's VariableClient hands actors a whole
+    # set of weights; an actor forward reading the learner's buffer while Adam rewrites it
+    # in place could mix two updates).  Two snapshot buffers: after each step the learner's
+    # stream copies the parameters into the one not published last (first waiting for every
+    # actor read of it that was issued), records an event and publishes it; an actor step
+    # waits for the published snapshot's event, reads it, and records its own read event.
+    def _ensure_snapshots(self) -> None:
+        if self._snap is None:
+            n = self._native
+            self._snap_lock = threading.Lock()
+            self._snap_buf = [n.params.clone(), n.params.clone()]
+            self._snap_ready = [torch.cuda.Event(), torch.cuda.Event()]
+            self._snap_reads = [{}, {}]  # per buffer: the last read event of each stream
+            for e in self._snap_ready:
+                e.record(torch.cuda.current_stream(n.device))
+            self._snap = 0  # the published buffer
+
+    def _publish_snapshot(self) -> None:
         n = self._native
-        net = NativeIMPALA(num_actions=n.num_actions, max_batch=int(max_rows),
-                           max_sequence_length=2, torso=n.torso, obs_dim=n.obs_dim,
-                           lstm_size=n.lstm_size, head_size=self._network.head_size,
-                           device=n.device, shared_params=n.params)
+        cur = torch.cuda.current_stream(n.device)
+        with self._snap_lock:
+            j = self._snap ^ 1
+            reads, self._snap_reads[j] = self._snap_reads[j], {}
+        for ev in reads.values():
+            cur.wait_event(ev)
+        self._snap_buf[j].copy_(n.params)
+        self._snap_ready[j].record(cur)
+        with self._snap_lock:
+            self._snap = j
+
+    def actor_policy(self, max_rows: int = 16):
+        """A policy_step for actor threads that does not share the learner's workspace: two
+        native networks bound to the learner's two parameter snapshots, on the thread's own
+        stream (actor inference overlaps learner steps; each actor step reads the latest
+        published snapshot, a whole set of weights, as a VariableClient refreshed every
+        step would)."""
+        n = self._native
+        self._ensure_snapshots()
+        nets = [NativeIMPALA(num_actions=n.num_actions, max_batch=int(max_rows),
+                             max_sequence_length=2, torso=n.torso, obs_dim=n.obs_dim,
+                             lstm_size=n.lstm_size, head_size=self._network.head_size,
+                             device=n.device, shared_params=buf) for buf in self._snap_buf]
         stream = torch.cuda.Stream(device=n.device)
         dt = torch.uint8 if self._network.torso == "atari" else torch.float32
         dev = n.device
@@ -116,16 +153,24 @@ class IMPALALearner(core.Learner, core.Saveable):
         def step(observation, prev_action, prev_reward, hidden, cell):
             t = lambda x, d: torch.as_tensor(np.asarray(x)).to(dev, d, non_blocking=True)  # noqa
             rows = int(np.asarray(prev_action).shape[0])
+            with self._snap_lock:
+                j = self._snap
+                stream.wait_event(self._snap_ready[j])
             with torch.cuda.stream(stream):
-                lg, v, h, c = net.policy_step(t(observation, dt).reshape(rows, -1),
-                                              t(prev_action, torch.int32),
-                                              t(prev_reward, torch.float32),
-                                              t(hidden, torch.float32), t(cell, torch.float32),
-                                              stream=stream)
+                lg, v, h, c = nets[j].policy_step(t(observation, dt).reshape(rows, -1),
+                                                  t(prev_action, torch.int32),
+                                                  t(prev_reward, torch.float32),
+                                                  t(hidden, torch.float32),
+                                                  t(cell, torch.float32), stream=stream)
+                done = torch.cuda.Event()
+                done.record(stream)
+                with self._snap_lock:
+                    self._snap_reads[j][id(stream)] = done  # later reads on a stream wait
+                                                            # for the earlier ones
                 out = [x.cpu().numpy() for x in (lg, v, h, c)]
             return tuple(out)
 
-        step.native = net  # keeps the network alive with the closure
+        step.native = nets  # keeps the networks alive with the closure
         return step
 
     def get_variables(self, names: List[str]) -> List[Dict[str, np.ndarray]]:

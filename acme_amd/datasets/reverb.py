@@ -27,7 +27,7 @@ counter block i.
 from __future__ import annotations
 
 import os
-from typing import Optional
+from typing import Any, Optional, Tuple
 
 import numpy as np
 import torch
@@ -43,6 +43,57 @@ _TORCH = {np.dtype(k): v for k, v in [
     ("int32", torch.int32), ("int64", torch.int64), ("float16", torch.float16),
     ("float32", torch.float32), ("float64", torch.float64), ("bool", torch.bool),
     ("uint64", torch.uint64), ("uint32", torch.uint32)]}
+
+
+class TensorSpec:
+    """Shape (None for a dimension known only at run time) and dtype of a yielded tensor:
+    the role tf.TensorSpec plays in the reference's dataset.element_spec (a leaf, not a
+    tuple, for acme_amd.utils.tree)."""
+    __slots__ = ("shape", "dtype")
+
+    def __init__(self, shape: Tuple[Optional[int], ...], dtype: Any):
+        self.shape = tuple(shape)
+        self.dtype = np.dtype(dtype)
+
+    def __eq__(self, other) -> bool:
+        return (isinstance(other, TensorSpec) and self.shape == other.shape
+                and self.dtype == other.dtype)
+
+    def __repr__(self) -> str:
+        return f"TensorSpec(shape={self.shape}, dtype={self.dtype})"
+
+
+def _adder_spec(transition_adder: bool, environment_spec, extra_spec):
+    """The structure of the items the adders write (acme/datasets/reverb.py:141-187):
+    transitions (o, a, r, d, o', [extras]) or Step(observation, action, reward, discount,
+    start_of_episode, extras)."""
+    if transition_adder:
+        spec = tuple(environment_spec) + (environment_spec.observations,)
+        if extra_spec:
+            spec += (extra_spec,)
+        return spec
+    from acme_amd import specs
+    return adders.Step(observation=environment_spec.observations,
+                       action=environment_spec.actions, reward=environment_spec.rewards,
+                       discount=environment_spec.discounts,
+                       start_of_episode=specs.Array(shape=(), dtype=bool),
+                       extras=() if not extra_spec else extra_spec)
+
+
+def _element_shapes(adder_spec, sequence_length, convert_zero_size_to_none, batch_size):
+    """Per-leaf TensorSpecs as the reference derives them (datasets/reverb.py:189-198; as
+    there, convert_zero_size_to_none replaces the sequence dimension rule) with the batch
+    dimension of the drop-remainder batching in front."""
+    def shape(x):
+        if convert_zero_size_to_none:
+            s = tuple(d if d else None for d in x.shape)
+        elif sequence_length:
+            s = (int(sequence_length),) + tuple(x.shape)
+        else:
+            s = tuple(x.shape)
+        return TensorSpec(((int(batch_size),) if batch_size else ()) + s, np.dtype(x.dtype))
+    leaves = tree.flatten(adder_spec)
+    return tree.unflatten_as(adder_spec, [shape(x) for x in leaves])
 
 
 def _server_of(address) -> replay.Server:
@@ -67,27 +118,70 @@ class ReplayDataset:
     of world * batch_size items (acme_amd.replay.sharding), so it holds a varying number of
     items (at most 2 * batch_size) whose probabilities are their global marginals."""
 
-    def __init__(self, table, batch_size: int, timeout: float = 60.0, prefetch: int = 0,
-                 global_sampling: Optional[bool] = None):
-        if batch_size is None or batch_size < 1:
-            raise ValueError("the GPU replay dataset needs a batch_size >= 1")
+    def __init__(self, table, batch_size: Optional[int], timeout: float = 60.0, prefetch: int = 0,
+                 global_sampling: Optional[bool] = None, data_spec=None):
+        if batch_size is not None and batch_size < 1:
+            raise ValueError("batch_size must be >= 1 (or None for single items)")
         if prefetch < 0:
             raise ValueError("prefetch_size must be >= 0")
         self.table = table
-        self.batch_size = int(batch_size)
+        # batch_size None: single items without a batch dimension (the reference's
+        # unbatched dataset), drawn as batches of one.
+        self.batched = batch_size is not None
+        self.batch_size = int(batch_size) if batch_size is not None else 1
         self.timeout = timeout
         self.prefetch = int(prefetch)
         self.global_sampling = global_sampling
+        self._data_spec = data_spec
+
+    @property
+    def element_spec(self) -> replay.ReplaySample:
+        """TensorSpecs of what next() yields (tf.data's element_spec): the data from the
+        environment spec given to make_reverb_dataset (as the reference), else from the
+        table's item layout; the info fields per item."""
+        B = (self.batch_size,) if self.batched else ()
+        data = self._data_spec
+        if data is None:
+            t = self.table
+            if t.fields is None:
+                raise ValueError("element_spec needs an environment_spec or a table signature")
+            data = tree.unflatten_as(t._structure, [  # noqa: SLF001
+                TensorSpec(B + tuple(f.shape), np.dtype(f.dtype)) for f in t.fields])
+        info = replay.SampleInfo(key=TensorSpec(B, np.dtype(np.uint64)),
+                                 probability=TensorSpec(B, np.dtype(np.float64)),
+                                 table_size=TensorSpec(B, np.dtype(np.int64)),
+                                 priority=TensorSpec(B, np.dtype(np.float64)))
+        return replay.ReplaySample(info=info, data=data)
 
     def __iter__(self):
         if isinstance(self.table, replay.QueueTable):
-            return _QueueIterator(self.table, self.batch_size, self.timeout)
-        dp = _data_parallel()
-        shard = dp if (self.global_sampling if self.global_sampling is not None
-                       else dp is not None) else None
-        if shard is None and self.global_sampling:
-            raise ValueError("global_sampling needs an initialised torch.distributed group")
-        return _TableIterator(self.table, self.batch_size, self.timeout, self.prefetch, shard)
+            it = _QueueIterator(self.table, self.batch_size, self.timeout)
+        else:
+            dp = _data_parallel()
+            shard = dp if (self.global_sampling if self.global_sampling is not None
+                           else dp is not None) else None
+            if shard is None and self.global_sampling:
+                raise ValueError("global_sampling needs an initialised torch.distributed group")
+            it = _TableIterator(self.table, self.batch_size, self.timeout, self.prefetch, shard)
+        return it if self.batched else _Unbatched(it)
+
+
+class _Unbatched:
+    """Single items (batch_size None): the batch-of-one samples with the batch dimension
+    dropped (views of the iterator's buffers, valid until it advances twice)."""
+
+    def __init__(self, it):
+        self._it = it
+
+    def __iter__(self):
+        return self
+
+    def __next__(self) -> replay.ReplaySample:
+        s = next(self._it)
+        first = lambda x: x[0]  # noqa: E731
+        return replay.ReplaySample(
+            info=replay.SampleInfo(*[None if x is None else x[0] for x in s.info]),
+            data=tree.unflatten_as(s.data, [first(x) for x in tree.flatten(s.data)]))
 
 
 class _TableIterator:
@@ -351,20 +445,33 @@ def make_reverb_dataset(server_address, environment_spec=None, batch_size: Optio
                         global_sampling: Optional[bool] = None) -> ReplayDataset:
     """Same arguments as the reference.  `prefetch_size` issues that many batches ahead on
     the dataset's stream (module docstring); the parallel-batch knob of the tf.data pipeline
-    has no equivalent; the environment/extra specs are only checked for consistency with
-    the table's layout."""
-    del parallel_batch_optimization, convert_zero_size_to_none
-    del using_deprecated_adder, sequence_length
+    has no equivalent.  The environment / extra specs, transition_adder, sequence_length and
+    convert_zero_size_to_none define `element_spec` as the reference's shapes and dtypes do
+    (datasets/reverb.py:141-198); the rows themselves come from the table's layout (a
+    sequence table stores T-step items, yielded [B, T, ...]), which is checked against the
+    spec when both are known.  The GPU table stores fixed-shape rows, so items whose zero-size
+    dimensions vary in length are refused at insert time."""
+    del parallel_batch_optimization, using_deprecated_adder
     server = _server_of(server_address)
     if table not in server.tables:
         raise ValueError(f"unknown table {table!r}")
     t = server.tables[table]
-    if environment_spec is not None and transition_adder and isinstance(t, replay.Table):
-        sig = adders.NStepTransitionAdder.signature(environment_spec, extra_spec or ())
-        if t.fields is not None and len(tree.flatten(sig)) != len(t.fields):
-            raise ValueError("environment_spec does not match the table's item layout")
+    data_spec = None
+    if environment_spec is not None:
+        data_spec = _element_shapes(_adder_spec(transition_adder, environment_spec, extra_spec),
+                                    sequence_length, convert_zero_size_to_none, batch_size)
+        if isinstance(t, replay.Table) and t.fields is not None:
+            leaves = tree.flatten(data_spec)
+            if len(leaves) != len(t.fields):
+                raise ValueError("environment_spec does not match the table's item layout")
+            nb = 1 if batch_size else 0
+            for x, f in zip(leaves, t.fields):
+                want = tuple(x.shape[nb:])
+                if None not in want and (want != tuple(f.shape) or np.dtype(x.dtype) != f.dtype):
+                    raise ValueError(f"environment_spec leaf {want} {np.dtype(x.dtype)} does not "
+                                     f"match the table's {tuple(f.shape)} {f.dtype}")
     return ReplayDataset(t, batch_size, prefetch=prefetch_size or 0,
-                         global_sampling=global_sampling)
+                         global_sampling=global_sampling, data_spec=data_spec)
 
 
 make_dataset = make_reverb_dataset

@@ -53,6 +53,12 @@ def _pack(state: Mapping) -> Dict[str, np.ndarray]:
 
 
 def _unpack(z: Mapping[str, np.ndarray]) -> Dict:
+    if _MANIFEST not in z:
+        # The round-1 format ('/'-joined flat keys) cannot be unflattened unambiguously:
+        # parameter names contain '/' themselves.
+        raise ValueError("unsupported checkpoint format: no manifest (a checkpoint.npz written "
+                         "by an older acme_amd with '/'-joined flat keys); re-save it with "
+                         "this version or start from a fresh directory")
     manifest = json.loads(str(z[_MANIFEST]))
     out: Dict = {}
     for i, entry in enumerate(manifest):

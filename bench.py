@@ -209,7 +209,8 @@ def setup_dqn(args, world, rank, dev):
     learner = DQNLearner(net, net, discount=0.99, importance_sampling_exponent=0.2,
                          learning_rate=1e-3, target_update_period=100, dataset=dataset,
                          replay_client=replay.Client(server), counter=counting.Counter(),
-                         logger=loggers.NoOpLogger(), seed=0, device=dev)
+                         logger=loggers.NoOpLogger(), seed=0, device=dev,
+                         reduce_logged_loss=False)
     meta = dict(
         metric=METRIC, dtype="f32",
         data="synthetic (device-generated uint8 Atari-shape transitions, random-init "

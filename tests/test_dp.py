@@ -80,7 +80,7 @@ def test_dp_gradient_mean_equals_global_batch_cpu():
         assert err <= 1e-12 * max(scale, 1.0), (err, scale)
 
 
-def _gpu_worker(rank, world, port, q):
+def _gpu_worker(rank, world, port, q, mixed_loggers=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -104,8 +104,11 @@ def _gpu_worker(rank, world, port, q):
             while True:
                 yield replay.ReplaySample(info=info, data=data)
 
+    # mixed_loggers: only rank 0 logs (a common setup); the loss all-reduce must still run
+    # on every rank or it pairs with a different collective on the others.
     log = loggers.InMemoryLogger()
-    learner = DQNLearner(net, net, 0.99, 0.2, 1e-3, 100, _Fixed(), logger=log,
+    learner = DQNLearner(net, net, 0.99, 0.2, 1e-3, 100, _Fixed(),
+                         logger=log if rank == 0 or not mixed_loggers else loggers.NoOpLogger(),
                          seed=rank)  # different seeds: the broadcast must equalise them
     for _ in range(3):
         learner.step()
@@ -116,13 +119,15 @@ def _gpu_worker(rank, world, port, q):
 
 
 @pytest.mark.gpu
-def test_dp_learner_matches_global_batch_gpu():
+@pytest.mark.parametrize("mixed_loggers", [False, True])
+def test_dp_learner_matches_global_batch_gpu(mixed_loggers):
     from acme_amd.native import NativeDQN
     from acme_amd.networks import MLP
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_gpu_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_gpu_worker, args=(r, world, port, q, mixed_loggers))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=300) for _ in range(world))
@@ -132,7 +137,10 @@ def test_dp_learner_matches_global_batch_gpu():
     losses = {r: res[r][1] for r in res}
     res = {r: res[r][0] for r in res}
     np.testing.assert_array_equal(res[0], res[1])  # replicas identical
-    assert losses[0] == losses[1]  # the logged loss is the global batch's on every rank
+    if mixed_loggers:
+        assert losses[1] == [] and len(losses[0]) == 3
+    else:
+        assert losses[0] == losses[1]  # the logged loss is the global batch's on every rank
     # Single process, global batch 64, same initial params (rank 0's seed).
     net = MLP(6, [16, 16], 3)
     d = NativeDQN(network="mlp", num_actions=3, max_batch=64, obs_dtype="float32", obs_dim=6,

@@ -75,8 +75,7 @@ def test_learner_step_on_dataset_f16_frames_bitwise():
         rew = torch.from_numpy(rng.standard_normal(B).astype(np.float32)).cuda()
         dis = torch.full((B,), 0.99 ** 4, dtype=torch.float32, device="cuda")
         pr = torch.from_numpy(rng.uniform(1e-6, 1e-3, B)).cuda()
-        fb = torch.cat([o1, o2]).to(torch.float32).view(torch.int32).bitwise_right_shift(16) \
-            .to(torch.int16).contiguous()
+        fb = torch.cat([o1, o2]).to(torch.float16).view(torch.int16).contiguous()
         a.step(o1, act, rew, dis, o2, pr)
         b.step(o1, act, rew, dis, o2, pr, obs_f16=fb)
         torch.cuda.synchronize()

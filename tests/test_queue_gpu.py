@@ -12,6 +12,7 @@ import pytest
 import torch
 
 from acme_amd import replay
+from acme_amd.adders import reverb as adders
 from acme_amd.datasets import make_reverb_dataset
 
 pytestmark = pytest.mark.gpu
@@ -27,7 +28,7 @@ def _item(k: int):
 
 def test_queue_gather_matches_keys_with_writers_blocked_on_full_queue():
     B, cap, writers, per_writer = 4, 8, 3, 160
-    q = replay.Table.queue("queue", cap)
+    q = replay.Table.queue(adders.DEFAULT_PRIORITY_TABLE, cap)
     server = replay.Server([q])
     order = {}  # insertion index -> the item's k
 

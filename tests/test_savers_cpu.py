@@ -64,6 +64,16 @@ def test_round_trip_every_learner_layout(tmp_path):
     assert isinstance(fresh["dqn"].state["num_steps"], int)
 
 
+def test_manifestless_checkpoint_is_rejected_clearly(tmp_path):
+    """A checkpoint.npz in the round-1 flat-key format (no manifest) raises a clear
+    ValueError from the restoring constructor instead of a KeyError."""
+    import pytest
+    np.savez(str(tmp_path / "checkpoint.npz"), **{"learner/network/a/b": np.ones(3, np.float32),
+                                                   "learner/num_steps": np.int64(4)})
+    with pytest.raises(ValueError, match="unsupported checkpoint format"):
+        savers.Checkpointer({"learner": _State(None)}, str(tmp_path))
+
+
 def test_time_gating(tmp_path):
     s = _State({"x": np.zeros(2)})
     ck = savers.Checkpointer({"o": s}, str(tmp_path), time_delta_minutes=60)
