@@ -124,6 +124,7 @@ enum {
   kScParams = kScTransient, kScTarget,
   kScCount
 };
+constexpr int64_t kParamAmaxPeriod = 8;
 
 int add_tensor(acme_dqn* l, const char* name, std::initializer_list<int64_t> shape) {
   Tensor t;
@@ -345,6 +346,8 @@ int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const torso:
     p.b_src = SRC(WP(l, wpl, l->t_fcw), (int64_t)kFlat * 2 * kHidden); p.slab = slab;
     // Producer / consumer waves with fragment reads one k16 step ahead (gemm_p3ws_kernel):
     // 65.2 -> 60.5 us against the single-role kernel, the same bits.
+    // (Two f16 planes, measured on the step: 256x128 / 128x256 WS tiles, 256x128 single-role
+    // tiles with split-K 8, and the LDS-DMA ring (3 or 4 stages) all slower or equal.)
     if (tune("WSN") == 1) ACME_P3_GEMM("fc_fwd", 128, 128, 2, 2, 32, p, splits);  // tests
     else ACME_P3WS_GEMM("fc_fwd", 128, 128, 2, 2, 32, p, splits, true);
     ACME_PROF("fc_head_fwd", st, 0.0, 4.0 * (double)rows * 2 * kHidden * (splits + 1));
@@ -440,7 +443,9 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st_main,
                              la.loss, st);
     if (rc != ACME_OK) return rc;
   }
-  {  // Head weight / bias gradients: one skinny GEMM over the batch + scatter.
+  {  // Head weight / bias gradients: one skinny GEMM over the batch + scatter.  (One
+     // launch without split-K, 64 units per block and the batch over 8 waves, took 38 us
+     // against 9.3 + 6.7: 17 blocks cannot hide the row loads.)
     DuelHeadWgrad p;
     p.M = 2 * kHidden; p.N = A + 1; p.K = B; p.k_chunk = chunk_for(B, kHeadBwdSplits);
     p.A = A; p.h = l->hid; p.g = l->g; p.act = l->a_cache; p.slab = hslab;
@@ -1082,15 +1087,17 @@ int acme_dqn_grad_split(const acme_dqn* l, int64_t* split) {
 // Adam (+ the parameter planes) and the periodic target copy; `copy` decided by the host.
 static int apply_impl(acme_dqn* l, bool copy, hipStream_t st) {
   const bool jax = l->cfg.semantics == ACME_SEMANTICS_JAX;
-  ACME_PROF("adam", st, 0.0, 28.0 * (double)l->logical);
-  // The parameter planes (plane path) are refreshed by the same pass.  t = num_steps + 1
-  // (snt.Adam / optix.adam count this step first).
-  int rc = launch_adam(l->params, l->grads, l->m, l->v, l->flat, l->cfg.learning_rate,
-                       l->cfg.adam_beta1, l->cfg.adam_beta2, l->cfg.adam_epsilon,
-                       l->num_steps + 1, l->p3_capable ? l->wpl : nullptr, l->flat, st,
-                       jax ? 1 : 0, nullptr,
-                       l->p3_capable ? l->scales + kScParams : nullptr);
-  if (rc != ACME_OK) return rc;
+  int rc;
+  {
+    // The parameter planes (plane path) are refreshed by the same pass.  t = num_steps + 1
+    // (snt.Adam / optix.adam count this step first).
+    ACME_PROF("adam", st, 0.0, 28.0 * (double)l->logical);
+    rc = launch_adam(l->params, l->grads, l->m, l->v, l->flat, l->cfg.learning_rate,
+                     l->cfg.adam_beta1, l->cfg.adam_beta2, l->cfg.adam_epsilon, l->num_steps + 1,
+                     l->p3_capable ? l->wpl : nullptr, l->flat, st, jax ? 1 : 0, nullptr,
+                     l->p3_capable ? l->scales + kScParams : nullptr);
+    if (rc != ACME_OK) return rc;
+  }
   if (copy) {
     ACME_PROF("target_copy", st, 0.0, 8.0 * (double)l->logical);
     ACME_HIP_TRY(hipMemcpyAsync(l->target, l->params, l->flat * sizeof(float),
@@ -1100,11 +1107,20 @@ static int apply_impl(acme_dqn* l, bool copy, hipStream_t st) {
                                   hipMemcpyDeviceToDevice, st));
   }
   if (l->p3_capable) {
-    // Next step's scales from this step's maxima; the target planes copied from the
-    // parameter planes take their scale.
-    ACME_PROF("plane_rescale", st, 0.0, 0.0);
-    rc = launch_plane_rescale(l->scales, kScTransient, kScCount, copy ? kScParams : -1,
-                              copy ? kScTarget : -1, l->overflow, st);
+    // The parameters' maximum every kParamAmaxPeriod steps (Adam moves a parameter by about
+    // lr per step, far inside the 2^8 headroom of its scale); then the next step's scales
+    // from this step's maxima, the target planes copied from the parameter planes taking
+    // their scale.
+    if (l->num_steps % kParamAmaxPeriod == 0) {
+      ACME_PROF("param_amax", st, 0.0, 4.0 * (double)l->flat);
+      if ((rc = launch_param_amax(l->params, l->flat, l->scales + kScParams, st)) != ACME_OK)
+        return rc;
+    }
+    {
+      ACME_PROF("plane_rescale", st, 0.0, 0.0);
+      rc = launch_plane_rescale(l->scales, kScTransient, kScTarget, copy ? kScParams : -1,
+                                copy ? kScTarget : -1, l->overflow, st);
+    }
   }
   return rc;
 }

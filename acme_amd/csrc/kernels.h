@@ -124,7 +124,7 @@ int launch_clip_adam(const ClipAdamArgs& a, hipStream_t st);
 
 // snt.Adam over n (multiple of 4) floats at step t (acme_adam_update); with `planes`
 // non-null the updated parameters are also written as f16 planes (stride pstride) at the
-// scale record psc's w, whose amax the pass raises.
+// scale record psc's w (the record's amax comes from launch_param_amax).
 // optix != 0: optix.adam's rounding order, p + (-lr) * (m_hat / (sqrt(v_hat) + eps)).
 // dev_steps (optional): the step count lives on the device (t = *dev_steps + 1, bias
 // corrections computed by the kernel, the count incremented by a one-thread launch after
@@ -139,9 +139,11 @@ int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float l
 int launch_split_planes(const float* x, int64_t n, uint16_t* planes, int64_t pstride,
                         gemm::PScale* sc, hipStream_t st, int* overflow = nullptr,
                         int keep_scale = 0);
+// max |x| of n floats into the record's amax slots (the parameter planes' next scale).
+int launch_param_amax(const float* x, int64_t n, gemm::PScale* sc, hipStream_t st);
 // End-of-step rescale of a record array (kernels.hip plane_rescale_kernel): records
-// [0, n_transient) transient, [n_transient, n) persistent; copy_to >= 0 took a plane copy of
-// copy_from's latest write.
+// [0, n_transient) transient, [n_transient, n) persistent (rewritten by every Adam pass);
+// copy_to >= n, if >= 0, took a plane copy of copy_from's latest write.
 int launch_plane_rescale(gemm::PScale* recs, int n_transient, int n, int copy_from, int copy_to,
                          int* overflow, hipStream_t st);
 // uint8 frames -> exact f16 (one plane): out[f][e] = f16(frame f byte e) for rows frames

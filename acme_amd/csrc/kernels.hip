@@ -693,7 +693,6 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p,
     bc2 = 1.f - powf(b2, tf);
   }
   const float pw = planes ? psc->w : 0.f;
-  float amx = 0.f;
 #pragma unroll 2
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -719,15 +718,10 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p,
     __builtin_nontemporal_store(mm, reinterpret_cast<f32x4*>(m) + i);
     __builtin_nontemporal_store(vv, reinterpret_cast<f32x4*>(v) + i);
     reinterpret_cast<f32x4*>(p)[i] = pp;
-    if (planes) amx = fmaxf(amx, store_planes4(planes, pstride, i, pp, pw));
-  }
-  if (planes) {  // one amax atomic per block
-    __shared__ float bm[4];
-    amx = gemm::wave_max(amx);
-    if ((threadIdx.x & 63) == 0) bm[threadIdx.x >> 6] = amx;
-    __syncthreads();
-    if (threadIdx.x < 64)
-      gemm::amax_commit(psc, threadIdx.x < 4 ? bm[threadIdx.x] : 0.f);
+    // (No amax here: a block handles about one float4 per thread, so a per-block
+    // reduction and atomic cost as much as the update; 45 -> 58 us measured.  The
+    // parameters' maximum is taken by launch_param_amax every few steps.)
+    if (planes) (void)store_planes4(planes, pstride, i, pp, pw);
   }
 }
 
@@ -795,33 +789,53 @@ __global__ void __launch_bounds__(64) plane_scale_set_kernel(gemm::PScale* __res
   sc->r = sc->wi = sc->rl = ldexpf(1.f, -e);
 }
 
-// End-of-step rescale of n records (one wave each; blockDim.x = 64 n).  Records [0, nt)
-// are transient (written and read within a step: the next step writes and reads at the new
-// scale), [nt, n) persistent (parameter planes, read in the step after the one that wrote
-// them: their r becomes the wi their writer used, then w moves).  copy_to >= 0: record
-// copy_to received a plane copy of record copy_from's latest write (r = its wi).  A record
-// whose amax is 0 keeps its scale.  overflow |= 1 when a write exceeded f16's range
-// (amax w >= 65520) or was not finite.
+// End-of-step rescale of n records (one wave each, and one more for the copy; blockDim.x =
+// 64 (n + 1)).  Records [0, nt) are transient (written and read within a step: the next
+// step writes and reads at the new scale), [nt, n) persistent (parameter planes, rewritten
+// by every Adam pass at w and read in the next step: r becomes the wi their writer used,
+// and w moves when an amax was taken).  copy_to >= 0 (outside [0, n)): record copy_to took
+// a plane copy of record copy_from's latest write (r = its wi).  A transient record whose
+// amax is 0 keeps its scale.  overflow |= 1 when a write exceeded f16's range (amax w >=
+// 65520) or was not finite.  All loads are issued in one round before one barrier, then
+// every store: the kernel sits between two steps on the critical path.
 __global__ void __launch_bounds__(1024) plane_rescale_kernel(gemm::PScale* __restrict__ s, int nt,
                                                              int n, int copy_from, int copy_to,
                                                              int* __restrict__ overflow) {
   const int i = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (threadIdx.x == 0 && copy_to >= 0) s[copy_to].r = s[copy_to].rl = s[copy_from].wi;
+  const int ic = i < n ? i : 0;
+  uint32_t a_bits = s[ic].slot[lane].v;
+  const float w0 = s[ic].w, r0 = s[ic].r, wi0 = s[ic].wi;
+  const float cwi = copy_to >= 0 ? s[copy_from].wi : 0.f;
   __syncthreads();
-  if (i >= n) return;
+  if (i >= n) {
+    if (i == n && lane == 0 && copy_to >= 0) {
+      s[copy_to].r = cwi;
+      s[copy_to].rl = cwi;
+    }
+    return;
+  }
+  s[i].slot[lane].v = 0u;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) a_bits = max(a_bits, (uint32_t)__shfl_xor((int)a_bits, o, 64));
+  if (lane != 0) return;
+  const float a = __builtin_bit_cast(float, a_bits);
+  const bool persistent = i >= nt;
+  const float stored = persistent ? wi0 : r0;  // the read scale of the planes stored now
   gemm::PScale* rec = s + i;
-  const float a = take_amax(rec, lane);
-  if (lane != 0 || a == 0.f) return;
-  if (!(a * rec->w < 65520.f)) atomicOr(overflow, 1);
+  if (a == 0.f) {  // no maximum taken: the scale stays
+    if (persistent) rec->r = rec->rl = stored;
+    else rec->rl = stored;
+    return;
+  }
+  if (!(a * w0 < 65520.f)) atomicOr(overflow, 1);
   const bool finite = a <= 3.0e38f;
-  if (i >= nt) rec->r = rec->wi;
-  rec->rl = rec->r;  // the planes stored now
   const int e = finite ? scale_exp(a) : 0;
-  const float w = finite ? ldexpf(1.f, e) : rec->w * 0x1p-16f;
-  const float wi = finite ? ldexpf(1.f, -e) : rec->wi * 0x1p16f;
+  const float w = finite ? ldexpf(1.f, e) : w0 * 0x1p-16f;
+  const float wi = finite ? ldexpf(1.f, -e) : wi0 * 0x1p16f;
   rec->w = w;
   rec->wi = wi;
-  if (i < nt) rec->r = wi;
+  rec->rl = stored;
+  rec->r = persistent ? stored : wi;
 }
 
 __global__ void __launch_bounds__(256) frames_f16_kernel(const uint8_t* __restrict__ a,
@@ -1167,13 +1181,23 @@ int launch_split_planes(const float* x, int64_t n, uint16_t* planes, int64_t pst
   return ACME_OK;
 }
 
+int launch_param_amax(const float* x, int64_t n, gemm::PScale* sc, hipStream_t st) {
+  ACME_CHECK_ARG(x && sc && n % 4 == 0, "bad amax arguments");
+  const int64_t n4 = n / 4;
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n4, 256 * 8), 1024);
+  amax_kernel<<<std::max(grid, 1u), 256, 0, st>>>(x, n4, sc);
+  ACME_LAUNCH_CHECK();
+  return ACME_OK;
+}
+
 int launch_plane_rescale(gemm::PScale* recs, int n_transient, int n, int copy_from, int copy_to,
                          int* overflow, hipStream_t st) {
-  ACME_CHECK_ARG(recs && overflow && n >= 1 && n <= 16 && n_transient >= 0 && n_transient <= n,
+  ACME_CHECK_ARG(recs && overflow && n >= 1 && n <= 15 && n_transient >= 0 && n_transient <= n,
                  "bad rescale arguments");
-  ACME_CHECK_ARG(copy_to < 16 && copy_from < 16, "bad rescale copy");
-  plane_rescale_kernel<<<1, (unsigned)(64 * n), 0, st>>>(recs, n_transient, n, copy_from, copy_to,
-                                                         overflow);
+  ACME_CHECK_ARG(copy_to < 0 || (copy_to >= n && copy_from >= 0 && copy_from < n),
+                 "bad rescale copy");
+  plane_rescale_kernel<<<1, (unsigned)(64 * (n + 1)), 0, st>>>(recs, n_transient, n, copy_from,
+                                                               copy_to, overflow);
   ACME_LAUNCH_CHECK();
   return ACME_OK;
 }

@@ -167,6 +167,7 @@ constexpr int kP3MaxWgradSplits = 512;
 // Image-resident convolution (gemm_p3i.h): FPB frames per block, WM x WN waves of 32*MT
 // rows; `frames` images.
 using I1F = gemm::ImgGeomPairs<G1>;
+using I2F = gemm::ImgGeom<G2, false>;
 using I3F = gemm::ImgGeom<G3, false>;
 using I3D = gemm::ImgGeom<G3, true>;
 #define P3I_GEMM(name, GI, FPB, BN, WM, WN, MT, prob, frames)                                 \
@@ -209,51 +210,58 @@ int64_t wgrad_slab_floats_p3() {
 
 int forward_p3(const PWeights& w, const Frames& frames, int rows, const PActs& a,
                hipStream_t st, int keep_x1) {
-  // Fused conv1 -> conv2 (gemm_p3c12.h; 81 us vs 34.8 + 50.3 us alone, but one 150-KB
-  // block per CU shares the GPU badly with the other stream): the target forward only
-  // (keep_x1 == 0, on the side stream), measured 0.716 -> 0.713 ms per step; fusing every
-  // forward measured 0.733, the online forward only 0.725.
-  const bool fused = keep_x1 == 0;
-  if (fused) {
+  // Frames [0, nsep) run conv1 then conv2 with x1 in HBM (the backward reads it); frames
+  // [nsep, rows) the fused conv1 -> conv2 kernel (gemm_p3c12.h), whose x1 stays in LDS.
+  // The target forward (keep_x1 == 0, on the side stream) is fused throughout: 0.716 ->
+  // 0.713 ms per step when it was introduced.  The online forward runs unfused: fusing its
+  // o_t rows (x1 kept for the o_tm1 rows only) measured 0.545 -> 0.603 ms per step with
+  // the f16 planes (the fused kernel's one block per CU beside the other stream).
+  const int nsep = keep_x1 == 0 ? 0 : rows;
+  if (nsep < rows) {
+    const int nf = rows - nsep;
+    const Frames fr = frames.rows_from(nsep);
     P3ConvFwd<G1, 1> p1;
-    p1.M = rows * G1::OPIX; p1.N = G1::CO; p1.K = G1::K; p1.k_chunk = G1::K;
-    p1.a_src = frames_src(frames, rows); p1.b_src = src(w.w1, G1::K * G1::CO);
-    p1.bias = w.b1; p1.y = pl(a.x1);
+    p1.M = nf * G1::OPIX; p1.N = G1::CO; p1.K = G1::K; p1.k_chunk = G1::K;
+    p1.a_src = frames_src(fr, nf); p1.b_src = src(w.w1, G1::K * G1::CO);
+    p1.bias = w.b1;
+    p1.y = Planes{a.x1.p + (int64_t)nsep * kX1, a.x1.stride, a.x1.sc};
     P3ConvFwd<G2, gemm::kPlanes> p2;
-    p2.M = rows * G2::OPIX; p2.N = G2::CO; p2.K = G2::K; p2.k_chunk = G2::K;
+    p2.M = nf * G2::OPIX; p2.N = G2::CO; p2.K = G2::K; p2.k_chunk = G2::K;
     p2.a_src = src(a.x1, (int64_t)rows * kX1); p2.b_src = src(w.w2, G2::K * G2::CO);
-    p2.bias = w.b2; p2.y = pl(a.x2);
+    p2.bias = w.b2;
+    p2.y = Planes{a.x2.p + (int64_t)nsep * kFlat, a.x2.stride, a.x2.sc};
     const double fl = 2.0 * p1.M * p1.N * (double)p1.K + 2.0 * p2.M * p2.N * (double)p2.K;
     ACME_PROF_PEAK("conv12_fwd", st, fl, 0.0, gemm::p3_peak_tflops<decltype(p2)>());
-    hipError_t e = gemm::launch_gemm_p3c12(p1, p2, rows, keep_x1 < 0 ? rows : keep_x1, st);
+    hipError_t e = gemm::launch_gemm_p3c12(p1, p2, nf, 0, st);
     if (e != hipSuccess) return (set_error("gemm launch failed: %s", hipGetErrorString(e)), ACME_ERR_HIP);
-  } else {
+  }
+  if (nsep > 0) {
     P3ConvFwd<G1, 1> p;
-    p.M = rows * G1::OPIX; p.N = G1::CO; p.K = G1::K; p.k_chunk = G1::K;
-    p.a_src = frames_src(frames, rows); p.b_src = src(w.w1, G1::K * G1::CO);
+    p.M = nsep * G1::OPIX; p.N = G1::CO; p.K = G1::K; p.k_chunk = G1::K;
+    p.a_src = frames_src(frames, nsep); p.b_src = src(w.w1, G1::K * G1::CO);
     p.bias = w.b1; p.y = pl(a.x1);
     // Image-resident frames (gemm_p3i.h pixel pairs): 39.6 -> 33.7 us vs the best im2col
     // tiling.
-    P3I_GEMM("conv1_fwd", I1F, 1, 32, 7, 1, 2, p, rows);
+    P3I_GEMM("conv1_fwd", I1F, 1, 32, 7, 1, 2, p, nsep);
   }
-  if (!fused) {
+  if (nsep > 0) {
     P3ConvFwd<G2, gemm::kPlanes> p;
-    p.M = rows * G2::OPIX; p.N = G2::CO; p.K = G2::K; p.k_chunk = G2::K;
-    p.a_src = src(a.x1, (int64_t)rows * kX1); p.b_src = src(w.w2, G2::K * G2::CO);
+    p.M = nsep * G2::OPIX; p.N = G2::CO; p.K = G2::K; p.k_chunk = G2::K;
+    p.a_src = src(a.x1, (int64_t)nsep * kX1); p.b_src = src(w.w2, G2::K * G2::CO);
     p.bias = w.b2; p.y = pl(a.x2);
-    // Producer / consumer waves (gemm_p3ws_kernel).  Alone this launch is slower (62 -> 69 us:
-    // one 512-thread block per CU instead of two 256-thread ones), but beside the target
-    // forward on the other stream the step is faster: 0.723 -> 0.700 ms (3 alternating runs
-    // each, one box).  tune WSN=1: the single-role kernel (same bits; tests).
-    if (tune_variant("WSN") == 1) P3_GEMM("conv2_fwd", 128, 64, 2, 2, 32, p, 1);
-    else P3WS_GEMM("conv2_fwd", 128, 64, 2, 2, p, 1);
+    // Image-resident x1 (gemm_p3i.h; two frames, 8 x 2 waves per block): with two f16
+    // planes a frame's x1 image is 56 KB, so two frames and the weight ring fit one CU.
+    // Step 0.573 -> 0.551 ms against the producer / consumer im2col kernel (two alternating
+    // runs each, one box; one frame per block: 0.571).
+    P3I_GEMM("conv2_fwd", I2F, 2, 64, 8, 2, 1, p, nsep);
   }
   {
     P3ConvFwd<G3, gemm::kPlanes> p;
     p.M = rows * G3::OPIX; p.N = G3::CO; p.K = G3::K; p.k_chunk = G3::K;
     p.a_src = src(a.x2, (int64_t)rows * kFlat); p.b_src = src(w.w3, G3::K * G3::CO);
     p.bias = w.b3; p.y = pl(a.x3);
-    // Image-resident, 4 x 2 waves (measured 50.1 -> 43.5 us vs the 128x64 im2col engine).
+    // Image-resident, 4 x 2 waves (measured 50.1 -> 43.5 us vs the 128x64 im2col engine;
+    // two frames per block measured slower on the step, 0.550 -> 0.568-0.618 ms).
     P3I_GEMM("conv3_fwd", I3F, 1, 64, 4, 2, 1, p, rows);
   }
   return ACME_OK;
