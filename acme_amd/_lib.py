@@ -156,6 +156,13 @@ _SIGS = {
     "acme_dqn_bind": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "acme_dqn_params_changed": (c_i32, [c_vp]),
     "acme_dqn_plane_overflow": (c_i32, [c_vp, ctypes.POINTER(c_i32), c_i32]),
+    "acme_dqn_dense_grads_ready": (c_i32, [c_vp, c_vp]),
+    "acme_dqn_dp_init": (c_i32, [c_vp, c_vp, c_i32]),
+    "acme_dqn_dp_step": (c_i32, [c_vp, ctypes.POINTER(TransitionBatch), ctypes.POINTER(DQNOutputs),
+                                 c_vp]),
+    "acme_nccl_get_unique_id": (c_i32, [c_vp]),
+    "acme_nccl_comm_init": (c_i32, [c_vp, c_i32, c_i32, ctypes.POINTER(c_vp)]),
+    "acme_nccl_comm_destroy": (c_i32, [c_vp]),
     "acme_dqn_scale_state": (c_i32, [c_vp, c_vp, c_i32, ctypes.POINTER(c_i32)]),
     "acme_dqn_set_scale_state": (c_i32, [c_vp, c_vp, c_i32]),
     "acme_dqn_forward_backward": (c_i32, [c_vp, ctypes.POINTER(TransitionBatch),

@@ -72,9 +72,26 @@ def stack_steps(steps: Sequence[Step]):
     return tree.map_structure(lambda *xs: np.stack([np.asarray(x) for x in xs]), *steps)
 
 
-def calculate_priorities(priority_fns: PriorityFnMapping, steps: Sequence[Step]) -> Dict[str, float]:
-    stacked = PriorityFnInput(*stack_steps(steps))
-    return {table: fn(stacked) for table, fn in priority_fns.items()}
+def uniform_priority(_) -> float:
+    """The default priority function (adders/reverb/base.py:91-92: lambda x: 1.)."""
+    return 1.
+
+
+def calculate_priorities(priority_fns: PriorityFnMapping, steps) -> Dict[str, float]:
+    """`steps`: the window, or a callable returning it.  The stacked window
+    (acme/adders/reverb/utils.py:97-103) is only built when some function reads it:
+    stacking an Atari window copies its frames (112 KB per transition) to feed the default
+    uniform_priority, which ignores its input."""
+    stacked = None
+    out = {}
+    for table, fn in priority_fns.items():
+        if fn is uniform_priority:
+            out[table] = 1.
+            continue
+        if stacked is None:
+            stacked = PriorityFnInput(*stack_steps(steps() if callable(steps) else steps))
+        out[table] = fn(stacked)
+    return out
 
 
 class ReverbAdder(base.Adder):
@@ -85,7 +102,7 @@ class ReverbAdder(base.Adder):
                  priority_fns: Optional[PriorityFnMapping] = None):
         self._client = client
         self._priority_fns = (dict(priority_fns) if priority_fns
-                              else {DEFAULT_PRIORITY_TABLE: lambda _: 1.0})
+                              else {DEFAULT_PRIORITY_TABLE: uniform_priority})
         self._max_sequence_length = max_sequence_length
         self._writer_kwargs = dict(delta_encoded=delta_encoded, chunk_length=chunk_length)
         self._active_writer = None
@@ -136,7 +153,8 @@ class ReverbAdder(base.Adder):
             self._write_last()
             self.reset()
 
-    def _emit(self, num_steps: int, steps: Sequence[Step]):
+    def _emit(self, num_steps: int, steps):
+        """steps: the window, or a callable building it (only priority functions read it)."""
         for table, priority in calculate_priorities(self._priority_fns, steps).items():
             self._writer.create_item(table=table, num_timesteps=num_steps, priority=priority)
 

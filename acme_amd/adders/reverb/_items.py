@@ -48,9 +48,9 @@ class NStepTransitionAdder(ReverbAdder):
 
     def _write(self):
         item = self._transition()
-        window = list(self._buffer) + [final_step_like(self._buffer[0], self._next_observation)]
+        buf, nxt = list(self._buffer), self._next_observation
         self._writer.append(item)
-        self._emit(1, window)
+        self._emit(1, lambda: buf + [final_step_like(buf[0], nxt)])
 
     def _write_last(self):
         # Drain: emit the shrinking windows that end at the final observation.

@@ -80,6 +80,8 @@ class DQNLearner(core.Learner, core.Saveable):
         # update of the global batch (the mean-then-apply order of the reference's only
         # data-parallel learner, acme/agents/tf/crr/recurrent_learning.py:346-358).
         self._dist = None
+        self._staged = False       # bench: the staged data-parallel path on one process
+        self._comm_stream = None
         if data_parallel:
             import torch.distributed as dist
             if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
@@ -116,34 +118,10 @@ class DQNLearner(core.Learner, core.Saveable):
         if fb is not None:
             fb = (fb[:2 * B] if obs_dt == torch.uint8 and fb.shape[0] >= 2 * B
                   and fb.shape[1] == self._obs_flat else None)
-        if self._dist is None:
+        if self._dist is None and not self._staged:
             self._native.step(*batch, obs_f16=fb)
         else:
-            # Gradient all-reduce in two buckets overlapped with the backward pass: the dense
-            # layers' gradients (the buffer's tail, ~99% of the bytes) are reduced on the
-            # collective stream while the torso backward runs on the compute stream.
-            dist = self._dist
-            n = self._native
-            # The IS normaliser's all-reduce (8 bytes) runs beside the forwards: only the
-            # loss (stage 3) reads it.
-            n.batch_min_probability(batch[5], self._gmin)
-            work_min = dist.all_reduce(self._gmin, op=dist.ReduceOp.MIN, async_op=True)
-            n.forward_backward_stage(2, *batch, mean_over=self._B, obs_f16=fb)
-            work_min.wait()
-            n.forward_backward_stage(3, *batch, global_min_probability=self._gmin,
-                                     mean_over=self._B, obs_f16=fb)
-            split = self._grad_split
-            tail, head = n.grads[split:], n.grads[:split]
-            op = self._avg_op if self._avg_op is not None else dist.ReduceOp.SUM
-            work = dist.all_reduce(tail, op=op, async_op=True)
-            n.forward_backward_stage(1, *batch, global_min_probability=self._gmin,
-                                     mean_over=self._B)
-            if split > 0:
-                dist.all_reduce(head, op=op)
-            work.wait()
-            if self._avg_op is None:  # gloo: sum, then scale
-                n.grads.mul_(1.0 / dist.get_world_size())
-            n.apply()
+            self._staged_step(batch, fb)
         if self._replay_client is not None:
             self._replay_client.update_priorities(table=adders.DEFAULT_PRIORITY_TABLE,
                                                   keys=keys,
@@ -164,6 +142,49 @@ class DQNLearner(core.Learner, core.Saveable):
         result = {"loss": loss} if self._log_loss else {}
         result.update(self._counter.increment(steps=1, walltime=elapsed))
         self._logger.write(result)
+
+    def _staged_step(self, batch, fb):
+        """The data-parallel step: the learner's stages with the collectives between them.
+        Gradient all-reduce in two buckets overlapped with the backward pass: the dense
+        layers' gradients (the buffer's tail, ~99% of the bytes) are reduced on a collective
+        stream as soon as the learner's second stream has produced them, while the torso
+        backward runs on the compute stream.  Without a process group (bench's
+        dp_staged_ms_per_step: the N = 1 point of a scaling curve) the same stages run with
+        the collectives left out."""
+        dist = self._dist
+        n = self._native
+        gmin = None
+        if dist is not None:
+            # The IS normaliser's all-reduce (8 bytes) runs beside the forwards: only the
+            # loss (stage 4) reads it.
+            gmin = self._gmin
+            n.batch_min_probability(batch[5], gmin)
+            work_min = dist.all_reduce(gmin, op=dist.ReduceOp.MIN, async_op=True)
+        n.forward_backward_stage(2, *batch, mean_over=self._B, obs_f16=fb)
+        if dist is not None:
+            work_min.wait()
+        n.forward_backward_stage(4, *batch, global_min_probability=gmin, mean_over=self._B,
+                                 obs_f16=fb)
+        if dist is not None:
+            split = self._grad_split
+            tail, head = n.grads[split:], n.grads[:split]
+            op = self._avg_op if self._avg_op is not None else dist.ReduceOp.SUM
+            if self._comm_stream is None:
+                self._comm_stream = torch.cuda.Stream(device=n.device)
+            cs = self._comm_stream
+            cs.wait_stream(torch.cuda.current_stream(n.device))
+            n.dense_grads_ready(cs)
+            with torch.cuda.stream(cs):
+                work = dist.all_reduce(tail, op=op, async_op=True)
+        n.forward_backward_stage(1, *batch, global_min_probability=gmin, mean_over=self._B)
+        if dist is not None:
+            if split > 0:
+                dist.all_reduce(head, op=op)
+            work.wait()
+            torch.cuda.current_stream(n.device).wait_stream(cs)
+            if self._avg_op is None:  # gloo: sum, then scale
+                n.grads.mul_(1.0 / dist.get_world_size())
+        n.apply()
 
     # ------------------------------------------------------------------ variables
     def q_values(self, observations, use_target: bool = False) -> np.ndarray:

@@ -30,6 +30,7 @@
 #include "gemm_x6.h"
 #include "kernels.h"
 #include "profiler.h"
+#include "rccl_dyn.h"
 #include "torso.h"
 
 using namespace acme;
@@ -109,6 +110,19 @@ struct acme_dqn {
   // by the backward; forward_backward_stage leaves its arguments here.
   LossArgs pending_la{};
   bool loss_pending = false;
+  // The dense layers' gradients (grads[grad_split:]) of the last stage 3 / 4 are complete
+  // at dense_ev: the side stream's event when their launches ran there, else ev_dense,
+  // recorded on the caller's stream.
+  hipEvent_t ev_dense = nullptr;
+  hipEvent_t dense_ev = nullptr;
+  bool dense_on_side = false;
+  // Data parallelism over a caller-owned RCCL communicator (acme_dqn_dp_*): the collective
+  // stream, its events, the global IS normaliser's minimum probability.
+  void* dp_comm = nullptr;
+  int dp_world = 0;
+  hipStream_t dp_stream = nullptr;
+  hipEvent_t dp_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  double* dp_gmin = nullptr;
   double* loss_part = nullptr;  // per-block loss partials of the fused loss + head dZ
 };
 
@@ -483,6 +497,7 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st_main,
       else ACME_P3WS_GEMM("fc_dgrad", 128, 128, 2, 2, 32, p, 1, true);
     }
     if (fork && join_dense) ACME_HIP_TRY(hipStreamWaitEvent(st_main, l->ev[3], 0));
+    l->dense_on_side = fork;
     return ACME_OK;
   }
   {  // FC weight + bias grad: [7744, 1024] = x3^T dZh (reduction over the batch).
@@ -700,6 +715,8 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
     }
     l->slab_floats = 1;
   }
+  if (hipEventCreateWithFlags(&l->ev_dense, hipEventDisableTiming) != hipSuccess)
+    return fail((set_error("event creation failed"), ACME_ERR_HIP));
   if ((rc = dev_alloc(l, &l->q_on, (int64_t)2 * B * A)) ||
       (rc = dev_alloc(l, &l->q_tg, (int64_t)B * A)) ||
       (rc = dev_alloc(l, &l->slab, l->slab_floats)) ||
@@ -720,6 +737,10 @@ int acme_dqn_destroy(acme_dqn* l) {
   for (auto& e : l->ev)
     if (e) (void)hipEventDestroy(e);
   if (l->side) (void)hipStreamDestroy(l->side);
+  if (l->ev_dense) (void)hipEventDestroy(l->ev_dense);
+  for (auto& e : l->dp_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (l->dp_stream) (void)hipStreamDestroy(l->dp_stream);
   delete l;
   return ACME_OK;
 }
@@ -923,7 +944,7 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
                                   const acme_dqn_outputs* out, int32_t stage, void* stream,
                                   bool join_dense) {
   ACME_CHECK_ARG(l && batch && l->params, "null argument or unbound learner");
-  ACME_CHECK_ARG(stage >= 0 && stage <= 3, "stage must be 0, 1, 2 or 3");
+  ACME_CHECK_ARG(stage >= 0 && stage <= 4, "stage must be 0, 1, 2, 3 or 4");
   ACME_CHECK_ARG(batch->o_tm1 && batch->a_tm1 && batch->r_t && batch->d_t && batch->o_t &&
                      batch->probabilities,
                  "transition batch has null fields");
@@ -963,10 +984,11 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
   int rc;
   // Stage 0 = stage 2 (the forwards) + stage 3 (loss and the dense backward); a
   // data-parallel rank splits them to run the IS-normaliser all-reduce beside the forwards.
-  if (stage == 3) {
-    ACME_CHECK_ARG(l->fwd_batch == (int64_t)B, "stage 3 needs the stage-2 forward of this batch");
+  if (stage == 3 || stage == 4) {
+    ACME_CHECK_ARG(l->fwd_batch == (int64_t)B, "stage %d needs the stage-2 forward of this batch",
+                   stage);
     l->fwd_batch = 0;
-    return loss_and_dense_backward(l, batch, out, st, join_dense);
+    return loss_and_dense_backward(l, batch, out, st, join_dense && stage == 3);
   }
   // Forward: online on [o_tm1; o_t] (q_tm1 rows 0..B-1, q_t_selector rows B..2B-1),
   // target on o_t (q_t_value).
@@ -1067,8 +1089,17 @@ static int loss_and_dense_backward(acme_dqn* l, const acme_transition_batch* bat
   if (out && out->q_tm1)
     ACME_HIP_TRY(hipMemcpyAsync(out->q_tm1, l->q_on, (size_t)B * A * sizeof(float),
                                 hipMemcpyDeviceToDevice, st));
-  return nature ? nature_backward(l, batch->o_tm1, B, st, join_dense)
-                : mlp_backward(l, batch->o_tm1, B, st);
+  l->dense_on_side = false;
+  rc = nature ? nature_backward(l, batch->o_tm1, B, st, join_dense)
+              : mlp_backward(l, batch->o_tm1, B, st);
+  if (rc != ACME_OK) return rc;
+  if (l->dense_on_side) {
+    l->dense_ev = l->ev[3];
+  } else {
+    ACME_HIP_TRY(hipEventRecord(l->ev_dense, st));
+    l->dense_ev = l->ev_dense;
+  }
+  return ACME_OK;
 }
 
 int acme_dqn_forward_backward(acme_dqn* l, const acme_transition_batch* batch,
@@ -1146,6 +1177,82 @@ static int step_impl(acme_dqn* l, const acme_transition_batch* batch, const acme
   if (rc == ACME_OK) rc = forward_backward_stage(l, batch, out, 1, st, false);
   if (rc == ACME_OK) rc = apply_impl(l, copy, st);
   return rc;
+}
+
+int acme_dqn_dense_grads_ready(acme_dqn* l, void* stream) {
+  ACME_CHECK_ARG(l && l->dense_ev, "no stage 3 / 4 has run");
+  ACME_HIP_TRY(hipStreamWaitEvent(as_stream(stream), l->dense_ev, 0));
+  return ACME_OK;
+}
+
+// ------------------------------------------------------------------ data parallelism
+int acme_dqn_dp_init(acme_dqn* l, void* nccl_comm, int32_t world_size) {
+  ACME_CHECK_ARG(l && nccl_comm && world_size >= 1, "bad data-parallel arguments");
+  if (!acme::rccl::api()) return ACME_ERR_HIP;
+  if (!l->dp_stream) {
+    ACME_HIP_TRY(hipStreamCreateWithFlags(&l->dp_stream, hipStreamNonBlocking));
+    for (auto& e : l->dp_ev) ACME_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    int rc = dev_alloc(l, &l->dp_gmin, 1);
+    if (rc != ACME_OK) return rc;
+  }
+  l->dp_comm = nccl_comm;
+  l->dp_world = world_size;
+  return ACME_OK;
+}
+
+// One data-parallel step (the order of DQNLearner's data_parallel path, itself that of the
+// reference's only data-parallel learner, acme/agents/tf/crr/recurrent_learning.py:346-358):
+// the batch minimum probability is all-reduced (MIN) on the collective stream beside the
+// forwards; the loss and dense backward read the global minimum; the dense gradients
+// (99% of the bytes) are all-reduced (AVG) beside the torso backward, as soon as the side
+// stream has produced them; then the torso bucket; then Adam on the caller's stream.
+int acme_dqn_dp_step(acme_dqn* l, const acme_transition_batch* batch, const acme_dqn_outputs* out,
+                     void* stream) {
+  ACME_CHECK_ARG(l && batch && l->params, "null argument or unbound learner");
+  ACME_CHECK_ARG(l->dp_comm, "acme_dqn_dp_init must be called first");
+  const acme::rccl::Api* r = acme::rccl::api();
+  if (!r) return ACME_ERR_HIP;
+  hipStream_t st = as_stream(stream), cs = l->dp_stream;
+  ncclComm_t comm = static_cast<ncclComm_t>(l->dp_comm);
+  auto nccl = [&](ncclResult_t e, const char* what) {
+    if (e == ncclSuccess) return ACME_OK;
+    set_error("%s: %s", what, r->GetErrorString(e));
+    return ACME_ERR_HIP;
+  };
+  int rc = acme_min_f64(batch->probabilities, batch->batch, l->dp_gmin, st);
+  if (rc != ACME_OK) return rc;
+  ACME_HIP_TRY(hipEventRecord(l->dp_ev[0], st));
+  ACME_HIP_TRY(hipStreamWaitEvent(cs, l->dp_ev[0], 0));
+  if ((rc = nccl(r->AllReduce(l->dp_gmin, l->dp_gmin, 1, ncclFloat64, ncclMin, comm, cs),
+                 "all-reduce (min probability)")))
+    return rc;
+  ACME_HIP_TRY(hipEventRecord(l->dp_ev[1], cs));
+  acme_transition_batch b = *batch;
+  b.global_min_probability = l->dp_gmin;
+  if ((rc = forward_backward_stage(l, &b, out, 2, st, false))) return rc;
+  ACME_HIP_TRY(hipStreamWaitEvent(st, l->dp_ev[1], 0));
+  if ((rc = forward_backward_stage(l, &b, out, 4, st, false))) return rc;
+  int64_t split = 0;
+  if ((rc = acme_dqn_grad_split(l, &split))) return rc;
+  ACME_HIP_TRY(hipStreamWaitEvent(cs, l->dense_ev, 0));
+  const ncclRedOp_t avg = static_cast<ncclRedOp_t>(ncclAvg);
+  if ((rc = nccl(r->AllReduce(l->grads + split, l->grads + split, (size_t)(l->flat - split),
+                              ncclFloat32, avg, comm, cs),
+                 "all-reduce (dense gradients)")))
+    return rc;
+  if ((rc = forward_backward_stage(l, &b, out, 1, st, false))) return rc;
+  if (split > 0) {
+    ACME_HIP_TRY(hipEventRecord(l->dp_ev[2], st));
+    ACME_HIP_TRY(hipStreamWaitEvent(cs, l->dp_ev[2], 0));
+    if ((rc = nccl(r->AllReduce(l->grads, l->grads, (size_t)split, ncclFloat32, avg, comm, cs),
+                   "all-reduce (torso gradients)")))
+      return rc;
+  }
+  ACME_HIP_TRY(hipEventRecord(l->dp_ev[3], cs));
+  ACME_HIP_TRY(hipStreamWaitEvent(st, l->dp_ev[3], 0));
+  if ((rc = apply_impl(l, copies_target(l), st))) return rc;
+  l->num_steps += 1;
+  return ACME_OK;
 }
 
 int acme_dqn_step(acme_dqn* l, const acme_transition_batch* batch, const acme_dqn_outputs* out,

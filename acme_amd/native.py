@@ -447,14 +447,32 @@ class NativeDQN:
                                q_tm1=None, stream=None, mean_over=None, obs_f16=None):
         """Stage 0: forwards, loss, head/dense backward (grads[grad_split:]); stage 1: torso
         backward (grads[:grad_split]).  Stage 0 may be issued as stage 2 (forwards) then
-        stage 3 (loss and dense backward; global_min_probability is read from here on).  mean_over: the batch mean's denominator (default
-        the batch; a data-parallel share passes the nominal per-rank batch)."""
+        stage 3 (loss and dense backward; global_min_probability is read from here on) or
+        stage 4 (stage 3 without ordering the stream after the dense gradients: see
+        dense_grads_ready).  mean_over: the batch mean's denominator (default the batch; a
+        data-parallel share passes the nominal per-rank batch)."""
         tb = self._batch(*batch, global_min_probability=global_min_probability,
                          mean_over=mean_over, obs_f16=obs_f16)
         out = self._outputs(q_tm1)
         check(lib().acme_dqn_forward_backward_stage(self._h, ctypes.byref(tb), ctypes.byref(out),
                                                     int(stage), stream_ptr(stream)),
               f"dqn forward_backward stage {stage}")
+
+    def dense_grads_ready(self, stream=None) -> None:
+        """Orders `stream` (default: the current one) after the dense gradients
+        grads[grad_split:] of the last stage 3 / 4."""
+        check(lib().acme_dqn_dense_grads_ready(self._h, stream_ptr(stream)), "dense grads ready")
+
+    def dp_init(self, comm, world_size: int) -> None:
+        """Binds a caller-owned RCCL communicator (ncclComm_t) for dp_step."""
+        check(lib().acme_dqn_dp_init(self._h, ctypes.c_void_p(comm), int(world_size)), "dp init")
+
+    def dp_step(self, *batch, mean_over=None, q_tm1=None, stream=None, obs_f16=None):
+        """One data-parallel step over the bound communicator (acme_dqn_dp_step)."""
+        tb = self._batch(*batch, mean_over=mean_over, obs_f16=obs_f16)
+        out = self._outputs(q_tm1)
+        check(lib().acme_dqn_dp_step(self._h, ctypes.byref(tb), ctypes.byref(out),
+                                     stream_ptr(stream)), "dqn dp step")
 
     @property
     def grad_split(self) -> int:
@@ -482,6 +500,26 @@ class NativeDQN:
         check(lib().acme_dqn_q_values(self._h, ptr(obs.contiguous()), B, 1 if use_target else 0,
                                       ptr(q), stream_ptr(stream)), "dqn q_values")
         return q
+
+
+def nccl_unique_id() -> bytes:
+    """A fresh RCCL unique id (128 bytes) for nccl_comm_init on every rank."""
+    buf = (ctypes.c_uint8 * 128)()
+    check(lib().acme_nccl_get_unique_id(buf), "nccl unique id")
+    return bytes(buf)
+
+
+def nccl_comm_init(uid: bytes, world_size: int, rank: int) -> int:
+    """An RCCL communicator handle (ncclComm_t as an int) for rank of world_size."""
+    buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+    comm = ctypes.c_void_p()
+    check(lib().acme_nccl_comm_init(buf, int(world_size), int(rank), ctypes.byref(comm)),
+          "nccl comm init")
+    return int(comm.value)
+
+
+def nccl_comm_destroy(comm: int) -> None:
+    check(lib().acme_nccl_comm_destroy(ctypes.c_void_p(comm)), "nccl comm destroy")
 
 
 class NativeD4PG:

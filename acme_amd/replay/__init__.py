@@ -121,9 +121,13 @@ class Table:
         self._native = None
         self._seed = int(seed)
         self._device = device
-        self._flush_every = int(flush_every)
-        self._pending: List[List[np.ndarray]] = []
-        self._pending_prio: List[float] = []
+        self._flush_every = max(1, int(flush_every))
+        # Items accepted but not yet committed: row i of every field's host buffer (packed
+        # at insert, one copy per field), copied to the native table's pinned staging chunk
+        # in one block per field at flush.
+        self._pend: Optional[List[np.ndarray]] = None
+        self._pend_prio = np.zeros(self._flush_every, np.float64)
+        self._fill = 0
         self._mu = threading.RLock()
         self._cv = threading.Condition(self._mu)
         self._draws = 0
@@ -144,6 +148,10 @@ class Table:
         from acme_amd.native import NativeReplay
         self._structure = structure
         self._fields = fields
+        self._flat_tuple = (isinstance(structure, tuple) and not hasattr(structure, "_fields")
+                            and len(structure) == len(fields))
+        self._pend = [np.zeros((self._flush_every, f.row_bytes), np.uint8) for f in fields]
+        self._fill = 0
         self._native = NativeReplay(self.max_size, [f.row_bytes for f in fields],
                                     prioritized=self._prioritized, priority_exponent=self._alpha,
                                     seed=self._seed, device=self._device)
@@ -159,7 +167,7 @@ class Table:
     def size(self) -> int:
         with self._mu:
             n = self._native.size() if self._native is not None else 0
-            return min(self.max_size, n + len(self._pending))
+            return min(self.max_size, n + self._fill)
 
     def can_sample(self, num_samples: int = 1) -> bool:
         return self.size() >= max(self._min_size, 1)
@@ -169,21 +177,25 @@ class Table:
         with self._mu:
             if self._fields is None:
                 self._init_layout(item, _layout_from_item(item))
-            leaves = tree.flatten(item)
+            # A flat tuple item (the transition adder's) is its own leaf list.
+            leaves = (item if self._flat_tuple and type(item) is tuple
+                      and len(item) == len(self._fields) else tree.flatten(item))
             if len(leaves) != len(self._fields):
                 raise ValueError(f"item has {len(leaves)} leaves, table expects "
                                  f"{len(self._fields)}")
             self._maybe_sequence_layout(leaves)
-            row = []
-            for leaf, f in zip(leaves, self._fields):
-                a = np.asarray(leaf, dtype=f.dtype)
+            r = self._fill
+            for leaf, f, buf in zip(leaves, self._fields, self._pend):
+                a = leaf if type(leaf) is np.ndarray and leaf.dtype == f.dtype else \
+                    np.asarray(leaf, dtype=f.dtype)
                 if a.shape != f.shape:
                     raise ValueError(f"leaf shape {a.shape} does not match table signature "
                                      f"{f.shape}")
-                row.append(a)
-            self._pending.append(row)
-            self._pending_prio.append(float(priority))
-            if len(self._pending) >= self._flush_every:
+                # One copy into the row (the bytes, in C order); the row padding stays 0.
+                buf[r, :f.nbytes].view(f.dtype).reshape(f.shape)[...] = a
+            self._pend_prio[r] = priority
+            self._fill = r + 1
+            if self._fill >= self._flush_every:
                 self.flush()
             self._cv.notify_all()
 
@@ -191,7 +203,7 @@ class Table:
         """Sequence items (SequenceAdder, R2D2): Reverb signatures are per timestep
         (adders/reverb/base.py:179-206) and the table stores T-step items.  The first item
         whose every leaf is [T] + the signature's shape fixes the stored layout to T steps."""
-        if self._seq_len is not None or self._pending or self._native.size() > 0:
+        if self._seq_len is not None or self._fill or self._native.size() > 0:
             return
         shapes = [np.shape(x) for x in leaves]
         if all(s == f.shape for s, f in zip(shapes, self._fields)):
@@ -226,27 +238,17 @@ class Table:
             torch.cuda.current_stream(self._native.device).wait_event(ev)
 
     def flush(self) -> None:
-        """Writes the pending items straight into the table's pinned staging chunks and
-        commits them: hipMemcpyAsync on the table's side stream, no host wait.  The native
-        table orders the copies after every stream that has read it (a queued prefetch
-        gather never sees a slot overwritten under it) and every later sample after them."""
+        """Commits the pending rows: one native call packs each field's block into the
+        table's pinned staging chunk (a C memcpy outside the GIL) and issues hipMemcpyAsync
+        on the table's side stream, no host wait.  The native table orders the copies after
+        every stream that has read it (a queued prefetch gather never sees a slot
+        overwritten under it) and every later sample after them."""
         with self._mu:
-            if not self._pending:
+            n = self._fill
+            if not n:
                 return
-            nat = self._native
-            cap = nat.stage_capacity()
-            prio = np.asarray(self._pending_prio, np.float64)
-            for s in range(0, len(self._pending), cap):
-                rows = self._pending[s:s + cap]
-                bufs = nat.stage(len(rows))
-                for i, f in enumerate(self._fields):
-                    b = bufs[i]
-                    for r, row in enumerate(rows):
-                        b[r, :f.nbytes] = np.ascontiguousarray(row[i]).reshape(-1).view(np.uint8)
-                    if f.row_bytes > f.nbytes:
-                        b[:, f.nbytes:] = 0
-                nat.commit(len(rows), prio[s:s + cap])
-            self._pending, self._pending_prio = [], []
+            self._native.insert([p[:n] for p in self._pend], self._pend_prio[:n])
+            self._fill = 0
 
     # -- checkpointing (optional replay state; core.Saveable interface)
     def save(self) -> Dict[str, Any]:
@@ -262,7 +264,7 @@ class Table:
 
     def restore(self, state: Dict[str, Any]) -> None:
         with self._mu:
-            self._pending, self._pending_prio = [], []
+            self._fill = 0
             if "keys" in state:
                 if self._native is None:
                     raise ValueError("restore needs the table layout (construct the table "

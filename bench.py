@@ -222,6 +222,7 @@ def setup_dqn(args, world, rank, dev):
                 "sampler": "prioritized(alpha=0.6), IS beta=0.2", "prefetch_size": args.prefetch,
                 "parallelism": f"dp{world}"})
     meta["_table"] = table
+    meta["_set_staged"] = lambda on: setattr(learner, "_staged", bool(on))
     return (learner.step, B, meta, lambda: float(learner.native.loss.item()),
             lambda: cpu_baseline(B, A, args.cpu_baseline_seconds))
 
@@ -650,6 +651,21 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    # The N = 1 point of a scaling curve: a data-parallel rank runs the learner's stages with
+    # the collectives between them (DQNLearner._staged_step); the same stages on one GPU with
+    # the collectives left out, timed like the line above (separately, after it).
+    staged_ms = None
+    if "_set_staged" in meta and world == 1 and args.steps > 0:
+        meta["_set_staged"](True)
+        for i in range(min(args.warmup, 10)):
+            step()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            step()
+        torch.cuda.synchronize(dev)
+        staged_ms = 1e3 * (time.perf_counter() - t0) / args.steps
+        meta["_set_staged"](False)
     # Per-kernel durations come from a separate pass with the in-library section profiler
     # (HIP event pairs on the launch stream), so its event records stay out of the timed
     # region above.
@@ -727,6 +743,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "gpu_busy_ms_per_step": None if busy is None else round(busy, 4),
+            "dp_staged_ms_per_step": None if staged_ms is None else round(staged_ms, 4),
             "kernels": sections,
         }
         print(json.dumps(out))

@@ -324,11 +324,31 @@ int acme_dqn_forward_backward(acme_dqn* l, const acme_transition_batch* batch,
  * all-reduce with the rest of the backward pass: stage 0 = forwards, loss, head and
  * dense-layer backward (writes grads[grad_split:]); stage 1 = torso backward (writes
  * grads[:grad_split]; a no-op for MLP networks, whose grad_split is 0).  Stage 0 may itself
- * be issued as stage 2 (the forwards) then stage 3 (loss, head and dense backward, the same
- * batch), so that batch->global_min_probability is only read from stage 3 on. */
+ * be issued as stage 2 (the forwards) then stage 3 or 4 (loss, head and dense backward, the
+ * same batch), so that batch->global_min_probability is only read from stage 3 on. */
 int acme_dqn_forward_backward_stage(acme_dqn* l, const acme_transition_batch* batch,
                                     const acme_dqn_outputs* out, int32_t stage, void* stream);
 int acme_dqn_grad_split(const acme_dqn* l, int64_t* split);
+/* Stage 4 (acme_dqn_forward_backward_stage) is stage 3 without ordering the caller's stream
+ * after the dense gradients grads[grad_split:] (computed beside it on the learner's second
+ * stream); acme_dqn_dense_grads_ready makes `stream` wait for them, e.g. a collective
+ * stream that all-reduces them while the caller's stream runs stage 1. */
+int acme_dqn_dense_grads_ready(acme_dqn* l, void* stream);
+/* Data parallelism over a caller-owned RCCL communicator (ncclComm_t; replaces a rank of
+ * DQNLearner's torch.distributed path for non-Python callers): one rank per
+ * GPU, each stepping on its share of the global batch (acme_transition_batch.mean_over =
+ * the nominal per-rank batch).  acme_dqn_dp_step = min-probability all-reduce beside the
+ * forwards, loss and dense backward, dense-gradient all-reduce (AVG) beside the torso
+ * backward, torso-gradient all-reduce, Adam and the target copy, num_steps += 1; every
+ * replica applies the same update.  RCCL is loaded at run time (librccl.so.1). */
+int acme_dqn_dp_init(acme_dqn* l, void* nccl_comm, int32_t world_size);
+int acme_dqn_dp_step(acme_dqn* l, const acme_transition_batch* batch,
+                     const acme_dqn_outputs* out, void* stream);
+/* Communicator helpers for callers that bring none: a 128-byte unique id made on one rank
+ * and shared with the others, then one communicator per rank. */
+int acme_nccl_get_unique_id(uint8_t* out128);
+int acme_nccl_comm_init(const uint8_t* id128, int32_t world_size, int32_t rank, void** comm);
+int acme_nccl_comm_destroy(void* comm);
 /* Adam on (params, grads), then target <- params when num_steps % period == 0, then
  * num_steps += 1 (acme/agents/tf/dqn/learning.py:147-161). */
 int acme_dqn_apply(acme_dqn* l, void* stream);

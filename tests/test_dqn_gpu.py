@@ -275,6 +275,51 @@ def test_fused_step_equals_staged_step_bitwise():
         assert a.loss.item() == b.loss.item()
 
 
+@pytest.mark.parametrize("path", ["stages_2_4_1", "rccl_world1"])
+def test_data_parallel_step_equals_fused_step_bitwise(path):
+    """The data-parallel rank's step on one GPU equals acme_dqn_step bit for bit, over steps
+    with a target copy: stages 2, 4 (no join of the dense gradients; the caller's stream is
+    ordered after them by dense_grads_ready), 1 and apply; and acme_dqn_dp_step over a
+    one-rank RCCL communicator (every all-reduce of one rank is the identity)."""
+    from acme_amd import native as N
+    from acme_amd.networks import DQNAtariNetwork
+    net = DQNAtariNetwork(18)
+    B = 32
+    p0, t0 = net.init(5), net.init(6)
+    a = _learner(net, B, target_update_period=2)
+    b = _learner(net, B, target_update_period=2)
+    a.set_params(p0, t0)
+    b.set_params(p0, t0)
+    comm = None
+    if path == "rccl_world1":
+        comm = N.nccl_comm_init(N.nccl_unique_id(), 1, 0)
+        b.dp_init(comm, 1)
+    rng = np.random.default_rng(13)
+    try:
+        for _ in range(3):
+            dev = _dev(_batch(rng, B, (84, 84, 4), 18))
+            a.step(*dev)
+            if comm is None:
+                b.forward_backward_stage(2, *dev)
+                b.forward_backward_stage(4, *dev)
+                b.dense_grads_ready()
+                b.forward_backward_stage(1, *dev)
+                b.apply()
+            else:
+                b.dp_step(*dev)
+            torch.cuda.synchronize()
+            assert a.loss.item() == b.loss.item()
+            for buf in ("params", "target", "m", "v"):
+                ga, gb = a.get_params(buf), b.get_params(buf)
+                for k in ga:
+                    np.testing.assert_array_equal(ga[k], gb[k], err_msg=f"{buf}/{k}")
+        assert a.num_steps == b.num_steps == 3
+    finally:
+        if comm is not None:
+            torch.cuda.synchronize()
+            N.nccl_comm_destroy(comm)
+
+
 def test_adjacent_frames_layout_bitwise():
     """The GPU dataset hands o_t directly after o_tm1 in one allocation; the step on that
     layout is bit-identical to the step on separate buffers."""
