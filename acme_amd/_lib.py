@@ -122,6 +122,13 @@ _SIGS = {
     "acme_replay_stage": (c_i32, [c_vp, c_i64, ctypes.POINTER(c_vp)]),
     "acme_replay_commit": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp]),
     "acme_replay_sync_inserts": (c_i32, [c_vp]),
+    "acme_nstep_writer_create": (c_i32, [c_vp, c_i32, c_f32, c_i64, c_i64, c_i64, c_vp]),
+    "acme_nstep_writer_destroy": (c_i32, [c_vp]),
+    "acme_nstep_writer_start": (c_i32, [c_vp, c_vp]),
+    "acme_nstep_writer_add": (c_i32, [c_vp, c_vp, c_f32, c_f32, c_vp, c_i32, c_f64]),
+    "acme_nstep_writer_flush": (c_i32, [c_vp]),
+    "acme_nstep_writer_reset": (c_i32, [c_vp]),
+    "acme_nstep_writer_pending": (c_i64, [c_vp]),
     "acme_replay_fill_synthetic": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_u64, c_vp]),
     "acme_replay_sample": (c_i32, [c_vp, c_i64, c_u64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "acme_replay_gather": (c_i32, [c_vp, c_vp, c_i64, ctypes.POINTER(c_vp), c_vp]),

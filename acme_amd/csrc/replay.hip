@@ -71,11 +71,14 @@ struct acme_replay {
   std::mutex mu;
   // Insert path.
   hipStream_t side = nullptr;
+  hipStream_t upload = nullptr;  // H2D of staged chunks into their device mirrors
   hipEvent_t insert_event = nullptr;  // recorded on `side` after each commit
   uint64_t insert_seq = 0;            // commits so far
   int64_t stage_items = 0;            // items per staging chunk
   int64_t stage_off[ACME_MAX_FIELDS + 3] = {};  // field rows, then keys, raw prio, leaves
   uint8_t* stage[kStageChunks] = {};
+  uint8_t* stage_dev[kStageChunks] = {};  // device mirror of each chunk (upload target)
+  hipEvent_t stage_up[kStageChunks] = {};  // the chunk's upload to its mirror completed
   hipEvent_t stage_done[kStageChunks] = {};
   bool stage_used[kStageChunks] = {};
   int stage_next = 0;
@@ -681,6 +684,28 @@ __global__ void restore_leaves_kernel(const double* __restrict__ raw, double* __
 }
 
 // Recompute all internal levels over the slot range touched by an insert.
+// The landing of a committed chunk: its device mirror's blocks (field rows, keys, raw
+// priorities, leaf weights) copied into the table's ring slots, every block in at most two
+// ring segments, in one launch of 4-byte words.
+constexpr int kMaxScatterSegs = 2 * (ACME_MAX_FIELDS + 3);
+struct ScatterSegs {
+  const uint32_t* src[kMaxScatterSegs];
+  uint32_t* dst[kMaxScatterSegs];
+  int64_t end[kMaxScatterSegs];  // cumulative words
+  int n;
+};
+
+__global__ void __launch_bounds__(256) stage_scatter_kernel(ScatterSegs s) {
+  const int64_t total = s.end[s.n - 1];
+  for (int64_t i = blockIdx.x * int64_t(256) + threadIdx.x; i < total;
+       i += int64_t(gridDim.x) * 256) {
+    int k = 0;
+    while (i >= s.end[k]) ++k;
+    const int64_t w = i - (k ? s.end[k - 1] : 0);
+    s.dst[k][w] = s.src[k][w];
+  }
+}
+
 int refresh_range(acme_replay* r, int64_t first_key, int64_t n, hipStream_t st) {
   const int64_t C = r->cfg.capacity;
   if (n <= 0) return ACME_OK;
@@ -756,6 +781,21 @@ int order_after_inserts(acme_replay* r, hipStream_t st, int64_t* size_out = null
   return ACME_OK;
 }
 
+// Byte layout of a staging chunk of n items: each field's rows, then keys, raw priorities
+// and leaf weights (8 B per item each), every block 256-B aligned.  Returns the chunk bytes.
+int64_t stage_layout(const acme_replay_config& cfg, int64_t n, int64_t* off) {
+  int64_t o = 0;
+  for (int f = 0; f < cfg.num_fields; ++f) {
+    off[f] = o;
+    o += (n * cfg.field_bytes[f] + 255) / 256 * 256;
+  }
+  for (int k = 0; k < 3; ++k) {
+    off[ACME_MAX_FIELDS + k] = o;
+    o += (n * 8 + 255) / 256 * 256;
+  }
+  return o;
+}
+
 // Side stream, staging chunks and events, created on the first host insert.
 int ensure_insert_path(acme_replay* r) {
   if (r->side) return ACME_OK;
@@ -764,25 +804,23 @@ int ensure_insert_path(acme_replay* r) {
   item += 3 * 8;
   int64_t n = std::max<int64_t>(1, kStageBytes / std::max<int64_t>(item, 1));
   n = std::min(n, r->cfg.capacity);
-  int64_t off = 0;
-  for (int f = 0; f < r->cfg.num_fields; ++f) {
-    r->stage_off[f] = off;
-    off += (n * r->cfg.field_bytes[f] + 255) / 256 * 256;
-  }
-  for (int k = 0; k < 3; ++k) {
-    r->stage_off[ACME_MAX_FIELDS + k] = off;
-    off += (n * 8 + 255) / 256 * 256;
-  }
+  const int64_t off = stage_layout(r->cfg, n, r->stage_off);
   for (int c = 0; c < kStageChunks; ++c) {
     if (hipHostMalloc(reinterpret_cast<void**>(&r->stage[c]), off, hipHostMallocDefault) !=
         hipSuccess) {
       set_error("hipHostMalloc of a %lld-byte insert staging chunk failed", (long long)off);
       return ACME_ERR_OOM;
     }
+    if (hipMalloc(reinterpret_cast<void**>(&r->stage_dev[c]), off) != hipSuccess) {
+      set_error("hipMalloc of a %lld-byte insert staging mirror failed", (long long)off);
+      return ACME_ERR_OOM;
+    }
     ACME_HIP_TRY(hipEventCreateWithFlags(&r->stage_done[c], hipEventDisableTiming));
+    ACME_HIP_TRY(hipEventCreateWithFlags(&r->stage_up[c], hipEventDisableTiming));
   }
   ACME_HIP_TRY(hipEventCreateWithFlags(&r->insert_event, hipEventDisableTiming));
   r->stage_items = n;
+  ACME_HIP_TRY(hipStreamCreateWithFlags(&r->upload, hipStreamNonBlocking));
   ACME_HIP_TRY(hipStreamCreateWithFlags(&r->side, hipStreamNonBlocking));
   return ACME_OK;
 }
@@ -796,21 +834,41 @@ int acquire_chunk(acme_replay* r, int* out) {
   return ACME_OK;
 }
 
-// Issues the n <= stage_items items staged in chunk c: keys, raw priorities and leaf
-// weights into the chunk, the side stream fenced after `after` and every stream that
-// touched the table, H2D copies in at most two ring segments, the tree refresh, events.
+// A pinned staging chunk: the table's ring (r->stage[c]) or an n-step writer's own.
+struct Chunk {
+  uint8_t* base;
+  const int64_t* off;  // stage_layout offsets
+  hipEvent_t done;     // recorded after the chunk's copies
+  uint8_t* dev;        // its device mirror
+  hipEvent_t up;       // recorded after the upload into the mirror
+  int64_t cap;         // items the layout holds
+};
+
+Chunk ring_chunk(acme_replay* r, int c) {
+  return {r->stage[c], r->stage_off, r->stage_done[c], r->stage_dev[c], r->stage_up[c],
+          r->stage_items};
+}
+
+// Issues the n items staged in chunk ch: keys, raw priorities and leaf weights into the
+// chunk; the chunk's used blocks uploaded (H2D, upload stream) into its device mirror with
+// no ordering against the table's readers (the mirror is private); then on the side stream,
+// fenced after the upload, `after` and every stream that touched the table, the landing
+// (one scatter launch into the ring slots) and the tree refresh.  The fence thus holds only
+// the few-microsecond landing, not the PCIe transfer, between the readers' earlier work and
+// their next draw.  Caller holds r->mu.
 //
 // dev (optional): device rows of the n items; then the copies run on `after` itself (the
 // caller's stream, which owns those buffers) instead of the side stream.  skip: keys
 // consumed before these items (an over-capacity insert).
-int commit_chunk(acme_replay* r, int c, int64_t n, const double* priorities, uint64_t* out_keys,
-                 hipStream_t after, const void* const* dev = nullptr, int64_t skip = 0) {
+int commit_chunk(acme_replay* r, const Chunk& ch, int64_t n, const double* priorities,
+                 uint64_t* out_keys, hipStream_t after, const void* const* dev = nullptr,
+                 int64_t skip = 0) {
   const int64_t C = r->cfg.capacity;
   const int64_t first_key = r->inserted + skip;
-  uint8_t* base = r->stage[c];
-  uint64_t* hkeys = reinterpret_cast<uint64_t*>(base + r->stage_off[ACME_MAX_FIELDS]);
-  double* hprio = reinterpret_cast<double*>(base + r->stage_off[ACME_MAX_FIELDS + 1]);
-  double* hleaf = reinterpret_cast<double*>(base + r->stage_off[ACME_MAX_FIELDS + 2]);
+  uint8_t* base = ch.base;
+  uint64_t* hkeys = reinterpret_cast<uint64_t*>(base + ch.off[ACME_MAX_FIELDS]);
+  double* hprio = reinterpret_cast<double*>(base + ch.off[ACME_MAX_FIELDS + 1]);
+  double* hleaf = reinterpret_cast<double*>(base + ch.off[ACME_MAX_FIELDS + 2]);
   for (int64_t i = 0; i < n; ++i) {
     const double p = priorities ? priorities[i] : 1.0;
     if (!(p >= 0.0)) {
@@ -844,32 +902,72 @@ int commit_chunk(acme_replay* r, int c, int64_t n, const double* priorities, uin
     }
   }
   hipStream_t st = dev ? after : r->side;
+  const int nf = r->cfg.num_fields;
+  if (!dev) {
+    // Upload: one copy when the chunk is full, else one per used block.
+    const int64_t full = ch.off[ACME_MAX_FIELDS + 2] + n * 8;
+    if (n == ch.cap) {
+      ACME_HIP_TRY(hipMemcpyAsync(ch.dev, base, full, hipMemcpyHostToDevice, r->upload));
+    } else {
+      for (int f = 0; f < nf; ++f)
+        ACME_HIP_TRY(hipMemcpyAsync(ch.dev + ch.off[f], base + ch.off[f],
+                                    n * r->cfg.field_bytes[f], hipMemcpyHostToDevice,
+                                    r->upload));
+      for (int k = 0; k < 3; ++k)
+        ACME_HIP_TRY(hipMemcpyAsync(ch.dev + ch.off[ACME_MAX_FIELDS + k],
+                                    base + ch.off[ACME_MAX_FIELDS + k], n * 8,
+                                    hipMemcpyHostToDevice, r->upload));
+    }
+    ACME_HIP_TRY(hipEventRecord(ch.up, r->upload));
+    ACME_HIP_TRY(hipStreamWaitEvent(st, ch.up, 0));
+  }
+  ScatterSegs segs{};
+  int64_t words = 0;
+  auto seg = [&](const uint8_t* src, uint8_t* dst, int64_t bytes) {
+    segs.src[segs.n] = reinterpret_cast<const uint32_t*>(src);
+    segs.dst[segs.n] = reinterpret_cast<uint32_t*>(dst);
+    words += bytes / 4;
+    segs.end[segs.n++] = words;
+  };
   int64_t done = 0;
   while (done < n) {
     const int64_t slot = (first_key + done) % C;
     const int64_t len = std::min(n - done, C - slot);
-    for (int f = 0; f < r->cfg.num_fields; ++f) {
+    for (int f = 0; f < nf; ++f) {
       const int64_t b = r->cfg.field_bytes[f];
       if (dev)
         ACME_HIP_TRY(hipMemcpyAsync(r->fields[f] + slot * b,
                                     static_cast<const uint8_t*>(dev[f]) + done * b, len * b,
                                     hipMemcpyDeviceToDevice, st));
       else
-        ACME_HIP_TRY(hipMemcpyAsync(r->fields[f] + slot * b, base + r->stage_off[f] + done * b,
-                                    len * b, hipMemcpyHostToDevice, st));
+        seg(ch.dev + ch.off[f] + done * b, r->fields[f] + slot * b, len * b);
     }
-    ACME_HIP_TRY(hipMemcpyAsync(r->keys + slot, hkeys + done, len * sizeof(uint64_t),
-                                hipMemcpyHostToDevice, st));
-    ACME_HIP_TRY(hipMemcpyAsync(r->raw_prio + slot, hprio + done, len * sizeof(double),
-                                hipMemcpyHostToDevice, st));
-    ACME_HIP_TRY(hipMemcpyAsync(r->levels[0] + slot, hleaf + done, len * sizeof(double),
-                                hipMemcpyHostToDevice, st));
+    if (dev) {
+      ACME_HIP_TRY(hipMemcpyAsync(r->keys + slot, hkeys + done, len * sizeof(uint64_t),
+                                  hipMemcpyHostToDevice, st));
+      ACME_HIP_TRY(hipMemcpyAsync(r->raw_prio + slot, hprio + done, len * sizeof(double),
+                                  hipMemcpyHostToDevice, st));
+      ACME_HIP_TRY(hipMemcpyAsync(r->levels[0] + slot, hleaf + done, len * sizeof(double),
+                                  hipMemcpyHostToDevice, st));
+    } else {
+      const int64_t o = done * 8;
+      seg(ch.dev + ch.off[ACME_MAX_FIELDS] + o, reinterpret_cast<uint8_t*>(r->keys + slot),
+          len * 8);
+      seg(ch.dev + ch.off[ACME_MAX_FIELDS + 1] + o,
+          reinterpret_cast<uint8_t*>(r->raw_prio + slot), len * 8);
+      seg(ch.dev + ch.off[ACME_MAX_FIELDS + 2] + o,
+          reinterpret_cast<uint8_t*>(r->levels[0] + slot), len * 8);
+    }
     done += len;
+  }
+  if (!dev) {
+    const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(words, 256 * 4), 2048);
+    stage_scatter_kernel<<<std::max(grid, 1u), 256, 0, st>>>(segs);
+    ACME_LAUNCH_CHECK();
   }
   int rc = refresh_range(r, first_key, n, st);
   if (rc != ACME_OK) return rc;
-  ACME_HIP_TRY(hipEventRecord(r->stage_done[c], st));
-  r->stage_used[c] = true;
+  ACME_HIP_TRY(hipEventRecord(ch.done, st));
   {
     std::lock_guard<std::mutex> lock(r->order_mu);
     ACME_HIP_TRY(hipEventRecord(r->insert_event, st));
@@ -954,11 +1052,14 @@ int acme_replay_destroy(acme_replay* r) {
     if (r->fields[f]) (void)hipFree(r->fields[f]);
   for (int c = 0; c < kStageChunks; ++c) {
     if (r->stage[c]) (void)hipHostFree(r->stage[c]);
+    if (r->stage_dev[c]) (void)hipFree(r->stage_dev[c]);
     if (r->stage_done[c]) (void)hipEventDestroy(r->stage_done[c]);
+    if (r->stage_up[c]) (void)hipEventDestroy(r->stage_up[c]);
   }
   for (int i = 0; i < r->nreaders; ++i) (void)hipEventDestroy(r->readers[i].ev);
   if (r->insert_event) (void)hipEventDestroy(r->insert_event);
   if (r->side) (void)hipStreamDestroy(r->side);
+  if (r->upload) (void)hipStreamDestroy(r->upload);
   delete r;
   return ACME_OK;
 }
@@ -1053,7 +1154,10 @@ int acme_replay_commit(acme_replay* r, int64_t n, const double* priorities, uint
   r->staged = -1;
   r->stage_cv.notify_all();
   if (n == 0) return ACME_OK;  // the chunk's last copies (if any) are still tracked
-  return commit_chunk(r, c, n, priorities, out_keys, as_stream(stream));
+  const int rc = commit_chunk(r, ring_chunk(r, c), n, priorities,
+                              out_keys, as_stream(stream));
+  if (rc == ACME_OK) r->stage_used[c] = true;
+  return rc;
 }
 
 int acme_replay_sync_inserts(acme_replay* r) {
@@ -1097,10 +1201,12 @@ int acme_replay_insert(acme_replay* r, const void* const* fields, int64_t n,
       if (src_on_device) dev[f] = src;  // HBM rows: copied on the caller's stream
       else std::memcpy(r->stage[c] + r->stage_off[f], src, len * b);  // pack into pinned
     }
-    rc = commit_chunk(r, c, len, priorities ? priorities + done : nullptr,
+    rc = commit_chunk(r, ring_chunk(r, c), len,
+                      priorities ? priorities + done : nullptr,
                       out_keys ? out_keys + done : nullptr, st,
                       src_on_device ? dev : nullptr, pending_skip);
     if (rc != ACME_OK) return rc;
+    r->stage_used[c] = true;
     pending_skip = 0;
     done += len;
   }
@@ -1498,6 +1604,201 @@ int acme_replay_update_priorities(acme_replay* r, const uint64_t* keys, const do
   prio_reset_kernel<<<g, 256, 0, st>>>(t_slots, t_valid, n, r->winner);
   ACME_LAUNCH_CHECK();
   return ACME_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- n-step transition writer
+// The native side of NStepTransitionAdder (acme/adders/reverb/transition.py:119-165) for a
+// transition table (o_tm1, a, R, D, o_t): the adder hands over each environment step's raw
+// fields and the writer keeps the last n steps (its own copies of their observations), forms
+// every item the reference writes (head = oldest step of the window; shorter windows at the
+// start of an episode and, on the last step, the drain of shrinking windows) straight into
+// rows of its own pinned chunk and commits a full chunk like acme_replay_commit.  No Python
+// work per field and one copy of each observation into the window plus one per row.
+//
+// The return and discount accumulate in f32 in the reference's order (the adder's numpy
+// float32 scalars: total_discount *= g; ret += r_i * total_discount; total_discount *= d_i),
+// each product and sum rounded on its own (no contraction).
+struct acme_nstep_writer {
+  acme_replay* r = nullptr;
+  int n = 1;
+  float g = 1.0f;
+  int64_t obs_bytes = 0, act_bytes = 0;  // payload bytes of o and a (rows may be padded)
+  int64_t rows = 0;                     // rows per chunk
+  int64_t off[ACME_MAX_FIELDS + 3] = {};
+  uint8_t* chunk[2] = {};
+  uint8_t* mirror[2] = {};
+  hipEvent_t done[2] = {}, up[2] = {};
+  bool used[2] = {};
+  int cur = 0;
+  int64_t fill = 0;
+  std::vector<double> prio;
+  // Window: steps [lo, steps) of the current episode; observation k (before step k) in
+  // obs slot k % (n + 1), step k's action / reward / discount in slot k % (n + 1).
+  std::vector<uint8_t> obs, act;
+  std::vector<float> rew, disc;
+  int64_t lo = 0, steps = 0;
+  bool started = false;
+  std::mutex mu;
+};
+
+namespace {
+
+int nstep_commit(acme_nstep_writer* w) {
+  if (w->fill == 0) return ACME_OK;
+  acme_replay* r = w->r;
+  std::lock_guard<std::mutex> lock(r->mu);
+  int rc = ensure_insert_path(r);
+  if (rc != ACME_OK) return rc;
+  const int c = w->cur;
+  rc = commit_chunk(r, {w->chunk[c], w->off, w->done[c], w->mirror[c], w->up[c], w->rows}, w->fill,
+                    w->prio.data(), nullptr, nullptr);
+  if (rc != ACME_OK) return rc;
+  w->used[c] = true;
+  w->cur = c ^ 1;
+  w->fill = 0;
+  return ACME_OK;
+}
+
+// One item: head step `lo`, window [lo, hi), next observation hi.
+int nstep_emit(acme_nstep_writer* w, int64_t lo, int64_t hi, double priority) {
+#pragma clang fp contract(off)
+  const int64_t m = w->n + 1;
+  if (w->fill == 0 && w->used[w->cur]) ACME_HIP_TRY(hipEventSynchronize(w->done[w->cur]));
+  float ret = w->rew[lo % m], dsc = w->disc[lo % m];
+  for (int64_t k = lo + 1; k < hi; ++k) {
+    dsc = dsc * w->g;
+    ret = ret + w->rew[k % m] * dsc;
+    dsc = dsc * w->disc[k % m];
+  }
+  const auto& fb = w->r->cfg.field_bytes;
+  uint8_t* base = w->chunk[w->cur];
+  const int64_t i = w->fill;
+  std::memcpy(base + w->off[0] + i * fb[0], w->obs.data() + (lo % m) * w->obs_bytes, w->obs_bytes);
+  std::memcpy(base + w->off[1] + i * fb[1], w->act.data() + (lo % m) * w->act_bytes, w->act_bytes);
+  std::memcpy(base + w->off[2] + i * fb[2], &ret, 4);
+  std::memcpy(base + w->off[3] + i * fb[3], &dsc, 4);
+  std::memcpy(base + w->off[4] + i * fb[4], w->obs.data() + (hi % m) * w->obs_bytes, w->obs_bytes);
+  w->prio[i] = priority;
+  w->fill = i + 1;
+  return w->fill == w->rows ? nstep_commit(w) : ACME_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int acme_nstep_writer_create(acme_replay* r, int32_t n_step, float discount, int64_t obs_bytes,
+                             int64_t action_bytes, int64_t rows_per_chunk,
+                             acme_nstep_writer** out) {
+  ACME_CHECK_ARG(r && out, "null argument");
+  ACME_CHECK_ARG(n_step >= 1, "n_step must be >= 1, got %d", n_step);
+  ACME_CHECK_ARG(rows_per_chunk >= 1, "rows_per_chunk must be >= 1");
+  const auto& cfg = r->cfg;
+  ACME_CHECK_ARG(cfg.num_fields == 5 && cfg.field_bytes[2] == 4 && cfg.field_bytes[3] == 4 &&
+                     cfg.field_bytes[0] == cfg.field_bytes[4],
+                 "table is not a transition table (o_tm1, a, f32 r, f32 d, o_t)");
+  ACME_CHECK_ARG(obs_bytes >= 1 && obs_bytes <= cfg.field_bytes[0] && action_bytes >= 1 &&
+                     action_bytes <= cfg.field_bytes[1],
+                 "observation / action bytes do not fit the table's rows");
+  auto* w = new acme_nstep_writer();
+  w->r = r;
+  w->n = n_step;
+  w->g = discount;
+  w->obs_bytes = obs_bytes;
+  w->act_bytes = action_bytes;
+  w->rows = std::min<int64_t>(rows_per_chunk, cfg.capacity);
+  const int64_t bytes = stage_layout(cfg, w->rows, w->off);
+  for (int c = 0; c < 2; ++c) {
+    if (hipHostMalloc(reinterpret_cast<void**>(&w->chunk[c]), bytes, hipHostMallocDefault) !=
+            hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&w->mirror[c]), bytes) != hipSuccess ||
+        hipEventCreateWithFlags(&w->done[c], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&w->up[c], hipEventDisableTiming) != hipSuccess) {
+      acme_nstep_writer_destroy(w);
+      set_error("n-step writer: pinned chunk of %lld bytes", (long long)bytes);
+      return ACME_ERR_OOM;
+    }
+    std::memset(w->chunk[c], 0, bytes);  // row padding stays zero
+  }
+  w->prio.assign(w->rows, 1.0);
+  w->obs.assign((n_step + 1) * obs_bytes, 0);
+  w->act.assign((n_step + 1) * action_bytes, 0);
+  w->rew.assign(n_step + 1, 0.0f);
+  w->disc.assign(n_step + 1, 0.0f);
+  *out = w;
+  return ACME_OK;
+}
+
+int acme_nstep_writer_destroy(acme_nstep_writer* w) {
+  if (!w) return ACME_OK;
+  for (int c = 0; c < 2; ++c) {
+    if (w->done[c]) {
+      if (w->used[c]) (void)hipEventSynchronize(w->done[c]);
+      (void)hipEventDestroy(w->done[c]);
+    }
+    if (w->up[c]) (void)hipEventDestroy(w->up[c]);
+    if (w->chunk[c]) (void)hipHostFree(w->chunk[c]);
+    if (w->mirror[c]) (void)hipFree(w->mirror[c]);
+  }
+  delete w;
+  return ACME_OK;
+}
+
+int acme_nstep_writer_start(acme_nstep_writer* w, const void* observation) {
+  ACME_CHECK_ARG(w && observation, "null argument");
+  std::lock_guard<std::mutex> lock(w->mu);
+  w->lo = w->steps = 0;
+  std::memcpy(w->obs.data(), observation, w->obs_bytes);
+  w->started = true;
+  return ACME_OK;
+}
+
+int acme_nstep_writer_add(acme_nstep_writer* w, const void* action, float reward,
+                          float discount, const void* next_observation, int32_t last,
+                          double priority) {
+  ACME_CHECK_ARG(w && action && next_observation, "null argument");
+  ACME_CHECK_ARG(priority >= 0.0, "priority %g must be >= 0", priority);
+  std::lock_guard<std::mutex> lock(w->mu);
+  ACME_CHECK_ARG(w->started, "add before start (adder.add_first)");
+  const int64_t m = w->n + 1, s = w->steps;
+  std::memcpy(w->act.data() + (s % m) * w->act_bytes, action, w->act_bytes);
+  w->rew[s % m] = reward;
+  w->disc[s % m] = discount;
+  w->steps = s + 1;
+  w->lo = std::max<int64_t>(w->lo, w->steps - w->n);
+  std::memcpy(w->obs.data() + (w->steps % m) * w->obs_bytes, next_observation, w->obs_bytes);
+  int rc = nstep_emit(w, w->lo, w->steps, priority);
+  if (rc != ACME_OK) return rc;
+  if (last) {  // the drain of transition.py:167-172
+    for (int64_t k = w->lo + 1; k < w->steps; ++k) {
+      rc = nstep_emit(w, k, w->steps, priority);
+      if (rc != ACME_OK) return rc;
+    }
+    w->started = false;
+  }
+  return ACME_OK;
+}
+
+int acme_nstep_writer_flush(acme_nstep_writer* w) {
+  ACME_CHECK_ARG(w, "null writer");
+  std::lock_guard<std::mutex> lock(w->mu);
+  return nstep_commit(w);
+}
+
+int acme_nstep_writer_reset(acme_nstep_writer* w) {
+  ACME_CHECK_ARG(w, "null writer");
+  std::lock_guard<std::mutex> lock(w->mu);
+  w->started = false;
+  w->lo = w->steps = 0;
+  return nstep_commit(w);
+}
+
+int64_t acme_nstep_writer_pending(acme_nstep_writer* w) {
+  if (!w) return 0;
+  std::lock_guard<std::mutex> lock(w->mu);
+  return w->fill;
 }
 
 }  // extern "C"

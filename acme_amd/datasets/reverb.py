@@ -358,9 +358,8 @@ class _TableIterator:
     def __next__(self) -> replay.ReplaySample:
         from acme_amd._lib import check, lib, stream_ptr
         t = self._t
-        t.flush()
         t.wait_for(self._B, self._timeout)
-        t.flush()
+        t.flush_for_sampling(self._B)
         if self._slots is None:
             self._alloc()
         L, h = lib(), t.native.handle

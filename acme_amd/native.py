@@ -63,6 +63,10 @@ class NativeReplay:
     def size(self) -> int:
         return int(lib().acme_replay_size(self._h))
 
+    def nstep_writer(self, n_step: int, discount: float, obs_bytes: int, action_bytes: int,
+                     rows_per_chunk: int = 64) -> "NativeNStepWriter":
+        return NativeNStepWriter(self, n_step, discount, obs_bytes, action_bytes, rows_per_chunk)
+
     def insert(self, fields: Sequence, priorities: Optional[np.ndarray] = None,
                stream=None) -> np.ndarray:
         """fields: per-field arrays/tensors with leading dim n (host numpy or device tensors)."""
@@ -216,6 +220,52 @@ class NativeReplay:
                                  ("keys", ks, np.uint64, n)):
             out[name] = _device_array(p.value, cnt, dt, self.device).cpu().numpy().view(dt).copy()
         return out
+
+
+class NativeNStepWriter:
+    """acme_nstep_writer: the native side of NStepTransitionAdder (rows formed and packed in
+    C, straight into pinned chunks).  `add_raw(act_ptr, reward, discount, obs_ptr, last,
+    priority)` is the per-step entry, with the pointers of host arrays the caller keeps alive
+    for the call."""
+
+    def __init__(self, table: NativeReplay, n_step: int, discount: float, obs_bytes: int,
+                 action_bytes: int, rows_per_chunk: int = 64):
+        h = ctypes.c_void_p()
+        L = lib()
+        check(L.acme_nstep_writer_create(table.handle, int(n_step), float(discount),
+                                         int(obs_bytes), int(action_bytes), int(rows_per_chunk),
+                                         ctypes.byref(h)), "n-step writer create")
+        self._table = table  # the writer commits into it: keep it alive
+        self._h = h
+        self._add = L.acme_nstep_writer_add
+        self._pending = L.acme_nstep_writer_pending
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                lib().acme_nstep_writer_destroy(h)
+            except Exception:  # interpreter shutdown
+                pass
+            self._h = None
+
+    def start(self, obs_ptr: int) -> None:
+        check(lib().acme_nstep_writer_start(self._h, obs_ptr), "n-step writer start")
+
+    def add_raw(self, act_ptr: int, reward: float, discount: float, obs_ptr: int, last: bool,
+                priority: float = 1.0) -> None:
+        rc = self._add(self._h, act_ptr, reward, discount, obs_ptr, 1 if last else 0, priority)
+        if rc:
+            check(rc, "n-step writer add")
+
+    def flush(self) -> None:
+        check(lib().acme_nstep_writer_flush(self._h), "n-step writer flush")
+
+    def reset(self) -> None:
+        check(lib().acme_nstep_writer_reset(self._h), "n-step writer reset")
+
+    def pending(self) -> int:
+        return int(self._pending(self._h))
 
 
 def _device_array(address: int, count: int, dtype, device) -> torch.Tensor:

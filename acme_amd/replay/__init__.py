@@ -25,6 +25,7 @@ import collections
 import itertools
 import threading
 import time
+import weakref
 from typing import Any, Dict, List, NamedTuple, Optional, Sequence
 
 import numpy as np
@@ -128,6 +129,9 @@ class Table:
         self._pend: Optional[List[np.ndarray]] = None
         self._pend_prio = np.zeros(self._flush_every, np.float64)
         self._fill = 0
+        # Native n-step writers feeding this table (NStepTransitionAdder's fast path): their
+        # pending rows count towards size() and a flush() commits them.
+        self._writers = weakref.WeakSet()
         self._mu = threading.RLock()
         self._cv = threading.Condition(self._mu)
         self._draws = 0
@@ -167,7 +171,15 @@ class Table:
     def size(self) -> int:
         with self._mu:
             n = self._native.size() if self._native is not None else 0
-            return min(self.max_size, n + self._fill)
+            return min(self.max_size, n + self._fill + sum(w.pending() for w in self._writers))
+
+    def committed_size(self) -> int:
+        """Items on the device (what a draw can return now)."""
+        return self._native.size() if self._native is not None else 0
+
+    def register_writer(self, writer) -> None:
+        with self._mu:
+            self._writers.add(writer)
 
     def can_sample(self, num_samples: int = 1) -> bool:
         return self.size() >= max(self._min_size, 1)
@@ -244,11 +256,22 @@ class Table:
         every stream that has read it (a queued prefetch gather never sees a slot
         overwritten under it) and every later sample after them."""
         with self._mu:
+            for w in list(self._writers):
+                w.flush()
             n = self._fill
             if not n:
                 return
             self._native.insert([p[:n] for p in self._pend], self._pend_prio[:n])
             self._fill = 0
+
+    def flush_for_sampling(self, batch_size: int) -> None:
+        """A reader's flush: commits pending rows only when the device table could not serve
+        the draw without them (it holds fewer than the batch or MinSize).  Otherwise rows
+        become visible when their writer's buffer fills or the writer closes, as Reverb
+        chunks do, so the learner's thread never packs or issues the actors' inserts."""
+        with self._mu:
+            if self.committed_size() < max(batch_size, self._min_size, 1):
+                self.flush()
 
     # -- checkpointing (optional replay state; core.Saveable interface)
     def save(self) -> Dict[str, Any]:
@@ -283,7 +306,8 @@ class Table:
                 if left <= 0:
                     raise RuntimeError(f"table '{self.name}' has {self.size()} items; "
                                        f"MinSize({self._min_size}) not reached within {timeout}s")
-                self._cv.wait(left)
+                # Native writers add without notifying: poll.
+                self._cv.wait(min(left, 0.01))
 
     def next_draw(self) -> int:
         with self._mu:
@@ -294,7 +318,7 @@ class Table:
     def update_priorities(self, keys, priorities) -> None:
         import torch
         with self._mu:
-            self.flush()
+            # Pending rows hold no keys yet: nothing to flush for an update.
             if self._native is None:
                 return
             k = keys if isinstance(keys, torch.Tensor) else torch.as_tensor(

@@ -230,20 +230,26 @@ def setup_dqn(args, world, rank, dev):
 def insert_bench(args, dev):
     """Actor-side insert path (north star: pinned hipMemcpyAsync on a side stream) into the
     1M-slot table of the headline config while the DQN learner steps.  Three measurements:
-    learner steps alone; the same steps with a host thread inserting through the adder-facing
-    Table.insert (one item per call, as Writer.create_item; flushes of 256 items into the
-    pinned staging ring); and with a host thread committing whole staged chunks (the
-    native stage/commit path, bulk).  Inserts/s counts items whose commit returned inside
-    the timed window of learner steps."""
+    learner steps alone; the same steps with a host thread stepping the reference DQN agent's
+    NStepTransitionAdder (n_step 5, agents/tf/dqn/agent.py:57,103-108: one adder.add per
+    environment step, one item each, through the table's native n-step writer) at the
+    reference's ratio of one insert per 32 sampled items; and with a host thread committing
+    whole staged chunks (the native stage/commit path, bulk).  Inserts/s counts items added
+    inside the timed window of learner steps.  The environment's timesteps are pre-built
+    (its own cost is not the insert path's)."""
     import threading
+    from acme_amd import dm_env, replay as rp
+    from acme_amd.adders import reverb as adders
     step, B, meta, _, _ = setup_dqn(args, 1, 0, dev)
     table = meta["_table"]
     nat = table.native
     rng = np.random.default_rng(0)
     pool = 512
     obs = rng.integers(0, 256, (pool, 84, 84, 4), dtype=np.uint8)
-    items = [(obs[i], np.int32(i % 18), np.float32(0.5), np.float32(0.99 ** 4),
-              obs[(i + 5) % pool]) for i in range(pool)]
+    acts = [np.int32(i % 18) for i in range(pool)]
+    steps_ts = [dm_env.transition(np.float32(0.5), obs[i], np.float32(0.99)) for i in range(pool)]
+    adder = adders.NStepTransitionAdder(rp.Client(rp.Server([table])), n_step=5, discount=0.99)
+    adder.add_first(dm_env.restart(obs[0]))
     rows = [obs.reshape(pool, -1), np.arange(pool, dtype=np.int32).view(np.uint8).reshape(pool, 4),
             np.full(pool, 0.5, np.float32).view(np.uint8).reshape(pool, 4),
             np.full(pool, 0.99 ** 4, np.float32).view(np.uint8).reshape(pool, 4),
@@ -279,9 +285,13 @@ def insert_bench(args, dev):
         nat.sync_inserts()
         return dt, (c1 - c0) / dt
 
+    env_t = [0]
+
     def adder_body(n=64):
-        for i in range(n):
-            table.insert(items[(done[0] + i) % pool], 1.0)
+        for _ in range(n):
+            t = env_t[0] % pool
+            adder.add(acts[t], steps_ts[t])
+            env_t[0] += 1
         return n
 
     # The reference agent's ratio: one insert per samples_per_insert = 32 sampled items
@@ -317,6 +327,7 @@ def insert_bench(args, dev):
         n += adder_body()
     table.flush()
     r_adder = n / (time.perf_counter() - t0)
+    assert adder._fast, "the adder did not take the native writer path"  # noqa: SLF001
     # Bulk inserts with no learner running: the host + PCIe ceiling of the path.
     t0 = time.perf_counter()
     n = 0
@@ -327,7 +338,8 @@ def insert_bench(args, dev):
     item_bytes = sum(f.row_bytes for f in table.fields)
     out = {
         "metric": "host->HBM inserts/s into the 1M-slot prioritized table (pinned staging ring, "
-                  "side-stream hipMemcpyAsync) while the DQN learner steps",
+                  "async upload to a device mirror, one-launch landing on the side stream) "
+                  "while the DQN learner steps",
         "value": round(r_bulk, 1), "unit": "items/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "higher_is_better": True, "vs_baseline": None,
         "dtype": "u8", "data": "synthetic uint8 Atari transitions (56,460 B per item)",

@@ -95,11 +95,14 @@ int acme_replay_destroy(acme_replay* r);
  * n * field_bytes[f] contiguous bytes, on the host when src_on_device == 0, else on the
  * device.  priorities: n raw priorities (host, NULL = 1.0).  out_keys (host, optional): the
  * keys assigned.  Items go to ring slots (insert_count + i) % capacity (Fifo remover).
- * Host rows are packed into the table's pinned staging ring and copied by hipMemcpyAsync
- * on the table's own side stream; the call returns without waiting for the copies.  The
- * insert is ordered after the work already issued on `stream` and on every stream that has
- * used the table; every later sample / gather / update_priorities (any stream) is ordered
- * after it.  Device rows are copied on `stream` itself. */
+ * Host rows are packed into the table's pinned staging ring, uploaded (hipMemcpyAsync on
+ * an upload stream, unordered against readers) into the chunk's device mirror, and landed
+ * into the ring slots by one scatter launch on the table's side stream, followed by the
+ * tree refresh; the call returns without waiting.  The landing is ordered after the upload,
+ * the work already issued on `stream` and on every stream that has used the table; every
+ * later sample / gather / update_priorities (any stream) is ordered after it, so a reader
+ * waits for the landing, not for the PCIe transfer.  Device rows are copied on `stream`
+ * itself. */
 int acme_replay_insert(acme_replay* r, const void* const* fields, int64_t n,
                        const double* priorities, int32_t src_on_device,
                        uint64_t* out_keys, void* stream);
@@ -114,6 +117,32 @@ int acme_replay_commit(acme_replay* r, int64_t n, const double* priorities, uint
                        void* stream);
 /* Host wait for every issued insert (tests, checkpoints, shutdown). */
 int acme_replay_sync_inserts(acme_replay* r);
+
+/* N-step transition writer: the native NStepTransitionAdder (acme/adders/reverb/
+ * transition.py:119-172; replaces its _write / _write_last + Writer.append / create_item)
+ * for a transition table (fields o_tm1, a, f32 R, f32 D, o_t).  The adder passes each
+ * environment step's raw fields: _start(first observation) on add_first, _add(action,
+ * reward, discount, next observation, last, priority) on add.  The writer keeps the last
+ * n_step steps, writes every item the reference writes (window head = oldest step; windows
+ * of 1, 2, ... steps at an episode's start; on the last step the drain of shrinking windows)
+ * as rows of its own pinned chunk of rows_per_chunk items, and commits a full chunk exactly
+ * as acme_replay_commit does (side-stream copies, no host wait).  R and D accumulate in f32
+ * in the reference's order.  obs_bytes / action_bytes: payload bytes (<= the field's row
+ * bytes; the rest of a row stays zero).  _flush commits the pending rows; _reset (adder.reset
+ * without a last step) commits them and drops the window; _pending: rows not yet committed.
+ * One thread adds; _flush / _pending may be called from any thread. */
+typedef struct acme_nstep_writer acme_nstep_writer;
+int acme_nstep_writer_create(acme_replay* r, int32_t n_step, float discount, int64_t obs_bytes,
+                             int64_t action_bytes, int64_t rows_per_chunk,
+                             acme_nstep_writer** out);
+int acme_nstep_writer_destroy(acme_nstep_writer* w);
+int acme_nstep_writer_start(acme_nstep_writer* w, const void* observation);
+int acme_nstep_writer_add(acme_nstep_writer* w, const void* action, float reward,
+                          float discount, const void* next_observation, int32_t last,
+                          double priority);
+int acme_nstep_writer_flush(acme_nstep_writer* w);
+int acme_nstep_writer_reset(acme_nstep_writer* w);
+int64_t acme_nstep_writer_pending(acme_nstep_writer* w);
 
 /* Fill n items with synthetic data generated on the device (benchmark/test helper,
  * no host traffic).  layout: 0 = DQN Atari transition (o_tm1 u8, a i32, r f32, d f32,
