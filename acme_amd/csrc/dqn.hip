@@ -104,6 +104,12 @@ struct acme_dqn {
   // stream; side_slab is its split-K scratch).
   hipStream_t side = nullptr;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  // Fused step (acme_dqn_step): the conv weight gradients stay split-K slabs and Adam
+  // reduces them on its read (launch_adam_slabs): three reduction launches fewer.
+  float* slab2 = nullptr;    // conv2's slab (conv3's is side_slab, conv1's slab)
+  bool fused_step = false;   // set by step_impl
+  bool slabs_pending = false;
+  torso::WgradSlab wslabs[3];
   float* side_slab = nullptr;
   torso::Plane x1p{}, x2p{}, x3p{}, t1p{}, t2p{}, t3p{}, dzhp{}, dz3p{}, dz2p{}, dz1p{};
   // Plane path: the loss is launched together with the head dZ (launch_dqn_loss_head_dz)
@@ -296,6 +302,18 @@ int slab_reduce(const float* slab, int splits, int64_t count, float* out0, int64
   return launch_slab_reduce(slab, splits, count, out0, split_at, out1, bias, ncols, relu, st);
 }
 
+// snt.Adam over the flat range [off, off + n) (tensor-aligned): the parameter planes (plane
+// path) are refreshed by the same pass.  t = num_steps + 1 (snt.Adam / optix.adam count this
+// step first).  Every element's update is independent, so ranges compose bit-exactly.
+int adam_range(acme_dqn* l, int64_t off, int64_t n, hipStream_t st) {
+  const bool jax = l->cfg.semantics == ACME_SEMANTICS_JAX;
+  return launch_adam(l->params + off, l->grads + off, l->m + off, l->v + off, n,
+                     l->cfg.learning_rate, l->cfg.adam_beta1, l->cfg.adam_beta2,
+                     l->cfg.adam_epsilon, l->num_steps + 1,
+                     l->p3_capable ? l->wpl + off : nullptr, l->flat, st, jax ? 1 : 0, nullptr,
+                     l->p3_capable ? l->scales + kScParams : nullptr);
+}
+
 torso::Weights torso_weights(const acme_dqn* l, const float* prm) {
   return torso::Weights{P(l, prm, l->t_c1w), P(l, prm, l->t_c1b), P(l, prm, l->t_c2w),
                         P(l, prm, l->t_c2b), P(l, prm, l->t_c3w), P(l, prm, l->t_c3b)};
@@ -425,7 +443,8 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st_main,
   const bool p3 = use_p3(l);
   int rc;
   // The fused kernel leaves the batch loss as per-block partials; their sum is the side
-  // stream's first launch (off the critical path).
+  // stream's first launch (off the critical path: folding it into the fused kernel's last
+  // block to finish measured 14.6 -> 20.5 us on the critical path).
   bool loss_sum = false;
   const LossArgs la = l->pending_la;
   if (p3 && l->loss_pending) {  // the loss and the head dZ planes, one launch
@@ -682,6 +701,7 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
         if (e != hipSuccess)
           return fail((set_error("side stream: %s", hipGetErrorString(e)), ACME_ERR_HIP));
         if ((rc = dev_alloc(l, &l->side_slab, l->slab_floats))) return fail(rc);
+        if ((rc = dev_alloc(l, &l->slab2, torso::wgrad_slab_floats_p3()))) return fail(rc);
       }
     }
   } else {
@@ -970,6 +990,13 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
         sd.slab = l->side_slab;
         for (int i = 0; i < 3; ++i) sd.e[i] = l->ev[i];
       }
+      l->slabs_pending = false;
+      if (l->fused_step && !l->calibrating && l->slab2) {
+        sd.slab = l->side_slab;
+        sd.slab2 = l->slab2;
+        sd.defer = l->wslabs;
+        l->slabs_pending = true;
+      }
       return torso::backward_p3(w, g, l->cur_frames, B,
                                 torso::PActs{l->x1p, l->x2p, l->x3p}, l->dz3p, l->dz2p, l->dz1p,
                                 l->slab, st, sd);
@@ -1117,17 +1144,32 @@ int acme_dqn_grad_split(const acme_dqn* l, int64_t* split) {
 
 // Adam (+ the parameter planes) and the periodic target copy; `copy` decided by the host.
 static int apply_impl(acme_dqn* l, bool copy, hipStream_t st) {
-  const bool jax = l->cfg.semantics == ACME_SEMANTICS_JAX;
   int rc;
-  {
-    // The parameter planes (plane path) are refreshed by the same pass.  t = num_steps + 1
-    // (snt.Adam / optix.adam count this step first).
+  if (l->slabs_pending) {  // the conv weight gradients reduced on Adam's read
+    l->slabs_pending = false;
     ACME_PROF("adam", st, 0.0, 28.0 * (double)l->logical);
-    rc = launch_adam(l->params, l->grads, l->m, l->v, l->flat, l->cfg.learning_rate,
-                     l->cfg.adam_beta1, l->cfg.adam_beta2, l->cfg.adam_epsilon, l->num_steps + 1,
-                     l->p3_capable ? l->wpl : nullptr, l->flat, st, jax ? 1 : 0, nullptr,
-                     l->p3_capable ? l->scales + kScParams : nullptr);
+    const int ten[3][2] = {{l->t_c1w, l->t_c1b}, {l->t_c2w, l->t_c2b}, {l->t_c3w, l->t_c3b}};
+    AdamSlabs a;
+    for (int k = 0; k < 3; ++k) {
+      const torso::WgradSlab& w = l->wslabs[k];
+      const int64_t count4 = (w.wcount + w.bcount) / 4;
+      for (int j = 0; j < 2; ++j) {
+        const Tensor& t = l->tensors[ten[k][j]];
+        a.seg[a.nseg++] = AdamSlabs::Seg{t.offset / 4, t.numel / 4, w.slab, w.splits, count4,
+                                         j ? w.wcount / 4 : 0};
+      }
+    }
+    a.dense_off4 = l->tensors[l->t_fcw].offset / 4;
+    a.dense_n4 = (l->flat - l->tensors[l->t_fcw].offset) / 4;
+    rc = launch_adam_slabs(l->params, l->grads, l->m, l->v, a, l->cfg.learning_rate,
+                           l->cfg.adam_beta1, l->cfg.adam_beta2, l->cfg.adam_epsilon,
+                           l->num_steps + 1, l->p3_capable ? l->wpl : nullptr, l->flat,
+                           l->p3_capable ? l->scales + kScParams : nullptr,
+                           l->cfg.semantics == ACME_SEMANTICS_JAX ? 1 : 0, st);
     if (rc != ACME_OK) return rc;
+  } else {
+    ACME_PROF("adam", st, 0.0, 28.0 * (double)l->logical);
+    if ((rc = adam_range(l, 0, l->flat, st)) != ACME_OK) return rc;
   }
   if (copy) {
     ACME_PROF("target_copy", st, 0.0, 8.0 * (double)l->logical);
@@ -1174,7 +1216,9 @@ int acme_dqn_apply(acme_dqn* l, void* stream) {
 static int step_impl(acme_dqn* l, const acme_transition_batch* batch, const acme_dqn_outputs* out,
                      bool copy, hipStream_t st) {
   int rc = forward_backward_stage(l, batch, out, 0, st, false);
+  l->fused_step = true;
   if (rc == ACME_OK) rc = forward_backward_stage(l, batch, out, 1, st, false);
+  l->fused_step = false;
   if (rc == ACME_OK) rc = apply_impl(l, copy, st);
   return rc;
 }

@@ -133,6 +133,27 @@ int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float l
                 float b2, float eps, int64_t t, uint16_t* planes, int64_t pstride, hipStream_t st,
                 int optix = 0, int64_t* dev_steps = nullptr, gemm::PScale* psc = nullptr);
 
+// launch_adam (snt.Adam, t >= 1) with some gradient ranges still split-K slabs: segment k
+// updates float4 [off4, off4 + n4) of the flat buffers from the deterministic reduction of
+// float4 [e4, e4 + n4) of a slab of `splits` rows of count4 float4 (the reduction and the
+// sums of launch_slab_reduce, bit for bit; the reduced gradient is also stored in g);
+// [dense_off4, dense_off4 + dense_n4) from g.  One launch.
+struct AdamSlabs {
+  static constexpr int kMaxSegs = 8;
+  struct Seg {
+    int64_t off4, n4;
+    const float* slab;
+    int splits;
+    int64_t count4, e4;
+  } seg[kMaxSegs];
+  int nseg = 0;
+  int block_end[kMaxSegs] = {};  // filled by the launcher
+  int64_t dense_off4 = 0, dense_n4 = 0;
+};
+int launch_adam_slabs(float* p, float* g, float* m, float* v, const AdamSlabs& slabs,
+                      float lr, float b1, float b2, float eps, int64_t t, uint16_t* planes,
+                      int64_t pstride, gemm::PScale* psc, int optix, hipStream_t st);
+
 // Two-plane split of n floats (n multiple of 4): planes[i * pstride + e], at the scale of
 // max |x| (sets the record sc: w, r = wi = 1 / w; overflow |= 1 on a non-finite x).
 // keep_scale: a record whose current read scale suits max |x| keeps it (checkpoint restore).

@@ -678,50 +678,109 @@ __global__ void __launch_bounds__(256) head_dz_planes_kernel(
   gemm::amax_commit(sc, mx);
 }
 
+// snt.Adam / optix.adam on float4 i of the flat buffers, the gradient given.
+struct AdamConsts {
+  float lr, b1, omb1, b2, omb2, bc1, bc2, eps;
+  int optix;
+};
+
+__device__ __forceinline__ void adam_update4(int64_t i, f32x4 gg, float* __restrict__ p,
+                                             float* __restrict__ m, float* __restrict__ v,
+                                             const AdamConsts& c, uint16_t* __restrict__ planes,
+                                             int64_t pstride, float pw) {
+  // The moments are streamed (read once, written once per step) with non-temporal
+  // accesses, so they bypass the caches the next step's forwards read the parameter planes
+  // through.
+  f32x4 mm = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(m) + i);
+  f32x4 vv = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(v) + i);
+  f32x4 pp = reinterpret_cast<f32x4*>(p)[i];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float mj = __fadd_rn(__fmul_rn(c.b1, mm[j]), __fmul_rn(c.omb1, gg[j]));
+    const float vj =
+        __fadd_rn(__fmul_rn(c.b2, vv[j]), __fmul_rn(c.omb2, __fmul_rn(gg[j], gg[j])));
+    const float mh = __fdiv_rn(mj, c.bc1);
+    const float vh = __fdiv_rn(vj, c.bc2);
+    const float den = __fadd_rn(__fsqrt_rn(vh), c.eps);
+    const float upd = c.optix ? __fmul_rn(c.lr, __fdiv_rn(mh, den))
+                              : __fdiv_rn(__fmul_rn(c.lr, mh), den);
+    mm[j] = mj;
+    vv[j] = vj;
+    pp[j] = __fsub_rn(pp[j], upd);
+  }
+  __builtin_nontemporal_store(mm, reinterpret_cast<f32x4*>(m) + i);
+  __builtin_nontemporal_store(vv, reinterpret_cast<f32x4*>(v) + i);
+  reinterpret_cast<f32x4*>(p)[i] = pp;
+  // (No amax here: a block handles about one float4 per thread, so a per-block
+  // reduction and atomic cost as much as the update; 45 -> 58 us measured.  The
+  // parameters' maximum is taken by launch_param_amax every few steps.)
+  if (planes) (void)store_planes4(planes, pstride, i, pp, pw);
+}
+
 __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p,
                                                    const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
-                                                   int64_t n4, float lr, float b1, float omb1,
-                                                   float b2, float omb2, float bc1, float bc2,
-                                                   float eps, uint16_t* __restrict__ planes,
+                                                   int64_t n4, AdamConsts c,
+                                                   uint16_t* __restrict__ planes,
                                                    int64_t pstride, gemm::PScale* __restrict__ psc,
-                                                   int optix,
                                                    const int64_t* __restrict__ dev_steps) {
   if (dev_steps) {  // device-side step count (graph replay): same expressions as the host's
     const float tf = (float)(*dev_steps + 1);
-    bc1 = 1.f - powf(b1, tf);
-    bc2 = 1.f - powf(b2, tf);
+    c.bc1 = 1.f - powf(c.b1, tf);
+    c.bc2 = 1.f - powf(c.b2, tf);
   }
   const float pw = planes ? psc->w : 0.f;
 #pragma unroll 2
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    // The gradient and the moments are streamed (read once, written once per step) with
-    // non-temporal accesses, so they bypass the caches the next step's forwards read the
-    // parameter planes through.
-    f32x4 gg = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(g) + i);
-    f32x4 mm = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(m) + i);
-    f32x4 vv = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(v) + i);
-    f32x4 pp = reinterpret_cast<f32x4*>(p)[i];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float mj = __fadd_rn(__fmul_rn(b1, mm[j]), __fmul_rn(omb1, gg[j]));
-      const float vj = __fadd_rn(__fmul_rn(b2, vv[j]), __fmul_rn(omb2, __fmul_rn(gg[j], gg[j])));
-      const float mh = __fdiv_rn(mj, bc1);
-      const float vh = __fdiv_rn(vj, bc2);
-      const float den = __fadd_rn(__fsqrt_rn(vh), eps);
-      const float upd = optix ? __fmul_rn(lr, __fdiv_rn(mh, den)) : __fdiv_rn(__fmul_rn(lr, mh), den);
-      mm[j] = mj;
-      vv[j] = vj;
-      pp[j] = __fsub_rn(pp[j], upd);
+       i += (int64_t)gridDim.x * blockDim.x)
+    adam_update4(i, __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(g) + i), p, m, v,
+                 c, planes, pstride, pw);
+}
+
+// Adam whose gradients for some ranges are still split-K slabs (the conv weight gradients
+// of the fused DQN step): the first blocks each reduce 16 float4 of a slab range exactly
+// as slab_reduce4_kernel does (16 split groups, the same addition order, so the same bits),
+// store the reduced gradient into g and update those parameters; the other blocks update
+// [dense_off4, dense_off4 + dense_n4) from g as adam_kernel does.
+__global__ void __launch_bounds__(256) adam_slabs_kernel(float* __restrict__ p,
+                                                         float* __restrict__ g,
+                                                         float* __restrict__ m,
+                                                         float* __restrict__ v, AdamSlabs s,
+                                                         AdamConsts c,
+                                                         uint16_t* __restrict__ planes,
+                                                         int64_t pstride,
+                                                         const gemm::PScale* __restrict__ psc) {
+  const float pw = planes ? psc->w : 0.f;
+  const int nsb = s.block_end[s.nseg - 1];
+  if ((int)blockIdx.x < nsb) {
+    __shared__ f32x4 red[16][16];
+    int k = 0;
+    while ((int)blockIdx.x >= s.block_end[k]) ++k;
+    const AdamSlabs::Seg& q = s.seg[k];
+    const int cc = threadIdx.x & 15, gq = threadIdx.x >> 4;
+    const int64_t f = (int64_t)(blockIdx.x - (k ? s.block_end[k - 1] : 0)) * 16 + cc;
+    const f32x4* s4 = reinterpret_cast<const f32x4*>(q.slab) + q.e4;
+    f32x4 acc{0.f, 0.f, 0.f, 0.f};
+    if (f < q.n4) {
+#pragma unroll 8
+      for (int sp = gq; sp < q.splits; sp += 16) acc += s4[(size_t)sp * q.count4 + f];
     }
-    __builtin_nontemporal_store(mm, reinterpret_cast<f32x4*>(m) + i);
-    __builtin_nontemporal_store(vv, reinterpret_cast<f32x4*>(v) + i);
-    reinterpret_cast<f32x4*>(p)[i] = pp;
-    // (No amax here: a block handles about one float4 per thread, so a per-block
-    // reduction and atomic cost as much as the update; 45 -> 58 us measured.  The
-    // parameters' maximum is taken by launch_param_amax every few steps.)
-    if (planes) (void)store_planes4(planes, pstride, i, pp, pw);
+    red[gq][cc] = acc;
+    __syncthreads();
+    if (gq == 0 && f < q.n4) {
+      f32x4 gg = red[0][cc];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) gg += red[r][cc];
+      reinterpret_cast<f32x4*>(g)[q.off4 + f] = gg;  // the step's gradient stays readable
+      adam_update4(q.off4 + f, gg, p, m, v, c, planes, pstride, pw);
+    }
+    return;
+  }
+  for (int64_t i = (int64_t)(blockIdx.x - nsb) * blockDim.x + threadIdx.x; i < s.dense_n4;
+       i += (int64_t)(gridDim.x - nsb) * blockDim.x) {
+    const int64_t j = s.dense_off4 + i;
+    adam_update4(j, __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(g) + j), p, m, v,
+                 c, planes, pstride, pw);
   }
 }
 
@@ -1148,22 +1207,45 @@ int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float l
   ACME_CHECK_ARG(n % 4 == 0, "adam buffer length must be a multiple of 4");
   ACME_CHECK_ARG(pstride % 4 == 0, "plane stride must be a multiple of 4");
   ACME_CHECK_ARG(t >= 1 || dev_steps, "adam step must be >= 1");
-  const float bc1 = dev_steps ? 0.f : 1.f - powf(b1, (float)t);
-  const float bc2 = dev_steps ? 0.f : 1.f - powf(b2, (float)t);
+  const AdamConsts c{lr, b1, 1.f - b1, b2, 1.f - b2,
+                     dev_steps ? 0.f : 1.f - powf(b1, (float)t),
+                     dev_steps ? 0.f : 1.f - powf(b2, (float)t), eps, optix};
   const int64_t n4 = n / 4;
-  const int gcap = tune_variant("ADAMG") > 0 ? tune_variant("ADAMG") : 8192;  // 47.7 -> 45.2 us vs 2048
-  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n4, 256), gcap);
-  // Non-temporal gradient / moment traffic: 45.8 -> 45.1 us, and the next step's forwards
-  // (which read the parameter planes) ~1 us faster each; step 0.689 -> 0.681 ms with the
-  // one-row head blocks (three alternating pairs on one box).
-  adam_kernel<<<std::max(grid, 1u), 256, 0, st>>>(p, g, m, v, n4, lr, b1, 1.f - b1, b2,
-                                                  1.f - b2, bc1, bc2, eps, planes, pstride,
-                                                  psc, optix, dev_steps);
+  // Grid cap 8192: 47.7 -> 45.2 us against 2048.  Non-temporal gradient / moment traffic:
+  // 45.8 -> 45.1 us, and the next step's forwards (which read the parameter planes) ~1 us
+  // faster each.
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n4, 256), 8192);
+  adam_kernel<<<std::max(grid, 1u), 256, 0, st>>>(p, g, m, v, n4, c, planes, pstride, psc,
+                                                  dev_steps);
   ACME_LAUNCH_CHECK();
   if (dev_steps) {
     count_step_kernel<<<1, 1, 0, st>>>(dev_steps);
     ACME_LAUNCH_CHECK();
   }
+  return ACME_OK;
+}
+
+int launch_adam_slabs(float* p, float* g, float* m, float* v, const AdamSlabs& slabs,
+                      float lr, float b1, float b2, float eps, int64_t t, uint16_t* planes,
+                      int64_t pstride, gemm::PScale* psc, int optix, hipStream_t st) {
+  ACME_CHECK_ARG(p && g && m && v && (!planes || psc), "null buffer");
+  ACME_CHECK_ARG(slabs.nseg >= 1 && slabs.nseg <= AdamSlabs::kMaxSegs && t >= 1,
+                 "bad slab Adam arguments");
+  AdamSlabs s = slabs;
+  int blocks = 0;
+  for (int k = 0; k < s.nseg; ++k) {
+    const AdamSlabs::Seg& q = s.seg[k];
+    ACME_CHECK_ARG(q.slab && q.splits >= 1 && q.n4 >= 1 && q.e4 + q.n4 <= q.count4,
+                   "bad slab segment %d", k);
+    blocks += (int)ceil_div(q.n4, 16);
+    s.block_end[k] = blocks;
+  }
+  const AdamConsts c{lr, b1, 1.f - b1, b2, 1.f - b2, 1.f - powf(b1, (float)t),
+                     1.f - powf(b2, (float)t), eps, optix};
+  const int dense = (int)std::min<int64_t>(ceil_div(s.dense_n4, 256), 8192);
+  adam_slabs_kernel<<<(unsigned)(blocks + std::max(dense, 1)), 256, 0, st>>>(
+      p, g, m, v, s, c, planes, pstride, psc);
+  ACME_LAUNCH_CHECK();
   return ACME_OK;
 }
 

@@ -80,10 +80,22 @@ int forward_p3(const PWeights& w, const Frames& frames, int rows, const PActs& a
 // Optional second stream for the weight gradients: conv3 / conv2 weight gradients run on
 // `side` (with their own split-K slab) beside the input gradients on the main stream;
 // events e[0..2] are scratch (hipEventDisableTiming).  side == nullptr: one stream.
+// A weight gradient left as its split-K slab: `splits` rows of (wcount + bcount) floats,
+// the weights' then the bias's partial sums (launch_slab_reduce's input).
+struct WgradSlab {
+  const float* slab = nullptr;
+  int splits = 0;
+  int64_t wcount = 0, bcount = 0;
+};
 struct Side {
   hipStream_t side = nullptr;
   float* slab = nullptr;
   hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+  // defer (optional, [3] = conv1, conv2, conv3): the weight gradients are not reduced but
+  // described here for the consumer (the fused step's Adam, launch_adam_slabs).  conv3 and
+  // conv2 then use `slab` and `slab2` (both needed, with or without the side stream).
+  float* slab2 = nullptr;
+  WgradSlab* defer = nullptr;
 };
 // dz3: conv3's dZ planes [rows][kFlat] (masked); dz2 / dz1 plane scratch.
 int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int rows,

@@ -276,8 +276,11 @@ int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int row
   // (two forks; one fork after conv3_dgrad saved an event record but measured 0.754 ->
   // 0.767 ms per step: the lost overlap costs more).
   const bool fork = sd.side != nullptr;
+  const bool defer = sd.defer != nullptr;
+  if (defer && !(sd.slab && sd.slab2))
+    return (set_error("deferred weight gradients need two side slabs"), ACME_ERR_INVALID);
   hipStream_t st = fork ? sd.side : st_main;
-  float* wslab = fork ? sd.slab : slab;
+  float* wslab = fork || defer ? sd.slab : slab;
   {  // conv3 weight + bias gradient
     if (fork) {
       ACME_HIP_TRY(hipEventRecord(sd.e[0], st_main));
@@ -290,7 +293,8 @@ int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int row
     p.a_src = src(a.x2, (int64_t)rows * kFlat); p.b_src = src(dz3, (int64_t)rows * kFlat);
     p.slab = wslab;
     P3_GEMM("conv3_wgrad", 128, 64, 2, 2, 32, p, splits);
-    if ((rc = p3_wgrad_reduce(p, splits, wslab, g.w3, g.b3, "conv3_wgrad_reduce", st)))
+    if (defer) sd.defer[2] = WgradSlab{wslab, splits, (int64_t)p.M * p.N, p.N};
+    else if ((rc = p3_wgrad_reduce(p, splits, wslab, g.w3, g.b3, "conv3_wgrad_reduce", st)))
       return rc;
   }
   st = st_main;
@@ -313,9 +317,11 @@ int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int row
     const int splits = kP3Conv2WgradSplits;
     p.k_chunk = chunk_for(p.K, splits);
     p.a_src = src(a.x1, (int64_t)rows * kX1); p.b_src = src(dz2, (int64_t)rows * kFlat);
-    p.slab = wslab;
+    float* slab2 = defer ? sd.slab2 : wslab;
+    p.slab = slab2;
     P3_GEMM("conv2_wgrad", 128, 64, 2, 2, 32, p, splits);
-    if ((rc = p3_wgrad_reduce(p, splits, wslab, g.w2, g.b2, "conv2_wgrad_reduce", st)))
+    if (defer) sd.defer[1] = WgradSlab{slab2, splits, (int64_t)p.M * p.N, p.N};
+    else if ((rc = p3_wgrad_reduce(p, splits, slab2, g.w2, g.b2, "conv2_wgrad_reduce", st)))
       return rc;
     if (fork) ACME_HIP_TRY(hipEventRecord(sd.e[2], sd.side));
   }
@@ -343,7 +349,8 @@ int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int row
     // Producer / consumer waves (gemm_p3ws_kernel): 28.5 -> 25.0 us, the same bits.
     if (tune_variant("WSN") == 1) P3_GEMM("conv1_wgrad", 256, 32, 4, 1, 32, p, splits);
     else P3WS_GEMM("conv1_wgrad", 256, 32, 4, 1, p, splits);
-    if ((rc = p3_wgrad_reduce(p, splits, slab, g.w1, g.b1, "conv1_wgrad_reduce", st)))
+    if (defer) sd.defer[0] = WgradSlab{slab, splits, (int64_t)p.M * p.N, p.N};
+    else if ((rc = p3_wgrad_reduce(p, splits, slab, g.w1, g.b1, "conv1_wgrad_reduce", st)))
       return rc;
   }
   if (fork) ACME_HIP_TRY(hipStreamWaitEvent(st_main, sd.e[2], 0));  // join
