@@ -700,9 +700,12 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
           if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
         if (e != hipSuccess)
           return fail((set_error("side stream: %s", hipGetErrorString(e)), ACME_ERR_HIP));
-        if ((rc = dev_alloc(l, &l->side_slab, l->slab_floats))) return fail(rc);
-        if ((rc = dev_alloc(l, &l->slab2, torso::wgrad_slab_floats_p3()))) return fail(rc);
       }
+      // The side stream's slab, and conv2's for the fused step's deferred reductions (also
+      // with one stream: ACME_V_SIDE=1 profiles the same kernels).
+      if ((rc = dev_alloc(l, &l->side_slab, l->slab_floats)) ||
+          (rc = dev_alloc(l, &l->slab2, torso::wgrad_slab_floats_p3())))
+        return fail(rc);
     }
   } else {
     ACME_CHECK_ARG(cfg->obs_dim >= 1, "obs_dim must be >= 1");
