@@ -73,10 +73,14 @@ struct acme_impala {
   int64_t* dev_step = nullptr;
   float* metrics_tmp = nullptr;
   float* norms = nullptr;
-  // Persistent LSTM forward: h_t exchange granules [2][B * H] (8 B: epoch tag | value bits)
-  // and the spin-timeout word, zeroed before every launch.
+  // Persistent LSTM unroll (H = 256, B <= 64): the forward's h_t granules [2][B * H] and the
+  // backward's partial-product granules [2][16][B * H] (8 B: tag | value bits), zeroed before
+  // every launch; the spin-timeout word.  lstm_steps: per-step launches instead (tests).
   unsigned long long* xg = nullptr;
+  unsigned long long* xb = nullptr;
   unsigned* tmo = nullptr;
+  bool lstm_steps = false;
+  unsigned lstm_epoch = 0;
   // Plane path of the Atari learner step (the DQN kernels: scaled two-plane f16 MFMA):
   // parameter planes of the torso + W_i prefix of the flat buffer, refreshed at the start
   // of every plane step; f16 frames; activation / gradient planes; its own split-K slab.
@@ -403,150 +407,338 @@ __global__ void __launch_bounds__(256) lstm_fwd_step_kernel(
   }
 }
 
-// ---------------------------------------------------------------- persistent forward
-// All T steps in ONE launch: H / kFwdUnits workgroups (co-resident: a cooperative launch),
-// each keeping its W_h columns in LDS for the whole unroll and its cells' c in registers.
-// Step t needs every unit's h_{t-1}: each workgroup publishes its h_t values as 8-byte
-// granules {tag = t + 1, value} with agent-scope relaxed atomic stores (write-through), and
-// one wave of every workgroup sweeps all B * H granules of step t - 1 (relaxed agent-scope
-// atomic loads) until every tag matches, then the workgroup computes.  The data is its own
-// flag (cdna_hip_programming.md Guideline 16, R2), the two granule buffers alternate by
-// step parity, and a workgroup cannot publish step t + 1 before every workgroup published
-// step t, so a buffer is only rewritten after all its readers are done.  Spins are
-// bounded: a timeout writes a code to `tmo` and every workgroup leaves the kernel.
+// ---------------------------------------------------------------- persistent unroll
+// The whole T-step LSTM forward (and, below, backward) in ONE launch for the Atari learner's
+// shape (H = 256): workgroup (rg, cg) owns kRgRows batch rows (a row group)
+// x kRgUnits units (cg), i.e. 4 * kRgUnits gate columns, and keeps its W_h slice (all 256 k
+// of those columns, 64 floats per thread) in registers for the whole unroll.  A step needs
+// h_{t-1} of its own rows only (the sequences are independent), so each workgroup exchanges
+// kRgRows x H values per step with the H / kRgUnits workgroups of its row group, as 8-byte
+// {tag, value} granules (agent-scope relaxed atomic stores and loads: the data is its own
+// flag, cdna_hip_programming.md G16 / MI355X_MICROARCH.md "handoff-1to1"; 4 granules per
+// thread per step).  Two granule buffers alternate by step parity; a workgroup cannot
+// publish step t + 1 before every workgroup of its row group has published step t, i.e.
+// finished reading step t - 1, so a buffer is only rewritten after its readers are done.
+// Spins are bounded: a timeout writes `tmo` and every workgroup leaves the kernel (the
+// step's logged losses then read NaN).  The workgroups must be co-resident: at most 256 of
+// them (B <= 64), 256 threads and 21 KB of LDS each, which an idle MI355X dispatches at once;
+// hipLaunchCooperativeKernel would guarantee it but measured a 13.5 us gap before and after
+// each launch, against 55 and 48 us for the kernels.  Granule tags carry a per-launch epoch
+// (next_lstm_tags), so the buffers are not cleared between launches.
+// (Round 2's persistent kernel split the columns only, so every workgroup swept all B * H
+// granules of every step: 16 us per step against 8 us of per-step launches.  Here a step
+// takes 2.5 us: the hand-off 0.9, the mat-vec 0.6, the cell update 0.7.)
 using gu64 = __attribute__((address_space(1))) unsigned long long;
 using gu32 = __attribute__((address_space(1))) unsigned;
 constexpr unsigned kSpinLimit = 1u << 22;
+constexpr int kRgH = 256;     // hidden size of the persistent kernels
+constexpr int kRgRows = 4;    // batch rows per row group
+constexpr int kRgUnits = 16;  // units per workgroup: 64 gate columns
+constexpr int kRgCols = 4 * kRgUnits;
+constexpr int kRgGroups = kRgH / kRgUnits;  // workgroups per row group
+constexpr int kRgMaxB = 64;                 // 16 row groups x 16 = 256 workgroups
 
 __device__ __forceinline__ void put_granule(unsigned long long* g, unsigned tag, float v) {
-  __hip_atomic_store((gu64*)(g),
-                     ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store((gu64*)(g), ((unsigned long long)tag << 32) | __float_as_uint(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// One wave: copies the n granules of g (tag `tag`) into dst as floats; false on timeout.
-__device__ bool sweep_into(const unsigned long long* g, int n, unsigned tag, float* dst,
-                           unsigned* tmo) {
-  const int lane = threadIdx.x & 63;
-  constexpr int CH = 16;  // granules per lane per pass
-  for (int base = 0; base < n; base += 64 * CH) {
-    unsigned long long v[CH];
-    for (unsigned spins = 0;; ++spins) {
-      bool ok = true;
+// Waits until the N granules at g[i * stride] (per-thread list, `live` masks absent rows)
+// carry `tag`, then returns their values; false on timeout (after writing `tmo`).
+template <int N>
+__device__ bool take_granules(const unsigned long long* const (&g)[N], const bool (&live)[N],
+                              unsigned tag, float (&out)[N], unsigned* tmo) {
+  for (unsigned spins = 0;; ++spins) {
+    bool ok = true;
 #pragma unroll
-      for (int k = 0; k < CH; ++k) {
-        const int i = base + k * 64 + lane;
-        v[k] = i < n ? __hip_atomic_load((const gu64*)(g + i), __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT)
-                     : ((unsigned long long)tag << 32);
-        ok &= (unsigned)(v[k] >> 32) == tag;
-      }
-      if (__all(ok)) break;
-      if (spins >= kSpinLimit) {
-        if (lane == 0)
-          __hip_atomic_store((gu32*)(tmo), 1u, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-        return false;
-      }
-      __builtin_amdgcn_s_sleep(1);
+    for (int k = 0; k < N; ++k) {
+      const unsigned long long v =
+          live[k] ? __hip_atomic_load((const gu64*)(g[k]), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT)
+                  : ((unsigned long long)tag << 32);
+      out[k] = __uint_as_float((unsigned)v);
+      ok &= (unsigned)(v >> 32) == tag;
     }
-#pragma unroll
-    for (int k = 0; k < CH; ++k) {
-      const int i = base + k * 64 + lane;
-      if (i < n) dst[i] = __uint_as_float((unsigned)v[k]);
+    if (__all(ok)) return true;
+    if (spins >= kSpinLimit) {
+      if ((threadIdx.x & 63) == 0)
+        __hip_atomic_store((gu32*)(tmo), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
     }
+    __builtin_amdgcn_s_sleep(1);
   }
-  return true;
 }
 
-__global__ void __launch_bounds__(256) lstm_fwd_persistent_kernel(
+using f32x2 = __attribute__((ext_vector_type(2))) float;
+
+// Rows (r, r + 1) of a mat-vec in one packed FMA (v_pk_fma_f32): each row's sum keeps its
+// own order, so the result is the scalar loop's.
+__device__ __forceinline__ f32x2 fma2(float a0, float a1, float w, f32x2 acc) {
+  return __builtin_elementwise_fma(f32x2{a0, a1}, f32x2{w, w}, acc);
+}
+
+// Global gate column of this workgroup's gate column `col` (gate q = col / kRgUnits).
+__device__ __forceinline__ int rg_gate_col(int cg, int col) {
+  return (col / kRgUnits) * kRgH + cg * kRgUnits + col % kRgUnits;
+}
+
+// Forward: thread (ks = wave, col = lane) accumulates 4 rows x its gate column over the
+// wave's 64-k slice (W in registers, h_{t-1} broadcast from LDS); the four slices are summed
+// in order with gx; threads < 64 run the cells (c in registers across the unroll).
+__global__ void __launch_bounds__(256) lstm_fwd_rg_kernel(
     const float* __restrict__ gx, const float* __restrict__ wh, const float* __restrict__ h0,
-    int64_t h0_stride, const float* __restrict__ c0, int64_t c0_stride, int B, int T, int H,
+    int64_t h0_stride, const float* __restrict__ c0, int64_t c0_stride, int B, int T,
     float* __restrict__ gates, float* __restrict__ h_out, float* __restrict__ c_out,
-    unsigned long long* xg, unsigned* tmo) {
-  constexpr int NC = 4 * kFwdUnits;
-  constexpr int KS = 256 / NC;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* hs = smem;                            // [B][H]
-  float* ws = hs + (size_t)B * H;              // [H][NC]
-  float* red = ws + (size_t)H * NC;            // [KS][kRowChunk][NC]
-  float* zs = red + KS * kRowChunk * NC;       // [B][NC]
+    unsigned long long* xg, unsigned tag0, unsigned* tmo) {
+  constexpr int H = kRgH, R = kRgRows, U = kRgUnits, NC = kRgCols;
+  __shared__ __attribute__((aligned(16))) float hs[R][H];
+  __shared__ float red[16][R][NC];
   __shared__ int s_fail;
-  const int u0 = blockIdx.x * kFwdUnits;
-  const int BH = B * H;
-  if (threadIdx.x == 0) s_fail = 0;
-  for (int e = threadIdx.x; e < H * 4; e += blockDim.x) {  // W_h columns, once
-    const int k = e / 4, q = e % 4;
-    *reinterpret_cast<f32x4*>(ws + (size_t)k * NC + q * kFwdUnits) =
-        *reinterpret_cast<const f32x4*>(wh + (size_t)k * 4 * H + q * H + u0);
+  const int RG = (B + R - 1) / R;
+  const int rg = blockIdx.x % RG, cg = blockIdx.x / RG;  // a row group's blocks: equal % 8
+  const int b0 = rg * R;
+  // Mat-vec thread: 4 gate columns (4 cq .. 4 cq + 3) x the 16-k slice ks: each h value read
+  // from LDS feeds 4 columns x 2 rows (LDS return bandwidth, not the FMAs, bounds the step).
+  const int tid = threadIdx.x, cq = tid & 15, ks = tid >> 4;
+  if (tid == 0) s_fail = 0;
+  float w[4][16];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int gc = rg_gate_col(cg, 4 * cq + c);
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) w[c][kk] = wh[(size_t)(ks * 16 + kk) * 4 * H + gc];
   }
-  const bool cell_thread = (int)threadIdx.x < B * kFwdUnits;
-  const int cb = threadIdx.x / kFwdUnits, cu = threadIdx.x % kFwdUnits;
-  float creg = cell_thread ? c0[(size_t)cb * c0_stride + u0 + cu] : 0.f;
-  const int c = threadIdx.x % NC, sl = threadIdx.x / NC;
+  // Cell threads: (row, unit) = (tid / U, tid % U) for tid < R * U.
+  const bool cell = tid < R * U;
+  const int crow = tid / U, cu = tid % U, cb = min(b0 + crow, B - 1), cj = cg * U + cu;
+  const bool cell_live = cell && b0 + crow < B;
+  float creg = cell ? c0[(size_t)cb * c0_stride + cj] : 0.f;
+  // The 4 h_{t-1} values this thread brings into LDS: e = 4 tid + i -> (row e / H, unit).
+  const unsigned long long* gp[4];
+  bool glive[4];
   for (int t = 0; t < T; ++t) {
+    // The cell's gx terms (its four gate columns), in flight early.
+    float gxv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      gxv[q] = cell ? gx[((size_t)cb * T + t) * 4 * H + q * H + cj] : 0.f;
+    float hv[4];
     if (t == 0) {
-      for (int e = threadIdx.x; e < BH / 4; e += blockDim.x) {
-        const int b = e / (H / 4), k = 4 * (e % (H / 4));
-        *reinterpret_cast<f32x4*>(hs + (size_t)b * H + k) =
-            *reinterpret_cast<const f32x4*>(h0 + (size_t)b * h0_stride + k);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int e = 4 * tid + i, r = e / H, u = e % H;
+        hv[i] = h0[(size_t)min(b0 + r, B - 1) * h0_stride + u];
       }
     } else {
-      // Every wave sweeps its quarter of the granules (one pass of 16 per lane at B*H = 4096).
-      const int wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
-      const int per = (BH + nw - 1) / nw, lo = wv * per;
-      const int cnt = lo < BH ? min(per, BH - lo) : 0;
-      if (!sweep_into(xg + (size_t)((t - 1) & 1) * BH + lo, cnt, (unsigned)t, hs + lo, tmo) &&
-          (threadIdx.x & 63) == 0)
-        s_fail = 1;
+      const unsigned long long* base = xg + (size_t)((t - 1) & 1) * B * H;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int e = 4 * tid + i, r = e / H, u = e % H;
+        glive[i] = b0 + r < B;
+        gp[i] = base + (size_t)min(b0 + r, B - 1) * H + u;
+      }
+      if (!take_granules<4>(gp, glive, tag0 + (unsigned)t, hv, tmo)) s_fail = 1;
+    }
+    *reinterpret_cast<f32x4*>(&hs[0][0] + 4 * tid) = f32x4{hv[0], hv[1], hv[2], hv[3]};
+    __syncthreads();
+    if (s_fail) return;  // every workgroup leaves on a timeout (its own wait fails too)
+    f32x2 a01[4], a23[4];  // per column: rows (0, 1) and (2, 3)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) a01[c] = a23[c] = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int k4 = 0; k4 < 4; ++k4) {
+      const f32x4 h0v = *reinterpret_cast<const f32x4*>(&hs[0][ks * 16 + 4 * k4]);
+      const f32x4 h1v = *reinterpret_cast<const f32x4*>(&hs[1][ks * 16 + 4 * k4]);
+      const f32x4 h2v = *reinterpret_cast<const f32x4*>(&hs[2][ks * 16 + 4 * k4]);
+      const f32x4 h3v = *reinterpret_cast<const f32x4*>(&hs[3][ks * 16 + 4 * k4]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          a01[c] = fma2(h0v[j], h1v[j], w[c][4 * k4 + j], a01[c]);
+          a23[c] = fma2(h2v[j], h3v[j], w[c][4 * k4 + j], a23[c]);
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      red[ks][0][4 * cq + c] = a01[c][0];
+      red[ks][1][4 * cq + c] = a01[c][1];
+      red[ks][2][4 * cq + c] = a23[c][0];
+      red[ks][3][4 * cq + c] = a23[c][1];
     }
     __syncthreads();
-    if (s_fail) return;  // every workgroup leaves on a timeout (its sweep fails too)
-    for (int b0 = 0; b0 < B; b0 += kRowChunk) {
-      const int oi = threadIdx.x / NC, occ = threadIdx.x % NC, ob = b0 + oi;
-      const float gxv = ob < B ? gx[((size_t)ob * T + t) * 4 * H + (occ / kFwdUnits) * H + u0 +
-                                    (occ % kFwdUnits)]
-                               : 0.f;
-      float acc[kRowChunk];
+    if (cell) {
+      // z = gx + the 16 k-slices' partial sums, in order.
+      float z[4];
 #pragma unroll
-      for (int i = 0; i < kRowChunk; ++i) acc[i] = 0.f;
-      int roff[kRowChunk];  // clamped rows, as lstm_fwd_step_kernel
+      for (int q = 0; q < 4; ++q) {
+        const int cc = q * U + cu;
+        float sum = red[0][crow][cc];
 #pragma unroll
-      for (int i = 0; i < kRowChunk; ++i) roff[i] = min(b0 + i, B - 1) * H;
-      for (int k = sl; k < H; k += KS) {
-        const float w = ws[k * NC + c];
-#pragma unroll
-        for (int i = 0; i < kRowChunk; ++i) acc[i] = fmaf(hs[roff[i] + k], w, acc[i]);
+        for (int k = 1; k < 16; ++k) sum += red[k][crow][cc];
+        z[q] = gxv[q] + sum;
       }
-#pragma unroll
-      for (int i = 0; i < kRowChunk; ++i) red[(sl * kRowChunk + i) * NC + c] = acc[i];
-      __syncthreads();
-      if (ob < B) {
-        float z = 0.f;
-        for (int s2 = 0; s2 < KS; ++s2) z += red[(s2 * kRowChunk + oi) * NC + occ];
-        zs[ob * NC + occ] = gxv + z;
-      }
-      __syncthreads();
-    }
-    if (cell_thread) {
-      const float* z = zs + (size_t)cb * NC;
-      const float ig = sigmoidf(z[cu]), fg = sigmoidf(z[kFwdUnits + cu]);
-      const float gg = tanhf(z[2 * kFwdUnits + cu]), og = sigmoidf(z[3 * kFwdUnits + cu]);
+      const float ig = sigmoidf(z[0]), fg = sigmoidf(z[1]);
+      const float gg = tanhf(z[2]), og = sigmoidf(z[3]);
       const float cn = __fadd_rn(__fmul_rn(fg, creg), __fmul_rn(ig, gg));
       const float hn = __fmul_rn(og, tanhf(cn));
       creg = cn;
-      const int j = u0 + cu;
-      const size_t row = (size_t)cb * T + t;
-      gates[row * 4 * H + j] = ig;
-      gates[row * 4 * H + H + j] = fg;
-      gates[row * 4 * H + 2 * H + j] = gg;
-      gates[row * 4 * H + 3 * H + j] = og;
-      c_out[row * H + j] = cn;
-      h_out[row * H + j] = hn;
-      if (t + 1 < T) put_granule(xg + (size_t)(t & 1) * BH + (size_t)cb * H + j, (unsigned)(t + 1), hn);
+      if (cell_live) {
+        const size_t row = (size_t)cb * T + t;
+        gates[row * 4 * H + cj] = ig;
+        gates[row * 4 * H + H + cj] = fg;
+        gates[row * 4 * H + 2 * H + cj] = gg;
+        gates[row * 4 * H + 3 * H + cj] = og;
+        c_out[row * H + cj] = cn;
+        h_out[row * H + cj] = hn;
+        if (t + 1 < T) put_granule(xg + (size_t)(t & 1) * B * H + (size_t)cb * H + cj,
+                                   tag0 + (unsigned)(t + 1), hn);
+      }
     }
-    __syncthreads();  // hs / zs are rewritten by the next step
   }
+}
+
+// Backward: per step t (T-1 .. 0) the cells of (row group, unit group) take dh = dh_head +
+// the partial products published at step t + 1 (summed over the 16 producers in order),
+// form their gate gradients (dgates, stored) and carry dc in registers; then thread u' (one
+// per unit) forms this workgroup's partial product for dh_{t-1}: sum over its 64 gate
+// columns g (in order) of dgates[row][g] W_h[u'][g], W_h row slice in registers, and
+// publishes the 4 rows x 256 values, each consumer reading its 16 units of every producer.
+__global__ void __launch_bounds__(256) lstm_bwd_rg_kernel(
+    const float* __restrict__ dh_head, const float* __restrict__ wh,
+    const float* __restrict__ gates, const float* __restrict__ c_all,
+    const float* __restrict__ c0, int64_t c0_stride, int B, int T,
+    float* __restrict__ dgates, unsigned long long* xb, unsigned tag0, unsigned* tmo) {
+  constexpr int H = kRgH, R = kRgRows, U = kRgUnits, NC = kRgCols, G = kRgGroups;
+  __shared__ float pp[G][R][U];
+  __shared__ __attribute__((aligned(16))) float dgs[R][NC];
+  __shared__ float red[4][R][H];
+  __shared__ int s_fail;
+  const int RG = (B + R - 1) / R;
+  const int rg = blockIdx.x % RG, cg = blockIdx.x / RG;
+  const int b0 = rg * R;
+  const int tid = threadIdx.x;
+  // Partial-product thread: units 4 uq .. 4 uq + 3 x the 16 gate columns of slice gs.
+  const int uq = tid & 63, gs = tid >> 6;
+  if (tid == 0) s_fail = 0;
+  float w[4][16];  // W_h[4 uq + uu][this workgroup's gate column 16 gs + gg]
+#pragma unroll
+  for (int uu = 0; uu < 4; ++uu)
+#pragma unroll
+    for (int gg = 0; gg < 16; ++gg)
+      w[uu][gg] = wh[(size_t)(4 * uq + uu) * 4 * H + rg_gate_col(cg, 16 * gs + gg)];
+  const bool cell = tid < R * U;
+  const int crow = tid / U, cu = tid % U, cb = min(b0 + crow, B - 1), cj = cg * U + cu;
+  const bool cell_live = cell && b0 + crow < B;
+  float dcarry = 0.f;
+  // Granules this thread takes: e = 4 tid + i -> (producer e / (R U), row, unit).
+  const unsigned long long* gp[4];
+  bool glive[4];
+  for (int t = T - 1; t >= 0; --t) {
+    const size_t row = (size_t)cb * T + t;
+    // Cell operands, loaded before the wait.
+    float ig = 0.f, fg = 0.f, gg = 0.f, og = 0.f, cn = 0.f, cprev = 0.f, dhh = 0.f;
+    if (cell) {
+      const float* gr = gates + row * 4 * H;
+      ig = gr[cj]; fg = gr[H + cj]; gg = gr[2 * H + cj]; og = gr[3 * H + cj];
+      cn = c_all[row * H + cj];
+      cprev = t > 0 ? c_all[(row - 1) * H + cj] : c0[(size_t)cb * c0_stride + cj];
+      dhh = dh_head[row * H + cj];
+    }
+    if (t + 1 < T) {
+      const unsigned long long* base = xb + (size_t)((t + 1) & 1) * G * B * H;
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int e = 4 * tid + i, pg = e / (R * U), r = (e / U) % R, u = e % U;
+        glive[i] = b0 + r < B;
+        gp[i] = base + ((size_t)pg * B + min(b0 + r, B - 1)) * H + cg * U + u;
+      }
+      if (!take_granules<4>(gp, glive, tag0 + (unsigned)(t + 1), v, tmo)) s_fail = 1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int e = 4 * tid + i;
+        (&pp[0][0][0])[e] = v[i];
+      }
+    }
+    __syncthreads();
+    if (s_fail) return;
+    if (cell) {
+      float dhn = 0.f;
+      if (t + 1 < T)
+        for (int pg = 0; pg < G; ++pg) dhn += pp[pg][crow][cu];
+      const float tc = tanhf(cn);
+      const float dh = dhh + dhn;
+      const float dc = dcarry + dh * og * (1.f - tc * tc);
+      const float di = dc * gg * ig * (1.f - ig), df = dc * cprev * fg * (1.f - fg);
+      const float dg = dc * ig * (1.f - gg * gg), dO = dh * tc * og * (1.f - og);
+      dcarry = dc * fg;
+      dgs[crow][cu] = di;
+      dgs[crow][U + cu] = df;
+      dgs[crow][2 * U + cu] = dg;
+      dgs[crow][3 * U + cu] = dO;
+      if (cell_live) {
+        float* d = dgates + row * 4 * H;
+        d[cj] = di;
+        d[H + cj] = df;
+        d[2 * H + cj] = dg;
+        d[3 * H + cj] = dO;
+      }
+    }
+    __syncthreads();
+    if (t > 0) {
+      f32x2 a01[4], a23[4];  // per unit: rows (0, 1) and (2, 3)
+#pragma unroll
+      for (int uu = 0; uu < 4; ++uu) a01[uu] = a23[uu] = f32x2{0.f, 0.f};
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const f32x4 d0 = *reinterpret_cast<const f32x4*>(&dgs[0][16 * gs + 4 * g4]);
+        const f32x4 d1 = *reinterpret_cast<const f32x4*>(&dgs[1][16 * gs + 4 * g4]);
+        const f32x4 d2 = *reinterpret_cast<const f32x4*>(&dgs[2][16 * gs + 4 * g4]);
+        const f32x4 d3 = *reinterpret_cast<const f32x4*>(&dgs[3][16 * gs + 4 * g4]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int uu = 0; uu < 4; ++uu) {
+            a01[uu] = fma2(d0[j], d1[j], w[uu][4 * g4 + j], a01[uu]);
+            a23[uu] = fma2(d2[j], d3[j], w[uu][4 * g4 + j], a23[uu]);
+          }
+      }
+#pragma unroll
+      for (int uu = 0; uu < 4; ++uu) {
+        red[gs][0][4 * uq + uu] = a01[uu][0];
+        red[gs][1][4 * uq + uu] = a01[uu][1];
+        red[gs][2][4 * uq + uu] = a23[uu][0];
+        red[gs][3][4 * uq + uu] = a23[uu][1];
+      }
+      __syncthreads();
+      // Thread u' = tid publishes this workgroup's partial for its unit, 4 rows (the four
+      // gate-column slices summed in order).
+      unsigned long long* out = xb + (size_t)(t & 1) * G * B * H + (size_t)cg * B * H;
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (b0 + r < B)
+          put_granule(out + (size_t)(b0 + r) * H + tid, tag0 + (unsigned)t,
+                      ((red[0][r][tid] + red[1][r][tid]) + red[2][r][tid]) + red[3][r][tid]);
+    }
+  }
+}
+
+// The persistent unroll's shape: H = 256 and at most 64 rows (256 co-resident workgroups).
+bool lstm_persistent(const acme_impala* l, int B) {
+  return l->H == kRgH && B <= kRgMaxB && l->xb && !l->lstm_steps;
+}
+
+// The granule tags of the next persistent launch: tag0 + t, tag0 = 128 x a per-learner launch
+// count, so no launch can match a granule an earlier one left (the buffers are never cleared
+// between launches); the buffers are cleared once the count wraps.
+unsigned next_lstm_tags(acme_impala* l, hipStream_t st) {
+  if (++l->lstm_epoch >= (1u << 24)) {
+    l->lstm_epoch = 1;
+    (void)hipMemsetAsync(l->xg, 0, (size_t)2 * l->cfg.max_batch * l->H * 8, st);
+    (void)hipMemsetAsync(l->xb, 0, (size_t)2 * kRgGroups * l->cfg.max_batch * l->H * 8, st);
+  }
+  return l->lstm_epoch << 7;
 }
 
 size_t lstm_fwd_smem(int B, int H) {
@@ -690,6 +882,7 @@ struct LossArgs {
   float* dpv;
   float *vs, *pg_adv;  // [(T-1) * B] time-major
   float* metrics;      // [4]
+  const unsigned* lstm_timeout;  // sticky: a persistent LSTM launch timed out (logs NaN)
 };
 
 __global__ void __launch_bounds__(256) impala_rowstats_kernel(const LossArgs a) {
@@ -760,10 +953,11 @@ __global__ void __launch_bounds__(64) impala_vtrace_kernel(const LossArgs a) {
     pg *= invN;
     cr *= invN;
     en *= invN;
-    a.metrics[0] = pg + a.baseline_cost * cr + a.entropy_cost * en;
-    a.metrics[1] = cr;
-    a.metrics[2] = en;
-    a.metrics[3] = pg;
+    const float bad = a.lstm_timeout && *a.lstm_timeout ? NAN : 0.f;
+    a.metrics[0] = pg + a.baseline_cost * cr + a.entropy_cost * en + bad;
+    a.metrics[1] = cr + bad;
+    a.metrics[2] = en + bad;
+    a.metrics[3] = pg + bad;
   }
 }
 
@@ -1001,22 +1195,12 @@ int network_forward(acme_impala* l, const void* obs, const int32_t* prev_a, cons
   {
     ACME_PROF("impala_lstm_fwd", st, 2.0 * rows * (double)H * 4 * H, 0.0);
     const size_t smem = lstm_fwd_smem(B, H);
-    if (T > 1 && tune_variant("LSTMP") == 2 && l->xg) {
-      // One cooperative launch for the whole unroll (lstm_fwd_persistent_kernel).  Opt-in:
-      // measured 328-352 us for T = 20 at B = 16, H = 256 against 20 x 16 us of per-step
-      // launches: a step is bound by its dependent phases (the h_{t-1} exchange or load,
-      // the k-sliced reduction, the cell update), not by the launch.
-      ACME_HIP_TRY(hipMemsetAsync(l->xg, 0, (size_t)2 * B * H * sizeof(unsigned long long), st));
-      const float* wh = P(l, l->params, l->t_wh);
-      float *g = l->gates, *ho = l->h, *co = l->c;
-      unsigned long long* xg = l->xg;
-      unsigned* tmo = l->tmo;
-      int Bv = B, Tv = T, Hv = H;
-      int64_t hs0 = state_stride, cs0 = state_stride;
-      const float* gxp = l->gx;
-      void* args[] = {&gxp, &wh, &h0, &hs0, &c0, &cs0, &Bv, &Tv, &Hv, &g, &ho, &co, &xg, &tmo};
-      ACME_HIP_TRY(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(lstm_fwd_persistent_kernel),
-                                              dim3(H / kFwdUnits), dim3(256), args, smem, st));
+    if (lstm_persistent(l, B)) {  // one launch for the whole unroll (lstm_fwd_rg_kernel)
+      const unsigned tag0 = next_lstm_tags(l, st);
+      lstm_fwd_rg_kernel<<<(unsigned)(ceil_div(B, kRgRows) * kRgGroups), 256, 0, st>>>(
+          l->gx, P(l, l->params, l->t_wh), h0, state_stride, c0, state_stride, B, T, l->gates,
+          l->h, l->c, l->xg, tag0, l->tmo);
+      IM_CHECK();
     } else
     for (int t = 0; t < T; ++t) {
       const float* hp = t == 0 ? h0 : l->h + (size_t)(t - 1) * H;
@@ -1068,6 +1252,7 @@ int impala_step_impl(acme_impala* l, const acme_sequence_batch* bt, float* metri
     a.dpv = l->dpv; a.vs = l->vs; a.pg_adv = l->pg_adv;
     a.lrho = l->lrho; a.lpa = l->lpa; a.ent = l->ent;
     a.metrics = metrics ? metrics : l->metrics_tmp;
+    a.lstm_timeout = l->tmo;
     const unsigned rb = (unsigned)ceil_div(rows, 4);
     impala_rowstats_kernel<<<rb, 256, 0, st>>>(a);
     IM_CHECK();
@@ -1101,12 +1286,20 @@ int impala_step_impl(acme_impala* l, const acme_sequence_batch* bt, float* metri
   }
   {  // BPTT
     ACME_PROF("impala_lstm_bwd", st, 2.0 * rows * (double)H * 4 * H, 0.0);
+    if (lstm_persistent(l, B)) {  // one launch for the whole BPTT (lstm_bwd_rg_kernel)
+      const unsigned tag0 = next_lstm_tags(l, st);
+      lstm_bwd_rg_kernel<<<(unsigned)(ceil_div(B, kRgRows) * kRgGroups), 256, 0, st>>>(
+          l->dh, P(l, l->params, l->t_wh), l->gates, l->c, bt->c0, bt->state_stride, B, T,
+          l->dgates, l->xb, tag0, l->tmo);
+      IM_CHECK();
+    } else {
     ACME_HIP_TRY(hipMemsetAsync(l->dc, 0, (size_t)B * H * sizeof(float), st));
     for (int t = T - 1; t >= 0; --t) {
       lstm_bwd_step_kernel<<<H / kUnits, 256, 0, st>>>(l->dh, P(l, l->params, l->t_wh), l->gates,
                                                        l->c, bt->c0, bt->state_stride, l->dc,
                                                        l->dgates, B, T, t, H);
       IM_CHECK();
+    }
     }
   }
   {  // LSTM weights: W_h over h_prev, W_i (+ b via colsum) over the OAR embedding
@@ -1223,7 +1416,10 @@ int acme_impala_create(const acme_impala_config* cfg, acme_impala** out) {
                  "max_sequence_length must be in [2, 64]");
   ACME_CHECK_ARG(cfg->lstm_size >= 8 && cfg->lstm_size % 8 == 0,
                  "lstm_size must be a positive multiple of 8");
-  ACME_CHECK_ARG(lstm_fwd_smem(cfg->max_batch, cfg->lstm_size) <= 65536,
+  // The per-step forward stages h_prev of every row in LDS; the one-launch unroll (lstm_size
+  // 256, at most 64 sequences) does not.
+  ACME_CHECK_ARG(lstm_fwd_smem(cfg->max_batch, cfg->lstm_size) <= 65536 ||
+                     (cfg->lstm_size == kRgH && cfg->max_batch <= kRgMaxB),
                  "max_batch * lstm_size + 16 * lstm_size must stay within 64 KB of LDS");
   ACME_CHECK_ARG(cfg->head_size >= 4 && cfg->head_size % 4 == 0,
                  "head_size must be a positive multiple of 4");
@@ -1279,6 +1475,9 @@ int acme_impala_create(const acme_impala_config* cfg, acme_impala** out) {
       (rc = dev_alloc(l, &l->metrics_tmp, 4)) || (rc = dev_alloc(l, &l->norms, 2)) ||
       (rc = dev_alloc(l, &l->xg, (int64_t)2 * B * H)) || (rc = dev_alloc(l, &l->tmo, 4)))
     return fail(rc);
+  if (H == kRgH && B <= kRgMaxB &&
+      (rc = dev_alloc(l, &l->xb, (int64_t)2 * kRgGroups * B * H)))
+    return fail(rc);
   // Plane path (Atari torso): each operand plane is addressed through a 31-bit byte range,
   // so the f16 frames of one step bound it (R < 38,000 frames); larger unrolls stay f32.
   if (cfg->torso == ACME_IMPALA_TORSO_ATARI && R * torso::kObsBytes * 2 < (int64_t)INT32_MAX &&
@@ -1315,13 +1514,23 @@ int acme_impala_create(const acme_impala_config* cfg, acme_impala** out) {
       return fail(rc);
   }
   if (hipMemset(l->dev_step, 0, sizeof(int64_t)) != hipSuccess ||
-      hipMemset(l->tmo, 0, 4 * sizeof(unsigned)) != hipSuccess)
+      hipMemset(l->tmo, 0, 4 * sizeof(unsigned)) != hipSuccess ||
+      (l->xg && hipMemset(l->xg, 0, (size_t)2 * B * H * 8) != hipSuccess) ||
+      (l->xb && hipMemset(l->xb, 0, (size_t)2 * kRgGroups * B * H * 8) != hipSuccess))
     return fail((set_error("hipMemset failed"), ACME_ERR_HIP));
   *out = l;
   return ACME_OK;
 }
 
 int64_t acme_impala_flat_size(const acme_impala* l) { return l ? l->flat : 0; }
+
+int acme_impala_set_lstm_unroll(acme_impala* l, int32_t mode) {
+  ACME_CHECK_ARG(l && (mode == 0 || mode == 1), "mode must be 0 (auto) or 1 (per-step)");
+  ACME_CHECK_ARG(mode == 0 || lstm_fwd_smem(l->cfg.max_batch, l->H) <= 65536,
+                 "per-step launches need max_batch * lstm_size within 64 KB of LDS");
+  l->lstm_steps = mode == 1;
+  return ACME_OK;
+}
 int32_t acme_impala_num_tensors(const acme_impala* l) { return l ? (int32_t)l->tensors.size() : 0; }
 
 int acme_impala_tensor_info(const acme_impala* l, int32_t i, int64_t* offset, int64_t* numel,

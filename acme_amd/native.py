@@ -796,6 +796,10 @@ class NativeIMPALA:
               "impala plane_overflow")
         return bool(v.value)
 
+    def set_lstm_unroll(self, per_step: bool) -> None:
+        """Per-step LSTM launches instead of the one-launch unroll (tests compare the two)."""
+        check(lib().acme_impala_set_lstm_unroll(self._h, 1 if per_step else 0), "lstm unroll")
+
     def step(self, observation, prev_action, prev_reward, action, reward, discount,
              behaviour_logits, h0, c0, stream=None):
         """Batch-major [B, T, ...] device tensors; h0 / c0 are [B, H] views (any row stride

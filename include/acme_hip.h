@@ -524,6 +524,12 @@ int acme_impala_step(acme_impala* l, const acme_sequence_batch* batch, float* me
                      void* stream);
 /* Plane-range check of the Atari plane path (as acme_dqn_plane_overflow). */
 int acme_impala_plane_overflow(acme_impala* l, int32_t* overflow, int32_t reset);
+/* The LSTM unroll of this learner: 0 (default) = one cooperative launch each for the
+ * forward and the backward when lstm_size = 256 and the batch is at most 64 sequences
+ * (workgroups own 4 sequences x 16 units and exchange h / dh partials as tagged granules;
+ * spins bounded, debug buffer "lstm_timeout"), per-step launches otherwise; 1 = always
+ * per-step launches. */
+int acme_impala_set_lstm_unroll(acme_impala* l, int32_t mode);
 /* One network step for `rows` independent actors (IMPALAActor.select_action): inputs
  * obs [rows, ...], prev_action / prev_reward [rows], state h / c [rows, lstm_size];
  * outputs logits [rows, A], values [rows], next state h_out / c_out. */

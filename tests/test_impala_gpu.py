@@ -134,7 +134,7 @@ def _compare(cfg, n, params, b, frob_only=()):
     _check_params(n.get_params("params"), st["params"], cfg.learning_rate)
 
 
-@pytest.mark.parametrize("B,T,H", [(4, 6, 16), (16, 20, 256), (3, 2, 8)])
+@pytest.mark.parametrize("B,T,H", [(4, 6, 16), (16, 20, 256), (3, 2, 8), (64, 3, 256)])
 def test_flat_torso_step_matches_oracle(B, T, H):
     cfg = O.IMPALAConfig(num_actions=5, torso="flat", obs_dim=12, lstm_size=H,
                          head_size=max(H // 2, 4) // 4 * 4, entropy_cost=0.01, baseline_cost=0.5)
@@ -182,34 +182,35 @@ def test_policy_step_matches_unroll():
     _close(c.cpu().numpy(), cache["cs"][:, 0], name="c")
 
 
-@pytest.mark.parametrize("B,T,H,torso", [(16, 20, 256, "flat"), (3, 7, 64, "flat"),
+@pytest.mark.parametrize("B,T,H,torso", [(16, 20, 256, "flat"), (3, 7, 256, "flat"),
+                                         (27, 5, 256, "flat"), (16, 2, 256, "flat"),
                                          (16, 20, 256, "atari")])
-def test_persistent_lstm_forward_bitwise(B, T, H, torso):
-    """The one-launch LSTM unroll (lstm_fwd_persistent_kernel: W_h resident in LDS across
-    the T steps, h_t exchanged between workgroups as tagged granules) against the
-    per-step launches (the default; ACME_V_LSTMP=2 selects the persistent kernel): h, c,
-    gate gradients and losses equal to fp32
-    rounding (the two kernels' instruction selection differs in the last bit), no spin
-    timeout.  Both are checked against the f64 oracle by the tests above."""
-    from acme_amd._lib import lib
+def test_persistent_lstm_unroll_matches_per_step(B, T, H, torso):
+    """The one-launch LSTM forward and backward (lstm_fwd_rg_kernel / lstm_bwd_rg_kernel:
+    workgroups own 4 sequences x 16 units with their W_h slice in registers across the
+    unroll and exchange h_t and the dh partial products as tagged granules; the default for
+    lstm_size 256 and at most 64 sequences) against the per-step launches: h, c, gate
+    gradients, the policy/value outputs and the losses equal to fp32 rounding (the sums run
+    in another order), no spin timeout.  Both are checked against the f64 oracle by the
+    tests above (64 sequences, 256 co-resident workgroups, there only: the per-step forward
+    holds every row's h in 64 KB of LDS); ragged row groups (B = 3, 27) and the shortest
+    unroll (T = 2) included."""
     cfg = O.IMPALAConfig(num_actions=18 if torso == "atari" else 5, torso=torso, obs_dim=12,
                          lstm_size=H, head_size=64, entropy_cost=0.01, baseline_cost=0.5)
     params = _params(cfg, 5)
     b = _batch(cfg, B, T, 6)
     res = {}
-    for v in (2, 0):
-        lib().acme_tune_set(b"LSTMP", v)
-        try:
-            n = _native(cfg, B, T)
-            n.set_params(params)
-            _run(n, b)
-            res[v] = {k: n.debug_buffer(k) for k in ("h", "c", "dgates", "pv")}
-            res[v]["metrics"] = n.metrics.cpu().numpy()
-            res[v]["tmo"] = n.debug_buffer("lstm_timeout")[:1].view(np.uint32)
-        finally:
-            lib().acme_tune_set(b"LSTMP", 0)
-    assert res[2]["tmo"][0] == 0
-    for k in ("h", "c", "dgates", "pv", "metrics"):
-        scale = float(np.abs(res[0][k]).max())
-        np.testing.assert_allclose(res[2][k], res[0][k], rtol=1e-5, atol=1e-6 * scale,
+    for per_step in (False, True):
+        n = _native(cfg, B, T)
+        n.set_lstm_unroll(per_step)
+        n.set_params(params)
+        _run(n, b)
+        res[per_step] = {k: n.debug_buffer(k) for k in ("h", "c", "dgates", "pv")}
+        res[per_step]["metrics"] = n.metrics.cpu().numpy()
+        res[per_step]["grads"] = n.grads.cpu().numpy()
+        res[per_step]["tmo"] = n.debug_buffer("lstm_timeout")[:1].view(np.uint32)
+    assert res[False]["tmo"][0] == 0
+    for k in ("h", "c", "dgates", "pv", "metrics", "grads"):
+        scale = float(np.abs(res[True][k]).max())
+        np.testing.assert_allclose(res[False][k], res[True][k], rtol=2e-5, atol=2e-6 * scale,
                                    err_msg=k)
