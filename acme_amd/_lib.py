@@ -122,6 +122,8 @@ _SIGS = {
     "acme_replay_stage": (c_i32, [c_vp, c_i64, ctypes.POINTER(c_vp)]),
     "acme_replay_commit": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp]),
     "acme_replay_sync_inserts": (c_i32, [c_vp]),
+    "acme_host_register": (c_i32, [c_vp, c_i64]),
+    "acme_host_unregister": (c_i32, [c_vp]),
     "acme_nstep_writer_create": (c_i32, [c_vp, c_i32, c_f32, c_i64, c_i64, c_i64, c_vp]),
     "acme_nstep_writer_destroy": (c_i32, [c_vp]),
     "acme_nstep_writer_start": (c_i32, [c_vp, c_vp]),

@@ -173,6 +173,13 @@ class IMPALALearner(core.Learner, core.Saveable):
         step.native = nets  # keeps the networks alive with the closure
         return step
 
+    def pipelined_policy(self, max_rows: int):
+        """actor_policy as two halves for a driver that keeps several policy calls in flight
+        (ProcessActorPool): issue(obs, prev_a, prev_r, h, c) stages the numpy inputs in pinned
+        memory and issues the copies, the network step and the copies back on this policy's
+        own stream without waiting; result() waits for them and returns (logits, v, h, c)."""
+        return _PipelinedPolicy(self, int(max_rows))
+
     def get_variables(self, names: List[str]) -> List[Dict[str, np.ndarray]]:
         return [self._native.get_params("params")]
 
@@ -201,3 +208,88 @@ class IMPALALearner(core.Learner, core.Saveable):
             for k, t in n.views(buf).items():
                 t.copy_(torch.as_tensor(np.asarray(src[k], np.float32)).view(t.shape))
         n.num_steps = int(state["num_steps"])
+
+
+class _PipelinedPolicy:
+    """IMPALALearner.pipelined_policy: two networks bound to the learner's parameter
+    snapshots (as actor_policy), one high-priority stream, and packed transfer blocks: the
+    small inputs (previous actions and rewards, LSTM state) go to the device in one copy and
+    the outputs (logits, values, LSTM state) come back in one, next to the observation copy
+    (straight from page-locked memory when the caller has it there)."""
+
+    def __init__(self, learner: "IMPALALearner", rows: int):
+        n = learner._native  # noqa: SLF001
+        learner._ensure_snapshots()  # noqa: SLF001
+        self._l = learner
+        self._nets = [NativeIMPALA(num_actions=n.num_actions, max_batch=rows,
+                                   max_sequence_length=2, torso=n.torso, obs_dim=n.obs_dim,
+                                   lstm_size=n.lstm_size,
+                                   head_size=learner._network.head_size,  # noqa: SLF001
+                                   device=n.device, shared_params=buf)
+                      for buf in learner._snap_buf]  # noqa: SLF001
+        try:  # the actors' policy ahead of the learner's kernels where both are queued
+            self._stream = torch.cuda.Stream(device=n.device, priority=-1)
+        except (RuntimeError, TypeError):
+            self._stream = torch.cuda.Stream(device=n.device)
+        A, H, dev = n.num_actions, n.lstm_size, n.device
+        net = learner._network  # noqa: SLF001
+        F = 84 * 84 * 4 if net.torso == "atari" else net.obs_dim
+        odt = torch.uint8 if net.torso == "atari" else torch.float32
+        self._rows, self._A, self._H = rows, A, H
+        self._pin_obs = torch.empty((rows, F), dtype=odt, pin_memory=True)
+        self._dev_obs = torch.empty((rows, F), dtype=odt, device=dev)
+        # Small inputs, 4-byte words: prev_a [rows] (int32 bits), prev_r [rows], h, c [rows, H].
+        self._nin = rows * (2 + 2 * H)
+        self._pin_in = torch.empty(self._nin, dtype=torch.float32, pin_memory=True)
+        self._dev_in = torch.empty(self._nin, dtype=torch.float32, device=dev)
+        # Outputs: logits [rows, A], values [rows], h, c [rows, H].
+        self._nout = rows * (A + 1 + 2 * H)
+        self._pin_out = torch.empty(self._nout, dtype=torch.float32, pin_memory=True)
+        self._dev_out = torch.empty(self._nout, dtype=torch.float32, device=dev)
+        self._done = torch.cuda.Event()
+        self._n = 0
+
+    def _in_views(self, buf, n):
+        R, H = self._rows, self._H
+        return (buf[:n].view(torch.int32), buf[R:R + n], buf[2 * R:2 * R + n * H].view(n, H),
+                buf[2 * R + R * H:2 * R + R * H + n * H].view(n, H))
+
+    def _out_views(self, buf, n):
+        R, A, H = self._rows, self._A, self._H
+        o1, o2, o3 = R * A, R * A + R, R * A + R + R * H
+        return (buf[:n * A].view(n, A), buf[o1:o1 + n], buf[o2:o2 + n * H].view(n, H),
+                buf[o3:o3 + n * H].view(n, H))
+
+    def issue(self, observation, prev_action, prev_reward, hidden, cell,
+              observation_pinned: bool = False) -> None:
+        """observation_pinned: the observation array lives in page-locked memory (e.g. a
+        registered shared-memory block) and is copied to the device from there directly."""
+        n = int(np.asarray(prev_action).shape[0])
+        self._n = n
+        pin = self._in_views(self._pin_in, n)
+        for dst, x in zip(pin, (prev_action, prev_reward, hidden, cell)):
+            dst.numpy()[...] = np.asarray(x).reshape(dst.shape)
+        if observation_pinned:
+            obs_src = torch.from_numpy(np.ascontiguousarray(observation).reshape(n, -1))
+        else:
+            np.copyto(self._pin_obs.numpy()[:n], np.asarray(observation).reshape(n, -1),
+                      casting="unsafe")
+            obs_src = self._pin_obs[:n]
+        l, st = self._l, self._stream
+        with l._snap_lock:  # noqa: SLF001
+            j = l._snap  # noqa: SLF001
+            st.wait_event(l._snap_ready[j])  # noqa: SLF001
+        with torch.cuda.stream(st):
+            self._dev_obs[:n].copy_(obs_src, non_blocking=True)
+            self._dev_in.copy_(self._pin_in, non_blocking=True)
+            outs = self._out_views(self._dev_out, n)
+            self._nets[j].policy_step(self._dev_obs[:n], *self._in_views(self._dev_in, n),
+                                      stream=st, out=outs)
+            self._pin_out.copy_(self._dev_out, non_blocking=True)
+            self._done.record(st)
+            with l._snap_lock:  # noqa: SLF001
+                l._snap_reads[j][id(st)] = self._done  # noqa: SLF001
+
+    def result(self):
+        self._done.synchronize()
+        return tuple(x.numpy().copy() for x in self._out_views(self._pin_out, self._n))

@@ -1160,6 +1160,18 @@ int acme_replay_commit(acme_replay* r, int64_t n, const double* priorities, uint
   return rc;
 }
 
+int acme_host_register(void* p, int64_t bytes) {
+  ACME_CHECK_ARG(p && bytes > 0, "bad host range");
+  ACME_HIP_TRY(hipHostRegister(p, (size_t)bytes, hipHostRegisterDefault));
+  return ACME_OK;
+}
+
+int acme_host_unregister(void* p) {
+  ACME_CHECK_ARG(p, "null host pointer");
+  ACME_HIP_TRY(hipHostUnregister(p));
+  return ACME_OK;
+}
+
 int acme_replay_sync_inserts(acme_replay* r) {
   ACME_CHECK_ARG(r, "null replay");
   if (r->side) ACME_HIP_TRY(hipStreamSynchronize(r->side));

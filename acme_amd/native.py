@@ -830,14 +830,16 @@ class NativeIMPALA:
         check(lib().acme_impala_step(self._h, ctypes.byref(b), ptr(self.metrics),
                                      stream_ptr(stream)), "impala step")
 
-    def policy_step(self, obs, prev_action, prev_reward, h, c, stream=None):
-        """One network step for `rows` actors; returns (logits, values, h, c)."""
+    def policy_step(self, obs, prev_action, prev_reward, h, c, stream=None, out=None):
+        """One network step for `rows` actors; returns (logits, values, h, c) (into `out`,
+        four contiguous device tensors of those shapes, when given)."""
         rows = int(prev_action.shape[0])
         A, H = self.num_actions, self.lstm_size
-        out = [torch.empty(rows, A, dtype=torch.float32, device=self.device),
-               torch.empty(rows, dtype=torch.float32, device=self.device),
-               torch.empty(rows, H, dtype=torch.float32, device=self.device),
-               torch.empty(rows, H, dtype=torch.float32, device=self.device)]
+        if out is None:
+            out = [torch.empty(rows, A, dtype=torch.float32, device=self.device),
+                   torch.empty(rows, dtype=torch.float32, device=self.device),
+                   torch.empty(rows, H, dtype=torch.float32, device=self.device),
+                   torch.empty(rows, H, dtype=torch.float32, device=self.device)]
         check(lib().acme_impala_policy_step(
             self._h, ptr(obs.contiguous()), ptr(prev_action.contiguous()),
             ptr(prev_reward.contiguous()), ptr(h.contiguous()), ptr(c.contiguous()), rows,

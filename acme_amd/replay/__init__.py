@@ -232,6 +232,16 @@ class Table:
         self._native = None
         self._init_layout(self._structure, seq)
 
+    def set_sequence_length(self, T: int) -> None:
+        """Fixes the stored layout to T-step items before the first insert (what the first
+        SequenceAdder item would do), e.g. for writers that pack rows themselves."""
+        with self._mu:
+            if self._seq_len == T:
+                return
+            if self._seq_len is not None or self._fill or self._native.size() > 0:
+                raise ValueError("the table's layout is already fixed")
+            self._maybe_sequence_layout([np.zeros((T,) + f.shape, f.dtype) for f in self._fields])
+
     @property
     def sequence_length(self) -> Optional[int]:
         """Steps per item for sequence tables (None until the first item, 0 if not)."""
@@ -371,6 +381,29 @@ class QueueTable(Table):
                 self._cv.wait(left)
             super().insert(item, priority)
             self._accepted += 1
+
+    def insert_rows(self, rows: Sequence[np.ndarray], n: int) -> None:
+        """n items already packed as the table's rows (rows[f]: uint8 [n, row_bytes[f]],
+        e.g. a shared-memory ring of actor processes): one native insert, FIFO after every
+        earlier item; blocks while the queue is full, as insert() does."""
+        if n <= 0:
+            return
+        deadline = time.time() + self._timeout
+        with self._cv:
+            while self._accepted - self._consumed + n > self.max_size:
+                self.flush()
+                left = deadline - time.time()
+                if left <= 0:
+                    raise RuntimeError(f"queue '{self.name}' stayed full ({self.max_size} items) "
+                                       f"for {self._timeout}s")
+                self._cv.wait(min(left, 0.01))
+            self.flush()  # earlier single inserts first (FIFO)
+            for r, f in zip(rows, self._fields):
+                if r.shape != (n, f.row_bytes):
+                    raise ValueError(f"rows {r.shape} do not match the table's {(n, f.row_bytes)}")
+            self._native.insert(list(rows), None)
+            self._accepted += n
+            self._cv.notify_all()
 
     def pop_slots(self, batch_size: int, timeout: Optional[float] = None,
                   read=None) -> int:

@@ -50,9 +50,17 @@ def parse():
                         "end (--actors host actor threads feeding the device queue); insert: "
                         "host inserts into the configs[1] table while its learner steps")
     p.add_argument("--actors", type=int, default=64, help="impala_actors: environments / actors")
+    p.add_argument("--actor-procs", type=int, default=12,
+                   help="impala_actors: worker processes owning the environments and their "
+                        "adders (ProcessActorPool; policy batched in this process); 0 = host "
+                        "threads (--actor-threads)")
+    p.add_argument("--actor-groups", type=int, default=1,
+                   help="impala_actors with processes: environment groups whose policy steps "
+                        "alternate with the other groups' environment steps")
     p.add_argument("--actor-threads", type=int, default=2,
-                   help="impala_actors: host threads stepping the environments in batches "
-                        "(VectorActorPool); 0 = one thread per actor (ActorPool)")
+                   help="impala_actors with --actor-procs 0: host threads stepping the "
+                        "environments in batches (VectorActorPool); 0 = one thread per actor "
+                        "(ActorPool)")
     p.add_argument("--batch", type=int, default=0, help="default 512 (dqn) / 256 (d4pg)")
     p.add_argument("--replay-size", type=int, default=1_000_000)
     p.add_argument("--num-actions", type=int, default=18)
@@ -486,7 +494,41 @@ def setup_impala(args, world, rank, dev):
             lambda: impala_cpu_baseline(B, T, args.cpu_baseline_seconds))
 
 
-def impala_actors_bench(args, dev):
+IMPALA_T, IMPALA_A, IMPALA_H = 20, 18, 256
+
+
+def impala_actor_signature():
+    """The configs[3] queue signature (CPU only: the actor processes need it before the
+    parent touches the GPU)."""
+    from acme_amd import specs
+    from acme_amd.adders import reverb as adders
+    from acme_amd.environments.atari_like import AtariLike
+    from acme_amd.networks import LSTMState
+    from acme_amd.wrappers import ObservationActionRewardWrapper
+    spec = specs.make_environment_spec(ObservationActionRewardWrapper(AtariLike(seed=0)))
+    H, A = IMPALA_H, IMPALA_A
+    extra = {"core_state": LSTMState(specs.Array((H,), np.float32), specs.Array((H,), np.float32)),
+             "logits": specs.Array((A,), np.float32)}
+    return spec, adders.SequenceAdder.signature(spec, extras_spec=extra)
+
+
+def start_actor_processes(args):
+    """ProcessActorPool for impala_actors, started before anything touches the GPU."""
+    from acme_amd.agents.impala.process_actors import (ProcessActorPool, atari_like_oar,
+                                                       sequence_fields)
+    from acme_amd.networks import IMPALAAtariNetwork
+    _, sig = impala_actor_signature()
+    net = IMPALAAtariNetwork(IMPALA_A)
+    pool = ProcessActorPool(atari_like_oar, sequence_fields(sig, IMPALA_T), (84, 84, 4),
+                            IMPALA_A, IMPALA_H, net.initial_state, num_actors=args.actors,
+                            processes=args.actor_procs, groups=args.actor_groups,
+                            sequence_length=IMPALA_T,
+                            period=IMPALA_T)
+    pool.start()
+    return pool
+
+
+def impala_actors_bench(args, dev, pool=None):
     """BASELINE configs[3] end to end: `--actors` host threads, each an Atari-shaped
     environment (acme_amd.environments.AtariLike), an IMPALAActor and a SequenceAdder
     (T = 20, period 20) writing into the device queue table; their policy calls are batched
@@ -521,6 +563,16 @@ def impala_actors_bench(args, dev):
     make_env = lambda i: ObservationActionRewardWrapper(AtariLike(seed=1 + i))  # noqa: E731
     make_adder = lambda i: adders.SequenceAdder(replay.Client(server), sequence_length=T,  # noqa: E731
                                                 period=T)
+    # The environment's own cost per step (what an actor pays before any policy or adder).
+    e, t0 = make_env(999), time.perf_counter()
+    e.reset()
+    for k in range(2000):
+        ts = e.step(np.int32(k % A))
+        if ts.last():
+            e.reset()
+    env_us = 1e6 * (time.perf_counter() - t0) / 2000
+    if pool is not None:
+        return impala_process_actors(args, dev, pool, queue, learner, B, T, A, H, env_us)
     if args.actor_threads > 0:  # K environments per host thread, one policy call per K steps
         th = args.actor_threads
         per = min(-(-args.actors // th), 16)  # the native policy's batch limit (LDS) at LSTM 256
@@ -565,12 +617,79 @@ def impala_actors_bench(args, dev):
         "config": {"workload": "impala_actor_learner (BASELINE configs[3])", "actors": args.actors,
                    "batch_sequences": B, "sequence_length": T, "sequence_period": T,
                    "obs": "uint8[84,84,4]", "num_actions": A, "lstm": H},
-        "actors": {"env_steps_per_s": round(env_rate, 1),
+        "actors": {"env_steps_per_s": round(env_rate, 1), "env_us_per_step": round(env_us, 2),
                    "host_threads": args.actor_threads if policy is None else args.actors,
                    "policy_batches": policy.batches if policy else None,
                    "mean_policy_rows": (round(policy.rows / max(policy.batches, 1), 2)
                                         if policy else min(-(-args.actors // args.actor_threads),
                                                            16))},
+    }
+    print(json.dumps(out))
+
+
+def impala_process_actors(args, dev, pool, queue, learner, B, T, A, H, env_us):
+    """impala_actors with the environments and adders in worker processes (ProcessActorPool):
+    a driver thread of this process runs the batched policy over one group of environments
+    while the workers step the other, and hands the workers' finished sequences to the
+    device queue in native inserts; the learner steps on this thread whenever the queue
+    holds a batch."""
+    import threading
+    queue.set_sequence_length(T)
+    fields = [(f.shape, f.dtype, f.nbytes, f.row_bytes) for f in queue.fields]
+    if fields != pool._fields:  # noqa: SLF001
+        raise RuntimeError("actor rings and the queue table disagree on the item layout")
+    G = args.actor_groups
+    rows = args.actors // G
+    policy = [learner.pipelined_policy(rows) for _ in range(G)]  # one per group
+    pool.register_pinned()
+    stop, errors = threading.Event(), []
+
+    def drive():
+        try:
+            pool.run(policy, queue.insert_rows, ticks=1 << 40, should_stop=stop.is_set)
+        except BaseException as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = threading.Thread(target=drive, daemon=True)
+    th.start()
+    try:
+        def learn(n):
+            done = 0
+            while done < n:
+                if errors:
+                    raise errors[0]
+                if queue.can_sample(B):
+                    learner.step()
+                    done += 1
+                else:
+                    time.sleep(0.0002)
+        learn(args.warmup)
+        torch.cuda.synchronize(dev)
+        s0, t0 = pool.env_steps, time.perf_counter()
+        learn(args.steps)
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+        env_rate = (pool.env_steps - s0) / dt
+    finally:
+        stop.set()
+        th.join(60)
+        pool.close()
+    out = {
+        "metric": "IMPALA learned frames/sec (B=16 x T=20 per step) with host actors feeding "
+                  "the device queue, 1 MI355X",
+        "value": round(B * T * args.steps / dt, 1), "unit": "frames/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic Atari-shaped environment (acme_amd.environments.AtariLike), "
+                "random-init IMPALAAtariNetwork",
+        "config": {"workload": "impala_actor_learner (BASELINE configs[3])", "actors": args.actors,
+                   "batch_sequences": B, "sequence_length": T, "sequence_period": T,
+                   "obs": "uint8[84,84,4]", "num_actions": A, "lstm": H},
+        "actors": {"env_steps_per_s": round(env_rate, 1), "env_us_per_step": round(env_us, 2),
+                   "actor_processes": args.actor_procs, "policy_rows": rows, "groups": G,
+                   "items_inserted": pool.items,
+                   "driver_us_per_act": {k[:-2]: round(1e6 * v / max(pool.stats["acts"], 1), 1)
+                                         for k, v in pool.stats.items() if k.endswith("_s")}},
     }
     print(json.dumps(out))
 
@@ -614,6 +733,9 @@ def main():
         if "WORLD_SIZE" not in os.environ and args.gpus > 1:
             sys.exit(spawn_ranks(args.gpus))
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
+    pool = None
+    if args.workload == "impala_actors" and args.actor_procs > 0 and world == 1:
+        pool = start_actor_processes(args)  # before this process touches the GPU
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # One rank per GPU.  More ranks than visible GPUs (a rehearsal on a one-GPU box) share
@@ -639,7 +761,10 @@ def main():
     if args.workload in ("insert", "impala_actors"):
         if world > 1:
             raise SystemExit(f"the {args.workload} workload is single-GPU")
-        (insert_bench if args.workload == "insert" else impala_actors_bench)(args, dev)
+        if args.workload == "insert":
+            insert_bench(args, dev)
+        else:
+            impala_actors_bench(args, dev, pool)
         return
     t_fill = time.perf_counter()
     setup = {"dqn": setup_dqn, "d4pg": setup_d4pg, "impala": setup_impala}[args.workload]

@@ -117,6 +117,11 @@ int acme_replay_commit(acme_replay* r, int64_t n, const double* priorities, uint
                        void* stream);
 /* Host wait for every issued insert (tests, checkpoints, shutdown). */
 int acme_replay_sync_inserts(acme_replay* r);
+/* Page-locks caller memory (hipHostRegister) so copies from it are DMA without staging,
+ * e.g. the shared-memory blocks actor processes write observations into; unregister
+ * before the memory is unmapped. */
+int acme_host_register(void* p, int64_t bytes);
+int acme_host_unregister(void* p);
 
 /* N-step transition writer: the native NStepTransitionAdder (acme/adders/reverb/
  * transition.py:119-172; replaces its _write / _write_last + Writer.append / create_item)
