@@ -92,7 +92,8 @@ struct acme_d4pg {
   float* values = nullptr;                // [atoms] support
   float* act_lo = nullptr;                // [act]
   float* act_scale = nullptr;             // [act]
-  float* lnslab = nullptr;                // LayerNorm parameter-gradient partials
+  float* lnslab = nullptr;                // LayerNorm parameter-gradient partials (critic)
+  float* lnslab2 = nullptr;               // (policy: both are reduced after the backward)
   float* ploss_part = nullptr;            // per-block dpg loss partials
   double* norm_part = nullptr;            // [2][kNormBlocks]
   float* norms = nullptr;                 // [2] global norms (policy, critic)
@@ -219,11 +220,19 @@ struct LnFirstArgs {
   float *z, *mean, *rstd, *h;
 };
 
-__global__ void __launch_bounds__(256) ln_first_kernel(const LnFirstArgs a) {
+// Two evaluations in one launch (the online and target networks): blockIdx.y picks the
+// argument set; blocks past that set's rows leave at once.
+struct LnFirstPair {
+  LnFirstArgs a[2];
+};
+
+__global__ void __launch_bounds__(256) ln_first_kernel(const LnFirstPair pair) {
   __shared__ float xs[kRows][kMaxIn];
   __shared__ float red[4][kRows];
+  const LnFirstArgs& a = pair.a[blockIdx.y];
   const int tid = threadIdx.x;
   const int r0 = blockIdx.x * kRows;
+  if (r0 >= a.rows) return;  // uniform per block
   const int din = a.da + a.db;
   for (int i = tid; i < kRows * din; i += 256) {
     const int r = i / din, k = i - r * din, row = r0 + r;
@@ -303,14 +312,27 @@ __global__ void __launch_bounds__(256) ln_first_kernel(const LnFirstArgs a) {
 // ------------------------------------------------------------------ policy head
 // One wave per row: u = h @ W + b (A <= 16 outputs), t = tanh(u),
 // a = (0.5 (t + 1)) * (max - min) + min  (TanhToSpec, rescaling.py:70-73).
-__global__ void __launch_bounds__(256) policy_head_kernel(const float* __restrict__ h,
-                                                          const float* __restrict__ w,
-                                                          const float* __restrict__ b,
-                                                          const float* __restrict__ lo,
-                                                          const float* __restrict__ scale,
-                                                          int rows, int H, int A,
-                                                          float* __restrict__ t_out,
-                                                          float* __restrict__ a_out) {
+struct PolicyHeadArgs {
+  const float *h, *w, *b;
+  int rows;
+  float *t_out, *a_out;
+};
+struct PolicyHeadPair {
+  PolicyHeadArgs a[2];  // blockIdx.y
+  const float *lo, *scale;
+  int H, A;
+};
+
+__global__ void __launch_bounds__(256) policy_head_kernel(const PolicyHeadPair pr) {
+  const PolicyHeadArgs& pa = pr.a[blockIdx.y];
+  const float* __restrict__ h = pa.h;
+  const float* __restrict__ w = pa.w;
+  const float* __restrict__ b = pa.b;
+  const float* __restrict__ lo = pr.lo;
+  const float* __restrict__ scale = pr.scale;
+  const int rows = pa.rows, H = pr.H, A = pr.A;
+  float* __restrict__ t_out = pa.t_out;
+  float* __restrict__ a_out = pa.a_out;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -628,6 +650,36 @@ int dense_fwd(const char* name, const float* x, int rows, int K, const float* w,
   return ACME_OK;
 }
 
+// The same layer of two evaluations (rows0 / rows1 rows, weights w0 / w1) in one launch.
+int dense_fwd_pair(const char* name, const float* x0, int rows0, const float* w0,
+                   const float* b0, float* y0, const float* x1, int rows1, const float* w1,
+                   const float* b1, float* y1, int K, int N, int act, hipStream_t st) {
+  if (rows1 == 0) return dense_fwd(name, x0, rows0, K, w0, b0, N, act, y0, st);
+  if (K % 4 != 0 || N % 4 != 0) {
+    int rc = dense_fwd(name, x0, rows0, K, w0, b0, N, act, y0, st);
+    return rc != ACME_OK ? rc : dense_fwd(name, x1, rows1, K, w1, b1, N, act, y1, st);
+  }
+  DenseFwd<true> q[2];
+  const float* xs[2] = {x0, x1};
+  const float* ws[2] = {w0, w1};
+  const float* bs[2] = {b0, b1};
+  float* ys[2] = {y0, y1};
+  const int rs[2] = {rows0, rows1};
+  for (int i = 0; i < 2; ++i) {
+    q[i].M = rs[i]; q[i].N = N; q[i].K = K; q[i].k_chunk = K;
+    q[i].x = xs[i]; q[i].x2 = xs[i]; q[i].split_b = rs[i]; q[i].ldx = K;
+    q[i].w = ws[i]; q[i].bias = bs[i]; q[i].y = ys[i]; q[i].act = act; q[i].slab = nullptr;
+  }
+  auto p = gemm::make_zset(q);
+  ACME_PROF_PEAK(name, st, 2.0 * (double)(rows0 + rows1) * N * K, 0.0, 157.3);
+  hipError_t e = launch_gemm<32, 32, 1, 1, 16, 8>(p, 2, st);
+  if (e != hipSuccess) {
+    set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(e), __FILE__, __LINE__);
+    return ACME_ERR_HIP;
+  }
+  return ACME_OK;
+}
+
 // dX = act'(xprev) * (dZ @ W^T): dz [rows][Nout], W [Nin][Nout], xprev/dx [rows][Nin].
 int dense_dgrad(const char* name, const float* dz, int rows, int Nout, const float* w, int Nin,
                 const float* xprev, int act, float* dx, hipStream_t st) {
@@ -645,92 +697,177 @@ int dense_dgrad(const char* name, const float* dz, int rows, int Nout, const flo
   return ACME_OK;
 }
 
-// dW = X^T dZ over `rows` rows, db = column sums of dZ.
-int dense_wgrad(const char* name, const float* x, int rows, int Nin, const float* dz, int Nout,
-                float* dw, float* db, hipStream_t st) {
-  if (Nin % 4 == 0 && Nout % 4 == 0) {
-    DenseWgrad<true> p;
-    p.M = Nin; p.N = Nout; p.K = rows; p.k_chunk = rows;
-    p.x = x; p.ldx = Nin; p.dz = dz; p.out = dw; p.bias_out = db;
-    D4_GEMM(name, p);
-  } else {
-    DenseWgrad<false> p;
-    p.M = Nin; p.N = Nout; p.K = rows; p.k_chunk = rows;
-    p.x = x; p.ldx = Nin; p.dz = dz; p.out = dw; p.bias_out = db;
-    D4_GEMM(name, p);
-  }
-  return ACME_OK;
-}
 
-// LayerNormMLP forward over rows of concat(xa, xb) (second source from row `split`).
-int lnmlp_forward(acme_d4pg* l, const NetDesc& d, const float* prm, const float* xa0,
-                  const float* xb0, const float* xa1, const float* xb1, int split, int da,
-                  int db, int rows, Acts& a, const char* tag, hipStream_t st) {
+// One input set of a LayerNormMLP evaluation: rows of concat(xa, xb), the second source
+// from row `split` (xa1, xb1), parameters from `prm`, activations into `acts`.
+struct NetIn {
+  const float* prm;
+  const float *xa0, *xb0, *xa1, *xb1;
+  int split, rows;
+  Acts* acts;
+};
+
+// Two evaluations of one LayerNormMLP (the online and the target network) in one launch
+// per layer: the LayerNorm first layer, the ELU layers.
+int lnmlp_forward_pair(acme_d4pg* l, const NetDesc& d, const NetIn (&in)[2], int da, int db,
+                       const char* tag, hipStream_t st) {
   {
-    ACME_PROF(tag, st, 2.0 * rows * (double)(da + db) * d.sizes[0], 0.0);
-    LnFirstArgs f;
-    f.xa0 = xa0; f.xb0 = xb0; f.xa1 = xa1; f.xb1 = xb1;
-    f.split = split; f.rows = rows; f.da = da; f.db = db; f.H = d.sizes[0];
-    f.w = P(l, prm, d.w1); f.b = P(l, prm, d.b1);
-    f.scale = P(l, prm, d.scale); f.offset = P(l, prm, d.offset);
-    f.eps = l->cfg.layer_norm_epsilon;
-    f.z = a.z1; f.mean = a.mean; f.rstd = a.rstd; f.h = a.h[0];
-    ln_first_kernel<<<(unsigned)ceil_div(rows, kRows), 256, 0, st>>>(f);
+    ACME_PROF(tag, st, 2.0 * (in[0].rows + in[1].rows) * (double)(da + db) * d.sizes[0], 0.0);
+    LnFirstPair f;
+    for (int i = 0; i < 2; ++i) {
+      LnFirstArgs& g = f.a[i];
+      g.xa0 = in[i].xa0; g.xb0 = in[i].xb0; g.xa1 = in[i].xa1; g.xb1 = in[i].xb1;
+      g.split = in[i].split; g.rows = in[i].rows; g.da = da; g.db = db; g.H = d.sizes[0];
+      g.w = P(l, in[i].prm, d.w1); g.b = P(l, in[i].prm, d.b1);
+      g.scale = P(l, in[i].prm, d.scale); g.offset = P(l, in[i].prm, d.offset);
+      g.eps = l->cfg.layer_norm_epsilon;
+      Acts& a = *in[i].acts;
+      g.z = a.z1; g.mean = a.mean; g.rstd = a.rstd; g.h = a.h[0];
+    }
+    const int rows = std::max(in[0].rows, in[1].rows);
+    ln_first_kernel<<<dim3((unsigned)ceil_div(rows, kRows), in[1].rows > 0 ? 2 : 1), 256, 0,
+                      st>>>(f);
     D4_CHECK();
   }
   for (int i = 1; i < d.nl; ++i) {
-    int rc = dense_fwd("d4pg_mlp_fwd", a.h[i - 1], rows, d.sizes[i - 1], P(l, prm, d.w[i]),
-                       P(l, prm, d.b[i]), d.sizes[i], ACT_ELU, a.h[i], st);
+    Acts &a0 = *in[0].acts, &a1 = *in[1].acts;
+    int rc = dense_fwd_pair("d4pg_mlp_fwd", a0.h[i - 1], in[0].rows, P(l, in[0].prm, d.w[i]),
+                            P(l, in[0].prm, d.b[i]), a0.h[i], a1.h[i - 1], in[1].rows,
+                            P(l, in[1].prm, d.w[i]), P(l, in[1].prm, d.b[i]), a1.h[i],
+                            d.sizes[i - 1], d.sizes[i], ACT_ELU, st);
     if (rc != ACME_OK) return rc;
   }
   return ACME_OK;
 }
 
-int policy_forward(acme_d4pg* l, const float* prm, const float* obs, int rows, Acts& a,
-                   float* actions, hipStream_t st) {
+// Up to two policy evaluations (TanhToSpec actions into out[i]); in[1].rows = 0: one.
+int policy_forward_pair(acme_d4pg* l, const NetIn (&in)[2], float* const (&out)[2],
+                        hipStream_t st) {
   const NetDesc& d = l->pol;
-  int rc = lnmlp_forward(l, d, prm, obs, nullptr, obs, nullptr, rows, l->cfg.obs_dim, 0, rows, a,
-                         "d4pg_policy_ln", st);
+  int rc = lnmlp_forward_pair(l, d, in, l->cfg.obs_dim, 0, "d4pg_policy_ln", st);
   if (rc != ACME_OK) return rc;
-  ACME_PROF("d4pg_policy_head", st, 2.0 * rows * (double)d.sizes[d.nl - 1] * d.nout, 0.0);
-  policy_head_kernel<<<(unsigned)ceil_div(rows, 4), 256, 0, st>>>(
-      a.h[d.nl - 1], P(l, prm, d.ow), P(l, prm, d.ob), l->act_lo, l->act_scale, rows,
-      d.sizes[d.nl - 1], d.nout, a.t, actions);
+  const int rows = std::max(in[0].rows, in[1].rows);
+  ACME_PROF("d4pg_policy_head", st,
+            2.0 * (in[0].rows + in[1].rows) * (double)d.sizes[d.nl - 1] * d.nout, 0.0);
+  PolicyHeadPair h;
+  for (int i = 0; i < 2; ++i) {
+    h.a[i].h = in[i].acts->h[d.nl - 1];
+    h.a[i].w = P(l, in[i].prm, d.ow);
+    h.a[i].b = P(l, in[i].prm, d.ob);
+    h.a[i].rows = in[i].rows;
+    h.a[i].t_out = in[i].acts->t;
+    h.a[i].a_out = out[i];
+  }
+  h.lo = l->act_lo; h.scale = l->act_scale; h.H = d.sizes[d.nl - 1]; h.A = d.nout;
+  policy_head_kernel<<<dim3((unsigned)ceil_div(rows, 4), in[1].rows > 0 ? 2 : 1), 256, 0,
+                       st>>>(h);
   D4_CHECK();
   return ACME_OK;
 }
 
-int critic_forward(acme_d4pg* l, const float* prm, const float* o0, const float* a0,
-                   const float* o1, const float* a1, int split, int rows, Acts& a,
-                   hipStream_t st) {
+// The online critic (2B rows: [o_tm1, a_tm1 ; o_t, dpg actions]) and the target critic
+// (B rows: [o_t, target actions]).
+int critic_forward_pair(acme_d4pg* l, const NetIn (&in)[2], hipStream_t st) {
   const NetDesc& d = l->cri;
-  int rc = lnmlp_forward(l, d, prm, o0, a0, o1, a1, split, l->cfg.obs_dim, l->cfg.act_dim, rows,
-                         a, "d4pg_critic_ln", st);
+  int rc = lnmlp_forward_pair(l, d, in, l->cfg.obs_dim, l->cfg.act_dim, "d4pg_critic_ln", st);
   if (rc != ACME_OK) return rc;
-  return dense_fwd("d4pg_critic_head", a.h[d.nl - 1], rows, d.sizes[d.nl - 1], P(l, prm, d.ow),
-                   P(l, prm, d.ob), d.nout, ACT_NONE, a.out, st);
+  Acts &a0 = *in[0].acts, &a1 = *in[1].acts;
+  return dense_fwd_pair("d4pg_critic_head", a0.h[d.nl - 1], in[0].rows, P(l, in[0].prm, d.ow),
+                        P(l, in[0].prm, d.ob), a0.out, a1.h[d.nl - 1], in[1].rows,
+                        P(l, in[1].prm, d.ow), P(l, in[1].prm, d.ob), a1.out,
+                        d.sizes[d.nl - 1], d.nout, ACT_NONE, st);
 }
 
 inline int act_of_layer(int i) { return i == 0 ? ACT_TANH : ACT_ELU; }
 
-// Backward through the MLP part of a LayerNormMLP: dz[nl-1] holds the pre-activation
-// gradient of the last layer over `rows` rows; weight gradients use the first `wrows`.
-// Leaves dLoss/d(LayerNorm output) in dz[0].
-int lnmlp_backward_mlp(acme_d4pg* l, const NetDesc& d, const Acts& a, float* const* dz, int rows,
-                       int wrows, hipStream_t st) {
-  for (int i = d.nl - 1; i >= 1; --i) {
-    int rc = dense_wgrad("d4pg_mlp_wgrad", a.h[i - 1], wrows, d.sizes[i - 1], dz[i], d.sizes[i],
-                         Pm(l, l->grads, d.w[i]), Pm(l, l->grads, d.b[i]), st);
+// The step's weight gradients, collected while the input-gradient chain runs and issued
+// after it as one launch per problem type (gemm::ZSet: every layer of both networks at
+// once), plus the LayerNorm parameter-gradient reductions: they feed only the optimizer.
+struct WgradBatch {
+  std::vector<DenseWgrad<true>> dense;
+  std::vector<DenseWgrad<false>> narrow;  // widths not a multiple of 4 (the heads)
+  std::vector<ConcatWgrad> first;
+  struct LnReduce {
+    const float* slab;
+    int nblk, H;
+    float *scale, *offset;
+  };
+  std::vector<LnReduce> ln;
+};
+
+// dW = X^T dZ over `rows` rows, db = column sums of dZ, into the batch.
+void add_wgrad(WgradBatch& wb, const float* x, int rows, int Nin, const float* dz, int Nout,
+               float* dw, float* db) {
+  auto fill = [&](auto& p) {
+    p.M = Nin; p.N = Nout; p.K = rows; p.k_chunk = rows;
+    p.x = x; p.ldx = Nin; p.dz = dz; p.out = dw; p.bias_out = db;
+  };
+  if (Nin % 4 == 0 && Nout % 4 == 0) {
+    DenseWgrad<true> p;
+    fill(p);
+    wb.dense.push_back(p);
+  } else {
+    DenseWgrad<false> p;
+    fill(p);
+    wb.narrow.push_back(p);
+  }
+}
+
+constexpr int kMaxZ = 8;
+
+template <class Q>
+int launch_zset(const char* name, const std::vector<Q>& qs, hipStream_t st) {
+  if (qs.empty()) return ACME_OK;
+  if (qs.size() > (size_t)kMaxZ) return (set_error("too many batched GEMMs"), ACME_ERR_INVALID);
+  gemm::ZSet<Q, kMaxZ> z;
+  static_cast<Q&>(z) = qs[0];
+  double flops = 0.0;
+  for (size_t i = 0; i < qs.size(); ++i) {
+    z.sub[i] = qs[i];
+    z.M = std::max(z.M, qs[i].M);
+    z.N = std::max(z.N, qs[i].N);
+    flops += 2.0 * qs[i].M * (double)qs[i].N * qs[i].K;
+  }
+  ACME_PROF_PEAK(name, st, flops, 0.0, 157.3);
+  hipError_t e = launch_gemm<32, 32, 1, 1, 16, 8>(z, (int)qs.size(), st);
+  if (e != hipSuccess) {
+    set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(e), __FILE__, __LINE__);
+    return ACME_ERR_HIP;
+  }
+  return ACME_OK;
+}
+
+int run_wgrads(const WgradBatch& wb, hipStream_t st) {
+  for (const auto& r : wb.ln) {
+    ACME_PROF("d4pg_ln_param_reduce", st, 0.0, 4.0 * (r.nblk + 1) * 2.0 * r.H);
+    int rc = launch_slab_reduce(r.slab, r.nblk, 2 * (int64_t)r.H, r.scale, r.H, r.offset, nullptr,
+                                1, 0, st);
     if (rc != ACME_OK) return rc;
-    rc = dense_dgrad("d4pg_mlp_dgrad", dz[i], rows, d.sizes[i], P(l, l->params, d.w[i]),
-                     d.sizes[i - 1], a.h[i - 1], act_of_layer(i - 1), dz[i - 1], st);
+  }
+  int rc = launch_zset("d4pg_wgrad_dense", wb.dense, st);
+  if (rc == ACME_OK) rc = launch_zset("d4pg_wgrad_narrow", wb.narrow, st);
+  if (rc == ACME_OK) rc = launch_zset("d4pg_wgrad_first", wb.first, st);
+  return rc;
+}
+
+// Backward through the MLP part of a LayerNormMLP: dz[nl-1] holds the pre-activation
+// gradient of the last layer over `rows` rows; weight gradients (over the first `wrows`)
+// go to the batch.  Leaves dLoss/d(LayerNorm output) in dz[0].
+int lnmlp_backward_mlp(acme_d4pg* l, const NetDesc& d, const Acts& a, float* const* dz, int rows,
+                       int wrows, WgradBatch& wb, hipStream_t st) {
+  for (int i = d.nl - 1; i >= 1; --i) {
+    add_wgrad(wb, a.h[i - 1], wrows, d.sizes[i - 1], dz[i], d.sizes[i], Pm(l, l->grads, d.w[i]),
+              Pm(l, l->grads, d.b[i]));
+    int rc = dense_dgrad("d4pg_mlp_dgrad", dz[i], rows, d.sizes[i], P(l, l->params, d.w[i]),
+                         d.sizes[i - 1], a.h[i - 1], act_of_layer(i - 1), dz[i - 1], st);
     if (rc != ACME_OK) return rc;
   }
   return ACME_OK;
 }
 
 int ln_backward(acme_d4pg* l, const NetDesc& d, const Acts& a, float* dy, int rows, int ce_rows,
-                bool dpg, const float* xa, const float* xb, int da, int db, hipStream_t st) {
+                bool dpg, const float* xa, const float* xb, int da, int db, float* slab,
+                WgradBatch& wb, hipStream_t st) {
   const int H = d.sizes[0];
   const int nblk = (int)ceil_div(rows, kRows);
   {
@@ -738,7 +875,7 @@ int ln_backward(acme_d4pg* l, const NetDesc& d, const Acts& a, float* dy, int ro
     LnBwdArgs b;
     b.dy = dy; b.z = a.z1; b.mean = a.mean; b.rstd = a.rstd;
     b.scale = P(l, l->params, d.scale);
-    b.rows = rows; b.ce_rows = ce_rows; b.H = H; b.colslab = l->lnslab;
+    b.rows = rows; b.ce_rows = ce_rows; b.H = H; b.colslab = slab;
     b.w1 = P(l, l->params, d.w1); b.act_off = l->cfg.obs_dim; b.A = l->cfg.act_dim;
     b.clip = l->cfg.clipping ? 1.f : 0.f; b.invB = 1.f / (float)ce_rows;
     b.t = l->pon.t; b.act_scale = l->act_scale;
@@ -746,15 +883,13 @@ int ln_backward(acme_d4pg* l, const NetDesc& d, const Acts& a, float* dy, int ro
     ln_bwd_kernel<<<(unsigned)nblk, 256, 0, st>>>(b);
     D4_CHECK();
   }
-  // LayerNorm scale / offset gradients: sum the block partials [nblk][2][H].
-  int rc = launch_slab_reduce(l->lnslab, nblk, 2 * (int64_t)H, Pm(l, l->grads, d.scale), H,
-                              Pm(l, l->grads, d.offset), nullptr, 1, 0, st);
-  if (rc != ACME_OK) return rc;
+  // LayerNorm scale / offset gradients: the block partials [nblk][2][H], summed later.
+  wb.ln.push_back({slab, nblk, H, Pm(l, l->grads, d.scale), Pm(l, l->grads, d.offset)});
   ConcatWgrad p;
   p.M = da + db; p.N = H; p.K = ce_rows; p.k_chunk = ce_rows;
   p.x0 = xa; p.d0 = da; p.x1 = xb; p.d1 = db; p.dz = dy;
   p.out = Pm(l, l->grads, d.w1); p.bias_out = Pm(l, l->grads, d.b1);
-  D4_GEMM("d4pg_first_wgrad", p);
+  wb.first.push_back(p);
   return ACME_OK;
 }
 
@@ -770,14 +905,18 @@ int d4pg_step_impl(acme_d4pg* l, const acme_d4pg_batch* bt, const acme_d4pg_outp
     ACME_HIP_TRY(hipMemcpyAsync(l->target, l->params, (size_t)l->flat * sizeof(float),
                                 hipMemcpyDeviceToDevice, st));
   }
-  // Forwards.
-  if ((rc = policy_forward(l, l->params, bt->o_t, B, l->pon, l->pon.out, st)) ||
-      (rc = policy_forward(l, l->target, bt->o_t, B, l->ptg, l->ptg.out, st)) ||
-      (rc = critic_forward(l, l->params, bt->o_tm1, bt->a_tm1, bt->o_t, l->pon.out, B, 2 * B,
-                           l->con, st)) ||
-      (rc = critic_forward(l, l->target, bt->o_t, l->ptg.out, bt->o_t, l->ptg.out, B, B, l->ctg,
-                           st)))
-    return rc;
+  // Forwards: the online and target evaluations of each network share every launch.
+  {
+    const NetIn pin[2] = {{l->params, bt->o_t, nullptr, bt->o_t, nullptr, B, B, &l->pon},
+                          {l->target, bt->o_t, nullptr, bt->o_t, nullptr, B, B, &l->ptg}};
+    float* const pout[2] = {l->pon.out, l->ptg.out};
+    if ((rc = policy_forward_pair(l, pin, pout, st))) return rc;
+  }
+  {
+    const NetIn cin[2] = {{l->params, bt->o_tm1, bt->a_tm1, bt->o_t, l->pon.out, B, 2 * B, &l->con},
+                          {l->target, bt->o_t, l->ptg.out, bt->o_t, l->ptg.out, B, B, &l->ctg}};
+    if ((rc = critic_forward_pair(l, cin, st))) return rc;
+  }
   {
     ACME_PROF("d4pg_loss", st, 0.0, 0.0);
     d4pg_loss_kernel<<<(unsigned)ceil_div(2 * B, 4), 256, 0, st>>>(
@@ -786,23 +925,26 @@ int d4pg_step_impl(acme_d4pg* l, const acme_d4pg_batch* bt, const acme_d4pg_outp
     D4_CHECK();
   }
   // Critic backward: 2B rows of dgrad (CE rows + dpg rows), weight grads from the first B.
+  WgradBatch wb;
   const int cL = cd.nl - 1;
-  if ((rc = dense_wgrad("d4pg_head_wgrad", l->con.h[cL], B, cd.sizes[cL], l->dlogits, cd.nout,
-                        Pm(l, l->grads, cd.ow), Pm(l, l->grads, cd.ob), st)) ||
-      (rc = dense_dgrad("d4pg_head_dgrad", l->dlogits, 2 * B, cd.nout, P(l, l->params, cd.ow),
+  add_wgrad(wb, l->con.h[cL], B, cd.sizes[cL], l->dlogits, cd.nout, Pm(l, l->grads, cd.ow),
+            Pm(l, l->grads, cd.ob));
+  if ((rc = dense_dgrad("d4pg_head_dgrad", l->dlogits, 2 * B, cd.nout, P(l, l->params, cd.ow),
                         cd.sizes[cL], l->con.h[cL], act_of_layer(cL), l->cdz[cL], st)) ||
-      (rc = lnmlp_backward_mlp(l, cd, l->con, l->cdz, 2 * B, B, st)) ||
+      (rc = lnmlp_backward_mlp(l, cd, l->con, l->cdz, 2 * B, B, wb, st)) ||
       (rc = ln_backward(l, cd, l->con, l->cdz[0], 2 * B, B, true, bt->o_tm1, bt->a_tm1, od, ad,
-                        st)))
+                        l->lnslab, wb, st)))
     return rc;
   // Policy backward from du = dloss/d(head pre-activation).
   const int pL = pd.nl - 1;
-  if ((rc = dense_wgrad("d4pg_phead_wgrad", l->pon.h[pL], B, pd.sizes[pL], l->du, ad,
-                        Pm(l, l->grads, pd.ow), Pm(l, l->grads, pd.ob), st)) ||
-      (rc = dense_dgrad("d4pg_phead_dgrad", l->du, B, ad, P(l, l->params, pd.ow), pd.sizes[pL],
+  add_wgrad(wb, l->pon.h[pL], B, pd.sizes[pL], l->du, ad, Pm(l, l->grads, pd.ow),
+            Pm(l, l->grads, pd.ob));
+  if ((rc = dense_dgrad("d4pg_phead_dgrad", l->du, B, ad, P(l, l->params, pd.ow), pd.sizes[pL],
                         l->pon.h[pL], act_of_layer(pL), l->pdz[pL], st)) ||
-      (rc = lnmlp_backward_mlp(l, pd, l->pon, l->pdz, B, B, st)) ||
-      (rc = ln_backward(l, pd, l->pon, l->pdz[0], B, B, false, bt->o_t, nullptr, od, 0, st)))
+      (rc = lnmlp_backward_mlp(l, pd, l->pon, l->pdz, B, B, wb, st)) ||
+      (rc = ln_backward(l, pd, l->pon, l->pdz[0], B, B, false, bt->o_t, nullptr, od, 0,
+                        l->lnslab2, wb, st)) ||
+      (rc = run_wgrads(wb, st)))
     return rc;
   // Global-norm clipping + Adam (t = steps taken including this one).
   {
@@ -947,6 +1089,7 @@ int acme_d4pg_create(const acme_d4pg_config* cfg, acme_d4pg** out) {
       (rc = dev_alloc(l, &l->act_lo, cfg->act_dim)) ||
       (rc = dev_alloc(l, &l->act_scale, cfg->act_dim)) ||
       (rc = dev_alloc(l, &l->lnslab, nblk * 2 * hmax)) ||
+      (rc = dev_alloc(l, &l->lnslab2, nblk * 2 * hmax)) ||
       (rc = dev_alloc(l, &l->ploss_part, nblk)) ||
       (rc = dev_alloc(l, &l->norm_part, 2 * kNormBlocks)) ||
       (rc = dev_alloc(l, &l->norms, 2)) || (rc = dev_alloc(l, &l->loss_tmp, 2)) ||
@@ -1039,9 +1182,12 @@ int acme_d4pg_policy(acme_d4pg* l, const float* obs, int64_t rows, int32_t use_t
   const int B = l->cfg.max_batch;
   for (int64_t r0 = 0; r0 < rows; r0 += B) {
     const int n = (int)std::min<int64_t>(B, rows - r0);
-    int rc = policy_forward(l, use_target ? l->target : l->params,
-                            obs + r0 * l->cfg.obs_dim, n, l->ptg,
-                            actions + r0 * l->cfg.act_dim, st);
+    const float* o = obs + r0 * l->cfg.obs_dim;
+    const NetIn in[2] = {{use_target ? l->target : l->params, o, nullptr, o, nullptr, n, n,
+                          &l->ptg},
+                         {l->params, o, nullptr, o, nullptr, n, 0, &l->ptg}};
+    float* const out[2] = {actions + r0 * l->cfg.act_dim, nullptr};
+    int rc = policy_forward_pair(l, in, out, st);
     if (rc != ACME_OK) return rc;
   }
   return ACME_OK;

@@ -181,6 +181,33 @@ __device__ __forceinline__ P z_select(const P& p) {
   else return p;
 }
 
+// Several problems of one type in one launch (e.g. the online and target networks' same
+// layer): blockIdx.z selects sub-problem z; the grid covers the largest M x N, and the tiles
+// past a smaller problem's extent load zeros and store nothing.  Each sub-problem's outputs
+// are computed exactly as by its own launch.
+template <class Q, int NZ>
+struct ZSet : Q {
+  static constexpr bool kZClass = true;
+  Q sub[NZ];
+  __host__ __device__ ZSet for_z(int z) const {
+    ZSet r = *this;
+    static_cast<Q&>(r) = sub[z];
+    return r;
+  }
+};
+
+template <class Q, int NZ>
+ZSet<Q, NZ> make_zset(const Q (&qs)[NZ]) {
+  ZSet<Q, NZ> s;
+  static_cast<Q&>(s) = qs[0];
+  for (int i = 0; i < NZ; ++i) {
+    s.sub[i] = qs[i];
+    s.M = s.M > qs[i].M ? s.M : qs[i].M;
+    s.N = s.N > qs[i].N ? s.N : qs[i].N;
+  }
+  return s;
+}
+
 // Problem concept (see conv.h):
 //   static constexpr int A_MODE, B_MODE;
 //   int M, N, K;            rows of A (= C rows), rows of B (= C cols), reduction length

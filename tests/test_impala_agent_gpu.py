@@ -183,3 +183,40 @@ def test_vector_actor_pool_feeds_device_queue_learner():
     assert learner.num_steps >= 5
     assert pool.env_steps >= 5 * B * T
     assert np.isfinite(learner.native.metrics.cpu().numpy()).all()
+
+
+@pytest.mark.parametrize("rows", [5, 64])
+def test_pipelined_policy_equals_actor_policy(rows):
+    """IMPALALearner.pipelined_policy (the process pool's policy: packed transfers, a
+    page-locked observation source, issue / result) returns exactly actor_policy's
+    logits, values and LSTM state for the same inputs, at 64 rows on the one-launch LSTM
+    step too; and two calls in flight on their own policies do not disturb each other."""
+    import ctypes
+    from acme_amd import _lib
+    from acme_amd.agents.impala import IMPALALearner
+    from acme_amd.networks import IMPALAAtariNetwork
+    A, H = 18, 256
+    net = IMPALAAtariNetwork(A, lstm_size=H, head_size=256)
+    learner = IMPALALearner(None, net, iter(()), learning_rate=1e-3,
+                            logger=loggers.NoOpLogger(), batch_size=2, sequence_length=4)
+    rng = np.random.default_rng(rows)
+    ins = [(rng.integers(0, 256, (rows, 84, 84, 4), dtype=np.uint8),
+            rng.integers(0, A, rows).astype(np.int32), rng.standard_normal(rows).astype(np.float32),
+            (0.3 * rng.standard_normal((rows, H))).astype(np.float32),
+            (0.3 * rng.standard_normal((rows, H))).astype(np.float32)) for _ in range(2)]
+    ref = [learner.actor_policy(max_rows=rows)(*x) for x in ins]
+    pols = [learner.pipelined_policy(rows) for _ in range(2)]
+    # The first call's observations from page-locked memory, the second's staged.
+    obs0 = np.empty_like(ins[0][0])
+    obs0[...] = ins[0][0]
+    L = _lib.lib()
+    _lib.check(L.acme_host_register(ctypes.c_void_p(obs0.ctypes.data), obs0.nbytes))
+    try:
+        pols[0].issue(obs0, *ins[0][1:], observation_pinned=True)
+        pols[1].issue(*ins[1])
+        got = [pols[0].result(), pols[1].result()]
+    finally:
+        L.acme_host_unregister(ctypes.c_void_p(obs0.ctypes.data))
+    for g, r in zip(got, ref):
+        for a, b in zip(g, r):
+            np.testing.assert_array_equal(a, b)
