@@ -396,12 +396,15 @@ __global__ void __launch_bounds__(256) d4pg_loss_kernel(
   const float pj = e / wave_sum(e);
   const float gd = discount * d[row];
   const float zc = fminf(fmaxf(r[row] + gd * vi, vmin), vmax);
+  // delta_hat = (sg dq) / d_pos - ((1 - sg) dq) / d_neg with sg = (dq >= 0): one of the two
+  // terms is an exact zero, so delta_hat = |dq| / (sg ? d_pos : d_neg), the same bits with
+  // one division.  Source atom j's values come from lane j by readlane (j is uniform).
   float tgt = 0.f;
   for (int j = 0; j < K; ++j) {
-    const float zcj = __shfl(zc, j, 64), pjj = __shfl(pj, j, 64);
+    const float zcj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(zc), j));
+    const float pjj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pj), j));
     const float dq = zcj - vi;
-    const float sg = dq >= 0.f ? 1.f : 0.f;
-    const float dh = (sg * dq) / dpos - ((1.f - sg) * dq) / dneg;
+    const float dh = fabsf(dq) / (dq >= 0.f ? dpos : dneg);
     tgt += fminf(fmaxf(1.f - dh, 0.f), 1.f) * pjj;
   }
   const float logp = ql - m2 - logf(s2);
@@ -680,24 +683,6 @@ int dense_fwd_pair(const char* name, const float* x0, int rows0, const float* w0
   return ACME_OK;
 }
 
-// dX = act'(xprev) * (dZ @ W^T): dz [rows][Nout], W [Nin][Nout], xprev/dx [rows][Nin].
-int dense_dgrad(const char* name, const float* dz, int rows, int Nout, const float* w, int Nin,
-                const float* xprev, int act, float* dx, hipStream_t st) {
-  if (Nout % 4 == 0 && Nin % 4 == 0) {
-    DenseDgrad<true> p;
-    p.M = rows; p.N = Nin; p.K = Nout; p.k_chunk = Nout;
-    p.dz = dz; p.w = w; p.xprev = xprev; p.ldx = Nin; p.dx = dx; p.act = act;
-    D4_GEMM(name, p);
-  } else {
-    DenseDgrad<false> p;
-    p.M = rows; p.N = Nin; p.K = Nout; p.k_chunk = Nout;
-    p.dz = dz; p.w = w; p.xprev = xprev; p.ldx = Nin; p.dx = dx; p.act = act;
-    D4_GEMM(name, p);
-  }
-  return ACME_OK;
-}
-
-
 // One input set of a LayerNormMLP evaluation: rows of concat(xa, xb), the second source
 // from row `split` (xa1, xb1), parameters from `prm`, activations into `acts`.
 struct NetIn {
@@ -780,23 +765,21 @@ int critic_forward_pair(acme_d4pg* l, const NetIn (&in)[2], hipStream_t st) {
 
 inline int act_of_layer(int i) { return i == 0 ? ACT_TANH : ACT_ELU; }
 
-// The step's weight gradients, collected while the input-gradient chain runs and issued
-// after it as one launch per problem type (gemm::ZSet: every layer of both networks at
-// once), plus the LayerNorm parameter-gradient reductions: they feed only the optimizer.
-struct WgradBatch {
-  std::vector<DenseWgrad<true>> dense;
-  std::vector<DenseWgrad<false>> narrow;  // widths not a multiple of 4 (the heads)
+// One backward launch (gemm::ZMulti): a layer's input gradient together with the weight
+// gradients whose dZ is already written (the same layer's, the previous LayerNorm's first
+// layer).  The problems read finished tensors and write disjoint outputs, so the weight
+// gradients fill CUs the input gradient leaves idle instead of running as launches of
+// their own.
+struct BwdGroup {
+  std::vector<DenseDgrad<true>> dg;
+  std::vector<DenseDgrad<false>> dgn;  // widths not a multiple of 4 (the heads)
+  std::vector<DenseWgrad<true>> wg;
+  std::vector<DenseWgrad<false>> wgn;
   std::vector<ConcatWgrad> first;
-  struct LnReduce {
-    const float* slab;
-    int nblk, H;
-    float *scale, *offset;
-  };
-  std::vector<LnReduce> ln;
 };
 
-// dW = X^T dZ over `rows` rows, db = column sums of dZ, into the batch.
-void add_wgrad(WgradBatch& wb, const float* x, int rows, int Nin, const float* dz, int Nout,
+// dW = X^T dZ over `rows` rows, db = column sums of dZ.
+void add_wgrad(BwdGroup& g, const float* x, int rows, int Nin, const float* dz, int Nout,
                float* dw, float* db) {
   auto fill = [&](auto& p) {
     p.M = Nin; p.N = Nout; p.K = rows; p.k_chunk = rows;
@@ -805,69 +788,167 @@ void add_wgrad(WgradBatch& wb, const float* x, int rows, int Nin, const float* d
   if (Nin % 4 == 0 && Nout % 4 == 0) {
     DenseWgrad<true> p;
     fill(p);
-    wb.dense.push_back(p);
+    g.wg.push_back(p);
   } else {
     DenseWgrad<false> p;
     fill(p);
-    wb.narrow.push_back(p);
+    g.wgn.push_back(p);
   }
 }
 
-constexpr int kMaxZ = 8;
+// dX = act'(xprev) * (dZ @ W^T): dz [rows][Nout], W [Nin][Nout], xprev/dx [rows][Nin].
+void add_dgrad(BwdGroup& g, const float* dz, int rows, int Nout, const float* w, int Nin,
+               const float* xprev, int act, float* dx) {
+  auto fill = [&](auto& p) {
+    p.M = rows; p.N = Nin; p.K = Nout; p.k_chunk = Nout;
+    p.dz = dz; p.w = w; p.xprev = xprev; p.ldx = Nin; p.dx = dx; p.act = act;
+  };
+  if (Nout % 4 == 0 && Nin % 4 == 0) {
+    DenseDgrad<true> p;
+    fill(p);
+    g.dg.push_back(p);
+  } else {
+    DenseDgrad<false> p;
+    fill(p);
+    g.dgn.push_back(p);
+  }
+}
+
+constexpr int kZ = 3;  // sub-problems of one type per backward launch
 
 template <class Q>
-int launch_zset(const char* name, const std::vector<Q>& qs, hipStream_t st) {
-  if (qs.empty()) return ACME_OK;
-  if (qs.size() > (size_t)kMaxZ) return (set_error("too many batched GEMMs"), ACME_ERR_INVALID);
-  gemm::ZSet<Q, kMaxZ> z;
-  static_cast<Q&>(z) = qs[0];
-  double flops = 0.0;
-  for (size_t i = 0; i < qs.size(); ++i) {
+bool fill_zset(gemm::ZSet<Q, kZ>& z, int& n, const std::vector<Q>& qs, int& tiles, int& count,
+               double& flops) {
+  if (qs.size() > (size_t)kZ) return false;
+  n = (int)qs.size();
+  if (!qs.empty()) static_cast<Q&>(z) = qs[0];
+  for (int i = 0; i < n; ++i) {
     z.sub[i] = qs[i];
-    z.M = std::max(z.M, qs[i].M);
-    z.N = std::max(z.N, qs[i].N);
+    tiles = std::max(tiles, (int)(ceil_div(qs[i].M, 32) * ceil_div(qs[i].N, 32)));
     flops += 2.0 * qs[i].M * (double)qs[i].N * qs[i].K;
   }
+  count += n;
+  return true;
+}
+
+template <class Q0, class... R>
+bool fill_multi(gemm::ZMulti<gemm::ZSet<Q0, kZ>, gemm::ZSet<R, kZ>...>& m, int& tiles,
+                int& count, double& flops, const std::vector<Q0>& q0, const std::vector<R>&... r) {
+  if (!fill_zset(m.s, m.n, q0, tiles, count, flops)) return false;
+  if constexpr (sizeof...(R) > 0) return fill_multi(m.rest, tiles, count, flops, r...);
+  return true;
+}
+
+// One launch over the problems of the given types (gemm_f32_multi_kernel instantiated for
+// exactly these types: its LDS and registers are their maximum).
+template <class... Q>
+int launch_multi(const char* name, hipStream_t st, const std::vector<Q>&... qs) {
+  gemm::ZMulti<gemm::ZSet<Q, kZ>...> m;
+  int tiles = 0, count = 0;
+  double flops = 0.0;
+  if (!fill_multi(m, tiles, count, flops, qs...))
+    return (set_error("too many GEMMs in one backward launch"), ACME_ERR_INVALID);
+  if (count == 0) return ACME_OK;
   ACME_PROF_PEAK(name, st, flops, 0.0, 157.3);
-  hipError_t e = launch_gemm<32, 32, 1, 1, 16, 8>(z, (int)qs.size(), st);
-  if (e != hipSuccess) {
-    set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(e), __FILE__, __LINE__);
-    return ACME_ERR_HIP;
-  }
+  hipLaunchKernelGGL((gemm::gemm_f32_multi_kernel<32, 32, 1, 1, 16, 8, gemm::ZSet<Q, kZ>...>),
+                     dim3((unsigned)tiles, 1, (unsigned)count), dim3(64 * 8), 0, st, m);
+  D4_CHECK();
   return ACME_OK;
 }
 
-int run_wgrads(const WgradBatch& wb, hipStream_t st) {
-  for (const auto& r : wb.ln) {
-    ACME_PROF("d4pg_ln_param_reduce", st, 0.0, 4.0 * (r.nblk + 1) * 2.0 * r.H);
-    int rc = launch_slab_reduce(r.slab, r.nblk, 2 * (int64_t)r.H, r.scale, r.H, r.offset, nullptr,
-                                1, 0, st);
-    if (rc != ACME_OK) return rc;
-  }
-  int rc = launch_zset("d4pg_wgrad_dense", wb.dense, st);
-  if (rc == ACME_OK) rc = launch_zset("d4pg_wgrad_narrow", wb.narrow, st);
-  if (rc == ACME_OK) rc = launch_zset("d4pg_wgrad_first", wb.first, st);
+// The hidden layers' launches carry 4-aligned problems only; the heads' and the first
+// layers' the rest.
+int launch_bwd(const char* name, BwdGroup& g, hipStream_t st) {
+  int rc;
+  if (g.dgn.empty() && g.wgn.empty() && g.first.empty())
+    rc = launch_multi(name, st, g.dg, g.wg);
+  else if (g.dg.empty() && g.wg.empty())
+    rc = launch_multi(name, st, g.dgn, g.wgn, g.first);
+  else
+    rc = launch_multi(name, st, g.dg, g.wg, g.dgn, g.wgn, g.first);
+  g = BwdGroup{};
   return rc;
 }
 
-// Backward through the MLP part of a LayerNormMLP: dz[nl-1] holds the pre-activation
-// gradient of the last layer over `rows` rows; weight gradients (over the first `wrows`)
-// go to the batch.  Leaves dLoss/d(LayerNorm output) in dz[0].
-int lnmlp_backward_mlp(acme_d4pg* l, const NetDesc& d, const Acts& a, float* const* dz, int rows,
-                       int wrows, WgradBatch& wb, hipStream_t st) {
-  for (int i = d.nl - 1; i >= 1; --i) {
-    add_wgrad(wb, a.h[i - 1], wrows, d.sizes[i - 1], dz[i], d.sizes[i], Pm(l, l->grads, d.w[i]),
-              Pm(l, l->grads, d.b[i]));
-    int rc = dense_dgrad("d4pg_mlp_dgrad", dz[i], rows, d.sizes[i], P(l, l->params, d.w[i]),
-                         d.sizes[i - 1], a.h[i - 1], act_of_layer(i - 1), dz[i - 1], st);
-    if (rc != ACME_OK) return rc;
+// LayerNorm scale / offset gradients of the step's LayerNorms: the block partials
+// [nblk][2][H] of ln_bwd_kernel, summed for both networks in one launch after the last
+// one (blockIdx.y = network): 16 float4 columns x 16 partial groups per block, group g
+// sums partials g, g+16, ... in order, then the groups are added in order.
+struct LnReduce {
+  const float* slab;
+  int nblk, H;
+  float *scale, *offset;
+};
+struct LnReducePair {
+  LnReduce r[2];
+};
+
+__global__ void __launch_bounds__(256) ln_param_reduce_kernel(const LnReducePair q) {
+  using f32x4 = gemm::f32x4;
+  const LnReduce a = q.r[blockIdx.y];
+  __shared__ f32x4 red[16][16];
+  const int c = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int count4 = a.H / 2;  // 2H floats per partial row
+  const int e = blockIdx.x * 16 + c;
+  if (blockIdx.x * 16 >= count4) return;  // block-uniform
+  const f32x4* s4 = reinterpret_cast<const f32x4*>(a.slab);
+  f32x4 acc{0.f, 0.f, 0.f, 0.f};
+  if (e < count4) {
+#pragma unroll 8
+    for (int sp = g; sp < a.nblk; sp += 16) acc += s4[(size_t)sp * count4 + e];
   }
+  red[g][c] = acc;
+  __syncthreads();
+  if (g == 0 && e < count4) {
+    f32x4 v = red[0][c];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) v += red[k][c];
+    const int h4 = a.H / 4;
+    if (e < h4) reinterpret_cast<f32x4*>(a.scale)[e] = v;
+    else reinterpret_cast<f32x4*>(a.offset)[e - h4] = v;
+  }
+}
+
+int run_ln_reduces(const std::vector<LnReduce>& ln, hipStream_t st) {
+  if (ln.empty()) return ACME_OK;
+  if (ln.size() > 2) return (set_error("too many LayerNorm reductions"), ACME_ERR_INVALID);
+  LnReducePair q;
+  int cols = 0;
+  double bytes = 0.0;
+  for (size_t i = 0; i < ln.size(); ++i) {
+    q.r[i] = ln[i];
+    cols = std::max(cols, ln[i].H / 2);
+    bytes += 4.0 * (ln[i].nblk + 1) * 2.0 * ln[i].H;
+  }
+  ACME_PROF("d4pg_ln_param_reduce", st, 0.0, bytes);
+  ln_param_reduce_kernel<<<dim3((unsigned)ceil_div(cols, 16), (unsigned)ln.size()), 256, 0, st>>>(q);
+  D4_CHECK();
   return ACME_OK;
 }
 
+// Backward through the MLP part of a LayerNormMLP: `g` holds the launch that forms dz[nl-1]
+// (the pre-activation gradient of the last hidden layer, `rows` rows) — it is issued here
+// with that layer's weight gradient's predecessor problems.  Each layer's launch: its input
+// gradient and its weight gradient (over the first `wrows` rows).  Leaves dLoss/d(LayerNorm
+// output) in dz[0].
+int lnmlp_backward_mlp(acme_d4pg* l, const NetDesc& d, const Acts& a, float* const* dz, int rows,
+                       int wrows, BwdGroup& g, const char* tag, hipStream_t st) {
+  int rc = launch_bwd(tag, g, st);
+  for (int i = d.nl - 1; i >= 1 && rc == ACME_OK; --i) {
+    add_wgrad(g, a.h[i - 1], wrows, d.sizes[i - 1], dz[i], d.sizes[i], Pm(l, l->grads, d.w[i]),
+              Pm(l, l->grads, d.b[i]));
+    add_dgrad(g, dz[i], rows, d.sizes[i], P(l, l->params, d.w[i]), d.sizes[i - 1], a.h[i - 1],
+              act_of_layer(i - 1), dz[i - 1]);
+    rc = launch_bwd("d4pg_bwd_mlp", g, st);
+  }
+  return rc;
+}
+
+// LayerNorm backward of the first layer; its weight gradient (concat inputs) joins the next
+// backward launch, its scale/offset partials the final reductions.
 int ln_backward(acme_d4pg* l, const NetDesc& d, const Acts& a, float* dy, int rows, int ce_rows,
                 bool dpg, const float* xa, const float* xb, int da, int db, float* slab,
-                WgradBatch& wb, hipStream_t st) {
+                BwdGroup& g, std::vector<LnReduce>& ln, hipStream_t st) {
   const int H = d.sizes[0];
   const int nblk = (int)ceil_div(rows, kRows);
   {
@@ -883,13 +964,12 @@ int ln_backward(acme_d4pg* l, const NetDesc& d, const Acts& a, float* dy, int ro
     ln_bwd_kernel<<<(unsigned)nblk, 256, 0, st>>>(b);
     D4_CHECK();
   }
-  // LayerNorm scale / offset gradients: the block partials [nblk][2][H], summed later.
-  wb.ln.push_back({slab, nblk, H, Pm(l, l->grads, d.scale), Pm(l, l->grads, d.offset)});
+  ln.push_back({slab, nblk, H, Pm(l, l->grads, d.scale), Pm(l, l->grads, d.offset)});
   ConcatWgrad p;
   p.M = da + db; p.N = H; p.K = ce_rows; p.k_chunk = ce_rows;
   p.x0 = xa; p.d0 = da; p.x1 = xb; p.d1 = db; p.dz = dy;
   p.out = Pm(l, l->grads, d.w1); p.bias_out = Pm(l, l->grads, d.b1);
-  wb.first.push_back(p);
+  g.first.push_back(p);
   return ACME_OK;
 }
 
@@ -924,27 +1004,30 @@ int d4pg_step_impl(acme_d4pg* l, const acme_d4pg_batch* bt, const acme_d4pg_outp
         l->dlogits, l->ce);
     D4_CHECK();
   }
-  // Critic backward: 2B rows of dgrad (CE rows + dpg rows), weight grads from the first B.
-  WgradBatch wb;
+  // Critic backward: 2B rows of input gradients (CE rows + dpg rows), weight gradients from
+  // the first B.  Launch k carries layer k's input gradient and weight gradient.
+  BwdGroup g;
+  std::vector<LnReduce> ln;
   const int cL = cd.nl - 1;
-  add_wgrad(wb, l->con.h[cL], B, cd.sizes[cL], l->dlogits, cd.nout, Pm(l, l->grads, cd.ow),
+  add_wgrad(g, l->con.h[cL], B, cd.sizes[cL], l->dlogits, cd.nout, Pm(l, l->grads, cd.ow),
             Pm(l, l->grads, cd.ob));
-  if ((rc = dense_dgrad("d4pg_head_dgrad", l->dlogits, 2 * B, cd.nout, P(l, l->params, cd.ow),
-                        cd.sizes[cL], l->con.h[cL], act_of_layer(cL), l->cdz[cL], st)) ||
-      (rc = lnmlp_backward_mlp(l, cd, l->con, l->cdz, 2 * B, B, wb, st)) ||
+  add_dgrad(g, l->dlogits, 2 * B, cd.nout, P(l, l->params, cd.ow), cd.sizes[cL], l->con.h[cL],
+            act_of_layer(cL), l->cdz[cL]);
+  if ((rc = lnmlp_backward_mlp(l, cd, l->con, l->cdz, 2 * B, B, g, "d4pg_bwd_head", st)) ||
       (rc = ln_backward(l, cd, l->con, l->cdz[0], 2 * B, B, true, bt->o_tm1, bt->a_tm1, od, ad,
-                        l->lnslab, wb, st)))
+                        l->lnslab, g, ln, st)))
     return rc;
-  // Policy backward from du = dloss/d(head pre-activation).
+  // Policy backward from du = dloss/d(head pre-activation); its head launch also carries the
+  // critic's first-layer weight gradient.
   const int pL = pd.nl - 1;
-  add_wgrad(wb, l->pon.h[pL], B, pd.sizes[pL], l->du, ad, Pm(l, l->grads, pd.ow),
+  add_wgrad(g, l->pon.h[pL], B, pd.sizes[pL], l->du, ad, Pm(l, l->grads, pd.ow),
             Pm(l, l->grads, pd.ob));
-  if ((rc = dense_dgrad("d4pg_phead_dgrad", l->du, B, ad, P(l, l->params, pd.ow), pd.sizes[pL],
-                        l->pon.h[pL], act_of_layer(pL), l->pdz[pL], st)) ||
-      (rc = lnmlp_backward_mlp(l, pd, l->pon, l->pdz, B, B, wb, st)) ||
+  add_dgrad(g, l->du, B, ad, P(l, l->params, pd.ow), pd.sizes[pL], l->pon.h[pL],
+            act_of_layer(pL), l->pdz[pL]);
+  if ((rc = lnmlp_backward_mlp(l, pd, l->pon, l->pdz, B, B, g, "d4pg_bwd_phead", st)) ||
       (rc = ln_backward(l, pd, l->pon, l->pdz[0], B, B, false, bt->o_t, nullptr, od, 0,
-                        l->lnslab2, wb, st)) ||
-      (rc = run_wgrads(wb, st)))
+                        l->lnslab2, g, ln, st)) ||
+      (rc = launch_bwd("d4pg_wgrad_first", g, st)) || (rc = run_ln_reduces(ln, st)))
     return rc;
   // Global-norm clipping + Adam (t = steps taken including this one).
   {

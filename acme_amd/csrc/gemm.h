@@ -221,9 +221,27 @@ ZSet<Q, NZ> make_zset(const Q (&qs)[NZ]) {
 // contiguous share of the block's K range through their own LDS stages, and the partial
 // accumulators are summed through LDS before the epilogue.  Small GEMMs (a few hundred
 // rows, K <= 1024) use it to put 4x more waves on the same output tiles.
+//
+// LDS floats of one block: two stages per k-group, reused after the k loop for the k-group
+// reduction: the accumulator partials, then the column-sum partials.
 template <int BM, int BN, int WM, int WN, int BK, int WK, class P>
-__global__ void __launch_bounds__(64 * WM * WN * WK) gemm_f32_kernel(const P p_in) {
-  const P p = z_select(p_in);
+constexpr int gemm_smem_floats() {
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int MT = TM / 32, NTL = TN / 32;
+  constexpr int STAGE = OperandPlan<BM, 64 * WM * WN, P::A_MODE, BK>::FLOATS +
+                        OperandPlan<BN, 64 * WM * WN, P::B_MODE, BK>::FLOATS;
+  constexpr int STAGE_FLOATS = 2 * STAGE * WK;
+  constexpr int RED_FLOATS = (WK - 1) * WM * WN * MT * NTL * 16 * 64;
+  constexpr int RED_ALL = RED_FLOATS + (WK - 1) * BN;
+  return STAGE_FLOATS > RED_ALL ? STAGE_FLOATS : RED_ALL;
+}
+
+// One output tile (`tile`, reduction split `split`) of problem p, LDS at `smem`
+// (gemm_smem_floats<...>() floats).  Blocks whose tile lies past p's extent leave at once
+// (block-uniform, before any barrier).
+template <int BM, int BN, int WM, int WN, int BK, int WK, class P>
+__device__ __forceinline__ void gemm_f32_block(const P& p, const int tile, const int split,
+                                               float* __restrict__ smem) {
   constexpr int NTG = 64 * WM * WN;  // threads per k-group
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int MT = TM / 32, NTL = TN / 32;
@@ -234,9 +252,6 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) gemm_f32_kernel(const P p_i
   constexpr int STAGE = PA::FLOATS + PB::FLOATS;
   constexpr int STAGE_FLOATS = 2 * STAGE * WK;
   constexpr int RED_FLOATS = (WK - 1) * WM * WN * MT * NTL * 16 * 64;
-  constexpr int SMEM = STAGE_FLOATS > RED_FLOATS ? STAGE_FLOATS : RED_FLOATS;
-
-  __shared__ __attribute__((aligned(16))) float smem[SMEM];
 
   const int tid_all = threadIdx.x;
   const int grp = tid_all / NTG;
@@ -244,10 +259,9 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) gemm_f32_kernel(const P p_i
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int tiles_n = (p.N + BN - 1) / BN;
-  const int tile = blockIdx.x;
   const int m0 = (tile / tiles_n) * BM;
   const int n0 = (tile % tiles_n) * BN;
-  const int split = HasZClass<P>::value ? 0 : blockIdx.z;
+  if (m0 >= p.M) return;
   int kbeg = split * p.k_chunk;
   int kend = kbeg + p.k_chunk;
   if (kend > p.K) kend = p.K;
@@ -262,7 +276,6 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) gemm_f32_kernel(const P p_i
     kbeg += s0 * BK;
   }
   float* my = smem + grp * 2 * STAGE;
-
   typename P::ARow arow[PA::PER_THREAD];
   typename P::BRow brow[PB::PER_THREAD];
 #pragma unroll
@@ -352,7 +365,7 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) gemm_f32_kernel(const P p_i
   if constexpr (WK > 1) {
     // Sum the k-groups' accumulators into group 0 (fixed order: group 0 + 1 + 2 + ...).
     constexpr int PER_WAVE = MT * NTL * 16 * 64;
-    __shared__ float cs_red[(WK - 1) * BN];
+    float* cs_red = smem + RED_FLOATS;  // the stages are dead after the loop's last barrier
     if (grp > 0) {
       float* dst = smem + ((grp - 1) * WM * WN + wave) * PER_WAVE;
 #pragma unroll
@@ -386,6 +399,55 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) gemm_f32_kernel(const P p_i
   if constexpr (kColSum) {
     if (do_colsum && n0 + tid < p.N) p.store_colsum(n0 + tid, colsum, split);
   }
+}
+
+
+template <int BM, int BN, int WM, int WN, int BK, int WK, class P>
+__global__ void __launch_bounds__(64 * WM * WN * WK) gemm_f32_kernel(const P p_in) {
+  __shared__ __attribute__((aligned(16))) float smem[gemm_smem_floats<BM, BN, WM, WN, BK, WK, P>()];
+  const P p = z_select(p_in);
+  gemm_f32_block<BM, BN, WM, WN, BK, WK>(p, blockIdx.x, HasZClass<P>::value ? 0 : blockIdx.z, smem);
+}
+
+// Problems of different types in one launch: ZMulti<S0, S1, ...> holds one ZSet per type
+// and its count n; blockIdx.z runs S0's sub-problems 0 .. n0-1, then S1's, and so on (the
+// input and weight gradients of a layer, which read the same dZ and are independent).
+// Each sub-problem's outputs are computed exactly as by its own launch.
+template <class... S>
+struct ZMulti;
+template <>
+struct ZMulti<> {};
+template <class S0, class... R>
+struct ZMulti<S0, R...> {
+  S0 s;
+  int n = 0;
+  ZMulti<R...> rest;
+};
+
+template <int BM, int BN, int WM, int WN, int BK, int WK, class S0, class... R>
+constexpr int zmulti_smem_floats() {
+  constexpr int a = gemm_smem_floats<BM, BN, WM, WN, BK, WK, S0>();
+  if constexpr (sizeof...(R) == 0) return a;
+  else {
+    constexpr int b = zmulti_smem_floats<BM, BN, WM, WN, BK, WK, R...>();
+    return a > b ? a : b;
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int BK, int WK, class S0, class... R>
+__device__ __forceinline__ void zmulti_run(const ZMulti<S0, R...>& q, int z, float* smem) {
+  if (z < q.n) {
+    const S0 p = q.s.for_z(z);
+    gemm_f32_block<BM, BN, WM, WN, BK, WK>(p, blockIdx.x, 0, smem);
+  } else if constexpr (sizeof...(R) > 0) {
+    zmulti_run<BM, BN, WM, WN, BK, WK>(q.rest, z - q.n, smem);
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int BK, int WK, class... S>
+__global__ void __launch_bounds__(64 * WM * WN * WK) gemm_f32_multi_kernel(const ZMulti<S...> q) {
+  __shared__ __attribute__((aligned(16))) float smem[zmulti_smem_floats<BM, BN, WM, WN, BK, WK, S...>()];
+  zmulti_run<BM, BN, WM, WN, BK, WK>(q, blockIdx.z, smem);
 }
 
 template <int BM, int BN, int WM, int WN, int BK = 16, int WK = 1, class P>

@@ -989,15 +989,19 @@ __global__ void __launch_bounds__(256) clip_adam_kernel(const ClipAdamArgs a) {
     scl[2 + k] = G;
     if (blockIdx.x == 0 && a.norms) a.norms[k] = G;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 64 && a.out_a) {
-    float t = 0.f;
-    for (int i = 0; i < a.n_a; ++i) t += a.sum_a[i];
-    *a.out_a = t / a.div_a;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 128 && a.out_b) {
-    float t = 0.f;
-    for (int i = 0; i < a.n_b; ++i) t += a.sum_b[i];
-    *a.out_b = t / a.div_b;
+  // The logged losses: wave 1 sums sum_a, wave 2 sum_b (lane-strided partials, then a
+  // fixed shuffle tree: deterministic).
+  if (blockIdx.x == 0 && (wave == 1 || wave == 2)) {
+    const float* src = wave == 1 ? a.sum_a : a.sum_b;
+    float* dst = wave == 1 ? a.out_a : a.out_b;
+    const int n = wave == 1 ? a.n_a : a.n_b;
+    if (dst) {
+      float t = 0.f;
+      for (int i = lane; i < n; i += 64) t += src[i];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+      if (lane == 0) *dst = t / (wave == 1 ? a.div_a : a.div_b);
+    }
   }
   __syncthreads();
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < a.n4; i += (int64_t)gridDim.x * 256) {

@@ -468,6 +468,45 @@ __global__ void __launch_bounds__(T) sample_gather_pair_kernel(
   }
 }
 
+// Sample + gather fused for rows of small fields only (the control-suite transitions:
+// every field under 1 KB): one wave per sampled row draws it (the sampling kernels'
+// arithmetic) and copies its fields, 4 rows per workgroup, no block barrier.
+template <bool PRIO>
+__global__ void __launch_bounds__(256) sample_gather_small_kernel(
+    TreeView tree, const double* __restrict__ raw_prio, const uint64_t* __restrict__ keys,
+    int64_t batch, int64_t size, uint64_t seed, uint64_t step, double prob_scale,
+    int64_t* out_slots, uint64_t* out_keys, double* out_probs, int64_t* out_size,
+    double* out_prio, SmallFields sm) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= batch) return;  // wave-uniform
+  int64_t slot;
+  double prob;
+  if (PRIO) {
+    draw_prioritized(tree, size, seed, step, r, &slot, &prob);
+  } else {
+    const double u = sample_uniform(seed, step, (uint32_t)r);
+    slot = (int64_t)(u * (double)size);
+    if (slot >= size) slot = size - 1;
+    prob = 1.0 / (double)size;
+  }
+  prob *= prob_scale;
+  if (lane == 0) {
+    out_slots[r] = slot;
+    if (out_keys) out_keys[r] = keys[slot];
+    if (out_probs) out_probs[r] = prob;
+    if (out_size) out_size[r] = size;
+    if (out_prio) out_prio[r] = raw_prio[slot];
+  }
+#pragma unroll
+  for (int q = 0; q < ACME_MAX_FIELDS; ++q) {
+    if (q >= sm.n) break;
+    for (int w = lane; w < sm.words[q]; w += 64)
+      reinterpret_cast<uint32_t*>(sm.dst[q] + r * 4 * sm.words[q])[w] =
+          reinterpret_cast<const uint32_t*>(sm.src[q] + slot * 4 * sm.words[q])[w];
+  }
+}
+
 // Recompute level[l] nodes from their 64 children (one wave per node).
 // Mode A: contiguous node range [node_begin, node_begin + count).
 // Mode B: node = slots[j] >> (6 l) for j < count (duplicates recompute identically).
@@ -1395,8 +1434,23 @@ static bool pair_layout(const acme_replay* r, void* const* out_fields, int* f0, 
   return true;
 }
 
+// Every field under 1 KB and a whole number of 4-byte words: the small-row fused path.
+static bool small_layout(const acme_replay* r, void* const* out_fields, SmallFields* sm) {
+  *sm = SmallFields{};
+  for (int f = 0; f < r->cfg.num_fields; ++f) {
+    if (r->cfg.field_bytes[f] >= 1024 || r->cfg.field_bytes[f] % 4 != 0 ||
+        reinterpret_cast<uintptr_t>(out_fields[f]) % 4 != 0)
+      return false;
+    sm->src[sm->n] = r->fields[f];
+    sm->dst[sm->n] = static_cast<uint8_t*>(out_fields[f]);
+    sm->words[sm->n] = (int32_t)(r->cfg.field_bytes[f] / 4);
+    sm->n++;
+  }
+  return sm->n > 0;
+}
+
 // Sample + gather as a unit (the caller holds r->mu): one fused launch for the transition
-// layout, else the sampling kernel then the gather.
+// layout and for rows of small fields, else the sampling kernel then the gather.
 static int sample_gather_impl(acme_replay* r, int64_t batch, uint64_t step_counter,
                               double prob_scale, int64_t* slots, uint64_t* keys,
                               double* probabilities, int64_t* table_size, double* priorities,
@@ -1445,6 +1499,36 @@ static int sample_gather_impl(acme_replay* r, int64_t batch, uint64_t step_count
       else ACME_SGP(false, 1024, 32);
     }
 #undef ACME_SGP
+    ACME_LAUNCH_CHECK();
+    return ACME_OK;
+  }
+  if (!pair && tune_variant("SGF") != 1 && tune_variant("GATH") == 0 &&
+      small_layout(r, out_fields, &sm)) {
+    hipStream_t st = as_stream(stream);
+    int64_t size = 0;
+    int rc = order_after_inserts(r, st, &size);
+    if (rc != ACME_OK) return rc;
+    if (size <= 0) {
+      set_error("cannot sample from an empty table (rate limiter MinSize(1))");
+      return ACME_ERR_EMPTY;
+    }
+    double row_bytes = 0;
+    for (int k = 0; k < r->cfg.num_fields; ++k) row_bytes += (double)r->cfg.field_bytes[k];
+    const bool prio = r->cfg.sampler == ACME_SAMPLER_PRIORITIZED;
+    ACME_PROF("replay_sample_gather", st, 0.0,
+              (double)batch * (2.0 * row_bytes + 40.0 + (prio ? 512.0 * r->nlevels : 0.0)));
+    TreeView tv;
+    for (int l = 0; l < 8; ++l) tv.level[l] = r->levels[l];
+    tv.nlevels = r->nlevels;
+    const unsigned gb = (unsigned)ceil_div(batch, 4);
+    if (prio)
+      sample_gather_small_kernel<true><<<gb, 256, 0, st>>>(
+          tv, r->raw_prio, r->keys, batch, size, r->cfg.seed, step_counter, prob_scale, slots,
+          keys, probabilities, table_size, priorities, sm);
+    else
+      sample_gather_small_kernel<false><<<gb, 256, 0, st>>>(
+          tv, r->raw_prio, r->keys, batch, size, r->cfg.seed, step_counter, prob_scale, slots,
+          keys, probabilities, table_size, priorities, sm);
     ACME_LAUNCH_CHECK();
     return ACME_OK;
   }

@@ -239,10 +239,12 @@ def test_gather_kernels_bit_identical(fields):
 
 
 @pytest.mark.parametrize("prioritized", [True, False])
-@pytest.mark.parametrize("fields", [[28224, 4, 4, 4, 28224], [2048, 4, 2048]])
+@pytest.mark.parametrize("fields", [[28224, 4, 4, 4, 28224], [2048, 4, 2048],
+                                    [96, 24, 4, 4, 96], [1020, 8]])
 def test_fused_sample_gather_matches_two_launches(prioritized, fields):
-    """acme_replay_sample_gather's fused kernel (the transition layout: draw + row copy in
-    one workgroup) against the sampling kernel + gather (SGF=1) and the oracle's draw."""
+    """acme_replay_sample_gather's fused kernels (the transition layout: draw + row copy in
+    one workgroup; rows of small fields: draw + copy per wave, e.g. D4PG's control
+    transitions) against the sampling kernel + gather (SGF=1) and the oracle's draw."""
     import ctypes
     from acme_amd._lib import lib
     rng = np.random.default_rng(5)
