@@ -21,20 +21,23 @@ import sys
 
 # kernel symbol pattern -> profiler section name (first match wins), per workload
 SECTIONS_D4PG = [
-    (r"DenseFwd<true.*|gemm_\w+_kernel<32, 32, 1, 1, 16, 4, acme::conv::DenseFwd<true", "d4pg_mlp_fwd"),
-    (r"gemm_\w+_kernel<32, 32, 1, 1, 16, 4, acme::conv::DenseDgrad<true", "d4pg_mlp_dgrad"),
-    (r"gemm_\w+_kernel<32, 32, 1, 1, 16, 4, acme::conv::DenseWgrad<true", "d4pg_mlp_wgrad"),
+    (r"gemm_f32_kernel<32, 32, 1, 1, 16, 8, acme::gemm::ZSet<acme::conv::DenseFwd<true", "d4pg_mlp_fwd"),
+    (r"gemm_f32_kernel<32, 32, 1, 1, 16, 8, acme::gemm::ZSet<acme::conv::DenseFwd<false", "d4pg_critic_head"),
+    (r"gemm_f32_multi_kernel<.*ZSet<acme::conv::DenseDgrad<true", "d4pg_bwd_mlp"),
+    (r"gemm_f32_multi_kernel<", "d4pg_bwd_heads_first"),
     (r"ln_bwd_kernel", "d4pg_ln_bwd"),
     (r"ln_first_kernel", "d4pg_ln_first"),
-    (r"clip_adam_kernel", "d4pg_adam"),
+    (r"d4pg_loss_kernel", "d4pg_loss"),
+    (r"grad_sumsq_kernel|clip_adam_kernel", "d4pg_adam"),
+    (r"sample_gather_small_kernel", "replay_sample_gather"),
 ]
 SECTIONS_IMPALA = [
     (r"DenseDgrad<true", "impala_feat_dgrad"),
     (r"OarFwd", "impala_oar_fwd"),
     (r"OarWgrad", "impala_wi_wgrad"),
-    (r"lstm_fwd_step", "impala_lstm_fwd_step"),
-    (r"lstm_bwd_step", "impala_lstm_bwd_step"),
-    (r"clip_adam_kernel", "impala_adam"),
+    (r"lstm_fwd_rg_kernel|lstm_fwd_step", "impala_lstm_fwd"),
+    (r"lstm_bwd_rg_kernel|lstm_bwd_step", "impala_lstm_bwd"),
+    (r"grad_sumsq_kernel|clip_adam_kernel", "impala_adam"),
     (r"ConvFwd<acme::conv::Geom<84,", "conv1_fwd"),
     (r"ConvFwd<acme::conv::Geom<21,", "conv2_fwd"),
     (r"ConvFwd<acme::conv::Geom<11,", "conv3_fwd"),
@@ -64,7 +67,7 @@ SECTIONS = [
     (r"ConvWgrad<acme::conv::Geom<11,", "conv3_wgrad"),
     (r"ConvDgradSub", "conv2_dgrad"),
     (r"ConvDgrad<", "conv3_dgrad"),
-    (r"(?<!clip_)adam_kernel", "adam"),
+    (r"(?<!clip_)adam_kernel|adam_slabs_kernel", "adam"),
     (r"sample_gather_pair_kernel", "replay_sample_gather"),
     (r"gather_fields_kernel|gather_pair_kernel|gather_pieces_kernel", "replay_gather"),
     (r"sample_prioritized_kernel", "replay_sample"),
