@@ -910,37 +910,55 @@ __global__ void __launch_bounds__(256) impala_rowstats_kernel(const LossArgs a) 
   }
 }
 
-__global__ void __launch_bounds__(64) impala_vtrace_kernel(const LossArgs a) {
+// The scan's inputs (value, reward, discount, log rho, log pi(a), entropy per row) are
+// loaded by the whole block into LDS first, every load in one round, when they fit
+// (kVtraceLdsRows); otherwise read from global memory inside the scan.  Threads 0..63 then
+// scan: thread b takes sequences b, b + 64, ...  Same arithmetic either way.  (Loads inside the
+// scan were ~19 dependent round trips per thread: 12.6 us.)
+constexpr int kVtraceLdsRows = 2048;  // 6 x 4 B x rows of LDS
+
+template <bool LDS>
+__device__ __forceinline__ void vtrace_scan(const LossArgs& a, const float* sv, const float* sr,
+                                            const float* sd, const float* sl, const float* sp,
+                                            const float* se) {
   __shared__ float red[64][3];
   const int b = threadIdx.x;
   const int T = a.T, W = a.A + 1;
+  auto V = [&](size_t row) { return LDS ? sv[row] : a.pv[row * W + a.A]; };
+  auto R = [&](size_t row) { return LDS ? sr[row] : a.reward[row]; };
+  auto D = [&](size_t row) { return LDS ? sd[row] : a.discount[row]; };
+  auto LR = [&](size_t row) { return LDS ? sl[row] : a.lrho[row]; };
+  auto LP = [&](size_t row) { return LDS ? sp[row] : a.lpa[row]; };
+  auto EN = [&](size_t row) { return LDS ? se[row] : a.ent[row]; };
   float s_pg = 0.f, s_cr = 0.f, s_en = 0.f;
-  for (int bb = b; bb < a.B; bb += 64) {
+  for (int bb = b; b < 64 && bb < a.B; bb += 64) {
     const size_t base = (size_t)bb * T;
-    const float boot = a.pv[(base + T - 1) * W + a.A];
+    const float boot = V(base + T - 1);
     float acc = 0.f, vs_next = boot, v1 = boot;
     for (int t = T - 2; t >= 0; --t) {
       const size_t row = base + t;
-      const float v = a.pv[row * W + a.A];
-      float r = a.reward[row];
+      const float v = V(row);
+      float r = R(row);
       r = fminf(fmaxf(r, -a.max_abs_reward), a.max_abs_reward);
-      const float g = a.gamma * a.discount[row];
-      const float cr = fminf(1.f, expf(a.lrho[row]));
+      const float g = a.gamma * D(row);
+      const float cr = fminf(1.f, expf(LR(row)));
       acc = cr * (r + g * v1 - v) + g * cr * acc;
       const float vs = acc + v;
       const float adv = cr * (r + g * vs_next - v);
       a.vs[(size_t)t * a.B + bb] = vs;
       a.pg_adv[(size_t)t * a.B + bb] = adv;
-      s_pg += -a.lpa[row] * adv;
+      s_pg += -LP(row) * adv;
       s_cr += (vs - v) * (vs - v);
-      s_en += -a.ent[row];
+      s_en += -EN(row);
       vs_next = vs;
       v1 = v;
     }
   }
-  red[b][0] = s_pg;
-  red[b][1] = s_cr;
-  red[b][2] = s_en;
+  if (b < 64) {
+    red[b][0] = s_pg;
+    red[b][1] = s_cr;
+    red[b][2] = s_en;
+  }
   __syncthreads();
   if (b == 0) {
     float pg = 0.f, cr = 0.f, en = 0.f;
@@ -958,6 +976,24 @@ __global__ void __launch_bounds__(64) impala_vtrace_kernel(const LossArgs a) {
     a.metrics[1] = cr + bad;
     a.metrics[2] = en + bad;
     a.metrics[3] = pg + bad;
+  }
+}
+
+__global__ void __launch_bounds__(256) impala_vtrace_kernel(const LossArgs a) {
+  extern __shared__ float sh[];  // [6][rows] when rows <= kVtraceLdsRows
+  const int rows = a.B * a.T, W = a.A + 1;
+  if (rows <= kVtraceLdsRows) {
+    float *sv = sh, *sr = sh + rows, *sd = sr + rows, *sl = sd + rows, *sp = sl + rows,
+          *se = sp + rows;
+    for (int i = threadIdx.x; i < rows; i += blockDim.x) {
+      const float v = a.pv[(size_t)i * W + a.A], r = a.reward[i], d = a.discount[i];
+      const float lr = a.lrho[i], lp = a.lpa[i], en = a.ent[i];
+      sv[i] = v; sr[i] = r; sd[i] = d; sl[i] = lr; sp[i] = lp; se[i] = en;
+    }
+    __syncthreads();
+    vtrace_scan<true>(a, sv, sr, sd, sl, sp, se);
+  } else {
+    vtrace_scan<false>(a, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
   }
 }
 
@@ -1090,33 +1126,52 @@ __global__ void __launch_bounds__(256) oar_finish_kernel(const float* __restrict
 
 // The last A + 1 rows of dW_i (the one-hot and tanh(prev r) embedding columns):
 // dW[F + j][n] = sum over rows with prev_a == j of dgates[m][n], dW[F + A][n] = sum of
-// tanh(prev_r[m]) dgates[m][n].  Block (n / 64, j): lane = column, wave w takes rows
-// m = w (mod 4); the four wave partials are summed in a fixed order through LDS.
-__global__ void __launch_bounds__(256) oar_wgrad_tail_kernel(const float* __restrict__ dg,
-                                                             int rows, int N,
-                                                             const int32_t* __restrict__ prev_a,
-                                                             const float* __restrict__ prev_r,
-                                                             int A, float* __restrict__ dw_tail) {
-  __shared__ float part[4][64];
+// tanh(prev_r[m]) dgates[m][n].  One pass over dgates: block = 64 columns x W waves (W =
+// blockDim.x / 64), wave w takes rows m = w, w + W, ... (kTailBatch loads in flight per
+// lane).  A row's action is wave-uniform, so the wave adds the row into its own LDS
+// accumulator row [w][a][lane]; the W wave partials of each output are then added in wave
+// order.  Deterministic.  (One block per output row, each re-reading all of dgates with 80
+// dependent loads per wave, took 21.6 us.)
+constexpr int kTailBatch = 10;
+inline int tail_waves(int A) { return A + 1 <= 32 ? 8 : 4; }  // LDS W (A + 1) 256 B <= 64 KB
+__global__ void __launch_bounds__(512) oar_wgrad_tail_kernel(
+    const float* __restrict__ dg, int rows, int N, const int32_t* __restrict__ prev_a,
+    const float* __restrict__ prev_r, int A, float* __restrict__ dw_tail) {
+  extern __shared__ float tacc[];  // [W][A + 1][64]
+  const int W = blockDim.x >> 6;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int n = blockIdx.x * 64 + lane, j = blockIdx.y;
-  float acc = 0.f;
-  if (n < N) {
-    if (j < A) {
-#pragma unroll 4
-      for (int m = wave; m < rows; m += 4) {
-        const float g = dg[(size_t)m * N + n];
-        acc += prev_a[m] == j ? g : 0.f;
-      }
-    } else {
-#pragma unroll 4
-      for (int m = wave; m < rows; m += 4) acc = fmaf(tanhf(prev_r[m]), dg[(size_t)m * N + n], acc);
+  const int n = blockIdx.x * 64 + lane, nc = min(n, N - 1);
+  const int J = A + 1;
+  float* my = tacc + (size_t)wave * J * 64;
+  for (int j = 0; j < J; ++j) my[j * 64 + lane] = 0.f;
+  float racc = 0.f;
+  for (int m0 = wave; m0 < rows; m0 += W * kTailBatch) {
+    float g[kTailBatch], tr[kTailBatch];
+    int act[kTailBatch];
+#pragma unroll
+    for (int b = 0; b < kTailBatch; ++b) {
+      const int mc = min(m0 + b * W, rows - 1);
+      g[b] = dg[(size_t)mc * N + nc];
+      act[b] = prev_a[mc];
+      tr[b] = prev_r[mc];
+    }
+#pragma unroll
+    for (int b = 0; b < kTailBatch; ++b) {
+      if (m0 + b * W >= rows) break;
+      const int a = __builtin_amdgcn_readfirstlane(act[b]);
+      if ((unsigned)a < (unsigned)A) my[a * 64 + lane] += g[b];
+      racc = fmaf(tanhf(tr[b]), g[b], racc);
     }
   }
-  part[wave][lane] = acc;
+  my[A * 64 + lane] = racc;
   __syncthreads();
-  if (wave == 0 && n < N)
-    dw_tail[(size_t)j * N + n] = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+  for (int e = threadIdx.x; e < J * 64; e += blockDim.x) {
+    const int j = e >> 6, nn = blockIdx.x * 64 + (e & 63);
+    if (nn >= N) continue;
+    float t = tacc[e];
+    for (int w = 1; w < W; ++w) t += tacc[(size_t)w * J * 64 + e];
+    dw_tail[(size_t)j * N + nn] = t;
+  }
 }
 
 torso::Weights torso_w(const acme_impala* l) {
@@ -1256,7 +1311,9 @@ int impala_step_impl(acme_impala* l, const acme_sequence_batch* bt, float* metri
     const unsigned rb = (unsigned)ceil_div(rows, 4);
     impala_rowstats_kernel<<<rb, 256, 0, st>>>(a);
     IM_CHECK();
-    impala_vtrace_kernel<<<1, 64, 0, st>>>(a);
+    const int vrows = B * T;
+    impala_vtrace_kernel<<<1, 256, vrows <= kVtraceLdsRows ? 6 * sizeof(float) * vrows : 0,
+                           st>>>(a);
     IM_CHECK();
     impala_loss_grad_kernel<<<rb, 256, 0, st>>>(a);
     IM_CHECK();
@@ -1327,7 +1384,9 @@ int impala_step_impl(acme_impala* l, const acme_sequence_batch* bt, float* metri
     }
     {
       ACME_PROF("impala_wi_wgrad_tail", st, 0.0, 4.0 * (double)rows * N);
-      oar_wgrad_tail_kernel<<<dim3((unsigned)ceil_div(N, 64), (unsigned)(A + 1)), 256, 0, st>>>(
+      const int tw = tail_waves(A);
+      oar_wgrad_tail_kernel<<<(unsigned)ceil_div(N, 64), 64 * tw,
+                              (size_t)tw * (A + 1) * 64 * sizeof(float), st>>>(
           l->dgates, rows, N, bt->prev_action, bt->prev_reward, A,
           Pm(l, gr, l->t_wi) + (size_t)F * N);
       IM_CHECK();
