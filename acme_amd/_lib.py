@@ -196,6 +196,7 @@ _SIGS = {
                                         ctypes.POINTER(c_i32), ctypes.POINTER(c_i64),
                                         ctypes.POINTER(ctypes.c_char_p)]),
     "acme_impala_bind": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "acme_impala_params_changed": (c_i32, [c_vp]),
     "acme_impala_step": (c_i32, [c_vp, ctypes.POINTER(SequenceBatch), c_vp, c_vp]),
     "acme_impala_set_lstm_unroll": (c_i32, [c_vp, c_i32]),
     "acme_impala_plane_overflow": (c_i32, [c_vp, ctypes.POINTER(c_i32), c_i32]),

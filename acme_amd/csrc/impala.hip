@@ -104,8 +104,11 @@ namespace {
 
 int64_t align64(int64_t x) { return (x + 63) & ~int64_t(63); }
 
-enum { kScX1, kScX2, kScX3, kScDz3, kScDz2, kScDz1, kScTransient, kScParams = kScTransient,
-       kScDgates, kScCount };
+// Every record is transient (written and read within a step, rescaled at its end from the
+// step's maxima): the activations, their gradients, dgates and the parameter planes (split
+// from the f32 parameters at the start of each forward).
+enum { kScX1, kScX2, kScX3, kScDz3, kScDz2, kScDz1, kScDgates, kScParams, kScTransient,
+       kScCount = kScTransient };
 
 int add_tensor(acme_impala* l, const std::string& name, std::initializer_list<int64_t> shape) {
   Tensor t;
@@ -1191,9 +1194,9 @@ int network_forward(acme_impala* l, const void* obs, const int32_t* prev_a, cons
     // the plane torso, then feat @ W_i[0:F] on the plane engine and the embedding tail.
     int rc;
     {
-      ACME_PROF("impala_planes", st, 0.0, 10.0 * (double)l->p3_prefix);
-      rc = launch_split_planes(l->params, l->p3_prefix, l->wpl, l->flat, l->scales + kScParams,
-                               st, l->overflow);
+      ACME_PROF("impala_planes", st, 0.0, 8.0 * (double)l->p3_prefix);
+      rc = launch_split_planes_lagged(l->params, l->p3_prefix, l->wpl, l->flat,
+                                      l->scales + kScParams, st);
       if (rc != ACME_OK) return rc;
     }
     {
@@ -1369,9 +1372,9 @@ int impala_step_impl(acme_impala* l, const acme_sequence_batch* bt, float* metri
   if (p3) {  // W_i, b and the embedding gradient on the plane engine, then the plane torso
     const int F = l->F, N = 4 * H;
     {
-      ACME_PROF("impala_dgates_planes", st, 0.0, 10.0 * (double)rows * N);
-      rc = launch_split_planes(l->dgates, (int64_t)rows * N, l->dgp.p, l->dgp.stride, l->dgp.sc,
-                               st, l->overflow);
+      ACME_PROF("impala_dgates_planes", st, 0.0, 8.0 * (double)rows * N);
+      rc = launch_split_planes_lagged(l->dgates, (int64_t)rows * N, l->dgp.p, l->dgp.stride,
+                                      l->dgp.sc, st);
       if (rc != ACME_OK) return rc;
     }
     {
@@ -1613,6 +1616,12 @@ int acme_impala_bind(acme_impala* l, float* params, float* grads, float* adam_m,
   l->grads = grads;
   l->m = adam_m;
   l->v = adam_v;
+  l->scales_ok = false;
+  return ACME_OK;
+}
+
+int acme_impala_params_changed(acme_impala* l) {
+  ACME_CHECK_ARG(l, "null learner");
   l->scales_ok = false;
   return ACME_OK;
 }

@@ -160,6 +160,10 @@ int launch_adam_slabs(float* p, float* g, float* m, float* v, const AdamSlabs& s
 int launch_split_planes(const float* x, int64_t n, uint16_t* planes, int64_t pstride,
                         gemm::PScale* sc, hipStream_t st, int* overflow = nullptr,
                         int keep_scale = 0);
+// Planes of x at the record's current w, max |x| committed to its amax slots (the record is
+// rescaled at the end of the step: lagged amax).  One launch.
+int launch_split_planes_lagged(const float* x, int64_t n, uint16_t* planes, int64_t pstride,
+                               gemm::PScale* sc, hipStream_t st);
 // max |x| of n floats into the record's amax slots (the parameter planes' next scale).
 int launch_param_amax(const float* x, int64_t n, gemm::PScale* sc, hipStream_t st);
 // End-of-step rescale of a record array (kernels.hip plane_rescale_kernel): records

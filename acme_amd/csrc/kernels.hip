@@ -798,6 +798,22 @@ __global__ void __launch_bounds__(256) split_planes_kernel(const float* __restri
     store_planes4(planes, pstride, i, reinterpret_cast<const f32x4*>(x)[i], w);
 }
 
+// Planes of x at the record's current write scale w, with the maximum of |x| committed to
+// the record's amax slots: the end-of-step rescale turns it into the next step's w (lagged
+// amax, as for the activations).  One pass instead of amax + scale set + split.
+__global__ void __launch_bounds__(256) split_planes_lagged_kernel(const float* __restrict__ x,
+                                                                  int64_t n4,
+                                                                  uint16_t* __restrict__ planes,
+                                                                  int64_t pstride,
+                                                                  gemm::PScale* __restrict__ sc) {
+  const float w = sc->w;
+  float mx = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x)
+    mx = fmaxf(mx, store_planes4(planes, pstride, i, reinterpret_cast<const f32x4*>(x)[i], w));
+  gemm::amax_commit(sc, mx);
+}
+
 // max |x| into sc->amax (which is 0 between rescales).
 __global__ void __launch_bounds__(256) amax_kernel(const float* __restrict__ x, int64_t n4,
                                                    gemm::PScale* __restrict__ sc) {
@@ -1297,6 +1313,16 @@ int launch_split_planes(const float* x, int64_t n, uint16_t* planes, int64_t pst
   plane_scale_set_kernel<<<1, 64, 0, st>>>(sc, overflow, keep_scale);
   ACME_LAUNCH_CHECK();
   split_planes_kernel<<<std::max(grid, 1u), 256, 0, st>>>(x, n4, planes, pstride, sc);
+  ACME_LAUNCH_CHECK();
+  return ACME_OK;
+}
+
+int launch_split_planes_lagged(const float* x, int64_t n, uint16_t* planes, int64_t pstride,
+                               gemm::PScale* sc, hipStream_t st) {
+  ACME_CHECK_ARG(n % 4 == 0 && pstride % 4 == 0 && sc, "plane split needs multiples of 4");
+  const int64_t n4 = n / 4;
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n4, 256), 2048);
+  split_planes_lagged_kernel<<<std::max(grid, 1u), 256, 0, st>>>(x, n4, planes, pstride, sc);
   ACME_LAUNCH_CHECK();
   return ACME_OK;
 }

@@ -773,6 +773,11 @@ class NativeIMPALA:
     def set_params(self, params: Dict[str, np.ndarray]) -> None:
         for name, t in self.views(self.params).items():
             t.copy_(torch.as_tensor(np.asarray(params[name], np.float32)).view(t.shape))
+        self.params_changed()
+
+    def params_changed(self) -> None:
+        """The bound parameters were written directly: plane scales recalibrate."""
+        check(lib().acme_impala_params_changed(self._h), "impala params_changed")
 
     @property
     def num_steps(self) -> int:

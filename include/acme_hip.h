@@ -523,14 +523,19 @@ int32_t acme_impala_num_tensors(const acme_impala* l);
 int acme_impala_tensor_info(const acme_impala* l, int32_t i, int64_t* offset, int64_t* numel,
                             int32_t* ndim, int64_t* shape4, const char** name);
 int acme_impala_bind(acme_impala* l, float* params, float* grads, float* adam_m, float* adam_v);
+/* Declares that the caller wrote the bound params buffer directly (restore, broadcast): the
+ * plane scales (the parameter planes' scale lags one step behind the parameters' maximum,
+ * like the activations') are recalibrated before the next step.  The learner's own updates
+ * need no call. */
+int acme_impala_params_changed(acme_impala* l);
 /* One SGD step; metrics (device, optional) = [loss, critic_loss, entropy_loss,
  * policy_gradient_loss] as logged by learning.py:162-167. */
 int acme_impala_step(acme_impala* l, const acme_sequence_batch* batch, float* metrics,
                      void* stream);
 /* Plane-range check of the Atari plane path (as acme_dqn_plane_overflow). */
 int acme_impala_plane_overflow(acme_impala* l, int32_t* overflow, int32_t reset);
-/* The LSTM unroll of this learner: 0 (default) = one cooperative launch each for the
- * forward and the backward when lstm_size = 256 and the batch is at most 64 sequences
+/* The LSTM unroll of this learner: 0 (default) = one launch each for the forward and the
+ * backward when lstm_size = 256 and the batch is at most 64 sequences
  * (workgroups own 4 sequences x 16 units and exchange h / dh partials as tagged granules;
  * spins bounded, debug buffer "lstm_timeout"), per-step launches otherwise; 1 = always
  * per-step launches. */
