@@ -66,7 +66,7 @@ def parse():
     p.add_argument("--num-actions", type=int, default=18)
     p.add_argument("--prefetch", type=int, default=4,
                    help="dataset prefetch_size (DQN; the reference DQN agent's default is 4)")
-    p.add_argument("--settle-seconds", type=float, default=0.3,
+    p.add_argument("--settle-seconds", type=float, default=0.5,
                    help="after the --warmup steps, further untimed steps until this much warm-up "
                         "time has passed (the GPU's clocks ramp over the first ~20 ms of load); "
                         "the count is reported as settle_steps")
