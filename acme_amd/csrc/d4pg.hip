@@ -1112,6 +1112,7 @@ extern "C" {
 
 int acme_d4pg_destroy(acme_d4pg* l) {
   if (!l) return ACME_OK;
+  (void)hipDeviceSynchronize();  // queued work of this learner finishes before its buffers go
   for (auto& g : l->graphs) (void)hipGraphExecDestroy(g.exec);
   if (l->capture) (void)hipStreamDestroy(l->capture);
   for (void* p : l->allocs) (void)hipFree(p);

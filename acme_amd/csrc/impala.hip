@@ -1459,6 +1459,9 @@ extern "C" {
 
 int acme_impala_destroy(acme_impala* l) {
   if (!l) return ACME_OK;
+  // Work of this learner may still be queued on a caller's stream (an actor network dropped
+  // right after its last step): drain it before the buffers go.
+  (void)hipDeviceSynchronize();
   for (void* p : l->allocs) (void)hipFree(p);
   delete l;
   return ACME_OK;
