@@ -123,6 +123,12 @@ _SIGS = {
     "acme_replay_commit": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp]),
     "acme_replay_sync_inserts": (c_i32, [c_vp]),
     "acme_host_register": (c_i32, [c_vp, c_i64]),
+    "acme_event_create": (c_i32, [ctypes.POINTER(c_vp)]),
+    "acme_event_destroy": (c_i32, [c_vp]),
+    "acme_event_record": (c_i32, [c_vp, c_vp]),
+    "acme_stream_wait_event": (c_i32, [c_vp, c_vp]),
+    "acme_event_query": (c_i32, [c_vp]),
+    "acme_event_synchronize": (c_i32, [c_vp]),
     "acme_host_unregister": (c_i32, [c_vp]),
     "acme_nstep_writer_create": (c_i32, [c_vp, c_i32, c_f32, c_i64, c_i64, c_i64, c_vp]),
     "acme_nstep_writer_destroy": (c_i32, [c_vp]),
@@ -182,6 +188,8 @@ _SIGS = {
     "acme_dqn_grad_split": (c_i32, [c_vp, ctypes.POINTER(c_i64)]),
     "acme_dqn_step": (c_i32, [c_vp, ctypes.POINTER(TransitionBatch), ctypes.POINTER(DQNOutputs),
                               c_vp]),
+    "acme_dqn_step_update": (c_i32, [c_vp, ctypes.POINTER(TransitionBatch),
+                                     ctypes.POINTER(DQNOutputs), c_vp, c_vp, c_vp]),
     "acme_dqn_q_values": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp]),
     "acme_dqn_num_steps": (c_i64, [c_vp]),
     "acme_dqn_debug_buffer": (c_i32, [c_vp, ctypes.c_char_p, ctypes.POINTER(c_vp),
@@ -285,6 +293,43 @@ def require_gpu() -> None:
 def stream_ptr(stream=None) -> int:
     s = stream if stream is not None else torch.cuda.current_stream()
     return int(s.cuda_stream)
+
+
+class OrderEvent:
+    """A device-scope stream-order event (acme_event_*), used like torch.cuda.Event for
+    record / wait / query between streams of one device.  torch's events fence at system
+    scope, which writes back and invalidates the caches: ~6 us of the recording stream's
+    time on MI355X.  Completion only: the host must not read device-written memory on the
+    strength of query() / synchronize()."""
+
+    def __init__(self):
+        self._lib = lib()
+        h = ctypes.c_void_p()
+        check(self._lib.acme_event_create(ctypes.byref(h)), "event create")
+        self._h = h
+
+    def record(self, stream=None) -> None:
+        check(self._lib.acme_event_record(self._h, stream_ptr(stream)), "event record")
+
+    def wait(self, stream=None) -> None:
+        check(self._lib.acme_stream_wait_event(stream_ptr(stream), self._h), "event wait")
+
+    def query(self) -> bool:
+        rc = self._lib.acme_event_query(self._h)
+        if rc < 0:
+            check(rc, "event query")
+        return rc == 1
+
+    def synchronize(self) -> None:
+        check(self._lib.acme_event_synchronize(self._h), "event synchronize")
+
+    def __del__(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h is not None and h.value:
+            try:
+                self._lib.acme_event_destroy(h)
+            except Exception:  # interpreter shutdown
+                pass
 
 
 def ptr(t) -> int:

@@ -118,11 +118,17 @@ class DQNLearner(core.Learner, core.Saveable):
         if fb is not None:
             fb = (fb[:2 * B] if obs_dt == torch.uint8 and fb.shape[0] >= 2 * B
                   and fb.shape[1] == self._obs_flat else None)
+        upd = None
         if self._dist is None and not self._staged:
-            self._native.step(*batch, obs_f16=fb)
+            # The priority write-back rides in the step (on the learner's second stream
+            # beside the backward) when the client's table offers it.
+            prep = getattr(self._replay_client, "prepare_priority_update", None)
+            if prep is not None:
+                upd = prep(adders.DEFAULT_PRIORITY_TABLE, keys)
+            self._native.step(*batch, obs_f16=fb, priority_update=upd)
         else:
             self._staged_step(batch, fb)
-        if self._replay_client is not None:
+        if self._replay_client is not None and upd is None:
             self._replay_client.update_priorities(table=adders.DEFAULT_PRIORITY_TABLE,
                                                   keys=keys,
                                                   priorities=self._native.priorities[:B])

@@ -65,6 +65,15 @@ bool use_x6() {
 }
 
 }  // namespace gemm
+
+hipError_t make_order_event(hipEvent_t* ev) {
+  // Device-scope release: no system-scope cache writeback / invalidation when the event
+  // is recorded or waited on (ACME_V_EVSYS=1 restores the default system-scope fence).
+  unsigned flags = hipEventDisableTiming;
+  if (tune_variant("EVSYS") != 1) flags |= hipEventDisableSystemFence;
+  return hipEventCreateWithFlags(ev, flags);
+}
+
 }  // namespace acme
 
 extern "C" {
@@ -89,5 +98,45 @@ int acme_tune_set(const char* key, int32_t value) {
 const char* acme_version(void) { return "acme_amd 0.1.0 (" __DATE__ " " __TIME__ ")"; }
 
 const char* acme_target_arch(void) { return "gfx950"; }
+
+int acme_event_create(void** ev) {
+  ACME_CHECK_ARG(ev, "null argument");
+  hipEvent_t e = nullptr;
+  ACME_HIP_TRY(acme::make_order_event(&e));
+  *ev = e;
+  return ACME_OK;
+}
+
+int acme_event_destroy(void* ev) {
+  if (ev) ACME_HIP_TRY(hipEventDestroy(static_cast<hipEvent_t>(ev)));
+  return ACME_OK;
+}
+
+int acme_event_record(void* ev, void* stream) {
+  ACME_CHECK_ARG(ev, "null event");
+  ACME_HIP_TRY(hipEventRecord(static_cast<hipEvent_t>(ev), acme::as_stream(stream)));
+  return ACME_OK;
+}
+
+int acme_stream_wait_event(void* stream, void* ev) {
+  ACME_CHECK_ARG(ev, "null event");
+  ACME_HIP_TRY(hipStreamWaitEvent(acme::as_stream(stream), static_cast<hipEvent_t>(ev), 0));
+  return ACME_OK;
+}
+
+int acme_event_query(void* ev) {
+  ACME_CHECK_ARG(ev, "null event");
+  const hipError_t e = hipEventQuery(static_cast<hipEvent_t>(ev));
+  if (e == hipSuccess) return 1;
+  if (e == hipErrorNotReady) return 0;
+  ACME_HIP_TRY(e);
+  return ACME_ERR_HIP;
+}
+
+int acme_event_synchronize(void* ev) {
+  ACME_CHECK_ARG(ev, "null event");
+  ACME_HIP_TRY(hipEventSynchronize(static_cast<hipEvent_t>(ev)));
+  return ACME_OK;
+}
 
 }  // extern "C"

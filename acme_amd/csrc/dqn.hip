@@ -108,6 +108,10 @@ struct acme_dqn {
   // reduces them on its read (launch_adam_slabs): three reduction launches fewer.
   float* slab2 = nullptr;    // conv2's slab (conv3's is side_slab, conv1's slab)
   bool fused_step = false;   // set by step_impl
+  // acme_dqn_step_update: the replay's priority write-back issued inside the step (on the
+  // second stream right after the loss), keys of the step's batch.
+  acme_replay* upd_replay = nullptr;
+  const uint64_t* upd_keys = nullptr;
   bool slabs_pending = false;
   torso::WgradSlab wslabs[3];
   float* side_slab = nullptr;
@@ -470,6 +474,13 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st_main,
     ACME_HIP_TRY(hipStreamWaitEvent(l->side, l->ev[2], 0));
     st = l->side;
   }
+  if (p3 && l->upd_replay && !l->calibrating) {  // the priority write-back, off the main
+                                                  // stream's tail
+    acme_replay* r = l->upd_replay;
+    l->upd_replay = nullptr;
+    if ((rc = acme_replay_update_priorities(r, l->upd_keys, la.prio, B, st)) != ACME_OK)
+      return rc;
+  }
   if (loss_sum) {
     ACME_PROF("loss_sum", st, 0.0, 0.0);
     rc = launch_dqn_loss_sum(la.loss_part, dqn_loss_head_dz_blocks(B, kHidden), la.mean_over,
@@ -697,7 +708,7 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
       if (tune("SIDE") != 1) {  // ACME_V_SIDE=1: single stream
         hipError_t e = hipStreamCreateWithFlags(&l->side, hipStreamNonBlocking);
         for (auto& ev : l->ev)
-          if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+          if (e == hipSuccess) e = make_order_event(&ev);
         if (e != hipSuccess)
           return fail((set_error("side stream: %s", hipGetErrorString(e)), ACME_ERR_HIP));
       }
@@ -738,7 +749,7 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
     }
     l->slab_floats = 1;
   }
-  if (hipEventCreateWithFlags(&l->ev_dense, hipEventDisableTiming) != hipSuccess)
+  if (make_order_event(&l->ev_dense) != hipSuccess)
     return fail((set_error("event creation failed"), ACME_ERR_HIP));
   if ((rc = dev_alloc(l, &l->q_on, (int64_t)2 * B * A)) ||
       (rc = dev_alloc(l, &l->q_tg, (int64_t)B * A)) ||
@@ -1238,7 +1249,7 @@ int acme_dqn_dp_init(acme_dqn* l, void* nccl_comm, int32_t world_size) {
   if (!acme::rccl::api()) return ACME_ERR_HIP;
   if (!l->dp_stream) {
     ACME_HIP_TRY(hipStreamCreateWithFlags(&l->dp_stream, hipStreamNonBlocking));
-    for (auto& e : l->dp_ev) ACME_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto& e : l->dp_ev) ACME_HIP_TRY(make_order_event(&e));
     int rc = dev_alloc(l, &l->dp_gmin, 1);
     if (rc != ACME_OK) return rc;
   }
@@ -1299,6 +1310,26 @@ int acme_dqn_dp_step(acme_dqn* l, const acme_transition_batch* batch, const acme
   ACME_HIP_TRY(hipStreamWaitEvent(st, l->dp_ev[3], 0));
   if ((rc = apply_impl(l, copies_target(l), st))) return rc;
   l->num_steps += 1;
+  return ACME_OK;
+}
+
+int acme_dqn_step_update(acme_dqn* l, const acme_transition_batch* batch,
+                         const acme_dqn_outputs* out, acme_replay* replay, const uint64_t* keys,
+                         void* stream) {
+  ACME_CHECK_ARG(l && batch && l->params, "null argument or unbound learner");
+  ACME_CHECK_ARG(replay && keys, "null replay or keys");
+  const bool inside = use_p3(l) && l->cfg.network == ACME_NET_NATURE_DQN && !l->calibrating;
+  l->upd_replay = inside ? replay : nullptr;
+  l->upd_keys = keys;
+  int rc = step_impl(l, batch, out, copies_target(l), as_stream(stream));
+  const bool pending = l->upd_replay != nullptr || !inside;
+  l->upd_replay = nullptr;
+  if (rc != ACME_OK) return rc;
+  l->num_steps += 1;
+  if (pending) {  // not issued inside the step (other paths): after it, on the stream
+    const double* prio = out && out->priorities ? out->priorities : l->prio_tmp;
+    return acme_replay_update_priorities(replay, keys, prio, batch->batch, stream);
+  }
   return ACME_OK;
 }
 

@@ -214,8 +214,10 @@ class _TableIterator:
         self._slots = []
         if self._P > 0:
             self._stream = torch.cuda.Stream(device=dev)
-            self._issued = torch.cuda.Event()
-            self._ready = [torch.cuda.Event() for _ in range(self._P + 2)]
+            # Device-scope events (no system-scope cache writeback and invalidation).
+            from acme_amd._lib import OrderEvent
+            self._issued = OrderEvent()
+            self._ready = [OrderEvent() for _ in range(self._P + 2)]
             self._next_slot = 0
         if self._shard is not None:
             import torch.distributed as dist

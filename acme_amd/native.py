@@ -538,11 +538,24 @@ class NativeDQN:
     def apply(self, stream=None):
         check(lib().acme_dqn_apply(self._h, stream_ptr(stream)), "dqn apply")
 
-    def step(self, *batch, q_tm1=None, stream=None, obs_f16=None):
+    def step(self, *batch, q_tm1=None, stream=None, obs_f16=None, priority_update=None):
+        """One SGD step.  priority_update = (native replay handle, uint64 keys tensor): the
+        batch's priorities are written back to that table as part of the step
+        (acme_dqn_step_update: beside the backward on the plane path)."""
         tb = self._batch(*batch, obs_f16=obs_f16)
         out = self._outputs(q_tm1)
-        check(lib().acme_dqn_step(self._h, ctypes.byref(tb), ctypes.byref(out),
-                                  stream_ptr(stream)), "dqn step")
+        if priority_update is None:
+            check(lib().acme_dqn_step(self._h, ctypes.byref(tb), ctypes.byref(out),
+                                      stream_ptr(stream)), "dqn step")
+            return
+        handle, keys = priority_update
+        if keys.dtype not in (torch.uint64, torch.int64) or not keys.is_contiguous():
+            raise ValueError("priority_update keys must be a contiguous 64-bit tensor")
+        if keys.numel() != int(tb.batch) or keys.device != self.device:
+            raise ValueError("priority_update keys must hold one key per batch row, on the "
+                             "learner's device")
+        check(lib().acme_dqn_step_update(self._h, ctypes.byref(tb), ctypes.byref(out), handle,
+                                         ptr(keys), stream_ptr(stream)), "dqn step")
 
     def q_values(self, obs: torch.Tensor, use_target: bool = False, stream=None) -> torch.Tensor:
         B = int(obs.shape[0])

@@ -325,6 +325,23 @@ class Table:
             self._draws += 1
             return d
 
+    def prepare_priority_update(self, keys):
+        """For a learner that writes the batch's priorities back inside its step
+        (acme_dqn_step_update): orders the current stream after the earlier prefetch reads,
+        as update_priorities does, and returns (native handle, device uint64 keys); None
+        when the table holds nothing to update."""
+        import torch
+        with self._mu:
+            if self._native is None:
+                return None
+            k = keys if isinstance(keys, torch.Tensor) else torch.as_tensor(
+                np.asarray(keys, np.uint64).view(np.int64)).view(torch.uint64)
+            k = k.to(self._native.device).contiguous()
+            if k.dtype == torch.int64:
+                k = k.view(torch.uint64)
+            self._after_readers()
+            return self._native.handle, k
+
     def update_priorities(self, keys, priorities) -> None:
         import torch
         with self._mu:
@@ -449,6 +466,9 @@ class QueueTable(Table):
     def update_priorities(self, keys, priorities) -> None:
         pass  # queue items carry no priorities (Reverb ignores updates of consumed items)
 
+    def prepare_priority_update(self, keys):
+        return None
+
 
 # ---------------------------------------------------------------- server / client
 _SERVERS: Dict[int, "Server"] = {}
@@ -545,6 +565,13 @@ class Client:
     def insert(self, data, priorities: Dict[str, float]):
         for table, p in priorities.items():
             self._server.tables[table].insert(data, p)
+
+    def prepare_priority_update(self, table: str, keys):
+        """(native handle, device keys) for a learner step that writes the priorities back
+        itself (Table.prepare_priority_update), or None."""
+        t = self._server.tables[table]
+        prep = getattr(t, "prepare_priority_update", None)
+        return prep(keys) if prep is not None else None
 
     def update_priorities(self, table: str, keys, priorities):
         """TFClient.update_priorities: device or host keys (u64) / priorities (f64)."""

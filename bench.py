@@ -75,6 +75,8 @@ def parse():
                    help="steps of the separate, untimed section-profiler pass")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-staged", action="store_true",
+                   help="dqn: skip the dp_staged_ms_per_step pass (kernel traces of the fused step)")
     return p.parse_args()
 
 
@@ -815,7 +817,7 @@ def main():
     # the collectives between them (DQNLearner._staged_step); the same stages on one GPU with
     # the collectives left out, timed like the line above (separately, after it).
     staged_ms = None
-    if "_set_staged" in meta and world == 1 and args.steps > 0:
+    if "_set_staged" in meta and world == 1 and args.steps > 0 and not args.no_staged:
         meta["_set_staged"](True)
         for i in range(min(args.warmup, 10)):
             step()

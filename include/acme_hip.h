@@ -56,6 +56,18 @@ const char* acme_version(void);
 /* Name of the GPU the library was built for ("gfx950"). */
 const char* acme_target_arch(void);
 
+/* Stream-order events between streams of one device (hipEventDisableTiming |
+ * hipEventDisableSystemFence): the record is a device-scope release, so it costs the
+ * recording stream no cache writeback; query / synchronize report completion only (the
+ * host must not read device-written memory on their strength).  Used by the dataset's
+ * prefetch ordering; the learners create theirs internally.  query: 1 complete, 0 pending. */
+int acme_event_create(void** ev);
+int acme_event_destroy(void* ev);
+int acme_event_record(void* ev, void* stream);
+int acme_stream_wait_event(void* stream, void* ev);
+int acme_event_query(void* ev);
+int acme_event_synchronize(void* ev);
+
 /* Matmul engine of the learners' dense layers (process-wide; default from the
  * ACME_MATMUL environment variable, "x6" unless it says "f32"):
  *   ACME_MATMUL_X6  f32 operands split exactly into three bf16 planes, six bf16 MFMAs
@@ -389,6 +401,17 @@ int acme_dqn_apply(acme_dqn* l, void* stream);
 /* forward_backward + apply. */
 int acme_dqn_step(acme_dqn* l, const acme_transition_batch* batch,
                   const acme_dqn_outputs* out, void* stream);
+/* acme_dqn_step followed by the learner's priority write-back of the batch
+ * (acme_replay_update_priorities(replay, keys, priorities, batch)), the order of
+ * DQNLearner._step then the replay client's update (acme/agents/tf/dqn/learning.py:
+ * 151-154).  On the uint8 Nature plane path the update is issued inside the step, on the
+ * learner's second stream as soon as the loss has written the priorities, so it runs
+ * beside the backward instead of after Adam; the step's final join orders it before the
+ * caller's later work.  The caller orders `stream` after earlier draws of the table
+ * (as for acme_replay_update_priorities).  Same results as the two calls. */
+int acme_dqn_step_update(acme_dqn* l, const acme_transition_batch* batch,
+                         const acme_dqn_outputs* out, acme_replay* replay,
+                         const uint64_t* keys, void* stream);
 /* Q forward only (online or target network) — actor/eval helper. */
 int acme_dqn_q_values(acme_dqn* l, const void* obs, int64_t batch, int32_t use_target,
                       float* q_out, void* stream);

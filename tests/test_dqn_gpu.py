@@ -386,3 +386,45 @@ def test_split_forward_stages_bitwise(kind):
     n.set_params(p0, t0)
     with pytest.raises(Exception):
         n.forward_backward_stage(3, *dev, global_min_probability=gmin)
+
+
+@pytest.mark.parametrize("kind", ["nature", "mlp"])
+def test_step_with_priority_update_equals_step_then_update(kind):
+    """acme_dqn_step_update (the write-back issued inside the step, on the second stream on
+    the plane path; after the step otherwise) equals acme_dqn_step followed by
+    acme_replay_update_priorities: same parameters, same raw priorities, same next draws."""
+    from acme_amd.native import NativeReplay
+    from acme_amd.networks import MLP, DQNAtariNetwork
+    net = DQNAtariNetwork(18) if kind == "nature" else MLP(8, [32, 32], 4)
+    B = 32
+    obs_shape = (84, 84, 4) if kind == "nature" else (8,)
+    p0, t0 = net.init(3), net.init(4)
+    a = _learner(net, B, target_update_period=2)
+    b = _learner(net, B, target_update_period=2)
+    a.set_params(p0, t0)
+    b.set_params(p0, t0)
+    tables = [NativeReplay(1000, [4], prioritized=True, priority_exponent=0.6, seed=77)
+              for _ in range(2)]
+    rows = np.arange(600, dtype=np.uint32).view(np.uint8).reshape(600, 4)
+    for t in tables:
+        t.insert([rows], np.linspace(0.5, 2.0, 600))
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(21)
+    for step in range(3):
+        keys = tables[0].sample(B, step)["keys"]
+        assert torch.equal(keys, tables[1].sample(B, step)["keys"])
+        dev = _dev(_batch(rng, B, obs_shape, net.num_actions, u8=kind == "nature"))
+        a.step(*dev, priority_update=(tables[0].handle, keys))
+        b.step(*dev)
+        tables[1].update_priorities(keys, b.priorities[:B])
+        torch.cuda.synchronize()
+        assert a.loss.item() == b.loss.item()
+        sa, sb = tables[0].export_state(), tables[1].export_state()
+        np.testing.assert_array_equal(sa["raw_priorities"], sb["raw_priorities"])
+        for buf in ("params", "target"):
+            ga, gb = a.get_params(buf), b.get_params(buf)
+            for k in ga:
+                np.testing.assert_array_equal(ga[k], gb[k], err_msg=f"{buf}/{k}")
+    da, db = tables[0].sample(B, 99), tables[1].sample(B, 99)
+    for k in da:
+        assert torch.equal(da[k], db[k]), k
