@@ -59,7 +59,7 @@ class DQNConfig(ctypes.Structure):
 class TransitionBatch(ctypes.Structure):
     _fields_ = [("o_tm1", c_vp), ("a_tm1", c_vp), ("r_t", c_vp), ("d_t", c_vp), ("o_t", c_vp),
                 ("probabilities", c_vp), ("batch", c_i64), ("global_min_probability", c_vp),
-                ("mean_over", c_i64), ("obs_f16", c_vp)]
+                ("mean_over", c_i64), ("obs_f16", c_vp), ("inputs_event", c_vp)]
 
 
 class DQNOutputs(ctypes.Structure):
@@ -189,7 +189,7 @@ _SIGS = {
     "acme_dqn_step": (c_i32, [c_vp, ctypes.POINTER(TransitionBatch), ctypes.POINTER(DQNOutputs),
                               c_vp]),
     "acme_dqn_step_update": (c_i32, [c_vp, ctypes.POINTER(TransitionBatch),
-                                     ctypes.POINTER(DQNOutputs), c_vp, c_vp, c_vp]),
+                                     ctypes.POINTER(DQNOutputs), c_vp, c_vp, c_vp, c_vp]),
     "acme_dqn_q_values": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp]),
     "acme_dqn_num_steps": (c_i64, [c_vp]),
     "acme_dqn_debug_buffer": (c_i32, [c_vp, ctypes.c_char_p, ctypes.POINTER(c_vp),
@@ -322,6 +322,11 @@ class OrderEvent:
 
     def synchronize(self) -> None:
         check(self._lib.acme_event_synchronize(self._h), "event synchronize")
+
+    @property
+    def handle(self) -> int:
+        """The raw hipEvent_t (for C entry points that take an event)."""
+        return int(self._h.value)
 
     def __del__(self):
         h, self._h = getattr(self, "_h", None), None

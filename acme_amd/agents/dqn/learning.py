@@ -14,6 +14,7 @@ reference's deepcopy + create_variables (agents/tf/dqn/agent.py:127-131).
 
 from __future__ import annotations
 
+import os
 import time
 from typing import Dict, List, Optional
 
@@ -105,12 +106,15 @@ class DQNLearner(core.Learner, core.Saveable):
         keys, probs = sample.info[:2]
         B = int(a_tm1.shape[0])
         obs_dt = torch.uint8 if self._network.obs_dtype == "uint8" else torch.float32
-        batch = (self._prepare(o_tm1.reshape(B, self._obs_flat), obs_dt),
-                 self._prepare(a_tm1.reshape(B), torch.int32),
-                 self._prepare(r_t.reshape(B), torch.float32),
-                 self._prepare(d_t.reshape(B), torch.float32),
-                 self._prepare(o_t.reshape(B, self._obs_flat), obs_dt),
-                 self._prepare(probs, torch.float64))
+        views = (o_tm1.reshape(B, self._obs_flat), a_tm1.reshape(B), r_t.reshape(B),
+                 d_t.reshape(B), o_t.reshape(B, self._obs_flat), probs)
+        batch = tuple(self._prepare(x, dt) for x, dt in zip(
+            views, (obs_dt, torch.int32, torch.float32, torch.float32, obs_dt, torch.float64)))
+        # The dataset's order event stands for the learner's fork of its second stream only if
+        # nothing was enqueued since (no dtype / layout conversion above).
+        inputs_event = getattr(self._iterator, "last_inputs_event", None)
+        if any(b is not v for b, v in zip(batch, views)) or os.environ.get("ACME_V_INEV") == "1":
+            inputs_event = None
         # The dataset's fused gather also wrote the exact f16 copy of [o_tm1; o_t] (uint8
         # tables; rows [0, B) and [B, 2B) of its buffer): the learner then skips its own
         # conversion (same bits).
@@ -123,9 +127,9 @@ class DQNLearner(core.Learner, core.Saveable):
             # The priority write-back rides in the step (on the learner's second stream
             # beside the backward) when the client's table offers it.
             prep = getattr(self._replay_client, "prepare_priority_update", None)
-            if prep is not None:
+            if prep is not None and os.environ.get("ACME_V_STEPUPD") != "1":  # 1: A/B off
                 upd = prep(adders.DEFAULT_PRIORITY_TABLE, keys)
-            self._native.step(*batch, obs_f16=fb, priority_update=upd)
+            self._native.step(*batch, obs_f16=fb, priority_update=upd, inputs_event=inputs_event)
         else:
             self._staged_step(batch, fb)
         if self._replay_client is not None and upd is None:

@@ -112,6 +112,7 @@ struct acme_dqn {
   // second stream right after the loss), keys of the step's batch.
   acme_replay* upd_replay = nullptr;
   const uint64_t* upd_keys = nullptr;
+  hipEvent_t upd_after = nullptr;  // the table's last device read (the update waits for it)
   bool slabs_pending = false;
   torso::WgradSlab wslabs[3];
   float* side_slab = nullptr;
@@ -478,6 +479,7 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st_main,
                                                   // stream's tail
     acme_replay* r = l->upd_replay;
     l->upd_replay = nullptr;
+    if (l->upd_after) ACME_HIP_TRY(hipStreamWaitEvent(st, l->upd_after, 0));
     if ((rc = acme_replay_update_priorities(r, l->upd_keys, la.prio, B, st)) != ACME_OK)
       return rc;
   }
@@ -1035,6 +1037,8 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
   // target on o_t (q_t_value).
   l->last_p3 = nature && use_p3(l);
   if (l->last_p3) {
+    // The caller's inputs event can stand for the fork only if nothing is enqueued here first.
+    const bool quiet = !l->planes_stale && l->scales_ok && batch->obs_f16 && !l->calibrating;
     if ((rc = sync_planes(l, st)) != ACME_OK) return rc;
     if (!l->scales_ok && !l->calibrating && (rc = calibrate_scales(l, batch, st)) != ACME_OK)
       return rc;
@@ -1053,8 +1057,12 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
     l->cur_frames = fwd_frames;
     // Target forward (q_t_value) on the side stream, beside the online forward.
     if (side) {
-      ACME_HIP_TRY(hipEventRecord(l->ev[0], st));
-      ACME_HIP_TRY(hipStreamWaitEvent(side, l->ev[0], 0));
+      if (quiet && batch->inputs_event) {
+        ACME_HIP_TRY(hipStreamWaitEvent(side, static_cast<hipEvent_t>(batch->inputs_event), 0));
+      } else {
+        ACME_HIP_TRY(hipEventRecord(l->ev[0], st));
+        ACME_HIP_TRY(hipStreamWaitEvent(side, l->ev[0], 0));
+      }
       tst = side;
     }
     if ((rc = nature_forward_p3(l, l->target, l->tpl, fwd_frames.rows_from(B), B,
@@ -1315,12 +1323,13 @@ int acme_dqn_dp_step(acme_dqn* l, const acme_transition_batch* batch, const acme
 
 int acme_dqn_step_update(acme_dqn* l, const acme_transition_batch* batch,
                          const acme_dqn_outputs* out, acme_replay* replay, const uint64_t* keys,
-                         void* stream) {
+                         void* after_event, void* stream) {
   ACME_CHECK_ARG(l && batch && l->params, "null argument or unbound learner");
   ACME_CHECK_ARG(replay && keys, "null replay or keys");
   const bool inside = use_p3(l) && l->cfg.network == ACME_NET_NATURE_DQN && !l->calibrating;
   l->upd_replay = inside ? replay : nullptr;
   l->upd_keys = keys;
+  l->upd_after = static_cast<hipEvent_t>(after_event);
   int rc = step_impl(l, batch, out, copies_target(l), as_stream(stream));
   const bool pending = l->upd_replay != nullptr || !inside;
   l->upd_replay = nullptr;
@@ -1328,6 +1337,8 @@ int acme_dqn_step_update(acme_dqn* l, const acme_transition_batch* batch,
   l->num_steps += 1;
   if (pending) {  // not issued inside the step (other paths): after it, on the stream
     const double* prio = out && out->priorities ? out->priorities : l->prio_tmp;
+    if (after_event)
+      ACME_HIP_TRY(hipStreamWaitEvent(as_stream(stream), static_cast<hipEvent_t>(after_event), 0));
     return acme_replay_update_priorities(replay, keys, prio, batch->batch, stream);
   }
   return ACME_OK;

@@ -481,6 +481,12 @@ class NativeDQN:
             tb.obs_f16 = ptr(obs_f16)
         return tb
 
+    @staticmethod
+    def _event_handle(ev) -> Optional[int]:
+        if ev is None:
+            return None
+        return ev.handle if hasattr(ev, "handle") else int(ev.cuda_event)
+
     def _outputs(self, q_tm1=None):
         o = _lib.DQNOutputs()
         o.loss, o.td_error, o.priorities = ptr(self.loss), ptr(self.td_error), ptr(self.priorities)
@@ -538,24 +544,29 @@ class NativeDQN:
     def apply(self, stream=None):
         check(lib().acme_dqn_apply(self._h, stream_ptr(stream)), "dqn apply")
 
-    def step(self, *batch, q_tm1=None, stream=None, obs_f16=None, priority_update=None):
-        """One SGD step.  priority_update = (native replay handle, uint64 keys tensor): the
-        batch's priorities are written back to that table as part of the step
-        (acme_dqn_step_update: beside the backward on the plane path)."""
+    def step(self, *batch, q_tm1=None, stream=None, obs_f16=None, priority_update=None,
+             inputs_event=None):
+        """One SGD step.  priority_update = (native replay handle, uint64 keys tensor[, raw
+        hipEvent_t of the table's last device read or None]): the batch's priorities are
+        written back to that table as part of the step (acme_dqn_step_update: beside the
+        backward on the plane path, after that read).  inputs_event: an event recorded on the
+        stream after the inputs were ready, with nothing enqueued on it since
+        (acme_transition_batch.inputs_event)."""
         tb = self._batch(*batch, obs_f16=obs_f16)
+        tb.inputs_event = self._event_handle(inputs_event)
         out = self._outputs(q_tm1)
         if priority_update is None:
             check(lib().acme_dqn_step(self._h, ctypes.byref(tb), ctypes.byref(out),
                                       stream_ptr(stream)), "dqn step")
             return
-        handle, keys = priority_update
+        handle, keys, after = (tuple(priority_update) + (None,))[:3]
         if keys.dtype not in (torch.uint64, torch.int64) or not keys.is_contiguous():
             raise ValueError("priority_update keys must be a contiguous 64-bit tensor")
         if keys.numel() != int(tb.batch) or keys.device != self.device:
             raise ValueError("priority_update keys must hold one key per batch row, on the "
                              "learner's device")
         check(lib().acme_dqn_step_update(self._h, ctypes.byref(tb), ctypes.byref(out), handle,
-                                         ptr(keys), stream_ptr(stream)), "dqn step")
+                                         ptr(keys), after, stream_ptr(stream)), "dqn step")
 
     def q_values(self, obs: torch.Tensor, use_target: bool = False, stream=None) -> torch.Tensor:
         B = int(obs.shape[0])

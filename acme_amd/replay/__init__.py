@@ -327,9 +327,10 @@ class Table:
 
     def prepare_priority_update(self, keys):
         """For a learner that writes the batch's priorities back inside its step
-        (acme_dqn_step_update): orders the current stream after the earlier prefetch reads,
-        as update_priorities does, and returns (native handle, device uint64 keys); None
-        when the table holds nothing to update."""
+        (acme_dqn_step_update): (native handle, device uint64 keys, raw event of the last
+        prefetch read still in flight or None), the read the update must follow (as
+        update_priorities orders the current stream after it); None when the table holds
+        nothing to update."""
         import torch
         with self._mu:
             if self._native is None:
@@ -339,8 +340,11 @@ class Table:
             k = k.to(self._native.device).contiguous()
             if k.dtype == torch.int64:
                 k = k.view(torch.uint64)
-            self._after_readers()
-            return self._native.handle, k
+            ev = self._reader_event
+            after = None
+            if ev is not None and not ev.query():
+                after = ev.handle if hasattr(ev, "handle") else int(ev.cuda_event)
+            return self._native.handle, k, after
 
     def update_priorities(self, keys, priorities) -> None:
         import torch

@@ -354,6 +354,13 @@ typedef struct acme_transition_batch {
    * u16, as acme_replay_sample_gather_frames writes it; the learner then skips its own
    * conversion (same bits).  NULL: the learner converts. */
   const uint16_t* obs_f16;
+  /* Optional (hipEvent_t): an event recorded on the caller's stream after which the caller
+   * enqueued nothing on it before this call, with the batch's inputs complete at it (a
+   * prefetching dataset's order event).  The learner's second stream then starts from it
+   * instead of from an event record of its own (which costs the caller's stream 5-9 us).
+   * Used only when the learner itself enqueues nothing first (no plane refresh,
+   * calibration or frame conversion).  NULL: the learner records its own. */
+  void* inputs_event;
 } acme_transition_batch;
 
 typedef struct acme_dqn_outputs {
@@ -407,11 +414,13 @@ int acme_dqn_step(acme_dqn* l, const acme_transition_batch* batch,
  * 151-154).  On the uint8 Nature plane path the update is issued inside the step, on the
  * learner's second stream as soon as the loss has written the priorities, so it runs
  * beside the backward instead of after Adam; the step's final join orders it before the
- * caller's later work.  The caller orders `stream` after earlier draws of the table
- * (as for acme_replay_update_priorities).  Same results as the two calls. */
+ * caller's later work.  after_event (hipEvent_t, optional): the table's last device read
+ * on another stream (a prefetching dataset's draw); the update waits for it on the stream
+ * that issues it, as a caller of acme_replay_update_priorities orders its stream after
+ * those draws.  Same results as the two calls. */
 int acme_dqn_step_update(acme_dqn* l, const acme_transition_batch* batch,
                          const acme_dqn_outputs* out, acme_replay* replay,
-                         const uint64_t* keys, void* stream);
+                         const uint64_t* keys, void* after_event, void* stream);
 /* Q forward only (online or target network) — actor/eval helper. */
 int acme_dqn_q_values(acme_dqn* l, const void* obs, int64_t batch, int32_t use_target,
                       float* q_out, void* stream);
