@@ -110,8 +110,9 @@ class DQNLearner(core.Learner, core.Saveable):
                  d_t.reshape(B), o_t.reshape(B, self._obs_flat), probs)
         batch = tuple(self._prepare(x, dt) for x, dt in zip(
             views, (obs_dt, torch.int32, torch.float32, torch.float32, obs_dt, torch.float64)))
-        # The dataset's order event stands for the learner's fork of its second stream only if
-        # nothing was enqueued since (no dtype / layout conversion above).
+        # The batch's ready event lets the learner start its target forward without waiting
+        # for the previous step's tail, unless a conversion above produced new tensors on
+        # this stream.
         inputs_event = getattr(self._iterator, "last_inputs_event", None)
         if any(b is not v for b, v in zip(batch, views)) or os.environ.get("ACME_V_INEV") == "1":
             inputs_event = None

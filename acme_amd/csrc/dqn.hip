@@ -116,6 +116,14 @@ struct acme_dqn {
   bool slabs_pending = false;
   torso::WgradSlab wslabs[3];
   float* side_slab = nullptr;
+  // The target forward's split-K slab (its own: the fused step's Adam reads side_slab while
+  // the side stream may already run the next step's target forward).
+  float* tslab = nullptr;
+  // The target forward starts on the side stream without ordering after the caller's
+  // stream (the batch's inputs event only), unless the caller's stream wrote target state
+  // since the last step: a target copy, q_values' forward, calibration.  The target's
+  // activation scale records (kScT1..kScT3) are rescaled on the side stream after it.
+  bool target_dirty = true;
   torso::Plane x1p{}, x2p{}, x3p{}, t1p{}, t2p{}, t3p{}, dzhp{}, dz3p{}, dz2p{}, dz1p{};
   // Plane path: the loss is launched together with the head dZ (launch_dqn_loss_head_dz)
   // by the backward; forward_backward_stage leaves its arguments here.
@@ -717,6 +725,7 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
       // The side stream's slab, and conv2's for the fused step's deferred reductions (also
       // with one stream: ACME_V_SIDE=1 profiles the same kernels).
       if ((rc = dev_alloc(l, &l->side_slab, l->slab_floats)) ||
+          (rc = dev_alloc(l, &l->tslab, l->slab_floats)) ||
           (rc = dev_alloc(l, &l->slab2, torso::wgrad_slab_floats_p3())))
         return fail(rc);
     }
@@ -817,6 +826,7 @@ int acme_dqn_params_changed(acme_dqn* l) {
   ACME_CHECK_ARG(l, "null learner");
   l->planes_stale = true;
   l->scales_ok = false;  // new parameters: recalibrate (unless a scale state is restored)
+  l->target_dirty = true;
   return ACME_OK;
 }
 
@@ -845,6 +855,7 @@ int acme_dqn_set_scale_state(acme_dqn* l, const float* in, int32_t count) {
   for (int i = 0; i < kScCount; ++i)
     ACME_HIP_TRY(hipMemcpy(l->scales + i, in + 4 * i, 4 * sizeof(float), hipMemcpyHostToDevice));
   l->scales_ok = true;
+  l->target_dirty = true;
   return ACME_OK;
 }
 
@@ -922,6 +933,7 @@ int acme_dqn_q_values(acme_dqn* l, const void* obs, int64_t batch, int32_t use_t
   const float* prm = use_target ? l->target : l->params;
   const int B = (int)batch;
   if (l->cfg.network == ACME_NET_NATURE_DQN && use_p3(l)) {
+    l->target_dirty = true;  // the target activations and their records, on this stream
     int rc = sync_planes(l, st);
     if (rc == ACME_OK) rc = convert_frames(l, obs, obs, B, B, st);
     // Uncalibrated scales: one forward to measure the activations, then the real one.
@@ -1057,17 +1069,24 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
     l->cur_frames = fwd_frames;
     // Target forward (q_t_value) on the side stream, beside the online forward.
     if (side) {
-      if (quiet && batch->inputs_event) {
+      // Early start: the side stream's own order covers the previous step's target work
+      // and T-record rescale; only the batch's inputs are waited for.
+      if (quiet && batch->inputs_event && !l->target_dirty && tune("TEARLY") != 1) {
         ACME_HIP_TRY(hipStreamWaitEvent(side, static_cast<hipEvent_t>(batch->inputs_event), 0));
       } else {
         ACME_HIP_TRY(hipEventRecord(l->ev[0], st));
         ACME_HIP_TRY(hipStreamWaitEvent(side, l->ev[0], 0));
       }
+      l->target_dirty = l->calibrating;
       tst = side;
+    } else {
+      l->target_dirty = true;  // the target forward runs on the caller's stream
     }
     if ((rc = nature_forward_p3(l, l->target, l->tpl, fwd_frames.rows_from(B), B,
                                 l->t1p, l->t2p, l->t3p, l->thid, l->q_tg, tst,
-                                side ? l->side_slab : l->slab, 0)) != ACME_OK)
+                                side ? l->tslab : l->slab, 0)) != ACME_OK)
+      return rc;
+    if (side && (rc = launch_plane_rescale(l->scales + kScT1, 3, 3, -1, -1, l->overflow, side)))
       return rc;
     if (side) ACME_HIP_TRY(hipEventRecord(l->ev[1], side));
     if ((rc = nature_forward_p3(l, l->params, l->wpl, fwd_frames, 2 * B, l->x1p, l->x2p, l->x3p,
@@ -1194,6 +1213,7 @@ static int apply_impl(acme_dqn* l, bool copy, hipStream_t st) {
     if ((rc = adam_range(l, 0, l->flat, st)) != ACME_OK) return rc;
   }
   if (copy) {
+    l->target_dirty = true;
     ACME_PROF("target_copy", st, 0.0, 8.0 * (double)l->logical);
     ACME_HIP_TRY(hipMemcpyAsync(l->target, l->params, l->flat * sizeof(float),
                                 hipMemcpyDeviceToDevice, st));
@@ -1213,8 +1233,12 @@ static int apply_impl(acme_dqn* l, bool copy, hipStream_t st) {
     }
     {
       ACME_PROF("plane_rescale", st, 0.0, 0.0);
+      // The target activations' records were rescaled on the side stream (which may already
+      // run the next step's target forward).
+      const bool side = side_stream(l) != nullptr;
       rc = launch_plane_rescale(l->scales, kScTransient, kScTarget, copy ? kScParams : -1,
-                                copy ? kScTarget : -1, l->overflow, st);
+                                copy ? kScTarget : -1, l->overflow, st, side ? kScT1 : -1,
+                                side ? kScT3 + 1 : -1);
     }
   }
   return rc;

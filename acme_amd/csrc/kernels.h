@@ -168,9 +168,10 @@ int launch_split_planes_lagged(const float* x, int64_t n, uint16_t* planes, int6
 int launch_param_amax(const float* x, int64_t n, gemm::PScale* sc, hipStream_t st);
 // End-of-step rescale of a record array (kernels.hip plane_rescale_kernel): records
 // [0, n_transient) transient, [n_transient, n) persistent (rewritten by every Adam pass);
-// copy_to >= n, if >= 0, took a plane copy of copy_from's latest write.
+// copy_to >= n, if >= 0, took a plane copy of copy_from's latest write.  Records in
+// [skip_lo, skip_hi) are left alone (rescaled on the stream that writes them).
 int launch_plane_rescale(gemm::PScale* recs, int n_transient, int n, int copy_from, int copy_to,
-                         int* overflow, hipStream_t st);
+                         int* overflow, hipStream_t st, int skip_lo = -1, int skip_hi = -1);
 // uint8 frames -> exact f16 (one plane): out[f][e] = f16(frame f byte e) for rows frames
 // of `frame_bytes` (multiple of 8), frames [0, split) from a and the rest from b.
 int launch_frames_f16(const uint8_t* a, const uint8_t* b, int split, int rows, int frame_bytes,

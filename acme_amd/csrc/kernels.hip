@@ -875,7 +875,8 @@ __global__ void __launch_bounds__(64) plane_scale_set_kernel(gemm::PScale* __res
 // every store: the kernel sits between two steps on the critical path.
 __global__ void __launch_bounds__(1024) plane_rescale_kernel(gemm::PScale* __restrict__ s, int nt,
                                                              int n, int copy_from, int copy_to,
-                                                             int* __restrict__ overflow) {
+                                                             int* __restrict__ overflow,
+                                                             int skip_lo, int skip_hi) {
   const int i = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ic = i < n ? i : 0;
   uint32_t a_bits = s[ic].slot[lane].v;
@@ -889,6 +890,7 @@ __global__ void __launch_bounds__(1024) plane_rescale_kernel(gemm::PScale* __res
     }
     return;
   }
+  if (i >= skip_lo && i < skip_hi) return;  // rescaled by their own stream
   s[i].slot[lane].v = 0u;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) a_bits = max(a_bits, (uint32_t)__shfl_xor((int)a_bits, o, 64));
@@ -1337,13 +1339,13 @@ int launch_param_amax(const float* x, int64_t n, gemm::PScale* sc, hipStream_t s
 }
 
 int launch_plane_rescale(gemm::PScale* recs, int n_transient, int n, int copy_from, int copy_to,
-                         int* overflow, hipStream_t st) {
+                         int* overflow, hipStream_t st, int skip_lo, int skip_hi) {
   ACME_CHECK_ARG(recs && overflow && n >= 1 && n <= 15 && n_transient >= 0 && n_transient <= n,
                  "bad rescale arguments");
   ACME_CHECK_ARG(copy_to < 0 || (copy_to >= n && copy_from >= 0 && copy_from < n),
                  "bad rescale copy");
   plane_rescale_kernel<<<1, (unsigned)(64 * (n + 1)), 0, st>>>(recs, n_transient, n, copy_from,
-                                                               copy_to, overflow);
+                                                               copy_to, overflow, skip_lo, skip_hi);
   ACME_LAUNCH_CHECK();
   return ACME_OK;
 }

@@ -281,8 +281,20 @@ int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int row
     return (set_error("deferred weight gradients need two side slabs"), ACME_ERR_INVALID);
   hipStream_t st = fork ? sd.side : st_main;
   float* wslab = fork || defer ? sd.slab : slab;
+  // ACME_V_TFORK=1: one fork after conv3's input gradient for both weight gradients (one
+  // event record fewer on the main stream).
+  const bool one_fork = fork && tune_variant("TFORK") == 1;
+  if (one_fork) {
+    P3ConvDgrad<G3> p;
+    p.M = rows * G3::IPIX; p.N = G3::CI; p.K = G3::KH * G3::KW * G3::CO; p.k_chunk = p.K;
+    p.a_src = src(dz3, (int64_t)rows * kFlat); p.b_src = src(w.w3, G3::K * G3::CO);
+    p.xprev = cp(a.x2); p.dx = pl(dz2);
+    P3I_GEMM("conv3_dgrad", I3D, 2, 64, 8, 2, 1, p, rows);
+    ACME_HIP_TRY(hipEventRecord(sd.e[1], st_main));
+    ACME_HIP_TRY(hipStreamWaitEvent(sd.side, sd.e[1], 0));
+  }
   {  // conv3 weight + bias gradient
-    if (fork) {
+    if (fork && !one_fork) {
       ACME_HIP_TRY(hipEventRecord(sd.e[0], st_main));
       ACME_HIP_TRY(hipStreamWaitEvent(sd.side, sd.e[0], 0));
     }
@@ -298,7 +310,7 @@ int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int row
       return rc;
   }
   st = st_main;
-  {
+  if (!one_fork) {
     P3ConvDgrad<G3> p;
     p.M = rows * G3::IPIX; p.N = G3::CI; p.K = G3::KH * G3::KW * G3::CO; p.k_chunk = p.K;
     p.a_src = src(dz3, (int64_t)rows * kFlat); p.b_src = src(w.w3, G3::K * G3::CO);
@@ -307,8 +319,10 @@ int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int row
     P3I_GEMM("conv3_dgrad", I3D, 2, 64, 8, 2, 1, p, rows);
   }
   if (fork) {
-    ACME_HIP_TRY(hipEventRecord(sd.e[1], st_main));
-    ACME_HIP_TRY(hipStreamWaitEvent(sd.side, sd.e[1], 0));
+    if (!one_fork) {
+      ACME_HIP_TRY(hipEventRecord(sd.e[1], st_main));
+      ACME_HIP_TRY(hipStreamWaitEvent(sd.side, sd.e[1], 0));
+    }
     st = sd.side;
   }
   {  // conv2

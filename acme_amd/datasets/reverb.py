@@ -381,15 +381,7 @@ class _TableIterator:
         # Under the section profiler the batches are issued on the caller's stream, so no
         # profiled kernel shares the GPU with a prefetch (same draws, same order).
         side = main if profiling() else self._stream
-        # The batch handed out below was issued by an earlier call (steady state): the
-        # caller's stream is ordered after it (if still in flight) before the order event,
-        # which then also marks the batch complete on the caller's stream: a learner may
-        # start its own second stream from it (`last_inputs_event`).
-        handed = self._queue[0] if self._queue else None
-        if handed is not None and not self._ready[handed].query():
-            main.wait_event(self._ready[handed])
         self._issued.record(main)
-        self.last_inputs_event = self._issued if handed is not None and side is not main else None
         side.wait_event(self._issued)
         st = stream_ptr(side)
         while len(self._queue) < self._P + 1:
@@ -404,8 +396,11 @@ class _TableIterator:
         # A batch issued P steps ago has normally landed: ordering the caller's stream
         # after a completed event is a no-op, and skipping the wait saves its queue-side
         # cost (each event wait / record on a stream leaves ~7 us before the next kernel).
-        if i != handed and not self._ready[i].query():
+        if not self._ready[i].query():
             main.wait_event(self._ready[i])
+        # The batch is complete at its ready event (recorded on the dataset's stream): a
+        # learner may start work on another stream of its own from it.
+        self.last_inputs_event = self._ready[i] if side is not main else None
         self.last_frames_f16 = self._fb[i]
         return self._sample_view(i, self._share[i])
 

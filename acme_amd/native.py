@@ -549,9 +549,8 @@ class NativeDQN:
         """One SGD step.  priority_update = (native replay handle, uint64 keys tensor[, raw
         hipEvent_t of the table's last device read or None]): the batch's priorities are
         written back to that table as part of the step (acme_dqn_step_update: beside the
-        backward on the plane path, after that read).  inputs_event: an event recorded on the
-        stream after the inputs were ready, with nothing enqueued on it since
-        (acme_transition_batch.inputs_event)."""
+        backward on the plane path, after that read).  inputs_event: an event at which the
+        batch's inputs are complete (acme_transition_batch.inputs_event)."""
         tb = self._batch(*batch, obs_f16=obs_f16)
         tb.inputs_event = self._event_handle(inputs_event)
         out = self._outputs(q_tm1)
@@ -562,7 +561,7 @@ class NativeDQN:
         handle, keys, after = (tuple(priority_update) + (None,))[:3]
         if keys.dtype not in (torch.uint64, torch.int64) or not keys.is_contiguous():
             raise ValueError("priority_update keys must be a contiguous 64-bit tensor")
-        if keys.numel() != int(tb.batch) or keys.device != self.device:
+        if keys.numel() != int(tb.batch) or not keys.is_cuda:
             raise ValueError("priority_update keys must hold one key per batch row, on the "
                              "learner's device")
         check(lib().acme_dqn_step_update(self._h, ctypes.byref(tb), ctypes.byref(out), handle,

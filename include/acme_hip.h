@@ -354,12 +354,16 @@ typedef struct acme_transition_batch {
    * u16, as acme_replay_sample_gather_frames writes it; the learner then skips its own
    * conversion (same bits).  NULL: the learner converts. */
   const uint16_t* obs_f16;
-  /* Optional (hipEvent_t): an event recorded on the caller's stream after which the caller
-   * enqueued nothing on it before this call, with the batch's inputs complete at it (a
-   * prefetching dataset's order event).  The learner's second stream then starts from it
-   * instead of from an event record of its own (which costs the caller's stream 5-9 us).
-   * Used only when the learner itself enqueues nothing first (no plane refresh,
-   * calibration or frame conversion).  NULL: the learner records its own. */
+  /* Optional (hipEvent_t): an event at which every input of the batch (fields and
+   * obs_f16) is complete, e.g. the prefetching dataset's ready event of the batch.  The
+   * uint8 Nature plane path then starts the target forward on its second stream from this
+   * event alone, without ordering it after the caller's stream, so it can overlap the end
+   * of the previous step (its Adam); the learner falls back to ordering after the caller's
+   * stream when that stream has written target state since the last step (a target copy,
+   * a q_values call, new parameters, calibration) or when it converts the frames itself.
+   * The caller must not write the target network's buffers, the learner's scale records
+   * or the batch's inputs on another stream meanwhile.  NULL: ordered after the caller's
+   * stream. */
   void* inputs_event;
 } acme_transition_batch;
 

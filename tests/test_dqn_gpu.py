@@ -428,3 +428,38 @@ def test_step_with_priority_update_equals_step_then_update(kind):
     da, db = tables[0].sample(B, 99), tables[1].sample(B, 99)
     for k in da:
         assert torch.equal(da[k], db[k]), k
+
+
+def test_early_target_forward_bitwise():
+    """With the batch's inputs event (acme_transition_batch.inputs_event) the target forward
+    starts on the second stream from that event alone and may overlap the previous step's
+    Adam; results equal the ordered schedule's bit for bit, across target copies (which
+    fall back to the ordered fork) and a q_values call between steps."""
+    from acme_amd._lib import OrderEvent
+    from acme_amd.networks import DQNAtariNetwork
+    net = DQNAtariNetwork(18)
+    B = 64
+    p0, t0 = net.init(7), net.init(8)
+    a = _learner(net, B, target_update_period=3)
+    b = _learner(net, B, target_update_period=3)
+    a.set_params(p0, t0)
+    b.set_params(p0, t0)
+    rng = np.random.default_rng(17)
+    for step in range(7):
+        dev = _dev(_batch(rng, B, (84, 84, 4), 18))
+        fb = torch.cat([dev[0], dev[4]]).reshape(2 * B, -1).to(torch.float16).view(torch.int16)
+        ev = OrderEvent()
+        ev.record()
+        a.step(*dev, obs_f16=fb, inputs_event=ev)
+        b.step(*dev, obs_f16=fb)
+        if step == 4:
+            qa = a.q_values(dev[4].reshape(B, -1), use_target=True)
+            qb = b.q_values(dev[4].reshape(B, -1), use_target=True)
+            assert torch.equal(qa, qb)
+        torch.cuda.synchronize()
+        assert a.loss.item() == b.loss.item(), step
+        assert torch.equal(a.priorities, b.priorities), step
+        for buf in ("params", "target", "m", "v"):
+            ga, gb = a.get_params(buf), b.get_params(buf)
+            for k in ga:
+                np.testing.assert_array_equal(ga[k], gb[k], err_msg=f"{step} {buf}/{k}")
