@@ -113,6 +113,8 @@ struct acme_dqn {
   acme_replay* upd_replay = nullptr;
   const uint64_t* upd_keys = nullptr;
   hipEvent_t upd_after = nullptr;  // the table's last device read (the update waits for it)
+  const double* upd_prio = nullptr;
+  int upd_n = 0;
   bool slabs_pending = false;
   torso::WgradSlab wslabs[3];
   float* side_slab = nullptr;
@@ -444,6 +446,16 @@ int mlp_forward(acme_dqn* l, const float* prm, const void* obs_a, const void* ob
   return ACME_OK;
 }
 
+// The step's priority write-back (acme_dqn_step_update), once, on `st`.
+int priority_update_tail(void* ctx, hipStream_t st) {
+  acme_dqn* l = static_cast<acme_dqn*>(ctx);
+  acme_replay* r = l->upd_replay;
+  if (!r || !l->upd_prio) return ACME_OK;
+  l->upd_replay = nullptr;
+  if (l->upd_after) ACME_HIP_TRY(hipStreamWaitEvent(st, l->upd_after, 0));
+  return acme_replay_update_priorities(r, l->upd_keys, l->upd_prio, l->upd_n, st);
+}
+
 // join_dense: the caller's stream waits for the side stream's dense weight gradients
 // before returning (stage 0 of a data-parallel step all-reduces them next); otherwise the
 // torso backward's final join covers them.
@@ -483,13 +495,13 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st_main,
     ACME_HIP_TRY(hipStreamWaitEvent(l->side, l->ev[2], 0));
     st = l->side;
   }
-  if (p3 && l->upd_replay && !l->calibrating) {  // the priority write-back, off the main
-                                                  // stream's tail
-    acme_replay* r = l->upd_replay;
-    l->upd_replay = nullptr;
-    if (l->upd_after) ACME_HIP_TRY(hipStreamWaitEvent(st, l->upd_after, 0));
-    if ((rc = acme_replay_update_priorities(r, l->upd_keys, la.prio, B, st)) != ACME_OK)
-      return rc;
+  if (p3 && l->upd_replay && !l->calibrating) {
+    l->upd_prio = la.prio;
+    l->upd_n = B;
+    // ACME_V_UPDQ=1: on the second stream right after the loss (its backward then ends
+    // ~20 us after the main stream's); default: at the end of the main stream's torso
+    // backward, before the join (priority_update_tail).
+    if (fork && tune("UPDQ") == 1 && (rc = priority_update_tail(l, st)) != ACME_OK) return rc;
   }
   if (loss_sum) {
     ACME_PROF("loss_sum", st, 0.0, 0.0);
@@ -1019,6 +1031,10 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
         for (int i = 0; i < 3; ++i) sd.e[i] = l->ev[i];
       }
       l->slabs_pending = false;
+      if (l->upd_replay && l->upd_prio && !l->calibrating) {
+        sd.tail = priority_update_tail;
+        sd.tail_ctx = l;
+      }
       if (l->fused_step && !l->calibrating && l->slab2) {
         sd.slab = l->side_slab;
         sd.slab2 = l->slab2;
@@ -1353,6 +1369,7 @@ int acme_dqn_step_update(acme_dqn* l, const acme_transition_batch* batch,
   const bool inside = use_p3(l) && l->cfg.network == ACME_NET_NATURE_DQN && !l->calibrating;
   l->upd_replay = inside ? replay : nullptr;
   l->upd_keys = keys;
+  l->upd_prio = nullptr;
   l->upd_after = static_cast<hipEvent_t>(after_event);
   int rc = step_impl(l, batch, out, copies_target(l), as_stream(stream));
   const bool pending = l->upd_replay != nullptr || !inside;

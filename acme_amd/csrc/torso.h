@@ -96,6 +96,10 @@ struct Side {
   // conv2 then use `slab` and `slab2` (both needed, with or without the side stream).
   float* slab2 = nullptr;
   WgradSlab* defer = nullptr;
+  // Optional work for the main stream after its last kernel, before the join (the DQN
+  // step's priority write-back, which balances the two streams' backward).
+  int (*tail)(void* ctx, hipStream_t st) = nullptr;
+  void* tail_ctx = nullptr;
 };
 // dz3: conv3's dZ planes [rows][kFlat] (masked); dz2 / dz1 plane scratch.
 int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int rows,

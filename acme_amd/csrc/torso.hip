@@ -367,6 +367,7 @@ int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int row
     else if ((rc = p3_wgrad_reduce(p, splits, slab, g.w1, g.b1, "conv1_wgrad_reduce", st)))
       return rc;
   }
+  if (sd.tail && (rc = sd.tail(sd.tail_ctx, st_main)) != ACME_OK) return rc;
   if (fork) ACME_HIP_TRY(hipStreamWaitEvent(st_main, sd.e[2], 0));  // join
   return ACME_OK;
 }
