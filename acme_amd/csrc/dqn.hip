@@ -728,7 +728,13 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
         return fail(rc);
       l->slab_floats = std::max(l->slab_floats, torso::wgrad_slab_floats_p3());
       if (tune("SIDE") != 1) {  // ACME_V_SIDE=1: single stream
-        hipError_t e = hipStreamCreateWithFlags(&l->side, hipStreamNonBlocking);
+        // ACME_V_SIDEPRIO=1 / 2: the second stream at the lowest / highest priority.
+        int lo = 0, hi = 0;
+        hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+        const int sp = tune("SIDEPRIO");
+        if (e == hipSuccess)
+          e = sp ? hipStreamCreateWithPriority(&l->side, hipStreamNonBlocking, sp == 1 ? lo : hi)
+                 : hipStreamCreateWithFlags(&l->side, hipStreamNonBlocking);
         for (auto& ev : l->ev)
           if (e == hipSuccess) e = make_order_event(&ev);
         if (e != hipSuccess)
