@@ -132,7 +132,7 @@ class DQNLearner(core.Learner, core.Saveable):
                 upd = prep(adders.DEFAULT_PRIORITY_TABLE, keys)
             self._native.step(*batch, obs_f16=fb, priority_update=upd, inputs_event=inputs_event)
         else:
-            self._staged_step(batch, fb)
+            self._staged_step(batch, fb, inputs_event)
         if self._replay_client is not None and upd is None:
             self._replay_client.update_priorities(table=adders.DEFAULT_PRIORITY_TABLE,
                                                   keys=keys,
@@ -154,7 +154,7 @@ class DQNLearner(core.Learner, core.Saveable):
         result.update(self._counter.increment(steps=1, walltime=elapsed))
         self._logger.write(result)
 
-    def _staged_step(self, batch, fb):
+    def _staged_step(self, batch, fb, inputs_event=None):
         """The data-parallel step: the learner's stages with the collectives between them.
         Gradient all-reduce in two buckets overlapped with the backward pass: the dense
         layers' gradients (the buffer's tail, ~99% of the bytes) are reduced on a collective
@@ -171,7 +171,8 @@ class DQNLearner(core.Learner, core.Saveable):
             gmin = self._gmin
             n.batch_min_probability(batch[5], gmin)
             work_min = dist.all_reduce(gmin, op=dist.ReduceOp.MIN, async_op=True)
-        n.forward_backward_stage(2, *batch, mean_over=self._B, obs_f16=fb)
+        n.forward_backward_stage(2, *batch, mean_over=self._B, obs_f16=fb,
+                                 inputs_event=inputs_event)
         if dist is not None:
             work_min.wait()
         n.forward_backward_stage(4, *batch, global_min_probability=gmin, mean_over=self._B,

@@ -500,15 +500,18 @@ class NativeDQN:
                                               stream_ptr(stream)), "dqn forward_backward")
 
     def forward_backward_stage(self, stage: int, *batch, global_min_probability=None,
-                               q_tm1=None, stream=None, mean_over=None, obs_f16=None):
+                               q_tm1=None, stream=None, mean_over=None, obs_f16=None,
+                               inputs_event=None):
         """Stage 0: forwards, loss, head/dense backward (grads[grad_split:]); stage 1: torso
         backward (grads[:grad_split]).  Stage 0 may be issued as stage 2 (forwards) then
         stage 3 (loss and dense backward; global_min_probability is read from here on) or
         stage 4 (stage 3 without ordering the stream after the dense gradients: see
         dense_grads_ready).  mean_over: the batch mean's denominator (default the batch; a
-        data-parallel share passes the nominal per-rank batch)."""
+        data-parallel share passes the nominal per-rank batch).  inputs_event: as for
+        step()."""
         tb = self._batch(*batch, global_min_probability=global_min_probability,
                          mean_over=mean_over, obs_f16=obs_f16)
+        tb.inputs_event = self._event_handle(inputs_event)
         out = self._outputs(q_tm1)
         check(lib().acme_dqn_forward_backward_stage(self._h, ctypes.byref(tb), ctypes.byref(out),
                                                     int(stage), stream_ptr(stream)),
