@@ -503,7 +503,10 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st_main,
     // backward, before the join (priority_update_tail).
     if (fork && tune("UPDQ") == 1 && (rc = priority_update_tail(l, st)) != ACME_OK) return rc;
   }
-  if (loss_sum) {
+  // The batch loss is summed by the head-gradient scatter's extra block (below); a
+  // separate loss-sum launch with ACME_V_LSUM=1.
+  const bool sum_in_scatter = loss_sum && tune("LSUM") != 1;
+  if (loss_sum && !sum_in_scatter) {
     ACME_PROF("loss_sum", st, 0.0, 0.0);
     rc = launch_dqn_loss_sum(la.loss_part, dqn_loss_head_dz_blocks(B, kHidden), la.mean_over,
                              la.loss, st);
@@ -517,9 +520,10 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st_main,
     p.A = A; p.h = l->hid; p.g = l->g; p.act = l->a_cache; p.slab = hslab;
     ACME_GEMM_N("head_wgrad", 64, 32, 2, 1, p, kHeadBwdSplits);
     ACME_PROF("head_wgrad_scatter", st, 0.0, 0.0);
-    rc = launch_duel_head_grad_scatter(hslab, kHeadBwdSplits, kHidden, A, Pm(l, gr, l->t_vw),
-                                       Pm(l, gr, l->t_vb), Pm(l, gr, l->t_aw), Pm(l, gr, l->t_ab),
-                                       st);
+    rc = launch_duel_head_grad_scatter(
+        hslab, kHeadBwdSplits, kHidden, A, Pm(l, gr, l->t_vw), Pm(l, gr, l->t_vb),
+        Pm(l, gr, l->t_aw), Pm(l, gr, l->t_ab), st, sum_in_scatter ? la.loss_part : nullptr,
+        dqn_loss_head_dz_blocks(B, kHidden), la.mean_over, la.loss);
     if (rc != ACME_OK) return rc;
   }
   if (p3) {

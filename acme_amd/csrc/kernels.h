@@ -40,7 +40,9 @@ int launch_head_dz_planes(const float* h, const float* g, const int32_t* a, int 
 // Sums the DuelHeadWgrad slab [splits][2H+1][A+1] and scatters its block-diagonal parts
 // into the head weight / bias gradients.
 int launch_duel_head_grad_scatter(const float* slab, int splits, int H, int A, float* dwv,
-                                  float* dbv, float* dwa, float* dba, hipStream_t st);
+                                  float* dbv, float* dwa, float* dba, hipStream_t st,
+                                  const double* part = nullptr, int64_t nparts = 0,
+                                  int mean_over = 1, float* loss = nullptr);
 
 // dZ of a plain linear Q head: dz[b][j] = g[b] * (j == a[b]).
 int launch_onehot_dq(const float* g, const int32_t* a, int B, int A, float* dz, hipStream_t st);

@@ -72,10 +72,31 @@ __global__ void duel_head_dz_kernel(const float* __restrict__ h, const float* __
 }
 
 // Sum of the DuelHeadWgrad slab + scatter of its block-diagonal parts.
-__global__ void duel_head_grad_scatter_kernel(const float* __restrict__ slab, int splits, int H,
-                                              int A, float* __restrict__ dwv,
-                                              float* __restrict__ dbv, float* __restrict__ dwa,
-                                              float* __restrict__ dba) {
+// Sum of the fused loss kernel's per-block loss partials over 256 threads, divided by
+// mean_over (one fixed order: strided per thread, then the wave tree, then the waves).
+__device__ __forceinline__ void loss_sum_block(const double* __restrict__ part, int64_t n,
+                                               int mean_over, float* __restrict__ loss) {
+  __shared__ double red[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  double s = 0.0;
+  for (int64_t i = tid; i < n; i += 256) s += part[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0) red[wave] = s;
+  __syncthreads();
+  if (tid == 0) loss[0] = (float)((((red[0] + red[1]) + red[2]) + red[3]) / (double)mean_over);
+}
+
+// The head weight gradients from the split-K slab; with `part`, one extra (last) block forms
+// the batch loss from the fused loss kernel's partials (the loss-sum launch folded in).
+__global__ void __launch_bounds__(256) duel_head_grad_scatter_kernel(
+    const float* __restrict__ slab, int splits, int H, int A, float* __restrict__ dwv,
+    float* __restrict__ dbv, float* __restrict__ dwa, float* __restrict__ dba,
+    const double* __restrict__ part, int64_t nparts, int mean_over, float* __restrict__ loss) {
+  if (part && blockIdx.x == gridDim.x - 1) {
+    loss_sum_block(part, nparts, mean_over, loss);
+    return;
+  }
   const int N = A + 1;
   const int64_t count = (int64_t)(2 * H + 1) * N;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1121,10 +1142,14 @@ int launch_duel_head_dz(const float* h, const float* g, const int32_t* a, int B,
 }
 
 int launch_duel_head_grad_scatter(const float* slab, int splits, int H, int A, float* dwv,
-                                  float* dbv, float* dwa, float* dba, hipStream_t st) {
+                                  float* dbv, float* dwa, float* dba, hipStream_t st,
+                                  const double* part, int64_t nparts, int mean_over,
+                                  float* loss) {
+  ACME_CHECK_ARG(!part || (loss && nparts >= 1 && mean_over >= 1), "bad loss sum args");
   const int64_t count = (int64_t)(2 * H + 1) * (A + 1);
-  duel_head_grad_scatter_kernel<<<(unsigned)ceil_div(count, 256), 256, 0, st>>>(
-      slab, splits, H, A, dwv, dbv, dwa, dba);
+  duel_head_grad_scatter_kernel<<<(unsigned)(ceil_div(count, 256) + (part ? 1 : 0)), 256, 0,
+                                  st>>>(slab, splits, H, A, dwv, dbv, dwa, dba, part, nparts,
+                                        mean_over, loss);
   ACME_LAUNCH_CHECK();
   return ACME_OK;
 }
@@ -1180,15 +1205,7 @@ int64_t dqn_loss_head_dz_blocks(int B, int H) { return ceil_div((int64_t)B * (2 
 __global__ void __launch_bounds__(256) dqn_loss_sum_kernel(const double* __restrict__ part,
                                                            int64_t n, int mean_over,
                                                            float* __restrict__ loss) {
-  __shared__ double red[4];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  double s = 0.0;
-  for (int64_t i = tid; i < n; i += 256) s += part[i];
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-  if (lane == 0) red[wave] = s;
-  __syncthreads();
-  if (tid == 0) loss[0] = (float)((((red[0] + red[1]) + red[2]) + red[3]) / (double)mean_over);
+  loss_sum_block(part, n, mean_over, loss);
 }
 
 int launch_dqn_loss_sum(const double* part, int64_t n, int mean_over, float* loss, hipStream_t st) {
