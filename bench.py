@@ -20,6 +20,7 @@ Prints ONE JSON line on rank 0 (contract in the task statement / DESIGN.md §6).
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import platform
@@ -800,6 +801,12 @@ def main():
         for i in range(settle):
             step()
         torch.cuda.synchronize(dev)
+    # The host issues a step in about half the GPU's step time, so a host pause early in a
+    # short timed window (the driver times 20 steps) stalls the GPU directly: Python's cyclic
+    # garbage collector is run before the window and paused inside it (nothing is skipped;
+    # the steps allocate no cyclic garbage).
+    gc.collect()
+    gc.disable()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
@@ -809,6 +816,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    gc.enable()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
