@@ -789,6 +789,7 @@ def main():
     # warm-up have passed; the count is the same on every rank (from the slowest rank's warm-up
     # rate), since every step issues collectives.
     settle = 0
+    gc.collect()
     if args.settle_seconds > 0 and args.steps > 0:
         spent = time.perf_counter() - tw
         per = spent / max(args.warmup, 1)
@@ -803,9 +804,9 @@ def main():
         torch.cuda.synchronize(dev)
     # The host issues a step in about half the GPU's step time, so a host pause early in a
     # short timed window (the driver times 20 steps) stalls the GPU directly: Python's cyclic
-    # garbage collector is run before the window and paused inside it (nothing is skipped;
-    # the steps allocate no cyclic garbage).
-    gc.collect()
+    # garbage collector ran before the settling steps (a collection right before the window
+    # idled the GPU long enough to drop its clocks: 20 timed steps 0.53 -> 0.58 ms) and is
+    # paused inside the window (nothing is skipped; the steps make no cyclic garbage).
     gc.disable()
     if world > 1:
         dist.barrier()
