@@ -779,6 +779,7 @@ def main():
     torch.cuda.synchronize(dev)
     t_fill = time.perf_counter() - t_fill
 
+    gc.collect()  # before the warm-up: no host pause between the settling steps and the window
     tw = time.perf_counter()
     for i in range(args.warmup):
         step()
@@ -789,7 +790,6 @@ def main():
     # warm-up have passed; the count is the same on every rank (from the slowest rank's warm-up
     # rate), since every step issues collectives.
     settle = 0
-    gc.collect()
     if args.settle_seconds > 0 and args.steps > 0:
         spent = time.perf_counter() - tw
         per = spent / max(args.warmup, 1)
@@ -804,7 +804,7 @@ def main():
         torch.cuda.synchronize(dev)
     # The host issues a step in about half the GPU's step time, so a host pause early in a
     # short timed window (the driver times 20 steps) stalls the GPU directly: Python's cyclic
-    # garbage collector ran before the settling steps (a collection right before the window
+    # garbage collector ran before the warm-up (a collection right before the window
     # idled the GPU long enough to drop its clocks: 20 timed steps 0.53 -> 0.58 ms) and is
     # paused inside the window (nothing is skipped; the steps make no cyclic garbage).
     gc.disable()
