@@ -1112,6 +1112,14 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
     } else {
       l->target_dirty = true;  // the target forward runs on the caller's stream
     }
+    // ACME_V_ONFIRST=1: the online forward (the critical path) issued before the target
+    // forward, so after a host wait (a timed window's first step) its kernels reach the GPU
+    // earlier.  Either order gives the same bits.
+    const bool online_first = side && tune("ONFIRST") == 1;
+    if (online_first &&
+        (rc = nature_forward_p3(l, l->params, l->wpl, fwd_frames, 2 * B, l->x1p, l->x2p, l->x3p,
+                                l->hid, l->q_on, st, nullptr, B)) != ACME_OK)
+      return rc;
     if ((rc = nature_forward_p3(l, l->target, l->tpl, fwd_frames.rows_from(B), B,
                                 l->t1p, l->t2p, l->t3p, l->thid, l->q_tg, tst,
                                 side ? l->tslab : l->slab, 0)) != ACME_OK)
@@ -1119,7 +1127,8 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
     if (side && (rc = launch_plane_rescale(l->scales + kScT1, 3, 3, -1, -1, l->overflow, side)))
       return rc;
     if (side) ACME_HIP_TRY(hipEventRecord(l->ev[1], side));
-    if ((rc = nature_forward_p3(l, l->params, l->wpl, fwd_frames, 2 * B, l->x1p, l->x2p, l->x3p,
+    if (!online_first &&
+        (rc = nature_forward_p3(l, l->params, l->wpl, fwd_frames, 2 * B, l->x1p, l->x2p, l->x3p,
                                 l->hid, l->q_on, st, nullptr, B)) != ACME_OK)
       return rc;
     if (side) ACME_HIP_TRY(hipStreamWaitEvent(st, l->ev[1], 0));
