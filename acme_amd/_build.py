@@ -14,8 +14,10 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
-LIB = os.path.join(HERE, "libacme_hip.so")
-OBJDIR = os.path.join(HERE, "csrc", "build")
+# ACME_BUILD_OUT / ACME_BUILD_OBJDIR: an experiment's variant library (e.g. with
+# ACME_EXTRA_CFLAGS=-DP3_FOUR_TERMS=1), loaded through ACME_LIB_PATH.
+LIB = os.environ.get("ACME_BUILD_OUT") or os.path.join(HERE, "libacme_hip.so")
+OBJDIR = os.environ.get("ACME_BUILD_OBJDIR") or os.path.join(HERE, "csrc", "build")
 ARCH = os.environ.get("ACME_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 

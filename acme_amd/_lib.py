@@ -153,6 +153,7 @@ _SIGS = {
     "acme_r2d2_importance_weights": (c_i32, [c_vp, c_i32, c_i64, ctypes.c_double, c_vp, c_vp]),
     "acme_frames_expand": (c_i32, [c_vp, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp, c_vp]),
     "acme_replay_update_priorities": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "acme_replay_update_priorities_gated": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "acme_replay_size": (c_i64, [c_vp]),
     "acme_replay_capacity": (c_i64, [c_vp]),
     "acme_replay_debug_leaves": (c_i32, [c_vp, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp),
@@ -171,6 +172,11 @@ _SIGS = {
     "acme_dqn_bind": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "acme_dqn_params_changed": (c_i32, [c_vp]),
     "acme_dqn_plane_overflow": (c_i32, [c_vp, ctypes.POINTER(c_i32), c_i32]),
+    "acme_dqn_skipped_steps": (c_i64, [c_vp]),
+    "acme_dqn_guard_state": (c_i32, [c_vp, ctypes.POINTER(c_i64)]),
+    "acme_dqn_set_applied_steps": (c_i32, [c_vp, c_i64]),
+    "acme_dqn_skip_word": (c_i32, [c_vp, ctypes.POINTER(c_vp)]),
+    "acme_dqn_set_data_parallel_gate": (c_i32, [c_vp, c_i32]),
     "acme_dqn_dense_grads_ready": (c_i32, [c_vp, c_vp]),
     "acme_dqn_dp_init": (c_i32, [c_vp, c_vp, c_i32]),
     "acme_dqn_dp_step": (c_i32, [c_vp, ctypes.POINTER(TransitionBatch), ctypes.POINTER(DQNOutputs),
@@ -208,6 +214,11 @@ _SIGS = {
     "acme_impala_step": (c_i32, [c_vp, ctypes.POINTER(SequenceBatch), c_vp, c_vp]),
     "acme_impala_set_lstm_unroll": (c_i32, [c_vp, c_i32]),
     "acme_impala_plane_overflow": (c_i32, [c_vp, ctypes.POINTER(c_i32), c_i32]),
+    "acme_impala_skipped_steps": (c_i64, [c_vp]),
+    "acme_impala_guard_state": (c_i32, [c_vp, ctypes.POINTER(c_i64)]),
+    "acme_impala_set_applied_steps": (c_i32, [c_vp, c_i64]),
+    "acme_impala_scale_state": (c_i32, [c_vp, c_vp, c_i32, ctypes.POINTER(c_i32)]),
+    "acme_impala_set_scale_state": (c_i32, [c_vp, c_vp, c_i32]),
     "acme_impala_policy_step": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
                                         c_vp, c_vp, c_vp]),
     "acme_impala_num_steps": (c_i64, [c_vp]),

@@ -10,11 +10,20 @@ scalar and fetched only when a log line is actually emitted.
 `network` / `target_network` are descriptors from acme_amd.networks (the reference
 takes Sonnet modules); the target starts from its own initialisation, like the
 reference's deepcopy + create_variables (agents/tf/dqn/agent.py:127-131).
+
+Plane overflow (the uint8 Nature path runs its GEMMs on scaled f16 planes, csrc/gemm_p3.h):
+a step in which some plane write overflowed f16 (a tensor's maximum grew more than ~2^8-fold
+since the previous step) is skipped on the device, the rule of automatic mixed precision:
+no parameter, Adam moment or count, target or priority changes, and the end-of-step rescale
+sets every scale from that step's true maxima.  The learner sees the count lazily (a pinned
+host word, no synchronisation); on a new skip it re-splits the parameter planes and
+recalibrates the scales before its next step (`on_plane_overflow="skip"`, logged as
+`skipped_steps`), or raises FloatingPointError (`"raise"`).  Adam's t counts applied
+updates; `num_steps` (the target period) counts step() calls.
 """
 
 from __future__ import annotations
 
-import os
 import time
 from typing import Dict, List, Optional
 
@@ -37,9 +46,13 @@ class DQNLearner(core.Learner, core.Saveable):
                  max_abs_reward: float = 1.0, batch_size: Optional[int] = None, seed: int = 0,
                  device=None, data_parallel: bool = True, semantics: str = "tf",
                  target_seed: Optional[int] = None, adam=None,
-                 reduce_logged_loss: bool = True):
+                 reduce_logged_loss: bool = True, on_plane_overflow: str = "skip"):
         if huber_loss_parameter < 0:
             raise ValueError("quadratic_linear_boundary must be >= 0.")
+        if on_plane_overflow not in ("skip", "raise"):
+            raise ValueError("on_plane_overflow must be 'skip' or 'raise'")
+        self._on_overflow = on_plane_overflow
+        self._skips_seen = 0
         self._network = network
         self._iterator = iter(dataset)
         B = batch_size or getattr(dataset, "batch_size", None) or 256
@@ -93,6 +106,10 @@ class DQNLearner(core.Learner, core.Saveable):
                 self._gmin = torch.empty(1, dtype=torch.float64, device=self._native.device)
                 self._grad_split = self._native.grad_split
                 self._avg_op = (dist.ReduceOp.AVG if dist.get_backend() == "nccl" else None)
+                # The ranks skip an overflowed step together: each rank's decision rides in
+                # the torso gradient bucket's all-reduce.
+                self._native.set_data_parallel_gate(True)
+        self._skip_word = self._native.skip_word
 
     # ------------------------------------------------------------------ step
     def _prepare(self, x: torch.Tensor, dtype) -> torch.Tensor:
@@ -100,7 +117,21 @@ class DQNLearner(core.Learner, core.Saveable):
             x = x.to(dtype)
         return x.contiguous()
 
+    def _check_guard(self) -> int:
+        """Skipped steps the device has reported so far (no synchronisation); on a new one,
+        re-split the planes and recalibrate the scales before the next step, or raise."""
+        n = self._native.skipped_steps
+        if n != self._skips_seen:
+            self._skips_seen = n
+            if self._on_overflow == "raise":
+                raise FloatingPointError(
+                    f"DQN learner: {n} step(s) skipped on f16 plane overflow (their updates "
+                    "were not applied)")
+            self._native.params_changed()
+        return n
+
     def step(self):
+        skipped = self._check_guard()
         sample = next(self._iterator)
         o_tm1, a_tm1, r_t, d_t, o_t = sample.data[:5]
         keys, probs = sample.info[:2]
@@ -114,7 +145,7 @@ class DQNLearner(core.Learner, core.Saveable):
         # for the previous step's tail, unless a conversion above produced new tensors on
         # this stream.
         inputs_event = getattr(self._iterator, "last_inputs_event", None)
-        if any(b is not v for b, v in zip(batch, views)) or os.environ.get("ACME_V_INEV") == "1":
+        if any(b is not v for b, v in zip(batch, views)):
             inputs_event = None
         # The dataset's fused gather also wrote the exact f16 copy of [o_tm1; o_t] (uint8
         # tables; rows [0, B) and [B, 2B) of its buffer): the learner then skips its own
@@ -128,15 +159,17 @@ class DQNLearner(core.Learner, core.Saveable):
             # The priority write-back rides in the step (on the learner's second stream
             # beside the backward) when the client's table offers it.
             prep = getattr(self._replay_client, "prepare_priority_update", None)
-            if prep is not None and os.environ.get("ACME_V_STEPUPD") != "1":  # 1: A/B off
+            if prep is not None:
                 upd = prep(adders.DEFAULT_PRIORITY_TABLE, keys)
             self._native.step(*batch, obs_f16=fb, priority_update=upd, inputs_event=inputs_event)
         else:
             self._staged_step(batch, fb, inputs_event)
         if self._replay_client is not None and upd is None:
+            # Gated on the step's skip word: a skipped step writes no priority.
+            kw = {"skip_word": self._skip_word} if self._skip_word else {}
             self._replay_client.update_priorities(table=adders.DEFAULT_PRIORITY_TABLE,
                                                   keys=keys,
-                                                  priorities=self._native.priorities[:B])
+                                                  priorities=self._native.priorities[:B], **kw)
         now = time.time()
         elapsed = now - self._timestamp if self._timestamp else 0
         self._timestamp = now
@@ -151,6 +184,8 @@ class DQNLearner(core.Learner, core.Saveable):
                 self._dist.all_reduce(loss)
                 loss.mul_(1.0 / self._dist.get_world_size())
         result = {"loss": loss} if self._log_loss else {}
+        if skipped:
+            result["skipped_steps"] = skipped
         result.update(self._counter.increment(steps=1, walltime=elapsed))
         self._logger.write(result)
 
@@ -202,7 +237,12 @@ class DQNLearner(core.Learner, core.Saveable):
     def q_values(self, observations, use_target: bool = False) -> np.ndarray:
         obs_dt = torch.uint8 if self._network.obs_dtype == "uint8" else torch.float32
         x = torch.as_tensor(np.asarray(observations)).to(self._native.device, obs_dt)
-        return self._native.q_values(x.reshape(x.shape[0], -1).contiguous(), use_target).cpu().numpy()
+        x = x.reshape(x.shape[0], -1).contiguous()
+        q = self._native.q_values(x, use_target).cpu().numpy()
+        if self._skip_word and self._native.guard_state()["q_values_overflowed"]:
+            # The forward overflowed its planes; its rescale set the scales from its maxima.
+            q = self._native.q_values(x, use_target).cpu().numpy()
+        return q
 
     def get_variables(self, names: List[str]) -> List[List[np.ndarray]]:
         # As the TF learner: one collection (the online trainable variables), names ignored.
@@ -224,8 +264,9 @@ class DQNLearner(core.Learner, core.Saveable):
     def save(self) -> Dict:
         n = self._native
         return {"network": n.get_params("params"), "target_network": n.get_params("target"),
+                # Adam's t: the updates applied (step() calls minus skipped steps).
                 "optimizer": {"m": n.get_params("m"), "v": n.get_params("v"),
-                              "step": n.num_steps},
+                              "step": n.applied_steps},
                 "num_steps": n.num_steps,
                 # f16 plane scales (csrc/gemm_p3.h): restoring them keeps a resumed run
                 # bit-identical to an uninterrupted one.
@@ -242,3 +283,4 @@ class DQNLearner(core.Learner, core.Saveable):
         if "plane_scales" in state:
             n.set_scale_state(state["plane_scales"])
         n.num_steps = int(state["num_steps"])
+        n.applied_steps = int(state["optimizer"].get("step", state["num_steps"]))

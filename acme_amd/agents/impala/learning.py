@@ -7,6 +7,11 @@ sequences from the dataset (Step(observation=OAR(...), action, reward, discount,
 start_of_episode, extras={'core_state': LSTMState, 'logits'})) and runs the whole step on
 the GPU (acme_impala_step): torso over all B*T frames, OAR projection, LSTM unroll from
 core_state[:, 0], policy/value head, V-trace, losses, BPTT, global-norm clip, Adam.
+
+A step whose f16 planes overflowed, or whose one-launch LSTM unroll timed out, applies no
+update (the device's step guard, as DQNLearner's): the learner sees the count lazily, logs
+`skipped_steps` and recalibrates the plane scales before its next step (or raises
+FloatingPointError with on_plane_overflow="raise").
 """
 
 from __future__ import annotations
@@ -39,7 +44,11 @@ class IMPALALearner(core.Learner, core.Saveable):
                  counter: Optional[counting.Counter] = None,
                  logger: Optional[loggers.Logger] = None, batch_size: Optional[int] = None,
                  sequence_length: Optional[int] = None, seed: int = 0, device=None,
-                 semantics: str = "tf", adam=None):
+                 semantics: str = "tf", adam=None, on_plane_overflow: str = "skip"):
+        if on_plane_overflow not in ("skip", "raise"):
+            raise ValueError("on_plane_overflow must be 'skip' or 'raise'")
+        self._on_overflow = on_plane_overflow
+        self._skips_seen = 0
         self._env_spec = environment_spec
         self._network = network
         self._iterator = iter(dataset)
@@ -63,7 +72,18 @@ class IMPALALearner(core.Learner, core.Saveable):
         # Parameter snapshots for actor networks (actor_policy): allocated on first use.
         self._snap = None
 
+    def _check_guard(self) -> int:
+        n = self._native.skipped_steps  # pinned host word: no synchronisation
+        if n != self._skips_seen:
+            self._skips_seen = n
+            if self._on_overflow == "raise":
+                raise FloatingPointError(f"IMPALA learner: {n} step(s) skipped (f16 plane "
+                                         "overflow or LSTM unroll timeout)")
+            self._native.params_changed()
+        return n
+
     def step(self):
+        skipped = self._check_guard()
         sample = next(self._iterator)
         data = sample.data
         obs = data.observation
@@ -89,6 +109,8 @@ class IMPALALearner(core.Learner, core.Saveable):
         elapsed = now - self._timestamp if self._timestamp else 0
         self._timestamp = now
         result = dict(self._metric_views)
+        if skipped:
+            result["skipped_steps"] = skipped
         result.update(self._counter.increment(steps=1, walltime=elapsed))
         self._logger.write(result)
 
@@ -198,8 +220,11 @@ class IMPALALearner(core.Learner, core.Saveable):
     def save(self) -> Dict:
         n = self._native
         return {"network": n.get_params("params"),
-                "optimizer": {"m": n.get_params("m"), "v": n.get_params("v")},
-                "num_steps": n.num_steps}
+                "optimizer": {"m": n.get_params("m"), "v": n.get_params("v"),
+                              "step": n.applied_steps},
+                "num_steps": n.num_steps,
+                # f16 plane scales: a resumed run is bit-identical to an uninterrupted one.
+                "plane_scales": n.scale_state()}
 
     def restore(self, state: Dict):
         n = self._native
@@ -208,6 +233,11 @@ class IMPALALearner(core.Learner, core.Saveable):
             for k, t in n.views(buf).items():
                 t.copy_(torch.as_tensor(np.asarray(src[k], np.float32)).view(t.shape))
         n.num_steps = int(state["num_steps"])
+        n.applied_steps = int(state["optimizer"].get("step", state["num_steps"]))
+        if "plane_scales" in state:
+            n.set_scale_state(state["plane_scales"])
+        if self._snap is not None:  # actors act with the restored weights from now on
+            self._publish_snapshot()
 
 
 class _PipelinedPolicy:

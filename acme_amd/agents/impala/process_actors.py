@@ -341,6 +341,9 @@ class ProcessActorPool:
         return int(self.S["steps"].sum())
 
     def _check(self) -> None:
+        err = getattr(self, "_drain_error", None)
+        if err is not None:  # the drain thread's failure, re-raised on the driver
+            raise RuntimeError(f"the queue drain thread failed: {err!r}") from err
         if self.S["error"].any():
             raise RuntimeError(f"actor worker(s) {np.nonzero(self.S['error'])[0].tolist()} failed")
         for w, p in enumerate(self._procs):
@@ -351,6 +354,8 @@ class ProcessActorPool:
     def _wait_group(self, g: int, timeout: float = 60.0) -> None:
         S, deadline = self.S, time.time() + timeout
         while (S["done"][:, g] < S["go"][:, g]).any():
+            if getattr(self, "_drain_error", None) is not None:
+                self._check()
             self.drain(block=False)  # a worker whose ring is full waits for it
             if time.time() > deadline:
                 self._check()
@@ -493,11 +498,15 @@ class ProcessActorPool:
         # Items are inserted by a thread of their own (the native insert copies outside the
         # GIL), so the driver only posts actions and issues policy steps.
         drained = threading.Event()
+        self._drain_error = None
 
         def drainer():
-            while not drained.is_set():
-                if not self.drain():
-                    time.sleep(2e-4)
+            try:
+                while not drained.is_set():
+                    if not self.drain():
+                        time.sleep(2e-4)
+            except BaseException as e:  # noqa: BLE001 - handed to the driver thread
+                self._drain_error = e
 
         dth = threading.Thread(target=drainer, daemon=True)
         dth.start()
@@ -530,4 +539,5 @@ class ProcessActorPool:
             self._wait_group(g)
         drained.set()
         dth.join()
+        self._check()
         self.drain()

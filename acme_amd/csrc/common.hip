@@ -68,10 +68,8 @@ bool use_x6() {
 
 hipError_t make_order_event(hipEvent_t* ev) {
   // Device-scope release: no system-scope cache writeback / invalidation when the event
-  // is recorded or waited on (ACME_V_EVSYS=1 restores the default system-scope fence).
-  unsigned flags = hipEventDisableTiming;
-  if (tune_variant("EVSYS") != 1) flags |= hipEventDisableSystemFence;
-  return hipEventCreateWithFlags(ev, flags);
+  // is recorded or waited on (nothing on the host reads device memory on their strength).
+  return hipEventCreateWithFlags(ev, hipEventDisableTiming | hipEventDisableSystemFence);
 }
 
 }  // namespace acme

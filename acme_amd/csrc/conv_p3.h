@@ -46,7 +46,7 @@ __device__ __forceinline__ float split8(const V8& v, float w, uint32_t (&h)[4], 
     gemm::split2_bits(v[2 * j + 1] * w, h1, l1);
     h[j] = (uint32_t)h0 | ((uint32_t)h1 << 16);
     l[j] = (uint32_t)l0 | ((uint32_t)l1 << 16);
-    mx = fmaxf(mx, fmaxf(fabsf(v[2 * j]), fabsf(v[2 * j + 1])));
+    mx = gemm::amax_max(mx, gemm::amax_max(fabsf(v[2 * j]), fabsf(v[2 * j + 1])));
   }
   return mx;
 }

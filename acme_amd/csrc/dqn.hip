@@ -145,6 +145,23 @@ struct acme_dqn {
   hipEvent_t dp_ev[4] = {nullptr, nullptr, nullptr, nullptr};
   double* dp_gmin = nullptr;
   double* loss_part = nullptr;  // per-block loss partials of the fused loss + head dZ
+  // Schedule variants fixed at creation (tests compare them bit for bit): one stream
+  // (ACME_V_SIDE=1), the single-role GEMM kernels instead of the producer / consumer ones
+  // (ACME_V_WSN=1).
+  bool single_stream = false;
+  bool single_role = false;
+  // Step guard (kernels.h StepGuard): the skip-on-overflow rule of the plane engine, Adam's
+  // device step count (applied updates) on every path.  seq counts the steps issued (the
+  // target forward's flag slot is seq & 1); host_skipped is a pinned mirror of the skipped
+  // count the end-of-step rescale writes (read by the host without a synchronisation).
+  StepGuard* guard = nullptr;
+  int64_t* host_skipped = nullptr;
+  int64_t seq = 0;
+  // Data parallelism: the ranks' skip decisions are combined through a padding word of the
+  // torso gradient bucket (stage 1 publishes the local one; the all-reduce combines them).
+  bool dp_gate = false;
+  int64_t dp_gate_index = -1;
+  bool param_rescale_pending = false;  // the parameter record's write scale moved last step
 };
 
 namespace {
@@ -222,6 +239,20 @@ int convert_frames(acme_dqn* l, const void* obs_a, const void* obs_b, int split,
 }
 inline Planes PP(const torso::Plane& x) { return Planes{x.p, x.stride, x.sc}; }
 bool use_p3(const acme_dqn* l) { return l->p3_capable && gemm::use_x6(); }
+// The gate of the step in flight (seq): its online records' flags, its target forward's, and
+// with data parallelism every rank's (the all-reduced padding word).
+Gate step_gate(const acme_dqn* l) {
+  Gate q;
+  q.g = l->guard;
+  q.par = (int)(l->seq & 1);
+  if (l->dp_gate) q.dp = l->grads + l->dp_gate_index;
+  return q;
+}
+// Clears the guard's flags (not its counts) after a calibration.
+int clear_guard_flags(acme_dqn* l, hipStream_t st) {
+  ACME_HIP_TRY(hipMemsetAsync(l->guard, 0, offsetof(StepGuard, applied), st));
+  return ACME_OK;
+}
 // The side stream is used unless the section profiler is on: profiled passes run every
 // kernel alone on one stream, so their per-kernel durations are uncontended.
 hipStream_t side_stream(const acme_dqn* l) { return prof::enabled() ? nullptr : l->side; }
@@ -249,7 +280,6 @@ inline int chunk_for(int K, int splits) {
   } while (0)
 #define ACME_GEMM_N(name, BM, BN, WM, WN, prob, splits) \
   ACME_GEMM_F(name, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, BM, BN, WM, WN, prob, splits)
-int tune(const char* key) { return tune_variant(key); }
 
 // Same with an explicit reduction stage depth BK (16 or 32).
 #ifndef ACME_BIG_BK
@@ -320,13 +350,15 @@ int slab_reduce(const float* slab, int splits, int64_t count, float* out0, int64
 // snt.Adam over the flat range [off, off + n) (tensor-aligned): the parameter planes (plane
 // path) are refreshed by the same pass.  t = num_steps + 1 (snt.Adam / optix.adam count this
 // step first).  Every element's update is independent, so ranges compose bit-exactly.
-int adam_range(acme_dqn* l, int64_t off, int64_t n, hipStream_t st) {
+int adam_range(acme_dqn* l, int64_t off, int64_t n, const Gate& gate, hipStream_t st) {
   const bool jax = l->cfg.semantics == ACME_SEMANTICS_JAX;
+  // Plane path: the step's gate and count from the rescale before Adam; otherwise no gate
+  // (f32 tensors cannot overflow) and a one-thread count after Adam.
+  const bool p3 = l->p3_capable;
   return launch_adam(l->params + off, l->grads + off, l->m + off, l->v + off, n,
                      l->cfg.learning_rate, l->cfg.adam_beta1, l->cfg.adam_beta2,
-                     l->cfg.adam_epsilon, l->num_steps + 1,
-                     l->p3_capable ? l->wpl + off : nullptr, l->flat, st, jax ? 1 : 0, nullptr,
-                     l->p3_capable ? l->scales + kScParams : nullptr);
+                     l->cfg.adam_epsilon, 0, p3 ? l->wpl + off : nullptr, l->flat, st, jax ? 1 : 0,
+                     &l->guard->applied, p3 ? l->scales + kScParams : nullptr, gate, !p3);
 }
 
 torso::Weights torso_weights(const acme_dqn* l, const float* prm) {
@@ -395,7 +427,7 @@ int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const torso:
     // 65.2 -> 60.5 us against the single-role kernel, the same bits.
     // (Two f16 planes, measured on the step: 256x128 / 128x256 WS tiles, 256x128 single-role
     // tiles with split-K 8, and the LDS-DMA ring (3 or 4 stages) all slower or equal.)
-    if (tune("WSN") == 1) ACME_P3_GEMM("fc_fwd", 128, 128, 2, 2, 32, p, splits);  // tests
+    if (l->single_role) ACME_P3_GEMM("fc_fwd", 128, 128, 2, 2, 32, p, splits);  // tests
     else ACME_P3WS_GEMM("fc_fwd", 128, 128, 2, 2, 32, p, splits, true);
     ACME_PROF("fc_head_fwd", st, 0.0, 4.0 * (double)rows * 2 * kHidden * (splits + 1));
     return launch_fc_head_forward(slab, splits, rows, kHidden, P(l, prm, l->t_fcb),
@@ -453,7 +485,8 @@ int priority_update_tail(void* ctx, hipStream_t st) {
   if (!r || !l->upd_prio) return ACME_OK;
   l->upd_replay = nullptr;
   if (l->upd_after) ACME_HIP_TRY(hipStreamWaitEvent(st, l->upd_after, 0));
-  return acme_replay_update_priorities(r, l->upd_keys, l->upd_prio, l->upd_n, st);
+  // Gated: a step that overflowed writes no priority.
+  return replay_update_priorities_gated(r, l->upd_keys, l->upd_prio, l->upd_n, step_gate(l), st);
 }
 
 // join_dense: the caller's stream waits for the side stream's dense weight gradients
@@ -498,20 +531,13 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st_main,
   if (p3 && l->upd_replay && !l->calibrating) {
     l->upd_prio = la.prio;
     l->upd_n = B;
-    // ACME_V_UPDQ=1: on the second stream right after the loss (its backward then ends
-    // ~20 us after the main stream's); default: at the end of the main stream's torso
-    // backward, before the join (priority_update_tail).
-    if (fork && tune("UPDQ") == 1 && (rc = priority_update_tail(l, st)) != ACME_OK) return rc;
+    // Issued at the end of the main stream's torso backward, before the join
+    // (priority_update_tail); on the second stream right after the loss its backward ended
+    // ~20 us after the main stream's.
   }
-  // The batch loss is summed by the head-gradient scatter's extra block (below); a
-  // separate loss-sum launch with ACME_V_LSUM=1.
-  const bool sum_in_scatter = loss_sum && tune("LSUM") != 1;
-  if (loss_sum && !sum_in_scatter) {
-    ACME_PROF("loss_sum", st, 0.0, 0.0);
-    rc = launch_dqn_loss_sum(la.loss_part, dqn_loss_head_dz_blocks(B, kHidden), la.mean_over,
-                             la.loss, st);
-    if (rc != ACME_OK) return rc;
-  }
+  // The batch loss is summed by the head-gradient scatter's extra block (below): a launch of
+  // its own on the second stream measured 0.5107 -> 0.5235 ms per step.
+  const bool sum_in_scatter = loss_sum;
   {  // Head weight / bias gradients: one skinny GEMM over the batch + scatter.  (One
      // launch without split-K, 64 units per block and the batch over 8 waves, took 38 us
      // against 9.3 + 6.7: 17 blocks cannot hide the row loads.)
@@ -549,7 +575,7 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st_main,
       // LDS-DMA staging (gemm_p3.h P3G) measured fastest for this shape.
       // Producer / consumer waves (gemm_p3ws_kernel): 51.4 -> 47.3 us against the LDS-DMA
       // ring, the same bits.
-      if (tune("WSN") == 1) ACME_P3G_GEMM("fc_dgrad", 128, 128, 2, 2, 32, 3, p, 1);  // tests
+      if (l->single_role) ACME_P3G_GEMM("fc_dgrad", 128, 128, 2, 2, 32, 3, p, 1);  // tests
       else ACME_P3WS_GEMM("fc_dgrad", 128, 128, 2, 2, 32, p, 1, true);
     }
     if (fork && join_dense) ACME_HIP_TRY(hipStreamWaitEvent(st_main, l->ev[3], 0));
@@ -642,11 +668,16 @@ int sync_planes(acme_dqn* l, hipStream_t st) {
   return rc;
 }
 
-// Initial scale records: w = r = wi = 1, amax slots 0.
+// Initial scale records: w = r = wi = 1, amax slots 0; each record's flag is the guard word
+// of the tensors it covers (the online step's, the target forward's, the parameters').
 int reset_scales(acme_dqn* l) {
   std::vector<gemm::PScale> init(kScCount);
   std::memset(init.data(), 0, init.size() * sizeof(gemm::PScale));
   for (auto& r : init) r.w = r.r = r.wi = r.rl = 1.f;
+  for (int i = 0; i < kScCount; ++i)
+    init[i].flag = i >= kScT1 && i <= kScT3 ? &l->guard->tt
+                   : i >= kScTransient     ? &l->guard->prm
+                                           : &l->guard->on;
   ACME_HIP_TRY(hipMemcpy(l->scales, init.data(), init.size() * sizeof(gemm::PScale),
                          hipMemcpyHostToDevice));
   ACME_HIP_TRY(hipMemset(l->overflow, 0, sizeof(int)));
@@ -671,6 +702,8 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
                  "unknown learner semantics %d", cfg->semantics);
   acme_dqn* l = new acme_dqn();
   l->cfg = *cfg;
+  l->single_stream = tune_variant("SIDE") == 1;
+  l->single_role = tune_variant("WSN") == 1;
   const int A = cfg->num_actions;
   const int B = cfg->max_batch;
   int rc = ACME_OK;
@@ -678,6 +711,12 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
     acme_dqn_destroy(l);
     return code;
   };
+  if ((rc = dev_alloc(l, &l->guard, 1)) != ACME_OK) return fail(rc);
+  if (hipMemset(l->guard, 0, sizeof(StepGuard)) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&l->host_skipped), sizeof(int64_t),
+                    hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+    return fail((set_error("step guard allocation failed"), ACME_ERR_HIP));
+  *l->host_skipped = 0;
   if (cfg->network == ACME_NET_NATURE_DQN) {
     l->t_c1w = add_tensor(l, "atari_torso/conv2_d/w", {8, 8, 4, 32});
     l->t_c1b = add_tensor(l, "atari_torso/conv2_d/b", {32});
@@ -731,18 +770,17 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
           (rc = plane_alloc(l, &l->dz1p, (int64_t)B * torso::kX1, kScDz1)))
         return fail(rc);
       l->slab_floats = std::max(l->slab_floats, torso::wgrad_slab_floats_p3());
-      if (tune("SIDE") != 1) {  // ACME_V_SIDE=1: single stream
+      // ACME_V_SIDE=1 at creation: a single stream (tests of the schedule).
+      if (!l->single_stream) {
         // The second stream at the lowest priority (1 on MI355X; the caller's streams are
         // normally 0): the dispatcher then favours the main stream's blocks, which carry
         // the step's critical path (the online forward, the input-gradient chain, Adam).
-        // 0.5308 -> 0.5260 ms per step (three alternating runs each); the highest priority
-        // measured slower.  ACME_V_SIDEPRIO=1: default priority.
+        // 0.5308 -> 0.5260 ms per step against the default priority (three alternating runs
+        // each); the highest priority measured slower.
         int lo = 0, hi = 0;
         hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
         if (e == hipSuccess)
-          e = tune("SIDEPRIO") != 1
-                  ? hipStreamCreateWithPriority(&l->side, hipStreamNonBlocking, lo)
-                  : hipStreamCreateWithFlags(&l->side, hipStreamNonBlocking);
+          e = hipStreamCreateWithPriority(&l->side, hipStreamNonBlocking, lo);
         for (auto& ev : l->ev)
           if (e == hipSuccess) e = make_order_event(&ev);
         if (e != hipSuccess)
@@ -812,6 +850,7 @@ int acme_dqn_destroy(acme_dqn* l) {
   for (auto& e : l->dp_ev)
     if (e) (void)hipEventDestroy(e);
   if (l->dp_stream) (void)hipStreamDestroy(l->dp_stream);
+  if (l->host_skipped) (void)hipHostFree(l->host_skipped);
   delete l;
   return ACME_OK;
 }
@@ -897,6 +936,52 @@ int acme_dqn_plane_overflow(acme_dqn* l, int32_t* overflow, int32_t reset) {
   return ACME_OK;
 }
 
+int64_t acme_dqn_skipped_steps(const acme_dqn* l) {
+  if (!l || !l->host_skipped) return 0;
+  return *reinterpret_cast<volatile const int64_t*>(l->host_skipped);
+}
+
+int acme_dqn_guard_state(acme_dqn* l, int64_t* out4) {
+  ACME_CHECK_ARG(l && out4 && l->guard, "null argument");
+  ACME_HIP_TRY(hipDeviceSynchronize());
+  StepGuard g;
+  ACME_HIP_TRY(hipMemcpy(&g, l->guard, sizeof(g), hipMemcpyDeviceToHost));
+  out4[0] = g.applied;
+  out4[1] = g.skipped;
+  out4[2] = g.last;
+  out4[3] = g.qv;
+  return ACME_OK;
+}
+
+int acme_dqn_set_applied_steps(acme_dqn* l, int64_t n) {
+  ACME_CHECK_ARG(l && l->guard && n >= 0, "bad argument");
+  ACME_HIP_TRY(hipDeviceSynchronize());
+  ACME_HIP_TRY(hipMemcpy(&l->guard->applied, &n, sizeof(n), hipMemcpyHostToDevice));
+  return ACME_OK;
+}
+
+int acme_dqn_skip_word(const acme_dqn* l, const uint32_t** out) {
+  ACME_CHECK_ARG(l && out, "null argument");
+  *out = l->p3_capable ? &l->guard->last : nullptr;
+  return ACME_OK;
+}
+
+int acme_dqn_set_data_parallel_gate(acme_dqn* l, int32_t enable) {
+  ACME_CHECK_ARG(l, "null learner");
+  if (enable && l->cfg.network == ACME_NET_NATURE_DQN && l->p3_capable) {
+    // conv1's bias (32 values) is padded to 64 floats: the first padding word of the torso
+    // bucket [0, grad_split) carries the gate (zero on every step that is applied, so its
+    // Adam update stays zero).
+    const Tensor& t = l->tensors[l->t_c1b];
+    ACME_CHECK_ARG(align64(t.offset + t.numel) > t.offset + t.numel, "no padding word for the gate");
+    l->dp_gate_index = t.offset + t.numel;
+    l->dp_gate = true;
+  } else {
+    l->dp_gate = false;
+  }
+  return ACME_OK;
+}
+
 int64_t acme_dqn_num_steps(const acme_dqn* l) { return l ? l->num_steps : 0; }
 int acme_dqn_set_num_steps(acme_dqn* l, int64_t n) {
   ACME_CHECK_ARG(l && n >= 0, "bad argument");
@@ -963,11 +1048,16 @@ int acme_dqn_q_values(acme_dqn* l, const void* obs, int64_t batch, int32_t use_t
     int rc = sync_planes(l, st);
     if (rc == ACME_OK) rc = convert_frames(l, obs, obs, B, B, st);
     // Uncalibrated scales: one forward to measure the activations, then the real one.
+    // Each pass ends with the target records' rescale; the last one's flag lands in the
+    // guard's qv word (acme_dqn_guard_state), so a caller can repeat an overflowed call.
     for (int pass = l->scales_ok ? 1 : 0; pass < 2 && rc == ACME_OK; ++pass) {
       rc = nature_forward_p3(l, prm, use_target ? l->tpl : l->wpl, torso::Frames{l->frames}, B,
                              l->t1p, l->t2p, l->t3p, l->thid, q_out, st);
-      if (rc == ACME_OK && pass == 0)
-        rc = launch_plane_rescale(l->scales, kScTransient, kScTransient, -1, -1, l->overflow, st);
+      RescaleGuard rg;
+      rg.g = l->guard;
+      rg.mode = kRgQValues;
+      if (rc == ACME_OK)
+        rc = launch_plane_rescale(l->scales + kScT1, 3, 3, -1, -1, l->overflow, st, -1, -1, rg);
     }
     return rc;
   }
@@ -988,18 +1078,24 @@ int acme_dqn_forward_backward_stage(acme_dqn* l, const acme_transition_batch* ba
 static int loss_and_dense_backward(acme_dqn* l, const acme_transition_batch* batch,
                                    const acme_dqn_outputs* out, hipStream_t st, bool join_dense);
 
-// Activation / gradient scales for new parameters (gemm_p3.h): two passes of the step's
-// forward, loss and backward on this batch (local IS normaliser, outputs to scratch; no
-// Adam, no target copy), each followed by a rescale of the transient records.  The first
-// pass runs at the current scales (1 after creation), whose maxima are measured before the
-// split and so are accurate even where that pass's planes lose precision; the second
-// refines them.  Writes nothing the real step does not overwrite.
+// Activation / gradient scales for new parameters (gemm_p3.h): kCalibrationPasses passes of
+// the step's forward, loss and backward on this batch (local IS normaliser, outputs to
+// scratch; no Adam, no target copy), each followed by a rescale of the transient records.
+// A pass measures each tensor's maximum before its split, so it is accurate even where the
+// planes are written at a poor scale; but a tensor computed from planes that underflowed to
+// zero at their scale measures 0 and keeps its scale, and only the next pass, reading its
+// input at a calibrated scale, measures it.  The input-gradient chain (head dZ -> dz3 ->
+// dz2 -> dz1) is four tensors deep, so four passes calibrate every record whatever the
+// gradients' magnitude (two left dz2 / dz1 at scale 1 when |TD| was ~1e-4: their planes
+// read as zeros, tests/test_step_guard_gpu.py).  Writes nothing the real step does not
+// overwrite.
+constexpr int kCalibrationPasses = 4;
 static int calibrate_scales(acme_dqn* l, const acme_transition_batch* batch, hipStream_t st) {
   acme_transition_batch cb = *batch;
   cb.global_min_probability = nullptr;
   l->calibrating = true;
   int rc = ACME_OK;
-  for (int pass = 0; pass < 2 && rc == ACME_OK; ++pass) {
+  for (int pass = 0; pass < kCalibrationPasses && rc == ACME_OK; ++pass) {
     rc = forward_backward_stage(l, &cb, nullptr, 2, st, false);
     if (rc == ACME_OK) rc = forward_backward_stage(l, &cb, nullptr, 3, st, false);
     if (rc == ACME_OK) rc = forward_backward_stage(l, &cb, nullptr, 1, st, false);
@@ -1010,6 +1106,7 @@ static int calibrate_scales(acme_dqn* l, const acme_transition_batch* batch, hip
   if (rc != ACME_OK) return rc;
   // Overflows at the initial scales are expected and corrected by the passes.
   ACME_HIP_TRY(hipMemsetAsync(l->overflow, 0, sizeof(int), st));
+  if ((rc = clear_guard_flags(l, st)) != ACME_OK) return rc;
   l->scales_ok = true;
   return ACME_OK;
 }
@@ -1039,6 +1136,7 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
                         WP(l, l->wpl, l->t_c3w), P(l, l->params, l->t_c1b),
                         P(l, l->params, l->t_c2b), P(l, l->params, l->t_c3b)};
       torso::Side sd;
+      sd.single_role = l->single_role;
       if (side_stream(l)) {
         sd.side = l->side;
         sd.slab = l->side_slab;
@@ -1055,9 +1153,17 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
         sd.defer = l->wslabs;
         l->slabs_pending = true;
       }
-      return torso::backward_p3(w, g, l->cur_frames, B,
-                                torso::PActs{l->x1p, l->x2p, l->x3p}, l->dz3p, l->dz2p, l->dz1p,
-                                l->slab, st, sd);
+      int rc = torso::backward_p3(w, g, l->cur_frames, B,
+                                  torso::PActs{l->x1p, l->x2p, l->x3p}, l->dz3p, l->dz2p, l->dz1p,
+                                  l->slab, st, sd);
+      // Data parallelism: this rank's skip decision into the torso bucket's padding word,
+      // which the ranks' all-reduce combines before Adam reads it (step_gate).
+      if (rc == ACME_OK && l->dp_gate && !l->calibrating) {
+        Gate local = step_gate(l);
+        local.dp = nullptr;
+        rc = launch_gate_publish(local, l->grads + l->dp_gate_index, st);
+      }
+      return rc;
     }
     torso::Grads g{Pm(l, l->grads, l->t_c1w), Pm(l, l->grads, l->t_c1b), Pm(l, l->grads, l->t_c2w),
                    Pm(l, l->grads, l->t_c2b), Pm(l, l->grads, l->t_c3w), Pm(l, l->grads, l->t_c3b)};
@@ -1101,7 +1207,7 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
     if (side) {
       // Early start: the side stream's own order covers the previous step's target work
       // and T-record rescale; only the batch's inputs are waited for.
-      if (quiet && batch->inputs_event && !l->target_dirty && tune("TEARLY") != 1) {
+      if (quiet && batch->inputs_event && !l->target_dirty) {
         ACME_HIP_TRY(hipStreamWaitEvent(side, static_cast<hipEvent_t>(batch->inputs_event), 0));
       } else {
         ACME_HIP_TRY(hipEventRecord(l->ev[0], st));
@@ -1112,10 +1218,11 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
     } else {
       l->target_dirty = true;  // the target forward runs on the caller's stream
     }
-    // ACME_V_ONFIRST=1: the online forward (the critical path) issued before the target
-    // forward, so after a host wait (a timed window's first step) its kernels reach the GPU
-    // earlier.  Either order gives the same bits.
-    const bool online_first = side && tune("ONFIRST") == 1;
+    // The online forward (the critical path) is issued before the target forward, so after a
+    // host wait (a timed window's first step) its kernels reach the GPU first (20-step
+    // windows 0.5208 -> 0.5181 ms, three alternating runs each).  Either order gives the
+    // same bits.
+    const bool online_first = side != nullptr;
     if (online_first &&
         (rc = nature_forward_p3(l, l->params, l->wpl, fwd_frames, 2 * B, l->x1p, l->x2p, l->x3p,
                                 l->hid, l->q_on, st, nullptr, B)) != ACME_OK)
@@ -1124,8 +1231,15 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
                                 l->t1p, l->t2p, l->t3p, l->thid, l->q_tg, tst,
                                 side ? l->tslab : l->slab, 0)) != ACME_OK)
       return rc;
-    if (side && (rc = launch_plane_rescale(l->scales + kScT1, 3, 3, -1, -1, l->overflow, side)))
-      return rc;
+    {  // the target records' scales, and their flag into the step's slot t[seq & 1]
+      RescaleGuard rg;
+      rg.g = l->guard;
+      rg.mode = kRgTarget;
+      rg.gate = step_gate(l);
+      if ((rc = launch_plane_rescale(l->scales + kScT1, 3, 3, -1, -1, l->overflow, tst, -1, -1,
+                                     rg)))
+        return rc;
+    }
     if (side) ACME_HIP_TRY(hipEventRecord(l->ev[1], side));
     if (!online_first &&
         (rc = nature_forward_p3(l, l->params, l->wpl, fwd_frames, 2 * B, l->x1p, l->x2p, l->x3p,
@@ -1225,6 +1339,26 @@ int acme_dqn_grad_split(const acme_dqn* l, int64_t* split) {
 // Adam (+ the parameter planes) and the periodic target copy; `copy` decided by the host.
 static int apply_impl(acme_dqn* l, bool copy, hipStream_t st) {
   int rc;
+  Gate gate;  // Adam reads the step's skip decision, made by the rescale below
+  if (l->p3_capable) {
+    // Every transient record's next scale from this step's maxima, and the step guard's
+    // decision (guard->last): skip when a plane write overflowed, when a tensor's maximum
+    // fell more than ~2^8-fold below its scale (its planes lost precision), or, with data
+    // parallelism, when any rank skips.  Before Adam, after every plane this step writes;
+    // the target forward's records were rescaled after it (on the side stream, which may
+    // already run the next step's target forward).
+    ACME_PROF("plane_rescale", st, 0.0, 0.0);
+    RescaleGuard rg;
+    rg.g = l->guard;
+    rg.mode = kRgStep;
+    rg.gate = step_gate(l);
+    rg.host_skipped = l->host_skipped;
+    if ((rc = launch_plane_rescale(l->scales, kScTransient, kScTransient, -1, -1, l->overflow, st,
+                                   kScT1, kScT3 + 1, rg)) != ACME_OK)
+      return rc;
+    gate.g = l->guard;
+    gate.use_last = 1;
+  }
   if (l->slabs_pending) {  // the conv weight gradients reduced on Adam's read
     l->slabs_pending = false;
     ACME_PROF("adam", st, 0.0, 28.0 * (double)l->logical);
@@ -1243,13 +1377,12 @@ static int apply_impl(acme_dqn* l, bool copy, hipStream_t st) {
     a.dense_n4 = (l->flat - l->tensors[l->t_fcw].offset) / 4;
     rc = launch_adam_slabs(l->params, l->grads, l->m, l->v, a, l->cfg.learning_rate,
                            l->cfg.adam_beta1, l->cfg.adam_beta2, l->cfg.adam_epsilon,
-                           l->num_steps + 1, l->p3_capable ? l->wpl : nullptr, l->flat,
-                           l->p3_capable ? l->scales + kScParams : nullptr,
-                           l->cfg.semantics == ACME_SEMANTICS_JAX ? 1 : 0, st);
+                           &l->guard->applied, l->wpl, l->flat, l->scales + kScParams,
+                           l->cfg.semantics == ACME_SEMANTICS_JAX ? 1 : 0, gate, st);
     if (rc != ACME_OK) return rc;
   } else {
     ACME_PROF("adam", st, 0.0, 28.0 * (double)l->logical);
-    if ((rc = adam_range(l, 0, l->flat, st)) != ACME_OK) return rc;
+    if ((rc = adam_range(l, 0, l->flat, gate, st)) != ACME_OK) return rc;
   }
   if (copy) {
     l->target_dirty = true;
@@ -1261,24 +1394,24 @@ static int apply_impl(acme_dqn* l, bool copy, hipStream_t st) {
                                   hipMemcpyDeviceToDevice, st));
   }
   if (l->p3_capable) {
-    // The parameters' maximum every kParamAmaxPeriod steps (Adam moves a parameter by about
-    // lr per step, far inside the 2^8 headroom of its scale); then the next step's scales
-    // from this step's maxima, the target planes copied from the parameter planes taking
-    // their scale.
-    if (l->num_steps % kParamAmaxPeriod == 0) {
+    // The parameter planes' record (persistent): the parameters' maximum every
+    // kParamAmaxPeriod steps (Adam moves a parameter by about lr per step, far inside the
+    // 2^8 headroom of its scale) moves the write scale; the step after it the read scale
+    // follows the planes Adam then wrote; a target copy takes the read scale of the planes
+    // it copied.  Other steps leave the record as it is (no launch).
+    const bool amax = l->num_steps % kParamAmaxPeriod == 0;
+    if (amax) {
       ACME_PROF("param_amax", st, 0.0, 4.0 * (double)l->flat);
       if ((rc = launch_param_amax(l->params, l->flat, l->scales + kScParams, st)) != ACME_OK)
         return rc;
     }
-    {
-      ACME_PROF("plane_rescale", st, 0.0, 0.0);
-      // The target activations' records were rescaled on the side stream (which may already
-      // run the next step's target forward).
-      const bool side = side_stream(l) != nullptr;
-      rc = launch_plane_rescale(l->scales, kScTransient, kScTarget, copy ? kScParams : -1,
-                                copy ? kScTarget : -1, l->overflow, st, side ? kScT1 : -1,
-                                side ? kScT3 + 1 : -1);
+    if (amax || copy || l->param_rescale_pending) {
+      ACME_PROF("param_rescale", st, 0.0, 0.0);
+      if ((rc = launch_plane_rescale(l->scales + kScParams, 0, 1, copy ? 0 : -1, copy ? 1 : -1,
+                                     l->overflow, st)) != ACME_OK)
+        return rc;
     }
+    l->param_rescale_pending = amax;
   }
   return rc;
 }
@@ -1295,6 +1428,7 @@ int acme_dqn_apply(acme_dqn* l, void* stream) {
   int rc = apply_impl(l, copies_target(l), as_stream(stream));
   if (rc != ACME_OK) return rc;
   l->num_steps += 1;
+  l->seq += 1;
   return ACME_OK;
 }
 
@@ -1326,7 +1460,7 @@ int acme_dqn_dp_init(acme_dqn* l, void* nccl_comm, int32_t world_size) {
   }
   l->dp_comm = nccl_comm;
   l->dp_world = world_size;
-  return ACME_OK;
+  return acme_dqn_set_data_parallel_gate(l, 1);
 }
 
 // One data-parallel step (the order of DQNLearner's data_parallel path, itself that of the
@@ -1381,6 +1515,7 @@ int acme_dqn_dp_step(acme_dqn* l, const acme_transition_batch* batch, const acme
   ACME_HIP_TRY(hipStreamWaitEvent(st, l->dp_ev[3], 0));
   if ((rc = apply_impl(l, copies_target(l), st))) return rc;
   l->num_steps += 1;
+  l->seq += 1;
   return ACME_OK;
 }
 
@@ -1399,11 +1534,18 @@ int acme_dqn_step_update(acme_dqn* l, const acme_transition_batch* batch,
   l->upd_replay = nullptr;
   if (rc != ACME_OK) return rc;
   l->num_steps += 1;
+  l->seq += 1;
   if (pending) {  // not issued inside the step (other paths): after it, on the stream
     const double* prio = out && out->priorities ? out->priorities : l->prio_tmp;
     if (after_event)
       ACME_HIP_TRY(hipStreamWaitEvent(as_stream(stream), static_cast<hipEvent_t>(after_event), 0));
-    return acme_replay_update_priorities(replay, keys, prio, batch->batch, stream);
+    Gate q;  // the plane path's step has ended: its skip decision is `last`
+    if (l->p3_capable) {
+      q.g = l->guard;
+      q.use_last = 1;
+    }
+    return replay_update_priorities_gated(replay, keys, prio, batch->batch, q,
+                                          as_stream(stream));
   }
   return ACME_OK;
 }
@@ -1414,6 +1556,7 @@ int acme_dqn_step(acme_dqn* l, const acme_transition_batch* batch, const acme_dq
   const int rc = step_impl(l, batch, out, copies_target(l), as_stream(stream));
   if (rc != ACME_OK) return rc;
   l->num_steps += 1;
+  l->seq += 1;
   return ACME_OK;
 }
 

@@ -115,13 +115,17 @@ constexpr int kPlanes = 2;
 //   wi   1 / w (a copy of the planes takes it as its r);
 //   rl   the r of the planes stored now, after a rescale moved r to the next step's scale
 //        (host-side joins of a transient tensor between steps: debug buffers);
+//   flag the step guard word a producer raises when one of its writes overflowed f16
+//        (|x| w >= 65520, or x not finite): the learner's gated kernels (Adam, the priority
+//        write-back, the rescale) then skip the step's update (StepGuard, kernels.h);
 //   slot max |x| written since the last rescale, spread over kAmaxSlots words on separate
 //        128-B lines (f32 bits; atomicMax as an unsigned: one address took ~12 ns per wave's
 //        atomic, 7,168 of them serialised added 87 us to conv1_fwd); the rescale reduces them.
 constexpr int kAmaxSlots = 64;
 struct PScale {
   float w, r, wi, rl;
-  uint32_t pad1[28];
+  uint32_t* flag;
+  uint32_t pad1[26];
   struct Slot {
     uint32_t v;
     uint32_t pad[31];
@@ -167,18 +171,28 @@ __device__ __forceinline__ uint32_t f16x2_of_bytes(uint32_t x, int sh) {
   return f16_of_byte(x, sh) | (f16_of_byte(x, sh + 8) << 16);
 }
 
+// Maximum of two magnitudes (non-negative floats, or NaN) that keeps NaN: non-negative
+// floats order as their bits, and a NaN (sign cleared by fabsf) above infinity.  A plane
+// computed from overflowed planes is NaN, and its record must see that.
+__device__ __forceinline__ float amax_max(float a, float b) {
+  return __builtin_bit_cast(float, max(__builtin_bit_cast(uint32_t, a),
+                                       __builtin_bit_cast(uint32_t, b)));
+}
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  for (int o = 32; o > 0; o >>= 1) v = amax_max(v, __shfl_xor(v, o, 64));
   return v;
 }
 // Raises one of sc's amax slots (chosen by the wave's position in the grid) to the wave's
-// maximum of v (v >= 0, or NaN); every lane of the wave calls.
+// maximum of v (v >= 0, or NaN) of planes written at sc->w, and raises the record's guard
+// flag when that maximum overflowed them; every lane of the wave calls.
 __device__ __forceinline__ void amax_commit(PScale* sc, float v) {
   v = wave_max(v);
   const int wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (sc && (threadIdx.x & 63) == 0 && v != 0.f)
+  if (sc && (threadIdx.x & 63) == 0 && v != 0.f) {
     atomicMax(&sc->slot[wid & (kAmaxSlots - 1)].v, __builtin_bit_cast(uint32_t, v));
+    if (!(v * sc->w < 65520.f) && sc->flag) atomicOr(sc->flag, 1u);
+  }
 }
 
 // A plane tensor: plane i of element e at p[i * stride + e], written as x * sc->w.
@@ -214,17 +228,22 @@ struct CPlanes {
 
 // The MFMA terms of one 32x32x16 product of an NPA-plane A fragment and an NPB-plane B
 // fragment, smallest first: (1,0), (0,1), (0,0).
+#ifndef P3_FOUR_TERMS
+#define P3_FOUR_TERMS 0  // 1: also the l*l term of two-plane products (exact products)
+#endif
 template <int NPA, int NPB>
 __device__ __forceinline__ void p3_terms(const f16x8 (&fa)[NPA], const f16x8 (&fb)[NPB],
                                          f32x16& acc) {
   static_assert((NPA == 1 || NPA == 2) && (NPB == 1 || NPB == 2), "1 or 2 planes per operand");
+  if constexpr (P3_FOUR_TERMS && NPA == 2 && NPB == 2)
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[1], fb[1], acc, 0, 0, 0);
   if constexpr (NPA == 2) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[1], fb[0], acc, 0, 0, 0);
   if constexpr (NPB == 2) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[0], fb[1], acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[0], fb[0], acc, 0, 0, 0);
 }
 template <int NPA, int NPB>
 constexpr int p3_nterms() {
-  return 1 + (NPA == 2 ? 1 : 0) + (NPB == 2 ? 1 : 0);
+  return 1 + (NPA == 2 ? 1 : 0) + (NPB == 2 ? 1 : 0) + (P3_FOUR_TERMS && NPA == 2 && NPB == 2 ? 1 : 0);
 }
 
 // Problems with `static constexpr bool kAmax = true` write a plane output whose scale
@@ -462,7 +481,7 @@ struct P3Core {
         const f32x4 lo = *reinterpret_cast<const f32x4*>(cw + row * PITCH + col);
         const f32x4 hi = *reinterpret_cast<const f32x4*>(cw + row * PITCH + col + 4);
         const float v8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        if (m < p.M && n < p.N) amx = fmaxf(amx, p.store8(m, n, v8, split));
+        if (m < p.M && n < p.N) amx = amax_max(amx, p.store8(m, n, v8, split));
       }
       __syncthreads();
     }

@@ -98,6 +98,11 @@ struct acme_impala {
   float* pslab = nullptr;
   bool last_p3 = false;  // the last learner step ran the plane path (debug buffers join planes)
   int64_t last_rows = 0;
+  // Step guard (kernels.h): a step whose planes overflowed or whose LSTM unroll timed out
+  // (tmo[0]; tmo[1] counts them, tmo[2] is the policy step's own timeout word) applies no
+  // update.  grad_sumsq folds the flags; clip_adam reads guard->last.
+  StepGuard* guard = nullptr;
+  int64_t* host_skipped = nullptr;
 };
 
 namespace {
@@ -1094,10 +1099,8 @@ torso::PWeights torso_pw(const acme_impala* l) {
                          P(l, l->params, l->t_c[5])};
 }
 // The plane path runs the learner steps of the Atari torso with enough frames to fill the
-// GEMMs (ACME_V_IMP3=1: the f32 engine throughout, for tests and A/B).
-bool use_p3(const acme_impala* l, int rows) {
-  return l->p3_capable && rows >= kP3MinRows && tune_variant("IMP3") != 1;
-}
+// GEMMs (ACME_V_IMP3=1 at creation: the f32 engine throughout, for tests).
+bool use_p3(const acme_impala* l, int rows) { return l->p3_capable && rows >= kP3MinRows; }
 
 // gx = OAR(emb) @ W_i + b from the plane GEMM's split-K partials of feat @ W_i[0:F]: the
 // one-hot(prev a) row of W_i, tanh(prev r) times its last row and the bias are added here
@@ -1186,7 +1189,7 @@ torso::Weights torso_w(const acme_impala* l) {
 // Network forward over rows = B*T frames: features, OAR projection, T LSTM steps, head.
 int network_forward(acme_impala* l, const void* obs, const int32_t* prev_a, const float* prev_r,
                     const float* h0, const float* c0, int64_t state_stride, int B, int T,
-                    hipStream_t st, bool p3 = false) {
+                    hipStream_t st, bool p3, unsigned* tmo) {
   const int rows = B * T, H = l->H, A = l->A;
   const float* feat;
   if (p3) {
@@ -1257,7 +1260,7 @@ int network_forward(acme_impala* l, const void* obs, const int32_t* prev_a, cons
       const unsigned tag0 = next_lstm_tags(l, st);
       lstm_fwd_rg_kernel<<<(unsigned)(ceil_div(B, kRgRows) * kRgGroups), 256, 0, st>>>(
           l->gx, P(l, l->params, l->t_wh), h0, state_stride, c0, state_stride, B, T, l->gates,
-          l->h, l->c, l->xg, tag0, l->tmo);
+          l->h, l->c, l->xg, tag0, tmo);
       IM_CHECK();
     } else
     for (int t = 0; t < T; ++t) {
@@ -1298,7 +1301,7 @@ int impala_step_impl(acme_impala* l, const acme_sequence_batch* bt, float* metri
   l->last_p3 = p3;
   l->last_rows = rows;
   int rc = network_forward(l, bt->observation, bt->prev_action, bt->prev_reward, bt->h0, bt->c0,
-                           bt->state_stride, B, T, st, p3);
+                           bt->state_stride, B, T, st, p3, l->tmo);
   if (rc != ACME_OK) return rc;
   {
     ACME_PROF("impala_loss", st, 0.0, 0.0);
@@ -1410,7 +1413,11 @@ int impala_step_impl(acme_impala* l, const acme_sequence_batch* bt, float* metri
                             l->pslab, st);
     if (rc != ACME_OK) return rc;
     // The next plane step's activation / gradient scales from this step's maxima.
-    rc = launch_plane_rescale(l->scales, kScTransient, kScTransient, -1, -1, l->overflow, st);
+    RescaleGuard rg;  // an overflowed or underflowed record skips the step (grad_sumsq)
+    rg.g = l->guard;
+    rg.mode = kRgFlag;
+    rc = launch_plane_rescale(l->scales, kScTransient, kScTransient, -1, -1, l->overflow, st, -1,
+                              -1, rg);
     if (rc != ACME_OK) return rc;
   } else {
     const float* feat = atari(l) ? l->x3 : static_cast<const float*>(bt->observation);
@@ -1437,7 +1444,8 @@ int impala_step_impl(acme_impala* l, const acme_sequence_batch* bt, float* metri
   {
     ACME_PROF("impala_adam", st, 0.0, 7.0 * 4.0 * (double)l->flat);
     const int64_t n4 = l->flat / 4;
-    rc = launch_grad_sumsq(gr, n4, n4, l->norm_part, kNormBlocks, l->dev_step, st);
+    rc = launch_grad_sumsq(gr, n4, n4, l->norm_part, kNormBlocks, l->dev_step, st, l->guard,
+                           l->tmo, l->host_skipped);
     if (rc != ACME_OK) return rc;
     ClipAdamArgs a;
     a.p = l->params; a.m = l->m; a.v = l->v; a.g = gr; a.n4 = n4; a.group0_4 = n4;
@@ -1447,6 +1455,8 @@ int impala_step_impl(acme_impala* l, const acme_sequence_batch* bt, float* metri
     a.lr0 = a.lr1 = l->cfg.learning_rate;
     a.b1 = l->cfg.adam_beta1; a.b2 = l->cfg.adam_beta2; a.eps = l->cfg.adam_epsilon;
     a.dev_step = l->dev_step; a.norms = l->norms;
+    a.gate.g = l->guard;
+    a.gate.use_last = 1;
     rc = launch_clip_adam(a, st);
     if (rc != ACME_OK) return rc;
   }
@@ -1463,6 +1473,7 @@ int acme_impala_destroy(acme_impala* l) {
   // right after its last step): drain it before the buffers go.
   (void)hipDeviceSynchronize();
   for (void* p : l->allocs) (void)hipFree(p);
+  if (l->host_skipped) (void)hipHostFree(l->host_skipped);
   delete l;
   return ACME_OK;
 }
@@ -1538,22 +1549,31 @@ int acme_impala_create(const acme_impala_config* cfg, acme_impala** out) {
       (rc = dev_alloc(l, &l->ent, R)) ||
       (rc = dev_alloc(l, &l->norm_part, 2 * kNormBlocks)) || (rc = dev_alloc(l, &l->dev_step, 1)) ||
       (rc = dev_alloc(l, &l->metrics_tmp, 4)) || (rc = dev_alloc(l, &l->norms, 2)) ||
-      (rc = dev_alloc(l, &l->xg, (int64_t)2 * B * H)) || (rc = dev_alloc(l, &l->tmo, 4)))
+      (rc = dev_alloc(l, &l->xg, (int64_t)2 * B * H)) || (rc = dev_alloc(l, &l->tmo, 4)) ||
+      (rc = dev_alloc(l, &l->guard, 1)))
     return fail(rc);
+  if (hipMemset(l->guard, 0, sizeof(StepGuard)) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&l->host_skipped), sizeof(int64_t),
+                    hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+    return fail((set_error("step guard allocation failed"), ACME_ERR_HIP));
+  *l->host_skipped = 0;
   if (H == kRgH && B <= kRgMaxB &&
       (rc = dev_alloc(l, &l->xb, (int64_t)2 * kRgGroups * B * H)))
     return fail(rc);
   // Plane path (Atari torso): each operand plane is addressed through a 31-bit byte range,
   // so the f16 frames of one step bound it (R < 38,000 frames); larger unrolls stay f32.
   if (cfg->torso == ACME_IMPALA_TORSO_ATARI && R * torso::kObsBytes * 2 < (int64_t)INT32_MAX &&
-      R >= kP3MinRows) {
+      R >= kP3MinRows && tune_variant("IMP3") != 1) {
     l->p3_capable = true;
     l->p3_prefix = align64(l->tensors[l->t_wi].offset + l->tensors[l->t_wi].numel);
     if ((rc = dev_alloc(l, &l->scales, kScCount)) || (rc = dev_alloc(l, &l->overflow, 1)))
       return fail(rc);
     std::vector<gemm::PScale> init(kScCount);
     std::memset(init.data(), 0, init.size() * sizeof(gemm::PScale));
-    for (auto& r : init) r.w = r.r = r.wi = r.rl = 1.f;
+    for (auto& r : init) {
+      r.w = r.r = r.wi = r.rl = 1.f;
+      r.flag = &l->guard->on;
+    }
     if (hipMemcpy(l->scales, init.data(), init.size() * sizeof(gemm::PScale),
                   hipMemcpyHostToDevice) != hipSuccess ||
         hipMemset(l->overflow, 0, sizeof(int)) != hipSuccess)
@@ -1646,13 +1666,18 @@ int acme_impala_step(acme_impala* l, const acme_sequence_batch* b, float* metric
   hipStream_t st = as_stream(stream);
   int rc = ACME_OK;
   if (atari(l) && use_p3(l, (int)(b->batch * b->sequence_length)) && !l->scales_ok) {
-    // Plane scales for newly bound parameters: two forward + backward passes without the
+    // Plane scales for newly bound parameters: forward + backward passes without the
     // update (the first at the current scales, whose maxima are measured before the split;
     // each ends with the rescale), then the step.  Overflows at the initial scales are
     // expected and cleared.
-    for (int pass = 0; pass < 2 && rc == ACME_OK; ++pass) rc = impala_step_impl(l, b, nullptr, st, false);
+    // Four passes: the input-gradient chain dgates -> dz3 -> dz2 -> dz1 is four tensors
+    // deep, and a tensor computed from planes that underflowed at their initial scale
+    // measures 0 until its input is calibrated (as the DQN learner's calibrate_scales).
+    for (int pass = 0; pass < 4 && rc == ACME_OK; ++pass) rc = impala_step_impl(l, b, nullptr, st, false);
     if (rc != ACME_OK) return rc;
     ACME_HIP_TRY(hipMemsetAsync(l->overflow, 0, sizeof(int), st));
+    ACME_HIP_TRY(hipMemsetAsync(l->guard, 0, offsetof(StepGuard, applied), st));
+    ACME_HIP_TRY(hipMemsetAsync(l->tmo, 0, sizeof(unsigned), st));
     l->scales_ok = true;
   }
   rc = impala_step_impl(l, b, metrics, st);
@@ -1683,7 +1708,9 @@ int acme_impala_policy_step(acme_impala* l, const void* obs, const int32_t* prev
                  "rows must be in [1, max_batch=%d]", l->cfg.max_batch);
   hipStream_t st = as_stream(stream);
   const int H = l->H, A = l->A;
-  int rc = network_forward(l, obs, prev_action, prev_reward, h, c, H, (int)rows, 1, st);
+  // The policy's unroll has its own timeout word (a learner step is not skipped for it).
+  int rc = network_forward(l, obs, prev_action, prev_reward, h, c, H, (int)rows, 1, st, false,
+                           l->tmo + 2);
   if (rc != ACME_OK) return rc;
   // Outputs are rows of the T = 1 unroll.
   if (logits)
@@ -1700,6 +1727,61 @@ int acme_impala_policy_step(acme_impala* l, const void* obs, const int32_t* prev
 }
 
 int64_t acme_impala_num_steps(const acme_impala* l) { return l ? l->num_steps : 0; }
+
+int acme_impala_set_applied_steps(acme_impala* l, int64_t n) {
+  ACME_CHECK_ARG(l && n >= 0, "bad argument");
+  ACME_HIP_TRY(hipDeviceSynchronize());
+  ACME_HIP_TRY(hipMemcpy(l->dev_step, &n, sizeof(n), hipMemcpyHostToDevice));
+  ACME_HIP_TRY(hipMemcpy(&l->guard->applied, &n, sizeof(n), hipMemcpyHostToDevice));
+  return ACME_OK;
+}
+
+// Scale state = (w, r, wi, rl) of every record (as acme_dqn_scale_state).
+int acme_impala_scale_state(const acme_impala* l, float* out, int32_t capacity, int32_t* count) {
+  ACME_CHECK_ARG(l && count, "null argument");
+  *count = l->scales ? 4 * kScCount : 0;
+  if (!l->scales || !out) return ACME_OK;
+  ACME_CHECK_ARG(capacity >= 4 * kScCount, "scale state needs %d floats", 4 * kScCount);
+  ACME_HIP_TRY(hipDeviceSynchronize());
+  for (int i = 0; i < kScCount; ++i)
+    ACME_HIP_TRY(hipMemcpy(out + 4 * i, l->scales + i, 4 * sizeof(float), hipMemcpyDeviceToHost));
+  return ACME_OK;
+}
+
+int acme_impala_set_scale_state(acme_impala* l, const float* in, int32_t count) {
+  ACME_CHECK_ARG(l && in, "null argument");
+  ACME_CHECK_ARG(l->scales && count == 4 * kScCount, "scale state of %d floats expected, got %d",
+                 l->scales ? 4 * kScCount : 0, count);
+  for (int i = 0; i < 4 * kScCount; ++i) {
+    int e;
+    const float m = std::frexp(in[i], &e);
+    ACME_CHECK_ARG(m == 0.5f, "scale state entries must be powers of two");
+  }
+  ACME_HIP_TRY(hipDeviceSynchronize());
+  for (int i = 0; i < kScCount; ++i)
+    ACME_HIP_TRY(hipMemcpy(l->scales + i, in + 4 * i, 4 * sizeof(float), hipMemcpyHostToDevice));
+  l->scales_ok = true;
+  return ACME_OK;
+}
+
+int64_t acme_impala_skipped_steps(const acme_impala* l) {
+  if (!l || !l->host_skipped) return 0;
+  return *reinterpret_cast<volatile const int64_t*>(l->host_skipped);
+}
+
+int acme_impala_guard_state(acme_impala* l, int64_t* out4) {
+  ACME_CHECK_ARG(l && out4 && l->guard, "null argument");
+  ACME_HIP_TRY(hipDeviceSynchronize());
+  StepGuard g;
+  unsigned t[4];
+  ACME_HIP_TRY(hipMemcpy(&g, l->guard, sizeof(g), hipMemcpyDeviceToHost));
+  ACME_HIP_TRY(hipMemcpy(t, l->tmo, sizeof(t), hipMemcpyDeviceToHost));
+  out4[0] = g.applied;
+  out4[1] = g.skipped;
+  out4[2] = g.last;
+  out4[3] = t[1];
+  return ACME_OK;
+}
 
 int acme_impala_set_num_steps(acme_impala* l, int64_t n) {
   ACME_CHECK_ARG(l && n >= 0, "bad argument");
@@ -1721,7 +1803,9 @@ int acme_impala_debug_buffer(const acme_impala* l, const char* name, const float
       {"pv", l->pv, R * (l->A + 1)}, {"vs", l->vs, R},        {"pg_adv", l->pg_adv, R},
       {"h", l->h, R * l->H},         {"c", l->c, R * l->H},   {"dpv", l->dpv, R * (l->A + 1)},
       {"dgates", l->dgates, R * 4 * l->H}, {"grad_norm", l->norms, 1},
-      {"lstm_timeout", reinterpret_cast<const float*>(l->tmo), 1},
+      {"lstm_timeout", reinterpret_cast<const float*>(l->tmo + 1), 1},
+      {"lstm_timeout_step", reinterpret_cast<const float*>(l->tmo), 1},
+      {"policy_lstm_timeout", reinterpret_cast<const float*>(l->tmo + 2), 1},
       {"hh", l->hh, R * l->H2},      {"x1", l->x1, l->x1 ? R * torso::kX1 : 0},
       {"x2", l->x2, l->x2 ? R * torso::kFlat : 0}, {"x3", l->x3, l->x3 ? R * torso::kFlat : 0},
   };

@@ -6,10 +6,57 @@
 
 #include <cstdint>
 
+typedef struct acme_replay acme_replay;  // include/acme_hip.h
+
 namespace acme {
 namespace gemm {
 struct PScale;  // gemm_p3.h: the scale record of a plane tensor
 }
+
+// Step guard of a learner on the f16 plane engine: the "skip the step on overflow" rule of
+// automatic mixed precision (a step whose f16 planes overflowed changes no parameter, Adam
+// moment or count, priority or target; the next step runs at rescaled planes).  Producers
+// raise their record's flag word (gemm_p3.h PScale::flag -> on / tt / prm); the gated
+// kernels read the Gate below before their first store; the end-of-step rescale counts the
+// step as applied or skipped and clears the flags.  Device memory, one per learner.
+struct StepGuard {
+  uint32_t on;       // the online forward's and the backward's records, this step
+  uint32_t tt;       // the target forward's records (the target rescale moves it to t[])
+  uint32_t prm;      // the parameter planes written by Adam
+  uint32_t last;     // the last step that ended was skipped (read after the step)
+  uint32_t t[2];     // the target forward of step s overflowed: t[s & 1]
+  uint32_t qv;       // the last q_values forward overflowed
+  uint32_t pad;
+  int64_t applied;   // updates applied: Adam's t - 1
+  int64_t skipped;   // steps skipped
+};
+// What a gated kernel reads: skip = on | t[par] | (dp && *dp > 0), or `last` (use_last).
+struct Gate {
+  const StepGuard* g = nullptr;  // null: never skip
+  int par = 0;
+  int use_last = 0;
+  const float* dp = nullptr;  // the data-parallel ranks' gate, all-reduced (a gradient word)
+};
+__device__ __forceinline__ bool gate_skip(const Gate& q) {
+  if (!q.g) return false;
+  if (q.use_last) return q.g->last != 0u;
+  return (q.g->on | q.g->t[q.par]) != 0u || (q.dp && *q.dp > 0.f);
+}
+// The end-of-step rescale's work on the guard (launch_plane_rescale).
+enum RescaleMode {
+  kRgNone = 0,
+  kRgTarget = 1,   // after the target forward: t[par] = tt | rescaled bad, tt = 0
+  kRgStep = 2,     // before Adam: last = skip, applied or skipped += 1, on = prm = 0
+  kRgClear = 3,    // after calibration: every flag 0 (the counts kept)
+  kRgQValues = 4,  // after q_values: qv = tt, tt = 0
+  kRgFlag = 5,     // on |= a record overflowed or underflowed (IMPALA: folded by grad_sumsq)
+};
+struct RescaleGuard {
+  StepGuard* g = nullptr;
+  int mode = kRgNone;
+  Gate gate{};                      // kRgStep: the step's gate
+  int64_t* host_skipped = nullptr;  // kRgStep: pinned host mirror of g->skipped (optional)
+};
 
 // Finishes the duelling head GEMM (conv.h DuelHeadFwd): sums the split-K slab
 // [splits][rows][A+1], adds biases and forms q = v + (adv - mean_a(adv))
@@ -92,9 +139,12 @@ int launch_slab_reduce(const float* slab, int splits, int64_t count, float* out0
 // Gradient global norms of two parameter groups ([0, group0_4) and [group0_4, n4) in
 // float4 units): f64 partial sums of squares per block into part[2][nparts], fixed order.
 // Block 0 also advances *dev_step (the Adam t read by launch_clip_adam), so a captured
-// step graph needs no per-step host argument.
+// step graph needs no per-step host argument.  With a guard, block 0 first folds the step's
+// flags (guard->on | *lstm_tmo) into guard->last and counts the step as applied (dev_step
+// advanced) or skipped; launch_clip_adam then reads `last` (Gate::use_last).
 int launch_grad_sumsq(const float* g, int64_t n4, int64_t group0_4, double* part, int nparts,
-                      int64_t* dev_step, hipStream_t st);
+                      int64_t* dev_step, hipStream_t st, StepGuard* guard = nullptr,
+                      uint32_t* lstm_tmo = nullptr, int64_t* host_skipped = nullptr);
 
 // tf.clip_by_global_norm per group (scale = clip * min(1/G, 1/clip) when clipping) then
 // snt.Adam with t = *dev_step and a per-group learning rate.  Optionally block 0 also
@@ -121,6 +171,7 @@ struct ClipAdamArgs {
   int n_b = 0;
   float div_b = 1.f;
   float* out_b = nullptr;
+  Gate gate{};  // skip: p, m, v unchanged
 };
 int launch_clip_adam(const ClipAdamArgs& a, hipStream_t st);
 
@@ -128,12 +179,17 @@ int launch_clip_adam(const ClipAdamArgs& a, hipStream_t st);
 // non-null the updated parameters are also written as f16 planes (stride pstride) at the
 // scale record psc's w (the record's amax comes from launch_param_amax).
 // optix != 0: optix.adam's rounding order, p + (-lr) * (m_hat / (sqrt(v_hat) + eps)).
-// dev_steps (optional): the step count lives on the device (t = *dev_steps + 1, bias
-// corrections computed by the kernel, the count incremented by a one-thread launch after
-// it), so a captured step graph replays correctly; `t` is then ignored.
+// dev_steps (optional): the step count lives on the device (bias corrections computed by
+// the kernel): with `count`, t = *dev_steps + 1 and a one-thread launch after Adam advances
+// it; without, the caller's rescale before Adam has counted this step and t = *dev_steps.
+// `t` is then ignored.
+// gate: a skipped step leaves p, m and v as they are and rewrites the planes of p at psc->w
+// (so the record's read scale stays that of the stored planes).  A plane write that
+// overflows commits the wave's max |p| to psc and raises its flag.
 int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,
                 float b2, float eps, int64_t t, uint16_t* planes, int64_t pstride, hipStream_t st,
-                int optix = 0, int64_t* dev_steps = nullptr, gemm::PScale* psc = nullptr);
+                int optix = 0, int64_t* dev_steps = nullptr, gemm::PScale* psc = nullptr,
+                const Gate& gate = Gate{}, bool count = true);
 
 // launch_adam (snt.Adam, t >= 1) with some gradient ranges still split-K slabs: segment k
 // updates float4 [off4, off4 + n4) of the flat buffers from the deterministic reduction of
@@ -152,9 +208,11 @@ struct AdamSlabs {
   int block_end[kMaxSegs] = {};  // filled by the launcher
   int64_t dense_off4 = 0, dense_n4 = 0;
 };
+// t = *dev_steps (this step counted by the caller's rescale before Adam); gate as launch_adam.
 int launch_adam_slabs(float* p, float* g, float* m, float* v, const AdamSlabs& slabs,
-                      float lr, float b1, float b2, float eps, int64_t t, uint16_t* planes,
-                      int64_t pstride, gemm::PScale* psc, int optix, hipStream_t st);
+                      float lr, float b1, float b2, float eps, const int64_t* dev_steps,
+                      uint16_t* planes, int64_t pstride, gemm::PScale* psc, int optix,
+                      const Gate& gate, hipStream_t st);
 
 // Two-plane split of n floats (n multiple of 4): planes[i * pstride + e], at the scale of
 // max |x| (sets the record sc: w, r = wi = 1 / w; overflow |= 1 on a non-finite x).
@@ -171,9 +229,19 @@ int launch_param_amax(const float* x, int64_t n, gemm::PScale* sc, hipStream_t s
 // End-of-step rescale of a record array (kernels.hip plane_rescale_kernel): records
 // [0, n_transient) transient, [n_transient, n) persistent (rewritten by every Adam pass);
 // copy_to >= n, if >= 0, took a plane copy of copy_from's latest write.  Records in
-// [skip_lo, skip_hi) are left alone (rescaled on the stream that writes them).
+// [skip_lo, skip_hi) are left alone (rescaled on the stream that writes them).  A record
+// whose maximum is not finite (planes computed from overflowed planes) takes the largest
+// scale reduction of the group's overflowed records with a finite maximum (its inputs
+// shrink by that factor at their new scale), else 2^-16.  rg: the step guard's work.
 int launch_plane_rescale(gemm::PScale* recs, int n_transient, int n, int copy_from, int copy_to,
-                         int* overflow, hipStream_t st, int skip_lo = -1, int skip_hi = -1);
+                         int* overflow, hipStream_t st, int skip_lo = -1, int skip_hi = -1,
+                         const RescaleGuard& rg = RescaleGuard{});
+// The replay's update_priorities (replay.hip) behind a gate: a skipped step writes none.
+int replay_update_priorities_gated(acme_replay* r, const uint64_t* keys, const double* prios,
+                                   int64_t n, const Gate& gate, hipStream_t st);
+// Data-parallel gate: *dst = the step's local skip (1.f or 0.f), a gradient word that the
+// ranks' all-reduce then combines (any rank's skip makes it > 0 on every rank).
+int launch_gate_publish(const Gate& gate, float* dst, hipStream_t st);
 // uint8 frames -> exact f16 (one plane): out[f][e] = f16(frame f byte e) for rows frames
 // of `frame_bytes` (multiple of 8), frames [0, split) from a and the rest from b.
 int launch_frames_f16(const uint8_t* a, const uint8_t* b, int split, int rows, int frame_bytes,

@@ -261,7 +261,7 @@ __device__ __forceinline__ float store_planes4(uint16_t* planes, int64_t pstride
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     gemm::split2_bits(x[j] * w, h[j], l[j]);
-    mx = fmaxf(mx, fabsf(x[j]));
+    mx = gemm::amax_max(mx, fabsf(x[j]));
   }
   auto pack = [](const uint16_t* q) {
     return uint2{(uint32_t)q[0] | ((uint32_t)q[1] << 16), (uint32_t)q[2] | ((uint32_t)q[3] << 16)};
@@ -576,7 +576,7 @@ __device__ __forceinline__ float store_planes8(uint16_t* planes, int64_t pstride
     gemm::split2_bits(d[2 * j + 1] * w, x1, y1);
     ph[j] = x0 | ((uint32_t)x1 << 16);
     pl[j] = y0 | ((uint32_t)y1 << 16);
-    mx = fmaxf(mx, fmaxf(fabsf(d[2 * j]), fabsf(d[2 * j + 1])));
+    mx = gemm::amax_max(mx, gemm::amax_max(fabsf(d[2 * j]), fabsf(d[2 * j + 1])));
   }
   *reinterpret_cast<uint4*>(planes + e) = uint4{ph[0], ph[1], ph[2], ph[3]};
   *reinterpret_cast<uint4*>(planes + pstride + e) = uint4{pl[0], pl[1], pl[2], pl[3]};
@@ -703,12 +703,19 @@ __global__ void __launch_bounds__(256) head_dz_planes_kernel(
 struct AdamConsts {
   float lr, b1, omb1, b2, omb2, bc1, bc2, eps;
   int optix;
+  int toff = 1;  // device count: t = *dev_steps + toff (0 when the step was counted before Adam)
 };
 
-__device__ __forceinline__ void adam_update4(int64_t i, f32x4 gg, float* __restrict__ p,
-                                             float* __restrict__ m, float* __restrict__ v,
-                                             const AdamConsts& c, uint16_t* __restrict__ planes,
-                                             int64_t pstride, float pw) {
+// Returns max |p| written to the planes (0 without planes).  skip (a guarded step that
+// overflowed): p, m and v stay; the planes of p are rewritten at pw.
+__device__ __forceinline__ float adam_update4(int64_t i, f32x4 gg, float* __restrict__ p,
+                                              float* __restrict__ m, float* __restrict__ v,
+                                              const AdamConsts& c, uint16_t* __restrict__ planes,
+                                              int64_t pstride, float pw, bool skip = false) {
+  if (skip) {
+    if (!planes) return 0.f;
+    return store_planes4(planes, pstride, i, reinterpret_cast<const f32x4*>(p)[i], pw);
+  }
   // The moments are streamed (read once, written once per step) with non-temporal
   // accesses, so they bypass the caches the next step's forwards read the parameter planes
   // through.
@@ -734,8 +741,25 @@ __device__ __forceinline__ void adam_update4(int64_t i, f32x4 gg, float* __restr
   reinterpret_cast<f32x4*>(p)[i] = pp;
   // (No amax here: a block handles about one float4 per thread, so a per-block
   // reduction and atomic cost as much as the update; 45 -> 58 us measured.  The
-  // parameters' maximum is taken by launch_param_amax every few steps.)
-  if (planes) (void)store_planes4(planes, pstride, i, pp, pw);
+  // parameters' maximum is taken by launch_param_amax every few steps; adam_planes_check
+  // commits it only when a write overflowed.)
+  return planes ? store_planes4(planes, pstride, i, pp, pw) : 0.f;
+}
+
+// A parameter-plane write that overflowed (rare): the wave's max |p| goes to the record,
+// whose flag it raises, so the end-of-step rescale moves the scale (the next step's forward
+// then overflows and is skipped, and its Adam pass rewrites the planes at the new scale).
+__device__ __forceinline__ void adam_planes_check(gemm::PScale* psc, float mx, float pw) {
+  if (psc && __builtin_amdgcn_ballot_w64(!(mx * pw < 65520.f)) != 0ull)
+    gemm::amax_commit(psc, mx);
+}
+
+__device__ __forceinline__ void adam_bias_corrections(AdamConsts& c, const int64_t* dev_steps) {
+  if (dev_steps) {  // device-side step count: same expressions as the host's
+    const float tf = (float)(*dev_steps + c.toff);
+    c.bc1 = 1.f - powf(c.b1, tf);
+    c.bc2 = 1.f - powf(c.b2, tf);
+  }
 }
 
 __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p,
@@ -744,18 +768,19 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p,
                                                    int64_t n4, AdamConsts c,
                                                    uint16_t* __restrict__ planes,
                                                    int64_t pstride, gemm::PScale* __restrict__ psc,
-                                                   const int64_t* __restrict__ dev_steps) {
-  if (dev_steps) {  // device-side step count (graph replay): same expressions as the host's
-    const float tf = (float)(*dev_steps + 1);
-    c.bc1 = 1.f - powf(c.b1, tf);
-    c.bc2 = 1.f - powf(c.b2, tf);
-  }
+                                                   const int64_t* __restrict__ dev_steps,
+                                                   const Gate gate) {
+  adam_bias_corrections(c, dev_steps);
+  const bool skip = gate_skip(gate);
   const float pw = planes ? psc->w : 0.f;
+  float mx = 0.f;
 #pragma unroll 2
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (int64_t)gridDim.x * blockDim.x)
-    adam_update4(i, __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(g) + i), p, m, v,
-                 c, planes, pstride, pw);
+    mx = gemm::amax_max(mx, adam_update4(i, skip ? f32x4{} : __builtin_nontemporal_load(
+                                                        reinterpret_cast<const f32x4*>(g) + i),
+                                p, m, v, c, planes, pstride, pw, skip));
+  if (planes) adam_planes_check(psc, mx, pw);
 }
 
 // Adam whose gradients for some ranges are still split-K slabs (the conv weight gradients
@@ -770,8 +795,13 @@ __global__ void __launch_bounds__(256) adam_slabs_kernel(float* __restrict__ p,
                                                          AdamConsts c,
                                                          uint16_t* __restrict__ planes,
                                                          int64_t pstride,
-                                                         const gemm::PScale* __restrict__ psc) {
+                                                         gemm::PScale* __restrict__ psc,
+                                                         const int64_t* __restrict__ dev_steps,
+                                                         const Gate gate) {
+  adam_bias_corrections(c, dev_steps);
+  const bool skip = gate_skip(gate);
   const float pw = planes ? psc->w : 0.f;
+  float mx = 0.f;
   const int nsb = s.block_end[s.nseg - 1];
   if ((int)blockIdx.x < nsb) {
     __shared__ f32x4 red[16][16];
@@ -793,16 +823,19 @@ __global__ void __launch_bounds__(256) adam_slabs_kernel(float* __restrict__ p,
 #pragma unroll
       for (int r = 1; r < 16; ++r) gg += red[r][cc];
       reinterpret_cast<f32x4*>(g)[q.off4 + f] = gg;  // the step's gradient stays readable
-      adam_update4(q.off4 + f, gg, p, m, v, c, planes, pstride, pw);
+      mx = adam_update4(q.off4 + f, gg, p, m, v, c, planes, pstride, pw, skip);
     }
+    if (planes) adam_planes_check(psc, mx, pw);
     return;
   }
   for (int64_t i = (int64_t)(blockIdx.x - nsb) * blockDim.x + threadIdx.x; i < s.dense_n4;
        i += (int64_t)(gridDim.x - nsb) * blockDim.x) {
     const int64_t j = s.dense_off4 + i;
-    adam_update4(j, __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(g) + j), p, m, v,
-                 c, planes, pstride, pw);
+    mx = gemm::amax_max(mx, adam_update4(j, skip ? f32x4{} : __builtin_nontemporal_load(
+                                                        reinterpret_cast<const f32x4*>(g) + j),
+                                p, m, v, c, planes, pstride, pw, skip));
   }
+  if (planes) adam_planes_check(psc, mx, pw);
 }
 
 __global__ void count_step_kernel(int64_t* c) { *c += 1; }
@@ -831,7 +864,7 @@ __global__ void __launch_bounds__(256) split_planes_lagged_kernel(const float* _
   float mx = 0.f;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (int64_t)gridDim.x * blockDim.x)
-    mx = fmaxf(mx, store_planes4(planes, pstride, i, reinterpret_cast<const f32x4*>(x)[i], w));
+    mx = gemm::amax_max(mx, store_planes4(planes, pstride, i, reinterpret_cast<const f32x4*>(x)[i], w));
   gemm::amax_commit(sc, mx);
 }
 
@@ -842,7 +875,8 @@ __global__ void __launch_bounds__(256) amax_kernel(const float* __restrict__ x, 
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (int64_t)gridDim.x * blockDim.x) {
     const f32x4 v = reinterpret_cast<const f32x4*>(x)[i];
-    mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+    mx = gemm::amax_max(mx, gemm::amax_max(gemm::amax_max(fabsf(v[0]), fabsf(v[1])),
+                                           gemm::amax_max(fabsf(v[2]), fabsf(v[3]))));
   }
   gemm::amax_commit(sc, mx);
 }
@@ -897,26 +931,83 @@ __global__ void __launch_bounds__(64) plane_scale_set_kernel(gemm::PScale* __res
 __global__ void __launch_bounds__(1024) plane_rescale_kernel(gemm::PScale* __restrict__ s, int nt,
                                                              int n, int copy_from, int copy_to,
                                                              int* __restrict__ overflow,
-                                                             int skip_lo, int skip_hi) {
+                                                             int skip_lo, int skip_hi,
+                                                             const RescaleGuard rg) {
+  // Scale reduction (log2 of new w / old w) of the group's overflowed records whose maximum
+  // is finite: the records computed from their planes take the largest one.
+  __shared__ int s_shift[16];
+  // A record of the group whose planes overflowed (maximum w >= 65520, or not finite) or
+  // underflowed (0 < maximum w < 1: the largest element's low plane is subnormal, so the
+  // tensor's planes carry less than an f32 rounding's precision relative to its maximum).
+  __shared__ int s_bad;
+  if (threadIdx.x == 0) s_bad = 0;
+  __syncthreads();
   const int i = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ic = i < n ? i : 0;
   uint32_t a_bits = s[ic].slot[lane].v;
   const float w0 = s[ic].w, r0 = s[ic].r, wi0 = s[ic].wi;
   const float cwi = copy_to >= 0 ? s[copy_from].wi : 0.f;
+  // The guard's inputs, read before the first store.
+  uint32_t gv[4] = {0u, 0u, 0u, 0u};
+  float dpv = 0.f;
+  if (rg.g && i == n && lane == 0) {
+    gv[0] = rg.g->on;
+    gv[1] = rg.g->tt;
+    gv[2] = rg.g->t[rg.gate.par & 1];
+    gv[3] = rg.g->prm;
+    if (rg.gate.dp) dpv = *rg.gate.dp;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) a_bits = max(a_bits, (uint32_t)__shfl_xor((int)a_bits, o, 64));
+  const float a = __builtin_bit_cast(float, a_bits);
+  const bool live = i < n && !(i >= skip_lo && i < skip_hi);
+  const bool finite = a <= 3.0e38f;
+  int wexp;
+  (void)frexpf(w0, &wexp);  // w0 = 2^(wexp - 1)
+  const int e = finite && a > 0.f ? scale_exp(a) : 0;
+  if (lane == 0 && i < 16) {
+    s_shift[i] = live && finite && a > 0.f && !(a * w0 < 65520.f) ? e - (wexp - 1) : 0;
+    if (live && a != 0.f && (!(a * w0 < 65520.f) || a * w0 < 1.f)) s_bad = 1;
+  }
   __syncthreads();
   if (i >= n) {
-    if (i == n && lane == 0 && copy_to >= 0) {
-      s[copy_to].r = cwi;
-      s[copy_to].rl = cwi;
+    if (i == n && lane == 0) {
+      if (copy_to >= 0) {
+        s[copy_to].r = cwi;
+        s[copy_to].rl = cwi;
+      }
+      StepGuard* g = rg.g;
+      const uint32_t bad = s_bad ? 1u : 0u;
+      if (g && rg.mode == kRgTarget) {
+        g->t[rg.gate.par & 1] = gv[1] | bad;
+        g->tt = 0u;
+      } else if (g && rg.mode == kRgQValues) {
+        g->qv = gv[1] | bad;
+        g->tt = 0u;
+      } else if (g && rg.mode == kRgFlag) {
+        if (bad) g->on = 1u;
+      } else if (g && rg.mode == kRgStep) {
+        const bool skip = (gv[0] | gv[2] | bad) != 0u || dpv > 0.f;
+        g->last = skip ? 1u : 0u;
+        if (skip) {
+          const int64_t k = g->skipped + 1;
+          g->skipped = k;
+          if (rg.host_skipped) *rg.host_skipped = k;
+        } else {
+          g->applied += 1;
+        }
+        g->on = 0u;
+        g->prm = 0u;
+      } else if (g && rg.mode == kRgClear) {
+        g->on = g->tt = g->prm = g->last = g->qv = 0u;
+        g->t[0] = g->t[1] = 0u;
+      }
     }
     return;
   }
-  if (i >= skip_lo && i < skip_hi) return;  // rescaled by their own stream
+  if (!live) return;  // rescaled by their own stream
   s[i].slot[lane].v = 0u;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) a_bits = max(a_bits, (uint32_t)__shfl_xor((int)a_bits, o, 64));
   if (lane != 0) return;
-  const float a = __builtin_bit_cast(float, a_bits);
   const bool persistent = i >= nt;
   const float stored = persistent ? wi0 : r0;  // the read scale of the planes stored now
   gemm::PScale* rec = s + i;
@@ -926,14 +1017,22 @@ __global__ void __launch_bounds__(1024) plane_rescale_kernel(gemm::PScale* __res
     return;
   }
   if (!(a * w0 < 65520.f)) atomicOr(overflow, 1);
-  const bool finite = a <= 3.0e38f;
-  const int e = finite ? scale_exp(a) : 0;
-  const float w = finite ? ldexpf(1.f, e) : w0 * 0x1p-16f;
-  const float wi = finite ? ldexpf(1.f, -e) : wi0 * 0x1p16f;
+  int shift = -16;  // a non-finite maximum: the largest reduction of the group, else 2^-16
+  if (!finite) {
+    int mn = 0;
+    for (int k = 0; k < n && k < 16; ++k) mn = min(mn, s_shift[k]);
+    if (mn < 0) shift = mn;
+  }
+  const float w = finite ? ldexpf(1.f, e) : ldexpf(w0, shift);
+  const float wi = finite ? ldexpf(1.f, -e) : ldexpf(wi0, -shift);
   rec->w = w;
   rec->wi = wi;
   rec->rl = stored;
   rec->r = persistent ? stored : wi;
+}
+
+__global__ void gate_publish_kernel(const Gate gate, float* dst) {
+  *dst = gate_skip(gate) ? 1.f : 0.f;
 }
 
 __global__ void __launch_bounds__(256) frames_f16_kernel(const uint8_t* __restrict__ a,
@@ -969,8 +1068,31 @@ __global__ void __launch_bounds__(256) join_planes_kernel(const uint16_t* __rest
 constexpr int kSumsqBatch = 8;
 __global__ void __launch_bounds__(256) grad_sumsq_kernel(const float* __restrict__ g, int64_t n4,
                                                          int64_t pol4, double* __restrict__ part,
-                                                         int64_t* __restrict__ dev_step) {
-  if (blockIdx.x == 0 && threadIdx.x == 0 && dev_step) *dev_step += 1;
+                                                         int64_t* __restrict__ dev_step,
+                                                         StepGuard* __restrict__ guard,
+                                                         uint32_t* __restrict__ tmo,
+                                                         int64_t* __restrict__ host_skipped) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    bool skip = false;
+    if (guard) {  // the step's flags: planes overflowed, or the LSTM unroll timed out
+      const uint32_t t = tmo ? tmo[0] : 0u;
+      skip = (guard->on | t) != 0u;
+      guard->last = skip ? 1u : 0u;
+      guard->on = 0u;
+      if (t) {
+        tmo[0] = 0u;
+        tmo[1] += 1u;  // timeouts so far (sticky count)
+      }
+      if (skip) {
+        const int64_t k = guard->skipped + 1;
+        guard->skipped = k;
+        if (host_skipped) *host_skipped = k;
+      } else {
+        guard->applied += 1;
+      }
+    }
+    if (dev_step && !skip) *dev_step += 1;
+  }
   __shared__ double red[2][4];
   double s0 = 0.0, s1 = 0.0;
   const int64_t stride = (int64_t)gridDim.x * 256;
@@ -1057,6 +1179,7 @@ __global__ void __launch_bounds__(256) clip_adam_kernel(const ClipAdamArgs a) {
     }
   }
   __syncthreads();
+  if (gate_skip(a.gate)) return;  // a skipped step: parameters and moments stay
   // kAdamBatch grid-stride positions per pass, every load issued before the first update
   // (clamped indices; the stores are guarded).
   constexpr int kAdamBatch = 4;
@@ -1177,7 +1300,7 @@ int launch_fc_head_forward(const float* slab, int splits, int rows, int H, const
   const bool wa16 = reinterpret_cast<uintptr_t>(wa) % 16 == 0 &&
                     reinterpret_cast<uintptr_t>(wv) % 16 == 0 &&
                     reinterpret_cast<uintptr_t>(fcb) % 16 == 0;
-  if (H == 512 && A == 18 && wa16 && (splits == 4 || splits == 8) && tune_variant("HEAD") != 1) {
+  if (H == 512 && A == 18 && wa16 && (splits == 4 || splits == 8)) {
     // One row per block (2 rows: 12.7 us, 4 rows: 16.3 us, 1 row: 11.4 us per launch).
     if (splits == 8)
       fc_head1024_kernel<8, 18, 1><<<rows, 256, 0, st>>>(slab, rows, fcb, wv, bv, wa, ba, hid, q);
@@ -1265,33 +1388,37 @@ int launch_slab_reduce(const float* slab, int splits, int64_t count, float* out0
 }
 
 int launch_grad_sumsq(const float* g, int64_t n4, int64_t group0_4, double* part, int nparts,
-                      int64_t* dev_step, hipStream_t st) {
+                      int64_t* dev_step, hipStream_t st, StepGuard* guard, uint32_t* lstm_tmo,
+                      int64_t* host_skipped) {
   ACME_CHECK_ARG(g && part && nparts >= 1, "bad argument");
-  grad_sumsq_kernel<<<(unsigned)nparts, 256, 0, st>>>(g, n4, group0_4, part, dev_step);
+  grad_sumsq_kernel<<<(unsigned)nparts, 256, 0, st>>>(g, n4, group0_4, part, dev_step, guard,
+                                                      lstm_tmo, host_skipped);
   ACME_LAUNCH_CHECK();
   return ACME_OK;
 }
 
 int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,
                 float b2, float eps, int64_t t, uint16_t* planes, int64_t pstride, hipStream_t st,
-                int optix, int64_t* dev_steps, gemm::PScale* psc) {
+                int optix, int64_t* dev_steps, gemm::PScale* psc, const Gate& gate, bool count) {
   ACME_CHECK_ARG(p && g && m && v, "null buffer");
   ACME_CHECK_ARG(!planes || psc, "parameter planes need a scale record");
   ACME_CHECK_ARG(n % 4 == 0, "adam buffer length must be a multiple of 4");
   ACME_CHECK_ARG(pstride % 4 == 0, "plane stride must be a multiple of 4");
   ACME_CHECK_ARG(t >= 1 || dev_steps, "adam step must be >= 1");
+  // With a device count not advanced here (count == false), the caller's rescale has
+  // already counted this step: t = *dev_steps.
   const AdamConsts c{lr, b1, 1.f - b1, b2, 1.f - b2,
                      dev_steps ? 0.f : 1.f - powf(b1, (float)t),
-                     dev_steps ? 0.f : 1.f - powf(b2, (float)t), eps, optix};
+                     dev_steps ? 0.f : 1.f - powf(b2, (float)t), eps, optix, count ? 1 : 0};
   const int64_t n4 = n / 4;
   // Grid cap 8192: 47.7 -> 45.2 us against 2048.  Non-temporal gradient / moment traffic:
   // 45.8 -> 45.1 us, and the next step's forwards (which read the parameter planes) ~1 us
   // faster each.
   const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n4, 256), 8192);
   adam_kernel<<<std::max(grid, 1u), 256, 0, st>>>(p, g, m, v, n4, c, planes, pstride, psc,
-                                                  dev_steps);
+                                                  dev_steps, gate);
   ACME_LAUNCH_CHECK();
-  if (dev_steps) {
+  if (dev_steps && count) {
     count_step_kernel<<<1, 1, 0, st>>>(dev_steps);
     ACME_LAUNCH_CHECK();
   }
@@ -1299,11 +1426,11 @@ int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float l
 }
 
 int launch_adam_slabs(float* p, float* g, float* m, float* v, const AdamSlabs& slabs,
-                      float lr, float b1, float b2, float eps, int64_t t, uint16_t* planes,
-                      int64_t pstride, gemm::PScale* psc, int optix, hipStream_t st) {
-  ACME_CHECK_ARG(p && g && m && v && (!planes || psc), "null buffer");
-  ACME_CHECK_ARG(slabs.nseg >= 1 && slabs.nseg <= AdamSlabs::kMaxSegs && t >= 1,
-                 "bad slab Adam arguments");
+                      float lr, float b1, float b2, float eps, const int64_t* dev_steps,
+                      uint16_t* planes, int64_t pstride, gemm::PScale* psc, int optix,
+                      const Gate& gate, hipStream_t st) {
+  ACME_CHECK_ARG(p && g && m && v && (!planes || psc) && dev_steps, "null buffer");
+  ACME_CHECK_ARG(slabs.nseg >= 1 && slabs.nseg <= AdamSlabs::kMaxSegs, "bad slab Adam arguments");
   AdamSlabs s = slabs;
   int blocks = 0;
   for (int k = 0; k < s.nseg; ++k) {
@@ -1313,11 +1440,10 @@ int launch_adam_slabs(float* p, float* g, float* m, float* v, const AdamSlabs& s
     blocks += (int)ceil_div(q.n4, 16);
     s.block_end[k] = blocks;
   }
-  const AdamConsts c{lr, b1, 1.f - b1, b2, 1.f - b2, 1.f - powf(b1, (float)t),
-                     1.f - powf(b2, (float)t), eps, optix};
+  const AdamConsts c{lr, b1, 1.f - b1, b2, 1.f - b2, 0.f, 0.f, eps, optix, 0};
   const int dense = (int)std::min<int64_t>(ceil_div(s.dense_n4, 256), 8192);
   adam_slabs_kernel<<<(unsigned)(blocks + std::max(dense, 1)), 256, 0, st>>>(
-      p, g, m, v, s, c, planes, pstride, psc);
+      p, g, m, v, s, c, planes, pstride, psc, dev_steps, gate);
   ACME_LAUNCH_CHECK();
   return ACME_OK;
 }
@@ -1356,13 +1482,22 @@ int launch_param_amax(const float* x, int64_t n, gemm::PScale* sc, hipStream_t s
 }
 
 int launch_plane_rescale(gemm::PScale* recs, int n_transient, int n, int copy_from, int copy_to,
-                         int* overflow, hipStream_t st, int skip_lo, int skip_hi) {
+                         int* overflow, hipStream_t st, int skip_lo, int skip_hi,
+                         const RescaleGuard& rg) {
   ACME_CHECK_ARG(recs && overflow && n >= 1 && n <= 15 && n_transient >= 0 && n_transient <= n,
                  "bad rescale arguments");
   ACME_CHECK_ARG(copy_to < 0 || (copy_to >= n && copy_from >= 0 && copy_from < n),
                  "bad rescale copy");
   plane_rescale_kernel<<<1, (unsigned)(64 * (n + 1)), 0, st>>>(recs, n_transient, n, copy_from,
-                                                               copy_to, overflow, skip_lo, skip_hi);
+                                                               copy_to, overflow, skip_lo, skip_hi,
+                                                               rg);
+  ACME_LAUNCH_CHECK();
+  return ACME_OK;
+}
+
+int launch_gate_publish(const Gate& gate, float* dst, hipStream_t st) {
+  ACME_CHECK_ARG(gate.g && dst, "null argument");
+  gate_publish_kernel<<<1, 1, 0, st>>>(gate, dst);
   ACME_LAUNCH_CHECK();
   return ACME_OK;
 }

@@ -31,6 +31,7 @@
 
 #include "common.h"
 #include "detmath.h"
+#include "kernels.h"
 #include "profiler.h"
 
 using namespace acme;
@@ -94,6 +95,10 @@ struct acme_replay {
   } readers[kMaxReaders] = {};
   int nreaders = 0;
   std::mutex order_mu;
+  // Gather kernel variants fixed at creation (tests compare them bit for bit): ACME_V_GATH
+  // 0 = transition pair / pieces (default), 1 = row per workgroup, 2 = wave pieces;
+  // ACME_V_GATHG: the pieces grid cap; ACME_V_SGF=1: sample_gather as two launches.
+  int gath = 0, gathg = 0, sgf = 0;
 };
 
 namespace {
@@ -550,9 +555,10 @@ __global__ void prio_write_kernel(const double* __restrict__ prios, int64_t n,
                                   const int64_t* __restrict__ slots,
                                   const int32_t* __restrict__ valid,
                                   const int32_t* __restrict__ winner, double alpha,
-                                  double* __restrict__ raw_prio, double* __restrict__ leaves) {
+                                  double* __restrict__ raw_prio, double* __restrict__ leaves,
+                                  const Gate gate) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n || !valid[j]) return;
+  if (j >= n || !valid[j] || gate_skip(gate)) return;
   const int64_t slot = slots[j];
   if (winner[slot] != (int32_t)j) return;
   const double p = prios[j];
@@ -590,11 +596,13 @@ struct FusedUpdateArgs {
   double* raw_prio;
   double* level[8];
   int nlevels;
+  Gate gate;  // a learner step that was skipped writes no priority
 };
 __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs a) {
   __shared__ int s_j[kFusedUpdateMax];
   __shared__ int64_t s_slot[kFusedUpdateMax];
   __shared__ int s_len;
+  if (gate_skip(a.gate)) return;
   const int tid = threadIdx.x, nt = blockDim.x;
   const int lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
   const int G = gridDim.x, bid = blockIdx.x;
@@ -1042,6 +1050,9 @@ int acme_replay_create(const acme_replay_config* cfg, acme_replay** out) {
 
   acme_replay* r = new acme_replay();
   r->cfg = *cfg;
+  r->gath = tune_variant("GATH");
+  r->gathg = tune_variant("GATHG");
+  r->sgf = tune_variant("SGF");
   // Level sizes.
   int64_t s = ceil_div(cfg->capacity, 64) * 64;
   r->level_size[0] = s;
@@ -1464,7 +1475,7 @@ static int sample_gather_impl(acme_replay* r, int64_t batch, uint64_t step_count
   ACME_CHECK_ARG(!frames_f16 || (pair && reinterpret_cast<uintptr_t>(frames_f16) % 16 == 0),
                  "a bf16 frame copy needs the transition layout (two equal big fields) and a "
                  "16-byte aligned buffer");
-  if (frames_f16 || (tune_variant("SGF") != 1 && tune_variant("GATH") == 0 && pair)) {
+  if (frames_f16 || (r->sgf != 1 && r->gath == 0 && pair)) {
     hipStream_t st = as_stream(stream);
     int64_t size = 0;
     int rc = order_after_inserts(r, st, &size);
@@ -1502,7 +1513,7 @@ static int sample_gather_impl(acme_replay* r, int64_t batch, uint64_t step_count
     ACME_LAUNCH_CHECK();
     return ACME_OK;
   }
-  if (!pair && tune_variant("SGF") != 1 && tune_variant("GATH") == 0 &&
+  if (!pair && r->sgf != 1 && r->gath == 0 &&
       small_layout(r, out_fields, &sm)) {
     hipStream_t st = as_stream(stream);
     int64_t size = 0;
@@ -1556,7 +1567,7 @@ int acme_replay_gather(acme_replay* r, const int64_t* slots, int64_t batch,
   ACME_PROF("replay_gather", st, 0.0, 2.0 * row_bytes * (double)batch + 8.0 * (double)batch);
   // Pieces path: every field a multiple of 4 B (always: acme_replay_create checks it) and
   // 16-B aligned rows and buffers for the big fields.
-  bool pieces = tune_variant("GATH") != 1;
+  bool pieces = r->gath != 1;
   PieceArgs pa = {};
   int64_t total = 0;
   for (int f = 0; f < r->cfg.num_fields && pieces; ++f) {
@@ -1570,7 +1581,7 @@ int acme_replay_gather(acme_replay* r, const int64_t* slots, int64_t batch,
     pa.nbig++;
   }
   pieces = pieces && total < (int64_t(1) << 30) && pa.nbig > 0;
-  const int gv = tune_variant("GATH");
+  const int gv = r->gath;
   // Transition layout: exactly two big fields of equal bytes, the rest small.
   if (pieces && pa.nbig == 2 && r->cfg.field_bytes[pa.big[0]] == r->cfg.field_bytes[pa.big[1]] &&
       gv == 0) {
@@ -1611,7 +1622,7 @@ int acme_replay_gather(acme_replay* r, const int64_t* slots, int64_t batch,
       if (r->cfg.field_bytes[f] < 1024) pa.big[pa.nbig + pa.nsmall++] = f;
     }
     constexpr int K = 8;
-    const int gcap = tune_variant("GATHG") > 0 ? tune_variant("GATHG") : 2048;
+    const int gcap = r->gathg > 0 ? r->gathg : 2048;
     const int64_t waves = std::max(ceil_div(total, K), (int64_t)pa.nsmall * ceil_div(batch, 64));
     const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(waves, 4), gcap));
     gather_pieces_kernel<K><<<grid, 256, 0, st>>>(pa, slots, (int32_t)batch);
@@ -1644,12 +1655,14 @@ int acme_replay_sample_gather_frames(acme_replay* r, int64_t batch, uint64_t ste
                             priorities, out_fields, stream, frames_f16);
 }
 
-int acme_replay_update_priorities(acme_replay* r, const uint64_t* keys, const double* prios,
-                                  int64_t n, void* stream) {
+}  // extern "C"
+
+int acme::replay_update_priorities_gated(acme_replay* r, const uint64_t* keys,
+                                         const double* prios, int64_t n, const Gate& gate,
+                                         hipStream_t st) {
   ACME_CHECK_ARG(r && (n == 0 || (keys && prios)), "null argument");
   ACME_CHECK_ARG(n >= 0 && n < (int64_t(1) << 31), "bad update count");
   if (n == 0) return ACME_OK;
-  hipStream_t st = as_stream(stream);
   std::lock_guard<std::mutex> lock(r->mu);
   int rc = order_after_inserts(r, st);
   if (rc != ACME_OK) return rc;
@@ -1670,10 +1683,11 @@ int acme_replay_update_priorities(acme_replay* r, const uint64_t* keys, const do
   const double alpha =
       r->cfg.sampler == ACME_SAMPLER_PRIORITIZED ? r->cfg.priority_exponent : 0.0;
   ACME_PROF("replay_update", st, 0.0, (double)n * (16.0 + 8.0 * 3 + 512.0 * (r->nlevels - 1)));
-  if (n <= kFusedUpdateMax && tune_variant("UPD") != 1) {
+  if (n <= kFusedUpdateMax) {
     FusedUpdateArgs a;
     a.upd_keys = keys; a.prios = prios; a.n = (int)n; a.capacity = r->cfg.capacity;
     a.keys = r->keys; a.alpha = alpha; a.raw_prio = r->raw_prio; a.nlevels = r->nlevels;
+    a.gate = gate;
     for (int l = 0; l < 8; ++l) a.level[l] = r->levels[l];
     prio_update_fused_kernel<<<kFusedUpdateBlocks, 256, 0, st>>>(a);
     ACME_LAUNCH_CHECK();
@@ -1690,7 +1704,7 @@ int acme_replay_update_priorities(acme_replay* r, const uint64_t* keys, const do
                                          r->winner);
   ACME_LAUNCH_CHECK();
   prio_write_kernel<<<g, 256, 0, st>>>(prios, n, t_slots, t_valid, r->winner, alpha,
-                                       r->raw_prio, r->levels[0]);
+                                       r->raw_prio, r->levels[0], gate);
   ACME_LAUNCH_CHECK();
   for (int l = 1; l < r->nlevels; ++l) {
     level_update_kernel<<<(unsigned)ceil_div(n, 4), 256, 0, st>>>(
@@ -1700,6 +1714,26 @@ int acme_replay_update_priorities(acme_replay* r, const uint64_t* keys, const do
   prio_reset_kernel<<<g, 256, 0, st>>>(t_slots, t_valid, n, r->winner);
   ACME_LAUNCH_CHECK();
   return ACME_OK;
+}
+
+extern "C" {
+
+int acme_replay_update_priorities(acme_replay* r, const uint64_t* keys, const double* prios,
+                                  int64_t n, void* stream) {
+  return replay_update_priorities_gated(r, keys, prios, n, Gate{}, as_stream(stream));
+}
+
+int acme_replay_update_priorities_gated(acme_replay* r, const uint64_t* keys, const double* prios,
+                                        int64_t n, const uint32_t* skip_word, void* stream) {
+  // skip_word (a learner's acme_dqn_skip_word): the update is dropped when it is non-zero on
+  // the device when the update runs.
+  Gate q;
+  if (skip_word) {
+    q.g = reinterpret_cast<const StepGuard*>(reinterpret_cast<const char*>(skip_word) -
+                                             offsetof(StepGuard, last));
+    q.use_last = 1;
+  }
+  return replay_update_priorities_gated(r, keys, prios, n, q, as_stream(stream));
 }
 
 }  // extern "C"

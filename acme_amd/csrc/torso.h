@@ -100,6 +100,9 @@ struct Side {
   // step's priority write-back, which balances the two streams' backward).
   int (*tail)(void* ctx, hipStream_t st) = nullptr;
   void* tail_ctx = nullptr;
+  // conv1's weight gradient on the single-role kernel instead of the producer / consumer one
+  // (the same bits; tests, ACME_V_WSN=1 at the learner's creation).
+  bool single_role = false;
 };
 // dz3: conv3's dZ planes [rows][kFlat] (masked); dz2 / dz1 plane scratch.
 int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int rows,

@@ -273,28 +273,16 @@ int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int row
   int rc;
   // Weight gradients of conv3 and conv2 go to the side stream (when given): each only
   // waits for its layer's dZ, and runs beside the next input gradient on the main stream
-  // (two forks; one fork after conv3_dgrad saved an event record but measured 0.754 ->
-  // 0.767 ms per step: the lost overlap costs more).
+  // (two forks; one fork after conv3_dgrad for both saved an event record but measured
+  // 0.754 -> 0.767 ms per step: the lost overlap costs more).
   const bool fork = sd.side != nullptr;
   const bool defer = sd.defer != nullptr;
   if (defer && !(sd.slab && sd.slab2))
     return (set_error("deferred weight gradients need two side slabs"), ACME_ERR_INVALID);
   hipStream_t st = fork ? sd.side : st_main;
   float* wslab = fork || defer ? sd.slab : slab;
-  // ACME_V_TFORK=1: one fork after conv3's input gradient for both weight gradients (one
-  // event record fewer on the main stream).
-  const bool one_fork = fork && tune_variant("TFORK") == 1;
-  if (one_fork) {
-    P3ConvDgrad<G3> p;
-    p.M = rows * G3::IPIX; p.N = G3::CI; p.K = G3::KH * G3::KW * G3::CO; p.k_chunk = p.K;
-    p.a_src = src(dz3, (int64_t)rows * kFlat); p.b_src = src(w.w3, G3::K * G3::CO);
-    p.xprev = cp(a.x2); p.dx = pl(dz2);
-    P3I_GEMM("conv3_dgrad", I3D, 2, 64, 8, 2, 1, p, rows);
-    ACME_HIP_TRY(hipEventRecord(sd.e[1], st_main));
-    ACME_HIP_TRY(hipStreamWaitEvent(sd.side, sd.e[1], 0));
-  }
   {  // conv3 weight + bias gradient
-    if (fork && !one_fork) {
+    if (fork) {
       ACME_HIP_TRY(hipEventRecord(sd.e[0], st_main));
       ACME_HIP_TRY(hipStreamWaitEvent(sd.side, sd.e[0], 0));
     }
@@ -310,7 +298,7 @@ int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int row
       return rc;
   }
   st = st_main;
-  if (!one_fork) {
+  {
     P3ConvDgrad<G3> p;
     p.M = rows * G3::IPIX; p.N = G3::CI; p.K = G3::KH * G3::KW * G3::CO; p.k_chunk = p.K;
     p.a_src = src(dz3, (int64_t)rows * kFlat); p.b_src = src(w.w3, G3::K * G3::CO);
@@ -319,10 +307,8 @@ int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int row
     P3I_GEMM("conv3_dgrad", I3D, 2, 64, 8, 2, 1, p, rows);
   }
   if (fork) {
-    if (!one_fork) {
-      ACME_HIP_TRY(hipEventRecord(sd.e[1], st_main));
-      ACME_HIP_TRY(hipStreamWaitEvent(sd.side, sd.e[1], 0));
-    }
+    ACME_HIP_TRY(hipEventRecord(sd.e[1], st_main));
+    ACME_HIP_TRY(hipStreamWaitEvent(sd.side, sd.e[1], 0));
     st = sd.side;
   }
   {  // conv2
@@ -361,7 +347,7 @@ int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int row
     p.a_src = frames_src(frames, rows); p.b_src = src(dz1, (int64_t)rows * kX1);
     p.slab = slab;
     // Producer / consumer waves (gemm_p3ws_kernel): 28.5 -> 25.0 us, the same bits.
-    if (tune_variant("WSN") == 1) P3_GEMM("conv1_wgrad", 256, 32, 4, 1, 32, p, splits);
+    if (sd.single_role) P3_GEMM("conv1_wgrad", 256, 32, 4, 1, 32, p, splits);
     else P3WS_GEMM("conv1_wgrad", 256, 32, 4, 1, p, splits);
     if (defer) sd.defer[0] = WgradSlab{slab, splits, (int64_t)p.M * p.N, p.N};
     else if ((rc = p3_wgrad_reduce(p, splits, slab, g.w1, g.b1, "conv1_wgrad_reduce", st)))

@@ -156,9 +156,17 @@ class NativeReplay:
         check(lib().acme_replay_gather(self._h, ptr(slots), int(slots.numel()), ptrs,
                                        stream_ptr(stream)), "replay gather")
 
-    def update_priorities(self, keys: torch.Tensor, priorities: torch.Tensor, stream=None) -> None:
+    def update_priorities(self, keys: torch.Tensor, priorities: torch.Tensor, stream=None,
+                          skip_word: Optional[int] = None) -> None:
+        """skip_word: a learner's device skip word (NativeDQN.skip_word): the update is
+        dropped when the step that produced the priorities was skipped."""
         keys = keys.to(self.device, torch.uint64).contiguous()
         priorities = priorities.to(self.device, torch.float64).contiguous()
+        if skip_word:
+            check(lib().acme_replay_update_priorities_gated(
+                self._h, ptr(keys), ptr(priorities), int(keys.numel()), ctypes.c_void_p(skip_word),
+                stream_ptr(stream)), "update_priorities")
+            return
         check(lib().acme_replay_update_priorities(self._h, ptr(keys), ptr(priorities),
                                                   int(keys.numel()), stream_ptr(stream)),
               "update_priorities")
@@ -426,6 +434,38 @@ class NativeDQN:
         v = ctypes.c_int32(0)
         check(lib().acme_dqn_plane_overflow(self._h, ctypes.byref(v), int(reset)), "dqn plane_overflow")
         return bool(v.value)
+
+    # ---- step guard (acme_dqn_guard_state: the skip-on-overflow rule of the plane path)
+    @property
+    def skipped_steps(self) -> int:
+        """Steps skipped so far among those the device has finished (no synchronisation)."""
+        return int(lib().acme_dqn_skipped_steps(self._h))
+
+    def guard_state(self) -> Dict[str, int]:
+        """{applied, skipped, last_skipped, q_values_overflowed} (synchronises the device)."""
+        a = (ctypes.c_int64 * 4)()
+        check(lib().acme_dqn_guard_state(self._h, a), "dqn guard_state")
+        return dict(applied=int(a[0]), skipped=int(a[1]), last_skipped=int(a[2]),
+                    q_values_overflowed=int(a[3]))
+
+    @property
+    def applied_steps(self) -> int:
+        """Updates applied (Adam's t after the last step); synchronises."""
+        return self.guard_state()["applied"]
+
+    @applied_steps.setter
+    def applied_steps(self, n: int) -> None:
+        check(lib().acme_dqn_set_applied_steps(self._h, int(n)), "dqn set_applied_steps")
+
+    @property
+    def skip_word(self) -> Optional[int]:
+        """Device address of the word an after-step priority update is gated on."""
+        p = ctypes.c_void_p()
+        check(lib().acme_dqn_skip_word(self._h, ctypes.byref(p)), "dqn skip_word")
+        return p.value
+
+    def set_data_parallel_gate(self, enable: bool) -> None:
+        check(lib().acme_dqn_set_data_parallel_gate(self._h, 1 if enable else 0), "dqn dp gate")
 
     def get_params(self, which: str = "params") -> Dict[str, np.ndarray]:
         flat = getattr(self, which)
@@ -826,6 +866,42 @@ class NativeIMPALA:
         check(lib().acme_impala_plane_overflow(self._h, ctypes.byref(v), int(reset)),
               "impala plane_overflow")
         return bool(v.value)
+
+    @property
+    def skipped_steps(self) -> int:
+        """Steps skipped (plane overflow or LSTM timeout) among those the device finished."""
+        return int(lib().acme_impala_skipped_steps(self._h))
+
+    def guard_state(self) -> Dict[str, int]:
+        """{applied, skipped, last_skipped, lstm_timeouts} (synchronises the device)."""
+        a = (ctypes.c_int64 * 4)()
+        check(lib().acme_impala_guard_state(self._h, a), "impala guard_state")
+        return dict(applied=int(a[0]), skipped=int(a[1]), last_skipped=int(a[2]),
+                    lstm_timeouts=int(a[3]))
+
+    @property
+    def applied_steps(self) -> int:
+        return self.guard_state()["applied"]
+
+    @applied_steps.setter
+    def applied_steps(self, n: int) -> None:
+        check(lib().acme_impala_set_applied_steps(self._h, int(n)), "impala set_applied_steps")
+
+    def scale_state(self) -> np.ndarray:
+        """The plane scales (learner state for checkpoints; empty without the plane path)."""
+        n = ctypes.c_int32(0)
+        check(lib().acme_impala_scale_state(self._h, None, 0, ctypes.byref(n)), "impala scales")
+        out = np.zeros(n.value, np.float32)
+        if n.value:
+            check(lib().acme_impala_scale_state(self._h, out.ctypes.data, n.value,
+                                                ctypes.byref(n)), "impala scales")
+        return out
+
+    def set_scale_state(self, state) -> None:
+        a = np.ascontiguousarray(np.asarray(state, np.float32))
+        if a.size:
+            check(lib().acme_impala_set_scale_state(self._h, a.ctypes.data, a.size),
+                  "impala set_scale_state")
 
     def set_lstm_unroll(self, per_step: bool) -> None:
         """Per-step LSTM launches instead of the one-launch unroll (tests compare the two)."""

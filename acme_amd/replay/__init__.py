@@ -274,14 +274,31 @@ class Table:
             self._native.insert([p[:n] for p in self._pend], self._pend_prio[:n])
             self._fill = 0
 
+    # Pending rows older than this are committed by the next draw (bounded staleness).
+    max_pending_seconds = 0.1
+
     def flush_for_sampling(self, batch_size: int) -> None:
-        """A reader's flush: commits pending rows only when the device table could not serve
-        the draw without them (it holds fewer than the batch or MinSize).  Otherwise rows
-        become visible when their writer's buffer fills or the writer closes, as Reverb
-        chunks do, so the learner's thread never packs or issues the actors' inserts."""
+        """A reader's flush: commits pending rows when the device table could not serve the
+        draw without them (it holds fewer than the batch or MinSize), or when rows have been
+        pending for longer than max_pending_seconds (a slow writer's rows become sampleable
+        within that bound).  Otherwise rows become visible when their writer's buffer fills
+        or the writer closes, as Reverb chunks do, so the learner's thread does not pack or
+        issue the actors' inserts in the steady state."""
         with self._mu:
             if self.committed_size() < max(batch_size, self._min_size, 1):
                 self.flush()
+                self._pending_since = None
+                return
+            if not (self._fill or any(w.pending() for w in self._writers)):
+                self._pending_since = None
+                return
+            now = time.monotonic()
+            since = getattr(self, "_pending_since", None)
+            if since is None:
+                self._pending_since = now
+            elif now - since > self.max_pending_seconds:
+                self.flush()
+                self._pending_since = None
 
     # -- checkpointing (optional replay state; core.Saveable interface)
     def save(self) -> Dict[str, Any]:
@@ -346,7 +363,9 @@ class Table:
                 after = ev.handle if hasattr(ev, "handle") else int(ev.cuda_event)
             return self._native.handle, k, after
 
-    def update_priorities(self, keys, priorities) -> None:
+    def update_priorities(self, keys, priorities, skip_word=None) -> None:
+        """skip_word (extension): a learner's device skip word; the update is dropped when
+        the step that produced the priorities was skipped (NativeDQN.skip_word)."""
         import torch
         with self._mu:
             # Pending rows hold no keys yet: nothing to flush for an update.
@@ -357,7 +376,7 @@ class Table:
             p = priorities if isinstance(priorities, torch.Tensor) else torch.as_tensor(
                 np.asarray(priorities, np.float64))
             self._after_readers()
-            self._native.update_priorities(k, p)
+            self._native.update_priorities(k, p, skip_word=skip_word)
 
 
 from acme_amd.replay.frame_table import _make_frame_table  # noqa: E402
@@ -467,7 +486,7 @@ class QueueTable(Table):
         raise NotImplementedError(f"queue table '{self.name}' is not checkpointable "
                                   f"(its items are consumed once; checkpoint the learner)")
 
-    def update_priorities(self, keys, priorities) -> None:
+    def update_priorities(self, keys, priorities, skip_word=None) -> None:
         pass  # queue items carry no priorities (Reverb ignores updates of consumed items)
 
     def prepare_priority_update(self, keys):
@@ -577,9 +596,13 @@ class Client:
         prep = getattr(t, "prepare_priority_update", None)
         return prep(keys) if prep is not None else None
 
-    def update_priorities(self, table: str, keys, priorities):
-        """TFClient.update_priorities: device or host keys (u64) / priorities (f64)."""
-        self._server.tables[table].update_priorities(keys, priorities)
+    def update_priorities(self, table: str, keys, priorities, skip_word=None):
+        """TFClient.update_priorities: device or host keys (u64) / priorities (f64).
+        skip_word (extension): see Table.update_priorities."""
+        if skip_word is None:
+            self._server.tables[table].update_priorities(keys, priorities)
+        else:
+            self._server.tables[table].update_priorities(keys, priorities, skip_word=skip_word)
 
     def mutate_priorities(self, table: str, updates: Optional[Dict[int, float]] = None,
                           deletes: Optional[Sequence[int]] = None):

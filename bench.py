@@ -99,8 +99,9 @@ def cpu_baseline(batch: int, num_actions: int, seconds: float):
     timed on the host cores: all of them (torch.set_num_threads), then one thread.  The
     frames of the 1M slots would be 56 GB of host memory, so slot s reads frame pair
     s mod 16,384 of a host pool (the tree, draws and priorities are the full 1M-slot ones).
-    Bounded sample: as many steps as fit in `seconds` for all threads (at least 2 after one
-    warm-up step) and in `seconds` / 2 for one thread (at least 1)."""
+    Sample: at least 200 timed steps with all threads, more if `seconds`
+    allows, after one warm-up step; one thread: a bounded sample of `seconds` / 2 (at least
+    1 step)."""
     from oracle.dqn_torch import TorchDQN
     from tests._oracle import OracleTable
     from acme_amd.networks import DQNAtariNetwork
@@ -138,7 +139,7 @@ def cpu_baseline(batch: int, num_actions: int, seconds: float):
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or cores
     prev = torch.get_num_threads()
     try:
-        v_all, n_all = timed(threads, seconds, 2)
+        v_all, n_all = timed(threads, seconds, 200)
         v_one, n_one = timed(1, seconds / 2, 1)
     finally:
         torch.set_num_threads(prev)
@@ -227,7 +228,10 @@ def setup_dqn(args, world, rank, dev):
                          logger=loggers.NoOpLogger(), seed=0, device=dev,
                          reduce_logged_loss=False)
     meta = dict(
-        metric=METRIC, dtype="f32",
+        # The arithmetic: every GEMM operand as two scaled f16 planes (22-23 significant
+        # bits, per-tensor power-of-two scale), three MFMA terms per product, f32
+        # accumulation (csrc/gemm_p3.h); f32 everywhere else.
+        metric=METRIC, dtype="f32 (2xf16 split planes, 3 MFMA terms)",
         data="synthetic (device-generated uint8 Atari-shape transitions, random-init "
              "Nature-CNN weights)",
         config={"workload": "dqn_nature_cnn_prioritized_replay (BASELINE configs[1])",
@@ -491,7 +495,11 @@ def setup_impala(args, world, rank, dev):
 
     meta = dict(
         metric="learner frames/sec (B=16 sequences x T=20) IMPALA Atari, 1 MI355X",
-        unit="frames/s", dtype="f32",
+        unit="frames/s", dtype="f32 (torso and W_i: 2xf16 split planes, 3 MFMA terms)",
+        # The one-launch LSTM unroll is a sequential latency chain, not an MFMA roofline: it
+        # is reported per timestep against a kernel boundary (below), and the roofline
+        # object names the dominant MFMA kernel among the others.
+        _roofline_exclude=("impala_lstm_fwd", "impala_lstm_bwd"), _lstm_T=T,
         data="synthetic (device-generated uint8 Atari sequences in a device-resident queue "
              "pool, random-init IMPALAAtariNetwork)",
         config={"workload": "impala_atari_lstm_vtrace (BASELINE configs[3])",
@@ -885,7 +893,8 @@ def main():
     ms_per_step = 1e3 * elapsed / args.steps
     value = world * B * args.steps / elapsed
     roofline = None
-    mfma = [s for s in sections if s.get("bound") == "mfma"]
+    mfma = [s for s in sections if s.get("bound") == "mfma"
+            and s["name"] not in meta.get("_roofline_exclude", ())]
     if mfma:
         dom = mfma[0]
         traffic, src = pmc_traffic(args.workload, dom["name"])
@@ -917,6 +926,17 @@ def main():
             "dp_staged_ms_per_step": None if staged_ms is None else round(staged_ms, 4),
             "kernels": sections,
         }
+        if "_lstm_T" in meta:
+            # The LSTM unroll per timestep (one launch each way) against a dependent kernel
+            # boundary on MI355X (1.45 us between trivial kernels, MI355X_MICROARCH.md
+            # "boundary"), the floor of one launch per timestep before any work.
+            lstm = {s["name"]: s for s in sections if s["name"] in meta["_roofline_exclude"]}
+            T = meta["_lstm_T"]
+            out["lstm"] = {k.replace("impala_", ""): {"us_per_launch": v["avg_us"],
+                                                       "us_per_timestep": round(v["avg_us"] / T, 3)}
+                           for k, v in lstm.items()}
+            out["lstm"]["boundary_us"] = 1.45
+            out["lstm"]["timesteps"] = T
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

@@ -247,6 +247,12 @@ int acme_r2d2_importance_weights(const double* probabilities, int32_t B,
  * applies updates in order). */
 int acme_replay_update_priorities(acme_replay* r, const uint64_t* keys,
                                   const double* priorities, int64_t n, void* stream);
+/* The same behind a learner's skip word (acme_dqn_skip_word, a device word): the update
+ * is dropped when the word is non-zero when the update runs on the device, i.e. when the
+ * learner step that produced the priorities was skipped (plane overflow, below). */
+int acme_replay_update_priorities_gated(acme_replay* r, const uint64_t* keys,
+                                        const double* priorities, int64_t n,
+                                        const uint32_t* skip_word, void* stream);
 
 int64_t acme_replay_size(const acme_replay* r);
 int64_t acme_replay_capacity(const acme_replay* r);
@@ -327,6 +333,28 @@ int acme_dqn_params_changed(acme_dqn* l);
  * maximum grew more than 2^8-fold within one step; the results of that step are then not
  * exact), else 0.  reset != 0 clears the flag. */
 int acme_dqn_plane_overflow(acme_dqn* l, int32_t* overflow, int32_t reset);
+/* Step guard of the plane path (the skip-on-overflow rule of automatic mixed precision):
+ * a step in which some f16 plane write overflowed (a tensor's maximum grew more than about
+ * 2^8-fold since the previous step) changes no parameter, Adam moment, Adam count, target
+ * or replay priority; its end-of-step rescale sets every scale from the step's true maxima,
+ * so the next step runs exactly.  Adam's t counts applied updates (acme_dqn_guard_state
+ * out4[0] + 1); num_steps (the target period) counts step calls.
+ *   acme_dqn_skipped_steps: steps skipped so far among those the device has finished
+ *     (a pinned host word the device writes; no synchronisation).
+ *   acme_dqn_guard_state: synchronises; out4 = {applied, skipped, last step skipped,
+ *     last q_values call overflowed (repeat it: the scales were reset from its maxima)}.
+ *   acme_dqn_set_applied_steps: restore Adam's count (checkpoints).
+ *   acme_dqn_skip_word: the device word acme_replay_update_priorities_gated reads after
+ *     a step (NULL without the plane path).
+ *   acme_dqn_set_data_parallel_gate: the ranks skip together: stage 1 writes this rank's
+ *     decision into a padding word of the torso gradient bucket [0, grad_split), which the
+ *     caller's all-reduce of that bucket combines before acme_dqn_apply (acme_dqn_dp_init
+ *     enables it). */
+int64_t acme_dqn_skipped_steps(const acme_dqn* l);
+int acme_dqn_guard_state(acme_dqn* l, int64_t* out4);
+int acme_dqn_set_applied_steps(acme_dqn* l, int64_t n);
+int acme_dqn_skip_word(const acme_dqn* l, const uint32_t** out);
+int acme_dqn_set_data_parallel_gate(acme_dqn* l, int32_t enable);
 /* The plane scales (powers of two) as learner state for checkpoints: acme_dqn_scale_state
  * writes *count floats to out (when out is non-NULL and capacity suffices);
  * acme_dqn_set_scale_state restores them after acme_dqn_params_changed, so the resumed
@@ -570,6 +598,18 @@ int acme_impala_step(acme_impala* l, const acme_sequence_batch* batch, float* me
                      void* stream);
 /* Plane-range check of the Atari plane path (as acme_dqn_plane_overflow). */
 int acme_impala_plane_overflow(acme_impala* l, int32_t* overflow, int32_t reset);
+/* Step guard (as acme_dqn_guard_state): a step whose plane writes overflowed, or whose
+ * one-launch LSTM unroll timed out, applies no update (Adam's device count stays);
+ * out4 = {applied, skipped, last step skipped, LSTM timeouts so far}.
+ * acme_impala_skipped_steps reads the pinned host mirror (no synchronisation). */
+int64_t acme_impala_skipped_steps(const acme_impala* l);
+int acme_impala_guard_state(acme_impala* l, int64_t* out4);
+/* Adam's device count (checkpoint restore; acme_impala_set_num_steps sets it to n too). */
+int acme_impala_set_applied_steps(acme_impala* l, int64_t n);
+/* Plane scales as learner state (as acme_dqn_scale_state / acme_dqn_set_scale_state): a
+ * resumed run restores them after acme_impala_params_changed instead of recalibrating. */
+int acme_impala_scale_state(const acme_impala* l, float* out, int32_t capacity, int32_t* count);
+int acme_impala_set_scale_state(acme_impala* l, const float* in, int32_t count);
 /* The LSTM unroll of this learner: 0 (default) = one launch each for the forward and the
  * backward when lstm_size = 256 and the batch is at most 64 sequences
  * (workgroups own 4 sequences x 16 units and exchange h / dh partials as tagged granules;

@@ -43,22 +43,29 @@ def huber(x: torch.Tensor, delta: float = 1.0) -> torch.Tensor:
 
 class TorchDQN:
     """Nature-CNN DQN learner state (params, target, Adam m / v, num_steps) as float32
-    torch tensors on the CPU."""
+    torch tensors on the CPU (dtype / device: e.g. a float64 reference trajectory on the
+    GPU for the plane engine's long-horizon test)."""
 
     def __init__(self, params: Dict[str, np.ndarray], num_actions: int, lr: float = 1e-3,
-                 discount: float = 0.99, beta: float = 0.2, period: int = 100):
+                 discount: float = 0.99, beta: float = 0.2, period: int = 100,
+                 target: Dict[str, np.ndarray] = None, dtype=torch.float32, device="cpu"):
         self.A = num_actions
+        self.dtype, self.device = dtype, torch.device(device)
         self.names = [n for n, _ in nature_tensor_shapes(num_actions)]
-        self.p = {k: torch.tensor(np.asarray(params[k], np.float32), requires_grad=True)
+        self.p = {k: torch.tensor(np.asarray(params[k], np.float32), dtype=dtype,
+                                  device=self.device, requires_grad=True)
                   for k in self.names}
         self.t = {k: v.detach().clone() for k, v in self.p.items()}
+        if target is not None:
+            for k in self.names:
+                self.t[k].copy_(torch.as_tensor(np.asarray(target[k], np.float32)))
         self.m = {k: torch.zeros_like(v) for k, v in self.t.items()}
         self.v = {k: torch.zeros_like(v) for k, v in self.t.items()}
         self.lr, self.discount, self.beta, self.period = lr, discount, beta, period
         self.num_steps = 0
 
     def q(self, p, obs_u8: torch.Tensor) -> torch.Tensor:
-        x = (obs_u8.to(torch.float32) / 255.0).permute(0, 3, 1, 2)  # NHWC -> NCHW
+        x = (obs_u8.to(self.device, self.dtype) / 255.0).permute(0, 3, 1, 2)  # NHWC -> NCHW
         for name, k, s in CONVS:
             H = x.shape[-1]
             out, pt, pb = same_pads(H, k, s)
@@ -84,7 +91,7 @@ class TorchDQN:
         target = r + d * q_t_value.gather(1, best[:, None])[:, 0]
         td = target - q_tm1.gather(1, a_tm1.long()[:, None])[:, 0]
         iw = (1.0 / probs) ** self.beta
-        w = torch.from_numpy((iw / iw.max()).astype(np.float32))
+        w = torch.from_numpy((iw / iw.max()).astype(np.float32)).to(self.device, self.dtype)
         loss = (w * huber(td)).mean()
         grads = torch.autograd.grad(loss, [self.p[k] for k in self.names])
         t = self.num_steps + 1
@@ -99,4 +106,4 @@ class TorchDQN:
                 for k in self.names:
                     self.t[k].copy_(self.p[k])
         self.num_steps += 1
-        return float(loss.detach()), td.detach().abs().double().numpy()
+        return float(loss.detach()), td.detach().abs().double().cpu().numpy()

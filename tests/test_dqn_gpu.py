@@ -122,34 +122,33 @@ def test_forward_backward_matches_oracle(netname, B):
 
 
 def test_single_stream_schedule_bitwise():
-    """ACME_V_SIDE=1 (every launch on the caller's stream, the profiling schedule) computes
-    the same step as the default two-stream schedule: the side stream only reorders
-    independent launches, each with its own deterministic split-K scratch."""
+    """ACME_V_SIDE=1 at creation (every launch on the caller's stream, the profiling
+    schedule) computes the same step as the default two-stream schedule: the side stream
+    only reorders independent launches, each with its own deterministic split-K scratch."""
     from acme_amd._lib import lib
     from acme_amd.networks import DQNAtariNetwork
     net = DQNAtariNetwork(18)
     B = 37
     p0, t0 = net.init(3), net.init(4)
     a = _learner(net, B)
-    b = _learner(net, B)
+    lib().acme_tune_set(b"SIDE", 1)  # read once, at the learner's creation
+    try:
+        b = _learner(net, B)
+    finally:
+        lib().acme_tune_set(b"SIDE", 0)
     a.set_params(p0, t0)
     b.set_params(p0, t0)
     rng = np.random.default_rng(8)
-    try:
-        for _ in range(2):
-            dev = _dev(_batch(rng, B, (84, 84, 4), 18))
-            a.step(*dev)
-            lib().acme_tune_set(b"SIDE", 1)
-            b.step(*dev)
-            lib().acme_tune_set(b"SIDE", 0)
-            torch.cuda.synchronize()
-            assert a.loss.item() == b.loss.item()
-            for buf in ("grads", "params", "m", "v"):
-                ga, gb = a.get_params(buf), b.get_params(buf)
-                for k in ga:
-                    np.testing.assert_array_equal(ga[k], gb[k], err_msg=f"{buf}/{k}")
-    finally:
-        lib().acme_tune_set(b"SIDE", 0)
+    for _ in range(2):
+        dev = _dev(_batch(rng, B, (84, 84, 4), 18))
+        a.step(*dev)
+        b.step(*dev)
+        torch.cuda.synchronize()
+        assert a.loss.item() == b.loss.item()
+        for buf in ("grads", "params", "m", "v"):
+            ga, gb = a.get_params(buf), b.get_params(buf)
+            for k in ga:
+                np.testing.assert_array_equal(ga[k], gb[k], err_msg=f"{buf}/{k}")
 
 
 def test_warp_specialised_gemms_bitwise():
@@ -163,27 +162,25 @@ def test_warp_specialised_gemms_bitwise():
     net = DQNAtariNetwork(18)
     for B in (37, 512):
         p0, t0 = net.init(3), net.init(4)
-        a = _learner(net, B)
+        lib().acme_tune_set(b"WSN", 1)  # read once, at the learner's creation
+        try:
+            a = _learner(net, B)
+        finally:
+            lib().acme_tune_set(b"WSN", 0)
         b = _learner(net, B)
         a.set_params(p0, t0)
         b.set_params(p0, t0)
         rng = np.random.default_rng(B)
-        try:
-            for _ in range(2):
-                dev = _dev(_batch(rng, B, (84, 84, 4), 18))
-                lib().acme_tune_set(b"WSN", 1)
-                a.step(*dev)
-                lib().acme_tune_set(b"WSN", 0)
-                b.step(*dev)
-                lib().acme_tune_set(b"WSN", 0)
-                torch.cuda.synchronize()
-                assert a.loss.item() == b.loss.item(), B
-                for buf in ("grads", "params", "m", "v"):
-                    ga, gb = a.get_params(buf), b.get_params(buf)
-                    for k in ga:
-                        np.testing.assert_array_equal(ga[k], gb[k], err_msg=f"B={B} {buf}/{k}")
-        finally:
-            lib().acme_tune_set(b"WSN", 0)
+        for _ in range(2):
+            dev = _dev(_batch(rng, B, (84, 84, 4), 18))
+            a.step(*dev)
+            b.step(*dev)
+            torch.cuda.synchronize()
+            assert a.loss.item() == b.loss.item(), B
+            for buf in ("grads", "params", "m", "v"):
+                ga, gb = a.get_params(buf), b.get_params(buf)
+                for k in ga:
+                    np.testing.assert_array_equal(ga[k], gb[k], err_msg=f"B={B} {buf}/{k}")
 
 
 def test_adam_and_target_copy_cadence():

@@ -154,15 +154,15 @@ def test_atari_torso_step_matches_oracle(B, T, f32):
     engine (the DQN kernels); f32: the f32 engine throughout (ACME_V_IMP3=1)."""
     from acme_amd._lib import lib
     cfg = O.IMPALAConfig(num_actions=18, torso="atari", entropy_cost=0.01, baseline_cost=0.5)
-    n = _native(cfg, B, T)
+    lib().acme_tune_set(b"IMP3", 1 if f32 else 0)  # read once, at the learner's creation
+    try:
+        n = _native(cfg, B, T)
+    finally:
+        lib().acme_tune_set(b"IMP3", 0)
     params = _params(cfg, 3)
     n.set_params(params)
     b = _batch(cfg, B, T, 4)
-    lib().acme_tune_set(b"IMP3", 1 if f32 else 0)
-    try:
-        _run(n, b)
-    finally:
-        lib().acme_tune_set(b"IMP3", 0)
+    _run(n, b)
     _compare(cfg, n, params, b)
 
 

@@ -219,19 +219,20 @@ def test_gather_kernels_bit_identical(fields):
     rng = np.random.default_rng(len(fields) * 31 + fields[0])
     cap, n, B = 700, 900, 333
     data = [rng.integers(0, 256, (n, b), dtype=np.uint8) for b in fields]
-    r = _native(cap, fields, True)
-    r.insert(data, rng.uniform(0.1, 2.0, n))
-    s = r.sample(B, 4)
-    keys = s["keys"].cpu().numpy().view(np.int64)
+    pr = rng.uniform(0.1, 2.0, n)
     outs = {}
     for gv in (0, 1, 2):
-        lib().acme_tune_set(b"GATH", gv)
+        lib().acme_tune_set(b"GATH", gv)  # read once, at the table's creation
         try:
-            o = [torch.full((B, b), 7, dtype=torch.uint8, device="cuda") for b in fields]
-            r.gather(s["slots"], o)
-            outs[gv] = [x.cpu().numpy() for x in o]
+            r = _native(cap, fields, True)
         finally:
             lib().acme_tune_set(b"GATH", 0)
+        r.insert(data, pr)
+        s = r.sample(B, 4)
+        keys = s["keys"].cpu().numpy().view(np.int64)
+        o = [torch.full((B, b), 7, dtype=torch.uint8, device="cuda") for b in fields]
+        r.gather(s["slots"], o)
+        outs[gv] = [x.cpu().numpy() for x in o]
     for f, b in enumerate(fields):
         np.testing.assert_array_equal(outs[0][f], data[f][keys])
         np.testing.assert_array_equal(outs[1][f], outs[0][f])
@@ -251,26 +252,26 @@ def test_fused_sample_gather_matches_two_launches(prioritized, fields):
     cap, n, B = 3000, 3500, 257
     data = [rng.integers(0, 256, (n, b), dtype=np.uint8) for b in fields]
     pr = rng.uniform(0.0, 2.0, n)
-    r = _native(cap, fields, prioritized)
-    r.insert(data, pr)
     o = OracleTable(cap, prioritized, 0.6, 1234)
     o.insert(pr)
     L = lib()
     res = {}
     for sgf in (0, 1):
-        L.acme_tune_set(b"SGF", sgf)
+        L.acme_tune_set(b"SGF", sgf)  # read once, at the table's creation
         try:
-            info = r.alloc_sample_info(B)
-            outs = [torch.zeros(B, b, dtype=torch.uint8, device="cuda") for b in fields]
-            ptrs = (ctypes.c_void_p * len(outs))(*[x.data_ptr() for x in outs])
-            raw = [info[k].data_ptr() for k in ("slots", "keys", "probabilities", "table_size",
-                                                  "priorities")]
-            assert L.acme_replay_sample_gather(r.handle, B, 77, *raw, ptrs, None) == 0
-            torch.cuda.synchronize()
-            res[sgf] = ({k: v.cpu().numpy() for k, v in info.items()},
-                        [x.cpu().numpy() for x in outs])
+            r = _native(cap, fields, prioritized)
         finally:
             L.acme_tune_set(b"SGF", 0)
+        r.insert(data, pr)
+        info = r.alloc_sample_info(B)
+        outs = [torch.zeros(B, b, dtype=torch.uint8, device="cuda") for b in fields]
+        ptrs = (ctypes.c_void_p * len(outs))(*[x.data_ptr() for x in outs])
+        raw = [info[k].data_ptr() for k in ("slots", "keys", "probabilities", "table_size",
+                                              "priorities")]
+        assert L.acme_replay_sample_gather(r.handle, B, 77, *raw, ptrs, None) == 0
+        torch.cuda.synchronize()
+        res[sgf] = ({k: v.cpu().numpy() for k, v in info.items()},
+                    [x.cpu().numpy() for x in outs])
     ref = o.sample(B, 77)
     for k in ("slots", "probabilities", "table_size", "priorities"):
         np.testing.assert_array_equal(res[0][0][k], ref[k])
