@@ -24,6 +24,7 @@
 
 #include "common.h"
 #include "conv.h"
+#include "rescale.h"
 #include "conv_p3.h"
 #include "gemm.h"
 #include "gemm_p3.h"
@@ -131,6 +132,12 @@ struct acme_dqn {
   // by the backward; forward_backward_stage leaves its arguments here.
   LossArgs pending_la{};
   bool loss_pending = false;
+  // The online forward left its duelling head (the fc split-K slab's reduction, hid, q_on) to
+  // the loss launch (launch_dqn_head_loss_dz, head_splits splits); loss_nparts: the loss
+  // partials the launch writes.
+  bool head_deferred = false;
+  int head_splits = 0;
+  int64_t loss_nparts = 0;
   // The dense layers' gradients (grads[grad_split:]) of the last stage 3 / 4 are complete
   // at dense_ev: the side stream's event when their launches ran there, else ev_dense,
   // recorded on the caller's stream.
@@ -150,6 +157,7 @@ struct acme_dqn {
   // (ACME_V_WSN=1).
   bool single_stream = false;
   bool single_role = false;
+  bool head_separate = false;  // ACME_V_HEADSEP=1: the online head as its own launch (tests)
   // Step guard (kernels.h StepGuard): the skip-on-overflow rule of the plane engine, Adam's
   // device step count (applied updates) on every path.  seq counts the steps issued (the
   // target forward's flag slot is seq & 1); host_skipped is a pinned mirror of the skipped
@@ -161,7 +169,9 @@ struct acme_dqn {
   // torso gradient bucket (stage 1 publishes the local one; the all-reduce combines them).
   bool dp_gate = false;
   int64_t dp_gate_index = -1;
-  bool param_rescale_pending = false;  // the parameter record's write scale moved last step
+  // The step's transient rescale ran inside the priority write-back's launch (deferred read
+  // scales, committed by Adam): apply_impl launches none of its own.
+  bool step_rescaled = false;
 };
 
 namespace {
@@ -350,7 +360,8 @@ int slab_reduce(const float* slab, int splits, int64_t count, float* out0, int64
 // snt.Adam over the flat range [off, off + n) (tensor-aligned): the parameter planes (plane
 // path) are refreshed by the same pass.  t = num_steps + 1 (snt.Adam / optix.adam count this
 // step first).  Every element's update is independent, so ranges compose bit-exactly.
-int adam_range(acme_dqn* l, int64_t off, int64_t n, const Gate& gate, hipStream_t st) {
+int adam_range(acme_dqn* l, int64_t off, int64_t n, const Gate& gate, const AdamTail& tail,
+               hipStream_t st) {
   const bool jax = l->cfg.semantics == ACME_SEMANTICS_JAX;
   // Plane path: the step's gate and count from the rescale before Adam; otherwise no gate
   // (f32 tensors cannot overflow) and a one-thread count after Adam.
@@ -358,7 +369,7 @@ int adam_range(acme_dqn* l, int64_t off, int64_t n, const Gate& gate, hipStream_
   return launch_adam(l->params + off, l->grads + off, l->m + off, l->v + off, n,
                      l->cfg.learning_rate, l->cfg.adam_beta1, l->cfg.adam_beta2,
                      l->cfg.adam_epsilon, 0, p3 ? l->wpl + off : nullptr, l->flat, st, jax ? 1 : 0,
-                     &l->guard->applied, p3 ? l->scales + kScParams : nullptr, gate, !p3);
+                     &l->guard->applied, p3 ? l->scales + kScParams : nullptr, gate, !p3, tail);
 }
 
 torso::Weights torso_weights(const acme_dqn* l, const float* prm) {
@@ -410,7 +421,7 @@ int nature_forward(acme_dqn* l, const float* prm, const void* obs_a, const void*
 int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const torso::Frames& frames,
                       int rows, const torso::Plane& x1, const torso::Plane& x2,
                       const torso::Plane& x3, float* hid, float* q, hipStream_t st,
-                      float* slab = nullptr, int keep_x1 = -1) {
+                      float* slab = nullptr, int keep_x1 = -1, bool defer_head = false) {
   if (!slab) slab = l->slab;
   torso::PWeights w{WP(l, wpl, l->t_c1w), WP(l, wpl, l->t_c2w), WP(l, wpl, l->t_c3w),
                     P(l, prm, l->t_c1b), P(l, prm, l->t_c2b), P(l, prm, l->t_c3b)};
@@ -429,6 +440,14 @@ int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const torso:
     // tiles with split-K 8, and the LDS-DMA ring (3 or 4 stages) all slower or equal.)
     if (l->single_role) ACME_P3_GEMM("fc_fwd", 128, 128, 2, 2, 32, p, splits);  // tests
     else ACME_P3WS_GEMM("fc_fwd", 128, 128, 2, 2, 32, p, splits, true);
+    // The online forward of a step: the head runs inside the loss launch (nature_backward).
+    if (defer_head && !l->head_separate &&
+        dqn_head_loss_dz_fusable(kHidden, l->cfg.num_actions, splits, P(l, prm, l->t_vw),
+                                 P(l, prm, l->t_aw), P(l, prm, l->t_fcb))) {
+      l->head_deferred = true;
+      l->head_splits = splits;
+      return ACME_OK;
+    }
     ACME_PROF("fc_head_fwd", st, 0.0, 4.0 * (double)rows * 2 * kHidden * (splits + 1));
     return launch_fc_head_forward(slab, splits, rows, kHidden, P(l, prm, l->t_fcb),
                                   P(l, prm, l->t_vw), P(l, prm, l->t_vb), P(l, prm, l->t_aw),
@@ -478,7 +497,28 @@ int mlp_forward(acme_dqn* l, const float* prm, const void* obs_a, const void* ob
   return ACME_OK;
 }
 
-// The step's priority write-back (acme_dqn_step_update), once, on `st`.
+// The step's transient rescale and skip decision (the guard's kRgStep): every plane of the
+// online forward and the backward is written by now; the target forward's records have their
+// own rescale.  defer_r: consumers may still read the planes on the second stream.
+RescaleJob step_rescale_job(acme_dqn* l, bool defer_r) {
+  RescaleJob j;
+  j.s = l->scales;
+  j.nt = j.n = kScTransient;
+  j.overflow = l->overflow;
+  j.skip_lo = kScT1;
+  j.skip_hi = kScT3 + 1;
+  j.defer_r = defer_r ? 1 : 0;
+  j.rg.g = l->guard;
+  j.rg.mode = kRgStep;
+  j.rg.gate = step_gate(l);
+  j.rg.host_skipped = l->host_skipped;
+  return j;
+}
+
+// The step's priority write-back (acme_dqn_step_update), once, on `st`, with the step's
+// rescale in an extra workgroup of its launch (one kernel boundary fewer on the step's
+// critical path; the read scales are committed by Adam, after the second stream's weight
+// gradients that still read the planes).
 int priority_update_tail(void* ctx, hipStream_t st) {
   acme_dqn* l = static_cast<acme_dqn*>(ctx);
   acme_replay* r = l->upd_replay;
@@ -486,7 +526,11 @@ int priority_update_tail(void* ctx, hipStream_t st) {
   l->upd_replay = nullptr;
   if (l->upd_after) ACME_HIP_TRY(hipStreamWaitEvent(st, l->upd_after, 0));
   // Gated: a step that overflowed writes no priority.
-  return replay_update_priorities_gated(r, l->upd_keys, l->upd_prio, l->upd_n, step_gate(l), st);
+  const RescaleJob job = step_rescale_job(l, true);
+  const int rc =
+      replay_update_priorities_gated(r, l->upd_keys, l->upd_prio, l->upd_n, step_gate(l), st, &job);
+  if (rc == ACME_OK) l->step_rescaled = true;
+  return rc;
 }
 
 // join_dense: the caller's stream waits for the side stream's dense weight gradients
@@ -505,9 +549,20 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st_main,
   // block to finish measured 14.6 -> 20.5 us on the critical path).
   bool loss_sum = false;
   const LossArgs la = l->pending_la;
-  if (p3 && l->loss_pending) {  // the loss and the head dZ planes, one launch
+  if (p3 && l->loss_pending && l->head_deferred) {  // online head + loss + head dZ, one launch
+    l->loss_pending = l->head_deferred = false;
+    loss_sum = true;
+    l->loss_nparts = B;
+    ACME_PROF("head_loss_dz", st, 0.0, 4.0 * (double)2 * B * 2 * kHidden * (l->head_splits + 1));
+    rc = launch_dqn_head_loss_dz(la, l->slab, l->head_splits, kHidden, P(l, prm, l->t_fcb),
+                                 P(l, prm, l->t_vw), P(l, prm, l->t_vb), P(l, prm, l->t_aw),
+                                 P(l, prm, l->t_ab), l->hid, l->dzhp.p, l->dzhp.stride,
+                                 l->dzhp.sc, st);
+    if (rc != ACME_OK) return rc;
+  } else if (p3 && l->loss_pending) {  // the loss and the head dZ planes, one launch
     l->loss_pending = false;
     loss_sum = la.loss_part != nullptr;
+    l->loss_nparts = dqn_loss_head_dz_blocks(B, kHidden);
     ACME_PROF("loss_head_dz", st, 0.0, 0.0);
     rc = launch_dqn_loss_head_dz(la, l->hid, kHidden, P(l, prm, l->t_vw),
                                  P(l, prm, l->t_aw), l->dzhp.p, l->dzhp.stride, l->dzhp.sc, st);
@@ -549,7 +604,7 @@ int nature_backward(acme_dqn* l, const void* o_tm1, int B, hipStream_t st_main,
     rc = launch_duel_head_grad_scatter(
         hslab, kHeadBwdSplits, kHidden, A, Pm(l, gr, l->t_vw), Pm(l, gr, l->t_vb),
         Pm(l, gr, l->t_aw), Pm(l, gr, l->t_ab), st, sum_in_scatter ? la.loss_part : nullptr,
-        dqn_loss_head_dz_blocks(B, kHidden), la.mean_over, la.loss);
+        l->loss_nparts, la.mean_over, la.loss);
     if (rc != ACME_OK) return rc;
   }
   if (p3) {
@@ -704,6 +759,7 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
   l->cfg = *cfg;
   l->single_stream = tune_variant("SIDE") == 1;
   l->single_role = tune_variant("WSN") == 1;
+  l->head_separate = tune_variant("HEADSEP") == 1;
   const int A = cfg->num_actions;
   const int B = cfg->max_batch;
   int rc = ACME_OK;
@@ -764,7 +820,8 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
           (rc = plane_alloc(l, &l->t2p, (int64_t)B * kFlat, kScT2)) ||
           (rc = plane_alloc(l, &l->t3p, (int64_t)B * kFlat, kScT3)) ||
           (rc = plane_alloc(l, &l->dzhp, (int64_t)B * 2 * kHidden, kScDzh)) ||
-          (rc = dev_alloc(l, &l->loss_part, dqn_loss_head_dz_blocks(B, kHidden))) ||
+          (rc = dev_alloc(l, &l->loss_part,
+                          std::max<int64_t>(B, dqn_loss_head_dz_blocks(B, kHidden)))) ||
           (rc = plane_alloc(l, &l->dz3p, (int64_t)B * kFlat, kScDz3)) ||
           (rc = plane_alloc(l, &l->dz2p, (int64_t)B * kFlat, kScDz2)) ||
           (rc = plane_alloc(l, &l->dz1p, (int64_t)B * torso::kX1, kScDz1)))
@@ -1223,9 +1280,10 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
     // windows 0.5208 -> 0.5181 ms, three alternating runs each).  Either order gives the
     // same bits.
     const bool online_first = side != nullptr;
+    l->head_deferred = false;
     if (online_first &&
         (rc = nature_forward_p3(l, l->params, l->wpl, fwd_frames, 2 * B, l->x1p, l->x2p, l->x3p,
-                                l->hid, l->q_on, st, nullptr, B)) != ACME_OK)
+                                l->hid, l->q_on, st, nullptr, B, true)) != ACME_OK)
       return rc;
     if ((rc = nature_forward_p3(l, l->target, l->tpl, fwd_frames.rows_from(B), B,
                                 l->t1p, l->t2p, l->t3p, l->thid, l->q_tg, tst,
@@ -1243,7 +1301,7 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
     if (side) ACME_HIP_TRY(hipEventRecord(l->ev[1], side));
     if (!online_first &&
         (rc = nature_forward_p3(l, l->params, l->wpl, fwd_frames, 2 * B, l->x1p, l->x2p, l->x3p,
-                                l->hid, l->q_on, st, nullptr, B)) != ACME_OK)
+                                l->hid, l->q_on, st, nullptr, B, true)) != ACME_OK)
       return rc;
     if (side) ACME_HIP_TRY(hipStreamWaitEvent(st, l->ev[1], 0));
   } else if (nature) {
@@ -1307,13 +1365,14 @@ static int loss_and_dense_backward(acme_dqn* l, const acme_transition_batch* bat
     ACME_PROF("loss", st, 0.0, 0.0);
     if ((rc = launch_dqn_loss(la, st)) != ACME_OK) return rc;
   }
-  if (out && out->q_tm1)
-    ACME_HIP_TRY(hipMemcpyAsync(out->q_tm1, l->q_on, (size_t)B * A * sizeof(float),
-                                hipMemcpyDeviceToDevice, st));
   l->dense_on_side = false;
   rc = nature ? nature_backward(l, batch->o_tm1, B, st, join_dense)
               : mlp_backward(l, batch->o_tm1, B, st);
   if (rc != ACME_OK) return rc;
+  // After the backward: on the plane path its first launch forms q_on (the online head).
+  if (out && out->q_tm1)
+    ACME_HIP_TRY(hipMemcpyAsync(out->q_tm1, l->q_on, (size_t)B * A * sizeof(float),
+                                hipMemcpyDeviceToDevice, st));
   if (l->dense_on_side) {
     l->dense_ev = l->ev[3];
   } else {
@@ -1338,26 +1397,32 @@ int acme_dqn_grad_split(const acme_dqn* l, int64_t* split) {
 
 // Adam (+ the parameter planes) and the periodic target copy; `copy` decided by the host.
 static int apply_impl(acme_dqn* l, bool copy, hipStream_t st) {
-  int rc;
-  Gate gate;  // Adam reads the step's skip decision, made by the rescale below
+  int rc = ACME_OK;
+  Gate gate;  // Adam reads the step's skip decision, made by the step's rescale
+  AdamTail tail;
   if (l->p3_capable) {
     // Every transient record's next scale from this step's maxima, and the step guard's
     // decision (guard->last): skip when a plane write overflowed, when a tensor's maximum
     // fell more than ~2^8-fold below its scale (its planes lost precision), or, with data
-    // parallelism, when any rank skips.  Before Adam, after every plane this step writes;
-    // the target forward's records were rescaled after it (on the side stream, which may
+    // parallelism, when any rank skips.  Before Adam, after every plane this step writes
+    // (the fused step's priority write-back already ran it, with deferred read scales); the
+    // target forward's records were rescaled after it (on the side stream, which may
     // already run the next step's target forward).
-    ACME_PROF("plane_rescale", st, 0.0, 0.0);
-    RescaleGuard rg;
-    rg.g = l->guard;
-    rg.mode = kRgStep;
-    rg.gate = step_gate(l);
-    rg.host_skipped = l->host_skipped;
-    if ((rc = launch_plane_rescale(l->scales, kScTransient, kScTransient, -1, -1, l->overflow, st,
-                                   kScT1, kScT3 + 1, rg)) != ACME_OK)
-      return rc;
+    if (!l->step_rescaled) {
+      ACME_PROF("plane_rescale", st, 0.0, 0.0);
+      if ((rc = launch_rescale_job(step_rescale_job(l, false), st)) != ACME_OK) return rc;
+    } else {
+      tail.commit = l->scales;
+      tail.ncommit = kScTransient;
+      tail.skip_lo = kScT1;
+      tail.skip_hi = kScT3 + 1;
+    }
+    l->step_rescaled = false;
     gate.g = l->guard;
     gate.use_last = 1;
+    tail.clear = l->guard;
+    tail.params = l->scales + kScParams;
+    if (copy) tail.target = l->scales + kScTarget;
   }
   if (l->slabs_pending) {  // the conv weight gradients reduced on Adam's read
     l->slabs_pending = false;
@@ -1378,11 +1443,11 @@ static int apply_impl(acme_dqn* l, bool copy, hipStream_t st) {
     rc = launch_adam_slabs(l->params, l->grads, l->m, l->v, a, l->cfg.learning_rate,
                            l->cfg.adam_beta1, l->cfg.adam_beta2, l->cfg.adam_epsilon,
                            &l->guard->applied, l->wpl, l->flat, l->scales + kScParams,
-                           l->cfg.semantics == ACME_SEMANTICS_JAX ? 1 : 0, gate, st);
+                           l->cfg.semantics == ACME_SEMANTICS_JAX ? 1 : 0, gate, tail, st);
     if (rc != ACME_OK) return rc;
   } else {
     ACME_PROF("adam", st, 0.0, 28.0 * (double)l->logical);
-    if ((rc = adam_range(l, 0, l->flat, gate, st)) != ACME_OK) return rc;
+    if ((rc = adam_range(l, 0, l->flat, gate, tail, st)) != ACME_OK) return rc;
   }
   if (copy) {
     l->target_dirty = true;
@@ -1393,25 +1458,18 @@ static int apply_impl(acme_dqn* l, bool copy, hipStream_t st) {
       ACME_HIP_TRY(hipMemcpyAsync(l->tpl, l->wpl, gemm::kPlanes * l->flat * sizeof(uint16_t),
                                   hipMemcpyDeviceToDevice, st));
   }
-  if (l->p3_capable) {
-    // The parameter planes' record (persistent): the parameters' maximum every
-    // kParamAmaxPeriod steps (Adam moves a parameter by about lr per step, far inside the
-    // 2^8 headroom of its scale) moves the write scale; the step after it the read scale
-    // follows the planes Adam then wrote; a target copy takes the read scale of the planes
-    // it copied.  Other steps leave the record as it is (no launch).
-    const bool amax = l->num_steps % kParamAmaxPeriod == 0;
-    if (amax) {
+  if (l->p3_capable && l->num_steps % kParamAmaxPeriod == 0) {
+    // The parameter planes' write scale from their maximum every kParamAmaxPeriod steps
+    // (Adam moves a parameter by about lr per step, far inside the 2^8 headroom of its
+    // scale); the read scale stays that of the planes stored now (Adam's tail set it; the
+    // next Adam pass writes at the new scale and moves it).
+    {
       ACME_PROF("param_amax", st, 0.0, 4.0 * (double)l->flat);
       if ((rc = launch_param_amax(l->params, l->flat, l->scales + kScParams, st)) != ACME_OK)
         return rc;
     }
-    if (amax || copy || l->param_rescale_pending) {
-      ACME_PROF("param_rescale", st, 0.0, 0.0);
-      if ((rc = launch_plane_rescale(l->scales + kScParams, 0, 1, copy ? 0 : -1, copy ? 1 : -1,
-                                     l->overflow, st)) != ACME_OK)
-        return rc;
-    }
-    l->param_rescale_pending = amax;
+    ACME_PROF("param_rescale", st, 0.0, 0.0);
+    rc = launch_plane_rescale(l->scales + kScParams, 0, 1, -1, -1, l->overflow, st);
   }
   return rc;
 }

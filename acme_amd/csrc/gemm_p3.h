@@ -174,7 +174,11 @@ __device__ __forceinline__ uint32_t f16x2_of_bytes(uint32_t x, int sh) {
 // Maximum of two magnitudes (non-negative floats, or NaN) that keeps NaN: non-negative
 // floats order as their bits, and a NaN (sign cleared by fabsf) above infinity.  A plane
 // computed from overflowed planes is NaN, and its record must see that.
+#ifndef ACME_AMAX_FMAXF
+#define ACME_AMAX_FMAXF 0  // experiment: fmaxf (drops NaN)
+#endif
 __device__ __forceinline__ float amax_max(float a, float b) {
+  if constexpr (ACME_AMAX_FMAXF) return fmaxf(a, b);
   return __builtin_bit_cast(float, max(__builtin_bit_cast(uint32_t, a),
                                        __builtin_bit_cast(uint32_t, b)));
 }

@@ -126,6 +126,16 @@ int launch_dqn_loss_head_dz(const LossArgs& args, const float* h, int H, const f
                             hipStream_t st);
 // Blocks of launch_dqn_loss_head_dz for a batch of B rows (the loss_part entries written).
 int64_t dqn_loss_head_dz_blocks(int B, int H);
+// The online duelling head (from the fc split-K slab of 2B rows: o_tm1 then o_t) fused with
+// the loss and the head dZ planes: one block per batch row; writes hid, args.q_on, the
+// loss outputs and args.loss_part[b] (B partials).  Nature head only (H = 512, A = 18,
+// splits 4 or 8): dqn_head_loss_dz_fusable.
+bool dqn_head_loss_dz_fusable(int H, int A, int splits, const float* wv, const float* wa,
+                              const float* fcb);
+int launch_dqn_head_loss_dz(const LossArgs& args, const float* slab, int splits, int H,
+                            const float* fcb, const float* wv, const float* bv, const float* wa,
+                            const float* ba, float* hid, uint16_t* planes, int64_t pstride,
+                            gemm::PScale* sc, hipStream_t st);
 // loss[0] = (sum of the n partials, in order) / mean_over.
 int launch_dqn_loss_sum(const double* part, int64_t n, int mean_over, float* loss, hipStream_t st);
 
@@ -186,10 +196,22 @@ int launch_clip_adam(const ClipAdamArgs& a, hipStream_t st);
 // gate: a skipped step leaves p, m and v as they are and rewrites the planes of p at psc->w
 // (so the record's read scale stays that of the stored planes).  A plane write that
 // overflows commits the wave's max |p| to psc and raises its flag.
+// The step's scale-record bookkeeping, done by the Adam launch's first workgroup (Adam runs
+// after every reader of the step's planes): the guard's flags cleared; the read scales of
+// transient records a deferred rescale left (RescaleJob::defer_r) moved to their wi; the
+// parameter record's r = the wi of the planes Adam writes (at w); a target copy of them takes
+// the same r.
+struct AdamTail {
+  StepGuard* clear = nullptr;
+  gemm::PScale* commit = nullptr;
+  int ncommit = 0, skip_lo = -1, skip_hi = -1;
+  gemm::PScale* params = nullptr;
+  gemm::PScale* target = nullptr;
+};
 int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,
                 float b2, float eps, int64_t t, uint16_t* planes, int64_t pstride, hipStream_t st,
                 int optix = 0, int64_t* dev_steps = nullptr, gemm::PScale* psc = nullptr,
-                const Gate& gate = Gate{}, bool count = true);
+                const Gate& gate = Gate{}, bool count = true, const AdamTail& tail = AdamTail{});
 
 // launch_adam (snt.Adam, t >= 1) with some gradient ranges still split-K slabs: segment k
 // updates float4 [off4, off4 + n4) of the flat buffers from the deterministic reduction of
@@ -212,7 +234,7 @@ struct AdamSlabs {
 int launch_adam_slabs(float* p, float* g, float* m, float* v, const AdamSlabs& slabs,
                       float lr, float b1, float b2, float eps, const int64_t* dev_steps,
                       uint16_t* planes, int64_t pstride, gemm::PScale* psc, int optix,
-                      const Gate& gate, hipStream_t st);
+                      const Gate& gate, const AdamTail& tail, hipStream_t st);
 
 // Two-plane split of n floats (n multiple of 4): planes[i * pstride + e], at the scale of
 // max |x| (sets the record sc: w, r = wi = 1 / w; overflow |= 1 on a non-finite x).
@@ -235,10 +257,16 @@ int launch_param_amax(const float* x, int64_t n, gemm::PScale* sc, hipStream_t s
 // shrink by that factor at their new scale), else 2^-16.  rg: the step guard's work.
 int launch_plane_rescale(gemm::PScale* recs, int n_transient, int n, int copy_from, int copy_to,
                          int* overflow, hipStream_t st, int skip_lo = -1, int skip_hi = -1,
-                         const RescaleGuard& rg = RescaleGuard{});
+                         const RescaleGuard& rg = RescaleGuard{}, int defer_r = 0);
+struct RescaleJob;  // rescale.h
+int launch_rescale_job(const RescaleJob& job, hipStream_t st);
 // The replay's update_priorities (replay.hip) behind a gate: a skipped step writes none.
+// job (optional): a scale rescale (rescale.h) run by an extra workgroup of the update's
+// launch (or its own launch when the update takes several), so the learner's step pays one
+// kernel boundary for both.
 int replay_update_priorities_gated(acme_replay* r, const uint64_t* keys, const double* prios,
-                                   int64_t n, const Gate& gate, hipStream_t st);
+                                   int64_t n, const Gate& gate, hipStream_t st,
+                                   const RescaleJob* job = nullptr);
 // Data-parallel gate: *dst = the step's local skip (1.f or 0.f), a gradient word that the
 // ranks' all-reduce then combines (any rank's skip makes it > 0 on every rank).
 int launch_gate_publish(const Gate& gate, float* dst, hipStream_t st);

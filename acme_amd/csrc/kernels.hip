@@ -1,6 +1,7 @@
 // Fused small kernels of the learner step: duelling head fwd/bwd, DQN loss, bias-grad
 // column sums, split-K slab reductions, snt.Adam.
 #include "kernels.h"
+#include "rescale.h"
 
 #include "conv.h"
 #include "gemm_p3.h"
@@ -675,6 +676,143 @@ __global__ void __launch_bounds__(256) dqn_loss_head_dz_kernel(
   gemm::amax_commit(sc, mx);
 }
 
+// The online duelling head fused with the loss and the head dZ (plane path, Nature head
+// 2H = 1024, compile-time A).  Block b owns batch row b: the split-K sum, bias and ReLU of
+// hidden rows b (o_tm1) and B + b (o_t, the double-Q selector) as fc_head1024_kernel, their
+// q rows, the row's loss outputs (loss_row: reward clip, double-Q target, TD, Huber, IS
+// weight; the normaliser from all B probabilities, read by every block), then dZ of hidden
+// row b as planes from the registers that hold its units and their weights (head_dz8's
+// terms in its order), masked by its ReLU.  One launch for the online head, the loss and
+// the head dZ: the head's launch and its boundary leave the step's critical path.
+template <int SPL, int A>
+__global__ void __launch_bounds__(256) dqn_head_loss_dz_kernel(
+    LossArgs p, const float* __restrict__ slab, const float* __restrict__ fcb,
+    const float* __restrict__ wv, const float* __restrict__ bv, const float* __restrict__ wa,
+    const float* __restrict__ ba, float* __restrict__ hid, uint16_t* __restrict__ planes,
+    int64_t pstride, gemm::PScale* __restrict__ sc) {
+  constexpr int N4 = 256, HALF = 128, R = 2, H = 512;
+  __shared__ float part[R][A + 1][HALF];
+  __shared__ float dots[R][A + 1];
+  __shared__ double red[4];
+  __shared__ float s_g;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int B = p.B, b = blockIdx.x;
+  const int64_t count4 = (int64_t)2 * B * N4;  // the online slab holds 2B rows
+  const f32x4* s4 = reinterpret_cast<const f32x4*>(slab);
+  f32x4 sp[R][SPL];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t e = (int64_t)(r == 0 ? b : B + b) * N4 + t;
+#pragma unroll
+    for (int k = 0; k < SPL; ++k) sp[r][k] = s4[(size_t)k * count4 + e];
+  }
+  const bool adv = t >= HALF;
+  const int c = adv ? t - HALF : t;  // this thread's 4 hidden units within its half
+  f32x4 w[A];
+  if (adv) {
+    const f32x4* wa4 = reinterpret_cast<const f32x4*>(wa) + (size_t)c * A;  // wa rows 4c .. 4c+3
+#pragma unroll
+    for (int i = 0; i < A; ++i) w[i] = wa4[i];
+  } else {
+    w[0] = reinterpret_cast<const f32x4*>(wv)[c];
+  }
+  const f32x4 bias = reinterpret_cast<const f32x4*>(fcb)[t];
+  const int ab = p.a[b];
+  // Importance-weight normaliser: max_b (1/p_b)^beta = (1/min_b p_b)^beta.
+  double pmin = INFINITY;
+  for (int i = t; i < B; i += 256) pmin = fmin(pmin, p.probs[i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) pmin = fmin(pmin, __shfl_xor(pmin, o, 64));
+  if (lane == 0) red[wave] = pmin;
+  f32x4 h_own;  // hidden row b, this thread's units (the dZ mask)
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    f32x4 v = sp[r][0];
+#pragma unroll
+    for (int k = 1; k < SPL; ++k) v += sp[r][k];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const float x = v[jj] + bias[jj];
+      v[jj] = x > 0.f ? x : 0.f;
+    }
+    reinterpret_cast<f32x4*>(hid)[(int64_t)(r == 0 ? b : B + b) * N4 + t] = v;
+    if (r == 0) h_own = v;
+    if (adv) {
+      const float* wf = reinterpret_cast<const float*>(w);  // [4][A], compile-time indices
+#pragma unroll
+      for (int o = 0; o < A; ++o) {
+        float acc = v[0] * wf[o];
+        acc = fmaf(v[1], wf[A + o], acc);
+        acc = fmaf(v[2], wf[2 * A + o], acc);
+        acc = fmaf(v[3], wf[3 * A + o], acc);
+        part[r][o][c] = acc;
+      }
+    } else {
+      float acc = v[0] * w[0][0];
+      acc = fmaf(v[1], w[0][1], acc);
+      acc = fmaf(v[2], w[0][2], acc);
+      acc = fmaf(v[3], w[0][3], acc);
+      part[r][A][c] = acc;
+    }
+  }
+  __syncthreads();
+  for (int j = wave; j < R * (A + 1); j += 4) {
+    const int r = j / (A + 1), o = j - r * (A + 1);
+    float x = part[r][o][2 * lane] + part[r][o][2 * lane + 1];
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d, 64);
+    if (lane == 0) dots[r][o] = x + (o == A ? bv[0] : ba[o]);
+  }
+  __syncthreads();
+  if (t < R * A) {
+    const int r = t / A, jj = t - r * A;
+    float mean = 0.f;
+    for (int k = 0; k < A; ++k) mean += dots[r][k];
+    mean /= (float)A;
+    const_cast<float*>(p.q_on)[(size_t)(r == 0 ? b : B + b) * A + jj] =
+        dots[r][A] + (dots[r][jj] - mean);
+  }
+  __syncthreads();  // the block's q rows are in global memory for loss_row
+  if (t == 0) {
+    pmin = fmin(fmin(red[0], red[1]), fmin(red[2], red[3]));
+    if (p.global_min_prob) pmin = *p.global_min_prob;
+    const double wmax = p.jax ? (double)powf((float)(1.0 / pmin), p.beta)
+                              : pow(1.0 / pmin, (double)p.beta);
+    const LossRow row = loss_row(p, b, wmax);
+    s_g = row.g;
+    p.g[b] = row.g;
+    p.td[b] = row.td;
+    p.prio[b] = (double)fabsf(row.td);
+    p.a_cache[b] = ab;
+    p.loss_part[b] = (double)row.hub_w;
+  }
+  __syncthreads();
+  // dZ of hidden units 4c .. 4c+3 of this thread's half (head_dz8's terms, in its order).
+  const float gb = s_g;
+  float v4[4];
+  if (!adv) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v4[j] = gb * w[0][j];
+  } else {
+    const float inv_a = 1.f / (float)A;
+    const float* wf = reinterpret_cast<const float*>(w);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v4[j] = 0.f;
+#pragma unroll
+    for (int i = 0; i < A; ++i) {
+      const float cc = gb * ((i == ab ? 1.f : 0.f) - inv_a);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v4[j] = fmaf(cc, wf[j * A + i], v4[j]);
+    }
+  }
+  f32x4 d;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) d[j] = h_own[j] > 0.f ? v4[j] : 0.f;
+  const int64_t i4 = ((int64_t)b * 2 * H + (adv ? H : 0) + 4 * c) / 4;
+  const float mx = store_planes4(planes, pstride, i4, d, sc->w);
+  gemm::amax_commit(sc, mx);
+}
+
 // dZ of the fused hidden layer as planes, 8 consecutive units per thread:
 // k < H: g_b wv[k];  k >= H: g_b (wa[k-H][a_b] - mean_j wa[k-H][j]); masked by hid > 0.
 __global__ void __launch_bounds__(256) head_dz_planes_kernel(
@@ -754,6 +892,21 @@ __device__ __forceinline__ void adam_planes_check(gemm::PScale* psc, float mx, f
     gemm::amax_commit(psc, mx);
 }
 
+__device__ __forceinline__ void adam_tail(const AdamTail& t) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  if (t.clear) {
+    t.clear->on = 0u;
+    t.clear->prm = 0u;
+  }
+  for (int i = 0; i < t.ncommit; ++i)
+    if (!(i >= t.skip_lo && i < t.skip_hi)) t.commit[i].r = t.commit[i].wi;
+  if (t.params) {
+    const float wi = t.params->wi;
+    t.params->r = t.params->rl = wi;
+    if (t.target) t.target->r = t.target->rl = wi;
+  }
+}
+
 __device__ __forceinline__ void adam_bias_corrections(AdamConsts& c, const int64_t* dev_steps) {
   if (dev_steps) {  // device-side step count: same expressions as the host's
     const float tf = (float)(*dev_steps + c.toff);
@@ -769,7 +922,8 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p,
                                                    uint16_t* __restrict__ planes,
                                                    int64_t pstride, gemm::PScale* __restrict__ psc,
                                                    const int64_t* __restrict__ dev_steps,
-                                                   const Gate gate) {
+                                                   const Gate gate, const AdamTail tail) {
+  adam_tail(tail);
   adam_bias_corrections(c, dev_steps);
   const bool skip = gate_skip(gate);
   const float pw = planes ? psc->w : 0.f;
@@ -797,7 +951,8 @@ __global__ void __launch_bounds__(256) adam_slabs_kernel(float* __restrict__ p,
                                                          int64_t pstride,
                                                          gemm::PScale* __restrict__ psc,
                                                          const int64_t* __restrict__ dev_steps,
-                                                         const Gate gate) {
+                                                         const Gate gate, const AdamTail tail) {
+  adam_tail(tail);
   adam_bias_corrections(c, dev_steps);
   const bool skip = gate_skip(gate);
   const float pw = planes ? psc->w : 0.f;
@@ -919,116 +1074,9 @@ __global__ void __launch_bounds__(64) plane_scale_set_kernel(gemm::PScale* __res
   sc->r = sc->wi = sc->rl = ldexpf(1.f, -e);
 }
 
-// End-of-step rescale of n records (one wave each, and one more for the copy; blockDim.x =
-// 64 (n + 1)).  Records [0, nt) are transient (written and read within a step: the next
-// step writes and reads at the new scale), [nt, n) persistent (parameter planes, rewritten
-// by every Adam pass at w and read in the next step: r becomes the wi their writer used,
-// and w moves when an amax was taken).  copy_to >= 0 (outside [0, n)): record copy_to took
-// a plane copy of record copy_from's latest write (r = its wi).  A transient record whose
-// amax is 0 keeps its scale.  overflow |= 1 when a write exceeded f16's range (amax w >=
-// 65520) or was not finite.  All loads are issued in one round before one barrier, then
-// every store: the kernel sits between two steps on the critical path.
-__global__ void __launch_bounds__(1024) plane_rescale_kernel(gemm::PScale* __restrict__ s, int nt,
-                                                             int n, int copy_from, int copy_to,
-                                                             int* __restrict__ overflow,
-                                                             int skip_lo, int skip_hi,
-                                                             const RescaleGuard rg) {
-  // Scale reduction (log2 of new w / old w) of the group's overflowed records whose maximum
-  // is finite: the records computed from their planes take the largest one.
-  __shared__ int s_shift[16];
-  // A record of the group whose planes overflowed (maximum w >= 65520, or not finite) or
-  // underflowed (0 < maximum w < 1: the largest element's low plane is subnormal, so the
-  // tensor's planes carry less than an f32 rounding's precision relative to its maximum).
-  __shared__ int s_bad;
-  if (threadIdx.x == 0) s_bad = 0;
-  __syncthreads();
-  const int i = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int ic = i < n ? i : 0;
-  uint32_t a_bits = s[ic].slot[lane].v;
-  const float w0 = s[ic].w, r0 = s[ic].r, wi0 = s[ic].wi;
-  const float cwi = copy_to >= 0 ? s[copy_from].wi : 0.f;
-  // The guard's inputs, read before the first store.
-  uint32_t gv[4] = {0u, 0u, 0u, 0u};
-  float dpv = 0.f;
-  if (rg.g && i == n && lane == 0) {
-    gv[0] = rg.g->on;
-    gv[1] = rg.g->tt;
-    gv[2] = rg.g->t[rg.gate.par & 1];
-    gv[3] = rg.g->prm;
-    if (rg.gate.dp) dpv = *rg.gate.dp;
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) a_bits = max(a_bits, (uint32_t)__shfl_xor((int)a_bits, o, 64));
-  const float a = __builtin_bit_cast(float, a_bits);
-  const bool live = i < n && !(i >= skip_lo && i < skip_hi);
-  const bool finite = a <= 3.0e38f;
-  int wexp;
-  (void)frexpf(w0, &wexp);  // w0 = 2^(wexp - 1)
-  const int e = finite && a > 0.f ? scale_exp(a) : 0;
-  if (lane == 0 && i < 16) {
-    s_shift[i] = live && finite && a > 0.f && !(a * w0 < 65520.f) ? e - (wexp - 1) : 0;
-    if (live && a != 0.f && (!(a * w0 < 65520.f) || a * w0 < 1.f)) s_bad = 1;
-  }
-  __syncthreads();
-  if (i >= n) {
-    if (i == n && lane == 0) {
-      if (copy_to >= 0) {
-        s[copy_to].r = cwi;
-        s[copy_to].rl = cwi;
-      }
-      StepGuard* g = rg.g;
-      const uint32_t bad = s_bad ? 1u : 0u;
-      if (g && rg.mode == kRgTarget) {
-        g->t[rg.gate.par & 1] = gv[1] | bad;
-        g->tt = 0u;
-      } else if (g && rg.mode == kRgQValues) {
-        g->qv = gv[1] | bad;
-        g->tt = 0u;
-      } else if (g && rg.mode == kRgFlag) {
-        if (bad) g->on = 1u;
-      } else if (g && rg.mode == kRgStep) {
-        const bool skip = (gv[0] | gv[2] | bad) != 0u || dpv > 0.f;
-        g->last = skip ? 1u : 0u;
-        if (skip) {
-          const int64_t k = g->skipped + 1;
-          g->skipped = k;
-          if (rg.host_skipped) *rg.host_skipped = k;
-        } else {
-          g->applied += 1;
-        }
-        g->on = 0u;
-        g->prm = 0u;
-      } else if (g && rg.mode == kRgClear) {
-        g->on = g->tt = g->prm = g->last = g->qv = 0u;
-        g->t[0] = g->t[1] = 0u;
-      }
-    }
-    return;
-  }
-  if (!live) return;  // rescaled by their own stream
-  s[i].slot[lane].v = 0u;
-  if (lane != 0) return;
-  const bool persistent = i >= nt;
-  const float stored = persistent ? wi0 : r0;  // the read scale of the planes stored now
-  gemm::PScale* rec = s + i;
-  if (a == 0.f) {  // no maximum taken: the scale stays
-    if (persistent) rec->r = rec->rl = stored;
-    else rec->rl = stored;
-    return;
-  }
-  if (!(a * w0 < 65520.f)) atomicOr(overflow, 1);
-  int shift = -16;  // a non-finite maximum: the largest reduction of the group, else 2^-16
-  if (!finite) {
-    int mn = 0;
-    for (int k = 0; k < n && k < 16; ++k) mn = min(mn, s_shift[k]);
-    if (mn < 0) shift = mn;
-  }
-  const float w = finite ? ldexpf(1.f, e) : ldexpf(w0, shift);
-  const float wi = finite ? ldexpf(1.f, -e) : ldexpf(wi0, -shift);
-  rec->w = w;
-  rec->wi = wi;
-  rec->rl = stored;
-  rec->r = persistent ? stored : wi;
+// A rescale job (rescale.h) as its own launch: one workgroup of 256 threads.
+__global__ void __launch_bounds__(256) plane_rescale_kernel(const RescaleJob job) {
+  rescale_block(job);
 }
 
 __global__ void gate_publish_kernel(const Gate gate, float* dst) {
@@ -1325,6 +1373,30 @@ int launch_fc_head_forward(const float* slab, int splits, int rows, int H, const
 
 int64_t dqn_loss_head_dz_blocks(int B, int H) { return ceil_div((int64_t)B * (2 * H / 8), 256); }
 
+bool dqn_head_loss_dz_fusable(int H, int A, int splits, const float* wv, const float* wa,
+                              const float* fcb) {
+  return H == 512 && A == 18 && (splits == 4 || splits == 8) &&
+         reinterpret_cast<uintptr_t>(wa) % 16 == 0 && reinterpret_cast<uintptr_t>(wv) % 16 == 0 &&
+         reinterpret_cast<uintptr_t>(fcb) % 16 == 0;
+}
+
+int launch_dqn_head_loss_dz(const LossArgs& args, const float* slab, int splits, int H,
+                            const float* fcb, const float* wv, const float* bv, const float* wa,
+                            const float* ba, float* hid, uint16_t* planes, int64_t pstride,
+                            gemm::PScale* sc, hipStream_t st) {
+  ACME_CHECK_ARG(dqn_head_loss_dz_fusable(H, args.A, splits, wv, wa, fcb) && args.loss_part &&
+                     planes && sc && args.B >= 1,
+                 "bad fused head / loss / head dZ arguments");
+  if (splits == 8)
+    dqn_head_loss_dz_kernel<8, 18><<<(unsigned)args.B, 256, 0, st>>>(args, slab, fcb, wv, bv, wa, ba,
+                                                                   hid, planes, pstride, sc);
+  else
+    dqn_head_loss_dz_kernel<4, 18><<<(unsigned)args.B, 256, 0, st>>>(args, slab, fcb, wv, bv, wa, ba,
+                                                                   hid, planes, pstride, sc);
+  ACME_LAUNCH_CHECK();
+  return ACME_OK;
+}
+
 __global__ void __launch_bounds__(256) dqn_loss_sum_kernel(const double* __restrict__ part,
                                                            int64_t n, int mean_over,
                                                            float* __restrict__ loss) {
@@ -1399,7 +1471,8 @@ int launch_grad_sumsq(const float* g, int64_t n4, int64_t group0_4, double* part
 
 int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,
                 float b2, float eps, int64_t t, uint16_t* planes, int64_t pstride, hipStream_t st,
-                int optix, int64_t* dev_steps, gemm::PScale* psc, const Gate& gate, bool count) {
+                int optix, int64_t* dev_steps, gemm::PScale* psc, const Gate& gate, bool count,
+                const AdamTail& tail) {
   ACME_CHECK_ARG(p && g && m && v, "null buffer");
   ACME_CHECK_ARG(!planes || psc, "parameter planes need a scale record");
   ACME_CHECK_ARG(n % 4 == 0, "adam buffer length must be a multiple of 4");
@@ -1416,7 +1489,7 @@ int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float l
   // faster each.
   const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n4, 256), 8192);
   adam_kernel<<<std::max(grid, 1u), 256, 0, st>>>(p, g, m, v, n4, c, planes, pstride, psc,
-                                                  dev_steps, gate);
+                                                  dev_steps, gate, tail);
   ACME_LAUNCH_CHECK();
   if (dev_steps && count) {
     count_step_kernel<<<1, 1, 0, st>>>(dev_steps);
@@ -1428,7 +1501,7 @@ int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float l
 int launch_adam_slabs(float* p, float* g, float* m, float* v, const AdamSlabs& slabs,
                       float lr, float b1, float b2, float eps, const int64_t* dev_steps,
                       uint16_t* planes, int64_t pstride, gemm::PScale* psc, int optix,
-                      const Gate& gate, hipStream_t st) {
+                      const Gate& gate, const AdamTail& tail, hipStream_t st) {
   ACME_CHECK_ARG(p && g && m && v && (!planes || psc) && dev_steps, "null buffer");
   ACME_CHECK_ARG(slabs.nseg >= 1 && slabs.nseg <= AdamSlabs::kMaxSegs, "bad slab Adam arguments");
   AdamSlabs s = slabs;
@@ -1443,7 +1516,7 @@ int launch_adam_slabs(float* p, float* g, float* m, float* v, const AdamSlabs& s
   const AdamConsts c{lr, b1, 1.f - b1, b2, 1.f - b2, 0.f, 0.f, eps, optix, 0};
   const int dense = (int)std::min<int64_t>(ceil_div(s.dense_n4, 256), 8192);
   adam_slabs_kernel<<<(unsigned)(blocks + std::max(dense, 1)), 256, 0, st>>>(
-      p, g, m, v, s, c, planes, pstride, psc, dev_steps, gate);
+      p, g, m, v, s, c, planes, pstride, psc, dev_steps, gate, tail);
   ACME_LAUNCH_CHECK();
   return ACME_OK;
 }
@@ -1481,18 +1554,31 @@ int launch_param_amax(const float* x, int64_t n, gemm::PScale* sc, hipStream_t s
   return ACME_OK;
 }
 
+int launch_rescale_job(const RescaleJob& job, hipStream_t st) {
+  plane_rescale_kernel<<<1, 256, 0, st>>>(job);
+  ACME_LAUNCH_CHECK();
+  return ACME_OK;
+}
+
 int launch_plane_rescale(gemm::PScale* recs, int n_transient, int n, int copy_from, int copy_to,
                          int* overflow, hipStream_t st, int skip_lo, int skip_hi,
-                         const RescaleGuard& rg) {
+                         const RescaleGuard& rg, int defer_r) {
   ACME_CHECK_ARG(recs && overflow && n >= 1 && n <= 15 && n_transient >= 0 && n_transient <= n,
                  "bad rescale arguments");
   ACME_CHECK_ARG(copy_to < 0 || (copy_to >= n && copy_from >= 0 && copy_from < n),
                  "bad rescale copy");
-  plane_rescale_kernel<<<1, (unsigned)(64 * (n + 1)), 0, st>>>(recs, n_transient, n, copy_from,
-                                                               copy_to, overflow, skip_lo, skip_hi,
-                                                               rg);
-  ACME_LAUNCH_CHECK();
-  return ACME_OK;
+  RescaleJob job;
+  job.s = recs;
+  job.nt = n_transient;
+  job.n = n;
+  job.copy_from = copy_from;
+  job.copy_to = copy_to;
+  job.overflow = overflow;
+  job.skip_lo = skip_lo;
+  job.skip_hi = skip_hi;
+  job.defer_r = defer_r;
+  job.rg = rg;
+  return launch_rescale_job(job, st);
 }
 
 int launch_gate_publish(const Gate& gate, float* dst, hipStream_t st) {

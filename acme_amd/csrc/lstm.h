@@ -1,0 +1,394 @@
+// The snt.LSTM unroll's building blocks shared by the recurrent learners (IMPALA, R2D2):
+// the OAR embedding loaders of the input projection (acme/tf/networks/embedding.py:26-45)
+// and the per-step cell kernels, forward and BPTT (snt.LSTM: gates = x W_i + h W_h + b
+// split as i, f, g, o; c' = sigmoid(f) c + sigmoid(i) tanh(g); h' = sigmoid(o) tanh(c')).
+// Included into each learner's translation unit (internal linkage).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+#include "conv.h"
+#include "gemm.h"
+
+namespace {
+
+using namespace acme;
+using namespace acme::conv;
+
+constexpr int kUnits = 8;  // LSTM units per block of the backward cell kernel
+
+__device__ __forceinline__ float sigmoidf(float x) { return 1.f / (1.f + expf(-x)); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ------------------------------------------------------------------ OAR embedding loaders
+// Embedding row m = [feat[m][0:F] | one_hot(prev_a[m], A) | tanh(prev_r[m])], D = F + A + 1.
+struct Oar {
+  const float* feat;  // [rows][F]
+  int F, A;
+  const int32_t* prev_a;
+  const float* prev_r;
+  __device__ float at(int m, int k) const {
+    if (k < F) return feat[(size_t)m * F + k];
+    k -= F;
+    if (k < A) return prev_a[m] == k ? 1.f : 0.f;
+    return k == A ? tanhf(prev_r[m]) : 0.f;
+  }
+  __device__ f32x4 four(int m, int k) const {
+    if ((F & 3) == 0 && k + 3 < F) return *reinterpret_cast<const f32x4*>(feat + (size_t)m * F + k);
+    f32x4 r;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = at(m, k + j);
+    return r;
+  }
+};
+
+// gx = emb @ W_i (+ b when not split): M = rows, N = 4H, K = D.
+struct OarFwd {
+  static constexpr int A_MODE = gemm::KCONTIG, B_MODE = gemm::RCONTIG;
+  int M, N, K, k_chunk;
+  Oar x;
+  const float* w;     // [D][4H]
+  const float* bias;  // [4H]
+  float* y;           // [rows][4H]
+  float* slab;        // split-K partials [splits][M][N] (bias added by the reduction)
+  struct ARow {
+    int m;
+  };
+  struct BRow {
+    int n;
+  };
+  __device__ ARow a_row(int m) const { return ARow{m}; }
+  __device__ f32x4 a_load(const ARow& a, int k) const {
+    if (a.m >= M || k >= K) return gemm::zero4();
+    f32x4 r = x.four(a.m, k);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (k + j >= K) r[j] = 0.f;
+    return r;
+  }
+  __device__ BRow b_row(int n) const { return BRow{n}; }
+  __device__ f32x4 b_load(const BRow& b, int k) const {
+    if (b.n >= N || k >= K) return gemm::zero4();
+    return load_row4<true>(w + (size_t)k * N, b.n, N);
+  }
+  __device__ void store(int m, int n, float v, int split) const {
+    if (slab) slab[((size_t)split * M + m) * N + n] = v;
+    else y[(size_t)m * N + n] = v + bias[n];
+  }
+};
+
+// dW_i = emb^T dgates (M = D, N = 4H, K = rows), db = column sums of dgates.
+struct OarWgrad {
+  static constexpr int A_MODE = gemm::RCONTIG, B_MODE = gemm::RCONTIG;
+  static constexpr bool kColSum = true;
+  int M, N, K, k_chunk;
+  Oar x;
+  const float* dz;  // [rows][4H]
+  float* out;
+  float* bias_out;
+  struct ARow {
+    int i;
+  };
+  struct BRow {
+    int n;
+  };
+  __device__ ARow a_row(int i) const { return ARow{i}; }
+  __device__ f32x4 a_load(const ARow& a, int m) const {
+    if (m >= K || a.i >= M) return gemm::zero4();
+    f32x4 r = x.four(m, a.i);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (a.i + j >= M) r[j] = 0.f;
+    return r;
+  }
+  __device__ BRow b_row(int n) const { return BRow{n}; }
+  __device__ f32x4 b_load(const BRow& b, int m) const {
+    if (b.n >= N || m >= K) return gemm::zero4();
+    return load_row4<true>(dz + (size_t)m * N, b.n, N);
+  }
+  __device__ void store(int i, int n, float v, int) const { out[(size_t)i * N + n] = v; }
+  __device__ void store_colsum(int n, float v, int) const { bias_out[n] = v; }
+};
+
+// ------------------------------------------------------------------ LSTM cell kernels
+// kUnits units per block (4 * kUnits = 32 gate columns q * H + u).  The recurrent
+// mat-vecs are spread over 256 threads as 32 columns (or units) x 8 (or 32) k-slices with
+// 16 batch rows per pass in registers, so every W_h element read feeds 16 FMAs and the
+// k-slices are summed once through LDS.
+constexpr int kRowChunk = 16;
+
+// Forward step t for all B sequences: z = gx + h_prev @ W_h, then the snt.LSTM cell
+// update.  h_prev row b lives at hp + b * hp_stride (the core state for t = 0, the
+// previous step's h otherwise).  Row (b, t) of gx / gates / h / c is b * rs_b + t * rs_t
+// (batch-major: rs_b = T, rs_t = 1; time-major: rs_b = 1, rs_t = B); grid.y blocks own bc
+// batch rows each (lstm_fwd_smem(bc, H) bytes of LDS).  kFwdUnits units per block (16 gate columns); the
+// block's W_h columns are staged through LDS in k-chunks with float4 loads.
+constexpr int kFwdUnits = 4;
+constexpr int kFwdPre = 4;  // float4 loads per thread of h_prev / W_h issued up front
+
+__global__ void __launch_bounds__(256) lstm_fwd_step_kernel(
+    const float* __restrict__ gx, const float* __restrict__ wh, const float* __restrict__ hp,
+    int64_t hp_stride, const float* __restrict__ cp, int64_t cp_stride, int B, int64_t rs_b,
+    int64_t rs_t, int t, int H, float* __restrict__ gates, float* __restrict__ h_out,
+    float* __restrict__ c_out, int bc) {
+  constexpr int NC = 4 * kFwdUnits;    // gate columns per block (4 segments of kFwdUnits)
+  constexpr int KS = 256 / NC;         // k-slices
+  static_assert(kRowChunk * NC == 256, "one reduction output per thread");
+  const int u0 = blockIdx.x * kFwdUnits;
+  {  // this block's batch rows [rb0, rb0 + bc): the pointers start at row rb0
+    const int rb0 = blockIdx.y * bc;
+    B = min(bc, B - rb0);
+    gx += (size_t)rb0 * rs_b * 4 * H;
+    hp += (size_t)rb0 * hp_stride;
+    cp += (size_t)rb0 * cp_stride;
+    gates += (size_t)rb0 * rs_b * 4 * H;
+    h_out += (size_t)rb0 * rs_b * H;
+    c_out += (size_t)rb0 * rs_b * H;
+  }
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* hs = smem;                            // [B][H] (this block's rows)
+  float* ws = hs + (size_t)B * H;              // [H][NC]
+  float* red = ws + (size_t)H * NC;            // [KS][kRowChunk][NC]
+  float* zs = red + KS * kRowChunk * NC;       // [B][NC]
+  // Every global load of the step is issued up front (the cell state this thread updates,
+  // h_prev, the block's W_h columns as float4 segments), so the step pays one latency.
+  const bool cell_thread = (int)threadIdx.x < B * kFwdUnits;  // B <= 64 for one pass
+  const float cprev_pre = cell_thread ? cp[(size_t)(threadIdx.x / kFwdUnits) * cp_stride + u0 +
+                                           threadIdx.x % kFwdUnits]
+                                      : 0.f;
+  const int oi = threadIdx.x / NC, occ = threadIdx.x % NC;
+  auto gx_at = [&](int ob) {
+    return ob < B ? gx[((size_t)ob * rs_b + (size_t)t * rs_t) * 4 * H + (occ / kFwdUnits) * H + u0 +
+                       (occ % kFwdUnits)]
+                  : 0.f;
+  };
+  const float gx0 = gx_at(oi);  // the first pass's gx term, in flight with the staging
+  const int nh4 = B * H / 4, nw4 = H * 4;
+  if (nh4 <= 256 * kFwdPre && nw4 <= 256 * kFwdPre) {
+    // Up to kFwdPre float4 of h_prev and of W_h per thread: every load issued (clamped
+    // addresses, no branches around them) before the first LDS store, one latency.
+    f32x4 hv[kFwdPre], wv[kFwdPre];
+#pragma unroll
+    for (int q = 0; q < kFwdPre; ++q) {
+      const int e = min((int)threadIdx.x + 256 * q, nh4 - 1);
+      const int b = e / (H / 4), k = 4 * (e % (H / 4));
+      hv[q] = *reinterpret_cast<const f32x4*>(hp + (size_t)b * hp_stride + k);
+    }
+#pragma unroll
+    for (int q = 0; q < kFwdPre; ++q) {
+      const int e = min((int)threadIdx.x + 256 * q, nw4 - 1);
+      const int k = e / 4, g = e % 4;
+      wv[q] = *reinterpret_cast<const f32x4*>(wh + (size_t)k * 4 * H + g * H + u0);
+    }
+#pragma unroll
+    for (int q = 0; q < kFwdPre; ++q) {
+      const int e = (int)threadIdx.x + 256 * q;
+      if (e < nh4) {
+        const int b = e / (H / 4), k = 4 * (e % (H / 4));
+        *reinterpret_cast<f32x4*>(hs + (size_t)b * H + k) = hv[q];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kFwdPre; ++q) {
+      const int e = (int)threadIdx.x + 256 * q;
+      if (e < nw4) {
+        const int k = e / 4, g = e % 4;
+        *reinterpret_cast<f32x4*>(ws + (size_t)k * NC + g * kFwdUnits) = wv[q];
+      }
+    }
+  } else {
+    for (int e = threadIdx.x; e < nh4; e += blockDim.x) {
+      const int b = e / (H / 4), k = 4 * (e % (H / 4));
+      *reinterpret_cast<f32x4*>(hs + (size_t)b * H + k) =
+          *reinterpret_cast<const f32x4*>(hp + (size_t)b * hp_stride + k);
+    }
+    for (int e = threadIdx.x; e < nw4; e += blockDim.x) {
+      const int k = e / 4, g = e % 4;
+      *reinterpret_cast<f32x4*>(ws + (size_t)k * NC + g * kFwdUnits) =
+          *reinterpret_cast<const f32x4*>(wh + (size_t)k * 4 * H + g * H + u0);
+    }
+  }
+  __syncthreads();
+  const int c = threadIdx.x % NC, sl = threadIdx.x / NC;
+  for (int b0 = 0; b0 < B; b0 += kRowChunk) {
+    // The gx term of this thread's reduction output.
+    const int ob = b0 + oi;
+    const float gxv = b0 == 0 ? gx0 : gx_at(ob);
+    float acc[kRowChunk];
+#pragma unroll
+    for (int i = 0; i < kRowChunk; ++i) acc[i] = 0.f;
+    // Rows past B read row B - 1 (clamped, no branch around the LDS reads: a branch per
+    // row serialised every read behind its own wait); their sums are never stored.
+    int roff[kRowChunk];
+#pragma unroll
+    for (int i = 0; i < kRowChunk; ++i) roff[i] = min(b0 + i, B - 1) * H;
+    for (int k = sl; k < H; k += KS) {
+      const float w = ws[k * NC + c];
+#pragma unroll
+      for (int i = 0; i < kRowChunk; ++i) acc[i] = fmaf(hs[roff[i] + k], w, acc[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < kRowChunk; ++i) red[(sl * kRowChunk + i) * NC + c] = acc[i];
+    __syncthreads();
+    if (ob < B) {  // 256 threads = kRowChunk rows x NC columns
+      float z = 0.f;
+      for (int s2 = 0; s2 < KS; ++s2) z += red[(s2 * kRowChunk + oi) * NC + occ];
+      zs[ob * NC + occ] = gxv + z;
+    }
+    __syncthreads();
+  }
+  for (int o = threadIdx.x; o < B * kFwdUnits; o += blockDim.x) {
+    const int b = o / kFwdUnits, u = o - b * kFwdUnits, j = u0 + u;
+    const float* z = zs + (size_t)b * NC;
+    const float ig = sigmoidf(z[u]), fg = sigmoidf(z[kFwdUnits + u]);
+    const float gg = tanhf(z[2 * kFwdUnits + u]), og = sigmoidf(z[3 * kFwdUnits + u]);
+    const float cprev = o == (int)threadIdx.x && cell_thread ? cprev_pre
+                                                             : cp[(size_t)b * cp_stride + j];
+    const float cn = __fadd_rn(__fmul_rn(fg, cprev), __fmul_rn(ig, gg));  // no contraction:
+    const float hn = __fmul_rn(og, tanhf(cn));  // the persistent kernel computes the same bits
+    const size_t row = (size_t)b * rs_b + (size_t)t * rs_t;
+    gates[row * 4 * H + j] = ig;
+    gates[row * 4 * H + H + j] = fg;
+    gates[row * 4 * H + 2 * H + j] = gg;
+    gates[row * 4 * H + 3 * H + j] = og;
+    c_out[row * H + j] = cn;
+    h_out[row * H + j] = hn;
+  }
+}
+
+size_t lstm_fwd_smem(int B, int H) {
+  constexpr int NC = 4 * kFwdUnits;
+  return ((size_t)B * H + (size_t)H * NC + (size_t)(256 / NC) * kRowChunk * NC +
+          (size_t)B * NC) * sizeof(float);
+}
+
+// Backward step t: dh = dh_head[t] + dgates[t+1] @ W_h^T (t < T-1), dc = dc_carry +
+// dh o (1 - tanh^2 c), gate gradients (pre-activation), dc_carry <- dc f.  Rows as the
+// forward's (b * rs_b + t * rs_t).
+__global__ void __launch_bounds__(256) lstm_bwd_step_kernel(
+    const float* __restrict__ dh_head, const float* __restrict__ wh, const float* __restrict__ gates,
+    const float* __restrict__ c_all, const float* __restrict__ c0, int64_t c0_stride,
+    float* __restrict__ dc_carry, float* __restrict__ dgates, int B, int T, int t, int H,
+    int64_t rs_b, int64_t rs_t) {
+  constexpr int KS = 256 / kUnits;  // 32 k-slices: consecutive threads read consecutive k
+  constexpr int KC = 256;           // k-chunk staged in LDS per pass
+  __shared__ float red[kUnits][kRowChunk][KS + 1];
+  __shared__ __attribute__((aligned(16))) float ds[kRowChunk][KC];
+  const int u0 = blockIdx.x * kUnits;
+  const int sl = threadIdx.x % KS, u = threadIdx.x / KS;
+  const float* w = wh + (size_t)(u0 + u) * 4 * H;
+  // The cell-gradient operands of this thread's (unit, row) in the first row pass, loaded
+  // before the mat-vec so that their latency overlaps it (clamped addresses, used only by
+  // the threads and rows that own them).
+  struct CellIn {
+    float ig, fg, gg, og, cn, cprev, dh, dc;
+  };
+  auto cell_in = [&](int b0) {
+    const int uu = threadIdx.x / kRowChunk, i = threadIdx.x % kRowChunk;
+    const int b = min(b0 + i, B - 1), j = u0 + min(uu, kUnits - 1);
+    const size_t row = (size_t)b * rs_b + (size_t)t * rs_t;
+    const float* g = gates + row * 4 * H;
+    CellIn x;
+    x.ig = g[j]; x.fg = g[H + j]; x.gg = g[2 * H + j]; x.og = g[3 * H + j];
+    x.cn = c_all[row * H + j];
+    x.cprev = t > 0 ? c_all[(row - rs_t) * H + j] : c0[(size_t)b * c0_stride + j];
+    x.dh = dh_head[row * H + j];
+    x.dc = dc_carry[(size_t)b * H + j];
+    return x;
+  };
+  const CellIn first = cell_in(0);
+  for (int b0 = 0; b0 < B; b0 += kRowChunk) {
+    float acc[kRowChunk];
+#pragma unroll
+    for (int i = 0; i < kRowChunk; ++i) acc[i] = 0.f;
+    if (t + 1 < T) {
+      // Stage dgates[t+1][b0 .. b0+15][kc .. kc+255] with float4 loads (4 per thread) and
+      // this thread's 8 W_h values; chunk kc + KC is loaded into registers before chunk kc
+      // is computed from LDS, so one load latency is exposed per step instead of one per
+      // chunk.  Loads past B or 4H read clamped addresses and are replaced by zeros
+      // (selects, not branches around the loads).
+      constexpr int NQ = kRowChunk * KC / 4 / 256;
+      float wv[KC / KS], wn[KC / KS];
+      f32x4 v4[NQ], vn[NQ];
+      auto load = [&](int kc, float (&wr)[KC / KS], f32x4 (&vr)[NQ]) {
+#pragma unroll
+        for (int j = 0; j < KC / KS; ++j) {
+          const int k = kc + sl + KS * j;
+          const float x = w[min(k, 4 * H - 1)];
+          wr[j] = k < 4 * H ? x : 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          const int e = (int)threadIdx.x + 256 * q;  // float4 index in the chunk
+          const int i = e / (KC / 4), k = kc + 4 * (e % (KC / 4));
+          const bool ok = b0 + i < B && k < 4 * H;
+          const f32x4 x = *reinterpret_cast<const f32x4*>(
+              dgates + ((size_t)min(b0 + i, B - 1) * rs_b + (size_t)(t + 1) * rs_t) * 4 * H +
+              min(k, 4 * H - 4));
+          vr[q] = ok ? x : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      };
+      load(0, wv, v4);
+      for (int kc = 0; kc < 4 * H; kc += KC) {
+        __syncthreads();  // previous chunk fully consumed
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          const int e = (int)threadIdx.x + 256 * q;
+          *reinterpret_cast<f32x4*>(&ds[e / (KC / 4)][4 * (e % (KC / 4))]) = v4[q];
+        }
+        __syncthreads();
+        // The next chunk (the last one again at the end: no branch around the loads, whose
+        // join would wait for them before the compute below).
+        load(kc + KC < 4 * H ? kc + KC : kc, wn, vn);
+#pragma unroll
+        for (int j = 0; j < KC / KS; ++j) {
+          const int k = sl + KS * j;
+#pragma unroll
+          for (int i = 0; i < kRowChunk; ++i) acc[i] = fmaf(ds[i][k], wv[j], acc[i]);
+        }
+#pragma unroll
+        for (int j = 0; j < KC / KS; ++j) wv[j] = wn[j];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) v4[q] = vn[q];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kRowChunk; ++i) red[u][i][sl] = acc[i];
+    __syncthreads();
+    if ((int)threadIdx.x < kUnits * kRowChunk) {
+      const int uu = threadIdx.x / kRowChunk, i = threadIdx.x % kRowChunk, b = b0 + i;
+      if (b < B) {
+        float dhn = 0.f;
+        for (int s2 = 0; s2 < KS; ++s2) dhn += red[uu][i][s2];
+        const int j = u0 + uu;
+        const size_t row = (size_t)b * rs_b + (size_t)t * rs_t;
+        const CellIn x = b0 == 0 ? first : cell_in(b0);
+        const float ig = x.ig, fg = x.fg, gg = x.gg, og = x.og;
+        const float cn = x.cn, cprev = x.cprev;
+        const float tc = tanhf(cn);
+        const float dh = x.dh + dhn;
+        const float dc = x.dc + dh * og * (1.f - tc * tc);
+        float* dg = dgates + row * 4 * H;
+        dg[j] = dc * gg * ig * (1.f - ig);
+        dg[H + j] = dc * cprev * fg * (1.f - fg);
+        dg[2 * H + j] = dc * ig * (1.f - gg * gg);
+        dg[3 * H + j] = dh * tc * og * (1.f - og);
+        dc_carry[(size_t)b * H + j] = dc * fg;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace

@@ -33,6 +33,7 @@
 #include "detmath.h"
 #include "kernels.h"
 #include "profiler.h"
+#include "rescale.h"
 
 using namespace acme;
 
@@ -597,15 +598,20 @@ struct FusedUpdateArgs {
   double* level[8];
   int nlevels;
   Gate gate;  // a learner step that was skipped writes no priority
+  RescaleJob job;  // job.s: run by one extra workgroup (blockIdx.x == kFusedUpdateBlocks)
 };
 __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs a) {
   __shared__ int s_j[kFusedUpdateMax];
   __shared__ int64_t s_slot[kFusedUpdateMax];
   __shared__ int s_len;
+  if ((int)blockIdx.x >= kFusedUpdateBlocks) {
+    rescale_block(a.job);
+    return;
+  }
   if (gate_skip(a.gate)) return;
   const int tid = threadIdx.x, nt = blockDim.x;
   const int lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
-  const int G = gridDim.x, bid = blockIdx.x;
+  const int G = kFusedUpdateBlocks, bid = blockIdx.x;
   const int h = a.nlevels >= 2 ? a.nlevels - 2 : 0;
   if (tid == 0) s_len = 0;
   __syncthreads();
@@ -1659,10 +1665,16 @@ int acme_replay_sample_gather_frames(acme_replay* r, int64_t batch, uint64_t ste
 
 int acme::replay_update_priorities_gated(acme_replay* r, const uint64_t* keys,
                                          const double* prios, int64_t n, const Gate& gate,
-                                         hipStream_t st) {
+                                         hipStream_t st, const RescaleJob* job) {
   ACME_CHECK_ARG(r && (n == 0 || (keys && prios)), "null argument");
   ACME_CHECK_ARG(n >= 0 && n < (int64_t(1) << 31), "bad update count");
-  if (n == 0) return ACME_OK;
+  if (n == 0 || n > kFusedUpdateMax) {  // the job as its own launch
+    if (job && job->s) {
+      const int rc = launch_rescale_job(*job, st);
+      if (rc != ACME_OK) return rc;
+    }
+    if (n == 0) return ACME_OK;
+  }
   std::lock_guard<std::mutex> lock(r->mu);
   int rc = order_after_inserts(r, st);
   if (rc != ACME_OK) return rc;
@@ -1688,8 +1700,9 @@ int acme::replay_update_priorities_gated(acme_replay* r, const uint64_t* keys,
     a.upd_keys = keys; a.prios = prios; a.n = (int)n; a.capacity = r->cfg.capacity;
     a.keys = r->keys; a.alpha = alpha; a.raw_prio = r->raw_prio; a.nlevels = r->nlevels;
     a.gate = gate;
+    if (job) a.job = *job;
     for (int l = 0; l < 8; ++l) a.level[l] = r->levels[l];
-    prio_update_fused_kernel<<<kFusedUpdateBlocks, 256, 0, st>>>(a);
+    prio_update_fused_kernel<<<kFusedUpdateBlocks + (a.job.s ? 1 : 0), 256, 0, st>>>(a);
     ACME_LAUNCH_CHECK();
     if (r->nlevels >= 2) {  // the top level, over all its entries that have children
       const int top = r->nlevels - 1;

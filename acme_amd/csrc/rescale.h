@@ -1,0 +1,175 @@
+// The plane scale records' rescale (gemm_p3.h PScale) as one workgroup's work, so that it can
+// run as its own launch (launch_plane_rescale) or as an extra workgroup of a launch already on
+// the stream (the DQN step's priority write-back: one kernel boundary fewer on the critical
+// path).  Records [0, nt) are transient (written and read within a step: the next step writes
+// and reads at the new scale), [nt, n) persistent (parameter planes, rewritten by every Adam
+// pass at w and read in the next step: r becomes the wi their writer used, and w moves when
+// an amax was taken).  copy_to >= 0 (outside [0, n)): record copy_to took a plane copy of
+// record copy_from's latest write (r = its wi).  Records in [skip_lo, skip_hi) are left alone
+// (rescaled on the stream that writes them).  A transient record whose amax is 0 keeps its
+// scale.  A record whose maximum is not finite (planes computed from overflowed planes) takes
+// the largest scale reduction of the group's overflowed records with a finite maximum (its
+// inputs shrink by that factor at their new scale), else 2^-16.  overflow |= 1 when a write
+// exceeded f16's range (amax w >= 65520) or was not finite.
+//
+// defer_r: the transient records' read scale r is NOT moved (w, wi and rl are): consumers
+// still running on another stream read the planes stored now at r; the step's Adam launch
+// then commits r = wi (adam_commit_read_scales) once every consumer has finished.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "gemm_p3.h"
+#include "kernels.h"
+
+namespace acme {
+
+struct RescaleJob {
+  gemm::PScale* s = nullptr;  // null: no job
+  int nt = 0, n = 0, copy_from = -1, copy_to = -1;
+  int* overflow = nullptr;
+  int skip_lo = -1, skip_hi = -1;
+  int defer_r = 0;
+  RescaleGuard rg{};
+};
+
+// The power of two w that puts a (> 0, finite) at 2^7 <= a w < 2^8 (gemm_p3.h); exponent
+// clamped so w and 1 / w stay normal f32.
+__device__ __forceinline__ int rescale_exp(float a) {
+  int k;
+  (void)frexpf(a, &k);  // a = m 2^k, m in [0.5, 1)
+  const int e = 8 - k;
+  return e < -100 ? -100 : (e > 100 ? 100 : e);
+}
+
+// One workgroup of blockDim.x = 64 W threads (W >= 1) does the whole job; every thread of
+// the workgroup calls.  All loads are issued before the first store.
+__device__ __forceinline__ void rescale_block(const RescaleJob& j) {
+  constexpr int kMax = 16;
+  __shared__ uint32_t s_a[kMax];   // each record's maximum (f32 bits)
+  __shared__ float s_w0[kMax], s_r0[kMax], s_wi0[kMax];
+  __shared__ int s_shift[kMax];
+  __shared__ int s_bad;
+  __shared__ uint32_t s_gv[4];
+  __shared__ float s_dp, s_cwi;
+  gemm::PScale* s = j.s;
+  const int n = j.n;
+  const int nw = blockDim.x >> 6, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // Phase 1: every record's slot maximum (a wave per record, records strided over waves).
+#pragma unroll
+  for (int k = 0; k < kMax; ++k) {
+    const int i = wv + k * nw;
+    if (i >= n) break;
+    uint32_t a = s[i].slot[lane].v;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) a = max(a, (uint32_t)__shfl_xor((int)a, o, 64));
+    if (lane == 0) {
+      s_a[i] = a;
+      s_w0[i] = s[i].w;
+      s_r0[i] = s[i].r;
+      s_wi0[i] = s[i].wi;
+    }
+  }
+  if (threadIdx.x == 0) {
+    s_bad = 0;
+    s_cwi = j.copy_to >= 0 ? s[j.copy_from].wi : 0.f;
+    const RescaleGuard& rg = j.rg;
+    s_gv[0] = s_gv[1] = s_gv[2] = s_gv[3] = 0u;
+    s_dp = 0.f;
+    if (rg.g) {  // the guard's inputs, read before any store
+      s_gv[0] = rg.g->on;
+      s_gv[1] = rg.g->tt;
+      s_gv[2] = rg.g->t[rg.gate.par & 1];
+      s_gv[3] = rg.g->prm;
+      if (rg.gate.dp) s_dp = *rg.gate.dp;
+    }
+  }
+  __syncthreads();
+  // Phase 2: per record, the overflow shift and the bad flag.
+  if (threadIdx.x < n) {
+    const int i = threadIdx.x;
+    const float a = __builtin_bit_cast(float, s_a[i]);
+    const bool live = !(i >= j.skip_lo && i < j.skip_hi);
+    const bool finite = a <= 3.0e38f;
+    int wexp;
+    (void)frexpf(s_w0[i], &wexp);  // w0 = 2^(wexp - 1)
+    const float aw = a * s_w0[i];
+    s_shift[i] = live && finite && a > 0.f && !(aw < 65520.f) ? rescale_exp(a) - (wexp - 1) : 0;
+    // Overflowed (max w >= 65520, or not finite) or underflowed (0 < max w < 1: the
+    // largest element's low plane is subnormal, so the planes carry less than an f32
+    // rounding's precision relative to the tensor's maximum).
+    if (live && a != 0.f && (!(aw < 65520.f) || aw < 1.f)) atomicOr(&s_bad, 1);
+  }
+  __syncthreads();
+  // Phase 3: stores.  Slots cleared by the record's wave; the record by thread i; the copy
+  // and the guard by the last thread.
+#pragma unroll
+  for (int k = 0; k < kMax; ++k) {
+    const int i = wv + k * nw;
+    if (i >= n) break;
+    if (!(i >= j.skip_lo && i < j.skip_hi)) s[i].slot[lane].v = 0u;
+  }
+  if (threadIdx.x < n && !(threadIdx.x >= j.skip_lo && threadIdx.x < j.skip_hi)) {
+    const int i = threadIdx.x;
+    const float a = __builtin_bit_cast(float, s_a[i]);
+    const float w0 = s_w0[i], wi0 = s_wi0[i];
+    const bool persistent = i >= j.nt;
+    const float stored = persistent ? wi0 : s_r0[i];  // the read scale of the planes stored now
+    gemm::PScale* rec = s + i;
+    if (a == 0.f) {  // no maximum taken: the scale stays
+      if (persistent) rec->r = rec->rl = stored;
+      else rec->rl = stored;
+    } else {
+      if (!(a * w0 < 65520.f) && j.overflow) atomicOr(j.overflow, 1);
+      const bool finite = a <= 3.0e38f;
+      int shift = -16;  // not finite: the largest reduction of the group, else 2^-16
+      if (!finite) {
+        int mn = 0;
+        for (int k = 0; k < n && k < kMax; ++k) mn = min(mn, s_shift[k]);
+        if (mn < 0) shift = mn;
+      }
+      const int e = finite ? rescale_exp(a) : 0;
+      const float w = finite ? ldexpf(1.f, e) : ldexpf(w0, shift);
+      const float wi = finite ? ldexpf(1.f, -e) : ldexpf(wi0, -shift);
+      rec->w = w;
+      rec->wi = wi;
+      rec->rl = stored;
+      if (persistent) rec->r = stored;
+      else if (!j.defer_r) rec->r = wi;
+    }
+  }
+  if (threadIdx.x == blockDim.x - 1) {
+    if (j.copy_to >= 0) {
+      s[j.copy_to].r = s_cwi;
+      s[j.copy_to].rl = s_cwi;
+    }
+    const RescaleGuard& rg = j.rg;
+    StepGuard* g = rg.g;
+    const uint32_t bad = s_bad ? 1u : 0u;
+    if (g && rg.mode == kRgTarget) {
+      g->t[rg.gate.par & 1] = s_gv[1] | bad;
+      g->tt = 0u;
+    } else if (g && rg.mode == kRgQValues) {
+      g->qv = s_gv[1] | bad;
+      g->tt = 0u;
+    } else if (g && rg.mode == kRgFlag) {
+      if (bad) g->on = 1u;
+    } else if (g && rg.mode == kRgStep) {
+      // The flags (on, prm) are cleared by the step's Adam launch, after every reader.
+      const bool skip = (s_gv[0] | s_gv[2] | bad) != 0u || s_dp > 0.f;
+      g->last = skip ? 1u : 0u;
+      if (skip) {
+        const int64_t k = g->skipped + 1;
+        g->skipped = k;
+        if (rg.host_skipped) *rg.host_skipped = k;
+      } else {
+        g->applied += 1;
+      }
+    } else if (g && rg.mode == kRgClear) {
+      g->on = g->tt = g->prm = g->last = g->qv = 0u;
+      g->t[0] = g->t[1] = 0u;
+    }
+  }
+}
+
+}  // namespace acme

@@ -1,0 +1,146 @@
+"""The bench's data-parallel DQN path (bench.py setup_dqn with WORLD_SIZE 2, what
+`bench.py --gpus 2` runs on every rank) rehearsed on one GPU with two gloo ranks.
+
+Each rank builds exactly the bench's learner: a device-filled uint8 Atari shard
+(fill_synthetic, priorities 1), make_reverb_dataset with prefetch, DQNLearner over
+torch.distributed (global-probability shares, the IS normaliser's MIN all-reduce, the two
+gradient buckets, the ranks' skip gate in the torso bucket).  Checked:
+  * every draw bit-exact against the C oracle's global draw over the two shards (shares
+    from the mass snapshot LAG draws earlier, each shard's own Philox stream), the oracle
+    tables taking the learners' priority write-backs in the dataset's order (draw k is
+    issued after the write-backs of steps < k - prefetch);
+  * both replicas end with bit-identical parameters and no skipped step;
+  * the replicas' parameters equal one learner stepping on the union batch with the
+    reported probabilities, averaged over N * B (free-running, the suite's trajectory bar).
+Reference: the only data-parallel learner of the reference, crr/recurrent_learning.py:346-358
+(mean of the replicas' gradients, then the update); DQNLearner._step
+(agents/tf/dqn/learning.py:112-168).
+"""
+
+import os
+import socket
+import sys
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+WORLD, B, STEPS, SHARD = 2, 32, 4, 1024
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if root not in sys.path:
+        sys.path.insert(0, root)
+    import bench
+    args = SimpleNamespace(batch=B, replay_size=WORLD * SHARD, num_actions=18, prefetch=2,
+                           cpu_baseline_seconds=0.0)
+    step, _, meta, _, _ = bench.setup_dqn(args, WORLD, rank, torch.device("cuda", 0))
+    learner = step.__self__
+    records = []
+
+    class _Rec:
+        def __init__(self, it):
+            self.it = it
+
+        def __iter__(self):
+            return self
+
+        def __next__(self):
+            s = next(self.it)
+            d = s.data
+            records.append(dict(keys=s.info.key.cpu().numpy().view(np.uint64).copy(),
+                                probs=s.info.probability.cpu().numpy().copy(),
+                                rows=[x.cpu().numpy().copy() for x in d[:5]]))
+            return s
+
+        def __getattr__(self, name):  # the dataset's events and frame copy
+            return getattr(self.it, name)
+
+    learner._iterator = _Rec(learner._iterator)
+    prios = []
+    for _ in range(STEPS):
+        step()
+        torch.cuda.synchronize()
+        n = len(records[len(prios)]["keys"])
+        prios.append(learner.native.priorities[:n].cpu().numpy().copy())
+    for rec, pr in zip(records, prios):
+        rec["prios"] = pr
+    q.put((rank, records, learner.native.params.cpu().numpy(), learner.native.guard_state()))
+    dist.destroy_process_group()
+
+
+def test_bench_data_parallel_path_two_ranks():
+    from acme_amd.native import NativeDQN
+    from acme_amd.networks import DQNAtariNetwork
+    from acme_amd.replay.sharding import LAG, allocate_shares
+    from tests._oracle import OracleTable
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(WORLD):
+        r, recs, params, guard = q.get(timeout=300)
+        res[r] = (recs, params, guard)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    np.testing.assert_array_equal(res[0][1], res[1][1])  # replicas identical
+    for r in range(WORLD):
+        assert res[r][2]["skipped"] == 0 and res[r][2]["applied"] == STEPS, res[r][2]
+    # Draws: the bench's shards (priorities 1, seeds 1234 + rank) against the oracle.
+    orc = []
+    for r in range(WORLD):
+        o = OracleTable(SHARD, True, 0.6, 1234 + r)
+        o.insert(np.ones(SHARD))
+        orc.append(o)
+    NB = WORLD * B
+    P = 2  # the bench's prefetch (args.prefetch above)
+    snaps, applied = [], 0
+    for k in range(STEPS):
+        while applied < k - P:  # write-backs of steps < k - P precede draw k
+            for r in range(WORLD):
+                rec = res[r][0][applied]
+                orc[r].update(rec["keys"].astype(np.int64), rec["prios"])
+            applied += 1
+        snaps.append([o.total() for o in orc])  # the mass snapshot after draw k
+        shares = [B] * WORLD if k < LAG else allocate_shares(snaps[k - LAG], NB, cap=2 * B)
+        for r in range(WORLD):
+            rec = res[r][0][k]
+            ref = orc[r].sample(shares[r], k)
+            np.testing.assert_array_equal(rec["keys"], ref["keys"], err_msg=f"step {k} rank {r}")
+            np.testing.assert_array_equal(rec["probs"], ref["probabilities"] * (shares[r] / NB))
+    # One learner on the union batches, mean over N * B (the bench's learner settings).
+    net = DQNAtariNetwork(18)
+    d = NativeDQN(network="nature", num_actions=18, max_batch=2 * NB, obs_dtype="uint8",
+                  discount=0.99, importance_sampling_exponent=0.2, learning_rate=1e-3,
+                  target_update_period=100)
+    d.set_params(net.init(0), net.init(1))
+    for k in range(STEPS):
+        cols = [np.concatenate([res[r][0][k]["rows"][c] for r in range(WORLD)]) for c in range(5)]
+        probs = np.concatenate([res[r][0][k]["probs"] for r in range(WORLD)])
+        dev = [torch.as_tensor(x).cuda().contiguous() for x in cols + [probs]]
+        d.step(*dev)
+    torch.cuda.synchronize()
+    got = d.params.cpu().numpy()
+    np.testing.assert_allclose(res[0][1], got, rtol=1e-5, atol=1e-3 + 1e-6)
+    assert np.mean(np.abs(res[0][1] - got) <= 1e-5 * np.abs(got) + 1e-6) > 0.98
