@@ -100,6 +100,22 @@ class IMPALAConfig(ctypes.Structure):
                 ("adam_beta2", c_f32), ("adam_epsilon", c_f32), ("semantics", c_i32)]
 
 
+class R2D2Config(ctypes.Structure):
+    _fields_ = [("torso", c_i32), ("obs_dim", c_i32), ("num_actions", c_i32),
+                ("max_batch", c_i32), ("max_sequence_length", c_i32), ("burn_in_length", c_i32),
+                ("lstm_size", c_i32), ("head_size", c_i32), ("n_step", c_i32),
+                ("store_lstm_state", c_i32), ("target_update_period", c_i32),
+                ("reserved", c_i32), ("max_replay_size", c_i64),
+                ("max_priority_weight", ctypes.c_double), ("discount", c_f32),
+                ("importance_sampling_exponent", c_f32),
+                ("learning_rate", c_f32), ("adam_beta1", c_f32), ("adam_beta2", c_f32),
+                ("adam_epsilon", c_f32)]
+
+
+class R2D2Outputs(ctypes.Structure):
+    _fields_ = [("loss", c_vp), ("errors", c_vp), ("priorities", c_vp)]
+
+
 class SequenceBatch(ctypes.Structure):
     _fields_ = [("observation", c_vp), ("prev_action", c_vp), ("prev_reward", c_vp),
                 ("action", c_vp), ("reward", c_vp), ("discount", c_vp),
@@ -202,6 +218,20 @@ _SIGS = {
                                       ctypes.POINTER(c_i64)]),
     "acme_dqn_set_num_steps": (c_i32, [c_vp, c_i64]),
     "acme_min_f64": (c_i32, [c_vp, c_i64, c_vp, c_vp]),
+    "acme_r2d2_create": (c_i32, [ctypes.POINTER(R2D2Config), ctypes.POINTER(c_vp)]),
+    "acme_r2d2_destroy": (c_i32, [c_vp]),
+    "acme_r2d2_flat_size": (c_i64, [c_vp]),
+    "acme_r2d2_num_tensors": (c_i32, [c_vp]),
+    "acme_r2d2_tensor_info": (c_i32, [c_vp, c_i32, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64),
+                                      ctypes.POINTER(c_i32), ctypes.POINTER(c_i64),
+                                      ctypes.POINTER(ctypes.c_char_p)]),
+    "acme_r2d2_bind": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "acme_r2d2_step": (c_i32, [c_vp, ctypes.POINTER(SequenceBatch), c_vp,
+                               ctypes.POINTER(R2D2Outputs), c_vp]),
+    "acme_r2d2_num_steps": (c_i64, [c_vp]),
+    "acme_r2d2_set_num_steps": (c_i32, [c_vp, c_i64]),
+    "acme_r2d2_debug_buffer": (c_i32, [c_vp, ctypes.c_char_p, ctypes.POINTER(c_vp),
+                                       ctypes.POINTER(c_i64)]),
     "acme_impala_create": (c_i32, [ctypes.POINTER(IMPALAConfig), ctypes.POINTER(c_vp)]),
     "acme_impala_destroy": (c_i32, [c_vp]),
     "acme_impala_flat_size": (c_i64, [c_vp]),
@@ -221,6 +251,7 @@ _SIGS = {
     "acme_impala_set_scale_state": (c_i32, [c_vp, c_vp, c_i32]),
     "acme_impala_policy_step": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
                                         c_vp, c_vp, c_vp]),
+    "acme_impala_set_policy_planes": (c_i32, [c_vp, c_i32]),
     "acme_impala_num_steps": (c_i64, [c_vp]),
     "acme_impala_set_num_steps": (c_i32, [c_vp, c_i64]),
     "acme_impala_debug_buffer": (c_i32, [c_vp, ctypes.c_char_p, ctypes.POINTER(c_vp),

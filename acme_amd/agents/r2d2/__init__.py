@@ -5,8 +5,8 @@ sequence dataset the agent wires up (agents/tf/r2d2/agent.py:72-103), and the le
 two replay-facing computations as device kernels (csrc/r2d2.hip):
   compute_priority     learning.py:230-236 (written back with update_priorities, :196-199)
   importance_weights   learning.py:178-183
-The R2D2 learner itself (recurrent Q-network, burn-in, transformed n-step loss) is not
-part of this build; these are the pieces that let a learner drive the GPU sequence table.
+and the learner itself, R2D2Learner (learning.py: csrc/r2d2_learner.hip, the recurrent
+duelling Q-network with burn-in and the transformed n-step loss).
 """
 
 from __future__ import annotations
@@ -18,6 +18,7 @@ import torch
 from acme_amd import replay
 from acme_amd.adders import reverb as adders
 from acme_amd.datasets import make_reverb_dataset
+from acme_amd.agents.r2d2.learning import R2D2Learner  # noqa: F401
 
 
 def _check(name, t, dtype):

@@ -80,6 +80,9 @@ struct acme_impala {
   unsigned long long* xb = nullptr;
   unsigned* tmo = nullptr;
   bool lstm_steps = false;
+  // Policy steps of an actor-side network on the plane engine (acme_impala_set_policy_planes):
+  // the torso and W_i on f16 planes, the records rescaled after every call.
+  bool policy_planes = false;
   unsigned lstm_epoch = 0;
   // Plane path of the Atari learner step (the DQN kernels: scaled two-plane f16 MFMA):
   // parameter planes of the torso + W_i prefix of the flat buffer, refreshed at the start
@@ -1351,10 +1354,28 @@ int acme_impala_policy_step(acme_impala* l, const void* obs, const int32_t* prev
                  "rows must be in [1, max_batch=%d]", l->cfg.max_batch);
   hipStream_t st = as_stream(stream);
   const int H = l->H, A = l->A;
-  // The policy's unroll has its own timeout word (a learner step is not skipped for it).
-  int rc = network_forward(l, obs, prev_action, prev_reward, h, c, H, (int)rows, 1, st, false,
-                           l->tmo + 2);
-  if (rc != ACME_OK) return rc;
+  const bool p3 = l->policy_planes && atari(l) && use_p3(l, (int)rows);
+  auto forward = [&]() {
+    // The policy's unroll has its own timeout word (a learner step is not skipped for it).
+    int rc = network_forward(l, obs, prev_action, prev_reward, h, c, H, (int)rows, 1, st, p3,
+                             l->tmo + 2);
+    if (rc != ACME_OK || !p3) return rc;
+    // The next call's scales from this call's maxima (lagged, 2^8 of headroom); a plane
+    // write that overflowed shows in acme_impala_plane_overflow.
+    RescaleGuard rg;
+    return launch_plane_rescale(l->scales, kScTransient, kScTransient, -1, -1, l->overflow, st,
+                                -1, -1, rg);
+  };
+  int rc;
+  if (p3 && !l->scales_ok) {
+    // First call (or new parameters): three passes set the chain frames -> x1 -> x2 -> x3
+    // (and the parameter planes) from real maxima before the call whose outputs count.
+    for (int pass = 0; pass < 3; ++pass)
+      if ((rc = forward()) != ACME_OK) return rc;
+    ACME_HIP_TRY(hipMemsetAsync(l->overflow, 0, sizeof(int), st));
+    l->scales_ok = true;
+  }
+  if ((rc = forward()) != ACME_OK) return rc;
   // Outputs are rows of the T = 1 unroll.
   if (logits)
     ACME_HIP_TRY(hipMemcpy2DAsync(logits, A * sizeof(float), l->pv, (A + 1) * sizeof(float),
@@ -1366,6 +1387,13 @@ int acme_impala_policy_step(acme_impala* l, const void* obs, const int32_t* prev
     ACME_HIP_TRY(hipMemcpyAsync(h_out, l->h, rows * H * sizeof(float), hipMemcpyDeviceToDevice, st));
   if (c_out)
     ACME_HIP_TRY(hipMemcpyAsync(c_out, l->c, rows * H * sizeof(float), hipMemcpyDeviceToDevice, st));
+  return ACME_OK;
+}
+
+int acme_impala_set_policy_planes(acme_impala* l, int32_t on) {
+  ACME_CHECK_ARG(l, "null learner");
+  l->policy_planes = on != 0;
+  l->scales_ok = false;
   return ACME_OK;
 }
 

@@ -208,15 +208,43 @@ __global__ void __launch_bounds__(256) lstm_fwd_step_kernel(
       }
     }
   } else {
-    for (int e = threadIdx.x; e < nh4; e += blockDim.x) {
-      const int b = e / (H / 4), k = 4 * (e % (H / 4));
-      *reinterpret_cast<f32x4*>(hs + (size_t)b * H + k) =
-          *reinterpret_cast<const f32x4*>(hp + (size_t)b * hp_stride + k);
+    // Larger staging (R2D2's H = 512 over tens of rows): rounds of kStageBatch float4 per
+    // thread, every load of a round issued before its stores (a load-store pair per
+    // iteration paid one memory latency per float4: 25 us per step at B 32, H 512).
+    constexpr int kStageBatch = 8;
+    for (int e0 = threadIdx.x; e0 < nh4; e0 += 256 * kStageBatch) {
+      f32x4 v[kStageBatch];
+#pragma unroll
+      for (int q = 0; q < kStageBatch; ++q) {
+        const int e = min(e0 + 256 * q, nh4 - 1);
+        const int b = e / (H / 4), k = 4 * (e % (H / 4));
+        v[q] = *reinterpret_cast<const f32x4*>(hp + (size_t)b * hp_stride + k);
+      }
+#pragma unroll
+      for (int q = 0; q < kStageBatch; ++q) {
+        const int e = e0 + 256 * q;
+        if (e < nh4) {
+          const int b = e / (H / 4), k = 4 * (e % (H / 4));
+          *reinterpret_cast<f32x4*>(hs + (size_t)b * H + k) = v[q];
+        }
+      }
     }
-    for (int e = threadIdx.x; e < nw4; e += blockDim.x) {
-      const int k = e / 4, g = e % 4;
-      *reinterpret_cast<f32x4*>(ws + (size_t)k * NC + g * kFwdUnits) =
-          *reinterpret_cast<const f32x4*>(wh + (size_t)k * 4 * H + g * H + u0);
+    for (int e0 = threadIdx.x; e0 < nw4; e0 += 256 * kStageBatch) {
+      f32x4 v[kStageBatch];
+#pragma unroll
+      for (int q = 0; q < kStageBatch; ++q) {
+        const int e = min(e0 + 256 * q, nw4 - 1);
+        const int k = e / 4, g = e % 4;
+        v[q] = *reinterpret_cast<const f32x4*>(wh + (size_t)k * 4 * H + g * H + u0);
+      }
+#pragma unroll
+      for (int q = 0; q < kStageBatch; ++q) {
+        const int e = e0 + 256 * q;
+        if (e < nw4) {
+          const int k = e / 4, g = e % 4;
+          *reinterpret_cast<f32x4*>(ws + (size_t)k * NC + g * kFwdUnits) = v[q];
+        }
+      }
     }
   }
   __syncthreads();
@@ -307,8 +335,11 @@ __global__ void __launch_bounds__(256) lstm_bwd_step_kernel(
     x.dc = dc_carry[(size_t)b * H + j];
     return x;
   };
-  const CellIn first = cell_in(0);
-  for (int b0 = 0; b0 < B; b0 += kRowChunk) {
+  // grid.y > 1: workgroup y takes the row chunks y, y + gridDim.y, ... (more workgroups in
+  // flight for a long batch; the IMPALA learner launches one).
+  const int bfirst = blockIdx.y * kRowChunk;
+  const CellIn first = cell_in(bfirst);
+  for (int b0 = bfirst; b0 < B; b0 += gridDim.y * kRowChunk) {
     float acc[kRowChunk];
 #pragma unroll
     for (int i = 0; i < kRowChunk; ++i) acc[i] = 0.f;
@@ -373,7 +404,7 @@ __global__ void __launch_bounds__(256) lstm_bwd_step_kernel(
         for (int s2 = 0; s2 < KS; ++s2) dhn += red[uu][i][s2];
         const int j = u0 + uu;
         const size_t row = (size_t)b * rs_b + (size_t)t * rs_t;
-        const CellIn x = b0 == 0 ? first : cell_in(b0);
+        const CellIn x = b0 == bfirst ? first : cell_in(b0);
         const float ig = x.ig, fg = x.fg, gg = x.gg, og = x.og;
         const float cn = x.cn, cprev = x.cprev;
         const float tc = tanhf(cn);

@@ -903,6 +903,11 @@ class NativeIMPALA:
             check(lib().acme_impala_set_scale_state(self._h, a.ctypes.data, a.size),
                   "impala set_scale_state")
 
+    def set_policy_planes(self, on: bool = True) -> None:
+        """Policy steps (>= 64 rows, Atari torso) on the plane engine: for actor-side networks
+        that only run policy steps (acme_impala_set_policy_planes)."""
+        check(lib().acme_impala_set_policy_planes(self._h, 1 if on else 0), "policy planes")
+
     def set_lstm_unroll(self, per_step: bool) -> None:
         """Per-step LSTM launches instead of the one-launch unroll (tests compare the two)."""
         check(lib().acme_impala_set_lstm_unroll(self._h, 1 if per_step else 0), "lstm unroll")
@@ -952,3 +957,147 @@ class NativeIMPALA:
             ptr(prev_reward.contiguous()), ptr(h.contiguous()), ptr(c.contiguous()), rows,
             *[ptr(o) for o in out], stream_ptr(stream)), "impala policy_step")
         return tuple(out)
+
+
+class NativeR2D2:
+    """acme_r2d2 learner + its flat buffers (params, target, grads, Adam m / v):
+    R2D2Learner._step (acme/agents/tf/r2d2/learning.py:112-200) on R2D2AtariNetwork."""
+
+    def __init__(self, *, num_actions: int, max_batch: int, max_sequence_length: int,
+                 burn_in_length: int, torso: str = "atari", obs_dim: int = 0,
+                 lstm_size: int = 512, head_size: int = 512, n_step: int = 5,
+                 discount: float = 0.99, importance_sampling_exponent: float = 0.2,
+                 max_replay_size: int = 1_000_000, max_priority_weight: float = 0.9,
+                 target_update_period: int = 100, learning_rate: float = 1e-3,
+                 adam_beta1: float = 0.9, adam_beta2: float = 0.999, adam_epsilon: float = 1e-3,
+                 store_lstm_state: bool = True, device=None):
+        """Defaults are R2D2Learner's (learning.py:47-66; snt.Adam epsilon 1e-3, :78)."""
+        _lib.require_gpu()
+        cfg = _lib.R2D2Config()
+        cfg.torso = _lib.IMPALA_TORSO_ATARI if torso == "atari" else _lib.IMPALA_TORSO_FLAT
+        cfg.obs_dim, cfg.num_actions = int(obs_dim), int(num_actions)
+        cfg.max_batch, cfg.max_sequence_length = int(max_batch), int(max_sequence_length)
+        cfg.burn_in_length = int(burn_in_length)
+        cfg.lstm_size, cfg.head_size, cfg.n_step = int(lstm_size), int(head_size), int(n_step)
+        cfg.store_lstm_state = 1 if store_lstm_state else 0
+        cfg.target_update_period = int(target_update_period)
+        cfg.max_replay_size = int(max_replay_size)
+        cfg.discount = discount
+        cfg.importance_sampling_exponent = importance_sampling_exponent
+        cfg.max_priority_weight = max_priority_weight
+        cfg.learning_rate = learning_rate
+        cfg.adam_beta1, cfg.adam_beta2, cfg.adam_epsilon = adam_beta1, adam_beta2, adam_epsilon
+        self.cfg = cfg
+        self.torso, self.obs_dim = torso, int(obs_dim)
+        self.num_actions, self.lstm_size = int(num_actions), int(lstm_size)
+        self.max_batch, self.max_sequence_length = int(max_batch), int(max_sequence_length)
+        self.burn_in_length = int(burn_in_length)
+        self.store_lstm_state = bool(store_lstm_state)
+        self.device = torch.device(device or "cuda")
+        h = ctypes.c_void_p()
+        L = lib()
+        with torch.cuda.device(self.device):
+            check(L.acme_r2d2_create(ctypes.byref(cfg), ctypes.byref(h)), "r2d2 create")
+        self._h = h
+        self.flat_size = int(L.acme_r2d2_flat_size(h))
+        self.tensors: List[Tuple[str, int, Tuple[int, ...]]] = []
+        for i in range(L.acme_r2d2_num_tensors(h)):
+            off, numel, nd = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int32()
+            shape = (ctypes.c_int64 * 4)()
+            name = ctypes.c_char_p()
+            check(L.acme_r2d2_tensor_info(h, i, ctypes.byref(off), ctypes.byref(numel),
+                                          ctypes.byref(nd), shape, ctypes.byref(name)))
+            self.tensors.append((name.value.decode(), int(off.value),
+                                 tuple(int(shape[k]) for k in range(nd.value))))
+        z = lambda: torch.zeros(self.flat_size, dtype=torch.float32, device=self.device)  # noqa
+        self.params, self.target, self.grads, self.m, self.v = z(), z(), z(), z(), z()
+        check(L.acme_r2d2_bind(h, ptr(self.params), ptr(self.target), ptr(self.grads),
+                               ptr(self.m), ptr(self.v)), "r2d2 bind")
+        T, B = self.max_sequence_length, self.max_batch
+        self.loss = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self._errors = torch.zeros(max(T - self.burn_in_length - 1, 1) * B, dtype=torch.float32,
+                                   device=self.device)
+        self._last = (1, B)
+        self.priorities = torch.zeros(B, dtype=torch.float64, device=self.device)
+
+    @property
+    def errors(self) -> torch.Tensor:
+        """The last step's errors [T - burn_in - 1, B] (time-major, extra.errors)."""
+        tm, b = self._last
+        return self._errors[:tm * b].view(tm, b)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                lib().acme_r2d2_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    views = NativeDQN.views
+    get_params = NativeDQN.get_params
+
+    def set_params(self, params: Dict[str, np.ndarray], target: Dict[str, np.ndarray]) -> None:
+        for buf, src in ((self.params, params), (self.target, target)):
+            for name, t in self.views(buf).items():
+                t.copy_(torch.as_tensor(np.asarray(src[name], np.float32)).view(t.shape))
+
+    @property
+    def num_steps(self) -> int:
+        return int(lib().acme_r2d2_num_steps(self._h))
+
+    @num_steps.setter
+    def num_steps(self, n: int) -> None:
+        check(lib().acme_r2d2_set_num_steps(self._h, int(n)))
+
+    def debug_buffer(self, name: str) -> np.ndarray:
+        p, n = ctypes.c_void_p(), ctypes.c_int64()
+        check(lib().acme_r2d2_debug_buffer(self._h, name.encode(), ctypes.byref(p),
+                                           ctypes.byref(n)))
+        return _device_array(p.value, n.value, np.float32, self.device).cpu().numpy().view(
+            np.float32).copy()
+
+    def step(self, observation, prev_action, prev_reward, action, reward, discount,
+             probabilities, h0=None, c0=None, stream=None):
+        """Batch-major [B, T, ...] device tensors (the sequence dataset's layout: the OAR
+        observation's frames, previous action and reward; action, reward, discount), the
+        sample's probabilities [B] (f64) and the core state at t = 0 (h0 / c0 [B, H] views
+        with unit inner stride; ignored with store_lstm_state=False).  Loss, errors
+        [T - burn_in - 1, B] and priorities [B] land in .loss / .errors / .priorities."""
+        B, T = int(action.shape[0]), int(action.shape[1])
+        want = torch.uint8 if self.torso == "atari" else torch.float32
+        checks = (("observation", observation, want), ("prev_action", prev_action, torch.int32),
+                  ("prev_reward", prev_reward, torch.float32), ("action", action, torch.int32),
+                  ("reward", reward, torch.float32), ("discount", discount, torch.float32))
+        for name, t, dt in checks:
+            if not (isinstance(t, torch.Tensor) and t.is_cuda and t.is_contiguous()
+                    and t.dtype == dt):
+                raise ValueError(f"{name} must be a contiguous {dt} device tensor")
+            if tuple(t.shape[:2]) != (B, T):
+                raise ValueError(f"{name} has shape {tuple(t.shape)}, expected [{B}, {T}, ...]")
+        if not (probabilities.is_cuda and probabilities.dtype == torch.float64
+                and probabilities.is_contiguous() and probabilities.numel() == B):
+            raise ValueError(f"probabilities must be a contiguous float64 [{B}] device tensor")
+        b = _lib.SequenceBatch()
+        b.observation, b.prev_action, b.prev_reward = ptr(observation), ptr(prev_action), ptr(prev_reward)
+        b.action, b.reward, b.discount = ptr(action), ptr(reward), ptr(discount)
+        b.behaviour_logits = None
+        if self.store_lstm_state:
+            for name, t in (("h0", h0), ("c0", c0)):
+                if (t is None or t.dtype != torch.float32 or t.shape != (B, self.lstm_size)
+                        or t.stride(1) != 1):
+                    raise ValueError(f"{name} must be float32 [{B}, {self.lstm_size}] with unit "
+                                     "inner stride")
+            if h0.stride(0) != c0.stride(0):
+                raise ValueError("h0 and c0 must share a row stride")
+            b.h0, b.c0, b.state_stride = ptr(h0), ptr(c0), int(h0.stride(0))
+        else:
+            b.h0 = b.c0 = None
+            b.state_stride = self.lstm_size
+        b.batch, b.sequence_length = B, T
+        o = _lib.R2D2Outputs()
+        o.loss, o.errors, o.priorities = ptr(self.loss), ptr(self._errors), ptr(self.priorities)
+        self._last = (T - self.burn_in_length - 1, B)
+        check(lib().acme_r2d2_step(self._h, ctypes.byref(b), ptr(probabilities), ctypes.byref(o),
+                                   stream_ptr(stream)), "r2d2 step")

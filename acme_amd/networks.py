@@ -338,3 +338,52 @@ class IMPALAAtariNetwork:
     def initial_state(self, batch_size: int) -> LSTMState:
         z = np.zeros((batch_size, self.lstm_size), np.float32)
         return LSTMState(z, z.copy())
+
+
+# ------------------------------------------------------------------ R2D2 (Atari)
+
+
+@dataclasses.dataclass(frozen=True)
+class R2D2AtariNetwork:
+    """R2D2AtariNetwork (acme/tf/networks/atari.py:72-112): OAREmbedding(AtariTorso) ->
+    snt.LSTM(lstm_size) -> DuellingMLP(num_actions, [head_size]) (duelling.py:26-59).  The
+    duelling MLP's two first layers are one fused [lstm_size, 2 head_size] tensor
+    [value | advantage] (as DQNAtariNetwork's).  torso="flat": the identity over a float
+    observation vector of obs_dim features."""
+
+    num_actions: int
+    lstm_size: int = 512
+    head_size: int = 512
+    torso: str = "atari"
+    obs_dim: int = 0
+
+    @property
+    def feat(self) -> int:
+        return 7744 if self.torso == "atari" else self.obs_dim
+
+    @property
+    def obs_dtype(self) -> str:
+        return "uint8" if self.torso == "atari" else "float32"
+
+    def tensor_shapes(self):
+        H, H2, A = self.lstm_size, self.head_size, self.num_actions
+        pre = "r2d2_atari_network"
+        out = []
+        if self.torso == "atari":
+            out += [(f"{pre}/atari_torso/conv2_d/w", (8, 8, 4, 32)),
+                    (f"{pre}/atari_torso/conv2_d/b", (32,)),
+                    (f"{pre}/atari_torso/conv2_d_1/w", (4, 4, 32, 64)),
+                    (f"{pre}/atari_torso/conv2_d_1/b", (64,)),
+                    (f"{pre}/atari_torso/conv2_d_2/w", (3, 3, 64, 64)),
+                    (f"{pre}/atari_torso/conv2_d_2/b", (64,))]
+        D = self.feat + A + 1
+        q = f"{pre}/duelling_q_network"
+        out += [(f"{pre}/lstm/w_i", (D, 4 * H)), (f"{pre}/lstm/w_h", (H, 4 * H)),
+                (f"{pre}/lstm/b", (4 * H,)),
+                (f"{q}/hidden/w", (H, 2 * H2)), (f"{q}/hidden/b", (2 * H2,)),
+                (f"{q}/mlp/linear_1/w", (H2, 1)), (f"{q}/mlp/linear_1/b", (1,)),
+                (f"{q}/mlp_1/linear_1/w", (H2, A)), (f"{q}/mlp_1/linear_1/b", (A,))]
+        return out
+
+    init = IMPALAAtariNetwork.init
+    initial_state = IMPALAAtariNetwork.initial_state

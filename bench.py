@@ -44,7 +44,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--workload", choices=("dqn", "d4pg", "impala", "impala_actors", "insert"),
+    p.add_argument("--workload", choices=("dqn", "d4pg", "impala", "impala_actors", "insert",
+                                          "r2d2"),
                    default="dqn",
                    help="dqn: the headline config (BASELINE configs[1]); d4pg: configs[2]; "
                         "impala: configs[3] (learner side); impala_actors: configs[3] end to "
@@ -509,6 +510,95 @@ def setup_impala(args, world, rank, dev):
             lambda: impala_cpu_baseline(B, T, args.cpu_baseline_seconds))
 
 
+def r2d2_cpu_baseline(B: int, T: int, burn_in: int, seconds: float):
+    """The numpy R2D2 oracle (oracle/r2d2_oracle.py, float32) on a bounded sample: B
+    sequences of the workload's T = burn-in + trace + 1 Atari frames, as many full learner
+    steps as fit in `seconds` (at least 2; the first is a warm-up)."""
+    from oracle import r2d2_oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    try:
+        from threadpoolctl import threadpool_limits
+        ctx = threadpool_limits(threads)
+    except ImportError:  # pragma: no cover
+        ctx = None
+    rng = np.random.default_rng(0)
+    A, H = 18, 512
+    batch = dict(obs=rng.integers(0, 256, (B, T, 84, 84, 4), dtype=np.uint8),
+                 prev_action=rng.integers(0, A, (B, T)).astype(np.int32),
+                 prev_reward=rng.standard_normal((B, T)).astype(np.float32),
+                 action=rng.integers(0, A, (B, T)).astype(np.int32),
+                 reward=rng.standard_normal((B, T)).astype(np.float32),
+                 discount=np.full((B, T), 1.0, np.float32),
+                 h0=np.zeros((B, H), np.float32), c0=np.zeros((B, H), np.float32),
+                 probabilities=np.full(B, 1e-4))
+    cfg = O.R2D2Config(num_actions=A, burn_in_length=burn_in)
+    from acme_amd.networks import R2D2AtariNetwork
+    p = R2D2AtariNetwork(A).init(0)
+    z = {k: np.zeros_like(v) for k, v in p.items()}
+    state = dict(params=p, target=dict(p), m=z, v=dict(z), num_steps=0)
+    state = O.r2d2_step(cfg, state, batch, np.float32)[2]
+    t0 = time.perf_counter()
+    n = 0
+    while n < 2 or time.perf_counter() - t0 < seconds:
+        state = O.r2d2_step(cfg, state, batch, np.float32)[2]
+        n += 1
+    dt = time.perf_counter() - t0
+    if ctx is not None and hasattr(ctx, "unregister"):
+        ctx.unregister()
+    return dict(value=round(B * n / dt, 3), unit="sequences/s", cores=threads, kind="port",
+                sample=(f"numpy float32 oracle (oracle/r2d2_oracle.py), {n} timed steps of "
+                        f"B={B} x T={T} Atari sequences (burn-in {burn_in}), {threads} BLAS "
+                        f"threads, {cpu_model()}"))
+
+
+def setup_r2d2(args, world, rank, dev):
+    """R2D2 widening: R2D2AtariNetwork (LSTM 512, duelling [512], 18
+    actions), batch 32 sequences (the agent's default, agents/tf/r2d2/agent.py:55) of
+    burn-in 40 + trace 80 + 1 = 121 frames (the R2D2 paper's Atari setting), n = 5.
+    Synthetic sequences from a device-resident pool of 2 batches; each step consumes the
+    next one and writes its priorities to a device buffer."""
+    from acme_amd.native import NativeR2D2
+    from acme_amd.networks import R2D2AtariNetwork
+    if world > 1:
+        raise SystemExit("the R2D2 workload is single-GPU")
+    B, BI, TR, A, H = args.batch or 32, 40, 80, 18, 512
+    T = BI + TR + 1
+    pool = 2
+    g = torch.Generator(device=dev).manual_seed(rank)
+    obs = torch.randint(0, 256, (pool, B, T, 84, 84, 4), dtype=torch.uint8, device=dev, generator=g)
+    ia = lambda: torch.randint(0, A, (pool, B, T), dtype=torch.int32, device=dev, generator=g)  # noqa
+    fl = lambda *s: torch.randn(*s, device=dev, generator=g)  # noqa
+    prev_a, act = ia(), ia()
+    prev_r, rew = fl(pool, B, T), fl(pool, B, T)
+    disc = torch.where(torch.rand(pool, B, T, device=dev, generator=g) < 0.01, 0.0, 1.0)
+    state = 0.1 * fl(pool, B, T, 2, H)
+    probs = (torch.rand(pool, B, device=dev, generator=g, dtype=torch.float64) + 0.5) * 1e-5
+    net = R2D2AtariNetwork(A)
+    n = NativeR2D2(num_actions=A, max_batch=B, max_sequence_length=T, burn_in_length=BI,
+                   device=dev)
+    n.set_params(net.init(0), net.init(1))
+    it = [0]
+
+    def step():
+        i = it[0] % pool
+        it[0] += 1
+        n.step(obs[i], prev_a[i], prev_r[i], act[i], rew[i], disc[i], probs[i],
+               state[i][:, 0, 0], state[i][:, 0, 1])
+
+    meta = dict(
+        metric=f"learner sequences/sec (B={B} x T={T}, burn-in {BI}) R2D2 Atari, 1 MI355X",
+        unit="sequences/s", dtype="f32 (x6 split-bf16 MFMA GEMMs, f32 LSTM cell)",
+        _roofline_exclude=("r2d2_lstm_fwd", "r2d2_lstm_bwd"),
+        data="synthetic (device-generated uint8 Atari sequences in a device-resident pool, "
+             "random-init R2D2AtariNetwork)",
+        config={"workload": "r2d2_atari_lstm_transformed_nstep (SURVEY §8(f) widening)",
+                "batch_sequences": B, "sequence_length": T, "burn_in": BI, "n_step": 5,
+                "frames_per_step": B * T, "obs": "uint8[84,84,4]", "num_actions": A,
+                "lstm": H, "parallelism": "dp1"})
+    return (step, B, meta, lambda: float(n.loss[0].item()),
+            lambda: r2d2_cpu_baseline(2, T, BI, args.cpu_baseline_seconds))
+
+
 IMPALA_T, IMPALA_A, IMPALA_H = 20, 18, 256
 
 
@@ -782,7 +872,8 @@ def main():
             impala_actors_bench(args, dev, pool)
         return
     t_fill = time.perf_counter()
-    setup = {"dqn": setup_dqn, "d4pg": setup_d4pg, "impala": setup_impala}[args.workload]
+    setup = {"dqn": setup_dqn, "d4pg": setup_d4pg, "impala": setup_impala,
+             "r2d2": setup_r2d2}[args.workload]
     step, B, meta, loss_fn, cpu_fn = setup(args, world, rank, dev)
     torch.cuda.synchronize(dev)
     t_fill = time.perf_counter() - t_fill

@@ -623,12 +623,76 @@ int acme_impala_policy_step(acme_impala* l, const void* obs, const int32_t* prev
                             const float* prev_reward, const float* h, const float* c,
                             int64_t rows, float* logits, float* values, float* h_out,
                             float* c_out, void* stream);
+/* Policy steps of this (actor-side) network on the plane engine: torso and W_i read f16
+ * planes (the learner's f32-equivalent engine, csrc/gemm_p3.h) at scales rescaled after
+ * every call from its maxima (calibrated by three passes on the first call); at least 64
+ * rows.  For networks that run policy steps only: a learner's own scales are its steps'. */
+int acme_impala_set_policy_planes(acme_impala* l, int32_t on);
 int64_t acme_impala_num_steps(const acme_impala* l);
 int acme_impala_set_num_steps(acme_impala* l, int64_t n);
 /* "logits" "values" [B*T] batch-major rows, "vs" "pg_adv" [(T-1)*B] time-major,
  * "h" [B*T, H], "dpv" [B*T, A+1], "grad_norm" [1]. */
 int acme_impala_debug_buffer(const acme_impala* l, const char* name, const float** out,
                              int64_t* count);
+
+/* ------------------------------------------------------------------ R2D2 -- */
+/* Replaces R2D2Learner._step (acme/agents/tf/r2d2/learning.py:112-200) with
+ * R2D2AtariNetwork (acme/tf/networks/atari.py:72-112): OAREmbedding(AtariTorso, or the
+ * observation vector with ACME_IMPALA_TORSO_FLAT) -> snt.LSTM(lstm_size) ->
+ * DuellingMLP(num_actions, [head_size]) (duelling.py:26-59; its two first layers are one
+ * fused [lstm_size, 2 head_size] tensor [value | advantage], as the DQN learner's).  The
+ * step: burn-in of both networks over the first burn_in_length steps from the stored core
+ * state (no gradient), online and target unrolls over the rest, greedy double-Q
+ * transformed n-step loss (losses/r2d2.py:29-169), importance weights (1 / (N p))^beta
+ * / max, snt.Adam(learning_rate, epsilon = adam_epsilon), target <- online when
+ * num_steps % target_update_period == 0 after the update, priorities eta max_t |e| +
+ * (1 - eta) mean_t |e| (learning.py:230-236). */
+typedef struct acme_r2d2 acme_r2d2;
+
+typedef struct acme_r2d2_config {
+  int32_t torso;                /* ACME_IMPALA_TORSO_ATARI or ACME_IMPALA_TORSO_FLAT */
+  int32_t obs_dim;              /* FLAT torso only */
+  int32_t num_actions;
+  int32_t max_batch;            /* sequences per step (B) */
+  int32_t max_sequence_length;  /* T = burn_in + trace + 1, <= 256 */
+  int32_t burn_in_length;
+  int32_t lstm_size;            /* multiple of 8 (512 in R2D2AtariNetwork) */
+  int32_t head_size;            /* multiple of 8 (512) */
+  int32_t n_step;               /* bootstrap_n (learning.py:65: 5) */
+  int32_t store_lstm_state;     /* 1: core state from extras (h0 / c0), 0: zeros */
+  int32_t target_update_period;
+  int32_t reserved;
+  int64_t max_replay_size;      /* N of the importance weights */
+  double max_priority_weight;   /* eta; eta and 1 - eta are rounded to f32 from double */
+  float discount, importance_sampling_exponent;
+  float learning_rate, adam_beta1, adam_beta2, adam_epsilon;  /* epsilon 1e-3 (:78) */
+} acme_r2d2_config;
+
+typedef struct acme_r2d2_outputs {
+  float* loss;          /* [1] (optional) */
+  float* errors;        /* [T - burn_in - 1][B] time-major, extra.errors (optional) */
+  double* priorities;   /* [B] (optional) */
+} acme_r2d2_outputs;
+
+int acme_r2d2_create(const acme_r2d2_config* cfg, acme_r2d2** out);
+int acme_r2d2_destroy(acme_r2d2* l);
+int64_t acme_r2d2_flat_size(const acme_r2d2* l);
+int32_t acme_r2d2_num_tensors(const acme_r2d2* l);
+int acme_r2d2_tensor_info(const acme_r2d2* l, int32_t i, int64_t* offset, int64_t* numel,
+                          int32_t* ndim, int64_t* shape4, const char** name);
+int acme_r2d2_bind(acme_r2d2* l, float* params, float* target, float* grads, float* adam_m,
+                   float* adam_v);
+/* One learner step on a batch of sequences (acme_sequence_batch: batch-major [B, T] fields;
+ * behaviour_logits unused; h0 / c0 = extras['core_state'] at t = 0) with the sample's
+ * probabilities [B] (f64). */
+int acme_r2d2_step(acme_r2d2* l, const acme_sequence_batch* batch, const double* probabilities,
+                   const acme_r2d2_outputs* out, void* stream);
+int64_t acme_r2d2_num_steps(const acme_r2d2* l);
+int acme_r2d2_set_num_steps(acme_r2d2* l, int64_t n);
+/* "q" / "target_q" [(T - burn_in) * B, A] time-major suffix rows, "h" [T * B, H]
+ * time-major, "g" [(T - burn_in) * B] d loss / d q[a], "hid", "x1" "x2" "x3". */
+int acme_r2d2_debug_buffer(const acme_r2d2* l, const char* name, const float** out,
+                           int64_t* count);
 
 /* ----------------------------------------------------------- elementwise ops -- */
 

@@ -182,6 +182,30 @@ def test_policy_step_matches_unroll():
     _close(c.cpu().numpy(), cache["cs"][:, 0], name="c")
 
 
+def test_policy_step_on_planes_matches_oracle():
+    """The actor-side policy step on the plane engine (acme_impala_set_policy_planes: Atari
+    torso and W_i on f16 planes, scales calibrated on the first call and rescaled after each)
+    against the f64 forward, for two consecutive 64-row calls (the second at the scales the
+    first one set), with no plane overflow."""
+    cfg = O.IMPALAConfig(num_actions=18, torso="atari", lstm_size=256, head_size=256)
+    rows = 64
+    n = _native(cfg, rows, 2)
+    n.set_policy_planes(True)
+    params = _params(cfg, 7)
+    n.set_params(params)
+    d = lambda x: torch.as_tensor(np.ascontiguousarray(x)).cuda()  # noqa: E731
+    for call in range(2):
+        b = _batch(cfg, rows, 1, 30 + call)
+        logits, values, cache = O.forward(cfg, params, b, np.float64)
+        lg, v, h, c = n.policy_step(d(b["obs"][:, 0]), d(b["prev_action"][:, 0]),
+                                    d(b["prev_reward"][:, 0]), d(b["h0"]), d(b["c0"]))
+        _close(lg.cpu().numpy(), logits[:, 0], name=f"logits {call}")
+        _close(v.cpu().numpy(), values[:, 0], name=f"values {call}")
+        _close(h.cpu().numpy(), cache["hs"][:, 0], name=f"h {call}")
+        _close(c.cpu().numpy(), cache["cs"][:, 0], name=f"c {call}")
+    assert not n.plane_overflow()
+
+
 @pytest.mark.parametrize("B,T,H,torso", [(16, 20, 256, "flat"), (3, 7, 256, "flat"),
                                          (27, 5, 256, "flat"), (16, 2, 256, "flat"),
                                          (16, 20, 256, "atari")])
