@@ -592,7 +592,9 @@ int acme_r2d2_create(const acme_r2d2_config* cfg, acme_r2d2** out) {
   // Rows of the LSTM forward step per workgroup: h_prev of those rows and the workgroup's
   // W_h columns are staged in LDS (up to 160 KB on gfx950).
   const int H = l->H, A = l->A, H2 = l->H2, B = cfg->max_batch;
-  l->bc = B;
+  // 16 rows (one mat-vec pass) per workgroup: the step's grid is H / 4 x B / 16 workgroups
+  // (256 at H 512, B 32), each staging a sixteenth of the batch's h_prev.
+  l->bc = std::min(B, 16);
   while (l->bc > 1 && lstm_fwd_smem(l->bc, H) > (size_t)kFwdLds) l->bc = (l->bc + 1) / 2;
   l->fwd_smem = lstm_fwd_smem(l->bc, H);
   ACME_CHECK_ARG(l->fwd_smem <= (size_t)kFwdLds, "lstm_size too large for the LSTM step kernel");

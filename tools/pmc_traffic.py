@@ -32,6 +32,10 @@ SECTIONS_D4PG = [
     (r"sample_gather_small_kernel", "replay_sample_gather"),
 ]
 SECTIONS_IMPALA = [
+    (r"P3DenseFwd", "impala_oar_fwd"),
+    (r"P3DenseWgrad", "impala_wi_wgrad"),
+    (r"P3DenseDgrad", "impala_feat_dgrad"),
+    (r"oar_finish_kernel", "impala_oar_reduce"),
     (r"DenseDgrad<true", "impala_feat_dgrad"),
     (r"OarFwd", "impala_oar_fwd"),
     (r"OarWgrad", "impala_wi_wgrad"),
@@ -55,6 +59,7 @@ SECTIONS = [
     (r"frames_f16_kernel", "frames_f16"),
     (r"head_dz_planes_kernel", "head_dz"),
     (r"dqn_loss_head_dz_kernel", "loss_head_dz"),
+    (r"dqn_head_loss_dz_kernel", "head_loss_dz"),
     (r"gemm_p3c12_kernel", "conv12_fwd"),
     (r"gemm_\w+_kernel<128, 128, 2, 2,.*DenseFwd<true", "fc_fwd"),
     (r"ConvFwd<acme::conv::Geom<84,", "conv1_fwd"),
@@ -73,7 +78,24 @@ SECTIONS = [
     (r"sample_prioritized_kernel", "replay_sample"),
     (r"prio_update_fused_kernel", "replay_update"),
 ]
-TABLES = {"dqn": SECTIONS, "d4pg": SECTIONS_D4PG, "impala": SECTIONS_IMPALA}
+SECTIONS_R2D2 = [
+    (r"OarFwd", "r2d2_oar_fwd"),
+    (r"OarWgrad", "r2d2_wi_wgrad"),
+    (r"HPrevTM", "r2d2_wh_wgrad"),
+    (r"<64, 128, 2, 2,.*DenseDgrad<true", "r2d2_feat_dgrad"),
+    (r"DenseDgrad<true", "r2d2_hidden_dgrad"),
+    (r"DenseWgrad<true", "r2d2_hidden_wgrad"),
+    (r"DenseFwd<true", "r2d2_hidden_fwd"),
+    (r"DuelHeadFwd", "r2d2_head_fwd"),
+    (r"DuelHeadWgrad", "r2d2_head_wgrad"),
+    (r"lstm_fwd_step", "r2d2_lstm_fwd"),
+    (r"lstm_bwd_step", "r2d2_lstm_bwd"),
+    (r"r2d2_loss_kernel", "r2d2_loss"),
+    (r"r2d2_permute_kernel", "r2d2_permute"),
+    (r"(?<!clip_)adam_kernel", "r2d2_adam"),
+] + [e for e in SECTIONS_IMPALA if e[1].startswith("conv")]
+TABLES = {"dqn": SECTIONS, "d4pg": SECTIONS_D4PG, "impala": SECTIONS_IMPALA,
+          "r2d2": SECTIONS_R2D2}
 TABLE = SECTIONS
 
 
