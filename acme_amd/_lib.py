@@ -228,6 +228,11 @@ _SIGS = {
     "acme_r2d2_bind": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "acme_r2d2_step": (c_i32, [c_vp, ctypes.POINTER(SequenceBatch), c_vp,
                                ctypes.POINTER(R2D2Outputs), c_vp]),
+    "acme_r2d2_params_changed": (c_i32, [c_vp]),
+    "acme_r2d2_skipped_steps": (c_i64, [c_vp]),
+    "acme_r2d2_guard_state": (c_i32, [c_vp, ctypes.POINTER(c_i64)]),
+    "acme_r2d2_skip_word": (c_vp, [c_vp]),
+    "acme_r2d2_set_applied_steps": (c_i32, [c_vp, c_i64]),
     "acme_r2d2_num_steps": (c_i64, [c_vp]),
     "acme_r2d2_set_num_steps": (c_i32, [c_vp, c_i64]),
     "acme_r2d2_debug_buffer": (c_i32, [c_vp, ctypes.c_char_p, ctypes.POINTER(c_vp),

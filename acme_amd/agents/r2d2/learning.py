@@ -66,11 +66,20 @@ class R2D2Learner(core.Learner, core.Saveable):
         self._native.set_params(network.init(seed),
                                 target_network.init(seed + 1 if target_seed is None
                                                     else target_seed))
+        self._skips_seen = 0
         self._counter = counter or counting.Counter(None, "learner")
         self._logger = logger or loggers.TerminalLogger("learner", time_delta=100.)
         self._timestamp = None
 
+    def _check_guard(self) -> int:
+        n = self._native.skipped_steps  # pinned host word: no synchronisation
+        if n != self._skips_seen:
+            self._skips_seen = n
+            self._native.params_changed()  # recalibrate the plane scales before the next step
+        return n
+
     def step(self):
+        skipped = self._check_guard()
         sample = next(self._iterator)
         data = sample.data
         obs = data.observation
@@ -96,13 +105,16 @@ class R2D2Learner(core.Learner, core.Saveable):
                c(data.reward.reshape(B, T), torch.float32),
                c(data.discount.reshape(B, T), torch.float32),
                c(probs, torch.float64), h0, c0)
-        if self._client is not None:  # learning.py:195-198
+        if self._client is not None:  # learning.py:195-198; a skipped step writes none
+            kw = {"skip_word": n.skip_word} if n.skip_word else {}
             self._client.update_priorities(table=adders.DEFAULT_PRIORITY_TABLE, keys=keys,
-                                           priorities=n.priorities[:B])
+                                           priorities=n.priorities[:B], **kw)
         now = time.time()
         elapsed = now - self._timestamp if self._timestamp else 0
         self._timestamp = now
         result = {"loss": n.loss[0]}
+        if skipped:
+            result["skipped_steps"] = skipped
         result.update(self._counter.increment(steps=1, walltime=elapsed))
         self._logger.write(result)
 
@@ -128,7 +140,7 @@ class R2D2Learner(core.Learner, core.Saveable):
         n = self._native
         return {"network": n.get_params("params"), "target_network": n.get_params("target"),
                 "optimizer": {"m": n.get_params("m"), "v": n.get_params("v"),
-                              "step": n.num_steps},
+                              "step": n.num_steps, "applied_steps": n.guard_state()["applied"]},
                 "num_steps": n.num_steps}
 
     def restore(self, state: Dict):
@@ -138,3 +150,5 @@ class R2D2Learner(core.Learner, core.Saveable):
             for k, t in n.views(buf).items():
                 t.copy_(torch.as_tensor(np.asarray(src[k], np.float32)).view(t.shape))
         n.num_steps = int(state["num_steps"])
+        if "applied_steps" in state["optimizer"]:
+            n.set_applied_steps(int(state["optimizer"]["applied_steps"]))

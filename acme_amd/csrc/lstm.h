@@ -211,7 +211,7 @@ __global__ void __launch_bounds__(256) lstm_fwd_step_kernel(
     // Larger staging (R2D2's H = 512 over tens of rows): rounds of kStageBatch float4 per
     // thread, every load of a round issued before its stores (a load-store pair per
     // iteration paid one memory latency per float4: 25 us per step at B 32, H 512).
-    constexpr int kStageBatch = 8;
+    constexpr int kStageBatch = 16;
     for (int e0 = threadIdx.x; e0 < nh4; e0 += 256 * kStageBatch) {
       f32x4 v[kStageBatch];
 #pragma unroll
@@ -220,13 +220,13 @@ __global__ void __launch_bounds__(256) lstm_fwd_step_kernel(
         const int b = e / (H / 4), k = 4 * (e % (H / 4));
         v[q] = *reinterpret_cast<const f32x4*>(hp + (size_t)b * hp_stride + k);
       }
+      // Stores at the clamped index too (a duplicate store of the same value): a store under
+      // a branch let the compiler sink its load into the branch, one exposed latency each.
 #pragma unroll
       for (int q = 0; q < kStageBatch; ++q) {
-        const int e = e0 + 256 * q;
-        if (e < nh4) {
-          const int b = e / (H / 4), k = 4 * (e % (H / 4));
-          *reinterpret_cast<f32x4*>(hs + (size_t)b * H + k) = v[q];
-        }
+        const int e = min(e0 + 256 * q, nh4 - 1);
+        const int b = e / (H / 4), k = 4 * (e % (H / 4));
+        *reinterpret_cast<f32x4*>(hs + (size_t)b * H + k) = v[q];
       }
     }
     for (int e0 = threadIdx.x; e0 < nw4; e0 += 256 * kStageBatch) {
@@ -239,11 +239,9 @@ __global__ void __launch_bounds__(256) lstm_fwd_step_kernel(
       }
 #pragma unroll
       for (int q = 0; q < kStageBatch; ++q) {
-        const int e = e0 + 256 * q;
-        if (e < nw4) {
-          const int k = e / 4, g = e % 4;
-          *reinterpret_cast<f32x4*>(ws + (size_t)k * NC + g * kFwdUnits) = v[q];
-        }
+        const int e = min(e0 + 256 * q, nw4 - 1);
+        const int k = e / 4, g = e % 4;
+        *reinterpret_cast<f32x4*>(ws + (size_t)k * NC + g * kFwdUnits) = v[q];
       }
     }
   }
@@ -419,6 +417,84 @@ __global__ void __launch_bounds__(256) lstm_bwd_step_kernel(
       }
     }
     __syncthreads();
+  }
+}
+
+// gx = OAR(emb) @ W_i + b from the plane GEMM's split-K partials of feat @ W_i[0:F]: the
+// one-hot(prev a) row of W_i, tanh(prev r) times its last row and the bias are added here
+// (the embedding's last A + 1 columns), one thread per (row, 4 gate columns).
+__global__ void __launch_bounds__(256) oar_finish_kernel(const float* __restrict__ slab,
+                                                         int splits, int rows, int N,
+                                                         const float* __restrict__ wi_tail,
+                                                         const float* __restrict__ bias,
+                                                         const int32_t* __restrict__ prev_a,
+                                                         const float* __restrict__ prev_r, int A,
+                                                         float* __restrict__ gx) {
+  const int n4 = N / 4;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)rows * n4) return;
+  const int m = (int)(i / n4), c = (int)(i - (int64_t)m * n4);
+  const int64_t cnt = (int64_t)rows * N;
+  f32x4 v = reinterpret_cast<const f32x4*>(slab)[i];
+  for (int s = 1; s < splits; ++s) v += reinterpret_cast<const f32x4*>(slab + s * cnt)[i];
+  const int a = prev_a[m];
+  const float tr = tanhf(prev_r[m]);
+  const f32x4 wa = reinterpret_cast<const f32x4*>(wi_tail + (size_t)a * N)[c];
+  const f32x4 wr = reinterpret_cast<const f32x4*>(wi_tail + (size_t)A * N)[c];
+  const f32x4 b = reinterpret_cast<const f32x4*>(bias)[c];
+  f32x4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = ((v[j] + wa[j]) + tr * wr[j]) + b[j];
+  reinterpret_cast<f32x4*>(gx)[i] = o;
+}
+
+// The last A + 1 rows of dW_i (the one-hot and tanh(prev r) embedding columns):
+// dW[F + j][n] = sum over rows with prev_a == j of dgates[m][n], dW[F + A][n] = sum of
+// tanh(prev_r[m]) dgates[m][n].  One pass over dgates: block = 64 columns x W waves (W =
+// blockDim.x / 64), wave w takes rows m = w, w + W, ... (kTailBatch loads in flight per
+// lane).  A row's action is wave-uniform, so the wave adds the row into its own LDS
+// accumulator row [w][a][lane]; the W wave partials of each output are then added in wave
+// order.  Deterministic.  (One block per output row, each re-reading all of dgates with 80
+// dependent loads per wave, took 21.6 us.)
+constexpr int kTailBatch = 10;
+inline int tail_waves(int A) { return A + 1 <= 32 ? 8 : 4; }  // LDS W (A + 1) 256 B <= 64 KB
+__global__ void __launch_bounds__(512) oar_wgrad_tail_kernel(
+    const float* __restrict__ dg, int rows, int N, const int32_t* __restrict__ prev_a,
+    const float* __restrict__ prev_r, int A, float* __restrict__ dw_tail) {
+  extern __shared__ float tacc[];  // [W][A + 1][64]
+  const int W = blockDim.x >> 6;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + lane, nc = min(n, N - 1);
+  const int J = A + 1;
+  float* my = tacc + (size_t)wave * J * 64;
+  for (int j = 0; j < J; ++j) my[j * 64 + lane] = 0.f;
+  float racc = 0.f;
+  for (int m0 = wave; m0 < rows; m0 += W * kTailBatch) {
+    float g[kTailBatch], tr[kTailBatch];
+    int act[kTailBatch];
+#pragma unroll
+    for (int b = 0; b < kTailBatch; ++b) {
+      const int mc = min(m0 + b * W, rows - 1);
+      g[b] = dg[(size_t)mc * N + nc];
+      act[b] = prev_a[mc];
+      tr[b] = prev_r[mc];
+    }
+#pragma unroll
+    for (int b = 0; b < kTailBatch; ++b) {
+      if (m0 + b * W >= rows) break;
+      const int a = __builtin_amdgcn_readfirstlane(act[b]);
+      if ((unsigned)a < (unsigned)A) my[a * 64 + lane] += g[b];
+      racc = fmaf(tanhf(tr[b]), g[b], racc);
+    }
+  }
+  my[A * 64 + lane] = racc;
+  __syncthreads();
+  for (int e = threadIdx.x; e < J * 64; e += blockDim.x) {
+    const int j = e >> 6, nn = blockIdx.x * 64 + (e & 63);
+    if (nn >= N) continue;
+    float t = tacc[e];
+    for (int w = 1; w < W; ++w) t += tacc[(size_t)w * J * 64 + e];
+    dw_tail[(size_t)j * N + nn] = t;
   }
 }
 

@@ -20,7 +20,11 @@
 //   backward over the suffix: duelling head, hidden layer, BPTT (t = T-1 .. burn_in), W_h,
 //     W_i (+ b), embedding -> conv3 dZ -> torso backward
 //   snt.Adam(lr, epsilon); target <- online when num_steps % period == 0     (:78, :181-189)
-// Engine: exact f32 MFMA (gemm.h), the same GEMM problems as the IMPALA learner.
+// Engines: the Atari torso, the OAR projection and their backward on the two-plane f16 engine
+// (csrc/gemm_p3.h, the DQN / IMPALA learners' f32-equivalent planes; frames as one exact
+// f16 plane; per-tensor power-of-two scales rescaled at the end of every step from its maxima,
+// the step guard skipping a step whose planes overflowed); the LSTM, the duelling head and the
+// flat torso on f32 MFMA (gemm.h / gemm_x6.h).  ACME_V_R2P3=1 at creation: f32 throughout.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -33,6 +37,8 @@
 #include "conv.h"
 #include "gemm.h"
 #include "gemm_x6.h"
+#include "gemm_p3.h"
+#include "conv_p3.h"
 #include "kernels.h"
 #include "profiler.h"
 #include "torso.h"
@@ -48,6 +54,12 @@ constexpr int kHeadFwdSplits = 16;  // duelling head [rows, A + 1] x K = 2 H2
 constexpr int kHeadBwdSplits = 8;   // duelling head weights [2 H2 + 1, A + 1] x K = rows
 constexpr int kMaxSeq = 256;        // sequence length bound (the loss kernel's LDS)
 constexpr int kFwdLds = 160 * 1024; // LDS per workgroup on gfx950
+constexpr int kOarSplitsP3 = 8;     // split-K of the plane-engine OAR projection (K = 7744)
+
+// Scale records of the plane path: the transient activations / gradients (the target and
+// online passes write the same activation planes: one record each, the maximum of both),
+// then the online and the target parameter planes (split at the start of every pass).
+enum { kScX1, kScX2, kScX3, kScDz3, kScDz2, kScDz1, kScDg, kScParams, kScTParams, kScCount };
 
 struct Tensor {
   std::string name;
@@ -91,6 +103,21 @@ struct acme_r2d2 {
   float* loss_tmp = nullptr;
   int bc = 0;        // batch rows per workgroup of the LSTM forward step
   size_t fwd_smem = 0;
+  // Plane path (Atari torso): parameter planes of the torso + W_i prefix of the online and
+  // the target network, f16 time-major frames, activation / gradient planes, scale records,
+  // split-K slab; the step guard (kernels.h StepGuard: a step whose planes overflowed applies
+  // no update; Adam's count is guard->applied).
+  bool p3 = false;
+  int64_t p3_prefix = 0;
+  uint16_t *wpl = nullptr, *tpl = nullptr, *frames16 = nullptr;
+  torso::Plane x1p{}, x2p{}, x3p{}, dz1p{}, dz2p{}, dz3p{}, dgp{};
+  gemm::PScale* scales = nullptr;
+  int* overflow = nullptr;
+  bool scales_ok = false;
+  float* pslab = nullptr;
+  StepGuard* guard = nullptr;
+  int64_t* host_skipped = nullptr;
+  int64_t last_rows = 0;
 };
 
 namespace {
@@ -147,6 +174,73 @@ inline int chunk_for(int K, int splits) {
   } while (0)
 
 #define R2_CHECK() ACME_LAUNCH_CHECK()
+
+#define R2_P3_GEMM(name, BM, BN, WM, WN, BKV, prob, splits)                                    \
+  do {                                                                                         \
+    ACME_PROF_PEAK(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0, \
+                   gemm::p3_peak_tflops<decltype(prob)>());                                    \
+    hipError_t _e = gemm::launch_gemm_p3<BM, BN, WM, WN, BKV>(prob, splits, st);              \
+    if (_e != hipSuccess) {                                                                    \
+      set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
+      return ACME_ERR_HIP;                                                                     \
+    }                                                                                          \
+  } while (0)
+#define R2_P3WS_GEMM(name, BM, BN, WM, WN, BKV, prob, splits)                                  \
+  do {                                                                                         \
+    ACME_PROF_PEAK(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0, \
+                   gemm::p3_peak_tflops<decltype(prob)>());                                    \
+    hipError_t _e = gemm::launch_gemm_p3ws<BM, BN, WM, WN, BKV, true>(prob, splits, st);      \
+    if (_e != hipSuccess) {                                                                    \
+      set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
+      return ACME_ERR_HIP;                                                                     \
+    }                                                                                          \
+  } while (0)
+
+// Plane views: tensor t of a parameter plane set (record rec), an activation's rows from `row`.
+torso::Plane WP(const acme_r2d2* l, uint16_t* planes, int rec, int t) {
+  return torso::Plane{planes + l->tensors[t].offset, l->flat, l->scales + rec};
+}
+torso::Plane rows_from(const torso::Plane& x, int64_t row, int64_t per_row) {
+  return torso::Plane{x.p + row * per_row, x.stride, x.sc};
+}
+gemm::PlaneSrc SRC(const torso::Plane& x, int64_t elems) {
+  return gemm::PlaneSrc{x.p, x.stride, (int32_t)(2 * elems), x.sc};
+}
+torso::PWeights torso_pw(const acme_r2d2* l, const float* prm, uint16_t* planes, int rec) {
+  return torso::PWeights{WP(l, planes, rec, l->t_c[0]), WP(l, planes, rec, l->t_c[2]),
+                         WP(l, planes, rec, l->t_c[4]), P(l, prm, l->t_c[1]),
+                         P(l, prm, l->t_c[3]), P(l, prm, l->t_c[5])};
+}
+
+// uint8 frames [B][T] -> exact f16 frames [T][B] (integers 0..255 are exact in f16): 16 bytes
+// in, 32 out per thread; the OAR side inputs ride in the same launch (the first B T threads).
+__global__ void __launch_bounds__(256) r2d2_frames_f16_kernel(
+    const uint4* __restrict__ src, uint4* __restrict__ dst, int64_t units, int B, int T,
+    const int32_t* __restrict__ pa, const float* __restrict__ pr, int32_t* __restrict__ pa_tm,
+    float* __restrict__ pr_tm) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t R = (int64_t)B * T;
+  if (i < R) {
+    const int b = (int)(i / T), t = (int)(i - (int64_t)b * T);
+    pa_tm[(int64_t)t * B + b] = pa[i];
+    pr_tm[(int64_t)t * B + b] = pr[i];
+  }
+  if (i >= R * units) return;
+  const int64_t row = i / units, u = i - row * units;
+  const int b = (int)(row / T), t = (int)(row - (int64_t)b * T);
+  const uint4 v = src[i];
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t o[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const uint32_t lo = (w[q >> 1] >> (16 * (q & 1))) & 0xffu, hi = (w[q >> 1] >> (16 * (q & 1) + 8)) & 0xffu;
+    const _Float16 a = (_Float16)(float)lo, c = (_Float16)(float)hi;
+    o[q] = (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, c) << 16);
+  }
+  uint4* d = dst + (((int64_t)t * B + b) * units + u) * 2;
+  d[0] = uint4{o[0], o[1], o[2], o[3]};
+  d[1] = uint4{o[4], o[5], o[6], o[7]};
+}
 
 // ------------------------------------------------------------------ input permutation
 // Batch-major rows (b * T + t) of `unit`-sized records to time-major rows (t * B + b),
@@ -344,11 +438,38 @@ torso::Weights torso_w(const acme_r2d2* l, const float* prm) {
 // One network's unroll over all T steps (time-major rows) from the core state, and its
 // duelling head over the suffix rows -> q_out [L B][A].
 int network_forward(acme_r2d2* l, const float* prm, const acme_sequence_batch* bt, int B, int T,
-                    float* q_out, hipStream_t st) {
+                    float* q_out, hipStream_t st, uint16_t* planes, int rec, bool online) {
   const int R = B * T, H = l->H, A = l->A, H2 = l->H2, BI = l->cfg.burn_in_length;
   const int L = T - BI, RL = L * B;
-  const float* feat;
-  if (atari(l)) {
+  const float* feat = nullptr;
+  if (l->p3) {
+    // The network's torso + W_i planes at its record's scale, the plane torso (the target's
+    // conv1 output stays in LDS: fused conv1 -> conv2), feat @ W_i[0:F] on the plane engine,
+    // then the embedding tail (one-hot(prev a), tanh(prev r) rows of W_i) and the bias.
+    int rc;
+    {
+      ACME_PROF("r2d2_planes", st, 0.0, 8.0 * (double)l->p3_prefix);
+      rc = launch_split_planes_lagged(prm, l->p3_prefix, planes, l->flat, l->scales + rec, st);
+      if (rc != ACME_OK) return rc;
+    }
+    rc = torso::forward_p3(torso_pw(l, prm, planes, rec), torso::Frames{l->frames16}, R,
+                           torso::PActs{l->x1p, l->x2p, l->x3p}, st, online ? -1 : 0);
+    if (rc != ACME_OK) return rc;
+    const int F = l->F, N = 4 * H;
+    P3DenseFwd p;
+    p.M = R; p.N = N; p.K = F; p.k_chunk = chunk_for(F, kOarSplitsP3);
+    p.a_src = SRC(l->x3p, (int64_t)R * F); p.ldx = F;
+    p.b_src = SRC(WP(l, planes, rec, l->t_wi), (int64_t)F * N); p.slab = l->pslab;
+    R2_P3WS_GEMM("r2d2_oar_fwd", 128, 128, 2, 2, 32, p, kOarSplitsP3);
+    {
+      ACME_PROF("r2d2_oar_reduce", st, 0.0, 4.0 * (kOarSplitsP3 + 1) * (double)R * N);
+      const int64_t n4 = (int64_t)R * N / 4;
+      oar_finish_kernel<<<(unsigned)ceil_div(n4, 256), 256, 0, st>>>(
+          l->pslab, kOarSplitsP3, R, N, P(l, prm, l->t_wi) + (size_t)F * N, P(l, prm, l->t_b),
+          l->pa_tm, l->pr_tm, A, l->gx);
+      R2_CHECK();
+    }
+  } else if (atari(l)) {
     int rc = torso::forward(torso_w(l, prm), true, l->obs_tm, l->obs_tm, R, R,
                             torso::Acts{l->x1, l->x2, l->x3}, st);
     if (rc != ACME_OK) return rc;
@@ -356,7 +477,7 @@ int network_forward(acme_r2d2* l, const float* prm, const acme_sequence_batch* b
   } else {
     feat = static_cast<const float*>(l->obs_tm);
   }
-  {
+  if (!l->p3) {
     OarFwd p;
     p.M = R; p.N = 4 * H; p.K = l->D;
     p.x = Oar{feat, l->F, A, l->pa_tm, l->pr_tm};
@@ -412,15 +533,22 @@ int network_forward(acme_r2d2* l, const float* prm, const acme_sequence_batch* b
   return ACME_OK;
 }
 
+// apply = false: forward, loss and backward only (the plane-scale calibration passes).
 int r2d2_step_impl(acme_r2d2* l, const acme_sequence_batch* bt, const double* probs,
-                   const acme_r2d2_outputs* out, hipStream_t st) {
+                   const acme_r2d2_outputs* out, hipStream_t st, bool apply = true) {
   const int B = (int)bt->batch, T = (int)bt->sequence_length, R = B * T;
   const int H = l->H, A = l->A, H2 = l->H2, BI = l->cfg.burn_in_length;
   const int L = T - BI, RL = L * B;
   int rc;
   {  // time-major inputs
-    ACME_PROF("r2d2_permute", st, 0.0, 2.0 * (double)R * (atari(l) ? torso::kObsBytes : 4 * l->F));
-    if (atari(l)) {
+    ACME_PROF("r2d2_permute", st, 0.0,
+              (l->p3 ? 3.0 : 2.0) * (double)R * (atari(l) ? torso::kObsBytes : 4 * l->F));
+    if (l->p3) {
+      const int64_t units = torso::kObsBytes / 16;
+      r2d2_frames_f16_kernel<<<(unsigned)ceil_div((int64_t)R * units, 256), 256, 0, st>>>(
+          static_cast<const uint4*>(bt->observation), reinterpret_cast<uint4*>(l->frames16),
+          units, B, T, bt->prev_action, bt->prev_reward, l->pa_tm, l->pr_tm);
+    } else if (atari(l)) {
       const int64_t units = torso::kObsBytes / 16;
       r2d2_permute_kernel<uint4><<<(unsigned)ceil_div((int64_t)R * units, 256), 256, 0, st>>>(
           static_cast<const uint4*>(bt->observation), static_cast<uint4*>(l->obs_tm), units, B, T,
@@ -434,8 +562,12 @@ int r2d2_step_impl(acme_r2d2* l, const acme_sequence_batch* bt, const double* pr
     R2_CHECK();
   }
   // Target network first (its activations are overwritten by the online pass).
-  if ((rc = network_forward(l, l->target, bt, B, T, l->tq, st)) != ACME_OK) return rc;
-  if ((rc = network_forward(l, l->params, bt, B, T, l->q, st)) != ACME_OK) return rc;
+  l->last_rows = R;
+  if ((rc = network_forward(l, l->target, bt, B, T, l->tq, st, l->tpl, kScTParams, false)) !=
+      ACME_OK)
+    return rc;
+  if ((rc = network_forward(l, l->params, bt, B, T, l->q, st, l->wpl, kScParams, true)) != ACME_OK)
+    return rc;
   float* errors = out && out->errors ? out->errors : l->err_tmp;
   double* prio = out && out->priorities ? out->priorities : l->prio_tmp;
   float* loss = out && out->loss ? out->loss : l->loss_tmp;
@@ -509,9 +641,66 @@ int r2d2_step_impl(acme_r2d2* l, const acme_sequence_batch* bt, const double* pr
     w.B = B; w.BI = BI; w.dz = l->dgates; w.out = Pm(l, gr, l->t_wh);
     R2_GEMM("r2d2_wh_wgrad", 64, 64, 2, 2, 1, w, 1);
   }
+  if (l->p3) {  // W_i, b and the embedding gradient on the plane engine, then the plane torso
+    const int F = l->F, N = 4 * H;
+    const int64_t off = (int64_t)BI * B;
+    {
+      ACME_PROF("r2d2_dgates_planes", st, 0.0, 8.0 * (double)RL * N);
+      rc = launch_split_planes_lagged(l->dgates, (int64_t)RL * N, l->dgp.p, l->dgp.stride,
+                                      l->dgp.sc, st);
+      if (rc != ACME_OK) return rc;
+    }
+    const torso::Plane x3s = rows_from(l->x3p, off, F);
+    {
+      P3DenseWgrad w;
+      w.M = F; w.N = N; w.K = RL; w.k_chunk = RL;
+      w.a_src = SRC(x3s, (int64_t)RL * F); w.ldx = F;
+      w.b_src = SRC(l->dgp, (int64_t)RL * N); w.out = Pm(l, gr, l->t_wi);
+      w.bias_out = Pm(l, gr, l->t_b);
+      R2_P3_GEMM("r2d2_wi_wgrad", 128, 128, 2, 2, 16, w, 1);
+    }
+    {
+      ACME_PROF("r2d2_wi_wgrad_tail", st, 0.0, 4.0 * (double)RL * N);
+      const int tw = tail_waves(A);
+      oar_wgrad_tail_kernel<<<(unsigned)ceil_div(N, 64), 64 * tw,
+                              (size_t)tw * (A + 1) * 64 * sizeof(float), st>>>(
+          l->dgates, RL, N, l->pa_tm + off, l->pr_tm + off, A,
+          Pm(l, gr, l->t_wi) + (size_t)F * N);
+      R2_CHECK();
+    }
+    {
+      P3DenseDgrad d;
+      d.M = RL; d.N = F; d.K = N; d.k_chunk = N;
+      d.a_src = SRC(l->dgp, (int64_t)RL * N);
+      d.b_src = SRC(WP(l, l->wpl, kScParams, l->t_wi), (int64_t)F * N);
+      d.xprev = CPlanes{x3s.p, x3s.stride, x3s.sc}; d.ldx = F;
+      d.dx = Planes{l->dz3p.p, l->dz3p.stride, l->dz3p.sc};
+      R2_P3WS_GEMM("r2d2_feat_dgrad", 128, 128, 2, 2, 32, d, 1);
+    }
+    torso::Grads g{Pm(l, gr, l->t_c[0]), Pm(l, gr, l->t_c[1]), Pm(l, gr, l->t_c[2]),
+                   Pm(l, gr, l->t_c[3]), Pm(l, gr, l->t_c[4]), Pm(l, gr, l->t_c[5])};
+    rc = torso::backward_p3(torso_pw(l, prm, l->wpl, kScParams), g,
+                            torso::Frames{l->frames16 + off * torso::kObsBytes}, RL,
+                            torso::PActs{rows_from(l->x1p, off, torso::kX1),
+                                         rows_from(l->x2p, off, F), x3s},
+                            l->dz3p, l->dz2p, l->dz1p, l->pslab, st);
+    if (rc != ACME_OK) return rc;
+    // Every record's next scale from this step's maxima; with apply, the guard's decision
+    // for this step (kRgStep: skip when a plane write overflowed or underflowed) and its
+    // counts, read by Adam's gate.
+    RescaleGuard rg;
+    if (apply) {
+      rg.g = l->guard;
+      rg.mode = kRgStep;
+      rg.host_skipped = l->host_skipped;
+    }
+    rc = launch_plane_rescale(l->scales, kScCount, kScCount, -1, -1, l->overflow, st, -1, -1, rg);
+    if (rc != ACME_OK) return rc;
+    if (!apply) return ACME_OK;
+  }
   const float* feat = atari(l) ? l->x3 + (size_t)BI * B * l->F
                                : static_cast<const float*>(l->obs_tm) + (size_t)BI * B * l->F;
-  {  // W_i (+ b) over the suffix's OAR embedding
+  if (!l->p3) {  // W_i (+ b) over the suffix's OAR embedding
     OarWgrad o;
     o.M = l->D; o.N = 4 * H; o.K = RL; o.k_chunk = RL;
     o.x = Oar{feat, l->F, A, l->pa_tm + (size_t)BI * B, l->pr_tm + (size_t)BI * B};
@@ -519,7 +708,7 @@ int r2d2_step_impl(acme_r2d2* l, const acme_sequence_batch* bt, const double* pr
     if (atari(l)) R2_GEMM("r2d2_wi_wgrad", 128, 128, 2, 2, 1, o, 1);
     else R2_GEMM("r2d2_wi_wgrad", 32, 32, 1, 1, 8, o, 1);
   }
-  if (atari(l)) {  // embedding features -> conv3 dZ -> torso backward over the suffix frames
+  if (atari(l) && !l->p3) {  // embedding features -> conv3 dZ -> torso backward (suffix frames)
     DenseDgrad<true> d;
     d.M = RL; d.N = l->F; d.K = 4 * H; d.k_chunk = 4 * H;
     d.dz = l->dgates; d.w = P(l, prm, l->t_wi); d.xprev = feat; d.ldx = l->F;
@@ -535,10 +724,23 @@ int r2d2_step_impl(acme_r2d2* l, const acme_sequence_batch* bt, const double* pr
                          l->dz3, l->dz2, l->dz1, l->slab, st);
     if (rc != ACME_OK) return rc;
   }
+  if (!apply) return ACME_OK;
   {
     ACME_PROF("r2d2_adam", st, 0.0, 7.0 * 4.0 * (double)l->flat);
-    rc = launch_adam(l->params, gr, l->m, l->v, l->flat, l->cfg.learning_rate, l->cfg.adam_beta1,
-                     l->cfg.adam_beta2, l->cfg.adam_epsilon, 0, nullptr, 0, st, 0, l->dev_step);
+    if (l->p3) {  // gated: a skipped step leaves p, m and v; t = the applied updates
+      Gate gate;
+      gate.g = l->guard;
+      gate.use_last = 1;
+      AdamTail tail;
+      tail.clear = l->guard;
+      rc = launch_adam(l->params, gr, l->m, l->v, l->flat, l->cfg.learning_rate,
+                       l->cfg.adam_beta1, l->cfg.adam_beta2, l->cfg.adam_epsilon, 0, nullptr, 0,
+                       st, 0, &l->guard->applied, nullptr, gate, false, tail);
+    } else {
+      rc = launch_adam(l->params, gr, l->m, l->v, l->flat, l->cfg.learning_rate,
+                       l->cfg.adam_beta1, l->cfg.adam_beta2, l->cfg.adam_epsilon, 0, nullptr, 0,
+                       st, 0, l->dev_step);
+    }
     if (rc != ACME_OK) return rc;
   }
   if (l->num_steps % l->cfg.target_update_period == 0)  // learning.py:185-189, after the update
@@ -555,6 +757,7 @@ int acme_r2d2_destroy(acme_r2d2* l) {
   if (!l) return ACME_OK;
   (void)hipDeviceSynchronize();
   for (void* p : l->allocs) (void)hipFree(p);
+  if (l->host_skipped) (void)hipHostFree(l->host_skipped);
   delete l;
   return ACME_OK;
 }
@@ -630,6 +833,7 @@ int acme_r2d2_create(const acme_r2d2_config* cfg, acme_r2d2** out) {
                                     (int64_t)64});
   if (cfg->torso == ACME_IMPALA_TORSO_ATARI) {
     slab = std::max<int64_t>({slab, torso::wgrad_slab_floats(), (int64_t)kOarSplits * R * 4 * H});
+    // (On the plane path x1..x3 serve the debug buffers only: the planes joined to f32.)
     if ((rc = dev_alloc(l, reinterpret_cast<uint8_t**>(&l->obs_tm), R * torso::kObsBytes)) ||
         (rc = dev_alloc(l, &l->x1, R * torso::kX1)) || (rc = dev_alloc(l, &l->x2, R * torso::kFlat)) ||
         (rc = dev_alloc(l, &l->x3, R * torso::kFlat)) || (rc = dev_alloc(l, &l->dz1, RL * torso::kX1)) ||
@@ -637,6 +841,52 @@ int acme_r2d2_create(const acme_r2d2_config* cfg, acme_r2d2** out) {
       return fail(rc);
   } else if ((rc = dev_alloc(l, reinterpret_cast<float**>(&l->obs_tm), R * l->F))) {
     return fail(rc);
+  }
+  // Plane path for the Atari torso (each operand plane is addressed through a 31-bit byte
+  // range: the f16 frames of one step bound the batch), unless ACME_V_R2P3=1.
+  l->p3 = cfg->torso == ACME_IMPALA_TORSO_ATARI && R * torso::kObsBytes * 2 < (int64_t)INT32_MAX &&
+          tune_variant("R2P3") != 1;
+  if ((rc = dev_alloc(l, &l->guard, 1))) return fail(rc);
+  if (hipMemset(l->guard, 0, sizeof(StepGuard)) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&l->host_skipped), sizeof(int64_t),
+                    hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+    return fail((set_error("step guard allocation failed"), ACME_ERR_HIP));
+  *l->host_skipped = 0;
+  if (l->p3) {
+    l->p3_prefix = align64(l->tensors[l->t_wi].offset + l->tensors[l->t_wi].numel);
+    if ((rc = dev_alloc(l, &l->scales, kScCount)) || (rc = dev_alloc(l, &l->overflow, 1)))
+      return fail(rc);
+    std::vector<gemm::PScale> init(kScCount);
+    std::memset(init.data(), 0, init.size() * sizeof(gemm::PScale));
+    for (auto& r : init) {
+      r.w = r.r = r.wi = r.rl = 1.f;
+      r.flag = &l->guard->on;
+    }
+    if (hipMemcpy(l->scales, init.data(), init.size() * sizeof(gemm::PScale),
+                  hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(l->overflow, 0, sizeof(int)) != hipSuccess)
+      return fail((set_error("scale record init failed"), ACME_ERR_HIP));
+    auto plane = [&](torso::Plane* x, int64_t count, int rec) {
+      const int64_t stride = align64(count);
+      uint16_t* q = nullptr;
+      int r = dev_alloc(l, &q, gemm::kPlanes * stride);
+      *x = torso::Plane{q, stride, l->scales + rec};
+      return r;
+    };
+    const int64_t N = 4 * (int64_t)H;
+    if ((rc = dev_alloc(l, &l->wpl, gemm::kPlanes * l->flat)) ||
+        (rc = dev_alloc(l, &l->tpl, gemm::kPlanes * l->flat)) ||
+        (rc = dev_alloc(l, &l->frames16, R * torso::kObsBytes)) ||
+        (rc = plane(&l->x1p, R * torso::kX1, kScX1)) ||
+        (rc = plane(&l->x2p, R * torso::kFlat, kScX2)) ||
+        (rc = plane(&l->x3p, R * torso::kFlat, kScX3)) ||
+        (rc = plane(&l->dz1p, RL * torso::kX1, kScDz1)) ||
+        (rc = plane(&l->dz2p, RL * torso::kFlat, kScDz2)) ||
+        (rc = plane(&l->dz3p, RL * torso::kFlat, kScDz3)) ||
+        (rc = plane(&l->dgp, RL * N, kScDg)) ||
+        (rc = dev_alloc(l, &l->pslab, std::max<int64_t>(torso::wgrad_slab_floats_p3(),
+                                                        (int64_t)kOarSplitsP3 * R * N))))
+      return fail(rc);
   }
   if ((rc = dev_alloc(l, &l->slab, slab)) || (rc = dev_alloc(l, &l->pa_tm, R)) ||
       (rc = dev_alloc(l, &l->pr_tm, R)) || (rc = dev_alloc(l, &l->zero_state, (int64_t)B * H)) ||
@@ -683,6 +933,13 @@ int acme_r2d2_bind(acme_r2d2* l, float* params, float* target, float* grads, flo
   l->grads = grads;
   l->m = adam_m;
   l->v = adam_v;
+  l->scales_ok = false;
+  return ACME_OK;
+}
+
+int acme_r2d2_params_changed(acme_r2d2* l) {
+  ACME_CHECK_ARG(l, "null learner");
+  l->scales_ok = false;
   return ACME_OK;
 }
 
@@ -707,10 +964,51 @@ int acme_r2d2_step(acme_r2d2* l, const acme_sequence_batch* b, const double* pro
   ACME_CHECK_ARG(!atari(l) || ((uintptr_t)b->observation & 15) == 0,
                  "frames must be 16-byte aligned");
   hipStream_t st = as_stream(stream);
-  const int rc = r2d2_step_impl(l, b, probabilities, out, st);
+  int rc = ACME_OK;
+  if (l->p3 && !l->scales_ok) {
+    // Plane scales for newly bound parameters: forward + backward passes without the update,
+    // each ending with the rescale; four, for the input-gradient chain dgates -> dz3 -> dz2
+    // -> dz1 (a tensor computed from planes that underflowed at their initial scale measures
+    // 0 until its input is calibrated, as the DQN / IMPALA learners' calibration).
+    for (int pass = 0; pass < 4 && rc == ACME_OK; ++pass)
+      rc = r2d2_step_impl(l, b, probabilities, out, st, false);
+    if (rc != ACME_OK) return rc;
+    ACME_HIP_TRY(hipMemsetAsync(l->overflow, 0, sizeof(int), st));
+    ACME_HIP_TRY(hipMemsetAsync(l->guard, 0, offsetof(StepGuard, applied), st));
+    l->scales_ok = true;
+  }
+  rc = r2d2_step_impl(l, b, probabilities, out, st);
   if (rc != ACME_OK) return rc;
   l->num_steps += 1;
   return ACME_OK;
+}
+
+int64_t acme_r2d2_skipped_steps(const acme_r2d2* l) {
+  if (!l || !l->host_skipped) return 0;
+  return *reinterpret_cast<volatile const int64_t*>(l->host_skipped);
+}
+
+int acme_r2d2_guard_state(acme_r2d2* l, int64_t* out3) {
+  ACME_CHECK_ARG(l && out3, "null argument");
+  ACME_HIP_TRY(hipDeviceSynchronize());
+  StepGuard g;
+  ACME_HIP_TRY(hipMemcpy(&g, l->guard, sizeof(g), hipMemcpyDeviceToHost));
+  out3[0] = l->p3 ? g.applied : l->num_steps;
+  out3[1] = g.skipped;
+  out3[2] = g.last;
+  return ACME_OK;
+}
+
+int acme_r2d2_set_applied_steps(acme_r2d2* l, int64_t n) {
+  ACME_CHECK_ARG(l && n >= 0, "bad argument");
+  ACME_HIP_TRY(hipDeviceSynchronize());
+  ACME_HIP_TRY(hipMemcpy(&l->guard->applied, &n, sizeof(n), hipMemcpyHostToDevice));
+  if (!l->p3) ACME_HIP_TRY(hipMemcpy(l->dev_step, &n, sizeof(n), hipMemcpyHostToDevice));
+  return ACME_OK;
+}
+
+const uint32_t* acme_r2d2_skip_word(const acme_r2d2* l) {
+  return l && l->p3 ? &l->guard->last : nullptr;
 }
 
 int64_t acme_r2d2_num_steps(const acme_r2d2* l) { return l ? l->num_steps : 0; }
@@ -720,6 +1018,7 @@ int acme_r2d2_set_num_steps(acme_r2d2* l, int64_t n) {
   l->num_steps = n;
   ACME_HIP_TRY(hipDeviceSynchronize());
   ACME_HIP_TRY(hipMemcpy(l->dev_step, &n, sizeof(n), hipMemcpyHostToDevice));
+  ACME_HIP_TRY(hipMemcpy(&l->guard->applied, &n, sizeof(n), hipMemcpyHostToDevice));
   return ACME_OK;
 }
 
@@ -734,9 +1033,19 @@ int acme_r2d2_debug_buffer(const acme_r2d2* l, const char* name, const float** o
   else if (n == "h") { *out = l->h; *count = B * T * l->H; }
   else if (n == "g") { *out = l->g; *count = RL; }
   else if (n == "hid") { *out = l->hid; *count = RL * 2 * l->H2; }
-  else if (n == "x1") { *out = l->x1; *count = l->x1 ? B * T * torso::kX1 : 0; }
-  else if (n == "x2") { *out = l->x2; *count = l->x2 ? B * T * torso::kFlat : 0; }
-  else if (n == "x3") { *out = l->x3; *count = l->x3 ? B * T * torso::kFlat : 0; }
+  else if (n == "x1" || n == "x2" || n == "x3") {
+    float* x = n == "x1" ? l->x1 : (n == "x2" ? l->x2 : l->x3);
+    const int64_t per = n == "x1" ? torso::kX1 : torso::kFlat;
+    *out = x;
+    *count = x ? B * T * per : 0;
+    if (x && l->p3) {  // the plane path keeps them as planes: join the last step's
+      const torso::Plane& pl = n == "x1" ? l->x1p : (n == "x2" ? l->x2p : l->x3p);
+      ACME_HIP_TRY(hipDeviceSynchronize());
+      const int rc = launch_join_planes(pl.p, pl.stride, l->last_rows * per, x, pl.sc, 0);
+      if (rc != ACME_OK) return rc;
+      ACME_HIP_TRY(hipDeviceSynchronize());
+    }
+  }
   else ACME_CHECK_ARG(false, "unknown debug buffer '%s'", name);
   return ACME_OK;
 }

@@ -1042,6 +1042,30 @@ class NativeR2D2:
         for buf, src in ((self.params, params), (self.target, target)):
             for name, t in self.views(buf).items():
                 t.copy_(torch.as_tensor(np.asarray(src[name], np.float32)).view(t.shape))
+        self.params_changed()
+
+    def params_changed(self) -> None:
+        """The bound buffers were written directly: the plane scales recalibrate."""
+        check(lib().acme_r2d2_params_changed(self._h), "r2d2 params_changed")
+
+    @property
+    def skipped_steps(self) -> int:
+        """Steps skipped on plane overflow among those the device finished."""
+        return int(lib().acme_r2d2_skipped_steps(self._h))
+
+    def guard_state(self) -> Dict[str, int]:
+        """{applied, skipped, last_skipped} (synchronises the device)."""
+        a = (ctypes.c_int64 * 3)()
+        check(lib().acme_r2d2_guard_state(self._h, a), "r2d2 guard_state")
+        return dict(applied=int(a[0]), skipped=int(a[1]), last_skipped=int(a[2]))
+
+    def set_applied_steps(self, n: int) -> None:
+        check(lib().acme_r2d2_set_applied_steps(self._h, int(n)), "r2d2 set_applied_steps")
+
+    @property
+    def skip_word(self) -> Optional[int]:
+        """Device address of the step's skip word (gates the priority write-back), or None."""
+        return lib().acme_r2d2_skip_word(self._h) or None
 
     @property
     def num_steps(self) -> int:

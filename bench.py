@@ -587,7 +587,8 @@ def setup_r2d2(args, world, rank, dev):
 
     meta = dict(
         metric=f"learner sequences/sec (B={B} x T={T}, burn-in {BI}) R2D2 Atari, 1 MI355X",
-        unit="sequences/s", dtype="f32 (x6 split-bf16 MFMA GEMMs, f32 LSTM cell)",
+        unit="sequences/s",
+        dtype="f32 (torso and W_i: 2xf16 split planes, 3 MFMA terms; LSTM and head: f32 MFMA)",
         _roofline_exclude=("r2d2_lstm_fwd", "r2d2_lstm_bwd"),
         data="synthetic (device-generated uint8 Atari sequences in a device-resident pool, "
              "random-init R2D2AtariNetwork)",

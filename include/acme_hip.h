@@ -682,6 +682,19 @@ int acme_r2d2_tensor_info(const acme_r2d2* l, int32_t i, int64_t* offset, int64_
                           int32_t* ndim, int64_t* shape4, const char** name);
 int acme_r2d2_bind(acme_r2d2* l, float* params, float* target, float* grads, float* adam_m,
                    float* adam_v);
+/* The caller wrote params / target directly (initialisation, restore): the Atari plane path
+ * recalibrates its scales before the next step (as acme_impala_params_changed). */
+int acme_r2d2_params_changed(acme_r2d2* l);
+/* Step guard of the Atari plane path (as the DQN / IMPALA learners'): a step whose plane
+ * writes overflowed applies no update; out3 = {applied, skipped, last step skipped};
+ * acme_r2d2_skipped_steps reads a pinned host mirror; acme_r2d2_skip_word is the device word
+ * that gates the step's priority write-back (acme_replay_update_priorities_gated; NULL
+ * without the plane path). */
+int64_t acme_r2d2_skipped_steps(const acme_r2d2* l);
+int acme_r2d2_guard_state(acme_r2d2* l, int64_t* out3);
+const uint32_t* acme_r2d2_skip_word(const acme_r2d2* l);
+/* Adam's step count (updates applied; checkpoint restore after acme_r2d2_set_num_steps). */
+int acme_r2d2_set_applied_steps(acme_r2d2* l, int64_t n);
 /* One learner step on a batch of sequences (acme_sequence_batch: batch-major [B, T] fields;
  * behaviour_logits unused; h0 / c0 = extras['core_state'] at t = 0) with the sample's
  * probabilities [B] (f64). */

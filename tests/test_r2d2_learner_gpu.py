@@ -146,9 +146,16 @@ def _relu_masks(cfg, n, params, b):
     return masks
 
 
-def _compare(cfg, B, T, seed=0, steps=1):
+def _compare(cfg, B, T, seed=0, steps=1, f32_engine=False):
+    from acme_amd._lib import lib
     from oracle.dqn_oracle import adam_update
-    n = _native(cfg, B, T)
+    if f32_engine:
+        lib().acme_tune_set(b"R2P3", 1)  # read at the learner's creation
+    try:
+        n = _native(cfg, B, T)
+    finally:
+        if f32_engine:
+            lib().acme_tune_set(b"R2P3", 0)
     p0, t0 = _params(cfg, 10 + seed), _params(cfg, 20 + seed)
     n.set_params(p0, t0)
     z = {k: np.zeros_like(v) for k, v in p0.items()}
@@ -215,6 +222,8 @@ def _compare(cfg, B, T, seed=0, steps=1):
                      m={kk: n.get_params("m")[kk].reshape(shp[kk]) for kk in p0},
                      v={kk: n.get_params("v")[kk].reshape(shp[kk]) for kk in p0},
                      num_steps=k + 1)
+    g = n.guard_state()
+    assert g["skipped"] == 0 and g["applied"] == steps, g
     return n
 
 
@@ -237,8 +246,11 @@ def test_r2d2_large_batch_row_chunks():
     _compare(_cfg(lstm_size=512, head_size=64, num_actions=18, obs_dim=24), B=80, T=6, seed=3)
 
 
-def test_r2d2_atari_step_matches_oracle():
-    """R2D2AtariNetwork's sizes (A = 18, LSTM 512, duelling [512]) on uint8 frames."""
+@pytest.mark.parametrize("f32_engine", [False, True])
+def test_r2d2_atari_step_matches_oracle(f32_engine):
+    """R2D2AtariNetwork's sizes (A = 18, LSTM 512, duelling [512]) on uint8 frames: the
+    torso and the OAR projection on the two-plane f16 engine (the default: scales calibrated
+    on the first step, the step guard) and on f32 MFMA (ACME_V_R2P3=1)."""
     cfg = _cfg(torso="atari", num_actions=18, lstm_size=512, head_size=512, obs_dim=0,
                burn_in_length=2, n_step=2)
-    _compare(cfg, B=3, T=6, seed=4, steps=2)
+    _compare(cfg, B=3, T=6, seed=4, steps=2, f32_engine=f32_engine)
