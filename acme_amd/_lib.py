@@ -106,8 +106,8 @@ class R2D2Config(ctypes.Structure):
                 ("lstm_size", c_i32), ("head_size", c_i32), ("n_step", c_i32),
                 ("store_lstm_state", c_i32), ("target_update_period", c_i32),
                 ("reserved", c_i32), ("max_replay_size", c_i64),
-                ("max_priority_weight", ctypes.c_double), ("discount", c_f32),
-                ("importance_sampling_exponent", c_f32),
+                ("max_priority_weight", ctypes.c_double),
+                ("importance_sampling_exponent", ctypes.c_double), ("discount", c_f32),
                 ("learning_rate", c_f32), ("adam_beta1", c_f32), ("adam_beta2", c_f32),
                 ("adam_epsilon", c_f32)]
 
@@ -235,6 +235,7 @@ _SIGS = {
     "acme_r2d2_set_applied_steps": (c_i32, [c_vp, c_i64]),
     "acme_r2d2_num_steps": (c_i64, [c_vp]),
     "acme_r2d2_set_num_steps": (c_i32, [c_vp, c_i64]),
+    "acme_r2d2_set_lstm_unroll": (c_i32, [c_vp, c_i32]),
     "acme_r2d2_debug_buffer": (c_i32, [c_vp, ctypes.c_char_p, ctypes.POINTER(c_vp),
                                        ctypes.POINTER(c_i64)]),
     "acme_impala_create": (c_i32, [ctypes.POINTER(IMPALAConfig), ctypes.POINTER(c_vp)]),

@@ -183,321 +183,11 @@ struct HPrevWgrad {
 };
 
 // ---------------------------------------------------------------- persistent unroll
-// The whole T-step LSTM forward (and, below, backward) in ONE launch for the Atari learner's
-// shape (H = 256): workgroup (rg, cg) owns kRgRows batch rows (a row group)
-// x kRgUnits units (cg), i.e. 4 * kRgUnits gate columns, and keeps its W_h slice (all 256 k
-// of those columns, 64 floats per thread) in registers for the whole unroll.  A step needs
-// h_{t-1} of its own rows only (the sequences are independent), so each workgroup exchanges
-// kRgRows x H values per step with the H / kRgUnits workgroups of its row group, as 8-byte
-// {tag, value} granules (agent-scope relaxed atomic stores and loads: the data is its own
-// flag, cdna_hip_programming.md G16 / MI355X_MICROARCH.md "handoff-1to1"; 4 granules per
-// thread per step).  Two granule buffers alternate by step parity; a workgroup cannot
-// publish step t + 1 before every workgroup of its row group has published step t, i.e.
-// finished reading step t - 1, so a buffer is only rewritten after its readers are done.
-// Spins are bounded: a timeout writes `tmo` and every workgroup leaves the kernel (the
-// step's logged losses then read NaN).  The workgroups must be co-resident: at most 256 of
-// them (B <= 64), 256 threads and 21 KB of LDS each, which an idle MI355X dispatches at once;
-// hipLaunchCooperativeKernel would guarantee it but measured a 13.5 us gap before and after
-// each launch, against 55 and 48 us for the kernels.  Granule tags carry a per-launch epoch
-// (next_lstm_tags), so the buffers are not cleared between launches.
-// (Round 2's persistent kernel split the columns only, so every workgroup swept all B * H
-// granules of every step: 16 us per step against 8 us of per-step launches.  Here a step
-// takes 2.5 us: the hand-off 0.9, the mat-vec 0.6, the cell update 0.7.)
-using gu64 = __attribute__((address_space(1))) unsigned long long;
-using gu32 = __attribute__((address_space(1))) unsigned;
-constexpr unsigned kSpinLimit = 1u << 22;
-constexpr int kRgH = 256;     // hidden size of the persistent kernels
-constexpr int kRgRows = 4;    // batch rows per row group
-constexpr int kRgUnits = 16;  // units per workgroup: 64 gate columns
-constexpr int kRgCols = 4 * kRgUnits;
-constexpr int kRgGroups = kRgH / kRgUnits;  // workgroups per row group
-constexpr int kRgMaxB = 64;                 // 16 row groups x 16 = 256 workgroups
-
-__device__ __forceinline__ void put_granule(unsigned long long* g, unsigned tag, float v) {
-  __hip_atomic_store((gu64*)(g), ((unsigned long long)tag << 32) | __float_as_uint(v),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Waits until the N granules at g[i * stride] (per-thread list, `live` masks absent rows)
-// carry `tag`, then returns their values; false on timeout (after writing `tmo`).
-template <int N>
-__device__ bool take_granules(const unsigned long long* const (&g)[N], const bool (&live)[N],
-                              unsigned tag, float (&out)[N], unsigned* tmo) {
-  for (unsigned spins = 0;; ++spins) {
-    bool ok = true;
-#pragma unroll
-    for (int k = 0; k < N; ++k) {
-      const unsigned long long v =
-          live[k] ? __hip_atomic_load((const gu64*)(g[k]), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT)
-                  : ((unsigned long long)tag << 32);
-      out[k] = __uint_as_float((unsigned)v);
-      ok &= (unsigned)(v >> 32) == tag;
-    }
-    if (__all(ok)) return true;
-    if (spins >= kSpinLimit) {
-      if ((threadIdx.x & 63) == 0)
-        __hip_atomic_store((gu32*)(tmo), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
-using f32x2 = __attribute__((ext_vector_type(2))) float;
-
-// Rows (r, r + 1) of a mat-vec in one packed FMA (v_pk_fma_f32): each row's sum keeps its
-// own order, so the result is the scalar loop's.
-__device__ __forceinline__ f32x2 fma2(float a0, float a1, float w, f32x2 acc) {
-  return __builtin_elementwise_fma(f32x2{a0, a1}, f32x2{w, w}, acc);
-}
-
-// Global gate column of this workgroup's gate column `col` (gate q = col / kRgUnits).
-__device__ __forceinline__ int rg_gate_col(int cg, int col) {
-  return (col / kRgUnits) * kRgH + cg * kRgUnits + col % kRgUnits;
-}
-
-// Forward: thread (ks = wave, col = lane) accumulates 4 rows x its gate column over the
-// wave's 64-k slice (W in registers, h_{t-1} broadcast from LDS); the four slices are summed
-// in order with gx; threads < 64 run the cells (c in registers across the unroll).
-__global__ void __launch_bounds__(256) lstm_fwd_rg_kernel(
-    const float* __restrict__ gx, const float* __restrict__ wh, const float* __restrict__ h0,
-    int64_t h0_stride, const float* __restrict__ c0, int64_t c0_stride, int B, int T,
-    float* __restrict__ gates, float* __restrict__ h_out, float* __restrict__ c_out,
-    unsigned long long* xg, unsigned tag0, unsigned* tmo) {
-  constexpr int H = kRgH, R = kRgRows, U = kRgUnits, NC = kRgCols;
-  __shared__ __attribute__((aligned(16))) float hs[R][H];
-  __shared__ float red[16][R][NC];
-  __shared__ int s_fail;
-  const int RG = (B + R - 1) / R;
-  const int rg = blockIdx.x % RG, cg = blockIdx.x / RG;  // a row group's blocks: equal % 8
-  const int b0 = rg * R;
-  // Mat-vec thread: 4 gate columns (4 cq .. 4 cq + 3) x the 16-k slice ks: each h value read
-  // from LDS feeds 4 columns x 2 rows (LDS return bandwidth, not the FMAs, bounds the step).
-  const int tid = threadIdx.x, cq = tid & 15, ks = tid >> 4;
-  if (tid == 0) s_fail = 0;
-  float w[4][16];
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const int gc = rg_gate_col(cg, 4 * cq + c);
-#pragma unroll
-    for (int kk = 0; kk < 16; ++kk) w[c][kk] = wh[(size_t)(ks * 16 + kk) * 4 * H + gc];
-  }
-  // Cell threads: (row, unit) = (tid / U, tid % U) for tid < R * U.
-  const bool cell = tid < R * U;
-  const int crow = tid / U, cu = tid % U, cb = min(b0 + crow, B - 1), cj = cg * U + cu;
-  const bool cell_live = cell && b0 + crow < B;
-  float creg = cell ? c0[(size_t)cb * c0_stride + cj] : 0.f;
-  // The 4 h_{t-1} values this thread brings into LDS: e = 4 tid + i -> (row e / H, unit).
-  const unsigned long long* gp[4];
-  bool glive[4];
-  for (int t = 0; t < T; ++t) {
-    // The cell's gx terms (its four gate columns), in flight early.
-    float gxv[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      gxv[q] = cell ? gx[((size_t)cb * T + t) * 4 * H + q * H + cj] : 0.f;
-    float hv[4];
-    if (t == 0) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int e = 4 * tid + i, r = e / H, u = e % H;
-        hv[i] = h0[(size_t)min(b0 + r, B - 1) * h0_stride + u];
-      }
-    } else {
-      const unsigned long long* base = xg + (size_t)((t - 1) & 1) * B * H;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int e = 4 * tid + i, r = e / H, u = e % H;
-        glive[i] = b0 + r < B;
-        gp[i] = base + (size_t)min(b0 + r, B - 1) * H + u;
-      }
-      if (!take_granules<4>(gp, glive, tag0 + (unsigned)t, hv, tmo)) s_fail = 1;
-    }
-    *reinterpret_cast<f32x4*>(&hs[0][0] + 4 * tid) = f32x4{hv[0], hv[1], hv[2], hv[3]};
-    __syncthreads();
-    if (s_fail) return;  // every workgroup leaves on a timeout (its own wait fails too)
-    f32x2 a01[4], a23[4];  // per column: rows (0, 1) and (2, 3)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) a01[c] = a23[c] = f32x2{0.f, 0.f};
-#pragma unroll
-    for (int k4 = 0; k4 < 4; ++k4) {
-      const f32x4 h0v = *reinterpret_cast<const f32x4*>(&hs[0][ks * 16 + 4 * k4]);
-      const f32x4 h1v = *reinterpret_cast<const f32x4*>(&hs[1][ks * 16 + 4 * k4]);
-      const f32x4 h2v = *reinterpret_cast<const f32x4*>(&hs[2][ks * 16 + 4 * k4]);
-      const f32x4 h3v = *reinterpret_cast<const f32x4*>(&hs[3][ks * 16 + 4 * k4]);
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          a01[c] = fma2(h0v[j], h1v[j], w[c][4 * k4 + j], a01[c]);
-          a23[c] = fma2(h2v[j], h3v[j], w[c][4 * k4 + j], a23[c]);
-        }
-    }
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      red[ks][0][4 * cq + c] = a01[c][0];
-      red[ks][1][4 * cq + c] = a01[c][1];
-      red[ks][2][4 * cq + c] = a23[c][0];
-      red[ks][3][4 * cq + c] = a23[c][1];
-    }
-    __syncthreads();
-    if (cell) {
-      // z = gx + the 16 k-slices' partial sums, in order.
-      float z[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int cc = q * U + cu;
-        float sum = red[0][crow][cc];
-#pragma unroll
-        for (int k = 1; k < 16; ++k) sum += red[k][crow][cc];
-        z[q] = gxv[q] + sum;
-      }
-      const float ig = sigmoidf(z[0]), fg = sigmoidf(z[1]);
-      const float gg = tanhf(z[2]), og = sigmoidf(z[3]);
-      const float cn = __fadd_rn(__fmul_rn(fg, creg), __fmul_rn(ig, gg));
-      const float hn = __fmul_rn(og, tanhf(cn));
-      creg = cn;
-      if (cell_live) {
-        const size_t row = (size_t)cb * T + t;
-        gates[row * 4 * H + cj] = ig;
-        gates[row * 4 * H + H + cj] = fg;
-        gates[row * 4 * H + 2 * H + cj] = gg;
-        gates[row * 4 * H + 3 * H + cj] = og;
-        c_out[row * H + cj] = cn;
-        h_out[row * H + cj] = hn;
-        if (t + 1 < T) put_granule(xg + (size_t)(t & 1) * B * H + (size_t)cb * H + cj,
-                                   tag0 + (unsigned)(t + 1), hn);
-      }
-    }
-  }
-}
-
-// Backward: per step t (T-1 .. 0) the cells of (row group, unit group) take dh = dh_head +
-// the partial products published at step t + 1 (summed over the 16 producers in order),
-// form their gate gradients (dgates, stored) and carry dc in registers; then thread u' (one
-// per unit) forms this workgroup's partial product for dh_{t-1}: sum over its 64 gate
-// columns g (in order) of dgates[row][g] W_h[u'][g], W_h row slice in registers, and
-// publishes the 4 rows x 256 values, each consumer reading its 16 units of every producer.
-__global__ void __launch_bounds__(256) lstm_bwd_rg_kernel(
-    const float* __restrict__ dh_head, const float* __restrict__ wh,
-    const float* __restrict__ gates, const float* __restrict__ c_all,
-    const float* __restrict__ c0, int64_t c0_stride, int B, int T,
-    float* __restrict__ dgates, unsigned long long* xb, unsigned tag0, unsigned* tmo) {
-  constexpr int H = kRgH, R = kRgRows, U = kRgUnits, NC = kRgCols, G = kRgGroups;
-  __shared__ float pp[G][R][U];
-  __shared__ __attribute__((aligned(16))) float dgs[R][NC];
-  __shared__ float red[4][R][H];
-  __shared__ int s_fail;
-  const int RG = (B + R - 1) / R;
-  const int rg = blockIdx.x % RG, cg = blockIdx.x / RG;
-  const int b0 = rg * R;
-  const int tid = threadIdx.x;
-  // Partial-product thread: units 4 uq .. 4 uq + 3 x the 16 gate columns of slice gs.
-  const int uq = tid & 63, gs = tid >> 6;
-  if (tid == 0) s_fail = 0;
-  float w[4][16];  // W_h[4 uq + uu][this workgroup's gate column 16 gs + gg]
-#pragma unroll
-  for (int uu = 0; uu < 4; ++uu)
-#pragma unroll
-    for (int gg = 0; gg < 16; ++gg)
-      w[uu][gg] = wh[(size_t)(4 * uq + uu) * 4 * H + rg_gate_col(cg, 16 * gs + gg)];
-  const bool cell = tid < R * U;
-  const int crow = tid / U, cu = tid % U, cb = min(b0 + crow, B - 1), cj = cg * U + cu;
-  const bool cell_live = cell && b0 + crow < B;
-  float dcarry = 0.f;
-  // Granules this thread takes: e = 4 tid + i -> (producer e / (R U), row, unit).
-  const unsigned long long* gp[4];
-  bool glive[4];
-  for (int t = T - 1; t >= 0; --t) {
-    const size_t row = (size_t)cb * T + t;
-    // Cell operands, loaded before the wait.
-    float ig = 0.f, fg = 0.f, gg = 0.f, og = 0.f, cn = 0.f, cprev = 0.f, dhh = 0.f;
-    if (cell) {
-      const float* gr = gates + row * 4 * H;
-      ig = gr[cj]; fg = gr[H + cj]; gg = gr[2 * H + cj]; og = gr[3 * H + cj];
-      cn = c_all[row * H + cj];
-      cprev = t > 0 ? c_all[(row - 1) * H + cj] : c0[(size_t)cb * c0_stride + cj];
-      dhh = dh_head[row * H + cj];
-    }
-    if (t + 1 < T) {
-      const unsigned long long* base = xb + (size_t)((t + 1) & 1) * G * B * H;
-      float v[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int e = 4 * tid + i, pg = e / (R * U), r = (e / U) % R, u = e % U;
-        glive[i] = b0 + r < B;
-        gp[i] = base + ((size_t)pg * B + min(b0 + r, B - 1)) * H + cg * U + u;
-      }
-      if (!take_granules<4>(gp, glive, tag0 + (unsigned)(t + 1), v, tmo)) s_fail = 1;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int e = 4 * tid + i;
-        (&pp[0][0][0])[e] = v[i];
-      }
-    }
-    __syncthreads();
-    if (s_fail) return;
-    if (cell) {
-      float dhn = 0.f;
-      if (t + 1 < T)
-        for (int pg = 0; pg < G; ++pg) dhn += pp[pg][crow][cu];
-      const float tc = tanhf(cn);
-      const float dh = dhh + dhn;
-      const float dc = dcarry + dh * og * (1.f - tc * tc);
-      const float di = dc * gg * ig * (1.f - ig), df = dc * cprev * fg * (1.f - fg);
-      const float dg = dc * ig * (1.f - gg * gg), dO = dh * tc * og * (1.f - og);
-      dcarry = dc * fg;
-      dgs[crow][cu] = di;
-      dgs[crow][U + cu] = df;
-      dgs[crow][2 * U + cu] = dg;
-      dgs[crow][3 * U + cu] = dO;
-      if (cell_live) {
-        float* d = dgates + row * 4 * H;
-        d[cj] = di;
-        d[H + cj] = df;
-        d[2 * H + cj] = dg;
-        d[3 * H + cj] = dO;
-      }
-    }
-    __syncthreads();
-    if (t > 0) {
-      f32x2 a01[4], a23[4];  // per unit: rows (0, 1) and (2, 3)
-#pragma unroll
-      for (int uu = 0; uu < 4; ++uu) a01[uu] = a23[uu] = f32x2{0.f, 0.f};
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const f32x4 d0 = *reinterpret_cast<const f32x4*>(&dgs[0][16 * gs + 4 * g4]);
-        const f32x4 d1 = *reinterpret_cast<const f32x4*>(&dgs[1][16 * gs + 4 * g4]);
-        const f32x4 d2 = *reinterpret_cast<const f32x4*>(&dgs[2][16 * gs + 4 * g4]);
-        const f32x4 d3 = *reinterpret_cast<const f32x4*>(&dgs[3][16 * gs + 4 * g4]);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int uu = 0; uu < 4; ++uu) {
-            a01[uu] = fma2(d0[j], d1[j], w[uu][4 * g4 + j], a01[uu]);
-            a23[uu] = fma2(d2[j], d3[j], w[uu][4 * g4 + j], a23[uu]);
-          }
-      }
-#pragma unroll
-      for (int uu = 0; uu < 4; ++uu) {
-        red[gs][0][4 * uq + uu] = a01[uu][0];
-        red[gs][1][4 * uq + uu] = a01[uu][1];
-        red[gs][2][4 * uq + uu] = a23[uu][0];
-        red[gs][3][4 * uq + uu] = a23[uu][1];
-      }
-      __syncthreads();
-      // Thread u' = tid publishes this workgroup's partial for its unit, 4 rows (the four
-      // gate-column slices summed in order).
-      unsigned long long* out = xb + (size_t)(t & 1) * G * B * H + (size_t)cg * B * H;
-#pragma unroll
-      for (int r = 0; r < R; ++r)
-        if (b0 + r < B)
-          put_granule(out + (size_t)(b0 + r) * H + tid, tag0 + (unsigned)t,
-                      ((red[0][r][tid] + red[1][r][tid]) + red[2][r][tid]) + red[3][r][tid]);
-    }
-  }
-}
+// The whole T-step LSTM forward and BPTT in one launch each (lstm.h lstm_fwd_rg_kernel /
+// lstm_bwd_rg_kernel, H = 256 here: 4 rows x 16 units per workgroup, up to 64 rows).
+constexpr int kRgH = 256;                       // hidden size of the persistent kernels
+constexpr int kRgGroups = RgShape<kRgH>::G;     // workgroups per row group
+constexpr int kRgMaxB = 64;                     // 16 row groups x 16 = 256 workgroups
 
 // The persistent unroll's shape: H = 256 and at most 64 rows (256 co-resident workgroups).
 bool lstm_persistent(const acme_impala* l, int B) {
@@ -826,9 +516,9 @@ int network_forward(acme_impala* l, const void* obs, const int32_t* prev_a, cons
     const size_t smem = lstm_fwd_smem(B, H);
     if (lstm_persistent(l, B)) {  // one launch for the whole unroll (lstm_fwd_rg_kernel)
       const unsigned tag0 = next_lstm_tags(l, st);
-      lstm_fwd_rg_kernel<<<(unsigned)(ceil_div(B, kRgRows) * kRgGroups), 256, 0, st>>>(
-          l->gx, P(l, l->params, l->t_wh), h0, state_stride, c0, state_stride, B, T, l->gates,
-          l->h, l->c, l->xg, tag0, tmo);
+      lstm_fwd_rg_kernel<kRgH><<<(unsigned)(ceil_div(B, kRgRows) * kRgGroups), 256, 0, st>>>(
+          l->gx, P(l, l->params, l->t_wh), h0, state_stride, c0, state_stride, B, T, T, 1,
+          l->gates, l->h, l->c, l->xg, tag0, tmo);
       IM_CHECK();
     } else
     for (int t = 0; t < T; ++t) {
@@ -919,9 +609,9 @@ int impala_step_impl(acme_impala* l, const acme_sequence_batch* bt, float* metri
     ACME_PROF("impala_lstm_bwd", st, 2.0 * rows * (double)H * 4 * H, 0.0);
     if (lstm_persistent(l, B)) {  // one launch for the whole BPTT (lstm_bwd_rg_kernel)
       const unsigned tag0 = next_lstm_tags(l, st);
-      lstm_bwd_rg_kernel<<<(unsigned)(ceil_div(B, kRgRows) * kRgGroups), 256, 0, st>>>(
-          l->dh, P(l, l->params, l->t_wh), l->gates, l->c, bt->c0, bt->state_stride, B, T,
-          l->dgates, l->xb, tag0, l->tmo);
+      lstm_bwd_rg_kernel<kRgH><<<(unsigned)(ceil_div(B, kRgRows) * kRgGroups), 256, 0, st>>>(
+          l->dh, P(l, l->params, l->t_wh), l->gates, l->c, bt->c0, bt->state_stride, B, T, 0,
+          T, 1, l->dgates, l->xb, tag0, l->tmo);
       IM_CHECK();
     } else {
     ACME_HIP_TRY(hipMemsetAsync(l->dc, 0, (size_t)B * H * sizeof(float), st));

@@ -420,6 +420,344 @@ __global__ void __launch_bounds__(256) lstm_bwd_step_kernel(
   }
 }
 
+// ---------------------------------------------------------------- persistent unroll
+// The whole LSTM forward (and, below, BPTT) in ONE launch: workgroup (rg, cg) owns kRgRows
+// batch rows (a row group) x kRgUnits units (cg), i.e. 4 * kRgUnits gate columns, and keeps
+// its W_h slice (all H k of those columns) in registers for the whole unroll.  A step needs
+// h_{t-1} of its own rows only (the sequences are independent), so each workgroup exchanges
+// kRgRows x H values per step with the H / kRgUnits workgroups of its row group, as 8-byte
+// {tag, value} granules (agent-scope relaxed atomic stores and loads: the data is its own
+// flag, cdna_hip_programming.md G16 / MI355X_MICROARCH.md "handoff-1to1").  Two granule
+// buffers alternate by step parity; a workgroup cannot publish step t + 1 before every
+// workgroup of its row group has published step t, i.e. finished reading step t - 1, so a
+// buffer is only rewritten after its readers are done.  Spins are bounded: a timeout writes
+// `tmo` and every workgroup leaves the kernel (the learner's logged loss then reads NaN).
+// The workgroups must be co-resident: at most 256 of them (ceil(B / 4) x H / 16), 256
+// threads each, which an idle MI355X dispatches at once (hipLaunchCooperativeKernel would
+// guarantee it but measured a 13.5 us gap before and after each launch).  Granule tags carry
+// a per-launch epoch, so the buffers are not cleared between launches.  A row group's
+// workgroups share blockIdx % RG, i.e. one XCD (one L2) when RG = 8.
+// Rows (b, t) of gx / gates / h / c / dh / dgates are b * rs_b + t * rs_t (IMPALA batch-major,
+// R2D2 time-major).  H = 256 (IMPALA): 2.5 us per step (hand-off 0.9, mat-vec 0.6, cell 0.7).
+using gu64 = __attribute__((address_space(1))) unsigned long long;
+using gu32 = __attribute__((address_space(1))) unsigned;
+constexpr unsigned kSpinLimit = 1u << 22;
+constexpr int kRgRows = 4;    // batch rows per row group
+constexpr int kRgUnits = 16;  // units per workgroup: 64 gate columns
+constexpr int kRgCols = 4 * kRgUnits;
+
+template <int H>
+struct RgShape {
+  static_assert(H % 256 == 0 && H <= 1024, "persistent unroll: H a multiple of 256");
+  static constexpr int G = H / kRgUnits;           // workgroups per row group
+  static constexpr int KW = H / 16;                // forward: k per slice (16 slices)
+  static constexpr int HV = kRgRows * H / 256;     // forward: h values brought in per thread
+  static constexpr int UT = H / 4;                 // backward: threads per gate-column slice
+  static constexpr int GS = 256 / UT;              // backward: gate-column slices
+  static constexpr int GW = kRgCols / GS;          // backward: gate columns per slice
+  static constexpr int PV = G * kRgRows * kRgUnits / 256;  // backward: granules per thread
+  static constexpr int PU = H / 256;               // backward: units published per thread
+};
+
+__device__ __forceinline__ void put_granule(unsigned long long* g, unsigned tag, float v) {
+  __hip_atomic_store((gu64*)(g), ((unsigned long long)tag << 32) | __float_as_uint(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Waits until the N granules at g[k] (per-thread list, `live` masks absent rows) carry `tag`,
+// then returns their values; false on timeout (after writing `tmo`).
+template <int N>
+__device__ bool take_granules(const unsigned long long* const (&g)[N], const bool (&live)[N],
+                              unsigned tag, float (&out)[N], unsigned* tmo) {
+  for (unsigned spins = 0;; ++spins) {
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      const unsigned long long v =
+          live[k] ? __hip_atomic_load((const gu64*)(g[k]), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT)
+                  : ((unsigned long long)tag << 32);
+      out[k] = __uint_as_float((unsigned)v);
+      ok &= (unsigned)(v >> 32) == tag;
+    }
+    if (__all(ok)) return true;
+    if (spins >= kSpinLimit) {
+      if ((threadIdx.x & 63) == 0)
+        __hip_atomic_store((gu32*)(tmo), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+using f32x2 = __attribute__((ext_vector_type(2))) float;
+
+// Rows (r, r + 1) of a mat-vec in one packed FMA (v_pk_fma_f32): each row's sum keeps its
+// own order, so the result is the scalar loop's.
+__device__ __forceinline__ f32x2 fma2(float a0, float a1, float w, f32x2 acc) {
+  return __builtin_elementwise_fma(f32x2{a0, a1}, f32x2{w, w}, acc);
+}
+
+// Global gate column of this workgroup's gate column `col` (gate q = col / kRgUnits).
+template <int H>
+__device__ __forceinline__ int rg_gate_col(int cg, int col) {
+  return (col / kRgUnits) * H + cg * kRgUnits + col % kRgUnits;
+}
+
+// Forward: thread (ks = tid / 16, cq = tid % 16) accumulates 4 rows x 4 gate columns over
+// the k-slice ks (W in registers, h_{t-1} broadcast from LDS: each h value read feeds 4
+// columns x 2 rows, LDS return bandwidth rather than the FMAs bounds the step); the 16
+// slices are summed in order with gx; threads < 64 run the cells (c in registers).
+template <int H>
+__global__ void __launch_bounds__(256) lstm_fwd_rg_kernel(
+    const float* __restrict__ gx, const float* __restrict__ wh, const float* __restrict__ h0,
+    int64_t h0_stride, const float* __restrict__ c0, int64_t c0_stride, int B, int T,
+    int64_t rs_b, int64_t rs_t, float* __restrict__ gates, float* __restrict__ h_out,
+    float* __restrict__ c_out, unsigned long long* xg, unsigned tag0, unsigned* tmo) {
+  using S = RgShape<H>;
+  constexpr int R = kRgRows, U = kRgUnits, NC = kRgCols, KW = S::KW, HV = S::HV;
+  __shared__ __attribute__((aligned(16))) float hs[R][H];
+  __shared__ float red[16][R][NC];
+  __shared__ int s_fail;
+  const int RG = (B + R - 1) / R;
+  const int rg = blockIdx.x % RG, cg = blockIdx.x / RG;
+  const int b0 = rg * R;
+  const int tid = threadIdx.x, cq = tid & 15, ks = tid >> 4;
+  if (tid == 0) s_fail = 0;
+  float w[4][KW];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int gc = rg_gate_col<H>(cg, 4 * cq + c);
+#pragma unroll
+    for (int kk = 0; kk < KW; ++kk) w[c][kk] = wh[(size_t)(ks * KW + kk) * 4 * H + gc];
+  }
+  // Cell threads: (row, unit) = (tid / U, tid % U) for tid < R * U.
+  const bool cell = tid < R * U;
+  const int crow = tid / U, cu = tid % U, cb = min(b0 + crow, B - 1), cj = cg * U + cu;
+  const bool cell_live = cell && b0 + crow < B;
+  float creg = cell ? c0[(size_t)cb * c0_stride + cj] : 0.f;
+  // The HV h_{t-1} values this thread brings into LDS: e = HV tid + i -> (row e / H, unit).
+  const unsigned long long* gp[HV];
+  bool glive[HV];
+  for (int t = 0; t < T; ++t) {
+    // The cell's gx terms (its four gate columns), in flight early.
+    float gxv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      gxv[q] = cell ? gx[((size_t)cb * rs_b + (size_t)t * rs_t) * 4 * H + q * H + cj] : 0.f;
+    float hv[HV];
+    if (t == 0) {
+#pragma unroll
+      for (int i = 0; i < HV; ++i) {
+        const int e = HV * tid + i, r = e / H, u = e % H;
+        hv[i] = h0[(size_t)min(b0 + r, B - 1) * h0_stride + u];
+      }
+    } else {
+      const unsigned long long* base = xg + (size_t)((t - 1) & 1) * B * H;
+#pragma unroll
+      for (int i = 0; i < HV; ++i) {
+        const int e = HV * tid + i, r = e / H, u = e % H;
+        glive[i] = b0 + r < B;
+        gp[i] = base + (size_t)min(b0 + r, B - 1) * H + u;
+      }
+      if (!take_granules<HV>(gp, glive, tag0 + (unsigned)t, hv, tmo)) s_fail = 1;
+    }
+#pragma unroll
+    for (int i = 0; i < HV; i += 4)
+      *reinterpret_cast<f32x4*>(&hs[0][0] + HV * tid + i) =
+          f32x4{hv[i], hv[i + 1], hv[i + 2], hv[i + 3]};
+    __syncthreads();
+    if (s_fail) return;  // every workgroup leaves on a timeout (its own wait fails too)
+    f32x2 a01[4], a23[4];  // per column: rows (0, 1) and (2, 3)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) a01[c] = a23[c] = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int k4 = 0; k4 < KW / 4; ++k4) {
+      const f32x4 h0v = *reinterpret_cast<const f32x4*>(&hs[0][ks * KW + 4 * k4]);
+      const f32x4 h1v = *reinterpret_cast<const f32x4*>(&hs[1][ks * KW + 4 * k4]);
+      const f32x4 h2v = *reinterpret_cast<const f32x4*>(&hs[2][ks * KW + 4 * k4]);
+      const f32x4 h3v = *reinterpret_cast<const f32x4*>(&hs[3][ks * KW + 4 * k4]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          a01[c] = fma2(h0v[j], h1v[j], w[c][4 * k4 + j], a01[c]);
+          a23[c] = fma2(h2v[j], h3v[j], w[c][4 * k4 + j], a23[c]);
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      red[ks][0][4 * cq + c] = a01[c][0];
+      red[ks][1][4 * cq + c] = a01[c][1];
+      red[ks][2][4 * cq + c] = a23[c][0];
+      red[ks][3][4 * cq + c] = a23[c][1];
+    }
+    __syncthreads();
+    if (cell) {
+      // z = gx + the 16 k-slices' partial sums, in order.
+      float z[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int cc = q * U + cu;
+        float sum = red[0][crow][cc];
+#pragma unroll
+        for (int k = 1; k < 16; ++k) sum += red[k][crow][cc];
+        z[q] = gxv[q] + sum;
+      }
+      const float ig = sigmoidf(z[0]), fg = sigmoidf(z[1]);
+      const float gg = tanhf(z[2]), og = sigmoidf(z[3]);
+      const float cn = __fadd_rn(__fmul_rn(fg, creg), __fmul_rn(ig, gg));
+      const float hn = __fmul_rn(og, tanhf(cn));
+      creg = cn;
+      if (cell_live) {
+        const size_t row = (size_t)cb * rs_b + (size_t)t * rs_t;
+        gates[row * 4 * H + cj] = ig;
+        gates[row * 4 * H + H + cj] = fg;
+        gates[row * 4 * H + 2 * H + cj] = gg;
+        gates[row * 4 * H + 3 * H + cj] = og;
+        c_out[row * H + cj] = cn;
+        h_out[row * H + cj] = hn;
+        if (t + 1 < T) put_granule(xg + (size_t)(t & 1) * B * H + (size_t)cb * H + cj,
+                                   tag0 + (unsigned)(t + 1), hn);
+      }
+    }
+  }
+}
+
+// Backward: per step t (T-1 .. t_stop) the cells of (row group, unit group) take dh =
+// dh_head + the partial products published at step t + 1 (summed over the G producers in
+// order), form their gate gradients (dgates, stored) and carry dc in registers; then thread
+// (gs = tid / UT, uq = tid % UT) forms its 4 units' share of this workgroup's partial
+// product for dh_{t-1} over the gate-column slice gs (W_h row slice in registers), and the
+// slices are summed in order and published (4 rows x H values), each consumer reading its 16
+// units of every producer.  BPTT stops at t_stop (R2D2's burn-in: no gradient into it).
+template <int H>
+__global__ void __launch_bounds__(256) lstm_bwd_rg_kernel(
+    const float* __restrict__ dh_head, const float* __restrict__ wh,
+    const float* __restrict__ gates, const float* __restrict__ c_all,
+    const float* __restrict__ c0, int64_t c0_stride, int B, int T, int t_stop, int64_t rs_b,
+    int64_t rs_t, float* __restrict__ dgates, unsigned long long* xb, unsigned tag0,
+    unsigned* tmo) {
+  using S = RgShape<H>;
+  constexpr int R = kRgRows, U = kRgUnits, NC = kRgCols, G = S::G;
+  constexpr int UT = S::UT, GS = S::GS, GW = S::GW, PV = S::PV, PU = S::PU;
+  __shared__ float pp[G][R][U];
+  __shared__ __attribute__((aligned(16))) float dgs[R][NC];
+  __shared__ float red[GS][R][H];
+  __shared__ int s_fail;
+  const int RG = (B + R - 1) / R;
+  const int rg = blockIdx.x % RG, cg = blockIdx.x / RG;
+  const int b0 = rg * R;
+  const int tid = threadIdx.x;
+  const int uq = tid % UT, gs = tid / UT;
+  if (tid == 0) s_fail = 0;
+  float w[4][GW];  // W_h[4 uq + uu][this workgroup's gate column GW gs + gg]
+#pragma unroll
+  for (int uu = 0; uu < 4; ++uu)
+#pragma unroll
+    for (int gg = 0; gg < GW; ++gg)
+      w[uu][gg] = wh[(size_t)(4 * uq + uu) * 4 * H + rg_gate_col<H>(cg, GW * gs + gg)];
+  const bool cell = tid < R * U;
+  const int crow = tid / U, cu = tid % U, cb = min(b0 + crow, B - 1), cj = cg * U + cu;
+  const bool cell_live = cell && b0 + crow < B;
+  float dcarry = 0.f;
+  // Granules this thread takes: e = PV tid + i -> (producer e / (R U), row, unit).
+  const unsigned long long* gp[PV];
+  bool glive[PV];
+  for (int t = T - 1; t >= t_stop; --t) {
+    const size_t row = (size_t)cb * rs_b + (size_t)t * rs_t;
+    // Cell operands, loaded before the wait.
+    float ig = 0.f, fg = 0.f, gg = 0.f, og = 0.f, cn = 0.f, cprev = 0.f, dhh = 0.f;
+    if (cell) {
+      const float* gr = gates + row * 4 * H;
+      ig = gr[cj]; fg = gr[H + cj]; gg = gr[2 * H + cj]; og = gr[3 * H + cj];
+      cn = c_all[row * H + cj];
+      cprev = t > 0 ? c_all[(row - rs_t) * H + cj] : c0[(size_t)cb * c0_stride + cj];
+      dhh = dh_head[row * H + cj];
+    }
+    if (t + 1 < T) {
+      const unsigned long long* base = xb + (size_t)((t + 1) & 1) * G * B * H;
+      float v[PV];
+#pragma unroll
+      for (int i = 0; i < PV; ++i) {
+        const int e = PV * tid + i, pg = e / (R * U), r = (e / U) % R, u = e % U;
+        glive[i] = b0 + r < B;
+        gp[i] = base + ((size_t)pg * B + min(b0 + r, B - 1)) * H + cg * U + u;
+      }
+      if (!take_granules<PV>(gp, glive, tag0 + (unsigned)(t + 1), v, tmo)) s_fail = 1;
+#pragma unroll
+      for (int i = 0; i < PV; ++i) (&pp[0][0][0])[PV * tid + i] = v[i];
+    }
+    __syncthreads();
+    if (s_fail) return;
+    if (cell) {
+      float dhn = 0.f;
+      if (t + 1 < T)
+        for (int pg = 0; pg < G; ++pg) dhn += pp[pg][crow][cu];
+      const float tc = tanhf(cn);
+      const float dh = dhh + dhn;
+      const float dc = dcarry + dh * og * (1.f - tc * tc);
+      const float di = dc * gg * ig * (1.f - ig), df = dc * cprev * fg * (1.f - fg);
+      const float dg = dc * ig * (1.f - gg * gg), dO = dh * tc * og * (1.f - og);
+      dcarry = dc * fg;
+      dgs[crow][cu] = di;
+      dgs[crow][U + cu] = df;
+      dgs[crow][2 * U + cu] = dg;
+      dgs[crow][3 * U + cu] = dO;
+      if (cell_live) {
+        float* d = dgates + row * 4 * H;
+        d[cj] = di;
+        d[H + cj] = df;
+        d[2 * H + cj] = dg;
+        d[3 * H + cj] = dO;
+      }
+    }
+    __syncthreads();
+    if (t > t_stop) {
+      f32x2 a01[4], a23[4];  // per unit: rows (0, 1) and (2, 3)
+#pragma unroll
+      for (int uu = 0; uu < 4; ++uu) a01[uu] = a23[uu] = f32x2{0.f, 0.f};
+#pragma unroll
+      for (int g4 = 0; g4 < GW / 4; ++g4) {
+        const f32x4 d0 = *reinterpret_cast<const f32x4*>(&dgs[0][GW * gs + 4 * g4]);
+        const f32x4 d1 = *reinterpret_cast<const f32x4*>(&dgs[1][GW * gs + 4 * g4]);
+        const f32x4 d2 = *reinterpret_cast<const f32x4*>(&dgs[2][GW * gs + 4 * g4]);
+        const f32x4 d3 = *reinterpret_cast<const f32x4*>(&dgs[3][GW * gs + 4 * g4]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int uu = 0; uu < 4; ++uu) {
+            a01[uu] = fma2(d0[j], d1[j], w[uu][4 * g4 + j], a01[uu]);
+            a23[uu] = fma2(d2[j], d3[j], w[uu][4 * g4 + j], a23[uu]);
+          }
+      }
+#pragma unroll
+      for (int uu = 0; uu < 4; ++uu) {
+        red[gs][0][4 * uq + uu] = a01[uu][0];
+        red[gs][1][4 * uq + uu] = a01[uu][1];
+        red[gs][2][4 * uq + uu] = a23[uu][0];
+        red[gs][3][4 * uq + uu] = a23[uu][1];
+      }
+      __syncthreads();
+      // Units tid, tid + 256, ...: this workgroup's partial for 4 rows (the gate-column
+      // slices summed in order).
+      unsigned long long* out = xb + (size_t)(t & 1) * G * B * H + (size_t)cg * B * H;
+#pragma unroll
+      for (int p = 0; p < PU; ++p) {
+        const int u = tid + 256 * p;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          if (b0 + r >= B) continue;
+          float v = red[0][r][u];
+#pragma unroll
+          for (int k = 1; k < GS; ++k) v += red[k][r][u];
+          put_granule(out + (size_t)(b0 + r) * H + u, tag0 + (unsigned)t, v);
+        }
+      }
+    }
+  }
+}
+
 // gx = OAR(emb) @ W_i + b from the plane GEMM's split-K partials of feat @ W_i[0:F]: the
 // one-hot(prev a) row of W_i, tanh(prev r) times its last row and the bias are added here
 // (the embedding's last A + 1 columns), one thread per (row, 4 gate columns).

@@ -118,9 +118,38 @@ struct acme_r2d2 {
   StepGuard* guard = nullptr;
   int64_t* host_skipped = nullptr;
   int64_t last_rows = 0;
+  // One-launch LSTM unroll and BPTT (lstm.h lstm_fwd_rg_kernel / lstm_bwd_rg_kernel) for
+  // H = 256 or 512 with at most 256 co-resident workgroups: the h / dh granule exchange
+  // buffers, the launch epoch of their tags, the sticky spin-timeout word; lstm_steps: the
+  // per-step kernels instead (acme_r2d2_set_lstm_unroll, tests).
+  unsigned long long *xg = nullptr, *xb = nullptr;
+  unsigned* tmo = nullptr;
+  unsigned lstm_epoch = 0;
+  bool lstm_steps = false;
 };
 
 namespace {
+
+// The one-launch unroll's shapes: H of 256 or 512 and ceil(B / 4) x H / 16 <= 256
+// workgroups (B <= 32 at H = 512, the R2D2 Atari batch).
+bool rg_shape(int H, int B) {
+  return (H == 256 || H == 512) && (int64_t)ceil_div(B, kRgRows) * (H / kRgUnits) <= 256;
+}
+bool lstm_persistent(const acme_r2d2* l, int B) {
+  return l->xg && !l->lstm_steps && rg_shape(l->H, B);
+}
+// The granule tags of the next one-launch unroll: tag0 + t (t < kMaxSeq = 256), tag0 = 256 x
+// a per-learner launch count, so no launch can match a granule an earlier one left; the
+// buffers are cleared once the count wraps.
+unsigned next_lstm_tags(acme_r2d2* l, hipStream_t st) {
+  if (++l->lstm_epoch >= (1u << 24)) {
+    l->lstm_epoch = 1;
+    const int B = l->cfg.max_batch, H = l->H;
+    (void)hipMemsetAsync(l->xg, 0, (size_t)2 * B * H * 8, st);
+    (void)hipMemsetAsync(l->xb, 0, (size_t)2 * (H / kRgUnits) * B * H * 8, st);
+  }
+  return l->lstm_epoch << 8;
+}
 
 int add_tensor(acme_r2d2* l, const std::string& name, std::initializer_list<int64_t> shape) {
   Tensor t;
@@ -275,7 +304,8 @@ struct R2Loss {
   const float *reward, *discount;
   const double* probs;    // [B]
   int B, T, BI, A, n;
-  float gamma, beta, eta, one_minus_eta;
+  float gamma, eta, one_minus_eta;
+  double beta;  // f64, as the reference's exponent of the f64 weights
   double n_replay;  // max_replay_size
   float* g;        // [L][B] d loss / d q[a] (row t * B + b)
   int32_t* act;    // [L][B]
@@ -341,10 +371,10 @@ __global__ void __launch_bounds__(64) r2d2_loss_kernel(const R2Loss a) {
   const int B = a.B, T = a.T, BI = a.BI, L = T - BI, Tm = L - 1;
   // Importance weight of this sequence: (1 / (N p))^beta / max_b, f64, cast to f32.
   double wmx = 0.0;
-  for (int i = lane; i < B; i += 64) wmx = fmax(wmx, pow(1.0 / (a.n_replay * a.probs[i]), (double)a.beta));
+  for (int i = lane; i < B; i += 64) wmx = fmax(wmx, pow(1.0 / (a.n_replay * a.probs[i]), a.beta));
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) wmx = fmax(wmx, __shfl_xor(wmx, o, 64));
-  const float w = (float)(pow(1.0 / (a.n_replay * a.probs[b]), (double)a.beta) / wmx);
+  const float w = (float)(pow(1.0 / (a.n_replay * a.probs[b]), a.beta) / wmx);
   const float inv_b = div_rn(1.f, (float)B);
   double sq = 0.0;
   for (int t = lane; t < Tm; t += 64) {
@@ -390,12 +420,13 @@ __global__ void __launch_bounds__(64) r2d2_loss_kernel(const R2Loss a) {
   }
 }
 
+// The batch loss; NaN once a one-launch LSTM unroll has timed out (the sticky word `tmo`).
 __global__ void r2d2_loss_sum_kernel(const double* __restrict__ part, int B,
-                                     float* __restrict__ loss) {
+                                     float* __restrict__ loss, const unsigned* __restrict__ tmo) {
   if (threadIdx.x != 0) return;
   double s = 0.0;
   for (int b = 0; b < B; ++b) s += part[b];
-  loss[0] = (float)(s / (double)B);
+  loss[0] = tmo && *tmo ? NAN : (float)(s / (double)B);
 }
 
 // dW_h = h_prev^T dgates over the suffix rows (time-major): h_prev of row m (global row
@@ -501,6 +532,19 @@ int network_forward(acme_r2d2* l, const float* prm, const acme_sequence_batch* b
     const float* h0 = l->cfg.store_lstm_state ? bt->h0 : l->zero_state;
     const float* c0 = l->cfg.store_lstm_state ? bt->c0 : l->zero_state;
     const int64_t s0 = l->cfg.store_lstm_state ? bt->state_stride : H;
+    if (lstm_persistent(l, B)) {  // one launch for the whole unroll, burn-in included
+      const unsigned tag0 = next_lstm_tags(l, st);
+      const unsigned nblk = (unsigned)(ceil_div(B, kRgRows) * (H / kRgUnits));
+      if (H == 512)
+        lstm_fwd_rg_kernel<512><<<nblk, 256, 0, st>>>(l->gx, P(l, prm, l->t_wh), h0, s0, c0, s0,
+                                                      B, T, 1, B, l->gates, l->h, l->c, l->xg,
+                                                      tag0, l->tmo);
+      else
+        lstm_fwd_rg_kernel<256><<<nblk, 256, 0, st>>>(l->gx, P(l, prm, l->t_wh), h0, s0, c0, s0,
+                                                      B, T, 1, B, l->gates, l->h, l->c, l->xg,
+                                                      tag0, l->tmo);
+      R2_CHECK();
+    } else {
     const dim3 grid((unsigned)(H / kFwdUnits), (unsigned)ceil_div(B, l->bc));
     for (int t = 0; t < T; ++t) {
       const float* hp = t == 0 ? h0 : l->h + (size_t)(t - 1) * B * H;
@@ -509,6 +553,7 @@ int network_forward(acme_r2d2* l, const float* prm, const acme_sequence_batch* b
       lstm_fwd_step_kernel<<<grid, 256, l->fwd_smem, st>>>(
           l->gx, P(l, prm, l->t_wh), hp, hs, cp, hs, B, 1, B, t, H, l->gates, l->h, l->c, l->bc);
       R2_CHECK();
+    }
     }
   }
   {  // DuellingMLP: the fused [value | advantage] hidden layer over the suffix rows
@@ -584,7 +629,7 @@ int r2d2_step_impl(acme_r2d2* l, const acme_sequence_batch* bt, const double* pr
     a.g = l->g; a.act = l->act; a.errors = errors; a.prio = prio; a.loss_part = l->loss_part;
     r2d2_loss_kernel<<<(unsigned)B, 64, 0, st>>>(a);
     R2_CHECK();
-    r2d2_loss_sum_kernel<<<1, 64, 0, st>>>(l->loss_part, B, loss);
+    r2d2_loss_sum_kernel<<<1, 64, 0, st>>>(l->loss_part, B, loss, l->tmo);
     R2_CHECK();
   }
   float* gr = l->grads;
@@ -622,15 +667,29 @@ int r2d2_step_impl(acme_r2d2* l, const acme_sequence_batch* bt, const double* pr
     ACME_PROF("r2d2_lstm_bwd", st, 2.0 * RL * (double)H * 4 * H, 0.0);
     const float* c0 = l->cfg.store_lstm_state ? bt->c0 : l->zero_state;
     const int64_t s0 = l->cfg.store_lstm_state ? bt->state_stride : H;
-    ACME_HIP_TRY(hipMemsetAsync(l->dc, 0, (size_t)B * H * sizeof(float), st));
     // dgates rows are those of the suffix: the kernel's row (t, b) = t B + b is offset by
     // -BI B so that t >= BI lands on dgates[(t - BI) B + b].
     float* dg = l->dgates - (ptrdiff_t)BI * B * 4 * H;
+    if (lstm_persistent(l, B)) {  // one launch for the whole BPTT, stopping at the burn-in
+      const unsigned tag0 = next_lstm_tags(l, st);
+      const unsigned nblk = (unsigned)(ceil_div(B, kRgRows) * (H / kRgUnits));
+      if (H == 512)
+        lstm_bwd_rg_kernel<512><<<nblk, 256, 0, st>>>(l->dh, P(l, prm, l->t_wh), l->gates, l->c,
+                                                      c0, s0, B, T, BI, 1, B, dg, l->xb, tag0,
+                                                      l->tmo);
+      else
+        lstm_bwd_rg_kernel<256><<<nblk, 256, 0, st>>>(l->dh, P(l, prm, l->t_wh), l->gates, l->c,
+                                                      c0, s0, B, T, BI, 1, B, dg, l->xb, tag0,
+                                                      l->tmo);
+      R2_CHECK();
+    } else {
+    ACME_HIP_TRY(hipMemsetAsync(l->dc, 0, (size_t)B * H * sizeof(float), st));
     const dim3 bgrid((unsigned)(H / kUnits), (unsigned)ceil_div(B, kRowChunk));
     for (int t = T - 1; t >= BI; --t) {
       lstm_bwd_step_kernel<<<bgrid, 256, 0, st>>>(l->dh, P(l, prm, l->t_wh), l->gates, l->c,
                                                        c0, s0, l->dc, dg, B, T, t, H, 1, B);
       R2_CHECK();
+    }
     }
   }
   {  // W_h over h_prev of the suffix rows
@@ -900,6 +959,16 @@ int acme_r2d2_create(const acme_r2d2_config* cfg, acme_r2d2** out) {
       (rc = dev_alloc(l, &l->err_tmp, RL)) || (rc = dev_alloc(l, &l->prio_tmp, B)) ||
       (rc = dev_alloc(l, &l->loss_tmp, 1)) || (rc = dev_alloc(l, &l->dev_step, 1)))
     return fail(rc);
+  if (rg_shape(H, B)) {  // the one-launch unroll's granule buffers (never cleared per launch)
+    const int64_t G = H / kRgUnits;
+    if ((rc = dev_alloc(l, &l->xg, (int64_t)2 * B * H)) ||
+        (rc = dev_alloc(l, &l->xb, 2 * G * B * H)) || (rc = dev_alloc(l, &l->tmo, 4)))
+      return fail(rc);
+    if (hipMemset(l->xg, 0, (size_t)2 * B * H * 8) != hipSuccess ||
+        hipMemset(l->xb, 0, (size_t)2 * G * B * H * 8) != hipSuccess ||
+        hipMemset(l->tmo, 0, 4 * sizeof(unsigned)) != hipSuccess)
+      return fail((set_error("hipMemset failed"), ACME_ERR_HIP));
+  }
   if (hipMemset(l->zero_state, 0, (size_t)B * H * sizeof(float)) != hipSuccess ||
       hipMemset(l->dev_step, 0, sizeof(int64_t)) != hipSuccess)
     return fail((set_error("hipMemset failed"), ACME_ERR_HIP));
@@ -983,6 +1052,12 @@ int acme_r2d2_step(acme_r2d2* l, const acme_sequence_batch* b, const double* pro
   return ACME_OK;
 }
 
+int acme_r2d2_set_lstm_unroll(acme_r2d2* l, int32_t mode) {
+  ACME_CHECK_ARG(l && (mode == 0 || mode == 1), "mode must be 0 (one launch) or 1 (per step)");
+  l->lstm_steps = mode == 1;
+  return ACME_OK;
+}
+
 int64_t acme_r2d2_skipped_steps(const acme_r2d2* l) {
   if (!l || !l->host_skipped) return 0;
   return *reinterpret_cast<volatile const int64_t*>(l->host_skipped);
@@ -1046,6 +1121,7 @@ int acme_r2d2_debug_buffer(const acme_r2d2* l, const char* name, const float** o
       ACME_HIP_TRY(hipDeviceSynchronize());
     }
   }
+  else if (n == "lstm_timeout") { *out = reinterpret_cast<const float*>(l->tmo); *count = l->tmo ? 1 : 0; }
   else ACME_CHECK_ARG(false, "unknown debug buffer '%s'", name);
   return ACME_OK;
 }

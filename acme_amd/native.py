@@ -1075,6 +1075,10 @@ class NativeR2D2:
     def num_steps(self, n: int) -> None:
         check(lib().acme_r2d2_set_num_steps(self._h, int(n)))
 
+    def set_lstm_unroll(self, per_step: bool) -> None:
+        """per_step=True: one LSTM launch per time step instead of the one-launch unroll."""
+        check(lib().acme_r2d2_set_lstm_unroll(self._h, 1 if per_step else 0), "r2d2 lstm unroll")
+
     def debug_buffer(self, name: str) -> np.ndarray:
         p, n = ctypes.c_void_p(), ctypes.c_int64()
         check(lib().acme_r2d2_debug_buffer(self._h, name.encode(), ctypes.byref(p),

@@ -664,7 +664,8 @@ typedef struct acme_r2d2_config {
   int32_t reserved;
   int64_t max_replay_size;      /* N of the importance weights */
   double max_priority_weight;   /* eta; eta and 1 - eta are rounded to f32 from double */
-  float discount, importance_sampling_exponent;
+  double importance_sampling_exponent;  /* beta: the f64 weights' exponent (learning.py:181) */
+  float discount;
   float learning_rate, adam_beta1, adam_beta2, adam_epsilon;  /* epsilon 1e-3 (:78) */
 } acme_r2d2_config;
 
@@ -702,8 +703,12 @@ int acme_r2d2_step(acme_r2d2* l, const acme_sequence_batch* batch, const double*
                    const acme_r2d2_outputs* out, void* stream);
 int64_t acme_r2d2_num_steps(const acme_r2d2* l);
 int acme_r2d2_set_num_steps(acme_r2d2* l, int64_t n);
+/* mode 0 (default): the LSTM unroll and BPTT in one launch each when lstm_size is 256 or 512
+ * and ceil(B / 4) * lstm_size / 16 <= 256; 1: one launch per time step (tests). */
+int acme_r2d2_set_lstm_unroll(acme_r2d2* l, int32_t mode);
 /* "q" / "target_q" [(T - burn_in) * B, A] time-major suffix rows, "h" [T * B, H]
- * time-major, "g" [(T - burn_in) * B] d loss / d q[a], "hid", "x1" "x2" "x3". */
+ * time-major, "g" [(T - burn_in) * B] d loss / d q[a], "hid", "x1" "x2" "x3", "lstm_timeout"
+ * (the one-launch unroll's sticky spin-timeout word; the loss reads NaN once it is set). */
 int acme_r2d2_debug_buffer(const acme_r2d2* l, const char* name, const float** out,
                            int64_t* count);
 

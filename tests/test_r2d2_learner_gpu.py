@@ -254,3 +254,34 @@ def test_r2d2_atari_step_matches_oracle(f32_engine):
     cfg = _cfg(torso="atari", num_actions=18, lstm_size=512, head_size=512, obs_dim=0,
                burn_in_length=2, n_step=2)
     _compare(cfg, B=3, T=6, seed=4, steps=2, f32_engine=f32_engine)
+
+
+@pytest.mark.parametrize("H,B", [(512, 32), (256, 5)])
+def test_r2d2_one_launch_unroll(H, B):
+    """The LSTM unroll and BPTT in one launch each (lstm.h lstm_fwd_rg_kernel /
+    lstm_bwd_rg_kernel, the default at H = 256 / 512 with <= 256 workgroups; B = 32 at
+    H = 512 is the bench's full grid, B = 5 a ragged row group): against the f64 oracle at
+    the bars above (two steps, BPTT stopping at the burn-in), then against the per-step
+    kernels on the same inputs (the same arithmetic in another summation order: h, q rtol
+    1e-5; errors 1e-5 absolute; every gradient within 1e-5 relative Frobenius)."""
+    cfg = _cfg(lstm_size=H, head_size=64, num_actions=18, obs_dim=24, burn_in_length=3)
+    T = 8
+    n = _compare(cfg, B=B, T=T, seed=6, steps=2)
+    assert n.debug_buffer("lstm_timeout")[0] == 0
+    p0, t0 = _params(cfg, 30), _params(cfg, 31)
+    b = _batch(cfg, B, T, 77)
+    outs = []
+    for per_step in (False, True):
+        m = _native(cfg, B, T)
+        m.set_lstm_unroll(per_step)
+        m.set_params(p0, t0)
+        _run(m, b)
+        outs.append((m.debug_buffer("h"), m.debug_buffer("q"), m.errors.cpu().numpy().copy(),
+                     m.get_params("grads")))
+    (h1, q1, e1, g1), (h2, q2, e2, g2) = outs
+    np.testing.assert_allclose(h1, h2, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(q1, q2, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(e1, e2, rtol=0, atol=1e-5)
+    for k in g2:
+        den = max(float(np.linalg.norm(g2[k])), 1e-30)
+        assert float(np.linalg.norm(g1[k] - g2[k])) <= 1e-5 * den, k
