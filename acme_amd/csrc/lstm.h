@@ -432,7 +432,7 @@ __global__ void __launch_bounds__(256) lstm_bwd_step_kernel(
 // workgroup of its row group has published step t, i.e. finished reading step t - 1, so a
 // buffer is only rewritten after its readers are done.  Spins are bounded: a timeout writes
 // `tmo` and every workgroup leaves the kernel (the learner's logged loss then reads NaN).
-// The workgroups must be co-resident: at most 256 of them (ceil(B / 4) x H / 16), 256
+// The workgroups must be co-resident: at most 256 of them (ceil(B / 4) x H / 16), H
 // threads each, which an idle MI355X dispatches at once (hipLaunchCooperativeKernel would
 // guarantee it but measured a 13.5 us gap before and after each launch).  Granule tags carry
 // a per-launch epoch, so the buffers are not cleared between launches.  A row group's
@@ -446,17 +446,20 @@ constexpr int kRgRows = 4;    // batch rows per row group
 constexpr int kRgUnits = 16;  // units per workgroup: 64 gate columns
 constexpr int kRgCols = 4 * kRgUnits;
 
+// A workgroup has NT = H threads (H / 64 waves), so every thread holds the same W_h share
+// (64 floats) and takes the same 4 granules per step at any H.
 template <int H>
 struct RgShape {
-  static_assert(H % 256 == 0 && H <= 1024, "persistent unroll: H a multiple of 256");
+  static_assert(H == 256 || H == 512, "persistent unroll: H of 256 or 512");
+  static constexpr int NT = H;                     // threads per workgroup
   static constexpr int G = H / kRgUnits;           // workgroups per row group
-  static constexpr int KW = H / 16;                // forward: k per slice (16 slices)
-  static constexpr int HV = kRgRows * H / 256;     // forward: h values brought in per thread
+  static constexpr int NS = NT / 16;               // forward: k-slices
+  static constexpr int KW = H / NS;                // forward: k per slice (16)
+  static constexpr int HV = kRgRows * H / NT;      // forward: h values brought in per thread
   static constexpr int UT = H / 4;                 // backward: threads per gate-column slice
-  static constexpr int GS = 256 / UT;              // backward: gate-column slices
-  static constexpr int GW = kRgCols / GS;          // backward: gate columns per slice
-  static constexpr int PV = G * kRgRows * kRgUnits / 256;  // backward: granules per thread
-  static constexpr int PU = H / 256;               // backward: units published per thread
+  static constexpr int GS = NT / UT;               // backward: gate-column slices (4)
+  static constexpr int GW = kRgCols / GS;          // backward: gate columns per slice (16)
+  static constexpr int PV = G * kRgRows * kRgUnits / NT;  // backward: granules per thread (4)
 };
 
 __device__ __forceinline__ void put_granule(unsigned long long* g, unsigned tag, float v) {
@@ -504,20 +507,34 @@ __device__ __forceinline__ int rg_gate_col(int cg, int col) {
   return (col / kRgUnits) * H + cg * kRgUnits + col % kRgUnits;
 }
 
+// Per-step timestamps of workgroup 0 (wall_clock64, 100 MHz) into trace[4 t + i] when a
+// trace buffer is given (debug_buffer "lstm_trace", ACME_V_RGTRACE=1 at creation).
+#define RG_STAMP(i)                                                  \
+  do {                                                               \
+    if (trace && blockIdx.x == 0 && threadIdx.x == 0)                \
+      trace[(size_t)t * 4 + (i)] = (unsigned long long)wall_clock64(); \
+  } while (0)
+
 // Forward: thread (ks = tid / 16, cq = tid % 16) accumulates 4 rows x 4 gate columns over
-// the k-slice ks (W in registers, h_{t-1} broadcast from LDS: each h value read feeds 4
-// columns x 2 rows, LDS return bandwidth rather than the FMAs bounds the step); the 16
+// the 16-k slice ks (W in registers, h_{t-1} broadcast from LDS: each h value read feeds 4
+// columns x 2 rows, LDS return bandwidth rather than the FMAs bounds the step); the H / 16
 // slices are summed in order with gx; threads < 64 run the cells (c in registers).
 template <int H>
-__global__ void __launch_bounds__(256) lstm_fwd_rg_kernel(
+__global__ void __launch_bounds__(H) lstm_fwd_rg_kernel(
     const float* __restrict__ gx, const float* __restrict__ wh, const float* __restrict__ h0,
     int64_t h0_stride, const float* __restrict__ c0, int64_t c0_stride, int B, int T,
     int64_t rs_b, int64_t rs_t, float* __restrict__ gates, float* __restrict__ h_out,
-    float* __restrict__ c_out, unsigned long long* xg, unsigned tag0, unsigned* tmo) {
+    float* __restrict__ c_out, unsigned long long* xg, unsigned tag0, unsigned* tmo,
+    unsigned long long* trace = nullptr) {
   using S = RgShape<H>;
-  constexpr int R = kRgRows, U = kRgUnits, NC = kRgCols, KW = S::KW, HV = S::HV;
+  constexpr int R = kRgRows, U = kRgUnits, NC = kRgCols, KW = S::KW, HV = S::HV, NS = S::NS;
+  // H = 512: the next step's gx is prefetched and the 32 slices are summed in two halves by
+  // all threads (a 32-long dependent chain of LDS reads in the 64 cell threads took 1.8 us
+  // per step); H = 256 keeps IMPALA's order and schedule.
+  constexpr bool kWide = H > 256;
   __shared__ __attribute__((aligned(16))) float hs[R][H];
-  __shared__ float red[16][R][NC];
+  __shared__ float red[NS][R][NC];
+  __shared__ float red2[2][R * NC];
   __shared__ int s_fail;
   const int RG = (B + R - 1) / R;
   const int rg = blockIdx.x % RG, cg = blockIdx.x / RG;
@@ -539,12 +556,19 @@ __global__ void __launch_bounds__(256) lstm_fwd_rg_kernel(
   // The HV h_{t-1} values this thread brings into LDS: e = HV tid + i -> (row e / H, unit).
   const unsigned long long* gp[HV];
   bool glive[HV];
-  for (int t = 0; t < T; ++t) {
-    // The cell's gx terms (its four gate columns), in flight early.
-    float gxv[4];
+  // The cell's gx terms (its four gate columns) of step t: loaded at the step's start, or
+  // (kWide) once step t - 1's h_{t-2} had arrived, so their latency overlaps a whole step.
+  float gxv[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      gxv[q] = cell ? gx[((size_t)cb * rs_b + (size_t)t * rs_t) * 4 * H + q * H + cj] : 0.f;
+  for (int q = 0; q < 4; ++q)
+    gxv[q] = kWide && cell ? gx[(size_t)cb * rs_b * 4 * H + q * H + cj] : 0.f;
+  for (int t = 0; t < T; ++t) {
+    RG_STAMP(0);
+    if (!kWide) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        gxv[q] = cell ? gx[((size_t)cb * rs_b + (size_t)t * rs_t) * 4 * H + q * H + cj] : 0.f;
+    }
     float hv[HV];
     if (t == 0) {
 #pragma unroll
@@ -562,6 +586,13 @@ __global__ void __launch_bounds__(256) lstm_fwd_rg_kernel(
       }
       if (!take_granules<HV>(gp, glive, tag0 + (unsigned)t, hv, tmo)) s_fail = 1;
     }
+    RG_STAMP(1);
+    float gxn[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      gxn[q] = kWide && cell && t + 1 < T
+                   ? gx[((size_t)cb * rs_b + (size_t)(t + 1) * rs_t) * 4 * H + q * H + cj]
+                   : 0.f;
 #pragma unroll
     for (int i = 0; i < HV; i += 4)
       *reinterpret_cast<f32x4*>(&hs[0][0] + HV * tid + i) =
@@ -573,10 +604,11 @@ __global__ void __launch_bounds__(256) lstm_fwd_rg_kernel(
     for (int c = 0; c < 4; ++c) a01[c] = a23[c] = f32x2{0.f, 0.f};
 #pragma unroll
     for (int k4 = 0; k4 < KW / 4; ++k4) {
-      const f32x4 h0v = *reinterpret_cast<const f32x4*>(&hs[0][ks * KW + 4 * k4]);
-      const f32x4 h1v = *reinterpret_cast<const f32x4*>(&hs[1][ks * KW + 4 * k4]);
-      const f32x4 h2v = *reinterpret_cast<const f32x4*>(&hs[2][ks * KW + 4 * k4]);
-      const f32x4 h3v = *reinterpret_cast<const f32x4*>(&hs[3][ks * KW + 4 * k4]);
+      const int k0 = ks * KW + 4 * k4;
+      const f32x4 h0v = *reinterpret_cast<const f32x4*>(&hs[0][k0]);
+      const f32x4 h1v = *reinterpret_cast<const f32x4*>(&hs[1][k0]);
+      const f32x4 h2v = *reinterpret_cast<const f32x4*>(&hs[2][k0]);
+      const f32x4 h3v = *reinterpret_cast<const f32x4*>(&hs[3][k0]);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -593,15 +625,30 @@ __global__ void __launch_bounds__(256) lstm_fwd_rg_kernel(
       red[ks][3][4 * cq + c] = a23[c][1];
     }
     __syncthreads();
+    if (kWide) {  // thread (half, output): the half's NS / 2 slices of one of R x NC outputs
+      const int o = tid % (R * NC), half = tid / (R * NC);
+      const float* rp = &red[half * (NS / 2)][0][0] + o;
+      float sum = rp[0];
+#pragma unroll
+      for (int k = 1; k < NS / 2; ++k) sum += rp[k * R * NC];
+      red2[half][o] = sum;
+      __syncthreads();
+    }
+    RG_STAMP(2);
     if (cell) {
-      // z = gx + the 16 k-slices' partial sums, in order.
+      // z = gx + the NS k-slices' partial sums, in order (kWide: two halves in order).
       float z[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int cc = q * U + cu;
-        float sum = red[0][crow][cc];
+        float sum;
+        if (kWide) {
+          sum = red2[0][crow * NC + cc] + red2[1][crow * NC + cc];
+        } else {
+          sum = red[0][crow][cc];
 #pragma unroll
-        for (int k = 1; k < 16; ++k) sum += red[k][crow][cc];
+          for (int k = 1; k < NS; ++k) sum += red[k][crow][cc];
+        }
         z[q] = gxv[q] + sum;
       }
       const float ig = sigmoidf(z[0]), fg = sigmoidf(z[1]);
@@ -621,6 +668,11 @@ __global__ void __launch_bounds__(256) lstm_fwd_rg_kernel(
                                    tag0 + (unsigned)(t + 1), hn);
       }
     }
+    RG_STAMP(3);
+    if (kWide) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) gxv[q] = gxn[q];
+    }
   }
 }
 
@@ -632,16 +684,21 @@ __global__ void __launch_bounds__(256) lstm_fwd_rg_kernel(
 // slices are summed in order and published (4 rows x H values), each consumer reading its 16
 // units of every producer.  BPTT stops at t_stop (R2D2's burn-in: no gradient into it).
 template <int H>
-__global__ void __launch_bounds__(256) lstm_bwd_rg_kernel(
+__global__ void __launch_bounds__(H) lstm_bwd_rg_kernel(
     const float* __restrict__ dh_head, const float* __restrict__ wh,
     const float* __restrict__ gates, const float* __restrict__ c_all,
     const float* __restrict__ c0, int64_t c0_stride, int B, int T, int t_stop, int64_t rs_b,
     int64_t rs_t, float* __restrict__ dgates, unsigned long long* xb, unsigned tag0,
-    unsigned* tmo) {
+    unsigned* tmo, unsigned long long* trace = nullptr) {
   using S = RgShape<H>;
   constexpr int R = kRgRows, U = kRgUnits, NC = kRgCols, G = S::G;
-  constexpr int UT = S::UT, GS = S::GS, GW = S::GW, PV = S::PV, PU = S::PU;
+  constexpr int UT = S::UT, GS = S::GS, GW = S::GW, PV = S::PV, NT = S::NT;
+  // H = 512: the 32 producers' partials are summed by all threads in 8 groups of 4, then by
+  // the cells over the 8 groups in order (IMPALA's H = 256 keeps one chain of 16).
+  constexpr bool kWide = H > 256;
+  constexpr int PG = NT / (R * U);  // producer groups (kWide)
   __shared__ float pp[G][R][U];
+  __shared__ float pp2[PG][R * U];
   __shared__ __attribute__((aligned(16))) float dgs[R][NC];
   __shared__ float red[GS][R][H];
   __shared__ int s_fail;
@@ -664,17 +721,29 @@ __global__ void __launch_bounds__(256) lstm_bwd_rg_kernel(
   // Granules this thread takes: e = PV tid + i -> (producer e / (R U), row, unit).
   const unsigned long long* gp[PV];
   bool glive[PV];
-  for (int t = T - 1; t >= t_stop; --t) {
-    const size_t row = (size_t)cb * rs_b + (size_t)t * rs_t;
-    // Cell operands, loaded before the wait.
-    float ig = 0.f, fg = 0.f, gg = 0.f, og = 0.f, cn = 0.f, cprev = 0.f, dhh = 0.f;
+  // Cell operands of step t; step t - 1's are loaded once step t's partial products have
+  // arrived, so their latency overlaps a whole step.
+  struct CellOps {
+    float ig, fg, gg, og, cn, cprev, dhh;
+  };
+  auto cell_ops = [&](int t) {
+    CellOps x{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (cell) {
+      const size_t row = (size_t)cb * rs_b + (size_t)t * rs_t;
       const float* gr = gates + row * 4 * H;
-      ig = gr[cj]; fg = gr[H + cj]; gg = gr[2 * H + cj]; og = gr[3 * H + cj];
-      cn = c_all[row * H + cj];
-      cprev = t > 0 ? c_all[(row - rs_t) * H + cj] : c0[(size_t)cb * c0_stride + cj];
-      dhh = dh_head[row * H + cj];
+      x.ig = gr[cj]; x.fg = gr[H + cj]; x.gg = gr[2 * H + cj]; x.og = gr[3 * H + cj];
+      x.cn = c_all[row * H + cj];
+      x.cprev = t > 0 ? c_all[(row - rs_t) * H + cj] : c0[(size_t)cb * c0_stride + cj];
+      x.dhh = dh_head[row * H + cj];
     }
+    return x;
+  };
+  CellOps ops = cell_ops(T - 1);
+  for (int t = T - 1; t >= t_stop; --t) {
+    RG_STAMP(0);
+    const size_t row = (size_t)cb * rs_b + (size_t)t * rs_t;
+    const float ig = ops.ig, fg = ops.fg, gg = ops.gg, og = ops.og, cn = ops.cn;
+    const float cprev = ops.cprev, dhh = ops.dhh;
     if (t + 1 < T) {
       const unsigned long long* base = xb + (size_t)((t + 1) & 1) * G * B * H;
       float v[PV];
@@ -688,12 +757,29 @@ __global__ void __launch_bounds__(256) lstm_bwd_rg_kernel(
 #pragma unroll
       for (int i = 0; i < PV; ++i) (&pp[0][0][0])[PV * tid + i] = v[i];
     }
+    RG_STAMP(1);
+    if (t > t_stop) ops = cell_ops(t - 1);
     __syncthreads();
     if (s_fail) return;
+    if (kWide && t + 1 < T) {
+      const int o = tid % (R * U), part = tid / (R * U);
+      const float* src = &pp[part * (G / PG)][0][0] + o;
+      float sum = src[0];
+#pragma unroll
+      for (int k = 1; k < G / PG; ++k) sum += src[k * R * U];
+      pp2[part][o] = sum;
+      __syncthreads();
+    }
     if (cell) {
       float dhn = 0.f;
-      if (t + 1 < T)
-        for (int pg = 0; pg < G; ++pg) dhn += pp[pg][crow][cu];
+      if (t + 1 < T) {
+        if (kWide) {
+#pragma unroll
+          for (int part = 0; part < PG; ++part) dhn += pp2[part][tid];
+        } else {
+          for (int pg = 0; pg < G; ++pg) dhn += pp[pg][crow][cu];
+        }
+      }
       const float tc = tanhf(cn);
       const float dh = dhh + dhn;
       const float dc = dcarry + dh * og * (1.f - tc * tc);
@@ -713,6 +799,7 @@ __global__ void __launch_bounds__(256) lstm_bwd_rg_kernel(
       }
     }
     __syncthreads();
+    RG_STAMP(2);
     if (t > t_stop) {
       f32x2 a01[4], a23[4];  // per unit: rows (0, 1) and (2, 3)
 #pragma unroll
@@ -739,24 +826,22 @@ __global__ void __launch_bounds__(256) lstm_bwd_rg_kernel(
         red[gs][3][4 * uq + uu] = a23[uu][1];
       }
       __syncthreads();
-      // Units tid, tid + 256, ...: this workgroup's partial for 4 rows (the gate-column
-      // slices summed in order).
+      // Thread u = tid publishes this workgroup's partial for its unit, 4 rows (the
+      // gate-column slices summed in order).
       unsigned long long* out = xb + (size_t)(t & 1) * G * B * H + (size_t)cg * B * H;
 #pragma unroll
-      for (int p = 0; p < PU; ++p) {
-        const int u = tid + 256 * p;
+      for (int r = 0; r < R; ++r) {
+        if (b0 + r >= B) continue;
+        float v = red[0][r][tid];
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          if (b0 + r >= B) continue;
-          float v = red[0][r][u];
-#pragma unroll
-          for (int k = 1; k < GS; ++k) v += red[k][r][u];
-          put_granule(out + (size_t)(b0 + r) * H + u, tag0 + (unsigned)t, v);
-        }
+        for (int k = 1; k < GS; ++k) v += red[k][r][tid];
+        put_granule(out + (size_t)(b0 + r) * H + tid, tag0 + (unsigned)t, v);
       }
     }
+    RG_STAMP(3);
   }
 }
+#undef RG_STAMP
 
 // gx = OAR(emb) @ W_i + b from the plane GEMM's split-K partials of feat @ W_i[0:F]: the
 // one-hot(prev a) row of W_i, tanh(prev r) times its last row and the bias are added here

@@ -126,6 +126,9 @@ struct acme_r2d2 {
   unsigned* tmo = nullptr;
   unsigned lstm_epoch = 0;
   bool lstm_steps = false;
+  // ACME_V_RGTRACE=1 at creation: per-step timestamps of the last forward and BPTT launches
+  // (debug_buffer "lstm_trace": [2][kMaxSeq][4] u64, forward then BPTT).
+  unsigned long long* rg_trace = nullptr;
 };
 
 namespace {
@@ -536,13 +539,13 @@ int network_forward(acme_r2d2* l, const float* prm, const acme_sequence_batch* b
       const unsigned tag0 = next_lstm_tags(l, st);
       const unsigned nblk = (unsigned)(ceil_div(B, kRgRows) * (H / kRgUnits));
       if (H == 512)
-        lstm_fwd_rg_kernel<512><<<nblk, 256, 0, st>>>(l->gx, P(l, prm, l->t_wh), h0, s0, c0, s0,
+        lstm_fwd_rg_kernel<512><<<nblk, 512, 0, st>>>(l->gx, P(l, prm, l->t_wh), h0, s0, c0, s0,
                                                       B, T, 1, B, l->gates, l->h, l->c, l->xg,
-                                                      tag0, l->tmo);
+                                                      tag0, l->tmo, l->rg_trace);
       else
         lstm_fwd_rg_kernel<256><<<nblk, 256, 0, st>>>(l->gx, P(l, prm, l->t_wh), h0, s0, c0, s0,
                                                       B, T, 1, B, l->gates, l->h, l->c, l->xg,
-                                                      tag0, l->tmo);
+                                                      tag0, l->tmo, l->rg_trace);
       R2_CHECK();
     } else {
     const dim3 grid((unsigned)(H / kFwdUnits), (unsigned)ceil_div(B, l->bc));
@@ -674,13 +677,13 @@ int r2d2_step_impl(acme_r2d2* l, const acme_sequence_batch* bt, const double* pr
       const unsigned tag0 = next_lstm_tags(l, st);
       const unsigned nblk = (unsigned)(ceil_div(B, kRgRows) * (H / kRgUnits));
       if (H == 512)
-        lstm_bwd_rg_kernel<512><<<nblk, 256, 0, st>>>(l->dh, P(l, prm, l->t_wh), l->gates, l->c,
+        lstm_bwd_rg_kernel<512><<<nblk, 512, 0, st>>>(l->dh, P(l, prm, l->t_wh), l->gates, l->c,
                                                       c0, s0, B, T, BI, 1, B, dg, l->xb, tag0,
-                                                      l->tmo);
+                                                      l->tmo, l->rg_trace ? l->rg_trace + 4 * kMaxSeq : nullptr);
       else
         lstm_bwd_rg_kernel<256><<<nblk, 256, 0, st>>>(l->dh, P(l, prm, l->t_wh), l->gates, l->c,
                                                       c0, s0, B, T, BI, 1, B, dg, l->xb, tag0,
-                                                      l->tmo);
+                                                      l->tmo, l->rg_trace ? l->rg_trace + 4 * kMaxSeq : nullptr);
       R2_CHECK();
     } else {
     ACME_HIP_TRY(hipMemsetAsync(l->dc, 0, (size_t)B * H * sizeof(float), st));
@@ -962,7 +965,8 @@ int acme_r2d2_create(const acme_r2d2_config* cfg, acme_r2d2** out) {
   if (rg_shape(H, B)) {  // the one-launch unroll's granule buffers (never cleared per launch)
     const int64_t G = H / kRgUnits;
     if ((rc = dev_alloc(l, &l->xg, (int64_t)2 * B * H)) ||
-        (rc = dev_alloc(l, &l->xb, 2 * G * B * H)) || (rc = dev_alloc(l, &l->tmo, 4)))
+        (rc = dev_alloc(l, &l->xb, 2 * G * B * H)) || (rc = dev_alloc(l, &l->tmo, 4)) ||
+        (tune_variant("RGTRACE") == 1 && (rc = dev_alloc(l, &l->rg_trace, 8 * kMaxSeq))))
       return fail(rc);
     if (hipMemset(l->xg, 0, (size_t)2 * B * H * 8) != hipSuccess ||
         hipMemset(l->xb, 0, (size_t)2 * G * B * H * 8) != hipSuccess ||
@@ -1120,6 +1124,10 @@ int acme_r2d2_debug_buffer(const acme_r2d2* l, const char* name, const float** o
       if (rc != ACME_OK) return rc;
       ACME_HIP_TRY(hipDeviceSynchronize());
     }
+  }
+  else if (n == "lstm_trace") {  // u64 words: count is in floats
+    *out = reinterpret_cast<const float*>(l->rg_trace);
+    *count = l->rg_trace ? 2 * 8 * kMaxSeq : 0;
   }
   else if (n == "lstm_timeout") { *out = reinterpret_cast<const float*>(l->tmo); *count = l->tmo ? 1 : 0; }
   else ACME_CHECK_ARG(false, "unknown debug buffer '%s'", name);
