@@ -588,8 +588,9 @@ def setup_r2d2(args, world, rank, dev):
     meta = dict(
         metric=f"learner sequences/sec (B={B} x T={T}, burn-in {BI}) R2D2 Atari, 1 MI355X",
         unit="sequences/s",
-        dtype="f32 (torso and W_i: 2xf16 split planes, 3 MFMA terms; LSTM and head: f32 MFMA)",
+        dtype="f32 (torso and W_i: 2xf16 split planes, 3 MFMA terms; LSTM: f32 one-launch unroll; head: f32 MFMA)",
         _roofline_exclude=("r2d2_lstm_fwd", "r2d2_lstm_bwd"),
+        _lstm_T={"r2d2_lstm_fwd": T, "r2d2_lstm_bwd": T - BI},
         data="synthetic (device-generated uint8 Atari sequences in a device-resident pool, "
              "random-init R2D2AtariNetwork)",
         config={"workload": "r2d2_atari_lstm_transformed_nstep (SURVEY §8(f) widening)",
@@ -1022,13 +1023,14 @@ def main():
             # The LSTM unroll per timestep (one launch each way) against a dependent kernel
             # boundary on MI355X (1.45 us between trivial kernels, MI355X_MICROARCH.md
             # "boundary"), the floor of one launch per timestep before any work.
+            # (R2D2: the BPTT launch covers the T - burn-in trained steps.)
             lstm = {s["name"]: s for s in sections if s["name"] in meta["_roofline_exclude"]}
             T = meta["_lstm_T"]
-            out["lstm"] = {k.replace("impala_", ""): {"us_per_launch": v["avg_us"],
-                                                       "us_per_timestep": round(v["avg_us"] / T, 3)}
-                           for k, v in lstm.items()}
+            steps_of = (lambda k: T[k]) if isinstance(T, dict) else (lambda k: T)
+            out["lstm"] = {k.replace("impala_", "").replace("r2d2_", ""): {
+                "us_per_launch": v["avg_us"], "timesteps": steps_of(k),
+                "us_per_timestep": round(v["avg_us"] / steps_of(k), 3)} for k, v in lstm.items()}
             out["lstm"]["boundary_us"] = 1.45
-            out["lstm"]["timesteps"] = T
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
