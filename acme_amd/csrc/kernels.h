@@ -56,6 +56,9 @@ struct RescaleGuard {
   int mode = kRgNone;
   Gate gate{};                      // kRgStep: the step's gate
   int64_t* host_skipped = nullptr;  // kRgStep: pinned host mirror of g->skipped (optional)
+  // kRgStep: a one-launch LSTM's timeout words (tmo[0] this step, tmo[1] the count): a
+  // timed-out step is skipped too, tmo[0] cleared and counted (optional).
+  uint32_t* tmo = nullptr;
 };
 
 // Finishes the duelling head GEMM (conv.h DuelHeadFwd): sums the split-K slab

@@ -82,7 +82,6 @@ struct acme_r2d2 {
       t_ab = -1;
   float *params = nullptr, *target = nullptr, *grads = nullptr, *m = nullptr, *v = nullptr;
   int64_t num_steps = 0;
-  int64_t* dev_step = nullptr;
   std::vector<void*> allocs;
   // Time-major inputs (R = T B rows): frames (uint8 Atari / f32 flat), prev action / reward.
   void* obs_tm = nullptr;
@@ -423,13 +422,31 @@ __global__ void __launch_bounds__(64) r2d2_loss_kernel(const R2Loss a) {
   }
 }
 
-// The batch loss; NaN once a one-launch LSTM unroll has timed out (the sticky word `tmo`).
+// The batch loss; NaN when this step's one-launch LSTM forward timed out (tmo[0]).
 __global__ void r2d2_loss_sum_kernel(const double* __restrict__ part, int B,
                                      float* __restrict__ loss, const unsigned* __restrict__ tmo) {
   if (threadIdx.x != 0) return;
   double s = 0.0;
   for (int b = 0; b < B; ++b) s += part[b];
   loss[0] = tmo && *tmo ? NAN : (float)(s / (double)B);
+}
+
+// The f32 path's step verdict before Adam: skipped when this step's one-launch LSTM timed
+// out (tmo[0], then cleared and counted in tmo[1]), else applied (Adam's t = applied).
+__global__ void r2d2_guard_kernel(StepGuard* __restrict__ g, unsigned* __restrict__ tmo,
+                                  int64_t* __restrict__ host_skipped) {
+  if (threadIdx.x != 0) return;
+  const bool skip = tmo && tmo[0] != 0u;
+  g->last = skip ? 1u : 0u;
+  if (skip) {
+    tmo[0] = 0u;
+    tmo[1] += 1u;
+    const int64_t k = g->skipped + 1;
+    g->skipped = k;
+    if (host_skipped) *host_skipped = k;
+  } else {
+    g->applied += 1;
+  }
 }
 
 // dW_h = h_prev^T dgates over the suffix rows (time-major): h_prev of row m (global row
@@ -755,6 +772,7 @@ int r2d2_step_impl(acme_r2d2* l, const acme_sequence_batch* bt, const double* pr
       rg.g = l->guard;
       rg.mode = kRgStep;
       rg.host_skipped = l->host_skipped;
+      rg.tmo = l->tmo;
     }
     rc = launch_plane_rescale(l->scales, kScCount, kScCount, -1, -1, l->overflow, st, -1, -1, rg);
     if (rc != ACME_OK) return rc;
@@ -798,10 +816,15 @@ int r2d2_step_impl(acme_r2d2* l, const acme_sequence_batch* bt, const double* pr
       rc = launch_adam(l->params, gr, l->m, l->v, l->flat, l->cfg.learning_rate,
                        l->cfg.adam_beta1, l->cfg.adam_beta2, l->cfg.adam_epsilon, 0, nullptr, 0,
                        st, 0, &l->guard->applied, nullptr, gate, false, tail);
-    } else {
+    } else {  // the same gate, decided here: only an LSTM timeout skips the f32 path
+      r2d2_guard_kernel<<<1, 64, 0, st>>>(l->guard, l->tmo, l->host_skipped);
+      R2_CHECK();
+      Gate gate;
+      gate.g = l->guard;
+      gate.use_last = 1;
       rc = launch_adam(l->params, gr, l->m, l->v, l->flat, l->cfg.learning_rate,
                        l->cfg.adam_beta1, l->cfg.adam_beta2, l->cfg.adam_epsilon, 0, nullptr, 0,
-                       st, 0, l->dev_step);
+                       st, 0, &l->guard->applied, nullptr, gate, false, AdamTail{});
     }
     if (rc != ACME_OK) return rc;
   }
@@ -960,7 +983,7 @@ int acme_r2d2_create(const acme_r2d2_config* cfg, acme_r2d2** out) {
       (rc = dev_alloc(l, &l->dh, R * H)) || (rc = dev_alloc(l, &l->dgates, RL * 4 * H)) ||
       (rc = dev_alloc(l, &l->dc, (int64_t)B * H)) || (rc = dev_alloc(l, &l->loss_part, B)) ||
       (rc = dev_alloc(l, &l->err_tmp, RL)) || (rc = dev_alloc(l, &l->prio_tmp, B)) ||
-      (rc = dev_alloc(l, &l->loss_tmp, 1)) || (rc = dev_alloc(l, &l->dev_step, 1)))
+      (rc = dev_alloc(l, &l->loss_tmp, 1)))
     return fail(rc);
   if (rg_shape(H, B)) {  // the one-launch unroll's granule buffers (never cleared per launch)
     const int64_t G = H / kRgUnits;
@@ -973,8 +996,7 @@ int acme_r2d2_create(const acme_r2d2_config* cfg, acme_r2d2** out) {
         hipMemset(l->tmo, 0, 4 * sizeof(unsigned)) != hipSuccess)
       return fail((set_error("hipMemset failed"), ACME_ERR_HIP));
   }
-  if (hipMemset(l->zero_state, 0, (size_t)B * H * sizeof(float)) != hipSuccess ||
-      hipMemset(l->dev_step, 0, sizeof(int64_t)) != hipSuccess)
+  if (hipMemset(l->zero_state, 0, (size_t)B * H * sizeof(float)) != hipSuccess)
     return fail((set_error("hipMemset failed"), ACME_ERR_HIP));
   *out = l;
   return ACME_OK;
@@ -1072,7 +1094,7 @@ int acme_r2d2_guard_state(acme_r2d2* l, int64_t* out3) {
   ACME_HIP_TRY(hipDeviceSynchronize());
   StepGuard g;
   ACME_HIP_TRY(hipMemcpy(&g, l->guard, sizeof(g), hipMemcpyDeviceToHost));
-  out3[0] = l->p3 ? g.applied : l->num_steps;
+  out3[0] = g.applied;
   out3[1] = g.skipped;
   out3[2] = g.last;
   return ACME_OK;
@@ -1082,13 +1104,10 @@ int acme_r2d2_set_applied_steps(acme_r2d2* l, int64_t n) {
   ACME_CHECK_ARG(l && n >= 0, "bad argument");
   ACME_HIP_TRY(hipDeviceSynchronize());
   ACME_HIP_TRY(hipMemcpy(&l->guard->applied, &n, sizeof(n), hipMemcpyHostToDevice));
-  if (!l->p3) ACME_HIP_TRY(hipMemcpy(l->dev_step, &n, sizeof(n), hipMemcpyHostToDevice));
   return ACME_OK;
 }
 
-const uint32_t* acme_r2d2_skip_word(const acme_r2d2* l) {
-  return l && l->p3 ? &l->guard->last : nullptr;
-}
+const uint32_t* acme_r2d2_skip_word(const acme_r2d2* l) { return l ? &l->guard->last : nullptr; }
 
 int64_t acme_r2d2_num_steps(const acme_r2d2* l) { return l ? l->num_steps : 0; }
 
@@ -1096,7 +1115,6 @@ int acme_r2d2_set_num_steps(acme_r2d2* l, int64_t n) {
   ACME_CHECK_ARG(l && n >= 0, "bad argument");
   l->num_steps = n;
   ACME_HIP_TRY(hipDeviceSynchronize());
-  ACME_HIP_TRY(hipMemcpy(l->dev_step, &n, sizeof(n), hipMemcpyHostToDevice));
   ACME_HIP_TRY(hipMemcpy(&l->guard->applied, &n, sizeof(n), hipMemcpyHostToDevice));
   return ACME_OK;
 }
@@ -1129,7 +1147,14 @@ int acme_r2d2_debug_buffer(const acme_r2d2* l, const char* name, const float** o
     *out = reinterpret_cast<const float*>(l->rg_trace);
     *count = l->rg_trace ? 2 * 8 * kMaxSeq : 0;
   }
-  else if (n == "lstm_timeout") { *out = reinterpret_cast<const float*>(l->tmo); *count = l->tmo ? 1 : 0; }
+  else if (n == "lstm_timeout_step") {  // u32: this step's timeout word (tests set it)
+    *out = reinterpret_cast<const float*>(l->tmo);
+    *count = l->tmo ? 1 : 0;
+  }
+  else if (n == "lstm_timeout") {  // u32: one-launch unroll timeouts so far (skipped steps)
+    *out = reinterpret_cast<const float*>(l->tmo ? l->tmo + 1 : nullptr);
+    *count = l->tmo ? 1 : 0;
+  }
   else ACME_CHECK_ARG(false, "unknown debug buffer '%s'", name);
   return ACME_OK;
 }

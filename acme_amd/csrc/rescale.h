@@ -156,7 +156,12 @@ __device__ __forceinline__ void rescale_block(const RescaleJob& j) {
       if (bad) g->on = 1u;
     } else if (g && rg.mode == kRgStep) {
       // The flags (on, prm) are cleared by the step's Adam launch, after every reader.
-      const bool skip = (s_gv[0] | s_gv[2] | bad) != 0u || s_dp > 0.f;
+      const bool timed_out = rg.tmo && rg.tmo[0] != 0u;
+      const bool skip = (s_gv[0] | s_gv[2] | bad) != 0u || s_dp > 0.f || timed_out;
+      if (timed_out) {
+        rg.tmo[0] = 0u;
+        rg.tmo[1] += 1u;
+      }
       g->last = skip ? 1u : 0u;
       if (skip) {
         const int64_t k = g->skipped + 1;

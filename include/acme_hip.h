@@ -686,11 +686,11 @@ int acme_r2d2_bind(acme_r2d2* l, float* params, float* target, float* grads, flo
 /* The caller wrote params / target directly (initialisation, restore): the Atari plane path
  * recalibrates its scales before the next step (as acme_impala_params_changed). */
 int acme_r2d2_params_changed(acme_r2d2* l);
-/* Step guard of the Atari plane path (as the DQN / IMPALA learners'): a step whose plane
- * writes overflowed applies no update; out3 = {applied, skipped, last step skipped};
- * acme_r2d2_skipped_steps reads a pinned host mirror; acme_r2d2_skip_word is the device word
- * that gates the step's priority write-back (acme_replay_update_priorities_gated; NULL
- * without the plane path). */
+/* Step guard (as the DQN / IMPALA learners'): a step whose plane writes overflowed (Atari
+ * plane path) or whose one-launch LSTM timed out applies no update; out3 = {applied,
+ * skipped, last step skipped}; acme_r2d2_skipped_steps reads a pinned host mirror;
+ * acme_r2d2_skip_word is the device word that gates the step's priority write-back
+ * (acme_replay_update_priorities_gated). */
 int64_t acme_r2d2_skipped_steps(const acme_r2d2* l);
 int acme_r2d2_guard_state(acme_r2d2* l, int64_t* out3);
 const uint32_t* acme_r2d2_skip_word(const acme_r2d2* l);

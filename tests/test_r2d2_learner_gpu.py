@@ -285,3 +285,44 @@ def test_r2d2_one_launch_unroll(H, B):
     for k in g2:
         den = max(float(np.linalg.norm(g2[k])), 1e-30)
         assert float(np.linalg.norm(g1[k] - g2[k])) <= 1e-5 * den, k
+
+
+@pytest.mark.parametrize("torso", ["flat", "atari"])
+def test_r2d2_lstm_timeout_skips_update(torso):
+    """A one-launch LSTM spin timeout (this step's timeout word set before the step, as the
+    kernels set it) skips the update on both engines: parameters, Adam moments, Adam's count
+    and the target unchanged bit for bit, the loss NaN, the skip counted (pinned host
+    mirror, guard state, the sticky timeout count); the next step applies normally."""
+    import ctypes
+
+    from acme_amd import _lib
+    from acme_amd.native import _memcpy_dtod
+    cfg = _cfg(torso=torso, num_actions=18, lstm_size=512, head_size=64,
+               obs_dim=0 if torso == "atari" else 24, burn_in_length=2, n_step=2,
+               target_update_period=1)
+    B, T = 3, 6
+    n = _native(cfg, B, T)
+    n.set_params(_params(cfg, 40), _params(cfg, 41))
+    _run(n, _batch(cfg, B, T, 1))
+    assert n.guard_state()["applied"] == 1
+    before = {buf: n.get_params(buf) for buf in ("params", "target", "m", "v")}
+    p, c = ctypes.c_void_p(), ctypes.c_int64()
+    _lib.check(_lib.lib().acme_r2d2_debug_buffer(n._h, b"lstm_timeout_step", ctypes.byref(p),
+                                                 ctypes.byref(c)))
+    one = torch.ones(1, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    _memcpy_dtod(p.value, one.data_ptr(), 4)
+    _run(n, _batch(cfg, B, T, 2))
+    assert np.isnan(n.loss.item())
+    g = n.guard_state()
+    assert g["applied"] == 1 and g["skipped"] == 1 and g["last_skipped"] == 1, g
+    assert n.skipped_steps == 1
+    assert n.debug_buffer("lstm_timeout").view(np.uint32)[0] == 1
+    for buf, ref in before.items():
+        got = n.get_params(buf)
+        for k in ref:
+            np.testing.assert_array_equal(got[k], ref[k], err_msg=f"{buf}/{k}")
+    _run(n, _batch(cfg, B, T, 3))
+    assert np.isfinite(n.loss.item())
+    g = n.guard_state()
+    assert g["applied"] == 2 and g["skipped"] == 1 and g["last_skipped"] == 0, g
