@@ -158,7 +158,6 @@ struct acme_dqn {
   bool single_stream = false;
   bool single_role = false;
   bool head_separate = false;  // ACME_V_HEADSEP=1: the online head as its own launch (tests)
-  bool fc_big = false;         // ACME_V_FCW=1: online fc_fwd on 256x128 WS tiles, split-K 8 (A/B)
   // Step guard (kernels.h StepGuard): the skip-on-overflow rule of the plane engine, Adam's
   // device step count (applied updates) on every path.  seq counts the steps issued (the
   // target forward's flag slot is seq & 1); host_skipped is a pinned mirror of the skipped
@@ -430,8 +429,14 @@ int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const torso:
   if (rc != ACME_OK) return rc;
   {
     P3DenseFwd p;
-    // Split-K: about one round of blocks (128x128 tiles, one block per CU at BK 32).
-    const int splits = rows > 512 && !l->fc_big ? 4 : kFcFwdSplits;
+    // Split-K 8: about one round of blocks (one block per CU at BK 32): the online forward's
+    // 2B = 1024 rows on 256x128 tiles (4 x 8 x 8), the target's 512 rows on 128x128.  The
+    // taller tile takes in 24 KB per k16 step for 768 MFMA cycles against 16 KB per 384
+    // (per-CU L2 intake): fc_fwd 47.0 -> 45.3 us, step 0.5037 -> 0.5028 ms
+    // over 200 steps and 0.5146 -> 0.5084 ms over 20-step windows (three alternating pairs,
+    // round 4; it had split-K 4 on 128x128 tiles).
+    const bool tall = rows > 512;
+    const int splits = kFcFwdSplits;
     p.M = rows; p.N = 2 * kHidden; p.K = kFlat; p.k_chunk = chunk_for(kFlat, splits);
     p.a_src = SRC(x3, (int64_t)rows * kFlat); p.ldx = kFlat;
     p.b_src = SRC(WP(l, wpl, l->t_fcw), (int64_t)kFlat * 2 * kHidden); p.slab = slab;
@@ -439,7 +444,8 @@ int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const torso:
     // 65.2 -> 60.5 us against the single-role kernel, the same bits.
     // (Two f16 planes, measured on the step: 256x128 / 128x256 WS tiles, 256x128 single-role
     // tiles with split-K 8, and the LDS-DMA ring (3 or 4 stages) all slower or equal.)
-    if (l->fc_big && rows > 512) ACME_P3WS_GEMM("fc_fwd", 256, 128, 2, 2, 32, p, splits, true);
+    if (tall && l->single_role) ACME_P3_GEMM("fc_fwd", 256, 128, 2, 2, 32, p, splits);  // tests
+    else if (tall) ACME_P3WS_GEMM("fc_fwd", 256, 128, 2, 2, 32, p, splits, true);
     else if (l->single_role) ACME_P3_GEMM("fc_fwd", 128, 128, 2, 2, 32, p, splits);  // tests
     else ACME_P3WS_GEMM("fc_fwd", 128, 128, 2, 2, 32, p, splits, true);
     // The online forward of a step: the head runs inside the loss launch (nature_backward).
@@ -762,7 +768,6 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
   l->single_stream = tune_variant("SIDE") == 1;
   l->single_role = tune_variant("WSN") == 1;
   l->head_separate = tune_variant("HEADSEP") == 1;
-  l->fc_big = tune_variant("FCW") == 1;
   const int A = cfg->num_actions;
   const int B = cfg->max_batch;
   int rc = ACME_OK;
