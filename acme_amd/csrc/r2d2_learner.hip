@@ -54,7 +54,7 @@ constexpr int kHeadFwdSplits = 16;  // duelling head [rows, A + 1] x K = 2 H2
 constexpr int kHeadBwdSplits = 8;   // duelling head weights [2 H2 + 1, A + 1] x K = rows
 constexpr int kMaxSeq = 256;        // sequence length bound (the loss kernel's LDS)
 constexpr int kFwdLds = 160 * 1024; // LDS per workgroup on gfx950
-constexpr int kOarSplitsP3 = 8;     // split-K of the plane-engine OAR projection (K = 7744)
+constexpr int kOarSplitsP3 = 4;     // split-K of the plane-engine OAR projection (K = 7744)
 
 // Scale records of the plane path: the transient activations / gradients (the target and
 // online passes write the same activation planes: one record each, the maximum of both),
@@ -508,15 +508,19 @@ int network_forward(acme_r2d2* l, const float* prm, const acme_sequence_batch* b
     if (rc != ACME_OK) return rc;
     const int F = l->F, N = 4 * H;
     P3DenseFwd p;
-    p.M = R; p.N = N; p.K = F; p.k_chunk = chunk_for(F, kOarSplitsP3);
+    // 256x128 tiles at split-K 4 (16 x 16 x 4 blocks at the bench shape): 433 -> 325 us,
+    // the split-K reduction 63 -> 30 us, the step 5.16 -> 4.87 ms against 128x128 at split-K
+    // 8 (two alternating pairs, round 4; DESIGN.md 4.1 on the per-CU intake).
+    const int splits = kOarSplitsP3;
+    p.M = R; p.N = N; p.K = F; p.k_chunk = chunk_for(F, splits);
     p.a_src = SRC(l->x3p, (int64_t)R * F); p.ldx = F;
     p.b_src = SRC(WP(l, planes, rec, l->t_wi), (int64_t)F * N); p.slab = l->pslab;
-    R2_P3WS_GEMM("r2d2_oar_fwd", 128, 128, 2, 2, 32, p, kOarSplitsP3);
+    R2_P3WS_GEMM("r2d2_oar_fwd", 256, 128, 2, 2, 32, p, splits);
     {
-      ACME_PROF("r2d2_oar_reduce", st, 0.0, 4.0 * (kOarSplitsP3 + 1) * (double)R * N);
+      ACME_PROF("r2d2_oar_reduce", st, 0.0, 4.0 * (splits + 1) * (double)R * N);
       const int64_t n4 = (int64_t)R * N / 4;
       oar_finish_kernel<<<(unsigned)ceil_div(n4, 256), 256, 0, st>>>(
-          l->pslab, kOarSplitsP3, R, N, P(l, prm, l->t_wi) + (size_t)F * N, P(l, prm, l->t_b),
+          l->pslab, splits, R, N, P(l, prm, l->t_wi) + (size_t)F * N, P(l, prm, l->t_b),
           l->pa_tm, l->pr_tm, A, l->gx);
       R2_CHECK();
     }
@@ -736,6 +740,7 @@ int r2d2_step_impl(acme_r2d2* l, const acme_sequence_batch* bt, const double* pr
       w.a_src = SRC(x3s, (int64_t)RL * F); w.ldx = F;
       w.b_src = SRC(l->dgp, (int64_t)RL * N); w.out = Pm(l, gr, l->t_wi);
       w.bias_out = Pm(l, gr, l->t_b);
+      // (256x128 tiles measured slower here: 236 -> 257 us.)
       R2_P3_GEMM("r2d2_wi_wgrad", 128, 128, 2, 2, 16, w, 1);
     }
     {
@@ -754,7 +759,8 @@ int r2d2_step_impl(acme_r2d2* l, const acme_sequence_batch* bt, const double* pr
       d.b_src = SRC(WP(l, l->wpl, kScParams, l->t_wi), (int64_t)F * N);
       d.xprev = CPlanes{x3s.p, x3s.stride, x3s.sc}; d.ldx = F;
       d.dx = Planes{l->dz3p.p, l->dz3p.stride, l->dz3p.sc};
-      R2_P3WS_GEMM("r2d2_feat_dgrad", 128, 128, 2, 2, 32, d, 1);
+      // 256x128 tiles (11 x 61 blocks): 311 -> 278 us against 128x128 (round 4).
+      R2_P3WS_GEMM("r2d2_feat_dgrad", 256, 128, 2, 2, 32, d, 1);
     }
     torso::Grads g{Pm(l, gr, l->t_c[0]), Pm(l, gr, l->t_c[1]), Pm(l, gr, l->t_c[2]),
                    Pm(l, gr, l->t_c[3]), Pm(l, gr, l->t_c[4]), Pm(l, gr, l->t_c[5])};
