@@ -442,24 +442,25 @@ __global__ void __launch_bounds__(256) lstm_bwd_step_kernel(
 using gu64 = __attribute__((address_space(1))) unsigned long long;
 using gu32 = __attribute__((address_space(1))) unsigned;
 constexpr unsigned kSpinLimit = 1u << 22;
-constexpr int kRgRows = 4;    // batch rows per row group
+constexpr int kRgRows = 4;    // batch rows per row group (2: twice the workgroups, small B)
 constexpr int kRgUnits = 16;  // units per workgroup: 64 gate columns
 constexpr int kRgCols = 4 * kRgUnits;
 
 // A workgroup has NT = H threads (H / 64 waves), so every thread holds the same W_h share
 // (64 floats) and takes the same 4 granules per step at any H.
-template <int H>
+template <int H, int R = kRgRows>
 struct RgShape {
   static_assert(H == 256 || H == 512, "persistent unroll: H of 256 or 512");
+  static_assert(R == 2 || R == 4, "persistent unroll: 2 or 4 rows per row group");
   static constexpr int NT = H;                     // threads per workgroup
   static constexpr int G = H / kRgUnits;           // workgroups per row group
   static constexpr int NS = NT / 16;               // forward: k-slices
   static constexpr int KW = H / NS;                // forward: k per slice (16)
-  static constexpr int HV = kRgRows * H / NT;      // forward: h values brought in per thread
+  static constexpr int HV = R * H / NT;            // forward: h values brought in per thread
   static constexpr int UT = H / 4;                 // backward: threads per gate-column slice
   static constexpr int GS = NT / UT;               // backward: gate-column slices (4)
   static constexpr int GW = kRgCols / GS;          // backward: gate columns per slice (16)
-  static constexpr int PV = G * kRgRows * kRgUnits / NT;  // backward: granules per thread (4)
+  static constexpr int PV = G * R * kRgUnits / NT; // backward: granules per thread (R)
 };
 
 __device__ __forceinline__ void put_granule(unsigned long long* g, unsigned tag, float v) {
@@ -519,19 +520,20 @@ __device__ __forceinline__ int rg_gate_col(int cg, int col) {
 // the 16-k slice ks (W in registers, h_{t-1} broadcast from LDS: each h value read feeds 4
 // columns x 2 rows, LDS return bandwidth rather than the FMAs bounds the step); the H / 16
 // slices are summed in order with gx; threads < 64 run the cells (c in registers).
-template <int H>
+template <int H, int R = kRgRows>
 __global__ void __launch_bounds__(H) lstm_fwd_rg_kernel(
     const float* __restrict__ gx, const float* __restrict__ wh, const float* __restrict__ h0,
     int64_t h0_stride, const float* __restrict__ c0, int64_t c0_stride, int B, int T,
     int64_t rs_b, int64_t rs_t, float* __restrict__ gates, float* __restrict__ h_out,
     float* __restrict__ c_out, unsigned long long* xg, unsigned tag0, unsigned* tmo,
     unsigned long long* trace = nullptr) {
-  using S = RgShape<H>;
-  constexpr int R = kRgRows, U = kRgUnits, NC = kRgCols, KW = S::KW, HV = S::HV, NS = S::NS;
+  using S = RgShape<H, R>;
+  constexpr int U = kRgUnits, NC = kRgCols, KW = S::KW, HV = S::HV, NS = S::NS;
   // H = 512: the next step's gx is prefetched and the 32 slices are summed in two halves by
   // all threads (a 32-long dependent chain of LDS reads in the 64 cell threads took 1.8 us
   // per step); H = 256 keeps IMPALA's order and schedule.
   constexpr bool kWide = H > 256;
+  static_assert(!kWide || R == 4, "H = 512: 4 rows per row group");
   __shared__ __attribute__((aligned(16))) float hs[R][H];
   __shared__ float red[NS][R][NC];
   __shared__ float red2[2][R * NC];
@@ -593,37 +595,44 @@ __global__ void __launch_bounds__(H) lstm_fwd_rg_kernel(
       gxn[q] = kWide && cell && t + 1 < T
                    ? gx[((size_t)cb * rs_b + (size_t)(t + 1) * rs_t) * 4 * H + q * H + cj]
                    : 0.f;
+    if constexpr (HV % 4 == 0) {
 #pragma unroll
-    for (int i = 0; i < HV; i += 4)
-      *reinterpret_cast<f32x4*>(&hs[0][0] + HV * tid + i) =
-          f32x4{hv[i], hv[i + 1], hv[i + 2], hv[i + 3]};
+      for (int i = 0; i < HV; i += 4)
+        *reinterpret_cast<f32x4*>(&hs[0][0] + HV * tid + i) =
+            f32x4{hv[i], hv[i + 1], hv[i + 2], hv[i + 3]};
+    } else {
+#pragma unroll
+      for (int i = 0; i < HV; i += 2)
+        *reinterpret_cast<f32x2*>(&hs[0][0] + HV * tid + i) = f32x2{hv[i], hv[i + 1]};
+    }
     __syncthreads();
     if (s_fail) return;  // every workgroup leaves on a timeout (its own wait fails too)
-    f32x2 a01[4], a23[4];  // per column: rows (0, 1) and (2, 3)
+    f32x2 acc[R / 2][4];  // per row pair (2p, 2p + 1) and column
 #pragma unroll
-    for (int c = 0; c < 4; ++c) a01[c] = a23[c] = f32x2{0.f, 0.f};
+    for (int pr = 0; pr < R / 2; ++pr)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[pr][c] = f32x2{0.f, 0.f};
 #pragma unroll
     for (int k4 = 0; k4 < KW / 4; ++k4) {
       const int k0 = ks * KW + 4 * k4;
-      const f32x4 h0v = *reinterpret_cast<const f32x4*>(&hs[0][k0]);
-      const f32x4 h1v = *reinterpret_cast<const f32x4*>(&hs[1][k0]);
-      const f32x4 h2v = *reinterpret_cast<const f32x4*>(&hs[2][k0]);
-      const f32x4 h3v = *reinterpret_cast<const f32x4*>(&hs[3][k0]);
+      f32x4 hr[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) hr[r] = *reinterpret_cast<const f32x4*>(&hs[r][k0]);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          a01[c] = fma2(h0v[j], h1v[j], w[c][4 * k4 + j], a01[c]);
-          a23[c] = fma2(h2v[j], h3v[j], w[c][4 * k4 + j], a23[c]);
-        }
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int pr = 0; pr < R / 2; ++pr)
+            acc[pr][c] = fma2(hr[2 * pr][j], hr[2 * pr + 1][j], w[c][4 * k4 + j], acc[pr][c]);
     }
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      red[ks][0][4 * cq + c] = a01[c][0];
-      red[ks][1][4 * cq + c] = a01[c][1];
-      red[ks][2][4 * cq + c] = a23[c][0];
-      red[ks][3][4 * cq + c] = a23[c][1];
-    }
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int pr = 0; pr < R / 2; ++pr) {
+        red[ks][2 * pr][4 * cq + c] = acc[pr][c][0];
+        red[ks][2 * pr + 1][4 * cq + c] = acc[pr][c][1];
+      }
     __syncthreads();
     if (kWide) {  // thread (half, output): the half's NS / 2 slices of one of R x NC outputs
       const int o = tid % (R * NC), half = tid / (R * NC);
@@ -683,19 +692,20 @@ __global__ void __launch_bounds__(H) lstm_fwd_rg_kernel(
 // product for dh_{t-1} over the gate-column slice gs (W_h row slice in registers), and the
 // slices are summed in order and published (4 rows x H values), each consumer reading its 16
 // units of every producer.  BPTT stops at t_stop (R2D2's burn-in: no gradient into it).
-template <int H>
+template <int H, int R = kRgRows>
 __global__ void __launch_bounds__(H) lstm_bwd_rg_kernel(
     const float* __restrict__ dh_head, const float* __restrict__ wh,
     const float* __restrict__ gates, const float* __restrict__ c_all,
     const float* __restrict__ c0, int64_t c0_stride, int B, int T, int t_stop, int64_t rs_b,
     int64_t rs_t, float* __restrict__ dgates, unsigned long long* xb, unsigned tag0,
     unsigned* tmo, unsigned long long* trace = nullptr) {
-  using S = RgShape<H>;
-  constexpr int R = kRgRows, U = kRgUnits, NC = kRgCols, G = S::G;
+  using S = RgShape<H, R>;
+  constexpr int U = kRgUnits, NC = kRgCols, G = S::G;
   constexpr int UT = S::UT, GS = S::GS, GW = S::GW, PV = S::PV, NT = S::NT;
   // H = 512: the 32 producers' partials are summed by all threads in 8 groups of 4, then by
   // the cells over the 8 groups in order (IMPALA's H = 256 keeps one chain of 16).
   constexpr bool kWide = H > 256;
+  static_assert(!kWide || R == 4, "H = 512: 4 rows per row group");
   constexpr int PG = NT / (R * U);  // producer groups (kWide)
   __shared__ float pp[G][R][U];
   __shared__ float pp2[PG][R * U];
@@ -801,32 +811,33 @@ __global__ void __launch_bounds__(H) lstm_bwd_rg_kernel(
     __syncthreads();
     RG_STAMP(2);
     if (t > t_stop) {
-      f32x2 a01[4], a23[4];  // per unit: rows (0, 1) and (2, 3)
+      f32x2 acc[R / 2][4];  // per row pair (2p, 2p + 1) and unit
 #pragma unroll
-      for (int uu = 0; uu < 4; ++uu) a01[uu] = a23[uu] = f32x2{0.f, 0.f};
+      for (int pr = 0; pr < R / 2; ++pr)
+#pragma unroll
+        for (int uu = 0; uu < 4; ++uu) acc[pr][uu] = f32x2{0.f, 0.f};
 #pragma unroll
       for (int g4 = 0; g4 < GW / 4; ++g4) {
-        const f32x4 d0 = *reinterpret_cast<const f32x4*>(&dgs[0][GW * gs + 4 * g4]);
-        const f32x4 d1 = *reinterpret_cast<const f32x4*>(&dgs[1][GW * gs + 4 * g4]);
-        const f32x4 d2 = *reinterpret_cast<const f32x4*>(&dgs[2][GW * gs + 4 * g4]);
-        const f32x4 d3 = *reinterpret_cast<const f32x4*>(&dgs[3][GW * gs + 4 * g4]);
+        f32x4 dr[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) dr[r] = *reinterpret_cast<const f32x4*>(&dgs[r][GW * gs + 4 * g4]);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
-          for (int uu = 0; uu < 4; ++uu) {
-            a01[uu] = fma2(d0[j], d1[j], w[uu][4 * g4 + j], a01[uu]);
-            a23[uu] = fma2(d2[j], d3[j], w[uu][4 * g4 + j], a23[uu]);
-          }
+          for (int uu = 0; uu < 4; ++uu)
+#pragma unroll
+            for (int pr = 0; pr < R / 2; ++pr)
+              acc[pr][uu] = fma2(dr[2 * pr][j], dr[2 * pr + 1][j], w[uu][4 * g4 + j], acc[pr][uu]);
       }
 #pragma unroll
-      for (int uu = 0; uu < 4; ++uu) {
-        red[gs][0][4 * uq + uu] = a01[uu][0];
-        red[gs][1][4 * uq + uu] = a01[uu][1];
-        red[gs][2][4 * uq + uu] = a23[uu][0];
-        red[gs][3][4 * uq + uu] = a23[uu][1];
-      }
+      for (int uu = 0; uu < 4; ++uu)
+#pragma unroll
+        for (int pr = 0; pr < R / 2; ++pr) {
+          red[gs][2 * pr][4 * uq + uu] = acc[pr][uu][0];
+          red[gs][2 * pr + 1][4 * uq + uu] = acc[pr][uu][1];
+        }
       __syncthreads();
-      // Thread u = tid publishes this workgroup's partial for its unit, 4 rows (the
+      // Thread u = tid publishes this workgroup's partial for its unit, R rows (the
       // gate-column slices summed in order).
       unsigned long long* out = xb + (size_t)(t & 1) * G * B * H + (size_t)cg * B * H;
 #pragma unroll
