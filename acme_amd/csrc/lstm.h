@@ -451,7 +451,7 @@ constexpr int kRgCols = 4 * kRgUnits;
 template <int H, int R = kRgRows>
 struct RgShape {
   static_assert(H == 256 || H == 512, "persistent unroll: H of 256 or 512");
-  static_assert(R == 2 || R == 4, "persistent unroll: 2 or 4 rows per row group");
+  static_assert(R == 1 || R == 2 || R == 4, "persistent unroll: 1, 2 or 4 rows per row group");
   static constexpr int NT = H;                     // threads per workgroup
   static constexpr int G = H / kRgUnits;           // workgroups per row group
   static constexpr int NS = NT / 16;               // forward: k-slices
@@ -600,6 +600,8 @@ __global__ void __launch_bounds__(H) lstm_fwd_rg_kernel(
       for (int i = 0; i < HV; i += 4)
         *reinterpret_cast<f32x4*>(&hs[0][0] + HV * tid + i) =
             f32x4{hv[i], hv[i + 1], hv[i + 2], hv[i + 3]};
+    } else if constexpr (HV == 1) {
+      (&hs[0][0])[tid] = hv[0];
     } else {
 #pragma unroll
       for (int i = 0; i < HV; i += 2)
@@ -607,6 +609,19 @@ __global__ void __launch_bounds__(H) lstm_fwd_rg_kernel(
     }
     __syncthreads();
     if (s_fail) return;  // every workgroup leaves on a timeout (its own wait fails too)
+    if constexpr (R == 1) {  // one row: scalar FMAs, the same per-row order
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k4 = 0; k4 < KW / 4; ++k4) {
+        const f32x4 h = *reinterpret_cast<const f32x4*>(&hs[0][ks * KW + 4 * k4]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) acc[c] = fmaf(h[j], w[c][4 * k4 + j], acc[c]);
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) red[ks][0][4 * cq + c] = acc[c];
+    } else {
     f32x2 acc[R / 2][4];  // per row pair (2p, 2p + 1) and column
 #pragma unroll
     for (int pr = 0; pr < R / 2; ++pr)
@@ -633,6 +648,7 @@ __global__ void __launch_bounds__(H) lstm_fwd_rg_kernel(
         red[ks][2 * pr][4 * cq + c] = acc[pr][c][0];
         red[ks][2 * pr + 1][4 * cq + c] = acc[pr][c][1];
       }
+    }
     __syncthreads();
     if (kWide) {  // thread (half, output): the half's NS / 2 slices of one of R x NC outputs
       const int o = tid % (R * NC), half = tid / (R * NC);
@@ -811,6 +827,19 @@ __global__ void __launch_bounds__(H) lstm_bwd_rg_kernel(
     __syncthreads();
     RG_STAMP(2);
     if (t > t_stop) {
+      if constexpr (R == 1) {  // one row: scalar FMAs, the same per-row order
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int g4 = 0; g4 < GW / 4; ++g4) {
+          const f32x4 d = *reinterpret_cast<const f32x4*>(&dgs[0][GW * gs + 4 * g4]);
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int uu = 0; uu < 4; ++uu) acc[uu] = fmaf(d[j], w[uu][4 * g4 + j], acc[uu]);
+        }
+#pragma unroll
+        for (int uu = 0; uu < 4; ++uu) red[gs][0][4 * uq + uu] = acc[uu];
+      } else {
       f32x2 acc[R / 2][4];  // per row pair (2p, 2p + 1) and unit
 #pragma unroll
       for (int pr = 0; pr < R / 2; ++pr)
@@ -836,6 +865,7 @@ __global__ void __launch_bounds__(H) lstm_bwd_rg_kernel(
           red[gs][2 * pr][4 * uq + uu] = acc[pr][uu][0];
           red[gs][2 * pr + 1][4 * uq + uu] = acc[pr][uu][1];
         }
+      }
       __syncthreads();
       // Thread u = tid publishes this workgroup's partial for its unit, R rows (the
       // gate-column slices summed in order).
