@@ -15,6 +15,7 @@ algorithmic bytes.  Usage:
 import collections
 import csv
 import glob
+import os
 import json
 import re
 import sys
@@ -79,6 +80,17 @@ SECTIONS = [
     (r"prio_update_fused_kernel", "replay_update"),
 ]
 SECTIONS_R2D2 = [
+    # The Atari plane path (the bench's), then the f32 engine's names.
+    (r"P3DenseFwd", "r2d2_oar_fwd"),
+    (r"P3DenseWgrad", "r2d2_wi_wgrad"),
+    (r"P3DenseDgrad", "r2d2_feat_dgrad"),
+    (r"oar_finish_kernel", "r2d2_oar_reduce"),
+    (r"oar_wgrad_tail_kernel", "r2d2_wi_wgrad_tail"),
+    (r"r2d2_frames_f16_kernel", "r2d2_permute"),
+    (r"split_planes_lagged_kernel", "r2d2_planes"),
+    (r"DenseWgradRC", "r2d2_hidden_wgrad"),
+    (r"lstm_fwd_rg_kernel", "r2d2_lstm_fwd"),
+    (r"lstm_bwd_rg_kernel", "r2d2_lstm_bwd"),
     (r"OarFwd", "r2d2_oar_fwd"),
     (r"OarWgrad", "r2d2_wi_wgrad"),
     (r"HPrevTM", "r2d2_wh_wgrad"),
@@ -107,8 +119,11 @@ def section(name):
 
 
 def per_launch(d, counter):
+    # The newest pass only: gpurun merges each run's output into the same local directory.
+    paths = glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)
+    paths = sorted(paths, key=os.path.getmtime)[-1:]
     vals = collections.defaultdict(list)
-    for path in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+    for path in paths:
         for r in csv.DictReader(open(path)):
             if r["Counter_Name"] != counter:
                 continue
