@@ -54,6 +54,8 @@ constexpr int kHeadFwdSplits = 16;  // duelling head [rows, A + 1] x K = 2 H2
 constexpr int kHeadBwdSplits = 8;   // duelling head weights [2 H2 + 1, A + 1] x K = rows
 constexpr int kMaxSeq = 256;        // sequence length bound (the loss kernel's LDS)
 constexpr int kFwdLds = 160 * 1024; // LDS per workgroup on gfx950
+constexpr int kHiddenWgradSplits = 4;  // split-K of the duelling hidden layer's weight gradient
+constexpr int kWhWgradSplits = 2;      // split-K of the W_h weight gradient
 constexpr int kOarSplitsP3 = 4;     // split-K of the plane-engine OAR projection (K = 7744)
 
 // Scale records of the plane path: the transient activations / gradients (the target and
@@ -461,6 +463,7 @@ struct DenseWgradRC {
   const float* dz;
   float* out;
   float* bias_out;
+  float* slab;  // split-K partials [splits][M + 1][N] (row M: the column sums), or direct
   struct ARow {
     int i;
   };
@@ -477,8 +480,14 @@ struct DenseWgradRC {
     if (b.n >= N || m >= K) return gemm::zero4();
     return load_row4<true>(dz + (size_t)m * N, b.n, N);
   }
-  __device__ void store(int i, int n, float v, int) const { out[(size_t)i * N + n] = v; }
-  __device__ void store_colsum(int n, float v, int) const { bias_out[n] = v; }
+  __device__ void store(int i, int n, float v, int split) const {
+    if (slab) slab[((size_t)split * (M + 1) + i) * N + n] = v;
+    else out[(size_t)i * N + n] = v;
+  }
+  __device__ void store_colsum(int n, float v, int split) const {
+    if (slab) slab[((size_t)split * (M + 1) + M) * N + n] = v;
+    else bias_out[n] = v;
+  }
 };
 
 // dW_h = h_prev^T dgates over the suffix rows (time-major): h_prev of row m (global row
@@ -492,6 +501,7 @@ struct HPrevTM {
   int B, BI;
   const float* dz;       // [L B][4H]
   float* out;
+  float* slab;           // split-K partials [splits][M][N], or direct
   struct ARow {
     int i;
   };
@@ -510,7 +520,10 @@ struct HPrevTM {
     if (b.n >= N || m >= K) return gemm::zero4();
     return load_row4<true>(dz + (size_t)m * N, b.n, N);
   }
-  __device__ void store(int i, int n, float v, int) const { out[(size_t)i * N + n] = v; }
+  __device__ void store(int i, int n, float v, int split) const {
+    if (slab) slab[((size_t)split * M + i) * N + n] = v;
+    else out[(size_t)i * N + n] = v;
+  }
 };
 
 torso::Weights torso_w(const acme_r2d2* l, const float* prm) {
@@ -709,10 +722,20 @@ int r2d2_step_impl(acme_r2d2* l, const acme_sequence_batch* bt, const double* pr
   }
   const float* hs = l->h + (size_t)BI * B * H;  // the suffix's LSTM outputs
   {  // hidden layer: weights over the suffix rows, and d h
+    // Split-K 4 over the 2,592 rows (8 x 16 tiles x 4 = 512 blocks), reduced with the bias.
     DenseWgradRC w;
-    w.M = H; w.N = 2 * H2; w.K = RL; w.k_chunk = RL;
+    w.M = H; w.N = 2 * H2; w.K = RL; w.k_chunk = chunk_for(RL, kHiddenWgradSplits);
     w.x = hs; w.ldx = H; w.dz = l->dzh; w.out = Pm(l, gr, l->t_hw); w.bias_out = Pm(l, gr, l->t_hb);
-    R2_GEMM("r2d2_hidden_wgrad", 64, 64, 2, 2, 1, w, 1);
+    w.slab = l->slab;
+    R2_GEMM("r2d2_hidden_wgrad", 64, 64, 2, 2, 1, w, kHiddenWgradSplits);
+    {
+      ACME_PROF("r2d2_hidden_wgrad_reduce", st, 0.0,
+                4.0 * (kHiddenWgradSplits + 1) * (double)(H + 1) * 2 * H2);
+      rc = launch_slab_reduce(l->slab, kHiddenWgradSplits, (int64_t)(H + 1) * 2 * H2,
+                              Pm(l, gr, l->t_hw), (int64_t)H * 2 * H2, Pm(l, gr, l->t_hb),
+                              nullptr, 0, 0, st);
+      if (rc != ACME_OK) return rc;
+    }
     DenseDgrad<true> d;
     d.M = RL; d.N = H; d.K = 2 * H2; d.k_chunk = 2 * H2;
     d.dz = l->dzh; d.w = P(l, prm, l->t_hw); d.xprev = nullptr; d.ldx = H;
@@ -754,7 +777,16 @@ int r2d2_step_impl(acme_r2d2* l, const acme_sequence_batch* bt, const double* pr
     w.h = l->h; w.h0 = l->cfg.store_lstm_state ? bt->h0 : l->zero_state;
     w.h0_stride = l->cfg.store_lstm_state ? bt->state_stride : H;
     w.B = B; w.BI = BI; w.dz = l->dgates; w.out = Pm(l, gr, l->t_wh);
-    R2_GEMM("r2d2_wh_wgrad", 64, 64, 2, 2, 1, w, 1);
+    // Split-K 2 (8 x 32 tiles x 2 = 512 blocks).
+    w.k_chunk = chunk_for(RL, kWhWgradSplits);
+    w.slab = l->slab;
+    R2_GEMM("r2d2_wh_wgrad", 64, 64, 2, 2, 1, w, kWhWgradSplits);
+    {
+      ACME_PROF("r2d2_wh_wgrad_reduce", st, 0.0, 4.0 * (kWhWgradSplits + 1) * (double)H * 4 * H);
+      rc = launch_slab_reduce(l->slab, kWhWgradSplits, (int64_t)H * 4 * H, Pm(l, gr, l->t_wh),
+                              (int64_t)H * 4 * H, nullptr, nullptr, 0, 0, st);
+      if (rc != ACME_OK) return rc;
+    }
   }
   if (l->p3) {  // W_i, b and the embedding gradient on the plane engine, then the plane torso
     const int F = l->F, N = 4 * H;
@@ -953,7 +985,8 @@ int acme_r2d2_create(const acme_r2d2_config* cfg, acme_r2d2** out) {
   int rc;
   int64_t slab = std::max<int64_t>({(int64_t)kHeadFwdSplits * RL * (A + 1),
                                     (int64_t)kHeadBwdSplits * (2 * H2 + 1) * (A + 1),
-                                    (int64_t)64});
+                                    (int64_t)kHiddenWgradSplits * (H + 1) * 2 * H2,
+                                    (int64_t)kWhWgradSplits * H * 4 * H, (int64_t)64});
   if (cfg->torso == ACME_IMPALA_TORSO_ATARI) {
     slab = std::max<int64_t>({slab, torso::wgrad_slab_floats(), (int64_t)kOarSplits * R * 4 * H});
     // (On the plane path x1..x3 serve the debug buffers only: the planes joined to f32.)
