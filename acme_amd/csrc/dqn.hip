@@ -435,8 +435,12 @@ int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const torso:
     // (per-CU L2 intake): fc_fwd 47.0 -> 45.3 us, step 0.5037 -> 0.5028 ms
     // over 200 steps and 0.5146 -> 0.5084 ms over 20-step windows (three alternating pairs,
     // round 4; it had split-K 4 on 128x128 tiles).
+    // The target forward at the headline batch (512 rows) on 256x128 tiles too, at split-K
+    // 16 (2 x 8 x 16 blocks; its head sums 16 partials): fc_fwd 45.2 -> 43.9 us averaged over
+    // both launches, the step unchanged (0.5040 vs 0.5037 ms, three alternating pairs).
     const bool tall = rows > 512;
-    const int splits = kFcFwdSplits;
+    const bool ttall = rows == 512 && !defer_head;
+    const int splits = ttall ? 16 : kFcFwdSplits;
     p.M = rows; p.N = 2 * kHidden; p.K = kFlat; p.k_chunk = chunk_for(kFlat, splits);
     p.a_src = SRC(x3, (int64_t)rows * kFlat); p.ldx = kFlat;
     p.b_src = SRC(WP(l, wpl, l->t_fcw), (int64_t)kFlat * 2 * kHidden); p.slab = slab;
@@ -444,7 +448,9 @@ int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const torso:
     // 65.2 -> 60.5 us against the single-role kernel, the same bits.
     // (Two f16 planes, measured on the step: 256x128 / 128x256 WS tiles, 256x128 single-role
     // tiles with split-K 8, and the LDS-DMA ring (3 or 4 stages) all slower or equal.)
-    if (tall && l->single_role) ACME_P3_GEMM("fc_fwd", 256, 128, 2, 2, 32, p, splits);  // tests
+    if (ttall && l->single_role) ACME_P3_GEMM("fc_fwd", 256, 128, 2, 2, 32, p, splits);  // tests
+    else if (ttall) ACME_P3WS_GEMM("fc_fwd", 256, 128, 2, 2, 32, p, splits, true);
+    else if (tall && l->single_role) ACME_P3_GEMM("fc_fwd", 256, 128, 2, 2, 32, p, splits);  // tests
     else if (tall) ACME_P3WS_GEMM("fc_fwd", 256, 128, 2, 2, 32, p, splits, true);
     else if (l->single_role) ACME_P3_GEMM("fc_fwd", 128, 128, 2, 2, 32, p, splits);  // tests
     else ACME_P3WS_GEMM("fc_fwd", 128, 128, 2, 2, 32, p, splits, true);

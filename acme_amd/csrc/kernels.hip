@@ -1348,9 +1348,11 @@ int launch_fc_head_forward(const float* slab, int splits, int rows, int H, const
   const bool wa16 = reinterpret_cast<uintptr_t>(wa) % 16 == 0 &&
                     reinterpret_cast<uintptr_t>(wv) % 16 == 0 &&
                     reinterpret_cast<uintptr_t>(fcb) % 16 == 0;
-  if (H == 512 && A == 18 && wa16 && (splits == 4 || splits == 8)) {
+  if (H == 512 && A == 18 && wa16 && (splits == 4 || splits == 8 || splits == 16)) {
     // One row per block (2 rows: 12.7 us, 4 rows: 16.3 us, 1 row: 11.4 us per launch).
-    if (splits == 8)
+    if (splits == 16)
+      fc_head1024_kernel<16, 18, 1><<<rows, 256, 0, st>>>(slab, rows, fcb, wv, bv, wa, ba, hid, q);
+    else if (splits == 8)
       fc_head1024_kernel<8, 18, 1><<<rows, 256, 0, st>>>(slab, rows, fcb, wv, bv, wa, ba, hid, q);
     else
       fc_head1024_kernel<4, 18, 1><<<rows, 256, 0, st>>>(slab, rows, fcb, wv, bv, wa, ba, hid, q);
