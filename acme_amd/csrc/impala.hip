@@ -672,6 +672,7 @@ int impala_step_impl(acme_impala* l, const acme_sequence_batch* bt, float* metri
       p.a_src = SRC(l->x3p, (int64_t)rows * F); p.ldx = F;
       p.b_src = SRC(l->dgp, (int64_t)rows * N); p.out = Pm(l, gr, l->t_wi);
       p.bias_out = Pm(l, gr, l->t_b);
+      // (256x128 warp-specialised tiles: 24.7 -> 26.6 us, round 4.)
       IM_P3_GEMM("impala_wi_wgrad", 128, 128, 2, 2, 16, p, 1);
     }
     {

@@ -804,8 +804,9 @@ int r2d2_step_impl(acme_r2d2* l, const acme_sequence_batch* bt, const double* pr
       w.a_src = SRC(x3s, (int64_t)RL * F); w.ldx = F;
       w.b_src = SRC(l->dgp, (int64_t)RL * N); w.out = Pm(l, gr, l->t_wi);
       w.bias_out = Pm(l, gr, l->t_b);
-      // (256x128 tiles measured slower here: 236 -> 257 us.)
-      R2_P3_GEMM("r2d2_wi_wgrad", 128, 128, 2, 2, 16, w, 1);
+      // 256x128 warp-specialised tiles over the 2,592-row reduction: 233 -> 188 us against
+      // 128x128 single-role at BK 16 (single-role 256x128: 257 us; round 4).
+      R2_P3WS_GEMM("r2d2_wi_wgrad", 256, 128, 2, 2, 32, w, 1);
     }
     {
       ACME_PROF("r2d2_wi_wgrad_tail", st, 0.0, 4.0 * (double)RL * N);
