@@ -1,0 +1,138 @@
+"""R2D2 drop-in path on the GPU end to end: ObservationActionRewardWrapper spec ->
+SequenceAdder -> prioritized sequence table -> dataset -> R2D2Learner.step() -> priority
+write-back, with the loss and priorities checked against the oracle on the very sequences
+the learner drew (acme/agents/tf/r2d2/agent.py:72-103, learning.py:112-200, 230-236), and
+the learner's save/restore round trip (learning.py:218-228)."""
+
+import numpy as np
+import pytest
+import torch
+
+from acme_amd import dm_env, specs
+from acme_amd.testing import fakes
+from acme_amd.utils import loggers
+from acme_amd.wrappers import ObservationActionRewardWrapper
+from oracle import r2d2_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+class _Recorder:
+    """Iterable over the dataset that keeps a host copy of every sample the learner draws."""
+
+    def __init__(self, dataset):
+        self._dataset, self.samples = dataset, []
+
+    def __iter__(self):
+        it = iter(self._dataset)
+
+        def gen():
+            for s in it:
+                self.samples.append(_host(s))
+                yield s
+        return gen()
+
+
+def _host(sample):
+    d, info = sample.data, sample.info
+    obs = d.observation
+    np_ = lambda x: x.detach().cpu().numpy()  # noqa: E731
+    keys, probs = np_(info.key).view(np.int64), np_(info.probability)
+    if probs.ndim == 2:
+        keys, probs = keys[:, 0], probs[:, 0]
+    h, c = d.extras["core_state"]
+    state = np.stack([np_(h), np_(c)], axis=2).astype(np.float32)  # [B, T, 2, H]
+    return dict(obs=np_(obs.observation).astype(np.float32),
+                prev_action=np_(obs.action).astype(np.int32),
+                prev_reward=np_(obs.reward).astype(np.float32),
+                action=np_(d.action).astype(np.int32), reward=np_(d.reward).astype(np.float32),
+                discount=np_(d.discount).astype(np.float32), state=state,
+                h0=state[:, 0, 0].copy(), c0=state[:, 0, 1].copy(),
+                probabilities=probs.astype(np.float64), keys=keys)
+
+
+def _drive(adder, rng, A, obs_dim, H, episodes=5, length=17):
+    from acme_amd.networks import LSTMState
+    from acme_amd.wrappers import OAR
+    for _ in range(episodes):
+        adder.add_first(dm_env.restart(OAR(rng.standard_normal(obs_dim).astype(np.float32),
+                                           np.int32(0), np.float32(0.0))))
+        for t in range(length):
+            a = np.int32(rng.integers(A))
+            r = np.float32(rng.standard_normal())
+            o = OAR(rng.standard_normal(obs_dim).astype(np.float32), a, r)
+            ts = (dm_env.termination(r, o) if t == length - 1 else
+                  dm_env.transition(r, o, np.float32(1.0)))
+            core = LSTMState((0.5 * rng.standard_normal(H)).astype(np.float32),
+                             (0.5 * rng.standard_normal(H)).astype(np.float32))
+            adder.add(a, ts, extras={"core_state": core})
+
+
+def test_r2d2_learner_through_sequence_replay():
+    from acme_amd import replay
+    from acme_amd.adders import reverb as adders
+    from acme_amd.agents import r2d2
+    from acme_amd.agents.r2d2.learning import R2D2Learner
+    from acme_amd.networks import LSTMState, R2D2AtariNetwork
+    A, H, obs_dim, B = 5, 16, 6, 4
+    burn, trace, period, n_step, size = 2, 5, 3, 3, 1000
+    T = burn + trace + 1
+    env = ObservationActionRewardWrapper(fakes.DiscreteEnvironment(num_actions=A,
+                                                                   obs_shape=(obs_dim,)))
+    spec = specs.make_environment_spec(env)
+    extra = {"core_state": LSTMState(specs.Array((H,), np.float32),
+                                     specs.Array((H,), np.float32))}
+    server, adder, dataset = r2d2.make_replay(spec, extra, burn, trace, period, batch_size=B,
+                                              max_replay_size=size)
+    _drive(adder, np.random.default_rng(0), A, obs_dim, H)
+    table = server.tables[adders.DEFAULT_PRIORITY_TABLE]
+    table.flush()
+    assert table.size() > 2 * B and table.sequence_length == T
+    net = R2D2AtariNetwork(A, lstm_size=H, head_size=8, torso="flat", obs_dim=obs_dim)
+    rec = _Recorder(dataset)
+    kw = dict(burn_in_length=burn, sequence_length=T, reverb_client=replay.Client(server),
+              logger=loggers.NoOpLogger(), n_step=n_step, target_update_period=2,
+              max_replay_size=size, batch_size=B, seed=5)
+    learner = R2D2Learner(spec, net, net, dataset=rec, **kw)
+    cfg = O.R2D2Config(num_actions=A, torso="flat", obs_dim=obs_dim, lstm_size=H, head_size=8,
+                       burn_in_length=burn, n_step=n_step, max_replay_size=size,
+                       target_update_period=2)
+    n = learner.native
+    for k in range(3):
+        params, target = n.get_params("params"), n.get_params("target")
+        learner.step()
+        torch.cuda.synchronize()
+        b = rec.samples[-1]
+        assert b["obs"].shape == (B, T, obs_dim) and b["action"].shape == (B, T)
+        ref, _ = O.loss_and_grads(cfg, params, target, b)
+        loss = n.loss.item()
+        assert np.isfinite(loss)
+        np.testing.assert_allclose(loss, ref["loss"], rtol=2e-4, err_msg=f"loss step {k}")
+        prio = n.priorities[:B].cpu().numpy()
+        np.testing.assert_allclose(prio, ref["priorities"], atol=2.5e-4, rtol=1e-4,
+                                   err_msg=f"priorities step {k}")
+        # The write-back: each drawn item's leaf is the learner's own priority ^ exponent
+        # (the last write of a key drawn twice wins).
+        leaves = table.native.debug_state()["leaves"]
+        last = {int(key) % size: float(p) for key, p in zip(b["keys"], prio)}
+        for slot, p in last.items():
+            assert leaves[slot] == pytest.approx(p ** 0.6, rel=1e-6), (k, slot)
+        assert learner.num_steps == k + 1
+        if k % 2 == 0:  # the target copy after the update, count before it (learning.py:185-189)
+            tgt = n.get_params("target")
+            for name, v in n.get_params("params").items():
+                np.testing.assert_array_equal(tgt[name], v, err_msg=f"target copy {name}")
+    assert n.guard_state()["applied"] == 3
+    # save / restore into a fresh learner on the same replay.
+    state = learner.save()
+    other = R2D2Learner(spec, net, net, dataset=dataset, **dict(kw, seed=11))
+    other.restore(state)
+    assert other.num_steps == 3
+    for which in ("params", "target", "m", "v"):
+        a, c = n.get_params(which), other.native.get_params(which)
+        for name in a:
+            np.testing.assert_array_equal(a[name], c[name], err_msg=f"{which} {name}")
+    assert other.native.guard_state()["applied"] == 3
+    other.step()
+    torch.cuda.synchronize()
+    assert other.num_steps == 4 and np.isfinite(other.native.loss.item())
