@@ -377,6 +377,9 @@ def insert_bench(args, dev):
             "learner_ms_per_step_with_bulk_inserts": round(1e3 * t_bulk / args.steps, 4),
             "reference_rate_needed_items_per_s": round(
                 B / 32.0 / (t_alone / args.steps), 1),  # samples_per_insert = 32
+            # The paced adder is held to B / 32 items per learner step, so its rate follows
+            # the learner: the ratio it reached inside the window (the reference's 32).
+            "paced_samples_per_insert": round(B * args.steps / max(r_paced * t_paced, 1e-9), 2),
         },
     }
     print(json.dumps(out))
