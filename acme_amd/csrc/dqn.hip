@@ -844,15 +844,14 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
       l->slab_floats = std::max(l->slab_floats, torso::wgrad_slab_floats_p3());
       // ACME_V_SIDE=1 at creation: a single stream (tests of the schedule).
       if (!l->single_stream) {
-        // The second stream at the lowest priority (1 on MI355X; the caller's streams are
-        // normally 0): the dispatcher then favours the main stream's blocks, which carry
-        // the step's critical path (the online forward, the input-gradient chain, Adam).
-        // 0.5308 -> 0.5260 ms per step against the default priority (three alternating runs
-        // each); the highest priority measured slower.
-        int lo = 0, hi = 0;
-        hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
-        if (e == hipSuccess)
-          e = hipStreamCreateWithPriority(&l->side, hipStreamNonBlocking, lo);
+        // The second stream at the default priority.  At the lowest priority (rounds 2-3:
+        // 0.5308 -> 0.5260 ms per step then, so the dispatcher favoured the main stream's
+        // critical path) the step time depended on the order the process created its
+        // streams: two streams created before the learner's first step (a table's insert
+        // path) left every main-stream kernel about 2x longer, 0.51 -> 1.10 ms per step
+        // (tools/insert_diag5.py); at the default priority 0.51 ms either way, and the same
+        // step time as the lowest priority otherwise (tools/ab_sprio.sh, round 4).
+        hipError_t e = hipStreamCreateWithFlags(&l->side, hipStreamNonBlocking);
         for (auto& ev : l->ev)
           if (e == hipSuccess) e = make_order_event(&ev);
         if (e != hipSuccess)
