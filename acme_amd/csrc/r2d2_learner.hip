@@ -56,7 +56,7 @@ constexpr int kMaxSeq = 256;        // sequence length bound (the loss kernel's 
 constexpr int kFwdLds = 160 * 1024; // LDS per workgroup on gfx950
 constexpr int kHiddenWgradSplits = 4;  // split-K of the duelling hidden layer's weight gradient
 constexpr int kWhWgradSplits = 2;      // split-K of the W_h weight gradient
-constexpr int kOarSplitsP3 = 4;     // split-K of the plane-engine OAR projection (K = 7744)
+constexpr int kOarSplitsP3 = 2;     // split-K of the plane-engine OAR projection (K = 7744)
 
 // Scale records of the plane path: the transient activations / gradients (the target and
 // online passes write the same activation planes: one record each, the maximum of both),
@@ -555,7 +555,9 @@ int network_forward(acme_r2d2* l, const float* prm, const acme_sequence_batch* b
     P3DenseFwd p;
     // 256x128 tiles at split-K 4 (16 x 16 x 4 blocks at the bench shape): 433 -> 325 us,
     // the split-K reduction 63 -> 30 us, the step 5.16 -> 4.87 ms against 128x128 at split-K
-    // 8 (two alternating pairs, round 4; DESIGN.md 4.1 on the per-CU intake).
+    // 8 (two alternating pairs, round 4; DESIGN.md 4.1 on the per-CU intake).  Split-K 2:
+    // 321 -> 301 us, the reduction 30 -> 20 us, the step 4.51 -> 4.44 ms; split-K 1 292 us
+    // but the step 4.46 ms (two alternating runs each, tools/ab_oars.sh).
     const int splits = kOarSplitsP3;
     p.M = R; p.N = N; p.K = F; p.k_chunk = chunk_for(F, splits);
     p.a_src = SRC(l->x3p, (int64_t)R * F); p.ldx = F;
