@@ -192,6 +192,9 @@ _SIGS = {
     "acme_dqn_guard_state": (c_i32, [c_vp, ctypes.POINTER(c_i64)]),
     "acme_dqn_set_applied_steps": (c_i32, [c_vp, c_i64]),
     "acme_dqn_skip_word": (c_i32, [c_vp, ctypes.POINTER(c_vp)]),
+    "acme_dqn_set_reissue": (c_i32, [c_vp, c_i32]),
+    "acme_dqn_verdicts_issued": (c_i64, [c_vp]),
+    "acme_dqn_step_verdict": (c_i32, [c_vp, c_i64, ctypes.POINTER(c_i32)]),
     "acme_dqn_set_data_parallel_gate": (c_i32, [c_vp, c_i32]),
     "acme_dqn_dense_grads_ready": (c_i32, [c_vp, c_vp]),
     "acme_dqn_dp_init": (c_i32, [c_vp, c_vp, c_i32]),

@@ -13,17 +13,27 @@ reference's deepcopy + create_variables (agents/tf/dqn/agent.py:127-131).
 
 Plane overflow (the uint8 Nature path runs its GEMMs on scaled f16 planes, csrc/gemm_p3.h):
 a step in which some plane write overflowed f16 (a tensor's maximum grew more than ~2^8-fold
-since the previous step) is skipped on the device, the rule of automatic mixed precision:
-no parameter, Adam moment or count, target or priority changes, and the end-of-step rescale
-sets every scale from that step's true maxima.  The learner sees the count lazily (a pinned
-host word, no synchronisation); on a new skip it re-splits the parameter planes and
-recalibrates the scales before its next step (`on_plane_overflow="skip"`, logged as
-`skipped_steps`), or raises FloatingPointError (`"raise"`).  Adam's t counts applied
-updates; `num_steps` (the target period) counts step() calls.
+since the previous step, or fell more than ~2^7-fold) is skipped on the device: no
+parameter, Adam moment or count, target or priority changes, and the end-of-step rescale
+sets every scale from that step's true maxima.  The reference applies every step
+(agents/tf/dqn/learning.py:147-161), so the learner RE-ISSUES a skipped step
+(`on_plane_overflow="reissue"`, the default): the device holds every later step skipped
+too (acme_dqn_set_reissue), and at the start of each step() call the learner reads the
+verdict of the step issued two calls earlier (a pinned ring the device writes: no
+synchronisation, and normally long decided, since the host runs at most two steps ahead).
+On a skip it re-splits the parameter planes, recalibrates the scales and issues the held
+batches again in their order, with the step counter of their first issue (so a due target
+copy lands), before drawing the next batch; save(), state, get_variables() and q_values()
+settle the last two steps the same way first.  So every step() call applies exactly one
+update, in the reference's order, and a skip only costs the re-issued steps' time.
+`"raise"` raises FloatingPointError instead; `"skip"` keeps the skip (the step's batch is
+dropped, as before round 5).  `num_steps` (the target period) counts step() calls; Adam's
+t counts applied updates.
 """
 
 from __future__ import annotations
 
+import collections
 import time
 from typing import Dict, List, Optional
 
@@ -34,6 +44,11 @@ from acme_amd import core
 from acme_amd.adders import reverb as adders
 from acme_amd.native import NativeDQN
 from acme_amd.utils import counting, loggers
+
+# Verdicts checked at step() call k: those of the steps issued up to call k - 2 (the
+# dataset's buffer ring keeps the batches of calls k - 2 and k - 1 until call k draws).
+_REISSUE_LAG = 2
+_REISSUE_ATTEMPTS = 3
 
 
 class DQNLearner(core.Learner, core.Saveable):
@@ -46,11 +61,11 @@ class DQNLearner(core.Learner, core.Saveable):
                  max_abs_reward: float = 1.0, batch_size: Optional[int] = None, seed: int = 0,
                  device=None, data_parallel: bool = True, semantics: str = "tf",
                  target_seed: Optional[int] = None, adam=None,
-                 reduce_logged_loss: bool = True, on_plane_overflow: str = "skip"):
+                 reduce_logged_loss: bool = True, on_plane_overflow: str = "reissue"):
         if huber_loss_parameter < 0:
             raise ValueError("quadratic_linear_boundary must be >= 0.")
-        if on_plane_overflow not in ("skip", "raise"):
-            raise ValueError("on_plane_overflow must be 'skip' or 'raise'")
+        if on_plane_overflow not in ("reissue", "skip", "raise"):
+            raise ValueError("on_plane_overflow must be 'reissue', 'skip' or 'raise'")
         self._on_overflow = on_plane_overflow
         self._skips_seen = 0
         self._network = network
@@ -110,6 +125,13 @@ class DQNLearner(core.Learner, core.Saveable):
                 # the torso gradient bucket's all-reduce.
                 self._native.set_data_parallel_gate(True)
         self._skip_word = self._native.skip_word
+        # Re-issue of skipped steps (the plane path): the last _REISSUE_LAG issued steps,
+        # their batches held (sequence number of their verdict, step counter at issue).
+        self._reissue = self._skip_word is not None and on_plane_overflow == "reissue"
+        self._native.set_reissue(self._reissue)
+        self._held = collections.deque(maxlen=_REISSUE_LAG)
+        self._checked = self._native.verdicts_issued  # verdicts below this are settled
+        self._reissued = 0
 
     # ------------------------------------------------------------------ step
     def _prepare(self, x: torch.Tensor, dtype) -> torch.Tensor:
@@ -120,6 +142,9 @@ class DQNLearner(core.Learner, core.Saveable):
     def _check_guard(self) -> int:
         """Skipped steps the device has reported so far (no synchronisation); on a new one,
         re-split the planes and recalibrate the scales before the next step, or raise."""
+        if self._reissue:
+            self._await_verdicts(settle=False)
+            return self._reissued
         n = self._native.skipped_steps
         if n != self._skips_seen:
             self._skips_seen = n
@@ -129,6 +154,84 @@ class DQNLearner(core.Learner, core.Saveable):
                     "were not applied)")
             self._native.params_changed()
         return n
+
+    def _await_verdicts(self, settle: bool) -> None:
+        """Reads the verdicts not yet settled: those of all steps but the last
+        _REISSUE_LAG - 1 issued (waiting for them: normally long decided), or with `settle`
+        of every issued step (after a synchronisation); re-issues from the first skipped."""
+        n = self._native
+        if settle:
+            torch.cuda.synchronize(n.device)
+        upto = n.verdicts_issued - (0 if settle else _REISSUE_LAG - 1)
+        deadline = None
+        while self._checked < upto:
+            v = n.step_verdict(self._checked)
+            if v is None:  # not decided yet: the device is behind (rare)
+                deadline = deadline or time.time() + 120.0
+                if time.time() > deadline:
+                    raise RuntimeError("DQN learner: step verdict not published within 120 s")
+                time.sleep(0)
+                continue
+            if v:
+                self._reissue_from(self._checked)
+            else:
+                self._checked += 1
+
+    def _reissue_from(self, seq: int) -> None:
+        """Step `seq` was skipped, and (sticky hold) every step issued after it: recalibrate
+        and issue their held batches again, in order."""
+        n = self._native
+        if self._on_overflow == "raise":
+            raise FloatingPointError(
+                "DQN learner: a step was skipped on f16 plane overflow (its update was not "
+                "applied)")
+        for _ in range(_REISSUE_ATTEMPTS):
+            torch.cuda.synchronize(n.device)
+            pend = [e for e in self._held if e["seq"] >= seq]
+            if not pend or pend[0]["seq"] != seq:
+                raise RuntimeError(f"DQN learner: skipped step (verdict {seq}) is no longer held")
+            n.params_changed()  # re-split the planes, recalibrate; clears the hold
+            n.num_steps = pend[0]["num_steps"]
+            for e in pend:
+                self._issue(e)
+                self._reissued += 1
+            torch.cuda.synchronize(n.device)
+            seq = next((e["seq"] for e in pend if n.step_verdict(e["seq"])), None)
+            if seq is None:
+                self._checked = n.verdicts_issued
+                self._skips_seen = n.skipped_steps
+                return
+        raise FloatingPointError(
+            f"DQN learner: a step was skipped {_REISSUE_ATTEMPTS} times on f16 plane overflow")
+
+    def _issue(self, e: Dict) -> None:
+        """Issues one held step (its batch, priority write-back and step counter)."""
+        n = self._native
+        e["seq"] = n.verdicts_issued
+        e["num_steps"] = n.num_steps
+        batch, fb, keys, B = e["batch"], e["fb"], e["keys"], e["B"]
+        inputs_event = e.pop("inputs_event", None)  # only for the first issue
+        upd = None
+        if self._dist is None and not self._staged:
+            # The priority write-back rides in the step (on the learner's second stream
+            # beside the backward) when the client's table offers it.
+            prep = getattr(self._replay_client, "prepare_priority_update", None)
+            if prep is not None:
+                upd = prep(adders.DEFAULT_PRIORITY_TABLE, keys)
+            n.step(*batch, obs_f16=fb, priority_update=upd, inputs_event=inputs_event)
+        else:
+            self._staged_step(batch, fb, inputs_event)
+        if self._replay_client is not None and upd is None:
+            # Gated on the step's skip word: a skipped step writes no priority.
+            kw = {"skip_word": self._skip_word} if self._skip_word else {}
+            self._replay_client.update_priorities(table=adders.DEFAULT_PRIORITY_TABLE,
+                                                  keys=keys, priorities=n.priorities[:B], **kw)
+
+    def _settle(self) -> None:
+        """Before the learner's state is read: every issued step decided, a skipped one
+        re-issued."""
+        if self._reissue:
+            self._await_verdicts(settle=True)
 
     def step(self):
         skipped = self._check_guard()
@@ -154,22 +257,10 @@ class DQNLearner(core.Learner, core.Saveable):
         if fb is not None:
             fb = (fb[:2 * B] if obs_dt == torch.uint8 and fb.shape[0] >= 2 * B
                   and fb.shape[1] == self._obs_flat else None)
-        upd = None
-        if self._dist is None and not self._staged:
-            # The priority write-back rides in the step (on the learner's second stream
-            # beside the backward) when the client's table offers it.
-            prep = getattr(self._replay_client, "prepare_priority_update", None)
-            if prep is not None:
-                upd = prep(adders.DEFAULT_PRIORITY_TABLE, keys)
-            self._native.step(*batch, obs_f16=fb, priority_update=upd, inputs_event=inputs_event)
-        else:
-            self._staged_step(batch, fb, inputs_event)
-        if self._replay_client is not None and upd is None:
-            # Gated on the step's skip word: a skipped step writes no priority.
-            kw = {"skip_word": self._skip_word} if self._skip_word else {}
-            self._replay_client.update_priorities(table=adders.DEFAULT_PRIORITY_TABLE,
-                                                  keys=keys,
-                                                  priorities=self._native.priorities[:B], **kw)
+        e = dict(batch=batch, fb=fb, keys=keys, B=B, inputs_event=inputs_event)
+        self._issue(e)
+        if self._reissue:
+            self._held.append(e)
         now = time.time()
         elapsed = now - self._timestamp if self._timestamp else 0
         self._timestamp = now
@@ -235,6 +326,7 @@ class DQNLearner(core.Learner, core.Saveable):
 
     # ------------------------------------------------------------------ variables
     def q_values(self, observations, use_target: bool = False) -> np.ndarray:
+        self._settle()
         obs_dt = torch.uint8 if self._network.obs_dtype == "uint8" else torch.float32
         x = torch.as_tensor(np.asarray(observations)).to(self._native.device, obs_dt)
         x = x.reshape(x.shape[0], -1).contiguous()
@@ -246,6 +338,7 @@ class DQNLearner(core.Learner, core.Saveable):
 
     def get_variables(self, names: List[str]) -> List[List[np.ndarray]]:
         # As the TF learner: one collection (the online trainable variables), names ignored.
+        self._settle()
         sonnet = self._network.to_sonnet(self._native.get_params("params"))
         return [[sonnet[k] for k in sorted(sonnet)]]
 
@@ -262,6 +355,7 @@ class DQNLearner(core.Learner, core.Saveable):
         return self.save()
 
     def save(self) -> Dict:
+        self._settle()
         n = self._native
         return {"network": n.get_params("params"), "target_network": n.get_params("target"),
                 # Adam's t: the updates applied (step() calls minus skipped steps).
@@ -273,6 +367,8 @@ class DQNLearner(core.Learner, core.Saveable):
                 "plane_scales": n.scale_state()}
 
     def restore(self, state: Dict):
+        self._settle()
+        self._held.clear()
         n = self._native
         n.set_params(state["network"], state["target_network"])
         for buf, src in ((n.m, state["optimizer"]["m"]), (n.v, state["optimizer"]["v"])):
@@ -284,3 +380,4 @@ class DQNLearner(core.Learner, core.Saveable):
             n.set_scale_state(state["plane_scales"])
         n.num_steps = int(state["num_steps"])
         n.applied_steps = int(state["optimizer"].get("step", state["num_steps"]))
+        self._checked = n.verdicts_issued

@@ -33,6 +33,11 @@ using gemm::Planes;
 using gemm::PlaneSrc;
 
 __device__ __forceinline__ uint32_t boff(int64_t elem) { return (uint32_t)(2 * elem); }
+// A operand offsets: f16 elements, or bytes when A is the uint8 frames (gemm_p3.h AU8).
+template <bool U8>
+__device__ __forceinline__ uint32_t aoff(int64_t elem) {
+  return U8 ? (uint32_t)elem : (uint32_t)(2 * elem);
+}
 
 using V8 = float[8];
 
@@ -77,10 +82,12 @@ __device__ __forceinline__ void relu_mask8(const CPlanes& x, int64_t e, V8& v) {
 }
 
 // ------------------------------------------------------------------ forward
-// NPA = 1: frames (the f16 copy of the uint8 values), result scaled by 1/255; NPA = 2:
-// f32 planes.
-template <class G, int NPA>
+// NPA = 1: frames (the f16 copy of the uint8 values, or with U8 the uint8 frames themselves,
+// widened exactly as they are staged), result scaled by 1/255; NPA = 2: f32 planes.
+template <class G, int NPA, bool U8 = false>
 struct P3ConvFwd {
+  static_assert(!U8 || NPA == 1, "uint8 frames are one plane");
+  static constexpr bool A_U8 = U8;
   static_assert(G::CI % 8 == 0 || (G::CI == 4 && G::KW % 2 == 0 && G::S % 2 == 0 &&
                                    G::PL % 2 == 0),
                 "8-k units need 8 channels, or 4-channel pixel pairs that never straddle "
@@ -95,6 +102,10 @@ struct P3ConvFwd {
   PlaneSrc b_src;        // W [K][CO]
   const float* bias;
   Planes y;              // [frames][OH][OW][CO]
+  // U8 image-resident fill (gemm_p3i.h): frames >= a_split come from a_src2 (numbered from
+  // 0 there), e.g. o_tm1 and o_t of a batch in two buffers.
+  PlaneSrc a_src2{};
+  int a_split = 1 << 30;
   __device__ gemm::PScale* amax_sc() const { return y.sc; }
   struct ARow {
     int pix;  // element offset of (frame, ih0, iw0)
@@ -122,7 +133,7 @@ struct P3ConvFwd {
     const int kw = r / G::CI, ci = r - kw * G::CI;
     const bool ok = a.ok && (unsigned)(a.ih0 + kh) < (unsigned)G::IH &&
                     (unsigned)(a.iw0 + kw) < (unsigned)G::IW;
-    return ok ? boff(a.pix + (kh * G::IW + kw) * G::CI + ci) : kOOB;
+    return ok ? aoff<U8>(a.pix + (kh * G::IW + kw) * G::CI + ci) : kOOB;
   }
   __device__ BRow b_row(int n) const { return BRow{n}; }
   __device__ uint32_t b_off(const BRow& b, int k0, int kk) const {
@@ -148,8 +159,10 @@ struct P3ConvFwd {
 };
 
 // ------------------------------------------------------------------ weight grad
-template <class G, int NPA>
+template <class G, int NPA, bool U8 = false>
 struct P3ConvWgrad {
+  static_assert(!U8 || NPA == 1, "uint8 frames are one plane");
+  static constexpr bool A_U8 = U8;
   static_assert(G::CI % 8 == 0 || (G::CI == 4 && G::KW % 2 == 0 && G::S % 2 == 0 &&
                                    G::PL % 2 == 0),
                 "see P3ConvFwd");
@@ -188,7 +201,7 @@ struct P3ConvWgrad {
     const int oh = r / G::OW, ow = r - oh * G::OW;
     const int ih = oh * G::S + a.dh, iw = ow * G::S + a.dw;
     const bool ok = a.ok && (unsigned)ih < (unsigned)G::IH && (unsigned)iw < (unsigned)G::IW;
-    return ok ? boff(((b * G::IPIX + ih * G::IW + iw) * G::CI) + a.ci) : kOOB;
+    return ok ? aoff<U8>(((b * G::IPIX + ih * G::IW + iw) * G::CI) + a.ci) : kOOB;
   }
   __device__ BRow b_row(int n) const { return BRow{n}; }
   __device__ uint32_t b_off(const BRow& b, int k0, int kk) const {

@@ -158,6 +158,8 @@ struct acme_dqn {
   bool single_stream = false;
   bool single_role = false;
   bool head_separate = false;  // ACME_V_HEADSEP=1: the online head as its own launch (tests)
+  // conv1 reads the batch's uint8 frames (ACME_V_F16FRAMES=1: an f16 copy, the round-4 path)
+  bool frames_u8 = true;
   // Step guard (kernels.h StepGuard): the skip-on-overflow rule of the plane engine, Adam's
   // device step count (applied updates) on every path.  seq counts the steps issued (the
   // target forward's flag slot is seq & 1); host_skipped is a pinned mirror of the skipped
@@ -165,6 +167,13 @@ struct acme_dqn {
   StepGuard* guard = nullptr;
   int64_t* host_skipped = nullptr;
   int64_t seq = 0;
+  // Step verdicts (re-issue of skipped steps, DQNLearner): every step's rescale publishes
+  // (verdict_seq << 1) | skip into the pinned ring host_verdicts[verdict_seq & 63], read by
+  // the host without a synchronisation; with `sticky`, a skip holds every later step skipped
+  // until a calibration clears it, so the host can re-issue the skipped steps in order.
+  uint32_t* host_verdicts = nullptr;
+  uint32_t verdict_seq = 0;
+  bool sticky = false;
   // Data parallelism: the ranks' skip decisions are combined through a padding word of the
   // torso gradient bucket (stage 1 publishes the local one; the all-reduce combines them).
   bool dp_gate = false;
@@ -187,6 +196,7 @@ enum {
   kScCount
 };
 constexpr int64_t kParamAmaxPeriod = 8;
+constexpr int kVerdictRing = 64;  // the pinned ring of step verdicts (acme_dqn_step_verdict)
 
 int add_tensor(acme_dqn* l, const char* name, std::initializer_list<int64_t> shape) {
   Tensor t;
@@ -526,6 +536,9 @@ RescaleJob step_rescale_job(acme_dqn* l, bool defer_r) {
   j.rg.mode = kRgStep;
   j.rg.gate = step_gate(l);
   j.rg.host_skipped = l->host_skipped;
+  j.rg.host_verdicts = l->host_verdicts;
+  j.rg.seq = l->verdict_seq++;
+  j.rg.sticky = l->sticky ? 1 : 0;
   return j;
 }
 
@@ -775,6 +788,7 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
   l->single_stream = tune_variant("SIDE") == 1;
   l->single_role = tune_variant("WSN") == 1;
   l->head_separate = tune_variant("HEADSEP") == 1;
+  l->frames_u8 = tune_variant("F16FRAMES") != 1;
   const int A = cfg->num_actions;
   const int B = cfg->max_batch;
   int rc = ACME_OK;
@@ -785,9 +799,12 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
   if ((rc = dev_alloc(l, &l->guard, 1)) != ACME_OK) return fail(rc);
   if (hipMemset(l->guard, 0, sizeof(StepGuard)) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void**>(&l->host_skipped), sizeof(int64_t),
+                    hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&l->host_verdicts), kVerdictRing * sizeof(uint32_t),
                     hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
     return fail((set_error("step guard allocation failed"), ACME_ERR_HIP));
   *l->host_skipped = 0;
+  for (int i = 0; i < kVerdictRing; ++i) l->host_verdicts[i] = 0xFFFFFFFFu;  // none decided
   if (cfg->network == ACME_NET_NATURE_DQN) {
     l->t_c1w = add_tensor(l, "atari_torso/conv2_d/w", {8, 8, 4, 32});
     l->t_c1b = add_tensor(l, "atari_torso/conv2_d/b", {32});
@@ -849,8 +866,8 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
         // critical path) the step time depended on the order the process created its
         // streams: two streams created before the learner's first step (a table's insert
         // path) left every main-stream kernel about 2x longer, 0.51 -> 1.10 ms per step
-        // (tools/insert_diag5.py); at the default priority 0.51 ms either way, and the same
-        // step time as the lowest priority otherwise (tools/ab_sprio.sh, round 4).
+        // (profiles/r04/tools/insert_diag5.py); at the default priority 0.51 ms either way, and the same
+        // step time as the lowest priority otherwise (profiles/r04/tools/ab_sprio.sh, round 4).
         hipError_t e = hipStreamCreateWithFlags(&l->side, hipStreamNonBlocking);
         for (auto& ev : l->ev)
           if (e == hipSuccess) e = make_order_event(&ev);
@@ -922,6 +939,7 @@ int acme_dqn_destroy(acme_dqn* l) {
     if (e) (void)hipEventDestroy(e);
   if (l->dp_stream) (void)hipStreamDestroy(l->dp_stream);
   if (l->host_skipped) (void)hipHostFree(l->host_skipped);
+  if (l->host_verdicts) (void)hipHostFree(l->host_verdicts);
   delete l;
   return ACME_OK;
 }
@@ -1021,6 +1039,26 @@ int acme_dqn_guard_state(acme_dqn* l, int64_t* out4) {
   out4[1] = g.skipped;
   out4[2] = g.last;
   out4[3] = g.qv;
+  return ACME_OK;
+}
+
+int acme_dqn_set_reissue(acme_dqn* l, int32_t enable) {
+  ACME_CHECK_ARG(l, "null learner");
+  l->sticky = enable != 0 && l->p3_capable;
+  return ACME_OK;
+}
+
+int64_t acme_dqn_verdicts_issued(const acme_dqn* l) { return l ? (int64_t)l->verdict_seq : 0; }
+
+int acme_dqn_step_verdict(const acme_dqn* l, int64_t seq, int32_t* state) {
+  ACME_CHECK_ARG(l && state && seq >= 0, "bad argument");
+  *state = -1;
+  if (!l->host_verdicts || seq >= (int64_t)l->verdict_seq) return ACME_OK;  // not issued
+  ACME_CHECK_ARG(seq + kVerdictRing >= (int64_t)l->verdict_seq,
+                 "verdict %lld is older than the ring's %d", (long long)seq, kVerdictRing);
+  const uint32_t v =
+      __atomic_load_n(l->host_verdicts + (seq & (kVerdictRing - 1)), __ATOMIC_ACQUIRE);
+  if ((v >> 1) == ((uint32_t)seq & 0x7fffffffu)) *state = (int32_t)(v & 1u);
   return ACME_OK;
 }
 
@@ -1232,7 +1270,8 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
       if (rc == ACME_OK && l->dp_gate && !l->calibrating) {
         Gate local = step_gate(l);
         local.dp = nullptr;
-        rc = launch_gate_publish(local, l->grads + l->dp_gate_index, st);
+        rc = launch_gate_publish(local, l->grads + l->dp_gate_index, st, l->scales,
+                                 kScTransient, kScT1, kScT3 + 1);
       }
       return rc;
     }
@@ -1256,8 +1295,15 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
   // target on o_t (q_t_value).
   l->last_p3 = nature && use_p3(l);
   if (l->last_p3) {
+    // conv1's input: the batch's uint8 frames themselves (conv1's kernels widen them exactly
+    // as they stage them: half the bytes of an f16 copy, and no copy), or an f16 copy (the
+    // dataset's obs_f16, else our own).
+    const bool u8 = !batch->obs_f16 && l->frames_u8 &&
+                    ((reinterpret_cast<uintptr_t>(batch->o_tm1) |
+                      reinterpret_cast<uintptr_t>(batch->o_t)) & 15) == 0;
     // The caller's inputs event can stand for the fork only if nothing is enqueued here first.
-    const bool quiet = !l->planes_stale && l->scales_ok && batch->obs_f16 && !l->calibrating;
+    const bool quiet =
+        !l->planes_stale && l->scales_ok && (batch->obs_f16 || u8) && !l->calibrating;
     if ((rc = sync_planes(l, st)) != ACME_OK) return rc;
     if (!l->scales_ok && !l->calibrating && (rc = calibrate_scales(l, batch, st)) != ACME_OK)
       return rc;
@@ -1267,12 +1313,14 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
     // conv1's input: an f16 copy of [o_tm1; o_t] on the main stream for everything.  (Reading
     // the batch's uint8 frames in the kernels instead measured slower beside the side stream,
     // 0.746 -> 0.750 ms per step: the uint8 image kernel is slower there than the 16-bit one.)
-    if (!batch->obs_f16 &&
+    if (!batch->obs_f16 && !u8 &&
         (rc = convert_frames(l, batch->o_tm1, batch->o_t, B, 2 * B, st)) != ACME_OK)
       return rc;
     // The dataset's fused gather may hand over the f16 copy (acme_replay_sample_gather_frames).
-    const torso::Frames fwd_frames{batch->obs_f16 ? static_cast<const void*>(batch->obs_f16)
-                                                   : static_cast<const void*>(l->frames)};
+    const torso::Frames fwd_frames =
+        u8 ? torso::Frames{batch->o_tm1, true, batch->o_t, B}
+           : torso::Frames{batch->obs_f16 ? static_cast<const void*>(batch->obs_f16)
+                                          : static_cast<const void*>(l->frames)};
     l->cur_frames = fwd_frames;
     // Target forward (q_t_value) on the side stream, beside the online forward.
     if (side) {
@@ -1466,11 +1514,14 @@ static int apply_impl(acme_dqn* l, bool copy, hipStream_t st) {
   if (copy) {
     l->target_dirty = true;
     ACME_PROF("target_copy", st, 0.0, 8.0 * (double)l->logical);
-    ACME_HIP_TRY(hipMemcpyAsync(l->target, l->params, l->flat * sizeof(float),
-                                hipMemcpyDeviceToDevice, st));
-    if (l->p3_capable)
-      ACME_HIP_TRY(hipMemcpyAsync(l->tpl, l->wpl, gemm::kPlanes * l->flat * sizeof(uint16_t),
+    if (l->p3_capable) {  // a skipped step copies nothing (gated on its verdict, as Adam)
+      if ((rc = launch_copy_gated(l->target, l->params, l->flat * sizeof(float), l->tpl, l->wpl,
+                                  gemm::kPlanes * l->flat * sizeof(uint16_t), gate, st)))
+        return rc;
+    } else {
+      ACME_HIP_TRY(hipMemcpyAsync(l->target, l->params, l->flat * sizeof(float),
                                   hipMemcpyDeviceToDevice, st));
+    }
   }
   if (l->p3_capable && l->num_steps % kParamAmaxPeriod == 0) {
     // The parameter planes' write scale from their maximum every kParamAmaxPeriod steps

@@ -171,6 +171,28 @@ __device__ __forceinline__ uint32_t f16x2_of_bytes(uint32_t x, int sh) {
   return f16_of_byte(x, sh) | (f16_of_byte(x, sh + 8) << 16);
 }
 
+// Problems whose A operand is the uint8 Atari frames themselves (`static constexpr bool
+// A_U8 = true`, byte offsets): a 16-B A unit (8 f16) is 8 frame bytes widened exactly, so
+// the frames are read from HBM once as bytes instead of as an f16 copy (half the bytes).
+template <class P, class = void>
+struct AU8 : std::false_type {};
+template <class P>
+struct AU8<P, std::void_t<decltype(P::A_U8)>> : std::integral_constant<bool, P::A_U8> {};
+__device__ __forceinline__ u32x4 f16x8_of_bytes(uint32_t lo, uint32_t hi) {
+  return u32x4{f16x2_of_bytes(lo, 0), f16x2_of_bytes(lo, 16), f16x2_of_bytes(hi, 0),
+               f16x2_of_bytes(hi, 16)};
+}
+// One 16-B A unit at byte offset `off` of plane descriptor r (kOOB: zeros).
+template <class P>
+__device__ __forceinline__ u32x4 load_a_unit(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  if constexpr (AU8<P>::value) {
+    const auto w = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+    return f16x8_of_bytes((uint32_t)w[0], (uint32_t)w[1]);
+  } else {
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+  }
+}
+
 // Maximum of two magnitudes (non-negative floats, or NaN) that keeps NaN: non-negative
 // floats order as their bits, and a NaN (sign cleared by fabsf) above infinity.  A plane
 // computed from overflowed planes is NaN, and its record must see that.
@@ -566,7 +588,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in, int
 #pragma unroll
       for (int pl = 0; pl < NPA; ++pl) {
         ra[set][i][pl] = (P3_EXP == 1 || P3_EXP >= 4) ? u32x4{off, (uint32_t)k0, 1u, 2u}
-                                     : __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srcA[pl], off, 0, 0));
+                                     : load_a_unit<P>(srcA[pl], off);
       }
     }
 #pragma unroll
@@ -764,6 +786,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3g_kernel(const P p_in, in
   using PB = typename C::PB;
   constexpr int NW = WM * WN, NPA = C::NPA, NPB = C::NPB, STAGE = C::STAGE;
   constexpr int PWA = (PA::BLOCKS + NW - 1) / NW, PWB = (PB::BLOCKS + NW - 1) / NW;
+  static_assert(!AU8<P>::value, "LDS-DMA copies bytes as they are: no uint8 A operand");
   constexpr int D = PWA * NPA + PWB * NPB;  // DMA instructions per wave per stage
   static_assert(STAGES >= 2 && STAGES <= 4, "2..4 LDS stages");
   static_assert((STAGES - 2) * D <= 63, "vmcnt range");
@@ -931,9 +954,7 @@ __global__ void __launch_bounds__(128 * WM * WN) gemm_p3ws_kernel(const P p_in, 
         const int kk = PA::kk_of(u);
         const uint32_t off = (PA::owns(u) && k0 + kk < kend) ? p.a_off(arow[i], k0, kk) : kOOB;
 #pragma unroll
-        for (int pl = 0; pl < NPA; ++pl)
-          ra[set][i][pl] =
-              __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srcA[pl], off, 0, 0));
+        for (int pl = 0; pl < NPA; ++pl) ra[set][i][pl] = load_a_unit<P>(srcA[pl], off);
       }
 #pragma unroll
       for (int i = 0; i < PB::PER_THREAD; ++i) {

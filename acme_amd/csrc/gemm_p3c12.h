@@ -21,9 +21,9 @@ namespace gemm {
 
 // conv1's epilogue sink: the frame's x1 image in LDS (both planes, x1's scale) and, when
 // `hbm`, the x1 planes in HBM (the same values as P3ConvFwd<G1, 1>::store8).
-template <class G1, class G2>
+template <class G1, class G2, bool U8 = false>
 struct P3C1ToLds {
-  using Base = conv::P3ConvFwd<G1, 1>;
+  using Base = conv::P3ConvFwd<G1, 1, U8>;
   using I2 = ImgGeom<G2, false>;
   static constexpr int A_MODE = Base::A_MODE, B_MODE = Base::B_MODE;
   static constexpr int A_PLANES = 1, B_PLANES = kPlanes;
@@ -55,14 +55,14 @@ struct P3C1ToLds {
   }
 };
 
-template <class G1, class G2>
+template <class G1, class G2, bool U8 = false>
 struct P3C12Cfg {
   using I1 = ImgGeomPairs<G1>;
   using I2 = ImgGeom<G2, false>;
-  using P1 = conv::P3ConvFwd<G1, 1>;
+  using P1 = conv::P3ConvFwd<G1, 1, U8>;
   using P2 = conv::P3ConvFwd<G2, kPlanes>;
   static constexpr int NP = kPlanes;
-  using P1L = P3C1ToLds<G1, G2>;
+  using P1L = P3C1ToLds<G1, G2, U8>;
   static constexpr int NT = 512, BK = 32, KS = 2;
   using C1 = P3Core<512, 32, 8, 1, BK, P1L>;  // 8 waves x 64 rows >= 441
   using C2 = P3Core<128, 64, 4, 2, BK, P2>;   // 4 x 2 waves of 32 x 32 (121 rows)
@@ -78,11 +78,11 @@ struct P3C12Cfg {
   static_assert(G1::OPIX <= 512 && I2::OPIX <= 128 && P2::A_PLANES == NP, "geometry");
 };
 
-template <class G1, class G2>
-__global__ void __launch_bounds__(512) gemm_p3c12_kernel(const conv::P3ConvFwd<G1, 1> p1,
+template <class G1, class G2, bool U8>
+__global__ void __launch_bounds__(512) gemm_p3c12_kernel(const conv::P3ConvFwd<G1, 1, U8> p1,
                                                          const conv::P3ConvFwd<G2, kPlanes> p2,
                                                          int frames, int hbm_frames) {
-  using Cfg = P3C12Cfg<G1, G2>;
+  using Cfg = P3C12Cfg<G1, G2, U8>;
   using I1 = typename Cfg::I1;
   using I2 = typename Cfg::I2;
   using PB1 = typename Cfg::PB1;
@@ -142,7 +142,28 @@ __global__ void __launch_bounds__(512) gemm_p3c12_kernel(const conv::P3ConvFwd<G
   fetch2(S1{}, BK);
 
   // ---- The frame image (f16 copy, pixel-pair units), each unit once; zero units.
-  {
+  if constexpr (AU8<P1>::value) {  // the uint8 frame itself, widened exactly (gemm_p3i.h)
+    constexpr int U8U = I1::UNITS / 2;
+    constexpr int PER = (U8U + NT - 1) / NT;
+    const __amdgpu_buffer_rsrc_t sa = plane_rsrc(p1.a_src, 0);
+    u32x4 v[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int u = tid + j * NT;
+      const uint32_t off = u < U8U ? (uint32_t)(((int64_t)f * U8U + u) * 16) : kOOB;
+      v[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(sa, off, 0, 0));
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int u = tid + j * NT;
+      if (u < U8U) {
+        *reinterpret_cast<u32x4*>(smem + I1::fill(0, 2 * u)) = f16x8_of_bytes(v[j][0], v[j][1]);
+        *reinterpret_cast<u32x4*>(smem + I1::fill(0, 2 * u + 1)) = f16x8_of_bytes(v[j][2], v[j][3]);
+      }
+    }
+    if (tid == 0) *reinterpret_cast<u32x4*>(smem + Cfg::FRAME - 16) = zero_u4();
+    if (tid < NP) *reinterpret_cast<u32x4*>(x1 + tid * Cfg::PLANE2 + Cfg::PLANE2 - 16) = zero_u4();
+  } else {
     constexpr int PER = (I1::UNITS + NT - 1) / NT;
     const __amdgpu_buffer_rsrc_t sa = plane_rsrc(p1.a_src, 0);
     u32x4 v[PER];
@@ -262,18 +283,18 @@ __global__ void __launch_bounds__(512) gemm_p3c12_kernel(const conv::P3ConvFwd<G
 }
 
 // frames images; x1 planes are written to HBM for frames [0, hbm_frames) only.
-template <class G1, class G2>
-inline hipError_t launch_gemm_p3c12(const conv::P3ConvFwd<G1, 1>& p1,
+template <class G1, class G2, bool U8>
+inline hipError_t launch_gemm_p3c12(const conv::P3ConvFwd<G1, 1, U8>& p1,
                                     const conv::P3ConvFwd<G2, kPlanes>& p2, int frames, int hbm_frames,
                                     hipStream_t st) {
-  using Cfg = P3C12Cfg<G1, G2>;
+  using Cfg = P3C12Cfg<G1, G2, U8>;
   static_assert(Cfg::LDS <= 160 * 1024, "LDS");
-  static hipError_t attr = p3_set_lds(&gemm_p3c12_kernel<G1, G2>, Cfg::LDS);
+  static hipError_t attr = p3_set_lds(&gemm_p3c12_kernel<G1, G2, U8>, Cfg::LDS);
   if (attr != hipSuccess) return attr;
   if (frames < 1 || p1.M != frames * G1::OPIX || p2.M != frames * G2::OPIX || p1.N > 32 ||
       p2.N > 64 || (p1.K / Cfg::BK) % 2 != 0 || (p2.K / Cfg::BK) % 2 != 0)
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL((gemm_p3c12_kernel<G1, G2>), dim3(frames), dim3(Cfg::NT), Cfg::LDS, st, p1, p2,
+  hipLaunchKernelGGL((gemm_p3c12_kernel<G1, G2, U8>), dim3(frames), dim3(Cfg::NT), Cfg::LDS, st, p1, p2,
                      frames, hbm_frames);
   return hipGetLastError();
 }

@@ -215,7 +215,32 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
   // ---- A: the block's frames, each unit of each plane loaded and stored once.
   constexpr int UB = 16;  // bytes per unit
   using UT = u32x4;
-  {
+  if constexpr (AU8<P>::value) {
+    // The uint8 frames themselves: a 16-B load holds two f16 units (units 2u, 2u + 1 of the
+    // same image row), widened exactly; frames from a_src, or from a_src2 past a_split.
+    static_assert(FPB == 1 && NPA == 1 && GI::UNITS % 2 == 0, "uint8 frames: one per block");
+    constexpr int U8U = GI::UNITS / 2;
+    constexpr int PER = (U8U + NT - 1) / NT;
+    const bool second = f0 >= p.a_split;
+    const __amdgpu_buffer_rsrc_t sa = plane_rsrc(second ? p.a_src2 : p.a_src, 0);
+    const int fl = second ? f0 - p.a_split : f0;
+    u32x4 v[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int u = tid + j * NT;
+      const uint32_t off = u < U8U ? (uint32_t)(((int64_t)fl * U8U + u) * 16) : kOOB;
+      v[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(sa, off, 0, 0));
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int u = tid + j * NT;
+      if (U8U % NT == 0 || u < U8U) {
+        *reinterpret_cast<u32x4*>(smem + GI::fill(0, 2 * u)) = f16x8_of_bytes(v[j][0], v[j][1]);
+        *reinterpret_cast<u32x4*>(smem + GI::fill(0, 2 * u + 1)) = f16x8_of_bytes(v[j][2], v[j][3]);
+      }
+    }
+    if (tid == 0) *reinterpret_cast<u32x4*>(smem + PLANE - 16) = zero_u4();
+  } else {
     constexpr int UNITS = FPB * GI::UNITS;
     constexpr int PER = (UNITS + NT - 1) / NT;
     __amdgpu_buffer_rsrc_t srcA[NPA];

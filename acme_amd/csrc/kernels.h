@@ -26,9 +26,13 @@ struct StepGuard {
   uint32_t last;     // the last step that ended was skipped (read after the step)
   uint32_t t[2];     // the target forward of step s overflowed: t[s & 1]
   uint32_t qv;       // the last q_values forward overflowed
-  uint32_t pad;
+  uint32_t hold;     // sticky skip (RescaleGuard::sticky): every later step skips until a
+                     // calibration clears it, so the host can re-issue the skipped steps in order
   int64_t applied;   // updates applied: Adam's t - 1
   int64_t skipped;   // steps skipped
+  uint32_t vseq;     // the last verdict: (seq << 1) | skip, one agent-scope store (the data
+                     // is its own flag: readers in the same launch spin on it)
+  uint32_t pad;
 };
 // What a gated kernel reads: skip = on | t[par] | (dp && *dp > 0), or `last` (use_last).
 struct Gate {
@@ -56,6 +60,11 @@ struct RescaleGuard {
   int mode = kRgNone;
   Gate gate{};                      // kRgStep: the step's gate
   int64_t* host_skipped = nullptr;  // kRgStep: pinned host mirror of g->skipped (optional)
+  // kRgStep: the verdict's sequence number (the host's count of issued verdicts), published
+  // as g->vseq and into the pinned ring host_verdicts[seq & 63] = (seq << 1) | skip (optional).
+  uint32_t seq = 0;
+  uint32_t* host_verdicts = nullptr;
+  int sticky = 0;  // kRgStep: a skip sets g->hold (every later step skips until cleared)
   // kRgStep: a one-launch LSTM's timeout words (tmo[0] this step, tmo[1] the count): a
   // timed-out step is skipped too, tmo[0] cleared and counted (optional).
   uint32_t* tmo = nullptr;
@@ -251,6 +260,10 @@ int launch_split_planes_lagged(const float* x, int64_t n, uint16_t* planes, int6
                                gemm::PScale* sc, hipStream_t st);
 // max |x| of n floats into the record's amax slots (the parameter planes' next scale).
 int launch_param_amax(const float* x, int64_t n, gemm::PScale* sc, hipStream_t st);
+// dst0 <- src0 and dst1 <- src1 (16-byte multiples) in one launch, unless the gate's step was
+// skipped (the DQN target copy: a skipped step copies nothing).
+int launch_copy_gated(void* dst0, const void* src0, size_t bytes0, void* dst1, const void* src1,
+                      size_t bytes1, const Gate& gate, hipStream_t st);
 // End-of-step rescale of a record array (kernels.hip plane_rescale_kernel): records
 // [0, n_transient) transient, [n_transient, n) persistent (rewritten by every Adam pass);
 // copy_to >= n, if >= 0, took a plane copy of copy_from's latest write.  Records in
@@ -272,7 +285,9 @@ int replay_update_priorities_gated(acme_replay* r, const uint64_t* keys, const d
                                    const RescaleJob* job = nullptr);
 // Data-parallel gate: *dst = the step's local skip (1.f or 0.f), a gradient word that the
 // ranks' all-reduce then combines (any rank's skip makes it > 0 on every rank).
-int launch_gate_publish(const Gate& gate, float* dst, hipStream_t st);
+int launch_gate_publish(const Gate& gate, float* dst, hipStream_t st,
+                        const gemm::PScale* s = nullptr, int n = 0, int skip_lo = -1,
+                        int skip_hi = -1);
 // uint8 frames -> exact f16 (one plane): out[f][e] = f16(frame f byte e) for rows frames
 // of `frame_bytes` (multiple of 8), frames [0, split) from a and the rest from b.
 int launch_frames_f16(const uint8_t* a, const uint8_t* b, int split, int rows, int frame_bytes,

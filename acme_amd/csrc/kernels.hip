@@ -892,7 +892,7 @@ __device__ __forceinline__ void adam_planes_check(gemm::PScale* psc, float mx, f
     gemm::amax_commit(psc, mx);
 }
 
-__device__ __forceinline__ void adam_tail(const AdamTail& t) {
+__device__ __forceinline__ void adam_tail(const AdamTail& t, const Gate& gate) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
   if (t.clear) {
     t.clear->on = 0u;
@@ -903,7 +903,9 @@ __device__ __forceinline__ void adam_tail(const AdamTail& t) {
   if (t.params) {
     const float wi = t.params->wi;
     t.params->r = t.params->rl = wi;
-    if (t.target) t.target->r = t.target->rl = wi;
+    // The target's planes take the parameters' at the step's copy, which a skipped step
+    // does not make (launch_copy_gated).
+    if (t.target && !gate_skip(gate)) t.target->r = t.target->rl = wi;
   }
 }
 
@@ -923,7 +925,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p,
                                                    int64_t pstride, gemm::PScale* __restrict__ psc,
                                                    const int64_t* __restrict__ dev_steps,
                                                    const Gate gate, const AdamTail tail) {
-  adam_tail(tail);
+  adam_tail(tail, gate);
   adam_bias_corrections(c, dev_steps);
   const bool skip = gate_skip(gate);
   const float pw = planes ? psc->w : 0.f;
@@ -952,7 +954,7 @@ __global__ void __launch_bounds__(256) adam_slabs_kernel(float* __restrict__ p,
                                                          gemm::PScale* __restrict__ psc,
                                                          const int64_t* __restrict__ dev_steps,
                                                          const Gate gate, const AdamTail tail) {
-  adam_tail(tail);
+  adam_tail(tail, gate);
   adam_bias_corrections(c, dev_steps);
   const bool skip = gate_skip(gate);
   const float pw = planes ? psc->w : 0.f;
@@ -994,6 +996,21 @@ __global__ void __launch_bounds__(256) adam_slabs_kernel(float* __restrict__ p,
 }
 
 __global__ void count_step_kernel(int64_t* c) { *c += 1; }
+
+// Two device copies (16-byte units) unless the gate's step was skipped.
+__global__ void __launch_bounds__(256) copy_gated_kernel(uint4* __restrict__ d0,
+                                                         const uint4* __restrict__ s0, int64_t n0,
+                                                         uint4* __restrict__ d1,
+                                                         const uint4* __restrict__ s1, int64_t n1,
+                                                         const Gate gate) {
+  if (gate_skip(gate)) return;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n0 + n1; i += stride) {
+    if (i < n0) d0[i] = s0[i];
+    else d1[i - n0] = s1[i - n0];
+  }
+}
+
 
 // Planes of x at the scale record's read scale (1 / r, set or kept by
 // plane_scale_set_kernel; exact for a power of two); no amax.
@@ -1079,8 +1096,24 @@ __global__ void __launch_bounds__(256) plane_rescale_kernel(const RescaleJob job
   rescale_block(job);
 }
 
-__global__ void gate_publish_kernel(const Gate gate, float* dst) {
-  *dst = gate_skip(gate) ? 1.f : 0.f;
+// This rank's skip decision into dst: its gate, the sticky hold, and the end-of-step
+// rescale's own test on the transient records [0, n) outside [skip_lo, skip_hi) (a tensor
+// that overflowed or underflowed its planes: rescale.h), so the ranks' all-reduced decision
+// is the one every rank's rescale would take.  One wave.
+__global__ void __launch_bounds__(64) gate_publish_kernel(const Gate gate, float* dst,
+                                                          const gemm::PScale* __restrict__ s,
+                                                          int n, int skip_lo, int skip_hi) {
+  const int lane = threadIdx.x;
+  bool bad = false;
+  for (int i = 0; i < n; ++i) {
+    if (i >= skip_lo && i < skip_hi) continue;
+    uint32_t a = s[i].slot[lane].v;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) a = max(a, (uint32_t)__shfl_xor((int)a, o, 64));
+    const float am = __builtin_bit_cast(float, a), aw = am * s[i].w;
+    bad = bad || (am != 0.f && (!(aw < 65520.f) || aw < 1.f));
+  }
+  if (lane == 0) *dst = (gate_skip(gate) || gate.g->hold != 0u || bad) ? 1.f : 0.f;
 }
 
 __global__ void __launch_bounds__(256) frames_f16_kernel(const uint8_t* __restrict__ a,
@@ -1583,9 +1616,26 @@ int launch_plane_rescale(gemm::PScale* recs, int n_transient, int n, int copy_fr
   return launch_rescale_job(job, st);
 }
 
-int launch_gate_publish(const Gate& gate, float* dst, hipStream_t st) {
-  ACME_CHECK_ARG(gate.g && dst, "null argument");
-  gate_publish_kernel<<<1, 1, 0, st>>>(gate, dst);
+int launch_copy_gated(void* dst0, const void* src0, size_t bytes0, void* dst1, const void* src1,
+                      size_t bytes1, const Gate& gate, hipStream_t st) {
+  if ((bytes0 | bytes1) % 16 != 0 ||
+      ((reinterpret_cast<uintptr_t>(dst0) | reinterpret_cast<uintptr_t>(src0) |
+        reinterpret_cast<uintptr_t>(dst1) | reinterpret_cast<uintptr_t>(src1)) & 15) != 0)
+    return (set_error("launch_copy_gated: 16-byte sizes and alignment"), ACME_ERR_INVALID);
+  const int64_t n0 = (int64_t)(bytes0 / 16), n1 = (int64_t)(bytes1 / 16);
+  if (n0 + n1 == 0) return ACME_OK;
+  const int64_t blocks = std::min<int64_t>(ceil_div(n0 + n1, 256), 2048);
+  copy_gated_kernel<<<(unsigned)blocks, 256, 0, st>>>(
+      static_cast<uint4*>(dst0), static_cast<const uint4*>(src0), n0, static_cast<uint4*>(dst1),
+      static_cast<const uint4*>(src1), n1, gate);
+  ACME_LAUNCH_CHECK();
+  return ACME_OK;
+}
+
+int launch_gate_publish(const Gate& gate, float* dst, hipStream_t st, const gemm::PScale* s,
+                        int n, int skip_lo, int skip_hi) {
+  ACME_CHECK_ARG(gate.g && dst && (n == 0 || s), "null argument");
+  gate_publish_kernel<<<1, 64, 0, st>>>(gate, dst, s, n, skip_lo, skip_hi);
   ACME_LAUNCH_CHECK();
   return ACME_OK;
 }

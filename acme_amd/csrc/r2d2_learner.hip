@@ -557,7 +557,7 @@ int network_forward(acme_r2d2* l, const float* prm, const acme_sequence_batch* b
     // the split-K reduction 63 -> 30 us, the step 5.16 -> 4.87 ms against 128x128 at split-K
     // 8 (two alternating pairs, round 4; DESIGN.md 4.1 on the per-CU intake).  Split-K 2:
     // 321 -> 301 us, the reduction 30 -> 20 us, the step 4.51 -> 4.44 ms; split-K 1 292 us
-    // but the step 4.46 ms (two alternating runs each, tools/ab_oars.sh).
+    // but the step 4.46 ms (two alternating runs each, profiles/r04/tools/ab_oars.sh).
     const int splits = kOarSplitsP3;
     p.M = R; p.N = N; p.K = F; p.k_chunk = chunk_for(F, splits);
     p.a_src = SRC(l->x3p, (int64_t)R * F); p.ldx = F;

@@ -598,20 +598,46 @@ struct FusedUpdateArgs {
   double* level[8];
   int nlevels;
   Gate gate;  // a learner step that was skipped writes no priority
-  RescaleJob job;  // job.s: run by one extra workgroup (blockIdx.x == kFusedUpdateBlocks)
+  // job.s: the learner step's rescale, run by workgroup 0 (the update workgroups are 1..G).
+  // With a step verdict (kRgStep) the update workgroups wait for it (StepGuard::vseq) and
+  // write nothing when the step was skipped, for every reason the rescale decides
+  // (overflow, underflow, a timed-out unroll, the sticky hold, another rank's skip).
+  RescaleJob job;
 };
+// Waits (bounded) for the verdict with sequence number seq; true when that step is skipped
+// (or the wait timed out: no priority is written).  Workgroup 0 of the same launch publishes
+// it and was dispatched first, so it is resident or done.
+__device__ __forceinline__ bool wait_verdict_skip(const StepGuard* g, uint32_t seq) {
+  __shared__ uint32_t s_v;
+  if (threadIdx.x == 0) {
+    uint32_t v = 0;
+    for (int it = 0; it < (1 << 22); ++it) {
+      v = __hip_atomic_load(&g->vseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((v >> 1) == (seq & 0x7fffffffu)) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    s_v = (v >> 1) == (seq & 0x7fffffffu) ? (v & 1u) : 1u;
+  }
+  __syncthreads();
+  return s_v != 0u;
+}
 __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs a) {
   __shared__ int s_j[kFusedUpdateMax];
   __shared__ int64_t s_slot[kFusedUpdateMax];
   __shared__ int s_len;
-  if ((int)blockIdx.x >= kFusedUpdateBlocks) {
+  const int first = a.job.s ? 1 : 0;
+  if (a.job.s && blockIdx.x == 0) {
     rescale_block(a.job);
     return;
   }
-  if (gate_skip(a.gate)) return;
+  if (a.job.s && a.job.rg.g && a.job.rg.mode == kRgStep) {
+    if (wait_verdict_skip(a.job.rg.g, a.job.rg.seq)) return;
+  } else if (gate_skip(a.gate)) {
+    return;
+  }
   const int tid = threadIdx.x, nt = blockDim.x;
   const int lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
-  const int G = kFusedUpdateBlocks, bid = blockIdx.x;
+  const int G = kFusedUpdateBlocks, bid = (int)blockIdx.x - first;
   const int h = a.nlevels >= 2 ? a.nlevels - 2 : 0;
   if (tid == 0) s_len = 0;
   __syncthreads();
@@ -1668,10 +1694,16 @@ int acme::replay_update_priorities_gated(acme_replay* r, const uint64_t* keys,
                                          hipStream_t st, const RescaleJob* job) {
   ACME_CHECK_ARG(r && (n == 0 || (keys && prios)), "null argument");
   ACME_CHECK_ARG(n >= 0 && n < (int64_t(1) << 31), "bad update count");
+  Gate eff = gate;
   if (n == 0 || n > kFusedUpdateMax) {  // the job as its own launch
     if (job && job->s) {
       const int rc = launch_rescale_job(*job, st);
       if (rc != ACME_OK) return rc;
+      if (job->rg.g && job->rg.mode == kRgStep) {  // its verdict, as Adam reads it
+        eff = Gate{};
+        eff.g = job->rg.g;
+        eff.use_last = 1;
+      }
     }
     if (n == 0) return ACME_OK;
   }
@@ -1717,7 +1749,7 @@ int acme::replay_update_priorities_gated(acme_replay* r, const uint64_t* keys,
                                          r->winner);
   ACME_LAUNCH_CHECK();
   prio_write_kernel<<<g, 256, 0, st>>>(prios, n, t_slots, t_valid, r->winner, alpha,
-                                       r->raw_prio, r->levels[0], gate);
+                                       r->raw_prio, r->levels[0], eff);
   ACME_LAUNCH_CHECK();
   for (int l = 1; l < r->nlevels; ++l) {
     level_update_kernel<<<(unsigned)ceil_div(n, 4), 256, 0, st>>>(

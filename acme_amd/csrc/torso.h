@@ -64,14 +64,22 @@ struct PActs {
   Plane x1, x2, x3;
 };
 int64_t wgrad_slab_floats_p3();
-// conv1's input: the f16 copy of the uint8 frames (launch_frames_f16), rows of 84*84*4.
+// conv1's input, rows of 84*84*4: the f16 copy of the uint8 frames (launch_frames_f16), or
+// with u8 the uint8 frames themselves (widened exactly where conv1's kernels stage them),
+// rows [0, split) at p and the rest at p2 (a batch's o_tm1 and o_t in two buffers).
 struct Frames {
   const void* p;
+  bool u8 = false;
+  const void* p2 = nullptr;
+  int split = 1 << 30;
   Frames rows_from(int r) const {
-    return Frames{static_cast<const uint8_t*>(p) + (size_t)r * kObsBytes * 2};
+    if (!u8) return Frames{static_cast<const uint8_t*>(p) + (size_t)r * kObsBytes * 2};
+    if (r >= split)
+      return Frames{static_cast<const uint8_t*>(p2) + (size_t)(r - split) * kObsBytes, true};
+    return Frames{static_cast<const uint8_t*>(p) + (size_t)r * kObsBytes, true, p2, split - r};
   }
 };
-// frames: f16 copies of the uint8 frames [rows][84*84*4] (launch_frames_f16).
+// frames: f16 copies of the uint8 frames [rows][84*84*4] (launch_frames_f16), or u8 frames.
 // keep_x1: frames [0, keep_x1) get their conv1 output x1 in HBM (the backward reads it);
 // -1: all.  With the fused conv1 -> conv2 kernel (gemm_p3c12.h, used when
 // keep_x1 == 0) x1 only lives in LDS.

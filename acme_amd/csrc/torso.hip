@@ -189,7 +189,71 @@ inline PlaneSrc src(const Plane& x, int64_t elems) {
 }
 inline PlaneSrc frames_src(const Frames& f, int rows) {
   return PlaneSrc{static_cast<const uint16_t*>(f.p), 0,
-                  (int32_t)(2 * (int64_t)rows * G1::IPIX * G1::CI)};
+                  (int32_t)((f.u8 ? 1 : 2) * (int64_t)rows * G1::IPIX * G1::CI)};
+}
+
+// conv1 forward (image-resident) over `rows` frames into y, f16 or uint8 frames.
+template <bool U8>
+int conv1_fwd_p3(const PWeights& w, const Frames& frames, int rows, const Planes& y,
+                 hipStream_t st) {
+  P3ConvFwd<G1, 1, U8> p;
+  p.M = rows * G1::OPIX; p.N = G1::CO; p.K = G1::K; p.k_chunk = G1::K;
+  const int n1 = U8 ? std::min(rows, frames.split) : rows;
+  p.a_src = frames_src(frames, n1); p.b_src = src(w.w1, G1::K * G1::CO);
+  if (U8 && n1 < rows) {
+    p.a_src2 = frames_src(frames.rows_from(n1), rows - n1);
+    p.a_split = n1;
+  }
+  p.bias = w.b1; p.y = y;
+  // Image-resident frames (gemm_p3i.h pixel pairs): 39.6 -> 33.7 us vs the best im2col
+  // tiling.
+  P3I_GEMM("conv1_fwd", I1F, 1, 32, 7, 1, 2, p, rows);
+  return ACME_OK;
+}
+
+// The fused conv1 -> conv2 forward (gemm_p3c12.h) over frames [nsep, rows).
+template <bool U8>
+int conv12_fwd_p3(const PWeights& w, const Frames& frames, int rows, int nsep, const PActs& a,
+                  hipStream_t st) {
+  const int nf = rows - nsep;
+  const Frames fr = frames.rows_from(nsep);
+  if (U8 && fr.split < nf)
+    return (set_error("the fused conv1 -> conv2 forward reads its frames from one buffer"),
+            ACME_ERR_INVALID);
+  P3ConvFwd<G1, 1, U8> p1;
+  p1.M = nf * G1::OPIX; p1.N = G1::CO; p1.K = G1::K; p1.k_chunk = G1::K;
+  p1.a_src = frames_src(fr, nf); p1.b_src = src(w.w1, G1::K * G1::CO);
+  p1.bias = w.b1;
+  p1.y = Planes{a.x1.p + (int64_t)nsep * kX1, a.x1.stride, a.x1.sc};
+  P3ConvFwd<G2, gemm::kPlanes> p2;
+  p2.M = nf * G2::OPIX; p2.N = G2::CO; p2.K = G2::K; p2.k_chunk = G2::K;
+  p2.a_src = src(a.x1, (int64_t)rows * kX1); p2.b_src = src(w.w2, G2::K * G2::CO);
+  p2.bias = w.b2;
+  p2.y = Planes{a.x2.p + (int64_t)nsep * kFlat, a.x2.stride, a.x2.sc};
+  const double fl = 2.0 * p1.M * p1.N * (double)p1.K + 2.0 * p2.M * p2.N * (double)p2.K;
+  ACME_PROF_PEAK("conv12_fwd", st, fl, 0.0, gemm::p3_peak_tflops<decltype(p2)>());
+  hipError_t e = gemm::launch_gemm_p3c12(p1, p2, nf, 0, st);
+  if (e != hipSuccess) return (set_error("gemm launch failed: %s", hipGetErrorString(e)), ACME_ERR_HIP);
+  return ACME_OK;
+}
+
+// conv1's weight + bias gradient (split-K slabs) from the frames of rows [0, rows).
+template <bool U8>
+int conv1_wgrad_p3(const Frames& frames, int rows, const Plane& dz1, float* slab, int splits,
+                   bool single_role, P3ConvWgrad<G1, 1, U8>& p, hipStream_t st) {
+  if (U8 && frames.split < rows)
+    return (set_error("conv1's weight gradient reads its frames from one buffer"),
+            ACME_ERR_INVALID);
+  P3ConvWgrad<G1, 1, U8> q;
+  q.M = G1::K; q.N = G1::CO; q.K = rows * G1::OPIX;
+  q.k_chunk = chunk_for(q.K, splits);
+  q.a_src = frames_src(frames, rows); q.b_src = src(dz1, (int64_t)rows * kX1);
+  q.slab = slab;
+  // Producer / consumer waves (gemm_p3ws_kernel): 28.5 -> 25.0 us, the same bits.
+  if (single_role) P3_GEMM("conv1_wgrad", 256, 32, 4, 1, 32, q, splits);
+  else P3WS_GEMM("conv1_wgrad", 256, 32, 4, 1, q, splits);
+  p = q;
+  return ACME_OK;
 }
 
 template <class P>
@@ -217,33 +281,14 @@ int forward_p3(const PWeights& w, const Frames& frames, int rows, const PActs& a
   // o_t rows (x1 kept for the o_tm1 rows only) measured 0.545 -> 0.603 ms per step with
   // the f16 planes (the fused kernel's one block per CU beside the other stream).
   const int nsep = keep_x1 == 0 ? 0 : rows;
-  if (nsep < rows) {
-    const int nf = rows - nsep;
-    const Frames fr = frames.rows_from(nsep);
-    P3ConvFwd<G1, 1> p1;
-    p1.M = nf * G1::OPIX; p1.N = G1::CO; p1.K = G1::K; p1.k_chunk = G1::K;
-    p1.a_src = frames_src(fr, nf); p1.b_src = src(w.w1, G1::K * G1::CO);
-    p1.bias = w.b1;
-    p1.y = Planes{a.x1.p + (int64_t)nsep * kX1, a.x1.stride, a.x1.sc};
-    P3ConvFwd<G2, gemm::kPlanes> p2;
-    p2.M = nf * G2::OPIX; p2.N = G2::CO; p2.K = G2::K; p2.k_chunk = G2::K;
-    p2.a_src = src(a.x1, (int64_t)rows * kX1); p2.b_src = src(w.w2, G2::K * G2::CO);
-    p2.bias = w.b2;
-    p2.y = Planes{a.x2.p + (int64_t)nsep * kFlat, a.x2.stride, a.x2.sc};
-    const double fl = 2.0 * p1.M * p1.N * (double)p1.K + 2.0 * p2.M * p2.N * (double)p2.K;
-    ACME_PROF_PEAK("conv12_fwd", st, fl, 0.0, gemm::p3_peak_tflops<decltype(p2)>());
-    hipError_t e = gemm::launch_gemm_p3c12(p1, p2, nf, 0, st);
-    if (e != hipSuccess) return (set_error("gemm launch failed: %s", hipGetErrorString(e)), ACME_ERR_HIP);
-  }
-  if (nsep > 0) {
-    P3ConvFwd<G1, 1> p;
-    p.M = nsep * G1::OPIX; p.N = G1::CO; p.K = G1::K; p.k_chunk = G1::K;
-    p.a_src = frames_src(frames, nsep); p.b_src = src(w.w1, G1::K * G1::CO);
-    p.bias = w.b1; p.y = pl(a.x1);
-    // Image-resident frames (gemm_p3i.h pixel pairs): 39.6 -> 33.7 us vs the best im2col
-    // tiling.
-    P3I_GEMM("conv1_fwd", I1F, 1, 32, 7, 1, 2, p, nsep);
-  }
+  int rc;
+  if (nsep < rows &&
+      (rc = frames.u8 ? conv12_fwd_p3<true>(w, frames, rows, nsep, a, st)
+                      : conv12_fwd_p3<false>(w, frames, rows, nsep, a, st)) != ACME_OK)
+    return rc;
+  if (nsep > 0 && (rc = frames.u8 ? conv1_fwd_p3<true>(w, frames, nsep, pl(a.x1), st)
+                                  : conv1_fwd_p3<false>(w, frames, nsep, pl(a.x1), st)) != ACME_OK)
+    return rc;
   if (nsep > 0) {
     P3ConvFwd<G2, gemm::kPlanes> p;
     p.M = nsep * G2::OPIX; p.N = G2::CO; p.K = G2::K; p.k_chunk = G2::K;
@@ -340,18 +385,26 @@ int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int row
     if (e != hipSuccess) return (set_error("gemm launch failed: %s", hipGetErrorString(e)), ACME_ERR_HIP);
   }
   {  // conv1 (no input gradient)
-    P3ConvWgrad<G1, 1> p;
-    p.M = G1::K; p.N = G1::CO; p.K = rows * G1::OPIX;
     const int splits = kP3Conv1WgradSplits;
-    p.k_chunk = chunk_for(p.K, splits);
-    p.a_src = frames_src(frames, rows); p.b_src = src(dz1, (int64_t)rows * kX1);
-    p.slab = slab;
-    // Producer / consumer waves (gemm_p3ws_kernel): 28.5 -> 25.0 us, the same bits.
-    if (sd.single_role) P3_GEMM("conv1_wgrad", 256, 32, 4, 1, 32, p, splits);
-    else P3WS_GEMM("conv1_wgrad", 256, 32, 4, 1, p, splits);
-    if (defer) sd.defer[0] = WgradSlab{slab, splits, (int64_t)p.M * p.N, p.N};
-    else if ((rc = p3_wgrad_reduce(p, splits, slab, g.w1, g.b1, "conv1_wgrad_reduce", st)))
-      return rc;
+    int64_t wcount;
+    int M1, N1;
+    if (frames.u8) {
+      P3ConvWgrad<G1, 1, true> p;
+      if ((rc = conv1_wgrad_p3<true>(frames, rows, dz1, slab, splits, sd.single_role, p, st)))
+        return rc;
+      M1 = p.M, N1 = p.N;
+      if (!defer && (rc = p3_wgrad_reduce(p, splits, slab, g.w1, g.b1, "conv1_wgrad_reduce", st)))
+        return rc;
+    } else {
+      P3ConvWgrad<G1, 1> p;
+      if ((rc = conv1_wgrad_p3<false>(frames, rows, dz1, slab, splits, sd.single_role, p, st)))
+        return rc;
+      M1 = p.M, N1 = p.N;
+      if (!defer && (rc = p3_wgrad_reduce(p, splits, slab, g.w1, g.b1, "conv1_wgrad_reduce", st)))
+        return rc;
+    }
+    wcount = (int64_t)M1 * N1;
+    if (defer) sd.defer[0] = WgradSlab{slab, splits, wcount, N1};
   }
   if (sd.tail && (rc = sd.tail(sd.tail_ctx, st_main)) != ACME_OK) return rc;
   if (fork) ACME_HIP_TRY(hipStreamWaitEvent(st_main, sd.e[2], 0));  // join

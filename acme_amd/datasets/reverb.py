@@ -266,7 +266,10 @@ class _TableIterator:
         fields are the two observations (fields 0 and 4); a shard's copy holds its share."""
         if isinstance(self._t, (replay.FrameTable, replay.QueueTable)):
             return False
-        if os.environ.get("ACME_DATASET_BF16", "1") == "0":  # A/B switch: learner converts
+        # Off by default since round 5: the DQN learner's conv1 reads the batch's uint8 frames
+        # directly (half the bytes, and no 57.8 MB copy per B = 512 batch); ACME_DATASET_F16=1
+        # brings back the copy (the round-4 path; bit-identical steps, tests/test_dp.py).
+        if os.environ.get("ACME_DATASET_F16", "0") != "1":
             return False
         f = self._t.fields
         big = [i for i, x in enumerate(f) if x.row_bytes >= 1024]

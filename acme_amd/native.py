@@ -464,6 +464,24 @@ class NativeDQN:
         check(lib().acme_dqn_skip_word(self._h, ctypes.byref(p)), "dqn skip_word")
         return p.value
 
+    # ---- re-issue of skipped steps (acme_dqn_set_reissue / _verdicts_issued / _step_verdict)
+    def set_reissue(self, enable: bool) -> None:
+        """A skipped step holds every later step skipped until the next calibration, so the
+        caller can re-issue the held batches in order (DQNLearner)."""
+        check(lib().acme_dqn_set_reissue(self._h, 1 if enable else 0), "dqn set_reissue")
+
+    @property
+    def verdicts_issued(self) -> int:
+        """Step verdicts issued so far (the next step's verdict has this sequence number)."""
+        return int(lib().acme_dqn_verdicts_issued(self._h))
+
+    def step_verdict(self, seq: int) -> Optional[bool]:
+        """None while verdict `seq` is undecided, else whether that step was skipped (no
+        synchronisation: a pinned ring the device writes)."""
+        v = ctypes.c_int32(-1)
+        check(lib().acme_dqn_step_verdict(self._h, int(seq), ctypes.byref(v)), "dqn step_verdict")
+        return None if v.value < 0 else bool(v.value)
+
     def set_data_parallel_gate(self, enable: bool) -> None:
         check(lib().acme_dqn_set_data_parallel_gate(self._h, 1 if enable else 0), "dqn dp gate")
 

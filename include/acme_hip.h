@@ -355,6 +355,18 @@ int acme_dqn_guard_state(acme_dqn* l, int64_t* out4);
 int acme_dqn_set_applied_steps(acme_dqn* l, int64_t n);
 int acme_dqn_skip_word(const acme_dqn* l, const uint32_t** out);
 int acme_dqn_set_data_parallel_gate(acme_dqn* l, int32_t enable);
+/* Re-issue of skipped steps (DQNLearner.step: every call applies one update, as
+ * acme/agents/tf/dqn/learning.py:147-161 does).  Every step's verdict gets a sequence number
+ * (acme_dqn_verdicts_issued: how many were issued so far) and is published by the device
+ * into a pinned 64-entry ring; acme_dqn_step_verdict reads verdict `seq` without a
+ * synchronisation: *state = -1 not decided yet, 0 applied, 1 skipped.
+ * acme_dqn_set_reissue(l, 1): a skipped step holds every later step skipped (nothing they
+ * compute from the un-updated parameters is applied) until the next calibration
+ * (acme_dqn_params_changed), so the caller can re-issue the held batches in order; a target
+ * copy due on a skipped step is not made (the re-issued step makes it). */
+int acme_dqn_set_reissue(acme_dqn* l, int32_t enable);
+int64_t acme_dqn_verdicts_issued(const acme_dqn* l);
+int acme_dqn_step_verdict(const acme_dqn* l, int64_t seq, int32_t* state);
 /* The plane scales (powers of two) as learner state for checkpoints: acme_dqn_scale_state
  * writes *count floats to out (when out is non-NULL and capacity suffices);
  * acme_dqn_set_scale_state restores them after acme_dqn_params_changed, so the resumed

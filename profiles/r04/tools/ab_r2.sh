@@ -1,5 +1,5 @@
 # A/B of tune variants on the DQN step: alternating step-time runs, then one profiled run each.
-# Usage: bash tools/ab_r2.sh "base HEAD=2,ADAMNT=1 ..." [rounds]
+# Usage: bash profiles/r04/tools/ab_r2.sh "base HEAD=2,ADAMNT=1 ..." [rounds]
 set -e
 mkdir -p gpurun_out/ab
 V=${1:-"base HEAD=2,ADAMNT=1"}

@@ -10,4 +10,4 @@ if [ $rc -ne 0 ]; then grep -E "^(FAILED|ERROR)" $B/gpu.log | head; exit $rc; fi
 bash tools/profile_round.sh dqn || exit $?
 f=$(find gpurun_out/prof_dqn -name '*kernel_stats.csv' | head -1); cp "$f" $B/rocprof_dqn_kernel_stats.csv
 find gpurun_out/prof_dqn -name '*kernel_trace.csv' -delete
-bash tools/r04_bench.sh
+bash profiles/r04/tools/r04_bench.sh

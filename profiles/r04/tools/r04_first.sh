@@ -3,4 +3,4 @@ set -e
 mkdir -p gpurun_out/r04a
 timeout -k 10 240 python3 bench.py --workload impala_actors --steps 300 --warmup 20 > gpurun_out/r04a/bench_impala_actors.json 2> gpurun_out/r04a/impala_actors.log
 cat gpurun_out/r04a/bench_impala_actors.json
-AB="base ONFIRST=1" bash tools/short_ab.sh
+AB="base ONFIRST=1" bash profiles/r04/tools/short_ab.sh

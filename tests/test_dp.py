@@ -319,8 +319,8 @@ def test_sharded_global_sampling_gpu(prefetch):
 
 def _nature_dp_worker(rank, world, port, q):
     """One rank of a Nature-CNN DP learner on a uint8 shard, run twice from the same state:
-    with the dataset's fused f16 frame copy (acme_replay_sample_share_frames) and with the
-    learner converting the frames itself (ACME_DATASET_BF16=0)."""
+    with the dataset's fused f16 frame copy (acme_replay_sample_share_frames,
+    ACME_DATASET_F16=1) and with the learner's conv1 reading the uint8 frames (the default)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -340,7 +340,7 @@ def _nature_dp_worker(rank, world, port, q):
     prios = rng.uniform(0.5, 1.5, 48) * (1.0 if rank == 0 else 3.0)
     out, copies = [], []
     for flag in ("1", "0"):
-        os.environ["ACME_DATASET_BF16"] = flag
+        os.environ["ACME_DATASET_F16"] = flag
         table = replay.Table(adders.DEFAULT_PRIORITY_TABLE, replay.selectors.Prioritized(0.6),
                              replay.selectors.Fifo(), 48, replay.rate_limiters.MinSize(1),
                              signature=adders.NStepTransitionAdder.signature(spec),
@@ -358,7 +358,7 @@ def _nature_dp_worker(rank, world, port, q):
         torch.cuda.synchronize()
         copies.append(getattr(learner._iterator, "last_frames_f16", None) is not None)
         out.append((learner.native.params.cpu().numpy(), learner.native.loss.item()))
-    os.environ.pop("ACME_DATASET_BF16")
+    os.environ.pop("ACME_DATASET_F16")
     q.put((rank, out, copies))
     dist.destroy_process_group()
 
@@ -367,7 +367,8 @@ def _nature_dp_worker(rank, world, port, q):
 def test_dp_nature_f16_frame_copy_gpu():
     """Sharded uint8 tables: the fused sample + gather + f16 copy of each rank's share feeds
     the DP learner's forward (rows [0, n) and [n, 2n) of the copy for a share of n rows);
-    the steps are bit-identical to the learner's own conversion, and replicas agree."""
+    the steps are bit-identical to the learner's conv1 reading the uint8 frames, and
+    replicas agree."""
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

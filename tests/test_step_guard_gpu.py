@@ -15,11 +15,17 @@ sets the next step's scales from the skipped step's true maxima.
     bar, Adam at t = 2: the skipped step did not count).
   * test_long_horizon_drift: 100 free-running steps at B = 64 (and 20 at the headline
     B = 512) from identical batches on the plane engine, on the exact-f32 engine
-    (acme_set_matmul_engine(ACME_MATMUL_F32)) and on the float64 torch restatement
-    (oracle/dqn_torch.py on the GPU, the reference trajectory).  The plane engine skips no
-    step, and its drift from the f64 trajectory (parameters, relative to how far training
-    moved them; the loss trajectory) stays within the f32 engine's own drift (x2, plus a
-    floor at f32 rounding).
+    (acme_set_matmul_engine(ACME_MATMUL_F32)), on torch float32 and on the float64 torch
+    restatement (oracle/dqn_torch.py on the GPU, the reference trajectory).  The plane
+    engine skips no step, and its divergence from the f64 trajectory (parameters, relative
+    to how far training moved them; the loss trajectory's maximum and median relative
+    error) is within 2x the worse float32 implementation's (PLANE_FACTOR).
+  * test_underflow_only_skip_writes_no_priority / test_skipped_step_makes_no_target_copy:
+    a skip decided by the rescale alone writes no priority on the fused path; a target copy
+    due on a skipped step is not made.
+  * test_learner_reissues_skipped_step: DQNLearner re-issues a skipped step (and the step
+    held after it) so every step() applies one update, bit-identical to a learner that never
+    skipped.
   * test_impala_timeout_skips_update: an LSTM unroll timeout (the timeout word set before the
     step) leaves parameters, moments and Adam's count unchanged and raises the skip count.
 
@@ -38,13 +44,14 @@ from oracle import dqn_oracle as O
 pytestmark = pytest.mark.gpu
 
 HEAD = ("duelling_q_network/mlp/linear_1/w", "duelling_q_network/mlp_1/linear_1/w")
-# Free-running drift from the f64 trajectory relative to the exact-f32 engine's.  A plane
-# product drops the l*l term (<= 2^-22 of the product) where the f32 MFMA rounds at 2^-24,
-# so the plane engine's per-step error is up to ~4x the f32 engine's, and free-running
-# trajectories (chaotic: Adam's normalised steps flip on near-zero gradients) leave the f64
-# one earlier.  Measured at B = 64 x 100 steps: 0.152 against 0.065 (round 4).  A build
-# with -DP3_FOUR_TERMS=1 adds the l*l term (+5% step time).
-PLANE_DRIFT_FACTOR = 4.0
+# Free-running divergence from the f64 trajectory (parameters, loss maximum and median)
+# relative to the worse of two float32 implementations (the exact-f32 engine, torch
+# float32).  Measured (round 5, profiles/r05/drift/): B = 64 x 100: drift plane 0.152,
+# f32 engine 0.065, torch f32 0.160; loss max 0.749 / 0.062 / 0.749, median 0.064 / 0.0035 /
+# 0.053.  B = 512 x 20: drift 0.060 / 0.063 / 0.065, loss max 0.251 / 0.250 / 0.250.  A
+# build with -DP3_FOUR_TERMS=1 (the l*l term) leaves these unchanged (0.154 drift, 0.749 /
+# 0.063 loss at B = 64) and costs 5 % step time, so three terms stay.
+PLANE_FACTOR = 2.0
 
 
 def _dev(batch):
@@ -148,6 +155,165 @@ def test_overflow_skips_step_and_recovers():
         np.testing.assert_allclose(got[k], want, rtol=1e-6, atol=1e-9, err_msg=k)
 
 
+def _head_scaled_params(net, scale=1e-4):
+    p0, t0 = net.init(1), net.init(2)
+    for k in HEAD:  # q ~ scale: |TD| ~ scale when r = d = 0
+        p0[k] = p0[k] * scale
+        t0[k] = t0[k] * scale
+    return p0, t0
+
+
+def test_underflow_only_skip_writes_no_priority():
+    """A step whose only fault is an underflow (a tensor's maximum fell more than ~2^7-fold
+    below its scale, so its planes carry too few bits) is skipped by the end-of-step
+    rescale, and the priority write-back fused into the same launch (acme_dqn_step_update)
+    must follow that verdict: no priority of the batch is written."""
+    from acme_amd.native import NativeDQN, NativeReplay
+    from acme_amd.networks import DQNAtariNetwork
+    B = 64
+    p0, t0 = _head_scaled_params(DQNAtariNetwork(18))
+    # A small learning rate keeps q ~ 1e-4 after the first update (Adam moves every
+    # parameter by about lr), so the second batch's |TD| stays ~1e-4.
+    d = NativeDQN(network="nature", num_actions=18, max_batch=B, obs_dtype="uint8",
+                  learning_rate=1e-7)
+    d.set_params(p0, t0)
+    table = NativeReplay(1000, [4], prioritized=True, priority_exponent=0.6, seed=5)
+    rows = np.arange(600, dtype=np.uint32).view(np.uint8).reshape(600, 4)
+    table.insert([rows], np.linspace(0.5, 2.0, 600))
+    rng = np.random.default_rng(4)
+    large = _batch(rng, B, 18, r=1.0, d=0.0)   # |TD| ~ 1
+    small = _batch(rng, B, 18, r=0.0, d=0.0)   # |TD| ~ 1e-4: the head dZ shrinks ~2^13-fold
+    d.step(*_dev(large), priority_update=(table.handle, table.sample(B, 0)["keys"]))
+    torch.cuda.synchronize()
+    assert d.guard_state()["applied"] == 1
+    raw1 = table.export_state()["raw_priorities"].copy()
+    state1 = {buf: d.get_params(buf) for buf in ("params", "m", "v")}
+    d.step(*_dev(small), priority_update=(table.handle, table.sample(B, 1)["keys"]))
+    torch.cuda.synchronize()
+    g = d.guard_state()
+    assert g["skipped"] == 1 and g["last_skipped"] == 1, g
+    assert not d.plane_overflow(), "the skip must come from the underflow test alone"
+    np.testing.assert_array_equal(table.export_state()["raw_priorities"], raw1)
+    for buf, ref in state1.items():
+        got = d.get_params(buf)
+        for k in ref:
+            np.testing.assert_array_equal(got[k], ref[k], err_msg=f"{buf}/{k}")
+
+
+def test_skipped_step_makes_no_target_copy():
+    """A target copy due on a skipped step (num_steps % period == 0) is not made: the stale
+    target stays (agents/tf/dqn/learning.py:157-161 copies after an update)."""
+    from acme_amd.native import NativeDQN
+    from acme_amd.networks import DQNAtariNetwork
+    B = 64
+    p0, t0 = _head_scaled_params(DQNAtariNetwork(18))
+    # A small learning rate keeps q ~ 1e-4 after the updates (Adam moves every parameter by
+    # about lr), so only the large batch jumps.
+    d = NativeDQN(network="nature", num_actions=18, max_batch=B, obs_dtype="uint8",
+                  target_update_period=2, learning_rate=1e-7)
+    d.set_params(p0, t0)
+    rng = np.random.default_rng(5)
+    small = [_batch(rng, B, 18, r=0.0, d=0.0) for _ in range(2)]
+    large = _batch(rng, B, 18, r=1.0, d=0.0)
+    d.step(*_dev(small[0]))  # num_steps 0: copy
+    d.step(*_dev(small[1]))  # num_steps 1: the online parameters move, the target is stale
+    torch.cuda.synchronize()
+    tgt1, prm1 = d.get_params("target"), d.get_params("params")
+    assert any(not np.array_equal(tgt1[k], prm1[k]) for k in tgt1)
+    d.step(*_dev(large))     # num_steps 2: copy due, the step overflows and is skipped
+    torch.cuda.synchronize()
+    g = d.guard_state()
+    assert g["skipped"] == 1 and g["last_skipped"] == 1, g
+    for k, v in d.get_params("target").items():
+        np.testing.assert_array_equal(v, tgt1[k], err_msg=k)
+
+
+class _FixedBatches:
+    """A dataset of fixed device batches, each ReplaySample handed out once."""
+
+    def __init__(self, samples):
+        self.samples = list(samples)
+        self.batch_size = int(samples[0].data[1].shape[0])
+
+    def __iter__(self):
+        return iter(self.samples)
+
+
+def _sample(b, first_key):
+    from acme_amd import replay
+    dev = _dev(b)
+    B = dev[1].shape[0]
+    keys = torch.arange(first_key, first_key + B, dtype=torch.int64, device="cuda").view(
+        torch.uint64)
+    zeros = torch.zeros(B, dtype=torch.float64, device="cuda")
+    info = replay.SampleInfo(key=keys, probability=dev[5],
+                             table_size=torch.zeros(B, dtype=torch.int64, device="cuda"),
+                             priority=zeros)
+    return replay.ReplaySample(info=info, data=tuple(dev[:5]))
+
+
+def test_learner_reissues_skipped_step():
+    """DQNLearner.step() applies every step, as the reference (agents/tf/dqn/learning.py:
+    147-161): a step the guard skips (here the forced ~2^13-fold head-dZ jump) holds the
+    steps after it skipped too, and the learner re-issues them in order at the next step()
+    (or when its state is read), with their step counters, so the due target copy lands.
+    Checked bit for bit against a learner that recalibrated before the large batch (so it
+    never skips), both writing their priorities back into their own tables."""
+    from acme_amd import replay, specs
+    from acme_amd.adders import reverb as adders
+    from acme_amd.agents.dqn import DQNLearner
+    from acme_amd.networks import DQNAtariNetwork
+    from acme_amd.utils import loggers
+    B, A = 64, 18
+    net = DQNAtariNetwork(A)
+    p0, t0 = _head_scaled_params(net)
+    rng = np.random.default_rng(6)
+    batches = [_batch(rng, B, A, r=0.0, d=0.0), _batch(rng, B, A, r=1.0, d=0.0),
+               _batch(rng, B, A), _batch(rng, B, A), _batch(rng, B, A)]
+    spec = specs.EnvironmentSpec(
+        observations=specs.Array((84, 84, 4), np.uint8), actions=specs.DiscreteArray(A, np.int32),
+        rewards=specs.Array((), np.float32), discounts=specs.BoundedArray((), np.float32, 0, 1))
+
+    def make(recalibrate_before=None):
+        table = replay.Table(adders.DEFAULT_PRIORITY_TABLE, replay.selectors.Prioritized(0.6),
+                             replay.selectors.Fifo(), 1000, replay.rate_limiters.MinSize(1),
+                             signature=adders.NStepTransitionAdder.signature(spec), seed=3)
+        table.native.fill_synthetic(1000, layout=0, num_actions=A, seed=0)
+        server = replay.Server([table])
+        ds = _FixedBatches([_sample(b, 64 * i) for i, b in enumerate(batches)])
+        lr = DQNLearner(net, net, discount=0.99, importance_sampling_exponent=0.2,
+                        learning_rate=1e-3, target_update_period=2, dataset=ds,
+                        replay_client=replay.Client(server), logger=loggers.NoOpLogger(),
+                        seed=0)
+        lr.native.set_params(p0, t0)
+        for i in range(len(batches)):
+            if i == recalibrate_before:
+                torch.cuda.synchronize()
+                lr.native.params_changed()
+            lr.step()
+        state = lr.save()  # settles: every issued step decided, a skipped one re-issued
+        return lr, state, table.native.export_state()["raw_priorities"]
+
+    got, s_got, raw_got = make()
+    ref, s_ref, raw_ref = make(recalibrate_before=1)
+    g_got, g_ref = got.native.guard_state(), ref.native.guard_state()
+    assert g_ref["skipped"] == 0 and g_ref["applied"] == len(batches), g_ref
+    # The large batch was skipped, with the batch issued after it held; both re-issued.
+    assert g_got["skipped"] == 2 and g_got["applied"] == len(batches), g_got
+    assert got._reissued == 2  # noqa: SLF001
+    assert s_got["num_steps"] == s_ref["num_steps"] == len(batches)
+    assert s_got["optimizer"]["step"] == s_ref["optimizer"]["step"] == len(batches)
+    for part in ("network", "target_network"):
+        for k in s_ref[part]:
+            np.testing.assert_array_equal(s_got[part][k], s_ref[part][k], err_msg=f"{part}/{k}")
+    for mom in ("m", "v"):
+        for k in s_ref["optimizer"][mom]:
+            np.testing.assert_array_equal(s_got["optimizer"][mom][k], s_ref["optimizer"][mom][k],
+                                          err_msg=f"{mom}/{k}")
+    np.testing.assert_array_equal(raw_got, raw_ref)
+    assert not np.array_equal(raw_got[:64 * len(batches)], np.ones(64 * len(batches)))
+
+
 def _rel(a, b, base):
     num = sum(float(np.sum((a[k].astype(np.float64) - b[k]) ** 2)) for k in a)
     den = sum(float(np.sum((b[k] - base[k].astype(np.float64)) ** 2)) for k in a)
@@ -170,12 +336,23 @@ def _teacher_forced(d, params, target, b, B):
 
 @pytest.mark.parametrize("B,steps,checks", [(64, 100, (0, 33, 66, 99)), (512, 20, (0, 19))])
 def test_long_horizon_drift(B, steps, checks):
-    """Free-running trajectories (each side applies its own gradients) of the plane engine,
-    the exact-f32 engine and the float64 restatement, from identical batches; at the
-    `checks` steps the plane engine's step is also checked teacher-forced against the f64
-    oracle from its own pre-step state (the north star's 1e-5 on the loss and TD, the
-    suite's gradient bar), so the per-step accuracy is shown not to degrade while the
-    scales follow 100 steps of training."""
+    """Free-running trajectories (each side applies its own gradients) from identical batches:
+    the plane engine, the exact-f32 engine, an independent float32 implementation (the torch
+    restatement oracle/dqn_torch.py in float32 on the GPU: MIOpen convolutions, rocBLAS
+    GEMMs, i.e. what the reference's own float32 TF learner is) and the float64 reference
+    trajectory.  Asserted (PLANE_FACTOR = 2): the plane engine skips no step; its first two
+    losses match float64 at the north star's 1e-5; its parameter drift from the float64
+    trajectory (relative to how far training moved the parameters) and its loss trajectory's
+    maximum and median relative error are within PLANE_FACTOR x those of the worse of the
+    two float32 implementations.  (Against the exact-f32 engine alone the B = 64 case does
+    not hold: that engine stays unusually close to float64 (drift 0.065, median loss error
+    3.5e-3) where torch float32 drifts as far as the plane engine (0.160 / 5.3e-2 against
+    0.152 / 6.4e-2; profiles/r05/drift/): free-running training is chaotic (Adam's normalised
+    steps flip on near-zero gradients, double-Q argmax ties flip), so any float32 rounding
+    difference grows to this size.)  At the `checks` steps the plane engine's step is also
+    checked teacher-forced against the f64 oracle from its own pre-step state (loss and TD at
+    1e-5, the suite's gradient bar), so per-step accuracy does not degrade as the scales
+    follow training."""
     from acme_amd._lib import lib
     from acme_amd.native import NativeDQN
     from acme_amd.networks import DQNAtariNetwork
@@ -188,16 +365,18 @@ def test_long_horizon_drift(B, steps, checks):
         for _ in range(steps):
             yield _batch(rng, B, 18)
 
-    # The float64 reference trajectory (torch on the GPU).
-    ref = TorchDQN(p0, 18, target=t0, dtype=torch.float64, device="cuda")
-    ref_loss = []
-    for b in batches():
-        dev = {k: torch.as_tensor(b[k]).cuda() for k in ("o_tm1", "a_tm1", "r_t", "d_t", "o_t")}
-        loss, _ = ref.step(dev["o_tm1"], dev["a_tm1"], dev["r_t"].double(), dev["d_t"].double(),
-                           dev["o_t"], b["probabilities"])
-        ref_loss.append(loss)
-    ref_p = {k: v.detach().cpu().numpy() for k, v in ref.p.items()}
-    ref_loss = np.array(ref_loss)
+    def torch_run(dtype):
+        t = TorchDQN(p0, 18, target=t0, dtype=dtype, device="cuda")
+        losses = []
+        for b in batches():
+            dev = {k: torch.as_tensor(b[k]).cuda() for k in ("o_tm1", "a_tm1", "r_t", "d_t", "o_t")}
+            loss, _ = t.step(dev["o_tm1"], dev["a_tm1"], dev["r_t"].to(dtype),
+                             dev["d_t"].to(dtype), dev["o_t"], b["probabilities"])
+            losses.append(loss)
+        return np.array(losses), {k: v.detach().cpu().numpy() for k, v in t.p.items()}
+
+    ref_loss, ref_p = torch_run(torch.float64)   # the reference trajectory
+    t32_loss, t32_p = torch_run(torch.float32)   # an independent float32 learner
 
     def run(engine, check=()):
         lib().acme_set_matmul_engine(engine)
@@ -225,13 +404,17 @@ def test_long_horizon_drift(B, steps, checks):
     # The first steps match the f64 trajectory at the north star's 1e-5.
     np.testing.assert_allclose(plane_loss[:2], ref_loss[:2], rtol=1e-5)
     np.testing.assert_allclose(f32_loss[:2], ref_loss[:2], rtol=1e-5)
-    d_plane = _rel(plane_p, ref_p, p0)
-    d_f32 = _rel(f32_p, ref_p, p0)
-    e_plane = np.abs(plane_loss - ref_loss) / np.abs(ref_loss)
-    e_f32 = np.abs(f32_loss - ref_loss) / np.abs(ref_loss)
-    print(f"B={B} steps={steps}: parameter drift plane {d_plane:.3e} f32 {d_f32:.3e}; "
-          f"max loss rel err plane {e_plane.max():.3e} f32 {e_f32.max():.3e}")
-    assert d_plane <= PLANE_DRIFT_FACTOR * d_f32 + 1e-5, (d_plane, d_f32)
+    drift = {k: _rel(p, ref_p, p0) for k, p in (("plane", plane_p), ("f32", f32_p),
+                                                ("torch32", t32_p))}
+    err = {k: np.abs(x - ref_loss) / np.abs(ref_loss)
+           for k, x in (("plane", plane_loss), ("f32", f32_loss), ("torch32", t32_loss))}
+    print(f"B={B} steps={steps}: parameter drift " +
+          " ".join(f"{k} {v:.3e}" for k, v in drift.items()) + "; loss rel err max / median " +
+          " ".join(f"{k} {e.max():.3e} / {np.median(e):.3e}" for k, e in err.items()))
+    worst = lambda f: max(f("f32"), f("torch32"))  # noqa: E731
+    assert drift["plane"] <= PLANE_FACTOR * worst(drift.get) + 1e-5, drift
+    assert err["plane"].max() <= PLANE_FACTOR * worst(lambda k: err[k].max()) + 1e-5
+    assert np.median(err["plane"]) <= PLANE_FACTOR * worst(lambda k: np.median(err[k])) + 1e-6
 
 
 def test_impala_timeout_skips_update():
