@@ -1486,9 +1486,18 @@ static int apply_impl(acme_dqn* l, bool copy, hipStream_t st) {
     tail.params = l->scales + kScParams;
     if (copy) tail.target = l->scales + kScTarget;
   }
+  // Adam's algorithmic bytes: 28 per parameter (p, m, v read and written, g read), the
+  // parameter planes it writes for the next forward (2 x 2 B), and on the fused step the conv
+  // weight gradients' split-K slabs it reduces on its read (and their reduced gradients).
+  const double adam_bytes = 28.0 * (double)l->logical + (l->p3_capable ? 4.0 * (double)l->flat : 0.0);
   if (l->slabs_pending) {  // the conv weight gradients reduced on Adam's read
     l->slabs_pending = false;
-    ACME_PROF("adam", st, 0.0, 28.0 * (double)l->logical);
+    double slab_bytes = 0.0;
+    for (int k = 0; k < 3; ++k) {
+      const double count4 = (double)((l->wslabs[k].wcount + l->wslabs[k].bcount) / 4);
+      slab_bytes += 16.0 * count4 * (double)(l->wslabs[k].splits + 1);
+    }
+    ACME_PROF("adam", st, 0.0, adam_bytes + slab_bytes);
     const int ten[3][2] = {{l->t_c1w, l->t_c1b}, {l->t_c2w, l->t_c2b}, {l->t_c3w, l->t_c3b}};
     AdamSlabs a;
     for (int k = 0; k < 3; ++k) {
@@ -1508,7 +1517,7 @@ static int apply_impl(acme_dqn* l, bool copy, hipStream_t st) {
                            l->cfg.semantics == ACME_SEMANTICS_JAX ? 1 : 0, gate, tail, st);
     if (rc != ACME_OK) return rc;
   } else {
-    ACME_PROF("adam", st, 0.0, 28.0 * (double)l->logical);
+    ACME_PROF("adam", st, 0.0, adam_bytes);
     if ((rc = adam_range(l, 0, l->flat, gate, tail, st)) != ACME_OK) return rc;
   }
   if (copy) {

@@ -65,6 +65,7 @@ struct acme_replay {
   double* raw_prio = nullptr;
   uint64_t* keys = nullptr;
   int32_t* winner = nullptr;  // per-slot scratch for last-wins priority updates
+  uint32_t* upd_done = nullptr;  // the fused update's finished-workgroup count (0 between launches)
   int64_t* upd_slots = nullptr;  // per-update scratch (resolved slot)
   int32_t* upd_valid = nullptr;  // per-update scratch (key still present)
   int64_t upd_cap = 0;
@@ -577,16 +578,21 @@ __global__ void prio_reset_kernel(const int64_t* __restrict__ slots,
 }
 
 // update_priorities in ONE launch.  Updates are partitioned over the workgroups by their
-// ancestor at level h = nlevels - 2 (owner = slot >> 6h, workgroup owner % gridDim.x), so
-// every update of a slot, and every touched node of levels 1..h, belongs to exactly one
-// workgroup: it elects the last valid update per slot in LDS (largest j wins, Reverb's
-// in-order application), writes raw priority and leaf p^alpha, and rescans its nodes of
-// levels 1..h with barriers between levels.  The top level (children written by many
-// workgroups) is rescanned by a second one-workgroup launch: a device-wide "last
-// workgroup" hand-off needs agent-scope fences, which on the multi-XCD part write back and
-// invalidate L2 and measured slower than the launch they replace.
+// ancestor at level h = nlevels - 2 (owner = slot >> 6h, workgroup owner % G), so every
+// update of a slot, and every touched node of levels 1..h, belongs to exactly one workgroup:
+// it elects the last valid update per slot in LDS (largest j wins, Reverb's in-order
+// application) and computes its leaves p^alpha and its nodes of levels 1..h.  The children
+// of those nodes are loaded up front (one round of loads issued together right after the
+// keys are resolved), the new values substituted in LDS and each node rescanned from LDS, so
+// no store has to be read back.  The top level (whose children many workgroups write) is
+// rescanned by the LAST workgroup to finish: the level-h values are stored write-through
+// (agent-scope atomic stores, drained before the workgroup counts itself) and read back by
+// agent-scope atomic loads, the hand-off form that needs no L2 writeback or invalidate
+// (cdna_hip_programming.md G16), so the update is one launch instead of two (round 4: a
+// 10.2 us kernel + a 5.2 us one-workgroup launch for the top level).
 constexpr int kFusedUpdateMax = 4096;
 constexpr int kFusedUpdateBlocks = 256;
+constexpr int kUpdPairs = 32;  // (level, node) pairs a workgroup prefetches; else read back
 struct FusedUpdateArgs {
   const uint64_t* upd_keys;
   const double* prios;
@@ -596,7 +602,9 @@ struct FusedUpdateArgs {
   double alpha;
   double* raw_prio;
   double* level[8];
+  int64_t top_nodes;  // nodes of level nlevels - 2 (the top level's entries that have children)
   int nlevels;
+  uint32_t* done;     // workgroups finished (the last one rescans the top; it resets the count)
   Gate gate;  // a learner step that was skipped writes no priority
   // job.s: the learner step's rescale, run by workgroup 0 (the update workgroups are 1..G).
   // With a step verdict (kRgStep) the update workgroups wait for it (StepGuard::vseq) and
@@ -621,27 +629,32 @@ __device__ __forceinline__ bool wait_verdict_skip(const StepGuard* g, uint32_t s
   __syncthreads();
   return s_v != 0u;
 }
+// A level-h value other workgroups' top rescan reads: write-through.
+__device__ __forceinline__ void store_shared_level(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs a) {
   __shared__ int s_j[kFusedUpdateMax];
   __shared__ int64_t s_slot[kFusedUpdateMax];
-  __shared__ int s_len;
+  __shared__ int s_len, s_np, s_ovf, s_last;
+  __shared__ double s_ch[kUpdPairs][64];  // children of each prefetched node
+  __shared__ int64_t s_node[kUpdPairs];
+  __shared__ int s_lvl[kUpdPairs];
+  __shared__ double s_val[kUpdPairs];
   const int first = a.job.s ? 1 : 0;
   if (a.job.s && blockIdx.x == 0) {
     rescale_block(a.job);
     return;
   }
-  if (a.job.s && a.job.rg.g && a.job.rg.mode == kRgStep) {
-    if (wait_verdict_skip(a.job.rg.g, a.job.rg.seq)) return;
-  } else if (gate_skip(a.gate)) {
-    return;
-  }
+  const bool verdict = a.job.s && a.job.rg.g && a.job.rg.mode == kRgStep;
   const int tid = threadIdx.x, nt = blockDim.x;
   const int lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
   const int G = kFusedUpdateBlocks, bid = (int)blockIdx.x - first;
   const int h = a.nlevels >= 2 ? a.nlevels - 2 : 0;
+  bool skip = !verdict && gate_skip(a.gate);
   if (tid == 0) s_len = 0;
   __syncthreads();
-  for (int j = tid; j < a.n; j += nt) {  // this workgroup's updates (valid keys only)
+  for (int j = tid; j < a.n && !skip; j += nt) {  // this workgroup's updates (valid keys only)
     const uint64_t k = a.upd_keys[j];
     const int64_t slot = (int64_t)(k % (uint64_t)a.capacity);
     if ((int)((slot >> (6 * h)) % G) != bid) continue;
@@ -652,27 +665,115 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
   }
   __syncthreads();
   const int len = s_len;
-  for (int e = tid; e < len; e += nt) {  // last update of each slot wins
-    const int64_t slot = s_slot[e];
-    const int j = s_j[e];
-    bool win = true;
-    for (int f = 0; f < len; ++f)
-      if (s_slot[f] == slot && s_j[f] > j) win = false;
-    if (win) {
-      const double p = a.prios[j];
-      a.raw_prio[slot] = p;
-      a.level[0][slot] = det_pow_priority(p, a.alpha);
-    }
-  }
-  __syncthreads();
-  for (int l = 1; l <= h; ++l) {  // this workgroup's ancestors, one wave per node
-    for (int e = wave; e < len; e += nw) {
-      const int64_t node = s_slot[e] >> (6 * l);
-      const double s = wave_scan64(a.level[l - 1][node * 64 + lane]);
-      if (lane == 63) a.level[l][node] = s;
+  if (len > 0) {
+    // The distinct nodes of levels 1..h this workgroup recomputes (one thread; a few per
+    // workgroup at the learner's batch sizes).
+    if (tid == 0) {
+      int np = 0, ovf = 0;
+      for (int l = 1; l <= h && !ovf; ++l)
+        for (int e = 0; e < len && !ovf; ++e) {
+          const int64_t node = s_slot[e] >> (6 * l);
+          bool seen = false;
+          for (int q = 0; q < np; ++q) seen = seen || (s_lvl[q] == l && s_node[q] == node);
+          if (seen) continue;
+          if (np == kUpdPairs) {
+            ovf = 1;
+          } else {
+            s_lvl[np] = l;
+            s_node[np] = node;
+            ++np;
+          }
+        }
+      s_np = np;
+      s_ovf = ovf;
     }
     __syncthreads();
+    const int np = s_np;
+    const bool pre = !s_ovf;
+    // One round of loads: each node's 64 children (a wave per node), each update's priority.
+    double pv[kFusedUpdateMax / 256];
+#pragma unroll
+    for (int i = 0; i < kFusedUpdateMax / 256; ++i) {
+      const int e = tid + i * nt;
+      pv[i] = e < len ? a.prios[s_j[e]] : 0.0;
+    }
+    if (pre) {
+      for (int q = wave; q < np; q += nw)
+        s_ch[q][lane] = a.level[s_lvl[q] - 1][s_node[q] * 64 + lane];
+    }
+    // The step's verdict (published by workgroup 0's rescale while this workgroup resolved
+    // its keys and loaded), before the first store.
+    if (verdict) skip = wait_verdict_skip(a.job.rg.g, a.job.rg.seq);
+    if (!skip) {
+      // Last update of each slot wins: its raw priority and leaf, substituted into its
+      // level-1 node's children.
+#pragma unroll
+      for (int i = 0; i < kFusedUpdateMax / 256; ++i) {
+        const int e = tid + i * nt;
+        if (e >= len) break;
+        const int64_t slot = s_slot[e];
+        const int j = s_j[e];
+        bool win = true;
+        for (int f = 0; f < len; ++f)
+          if (s_slot[f] == slot && s_j[f] > j) win = false;
+        if (!win) continue;
+        const double leaf = det_pow_priority(pv[i], a.alpha);
+        a.raw_prio[slot] = pv[i];
+        if (h == 0) store_shared_level(a.level[0] + slot, leaf);
+        else a.level[0][slot] = leaf;
+        if (pre)
+          for (int q = 0; q < np; ++q)
+            if (s_lvl[q] == 1 && s_node[q] == (slot >> 6)) s_ch[q][slot & 63] = leaf;
+      }
+      __syncthreads();
+      for (int l = 1; l <= h; ++l) {  // level by level
+        if (pre) {
+          for (int q = wave; q < np; q += nw) {
+            if (s_lvl[q] != l) continue;
+            const double v = wave_scan64(s_ch[q][lane]);
+            if (lane == 63) {
+              s_val[q] = v;
+              if (l == h) store_shared_level(a.level[l] + s_node[q], v);
+              else a.level[l][s_node[q]] = v;
+            }
+          }
+          __syncthreads();
+          if (tid < np && s_lvl[tid] == l)  // into the parent's children
+            for (int q = 0; q < np; ++q)
+              if (s_lvl[q] == l + 1 && s_node[q] == (s_node[tid] >> 6))
+                s_ch[q][s_node[tid] & 63] = s_val[tid];
+        } else {  // read back what this workgroup stored (levels below are its own)
+          for (int e = wave; e < len; e += nw) {
+            const int64_t node = s_slot[e] >> (6 * l);
+            const double v = wave_scan64(a.level[l - 1][node * 64 + lane]);
+            if (lane == 63) {
+              if (l == h) store_shared_level(a.level[l] + node, v);
+              else a.level[l][node] = v;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
   }
+  if (a.nlevels < 2) return;
+  // Count this workgroup finished once its write-through stores have left (drained), then
+  // the last one rescans the top level from them.
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (tid == 0)
+    s_last = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             (uint32_t)(G - 1);
+  __syncthreads();
+  if (!s_last) return;
+  const int top = a.nlevels - 1;
+  for (int64_t node = wave; node < a.top_nodes; node += nw) {
+    const double c = __hip_atomic_load(a.level[top - 1] + node * 64 + lane, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+    const double v = wave_scan64(c);
+    if (lane == 63) a.level[top][node] = v;
+  }
+  if (tid == 0) __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 
@@ -1107,6 +1208,9 @@ int acme_replay_create(const acme_replay_config* cfg, acme_replay** out) {
   if (hipMalloc(&r->raw_prio, cfg->capacity * sizeof(double)) != hipSuccess) return fail("prio");
   if (hipMalloc(&r->keys, cfg->capacity * sizeof(uint64_t)) != hipSuccess) return fail("keys");
   if (hipMalloc(&r->winner, cfg->capacity * sizeof(int32_t)) != hipSuccess) return fail("winner");
+  if (hipMalloc(&r->upd_done, sizeof(uint32_t)) != hipSuccess ||
+      hipMemset(r->upd_done, 0, sizeof(uint32_t)) != hipSuccess)
+    return fail("update count");
   (void)hipMemset(r->raw_prio, 0, cfg->capacity * sizeof(double));
   // Keys of never-written slots must not match any real key: fill with all-ones.
   (void)hipMemset(r->keys, 0xFF, cfg->capacity * sizeof(uint64_t));
@@ -1128,6 +1232,7 @@ int acme_replay_destroy(acme_replay* r) {
   if (r->raw_prio) (void)hipFree(r->raw_prio);
   if (r->keys) (void)hipFree(r->keys);
   if (r->winner) (void)hipFree(r->winner);
+  if (r->upd_done) (void)hipFree(r->upd_done);
   if (r->upd_slots) (void)hipFree(r->upd_slots);
   if (r->upd_valid) (void)hipFree(r->upd_valid);
   for (int f = 0; f < ACME_MAX_FIELDS; ++f)
@@ -1734,15 +1839,10 @@ int acme::replay_update_priorities_gated(acme_replay* r, const uint64_t* keys,
     a.gate = gate;
     if (job) a.job = *job;
     for (int l = 0; l < 8; ++l) a.level[l] = r->levels[l];
+    a.top_nodes = r->nlevels >= 2 ? r->level_size[r->nlevels - 2] / 64 : 0;
+    a.done = r->upd_done;
     prio_update_fused_kernel<<<kFusedUpdateBlocks + (a.job.s ? 1 : 0), 256, 0, st>>>(a);
     ACME_LAUNCH_CHECK();
-    if (r->nlevels >= 2) {  // the top level, over all its entries that have children
-      const int top = r->nlevels - 1;
-      const int64_t nodes = r->level_size[top - 1] / 64;
-      level_update_kernel<<<(unsigned)ceil_div(nodes, 4), 256, 0, st>>>(
-          r->levels[top - 1], r->levels[top], 0, nodes, nullptr, nullptr, 0);
-      ACME_LAUNCH_CHECK();
-    }
     return ACME_OK;
   }
   prio_resolve_kernel<<<g, 256, 0, st>>>(keys, n, r->keys, r->cfg.capacity, t_slots, t_valid,

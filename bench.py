@@ -126,30 +126,34 @@ def cpu_baseline(batch: int, num_actions: int, seconds: float):
         _, prio = learner.step(obs[k], act[k], rew[k], dis[k], nxt[k], s["probabilities"])
         table.update(s["keys"], prio)
 
-    def timed(threads, budget, least):
+    def timed(threads, budget, least, cap=float("inf")):
         torch.set_num_threads(threads)
         one()  # warm-up (page faults, oneDNN primitive creation)
         t0 = time.perf_counter()
         n = 0
-        while n < least or time.perf_counter() - t0 < budget:
+        while (n < least or time.perf_counter() - t0 < budget) and time.perf_counter() - t0 < cap:
             one()
             n += 1
         return batch * n / (time.perf_counter() - t0), n
 
+    # Every visible host core (the box's OMP_NUM_THREADS, 16, is ignored here: SURVEY §8(d)
+    # times the reference CPU learner on the host cores of the same box), at least 200 timed
+    # steps (capped at 150 s); then 16 threads and 1 thread on bounded samples.
     cores = len(os.sched_getaffinity(0))
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or cores
     prev = torch.get_num_threads()
     try:
-        v_all, n_all = timed(threads, seconds, 200)
+        v_all, n_all = timed(cores, seconds, 200, cap=150.0)
+        v_16, n_16 = timed(min(16, cores), seconds / 2, 2)
         v_one, n_one = timed(1, seconds / 2, 1)
     finally:
         torch.set_num_threads(prev)
-    return dict(value=round(v_all, 2), unit="transitions/s", cores=threads, kind="port",
-                value_1thread=round(v_one, 2),
+    return dict(value=round(v_all, 2), unit="transitions/s", cores=cores, kind="port",
+                value_16threads=round(v_16, 2), value_1thread=round(v_one, 2),
                 sample=(f"float32 torch-CPU restatement of the TF DQN step (oracle/dqn_torch.py) "
                         f"+ C sum-tree oracle over 1,000,000 slots (frames from a {pool}-slot "
-                        f"host pool), batch {batch}: {n_all} timed steps on {threads} threads, "
-                        f"{n_one} on 1 thread; {cpu_model()}, {cores} cores visible"))
+                        f"host pool), batch {batch}: {n_all} timed steps on all {cores} visible "
+                        f"cores, {n_16} on {min(16, cores)} threads, {n_one} on 1 thread; "
+                        f"{cpu_model()}"))
 
 
 def d4pg_cpu_baseline(batch: int, seconds: float):
@@ -158,7 +162,7 @@ def d4pg_cpu_baseline(batch: int, seconds: float):
     in `seconds` (at least 2; the first is a warm-up)."""
     from oracle import d4pg_oracle as O
     from acme_amd.networks import DistributionalCritic, LayerNormMLPPolicy
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    threads = len(os.sched_getaffinity(0))  # every visible host core (SURVEY §8(d))
     try:
         from threadpoolctl import threadpool_limits
         ctx = threadpool_limits(threads)
@@ -431,7 +435,7 @@ def impala_cpu_baseline(B: int, T: int, seconds: float):
     the first is a warm-up)."""
     from oracle import impala_oracle as O
     from acme_amd.networks import IMPALAAtariNetwork
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    threads = len(os.sched_getaffinity(0))  # every visible host core (SURVEY §8(d))
     try:
         from threadpoolctl import threadpool_limits
         ctx = threadpool_limits(threads)
@@ -518,7 +522,7 @@ def r2d2_cpu_baseline(B: int, T: int, burn_in: int, seconds: float):
     sequences of the workload's T = burn-in + trace + 1 Atari frames, as many full learner
     steps as fit in `seconds` (at least 2; the first is a warm-up)."""
     from oracle import r2d2_oracle as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    threads = len(os.sched_getaffinity(0))  # every visible host core (SURVEY §8(d))
     try:
         from threadpoolctl import threadpool_limits
         ctx = threadpool_limits(threads)

@@ -65,8 +65,9 @@ def _cpu_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_dp_gradient_mean_equals_global_batch_cpu():
-    world, port = 2, _free_port()
+@pytest.mark.parametrize("world", [2, 8])
+def test_dp_gradient_mean_equals_global_batch_cpu(world):
+    port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_cpu_worker, args=(r, world, port, q)) for r in range(world)]

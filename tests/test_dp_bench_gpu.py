@@ -1,5 +1,8 @@
-"""The bench's data-parallel DQN path (bench.py setup_dqn with WORLD_SIZE 2, what
-`bench.py --gpus 2` runs on every rank) rehearsed on one GPU with two gloo ranks.
+"""The bench's data-parallel DQN path (bench.py setup_dqn with WORLD_SIZE N, what
+`bench.py --gpus N` runs on every rank) rehearsed on one GPU with N gloo ranks: N = 2 at
+B = 32 per rank, and N = 8 (the 8-GPU node's rank count) at B = 16 per rank, so share
+allocation, the 2 B cap per rank, the LAG = 2 mass snapshots and the ordering of the
+per-step collectives run at the real rank count before the driver's first 8-GPU run.
 
 Each rank builds exactly the bench's learner: a device-filled uint8 Atari shard
 (fill_synthetic, priorities 1), make_reverb_dataset with prefetch, DQNLearner over
@@ -30,7 +33,7 @@ import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
 
-WORLD, B, STEPS, SHARD = 2, 32, 4, 1024
+STEPS, SHARD = 4, 1024
 
 
 def _free_port():
@@ -41,7 +44,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, port, q):
+def _worker(rank, WORLD, B, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=WORLD)
@@ -86,7 +89,8 @@ def _worker(rank, port, q):
     dist.destroy_process_group()
 
 
-def test_bench_data_parallel_path_two_ranks():
+@pytest.mark.parametrize("WORLD,B", [(2, 32), (8, 16)])
+def test_bench_data_parallel_path(WORLD, B):
     from acme_amd.native import NativeDQN
     from acme_amd.networks import DQNAtariNetwork
     from acme_amd.replay.sharding import LAG, allocate_shares
@@ -94,7 +98,7 @@ def test_bench_data_parallel_path_two_ranks():
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_worker, args=(r, WORLD, B, port, q)) for r in range(WORLD)]
     for p in procs:
         p.start()
     res = {}
@@ -104,7 +108,8 @@ def test_bench_data_parallel_path_two_ranks():
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    np.testing.assert_array_equal(res[0][1], res[1][1])  # replicas identical
+    for r in range(1, WORLD):
+        np.testing.assert_array_equal(res[0][1], res[r][1])  # replicas identical
     for r in range(WORLD):
         assert res[r][2]["skipped"] == 0 and res[r][2]["applied"] == STEPS, res[r][2]
     # Draws: the bench's shards (priorities 1, seeds 1234 + rank) against the oracle.
