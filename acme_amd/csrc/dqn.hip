@@ -157,7 +157,6 @@ struct acme_dqn {
   // (ACME_V_WSN=1).
   bool single_stream = false;
   bool single_role = false;
-  bool head_separate = false;  // ACME_V_HEADSEP=1: the online head as its own launch (tests)
   // conv1 reads the batch's uint8 frames (ACME_V_F16FRAMES=1: an f16 copy, the round-4 path)
   bool frames_u8 = true;
   // Step guard (kernels.h StepGuard): the skip-on-overflow rule of the plane engine, Adam's
@@ -465,7 +464,7 @@ int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const torso:
     else if (l->single_role) ACME_P3_GEMM("fc_fwd", 128, 128, 2, 2, 32, p, splits);  // tests
     else ACME_P3WS_GEMM("fc_fwd", 128, 128, 2, 2, 32, p, splits, true);
     // The online forward of a step: the head runs inside the loss launch (nature_backward).
-    if (defer_head && !l->head_separate &&
+    if (defer_head &&
         dqn_head_loss_dz_fusable(kHidden, l->cfg.num_actions, splits, P(l, prm, l->t_vw),
                                  P(l, prm, l->t_aw), P(l, prm, l->t_fcb))) {
       l->head_deferred = true;
@@ -787,7 +786,6 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
   l->cfg = *cfg;
   l->single_stream = tune_variant("SIDE") == 1;
   l->single_role = tune_variant("WSN") == 1;
-  l->head_separate = tune_variant("HEADSEP") == 1;
   l->frames_u8 = tune_variant("F16FRAMES") != 1;
   const int A = cfg->num_actions;
   const int B = cfg->max_batch;

@@ -100,7 +100,6 @@ struct acme_replay {
   // Gather kernel variants fixed at creation (tests compare them bit for bit): ACME_V_GATH
   // 0 = transition pair / pieces (default), 1 = row per workgroup, 2 = wave pieces;
   // ACME_V_GATHG: the pieces grid cap; ACME_V_SGF=1: sample_gather as two launches.
-  int gath = 0, gathg = 0, sgf = 0;
 };
 
 namespace {
@@ -1183,9 +1182,6 @@ int acme_replay_create(const acme_replay_config* cfg, acme_replay** out) {
 
   acme_replay* r = new acme_replay();
   r->cfg = *cfg;
-  r->gath = tune_variant("GATH");
-  r->gathg = tune_variant("GATHG");
-  r->sgf = tune_variant("SGF");
   // Level sizes.
   int64_t s = ceil_div(cfg->capacity, 64) * 64;
   r->level_size[0] = s;
@@ -1612,7 +1608,7 @@ static int sample_gather_impl(acme_replay* r, int64_t batch, uint64_t step_count
   ACME_CHECK_ARG(!frames_f16 || (pair && reinterpret_cast<uintptr_t>(frames_f16) % 16 == 0),
                  "a bf16 frame copy needs the transition layout (two equal big fields) and a "
                  "16-byte aligned buffer");
-  if (frames_f16 || (r->sgf != 1 && r->gath == 0 && pair)) {
+  if (frames_f16 || pair) {
     hipStream_t st = as_stream(stream);
     int64_t size = 0;
     int rc = order_after_inserts(r, st, &size);
@@ -1650,8 +1646,7 @@ static int sample_gather_impl(acme_replay* r, int64_t batch, uint64_t step_count
     ACME_LAUNCH_CHECK();
     return ACME_OK;
   }
-  if (!pair && r->sgf != 1 && r->gath == 0 &&
-      small_layout(r, out_fields, &sm)) {
+  if (!pair && small_layout(r, out_fields, &sm)) {
     hipStream_t st = as_stream(stream);
     int64_t size = 0;
     int rc = order_after_inserts(r, st, &size);
@@ -1704,7 +1699,7 @@ int acme_replay_gather(acme_replay* r, const int64_t* slots, int64_t batch,
   ACME_PROF("replay_gather", st, 0.0, 2.0 * row_bytes * (double)batch + 8.0 * (double)batch);
   // Pieces path: every field a multiple of 4 B (always: acme_replay_create checks it) and
   // 16-B aligned rows and buffers for the big fields.
-  bool pieces = r->gath != 1;
+  bool pieces = true;
   PieceArgs pa = {};
   int64_t total = 0;
   for (int f = 0; f < r->cfg.num_fields && pieces; ++f) {
@@ -1718,10 +1713,8 @@ int acme_replay_gather(acme_replay* r, const int64_t* slots, int64_t batch,
     pa.nbig++;
   }
   pieces = pieces && total < (int64_t(1) << 30) && pa.nbig > 0;
-  const int gv = r->gath;
   // Transition layout: exactly two big fields of equal bytes, the rest small.
-  if (pieces && pa.nbig == 2 && r->cfg.field_bytes[pa.big[0]] == r->cfg.field_bytes[pa.big[1]] &&
-      gv == 0) {
+  if (pieces && pa.nbig == 2 && r->cfg.field_bytes[pa.big[0]] == r->cfg.field_bytes[pa.big[1]]) {
     const int f0 = pa.big[0], f1 = pa.big[1];
     const int32_t nvec = (int32_t)(r->cfg.field_bytes[f0] / 16);
     SmallFields sm = {};
@@ -1750,7 +1743,7 @@ int acme_replay_gather(acme_replay* r, const int64_t* slots, int64_t batch,
       return ACME_OK;
     }
   }
-  if (pieces && gv != 1) {
+  if (pieces) {
     pa.first[pa.nbig] = (int32_t)total;
     for (int f = 0; f < r->cfg.num_fields; ++f) {
       pa.src[f] = g.src[f];
@@ -1759,7 +1752,7 @@ int acme_replay_gather(acme_replay* r, const int64_t* slots, int64_t batch,
       if (r->cfg.field_bytes[f] < 1024) pa.big[pa.nbig + pa.nsmall++] = f;
     }
     constexpr int K = 8;
-    const int gcap = r->gathg > 0 ? r->gathg : 2048;
+    const int gcap = 2048;
     const int64_t waves = std::max(ceil_div(total, K), (int64_t)pa.nsmall * ceil_div(batch, 64));
     const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(waves, 4), gcap));
     gather_pieces_kernel<K><<<grid, 256, 0, st>>>(pa, slots, (int32_t)batch);

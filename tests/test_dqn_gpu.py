@@ -183,44 +183,6 @@ def test_warp_specialised_gemms_bitwise():
                     np.testing.assert_array_equal(ga[k], gb[k], err_msg=f"B={B} {buf}/{k}")
 
 
-def test_online_head_fused_into_loss_bitwise():
-    """The online duelling head runs inside the loss launch (dqn_head_loss_dz_kernel: the fc
-    slab's reduction, ReLU, q rows, loss and head dZ per batch row) with the same terms as
-    the separate head launch (ACME_V_HEADSEP=1: fc_head_forward then the fused loss + head
-    dZ kernel): the step is bit-identical; only the batch loss's f64 partials are grouped
-    differently (one per row instead of one per block).  B = 37 and 200: 8 fc splits;
-    B = 512: 4."""
-    from acme_amd._lib import lib
-    from acme_amd.networks import DQNAtariNetwork
-    net = DQNAtariNetwork(18)
-    for B in (37, 200, 512):
-        p0, t0 = net.init(5), net.init(6)
-        lib().acme_tune_set(b"HEADSEP", 1)  # read once, at the learner's creation
-        try:
-            a = _learner(net, B)
-        finally:
-            lib().acme_tune_set(b"HEADSEP", 0)
-        b = _learner(net, B)
-        a.set_params(p0, t0)
-        b.set_params(p0, t0)
-        rng = np.random.default_rng(B + 1)
-        for _ in range(2):
-            dev = _dev(_batch(rng, B, (84, 84, 4), 18))
-            qa = torch.empty(B, 18, device="cuda")
-            qb = torch.empty(B, 18, device="cuda")
-            a.step(*dev, q_tm1=qa)
-            b.step(*dev, q_tm1=qb)
-            torch.cuda.synchronize()
-            np.testing.assert_allclose(a.loss.item(), b.loss.item(), rtol=1e-6)
-            assert torch.equal(qa, qb), B
-            assert torch.equal(a.td_error[:B], b.td_error[:B]), B
-            assert torch.equal(a.priorities[:B], b.priorities[:B]), B
-            for buf in ("grads", "params", "m", "v"):
-                ga, gb = a.get_params(buf), b.get_params(buf)
-                for k in ga:
-                    np.testing.assert_array_equal(ga[k], gb[k], err_msg=f"B={B} {buf}/{k}")
-
-
 def test_adam_and_target_copy_cadence():
     from acme_amd.networks import MLP
     net = MLP(4, [50, 50], 2)
