@@ -109,6 +109,9 @@ struct acme_d4pg {
   };
   std::vector<Graph> graphs;
   hipStream_t capture = nullptr;
+  // The forwards as one row-blocked launch per pass (ACME_V_D4L=1: the per-layer launches,
+  // the round-4 path; tests compare them).
+  bool rows_fwd = true;
 };
 
 namespace {
@@ -610,6 +613,260 @@ struct ConcatWgrad {
   __device__ void store_colsum(int n, float v, int) const { bias_out[n] = v; }
 };
 
+// ------------------------------------------------------------------ row-blocked forward
+// One launch per network pass (round 5): a workgroup carries kRB rows of one evaluation
+// (blockIdx.y: the online / target network) through every layer -- the LayerNorm first
+// layer (the arithmetic of ln_first_kernel, so the same bits), the ELU layers on the f32
+// MFMA (v_mfma_f32_16x16x4_f32: exact f32 products, f32 accumulation; 16 output columns per
+// wave tile), the head -- with the rows' activations in LDS and each layer's weights
+// streamed through LDS in kRBKc-row chunks (double buffered: the next chunk's loads are in
+// flight while the current one is multiplied).  The rows are independent, so no grid
+// synchronisation is needed; every activation the backward reads (z1, mean, rstd, each h,
+// the head outputs) is written as the per-layer launches wrote it.  Replaces the 4 launches
+// of a pass (ln_first, two dense layers, the head), whose bodies were latency-bound.
+constexpr int kRB = 16;       // rows per workgroup (the MFMA's M)
+constexpr int kRBMaxW = 512;  // widest layer
+constexpr int kRBStride = kRBMaxW + 4;
+constexpr int kRBKc = 16;     // weight rows per staged chunk
+constexpr int kRBLds = (kRB * kMaxIn + 2 * kRB * kRBStride + 2 * kRBKc * kRBMaxW) * 4;
+struct RowNetArgs {
+  const float *xa0, *xb0, *xa1, *xb1;
+  int split, rows;
+  const float *w1, *b1, *scale, *offset;
+  const float* w[ACME_D4PG_MAX_LAYERS];
+  const float* b[ACME_D4PG_MAX_LAYERS];
+  const float *ow, *ob;
+  float *z1, *mean, *rstd;
+  float* h[ACME_D4PG_MAX_LAYERS];
+  float *out, *t;
+};
+struct RowNetPair {
+  RowNetArgs a[2];
+  int da, db, nl, nout, policy;
+  int sizes[ACME_D4PG_MAX_LAYERS];
+  float eps;
+  const float *lo, *ascale;  // policy: TanhToSpec
+};
+
+// out[kRB rows][N] = ain[kRB][K] @ W[K][N] on the f32 MFMA, N a multiple of 64 (<= 512), K of
+// kRBKc; wave w owns columns [w N / 4, (w + 1) N / 4).  W (row stride ldw) is staged through
+// wst in kRBKc-row chunks.  acc[t] = the wave's 16-column tile t (D[4 (lane / 16) + j][lane % 16]).
+__device__ __forceinline__ void rb_matmul(const float* __restrict__ ain, const float* __restrict__ W,
+                                          int ldw, int K, int N, float* wst, f32x4 (&acc)[8]) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ntw = N / 64, cw = wave * (N / 4), n4 = N / 4;
+  const int per = N / 64;  // float4 per thread per chunk (kRBKc * N / 4 / 256)
+#pragma unroll
+  for (int t = 0; t < 8; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 st[8];
+  auto load = [&](int c) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (u < per) {
+        const int idx = tid + 256 * u, row = idx / n4, c4 = idx - row * n4;
+        st[u] = *reinterpret_cast<const f32x4*>(W + (size_t)(c * kRBKc + row) * ldw + 4 * c4);
+      }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (u < per) {
+        const int idx = tid + 256 * u, row = idx / n4, c4 = idx - row * n4;
+        *reinterpret_cast<f32x4*>(wst + (buf * kRBKc + row) * kRBMaxW + 4 * c4) = st[u];
+      }
+  };
+  const int nch = K / kRBKc;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    if (c + 1 < nch) load(c + 1);
+    const float* wb = wst + (c & 1) * kRBKc * kRBMaxW;
+#pragma unroll
+    for (int s = 0; s < kRBKc / 4; ++s) {
+      const int kk = 4 * s + (lane >> 4);
+      const float av = ain[(lane & 15) * kRBStride + c * kRBKc + kk];
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+        if (t < ntw)
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+              av, wb[kk * kRBMaxW + cw + 16 * t + (lane & 15)], acc[t], 0, 0, 0);
+    }
+    if (c + 1 < nch) store((c + 1) & 1);
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(256) lnmlp_rows_kernel(const RowNetPair pr) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* xs = sm;                                // [kRB][kMaxIn]
+  float* act[2] = {xs + kRB * kMaxIn, xs + kRB * kMaxIn + kRB * kRBStride};
+  float* wst = act[1] + kRB * kRBStride;         // [2][kRBKc][kRBMaxW]
+  __shared__ float red[4][kRB];
+  const RowNetArgs& a = pr.a[blockIdx.y];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r0 = blockIdx.x * kRB;
+  if (r0 >= a.rows) return;  // uniform per block
+  const int din = pr.da + pr.db, H = pr.sizes[0];
+  for (int i = tid; i < kRB * din; i += 256) {
+    const int r = i / din, k = i - r * din, row = r0 + r;
+    float v = 0.f;
+    if (row < a.rows) {
+      const bool second = row >= a.split;
+      const int rr = second ? row - a.split : row;
+      v = k < pr.da ? (second ? a.xa1 : a.xa0)[(size_t)rr * pr.da + k]
+                    : (second ? a.xb1 : a.xb0)[(size_t)rr * pr.db + (k - pr.da)];
+    }
+    xs[r * kMaxIn + k] = v;
+  }
+  __syncthreads();
+  // ---- LayerNorm first layer (ln_first_kernel's arithmetic, kRB rows).
+  {
+    constexpr int C = kRBMaxW / 256;
+    float acc[kRB][C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const int j = tid + 256 * c;
+#pragma unroll
+      for (int r = 0; r < kRB; ++r) acc[r][c] = 0.f;
+      if (j < H) {
+        for (int k = 0; k < din; ++k) {
+          const float wk = a.w1[(size_t)k * H + j];
+#pragma unroll
+          for (int r = 0; r < kRB; ++r) acc[r][c] = fmaf(xs[r * kMaxIn + k], wk, acc[r][c]);
+        }
+        const float bj = a.b1[j];
+#pragma unroll
+        for (int r = 0; r < kRB; ++r) acc[r][c] += bj;
+      }
+    }
+    float sq[kRB];
+#pragma unroll
+    for (int r = 0; r < kRB; ++r) {
+      sq[r] = 0.f;
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+        if (tid + 256 * c < H) sq[r] += acc[r][c];
+    }
+    block_sum256<kRB>(sq, red);
+    const float invH = 1.f / (float)H;
+    float mean[kRB];
+#pragma unroll
+    for (int r = 0; r < kRB; ++r) {
+      mean[r] = sq[r] * invH;
+      float q = 0.f;
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+        if (tid + 256 * c < H) {
+          const float dv = acc[r][c] - mean[r];
+          q = fmaf(dv, dv, q);
+        }
+      sq[r] = q;
+    }
+    block_sum256<kRB>(sq, red);
+#pragma unroll
+    for (int r = 0; r < kRB; ++r) {
+      const int row = r0 + r;
+      const bool live = row < a.rows;
+      const float rs = 1.f / sqrtf(sq[r] * invH + pr.eps);
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const int j = tid + 256 * c;
+        if (j >= H) continue;
+        const float hv = tanhf((acc[r][c] - mean[r]) * rs * a.scale[j] + a.offset[j]);
+        act[0][r * kRBStride + j] = live ? hv : 0.f;
+        if (live) {
+          const size_t idx = (size_t)row * H + j;
+          a.z1[idx] = acc[r][c];
+          a.h[0][idx] = hv;
+        }
+      }
+      if (live && tid == 0) {
+        a.mean[row] = mean[r];
+        a.rstd[row] = rs;
+      }
+    }
+  }
+  __syncthreads();
+  // ---- ELU layers.
+  int cur = 0;
+  for (int li = 1; li < pr.nl; ++li) {
+    const int K = pr.sizes[li - 1], N = pr.sizes[li];
+    f32x4 acc[8];
+    rb_matmul(act[cur], a.w[li], N, K, N, wst, acc);
+    const int cw = wave * (N / 4);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      if (t >= N / 64) break;
+      const int col = cw + 16 * t + (lane & 15);
+      const float bv = a.b[li][col];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = 4 * (lane >> 4) + j, row = r0 + r;
+        const float v = act_fwd(ACT_ELU, acc[t][j] + bv);
+        act[cur ^ 1][r * kRBStride + col] = row < a.rows ? v : 0.f;
+        if (row < a.rows) a.h[li][(size_t)row * N + col] = v;
+      }
+    }
+    cur ^= 1;
+    __syncthreads();
+  }
+  const float* hl = act[cur];
+  const int HL = pr.sizes[pr.nl - 1];
+  if (pr.policy) {
+    // TanhToSpec head: one wave per row (policy_head_kernel's arithmetic).
+    const int A = pr.nout;
+    for (int r = wave; r < kRB; r += 4) {
+      const int row = r0 + r;
+      if (row >= a.rows) break;
+      float acc[ACME_D4PG_MAX_ACT];
+#pragma unroll
+      for (int j = 0; j < ACME_D4PG_MAX_ACT; ++j) acc[j] = 0.f;
+      for (int k = lane; k < HL; k += 64) {
+        const float hv = hl[r * kRBStride + k];
+#pragma unroll
+        for (int j = 0; j < ACME_D4PG_MAX_ACT; ++j)
+          if (j < A) acc[j] = fmaf(hv, a.ow[(size_t)k * A + j], acc[j]);
+      }
+      float mine = 0.f;
+#pragma unroll
+      for (int j = 0; j < ACME_D4PG_MAX_ACT; ++j) {
+        if (j >= A) break;
+        const float sv = wave_sum(acc[j]);
+        if (lane == j) mine = sv;
+      }
+      if (lane < A) {
+        const float t = tanhf(mine + a.ob[lane]);
+        if (a.t) a.t[(size_t)row * A + lane] = t;
+        a.out[(size_t)row * A + lane] = (0.5f * (t + 1.f)) * pr.ascale[lane] + pr.lo[lane];
+      }
+    }
+    return;
+  }
+  // Linear head (the critic's logits, nout <= 64): W staged zero-padded to 64 columns.
+  const int NO = pr.nout;
+  for (int i = tid; i < HL * 64; i += 256) {
+    const int k = i >> 6, n = i & 63;
+    wst[i] = n < NO ? a.ow[(size_t)k * NO + n] : 0.f;
+  }
+  __syncthreads();
+  f32x4 acc{0.f, 0.f, 0.f, 0.f};
+  const int col = 16 * wave + (lane & 15);
+  for (int k0 = 0; k0 < HL; k0 += 4) {
+    const int kk = k0 + (lane >> 4);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(hl[(lane & 15) * kRBStride + kk], wst[kk * 64 + col],
+                                               acc, 0, 0, 0);
+  }
+  if (col < NO) {
+    const float bv = a.ob[col];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = r0 + 4 * (lane >> 4) + j;
+      if (row < a.rows) a.out[(size_t)row * NO + col] = acc[j] + bv;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ orchestration
 
 // Small GEMMs: 32x32 output tiles, one wave per tile and k-group, 8 k-groups per block
@@ -725,10 +982,67 @@ int lnmlp_forward_pair(acme_d4pg* l, const NetDesc& d, const NetIn (&in)[2], int
   return ACME_OK;
 }
 
+// The row-blocked single-launch forward (lnmlp_rows_kernel) takes networks whose widths are
+// multiples of 64 up to 512 (the critic's last hidden layer up to 256, its head up to 64
+// outputs) and inputs of up to kMaxIn features; others run the per-layer launches.
+bool rows_fit(const NetDesc& d, int din, bool policy) {
+  if (din > kMaxIn || d.nl < 1) return false;
+  for (int i = 0; i < d.nl; ++i)
+    if (d.sizes[i] > kRBMaxW || d.sizes[i] % 64 != 0) return false;
+  return policy ? d.nout <= ACME_D4PG_MAX_ACT : (d.nout <= 64 && d.sizes[d.nl - 1] <= 256);
+}
+
+// Up to two evaluations of one network in one row-blocked launch; out[i]: the policy's
+// actions (the critic writes its logits to acts.out).
+int lnmlp_forward_rows(acme_d4pg* l, const NetDesc& d, const NetIn (&in)[2], int da, int db,
+                       bool policy, float* const (&out)[2], hipStream_t st) {
+  static hipError_t attr = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(&lnmlp_rows_kernel),
+      hipFuncAttributeMaxDynamicSharedMemorySize, kRBLds);
+  if (attr != hipSuccess) return (set_error("LDS attribute: %s", hipGetErrorString(attr)), ACME_ERR_HIP);
+  RowNetPair pr;
+  double flops = 0.0;
+  for (int i = 0; i < 2; ++i) {
+    RowNetArgs& g = pr.a[i];
+    const NetIn& n = in[i];
+    g.xa0 = n.xa0; g.xb0 = n.xb0; g.xa1 = n.xa1; g.xb1 = n.xb1;
+    g.split = n.split; g.rows = n.rows;
+    g.w1 = P(l, n.prm, d.w1); g.b1 = P(l, n.prm, d.b1);
+    g.scale = P(l, n.prm, d.scale); g.offset = P(l, n.prm, d.offset);
+    for (int li = 1; li < d.nl; ++li) {
+      g.w[li] = P(l, n.prm, d.w[li]);
+      g.b[li] = P(l, n.prm, d.b[li]);
+    }
+    g.ow = P(l, n.prm, d.ow); g.ob = P(l, n.prm, d.ob);
+    if (n.rows > 0) {
+      Acts& a = *n.acts;
+      g.z1 = a.z1; g.mean = a.mean; g.rstd = a.rstd;
+      for (int li = 0; li < d.nl; ++li) g.h[li] = a.h[li];
+      g.out = policy ? out[i] : a.out;
+      g.t = policy ? a.t : nullptr;
+    }
+    double per = (double)(da + db) * d.sizes[0] + (double)d.sizes[d.nl - 1] * d.nout;
+    for (int li = 1; li < d.nl; ++li) per += (double)d.sizes[li - 1] * d.sizes[li];
+    flops += 2.0 * n.rows * per;
+  }
+  pr.da = da; pr.db = db; pr.nl = d.nl; pr.nout = d.nout; pr.policy = policy ? 1 : 0;
+  for (int li = 0; li < d.nl; ++li) pr.sizes[li] = d.sizes[li];
+  pr.eps = l->cfg.layer_norm_epsilon;
+  pr.lo = l->act_lo; pr.ascale = l->act_scale;
+  const int rows = std::max(in[0].rows, in[1].rows);
+  ACME_PROF_PEAK(policy ? "d4pg_policy_fwd" : "d4pg_critic_fwd", st, flops, 0.0, 157.3);
+  lnmlp_rows_kernel<<<dim3((unsigned)ceil_div(rows, kRB), in[1].rows > 0 ? 2 : 1), 256, kRBLds,
+                      st>>>(pr);
+  D4_CHECK();
+  return ACME_OK;
+}
+
 // Up to two policy evaluations (TanhToSpec actions into out[i]); in[1].rows = 0: one.
 int policy_forward_pair(acme_d4pg* l, const NetIn (&in)[2], float* const (&out)[2],
                         hipStream_t st) {
   const NetDesc& d = l->pol;
+  if (l->rows_fwd && rows_fit(d, l->cfg.obs_dim, true))
+    return lnmlp_forward_rows(l, d, in, l->cfg.obs_dim, 0, true, out, st);
   int rc = lnmlp_forward_pair(l, d, in, l->cfg.obs_dim, 0, "d4pg_policy_ln", st);
   if (rc != ACME_OK) return rc;
   const int rows = std::max(in[0].rows, in[1].rows);
@@ -754,6 +1068,10 @@ int policy_forward_pair(acme_d4pg* l, const NetIn (&in)[2], float* const (&out)[
 // (B rows: [o_t, target actions]).
 int critic_forward_pair(acme_d4pg* l, const NetIn (&in)[2], hipStream_t st) {
   const NetDesc& d = l->cri;
+  if (l->rows_fwd && rows_fit(d, l->cfg.obs_dim + l->cfg.act_dim, false)) {
+    float* const none[2] = {nullptr, nullptr};
+    return lnmlp_forward_rows(l, d, in, l->cfg.obs_dim, l->cfg.act_dim, false, none, st);
+  }
   int rc = lnmlp_forward_pair(l, d, in, l->cfg.obs_dim, l->cfg.act_dim, "d4pg_critic_ln", st);
   if (rc != ACME_OK) return rc;
   Acts &a0 = *in[0].acts, &a1 = *in[1].acts;
@@ -1143,6 +1461,7 @@ int acme_d4pg_create(const acme_d4pg_config* cfg, acme_d4pg** out) {
                    "critic layer sizes must be multiples of 4 in [4, %d]", kMaxWidth);
   acme_d4pg* l = new acme_d4pg();
   l->cfg = *cfg;
+  l->rows_fwd = tune_variant("D4L") != 1;
   auto fail = [&](int code) {
     acme_d4pg_destroy(l);
     return code;
