@@ -109,9 +109,10 @@ struct acme_d4pg {
   };
   std::vector<Graph> graphs;
   hipStream_t capture = nullptr;
-  // The forwards as one row-blocked launch per pass (ACME_V_D4L=1: the per-layer launches,
-  // the round-4 path; tests compare them).
+  // The forwards as one row-blocked launch per pass, the input-gradient chains likewise
+  // (ACME_V_D4L=1: the per-layer launches, the round-4 path).
   bool rows_fwd = true;
+  int cur_B = 0;  // the batch of the step being issued
 };
 
 namespace {
@@ -613,6 +614,8 @@ struct ConcatWgrad {
   __device__ void store_colsum(int n, float v, int) const { bias_out[n] = v; }
 };
 
+__device__ __forceinline__ int act_of_layer_dev(int i) { return i == 0 ? ACT_TANH : ACT_ELU; }
+
 // ------------------------------------------------------------------ row-blocked forward
 // One launch per network pass (round 5): a workgroup carries kRB rows of one evaluation
 // (blockIdx.y: the online / target network) through every layer -- the LayerNorm first
@@ -648,9 +651,12 @@ struct RowNetPair {
   const float *lo, *ascale;  // policy: TanhToSpec
 };
 
-// out[kRB rows][N] = ain[kRB][K] @ W[K][N] on the f32 MFMA, N a multiple of 64 (<= 512), K of
-// kRBKc; wave w owns columns [w N / 4, (w + 1) N / 4).  W (row stride ldw) is staged through
-// wst in kRBKc-row chunks.  acc[t] = the wave's 16-column tile t (D[4 (lane / 16) + j][lane % 16]).
+// out[kRB rows][N] = ain[kRB][K] @ B on the f32 MFMA, N a multiple of 64 (<= 512), K of
+// kRBKc; wave w owns columns [w N / 4, (w + 1) N / 4).  B = W [K][N] (row stride ldw), or with
+// TRANS B = W^T for W [N][K] (row stride ldw: an input gradient's dZ @ W^T), staged through
+// wst in kRBKc-row chunks ([k][n] either way).  acc[t] = the wave's 16-column tile t
+// (D[4 (lane / 16) + j][lane % 16]).
+template <bool TRANS = false>
 __device__ __forceinline__ void rb_matmul(const float* __restrict__ ain, const float* __restrict__ W,
                                           int ldw, int K, int N, float* wst, f32x4 (&acc)[8]) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -663,16 +669,29 @@ __device__ __forceinline__ void rb_matmul(const float* __restrict__ ain, const f
 #pragma unroll
     for (int u = 0; u < 8; ++u)
       if (u < per) {
-        const int idx = tid + 256 * u, row = idx / n4, c4 = idx - row * n4;
-        st[u] = *reinterpret_cast<const f32x4*>(W + (size_t)(c * kRBKc + row) * ldw + 4 * c4);
+        const int idx = tid + 256 * u;
+        if constexpr (TRANS) {  // W[n][c kRBKc + 4 q .. + 3]: 4 float4 per n
+          const int n = idx >> 2, q = idx & 3;
+          st[u] = *reinterpret_cast<const f32x4*>(W + (size_t)n * ldw + c * kRBKc + 4 * q);
+        } else {
+          const int row = idx / n4, c4 = idx - row * n4;
+          st[u] = *reinterpret_cast<const f32x4*>(W + (size_t)(c * kRBKc + row) * ldw + 4 * c4);
+        }
       }
   };
   auto store = [&](int buf) {
 #pragma unroll
     for (int u = 0; u < 8; ++u)
       if (u < per) {
-        const int idx = tid + 256 * u, row = idx / n4, c4 = idx - row * n4;
-        *reinterpret_cast<f32x4*>(wst + (buf * kRBKc + row) * kRBMaxW + 4 * c4) = st[u];
+        const int idx = tid + 256 * u;
+        if constexpr (TRANS) {
+          const int n = idx >> 2, q = idx & 3;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) wst[(buf * kRBKc + 4 * q + e) * kRBMaxW + n] = st[u][e];
+        } else {
+          const int row = idx / n4, c4 = idx - row * n4;
+          *reinterpret_cast<f32x4*>(wst + (buf * kRBKc + row) * kRBMaxW + 4 * c4) = st[u];
+        }
       }
   };
   const int nch = K / kRBKc;
@@ -793,7 +812,7 @@ __global__ void __launch_bounds__(256) lnmlp_rows_kernel(const RowNetPair pr) {
   for (int li = 1; li < pr.nl; ++li) {
     const int K = pr.sizes[li - 1], N = pr.sizes[li];
     f32x4 acc[8];
-    rb_matmul(act[cur], a.w[li], N, K, N, wst, acc);
+    rb_matmul<false>(act[cur], a.w[li], N, K, N, wst, acc);
     const int cw = wave * (N / 4);
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
@@ -864,6 +883,208 @@ __global__ void __launch_bounds__(256) lnmlp_rows_kernel(const RowNetPair pr) {
       const int row = r0 + 4 * (lane >> 4) + j;
       if (row < a.rows) a.out[(size_t)row * NO + col] = acc[j] + bv;
     }
+  }
+}
+
+// ------------------------------------------------------------------ row-blocked backward
+// The input-gradient chain of one network pass in one launch (round 5): a workgroup takes
+// kRB rows from the head's pre-activation gradient (the critic's dlogits, the policy's du)
+// down to the LayerNorm input -- dZ @ W^T on the f32 MFMA with the activation derivatives
+// from the forward's outputs, the LayerNorm backward (ln_bwd_kernel's arithmetic for kRB
+// rows, with its column partials and, for the critic's dpg rows, dq/da, clip_by_norm, du
+// and the policy-loss partials) -- keeping the rows' gradients in LDS; every dZ the weight
+// gradients read is written.  Replaces the chain of per-layer input-gradient launches.
+struct RowBwdArgs {
+  const float* dtop;  // [rows][nout] gradient at the head's pre-activation
+  int nout;
+  const float* ow;    // head weight [HL][nout]
+  const float* w[ACME_D4PG_MAX_LAYERS];  // mlp weights [sizes[li-1]][sizes[li]]
+  const float* h[ACME_D4PG_MAX_LAYERS];  // forward outputs
+  float* dz[ACME_D4PG_MAX_LAYERS];       // pre-activation gradients (dz[0]: LayerNorm input)
+  const float *z1, *mean, *rstd, *scale;
+  int rows, ce_rows, nl;
+  int sizes[ACME_D4PG_MAX_LAYERS];
+  float* colslab;  // [gridDim.x][2][H0]
+  // dpg rows (rows >= ce_rows; the critic)
+  const float* w1;
+  int act_off, A;
+  float clip, invB;
+  const float *t, *act_scale;
+  float *du, *dqda, *ploss_part;
+};
+
+__global__ void __launch_bounds__(256) lnmlp_bwd_rows_kernel(const RowBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smb[];
+  float* base = smb + kRB * kMaxIn;
+  float* act[2];
+  act[0] = base;
+  act[1] = base + kRB * kRBStride;
+  float* wst = act[1] + kRB * kRBStride;
+  __shared__ float red[4][2 * kRB];
+  __shared__ float dq_s[kRB][ACME_D4PG_MAX_ACT];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r0 = blockIdx.x * kRB;
+  if (r0 >= a.rows) return;  // uniform per block
+  const int NO = a.nout, NOp = (NO + 3) & ~3;
+  const int HL = a.sizes[a.nl - 1];
+  // The head's gradient rows (zero-padded to a multiple of 4 columns) and its weight^T.
+  for (int i = tid; i < kRB * NOp; i += 256) {
+    const int r = i / NOp, k = i - r * NOp, row = r0 + r;
+    act[0][r * kRBStride + k] = (row < a.rows && k < NO) ? a.dtop[(size_t)row * NO + k] : 0.f;
+  }
+  for (int i = tid; i < NOp * HL; i += 256) {
+    const int k = i / HL, n = i - k * HL;
+    wst[k * kRBMaxW + n] = k < NO ? a.ow[(size_t)n * NO + k] : 0.f;
+  }
+  __syncthreads();
+  int cur = 0;
+  // Layer li's input gradient: dz[li - 1] = act'(h[li - 1]) * (dz[li] @ W_li^T); li = nl: the
+  // head (its weight staged above).
+  for (int li = a.nl; li >= 1; --li) {
+    const int N = a.sizes[li - 1];
+    f32x4 acc[8];
+    if (li == a.nl) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int cw = wave * (N / 4);
+      for (int k0 = 0; k0 < NOp; k0 += 4) {
+        const int kk = k0 + (lane >> 4);
+        const float av = act[cur][(lane & 15) * kRBStride + kk];
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+          if (t < N / 64)
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                av, wst[kk * kRBMaxW + cw + 16 * t + (lane & 15)], acc[t], 0, 0, 0);
+      }
+      __syncthreads();  // wst is restaged by the next layer
+    } else {
+      rb_matmul<true>(act[cur], a.w[li], a.sizes[li], a.sizes[li], N, wst, acc);
+    }
+    const int cw = wave * (N / 4);
+    const int fn = act_of_layer_dev(li - 1);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      if (t >= N / 64) break;
+      const int col = cw + 16 * t + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = 4 * (lane >> 4) + j, row = r0 + r;
+        float g = 0.f;
+        if (row < a.rows) {
+          g = act_bwd(fn, a.h[li - 1][(size_t)row * N + col], acc[t][j]);
+          a.dz[li - 1][(size_t)row * N + col] = g;
+        }
+        act[cur ^ 1][r * kRBStride + col] = g;
+      }
+    }
+    cur ^= 1;
+    __syncthreads();
+  }
+  // ---- LayerNorm backward (ln_bwd_kernel, kRB rows); dy = act[cur] (tanh' applied).
+  constexpr int C = kRBMaxW / 256;
+  const int H = a.sizes[0];
+  const float invH = 1.f / (float)H;
+  float g[kRB][C], xh[kRB][C];
+  float s[2 * kRB];
+  float sc[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) sc[c] = a.scale[min(tid + 256 * c, H - 1)];
+#pragma unroll
+  for (int r = 0; r < kRB; ++r) {
+    const int row = r0 + r;
+    const bool ok = row < a.rows;
+    const float mu = ok ? a.mean[row] : 0.f, rs = ok ? a.rstd[row] : 0.f;
+    s[2 * r] = s[2 * r + 1] = 0.f;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const int j = tid + 256 * c;
+      const bool v = ok && j < H;
+      const float dy = v ? act[cur][r * kRBStride + j] : 0.f;
+      const float z = v ? a.z1[(size_t)row * H + j] : 0.f;
+      xh[r][c] = v ? (z - mu) * rs : 0.f;
+      g[r][c] = v ? dy * sc[c] : 0.f;
+      s[2 * r] += g[r][c];
+      s[2 * r + 1] = fmaf(g[r][c], xh[r][c], s[2 * r + 1]);
+    }
+  }
+  block_sum256<2 * kRB>(s, red);
+  float cs_x[C], cs_1[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) cs_x[c] = cs_1[c] = 0.f;
+  bool any_dpg = false;
+#pragma unroll
+  for (int r = 0; r < kRB; ++r) {
+    const int row = r0 + r;
+    if (row >= a.rows) continue;
+    const float rs = a.rstd[row];
+    const float m1 = s[2 * r] * invH, m2 = s[2 * r + 1] * invH;
+    const bool ce = row < a.ce_rows;
+    any_dpg |= !ce;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const int j = tid + 256 * c;
+      if (j >= H) continue;
+      const float dz = rs * (g[r][c] - m1 - xh[r][c] * m2);
+      float* cell = act[cur] + r * kRBStride + j;
+      if (ce) {
+        const float dyv = *cell;
+        a.dz[0][(size_t)row * H + j] = dz;
+        cs_x[c] = fmaf(dyv, xh[r][c], cs_x[c]);
+        cs_1[c] += dyv;
+      } else {
+        *cell = dz;  // the dpg row's dz, for dq/da below (this thread's cell only)
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const int j = tid + 256 * c;
+    if (j < H) {
+      a.colslab[((size_t)blockIdx.x * 2 + 0) * H + j] = cs_x[c];
+      a.colslab[((size_t)blockIdx.x * 2 + 1) * H + j] = cs_1[c];
+    }
+  }
+  if (!a.ploss_part) return;
+  if (!__syncthreads_or(any_dpg)) {
+    if (tid == 0) a.ploss_part[blockIdx.x] = 0.f;
+    return;
+  }
+  // dq/da = dz @ W1[action rows]^T of each dpg row: one wave per row.
+  for (int r = wave; r < kRB; r += 4) {
+    const int row = r0 + r;
+    if (row >= a.rows || row < a.ce_rows) continue;  // wave-uniform
+    for (int k = 0; k < a.A; ++k) {
+      float v = 0.f;
+      for (int j = lane; j < H; j += 64)
+        v = fmaf(act[cur][r * kRBStride + j], a.w1[(size_t)(a.act_off + k) * H + j], v);
+      v = wave_sum(v);
+      if (lane == 0) dq_s[r][k] = v;
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {
+    float pl = 0.f;
+    if (tid < kRB) {
+      const int row = r0 + tid;
+      if (row < a.rows && row >= a.ce_rows) {
+        const int b = row - a.ce_rows;
+        float n2 = 0.f;
+        for (int k = 0; k < a.A; ++k) n2 = fmaf(dq_s[tid][k], dq_s[tid][k], n2);
+        const float nrm = n2 > 0.f ? sqrtf(n2) : 0.f;
+        const float den = a.clip > 0.f ? fmaxf(nrm, a.clip) : 1.f;
+        const float cm = a.clip > 0.f ? a.clip : 1.f;
+        for (int k = 0; k < a.A; ++k) {
+          const float dq = (dq_s[tid][k] * cm) / den;
+          a.dqda[(size_t)b * a.A + k] = dq;
+          pl = fmaf(0.5f * dq, dq, pl);
+          const float tk = a.t[(size_t)b * a.A + k];
+          const float da = -dq * a.invB;
+          a.du[(size_t)b * a.A + k] = da * a.act_scale[k] * 0.5f * (1.f - tk * tk);
+        }
+      }
+    }
+    pl = wave_sum(pl);
+    if (tid == 0) a.ploss_part[blockIdx.x] = pl;
   }
 }
 
@@ -1132,7 +1353,7 @@ void add_dgrad(BwdGroup& g, const float* dz, int rows, int Nout, const float* w,
   }
 }
 
-constexpr int kZ = 3;  // sub-problems of one type per backward launch
+constexpr int kZ = 4;  // sub-problems of one type per backward launch
 
 template <class Q>
 bool fill_zset(gemm::ZSet<Q, kZ>& z, int& n, const std::vector<Q>& qs, int& tiles, int& count,
@@ -1291,9 +1512,12 @@ int ln_backward(acme_d4pg* l, const NetDesc& d, const Acts& a, float* dy, int ro
   return ACME_OK;
 }
 
+int clip_adam_step(acme_d4pg* l, const acme_d4pg_outputs* out, int nploss, hipStream_t st);
+
 int d4pg_step_impl(acme_d4pg* l, const acme_d4pg_batch* bt, const acme_d4pg_outputs* out,
                    bool copy_target, hipStream_t st) {
   const int B = (int)bt->batch;
+  l->cur_B = B;
   const int od = l->cfg.obs_dim, ad = l->cfg.act_dim;
   const NetDesc& pd = l->pol;
   const NetDesc& cd = l->cri;
@@ -1322,10 +1546,63 @@ int d4pg_step_impl(acme_d4pg* l, const acme_d4pg_batch* bt, const acme_d4pg_outp
         l->dlogits, l->ce);
     D4_CHECK();
   }
-  // Critic backward: 2B rows of input gradients (CE rows + dpg rows), weight gradients from
-  // the first B.  Launch k carries layer k's input gradient and weight gradient.
   BwdGroup g;
   std::vector<LnReduce> ln;
+  if (l->rows_fwd && rows_fit(cd, od + ad, false) && rows_fit(pd, od, true)) {
+    // Row-blocked input-gradient chains (critic, then the policy from its du), then every
+    // weight gradient of both networks in one launch.
+    static hipError_t attr = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&lnmlp_bwd_rows_kernel),
+        hipFuncAttributeMaxDynamicSharedMemorySize, kRBLds);
+    if (attr != hipSuccess)
+      return (set_error("LDS attribute: %s", hipGetErrorString(attr)), ACME_ERR_HIP);
+    for (int net = 0; net < 2; ++net) {
+      const bool critic = net == 0;
+      const NetDesc& d = critic ? cd : pd;
+      const Acts& ac = critic ? l->con : l->pon;
+      const int rows = critic ? 2 * B : B;
+      RowBwdArgs r;
+      r.dtop = critic ? l->dlogits : l->du;
+      r.nout = d.nout;
+      r.ow = P(l, l->params, d.ow);
+      for (int li = 0; li < d.nl; ++li) {
+        if (li >= 1) r.w[li] = P(l, l->params, d.w[li]);
+        r.h[li] = ac.h[li];
+        r.dz[li] = critic ? l->cdz[li] : l->pdz[li];
+        r.sizes[li] = d.sizes[li];
+      }
+      r.z1 = ac.z1; r.mean = ac.mean; r.rstd = ac.rstd; r.scale = P(l, l->params, d.scale);
+      r.rows = rows; r.ce_rows = B; r.nl = d.nl;
+      r.colslab = critic ? l->lnslab : l->lnslab2;
+      r.w1 = P(l, l->params, d.w1); r.act_off = od; r.A = ad;
+      r.clip = l->cfg.clipping ? 1.f : 0.f; r.invB = 1.f / (float)B;
+      r.t = l->pon.t; r.act_scale = l->act_scale;
+      r.du = l->du; r.dqda = l->dqda; r.ploss_part = critic ? l->ploss_part : nullptr;
+      const int nblk = (int)ceil_div(rows, kRB);
+      ACME_PROF(critic ? "d4pg_critic_bwd" : "d4pg_policy_bwd", st, 0.0, 0.0);
+      lnmlp_bwd_rows_kernel<<<(unsigned)nblk, 256, kRBLds, st>>>(r);
+      D4_CHECK();
+      ln.push_back({r.colslab, nblk, d.sizes[0], Pm(l, l->grads, d.scale),
+                    Pm(l, l->grads, d.offset)});
+      const int L = d.nl - 1;
+      add_wgrad(g, ac.h[L], B, d.sizes[L], r.dtop, d.nout, Pm(l, l->grads, d.ow),
+                Pm(l, l->grads, d.ob));
+      for (int li = d.nl - 1; li >= 1; --li)
+        add_wgrad(g, ac.h[li - 1], B, d.sizes[li - 1], r.dz[li], d.sizes[li],
+                  Pm(l, l->grads, d.w[li]), Pm(l, l->grads, d.b[li]));
+      ConcatWgrad p;
+      p.M = critic ? od + ad : od; p.N = d.sizes[0]; p.K = B; p.k_chunk = B;
+      p.x0 = critic ? bt->o_tm1 : bt->o_t; p.d0 = od;
+      p.x1 = critic ? bt->a_tm1 : nullptr; p.d1 = critic ? ad : 0;
+      p.dz = r.dz[0];
+      p.out = Pm(l, l->grads, d.w1); p.bias_out = Pm(l, l->grads, d.b1);
+      g.first.push_back(p);
+    }
+    if ((rc = launch_bwd("d4pg_wgrads", g, st)) || (rc = run_ln_reduces(ln, st))) return rc;
+    return clip_adam_step(l, out, (int)ceil_div(2 * B, kRB), st);
+  }
+  // Critic backward: 2B rows of input gradients (CE rows + dpg rows), weight gradients from
+  // the first B.  Launch k carries layer k's input gradient and weight gradient.
   const int cL = cd.nl - 1;
   add_wgrad(g, l->con.h[cL], B, cd.sizes[cL], l->dlogits, cd.nout, Pm(l, l->grads, cd.ow),
             Pm(l, l->grads, cd.ob));
@@ -1347,7 +1624,13 @@ int d4pg_step_impl(acme_d4pg* l, const acme_d4pg_batch* bt, const acme_d4pg_outp
                         l->lnslab2, g, ln, st)) ||
       (rc = launch_bwd("d4pg_wgrad_first", g, st)) || (rc = run_ln_reduces(ln, st)))
     return rc;
-  // Global-norm clipping + Adam (t = steps taken including this one).
+  return clip_adam_step(l, out, (int)ceil_div(2 * B, kRows), st);
+}
+
+// Global-norm clipping + Adam (t = steps taken including this one); nploss = the policy-loss
+// partials the dpg rows' LayerNorm backward wrote.
+int clip_adam_step(acme_d4pg* l, const acme_d4pg_outputs* out, int nploss, hipStream_t st) {
+  const int B = l->cur_B;
   {
     ACME_PROF("d4pg_adam", st, 0.0, 7.0 * 4.0 * (double)l->flat);
     const int64_t n4 = l->flat / 4, pol4 = l->policy_flat / 4;
@@ -1360,7 +1643,7 @@ int d4pg_step_impl(acme_d4pg* l, const acme_d4pg_batch* bt, const acme_d4pg_outp
     a.lr0 = l->cfg.policy_learning_rate; a.lr1 = l->cfg.critic_learning_rate;
     a.b1 = l->cfg.adam_beta1; a.b2 = l->cfg.adam_beta2; a.eps = l->cfg.adam_epsilon;
     a.dev_step = l->dev_step; a.norms = l->norms;
-    a.sum_a = l->ploss_part; a.n_a = (int)ceil_div(2 * B, kRows); a.div_a = (float)B;
+    a.sum_a = l->ploss_part; a.n_a = nploss; a.div_a = (float)B;
     a.out_a = out && out->policy_loss ? out->policy_loss : l->loss_tmp + 1;
     a.sum_b = l->ce; a.n_b = B; a.div_b = (float)B;
     a.out_b = out && out->critic_loss ? out->critic_loss : l->loss_tmp;
