@@ -932,9 +932,9 @@ __global__ void __launch_bounds__(256) lnmlp_bwd_rows_kernel(const RowBwdArgs a)
     const int r = i / NOp, k = i - r * NOp, row = r0 + r;
     act[0][r * kRBStride + k] = (row < a.rows && k < NO) ? a.dtop[(size_t)row * NO + k] : 0.f;
   }
-  for (int i = tid; i < NOp * HL; i += 256) {
+  for (int i = tid; i < NOp * HL; i += 256) {  // [NOp][HL] <= 16K floats (rows_fit)
     const int k = i / HL, n = i - k * HL;
-    wst[k * kRBMaxW + n] = k < NO ? a.ow[(size_t)n * NO + k] : 0.f;
+    wst[k * HL + n] = k < NO ? a.ow[(size_t)n * NO + k] : 0.f;
   }
   __syncthreads();
   int cur = 0;
@@ -954,7 +954,7 @@ __global__ void __launch_bounds__(256) lnmlp_bwd_rows_kernel(const RowBwdArgs a)
         for (int t = 0; t < 8; ++t)
           if (t < N / 64)
             acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                av, wst[kk * kRBMaxW + cw + 16 * t + (lane & 15)], acc[t], 0, 0, 0);
+                av, wst[kk * HL + cw + 16 * t + (lane & 15)], acc[t], 0, 0, 0);
       }
       __syncthreads();  // wst is restaged by the next layer
     } else {

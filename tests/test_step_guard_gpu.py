@@ -15,11 +15,11 @@ sets the next step's scales from the skipped step's true maxima.
     bar, Adam at t = 2: the skipped step did not count).
   * test_long_horizon_drift: 100 free-running steps at B = 64 (and 20 at the headline
     B = 512) from identical batches on the plane engine, on the exact-f32 engine
-    (acme_set_matmul_engine(ACME_MATMUL_F32)), on torch float32 and on the float64 torch
-    restatement (oracle/dqn_torch.py on the GPU, the reference trajectory).  The plane
-    engine skips no step, and its divergence from the f64 trajectory (parameters, relative
-    to how far training moved them; the loss trajectory's maximum and median relative
-    error) is within 2x the worse float32 implementation's (PLANE_FACTOR).
+    (acme_set_matmul_engine(ACME_MATMUL_F32)) and on the float64 torch restatement
+    (oracle/dqn_torch.py on the GPU, the reference trajectory).  The plane engine skips no
+    step; its parameter drift from the f64 trajectory is within 2x (B = 512) / 3x (B = 64)
+    the f32 engine's, and its loss trajectory within 2x the f32 engine's at B = 512 and
+    under stated bounds at B = 64 (see the test).
   * test_underflow_only_skip_writes_no_priority / test_skipped_step_makes_no_target_copy:
     a skip decided by the rescale alone writes no priority on the fused path; a target copy
     due on a skipped step is not made.
@@ -44,14 +44,8 @@ from oracle import dqn_oracle as O
 pytestmark = pytest.mark.gpu
 
 HEAD = ("duelling_q_network/mlp/linear_1/w", "duelling_q_network/mlp_1/linear_1/w")
-# Free-running divergence from the f64 trajectory (parameters, loss maximum and median)
-# relative to the worse of two float32 implementations (the exact-f32 engine, torch
-# float32).  Measured (round 5, profiles/r05/drift/): B = 64 x 100: drift plane 0.152,
-# f32 engine 0.065, torch f32 0.160; loss max 0.749 / 0.062 / 0.749, median 0.064 / 0.0035 /
-# 0.053.  B = 512 x 20: drift 0.060 / 0.063 / 0.065, loss max 0.251 / 0.250 / 0.250.  A
-# build with -DP3_FOUR_TERMS=1 (the l*l term) leaves these unchanged (0.154 drift, 0.749 /
-# 0.063 loss at B = 64) and costs 5 % step time, so three terms stay.
-PLANE_FACTOR = 2.0
+# A build with -DP3_FOUR_TERMS=1 (the l*l term) leaves the free-running numbers unchanged
+# (drift 0.154, loss 0.749 / 0.063 at B = 64; profiles/r05/drift/) and costs 5 % of the step.
 
 
 def _dev(batch):
@@ -334,25 +328,26 @@ def _teacher_forced(d, params, target, b, B):
     _check_grads(d.get_params("grads"), grads)
 
 
-@pytest.mark.parametrize("B,steps,checks", [(64, 100, (0, 33, 66, 99)), (512, 20, (0, 19))])
-def test_long_horizon_drift(B, steps, checks):
-    """Free-running trajectories (each side applies its own gradients) from identical batches:
-    the plane engine, the exact-f32 engine, an independent float32 implementation (the torch
-    restatement oracle/dqn_torch.py in float32 on the GPU: MIOpen convolutions, rocBLAS
-    GEMMs, i.e. what the reference's own float32 TF learner is) and the float64 reference
-    trajectory.  Asserted (PLANE_FACTOR = 2): the plane engine skips no step; its first two
-    losses match float64 at the north star's 1e-5; its parameter drift from the float64
-    trajectory (relative to how far training moved the parameters) and its loss trajectory's
-    maximum and median relative error are within PLANE_FACTOR x those of the worse of the
-    two float32 implementations.  (Against the exact-f32 engine alone the B = 64 case does
-    not hold: that engine stays unusually close to float64 (drift 0.065, median loss error
-    3.5e-3) where torch float32 drifts as far as the plane engine (0.160 / 5.3e-2 against
-    0.152 / 6.4e-2; profiles/r05/drift/): free-running training is chaotic (Adam's normalised
-    steps flip on near-zero gradients, double-Q argmax ties flip), so any float32 rounding
-    difference grows to this size.)  At the `checks` steps the plane engine's step is also
-    checked teacher-forced against the f64 oracle from its own pre-step state (loss and TD at
-    1e-5, the suite's gradient bar), so per-step accuracy does not degrade as the scales
-    follow training."""
+@pytest.mark.parametrize("B,steps,checks,drift_f,loss_max,loss_med",
+                         [(64, 100, (0, 33, 66, 99), 3.0, 1.0, 0.1),
+                          (512, 20, (0, 19), 2.0, None, None)])
+def test_long_horizon_drift(B, steps, checks, drift_f, loss_max, loss_med):
+    """Free-running trajectories (each side applies its own gradients) of the plane engine
+    and the exact-f32 engine from identical batches, against the float64 torch restatement
+    (oracle/dqn_torch.py on the GPU, the reference trajectory).  Asserted: the plane engine
+    skips no step; its first two losses match float64 at the north star's 1e-5; its
+    parameter drift from the float64 trajectory (relative to how far training moved the
+    parameters) is within drift_f x the f32 engine's; its loss trajectory (relative error
+    per step): at the headline batch (B = 512 x 20) maximum and median within 2x the f32
+    engine's, at B = 64 x 100 maximum <= loss_max and median <= loss_med.  (Measured, round
+    5, profiles/r05/drift/: B = 512: drift 0.060 against 0.063, loss max 0.251 / 0.250,
+    median 0.0081 / 0.0079; B = 64: drift 0.152 against 0.065 and loss max / median 0.749 /
+    0.064 against 0.062 / 0.0035 -- at small batches the plane engine leaves the float64
+    trajectory faster than the exact-f32 engine, from its first step's conv weight gradients
+    (7x the f32 engine's error).)  At the `checks` steps the plane engine's
+    step is also checked teacher-forced against the f64 oracle from its own pre-step state
+    (loss and TD at 1e-5, the suite's gradient bar), so per-step accuracy does not degrade as
+    the scales follow training."""
     from acme_amd._lib import lib
     from acme_amd.native import NativeDQN
     from acme_amd.networks import DQNAtariNetwork
@@ -365,18 +360,16 @@ def test_long_horizon_drift(B, steps, checks):
         for _ in range(steps):
             yield _batch(rng, B, 18)
 
-    def torch_run(dtype):
-        t = TorchDQN(p0, 18, target=t0, dtype=dtype, device="cuda")
-        losses = []
-        for b in batches():
-            dev = {k: torch.as_tensor(b[k]).cuda() for k in ("o_tm1", "a_tm1", "r_t", "d_t", "o_t")}
-            loss, _ = t.step(dev["o_tm1"], dev["a_tm1"], dev["r_t"].to(dtype),
-                             dev["d_t"].to(dtype), dev["o_t"], b["probabilities"])
-            losses.append(loss)
-        return np.array(losses), {k: v.detach().cpu().numpy() for k, v in t.p.items()}
-
-    ref_loss, ref_p = torch_run(torch.float64)   # the reference trajectory
-    t32_loss, t32_p = torch_run(torch.float32)   # an independent float32 learner
+    # The float64 reference trajectory (torch on the GPU).
+    ref = TorchDQN(p0, 18, target=t0, dtype=torch.float64, device="cuda")
+    ref_loss = []
+    for b in batches():
+        dev = {k: torch.as_tensor(b[k]).cuda() for k in ("o_tm1", "a_tm1", "r_t", "d_t", "o_t")}
+        loss, _ = ref.step(dev["o_tm1"], dev["a_tm1"], dev["r_t"].double(), dev["d_t"].double(),
+                           dev["o_t"], b["probabilities"])
+        ref_loss.append(loss)
+    ref_p = {k: v.detach().cpu().numpy() for k, v in ref.p.items()}
+    ref_loss = np.array(ref_loss)
 
     def run(engine, check=()):
         lib().acme_set_matmul_engine(engine)
@@ -404,17 +397,19 @@ def test_long_horizon_drift(B, steps, checks):
     # The first steps match the f64 trajectory at the north star's 1e-5.
     np.testing.assert_allclose(plane_loss[:2], ref_loss[:2], rtol=1e-5)
     np.testing.assert_allclose(f32_loss[:2], ref_loss[:2], rtol=1e-5)
-    drift = {k: _rel(p, ref_p, p0) for k, p in (("plane", plane_p), ("f32", f32_p),
-                                                ("torch32", t32_p))}
-    err = {k: np.abs(x - ref_loss) / np.abs(ref_loss)
-           for k, x in (("plane", plane_loss), ("f32", f32_loss), ("torch32", t32_loss))}
-    print(f"B={B} steps={steps}: parameter drift " +
-          " ".join(f"{k} {v:.3e}" for k, v in drift.items()) + "; loss rel err max / median " +
-          " ".join(f"{k} {e.max():.3e} / {np.median(e):.3e}" for k, e in err.items()))
-    worst = lambda f: max(f("f32"), f("torch32"))  # noqa: E731
-    assert drift["plane"] <= PLANE_FACTOR * worst(drift.get) + 1e-5, drift
-    assert err["plane"].max() <= PLANE_FACTOR * worst(lambda k: err[k].max()) + 1e-5
-    assert np.median(err["plane"]) <= PLANE_FACTOR * worst(lambda k: np.median(err[k])) + 1e-6
+    d_plane, d_f32 = _rel(plane_p, ref_p, p0), _rel(f32_p, ref_p, p0)
+    e_plane = np.abs(plane_loss - ref_loss) / np.abs(ref_loss)
+    e_f32 = np.abs(f32_loss - ref_loss) / np.abs(ref_loss)
+    print(f"B={B} steps={steps}: parameter drift plane {d_plane:.3e} f32 {d_f32:.3e}; loss rel "
+          f"err max / median plane {e_plane.max():.3e} / {np.median(e_plane):.3e} f32 "
+          f"{e_f32.max():.3e} / {np.median(e_f32):.3e}")
+    assert d_plane <= drift_f * d_f32 + 1e-5, (d_plane, d_f32)
+    if loss_max is None:  # the headline batch: within 2x the f32 engine's loss trajectory
+        assert e_plane.max() <= 2.0 * e_f32.max() + 1e-5, (e_plane.max(), e_f32.max())
+        assert np.median(e_plane) <= 2.0 * np.median(e_f32) + 1e-6
+    else:
+        assert e_plane.max() <= loss_max and np.median(e_plane) <= loss_med, (
+            e_plane.max(), np.median(e_plane))
 
 
 def test_impala_timeout_skips_update():
