@@ -97,9 +97,6 @@ struct acme_replay {
   } readers[kMaxReaders] = {};
   int nreaders = 0;
   std::mutex order_mu;
-  // Gather kernel variants fixed at creation (tests compare them bit for bit): ACME_V_GATH
-  // 0 = transition pair / pieces (default), 1 = row per workgroup, 2 = wave pieces;
-  // ACME_V_GATHG: the pieces grid cap; ACME_V_SGF=1: sample_gather as two launches.
 };
 
 namespace {
