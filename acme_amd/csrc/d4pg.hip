@@ -109,10 +109,6 @@ struct acme_d4pg {
   };
   std::vector<Graph> graphs;
   hipStream_t capture = nullptr;
-  // The forwards as one row-blocked launch per pass, the input-gradient chains likewise
-  // (ACME_V_D4L=1: the per-layer launches, the round-4 path).
-  bool rows_fwd = true;
-  int cur_B = 0;  // the batch of the step being issued
 };
 
 namespace {
@@ -614,480 +610,6 @@ struct ConcatWgrad {
   __device__ void store_colsum(int n, float v, int) const { bias_out[n] = v; }
 };
 
-__device__ __forceinline__ int act_of_layer_dev(int i) { return i == 0 ? ACT_TANH : ACT_ELU; }
-
-// ------------------------------------------------------------------ row-blocked forward
-// One launch per network pass (round 5): a workgroup carries kRB rows of one evaluation
-// (blockIdx.y: the online / target network) through every layer -- the LayerNorm first
-// layer (the arithmetic of ln_first_kernel, so the same bits), the ELU layers on the f32
-// MFMA (v_mfma_f32_16x16x4_f32: exact f32 products, f32 accumulation; 16 output columns per
-// wave tile), the head -- with the rows' activations in LDS and each layer's weights
-// streamed through LDS in kRBKc-row chunks (double buffered: the next chunk's loads are in
-// flight while the current one is multiplied).  The rows are independent, so no grid
-// synchronisation is needed; every activation the backward reads (z1, mean, rstd, each h,
-// the head outputs) is written as the per-layer launches wrote it.  Replaces the 4 launches
-// of a pass (ln_first, two dense layers, the head), whose bodies were latency-bound.
-constexpr int kRB = 16;       // rows per workgroup (the MFMA's M)
-constexpr int kRBMaxW = 512;  // widest layer
-constexpr int kRBStride = kRBMaxW + 4;
-constexpr int kRBKc = 16;     // weight rows per staged chunk
-constexpr int kRBLds = (kRB * kMaxIn + 2 * kRB * kRBStride + 2 * kRBKc * kRBMaxW) * 4;
-struct RowNetArgs {
-  const float *xa0, *xb0, *xa1, *xb1;
-  int split, rows;
-  const float *w1, *b1, *scale, *offset;
-  const float* w[ACME_D4PG_MAX_LAYERS];
-  const float* b[ACME_D4PG_MAX_LAYERS];
-  const float *ow, *ob;
-  float *z1, *mean, *rstd;
-  float* h[ACME_D4PG_MAX_LAYERS];
-  float *out, *t;
-};
-struct RowNetPair {
-  RowNetArgs a[2];
-  int da, db, nl, nout, policy;
-  int sizes[ACME_D4PG_MAX_LAYERS];
-  float eps;
-  const float *lo, *ascale;  // policy: TanhToSpec
-};
-
-// out[kRB rows][N] = ain[kRB][K] @ B on the f32 MFMA, N a multiple of 64 (<= 512), K of
-// kRBKc; wave w owns columns [w N / 4, (w + 1) N / 4).  B = W [K][N] (row stride ldw), or with
-// TRANS B = W^T for W [N][K] (row stride ldw: an input gradient's dZ @ W^T), staged through
-// wst in kRBKc-row chunks ([k][n] either way).  acc[t] = the wave's 16-column tile t
-// (D[4 (lane / 16) + j][lane % 16]).
-template <bool TRANS = false>
-__device__ __forceinline__ void rb_matmul(const float* __restrict__ ain, const float* __restrict__ W,
-                                          int ldw, int K, int N, float* wst, f32x4 (&acc)[8]) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int ntw = N / 64, cw = wave * (N / 4), n4 = N / 4;
-  const int per = N / 64;  // float4 per thread per chunk (kRBKc * N / 4 / 256)
-#pragma unroll
-  for (int t = 0; t < 8; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 st[8];
-  auto load = [&](int c) {
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (u < per) {
-        const int idx = tid + 256 * u;
-        if constexpr (TRANS) {  // W[n][c kRBKc + 4 q .. + 3]: 4 float4 per n
-          const int n = idx >> 2, q = idx & 3;
-          st[u] = *reinterpret_cast<const f32x4*>(W + (size_t)n * ldw + c * kRBKc + 4 * q);
-        } else {
-          const int row = idx / n4, c4 = idx - row * n4;
-          st[u] = *reinterpret_cast<const f32x4*>(W + (size_t)(c * kRBKc + row) * ldw + 4 * c4);
-        }
-      }
-  };
-  auto store = [&](int buf) {
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (u < per) {
-        const int idx = tid + 256 * u;
-        if constexpr (TRANS) {
-          const int n = idx >> 2, q = idx & 3;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) wst[(buf * kRBKc + 4 * q + e) * kRBMaxW + n] = st[u][e];
-        } else {
-          const int row = idx / n4, c4 = idx - row * n4;
-          *reinterpret_cast<f32x4*>(wst + (buf * kRBKc + row) * kRBMaxW + 4 * c4) = st[u];
-        }
-      }
-  };
-  const int nch = K / kRBKc;
-  load(0);
-  store(0);
-  __syncthreads();
-  for (int c = 0; c < nch; ++c) {
-    if (c + 1 < nch) load(c + 1);
-    const float* wb = wst + (c & 1) * kRBKc * kRBMaxW;
-#pragma unroll
-    for (int s = 0; s < kRBKc / 4; ++s) {
-      const int kk = 4 * s + (lane >> 4);
-      const float av = ain[(lane & 15) * kRBStride + c * kRBKc + kk];
-#pragma unroll
-      for (int t = 0; t < 8; ++t)
-        if (t < ntw)
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-              av, wb[kk * kRBMaxW + cw + 16 * t + (lane & 15)], acc[t], 0, 0, 0);
-    }
-    if (c + 1 < nch) store((c + 1) & 1);
-    __syncthreads();
-  }
-}
-
-__global__ void __launch_bounds__(256) lnmlp_rows_kernel(const RowNetPair pr) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* xs = sm;                                // [kRB][kMaxIn]
-  float* act[2] = {xs + kRB * kMaxIn, xs + kRB * kMaxIn + kRB * kRBStride};
-  float* wst = act[1] + kRB * kRBStride;         // [2][kRBKc][kRBMaxW]
-  __shared__ float red[4][kRB];
-  const RowNetArgs& a = pr.a[blockIdx.y];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r0 = blockIdx.x * kRB;
-  if (r0 >= a.rows) return;  // uniform per block
-  const int din = pr.da + pr.db, H = pr.sizes[0];
-  for (int i = tid; i < kRB * din; i += 256) {
-    const int r = i / din, k = i - r * din, row = r0 + r;
-    float v = 0.f;
-    if (row < a.rows) {
-      const bool second = row >= a.split;
-      const int rr = second ? row - a.split : row;
-      v = k < pr.da ? (second ? a.xa1 : a.xa0)[(size_t)rr * pr.da + k]
-                    : (second ? a.xb1 : a.xb0)[(size_t)rr * pr.db + (k - pr.da)];
-    }
-    xs[r * kMaxIn + k] = v;
-  }
-  __syncthreads();
-  // ---- LayerNorm first layer (ln_first_kernel's arithmetic, kRB rows).
-  {
-    constexpr int C = kRBMaxW / 256;
-    float acc[kRB][C];
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const int j = tid + 256 * c;
-#pragma unroll
-      for (int r = 0; r < kRB; ++r) acc[r][c] = 0.f;
-      if (j < H) {
-        for (int k = 0; k < din; ++k) {
-          const float wk = a.w1[(size_t)k * H + j];
-#pragma unroll
-          for (int r = 0; r < kRB; ++r) acc[r][c] = fmaf(xs[r * kMaxIn + k], wk, acc[r][c]);
-        }
-        const float bj = a.b1[j];
-#pragma unroll
-        for (int r = 0; r < kRB; ++r) acc[r][c] += bj;
-      }
-    }
-    float sq[kRB];
-#pragma unroll
-    for (int r = 0; r < kRB; ++r) {
-      sq[r] = 0.f;
-#pragma unroll
-      for (int c = 0; c < C; ++c)
-        if (tid + 256 * c < H) sq[r] += acc[r][c];
-    }
-    block_sum256<kRB>(sq, red);
-    const float invH = 1.f / (float)H;
-    float mean[kRB];
-#pragma unroll
-    for (int r = 0; r < kRB; ++r) {
-      mean[r] = sq[r] * invH;
-      float q = 0.f;
-#pragma unroll
-      for (int c = 0; c < C; ++c)
-        if (tid + 256 * c < H) {
-          const float dv = acc[r][c] - mean[r];
-          q = fmaf(dv, dv, q);
-        }
-      sq[r] = q;
-    }
-    block_sum256<kRB>(sq, red);
-#pragma unroll
-    for (int r = 0; r < kRB; ++r) {
-      const int row = r0 + r;
-      const bool live = row < a.rows;
-      const float rs = 1.f / sqrtf(sq[r] * invH + pr.eps);
-#pragma unroll
-      for (int c = 0; c < C; ++c) {
-        const int j = tid + 256 * c;
-        if (j >= H) continue;
-        const float hv = tanhf((acc[r][c] - mean[r]) * rs * a.scale[j] + a.offset[j]);
-        act[0][r * kRBStride + j] = live ? hv : 0.f;
-        if (live) {
-          const size_t idx = (size_t)row * H + j;
-          a.z1[idx] = acc[r][c];
-          a.h[0][idx] = hv;
-        }
-      }
-      if (live && tid == 0) {
-        a.mean[row] = mean[r];
-        a.rstd[row] = rs;
-      }
-    }
-  }
-  __syncthreads();
-  // ---- ELU layers.
-  int cur = 0;
-  for (int li = 1; li < pr.nl; ++li) {
-    const int K = pr.sizes[li - 1], N = pr.sizes[li];
-    f32x4 acc[8];
-    rb_matmul<false>(act[cur], a.w[li], N, K, N, wst, acc);
-    const int cw = wave * (N / 4);
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      if (t >= N / 64) break;
-      const int col = cw + 16 * t + (lane & 15);
-      const float bv = a.b[li][col];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int r = 4 * (lane >> 4) + j, row = r0 + r;
-        const float v = act_fwd(ACT_ELU, acc[t][j] + bv);
-        act[cur ^ 1][r * kRBStride + col] = row < a.rows ? v : 0.f;
-        if (row < a.rows) a.h[li][(size_t)row * N + col] = v;
-      }
-    }
-    cur ^= 1;
-    __syncthreads();
-  }
-  const float* hl = act[cur];
-  const int HL = pr.sizes[pr.nl - 1];
-  if (pr.policy) {
-    // TanhToSpec head: one wave per row (policy_head_kernel's arithmetic).
-    const int A = pr.nout;
-    for (int r = wave; r < kRB; r += 4) {
-      const int row = r0 + r;
-      if (row >= a.rows) break;
-      float acc[ACME_D4PG_MAX_ACT];
-#pragma unroll
-      for (int j = 0; j < ACME_D4PG_MAX_ACT; ++j) acc[j] = 0.f;
-      for (int k = lane; k < HL; k += 64) {
-        const float hv = hl[r * kRBStride + k];
-#pragma unroll
-        for (int j = 0; j < ACME_D4PG_MAX_ACT; ++j)
-          if (j < A) acc[j] = fmaf(hv, a.ow[(size_t)k * A + j], acc[j]);
-      }
-      float mine = 0.f;
-#pragma unroll
-      for (int j = 0; j < ACME_D4PG_MAX_ACT; ++j) {
-        if (j >= A) break;
-        const float sv = wave_sum(acc[j]);
-        if (lane == j) mine = sv;
-      }
-      if (lane < A) {
-        const float t = tanhf(mine + a.ob[lane]);
-        if (a.t) a.t[(size_t)row * A + lane] = t;
-        a.out[(size_t)row * A + lane] = (0.5f * (t + 1.f)) * pr.ascale[lane] + pr.lo[lane];
-      }
-    }
-    return;
-  }
-  // Linear head (the critic's logits, nout <= 64): W staged zero-padded to 64 columns.
-  const int NO = pr.nout;
-  for (int i = tid; i < HL * 64; i += 256) {
-    const int k = i >> 6, n = i & 63;
-    wst[i] = n < NO ? a.ow[(size_t)k * NO + n] : 0.f;
-  }
-  __syncthreads();
-  f32x4 acc{0.f, 0.f, 0.f, 0.f};
-  const int col = 16 * wave + (lane & 15);
-  for (int k0 = 0; k0 < HL; k0 += 4) {
-    const int kk = k0 + (lane >> 4);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(hl[(lane & 15) * kRBStride + kk], wst[kk * 64 + col],
-                                               acc, 0, 0, 0);
-  }
-  if (col < NO) {
-    const float bv = a.ob[col];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int row = r0 + 4 * (lane >> 4) + j;
-      if (row < a.rows) a.out[(size_t)row * NO + col] = acc[j] + bv;
-    }
-  }
-}
-
-// ------------------------------------------------------------------ row-blocked backward
-// The input-gradient chain of one network pass in one launch (round 5): a workgroup takes
-// kRB rows from the head's pre-activation gradient (the critic's dlogits, the policy's du)
-// down to the LayerNorm input -- dZ @ W^T on the f32 MFMA with the activation derivatives
-// from the forward's outputs, the LayerNorm backward (ln_bwd_kernel's arithmetic for kRB
-// rows, with its column partials and, for the critic's dpg rows, dq/da, clip_by_norm, du
-// and the policy-loss partials) -- keeping the rows' gradients in LDS; every dZ the weight
-// gradients read is written.  Replaces the chain of per-layer input-gradient launches.
-struct RowBwdArgs {
-  const float* dtop;  // [rows][nout] gradient at the head's pre-activation
-  int nout;
-  const float* ow;    // head weight [HL][nout]
-  const float* w[ACME_D4PG_MAX_LAYERS];  // mlp weights [sizes[li-1]][sizes[li]]
-  const float* h[ACME_D4PG_MAX_LAYERS];  // forward outputs
-  float* dz[ACME_D4PG_MAX_LAYERS];       // pre-activation gradients (dz[0]: LayerNorm input)
-  const float *z1, *mean, *rstd, *scale;
-  int rows, ce_rows, nl;
-  int sizes[ACME_D4PG_MAX_LAYERS];
-  float* colslab;  // [gridDim.x][2][H0]
-  // dpg rows (rows >= ce_rows; the critic)
-  const float* w1;
-  int act_off, A;
-  float clip, invB;
-  const float *t, *act_scale;
-  float *du, *dqda, *ploss_part;
-};
-
-__global__ void __launch_bounds__(256) lnmlp_bwd_rows_kernel(const RowBwdArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float smb[];
-  float* base = smb + kRB * kMaxIn;
-  float* act[2];
-  act[0] = base;
-  act[1] = base + kRB * kRBStride;
-  float* wst = act[1] + kRB * kRBStride;
-  __shared__ float red[4][2 * kRB];
-  __shared__ float dq_s[kRB][ACME_D4PG_MAX_ACT];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r0 = blockIdx.x * kRB;
-  if (r0 >= a.rows) return;  // uniform per block
-  const int NO = a.nout, NOp = (NO + 3) & ~3;
-  const int HL = a.sizes[a.nl - 1];
-  // The head's gradient rows (zero-padded to a multiple of 4 columns) and its weight^T.
-  for (int i = tid; i < kRB * NOp; i += 256) {
-    const int r = i / NOp, k = i - r * NOp, row = r0 + r;
-    act[0][r * kRBStride + k] = (row < a.rows && k < NO) ? a.dtop[(size_t)row * NO + k] : 0.f;
-  }
-  for (int i = tid; i < NOp * HL; i += 256) {  // [NOp][HL] <= 16K floats (rows_fit)
-    const int k = i / HL, n = i - k * HL;
-    wst[k * HL + n] = k < NO ? a.ow[(size_t)n * NO + k] : 0.f;
-  }
-  __syncthreads();
-  int cur = 0;
-  // Layer li's input gradient: dz[li - 1] = act'(h[li - 1]) * (dz[li] @ W_li^T); li = nl: the
-  // head (its weight staged above).
-  for (int li = a.nl; li >= 1; --li) {
-    const int N = a.sizes[li - 1];
-    f32x4 acc[8];
-    if (li == a.nl) {
-#pragma unroll
-      for (int t = 0; t < 8; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const int cw = wave * (N / 4);
-      for (int k0 = 0; k0 < NOp; k0 += 4) {
-        const int kk = k0 + (lane >> 4);
-        const float av = act[cur][(lane & 15) * kRBStride + kk];
-#pragma unroll
-        for (int t = 0; t < 8; ++t)
-          if (t < N / 64)
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                av, wst[kk * HL + cw + 16 * t + (lane & 15)], acc[t], 0, 0, 0);
-      }
-      __syncthreads();  // wst is restaged by the next layer
-    } else {
-      rb_matmul<true>(act[cur], a.w[li], a.sizes[li], a.sizes[li], N, wst, acc);
-    }
-    const int cw = wave * (N / 4);
-    const int fn = act_of_layer_dev(li - 1);
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      if (t >= N / 64) break;
-      const int col = cw + 16 * t + (lane & 15);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int r = 4 * (lane >> 4) + j, row = r0 + r;
-        float g = 0.f;
-        if (row < a.rows) {
-          g = act_bwd(fn, a.h[li - 1][(size_t)row * N + col], acc[t][j]);
-          a.dz[li - 1][(size_t)row * N + col] = g;
-        }
-        act[cur ^ 1][r * kRBStride + col] = g;
-      }
-    }
-    cur ^= 1;
-    __syncthreads();
-  }
-  // ---- LayerNorm backward (ln_bwd_kernel, kRB rows); dy = act[cur] (tanh' applied).
-  constexpr int C = kRBMaxW / 256;
-  const int H = a.sizes[0];
-  const float invH = 1.f / (float)H;
-  float g[kRB][C], xh[kRB][C];
-  float s[2 * kRB];
-  float sc[C];
-#pragma unroll
-  for (int c = 0; c < C; ++c) sc[c] = a.scale[min(tid + 256 * c, H - 1)];
-#pragma unroll
-  for (int r = 0; r < kRB; ++r) {
-    const int row = r0 + r;
-    const bool ok = row < a.rows;
-    const float mu = ok ? a.mean[row] : 0.f, rs = ok ? a.rstd[row] : 0.f;
-    s[2 * r] = s[2 * r + 1] = 0.f;
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const int j = tid + 256 * c;
-      const bool v = ok && j < H;
-      const float dy = v ? act[cur][r * kRBStride + j] : 0.f;
-      const float z = v ? a.z1[(size_t)row * H + j] : 0.f;
-      xh[r][c] = v ? (z - mu) * rs : 0.f;
-      g[r][c] = v ? dy * sc[c] : 0.f;
-      s[2 * r] += g[r][c];
-      s[2 * r + 1] = fmaf(g[r][c], xh[r][c], s[2 * r + 1]);
-    }
-  }
-  block_sum256<2 * kRB>(s, red);
-  float cs_x[C], cs_1[C];
-#pragma unroll
-  for (int c = 0; c < C; ++c) cs_x[c] = cs_1[c] = 0.f;
-  bool any_dpg = false;
-#pragma unroll
-  for (int r = 0; r < kRB; ++r) {
-    const int row = r0 + r;
-    if (row >= a.rows) continue;
-    const float rs = a.rstd[row];
-    const float m1 = s[2 * r] * invH, m2 = s[2 * r + 1] * invH;
-    const bool ce = row < a.ce_rows;
-    any_dpg |= !ce;
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const int j = tid + 256 * c;
-      if (j >= H) continue;
-      const float dz = rs * (g[r][c] - m1 - xh[r][c] * m2);
-      float* cell = act[cur] + r * kRBStride + j;
-      if (ce) {
-        const float dyv = *cell;
-        a.dz[0][(size_t)row * H + j] = dz;
-        cs_x[c] = fmaf(dyv, xh[r][c], cs_x[c]);
-        cs_1[c] += dyv;
-      } else {
-        *cell = dz;  // the dpg row's dz, for dq/da below (this thread's cell only)
-      }
-    }
-  }
-#pragma unroll
-  for (int c = 0; c < C; ++c) {
-    const int j = tid + 256 * c;
-    if (j < H) {
-      a.colslab[((size_t)blockIdx.x * 2 + 0) * H + j] = cs_x[c];
-      a.colslab[((size_t)blockIdx.x * 2 + 1) * H + j] = cs_1[c];
-    }
-  }
-  if (!a.ploss_part) return;
-  if (!__syncthreads_or(any_dpg)) {
-    if (tid == 0) a.ploss_part[blockIdx.x] = 0.f;
-    return;
-  }
-  // dq/da = dz @ W1[action rows]^T of each dpg row: one wave per row.
-  for (int r = wave; r < kRB; r += 4) {
-    const int row = r0 + r;
-    if (row >= a.rows || row < a.ce_rows) continue;  // wave-uniform
-    for (int k = 0; k < a.A; ++k) {
-      float v = 0.f;
-      for (int j = lane; j < H; j += 64)
-        v = fmaf(act[cur][r * kRBStride + j], a.w1[(size_t)(a.act_off + k) * H + j], v);
-      v = wave_sum(v);
-      if (lane == 0) dq_s[r][k] = v;
-    }
-  }
-  __syncthreads();
-  if (tid < 64) {
-    float pl = 0.f;
-    if (tid < kRB) {
-      const int row = r0 + tid;
-      if (row < a.rows && row >= a.ce_rows) {
-        const int b = row - a.ce_rows;
-        float n2 = 0.f;
-        for (int k = 0; k < a.A; ++k) n2 = fmaf(dq_s[tid][k], dq_s[tid][k], n2);
-        const float nrm = n2 > 0.f ? sqrtf(n2) : 0.f;
-        const float den = a.clip > 0.f ? fmaxf(nrm, a.clip) : 1.f;
-        const float cm = a.clip > 0.f ? a.clip : 1.f;
-        for (int k = 0; k < a.A; ++k) {
-          const float dq = (dq_s[tid][k] * cm) / den;
-          a.dqda[(size_t)b * a.A + k] = dq;
-          pl = fmaf(0.5f * dq, dq, pl);
-          const float tk = a.t[(size_t)b * a.A + k];
-          const float da = -dq * a.invB;
-          a.du[(size_t)b * a.A + k] = da * a.act_scale[k] * 0.5f * (1.f - tk * tk);
-        }
-      }
-    }
-    pl = wave_sum(pl);
-    if (tid == 0) a.ploss_part[blockIdx.x] = pl;
-  }
-}
-
 // ------------------------------------------------------------------ orchestration
 
 // Small GEMMs: 32x32 output tiles, one wave per tile and k-group, 8 k-groups per block
@@ -1203,67 +725,10 @@ int lnmlp_forward_pair(acme_d4pg* l, const NetDesc& d, const NetIn (&in)[2], int
   return ACME_OK;
 }
 
-// The row-blocked single-launch forward (lnmlp_rows_kernel) takes networks whose widths are
-// multiples of 64 up to 512 (the critic's last hidden layer up to 256, its head up to 64
-// outputs) and inputs of up to kMaxIn features; others run the per-layer launches.
-bool rows_fit(const NetDesc& d, int din, bool policy) {
-  if (din > kMaxIn || d.nl < 1) return false;
-  for (int i = 0; i < d.nl; ++i)
-    if (d.sizes[i] > kRBMaxW || d.sizes[i] % 64 != 0) return false;
-  return policy ? d.nout <= ACME_D4PG_MAX_ACT : (d.nout <= 64 && d.sizes[d.nl - 1] <= 256);
-}
-
-// Up to two evaluations of one network in one row-blocked launch; out[i]: the policy's
-// actions (the critic writes its logits to acts.out).
-int lnmlp_forward_rows(acme_d4pg* l, const NetDesc& d, const NetIn (&in)[2], int da, int db,
-                       bool policy, float* const (&out)[2], hipStream_t st) {
-  static hipError_t attr = hipFuncSetAttribute(
-      reinterpret_cast<const void*>(&lnmlp_rows_kernel),
-      hipFuncAttributeMaxDynamicSharedMemorySize, kRBLds);
-  if (attr != hipSuccess) return (set_error("LDS attribute: %s", hipGetErrorString(attr)), ACME_ERR_HIP);
-  RowNetPair pr;
-  double flops = 0.0;
-  for (int i = 0; i < 2; ++i) {
-    RowNetArgs& g = pr.a[i];
-    const NetIn& n = in[i];
-    g.xa0 = n.xa0; g.xb0 = n.xb0; g.xa1 = n.xa1; g.xb1 = n.xb1;
-    g.split = n.split; g.rows = n.rows;
-    g.w1 = P(l, n.prm, d.w1); g.b1 = P(l, n.prm, d.b1);
-    g.scale = P(l, n.prm, d.scale); g.offset = P(l, n.prm, d.offset);
-    for (int li = 1; li < d.nl; ++li) {
-      g.w[li] = P(l, n.prm, d.w[li]);
-      g.b[li] = P(l, n.prm, d.b[li]);
-    }
-    g.ow = P(l, n.prm, d.ow); g.ob = P(l, n.prm, d.ob);
-    if (n.rows > 0) {
-      Acts& a = *n.acts;
-      g.z1 = a.z1; g.mean = a.mean; g.rstd = a.rstd;
-      for (int li = 0; li < d.nl; ++li) g.h[li] = a.h[li];
-      g.out = policy ? out[i] : a.out;
-      g.t = policy ? a.t : nullptr;
-    }
-    double per = (double)(da + db) * d.sizes[0] + (double)d.sizes[d.nl - 1] * d.nout;
-    for (int li = 1; li < d.nl; ++li) per += (double)d.sizes[li - 1] * d.sizes[li];
-    flops += 2.0 * n.rows * per;
-  }
-  pr.da = da; pr.db = db; pr.nl = d.nl; pr.nout = d.nout; pr.policy = policy ? 1 : 0;
-  for (int li = 0; li < d.nl; ++li) pr.sizes[li] = d.sizes[li];
-  pr.eps = l->cfg.layer_norm_epsilon;
-  pr.lo = l->act_lo; pr.ascale = l->act_scale;
-  const int rows = std::max(in[0].rows, in[1].rows);
-  ACME_PROF_PEAK(policy ? "d4pg_policy_fwd" : "d4pg_critic_fwd", st, flops, 0.0, 157.3);
-  lnmlp_rows_kernel<<<dim3((unsigned)ceil_div(rows, kRB), in[1].rows > 0 ? 2 : 1), 256, kRBLds,
-                      st>>>(pr);
-  D4_CHECK();
-  return ACME_OK;
-}
-
 // Up to two policy evaluations (TanhToSpec actions into out[i]); in[1].rows = 0: one.
 int policy_forward_pair(acme_d4pg* l, const NetIn (&in)[2], float* const (&out)[2],
                         hipStream_t st) {
   const NetDesc& d = l->pol;
-  if (l->rows_fwd && rows_fit(d, l->cfg.obs_dim, true))
-    return lnmlp_forward_rows(l, d, in, l->cfg.obs_dim, 0, true, out, st);
   int rc = lnmlp_forward_pair(l, d, in, l->cfg.obs_dim, 0, "d4pg_policy_ln", st);
   if (rc != ACME_OK) return rc;
   const int rows = std::max(in[0].rows, in[1].rows);
@@ -1289,10 +754,6 @@ int policy_forward_pair(acme_d4pg* l, const NetIn (&in)[2], float* const (&out)[
 // (B rows: [o_t, target actions]).
 int critic_forward_pair(acme_d4pg* l, const NetIn (&in)[2], hipStream_t st) {
   const NetDesc& d = l->cri;
-  if (l->rows_fwd && rows_fit(d, l->cfg.obs_dim + l->cfg.act_dim, false)) {
-    float* const none[2] = {nullptr, nullptr};
-    return lnmlp_forward_rows(l, d, in, l->cfg.obs_dim, l->cfg.act_dim, false, none, st);
-  }
   int rc = lnmlp_forward_pair(l, d, in, l->cfg.obs_dim, l->cfg.act_dim, "d4pg_critic_ln", st);
   if (rc != ACME_OK) return rc;
   Acts &a0 = *in[0].acts, &a1 = *in[1].acts;
@@ -1353,7 +814,7 @@ void add_dgrad(BwdGroup& g, const float* dz, int rows, int Nout, const float* w,
   }
 }
 
-constexpr int kZ = 4;  // sub-problems of one type per backward launch
+constexpr int kZ = 3;  // sub-problems of one type per backward launch
 
 template <class Q>
 bool fill_zset(gemm::ZSet<Q, kZ>& z, int& n, const std::vector<Q>& qs, int& tiles, int& count,
@@ -1512,12 +973,9 @@ int ln_backward(acme_d4pg* l, const NetDesc& d, const Acts& a, float* dy, int ro
   return ACME_OK;
 }
 
-int clip_adam_step(acme_d4pg* l, const acme_d4pg_outputs* out, int nploss, hipStream_t st);
-
 int d4pg_step_impl(acme_d4pg* l, const acme_d4pg_batch* bt, const acme_d4pg_outputs* out,
                    bool copy_target, hipStream_t st) {
   const int B = (int)bt->batch;
-  l->cur_B = B;
   const int od = l->cfg.obs_dim, ad = l->cfg.act_dim;
   const NetDesc& pd = l->pol;
   const NetDesc& cd = l->cri;
@@ -1546,63 +1004,10 @@ int d4pg_step_impl(acme_d4pg* l, const acme_d4pg_batch* bt, const acme_d4pg_outp
         l->dlogits, l->ce);
     D4_CHECK();
   }
-  BwdGroup g;
-  std::vector<LnReduce> ln;
-  if (l->rows_fwd && rows_fit(cd, od + ad, false) && rows_fit(pd, od, true)) {
-    // Row-blocked input-gradient chains (critic, then the policy from its du), then every
-    // weight gradient of both networks in one launch.
-    static hipError_t attr = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&lnmlp_bwd_rows_kernel),
-        hipFuncAttributeMaxDynamicSharedMemorySize, kRBLds);
-    if (attr != hipSuccess)
-      return (set_error("LDS attribute: %s", hipGetErrorString(attr)), ACME_ERR_HIP);
-    for (int net = 0; net < 2; ++net) {
-      const bool critic = net == 0;
-      const NetDesc& d = critic ? cd : pd;
-      const Acts& ac = critic ? l->con : l->pon;
-      const int rows = critic ? 2 * B : B;
-      RowBwdArgs r;
-      r.dtop = critic ? l->dlogits : l->du;
-      r.nout = d.nout;
-      r.ow = P(l, l->params, d.ow);
-      for (int li = 0; li < d.nl; ++li) {
-        if (li >= 1) r.w[li] = P(l, l->params, d.w[li]);
-        r.h[li] = ac.h[li];
-        r.dz[li] = critic ? l->cdz[li] : l->pdz[li];
-        r.sizes[li] = d.sizes[li];
-      }
-      r.z1 = ac.z1; r.mean = ac.mean; r.rstd = ac.rstd; r.scale = P(l, l->params, d.scale);
-      r.rows = rows; r.ce_rows = B; r.nl = d.nl;
-      r.colslab = critic ? l->lnslab : l->lnslab2;
-      r.w1 = P(l, l->params, d.w1); r.act_off = od; r.A = ad;
-      r.clip = l->cfg.clipping ? 1.f : 0.f; r.invB = 1.f / (float)B;
-      r.t = l->pon.t; r.act_scale = l->act_scale;
-      r.du = l->du; r.dqda = l->dqda; r.ploss_part = critic ? l->ploss_part : nullptr;
-      const int nblk = (int)ceil_div(rows, kRB);
-      ACME_PROF(critic ? "d4pg_critic_bwd" : "d4pg_policy_bwd", st, 0.0, 0.0);
-      lnmlp_bwd_rows_kernel<<<(unsigned)nblk, 256, kRBLds, st>>>(r);
-      D4_CHECK();
-      ln.push_back({r.colslab, nblk, d.sizes[0], Pm(l, l->grads, d.scale),
-                    Pm(l, l->grads, d.offset)});
-      const int L = d.nl - 1;
-      add_wgrad(g, ac.h[L], B, d.sizes[L], r.dtop, d.nout, Pm(l, l->grads, d.ow),
-                Pm(l, l->grads, d.ob));
-      for (int li = d.nl - 1; li >= 1; --li)
-        add_wgrad(g, ac.h[li - 1], B, d.sizes[li - 1], r.dz[li], d.sizes[li],
-                  Pm(l, l->grads, d.w[li]), Pm(l, l->grads, d.b[li]));
-      ConcatWgrad p;
-      p.M = critic ? od + ad : od; p.N = d.sizes[0]; p.K = B; p.k_chunk = B;
-      p.x0 = critic ? bt->o_tm1 : bt->o_t; p.d0 = od;
-      p.x1 = critic ? bt->a_tm1 : nullptr; p.d1 = critic ? ad : 0;
-      p.dz = r.dz[0];
-      p.out = Pm(l, l->grads, d.w1); p.bias_out = Pm(l, l->grads, d.b1);
-      g.first.push_back(p);
-    }
-    if ((rc = launch_bwd("d4pg_wgrads", g, st)) || (rc = run_ln_reduces(ln, st))) return rc;
-    return clip_adam_step(l, out, (int)ceil_div(2 * B, kRB), st);
-  }
   // Critic backward: 2B rows of input gradients (CE rows + dpg rows), weight gradients from
   // the first B.  Launch k carries layer k's input gradient and weight gradient.
+  BwdGroup g;
+  std::vector<LnReduce> ln;
   const int cL = cd.nl - 1;
   add_wgrad(g, l->con.h[cL], B, cd.sizes[cL], l->dlogits, cd.nout, Pm(l, l->grads, cd.ow),
             Pm(l, l->grads, cd.ob));
@@ -1624,13 +1029,7 @@ int d4pg_step_impl(acme_d4pg* l, const acme_d4pg_batch* bt, const acme_d4pg_outp
                         l->lnslab2, g, ln, st)) ||
       (rc = launch_bwd("d4pg_wgrad_first", g, st)) || (rc = run_ln_reduces(ln, st)))
     return rc;
-  return clip_adam_step(l, out, (int)ceil_div(2 * B, kRows), st);
-}
-
-// Global-norm clipping + Adam (t = steps taken including this one); nploss = the policy-loss
-// partials the dpg rows' LayerNorm backward wrote.
-int clip_adam_step(acme_d4pg* l, const acme_d4pg_outputs* out, int nploss, hipStream_t st) {
-  const int B = l->cur_B;
+  // Global-norm clipping + Adam (t = steps taken including this one).
   {
     ACME_PROF("d4pg_adam", st, 0.0, 7.0 * 4.0 * (double)l->flat);
     const int64_t n4 = l->flat / 4, pol4 = l->policy_flat / 4;
@@ -1643,7 +1042,7 @@ int clip_adam_step(acme_d4pg* l, const acme_d4pg_outputs* out, int nploss, hipSt
     a.lr0 = l->cfg.policy_learning_rate; a.lr1 = l->cfg.critic_learning_rate;
     a.b1 = l->cfg.adam_beta1; a.b2 = l->cfg.adam_beta2; a.eps = l->cfg.adam_epsilon;
     a.dev_step = l->dev_step; a.norms = l->norms;
-    a.sum_a = l->ploss_part; a.n_a = nploss; a.div_a = (float)B;
+    a.sum_a = l->ploss_part; a.n_a = (int)ceil_div(2 * B, kRows); a.div_a = (float)B;
     a.out_a = out && out->policy_loss ? out->policy_loss : l->loss_tmp + 1;
     a.sum_b = l->ce; a.n_b = B; a.div_b = (float)B;
     a.out_b = out && out->critic_loss ? out->critic_loss : l->loss_tmp;
@@ -1744,7 +1143,6 @@ int acme_d4pg_create(const acme_d4pg_config* cfg, acme_d4pg** out) {
                    "critic layer sizes must be multiples of 4 in [4, %d]", kMaxWidth);
   acme_d4pg* l = new acme_d4pg();
   l->cfg = *cfg;
-  l->rows_fwd = tune_variant("D4L") != 1;
   auto fail = [&](int code) {
     acme_d4pg_destroy(l);
     return code;

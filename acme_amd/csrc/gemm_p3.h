@@ -182,15 +182,23 @@ __device__ __forceinline__ u32x4 f16x8_of_bytes(uint32_t lo, uint32_t hi) {
   return u32x4{f16x2_of_bytes(lo, 0), f16x2_of_bytes(lo, 16), f16x2_of_bytes(hi, 0),
                f16x2_of_bytes(hi, 16)};
 }
-// One 16-B A unit at byte offset `off` of plane descriptor r (kOOB: zeros).
+// One 16-B A unit at byte offset `off` of plane descriptor r (kOOB: zeros), as loaded: for
+// uint8 frames the 8 bytes sit in the first two words and a_unit_f16 widens them when the
+// unit is stored to LDS, so the widening waits for the load there and not at the fetch
+// (which would end the fetch's look-ahead: round 5, conv1_wgrad 25.7 -> 32.5 us until this).
 template <class P>
 __device__ __forceinline__ u32x4 load_a_unit(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   if constexpr (AU8<P>::value) {
     const auto w = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
-    return f16x8_of_bytes((uint32_t)w[0], (uint32_t)w[1]);
+    return u32x4{(uint32_t)w[0], (uint32_t)w[1], 0u, 0u};
   } else {
     return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
   }
+}
+template <class P>
+__device__ __forceinline__ u32x4 a_unit_f16(const u32x4& v) {
+  if constexpr (AU8<P>::value) return f16x8_of_bytes(v[0], v[1]);
+  else return v;
 }
 
 // Maximum of two magnitudes (non-negative floats, or NaN) that keeps NaN: non-negative
@@ -614,7 +622,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in, int
       const int off = PA::offset(u);
 #pragma unroll
       for (int pl = 0; pl < NPA; ++pl)
-        *reinterpret_cast<u32x4*>(sa + pl * PA::PLANE + off) = ra[set][i][pl];
+        *reinterpret_cast<u32x4*>(sa + pl * PA::PLANE + off) = a_unit_f16<P>(ra[set][i][pl]);
     }
 #pragma unroll
     for (int i = 0; i < PB::PER_THREAD; ++i) {
@@ -637,7 +645,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in, int
       const int i = k / NPA, pl = k % NPA;
       const int u = tid + i * NT;
       if (PA::owns(u))
-        *reinterpret_cast<u32x4*>(sa + pl * PA::PLANE + PA::offset(u)) = ra[set][i][pl];
+        *reinterpret_cast<u32x4*>(sa + pl * PA::PLANE + PA::offset(u)) = a_unit_f16<P>(ra[set][i][pl]);
     } else {
       const int kb = k - PA::PER_THREAD * NPA;
       const int i = kb / NPB, pl = kb % NPB;
@@ -977,7 +985,8 @@ __global__ void __launch_bounds__(128 * WM * WN) gemm_p3ws_kernel(const P p_in, 
         if (!PA::owns(u)) continue;
 #pragma unroll
         for (int pl = 0; pl < NPA; ++pl)
-          *reinterpret_cast<u32x4*>(sa + pl * PA::PLANE + PA::offset(u)) = ra[set][i][pl];
+          *reinterpret_cast<u32x4*>(sa + pl * PA::PLANE + PA::offset(u)) =
+              a_unit_f16<P>(ra[set][i][pl]);
       }
 #pragma unroll
       for (int i = 0; i < PB::PER_THREAD; ++i) {

@@ -9,5 +9,4 @@ fi
 timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_d4pg_gpu.py > $O/tests_d4pg.log 2>&1
 rc2=$?; grep -E "PASSED|FAILED|ERROR|passed|failed" $O/tests_d4pg.log | tail -20
 if [ $rc2 -ne 0 ]; then grep -E "Error|assert" $O/tests_d4pg.log | head -20; exit $rc2; fi
-W=d4pg A="" B="ACME_V_D4L=1" timeout -k 10 600 bash tools/ab_env.sh $O/ab_d4l > $O/ab_d4l.log 2>&1; cat $O/ab_d4l.log
 exit $rc
