@@ -10,6 +10,11 @@
 //                                             wave_scan_total(level[l-1][64j..64j+63])
 // S0 = roundup(capacity, 64); S_{l+1} = roundup(S_l / 64, 64) until S_l == 64 (the top
 // level has exactly 64 entries; the root total is recomputed by the sampling wave).
+// When the top level has at most kTopComputed entries with children (1M slots: 4), readers
+// compute them from their children (the same wave scans, so the same bits) instead of
+// reading the stored top, and the one-launch priority update does not maintain it: the
+// top was the one level many workgroups of that launch write into, which cost it a
+// last-workgroup hand-off (round 5).
 //
 // The fan-out is the wavefront width: one wave reads the 64 children of a node in one
 // coalesced 512-B load, prefix-sums them with a 6-step shuffle scan, and picks the child
@@ -123,11 +128,35 @@ __device__ __forceinline__ int select_child(double v, double s, double t) {
   return idx;
 }
 
-// One wave per draw.  levels passed top-first in a small struct by value.
+// One wave per draw.  levels passed top-first in a small struct by value.  top_nodes > 0:
+// the top level's first top_nodes entries are computed from level nlevels - 2 (the rest are
+// zero), not read.
+constexpr int kTopComputed = 16;
 struct TreeView {
   const double* level[8];
   int nlevels;
+  int top_nodes = 0;
 };
+
+// The top level's entry `lane` as its writers store it: the scan total of its 64 children
+// (tree.top_nodes > 0), else the stored entry.  All children loads issue before the scans.
+__device__ __forceinline__ double top_entry(const double* const* level, int nlevels,
+                                            int top_nodes) {
+  const int lane = threadIdx.x & 63;
+  if (top_nodes <= 0) return level[nlevels - 1][lane];
+  const double* c = level[nlevels - 2];
+  double ch[kTopComputed];
+#pragma unroll
+  for (int g = 0; g < kTopComputed; ++g) ch[g] = g < top_nodes ? c[g * 64 + lane] : 0.0;
+  double v = 0.0;
+#pragma unroll
+  for (int g = 0; g < kTopComputed; ++g) {
+    if (g >= top_nodes) break;  // wave-uniform
+    const double t = __shfl(wave_scan64(ch[g]), 63, 64);
+    if (lane == g) v = t;
+  }
+  return v;
+}
 
 // Draw j of a prioritized sample by one wave (every lane returns the same slot and
 // probability): the descent the oracle restates (oracle/replay_oracle.c).
@@ -141,7 +170,8 @@ __device__ __forceinline__ void draw_prioritized(const TreeView& tree, int64_t s
   double t = 0.0, total = 0.0, leaf_value = 0.0;
   for (int l = tree.nlevels - 1; l >= 0; --l) {
     const int64_t base = node * 64;
-    const double v = tree.level[l][base + lane];
+    const double v = l == tree.nlevels - 1 ? top_entry(tree.level, tree.nlevels, tree.top_nodes)
+                                           : tree.level[l][base + lane];
     const double s = wave_scan64(v);
     if (l == tree.nlevels - 1) {
       total = __shfl(s, 63, 64);
@@ -207,16 +237,31 @@ __global__ void sample_uniform_kernel(const double* __restrict__ raw_prio,
   if (out_prio) out_prio[j] = raw_prio[slot];
 }
 
+// The top level's entries with children, when few enough for readers to compute them
+// (TreeView::top_nodes), else 0 (read the stored top).
+int computed_top_nodes(const acme_replay* r) {
+  if (r->nlevels < 2) return 0;
+  const int64_t n = r->level_size[r->nlevels - 2] / 64;
+  return n <= kTopComputed ? (int)n : 0;
+}
+TreeView tree_view(const acme_replay* r) {
+  TreeView tv;
+  for (int l = 0; l < 8; ++l) tv.level[l] = r->levels[l];
+  tv.nlevels = r->nlevels;
+  tv.top_nodes = computed_top_nodes(r);
+  return tv;
+}
+
 // Sampling mass of the table (one wave): the prioritized root total with the sampler's own
 // scan (same bits as `total` in sample_prioritized_kernel), or the item count (uniform).
-__global__ void total_kernel(const double* __restrict__ top, int prioritized, int64_t size,
+__global__ void total_kernel(TreeView tree, int prioritized, int64_t size,
                              double* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   if (!prioritized) {
     if (lane == 0) *out = (double)size;
     return;
   }
-  const double s = wave_scan64(top[lane]);
+  const double s = wave_scan64(top_entry(tree.level, tree.nlevels, tree.top_nodes));
   if (lane == 63) *out = s;
 }
 
@@ -599,6 +644,7 @@ struct FusedUpdateArgs {
   double* raw_prio;
   double* level[8];
   int64_t top_nodes;  // nodes of level nlevels - 2 (the top level's entries that have children)
+  int top_computed;   // readers compute the top level (computed_top_nodes > 0): not stored
   int nlevels;
   uint32_t* done;     // workgroups finished (the last one rescans the top; it resets the count)
   Gate gate;  // a learner step that was skipped writes no priority
@@ -650,14 +696,36 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
   bool skip = !verdict && gate_skip(a.gate);
   if (tid == 0) s_len = 0;
   __syncthreads();
-  for (int j = tid; j < a.n && !skip; j += nt) {  // this workgroup's updates (valid keys only)
-    const uint64_t k = a.upd_keys[j];
-    const int64_t slot = (int64_t)(k % (uint64_t)a.capacity);
-    if ((int)((slot >> (6 * h)) % G) != bid) continue;
-    if (a.keys[slot] != k) continue;  // evicted since it was sampled: ignored
-    const int e = atomicAdd(&s_len, 1);
-    s_j[e] = j;
-    s_slot[e] = slot;
+  if (!skip) {  // this workgroup's updates (valid keys only): two rounds of loads in all
+    constexpr int R = kFusedUpdateMax / 256;
+    uint64_t kv[R], kt[R];
+    int64_t sl[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      if (i * nt >= a.n) break;  // workgroup-uniform
+      const int j = tid + i * nt;
+      kv[i] = a.upd_keys[j < a.n ? j : a.n - 1];
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      if (i * nt >= a.n) break;
+      const int j = tid + i * nt;
+      const int64_t slot = (int64_t)(kv[i] % (uint64_t)a.capacity);
+      sl[i] = j < a.n && (int)((slot >> (6 * h)) % G) == bid ? slot : -1;
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      if (i * nt >= a.n) break;
+      kt[i] = a.keys[sl[i] >= 0 ? sl[i] : 0];
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      if (i * nt >= a.n) break;
+      if (sl[i] < 0 || kt[i] != kv[i]) continue;  // another workgroup's, or evicted since sampled
+      const int e = atomicAdd(&s_len, 1);
+      s_j[e] = tid + i * nt;
+      s_slot[e] = sl[i];
+    }
   }
   __syncthreads();
   const int len = s_len;
@@ -715,7 +783,7 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
         if (!win) continue;
         const double leaf = det_pow_priority(pv[i], a.alpha);
         a.raw_prio[slot] = pv[i];
-        if (h == 0) store_shared_level(a.level[0] + slot, leaf);
+        if (h == 0 && !a.top_computed) store_shared_level(a.level[0] + slot, leaf);
         else a.level[0][slot] = leaf;
         if (pre)
           for (int q = 0; q < np; ++q)
@@ -729,7 +797,7 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
             const double v = wave_scan64(s_ch[q][lane]);
             if (lane == 63) {
               s_val[q] = v;
-              if (l == h) store_shared_level(a.level[l] + s_node[q], v);
+              if (l == h && !a.top_computed) store_shared_level(a.level[l] + s_node[q], v);
               else a.level[l][s_node[q]] = v;
             }
           }
@@ -743,7 +811,7 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
             const int64_t node = s_slot[e] >> (6 * l);
             const double v = wave_scan64(a.level[l - 1][node * 64 + lane]);
             if (lane == 63) {
-              if (l == h) store_shared_level(a.level[l] + node, v);
+              if (l == h && !a.top_computed) store_shared_level(a.level[l] + node, v);
               else a.level[l][node] = v;
             }
           }
@@ -752,7 +820,7 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
       }
     }
   }
-  if (a.nlevels < 2) return;
+  if (a.nlevels < 2 || a.top_computed) return;  // readers compute the top (TreeView)
   // Count this workgroup finished once its write-through stores have left (drained), then
   // the last one rescans the top level from them.
   __builtin_amdgcn_s_waitcnt(0);
@@ -1488,8 +1556,8 @@ int acme_replay_total(acme_replay* r, double* out, void* stream) {
   int64_t size = 0;
   int rc = order_after_inserts(r, st, &size);
   if (rc != ACME_OK) return rc;
-  total_kernel<<<1, 64, 0, st>>>(r->levels[r->nlevels - 1],
-                                 r->cfg.sampler == ACME_SAMPLER_PRIORITIZED, size, out);
+  total_kernel<<<1, 64, 0, st>>>(tree_view(r), r->cfg.sampler == ACME_SAMPLER_PRIORITIZED,
+                                 size, out);
   ACME_LAUNCH_CHECK();
   return ACME_OK;
 }
@@ -1535,9 +1603,7 @@ static int sample_impl(acme_replay* r, int64_t batch, uint64_t step_counter, dou
   }
   ACME_PROF("replay_sample", st, 0.0, (double)batch * (r->cfg.sampler == ACME_SAMPLER_PRIORITIZED ? 512.0 * r->nlevels + 40.0 : 48.0));
   if (r->cfg.sampler == ACME_SAMPLER_PRIORITIZED) {
-    TreeView tv;
-    for (int l = 0; l < 8; ++l) tv.level[l] = r->levels[l];
-    tv.nlevels = r->nlevels;
+    const TreeView tv = tree_view(r);
     sample_prioritized_kernel<<<(unsigned)ceil_div(batch, 4), 256, 0, st>>>(
         tv, r->raw_prio, r->keys, batch, size, r->cfg.seed, step_counter, prob_scale, slots,
         keys, probabilities, table_size, priorities);
@@ -1620,9 +1686,7 @@ static int sample_gather_impl(acme_replay* r, int64_t batch, uint64_t step_count
     ACME_PROF("replay_sample_gather", st, 0.0,
               (double)batch * (2.0 * row_bytes + 40.0 + (prio ? 512.0 * r->nlevels : 0.0) +
                                (frames_f16 ? 4.0 * (double)r->cfg.field_bytes[f0] : 0.0)));
-    TreeView tv;
-    for (int l = 0; l < 8; ++l) tv.level[l] = r->levels[l];
-    tv.nlevels = r->nlevels;
+    const TreeView tv = tree_view(r);
     const int32_t nvec = (int32_t)(r->cfg.field_bytes[f0] / 16);
     const unsigned gb = (unsigned)batch;
     const uint8_t *s0 = r->fields[f0], *s1 = r->fields[f1];
@@ -1657,9 +1721,7 @@ static int sample_gather_impl(acme_replay* r, int64_t batch, uint64_t step_count
     const bool prio = r->cfg.sampler == ACME_SAMPLER_PRIORITIZED;
     ACME_PROF("replay_sample_gather", st, 0.0,
               (double)batch * (2.0 * row_bytes + 40.0 + (prio ? 512.0 * r->nlevels : 0.0)));
-    TreeView tv;
-    for (int l = 0; l < 8; ++l) tv.level[l] = r->levels[l];
-    tv.nlevels = r->nlevels;
+    const TreeView tv = tree_view(r);
     const unsigned gb = (unsigned)ceil_div(batch, 4);
     if (prio)
       sample_gather_small_kernel<true><<<gb, 256, 0, st>>>(
@@ -1830,6 +1892,7 @@ int acme::replay_update_priorities_gated(acme_replay* r, const uint64_t* keys,
     if (job) a.job = *job;
     for (int l = 0; l < 8; ++l) a.level[l] = r->levels[l];
     a.top_nodes = r->nlevels >= 2 ? r->level_size[r->nlevels - 2] / 64 : 0;
+    a.top_computed = computed_top_nodes(r) > 0 ? 1 : 0;
     a.done = r->upd_done;
     prio_update_fused_kernel<<<kFusedUpdateBlocks + (a.job.s ? 1 : 0), 256, 0, st>>>(a);
     ACME_LAUNCH_CHECK();

@@ -231,7 +231,9 @@ def setup_dqn(args, world, rank, dev):
                          learning_rate=1e-3, target_update_period=100, dataset=dataset,
                          replay_client=replay.Client(server), counter=counting.Counter(),
                          logger=loggers.NoOpLogger(), seed=0, device=dev,
-                         reduce_logged_loss=False)
+                         reduce_logged_loss=False,
+                         # timing-only builds (tools/, e.g. -DWS_EXP) compute garbage: skip
+                         on_plane_overflow=os.environ.get("ACME_BENCH_ON_OVERFLOW", "reissue"))
     meta = dict(
         # The arithmetic: every GEMM operand as two scaled f16 planes (22-23 significant
         # bits, per-tensor power-of-two scale), three MFMA terms per product, f32

@@ -43,7 +43,7 @@ def main():
     for path in paths:
         for r in csv.DictReader(open(path)):
             sec = P.section(r["Kernel_Name"])
-            if sec and r["Counter_Name"] in COUNTERS:
+            if sec:
                 per[(sec, r.get("Dispatch_Id") or r.get("Correlation_Id"))][r["Counter_Name"]] += \
                     float(r["Counter_Value"])
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
@@ -65,11 +65,15 @@ def main():
                     row[name] = round(m[k] / wc, 4)
         row["launches"] = len(next(iter(c.values())))
         res[sec] = row
-    json.dump({"method": "rocprofv3 --pmc " + " ".join(COUNTERS) + " (one pass, kernels "
+    names = sorted({k for c in agg.values() for k in c})
+    json.dump({"method": "rocprofv3 --pmc " + " ".join(names) + " (one pass, kernels "
                "serialised by the counter collection); mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / "
                "(1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs); wait_* / active = share of "
                "SQ_WAVE_CYCLES; per launch", "kernels": res}, open(out, "w"), indent=1)
     for k, v in sorted(res.items(), key=lambda kv: -kv[1].get("GRBM_GUI_ACTIVE", 0)):
+        if "SQ_VALU_MFMA_BUSY_CYCLES" not in v:
+            print(f"{k:22s} " + " ".join(f"{n}={v[n]}" for n in names if n in v))
+            continue
         print(f"{k:22s} mfma_busy {v.get('mfma_busy', float('nan')):.3f}  wait_any "
               f"{v.get('wait_any', float('nan')):.3f}  wait_inst {v.get('wait_inst', float('nan')):.3f}"
               f"  active {v.get('active', float('nan')):.3f}  wait_lds {v.get('wait_lds', float('nan')):.3f}")
