@@ -80,7 +80,6 @@ struct acme_dqn {
   float *dzh = nullptr, *dz3 = nullptr, *dz2 = nullptr, *dz1 = nullptr;
   float* slab = nullptr;
   int64_t slab_floats = 0;
-  int fct = 0;  // ACME_V_FCT experiment (fc_fwd tiles)
   float* g = nullptr;  // per-sample dLoss/dq_tm1[a]
   int32_t* a_cache = nullptr;  // actions of the current batch (for the backward kernels)
   float* loss_tmp = nullptr;
@@ -460,12 +459,6 @@ int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const torso:
     // tiles with split-K 8, and the LDS-DMA ring (3 or 4 stages) all slower or equal.)
     if (ttall && l->single_role) ACME_P3_GEMM("fc_fwd", 256, 128, 2, 2, 32, p, splits);  // tests
     else if (ttall) ACME_P3WS_GEMM("fc_fwd", 256, 128, 2, 2, 32, p, splits, true);
-    else if (tall && l->fct == 1) {  // experiment: 256x256 tiles, one register set
-      ACME_PROF_PEAK("fc_fwd", st, 2.0 * (double)p.M * (double)p.N * (double)p.K, 0.0,
-                     gemm::p3_peak_tflops<decltype(p)>());
-      hipError_t e = gemm::launch_gemm_p3<256, 256, 2, 2, 32, false>(p, splits, st);
-      if (e != hipSuccess) return (set_error("gemm launch failed: %s", hipGetErrorString(e)), ACME_ERR_HIP);
-    }
     else if (tall && l->single_role) ACME_P3_GEMM("fc_fwd", 256, 128, 2, 2, 32, p, splits);  // tests
     else if (tall) ACME_P3WS_GEMM("fc_fwd", 256, 128, 2, 2, 32, p, splits, true);
     else if (l->single_role) ACME_P3_GEMM("fc_fwd", 128, 128, 2, 2, 32, p, splits);  // tests
@@ -793,7 +786,6 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
   l->cfg = *cfg;
   l->single_stream = tune_variant("SIDE") == 1;
   l->single_role = tune_variant("WSN") == 1;
-  l->fct = tune_variant("FCT");
   l->frames_u8 = tune_variant("F16FRAMES") != 1;
   const int A = cfg->num_actions;
   const int B = cfg->max_batch;

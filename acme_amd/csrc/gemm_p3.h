@@ -906,6 +906,13 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3g_kernel(const P p_in, in
 #endif
 }
 
+#ifndef WS_EXP
+#define WS_EXP 0  // bottleneck experiments: 1 producers idle, 2 consumers idle
+#endif
+#ifndef WS_FENCE
+#define WS_FENCE 1  // consumers' pipelined loop: 1 fences (round 5: step 0.5096 -> 0.5048 ms), 2 reads threaded among the MFMAs (0.5132)
+#endif
+
 // Warp-specialised kernel: WM x WN consumer waves (fragment reads + MFMAs only, the same
 // P3Core::mma as gemm_p3_kernel, so the same bits) and as many producer waves (global ->
 // VGPR -> LDS only), two waves per SIMD, so one wave's staging instructions issue in the
@@ -997,9 +1004,7 @@ __global__ void __launch_bounds__(128 * WM * WN) gemm_p3ws_kernel(const P p_in, 
           *reinterpret_cast<u32x4*>(sb + pl * PB::PLANE + PB::offset(u)) = rb[set][i][pl];
       }
     };
-#ifndef WS_EXP
-#define WS_EXP 0  // bottleneck experiments: 1 producers idle, 2 consumers idle
-#endif
+
     if constexpr (WS_EXP == 1) {
       __syncthreads();
       for (int kt = 0; kt < nk; ++kt) __syncthreads();
@@ -1074,10 +1079,36 @@ __global__ void __launch_bounds__(128 * WM * WN) gemm_p3ws_kernel(const P p_in, 
       const uint8_t* sa = smem + rbuf * STAGE;
       rbuf = rbuf == RING - 1 ? 0 : rbuf + 1;
       const uint8_t* na = smem + rbuf * STAGE;
+      // Scheduling fences (WS_FENCE): without them the compiler sinks each read to just
+      // before its first MFMA, to save registers, and the wave waits out the LDS latency
+      // there several times per stage (round 5: lgkmcnt(0) waits between the MFMAs).
+      // WS_FENCE 2 (no column sums): each k16 step's MFMAs with the other step's fragment
+      // reads threaded between them, one read per MFMA gap, so no read waits behind a burst
+      // of reads and the next step's operands land while this step's MFMAs run.
+      constexpr bool kThread = WS_FENCE == 2 && !C::kColSum;
+      constexpr int RD = C::MT * NPA * (P::A_MODE == KCONTIG ? 1 : 2) +
+                         C::NTL * NPB * (P::B_MODE == KCONTIG ? 1 : 2);
+      constexpr int MF = C::MT * C::NTL * p3_nterms<NPA, NPB>();
+      auto thread_reads = [&]() {
+        if constexpr (kThread) {
+#pragma unroll
+          for (int q = 0; q < (RD < MF ? RD : MF); ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          }
+          if constexpr (MF > RD) __builtin_amdgcn_sched_group_barrier(0x008, MF - RD, 0);
+        }
+      };
       C::read_frags(sa, sa + PA::BYTES, wm, wn, 1, lane, fa1, fb1);
+      if constexpr (WS_FENCE == 1 || (WS_FENCE == 2 && !kThread)) __builtin_amdgcn_sched_barrier(0);
       C::mfma_frags(fa0, fb0, acc, cs, do_colsum);
+      thread_reads();
+      if constexpr (WS_FENCE) __builtin_amdgcn_sched_barrier(0);
       C::read_frags(na, na + PA::BYTES, wm, wn, 0, lane, fa0, fb0);
+      if constexpr (WS_FENCE == 1 || (WS_FENCE == 2 && !kThread)) __builtin_amdgcn_sched_barrier(0);
       C::mfma_frags(fa1, fb1, acc, cs, do_colsum);
+      thread_reads();
+      if constexpr (WS_FENCE) __builtin_amdgcn_sched_barrier(0);
       __syncthreads();
     }
   } else {

@@ -130,6 +130,13 @@ struct ImgGeomPairs {
   }
 };
 
+#ifndef P3I_SCHED
+#define P3I_SCHED 1  // fenced issue order in the image-resident kernels' k loop
+#endif
+#ifndef P3I_RSETS
+#define P3I_RSETS 3  // weight-panel register sets (2: loads one iteration ahead, 3: two)
+#endif
+
 template <class GI, int FPB, int BN, int WM, int WN, int MT, class P>
 struct P3ICfg {
   static constexpr int BK = 32, KS = 2;
@@ -179,7 +186,8 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
   __amdgpu_buffer_rsrc_t srcB[NPB];
 #pragma unroll
   for (int pl = 0; pl < NPB; ++pl) srcB[pl] = plane_rsrc(p.b_src, pl);
-  u32x4 rb[2][PB::PER_THREAD][NPB];
+  constexpr int RS = P3I_RSETS;  // register sets: weight loads issued RS - 1 iterations ahead
+  u32x4 rb[RS][PB::PER_THREAD][NPB];
   auto fetch_b = [&](auto S, int k0) {
     constexpr int set = decltype(S)::value;
 #pragma unroll
@@ -209,8 +217,10 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
 
   using S0 = std::integral_constant<int, 0>;
   using S1 = std::integral_constant<int, 1>;
+  using S2 = std::integral_constant<int, 2>;
   fetch_b(S0{}, 0);
   fetch_b(S1{}, BK);
+  if constexpr (RS == 3) fetch_b(S2{}, 2 * BK);
 
   // ---- A: the block's frames, each unit of each plane loaded and stored once.
   constexpr int UB = 16;  // bytes per unit
@@ -296,6 +306,35 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
     typename GI::Stage sg[MT];
 #pragma unroll
     for (int i = 0; i < MT; ++i) sg[i] = GI::stage(ln[i], k0);
+    if constexpr (P3I_SCHED) {
+      // Every fragment of the stage read first, then the MFMAs (fenced): one LDS latency per
+      // stage instead of one per k16 step (the scheduler otherwise sinks each read to its
+      // first use).
+      f16x8 fb[KS][NTL][NPB], fa[KS][MT][NPA];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+#pragma unroll
+        for (int j = 0; j < NTL; ++j)
+#pragma unroll
+          for (int pl = 0; pl < NPB; ++pl) fb[s][j][pl] = PB::frag(sb, pl, wn * TN + j * 32, s, lane);
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          const int u = GI::unit(sg[i], ln[i], k0, s, lane >> 5);
+          const int a = u >= 0 ? u : PLANE - 16;
+#pragma unroll
+          for (int pl = 0; pl < NPA; ++pl)
+            fa[s][i][pl] = *reinterpret_cast<const f16x8*>(smem + pl * PLANE + a);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int j = 0; j < NTL; ++j) p3_terms<NPA, NPB>(fa[s][i], fb[s][j], acc[i][j]);
+      return;
+    }
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       f16x8 fb[NTL][NPB];
@@ -317,23 +356,37 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
     }
   };
 
-  // Iteration kt: LDS buffer kt & 1 holds B of stage kt, register set (kt + 1) & 1 holds
-  // stage kt + 1 (stashed first: its buffer was last read in iteration kt - 1, before the
-  // barrier), then stage kt + 2 is fetched into set kt & 1 (zeros past the end).
+  // Iteration kt: LDS buffer kt & 1 holds B of stage kt, register set (kt + 1) % RS holds
+  // stage kt + 1 (stashed first into buffer (kt + 1) & 1: last read in iteration kt - 1,
+  // before the barrier), then stage kt + RS is fetched into set kt % RS (zeros past the end).
   auto iter = [&](auto S, int kt) {
     constexpr int set = decltype(S)::value;
-    using Other = std::integral_constant<int, set ^ 1>;
-    stash_b(Other{}, set ^ 1);
-    fetch_b(S, (kt + 2) * BK);
-    compute(kt * BK, set);
+    using Next = std::integral_constant<int, (set + 1) % RS>;
+    stash_b(Next{}, (kt + 1) & 1);
+    fetch_b(S, (kt + RS) * BK);
+    // The weight loads issue before the MFMAs (fenced), so they have the whole iteration
+    // to land before the next iteration stores them (round 5: the scheduler had sunk them
+    // to just before the barrier, and the next store waited out their latency).
+    if constexpr (P3I_SCHED) __builtin_amdgcn_sched_barrier(0);
+    compute(kt * BK, kt & 1);
     __syncthreads();
   };
   int kt = 0;
-  for (; kt + 1 < nk; kt += 2) {
-    iter(S0{}, kt);
-    iter(S1{}, kt + 1);
+  if constexpr (RS == 3) {
+    for (; kt + 2 < nk; kt += 3) {
+      iter(S0{}, kt);
+      iter(S1{}, kt + 1);
+      iter(S2{}, kt + 2);
+    }
+    if (kt < nk) iter(S0{}, kt);
+    if (kt + 1 < nk) iter(S1{}, kt + 1);
+  } else {
+    for (; kt + 1 < nk; kt += 2) {
+      iter(S0{}, kt);
+      iter(S1{}, kt + 1);
+    }
+    if (kt < nk) iter(S0{}, kt);
   }
-  if (kt < nk) iter(S0{}, kt);
 
   f32x16 cs[C::NCS];
   C::epilogue(p, smem, m0, 0, wave, wm, wn, lane, 0, acc, cs, false);
