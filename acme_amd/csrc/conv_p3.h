@@ -385,6 +385,7 @@ struct P3DenseFwd {
   PlaneSrc b_src;  // W
   float* slab;     // [splits][M][N] partial sums (already read-scaled; finalised by the
                    // slab reduction)
+  uint64_t* stamps = nullptr;  // timing experiment (gemm_p3.h HasStamps)
   struct ARow {
     int off;
     bool ok;

@@ -80,6 +80,8 @@ struct acme_dqn {
   float *dzh = nullptr, *dz3 = nullptr, *dz2 = nullptr, *dz1 = nullptr;
   float* slab = nullptr;
   int64_t slab_floats = 0;
+  bool stamps_on = false;      // ACME_V_STAMPS=1: the online fc_fwd launch stamps its phases
+  uint64_t* stamps = nullptr;  // [4096][8] (debug_buffer "gemm_stamps")
   float* g = nullptr;  // per-sample dLoss/dq_tm1[a]
   int32_t* a_cache = nullptr;  // actions of the current batch (for the backward kernels)
   float* loss_tmp = nullptr;
@@ -453,6 +455,7 @@ int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const torso:
     p.M = rows; p.N = 2 * kHidden; p.K = kFlat; p.k_chunk = chunk_for(kFlat, splits);
     p.a_src = SRC(x3, (int64_t)rows * kFlat); p.ldx = kFlat;
     p.b_src = SRC(WP(l, wpl, l->t_fcw), (int64_t)kFlat * 2 * kHidden); p.slab = slab;
+    if (tall) p.stamps = l->stamps;
     // Producer / consumer waves with fragment reads one k16 step ahead (gemm_p3ws_kernel):
     // 65.2 -> 60.5 us against the single-role kernel, the same bits.
     // (Two f16 planes, measured on the step: 256x128 / 128x256 WS tiles, 256x128 single-role
@@ -786,6 +789,7 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
   l->cfg = *cfg;
   l->single_stream = tune_variant("SIDE") == 1;
   l->single_role = tune_variant("WSN") == 1;
+  l->stamps_on = tune_variant("STAMPS") == 1;
   l->frames_u8 = tune_variant("F16FRAMES") != 1;
   const int A = cfg->num_actions;
   const int B = cfg->max_batch;
@@ -917,7 +921,8 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
       (rc = dev_alloc(l, &l->slab, l->slab_floats)) ||
       (rc = dev_alloc(l, &l->g, (int64_t)B)) || (rc = dev_alloc(l, &l->a_cache, (int64_t)B)) ||
       (rc = dev_alloc(l, &l->loss_tmp, 4)) || (rc = dev_alloc(l, &l->td_tmp, (int64_t)B)) ||
-      (rc = dev_alloc(l, &l->prio_tmp, (int64_t)B)))
+      (rc = dev_alloc(l, &l->prio_tmp, (int64_t)B)) ||
+      (l->stamps_on && (rc = dev_alloc(l, &l->stamps, (int64_t)4096 * 8))))
     return fail(rc);
   if (hipDeviceSynchronize() != hipSuccess)
     return fail((set_error("learner init failed"), ACME_ERR_HIP));
@@ -1104,7 +1109,8 @@ int acme_dqn_debug_buffer(const acme_dqn* l, const char* name, const float** out
     const char* n;
     const float* p;
     int64_t c;
-  } tab[] = {{"x1", l->x1, 2 * B * 441 * 32}, {"x2", l->x2, 2 * B * kFlat},
+  } tab[] = {{"gemm_stamps", reinterpret_cast<const float*>(l->stamps), 2 * 4096 * 8},
+             {"x1", l->x1, 2 * B * 441 * 32}, {"x2", l->x2, 2 * B * kFlat},
              {"x3", l->x3, 2 * B * kFlat},    {"hid", l->hid, 2 * B * 2 * kHidden},
              {"dzh", l->dzh, B * 2 * kHidden}, {"dz3", l->dz3, B * kFlat},
              {"dz2", l->dz2, B * kFlat},       {"dz1", l->dz1, B * 441 * 32},

@@ -174,6 +174,15 @@ __device__ __forceinline__ uint32_t f16x2_of_bytes(uint32_t x, int sh) {
 // Problems whose A operand is the uint8 Atari frames themselves (`static constexpr bool
 // A_U8 = true`, byte offsets): a 16-B A unit (8 f16) is 8 frame bytes widened exactly, so
 // the frames are read from HBM once as bytes instead of as an f16 copy (half the bytes).
+// Problems with a `uint64_t* stamps` member (timing experiments, ACME_V_STAMPS=1): when it is
+// set, the WS kernel's consumer wave 0 stamps its workgroup's phases (s_memrealtime at entry
+// and exit, s_memtime at entry, after the prologue's first barrier, after the k loop and at
+// exit) into stamps[8 * (flat block id) + 0..5].
+template <class P, class = void>
+struct HasStamps : std::false_type {};
+template <class P>
+struct HasStamps<P, std::void_t<decltype(std::declval<P>().stamps)>> : std::true_type {};
+
 template <class P, class = void>
 struct AU8 : std::false_type {};
 template <class P>
@@ -1051,6 +1060,15 @@ __global__ void __launch_bounds__(128 * WM * WN) gemm_p3ws_kernel(const P p_in, 
 
   const int wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
+  uint64_t st_rt0 = 0, st_t0 = 0, st_t1 = 0, st_t2 = 0;
+  bool stamp = false;
+  if constexpr (HasStamps<P>::value) {
+    stamp = p.stamps != nullptr && tid == 0;
+    if (stamp) {
+      st_rt0 = __builtin_amdgcn_s_memrealtime();
+      st_t0 = __builtin_amdgcn_s_memtime();
+    }
+  }
   f32x16 acc[C::MT][C::NTL];
   f32x16 cs[C::NCS];
 #pragma unroll
@@ -1065,6 +1083,8 @@ __global__ void __launch_bounds__(128 * WM * WN) gemm_p3ws_kernel(const P p_in, 
     for (int v = 0; v < 16; ++v) cs[j][v] = 0.f;
   const bool do_colsum = C::kColSum && m0 == 0 && wm == 0;
   __syncthreads();
+  if constexpr (HasStamps<P>::value)
+    if (stamp) st_t1 = __builtin_amdgcn_s_memtime();
   int rbuf = 0;
   if constexpr (WS_EXP == 2) {
     for (int kt = 0; kt < nk; ++kt) __syncthreads();
@@ -1119,7 +1139,21 @@ __global__ void __launch_bounds__(128 * WM * WN) gemm_p3ws_kernel(const P p_in, 
       __syncthreads();
     }
   }
+  if constexpr (HasStamps<P>::value)
+    if (stamp) st_t2 = __builtin_amdgcn_s_memtime();
   C::epilogue(p, smem, m0, n0, wave, wm, wn, lane, split, acc, cs, do_colsum);
+  if constexpr (HasStamps<P>::value) {
+    if (stamp) {
+      const uint64_t t3 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+      uint64_t* o = p.stamps + 8 * ((int64_t)blockIdx.z * gridDim.x + blockIdx.x);
+      o[0] = st_rt0;
+      o[1] = rt1;
+      o[2] = st_t0;
+      o[3] = st_t1;
+      o[4] = st_t2;
+      o[5] = t3;
+    }
+  }
 }
 
 // Tile order: B's panels slowest when B is the larger operand (N * planes > M * planes).

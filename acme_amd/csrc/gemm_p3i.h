@@ -131,11 +131,10 @@ struct ImgGeomPairs {
 };
 
 #ifndef P3I_SCHED
-#define P3I_SCHED 1  // fenced issue order in the image-resident kernels' k loop
+#define P3I_SCHED 1  // fenced issue order in the image-resident kernels' k loop (round 5: step
+                     // 0.4969 -> 0.4949 ms, three alternating 300-step runs)
 #endif
-#ifndef P3I_RSETS
-#define P3I_RSETS 3  // weight-panel register sets (2: loads one iteration ahead, 3: two)
-#endif
+
 
 template <class GI, int FPB, int BN, int WM, int WN, int MT, class P>
 struct P3ICfg {
@@ -186,7 +185,9 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
   __amdgpu_buffer_rsrc_t srcB[NPB];
 #pragma unroll
   for (int pl = 0; pl < NPB; ++pl) srcB[pl] = plane_rsrc(p.b_src, pl);
-  constexpr int RS = P3I_RSETS;  // register sets: weight loads issued RS - 1 iterations ahead
+  // Two register sets (round 5: a third, loads two iterations ahead, measured slower on the
+  // step: 0.4949 -> 0.5011 ms).
+  constexpr int RS = 2;
   u32x4 rb[RS][PB::PER_THREAD][NPB];
   auto fetch_b = [&](auto S, int k0) {
     constexpr int set = decltype(S)::value;
@@ -217,10 +218,8 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
 
   using S0 = std::integral_constant<int, 0>;
   using S1 = std::integral_constant<int, 1>;
-  using S2 = std::integral_constant<int, 2>;
   fetch_b(S0{}, 0);
   fetch_b(S1{}, BK);
-  if constexpr (RS == 3) fetch_b(S2{}, 2 * BK);
 
   // ---- A: the block's frames, each unit of each plane loaded and stored once.
   constexpr int UB = 16;  // bytes per unit
@@ -372,21 +371,11 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
     __syncthreads();
   };
   int kt = 0;
-  if constexpr (RS == 3) {
-    for (; kt + 2 < nk; kt += 3) {
-      iter(S0{}, kt);
-      iter(S1{}, kt + 1);
-      iter(S2{}, kt + 2);
-    }
-    if (kt < nk) iter(S0{}, kt);
-    if (kt + 1 < nk) iter(S1{}, kt + 1);
-  } else {
-    for (; kt + 1 < nk; kt += 2) {
-      iter(S0{}, kt);
-      iter(S1{}, kt + 1);
-    }
-    if (kt < nk) iter(S0{}, kt);
+  for (; kt + 1 < nk; kt += 2) {
+    iter(S0{}, kt);
+    iter(S1{}, kt + 1);
   }
+  if (kt < nk) iter(S0{}, kt);
 
   f32x16 cs[C::NCS];
   C::epilogue(p, smem, m0, 0, wave, wm, wn, lane, 0, acc, cs, false);

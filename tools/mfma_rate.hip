@@ -13,11 +13,13 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <int KIND>
 __global__ void __launch_bounds__(256) mfma_loop(int n, float* out, long long* cyc) {
-  f16x8 a, b;
+  f16x8 a, b, a2, b2;
   bf16x8 c, d;
   for (int j = 0; j < 8; ++j) {
     a[j] = (_Float16)(threadIdx.x * 1e-3f + j);
     b[j] = (_Float16)(j * 1e-3f);
+    a2[j] = (_Float16)(threadIdx.x * 2e-3f - j);
+    b2[j] = (_Float16)(j * -1e-3f);
     c[j] = (__bf16)(threadIdx.x * 1e-3f + j);
     d[j] = (__bf16)(j * 1e-3f);
   }
@@ -34,6 +36,11 @@ __global__ void __launch_bounds__(256) mfma_loop(int n, float* out, long long* c
       if constexpr (KIND == 0) acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc[q], 0, 0, 0);
       if constexpr (KIND == 1) acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c, d, acc[q], 0, 0, 0);
       if constexpr (KIND == 2) acc4[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, acc4[q], 0, 0, 0);
+      if constexpr (KIND == 3) {  // the plane engine's pattern: 3 dependent terms per accumulator
+        acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc[q], 0, 0, 0);
+        acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b2, acc[q], 0, 0, 0);
+        acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2, b, acc[q], 0, 0, 0);
+      }
     }
   }
   const long long t1 = __builtin_amdgcn_s_memtime();
@@ -62,9 +69,10 @@ void run(const char* name, double flops_per) {
   (void)hipEventElapsedTime(&ms, e0, e1);
   long long c = 0;
   (void)hipMemcpy(&c, cyc, sizeof(c), hipMemcpyDeviceToHost);
-  const double total = (double)blocks * 4 * n * 4 * flops_per;  // waves x MFMAs x flops
+  const int per = KIND == 3 ? 12 : 4;  // MFMAs per loop iteration
+  const double total = (double)blocks * 4 * n * per * flops_per;  // waves x MFMAs x flops
   printf("%-28s %8.3f ms  %7.1f TFLOP/s  %6.1f memtime-ticks per MFMA (one wave)\n", name, ms,
-         total / (ms * 1e-3) / 1e12, (double)c / (4.0 * n));
+         total / (ms * 1e-3) / 1e12, (double)c / ((double)per * n));
   (void)hipFree(out);
   (void)hipFree(cyc);
 }
@@ -73,5 +81,6 @@ int main() {
   run<0>("v_mfma_f32_32x32x16_f16", 2.0 * 32 * 32 * 16);
   run<1>("v_mfma_f32_32x32x16_bf16", 2.0 * 32 * 32 * 16);
   run<2>("v_mfma_f32_16x16x32_f16", 2.0 * 16 * 16 * 32);
+  run<3>("32x32x16_f16 3-term chains", 2.0 * 32 * 32 * 16);
   return 0;
 }
