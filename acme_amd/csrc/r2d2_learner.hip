@@ -1144,6 +1144,8 @@ int acme_r2d2_step(acme_r2d2* l, const acme_sequence_batch* b, const double* pro
     if (rc != ACME_OK) return rc;
     ACME_HIP_TRY(hipMemsetAsync(l->overflow, 0, sizeof(int), st));
     ACME_HIP_TRY(hipMemsetAsync(l->guard, 0, offsetof(StepGuard, applied), st));
+    // A calibration pass's LSTM timeout is not the first step's (as IMPALA's calibration).
+    if (l->tmo) ACME_HIP_TRY(hipMemsetAsync(l->tmo, 0, sizeof(unsigned), st));
     l->scales_ok = true;
   }
   rc = r2d2_step_impl(l, b, probabilities, out, st);
