@@ -901,9 +901,16 @@ int r2d2_step_impl(acme_r2d2* l, const acme_sequence_batch* bt, const double* pr
     }
     if (rc != ACME_OK) return rc;
   }
-  if (l->num_steps % l->cfg.target_update_period == 0)  // learning.py:185-189, after the update
-    ACME_HIP_TRY(hipMemcpyAsync(l->target, l->params, (size_t)l->flat * sizeof(float),
-                                hipMemcpyDeviceToDevice, st));
+  if (l->num_steps % l->cfg.target_update_period == 0) {  // learning.py:185-189, after the update
+    // Gated on the step's verdict: a skipped step copies nothing (its parameters are the
+    // pre-step ones).
+    Gate gate;
+    gate.g = l->guard;
+    gate.use_last = 1;
+    if ((rc = launch_copy_gated(l->target, l->params, (size_t)l->flat * sizeof(float), nullptr,
+                                nullptr, 0, gate, st)) != ACME_OK)
+      return rc;
+  }
   return ACME_OK;
 }
 

@@ -1,0 +1,10 @@
+# Round 5: the whole -m gpu suite and smoke().
+set -u
+O=gpurun_out/r05check; mkdir -p $O
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/tests.log 2>&1
+rc=$?
+grep -E "FAILED|ERROR" $O/tests.log | head; tail -2 $O/tests.log
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -5 $O/smoke.log; exit 3; }
+tail -1 $O/smoke.log
+exit $rc
