@@ -130,16 +130,22 @@ def cpu_baseline(batch: int, num_actions: int, seconds: float):
         torch.set_num_threads(threads)
         one()  # warm-up (page faults, oneDNN primitive creation)
         t0 = time.perf_counter()
-        n = 0
+        n, shown = 0, t0
         while (n < least or time.perf_counter() - t0 < budget) and time.perf_counter() - t0 < cap:
             one()
             n += 1
+            if time.perf_counter() - shown > 15.0:  # a progress line (a silent minute reads as hung)
+                shown = time.perf_counter()
+                print(f"[bench] cpu baseline: {threads} threads, {n} steps in "
+                      f"{shown - t0:.0f} s", file=sys.stderr, flush=True)
         return batch * n / (time.perf_counter() - t0), n
 
     # Every visible host core (the box's OMP_NUM_THREADS, 16, is ignored here: SURVEY §8(d)
     # times the reference CPU learner on the host cores of the same box), at least 200 timed
     # steps (capped at 150 s); then 16 threads and 1 thread on bounded samples.
     cores = len(os.sched_getaffinity(0))
+    print(f"[bench] cpu baseline: {cores} visible cores, then 16 threads, then 1", file=sys.stderr,
+          flush=True)
     prev = torch.get_num_threads()
     try:
         v_all, n_all = timed(cores, seconds, 200, cap=150.0)
