@@ -140,25 +140,32 @@ def cpu_baseline(batch: int, num_actions: int, seconds: float):
                       f"{shown - t0:.0f} s", file=sys.stderr, flush=True)
         return batch * n / (time.perf_counter() - t0), n
 
-    # Every visible host core (the box's OMP_NUM_THREADS, 16, is ignored here: SURVEY §8(d)
-    # times the reference CPU learner on the host cores of the same box), at least 200 timed
-    # steps (capped at 150 s); then 16 threads and 1 thread on bounded samples.
+    # Three thread counts (SURVEY §8(d) times the reference CPU learner on the host cores of
+    # the same box): every visible core (sched_getaffinity; the box's OMP_NUM_THREADS, 16, is
+    # ignored), 16 threads and 1 thread.  On the GPU box 256 cores are visible but the box's
+    # CPU share is 16 (round 5: 256 threads ran 29 transitions/s, 9 steps in 150 s, against
+    # 2,603/s on 16 threads), so the all-cores sample is bounded (`seconds`, at least 1 step)
+    # and the 16-thread one takes the >= 200 timed steps; `value` is the fastest of the three
+    # and `cores` its thread count, with all three reported.
     cores = len(os.sched_getaffinity(0))
     print(f"[bench] cpu baseline: {cores} visible cores, then 16 threads, then 1", file=sys.stderr,
           flush=True)
     prev = torch.get_num_threads()
     try:
-        v_all, n_all = timed(cores, seconds, 200, cap=150.0)
-        v_16, n_16 = timed(min(16, cores), seconds / 2, 2)
+        v_all, n_all = timed(cores, seconds, 1, cap=seconds)
+        t16 = min(16, cores)
+        v_16, n_16 = timed(t16, seconds, 200, cap=150.0)
         v_one, n_one = timed(1, seconds / 2, 1)
     finally:
         torch.set_num_threads(prev)
-    return dict(value=round(v_all, 2), unit="transitions/s", cores=cores, kind="port",
+    best = max((v_all, cores), (v_16, t16), (v_one, 1))
+    return dict(value=round(best[0], 2), unit="transitions/s", cores=best[1], kind="port",
+                value_all_cores=round(v_all, 2), visible_cores=cores,
                 value_16threads=round(v_16, 2), value_1thread=round(v_one, 2),
                 sample=(f"float32 torch-CPU restatement of the TF DQN step (oracle/dqn_torch.py) "
                         f"+ C sum-tree oracle over 1,000,000 slots (frames from a {pool}-slot "
-                        f"host pool), batch {batch}: {n_all} timed steps on all {cores} visible "
-                        f"cores, {n_16} on {min(16, cores)} threads, {n_one} on 1 thread; "
+                        f"host pool), batch {batch}: {n_16} timed steps on {t16} threads, {n_all} "
+                        f"on all {cores} visible cores, {n_one} on 1 thread; value = the fastest; "
                         f"{cpu_model()}"))
 
 
