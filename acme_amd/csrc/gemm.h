@@ -361,7 +361,7 @@ __device__ __forceinline__ void gemm_f32_block(const P& p, const int tile, const
     // it is stored to LDS, so a k-group's short k range (the small GEMMs of D4PG: 4 stages)
     // waits out about one load latency instead of one per stage.  Loads past the group's end
     // read zeros (fetch_s), so they need no branch.
-    constexpr int R = F32_RING;
+    constexpr int R = F32_RING > 0 ? F32_RING : 2;  // (the else branch runs when F32_RING is 0)
     f32x4 qa[R][PA::PER_THREAD], qb[R][PB::PER_THREAD];
     auto fetch_s = [&](auto S, int k0) {
       constexpr int q = decltype(S)::value;
