@@ -254,18 +254,10 @@ __global__ void __launch_bounds__(256) ln_first_kernel(const LnFirstPair pair) {
 #pragma unroll
     for (int r = 0; r < kRows; ++r) acc[r][c] = 0.f;
     if (j < a.H) {
-      // The weights in chunks of 16 loads issued together (a plain loop over k waited out
-      // one load per k: din = 24-30 dependent round trips).
-      for (int k0 = 0; k0 < din; k0 += 16) {
-        float wk[16];
+      for (int k = 0; k < din; ++k) {
+        const float wk = a.w[(size_t)k * a.H + j];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) wk[u] = a.w[(size_t)min(k0 + u, din - 1) * a.H + j];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-          if (k0 + u >= din) break;
-#pragma unroll
-          for (int r = 0; r < kRows; ++r) acc[r][c] = fmaf(xs[r][k0 + u], wk[u], acc[r][c]);
-        }
+        for (int r = 0; r < kRows; ++r) acc[r][c] = fmaf(xs[r][k], wk, acc[r][c]);
       }
       const float bj = a.b[j];
 #pragma unroll
@@ -347,23 +339,11 @@ __global__ void __launch_bounds__(256) policy_head_kernel(const PolicyHeadPair p
   float acc[ACME_D4PG_MAX_ACT];
 #pragma unroll
   for (int j = 0; j < ACME_D4PG_MAX_ACT; ++j) acc[j] = 0.f;
-  // Four k's per lane loaded together before their FMAs (same order of accumulation).
-  for (int k0 = lane; k0 < H; k0 += 256) {
-    float hv[4], wv[4][ACME_D4PG_MAX_ACT];
+  for (int k = lane; k < H; k += 64) {
+    const float hv = h[(size_t)row * H + k];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int k = min(k0 + 64 * u, H - 1);
-      hv[u] = h[(size_t)row * H + k];
-#pragma unroll
-      for (int j = 0; j < ACME_D4PG_MAX_ACT; ++j) wv[u][j] = w[(size_t)k * A + min(j, A - 1)];
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (k0 + 64 * u >= H) break;
-#pragma unroll
-      for (int j = 0; j < ACME_D4PG_MAX_ACT; ++j)
-        if (j < A) acc[j] = fmaf(hv[u], wv[u][j], acc[j]);
-    }
+    for (int j = 0; j < ACME_D4PG_MAX_ACT; ++j)
+      if (j < A) acc[j] = fmaf(hv, w[(size_t)k * A + j], acc[j]);
   }
   float mine = 0.f;
 #pragma unroll

@@ -236,10 +236,6 @@ constexpr int gemm_smem_floats() {
   return STAGE_FLOATS > RED_ALL ? STAGE_FLOATS : RED_ALL;
 }
 
-#ifndef F32_RING
-#define F32_RING 4  // register ring depth of the f32 engine's k loop (0: the round-4 loop)
-#endif
-
 // One output tile (`tile`, reduction split `split`) of problem p, LDS at `smem`
 // (gemm_smem_floats<...>() floats).  Blocks whose tile lies past p's extent leave at once
 // (block-uniform, before any barrier).
@@ -325,11 +321,18 @@ __device__ __forceinline__ void gemm_f32_block(const P& p, const int tile, const
   constexpr bool kColSum = HasColSum<P>::value;
   const bool do_colsum = kColSum && m0 == 0 && tid < BN;
   float colsum = 0.f;
-  // One stage's MFMAs: the k-group's stage kt from LDS buffer kt & 1.
-  auto compute = [&](int kt) {
+  if (nk > 0) {
+    fetch(kbeg);
+    stash(0);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk_all; ++kt) {
+    const bool active = kt < nk;  // uniform per k-group
+    const bool more = kt + 1 < nk;
+    if (more) fetch(kbeg + (kt + 1) * BK);
     const float* sa = my + (kt & 1) * STAGE;
     const float* sb = sa + PA::FLOATS;
-    {
+    if (active) {
       if constexpr (kColSum) {
         if (do_colsum) {
 #pragma unroll
@@ -355,82 +358,8 @@ __device__ __forceinline__ void gemm_f32_block(const P& p, const int tile, const
               acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][t], bf[j][t], acc[i][j], 0, 0, 0);
       }
     }
-  };
-  if constexpr (F32_RING > 0) {
-    // Register ring of F32_RING stages: a stage's loads are issued F32_RING - 1 stages before
-    // it is stored to LDS, so a k-group's short k range (the small GEMMs of D4PG: 4 stages)
-    // waits out about one load latency instead of one per stage.  Loads past the group's end
-    // read zeros (fetch_s), so they need no branch.
-    constexpr int R = F32_RING > 0 ? F32_RING : 2;  // (the else branch runs when F32_RING is 0)
-    f32x4 qa[R][PA::PER_THREAD], qb[R][PB::PER_THREAD];
-    auto fetch_s = [&](auto S, int k0) {
-      constexpr int q = decltype(S)::value;
-#pragma unroll
-      for (int i = 0; i < PA::PER_THREAD; ++i) {
-        const int k = k0 + PA::kk_of(tid + i * NTG);
-        qa[q][i] = (PA::owns(tid + i * NTG) && k < kend) ? p.a_load(arow[i], k) : zero4();
-      }
-#pragma unroll
-      for (int i = 0; i < PB::PER_THREAD; ++i) {
-        const int k = k0 + PB::kk_of(tid + i * NTG);
-        qb[q][i] = (PB::owns(tid + i * NTG) && k < kend) ? p.b_load(brow[i], k) : zero4();
-      }
-    };
-    auto stash_s = [&](auto S, int buf) {
-      constexpr int q = decltype(S)::value;
-      float* sa = my + buf * STAGE;
-      float* sb = sa + PA::FLOATS;
-#pragma unroll
-      for (int i = 0; i < PA::PER_THREAD; ++i)
-        if (PA::owns(tid + i * NTG)) PA::store(sa, tid + i * NTG, qa[q][i]);
-#pragma unroll
-      for (int i = 0; i < PB::PER_THREAD; ++i)
-        if (PB::owns(tid + i * NTG)) PB::store(sb, tid + i * NTG, qb[q][i]);
-    };
-    using Q0 = std::integral_constant<int, 0>;
-    using Q1 = std::integral_constant<int, 1 % R>;
-    using Q2 = std::integral_constant<int, 2 % R>;
-    using Q3 = std::integral_constant<int, 3 % R>;
-    static_assert(R == 2 || R == 4, "ring of 2 or 4 stages");
-    fetch_s(Q0{}, kbeg);
-    fetch_s(Q1{}, kbeg + BK);
-    if constexpr (R == 4) {
-      fetch_s(Q2{}, kbeg + 2 * BK);
-      fetch_s(Q3{}, kbeg + 3 * BK);
-    }
-    stash_s(Q0{}, 0);
+    if (more) stash((kt + 1) & 1);
     __syncthreads();
-    // Iteration kt: compute stage kt; store stage kt + 1 (ring slot (kt + 1) % R) into the
-    // other buffer (last read in iteration kt - 1, before the barrier); fetch stage kt + R
-    // into slot kt % R (its stage was stored in iteration kt - 1).
-    auto iter = [&](auto S, auto N, int kt) {
-      if (kt < nk) compute(kt);  // uniform per k-group
-      stash_s(N, (kt + 1) & 1);
-      fetch_s(S, kbeg + (kt + R) * BK);
-      __syncthreads();
-    };
-    for (int kt = 0; kt < nk_all; kt += R) {
-      iter(Q0{}, Q1{}, kt);
-      if (kt + 1 < nk_all) iter(Q1{}, Q2{}, kt + 1);
-      if constexpr (R == 4) {
-        if (kt + 2 < nk_all) iter(Q2{}, Q3{}, kt + 2);
-        if (kt + 3 < nk_all) iter(Q3{}, Q0{}, kt + 3);
-      }
-    }
-  } else {
-    if (nk > 0) {
-      fetch(kbeg);
-      stash(0);
-    }
-    __syncthreads();
-    for (int kt = 0; kt < nk_all; ++kt) {
-      const bool active = kt < nk;  // uniform per k-group
-      const bool more = kt + 1 < nk;
-      if (more) fetch(kbeg + (kt + 1) * BK);
-      if (active) compute(kt);
-      if (more) stash((kt + 1) & 1);
-      __syncthreads();
-    }
   }
 
   if constexpr (WK > 1) {
