@@ -232,6 +232,8 @@ _SIGS = {
     "acme_r2d2_step": (c_i32, [c_vp, ctypes.POINTER(SequenceBatch), c_vp,
                                ctypes.POINTER(R2D2Outputs), c_vp]),
     "acme_r2d2_params_changed": (c_i32, [c_vp]),
+    "acme_r2d2_scale_state": (c_i32, [c_vp, c_vp, c_i32, ctypes.POINTER(c_i32)]),
+    "acme_r2d2_set_scale_state": (c_i32, [c_vp, c_vp, c_i32]),
     "acme_r2d2_skipped_steps": (c_i64, [c_vp]),
     "acme_r2d2_guard_state": (c_i32, [c_vp, ctypes.POINTER(c_i64)]),
     "acme_r2d2_skip_word": (c_vp, [c_vp]),

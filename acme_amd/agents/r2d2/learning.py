@@ -47,7 +47,14 @@ class R2D2Learner(core.Learner, core.Saveable):
                  max_replay_size: int = 1_000_000, learning_rate: float = 1e-3,
                  store_lstm_state: bool = True, max_priority_weight: float = 0.9,
                  n_step: int = 5, batch_size: Optional[int] = None, seed: int = 0,
-                 target_seed: Optional[int] = None, device=None):
+                 target_seed: Optional[int] = None, device=None,
+                 on_plane_overflow: str = "skip"):
+        # A step whose f16 planes overflowed (or whose LSTM unroll timed out) is skipped on
+        # the device and the scales recalibrated ("skip", as IMPALA), or raises
+        # FloatingPointError at the next step() ("raise").
+        if on_plane_overflow not in ("skip", "raise"):
+            raise ValueError("on_plane_overflow must be 'skip' or 'raise'")
+        self._on_overflow = on_plane_overflow
         self._env_spec = environment_spec
         self._network = network
         self._iterator = iter(dataset)
@@ -75,6 +82,10 @@ class R2D2Learner(core.Learner, core.Saveable):
         n = self._native.skipped_steps  # pinned host word: no synchronisation
         if n != self._skips_seen:
             self._skips_seen = n
+            if self._on_overflow == "raise":
+                raise FloatingPointError(
+                    f"R2D2 learner: {n} step(s) skipped on f16 plane overflow or an LSTM "
+                    "timeout (their updates were not applied)")
             self._native.params_changed()  # recalibrate the plane scales before the next step
         return n
 
@@ -138,10 +149,14 @@ class R2D2Learner(core.Learner, core.Saveable):
 
     def save(self) -> Dict:
         n = self._native
+        # The DQN / IMPALA learners' format: Adam's t (the updates applied) as
+        # optimizer["step"], num_steps the step() calls, and the f16 plane scales, so a
+        # resumed run is bit-identical to an uninterrupted one.
         return {"network": n.get_params("params"), "target_network": n.get_params("target"),
                 "optimizer": {"m": n.get_params("m"), "v": n.get_params("v"),
-                              "step": n.num_steps, "applied_steps": n.guard_state()["applied"]},
-                "num_steps": n.num_steps}
+                              "step": n.guard_state()["applied"]},
+                "num_steps": n.num_steps,
+                "plane_scales": n.scale_state()}
 
     def restore(self, state: Dict):
         n = self._native
@@ -149,6 +164,10 @@ class R2D2Learner(core.Learner, core.Saveable):
         for buf, src in ((n.m, state["optimizer"]["m"]), (n.v, state["optimizer"]["v"])):
             for k, t in n.views(buf).items():
                 t.copy_(torch.as_tensor(np.asarray(src[k], np.float32)).view(t.shape))
+        n.params_changed()
+        if "plane_scales" in state:
+            n.set_scale_state(state["plane_scales"])
         n.num_steps = int(state["num_steps"])
-        if "applied_steps" in state["optimizer"]:
-            n.set_applied_steps(int(state["optimizer"]["applied_steps"]))
+        opt = state["optimizer"]
+        # round-4 checkpoints: "step" = num_steps, the applied count in "applied_steps"
+        n.set_applied_steps(int(opt.get("applied_steps", opt.get("step", state["num_steps"]))))

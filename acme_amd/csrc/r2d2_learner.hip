@@ -1119,6 +1119,33 @@ int acme_r2d2_params_changed(acme_r2d2* l) {
   return ACME_OK;
 }
 
+int acme_r2d2_scale_state(const acme_r2d2* l, float* out, int32_t capacity, int32_t* count) {
+  ACME_CHECK_ARG(l && count, "null argument");
+  *count = l->scales ? 4 * kScCount : 0;
+  if (!l->scales || !out) return ACME_OK;
+  ACME_CHECK_ARG(capacity >= 4 * kScCount, "scale state needs %d floats", 4 * kScCount);
+  ACME_HIP_TRY(hipDeviceSynchronize());
+  for (int i = 0; i < kScCount; ++i)
+    ACME_HIP_TRY(hipMemcpy(out + 4 * i, l->scales + i, 4 * sizeof(float), hipMemcpyDeviceToHost));
+  return ACME_OK;
+}
+
+int acme_r2d2_set_scale_state(acme_r2d2* l, const float* in, int32_t count) {
+  ACME_CHECK_ARG(l && in, "null argument");
+  ACME_CHECK_ARG(l->scales && count == 4 * kScCount, "scale state of %d floats expected, got %d",
+                 l->scales ? 4 * kScCount : 0, count);
+  for (int i = 0; i < 4 * kScCount; ++i) {
+    int e;
+    const float m = std::frexp(in[i], &e);
+    ACME_CHECK_ARG(m == 0.5f, "scale state entries must be powers of two");
+  }
+  ACME_HIP_TRY(hipDeviceSynchronize());
+  for (int i = 0; i < kScCount; ++i)
+    ACME_HIP_TRY(hipMemcpy(l->scales + i, in + 4 * i, 4 * sizeof(float), hipMemcpyHostToDevice));
+  l->scales_ok = true;
+  return ACME_OK;
+}
+
 int acme_r2d2_step(acme_r2d2* l, const acme_sequence_batch* b, const double* probabilities,
                    const acme_r2d2_outputs* out, void* stream) {
   ACME_CHECK_ARG(l && b && probabilities, "null argument");

@@ -1071,6 +1071,23 @@ class NativeR2D2:
         """Steps skipped on plane overflow among those the device finished."""
         return int(lib().acme_r2d2_skipped_steps(self._h))
 
+    def scale_state(self) -> np.ndarray:
+        """The plane scales (learner state for checkpoints; empty without the plane path)."""
+        n = ctypes.c_int32(0)
+        check(lib().acme_r2d2_scale_state(self._h, None, 0, ctypes.byref(n)), "r2d2 scales")
+        out = np.zeros(n.value, np.float32)
+        if n.value:
+            check(lib().acme_r2d2_scale_state(self._h, out.ctypes.data, n.value,
+                                              ctypes.byref(n)), "r2d2 scales")
+        return out
+
+    def set_scale_state(self, state) -> None:
+        """Restores scale_state() (after params_changed): resumed steps are bit-identical."""
+        a = np.ascontiguousarray(np.asarray(state, np.float32))
+        if a.size:
+            check(lib().acme_r2d2_set_scale_state(self._h, a.ctypes.data, a.size),
+                  "r2d2 set_scale_state")
+
     def guard_state(self) -> Dict[str, int]:
         """{applied, skipped, last_skipped} (synchronises the device)."""
         a = (ctypes.c_int64 * 3)()

@@ -698,6 +698,10 @@ int acme_r2d2_bind(acme_r2d2* l, float* params, float* target, float* grads, flo
 /* The caller wrote params / target directly (initialisation, restore): the Atari plane path
  * recalibrates its scales before the next step (as acme_impala_params_changed). */
 int acme_r2d2_params_changed(acme_r2d2* l);
+/* Plane scales as learner state (as acme_dqn_scale_state / acme_dqn_set_scale_state): a
+ * checkpoint restored with them resumes bit-identically (0 floats without the plane path). */
+int acme_r2d2_scale_state(const acme_r2d2* l, float* out, int32_t capacity, int32_t* count);
+int acme_r2d2_set_scale_state(acme_r2d2* l, const float* in, int32_t count);
 /* Step guard (as the DQN / IMPALA learners'): a step whose plane writes overflowed (Atari
  * plane path) or whose one-launch LSTM timed out applies no update; out3 = {applied,
  * skipped, last step skipped}; acme_r2d2_skipped_steps reads a pinned host mirror;

@@ -125,9 +125,12 @@ def test_r2d2_learner_through_sequence_replay():
     assert n.guard_state()["applied"] == 3
     # save / restore into a fresh learner on the same replay.
     state = learner.save()
+    # The DQN / IMPALA checkpoint format: Adam's t as optimizer["step"], and the plane scales.
+    assert state["optimizer"]["step"] == 3 and "plane_scales" in state
     other = R2D2Learner(spec, net, net, dataset=dataset, **dict(kw, seed=11))
     other.restore(state)
     assert other.num_steps == 3
+    np.testing.assert_array_equal(other.native.scale_state(), n.scale_state())
     for which in ("params", "target", "m", "v"):
         a, c = n.get_params(which), other.native.get_params(which)
         for name in a:
