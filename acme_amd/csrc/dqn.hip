@@ -159,7 +159,8 @@ struct acme_dqn {
   // (ACME_V_WSN=1).
   bool single_stream = false;
   bool single_role = false;
-  // conv1 reads the batch's uint8 frames (ACME_V_F16FRAMES=1: an f16 copy, the round-4 path)
+  // conv1 reads the batch's uint8 frames (unless the batch carries the f16 copy, obs_f16, or
+  // the frames are not 16-byte aligned: then the step makes the f16 copy, the round-4 path)
   bool frames_u8 = true;
   // Step guard (kernels.h StepGuard): the skip-on-overflow rule of the plane engine, Adam's
   // device step count (applied updates) on every path.  seq counts the steps issued (the
@@ -790,7 +791,6 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
   l->single_stream = tune_variant("SIDE") == 1;
   l->single_role = tune_variant("WSN") == 1;
   l->stamps_on = tune_variant("STAMPS") == 1;
-  l->frames_u8 = tune_variant("F16FRAMES") != 1;
   const int A = cfg->num_actions;
   const int B = cfg->max_batch;
   int rc = ACME_OK;

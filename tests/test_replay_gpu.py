@@ -170,6 +170,34 @@ def test_priority_updates_deep_tree(n_upd):
         _cmp_sample(r, o, 512, 200 + it)
 
 
+@pytest.mark.parametrize("capacity", [1024, 1088, 65536, 69632])
+def test_top_level_computed_and_stored(capacity):
+    """The top level's entries with children are computed by the readers when there are at
+    most 16 of them (replay.hip kTopComputed; the one-launch update then leaves the stored
+    top alone) and read when there are more: 1024 / 65536 slots have 16, 1088 / 69632 have
+    17.  Both paths: draws, probabilities and the sampling mass bit-exact against the
+    oracle after one-launch priority updates (a total that read a stale top would differ)."""
+    import ctypes
+    from acme_amd._lib import lib
+    rng = np.random.default_rng(capacity)
+    r = _native(capacity, [4], True)
+    o = OracleTable(capacity, True, 0.6, 1234)
+    pr = rng.uniform(0.1, 2.0, capacity)
+    r.insert([np.zeros((capacity, 1), np.int32)], pr)
+    o.insert(pr)
+    out = torch.zeros(1, dtype=torch.float64, device="cuda")
+    for it in range(3):
+        keys = rng.integers(0, capacity, 512).astype(np.uint64)
+        newp = rng.uniform(0.0, 3.0, 512)
+        r.update_priorities(torch.as_tensor(keys.view(np.int64)).cuda().view(torch.uint64),
+                            torch.as_tensor(newp).cuda())
+        o.update(keys, newp)
+        _cmp_sample(r, o, 512, 300 + it)
+        assert lib().acme_replay_total(r._h, ctypes.c_void_p(out.data_ptr()), None) == 0
+        torch.cuda.synchronize()
+        assert out.item() == o.total(), (it, out.item(), o.total())
+
+
 @pytest.mark.parametrize("prefetch", [0, 1, 4])
 def test_prefetched_dataset_draw_order(prefetch):
     """make_reverb_dataset(prefetch_size=P): batch k is drawn (Philox counter k) after the

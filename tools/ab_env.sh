@@ -1,6 +1,6 @@
 # A/B of two environment settings on a workload's step (same library): alternating 300-step
 # runs, then one profiled run each.  Usage: A="..." B="..." [W=d4pg] bash tools/ab_env.sh OUTDIR
-#   e.g. A="" B="ACME_V_F16FRAMES=1 ACME_DATASET_F16=1"
+#   e.g. A="" B="ACME_DATASET_F16=1"
 set -e
 O=${1:-gpurun_out/abe}; mkdir -p $O
 for i in 1 2 3; do
