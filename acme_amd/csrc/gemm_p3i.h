@@ -130,9 +130,6 @@ struct ImgGeomPairs {
   }
 };
 
-#ifndef P3I_OCC
-#define P3I_OCC 1  // see P3ICfg::MINW
-#endif
 #ifndef P3I_SCHED
 #define P3I_SCHED 1  // fenced issue order in the image-resident kernels' k loop (round 5: step
                      // 0.4969 -> 0.4949 ms, three alternating 300-step runs)
@@ -155,16 +152,10 @@ struct P3ICfg {
   static constexpr int STAGE_B = PB::BYTES;
   static constexpr int MAIN = IMG + 2 * STAGE_B;
   static constexpr int LDS = MAIN > Core::EPI_BYTES ? MAIN : Core::EPI_BYTES;
-  // Occupancy: when the LDS admits three blocks of at most 8 waves per CU (conv3's forward:
-  // 47 KB, 8 waves), ask for 6 waves per SIMD, so the registers (88 VGPRs unconstrained, 5
-  // waves) do not cut it to two blocks (P3I_OCC).
-  static constexpr int WGS = (160 * 1024) / LDS;
-  static constexpr int MINW = (P3I_OCC && NW <= 8 && WGS >= 3) ? 6 : 1;
 };
 
 template <class GI, int FPB, int BN, int WM, int WN, int MT, class P>
-__global__ void __launch_bounds__(64 * WM * WN, (P3ICfg<GI, FPB, BN, WM, WN, MT, P>::MINW))
-    gemm_p3i_kernel(const P p_in, int frames) {
+__global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, int frames) {
   using Cfg = P3ICfg<GI, FPB, BN, WM, WN, MT, P>;
   using C = typename Cfg::Core;
   using PB = typename Cfg::PB;
