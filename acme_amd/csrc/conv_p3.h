@@ -106,6 +106,7 @@ struct P3ConvFwd {
   // 0 there), e.g. o_tm1 and o_t of a batch in two buffers.
   PlaneSrc a_src2{};
   int a_split = 1 << 30;
+  uint64_t* stamps = nullptr;  // timing experiment (gemm_p3i.h phase stamps, HasStamps)
   __device__ gemm::PScale* amax_sc() const { return y.sc; }
   struct ARow {
     int pix;  // element offset of (frame, ih0, iw0)

@@ -169,6 +169,17 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
+  // Phase stamps (timing experiment, as gemm_p3ws_kernel's): entry, after the image fill's
+  // barrier, after the k loop, exit.
+  uint64_t st_rt0 = 0, st_t0 = 0, st_t1 = 0, st_t2 = 0;
+  bool stamp = false;
+  if constexpr (HasStamps<P>::value) {
+    stamp = p_in.stamps != nullptr && tid == 0;
+    if (stamp) {
+      st_rt0 = __builtin_amdgcn_s_memrealtime();
+      st_t0 = __builtin_amdgcn_s_memtime();
+    }
+  }
   const int f0 = blockIdx.x * FPB;
   const int nf = frames - f0 < FPB ? frames - f0 : FPB;
   const int rows = nf * GI::OPIX;
@@ -291,6 +302,8 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
     ln[i] = GI::lane(f, lr - f * GI::OPIX, lr < rows);
   }
   __syncthreads();
+  if constexpr (HasStamps<P>::value)
+    if (stamp) st_t1 = __builtin_amdgcn_s_memtime();
 
   f32x16 acc[MT][NTL];
 #pragma unroll
@@ -378,7 +391,20 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
   if (kt < nk) iter(S0{}, kt);
 
   f32x16 cs[C::NCS];
+  if constexpr (HasStamps<P>::value)
+    if (stamp) st_t2 = __builtin_amdgcn_s_memtime();
   C::epilogue(p, smem, m0, 0, wave, wm, wn, lane, 0, acc, cs, false);
+  if constexpr (HasStamps<P>::value) {
+    if (stamp) {
+      uint64_t* o = p_in.stamps + 8 * (int64_t)blockIdx.x;
+      o[0] = st_rt0;
+      o[1] = __builtin_amdgcn_s_memrealtime();
+      o[2] = st_t0;
+      o[3] = st_t1;
+      o[4] = st_t2;
+      o[5] = __builtin_amdgcn_s_memtime();
+    }
+  }
 }
 
 // frames: the number of images (p.M = frames * GI::OPIX rows).

@@ -60,6 +60,11 @@ struct PWeights {
   Plane w1, w2, w3;  // views into the flat parameter planes
   const float *b1, *b2, *b3;
 };
+// Timing experiment (ACME_V_STAMPS=1, tools/gemm_stamps.py): when set, the online
+// forward's conv1 / conv2 / conv3 launches stamp their workgroups' phases here
+// ([workgroups][8] u64 each, gemm_p3i.h).
+extern uint64_t* g_stamps_conv[3];
+
 struct PActs {
   Plane x1, x2, x3;
 };

@@ -195,8 +195,9 @@ inline PlaneSrc frames_src(const Frames& f, int rows) {
 // conv1 forward (image-resident) over `rows` frames into y, f16 or uint8 frames.
 template <bool U8>
 int conv1_fwd_p3(const PWeights& w, const Frames& frames, int rows, const Planes& y,
-                 hipStream_t st) {
+                 hipStream_t st, uint64_t* stamps = nullptr) {
   P3ConvFwd<G1, 1, U8> p;
+  p.stamps = stamps;
   p.M = rows * G1::OPIX; p.N = G1::CO; p.K = G1::K; p.k_chunk = G1::K;
   const int n1 = U8 ? std::min(rows, frames.split) : rows;
   p.a_src = frames_src(frames, n1); p.b_src = src(w.w1, G1::K * G1::CO);
@@ -266,6 +267,8 @@ int p3_wgrad_reduce(const P& p, int splits, float* slab, float* dw, float* db, c
 
 }  // namespace
 
+uint64_t* g_stamps_conv[3] = {nullptr, nullptr, nullptr};
+
 int64_t wgrad_slab_floats_p3() {
   return std::max<int64_t>({(int64_t)kP3MaxWgradSplits * (G1::K + 1) * G1::CO,
                             (int64_t)kP3MaxWgradSplits * (G2::K + 1) * G2::CO,
@@ -286,14 +289,15 @@ int forward_p3(const PWeights& w, const Frames& frames, int rows, const PActs& a
       (rc = frames.u8 ? conv12_fwd_p3<true>(w, frames, rows, nsep, a, st)
                       : conv12_fwd_p3<false>(w, frames, rows, nsep, a, st)) != ACME_OK)
     return rc;
-  if (nsep > 0 && (rc = frames.u8 ? conv1_fwd_p3<true>(w, frames, nsep, pl(a.x1), st)
-                                  : conv1_fwd_p3<false>(w, frames, nsep, pl(a.x1), st)) != ACME_OK)
+  if (nsep > 0 && (rc = frames.u8 ? conv1_fwd_p3<true>(w, frames, nsep, pl(a.x1), st, g_stamps_conv[0])
+                                  : conv1_fwd_p3<false>(w, frames, nsep, pl(a.x1), st, g_stamps_conv[0])) != ACME_OK)
     return rc;
   if (nsep > 0) {
     P3ConvFwd<G2, gemm::kPlanes> p;
     p.M = nsep * G2::OPIX; p.N = G2::CO; p.K = G2::K; p.k_chunk = G2::K;
     p.a_src = src(a.x1, (int64_t)nsep * kX1); p.b_src = src(w.w2, G2::K * G2::CO);
     p.bias = w.b2; p.y = pl(a.x2);
+    p.stamps = g_stamps_conv[1];
     // Image-resident x1 (gemm_p3i.h; two frames, 8 x 2 waves per block): with two f16
     // planes a frame's x1 image is 56 KB, so two frames and the weight ring fit one CU.
     // Step 0.573 -> 0.551 ms against the producer / consumer im2col kernel (two alternating
@@ -305,6 +309,7 @@ int forward_p3(const PWeights& w, const Frames& frames, int rows, const PActs& a
     p.M = rows * G3::OPIX; p.N = G3::CO; p.K = G3::K; p.k_chunk = G3::K;
     p.a_src = src(a.x2, (int64_t)rows * kFlat); p.b_src = src(w.w3, G3::K * G3::CO);
     p.bias = w.b3; p.y = pl(a.x3);
+    if (keep_x1 != 0) p.stamps = g_stamps_conv[2];  // the online forward's
     // Image-resident, 4 x 2 waves (measured 50.1 -> 43.5 us vs the 128x64 im2col engine;
     // two frames per block measured slower on the step, 0.550 -> 0.568-0.618 ms).
     P3I_GEMM("conv3_fwd", I3F, 1, 64, 4, 2, 1, p, rows);

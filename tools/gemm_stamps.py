@@ -1,4 +1,4 @@
-"""Phase stamps of the online fc_fwd launch (gemm_p3.h HasStamps; ACME_V_STAMPS=1): the
+"""Phase stamps of the online fc_fwd, conv1_fwd, conv2_fwd and conv3_fwd launches (gemm_p3.h HasStamps; ACME_V_STAMPS=1): the
 bench's DQN learner runs a few steps, then each workgroup's entry / exit (s_memrealtime,
 100 MHz, comparable across workgroups) and its prologue, k loop and epilogue lengths
 (s_memtime, shader clocks) are summarised.  Run under gpurun: python3 tools/gemm_stamps.py"""
@@ -29,21 +29,23 @@ def main():
     for _ in range(5):
         d.step(o, a, r, dd, o2, pr)
     torch.cuda.synchronize()
-    st = d.debug_buffer("gemm_stamps").view(np.int64).reshape(4096, 8)
-    st = st[st[:, 0] != 0]
-    n = len(st)
-    rt0, rt1, t0, t1, t2, t3 = (st[:, i].astype(np.float64) for i in range(6))
-    clk = (t3 - t0) / ((rt1 - rt0) * 10e-3)  # shader clocks per us
-    print(f"{n} workgroups; shader clock {np.median(clk):.0f} MHz (median)")
-    span = (rt1.max() - rt0.min()) * 0.01
-    print(f"launch span (first entry to last exit) {span:.1f} us; entry spread "
-          f"{(rt0.max() - rt0.min()) * 0.01:.1f} us; exit spread {(rt1.max() - rt1.min()) * 0.01:.1f} us")
-    mhz = np.median(clk)
-    for name, v in (("prologue (to first barrier)", t1 - t0), ("k loop", t2 - t1),
-                    ("epilogue", t3 - t2), ("total", t3 - t0)):
-        us = v / mhz
-        print(f"  {name:28s} median {np.median(us):6.2f} us  min {us.min():6.2f}  max {us.max():6.2f}")
-
+    allst = d.debug_buffer("gemm_stamps").view(np.int64).reshape(4, 4096, 8)
+    for name, st in zip(("fc_fwd (online)", "conv1_fwd", "conv2_fwd", "conv3_fwd (online)"),
+                        allst):
+        st = st[st[:, 0] != 0]
+        if not len(st):
+            continue
+        rt0, rt1, t0, t1, t2, t3 = (st[:, i].astype(np.float64) for i in range(6))
+        mhz = np.median((t3 - t0) / ((rt1 - rt0) * 10e-3))  # shader clocks per us
+        print(f"{name}: {len(st)} workgroups; shader clock {mhz:.0f} MHz (median); launch "
+              f"span {(rt1.max() - rt0.min()) * 0.01:.1f} us, entry spread "
+              f"{(rt0.max() - rt0.min()) * 0.01:.1f} us, exit spread "
+              f"{(rt1.max() - rt1.min()) * 0.01:.1f} us")
+        for ph, v in (("prologue (to first barrier)", t1 - t0), ("k loop", t2 - t1),
+                      ("epilogue", t3 - t2), ("total", t3 - t0)):
+            us = v / mhz
+            print(f"  {ph:28s} median {np.median(us):6.2f} us  min {us.min():6.2f}  max "
+                  f"{us.max():6.2f}")
 
 if __name__ == "__main__":
     main()
