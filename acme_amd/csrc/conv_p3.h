@@ -157,6 +157,38 @@ struct P3ConvFwd {
     act8(n, acc, v);
     return put8(y, (int64_t)m * G::CO + n, v);
   }
+  // The epilogue's constants for columns n..n+7, loaded before the k loop (gemm_p3.h EpiPre).
+  struct Pre {
+    float b[8];
+    float rs, w;
+    uint32_t* flag;
+  };
+  __device__ Pre pre(int n) const {
+    Pre q;
+    const int nn = n < N ? n : 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) q.b[j] = bias[nn + j];
+    q.rs = gemm::result_scale(a_src, b_src);
+    q.w = y.sc->w;
+    q.flag = y.sc->flag;
+    return q;
+  }
+  __device__ float store8p(int m, int n, const V8& acc, int, const Pre& q) const {
+    V8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float x = acc[j] * q.rs;
+      if constexpr (NPA == 1) x = x / 255.0f;
+      x += q.b[j];
+      v[j] = x > 0.f ? x : 0.f;
+    }
+    uint32_t h[4], l[4];
+    const float mx = split8(v, q.w, h, l);
+    const int64_t e = (int64_t)m * G::CO + n;
+    *reinterpret_cast<uint4*>(y.p + e) = uint4{h[0], h[1], h[2], h[3]};
+    *reinterpret_cast<uint4*>(y.p + y.stride + e) = uint4{l[0], l[1], l[2], l[3]};
+    return mx;
+  }
 };
 
 // ------------------------------------------------------------------ weight grad

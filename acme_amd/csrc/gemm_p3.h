@@ -238,6 +238,35 @@ __device__ __forceinline__ void amax_commit(PScale* sc, float v) {
   }
 }
 
+// As amax_commit, with the record's w and flag loaded beforehand (EpiPre below).
+__device__ __forceinline__ void amax_commit_pre(PScale* sc, float v, float w, uint32_t* flag) {
+  v = wave_max(v);
+  const int wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (sc && (threadIdx.x & 63) == 0 && v != 0.f) {
+    atomicMax(&sc->slot[wid & (kAmaxSlots - 1)].v, __builtin_bit_cast(uint32_t, v));
+    if (!(v * w < 65520.f) && flag) atomicOr(flag, 1u);
+  }
+}
+
+// Problems whose epilogue constants (bias, read scales, the output record's w and flag) a
+// lane can load before the k loop (`Pre pre(int n)` for the lane's 8 columns n..n+7, then
+// `store8p(m, n, v, split, pre)`): their latency then overlaps the k loop instead of
+// stalling the epilogue's first store (round 5 stamps: conv1's epilogue took longer than
+// its k loop).
+template <class P, class = void>
+struct EpiPre {
+  struct type {};
+  static constexpr bool has = false;
+};
+#ifndef EPI_PRE
+#define EPI_PRE 1  // 0: the epilogue loads its constants when it runs (the round-4 order)
+#endif
+template <class P>
+struct EpiPre<P, std::void_t<typename P::Pre>> {
+  using type = typename P::Pre;
+  static constexpr bool has = EPI_PRE != 0;
+};
+
 // A plane tensor: plane i of element e at p[i * stride + e], written as x * sc->w.
 struct Planes {
   uint16_t* p;
@@ -495,12 +524,20 @@ struct P3Core {
   // Epilogue.  C/D map of the 32x32 MFMA: col = lane & 31, row = (v&3) + 8(v>>2) + 4h.
   // The LDS is free (every stage consumed) when this runs; it contains barriers, so all
   // waves of the block call it.
+  // A lane's epilogue columns: n0 + wn TN + epi_col(lane) (the same in every chunk).
+  __device__ static __forceinline__ int epi_col(int lane) {
+    static_assert(64 % (TN / 8) == 0, "a lane's chunk columns repeat");
+    return 8 * (lane % (TN / 8));
+  }
   __device__ static __forceinline__ void epilogue(const P& p, uint8_t* smem, int m0, int n0,
                                                   int wave, int wm, int wn, int lane, int split,
                                                   f32x16 (&acc)[MT][NTL], f32x16 (&cs)[NCS],
-                                                  bool do_colsum) {
+                                                  bool do_colsum,
+                                                  const typename EpiPre<P>::type* pre = nullptr) {
     static_assert(HasStore8<P>::value, "plane problems store 8 columns at a time");
     const int r = lane & 31, h = lane >> 5;
+    typename EpiPre<P>::type pl{};
+    if constexpr (EpiPre<P>::has) pl = pre ? *pre : p.pre(n0 + wn * TN + epi_col(lane));
     // Row-major restage through LDS, one 32-row block of the wave's tile at a time, so
     // each lane finishes 8 consecutive columns of one row (one decode per 8 outputs,
     // 16-byte plane / 32-byte f32 stores).
@@ -524,11 +561,18 @@ struct P3Core {
         const f32x4 lo = *reinterpret_cast<const f32x4*>(cw + row * PITCH + col);
         const f32x4 hi = *reinterpret_cast<const f32x4*>(cw + row * PITCH + col + 4);
         const float v8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        if (m < p.M && n < p.N) amx = amax_max(amx, p.store8(m, n, v8, split));
+        if constexpr (EpiPre<P>::has) {
+          if (m < p.M && n < p.N) amx = amax_max(amx, p.store8p(m, n, v8, split, pl));
+        } else {
+          if (m < p.M && n < p.N) amx = amax_max(amx, p.store8(m, n, v8, split));
+        }
       }
       __syncthreads();
     }
-    if constexpr (HasAmax<P>::value) amax_commit(p.amax_sc(), amx);
+    if constexpr (HasAmax<P>::value) {
+      if constexpr (EpiPre<P>::has) amax_commit_pre(p.amax_sc(), amx, pl.w, pl.flag);
+      else amax_commit(p.amax_sc(), amx);
+    }
     if constexpr (kColSum) {
       if (do_colsum && h == 0) {
 #pragma unroll

@@ -312,6 +312,9 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
     for (int j = 0; j < NTL; ++j)
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
+  // The epilogue's constants, loaded now (their latency hides under the k loop).
+  typename EpiPre<P>::type pre{};
+  if constexpr (EpiPre<P>::has) pre = p.pre(wn * TN + C::epi_col(lane));
 
   auto compute = [&](int k0, int buf) {
     const uint8_t* sb = smem + Cfg::IMG + buf * Cfg::STAGE_B;
@@ -393,7 +396,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
   f32x16 cs[C::NCS];
   if constexpr (HasStamps<P>::value)
     if (stamp) st_t2 = __builtin_amdgcn_s_memtime();
-  C::epilogue(p, smem, m0, 0, wave, wm, wn, lane, 0, acc, cs, false);
+  C::epilogue(p, smem, m0, 0, wave, wm, wn, lane, 0, acc, cs, false, &pre);
   if constexpr (HasStamps<P>::value) {
     if (stamp) {
       uint64_t* o = p_in.stamps + 8 * (int64_t)blockIdx.x;
