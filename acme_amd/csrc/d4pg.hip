@@ -40,14 +40,6 @@ using namespace acme;
 using namespace acme::conv;
 using acme::gemm::launch_gemm;
 
-#ifndef D4PG_BK
-#define D4PG_BK 16  // the dense layers' f32-engine stage depth
-#endif
-#ifndef D4PG_WK
-#define D4PG_WK 8   // k-groups per 32x32 tile
-#endif
-constexpr int kD4BK = D4PG_BK, kD4WK = D4PG_WK;
-
 namespace {
 
 constexpr int kRows = 4;      // rows per block of the LayerNorm row kernels
@@ -626,7 +618,7 @@ struct ConcatWgrad {
 #define D4_GEMM(name, prob)                                                                   \
   do {                                                                                        \
     ACME_PROF_PEAK(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0, 157.3);       \
-    hipError_t _e = launch_gemm<32, 32, 1, 1, kD4BK, kD4WK>(prob, 1, st);                             \
+    hipError_t _e = launch_gemm<32, 32, 1, 1, 16, 8>(prob, 1, st);                             \
     if (_e != hipSuccess) {                                                                   \
       set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
       return ACME_ERR_HIP;                                                                    \
@@ -683,7 +675,7 @@ int dense_fwd_pair(const char* name, const float* x0, int rows0, const float* w0
   }
   auto p = gemm::make_zset(q);
   ACME_PROF_PEAK(name, st, 2.0 * (double)(rows0 + rows1) * N * K, 0.0, 157.3);
-  hipError_t e = launch_gemm<32, 32, 1, 1, kD4BK, kD4WK>(p, 2, st);
+  hipError_t e = launch_gemm<32, 32, 1, 1, 16, 8>(p, 2, st);
   if (e != hipSuccess) {
     set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(e), __FILE__, __LINE__);
     return ACME_ERR_HIP;
@@ -858,7 +850,7 @@ int launch_multi(const char* name, hipStream_t st, const std::vector<Q>&... qs) 
     return (set_error("too many GEMMs in one backward launch"), ACME_ERR_INVALID);
   if (count == 0) return ACME_OK;
   ACME_PROF_PEAK(name, st, flops, 0.0, 157.3);
-  hipLaunchKernelGGL((gemm::gemm_f32_multi_kernel<32, 32, 1, 1, kD4BK, kD4WK, gemm::ZSet<Q, kZ>...>),
+  hipLaunchKernelGGL((gemm::gemm_f32_multi_kernel<32, 32, 1, 1, 16, 8, gemm::ZSet<Q, kZ>...>),
                      dim3((unsigned)tiles, 1, (unsigned)count), dim3(64 * 8), 0, st, m);
   D4_CHECK();
   return ACME_OK;
