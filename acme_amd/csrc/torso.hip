@@ -283,10 +283,7 @@ int forward_p3(const PWeights& w, const Frames& frames, int rows, const PActs& a
   // 0.713 ms per step when it was introduced.  The online forward runs unfused: fusing its
   // o_t rows (x1 kept for the o_tm1 rows only) measured 0.545 -> 0.603 ms per step with
   // the f16 planes (the fused kernel's one block per CU beside the other stream).
-#ifndef C12_OT
-#define C12_OT 0  // experiment: the online forward's o_t rows through the fused conv1 -> conv2
-#endif
-  const int nsep = keep_x1 == 0 ? 0 : (C12_OT && keep_x1 > 0 && keep_x1 < rows ? keep_x1 : rows);
+  const int nsep = keep_x1 == 0 ? 0 : rows;
   int rc;
   if (nsep < rows &&
       (rc = frames.u8 ? conv12_fwd_p3<true>(w, frames, rows, nsep, a, st)
