@@ -452,10 +452,7 @@ int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const torso:
     // both launches, the step unchanged (0.5040 vs 0.5037 ms, three alternating pairs).
     const bool tall = rows > 512;
     const bool ttall = rows == 512 && !defer_head;
-#ifndef FC_ONLINE_SPLITS
-#define FC_ONLINE_SPLITS 8  // experiment: the online launch's split-K
-#endif
-    const int splits = ttall ? 16 : (tall ? FC_ONLINE_SPLITS : kFcFwdSplits);
+    const int splits = ttall ? 16 : kFcFwdSplits;
     p.M = rows; p.N = 2 * kHidden; p.K = kFlat; p.k_chunk = chunk_for(kFlat, splits);
     p.a_src = SRC(x3, (int64_t)rows * kFlat); p.ldx = kFlat;
     p.b_src = SRC(WP(l, wpl, l->t_fcw), (int64_t)kFlat * 2 * kHidden); p.slab = slab;
