@@ -33,8 +33,13 @@
 #include "common.h"
 #include "conv.h"
 #include "gemm.h"
+#include "gemm_direct.h"
 #include "kernels.h"
 #include "profiler.h"
+
+#ifndef D4_DIRECT
+#define D4_DIRECT 1
+#endif
 
 using namespace acme;
 using namespace acme::conv;
@@ -572,7 +577,13 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const LnBwdArgs a) {
 // ------------------------------------------------------------------ weight gradient of the
 // first layer: dW = concat(x0, x1)^T dZ over the batch, bias = column sums of dZ.
 struct ConcatWgrad {
+#if D4_DIRECT
+  // Direct engine: k-contiguous runs over the batch (4 scalar loads per vector, coalesced
+  // across the lanes' features / columns).
+  static constexpr int A_MODE = gemm::KCONTIG, B_MODE = gemm::KCONTIG;
+#else
   static constexpr int A_MODE = gemm::RCONTIG, B_MODE = gemm::RCONTIG;
+#endif
   static constexpr bool kColSum = true;
   int M, N, K, k_chunk;  // M = d0 + d1 (inputs), N = H, K = batch rows
   const float* x0;
@@ -597,14 +608,26 @@ struct ConcatWgrad {
   __device__ f32x4 a_load(const ARow& a, int m) const {
     f32x4 r = gemm::zero4();
     if (m >= K) return r;
+#if D4_DIRECT
+    if (a.i >= M) return r;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = m + j < K ? x_at(m + j, a.i) : 0.f;
+#else
 #pragma unroll
     for (int j = 0; j < 4; ++j) r[j] = x_at(m, a.i + j);
+#endif
     return r;
   }
   __device__ BRow b_row(int n) const { return BRow{n}; }
   __device__ f32x4 b_load(const BRow& b, int m) const {
     if (b.n >= N || m >= K) return gemm::zero4();
+#if D4_DIRECT
+    const float* p = dz + (size_t)m * N + b.n;
+    return f32x4{p[0], m + 1 < K ? p[N] : 0.f, m + 2 < K ? p[2 * N] : 0.f,
+                 m + 3 < K ? p[3 * N] : 0.f};
+#else
     return load_row4<true>(dz + (size_t)m * N, b.n, N);
+#endif
   }
   __device__ void store(int i, int n, float v, int) const { out[(size_t)i * N + n] = v; }
   __device__ void store_colsum(int n, float v, int) const { bias_out[n] = v; }
@@ -612,13 +635,19 @@ struct ConcatWgrad {
 
 // ------------------------------------------------------------------ orchestration
 
-// Small GEMMs: 32x32 output tiles, one wave per tile and k-group, 8 k-groups per block
-// (intra-block split-K: 4 stages of BK 16 per wave at K = 512; 4 groups measured 0.354 ->
-// 0.328 ms per step with 8), so a 512 x 512 x 512 layer runs 2048 waves.
+// Small GEMMs: 32x32 output tiles, 8 waves per block splitting the reduction, so a
+// 512 x 512 x 512 layer runs 2048 waves.  D4_DIRECT (default): the register-operand engine
+// (gemm_direct.h, one load burst per wave); 0: the staged engine (gemm.h, 8 k-groups of
+// BK-16 stages; 4 groups measured 0.354 -> 0.328 ms per step with 8).
+#if D4_DIRECT
+#define D4_LAUNCH(prob, nz) gemm::launch_direct(prob, nz, (prob).K, st)
+#else
+#define D4_LAUNCH(prob, nz) launch_gemm<32, 32, 1, 1, 16, 8>(prob, nz, st)
+#endif
 #define D4_GEMM(name, prob)                                                                   \
   do {                                                                                        \
     ACME_PROF_PEAK(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0, 157.3);       \
-    hipError_t _e = launch_gemm<32, 32, 1, 1, 16, 8>(prob, 1, st);                             \
+    hipError_t _e = D4_LAUNCH(prob, 1);                                                       \
     if (_e != hipSuccess) {                                                                   \
       set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__); \
       return ACME_ERR_HIP;                                                                    \
@@ -675,7 +704,7 @@ int dense_fwd_pair(const char* name, const float* x0, int rows0, const float* w0
   }
   auto p = gemm::make_zset(q);
   ACME_PROF_PEAK(name, st, 2.0 * (double)(rows0 + rows1) * N * K, 0.0, 157.3);
-  hipError_t e = launch_gemm<32, 32, 1, 1, 16, 8>(p, 2, st);
+  hipError_t e = D4_LAUNCH(p, 2);
   if (e != hipSuccess) {
     set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(e), __FILE__, __LINE__);
     return ACME_ERR_HIP;
@@ -818,7 +847,7 @@ constexpr int kZ = 3;  // sub-problems of one type per backward launch
 
 template <class Q>
 bool fill_zset(gemm::ZSet<Q, kZ>& z, int& n, const std::vector<Q>& qs, int& tiles, int& count,
-               double& flops) {
+               double& flops, int& kmax) {
   if (qs.size() > (size_t)kZ) return false;
   n = (int)qs.size();
   if (!qs.empty()) static_cast<Q&>(z) = qs[0];
@@ -826,6 +855,7 @@ bool fill_zset(gemm::ZSet<Q, kZ>& z, int& n, const std::vector<Q>& qs, int& tile
     z.sub[i] = qs[i];
     tiles = std::max(tiles, (int)(ceil_div(qs[i].M, 32) * ceil_div(qs[i].N, 32)));
     flops += 2.0 * qs[i].M * (double)qs[i].N * qs[i].K;
+    kmax = std::max(kmax, qs[i].K);
   }
   count += n;
   return true;
@@ -833,9 +863,10 @@ bool fill_zset(gemm::ZSet<Q, kZ>& z, int& n, const std::vector<Q>& qs, int& tile
 
 template <class Q0, class... R>
 bool fill_multi(gemm::ZMulti<gemm::ZSet<Q0, kZ>, gemm::ZSet<R, kZ>...>& m, int& tiles,
-                int& count, double& flops, const std::vector<Q0>& q0, const std::vector<R>&... r) {
-  if (!fill_zset(m.s, m.n, q0, tiles, count, flops)) return false;
-  if constexpr (sizeof...(R) > 0) return fill_multi(m.rest, tiles, count, flops, r...);
+                int& count, double& flops, int& kmax, const std::vector<Q0>& q0,
+                const std::vector<R>&... r) {
+  if (!fill_zset(m.s, m.n, q0, tiles, count, flops, kmax)) return false;
+  if constexpr (sizeof...(R) > 0) return fill_multi(m.rest, tiles, count, flops, kmax, r...);
   return true;
 }
 
@@ -844,14 +875,23 @@ bool fill_multi(gemm::ZMulti<gemm::ZSet<Q0, kZ>, gemm::ZSet<R, kZ>...>& m, int& 
 template <class... Q>
 int launch_multi(const char* name, hipStream_t st, const std::vector<Q>&... qs) {
   gemm::ZMulti<gemm::ZSet<Q, kZ>...> m;
-  int tiles = 0, count = 0;
+  int tiles = 0, count = 0, kmax = 0;
   double flops = 0.0;
-  if (!fill_multi(m, tiles, count, flops, qs...))
+  if (!fill_multi(m, tiles, count, flops, kmax, qs...))
     return (set_error("too many GEMMs in one backward launch"), ACME_ERR_INVALID);
   if (count == 0) return ACME_OK;
   ACME_PROF_PEAK(name, st, flops, 0.0, 157.3);
+#if D4_DIRECT
+  const hipError_t e = gemm::launch_direct_multi(m, tiles, count, kmax, st);
+  if (e != hipSuccess) {
+    set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(e), __FILE__, __LINE__);
+    return ACME_ERR_HIP;
+  }
+#else
+  (void)kmax;
   hipLaunchKernelGGL((gemm::gemm_f32_multi_kernel<32, 32, 1, 1, 16, 8, gemm::ZSet<Q, kZ>...>),
                      dim3((unsigned)tiles, 1, (unsigned)count), dim3(64 * 8), 0, st, m);
+#endif
   D4_CHECK();
   return ACME_OK;
 }
