@@ -455,6 +455,14 @@ struct DenseFwd {
     if (slab) slab[((size_t)split * M + m) * N + n] = v;
     else y[(size_t)m * N + n] = v;
   }
+  // Direct engine (gemm_direct.h): x [M][ldx] rows, W [K][N] columns.  Requires
+  // split_b >= M (one input: the descriptor has one base).
+  static constexpr bool kStrided = sizeof(typename In::T) == 4;
+  static constexpr bool kAVec = VEC, kBVec = false;
+  __device__ gemm::StridedOp a_op() const {
+    return {reinterpret_cast<const float*>(x), (uint32_t)(4u * M * ldx), 4u * ldx, 4u};
+  }
+  __device__ gemm::StridedOp b_op() const { return {w, (uint32_t)(4u * K * N), 4u, 4u * N}; }
 };
 
 // Weight gradient of a dense layer, single split: dW = X^T dZ written straight into the
@@ -500,7 +508,16 @@ struct DenseWgrad {
                  m + 3 < K ? p[3 * N] : 0.f};
   }
   __device__ void store(int i, int n, float v, int) const { out[(size_t)i * N + n] = v; }
-  __device__ void store_colsum(int n, float v, int) const { bias_out[n] = v; }
+  __device__ void store_colsum(int n, float v, int) const {
+    if (bias_out) bias_out[n] = v;  // null: a bias gradient another problem writes
+  }
+  // Direct engine (gemm_direct.h): x [K][ldx] and dz [K][N] read down their columns.
+  static constexpr bool kStrided = sizeof(typename In::T) == 4;
+  static constexpr bool kAVec = false, kBVec = false;
+  __device__ gemm::StridedOp a_op() const {
+    return {reinterpret_cast<const float*>(x), (uint32_t)(4u * K * ldx), 4u, 4u * ldx};
+  }
+  __device__ gemm::StridedOp b_op() const { return {dz, (uint32_t)(4u * K * N), 4u, 4u * N}; }
 };
 
 template <bool VEC>
@@ -542,6 +559,11 @@ struct DenseDgrad {
   }
   __device__ float finish(float v, float xp) const { return xprev ? act_bwd(act, xp, v) : v; }
   __device__ void put(int m, int n, float v, int) const { dx[(size_t)m * ldx + n] = v; }
+  // Direct engine (gemm_direct.h): dz [M][K] and W [N][K] rows.
+  static constexpr bool kStrided = true;
+  static constexpr bool kAVec = VEC, kBVec = VEC;
+  __device__ gemm::StridedOp a_op() const { return {dz, (uint32_t)(4u * M * K), 4u * K, 4u}; }
+  __device__ gemm::StridedOp b_op() const { return {w, (uint32_t)(4u * N * K), 4u * K, 4u}; }
 };
 
 // ------------------------------------------------------------------ duelling head

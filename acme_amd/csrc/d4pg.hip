@@ -231,6 +231,7 @@ struct LnFirstPair {
   LnFirstArgs a[2];
 };
 
+template <int C>  // feature columns per thread: H <= 256 C
 __global__ void __launch_bounds__(256) ln_first_kernel(const LnFirstPair pair) {
   __shared__ float xs[kRows][kMaxIn];
   __shared__ float red[4][kRows];
@@ -251,7 +252,6 @@ __global__ void __launch_bounds__(256) ln_first_kernel(const LnFirstPair pair) {
     xs[r][k] = v;
   }
   __syncthreads();
-  constexpr int C = kMaxWidth / 256;
   float acc[kRows][C];
 #pragma unroll
   for (int c = 0; c < C; ++c) {
@@ -259,10 +259,20 @@ __global__ void __launch_bounds__(256) ln_first_kernel(const LnFirstPair pair) {
 #pragma unroll
     for (int r = 0; r < kRows; ++r) acc[r][c] = 0.f;
     if (j < a.H) {
-      for (int k = 0; k < din; ++k) {
-        const float wk = a.w[(size_t)k * a.H + j];
+      // 16 weight loads in flight per chunk (one round trip per 16 inputs, not per input);
+      // the products still run in k order.
+      constexpr int KU = 16;
+      for (int k0 = 0; k0 < din; k0 += KU) {
+        float wk[KU];
 #pragma unroll
-        for (int r = 0; r < kRows; ++r) acc[r][c] = fmaf(xs[r][k], wk, acc[r][c]);
+        for (int u = 0; u < KU; ++u)
+          wk[u] = k0 + u < din ? a.w[(size_t)(k0 + u) * a.H + j] : 0.f;
+#pragma unroll
+        for (int u = 0; u < KU; ++u) {
+          if (k0 + u >= din) break;
+#pragma unroll
+          for (int r = 0; r < kRows; ++r) acc[r][c] = fmaf(xs[r][k0 + u], wk[u], acc[r][c]);
+        }
       }
       const float bj = a.b[j];
 #pragma unroll
@@ -440,11 +450,13 @@ struct LnBwdArgs {
   float *du, *dqda, *ploss_part;
 };
 
+// C: feature columns per thread (H <= 256 C); AM: action slots (A <= AM).  Both sized per
+// launch: the widest instantiation (C = 4, AM = 16) spills at H = 512, A = 6.
+template <int C, int AM>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(const LnBwdArgs a) {
-  constexpr int C = kMaxWidth / 256;
   __shared__ float red[4][2 * kRows];
-  __shared__ float redq[4][kRows * ACME_D4PG_MAX_ACT];
-  __shared__ float dq_s[kRows][ACME_D4PG_MAX_ACT];
+  __shared__ float redq[4][kRows * AM];
+  __shared__ float dq_s[kRows][AM];
   const int tid = threadIdx.x;
   const int r0 = blockIdx.x * kRows;
   const float invH = 1.f / (float)a.H;
@@ -455,12 +467,12 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const LnBwdArgs a) {
   // entries contribute exact zeros to the sums.
   const int last = a.rows - 1;
   const bool has_dpg = r0 + kRows - 1 >= a.ce_rows && r0 < a.rows;  // uniform per block
-  float w1v[C][ACME_D4PG_MAX_ACT];
+  float w1v[C][AM];
   if (has_dpg) {
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
-      for (int k = 0; k < ACME_D4PG_MAX_ACT; ++k)
+      for (int k = 0; k < AM; ++k)
         w1v[c][k] = a.w1[(size_t)(a.act_off + min(k, a.A - 1)) * a.H + min(tid + 256 * c, a.H - 1)];
   }
   float sc[C];
@@ -490,11 +502,11 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const LnBwdArgs a) {
   float cs_x[C], cs_1[C];
 #pragma unroll
   for (int c = 0; c < C; ++c) cs_x[c] = cs_1[c] = 0.f;
-  float dqp[kRows][ACME_D4PG_MAX_ACT];
+  float dqp[kRows][AM];
 #pragma unroll
   for (int r = 0; r < kRows; ++r)
 #pragma unroll
-    for (int k = 0; k < ACME_D4PG_MAX_ACT; ++k) dqp[r][k] = 0.f;
+    for (int k = 0; k < AM; ++k) dqp[r][k] = 0.f;
   bool any_dpg = false;
 #pragma unroll
   for (int r = 0; r < kRows; ++r) {
@@ -515,7 +527,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const LnBwdArgs a) {
         cs_1[c] += dyv[r][c];
       } else {
 #pragma unroll
-        for (int k = 0; k < ACME_D4PG_MAX_ACT; ++k)
+        for (int k = 0; k < AM; ++k)
           dqp[r][k] = k < a.A ? fmaf(dz, w1v[c][k], dqp[r][k]) : dqp[r][k];
       }
     }
@@ -536,14 +548,14 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const LnBwdArgs a) {
 #pragma unroll
   for (int r = 0; r < kRows; ++r)
 #pragma unroll
-    for (int k = 0; k < ACME_D4PG_MAX_ACT; ++k) {
+    for (int k = 0; k < AM; ++k) {
       if (k >= a.A) break;
       const float v = wave_sum(dqp[r][k]);
-      if (lane == 0) redq[wave][r * ACME_D4PG_MAX_ACT + k] = v;
+      if (lane == 0) redq[wave][r * AM + k] = v;
     }
   __syncthreads();
-  if (tid < kRows * ACME_D4PG_MAX_ACT) {
-    const int r = tid / ACME_D4PG_MAX_ACT, k = tid % ACME_D4PG_MAX_ACT;
+  if (tid < kRows * AM) {
+    const int r = tid / AM, k = tid % AM;
     dq_s[r][k] = ((redq[0][tid] + redq[1][tid]) + redq[2][tid]) + redq[3][tid];
   }
   __syncthreads();
@@ -575,15 +587,10 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const LnBwdArgs a) {
 }
 
 // ------------------------------------------------------------------ weight gradient of the
-// first layer: dW = concat(x0, x1)^T dZ over the batch, bias = column sums of dZ.
+// first layer: dW = concat(x0, x1)^T dZ over the batch, bias = column sums of dZ (staged
+// engine; the direct engine runs it as two DenseWgrad problems).
 struct ConcatWgrad {
-#if D4_DIRECT
-  // Direct engine: k-contiguous runs over the batch (4 scalar loads per vector, coalesced
-  // across the lanes' features / columns).
-  static constexpr int A_MODE = gemm::KCONTIG, B_MODE = gemm::KCONTIG;
-#else
   static constexpr int A_MODE = gemm::RCONTIG, B_MODE = gemm::RCONTIG;
-#endif
   static constexpr bool kColSum = true;
   int M, N, K, k_chunk;  // M = d0 + d1 (inputs), N = H, K = batch rows
   const float* x0;
@@ -608,26 +615,14 @@ struct ConcatWgrad {
   __device__ f32x4 a_load(const ARow& a, int m) const {
     f32x4 r = gemm::zero4();
     if (m >= K) return r;
-#if D4_DIRECT
-    if (a.i >= M) return r;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) r[j] = m + j < K ? x_at(m + j, a.i) : 0.f;
-#else
 #pragma unroll
     for (int j = 0; j < 4; ++j) r[j] = x_at(m, a.i + j);
-#endif
     return r;
   }
   __device__ BRow b_row(int n) const { return BRow{n}; }
   __device__ f32x4 b_load(const BRow& b, int m) const {
     if (b.n >= N || m >= K) return gemm::zero4();
-#if D4_DIRECT
-    const float* p = dz + (size_t)m * N + b.n;
-    return f32x4{p[0], m + 1 < K ? p[N] : 0.f, m + 2 < K ? p[2 * N] : 0.f,
-                 m + 3 < K ? p[3 * N] : 0.f};
-#else
     return load_row4<true>(dz + (size_t)m * N, b.n, N);
-#endif
   }
   __device__ void store(int i, int n, float v, int) const { out[(size_t)i * N + n] = v; }
   __device__ void store_colsum(int n, float v, int) const { bias_out[n] = v; }
@@ -687,7 +682,13 @@ int dense_fwd_pair(const char* name, const float* x0, int rows0, const float* w0
                    const float* b0, float* y0, const float* x1, int rows1, const float* w1,
                    const float* b1, float* y1, int K, int N, int act, hipStream_t st) {
   if (rows1 == 0) return dense_fwd(name, x0, rows0, K, w0, b0, N, act, y0, st);
+#if D4_DIRECT
+  // The direct engine reads W by columns whatever N is; only the x rows' vector loads need
+  // K % 4 == 0.
+  if (K % 4 != 0) {
+#else
   if (K % 4 != 0 || N % 4 != 0) {
+#endif
     int rc = dense_fwd(name, x0, rows0, K, w0, b0, N, act, y0, st);
     return rc != ACME_OK ? rc : dense_fwd(name, x1, rows1, K, w1, b1, N, act, y1, st);
   }
@@ -739,8 +740,9 @@ int lnmlp_forward_pair(acme_d4pg* l, const NetDesc& d, const NetIn (&in)[2], int
       g.z = a.z1; g.mean = a.mean; g.rstd = a.rstd; g.h = a.h[0];
     }
     const int rows = std::max(in[0].rows, in[1].rows);
-    ln_first_kernel<<<dim3((unsigned)ceil_div(rows, kRows), in[1].rows > 0 ? 2 : 1), 256, 0,
-                      st>>>(f);
+    const int H = d.sizes[0];
+    auto k = H <= 256 ? ln_first_kernel<1> : H <= 512 ? ln_first_kernel<2> : ln_first_kernel<4>;
+    k<<<dim3((unsigned)ceil_div(rows, kRows), in[1].rows > 0 ? 2 : 1), 256, 0, st>>>(f);
     D4_CHECK();
   }
   for (int i = 1; i < d.nl; ++i) {
@@ -900,12 +902,22 @@ int launch_multi(const char* name, hipStream_t st, const std::vector<Q>&... qs) 
 // layers' the rest.
 int launch_bwd(const char* name, BwdGroup& g, hipStream_t st) {
   int rc;
+#if D4_DIRECT
+  // (No ConcatWgrad problems: ln_backward splits them into DenseWgrad ones.)
+  if (g.dgn.empty() && g.wgn.empty())
+    rc = launch_multi(name, st, g.dg, g.wg);
+  else if (g.dg.empty() && g.wg.empty())
+    rc = launch_multi(name, st, g.dgn, g.wgn);
+  else
+    rc = launch_multi(name, st, g.dg, g.wg, g.dgn, g.wgn);
+#else
   if (g.dgn.empty() && g.wgn.empty() && g.first.empty())
     rc = launch_multi(name, st, g.dg, g.wg);
   else if (g.dg.empty() && g.wg.empty())
     rc = launch_multi(name, st, g.dgn, g.wgn, g.first);
   else
     rc = launch_multi(name, st, g.dg, g.wg, g.dgn, g.wgn, g.first);
+#endif
   g = BwdGroup{};
   return rc;
 }
@@ -1001,15 +1013,28 @@ int ln_backward(acme_d4pg* l, const NetDesc& d, const Acts& a, float* dy, int ro
     b.clip = l->cfg.clipping ? 1.f : 0.f; b.invB = 1.f / (float)ce_rows;
     b.t = l->pon.t; b.act_scale = l->act_scale;
     b.du = l->du; b.dqda = l->dqda; b.ploss_part = dpg ? l->ploss_part : nullptr;
-    ln_bwd_kernel<<<(unsigned)nblk, 256, 0, st>>>(b);
+    const int c = H <= 256 ? 1 : H <= 512 ? 2 : 4;
+    const int am = !dpg || b.A <= 4 ? 4 : b.A <= 8 ? 8 : 16;
+    auto k = c == 1 ? (am == 4 ? ln_bwd_kernel<1, 4> : am == 8 ? ln_bwd_kernel<1, 8> : ln_bwd_kernel<1, 16>)
+           : c == 2 ? (am == 4 ? ln_bwd_kernel<2, 4> : am == 8 ? ln_bwd_kernel<2, 8> : ln_bwd_kernel<2, 16>)
+                    : (am == 4 ? ln_bwd_kernel<4, 4> : am == 8 ? ln_bwd_kernel<4, 8> : ln_bwd_kernel<4, 16>);
+    k<<<(unsigned)nblk, 256, 0, st>>>(b);
     D4_CHECK();
   }
   ln.push_back({slab, nblk, H, Pm(l, l->grads, d.scale), Pm(l, l->grads, d.offset)});
+#if D4_DIRECT
+  // dW1 = concat(xa, xb)^T dz: the xa rows and the xb rows of dW1 as two weight gradients
+  // (strided operands); the bias gradient (column sums of dz) from the first.
+  float* dw = Pm(l, l->grads, d.w1);
+  add_wgrad(g, xa, ce_rows, da, dy, H, dw, Pm(l, l->grads, d.b1));
+  if (db > 0) add_wgrad(g, xb, ce_rows, db, dy, H, dw + (size_t)da * H, nullptr);
+#else
   ConcatWgrad p;
   p.M = da + db; p.N = H; p.K = ce_rows; p.k_chunk = ce_rows;
   p.x0 = xa; p.d0 = da; p.x1 = xb; p.d1 = db; p.dz = dy;
   p.out = Pm(l, l->grads, d.w1); p.bias_out = Pm(l, l->grads, d.b1);
   g.first.push_back(p);
+#endif
   return ACME_OK;
 }
 

@@ -208,6 +208,13 @@ ZSet<Q, NZ> make_zset(const Q (&qs)[NZ]) {
   return s;
 }
 
+// One operand as a single buffer for the direct engine's strided loads (gemm_direct.h):
+// element (row, k) at byte offset row * row_bytes + k * k_bytes, `bytes` long.
+struct StridedOp {
+  const float* base;
+  uint32_t bytes, row_bytes, k_bytes;
+};
+
 // Problem concept (see conv.h):
 //   static constexpr int A_MODE, B_MODE;
 //   int M, N, K;            rows of A (= C rows), rows of B (= C cols), reduction length

@@ -25,6 +25,52 @@ namespace gemm {
 
 constexpr int kDirectWaves = 8;
 
+// Optional strided-operand hook: a problem with `static constexpr bool kStrided = true`
+// describes each operand as one buffer, element (row, k) at byte offset
+// row * row_bytes + k * k_bytes (VEC: k_bytes = 4, rows 16-byte aligned, loaded 4 k at a
+// time), and the direct block reads whole chunks with buffer loads — one VGPR offset per
+// lane, the k step in the scalar offset, no branch per load.  Offsets past `bytes` read zero
+// (rows >= M of a row-major operand); rows past N of a column operand may read neighbouring
+// elements, which reach only output columns that are never stored.  Elements past K read
+// zero (their offsets are pushed past the buffer).
+// (StridedOp: gemm.h.)
+template <class P, class = void>
+struct HasStrided {
+  static constexpr bool value = false;
+};
+template <class P>
+struct HasStrided<P, decltype(void(P::kStrided))> {
+  static constexpr bool value = P::kStrided;
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t strided_rsrc(const StridedOp& o) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(o.base), (short)0, o.bytes,
+                                           0x00020000);
+}
+
+// KL / 4 vectors of elements k0 .. k0 + KL - 1 of `row`; elements at k >= K read zero (their
+// offset is pushed past the buffer; VEC operands have K % 4 == 0).
+template <int KL, bool VEC>
+__device__ __forceinline__ void strided_run(const StridedOp& o, __amdgpu_buffer_rsrc_t rs, int row,
+                                            int k0, int K, f32x4 (&out)[KL / 4]) {
+  constexpr uint32_t kOut = 0x80000000u;
+  const uint32_t off = (uint32_t)row * o.row_bytes + (uint32_t)k0 * o.k_bytes;
+  if constexpr (VEC) {
+#pragma unroll
+    for (int i = 0; i < KL / 4; ++i)
+      out[i] = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, k0 + 4 * i < K ? off + 16 * i : kOut, 0, 0));
+  } else {
+#pragma unroll
+    for (int i = 0; i < KL / 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        out[i][j] = __builtin_bit_cast(
+            float, __builtin_amdgcn_raw_buffer_load_b32(rs, k0 + 4 * i + j < K ? off : kOut,
+                                                        (4 * i + j) * o.k_bytes, 0));
+  }
+}
+
 // LDS floats of a direct block: NW partial 32 x 32 tiles plus NW x 64 column-sum lanes.
 template <int NW>
 constexpr int direct_smem_floats() {
@@ -63,15 +109,29 @@ __device__ __forceinline__ void direct_block(const P& p, const int tile, float* 
   constexpr bool kColSum = HasColSum<P>::value;
   const bool do_colsum = kColSum && m0 == 0;
   float cs = 0.f;
+  StridedOp oa{}, ob{};
+  if constexpr (HasStrided<P>::value) {
+    oa = p.a_op();
+    ob = p.b_op();
+  }
+  const __amdgpu_buffer_rsrc_t ra = strided_rsrc(oa), rb = strided_rsrc(ob);
   for (int kb = w * 2 * KL; kb < p.K; kb += NW * 2 * KL) {
     const int k0 = kb + h * KL;
     f32x4 a[KL / 4], b[KL / 4];
+    if constexpr (HasStrided<P>::value) {
+      strided_run<KL, P::kAVec>(oa, ra, m0 + r, k0, p.K, a);
+      strided_run<KL, P::kBVec>(ob, rb, n0 + r, k0, p.K, b);
+    } else {
 #pragma unroll
-    for (int i = 0; i < KL / 4; ++i) {
-      const bool in = k0 + 4 * i < p.K;
-      a[i] = in ? p.a_load(ar, k0 + 4 * i) : zero4();
-      b[i] = in ? p.b_load(br, k0 + 4 * i) : zero4();
+      for (int i = 0; i < KL / 4; ++i) {
+        const bool in = k0 + 4 * i < p.K;
+        a[i] = in ? p.a_load(ar, k0 + 4 * i) : zero4();
+        b[i] = in ? p.b_load(br, k0 + 4 * i) : zero4();
+      }
     }
+    // Every load of the chunk is issued before the first product: left alone, the scheduler
+    // interleaves them with the MFMAs to save registers and keeps only ~8 in flight.
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < KL / 4; ++i)
 #pragma unroll
