@@ -40,6 +40,10 @@
 #ifndef D4_DIRECT
 #define D4_DIRECT 1
 #endif
+// 1: the learner step's policy heads run inside the critic's first-layer launch.
+#ifndef D4_FUSED_HEAD
+#define D4_FUSED_HEAD 1
+#endif
 
 using namespace acme;
 using namespace acme::conv;
@@ -217,19 +221,73 @@ __device__ __forceinline__ void block_sum256(float (&v)[N], float (*red)[N]) {
 // ------------------------------------------------------------------ LayerNorm first layer
 // h = tanh(LayerNorm(concat(xa, xb) @ W + b)) for kRows rows per 256-thread block.
 // Rows < split read (xa0, xb0), the others (xa1, xb1) at row - split.
+// The policy head in front of the critic: part p's xb (the actions) computed in the block from
+// the policy's last hidden layer when head[p].h is set (and written to head[p].t / .a as
+// policy_head_kernel would), instead of read from xb.
+struct PolHeadSrc {
+  const float* h;  // [rows of the part][Hp], null: xb is given
+  float *t, *a;    // tanh outputs, actions
+};
 struct LnFirstArgs {
   const float *xa0, *xb0, *xa1, *xb1;
   int split, rows, da, db, H;
   const float *w, *b, *scale, *offset;
   float eps;
   float *z, *mean, *rstd, *h;
+  PolHeadSrc head[2];
+  const float *hw, *hb;  // the policy head of this evaluation's network
 };
 
 // Two evaluations in one launch (the online and target networks): blockIdx.y picks the
 // argument set; blocks past that set's rows leave at once.
 struct LnFirstPair {
   LnFirstArgs a[2];
+  const float *lo, *scale;  // TanhToSpec range of the fused policy heads
+  int Hp;                   // policy hidden width
 };
+
+// One row of the policy head, lane j < A: u_j = h_row . W[:, j] (lane-strided partial sums,
+// then the butterfly sum) and the TanhToSpec action; policy_head_kernel and the fused head
+// of ln_first_kernel share it, so both give the same bits.
+__device__ __forceinline__ void policy_head_row(const float* __restrict__ h, const float* __restrict__ w,
+                                                const float* __restrict__ b, const float* __restrict__ lo,
+                                                const float* __restrict__ scale, int H, int A,
+                                                int lane, float& t, float& act) {
+  float acc[ACME_D4PG_MAX_ACT];
+#pragma unroll
+  for (int j = 0; j < ACME_D4PG_MAX_ACT; ++j) acc[j] = 0.f;
+  // Four k steps per chunk with their loads issued together (the sums still run k by k).
+  for (int k0 = lane; k0 < H; k0 += 4 * 64) {
+    float hv[4], wv[4][ACME_D4PG_MAX_ACT];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = min(k0 + 64 * u, H - 1);
+      hv[u] = h[k];
+#pragma unroll
+      for (int j = 0; j < ACME_D4PG_MAX_ACT; ++j) wv[u][j] = j < A ? w[(size_t)k * A + j] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (k0 + 64 * u >= H) break;
+#pragma unroll
+      for (int j = 0; j < ACME_D4PG_MAX_ACT; ++j)
+        if (j < A) acc[j] = fmaf(hv[u], wv[u][j], acc[j]);
+    }
+  }
+  float mine = 0.f;
+#pragma unroll
+  for (int j = 0; j < ACME_D4PG_MAX_ACT; ++j) {
+    if (j >= A) break;
+    const float s = wave_sum(acc[j]);
+    if (lane == j) mine = s;
+  }
+  t = 0.f;
+  act = 0.f;
+  if (lane < A) {
+    t = tanhf(mine + b[lane]);
+    act = (0.5f * (t + 1.f)) * scale[lane] + lo[lane];
+  }
+}
 
 template <int C>  // feature columns per thread: H <= 256 C
 __global__ void __launch_bounds__(256) ln_first_kernel(const LnFirstPair pair) {
@@ -240,16 +298,49 @@ __global__ void __launch_bounds__(256) ln_first_kernel(const LnFirstPair pair) {
   const int r0 = blockIdx.x * kRows;
   if (r0 >= a.rows) return;  // uniform per block
   const int din = a.da + a.db;
+  // Loads that depend on nothing go out first: the bias / LayerNorm parameters of this
+  // thread's columns and the first KU input rows of their weights (clamped indices; the
+  // products below still run in k order).
+  constexpr int KU = 32;
+  float bj[C], scj[C], ofj[C], wk[C][KU];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const int j = min(tid + 256 * c, a.H - 1);
+    bj[c] = a.b[j];
+    scj[c] = a.scale[j];
+    ofj[c] = a.offset[j];
+#pragma unroll
+    for (int u = 0; u < KU; ++u) wk[c][u] = a.w[(size_t)min(u, din - 1) * a.H + j];
+  }
   for (int i = tid; i < kRows * din; i += 256) {
     const int r = i / din, k = i - r * din, row = r0 + r;
     float v = 0.f;
     if (row < a.rows) {
       const bool second = row >= a.split;
       const int rr = second ? row - a.split : row;
+      if (k >= a.da && a.head[second].h) continue;  // the fused head writes it
       v = k < a.da ? (second ? a.xa1 : a.xa0)[(size_t)rr * a.da + k]
                    : (second ? a.xb1 : a.xb0)[(size_t)rr * a.db + (k - a.da)];
     }
     xs[r][k] = v;
+  }
+  {
+    // Fused policy head: wave r computes row r0 + r's actions.
+    static_assert(kRows == 4, "one wave per row of the block");
+    const int r = tid >> 6, lane = tid & 63, row = r0 + r;
+    const bool second = row >= a.split;
+    const PolHeadSrc hs = a.head[second];
+    if (row < a.rows && hs.h) {  // uniform per wave
+      const int rr = second ? row - a.split : row;
+      float t, act;
+      policy_head_row(hs.h + (size_t)rr * pair.Hp, a.hw, a.hb, pair.lo, pair.scale, pair.Hp,
+                      a.db, lane, t, act);
+      if (lane < a.db) {
+        if (hs.t) hs.t[(size_t)rr * a.db + lane] = t;
+        hs.a[(size_t)rr * a.db + lane] = act;
+        xs[r][a.da + lane] = act;
+      }
+    }
   }
   __syncthreads();
   float acc[kRows][C];
@@ -259,24 +350,21 @@ __global__ void __launch_bounds__(256) ln_first_kernel(const LnFirstPair pair) {
 #pragma unroll
     for (int r = 0; r < kRows; ++r) acc[r][c] = 0.f;
     if (j < a.H) {
-      // 16 weight loads in flight per chunk (one round trip per 16 inputs, not per input);
-      // the products still run in k order.
-      constexpr int KU = 16;
       for (int k0 = 0; k0 < din; k0 += KU) {
-        float wk[KU];
+        if (k0 > 0) {
 #pragma unroll
-        for (int u = 0; u < KU; ++u)
-          wk[u] = k0 + u < din ? a.w[(size_t)(k0 + u) * a.H + j] : 0.f;
+          for (int u = 0; u < KU; ++u)
+            wk[c][u] = k0 + u < din ? a.w[(size_t)(k0 + u) * a.H + j] : 0.f;
+        }
 #pragma unroll
         for (int u = 0; u < KU; ++u) {
           if (k0 + u >= din) break;
 #pragma unroll
-          for (int r = 0; r < kRows; ++r) acc[r][c] = fmaf(xs[r][k0 + u], wk[u], acc[r][c]);
+          for (int r = 0; r < kRows; ++r) acc[r][c] = fmaf(xs[r][k0 + u], wk[c][u], acc[r][c]);
         }
       }
-      const float bj = a.b[j];
 #pragma unroll
-      for (int r = 0; r < kRows; ++r) acc[r][c] += bj;
+      for (int r = 0; r < kRows; ++r) acc[r][c] += bj[c];
     }
   }
   // tf.nn.moments over the feature axis: mean, then mean of squared deviations.
@@ -314,7 +402,7 @@ __global__ void __launch_bounds__(256) ln_first_kernel(const LnFirstPair pair) {
       if (j >= a.H) continue;
       const size_t idx = (size_t)row * a.H + j;
       a.z[idx] = acc[r][c];
-      const float y = (acc[r][c] - mean[r]) * rs * a.scale[j] + a.offset[j];
+      const float y = (acc[r][c] - mean[r]) * rs * scj[c] + ofj[c];
       a.h[idx] = tanhf(y);
     }
     if (tid == 0) {
@@ -351,26 +439,11 @@ __global__ void __launch_bounds__(256) policy_head_kernel(const PolicyHeadPair p
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
-  float acc[ACME_D4PG_MAX_ACT];
-#pragma unroll
-  for (int j = 0; j < ACME_D4PG_MAX_ACT; ++j) acc[j] = 0.f;
-  for (int k = lane; k < H; k += 64) {
-    const float hv = h[(size_t)row * H + k];
-#pragma unroll
-    for (int j = 0; j < ACME_D4PG_MAX_ACT; ++j)
-      if (j < A) acc[j] = fmaf(hv, w[(size_t)k * A + j], acc[j]);
-  }
-  float mine = 0.f;
-#pragma unroll
-  for (int j = 0; j < ACME_D4PG_MAX_ACT; ++j) {
-    if (j >= A) break;
-    const float s = wave_sum(acc[j]);
-    if (lane == j) mine = s;
-  }
+  float t, act;
+  policy_head_row(h + (size_t)row * H, w, b, lo, scale, H, A, lane, t, act);
   if (lane < A) {
-    const float t = tanhf(mine + b[lane]);
     if (t_out) t_out[(size_t)row * A + lane] = t;
-    a_out[(size_t)row * A + lane] = (0.5f * (t + 1.f)) * scale[lane] + lo[lane];
+    a_out[(size_t)row * A + lane] = act;
   }
 }
 
@@ -720,6 +793,8 @@ struct NetIn {
   const float *xa0, *xb0, *xa1, *xb1;
   int split, rows;
   Acts* acts;
+  PolHeadSrc head[2] = {};  // critic inputs: policy heads fused into the first layer
+  const float* head_prm = nullptr;  // parameters holding that policy head
 };
 
 // Two evaluations of one LayerNormMLP (the online and the target network) in one launch
@@ -738,7 +813,12 @@ int lnmlp_forward_pair(acme_d4pg* l, const NetDesc& d, const NetIn (&in)[2], int
       g.eps = l->cfg.layer_norm_epsilon;
       Acts& a = *in[i].acts;
       g.z = a.z1; g.mean = a.mean; g.rstd = a.rstd; g.h = a.h[0];
+      g.head[0] = in[i].head[0];
+      g.head[1] = in[i].head[1];
+      g.hw = in[i].head_prm ? P(l, in[i].head_prm, l->pol.ow) : nullptr;
+      g.hb = in[i].head_prm ? P(l, in[i].head_prm, l->pol.ob) : nullptr;
     }
+    f.lo = l->act_lo; f.scale = l->act_scale; f.Hp = l->pol.sizes[l->pol.nl - 1];
     const int rows = std::max(in[0].rows, in[1].rows);
     const int H = d.sizes[0];
     auto k = H <= 256 ? ln_first_kernel<1> : H <= 512 ? ln_first_kernel<2> : ln_first_kernel<4>;
@@ -961,6 +1041,40 @@ __global__ void __launch_bounds__(256) ln_param_reduce_kernel(const LnReducePair
   }
 }
 
+// The same reduction as a member of the last backward launch (gemm_direct.h kCustom): a
+// 512-thread block sums 16 float4 columns over 32 partial groups (group g: partials g, g+32,
+// ...), then the groups in order.  M x N = 32 x (32 blocks) sizes the launch's grid.
+struct LnReduceBlock {
+  static constexpr bool kCustom = true;
+  int M, N, K, k_chunk;
+  LnReduce r;
+  __device__ void run_block(int blk, float* smem) const {
+    using f32x4 = gemm::f32x4;
+    static_assert(gemm::kDirectWaves == 8, "512-thread blocks");
+    f32x4* red = reinterpret_cast<f32x4*>(smem);  // [32][16]
+    const int c = threadIdx.x & 15, g = threadIdx.x >> 4;
+    const int count4 = r.H / 2;
+    const int e = blk * 16 + c;
+    if (blk * 16 >= count4) return;  // block-uniform
+    const f32x4* s4 = reinterpret_cast<const f32x4*>(r.slab);
+    f32x4 acc{0.f, 0.f, 0.f, 0.f};
+    if (e < count4) {
+#pragma unroll 4
+      for (int sp = g; sp < r.nblk; sp += 32) acc += s4[(size_t)sp * count4 + e];
+    }
+    red[g * 16 + c] = acc;
+    __syncthreads();
+    if (g == 0 && e < count4) {
+      f32x4 v = red[c];
+#pragma unroll
+      for (int k = 1; k < 32; ++k) v += red[k * 16 + c];
+      const int h4 = r.H / 4;
+      if (e < h4) reinterpret_cast<f32x4*>(r.scale)[e] = v;
+      else reinterpret_cast<f32x4*>(r.offset)[e - h4] = v;
+    }
+  }
+};
+
 int run_ln_reduces(const std::vector<LnReduce>& ln, hipStream_t st) {
   if (ln.empty()) return ACME_OK;
   if (ln.size() > 2) return (set_error("too many LayerNorm reductions"), ACME_ERR_INVALID);
@@ -976,6 +1090,34 @@ int run_ln_reduces(const std::vector<LnReduce>& ln, hipStream_t st) {
   ln_param_reduce_kernel<<<dim3((unsigned)ceil_div(cols, 16), (unsigned)ln.size()), 256, 0, st>>>(q);
   D4_CHECK();
   return ACME_OK;
+}
+
+// The step's last backward launch and the LayerNorm parameter reductions: one launch
+// (direct engine; the reductions read only ln_bwd's partials), else two.
+int launch_bwd_last(const char* name, BwdGroup& g, const std::vector<LnReduce>& ln,
+                    hipStream_t st) {
+#if D4_DIRECT
+  std::vector<LnReduceBlock> lr;
+  for (const LnReduce& x : ln) {
+    LnReduceBlock b;
+    b.M = 32;
+    b.N = 32 * (int)ceil_div(x.H / 2, 16);
+    b.K = 0;
+    b.k_chunk = 0;
+    b.r = x;
+    lr.push_back(b);
+  }
+  int rc;
+  if (g.dgn.empty() && g.wgn.empty())
+    rc = launch_multi(name, st, g.dg, g.wg, lr);
+  else
+    rc = launch_multi(name, st, g.dg, g.wg, g.dgn, g.wgn, lr);
+  g = BwdGroup{};
+  return rc;
+#else
+  const int rc = launch_bwd(name, g, st);
+  return rc != ACME_OK ? rc : run_ln_reduces(ln, st);
+#endif
 }
 
 // Backward through the MLP part of a LayerNormMLP: `g` holds the launch that forms dz[nl-1]
@@ -1054,12 +1196,25 @@ int d4pg_step_impl(acme_d4pg* l, const acme_d4pg_batch* bt, const acme_d4pg_outp
   {
     const NetIn pin[2] = {{l->params, bt->o_t, nullptr, bt->o_t, nullptr, B, B, &l->pon},
                           {l->target, bt->o_t, nullptr, bt->o_t, nullptr, B, B, &l->ptg}};
+#if D4_FUSED_HEAD
+    // The policy heads run inside the critic's first-layer launch below.
+    if ((rc = lnmlp_forward_pair(l, pd, pin, od, 0, "d4pg_policy_ln", st))) return rc;
+#else
     float* const pout[2] = {l->pon.out, l->ptg.out};
     if ((rc = policy_forward_pair(l, pin, pout, st))) return rc;
+#endif
   }
   {
-    const NetIn cin[2] = {{l->params, bt->o_tm1, bt->a_tm1, bt->o_t, l->pon.out, B, 2 * B, &l->con},
-                          {l->target, bt->o_t, l->ptg.out, bt->o_t, l->ptg.out, B, B, &l->ctg}};
+    NetIn cin[2] = {{l->params, bt->o_tm1, bt->a_tm1, bt->o_t, l->pon.out, B, 2 * B, &l->con},
+                    {l->target, bt->o_t, l->ptg.out, bt->o_t, l->ptg.out, B, B, &l->ctg}};
+#if D4_FUSED_HEAD
+    // Online rows B.. take the online policy's actions (part 1), every target row the
+    // target policy's (part 0).
+    cin[0].head[1] = {l->pon.h[pd.nl - 1], l->pon.t, l->pon.out};
+    cin[0].head_prm = l->params;
+    cin[1].head[0] = {l->ptg.h[pd.nl - 1], l->ptg.t, l->ptg.out};
+    cin[1].head_prm = l->target;
+#endif
     if ((rc = critic_forward_pair(l, cin, st))) return rc;
   }
   {
@@ -1092,7 +1247,7 @@ int d4pg_step_impl(acme_d4pg* l, const acme_d4pg_batch* bt, const acme_d4pg_outp
   if ((rc = lnmlp_backward_mlp(l, pd, l->pon, l->pdz, B, B, g, "d4pg_bwd_phead", st)) ||
       (rc = ln_backward(l, pd, l->pon, l->pdz[0], B, B, false, bt->o_t, nullptr, od, 0,
                         l->lnslab2, g, ln, st)) ||
-      (rc = launch_bwd("d4pg_wgrad_first", g, st)) || (rc = run_ln_reduces(ln, st)))
+      (rc = launch_bwd_last("d4pg_wgrad_first", g, ln, st)))
     return rc;
   // Global-norm clipping + Adam (t = steps taken including this one).
   {

@@ -189,11 +189,24 @@ __global__ void __launch_bounds__(64 * NW) gemm_direct_kernel(const P p_in) {
   direct_block<KL, NW>(p, blockIdx.x, smem);
 }
 
+// Optional non-GEMM member of a multi launch: a problem with `static constexpr bool kCustom =
+// true` runs p.run_block(blockIdx.x, smem) (64 NW threads, direct_smem_floats<NW>() floats of
+// LDS) instead of a GEMM tile; its M x N in 32 x 32 tiles sizes the launch's grid.
+template <class P, class = void>
+struct HasCustomBlock {
+  static constexpr bool value = false;
+};
+template <class P>
+struct HasCustomBlock<P, decltype(void(P::kCustom))> {
+  static constexpr bool value = P::kCustom;
+};
+
 template <int KL, int NW, class S0, class... R>
 __device__ __forceinline__ void direct_multi_run(const ZMulti<S0, R...>& q, int z, float* smem) {
   if (z < q.n) {
     const S0 p = q.s.for_z(z);
-    direct_block<KL, NW>(p, blockIdx.x, smem);
+    if constexpr (HasCustomBlock<S0>::value) p.run_block(blockIdx.x, smem);
+    else direct_block<KL, NW>(p, blockIdx.x, smem);
   } else if constexpr (sizeof...(R) > 0) {
     direct_multi_run<KL, NW>(q.rest, z - q.n, smem);
   }
