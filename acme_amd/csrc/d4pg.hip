@@ -40,10 +40,6 @@
 #ifndef D4_DIRECT
 #define D4_DIRECT 1
 #endif
-// 1: the learner step's policy heads run inside the critic's first-layer launch.
-#ifndef D4_FUSED_HEAD
-#define D4_FUSED_HEAD 1
-#endif
 
 using namespace acme;
 using namespace acme::conv;
@@ -453,17 +449,15 @@ __global__ void __launch_bounds__(256) policy_head_kernel(const PolicyHeadPair p
 //               written exactly as l2_project (:44-83); dlogits = (softmax - target) / B,
 //               ce[row] = cross-entropy (summed into the loss by adam_clip_kernel).
 //   rows >= B : dpg rows; q = sum softmax * values, dq/dlogits = (values - q) * softmax.
-__global__ void __launch_bounds__(256) d4pg_loss_kernel(
-    const float* __restrict__ c_logits, const float* __restrict__ t_logits,
-    const float* __restrict__ r, const float* __restrict__ d, const float* __restrict__ values,
-    int B, int K, float discount, float* __restrict__ dlogits, float* __restrict__ ce_out) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= 2 * B) return;
+// The loss math of one row from its logits in registers (ql: the online critic's, tl: the
+// target critic's, lane = atom, -inf past K).
+__device__ __forceinline__ void loss_row(float ql, float tl, int row, int lane,
+                                         const float* __restrict__ r, const float* __restrict__ d,
+                                         const float* __restrict__ values, int B, int K,
+                                         float discount, float* __restrict__ dlogits,
+                                         float* __restrict__ ce_out) {
   const bool on = lane < K;
-  const float NEG = -INFINITY;
   const float vi = on ? values[lane] : 0.f;
-  const float ql = on ? c_logits[(size_t)row * K + lane] : NEG;
   const float m2 = wave_max(ql);
   const float e2 = on ? expf(ql - m2) : 0.f;
   const float s2 = wave_sum(e2);
@@ -478,7 +472,6 @@ __global__ void __launch_bounds__(256) d4pg_loss_kernel(
   // Zq[i] - Zq[i-1] (wrapping to vmax).
   const float dpos = on ? ((lane + 1 < K ? values[lane + 1] : vmin) - vi) : 1.f;
   const float dneg = on ? (vi - (lane > 0 ? values[lane - 1] : vmax)) : 1.f;
-  const float tl = on ? t_logits[(size_t)row * K + lane] : NEG;
   const float mx = wave_max(tl);
   const float e = on ? expf(tl - mx) : 0.f;
   const float pj = e / wave_sum(e);
@@ -499,6 +492,19 @@ __global__ void __launch_bounds__(256) d4pg_loss_kernel(
   const float ce = wave_sum(on ? -tgt * logp : 0.f);
   if (on) dlogits[(size_t)row * K + lane] = (1.f / (float)B) * (sm - tgt);
   if (lane == 0) ce_out[row] = ce;
+}
+
+__global__ void __launch_bounds__(256) d4pg_loss_kernel(
+    const float* __restrict__ c_logits, const float* __restrict__ t_logits,
+    const float* __restrict__ r, const float* __restrict__ d, const float* __restrict__ values,
+    int B, int K, float discount, float* __restrict__ dlogits, float* __restrict__ ce_out) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= 2 * B) return;
+  const bool on = lane < K;
+  const float ql = on ? c_logits[(size_t)row * K + lane] : -INFINITY;
+  const float tl = on && row < B ? t_logits[(size_t)row * K + lane] : -INFINITY;
+  loss_row(ql, tl, row, lane, r, d, values, B, K, discount, dlogits, ce_out);
 }
 
 // ------------------------------------------------------------------ LayerNorm backward
@@ -1196,25 +1202,19 @@ int d4pg_step_impl(acme_d4pg* l, const acme_d4pg_batch* bt, const acme_d4pg_outp
   {
     const NetIn pin[2] = {{l->params, bt->o_t, nullptr, bt->o_t, nullptr, B, B, &l->pon},
                           {l->target, bt->o_t, nullptr, bt->o_t, nullptr, B, B, &l->ptg}};
-#if D4_FUSED_HEAD
-    // The policy heads run inside the critic's first-layer launch below.
+    // The policy heads run inside the critic's first-layer launch below (a launch of their
+    // own measured 2 us slower per step, profiles/r05/ab/d4pg_fused_head.log).
     if ((rc = lnmlp_forward_pair(l, pd, pin, od, 0, "d4pg_policy_ln", st))) return rc;
-#else
-    float* const pout[2] = {l->pon.out, l->ptg.out};
-    if ((rc = policy_forward_pair(l, pin, pout, st))) return rc;
-#endif
   }
   {
     NetIn cin[2] = {{l->params, bt->o_tm1, bt->a_tm1, bt->o_t, l->pon.out, B, 2 * B, &l->con},
                     {l->target, bt->o_t, l->ptg.out, bt->o_t, l->ptg.out, B, B, &l->ctg}};
-#if D4_FUSED_HEAD
     // Online rows B.. take the online policy's actions (part 1), every target row the
     // target policy's (part 0).
     cin[0].head[1] = {l->pon.h[pd.nl - 1], l->pon.t, l->pon.out};
     cin[0].head_prm = l->params;
     cin[1].head[0] = {l->ptg.h[pd.nl - 1], l->ptg.t, l->ptg.out};
     cin[1].head_prm = l->target;
-#endif
     if ((rc = critic_forward_pair(l, cin, st))) return rc;
   }
   {

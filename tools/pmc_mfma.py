@@ -42,7 +42,7 @@ def main():
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     for path in paths:
         for r in csv.DictReader(open(path)):
-            sec = P.section(r["Kernel_Name"])
+            sec = P.section(r["Kernel_Name"], r.get("Grid_Size"))
             if sec:
                 per[(sec, r.get("Dispatch_Id") or r.get("Correlation_Id"))][r["Counter_Name"]] += \
                     float(r["Counter_Value"])

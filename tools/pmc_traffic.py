@@ -21,7 +21,15 @@ import re
 import sys
 
 # kernel symbol pattern -> profiler section name (first match wins), per workload
+# (Patterns see "<kernel name> grid=<Grid_Size>": the critic head and the policy's hidden
+# layers are one instantiation of the direct engine, told apart by their grids.)
 SECTIONS_D4PG = [
+    (r"gemm_direct_kernel<16, 8, .*DenseFwd<.* grid=32768$", "d4pg_critic_head"),
+    (r"gemm_direct_kernel<.*DenseFwd<true", "d4pg_mlp_fwd"),
+    (r"gemm_direct_multi_kernel<\d+, 8, acme::gemm::ZSet<acme::conv::DenseDgrad<true>, 3>, "
+     r"acme::gemm::ZSet<acme::conv::DenseWgrad<true, acme::conv::InF32>, 3> >", "d4pg_bwd_mlp"),
+    (r"gemm_direct_multi_kernel<", "d4pg_bwd_heads_first"),
+    # the staged engine (rounds 1-4, -DD4_DIRECT=0)
     (r"gemm_f32_kernel<32, 32, 1, 1, 16, 8, acme::gemm::ZSet<acme::conv::DenseFwd<true", "d4pg_mlp_fwd"),
     (r"gemm_f32_kernel<32, 32, 1, 1, 16, 8, acme::gemm::ZSet<acme::conv::DenseFwd<false", "d4pg_critic_head"),
     (r"gemm_f32_multi_kernel<.*ZSet<acme::conv::DenseDgrad<true", "d4pg_bwd_mlp"),
@@ -111,9 +119,10 @@ TABLES = {"dqn": SECTIONS, "d4pg": SECTIONS_D4PG, "impala": SECTIONS_IMPALA,
 TABLE = SECTIONS
 
 
-def section(name):
+def section(name, grid=None):
+    key = f"{name} grid={grid}" if grid is not None else name
     for pat, sec in TABLE:
-        if re.search(pat, name):
+        if re.search(pat, key):
             return sec
     return None
 
@@ -127,7 +136,7 @@ def per_launch(d, counter):
         for r in csv.DictReader(open(path)):
             if r["Counter_Name"] != counter:
                 continue
-            sec = section(r["Kernel_Name"])
+            sec = section(r["Kernel_Name"], r.get("Grid_Size"))
             if sec:
                 vals[sec].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in vals.items()}
