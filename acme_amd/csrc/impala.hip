@@ -25,6 +25,7 @@
 #include "conv.h"
 #include "conv_p3.h"
 #include "gemm.h"
+#include "gemm_direct.h"
 #include "gemm_p3.h"
 #include "gemm_x6.h"
 #include "kernels.h"
@@ -394,6 +395,24 @@ __global__ void __launch_bounds__(256) impala_loss_grad_kernel(const LossArgs a)
     }                                                                                          \
   } while (0)
 
+// The small f32 layers after the LSTM (a few hundred rows): the register-operand engine
+// (gemm_direct.h: each lane's k run in one burst, 8 waves per 32 x 32 tile); -DIM_DIRECT=0:
+// the staged f32 engine (the A/B).
+#ifndef IM_DIRECT
+#define IM_DIRECT 1
+#endif
+#define IM_DGEMM(name, prob)                                                                   \
+  do {                                                                                         \
+    ACME_PROF_PEAK(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0,  \
+                   157.3);                                                                     \
+    hipError_t _e = IM_DIRECT ? gemm::launch_direct(prob, 1, (prob).K, st)                     \
+                              : gemm::launch_matmul<32, 32, 1, 1, 16, 8>(prob, 1, st);          \
+    if (_e != hipSuccess) {                                                                    \
+      set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__);  \
+      return ACME_ERR_HIP;                                                                     \
+    }                                                                                          \
+  } while (0)
+
 #define IM_CHECK()                                                                             \
   do {                                                                                         \
     hipError_t _e = hipGetLastError();                                                         \
@@ -556,7 +575,7 @@ int network_forward(acme_impala* l, const void* obs, const int32_t* prev_a, cons
     p.x = l->h; p.x2 = l->h; p.split_b = rows; p.ldx = H;
     p.w = P(l, l->params, l->t_w1); p.bias = P(l, l->params, l->t_b1); p.y = l->hh;
     p.act = ACT_RELU; p.slab = nullptr;
-    IM_GEMM("impala_head_fwd", 32, 32, 1, 1, 8, p, 1);
+    IM_DGEMM("impala_head_fwd", p);
   }
   {
     DenseFwd<false> p;
@@ -564,7 +583,7 @@ int network_forward(acme_impala* l, const void* obs, const int32_t* prev_a, cons
     p.x = l->hh; p.x2 = l->hh; p.split_b = rows; p.ldx = l->H2;
     p.w = P(l, l->params, l->t_wpv); p.bias = P(l, l->params, l->t_bpv); p.y = l->pv;
     p.act = ACT_NONE; p.slab = nullptr;
-    IM_GEMM("impala_pv_fwd", 32, 32, 1, 1, 8, p, 1);
+    IM_DGEMM("impala_pv_fwd", p);
   }
   return ACME_OK;
 }
@@ -607,22 +626,22 @@ int impala_step_impl(acme_impala* l, const acme_sequence_batch* bt, float* metri
     w.M = l->H2; w.N = A + 1; w.K = rows; w.k_chunk = rows;
     w.x = l->hh; w.ldx = l->H2; w.dz = l->dpv; w.out = Pm(l, gr, l->t_wpv);
     w.bias_out = Pm(l, gr, l->t_bpv);
-    IM_GEMM("impala_pv_wgrad", 32, 32, 1, 1, 8, w, 1);
+    IM_DGEMM("impala_pv_wgrad", w);
     DenseDgrad<false> d;
     d.M = rows; d.N = l->H2; d.K = A + 1; d.k_chunk = A + 1;
     d.dz = l->dpv; d.w = P(l, l->params, l->t_wpv); d.xprev = l->hh; d.ldx = l->H2; d.dx = l->dhh;
     d.act = ACT_RELU;
-    IM_GEMM("impala_pv_dgrad", 32, 32, 1, 1, 8, d, 1);
+    IM_DGEMM("impala_pv_dgrad", d);
   }
   {  // Linear(256) after the LSTM
     DenseWgrad<true> w;
     w.M = H; w.N = l->H2; w.K = rows; w.k_chunk = rows;
     w.x = l->h; w.ldx = H; w.dz = l->dhh; w.out = Pm(l, gr, l->t_w1); w.bias_out = Pm(l, gr, l->t_b1);
-    IM_GEMM("impala_head_wgrad", 32, 32, 1, 1, 8, w, 1);
+    IM_DGEMM("impala_head_wgrad", w);
     DenseDgrad<true> d;
     d.M = rows; d.N = H; d.K = l->H2; d.k_chunk = l->H2;
     d.dz = l->dhh; d.w = P(l, l->params, l->t_w1); d.xprev = nullptr; d.ldx = H; d.dx = l->dh;
-    IM_GEMM("impala_head_dgrad", 32, 32, 1, 1, 8, d, 1);
+    IM_DGEMM("impala_head_dgrad", d);
   }
   {  // BPTT
     ACME_PROF("impala_lstm_bwd", st, 2.0 * rows * (double)H * 4 * H, 0.0);
