@@ -922,10 +922,12 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
       (rc = dev_alloc(l, &l->g, (int64_t)B)) || (rc = dev_alloc(l, &l->a_cache, (int64_t)B)) ||
       (rc = dev_alloc(l, &l->loss_tmp, 4)) || (rc = dev_alloc(l, &l->td_tmp, (int64_t)B)) ||
       (rc = dev_alloc(l, &l->prio_tmp, (int64_t)B)) ||
-      (l->stamps_on && (rc = dev_alloc(l, &l->stamps, (int64_t)4 * 4096 * 8))))
+      (l->stamps_on && (rc = dev_alloc(l, &l->stamps, (int64_t)5 * 4096 * 8))))
     return fail(rc);
-  if (l->stamps_on)  // [fc_fwd, conv1, conv2, conv3][4096][8] (one learner at a time)
+  if (l->stamps_on) {  // [fc_fwd, conv1, conv2, conv3, update][4096][8] (one learner at a time)
     for (int i = 0; i < 3; ++i) torso::g_stamps_conv[i] = l->stamps + (int64_t)(i + 1) * 4096 * 8;
+    g_update_stamps = l->stamps + (int64_t)4 * 4096 * 8;
+  }
   if (hipDeviceSynchronize() != hipSuccess)
     return fail((set_error("learner init failed"), ACME_ERR_HIP));
   *out = l;
@@ -935,8 +937,10 @@ int acme_dqn_create(const acme_dqn_config* cfg, acme_dqn** out) {
 int acme_dqn_destroy(acme_dqn* l) {
   if (!l) return ACME_OK;
   (void)hipDeviceSynchronize();
-  if (l->stamps_on)
+  if (l->stamps_on) {
     for (auto& p : torso::g_stamps_conv) p = nullptr;
+    g_update_stamps = nullptr;
+  }
   for (void* p : l->allocs) (void)hipFree(p);
   for (auto& e : l->ev)
     if (e) (void)hipEventDestroy(e);
@@ -1113,7 +1117,7 @@ int acme_dqn_debug_buffer(const acme_dqn* l, const char* name, const float** out
     const char* n;
     const float* p;
     int64_t c;
-  } tab[] = {{"gemm_stamps", reinterpret_cast<const float*>(l->stamps), 2 * 4 * 4096 * 8},
+  } tab[] = {{"gemm_stamps", reinterpret_cast<const float*>(l->stamps), 2 * 5 * 4096 * 8},
              {"x1", l->x1, 2 * B * 441 * 32}, {"x2", l->x2, 2 * B * kFlat},
              {"x3", l->x3, 2 * B * kFlat},    {"hid", l->hid, 2 * B * 2 * kHidden},
              {"dzh", l->dzh, B * 2 * kHidden}, {"dz3", l->dz3, B * kFlat},

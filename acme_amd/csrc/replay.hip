@@ -40,6 +40,11 @@
 #include "profiler.h"
 #include "rescale.h"
 
+namespace acme {
+// Timing experiment hook (rescale.h): the DQN learner sets it while ACME_V_STAMPS=1.
+uint64_t* g_update_stamps = nullptr;
+}  // namespace acme
+
 using namespace acme;
 
 // Host inserts (the actor side, adders/reverb/transition.py:119-165 -> one item per env
@@ -653,6 +658,11 @@ struct FusedUpdateArgs {
   // write nothing when the step was skipped, for every reason the rescale decides
   // (overflow, underflow, a timed-out unroll, the sticky hold, another rank's skip).
   RescaleJob job;
+  // Timing experiment (ACME_V_STAMPS=1 in the DQN learner, tools/update_stamps.py): thread 0 of
+  // each workgroup stores s_memrealtime (100 MHz) at its phase boundaries, 8 slots per
+  // workgroup: entry, keys resolved (workgroup 0: rescale done), node list, verdict, leaves,
+  // levels, exit.
+  uint64_t* stamps = nullptr;
 };
 // Waits (bounded) for the verdict with sequence number seq; true when that step is skipped
 // (or the wait timed out: no priority is written).  Workgroup 0 of the same launch publishes
@@ -684,8 +694,14 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
   __shared__ int s_lvl[kUpdPairs];
   __shared__ double s_val[kUpdPairs];
   const int first = a.job.s ? 1 : 0;
+  auto stamp = [&](int ph) {
+    if (a.stamps && threadIdx.x == 0)
+      a.stamps[8 * (int64_t)blockIdx.x + ph] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   if (a.job.s && blockIdx.x == 0) {
     rescale_block(a.job);
+    stamp(1);
     return;
   }
   const bool verdict = a.job.s && a.job.rg.g && a.job.rg.mode == kRgStep;
@@ -728,6 +744,7 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
     }
   }
   __syncthreads();
+  stamp(1);
   const int len = s_len;
   if (len > 0) {
     // The distinct nodes of levels 1..h this workgroup recomputes (one thread; a few per
@@ -752,6 +769,7 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
       s_ovf = ovf;
     }
     __syncthreads();
+    stamp(2);
     const int np = s_np;
     const bool pre = !s_ovf;
     // One round of loads: each node's 64 children (a wave per node), each update's priority.
@@ -768,6 +786,7 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
     // The step's verdict (published by workgroup 0's rescale while this workgroup resolved
     // its keys and loaded), before the first store.
     if (verdict) skip = wait_verdict_skip(a.job.rg.g, a.job.rg.seq);
+    stamp(3);
     if (!skip) {
       // Last update of each slot wins: its raw priority and leaf, substituted into its
       // level-1 node's children.
@@ -790,6 +809,7 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
             if (s_lvl[q] == 1 && s_node[q] == (slot >> 6)) s_ch[q][slot & 63] = leaf;
       }
       __syncthreads();
+      stamp(4);
       for (int l = 1; l <= h; ++l) {  // level by level
         if (pre) {
           for (int q = wave; q < np; q += nw) {
@@ -818,8 +838,10 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
         }
         __syncthreads();
       }
+      stamp(5);
     }
   }
+  stamp(6);
   if (a.nlevels < 2 || a.top_computed) return;  // readers compute the top (TreeView)
   // Count this workgroup finished once its write-through stores have left (drained), then
   // the last one rescans the top level from them.
@@ -1894,6 +1916,7 @@ int acme::replay_update_priorities_gated(acme_replay* r, const uint64_t* keys,
     a.top_nodes = r->nlevels >= 2 ? r->level_size[r->nlevels - 2] / 64 : 0;
     a.top_computed = computed_top_nodes(r) > 0 ? 1 : 0;
     a.done = r->upd_done;
+    a.stamps = g_update_stamps;
     prio_update_fused_kernel<<<kFusedUpdateBlocks + (a.job.s ? 1 : 0), 256, 0, st>>>(a);
     ACME_LAUNCH_CHECK();
     return ACME_OK;

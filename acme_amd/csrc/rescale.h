@@ -24,6 +24,10 @@
 
 namespace acme {
 
+// Timing experiment (replay.hip prio_update_fused_kernel phase stamps, 8 per workgroup):
+// non-null while a DQN learner created with ACME_V_STAMPS=1 lives.
+extern uint64_t* g_update_stamps;
+
 struct RescaleJob {
   gemm::PScale* s = nullptr;  // null: no job
   int nt = 0, n = 0, copy_from = -1, copy_to = -1;
