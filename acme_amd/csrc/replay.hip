@@ -747,27 +747,33 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
   stamp(1);
   const int len = s_len;
   if (len > 0) {
-    // The distinct nodes of levels 1..h this workgroup recomputes (one thread; a few per
-    // workgroup at the learner's batch sizes).
+    // The distinct nodes of levels 1..h this workgroup recomputes: a thread per (level,
+    // update) keeps the node if no earlier update of the list has the same ancestor at that
+    // level (a serial scan by one thread took up to 7 us on the workgroup with the most
+    // updates, profiles/r05/update_stamps/).  The list's order is the threads' (atomic slot
+    // order); every use below matches nodes by (level, node), so the result does not depend
+    // on it.
     if (tid == 0) {
-      int np = 0, ovf = 0;
-      for (int l = 1; l <= h && !ovf; ++l)
-        for (int e = 0; e < len && !ovf; ++e) {
-          const int64_t node = s_slot[e] >> (6 * l);
-          bool seen = false;
-          for (int q = 0; q < np; ++q) seen = seen || (s_lvl[q] == l && s_node[q] == node);
-          if (seen) continue;
-          if (np == kUpdPairs) {
-            ovf = 1;
-          } else {
-            s_lvl[np] = l;
-            s_node[np] = node;
-            ++np;
-          }
-        }
-      s_np = np;
-      s_ovf = ovf;
+      s_np = 0;
+      s_ovf = 0;
     }
+    __syncthreads();
+    for (int idx = tid; idx < h * len; idx += nt) {
+      const int l = 1 + idx / len, e = idx - (l - 1) * len;
+      const int64_t node = s_slot[e] >> (6 * l);
+      bool first = true;
+      for (int f = 0; f < e && first; ++f) first = (s_slot[f] >> (6 * l)) != node;
+      if (!first) continue;
+      const int q = atomicAdd(&s_np, 1);
+      if (q < kUpdPairs) {
+        s_lvl[q] = l;
+        s_node[q] = node;
+      } else {
+        s_ovf = 1;
+      }
+    }
+    __syncthreads();
+    if (tid == 0 && s_np > kUpdPairs) s_np = kUpdPairs;  // (with s_ovf: the read-back path)
     __syncthreads();
     stamp(2);
     const int np = s_np;
