@@ -789,50 +789,69 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
       for (int q = wave; q < np; q += nw)
         s_ch[q][lane] = a.level[s_lvl[q] - 1][s_node[q] * 64 + lane];
     }
+    // Everything but the stores before the verdict: the last update of each slot wins (its
+    // leaf p^alpha kept in registers and substituted into its level-1 node's children) and,
+    // on the prefetched path, every node's new value rescanned level by level in LDS.
+    constexpr int R = kFusedUpdateMax / 256;
+    bool winv[R];
+    double leafv[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int e = tid + i * nt;
+      if (e >= len) break;
+      const int64_t slot = s_slot[e];
+      const int j = s_j[e];
+      bool win = true;
+      for (int f = 0; f < len; ++f)
+        if (s_slot[f] == slot && s_j[f] > j) win = false;
+      winv[i] = win;
+      if (!win) continue;
+      leafv[i] = det_pow_priority(pv[i], a.alpha);
+      if (pre)
+        for (int q = 0; q < np; ++q)
+          if (s_lvl[q] == 1 && s_node[q] == (slot >> 6)) s_ch[q][slot & 63] = leafv[i];
+    }
+    __syncthreads();
+    if (pre) {
+      for (int l = 1; l <= h; ++l) {
+        for (int q = wave; q < np; q += nw) {
+          if (s_lvl[q] != l) continue;
+          const double v = wave_scan64(s_ch[q][lane]);
+          if (lane == 63) s_val[q] = v;
+        }
+        __syncthreads();
+        if (tid < np && s_lvl[tid] == l)  // into the parent's children
+          for (int q = 0; q < np; ++q)
+            if (s_lvl[q] == l + 1 && s_node[q] == (s_node[tid] >> 6))
+              s_ch[q][s_node[tid] & 63] = s_val[tid];
+        __syncthreads();
+      }
+    }
     // The step's verdict (published by workgroup 0's rescale while this workgroup resolved
-    // its keys and loaded), before the first store.
+    // its keys, loaded and computed), before the first store.
     if (verdict) skip = wait_verdict_skip(a.job.rg.g, a.job.rg.seq);
     stamp(3);
     if (!skip) {
-      // Last update of each slot wins: its raw priority and leaf, substituted into its
-      // level-1 node's children.
 #pragma unroll
-      for (int i = 0; i < kFusedUpdateMax / 256; ++i) {
+      for (int i = 0; i < R; ++i) {
         const int e = tid + i * nt;
         if (e >= len) break;
+        if (!winv[i]) continue;
         const int64_t slot = s_slot[e];
-        const int j = s_j[e];
-        bool win = true;
-        for (int f = 0; f < len; ++f)
-          if (s_slot[f] == slot && s_j[f] > j) win = false;
-        if (!win) continue;
-        const double leaf = det_pow_priority(pv[i], a.alpha);
         a.raw_prio[slot] = pv[i];
-        if (h == 0 && !a.top_computed) store_shared_level(a.level[0] + slot, leaf);
-        else a.level[0][slot] = leaf;
-        if (pre)
-          for (int q = 0; q < np; ++q)
-            if (s_lvl[q] == 1 && s_node[q] == (slot >> 6)) s_ch[q][slot & 63] = leaf;
+        if (h == 0 && !a.top_computed) store_shared_level(a.level[0] + slot, leafv[i]);
+        else a.level[0][slot] = leafv[i];
       }
-      __syncthreads();
       stamp(4);
-      for (int l = 1; l <= h; ++l) {  // level by level
-        if (pre) {
-          for (int q = wave; q < np; q += nw) {
-            if (s_lvl[q] != l) continue;
-            const double v = wave_scan64(s_ch[q][lane]);
-            if (lane == 63) {
-              s_val[q] = v;
-              if (l == h && !a.top_computed) store_shared_level(a.level[l] + s_node[q], v);
-              else a.level[l][s_node[q]] = v;
-            }
-          }
-          __syncthreads();
-          if (tid < np && s_lvl[tid] == l)  // into the parent's children
-            for (int q = 0; q < np; ++q)
-              if (s_lvl[q] == l + 1 && s_node[q] == (s_node[tid] >> 6))
-                s_ch[q][s_node[tid] & 63] = s_val[tid];
-        } else {  // read back what this workgroup stored (levels below are its own)
+      if (pre) {
+        for (int q = tid; q < np; q += nt) {
+          const int l = s_lvl[q];
+          if (l == h && !a.top_computed) store_shared_level(a.level[l] + s_node[q], s_val[q]);
+          else a.level[l][s_node[q]] = s_val[q];
+        }
+      } else {
+        __syncthreads();
+        for (int l = 1; l <= h; ++l) {  // read back what this workgroup stored (levels below are its own)
           for (int e = wave; e < len; e += nw) {
             const int64_t node = s_slot[e] >> (6 * l);
             const double v = wave_scan64(a.level[l - 1][node * 64 + lane]);
@@ -841,8 +860,8 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
               else a.level[l][node] = v;
             }
           }
+          __syncthreads();
         }
-        __syncthreads();
       }
       stamp(5);
     }
