@@ -153,6 +153,37 @@ def test_full_size_steps_match_oracle(B):
     assert n.num_steps == 3
 
 
+@pytest.mark.parametrize("B", [45, 600])
+def test_odd_shapes_match_oracle(B):
+    """Widths that are not multiples of the 32-wide tiles, a 1024-wide layer input (two
+    passes of the register-operand engine's k loop), 21 atoms, 3 actions, 7 observations,
+    a ragged batch and one past 512 rows (two k passes in the weight gradients): the direct
+    engine's edges (rows and columns past M and N, k past K read as zero) and the widest
+    LayerNorm instantiations, two steps against the float64 oracle."""
+    cfg = O.D4PGConfig(obs_dim=7, act_dim=3, policy_sizes=(36, 100),
+                       critic_sizes=(1024, 132, 44), num_atoms=21, vmin=-10.0, vmax=10.0,
+                       action_min=(-1.0,) * 3, action_max=(1.0,) * 3, target_update_period=2)
+    n = _native(cfg, B)
+    params, target = _random_params(cfg, 7), _random_params(cfg, 8)
+    n.set_params(params, target)
+    z = {k: np.zeros_like(v) for k, v in params.items()}
+    state = dict(params=params, target=target, m=z, v=dict(z), num_steps=0)
+    for s in range(2):
+        batch = _batch(cfg, B, 20 + s)
+        n.step(*_dev(batch))
+        torch.cuda.synchronize()
+        ref, raw, state = O.d4pg_step(cfg, state, batch, np.float64)
+        _close(n.critic_loss.item(), ref["critic_loss"], name=f"critic_loss@{s}")
+        _close(n.policy_loss.item(), ref["policy_loss"], rtol=1e-4, name=f"policy_loss@{s}")
+        _check_grads(n, raw)
+        got = n.get_params("params")
+        _check_params(got, state["params"], cfg.policy_lr)
+        state["params"] = {k: got[k].astype(np.float32) for k in got}
+        state["m"] = n.get_params("m")
+        state["v"] = n.get_params("v")
+        state["target"] = n.get_params("target")
+
+
 def test_policy_forward_matches_oracle():
     cfg = O.D4PGConfig(action_min=(-2.0,) * 6, action_max=(0.5,) * 6)
     n = _native(cfg, 64)
