@@ -131,6 +131,8 @@ _SIGS = {
     "acme_set_matmul_engine": (c_i32, [c_i32]),
     "acme_matmul_engine": (c_i32, []),
     "acme_dense_forward": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp]),
+    "acme_dense_forward_staged": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_i32, c_vp,
+                                          c_i32, c_i32, c_i32, c_vp]),
     "acme_replay_create": (c_i32, [ctypes.POINTER(ReplayConfig), ctypes.POINTER(c_vp)]),
     "acme_replay_destroy": (c_i32, [c_vp]),
     "acme_replay_insert": (c_i32, [c_vp, ctypes.POINTER(c_vp), c_i64, c_vp, c_i32, c_vp, c_vp]),
@@ -190,6 +192,7 @@ _SIGS = {
     "acme_dqn_plane_overflow": (c_i32, [c_vp, ctypes.POINTER(c_i32), c_i32]),
     "acme_dqn_skipped_steps": (c_i64, [c_vp]),
     "acme_dqn_guard_state": (c_i32, [c_vp, ctypes.POINTER(c_i64)]),
+    "acme_dqn_verdict_timeouts": (c_i32, [c_vp, ctypes.POINTER(c_i64)]),
     "acme_dqn_set_applied_steps": (c_i32, [c_vp, c_i64]),
     "acme_dqn_skip_word": (c_i32, [c_vp, ctypes.POINTER(c_vp)]),
     "acme_dqn_set_reissue": (c_i32, [c_vp, c_i32]),

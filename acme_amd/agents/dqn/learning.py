@@ -26,6 +26,12 @@ batches again in their order, with the step counter of their first issue (so a d
 copy lands), before drawing the next batch; save(), state, get_variables() and q_values()
 settle the last two steps the same way first.  So every step() call applies exactly one
 update, in the reference's order, and a skip only costs the re-issued steps' time.
+Re-issue needs the batches of the last two step() calls intact until the next draw: the
+repo's own dataset iterators guarantee it (`holds_last_batches = 2`, their buffer rings);
+with any other iterator the learner keeps its own copy of each held batch (one device copy
+per step).  A write-back inside the step that timed out waiting for the step's verdict
+(never expected; it would leave a step applied without its priorities) raises RuntimeError
+when the learner next settles (save(), state, get_variables(), q_values()).
 `"raise"` raises FloatingPointError instead; `"skip"` keeps the skip (the step's batch is
 dropped, as before round 5).  `num_steps` (the target period) counts step() calls; Adam's
 t counts applied updates.
@@ -132,6 +138,9 @@ class DQNLearner(core.Learner, core.Saveable):
         self._held = collections.deque(maxlen=_REISSUE_LAG)
         self._checked = self._native.verdicts_issued  # verdicts below this are settled
         self._reissued = 0
+        # A foreign iterator may reuse its buffers on the next draw: hold copies then.
+        self._copy_held = (self._reissue and getattr(self._iterator, "holds_last_batches", 0)
+                           < _REISSUE_LAG)
 
     # ------------------------------------------------------------------ step
     def _prepare(self, x: torch.Tensor, dtype) -> torch.Tensor:
@@ -176,6 +185,9 @@ class DQNLearner(core.Learner, core.Saveable):
                 self._reissue_from(self._checked)
             else:
                 self._checked += 1
+        if settle and n.guard_state()["verdict_timeouts"]:
+            raise RuntimeError("DQN learner: a priority write-back timed out waiting for its "
+                               "step's verdict (the step's priorities were not written)")
 
     def _reissue_from(self, seq: int) -> None:
         """Step `seq` was skipped, and (sticky hold) every step issued after it: recalibrate
@@ -257,6 +269,10 @@ class DQNLearner(core.Learner, core.Saveable):
         if fb is not None:
             fb = (fb[:2 * B] if obs_dt == torch.uint8 and fb.shape[0] >= 2 * B
                   and fb.shape[1] == self._obs_flat else None)
+        if self._copy_held:
+            batch = tuple(x.clone() for x in batch)
+            keys = keys.clone()
+            fb = None if fb is None else fb.clone()
         e = dict(batch=batch, fb=fb, keys=keys, B=B, inputs_event=inputs_event)
         self._issue(e)
         if self._reissue:

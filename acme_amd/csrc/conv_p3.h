@@ -412,6 +412,7 @@ struct P3ConvDgradSubZ {
 struct P3DenseFwd {
   static constexpr int A_MODE = gemm::KCONTIG, B_MODE = gemm::RCONTIG;
   static constexpr int A_PLANES = gemm::kPlanes, B_PLANES = gemm::kPlanes;
+  static constexpr bool kNoSplitAcc = true;  // gemm_p3.h P3Acc
   int M, N, K, k_chunk;
   PlaneSrc a_src;  // X
   int ldx;
@@ -449,6 +450,7 @@ struct P3DenseFwd {
 struct P3DenseWgrad {
   static constexpr int A_MODE = gemm::RCONTIG, B_MODE = gemm::RCONTIG;
   static constexpr int A_PLANES = gemm::kPlanes, B_PLANES = gemm::kPlanes;
+  static constexpr bool kNoSplitAcc = true;  // gemm_p3.h P3Acc
   static constexpr bool kColSum = true;
   int M, N, K, k_chunk;  // M = Kin, N = Nout, K = rows (batch)
   PlaneSrc a_src;        // X [rows][ldx]

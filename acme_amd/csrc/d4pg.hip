@@ -37,13 +37,9 @@
 #include "kernels.h"
 #include "profiler.h"
 
-#ifndef D4_DIRECT
-#define D4_DIRECT 1
-#endif
 
 using namespace acme;
 using namespace acme::conv;
-using acme::gemm::launch_gemm;
 
 namespace {
 
@@ -665,59 +661,13 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const LnBwdArgs a) {
   }
 }
 
-// ------------------------------------------------------------------ weight gradient of the
-// first layer: dW = concat(x0, x1)^T dZ over the batch, bias = column sums of dZ (staged
-// engine; the direct engine runs it as two DenseWgrad problems).
-struct ConcatWgrad {
-  static constexpr int A_MODE = gemm::RCONTIG, B_MODE = gemm::RCONTIG;
-  static constexpr bool kColSum = true;
-  int M, N, K, k_chunk;  // M = d0 + d1 (inputs), N = H, K = batch rows
-  const float* x0;
-  int d0;
-  const float* x1;
-  int d1;
-  const float* dz;  // [K][N]
-  float* out;       // [M][N]
-  float* bias_out;  // [N]
-  struct ARow {
-    int i;
-  };
-  struct BRow {
-    int n;
-  };
-  __device__ ARow a_row(int i) const { return ARow{i}; }
-  __device__ float x_at(int m, int f) const {
-    if (f < d0) return x0[(size_t)m * d0 + f];
-    if (f < d0 + d1) return x1[(size_t)m * d1 + (f - d0)];
-    return 0.f;
-  }
-  __device__ f32x4 a_load(const ARow& a, int m) const {
-    f32x4 r = gemm::zero4();
-    if (m >= K) return r;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) r[j] = x_at(m, a.i + j);
-    return r;
-  }
-  __device__ BRow b_row(int n) const { return BRow{n}; }
-  __device__ f32x4 b_load(const BRow& b, int m) const {
-    if (b.n >= N || m >= K) return gemm::zero4();
-    return load_row4<true>(dz + (size_t)m * N, b.n, N);
-  }
-  __device__ void store(int i, int n, float v, int) const { out[(size_t)i * N + n] = v; }
-  __device__ void store_colsum(int n, float v, int) const { bias_out[n] = v; }
-};
-
 // ------------------------------------------------------------------ orchestration
 
 // Small GEMMs: 32x32 output tiles, 8 waves per block splitting the reduction, so a
-// 512 x 512 x 512 layer runs 2048 waves.  D4_DIRECT (default): the register-operand engine
-// (gemm_direct.h, one load burst per wave); 0: the staged engine (gemm.h, 8 k-groups of
-// BK-16 stages; 4 groups measured 0.354 -> 0.328 ms per step with 8).
-#if D4_DIRECT
+// 512 x 512 x 512 layer runs 2048 waves: the register-operand engine (gemm_direct.h, one
+// load burst per wave; round 5: 0.196 -> 0.164 ms per step against the staged f32 engine of
+// gemm.h, profiles/r05/ab/d4pg_direct_*.log).
 #define D4_LAUNCH(prob, nz) gemm::launch_direct(prob, nz, (prob).K, st)
-#else
-#define D4_LAUNCH(prob, nz) launch_gemm<32, 32, 1, 1, 16, 8>(prob, nz, st)
-#endif
 #define D4_GEMM(name, prob)                                                                   \
   do {                                                                                        \
     ACME_PROF_PEAK(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0, 157.3);       \
@@ -761,13 +711,9 @@ int dense_fwd_pair(const char* name, const float* x0, int rows0, const float* w0
                    const float* b0, float* y0, const float* x1, int rows1, const float* w1,
                    const float* b1, float* y1, int K, int N, int act, hipStream_t st) {
   if (rows1 == 0) return dense_fwd(name, x0, rows0, K, w0, b0, N, act, y0, st);
-#if D4_DIRECT
   // The direct engine reads W by columns whatever N is; only the x rows' vector loads need
   // K % 4 == 0.
   if (K % 4 != 0) {
-#else
-  if (K % 4 != 0 || N % 4 != 0) {
-#endif
     int rc = dense_fwd(name, x0, rows0, K, w0, b0, N, act, y0, st);
     return rc != ACME_OK ? rc : dense_fwd(name, x1, rows1, K, w1, b1, N, act, y1, st);
   }
@@ -892,7 +838,6 @@ struct BwdGroup {
   std::vector<DenseDgrad<false>> dgn;  // widths not a multiple of 4 (the heads)
   std::vector<DenseWgrad<true>> wg;
   std::vector<DenseWgrad<false>> wgn;
-  std::vector<ConcatWgrad> first;
 };
 
 // dW = X^T dZ over `rows` rows, db = column sums of dZ.
@@ -969,17 +914,11 @@ int launch_multi(const char* name, hipStream_t st, const std::vector<Q>&... qs) 
     return (set_error("too many GEMMs in one backward launch"), ACME_ERR_INVALID);
   if (count == 0) return ACME_OK;
   ACME_PROF_PEAK(name, st, flops, 0.0, 157.3);
-#if D4_DIRECT
   const hipError_t e = gemm::launch_direct_multi(m, tiles, count, kmax, st);
   if (e != hipSuccess) {
     set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(e), __FILE__, __LINE__);
     return ACME_ERR_HIP;
   }
-#else
-  (void)kmax;
-  hipLaunchKernelGGL((gemm::gemm_f32_multi_kernel<32, 32, 1, 1, 16, 8, gemm::ZSet<Q, kZ>...>),
-                     dim3((unsigned)tiles, 1, (unsigned)count), dim3(64 * 8), 0, st, m);
-#endif
   D4_CHECK();
   return ACME_OK;
 }
@@ -988,22 +927,13 @@ int launch_multi(const char* name, hipStream_t st, const std::vector<Q>&... qs) 
 // layers' the rest.
 int launch_bwd(const char* name, BwdGroup& g, hipStream_t st) {
   int rc;
-#if D4_DIRECT
-  // (No ConcatWgrad problems: ln_backward splits them into DenseWgrad ones.)
+  // (The concat first layer's weight gradient is two DenseWgrad problems, ln_backward.)
   if (g.dgn.empty() && g.wgn.empty())
     rc = launch_multi(name, st, g.dg, g.wg);
   else if (g.dg.empty() && g.wg.empty())
     rc = launch_multi(name, st, g.dgn, g.wgn);
   else
     rc = launch_multi(name, st, g.dg, g.wg, g.dgn, g.wgn);
-#else
-  if (g.dgn.empty() && g.wgn.empty() && g.first.empty())
-    rc = launch_multi(name, st, g.dg, g.wg);
-  else if (g.dg.empty() && g.wg.empty())
-    rc = launch_multi(name, st, g.dgn, g.wgn, g.first);
-  else
-    rc = launch_multi(name, st, g.dg, g.wg, g.dgn, g.wgn, g.first);
-#endif
   g = BwdGroup{};
   return rc;
 }
@@ -1102,7 +1032,6 @@ int run_ln_reduces(const std::vector<LnReduce>& ln, hipStream_t st) {
 // (direct engine; the reductions read only ln_bwd's partials), else two.
 int launch_bwd_last(const char* name, BwdGroup& g, const std::vector<LnReduce>& ln,
                     hipStream_t st) {
-#if D4_DIRECT
   std::vector<LnReduceBlock> lr;
   for (const LnReduce& x : ln) {
     LnReduceBlock b;
@@ -1120,10 +1049,6 @@ int launch_bwd_last(const char* name, BwdGroup& g, const std::vector<LnReduce>& 
     rc = launch_multi(name, st, g.dg, g.wg, g.dgn, g.wgn, lr);
   g = BwdGroup{};
   return rc;
-#else
-  const int rc = launch_bwd(name, g, st);
-  return rc != ACME_OK ? rc : run_ln_reduces(ln, st);
-#endif
 }
 
 // Backward through the MLP part of a LayerNormMLP: `g` holds the launch that forms dz[nl-1]
@@ -1170,19 +1095,11 @@ int ln_backward(acme_d4pg* l, const NetDesc& d, const Acts& a, float* dy, int ro
     D4_CHECK();
   }
   ln.push_back({slab, nblk, H, Pm(l, l->grads, d.scale), Pm(l, l->grads, d.offset)});
-#if D4_DIRECT
   // dW1 = concat(xa, xb)^T dz: the xa rows and the xb rows of dW1 as two weight gradients
   // (strided operands); the bias gradient (column sums of dz) from the first.
   float* dw = Pm(l, l->grads, d.w1);
   add_wgrad(g, xa, ce_rows, da, dy, H, dw, Pm(l, l->grads, d.b1));
   if (db > 0) add_wgrad(g, xb, ce_rows, db, dy, H, dw + (size_t)da * H, nullptr);
-#else
-  ConcatWgrad p;
-  p.M = da + db; p.N = H; p.K = ce_rows; p.k_chunk = ce_rows;
-  p.x0 = xa; p.d0 = da; p.x1 = xb; p.d1 = db; p.dz = dy;
-  p.out = Pm(l, l->grads, d.w1); p.bias_out = Pm(l, l->grads, d.b1);
-  g.first.push_back(p);
-#endif
   return ACME_OK;
 }
 

@@ -304,9 +304,6 @@ inline int chunk_for(int K, int splits) {
   ACME_GEMM_F(name, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, BM, BN, WM, WN, prob, splits)
 
 // Same with an explicit reduction stage depth BK (16 or 32).
-#ifndef ACME_BIG_BK
-#define ACME_BIG_BK 16
-#endif
 #define ACME_GEMM_NK(name, BM, BN, WM, WN, BKV, prob, splits)                                 \
   do {                                                                                         \
     ACME_PROF_PEAK(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0, \
@@ -1050,6 +1047,17 @@ int acme_dqn_guard_state(acme_dqn* l, int64_t* out4) {
   out4[1] = g.skipped;
   out4[2] = g.last;
   out4[3] = g.qv;
+  return ACME_OK;
+}
+
+int acme_dqn_verdict_timeouts(acme_dqn* l, int64_t* out) {
+  ACME_CHECK_ARG(l && out, "null argument");
+  *out = 0;
+  if (!l->guard) return ACME_OK;
+  ACME_HIP_TRY(hipDeviceSynchronize());
+  StepGuard g;
+  ACME_HIP_TRY(hipMemcpy(&g, l->guard, sizeof(g), hipMemcpyDeviceToHost));
+  *out = g.vtimeout;
   return ACME_OK;
 }
 

@@ -457,11 +457,35 @@ __global__ void __launch_bounds__(64 * WM * WN * WK) gemm_f32_multi_kernel(const
   zmulti_run<BM, BN, WM, WN, BK, WK>(q, blockIdx.z, smem);
 }
 
+// The block size of every f32-engine launch is derived here from the kernel's own template
+// parameters: a (BK, WK) build experiment in round 5 launched the multi kernel instantiated
+// for WK = 4 (256 threads) with a hard-coded 512-thread block, so k-groups 4..7 indexed LDS
+// and the reduction buffers of groups that do not exist ("unspecified launch failure",
+// VERDICT r5 item 4).  The LDS of a block must also fit the CU's 160 KB.
+template <int BM, int BN, int WM, int WN, int BK, int WK>
+constexpr int gemm_threads() {
+  static_assert(64 * WM * WN * WK <= 1024, "at most 1024 threads per block");
+  return 64 * WM * WN * WK;
+}
+
 template <int BM, int BN, int WM, int WN, int BK = 16, int WK = 1, class P>
 inline hipError_t launch_gemm(const P& p, int splits, hipStream_t st) {
+  static_assert(gemm_smem_floats<BM, BN, WM, WN, BK, WK, P>() * 4 <= 160 * 1024,
+                "block LDS exceeds 160 KB");
   const int tiles = ((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
   hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, BK, WK, P>), dim3(tiles, 1, splits),
-                     dim3(64 * WM * WN * WK), 0, st, p);
+                     dim3(gemm_threads<BM, BN, WM, WN, BK, WK>()), 0, st, p);
+  return hipGetLastError();
+}
+
+// gemm_f32_multi_kernel over `count` sub-problems of `tiles` tiles each (grid z = count).
+template <int BM, int BN, int WM, int WN, int BK, int WK, class... S>
+inline hipError_t launch_gemm_multi(const ZMulti<S...>& q, int tiles, int count, hipStream_t st) {
+  static_assert(zmulti_smem_floats<BM, BN, WM, WN, BK, WK, S...>() * 4 <= 160 * 1024,
+                "block LDS exceeds 160 KB");
+  hipLaunchKernelGGL((gemm_f32_multi_kernel<BM, BN, WM, WN, BK, WK, S...>),
+                     dim3((unsigned)tiles, 1, (unsigned)count),
+                     dim3(gemm_threads<BM, BN, WM, WN, BK, WK>()), 0, st, q);
   return hipGetLastError();
 }
 

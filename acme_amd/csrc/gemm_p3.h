@@ -56,11 +56,6 @@
 #include "gemm.h"
 #include "gemm_x6.h"
 
-#ifndef P3_EXP
-#define P3_EXP 0  // bottleneck experiments: 1 no global loads, 2 no LDS fragment reads, 3 no MFMA,
-                  // 4 no loads and no LDS stores, 5 = 4 without the per-stage barrier
-#endif
-
 namespace acme {
 namespace gemm {
 
@@ -213,11 +208,7 @@ __device__ __forceinline__ u32x4 a_unit_f16(const u32x4& v) {
 // Maximum of two magnitudes (non-negative floats, or NaN) that keeps NaN: non-negative
 // floats order as their bits, and a NaN (sign cleared by fabsf) above infinity.  A plane
 // computed from overflowed planes is NaN, and its record must see that.
-#ifndef ACME_AMAX_FMAXF
-#define ACME_AMAX_FMAXF 0  // experiment: fmaxf (drops NaN)
-#endif
 __device__ __forceinline__ float amax_max(float a, float b) {
-  if constexpr (ACME_AMAX_FMAXF) return fmaxf(a, b);
   return __builtin_bit_cast(float, max(__builtin_bit_cast(uint32_t, a),
                                        __builtin_bit_cast(uint32_t, b)));
 }
@@ -258,13 +249,10 @@ struct EpiPre {
   struct type {};
   static constexpr bool has = false;
 };
-#ifndef EPI_PRE
-#define EPI_PRE 1  // 0: the epilogue loads its constants when it runs (the round-4 order)
-#endif
 template <class P>
 struct EpiPre<P, std::void_t<typename P::Pre>> {
   using type = typename P::Pre;
-  static constexpr bool has = EPI_PRE != 0;
+  static constexpr bool has = true;
 };
 
 // A plane tensor: plane i of element e at p[i * stride + e], written as x * sc->w.
@@ -318,6 +306,111 @@ constexpr int p3_nterms() {
   return 1 + (NPA == 2 ? 1 : 0) + (NPB == 2 ? 1 : 0) + (P3_FOUR_TERMS && NPA == 2 && NPB == 2 ? 1 : 0);
 }
 
+__device__ __forceinline__ f16x8 ones16() {
+  const _Float16 o = (_Float16)1.f;
+  return f16x8{o, o, o, o, o, o, o, o};
+}
+
+// Accumulators of a wave's tile (round 6).  v_mfma_f32_32x32x16_f16 does
+// not accumulate without bias: the three terms of each product summed into one running
+// accumulator carry an error whose mean is -0.05 (K = 256) to -0.13 (K = 4096) of its rms,
+// against 0 for the f32 MFMA (tools/mfma_bias.hip, profiles/r06/accuracy/mfma_bias.log), and
+// every dZ and activation tensor of the step inherited a mean of about -0.04 of its error
+// rms.  A convolution's weight gradient sums such a tensor against non-negative activations
+// over B x pixels rows, where a bias adds up linearly and unbiased errors as a square root:
+// at B = 64 the conv weight gradients carried 2.5-7x the exact-f32 engine's error
+// (profiles/r05/drift/grad_err_B64_step0.log).  The bits are lost where the small terms
+// (l, h) and (h, l) -- 2^-11 of the (h, h) term -- meet a large accumulator: accumulated in
+// their own tile (SPLIT) the bias falls 5x (K = 256) to 30x (K = 4096) and the rms error
+// 1.6x, and the tiles are added (one f32 add per element) before the epilogue.  The column
+// sums (bias gradients: ones x each B plane) split the same way (l plane apart).  Where the
+// split applies: products of two two-plane operands (the uint8 frames are one exact plane:
+// conv1's outputs carried a mean of -0.008 only) on wave tiles of at most four 32 x 32 MFMA
+// tiles, except problems with `kNoSplitAcc` -- the dense forward (fc_fwd's 128 x 64 consumer
+// tiles already hold 128 accumulators: a second set would not fit two waves per SIMD; its
+// output feeds only the head) and the dense weight gradient (a batch-long reduction whose
+// result is summed nowhere else; one block per CU instead of two with the second set).
+#ifndef P3_SPLIT_ACC
+#define P3_SPLIT_ACC 1  // 0: one accumulator per tile (the round-5 arithmetic; accuracy A/B)
+#endif
+template <class P, class = void>
+struct P3NoSplit : std::false_type {};
+template <class P>
+struct P3NoSplit<P, std::void_t<decltype(P::kNoSplitAcc)>>
+    : std::integral_constant<bool, P::kNoSplitAcc> {};
+template <class P, int MT, int NTL>
+constexpr bool p3_split_acc() {
+  return P3_SPLIT_ACC != 0 && P::A_PLANES == 2 && P::B_PLANES == 2 && MT * NTL <= 4 &&
+         !P3NoSplit<P>::value;
+}
+template <int MT, int NTL, int NCS, bool SPLIT>
+struct P3Acc {
+  static constexpr int SM = SPLIT ? MT : 1, SN = SPLIT ? NTL : 1, SC = SPLIT ? NCS : 1;
+  f32x16 a[MT][NTL];  // the (h, h) terms (every term without SPLIT)
+  f32x16 s[SM][SN];   // the small terms
+  f32x16 c[NCS];      // column sums of B's h plane (every plane without SPLIT)
+  f32x16 cl[SC];      // of its l plane
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NTL; ++j)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) a[i][j][v] = 0.f;
+#pragma unroll
+    for (int i = 0; i < SM; ++i)
+#pragma unroll
+      for (int j = 0; j < SN; ++j)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) s[i][j][v] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NCS; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) c[j][v] = 0.f;
+#pragma unroll
+    for (int j = 0; j < SC; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) cl[j][v] = 0.f;
+  }
+  // The terms of tile (i, j): smallest first, (1,0), (0,1) [, (1,1)] into s (SPLIT) or a,
+  // then (0,0) into a.
+  template <int NPA, int NPB>
+  __device__ __forceinline__ void terms(int i, int j, const f16x8 (&fa)[NPA],
+                                        const f16x8 (&fb)[NPB]) {
+    static_assert((NPA == 1 || NPA == 2) && (NPB == 1 || NPB == 2), "1 or 2 planes per operand");
+    if constexpr (SPLIT) {
+      f32x16& x = s[i][j];
+      if constexpr (P3_FOUR_TERMS && NPA == 2 && NPB == 2)
+        x = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[1], fb[1], x, 0, 0, 0);
+      if constexpr (NPA == 2) x = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[1], fb[0], x, 0, 0, 0);
+      if constexpr (NPB == 2) x = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[0], fb[1], x, 0, 0, 0);
+      a[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[0], fb[0], a[i][j], 0, 0, 0);
+    } else {
+      p3_terms<NPA, NPB>(fa, fb, a[i][j]);
+    }
+  }
+  // Column sums of B tile j: ones x each plane, the l plane first.
+  template <int NPB>
+  __device__ __forceinline__ void colsum(int j, const f16x8 (&fb)[NPB]) {
+    if constexpr (NPB == 2) {
+      f32x16& x = SPLIT ? cl[SPLIT ? j : 0] : c[j];
+      x = __builtin_amdgcn_mfma_f32_32x32x16_f16(ones16(), fb[1], x, 0, 0, 0);
+    }
+    c[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ones16(), fb[0], c[j], 0, 0, 0);
+  }
+  // a += s, c += cl (before the epilogue).
+  __device__ __forceinline__ void fold() {
+    if constexpr (SPLIT) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NTL; ++j) a[i][j] += s[i][j];
+#pragma unroll
+      for (int j = 0; j < NCS; ++j) c[j] += cl[j];
+    }
+  }
+};
+
 // Problems with `static constexpr bool kAmax = true` write a plane output whose scale
 // record amax_sc() collects max |x|.
 template <class P, class = void>
@@ -340,11 +433,6 @@ template <class P>
 struct HasStore8<P, decltype(void(P::kStore8))> {
   static constexpr bool value = P::kStore8;
 };
-
-__device__ __forceinline__ f16x8 ones16() {
-  const _Float16 o = (_Float16)1.f;
-  return f16x8{o, o, o, o, o, o, o, o};
-}
 
 template <int BK>
 __device__ __forceinline__ int p3_kswz(int row) {
@@ -436,16 +524,13 @@ struct P3Core {
   static constexpr bool kColSum = HasColSum<P>::value;
   static constexpr int NCS = kColSum ? NTL : 1;
   static constexpr int EPI_BYTES = HasStore8<P>::value ? WM * WN * 32 * (TN + 4) * 4 : 0;
+  static constexpr bool SPLIT = p3_split_acc<P, MT, NTL>();
+  using Acc = P3Acc<MT, NTL, NCS, SPLIT>;
 
-  struct NoHook {
-    __device__ void operator()(int) const {}
-  };
-  // hook(g) runs after MFMA group g = i * NTL + j of step S0 (the interleaving point for
-  // the next stage's LDS stores).
-  template <int S0 = 0, int S1 = BK / 16, class Hook = NoHook>
+  // The MFMAs of k16 steps S0 .. S1 - 1 of the stage at (sa, sb).
+  template <int S0 = 0, int S1 = BK / 16>
   __device__ static __forceinline__ void mma(const uint8_t* sa, const uint8_t* sb, int wm, int wn,
-                                             int lane, f32x16 (&acc)[MT][NTL], f32x16 (&cs)[NCS],
-                                             bool do_colsum, const Hook& hook = Hook()) {
+                                             int lane, Acc& acc, bool do_colsum) {
 #pragma unroll
     for (int s = S0; s < S1; ++s) {
       f16x8 fa[MT][NPA], fb[NTL][NPB];
@@ -453,35 +538,20 @@ struct P3Core {
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int pl = 0; pl < NPA; ++pl)
-          fa[i][pl] = P3_EXP == 2 ? ones16() : PA::frag(sa, pl, wm * TM + i * 32, s, lane);
+          fa[i][pl] = PA::frag(sa, pl, wm * TM + i * 32, s, lane);
 #pragma unroll
       for (int j = 0; j < NTL; ++j)
 #pragma unroll
         for (int pl = 0; pl < NPB; ++pl)
-          fb[j][pl] = P3_EXP == 2 ? ones16() : PB::frag(sb, pl, wn * TN + j * 32, s, lane);
-      if constexpr (P3_EXP == 3) {
-#pragma unroll
-        for (int i = 0; i < MT; ++i)
-#pragma unroll
-          for (int j = 0; j < NTL; ++j)
-            acc[i][j][0] += (float)fa[i][0][0] + (float)fb[j][0][0] + (float)fa[i][NPA - 1][1] +
-                            (float)fb[j][NPB - 1][1];
-        continue;
-      }
+          fb[j][pl] = PB::frag(sb, pl, wn * TN + j * 32, s, lane);
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
-        for (int j = 0; j < NTL; ++j) {
-          p3_terms<NPA, NPB>(fa[i], fb[j], acc[i][j]);
-          if (s == S0) hook(i * NTL + j);
-        }
+        for (int j = 0; j < NTL; ++j) acc.terms(i, j, fa[i], fb[j]);
       if constexpr (kColSum) {
         if (do_colsum) {
 #pragma unroll
-          for (int j = 0; j < NTL; ++j)
-#pragma unroll
-            for (int pl = NPB - 1; pl >= 0; --pl)
-              cs[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ones16(), fb[j][pl], cs[j], 0, 0, 0);
+          for (int j = 0; j < NTL; ++j) acc.colsum(j, fb[j]);
         }
       }
     }
@@ -503,20 +573,16 @@ struct P3Core {
 #pragma unroll
       for (int pl = 0; pl < NPB; ++pl) fb[j][pl] = PB::frag(sb, pl, wn * TN + j * 32, s, lane);
   }
-  __device__ static __forceinline__ void mfma_frags(const FragA& fa, const FragB& fb,
-                                                    f32x16 (&acc)[MT][NTL], f32x16 (&cs)[NCS],
+  __device__ static __forceinline__ void mfma_frags(const FragA& fa, const FragB& fb, Acc& acc,
                                                     bool do_colsum) {
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
-      for (int j = 0; j < NTL; ++j) p3_terms<NPA, NPB>(fa[i], fb[j], acc[i][j]);
+      for (int j = 0; j < NTL; ++j) acc.terms(i, j, fa[i], fb[j]);
     if constexpr (kColSum) {
       if (do_colsum) {
 #pragma unroll
-        for (int j = 0; j < NTL; ++j)
-#pragma unroll
-          for (int pl = NPB - 1; pl >= 0; --pl)
-            cs[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ones16(), fb[j][pl], cs[j], 0, 0, 0);
+        for (int j = 0; j < NTL; ++j) acc.colsum(j, fb[j]);
       }
     }
   }
@@ -528,6 +594,16 @@ struct P3Core {
   __device__ static __forceinline__ int epi_col(int lane) {
     static_assert(64 % (TN / 8) == 0, "a lane's chunk columns repeat");
     return 8 * (lane % (TN / 8));
+  }
+  // The epilogue of an accumulator struct: its tiles folded first (a += s, c += cl).
+  template <int M2, int N2, int C2, bool S2>
+  __device__ static __forceinline__ void epilogue(const P& p, uint8_t* smem, int m0, int n0,
+                                                  int wave, int wm, int wn, int lane, int split,
+                                                  P3Acc<M2, N2, C2, S2>& acc, bool do_colsum,
+                                                  const typename EpiPre<P>::type* pre = nullptr) {
+    static_assert(M2 == MT && N2 == NTL && C2 == NCS, "the accumulators of this tile");
+    acc.fold();
+    epilogue(p, smem, m0, n0, wave, wm, wn, lane, split, acc.a, acc.c, do_colsum, pre);
   }
   __device__ static __forceinline__ void epilogue(const P& p, uint8_t* smem, int m0, int n0,
                                                   int wave, int wm, int wn, int lane, int split,
@@ -585,25 +661,10 @@ struct P3Core {
   }
 };
 
-#ifndef P3_SPLIT
-#define P3_SPLIT 1  // 1: LDS stores between the two k16 steps of a BK-32 stage (measured +7% fc_fwd)
-#endif
-#ifndef P3_SCHED
-#define P3_SCHED 0
-#endif
-#ifndef P3_FETCH_FIRST
-#define P3_FETCH_FIRST 0  // 1: stage kt+2 loads issued at the top of iteration kt (see iter);
-                          // measured slower (fc_fwd 64 -> 75 us), kept as an experiment switch
-#endif
-#ifndef P3_EARLY_STASH
-#define P3_EARLY_STASH 1
-#endif
-
 // Register-staged kernel: global -> VGPR -> LDS, two LDS stages; with DEEP two register
 // sets so a stage's loads are issued two stages before its compute.
 template <int BM, int BN, int WM, int WN, int BK, bool DEEP, class P>
 __global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in, int n_major) {
-  constexpr bool EARLY_STASH = P3_EARLY_STASH;
   using C = P3Core<BM, BN, WM, WN, BK, P>;
   using PA = typename C::PA;
   using PB = typename C::PB;
@@ -648,8 +709,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in, int
       const uint32_t off = (PA::owns(u) && k0 + kk < kend) ? p.a_off(arow[i], k0, kk) : kOOB;
 #pragma unroll
       for (int pl = 0; pl < NPA; ++pl) {
-        ra[set][i][pl] = (P3_EXP == 1 || P3_EXP >= 4) ? u32x4{off, (uint32_t)k0, 1u, 2u}
-                                     : load_a_unit<P>(srcA[pl], off);
+        ra[set][i][pl] = load_a_unit<P>(srcA[pl], off);
       }
     }
 #pragma unroll
@@ -659,13 +719,12 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in, int
       const uint32_t off = (PB::owns(u) && k0 + kk < kend) ? p.b_off(brow[i], k0, kk) : kOOB;
 #pragma unroll
       for (int pl = 0; pl < NPB; ++pl)
-        rb[set][i][pl] = (P3_EXP == 1 || P3_EXP >= 4) ? u32x4{off, (uint32_t)k0, 1u, 2u}
-                                     : __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srcB[pl], off, 0, 0));
+        rb[set][i][pl] =
+            __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srcB[pl], off, 0, 0));
     }
   };
   auto stash = [&](auto S, int buf) {
     constexpr int set = decltype(S)::value;
-    if constexpr (P3_EXP >= 4) return;
     uint8_t* sa = smem + buf * STAGE;
     uint8_t* sb = sa + PA::BYTES;
 #pragma unroll
@@ -688,42 +747,12 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in, int
     }
   };
 
-  // One LDS store of the stash (k < WR: A units first, then B), for interleaving.
-  constexpr int WR = PA::PER_THREAD * NPA + PB::PER_THREAD * NPB;
-  auto stash_one = [&](auto S, int buf, int k) {
-    constexpr int set = decltype(S)::value;
-    uint8_t* sa = smem + buf * STAGE;
-    uint8_t* sb = sa + PA::BYTES;
-    if (k < PA::PER_THREAD * NPA) {
-      const int i = k / NPA, pl = k % NPA;
-      const int u = tid + i * NT;
-      if (PA::owns(u))
-        *reinterpret_cast<u32x4*>(sa + pl * PA::PLANE + PA::offset(u)) = a_unit_f16<P>(ra[set][i][pl]);
-    } else {
-      const int kb = k - PA::PER_THREAD * NPA;
-      const int i = kb / NPB, pl = kb % NPB;
-      const int u = tid + i * NT;
-      if (PB::owns(u))
-        *reinterpret_cast<u32x4*>(sb + pl * PB::PLANE + PB::offset(u)) = rb[set][i][pl];
-    }
-  };
-
-  f32x16 acc[C::MT][C::NTL];
-  f32x16 cs[C::NCS];
-#pragma unroll
-  for (int i = 0; i < C::MT; ++i)
-#pragma unroll
-    for (int j = 0; j < C::NTL; ++j)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
-#pragma unroll
-  for (int j = 0; j < C::NCS; ++j)
-#pragma unroll
-    for (int v = 0; v < 16; ++v) cs[j][v] = 0.f;
+  typename C::Acc acc;
+  acc.zero();
   const bool do_colsum = C::kColSum && m0 == 0 && wm == 0;
   auto compute = [&](int buf) {
     const uint8_t* sa = smem + buf * STAGE;
-    C::mma(sa, sa + PA::BYTES, wm, wn, lane, acc, cs, do_colsum);
+    C::mma(sa, sa + PA::BYTES, wm, wn, lane, acc, do_colsum);
   };
 
   using S0 = std::integral_constant<int, 0>;
@@ -743,70 +772,24 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in, int
     auto iter = [&](auto S, int kt) {
       constexpr int set = decltype(S)::value;
       using Other = std::integral_constant<int, set ^ 1>;
-      if constexpr (EARLY_STASH) {
-        // Branch-free body (one basic block, so the scheduler can spread the LDS stores
-        // and loads among the MFMAs): past the end, fetch reads zeros (offsets beyond kend
-        // are kOOB) and stash fills a buffer that is never read.
-        if constexpr (P3_SPLIT && BK == 32) {
-          // First k16 step's MFMAs, then the LDS stores of stage kt + 1 and the loads of
-          // stage kt + 2, then the second step: the stores overlap MFMAs already queued.
-          const uint8_t* sa = smem + set * STAGE;
-          if constexpr (P3_SPLIT == 2) {
-            // Stores interleaved among the first step's MFMA groups (source order).
-            constexpr int G = C::MT * C::NTL;
-            auto hook = [&](int g) {
-#pragma unroll
-              for (int k = g * WR / G; k < (g + 1) * WR / G; ++k) stash_one(Other{}, set ^ 1, k);
-            };
-            C::template mma<0, 1>(sa, sa + PA::BYTES, wm, wn, lane, acc, cs, do_colsum, hook);
-          } else if constexpr (P3_FETCH_FIRST) {
-            // The global loads of stage kt + 2 first (their registers were stashed in
-            // iteration kt - 1), fenced so the scheduler cannot sink them behind the MFMAs:
-            // they get two whole iterations to land before their stash.
-            fetch(S, kbeg + (kt + 2) * BK);
-            __builtin_amdgcn_sched_barrier(0);
-            C::template mma<0, 1>(sa, sa + PA::BYTES, wm, wn, lane, acc, cs, do_colsum);
-            stash(Other{}, set ^ 1);
-          } else {
-            C::template mma<0, 1>(sa, sa + PA::BYTES, wm, wn, lane, acc, cs, do_colsum);
-            stash(Other{}, set ^ 1);
-          }
-          if constexpr (!P3_FETCH_FIRST || P3_SPLIT == 2) fetch(S, kbeg + (kt + 2) * BK);
-          C::template mma<1, 2>(sa, sa + PA::BYTES, wm, wn, lane, acc, cs, do_colsum);
-        } else {
-          stash(Other{}, set ^ 1);
-          fetch(S, kbeg + (kt + 2) * BK);
-          compute(set);
-        }
-        if constexpr (P3_SCHED) {
-          // Issue order for the scheduler: the first k16 step's fragment reads, then each
-          // MFMA followed by at most one LDS store, one global load and (for the next k16
-          // step) fragment reads, so the stores and loads ride in the MFMAs' issue gaps
-          // instead of delaying the first MFMA.
-          constexpr int RD = C::MT * NPA * (P::A_MODE == KCONTIG ? 1 : 2) +
-                             C::NTL * NPB * (P::B_MODE == KCONTIG ? 1 : 2);
-          constexpr int TERMS = p3_nterms<NPA, NPB>();
-          constexpr int MF = C::MT * C::NTL * TERMS;
-          constexpr int WR = PA::PER_THREAD * NPA + PB::PER_THREAD * NPB;
-          constexpr int STEPS = BK / 16;
-          __builtin_amdgcn_sched_group_barrier(0x100, RD, 0);
-#pragma unroll
-          for (int st = 0; st < STEPS; ++st) {
-#pragma unroll
-            for (int m = 0; m < MF; ++m) {
-              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-              if (st == 0 && m < WR) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-              if (st == 0 && m < WR) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-              if (st + 1 < STEPS && m >= MF - RD) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-            }
-          }
-        }
+      // Branch-free body (one basic block, so the scheduler can spread the LDS stores and
+      // loads among the MFMAs): past the end, fetch reads zeros (offsets beyond kend are
+      // kOOB) and stash fills a buffer that is never read.
+      if constexpr (BK == 32) {
+        // First k16 step's MFMAs, then the LDS stores of stage kt + 1 and the loads of stage
+        // kt + 2, then the second step: the stores overlap MFMAs already queued (measured
+        // +7% fc_fwd against the stores before the first step).
+        const uint8_t* sa = smem + set * STAGE;
+        C::template mma<0, 1>(sa, sa + PA::BYTES, wm, wn, lane, acc, do_colsum);
+        stash(Other{}, set ^ 1);
+        fetch(S, kbeg + (kt + 2) * BK);
+        C::template mma<1, 2>(sa, sa + PA::BYTES, wm, wn, lane, acc, do_colsum);
       } else {
-        if (kt + 2 < nk) fetch(S, kbeg + (kt + 2) * BK);
+        stash(Other{}, set ^ 1);
+        fetch(S, kbeg + (kt + 2) * BK);
         compute(set);
-        if (kt + 1 < nk) stash(Other{}, set ^ 1);
       }
-      if constexpr (P3_EXP != 5) __syncthreads();
+      __syncthreads();
     };
     int kt = 0;
     for (; kt + 1 < nk; kt += 2) {
@@ -828,7 +811,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3_kernel(const P p_in, int
       __syncthreads();
     }
   }
-  C::epilogue(p, smem, m0, n0, wave, wm, wn, lane, split, acc, cs, do_colsum);
+  C::epilogue(p, smem, m0, n0, wave, wm, wn, lane, split, acc, do_colsum);
 }
 
 // LDS-DMA kernel: every operand unit goes HBM -> LDS by buffer_load ... lds (no VGPR
@@ -921,18 +904,8 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3g_kernel(const P p_in, in
     }
   };
 
-  f32x16 acc[C::MT][C::NTL];
-  f32x16 cs[C::NCS];
-#pragma unroll
-  for (int i = 0; i < C::MT; ++i)
-#pragma unroll
-    for (int j = 0; j < C::NTL; ++j)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
-#pragma unroll
-  for (int j = 0; j < C::NCS; ++j)
-#pragma unroll
-    for (int v = 0; v < 16; ++v) cs[j][v] = 0.f;
+  typename C::Acc acc;
+  acc.zero();
   const bool do_colsum = C::kColSum && m0 == 0 && wm == 0;
 
   // s_waitcnt immediates (gfx9 encoding): vmcnt(n) alone, and vmcnt(0) + lgkmcnt(0).
@@ -949,22 +922,15 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3g_kernel(const P p_in, in
     const int nb = buf == 0 ? STAGES - 1 : buf - 1;  // (kt + STAGES - 1) % STAGES
     issue(kt + STAGES - 1, nb);
     const uint8_t* sa = smem + buf * STAGE;
-    C::mma(sa, sa + PA::BYTES, wm, wn, lane, acc, cs, do_colsum);
+    C::mma(sa, sa + PA::BYTES, wm, wn, lane, acc, do_colsum);
     buf = buf == STAGES - 1 ? 0 : buf + 1;
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  C::epilogue(p, smem, m0, n0, wave, wm, wn, lane, split, acc, cs, do_colsum);
+  C::epilogue(p, smem, m0, n0, wave, wm, wn, lane, split, acc, do_colsum);
 #endif
 }
-
-#ifndef WS_EXP
-#define WS_EXP 0  // bottleneck experiments: 1 producers idle, 2 consumers idle
-#endif
-#ifndef WS_FENCE
-#define WS_FENCE 1  // consumers' pipelined loop: 1 fences (round 5: step 0.5096 -> 0.5048 ms), 2 reads threaded among the MFMAs (0.5132)
-#endif
 
 // Warp-specialised kernel: WM x WN consumer waves (fragment reads + MFMAs only, the same
 // P3Core::mma as gemm_p3_kernel, so the same bits) and as many producer waves (global ->
@@ -1058,16 +1024,6 @@ __global__ void __launch_bounds__(128 * WM * WN) gemm_p3ws_kernel(const P p_in, 
       }
     };
 
-    if constexpr (WS_EXP == 1) {
-      __syncthreads();
-      for (int kt = 0; kt < nk; ++kt) __syncthreads();
-      if constexpr (HasStore8<P>::value)
-        for (int i = 0; i < C::MT; ++i) {
-          __syncthreads();
-          __syncthreads();
-        }
-      return;
-    }
     fetch(S0{}, 0);
     fetch(S1{}, 1);
     stash(S0{}, 0);
@@ -1113,26 +1069,14 @@ __global__ void __launch_bounds__(128 * WM * WN) gemm_p3ws_kernel(const P p_in, 
       st_t0 = __builtin_amdgcn_s_memtime();
     }
   }
-  f32x16 acc[C::MT][C::NTL];
-  f32x16 cs[C::NCS];
-#pragma unroll
-  for (int i = 0; i < C::MT; ++i)
-#pragma unroll
-    for (int j = 0; j < C::NTL; ++j)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
-#pragma unroll
-  for (int j = 0; j < C::NCS; ++j)
-#pragma unroll
-    for (int v = 0; v < 16; ++v) cs[j][v] = 0.f;
+  typename C::Acc acc;
+  acc.zero();
   const bool do_colsum = C::kColSum && m0 == 0 && wm == 0;
   __syncthreads();
   if constexpr (HasStamps<P>::value)
     if (stamp) st_t1 = __builtin_amdgcn_s_memtime();
   int rbuf = 0;
-  if constexpr (WS_EXP == 2) {
-    for (int kt = 0; kt < nk; ++kt) __syncthreads();
-  } else if constexpr (PIPE && BK == 32) {
+  if constexpr (PIPE && BK == 32) {
     // Fragment reads one k16 step ahead: step 1 of stage kt is read before step 0's
     // MFMAs, and step 0 of stage kt + 1 (published by the previous barrier) before step
     // 1's, so no MFMA waits on the LDS latency of its own reads.
@@ -1143,49 +1087,31 @@ __global__ void __launch_bounds__(128 * WM * WN) gemm_p3ws_kernel(const P p_in, 
       const uint8_t* sa = smem + rbuf * STAGE;
       rbuf = rbuf == RING - 1 ? 0 : rbuf + 1;
       const uint8_t* na = smem + rbuf * STAGE;
-      // Scheduling fences (WS_FENCE): without them the compiler sinks each read to just
-      // before its first MFMA, to save registers, and the wave waits out the LDS latency
-      // there several times per stage (round 5: lgkmcnt(0) waits between the MFMAs).
-      // WS_FENCE 2 (no column sums): each k16 step's MFMAs with the other step's fragment
-      // reads threaded between them, one read per MFMA gap, so no read waits behind a burst
-      // of reads and the next step's operands land while this step's MFMAs run.
-      constexpr bool kThread = WS_FENCE == 2 && !C::kColSum;
-      constexpr int RD = C::MT * NPA * (P::A_MODE == KCONTIG ? 1 : 2) +
-                         C::NTL * NPB * (P::B_MODE == KCONTIG ? 1 : 2);
-      constexpr int MF = C::MT * C::NTL * p3_nterms<NPA, NPB>();
-      auto thread_reads = [&]() {
-        if constexpr (kThread) {
-#pragma unroll
-          for (int q = 0; q < (RD < MF ? RD : MF); ++q) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          }
-          if constexpr (MF > RD) __builtin_amdgcn_sched_group_barrier(0x008, MF - RD, 0);
-        }
-      };
+      // Scheduling fences: without them the compiler sinks each read to just before its
+      // first MFMA, to save registers, and the wave waits out the LDS latency there several
+      // times per stage (round 5: lgkmcnt(0) waits between the MFMAs; fenced, the step went
+      // 0.5096 -> 0.5048 ms; reads threaded one per MFMA gap measured 0.5132).
       C::read_frags(sa, sa + PA::BYTES, wm, wn, 1, lane, fa1, fb1);
-      if constexpr (WS_FENCE == 1 || (WS_FENCE == 2 && !kThread)) __builtin_amdgcn_sched_barrier(0);
-      C::mfma_frags(fa0, fb0, acc, cs, do_colsum);
-      thread_reads();
-      if constexpr (WS_FENCE) __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_sched_barrier(0);
+      C::mfma_frags(fa0, fb0, acc, do_colsum);
+      __builtin_amdgcn_sched_barrier(0);
       C::read_frags(na, na + PA::BYTES, wm, wn, 0, lane, fa0, fb0);
-      if constexpr (WS_FENCE == 1 || (WS_FENCE == 2 && !kThread)) __builtin_amdgcn_sched_barrier(0);
-      C::mfma_frags(fa1, fb1, acc, cs, do_colsum);
-      thread_reads();
-      if constexpr (WS_FENCE) __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_sched_barrier(0);
+      C::mfma_frags(fa1, fb1, acc, do_colsum);
+      __builtin_amdgcn_sched_barrier(0);
       __syncthreads();
     }
   } else {
     for (int kt = 0; kt < nk; ++kt) {
       const uint8_t* sa = smem + rbuf * STAGE;
-      C::mma(sa, sa + PA::BYTES, wm, wn, lane, acc, cs, do_colsum);
+      C::mma(sa, sa + PA::BYTES, wm, wn, lane, acc, do_colsum);
       rbuf = rbuf == RING - 1 ? 0 : rbuf + 1;
       __syncthreads();
     }
   }
   if constexpr (HasStamps<P>::value)
     if (stamp) st_t2 = __builtin_amdgcn_s_memtime();
-  C::epilogue(p, smem, m0, n0, wave, wm, wn, lane, split, acc, cs, do_colsum);
+  C::epilogue(p, smem, m0, n0, wave, wm, wn, lane, split, acc, do_colsum);
   if constexpr (HasStamps<P>::value) {
     if (stamp) {
       const uint64_t t3 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();

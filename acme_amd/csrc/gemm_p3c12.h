@@ -192,11 +192,8 @@ __global__ void __launch_bounds__(512) gemm_p3c12_kernel(const conv::P3ConvFwd<G
       const int lr = wave * 64 + i * 32 + (lane & 31);
       ln[i] = I1::lane(0, lr, lr < G1::OPIX);
     }
-    f32x16 acc[2][1];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][0][e] = 0.f;
+    typename Cfg::C1::Acc acc;
+    acc.zero();
     auto compute = [&](int k0, int buf) {
       const uint8_t* sb = smem + Cfg::RING1 + buf * PB1::BYTES;
       typename I1::Stage sg[2];
@@ -211,7 +208,7 @@ __global__ void __launch_bounds__(512) gemm_p3c12_kernel(const conv::P3ConvFwd<G
         for (int i = 0; i < 2; ++i) {
           const int u = I1::unit(sg[i], ln[i], k0, s, lane >> 5);
           const f16x8 fa[1] = {*reinterpret_cast<const f16x8*>(smem + (u >= 0 ? u : Cfg::FRAME - 16))};
-          p3_terms<1, NP>(fa, fb, acc[i][0]);
+          acc.terms(i, 0, fa, fb);
         }
       }
     };
@@ -232,8 +229,7 @@ __global__ void __launch_bounds__(512) gemm_p3c12_kernel(const conv::P3ConvFwd<G
     q.M = (f + 1) * G1::OPIX < p1.M ? (f + 1) * G1::OPIX : p1.M;
     q.N = p1.N; q.K = p1.K; q.k_chunk = p1.k_chunk;
     q.base = p1; q.x1 = x1; q.plane = Cfg::PLANE2; q.m0 = f * G1::OPIX; q.hbm = f < hbm_frames;
-    f32x16 cs[1];
-    Cfg::C1::epilogue(q, smem, q.m0, 0, wave, wave, 0, lane, 0, acc, cs, false);  // ends on a barrier
+    Cfg::C1::epilogue(q, smem, q.m0, 0, wave, wave, 0, lane, 0, acc, false);  // ends on a barrier
   }
 
   // ---- conv2 on the x1 image: 4 x 2 waves of 32 x 32.
@@ -243,9 +239,8 @@ __global__ void __launch_bounds__(512) gemm_p3c12_kernel(const conv::P3ConvFwd<G
     const int wm = wave >> 1, wn = wave & 1;
     const int lr = wm * 32 + (lane & 31);
     const typename I2::Lane ln = I2::lane(0, lr, lr < I2::OPIX);
-    f32x16 acc[1][1];
-#pragma unroll
-    for (int e = 0; e < 16; ++e) acc[0][0][e] = 0.f;
+    typename Cfg::C2::Acc acc;
+    acc.zero();
     auto compute = [&](int k0, int buf) {
       const uint8_t* sb = smem + buf * PB2::BYTES;
       const typename I2::Stage sg = I2::stage(ln, k0);
@@ -259,7 +254,7 @@ __global__ void __launch_bounds__(512) gemm_p3c12_kernel(const conv::P3ConvFwd<G
         f16x8 fa[NP];
 #pragma unroll
         for (int pl = 0; pl < NP; ++pl) fa[pl] = *reinterpret_cast<const f16x8*>(a + pl * Cfg::PLANE2);
-        p3_terms<NP, NP>(fa, fb, acc[0][0]);
+        acc.terms(0, 0, fa, fb);
       }
     };
     auto iter = [&](auto S, int kt) {
@@ -277,8 +272,7 @@ __global__ void __launch_bounds__(512) gemm_p3c12_kernel(const conv::P3ConvFwd<G
     }
     P2 q = p2;
     q.M = (f + 1) * I2::OPIX < p2.M ? (f + 1) * I2::OPIX : p2.M;
-    f32x16 cs[1];
-    Cfg::C2::epilogue(q, smem, f * I2::OPIX, 0, wave, wm, wn, lane, 0, acc, cs, false);
+    Cfg::C2::epilogue(q, smem, f * I2::OPIX, 0, wave, wm, wn, lane, 0, acc, false);
   }
 }
 

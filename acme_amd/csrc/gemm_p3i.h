@@ -130,11 +130,6 @@ struct ImgGeomPairs {
   }
 };
 
-#ifndef P3I_SCHED
-#define P3I_SCHED 1  // fenced issue order in the image-resident kernels' k loop (round 5: step
-                     // 0.4969 -> 0.4949 ms, three alternating 300-step runs)
-#endif
-
 
 template <class GI, int FPB, int BN, int WM, int WN, int MT, class P>
 struct P3ICfg {
@@ -305,13 +300,8 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
   if constexpr (HasStamps<P>::value)
     if (stamp) st_t1 = __builtin_amdgcn_s_memtime();
 
-  f32x16 acc[MT][NTL];
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int j = 0; j < NTL; ++j)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
+  typename C::Acc acc;
+  acc.zero();
   // The epilogue's constants, loaded now (their latency hides under the k loop).
   typename EpiPre<P>::type pre{};
   if constexpr (EpiPre<P>::has) pre = p.pre(wn * TN + C::epi_col(lane));
@@ -321,54 +311,32 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
     typename GI::Stage sg[MT];
 #pragma unroll
     for (int i = 0; i < MT; ++i) sg[i] = GI::stage(ln[i], k0);
-    if constexpr (P3I_SCHED) {
-      // Every fragment of the stage read first, then the MFMAs (fenced): one LDS latency per
-      // stage instead of one per k16 step (the scheduler otherwise sinks each read to its
-      // first use).
-      f16x8 fb[KS][NTL][NPB], fa[KS][MT][NPA];
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-#pragma unroll
-        for (int j = 0; j < NTL; ++j)
-#pragma unroll
-          for (int pl = 0; pl < NPB; ++pl) fb[s][j][pl] = PB::frag(sb, pl, wn * TN + j * 32, s, lane);
-#pragma unroll
-        for (int i = 0; i < MT; ++i) {
-          const int u = GI::unit(sg[i], ln[i], k0, s, lane >> 5);
-          const int a = u >= 0 ? u : PLANE - 16;
-#pragma unroll
-          for (int pl = 0; pl < NPA; ++pl)
-            fa[s][i][pl] = *reinterpret_cast<const f16x8*>(smem + pl * PLANE + a);
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int s = 0; s < KS; ++s)
-#pragma unroll
-        for (int i = 0; i < MT; ++i)
-#pragma unroll
-          for (int j = 0; j < NTL; ++j) p3_terms<NPA, NPB>(fa[s][i], fb[s][j], acc[i][j]);
-      return;
-    }
+    // Every fragment of the stage read first, then the MFMAs (fenced): one LDS latency per
+    // stage instead of one per k16 step (the scheduler otherwise sinks each read to its first
+    // use; round 5: step 0.4969 -> 0.4949 ms with the fences here and in iter below).
+    f16x8 fb[KS][NTL][NPB], fa[KS][MT][NPA];
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      f16x8 fb[NTL][NPB];
 #pragma unroll
       for (int j = 0; j < NTL; ++j)
 #pragma unroll
-        for (int pl = 0; pl < NPB; ++pl) fb[j][pl] = PB::frag(sb, pl, wn * TN + j * 32, s, lane);
+        for (int pl = 0; pl < NPB; ++pl) fb[s][j][pl] = PB::frag(sb, pl, wn * TN + j * 32, s, lane);
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
         const int u = GI::unit(sg[i], ln[i], k0, s, lane >> 5);
         const int a = u >= 0 ? u : PLANE - 16;
-        f16x8 fa[NPA];
 #pragma unroll
         for (int pl = 0; pl < NPA; ++pl)
-          fa[pl] = *reinterpret_cast<const f16x8*>(smem + pl * PLANE + a);
-#pragma unroll
-        for (int j = 0; j < NTL; ++j) p3_terms<NPA, NPB>(fa, fb[j], acc[i][j]);
+          fa[s][i][pl] = *reinterpret_cast<const f16x8*>(smem + pl * PLANE + a);
       }
     }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NTL; ++j) acc.terms(i, j, fa[s][i], fb[s][j]);
   };
 
   // Iteration kt: LDS buffer kt & 1 holds B of stage kt, register set (kt + 1) % RS holds
@@ -382,7 +350,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
     // The weight loads issue before the MFMAs (fenced), so they have the whole iteration
     // to land before the next iteration stores them (round 5: the scheduler had sunk them
     // to just before the barrier, and the next store waited out their latency).
-    if constexpr (P3I_SCHED) __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_sched_barrier(0);
     compute(kt * BK, kt & 1);
     __syncthreads();
   };
@@ -393,10 +361,9 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_p3i_kernel(const P p_in, in
   }
   if (kt < nk) iter(S0{}, kt);
 
-  f32x16 cs[C::NCS];
   if constexpr (HasStamps<P>::value)
     if (stamp) st_t2 = __builtin_amdgcn_s_memtime();
-  C::epilogue(p, smem, m0, 0, wave, wm, wn, lane, 0, acc, cs, false, &pre);
+  C::epilogue(p, smem, m0, 0, wave, wm, wn, lane, 0, acc, false, &pre);
   if constexpr (HasStamps<P>::value) {
     if (stamp) {
       uint64_t* o = p_in.stamps + 8 * (int64_t)blockIdx.x;

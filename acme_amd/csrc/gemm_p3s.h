@@ -141,11 +141,8 @@ __global__ void __launch_bounds__(64 * 2 * G::S * G::S * FPB) gemm_p3s_kernel(
   }
   __syncthreads();
 
-  f32x16 acc[MT][1];
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) acc[i][0][e] = 0.f;
+  typename C::Acc acc;
+  acc.zero();
 
   auto compute = [&](int k0, int buf) {
     const uint8_t* sb = smem + Cfg::IMG + buf * Cfg::STAGE_B + z * PB::BYTES;
@@ -174,7 +171,7 @@ __global__ void __launch_bounds__(64 * 2 * G::S * G::S * FPB) gemm_p3s_kernel(
 #pragma unroll
         for (int pl = 0; pl < NP; ++pl)
           fa[pl] = *reinterpret_cast<const f16x8*>(a + pl * PLANE);
-        p3_terms<NP, NP>(fa, fb, acc[i][0]);
+        acc.terms(i, 0, fa, fb);
       }
     }
   };
@@ -191,9 +188,8 @@ __global__ void __launch_bounds__(64 * 2 * G::S * G::S * FPB) gemm_p3s_kernel(
     iter(S1{}, kt + 1);
   }
 
-  f32x16 cs[C::NCS];
   // Row m = m0 + half * 64 + i * 32 + r of class z; LDS staging region of this wave.
-  C::epilogue(pz, smem, m0, 0, wave, half, 0, lane, 0, acc, cs, false);
+  C::epilogue(pz, smem, m0, 0, wave, half, 0, lane, 0, acc, false);
 }
 
 template <class G, int FPB = 1>

@@ -30,10 +30,6 @@
 
 #include "gemm.h"
 
-#ifndef ACME_X6_EXPERIMENT
-#define ACME_X6_EXPERIMENT 0
-#endif
-
 namespace acme {
 namespace gemm {
 
@@ -50,11 +46,6 @@ __device__ __forceinline__ int x6_swz(int row) {
 }
 
 __device__ __forceinline__ void split3(const f32x4 x, bf16x4& h, bf16x4& m, bf16x4& l) {
-#if ACME_X6_EXPERIMENT == 1
-  for (int j = 0; j < 4; ++j) h[j] = (__bf16)x[j];
-  m = h; l = h;
-  return;
-#endif
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const __bf16 hj = (__bf16)x[j];
@@ -150,11 +141,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_x6_kernel(const P p_in) {
       const int k = k0 + PA::kk_of(u);
 #pragma unroll
       for (int v = 0; v < PA::VECS; ++v)
-#if ACME_X6_EXPERIMENT == 2
-        ra[i][v] = f32x4{(float)k, 1.f, 2.f, 3.f};
-#else
         ra[i][v] = (PA::owns(u) && k + v < kend) ? p.a_load(arow[i], k + v) : zero4();
-#endif
     }
 #pragma unroll
     for (int i = 0; i < PB::PER_THREAD; ++i) {
@@ -162,11 +149,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_x6_kernel(const P p_in) {
       const int k = k0 + PB::kk_of(u);
 #pragma unroll
       for (int v = 0; v < PB::VECS; ++v)
-#if ACME_X6_EXPERIMENT == 2
-        rb[i][v] = f32x4{(float)k, 1.f, 2.f, 3.f};
-#else
         rb[i][v] = (PB::owns(u) && k + v < kend) ? p.b_load(brow[i], k + v) : zero4();
-#endif
     }
   };
   // KCONTIG vectors already hold 4 k of one row; RCONTIG 4x4 blocks are transposed so

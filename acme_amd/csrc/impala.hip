@@ -396,17 +396,13 @@ __global__ void __launch_bounds__(256) impala_loss_grad_kernel(const LossArgs a)
   } while (0)
 
 // The small f32 layers after the LSTM (a few hundred rows): the register-operand engine
-// (gemm_direct.h: each lane's k run in one burst, 8 waves per 32 x 32 tile); -DIM_DIRECT=0:
-// the staged f32 engine (the A/B).
-#ifndef IM_DIRECT
-#define IM_DIRECT 1
-#endif
+// (gemm_direct.h: each lane's k run in one burst, 8 waves per 32 x 32 tile; round 5: faster
+// than the staged f32 engine, profiles/r05/ab/impala_direct_small_layers.log).
 #define IM_DGEMM(name, prob)                                                                   \
   do {                                                                                         \
     ACME_PROF_PEAK(name, st, 2.0 * (double)(prob).M * (double)(prob).N * (double)(prob).K, 0.0,  \
                    157.3);                                                                     \
-    hipError_t _e = IM_DIRECT ? gemm::launch_direct(prob, 1, (prob).K, st)                     \
-                              : gemm::launch_matmul<32, 32, 1, 1, 16, 8>(prob, 1, st);          \
+    hipError_t _e = gemm::launch_direct(prob, 1, (prob).K, st);                                \
     if (_e != hipSuccess) {                                                                    \
       set_error("gemm launch failed: %s (%s:%d)", hipGetErrorString(_e), __FILE__, __LINE__);  \
       return ACME_ERR_HIP;                                                                     \

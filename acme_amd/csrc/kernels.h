@@ -32,7 +32,8 @@ struct StepGuard {
   int64_t skipped;   // steps skipped
   uint32_t vseq;     // the last verdict: (seq << 1) | skip, one agent-scope store (the data
                      // is its own flag: readers in the same launch spin on it)
-  uint32_t pad;
+  uint32_t vtimeout; // priority write-backs that timed out waiting for vseq (and so wrote
+                     // nothing): acme_dqn_verdict_timeouts; DQNLearner raises on one
 };
 // What a gated kernel reads: skip = on | t[par] | (dp && *dp > 0), or `last` (use_last).
 struct Gate {

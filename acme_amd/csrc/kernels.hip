@@ -320,14 +320,8 @@ __global__ void __launch_bounds__(256) slab_reduce4_kernel(const float* __restri
 // (acme/tf/networks/duelling.py:51-57).  4 rows per 256-thread block: the advantage
 // weights are staged once per block in LDS, each wave finishes one row with lane-parallel
 // partial dot products and a fixed shuffle tree (deterministic).
-#ifndef ACME_HEAD_ROWS
-#define ACME_HEAD_ROWS 4
-#endif
-constexpr int kHeadRows = ACME_HEAD_ROWS;
+constexpr int kHeadRows = 4;
 constexpr int kHeadChunk = 8;  // advantage outputs per accumulation pass
-#ifndef HEAD_EXP
-#define HEAD_EXP 0  // experiments: 1 skip the dot products, 2 skip the slab sum
-#endif
 template <int SPL, int HC>
 __global__ void __launch_bounds__(256) fc_head_forward_kernel(
     const float* __restrict__ slab, int splits, int rows, int H_, const float* __restrict__ fcb,
@@ -359,9 +353,7 @@ __global__ void __launch_bounds__(256) fc_head_forward_kernel(
     if (row >= rows) continue;
     const int64_t e = (int64_t)row * n4 + c4;
     f32x4 v;
-    if constexpr (HEAD_EXP == 2) {
-      v = s4[e];
-    } else if constexpr (SPL > 0) {
+    if constexpr (SPL > 0) {
       f32x4 part[SPL];
 #pragma unroll
       for (int sp = 0; sp < SPL; ++sp) part[sp] = s4[(size_t)sp * count4 + e];
@@ -391,7 +383,6 @@ __global__ void __launch_bounds__(256) fc_head_forward_kernel(
   if (threadIdx.x == 0) zero[0] = 0.f;
   __syncthreads();
   for (int rr = wave; rr < kHeadRows; rr += 4) {
-    if constexpr (HEAD_EXP == 1) break;
     const float* h = sh + rr * 2 * H;
     for (int o0 = 0; o0 <= A; o0 += kHeadChunk) {
       // Per-output weight column (uniform): advantage o -> wa[:, o] (stride A) over
@@ -1695,6 +1686,49 @@ int acme_dense_forward(const float* x, int64_t rows, int64_t in, const float* w,
   p.x = x; p.x2 = x; p.split_b = (int)rows; p.ldx = (int)in;
   p.w = w; p.bias = b; p.y = y; p.act = act; p.slab = nullptr;
   hipError_t e = acme::gemm::launch_matmul<128, 128, 2, 2>(p, 1, acme::as_stream(stream));
+  if (e != hipSuccess) {
+    acme::set_error("dense launch failed: %s", hipGetErrorString(e));
+    return ACME_ERR_HIP;
+  }
+  return ACME_OK;
+}
+
+extern "C++" {
+namespace {
+template <int BK, int WK>
+hipError_t dense_staged(const acme::conv::DenseFwd<true>& p, int multi, hipStream_t st) {
+  if (!multi) return acme::gemm::launch_gemm<32, 32, 1, 1, BK, WK>(p, 1, st);
+  using Q = acme::conv::DenseFwd<true>;
+  acme::gemm::ZMulti<acme::gemm::ZSet<Q, 1>> m;
+  const Q one[1] = {p};
+  m.s = acme::gemm::make_zset(one);
+  m.n = 1;
+  const int tiles = ((p.N + 31) / 32) * ((p.M + 31) / 32);
+  return acme::gemm::launch_gemm_multi<32, 32, 1, 1, BK, WK>(m, tiles, 1, st);
+}
+}  // namespace
+}  // extern "C++"
+
+int acme_dense_forward_staged(const float* x, int64_t rows, int64_t in, const float* w,
+                              const float* b, int64_t out, int32_t act, float* y, int32_t bk,
+                              int32_t wk, int32_t multi, void* stream) {
+  ACME_CHECK_ARG(x && w && b && y, "null buffer");
+  ACME_CHECK_ARG(rows >= 1 && rows < (1 << 30) && in >= 4 && in % 4 == 0 && out >= 4 &&
+                     out % 4 == 0 && in < (1 << 30) && out < (1 << 30),
+                 "bad dense shape [%lld x %lld] -> %lld", (long long)rows, (long long)in,
+                 (long long)out);
+  ACME_CHECK_ARG(act >= 0 && act <= 3, "unknown activation %d", act);
+  acme::conv::DenseFwd<true> p;
+  p.M = (int)rows; p.N = (int)out; p.K = (int)in; p.k_chunk = (int)in;
+  p.x = x; p.x2 = x; p.split_b = (int)rows; p.ldx = (int)in;
+  p.w = w; p.bias = b; p.y = y; p.act = act; p.slab = nullptr;
+  const hipStream_t st = acme::as_stream(stream);
+  hipError_t e;
+  if (bk == 16 && wk == 8) e = dense_staged<16, 8>(p, multi, st);
+  else if (bk == 32 && wk == 4) e = dense_staged<32, 4>(p, multi, st);
+  else if (bk == 32 && wk == 8) e = dense_staged<32, 8>(p, multi, st);
+  else if (bk == 16 && wk == 16) e = dense_staged<16, 16>(p, multi, st);
+  else return (acme::set_error("unsupported (BK %d, WK %d)", bk, wk), ACME_ERR_INVALID);
   if (e != hipSuccess) {
     acme::set_error("dense launch failed: %s", hipGetErrorString(e));
     return ACME_ERR_HIP;

@@ -665,9 +665,10 @@ struct FusedUpdateArgs {
   uint64_t* stamps = nullptr;
 };
 // Waits (bounded) for the verdict with sequence number seq; true when that step is skipped
-// (or the wait timed out: no priority is written).  Workgroup 0 of the same launch publishes
-// it and was dispatched first, so it is resident or done.
-__device__ __forceinline__ bool wait_verdict_skip(const StepGuard* g, uint32_t seq) {
+// (or the wait timed out: no priority is written, and the timeout is counted in
+// g->vtimeout, which the host reads: acme_dqn_verdict_timeouts).  Workgroup 0 of the same
+// launch publishes it and was dispatched first, so it is resident or done.
+__device__ __forceinline__ bool wait_verdict_skip(StepGuard* g, uint32_t seq) {
   __shared__ uint32_t s_v;
   if (threadIdx.x == 0) {
     uint32_t v = 0;
@@ -676,7 +677,9 @@ __device__ __forceinline__ bool wait_verdict_skip(const StepGuard* g, uint32_t s
       if ((v >> 1) == (seq & 0x7fffffffu)) break;
       __builtin_amdgcn_s_sleep(2);
     }
-    s_v = (v >> 1) == (seq & 0x7fffffffu) ? (v & 1u) : 1u;
+    const bool got = (v >> 1) == (seq & 0x7fffffffu);
+    if (!got) atomicAdd(&g->vtimeout, 1u);
+    s_v = got ? (v & 1u) : 1u;
   }
   __syncthreads();
   return s_v != 0u;
@@ -805,11 +808,22 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
       for (int f = 0; f < len; ++f)
         if (s_slot[f] == slot && s_j[f] > j) win = false;
       winv[i] = win;
-      if (!win) continue;
-      leafv[i] = det_pow_priority(pv[i], a.alpha);
-      if (pre)
+      if (win) leafv[i] = det_pow_priority(pv[i], a.alpha);
+    }
+    // The children rows above are filled by wave (q % nw), the substitutions below by the
+    // winning update's thread (any wave): the barrier orders every row's fill before them
+    // (without it a late fill could overwrite a substituted leaf).
+    __syncthreads();
+    if (pre) {
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const int e = tid + i * nt;
+        if (e >= len) break;
+        if (!winv[i]) continue;
+        const int64_t slot = s_slot[e];
         for (int q = 0; q < np; ++q)
           if (s_lvl[q] == 1 && s_node[q] == (slot >> 6)) s_ch[q][slot & 63] = leafv[i];
+      }
     }
     __syncthreads();
     if (pre) {
@@ -868,15 +882,18 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
   }
   stamp(6);
   if (a.nlevels < 2 || a.top_computed) return;  // readers compute the top (TreeView)
-  // Count this workgroup finished once its write-through stores have left (drained), then
-  // the last one rescans the top level from them.
-  __builtin_amdgcn_s_waitcnt(0);
+  // Count this workgroup finished once its level-h stores are released at agent scope (every
+  // thread's own release fence, then the workgroup barrier, then a release increment), and
+  // the last one acquires them (the increment's acquire side and an agent-scope acquire fence
+  // in every thread) before it rescans the top level (a waitcnt is no fence).
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   __syncthreads();
   if (tid == 0)
-    s_last = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+    s_last = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
              (uint32_t)(G - 1);
   __syncthreads();
   if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   const int top = a.nlevels - 1;
   for (int64_t node = wave; node < a.top_nodes; node += nw) {
     const double c = __hip_atomic_load(a.level[top - 1] + node * 64 + lane, __ATOMIC_RELAXED,

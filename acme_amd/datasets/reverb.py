@@ -185,6 +185,11 @@ class _Unbatched:
 
 
 class _TableIterator:
+    # The batches handed out by the last two next() calls stay intact until the following
+    # next() (the buffer ring holds 2, or P + 2 with prefetch): DQNLearner re-issues a skipped
+    # step from them without copying (acme_amd/agents/dqn/learning.py).
+    holds_last_batches = 2
+
     def __init__(self, table: replay.Table, batch: int, timeout: float, prefetch: int = 0,
                  shard=None):
         self._t = table

@@ -442,11 +442,14 @@ class NativeDQN:
         return int(lib().acme_dqn_skipped_steps(self._h))
 
     def guard_state(self) -> Dict[str, int]:
-        """{applied, skipped, last_skipped, q_values_overflowed} (synchronises the device)."""
+        """{applied, skipped, last_skipped, q_values_overflowed, verdict_timeouts} (synchronises
+        the device)."""
         a = (ctypes.c_int64 * 4)()
         check(lib().acme_dqn_guard_state(self._h, a), "dqn guard_state")
+        t = ctypes.c_int64()
+        check(lib().acme_dqn_verdict_timeouts(self._h, ctypes.byref(t)), "dqn verdict_timeouts")
         return dict(applied=int(a[0]), skipped=int(a[1]), last_skipped=int(a[2]),
-                    q_values_overflowed=int(a[3]))
+                    q_values_overflowed=int(a[3]), verdict_timeouts=int(t.value))
 
     @property
     def applied_steps(self) -> int:

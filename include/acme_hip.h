@@ -81,6 +81,13 @@ int32_t acme_matmul_engine(void);
  * (act: 0 none, 1 relu, 2 elu, 3 tanh); in and out multiples of 4.  Device pointers. */
 int acme_dense_forward(const float* x, int64_t rows, int64_t in, const float* w, const float* b,
                        int64_t out, int32_t act, float* y, void* stream);
+/* The same layer on the staged f32 engine (csrc/gemm.h, 32 x 32 tiles of one wave per k-group)
+ * at stage depth bk and wk k-groups, (bk, wk) in {(16, 8), (32, 4), (32, 8), (16, 16)};
+ * multi != 0 runs it through the multi-problem kernel the D4PG backward launches use
+ * (gemm_f32_multi_kernel).  Tests of the engine's configurations. */
+int acme_dense_forward_staged(const float* x, int64_t rows, int64_t in, const float* w,
+                              const float* b, int64_t out, int32_t act, float* y, int32_t bk,
+                              int32_t wk, int32_t multi, void* stream);
 
 /* ------------------------------------------------------------------ replay -- */
 
@@ -365,6 +372,10 @@ int acme_dqn_set_data_parallel_gate(acme_dqn* l, int32_t enable);
  * (acme_dqn_params_changed), so the caller can re-issue the held batches in order; a target
  * copy due on a skipped step is not made (the re-issued step makes it). */
 int acme_dqn_set_reissue(acme_dqn* l, int32_t enable);
+/* Priority write-backs inside the step (acme_dqn_step_update) that gave up waiting for the
+ * step's verdict (a bounded spin) and so wrote no priority although the step may have been
+ * applied; synchronises.  Never expected; DQNLearner raises RuntimeError when it is non-zero. */
+int acme_dqn_verdict_timeouts(acme_dqn* l, int64_t* out);
 int64_t acme_dqn_verdicts_issued(const acme_dqn* l);
 int acme_dqn_step_verdict(const acme_dqn* l, int64_t seq, int32_t* state);
 /* The plane scales (powers of two) as learner state for checkpoints: acme_dqn_scale_state

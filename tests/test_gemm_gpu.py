@@ -63,3 +63,29 @@ def test_dense_activation_epilogues():
     for act, ref in ((1, np.maximum(z, 0)), (2, np.where(z < 0, np.expm1(z), z)), (3, np.tanh(z))):
         y = _dense(_lib.lib().acme_matmul_engine(), t(x), t(w), t(b), act)
         np.testing.assert_allclose(y, ref, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("bk,wk", [(16, 8), (32, 4), (32, 8), (16, 16)])
+@pytest.mark.parametrize("multi", [0, 1])
+def test_staged_engine_configurations(bk, wk, multi):
+    """The staged f32 engine at every (BK, WK) the D4PG / IMPALA layers were tried with, alone
+    and through the multi-problem kernel (round 5 recorded a fault at BK 32 / 4 k-groups: the
+    multi launch's block size was hard-coded for 8 k-groups; csrc/gemm.h now derives it from
+    the kernel's parameters).  Shapes of the D4PG critic (rows 512, 30 -> 512; 512 -> 512;
+    512 -> 256 and the ragged 256 -> 52): within the f32 engine's error of float64."""
+    from acme_amd import _lib
+    L = _lib.lib()
+    rng = np.random.default_rng(bk * 100 + wk)
+    t = lambda a: torch.as_tensor(a).cuda()  # noqa: E731
+    for M, K, N in ((512, 32, 512), (512, 512, 512), (512, 512, 256), (256, 256, 52)):
+        x = rng.standard_normal((M, K)).astype(np.float32)
+        w = (rng.standard_normal((K, N)) / np.sqrt(K)).astype(np.float32)
+        b = (0.1 * rng.standard_normal(N)).astype(np.float32)
+        exact = np.tanh(x.astype(np.float64) @ w.astype(np.float64) + b)
+        y = torch.empty(M, N, dtype=torch.float32, device="cuda")
+        xd, wd, bd = t(x), t(w), t(b)
+        _lib.check(L.acme_dense_forward_staged(xd.data_ptr(), M, K, wd.data_ptr(), bd.data_ptr(),
+                                               N, 3, y.data_ptr(), bk, wk, multi,
+                                               _lib.stream_ptr()))
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(y.cpu().numpy(), exact, rtol=0, atol=2e-6)

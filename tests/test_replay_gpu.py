@@ -170,6 +170,36 @@ def test_priority_updates_deep_tree(n_upd):
         _cmp_sample(r, o, 512, 200 + it)
 
 
+def test_priority_updates_many_per_workgroup():
+    """ADVICE r5 (the LDS race of the one-launch update): 4096 updates on a 1M-slot table give
+    each of the 256 update workgroups ~16 updates under distinct level-1 nodes, so the rows of
+    children a workgroup prefetches are filled by other waves than the threads substituting
+    the new leaves.  Every iteration: the leaves, the sampling mass (recomputed from the
+    stored level sums: a level-1 node missing its update changes it) and 512 draws bit-exact
+    against the oracle."""
+    import ctypes
+    from acme_amd._lib import lib
+    rng = np.random.default_rng(77)
+    cap = 1_000_000
+    r = _native(cap, [4], True)
+    o = OracleTable(cap, True, 0.6, 1234)
+    pr = rng.uniform(0.1, 2.0, cap)
+    r.insert([np.zeros((cap, 1), np.int32)], pr)
+    o.insert(pr)
+    out = torch.zeros(1, dtype=torch.float64, device="cuda")
+    for it in range(6):
+        keys = rng.choice(cap, 4096, replace=False).astype(np.uint64)
+        newp = rng.uniform(0.0, 3.0, 4096)
+        r.update_priorities(torch.as_tensor(keys.view(np.int64)).cuda().view(torch.uint64),
+                            torch.as_tensor(newp).cuda())
+        o.update(keys, newp)
+        assert lib().acme_replay_total(r._h, ctypes.c_void_p(out.data_ptr()), None) == 0
+        torch.cuda.synchronize()
+        assert out.item() == o.total(), (it, out.item(), o.total())
+        np.testing.assert_array_equal(r.debug_state()["leaves"], o.leaves()[:cap])
+        _cmp_sample(r, o, 512, 400 + it)
+
+
 @pytest.mark.parametrize("capacity", [1024, 1088, 65536, 69632])
 def test_top_level_computed_and_stored(capacity):
     """The top level's entries with children are computed by the readers when there are at

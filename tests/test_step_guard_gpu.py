@@ -223,14 +223,44 @@ def test_skipped_step_makes_no_target_copy():
 
 
 class _FixedBatches:
-    """A dataset of fixed device batches, each ReplaySample handed out once."""
+    """A dataset of fixed device batches, each ReplaySample handed out once (each in its own
+    tensors, so every batch stays intact)."""
+    holds_last_batches = 1 << 30
 
     def __init__(self, samples):
         self.samples = list(samples)
         self.batch_size = int(samples[0].data[1].shape[0])
 
     def __iter__(self):
-        return iter(self.samples)
+        return self
+
+    def __next__(self):
+        return self.samples.pop(0)
+
+
+class _ReusingBatches:
+    """A dataset that writes every batch into the same device buffers (a foreign iterator
+    without the repo iterators' buffer ring): the learner must hold its own copies."""
+
+    def __init__(self, samples):
+        self.samples = list(samples)
+        self.batch_size = int(samples[0].data[1].shape[0])
+        self.buf = None
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        from acme_amd import replay
+        s = self.samples.pop(0)
+        flat = list(s.data) + [s.info.key, s.info.probability]
+        if self.buf is None:
+            self.buf = [torch.empty_like(x) for x in flat]
+        for dst, src in zip(self.buf, flat):
+            dst.copy_(src)
+        info = replay.SampleInfo(key=self.buf[5], probability=self.buf[6],
+                                 table_size=s.info.table_size, priority=s.info.priority)
+        return replay.ReplaySample(info=info, data=tuple(self.buf[:5]))
 
 
 def _sample(b, first_key):
@@ -246,13 +276,16 @@ def _sample(b, first_key):
     return replay.ReplaySample(info=info, data=tuple(dev[:5]))
 
 
-def test_learner_reissues_skipped_step():
+@pytest.mark.parametrize("dataset", ["fixed", "reusing"])
+def test_learner_reissues_skipped_step(dataset):
     """DQNLearner.step() applies every step, as the reference (agents/tf/dqn/learning.py:
     147-161): a step the guard skips (here the forced ~2^13-fold head-dZ jump) holds the
     steps after it skipped too, and the learner re-issues them in order at the next step()
     (or when its state is read), with their step counters, so the due target copy lands.
     Checked bit for bit against a learner that recalibrated before the large batch (so it
-    never skips), both writing their priorities back into their own tables."""
+    never skips), both writing their priorities back into their own tables.  With a dataset
+    that reuses one set of buffers ("reusing") the learner holds copies of the
+    batches it may re-issue."""
     from acme_amd import replay, specs
     from acme_amd.adders import reverb as adders
     from acme_amd.agents.dqn import DQNLearner
@@ -274,7 +307,9 @@ def test_learner_reissues_skipped_step():
                              signature=adders.NStepTransitionAdder.signature(spec), seed=3)
         table.native.fill_synthetic(1000, layout=0, num_actions=A, seed=0)
         server = replay.Server([table])
-        ds = _FixedBatches([_sample(b, 64 * i) for i, b in enumerate(batches)])
+        kind = _ReusingBatches if recalibrate_before is None and dataset == "reusing" \
+            else _FixedBatches
+        ds = kind([_sample(b, 64 * i) for i, b in enumerate(batches)])
         lr = DQNLearner(net, net, discount=0.99, importance_sampling_exponent=0.2,
                         learning_rate=1e-3, target_update_period=2, dataset=ds,
                         replay_client=replay.Client(server), logger=loggers.NoOpLogger(),
@@ -295,6 +330,7 @@ def test_learner_reissues_skipped_step():
     # The large batch was skipped, with the batch issued after it held; both re-issued.
     assert g_got["skipped"] == 2 and g_got["applied"] == len(batches), g_got
     assert got._reissued == 2  # noqa: SLF001
+    assert got._copy_held == (dataset == "reusing")  # noqa: SLF001
     assert s_got["num_steps"] == s_ref["num_steps"] == len(batches)
     assert s_got["optimizer"]["step"] == s_ref["optimizer"]["step"] == len(batches)
     for part in ("network", "target_network"):
@@ -328,26 +364,25 @@ def _teacher_forced(d, params, target, b, B):
     _check_grads(d.get_params("grads"), grads)
 
 
-@pytest.mark.parametrize("B,steps,checks,drift_f,loss_max,loss_med",
-                         [(64, 100, (0, 33, 66, 99), 3.0, 1.0, 0.1),
-                          (512, 20, (0, 19), 2.0, None, None)])
-def test_long_horizon_drift(B, steps, checks, drift_f, loss_max, loss_med):
+@pytest.mark.parametrize("B,steps,checks", [(64, 100, (0, 33, 66, 99)), (256, 50, (0, 49)),
+                                             (512, 20, (0, 19))])
+def test_long_horizon_drift(B, steps, checks):
     """Free-running trajectories (each side applies its own gradients) of the plane engine
     and the exact-f32 engine from identical batches, against the float64 torch restatement
-    (oracle/dqn_torch.py on the GPU, the reference trajectory).  Asserted: the plane engine
-    skips no step; its first two losses match float64 at the north star's 1e-5; its
+    (oracle/dqn_torch.py on the GPU, the reference trajectory), at the reference DQN agent's
+    default batch (256, agents/tf/dqn/agent.py:49), a small one and the headline one.
+    Asserted: the plane engine skips no step; the first loss matches
+    float64 at the north star's 1e-5 on both engines; the second (after one free-running
+    Adam step: at t = 1 the update is lr * sign(g), so a gradient element near zero flips on
+    any f32-accurate engine) within 1e-5 or 2x the f32 engine's error; the plane engine's
     parameter drift from the float64 trajectory (relative to how far training moved the
-    parameters) is within drift_f x the f32 engine's; its loss trajectory (relative error
-    per step): at the headline batch (B = 512 x 20) maximum and median within 2x the f32
-    engine's, at B = 64 x 100 maximum <= loss_max and median <= loss_med.  (Measured, round
-    5, profiles/r05/drift/: B = 512: drift 0.060 against 0.063, loss max 0.251 / 0.250,
-    median 0.0081 / 0.0079; B = 64: drift 0.152 against 0.065 and loss max / median 0.749 /
-    0.064 against 0.062 / 0.0035 -- at small batches the plane engine leaves the float64
-    trajectory faster than the exact-f32 engine, from its first step's conv weight gradients
-    (7x the f32 engine's error).)  At the `checks` steps the plane engine's
-    step is also checked teacher-forced against the f64 oracle from its own pre-step state
-    (loss and TD at 1e-5, the suite's gradient bar), so per-step accuracy does not degrade as
-    the scales follow training."""
+    parameters), and the maximum and median of its loss trajectory's relative error, each
+    within 2x the exact-f32 engine's.  (Round 5's engine, one accumulator per tile, failed this
+    at B = 64: loss error max 12x and median 18x the f32 engine's, from conv weight gradients
+    with 2.5-7x its error -- the f16 MFMA's biased accumulation, csrc/gemm_p3.h P3Acc.)  At the
+    `checks` steps the plane engine's step is also checked teacher-forced against the f64
+    oracle from its own pre-step state (loss and TD at 1e-5, the suite's gradient bar), so
+    per-step accuracy does not degrade as the scales follow training."""
     from acme_amd._lib import lib
     from acme_amd.native import NativeDQN
     from acme_amd.networks import DQNAtariNetwork
@@ -394,22 +429,22 @@ def test_long_horizon_drift(B, steps, checks, drift_f, loss_max, loss_med):
     f32_loss, f32_p, f32_g = run(0)
     assert plane_g["skipped"] == 0 and plane_g["applied"] == steps, plane_g
     assert f32_g["skipped"] == 0 and f32_g["applied"] == steps, f32_g
-    # The first steps match the f64 trajectory at the north star's 1e-5.
-    np.testing.assert_allclose(plane_loss[:2], ref_loss[:2], rtol=1e-5)
-    np.testing.assert_allclose(f32_loss[:2], ref_loss[:2], rtol=1e-5)
     d_plane, d_f32 = _rel(plane_p, ref_p, p0), _rel(f32_p, ref_p, p0)
     e_plane = np.abs(plane_loss - ref_loss) / np.abs(ref_loss)
     e_f32 = np.abs(f32_loss - ref_loss) / np.abs(ref_loss)
     print(f"B={B} steps={steps}: parameter drift plane {d_plane:.3e} f32 {d_f32:.3e}; loss rel "
           f"err max / median plane {e_plane.max():.3e} / {np.median(e_plane):.3e} f32 "
-          f"{e_f32.max():.3e} / {np.median(e_f32):.3e}")
-    assert d_plane <= drift_f * d_f32 + 1e-5, (d_plane, d_f32)
-    if loss_max is None:  # the headline batch: within 2x the f32 engine's loss trajectory
-        assert e_plane.max() <= 2.0 * e_f32.max() + 1e-5, (e_plane.max(), e_f32.max())
-        assert np.median(e_plane) <= 2.0 * np.median(e_f32) + 1e-6
-    else:
-        assert e_plane.max() <= loss_max and np.median(e_plane) <= loss_med, (
-            e_plane.max(), np.median(e_plane))
+          f"{e_f32.max():.3e} / {np.median(e_f32):.3e}; first two steps plane "
+          f"{e_plane[0]:.2e} {e_plane[1]:.2e} f32 {e_f32[0]:.2e} {e_f32[1]:.2e}")
+    # The first step matches the f64 trajectory at the north star's 1e-5; the second within
+    # 1e-5 or 2x the f32 engine's error.
+    np.testing.assert_allclose(plane_loss[:1], ref_loss[:1], rtol=1e-5)
+    np.testing.assert_allclose(f32_loss[:1], ref_loss[:1], rtol=1e-5)
+    assert e_plane[1] <= max(1e-5, 2.0 * e_f32[1]), (e_plane[1], e_f32[1])
+    assert d_plane <= 2.0 * d_f32 + 1e-5, (d_plane, d_f32)
+    assert e_plane.max() <= 2.0 * e_f32.max() + 1e-5, (e_plane.max(), e_f32.max())
+    assert np.median(e_plane) <= 2.0 * np.median(e_f32) + 1e-6, (np.median(e_plane),
+                                                                 np.median(e_f32))
 
 
 def test_impala_timeout_skips_update():

@@ -38,7 +38,7 @@ def ref_grads(params, target, b, A=18):
     w = torch.from_numpy((iw / iw.max()).astype(np.float32)).cuda().double()
     loss = (w * huber(td)).mean()
     g = torch.autograd.grad(loss, [t.p[k] for k in t.names])
-    return {k: v.cpu().numpy() for k, v in zip(t.names, g)}, float(loss)
+    return {k: v.cpu().numpy() for k, v in zip(t.names, g)}, float(loss.detach())
 
 
 def ref_tensors(params, target, b, A=18):
@@ -145,12 +145,12 @@ def main():
                               f"{np.linalg.norm(mine - wg) / np.linalg.norm(wg):.2e}; own dz1's "
                               f"f64 wgrad vs reference {np.linalg.norm(wg - rw) / np.linalg.norm(rw):.2e}",
                               flush=True)
-                    e = got - r
+                    ev = got - r
                     sg = np.sign(r)
-                    print(f"  {name} error structure: mean/rms {e.mean() / np.sqrt((e ** 2).mean()):+.3f}"
-                          f"  corr(err, sign) {np.mean(e * sg) / np.sqrt((e ** 2).mean()):+.3f}"
-                          f"  corr(err, x) {np.corrcoef(e.ravel(), r.ravel())[0, 1]:+.3f}"
-                          f"  err/|x| median {np.median(np.abs(e[r != 0]) / np.abs(r[r != 0])):.2e}",
+                    print(f"  {name} error structure: mean/rms {ev.mean() / np.sqrt((ev ** 2).mean()):+.3f}"
+                          f"  corr(err, sign) {np.mean(ev * sg) / np.sqrt((ev ** 2).mean()):+.3f}"
+                          f"  corr(err, x) {np.corrcoef(ev.ravel(), r.ravel())[0, 1]:+.3f}"
+                          f"  err/|x| median {np.median(np.abs(ev[r != 0]) / np.abs(r[r != 0])):.2e}",
                           flush=True)
                     print(f"  {name}: fro {np.linalg.norm(err) / np.linalg.norm(r):.2e} "
                           f"maxerr/max {err.max() / mx:.2e}; |x| quantiles/max "
