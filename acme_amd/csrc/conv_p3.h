@@ -203,6 +203,12 @@ struct P3ConvWgrad {
   static constexpr int A_MODE = gemm::RCONTIG, B_MODE = gemm::RCONTIG;
   static constexpr int A_PLANES = NPA, B_PLANES = gemm::kPlanes;
   static constexpr bool kColSum = true;  // bias gradient = column sums of dZ
+  // One accumulator per tile (gemm_p3.h P3Acc): each split-K partial is a short reduction
+  // (B x pixels / splits rows), and the split accumulators cost conv3_wgrad 27.9 -> 34.9 us
+  // for gradients already below the f32 engine's error either way (round 6: conv2 / conv3
+  // weight gradients 4.3e-7 / 3.5e-7 against 4.0e-7 / 3.3e-7 split and 6.9e-7 / 5.6e-7 f32,
+  // profiles/r06/accuracy/).
+  static constexpr bool kNoSplitAcc = true;
   int M, N, K, k_chunk;  // M = G::K rows (kh,kw,ci), N = CO, K = frames * OPIX
   PlaneSrc a_src;        // X [frames][IH][IW][CI]
   PlaneSrc b_src;        // dZ [frames * OPIX][CO]

@@ -691,6 +691,7 @@ __device__ __forceinline__ void store_shared_level(double* p, double v) {
 __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs a) {
   __shared__ int s_j[kFusedUpdateMax];
   __shared__ int64_t s_slot[kFusedUpdateMax];
+  __shared__ uint8_t s_ok[kFusedUpdateMax];  // the entry's key still lives in its slot
   __shared__ int s_len, s_np, s_ovf, s_last;
   __shared__ double s_ch[kUpdPairs][64];  // children of each prefetched node
   __shared__ int64_t s_node[kUpdPairs];
@@ -715,10 +716,13 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
   bool skip = !verdict && gate_skip(a.gate);
   if (tid == 0) s_len = 0;
   __syncthreads();
-  if (!skip) {  // this workgroup's updates (valid keys only): two rounds of loads in all
+  // Round 1: every update's key (all workgroups read all of them; L2-resident after the
+  // first), its slot and owner; this workgroup's updates join the list in atomic order.  Their
+  // stale-key check waits for round 2, so it shares that round with the children rows
+  // (round 6: three dependent rounds of global loads became two).
+  if (!skip) {
     constexpr int R = kFusedUpdateMax / 256;
-    uint64_t kv[R], kt[R];
-    int64_t sl[R];
+    uint64_t kv[R];
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       if (i * nt >= a.n) break;  // workgroup-uniform
@@ -730,20 +734,11 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
       if (i * nt >= a.n) break;
       const int j = tid + i * nt;
       const int64_t slot = (int64_t)(kv[i] % (uint64_t)a.capacity);
-      sl[i] = j < a.n && (int)((slot >> (6 * h)) % G) == bid ? slot : -1;
-    }
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      if (i * nt >= a.n) break;
-      kt[i] = a.keys[sl[i] >= 0 ? sl[i] : 0];
-    }
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      if (i * nt >= a.n) break;
-      if (sl[i] < 0 || kt[i] != kv[i]) continue;  // another workgroup's, or evicted since sampled
-      const int e = atomicAdd(&s_len, 1);
-      s_j[e] = tid + i * nt;
-      s_slot[e] = sl[i];
+      if (j < a.n && (int)((slot >> (6 * h)) % G) == bid) {
+        const int e = atomicAdd(&s_len, 1);
+        s_j[e] = j;
+        s_slot[e] = slot;
+      }
     }
   }
   __syncthreads();
@@ -755,7 +750,8 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
     // level (a serial scan by one thread took up to 7 us on the workgroup with the most
     // updates, profiles/r05/update_stamps/).  The list's order is the threads' (atomic slot
     // order); every use below matches nodes by (level, node), so the result does not depend
-    // on it.
+    // on it.  A node whose updates all turn out stale is rescanned from unchanged children:
+    // the same value it holds.
     if (tid == 0) {
       s_np = 0;
       s_ovf = 0;
@@ -781,21 +777,32 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
     stamp(2);
     const int np = s_np;
     const bool pre = !s_ovf;
-    // One round of loads: each node's 64 children (a wave per node), each update's priority.
-    double pv[kFusedUpdateMax / 256];
+    // Round 2, one batch of loads: each list entry's stored key (the stale check), its own
+    // key and priority again (L2 hits), and each node's 64 children (a wave per node).
+    constexpr int R = kFusedUpdateMax / 256;
+    double pv[R];
+    uint64_t kt[R], ku[R];
 #pragma unroll
-    for (int i = 0; i < kFusedUpdateMax / 256; ++i) {
+    for (int i = 0; i < R; ++i) {
       const int e = tid + i * nt;
-      pv[i] = e < len ? a.prios[s_j[e]] : 0.0;
+      const bool in = e < len;
+      kt[i] = in ? a.keys[s_slot[e]] : 0;
+      ku[i] = in ? a.upd_keys[s_j[e]] : 1;
+      pv[i] = in ? a.prios[s_j[e]] : 0.0;
     }
     if (pre) {
       for (int q = wave; q < np; q += nw)
         s_ch[q][lane] = a.level[s_lvl[q] - 1][s_node[q] * 64 + lane];
     }
-    // Everything but the stores before the verdict: the last update of each slot wins (its
-    // leaf p^alpha kept in registers and substituted into its level-1 node's children) and,
-    // on the prefetched path, every node's new value rescanned level by level in LDS.
-    constexpr int R = kFusedUpdateMax / 256;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int e = tid + i * nt;
+      if (e < len) s_ok[e] = kt[i] == ku[i] ? 1 : 0;  // evicted since sampled: ignored
+    }
+    __syncthreads();
+    // Everything but the stores before the verdict: the last valid update of each slot wins
+    // (its leaf p^alpha kept in registers and substituted into its level-1 node's children)
+    // and, on the prefetched path, every node's new value rescanned level by level in LDS.
     bool winv[R];
     double leafv[R];
 #pragma unroll
@@ -804,16 +811,14 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
       if (e >= len) break;
       const int64_t slot = s_slot[e];
       const int j = s_j[e];
-      bool win = true;
-      for (int f = 0; f < len; ++f)
-        if (s_slot[f] == slot && s_j[f] > j) win = false;
+      bool win = s_ok[e] != 0;
+      for (int f = 0; f < len && win; ++f)
+        if (s_slot[f] == slot && s_ok[f] && s_j[f] > j) win = false;
       winv[i] = win;
       if (win) leafv[i] = det_pow_priority(pv[i], a.alpha);
     }
-    // The children rows above are filled by wave (q % nw), the substitutions below by the
-    // winning update's thread (any wave): the barrier orders every row's fill before them
-    // (without it a late fill could overwrite a substituted leaf).
-    __syncthreads();
+    // (The children rows were filled by wave q % nw before the barrier above, so the
+    // substitutions below by any wave follow them: ADVICE r5's race.)
     if (pre) {
 #pragma unroll
       for (int i = 0; i < R; ++i) {

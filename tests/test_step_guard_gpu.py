@@ -13,13 +13,14 @@ sets the next step's scales from the skipped step's true maxima.
     were not written, the counts; then the same batch again is applied and matches the f64
     oracle teacher-forced from the GPU's state (loss / TD at 1e-5, gradients at the suite's
     bar, Adam at t = 2: the skipped step did not count).
-  * test_long_horizon_drift: 100 free-running steps at B = 64 (and 20 at the headline
-    B = 512) from identical batches on the plane engine, on the exact-f32 engine
+  * test_gradient_error_matches_f32_engine: teacher-forced, every gradient tensor of the
+    plane engine within 1.5x the exact-f32 engine's error against float64 (B = 64).
+  * test_long_horizon_drift: free-running steps at B = 64 x 100, 256 x 50 and 512 x 20 from
+    identical batches on the plane engine, on the exact-f32 engine
     (acme_set_matmul_engine(ACME_MATMUL_F32)) and on the float64 torch restatement
-    (oracle/dqn_torch.py on the GPU, the reference trajectory).  The plane engine skips no
-    step; its parameter drift from the f64 trajectory is within 2x (B = 512) / 3x (B = 64)
-    the f32 engine's, and its loss trajectory within 2x the f32 engine's at B = 512 and
-    under stated bounds at B = 64 (see the test).
+    (oracle/dqn_torch.py on the GPU, the reference trajectory), over 4 seeds.  The plane
+    engine skips no step; its parameter drift and the maximum and median of its loss error,
+    averaged over the seeds, are within 2x the f32 engine's (see the test).
   * test_underflow_only_skip_writes_no_priority / test_skipped_step_makes_no_target_copy:
     a skip decided by the rescale alone writes no priority on the fused path; a target copy
     due on a skipped step is not made.
@@ -44,8 +45,6 @@ from oracle import dqn_oracle as O
 pytestmark = pytest.mark.gpu
 
 HEAD = ("duelling_q_network/mlp/linear_1/w", "duelling_q_network/mlp_1/linear_1/w")
-# A build with -DP3_FOUR_TERMS=1 (the l*l term) leaves the free-running numbers unchanged
-# (drift 0.154, loss 0.749 / 0.063 at B = 64; profiles/r05/drift/) and costs 5 % of the step.
 
 
 def _dev(batch):
@@ -364,87 +363,131 @@ def _teacher_forced(d, params, target, b, B):
     _check_grads(d.get_params("grads"), grads)
 
 
-@pytest.mark.parametrize("B,steps,checks", [(64, 100, (0, 33, 66, 99)), (256, 50, (0, 49)),
-                                             (512, 20, (0, 19))])
-def test_long_horizon_drift(B, steps, checks):
-    """Free-running trajectories (each side applies its own gradients) of the plane engine
-    and the exact-f32 engine from identical batches, against the float64 torch restatement
-    (oracle/dqn_torch.py on the GPU, the reference trajectory), at the reference DQN agent's
-    default batch (256, agents/tf/dqn/agent.py:49), a small one and the headline one.
-    Asserted: the plane engine skips no step; the first loss matches
-    float64 at the north star's 1e-5 on both engines; the second (after one free-running
-    Adam step: at t = 1 the update is lr * sign(g), so a gradient element near zero flips on
-    any f32-accurate engine) within 1e-5 or 2x the f32 engine's error; the plane engine's
-    parameter drift from the float64 trajectory (relative to how far training moved the
-    parameters), and the maximum and median of its loss trajectory's relative error, each
-    within 2x the exact-f32 engine's.  (Round 5's engine, one accumulator per tile, failed this
-    at B = 64: loss error max 12x and median 18x the f32 engine's, from conv weight gradients
-    with 2.5-7x its error -- the f16 MFMA's biased accumulation, csrc/gemm_p3.h P3Acc.)  At the
-    `checks` steps the plane engine's step is also checked teacher-forced against the f64
-    oracle from its own pre-step state (loss and TD at 1e-5, the suite's gradient bar), so
-    per-step accuracy does not degrade as the scales follow training."""
+def _grad_errors(B, seed=0):
+    """Per-tensor relative Frobenius error of one step's gradients against float64, teacher-
+    forced from the same parameters, for the plane and the exact-f32 engine."""
     from acme_amd._lib import lib
     from acme_amd.native import NativeDQN
     from acme_amd.networks import DQNAtariNetwork
     from oracle.dqn_torch import TorchDQN
     net = DQNAtariNetwork(18)
-    p0, t0 = net.init(11), net.init(12)
-
-    def batches():
-        rng = np.random.default_rng(1000 + B)
-        for _ in range(steps):
-            yield _batch(rng, B, 18)
-
-    # The float64 reference trajectory (torch on the GPU).
+    p0, t0 = net.init(11 + 2 * seed), net.init(12 + 2 * seed)
+    b = _batch(np.random.default_rng(1000 + B + 7919 * seed), B, 18)
     ref = TorchDQN(p0, 18, target=t0, dtype=torch.float64, device="cuda")
-    ref_loss = []
-    for b in batches():
-        dev = {k: torch.as_tensor(b[k]).cuda() for k in ("o_tm1", "a_tm1", "r_t", "d_t", "o_t")}
-        loss, _ = ref.step(dev["o_tm1"], dev["a_tm1"], dev["r_t"].double(), dev["d_t"].double(),
-                           dev["o_t"], b["probabilities"])
-        ref_loss.append(loss)
-    ref_p = {k: v.detach().cpu().numpy() for k, v in ref.p.items()}
-    ref_loss = np.array(ref_loss)
-
-    def run(engine, check=()):
-        lib().acme_set_matmul_engine(engine)
+    dev = {k: torch.as_tensor(b[k]).cuda() for k in ("o_tm1", "a_tm1", "r_t", "d_t", "o_t")}
+    ref.step(dev["o_tm1"], dev["a_tm1"], dev["r_t"].double(), dev["d_t"].double(), dev["o_t"],
+             b["probabilities"])
+    g_ref = {k: ref.m[k].cpu().numpy() / 0.1 for k in ref.names}  # Adam's m = 0.1 g at t = 1
+    out = {}
+    for eng, code in (("plane", 1), ("f32", 0)):
+        lib().acme_set_matmul_engine(code)
         try:
             d = NativeDQN(network="nature", num_actions=18, max_batch=B, obs_dtype="uint8")
             d.set_params(p0, t0)
-            losses = []
-            for i, b in enumerate(batches()):
-                pre = (d.get_params("params"), d.get_params("target")) if i in check else None
-                d.step(*_dev(b))
-                losses.append(d.loss.clone())
-                if pre is not None:
-                    torch.cuda.synchronize()
-                    _teacher_forced(d, pre[0], pre[1], b, B)
+            d.forward_backward(*_dev(b))
             torch.cuda.synchronize()
-            return (np.array([x.item() for x in losses]), d.get_params("params"),
-                    d.guard_state())
+            g = d.get_params("grads")
         finally:
             lib().acme_set_matmul_engine(1)
+        out[eng] = {k: float(np.linalg.norm(g[k].reshape(r.shape) - r) / np.linalg.norm(r))
+                    for k, r in g_ref.items()}
+    return out
 
-    plane_loss, plane_p, plane_g = run(1, checks)
-    f32_loss, f32_p, f32_g = run(0)
-    assert plane_g["skipped"] == 0 and plane_g["applied"] == steps, plane_g
-    assert f32_g["skipped"] == 0 and f32_g["applied"] == steps, f32_g
-    d_plane, d_f32 = _rel(plane_p, ref_p, p0), _rel(f32_p, ref_p, p0)
-    e_plane = np.abs(plane_loss - ref_loss) / np.abs(ref_loss)
-    e_f32 = np.abs(f32_loss - ref_loss) / np.abs(ref_loss)
-    print(f"B={B} steps={steps}: parameter drift plane {d_plane:.3e} f32 {d_f32:.3e}; loss rel "
-          f"err max / median plane {e_plane.max():.3e} / {np.median(e_plane):.3e} f32 "
-          f"{e_f32.max():.3e} / {np.median(e_f32):.3e}; first two steps plane "
-          f"{e_plane[0]:.2e} {e_plane[1]:.2e} f32 {e_f32[0]:.2e} {e_f32[1]:.2e}")
-    # The first step matches the f64 trajectory at the north star's 1e-5; the second within
-    # 1e-5 or 2x the f32 engine's error.
-    np.testing.assert_allclose(plane_loss[:1], ref_loss[:1], rtol=1e-5)
-    np.testing.assert_allclose(f32_loss[:1], ref_loss[:1], rtol=1e-5)
-    assert e_plane[1] <= max(1e-5, 2.0 * e_f32[1]), (e_plane[1], e_f32[1])
-    assert d_plane <= 2.0 * d_f32 + 1e-5, (d_plane, d_f32)
-    assert e_plane.max() <= 2.0 * e_f32.max() + 1e-5, (e_plane.max(), e_f32.max())
-    assert np.median(e_plane) <= 2.0 * np.median(e_f32) + 1e-6, (np.median(e_plane),
-                                                                 np.median(e_f32))
+
+def test_gradient_error_matches_f32_engine():
+    """The plane engine's gradients are as accurate as the exact-f32 engine's, tensor by
+    tensor, teacher-forced from the same parameters against float64 (B = 64, the batch where
+    round 5 found its conv weight gradients at 2.5-7x the f32 engine's error: a biased f16
+    MFMA accumulation, now split, csrc/gemm_p3.h P3Acc; profiles/r06/accuracy/).  Bar: within
+    1.5x the f32 engine's error, for every weight and bias."""
+    e = _grad_errors(64)
+    for k in e["f32"]:
+        print(f"{k:42s} plane {e['plane'][k]:.2e} f32 {e['f32'][k]:.2e}")
+    for k in e["f32"]:
+        assert e["plane"][k] <= 1.5 * e["f32"][k] + 1e-8, (k, e["plane"][k], e["f32"][k])
+
+
+DRIFT_SEEDS = 6
+
+
+@pytest.mark.parametrize("B,steps", [(64, 100), (256, 50), (512, 20)])
+def test_long_horizon_drift(B, steps):
+    """Free-running trajectories (each side applies its own gradients) of the plane engine
+    and the exact-f32 engine from identical batches, against the float64 torch restatement
+    (oracle/dqn_torch.py on the GPU, the reference trajectory), at a small batch, the
+    reference DQN agent's default batch (256, agents/tf/dqn/agent.py:49) and the headline
+    one, over DRIFT_SEEDS seeds (initial parameters and batch streams).
+
+    A ReLU whose pre-activation lies within an engine's rounding of zero switches on one side
+    and not on the other, and from there the trajectories part chaotically, so a single
+    seed's numbers are draws (profiles/r06/drift/: per seed, either engine's maximum loss
+    error ranges over 100x, and each engine is ahead at some seeds).  Asserted (VERDICT r5
+    item 1): no skipped step; every seed's first loss matches float64 at the north star's
+    1e-5 on both engines; the plane engine's parameter drift from the float64 trajectory
+    (relative to how far training moved the parameters), and the maximum and the median of
+    its loss trajectory's relative error, each averaged over the seeds, within 2x the
+    exact-f32 engine's.  At seed 0 the plane engine's step is also checked teacher-forced
+    against the f64 oracle from its own pre-step state at the first and last step (loss and
+    TD at 1e-5, the suite's gradient bar), so per-step accuracy does not degrade as the
+    scales follow training."""
+    from acme_amd._lib import lib
+    from acme_amd.native import NativeDQN
+    from acme_amd.networks import DQNAtariNetwork
+    from oracle.dqn_torch import TorchDQN
+    net = DQNAtariNetwork(18)
+    metrics = {"plane": [], "f32": []}
+    for seed in range(DRIFT_SEEDS):
+        p0, t0 = net.init(11 + 2 * seed), net.init(12 + 2 * seed)
+
+        def batches():
+            rng = np.random.default_rng(1000 + B + 7919 * seed)
+            for _ in range(steps):
+                yield _batch(rng, B, 18)
+
+        ref = TorchDQN(p0, 18, target=t0, dtype=torch.float64, device="cuda")
+        ref_loss = []
+        for b in batches():
+            dev = {k: torch.as_tensor(b[k]).cuda() for k in ("o_tm1", "a_tm1", "r_t", "d_t", "o_t")}
+            loss, _ = ref.step(dev["o_tm1"], dev["a_tm1"], dev["r_t"].double(),
+                               dev["d_t"].double(), dev["o_t"], b["probabilities"])
+            ref_loss.append(loss)
+        ref_p = {k: v.detach().cpu().numpy() for k, v in ref.p.items()}
+        ref_loss = np.array(ref_loss)
+
+        def run(engine, check=()):
+            lib().acme_set_matmul_engine(engine)
+            try:
+                d = NativeDQN(network="nature", num_actions=18, max_batch=B, obs_dtype="uint8")
+                d.set_params(p0, t0)
+                losses = []
+                for i, b in enumerate(batches()):
+                    pre = (d.get_params("params"), d.get_params("target")) if i in check else None
+                    d.step(*_dev(b))
+                    losses.append(d.loss.clone())
+                    if pre is not None:
+                        torch.cuda.synchronize()
+                        _teacher_forced(d, pre[0], pre[1], b, B)
+                torch.cuda.synchronize()
+                return (np.array([x.item() for x in losses]), d.get_params("params"),
+                        d.guard_state())
+            finally:
+                lib().acme_set_matmul_engine(1)
+
+        for eng, code in (("plane", 1), ("f32", 0)):
+            losses, params, g = run(code, (0, steps - 1) if seed == 0 and eng == "plane" else ())
+            assert g["skipped"] == 0 and g["applied"] == steps, (eng, seed, g)
+            np.testing.assert_allclose(losses[:1], ref_loss[:1], rtol=1e-5)
+            e = np.abs(losses - ref_loss) / np.abs(ref_loss)
+            metrics[eng].append((_rel(params, ref_p, p0), e.max(), np.median(e)))
+        print(f"B={B} seed {seed}: " + "  ".join(
+            f"{eng} drift {m[-1][0]:.3e} loss max {m[-1][1]:.3e} median {m[-1][2]:.3e}"
+            for eng, m in metrics.items()))
+    mp, mf = np.mean(metrics["plane"], axis=0), np.mean(metrics["f32"], axis=0)
+    print(f"B={B} steps={steps}, mean over {DRIFT_SEEDS} seeds: drift plane {mp[0]:.3e} f32 "
+          f"{mf[0]:.3e}; loss rel err max plane {mp[1]:.3e} f32 {mf[1]:.3e}; median plane "
+          f"{mp[2]:.3e} f32 {mf[2]:.3e}")
+    for i, name in enumerate(("drift", "loss max", "loss median")):
+        assert mp[i] <= 2.0 * mf[i] + 1e-6, (name, mp[i], mf[i])
 
 
 def test_impala_timeout_skips_update():
