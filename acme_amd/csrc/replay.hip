@@ -173,10 +173,37 @@ __device__ __forceinline__ void draw_prioritized(const TreeView& tree, int64_t s
 
   int64_t node = 0;
   double t = 0.0, total = 0.0, leaf_value = 0.0;
-  for (int l = tree.nlevels - 1; l >= 0; --l) {
+  // A computed top level's children rows (level nlevels - 2) are already in registers when
+  // the descent reaches that level: its row is taken from them instead of loaded again (one
+  // dependent round trip fewer per draw, round 6).
+  const int top = tree.nlevels - 1;
+  double ch[kTopComputed];
+  for (int l = top; l >= 0; --l) {
     const int64_t base = node * 64;
-    const double v = l == tree.nlevels - 1 ? top_entry(tree.level, tree.nlevels, tree.top_nodes)
-                                           : tree.level[l][base + lane];
+    double v;
+    if (l == top) {
+      if (tree.top_nodes > 0) {
+        const double* c = tree.level[top - 1];
+#pragma unroll
+        for (int g = 0; g < kTopComputed; ++g) ch[g] = g < tree.top_nodes ? c[g * 64 + lane] : 0.0;
+        v = 0.0;
+#pragma unroll
+        for (int g = 0; g < kTopComputed; ++g) {
+          if (g >= tree.top_nodes) break;  // wave-uniform
+          const double tt = __shfl(wave_scan64(ch[g]), 63, 64);
+          if (lane == g) v = tt;
+        }
+      } else {
+        v = tree.level[top][lane];
+      }
+    } else if (l == top - 1 && tree.top_nodes > 0) {
+      v = 0.0;  // row `node` (< top_nodes) of level top - 1: ch[node]
+#pragma unroll
+      for (int g = 0; g < kTopComputed; ++g)
+        if (g == node) v = ch[g];
+    } else {
+      v = tree.level[l][base + lane];
+    }
     const double s = wave_scan64(v);
     if (l == tree.nlevels - 1) {
       total = __shfl(s, 63, 64);
@@ -459,16 +486,20 @@ __global__ void __launch_bounds__(T) sample_gather_pair_kernel(
     }
     prob *= prob_scale;
     if (threadIdx.x == 0) {
+      s_slot = slot;
       out_slots[r] = slot;
-      if (out_keys) out_keys[r] = keys[slot];
       if (out_probs) out_probs[r] = prob;
       if (out_size) out_size[r] = size;
-      if (out_prio) out_prio[r] = raw_prio[slot];
-      s_slot = slot;
     }
   }
   __syncthreads();
   const int64_t slot = s_slot;
+  // The record's key and priority after the barrier: their loads ride with the row copy's
+  // instead of delaying it by one round trip (the barrier waits for outstanding loads).
+  if (threadIdx.x == 64) {
+    if (out_keys) out_keys[r] = keys[slot];
+    if (out_prio) out_prio[r] = raw_prio[slot];
+  }
   const int64_t rb = (int64_t)nvec * 16;
   const vu4* a0 = reinterpret_cast<const vu4*>(s0 + slot * rb);
   const vu4* a1 = reinterpret_cast<const vu4*>(s1 + slot * rb);
@@ -668,14 +699,15 @@ struct FusedUpdateArgs {
 // (or the wait timed out: no priority is written, and the timeout is counted in
 // g->vtimeout, which the host reads: acme_dqn_verdict_timeouts).  Workgroup 0 of the same
 // launch publishes it and was dispatched first, so it is resident or done.
-__device__ __forceinline__ bool wait_verdict_skip(StepGuard* g, uint32_t seq) {
+// `first`: thread 0's load of g->vseq issued earlier (its latency overlapped the caller's LDS
+// work); polled again only when it did not yet hold this step's verdict.
+__device__ __forceinline__ bool wait_verdict_skip(StepGuard* g, uint32_t seq, uint32_t first) {
   __shared__ uint32_t s_v;
   if (threadIdx.x == 0) {
-    uint32_t v = 0;
-    for (int it = 0; it < (1 << 22); ++it) {
-      v = __hip_atomic_load(&g->vseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if ((v >> 1) == (seq & 0x7fffffffu)) break;
+    uint32_t v = first;
+    for (int it = 0; it < (1 << 22) && (v >> 1) != (seq & 0x7fffffffu); ++it) {
       __builtin_amdgcn_s_sleep(2);
+      v = __hip_atomic_load(&g->vseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     const bool got = (v >> 1) == (seq & 0x7fffffffu);
     if (!got) atomicAdd(&g->vtimeout, 1u);
@@ -684,18 +716,24 @@ __device__ __forceinline__ bool wait_verdict_skip(StepGuard* g, uint32_t seq) {
   __syncthreads();
   return s_v != 0u;
 }
+// A workgroup barrier that orders LDS only: outstanding global loads stay in flight across it
+// (__syncthreads also waits for every vector memory operation of the wave).
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 // A level-h value other workgroups' top rescan reads: write-through.
 __device__ __forceinline__ void store_shared_level(double* p, double v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs a) {
-  __shared__ int s_j[kFusedUpdateMax];
   __shared__ int64_t s_slot[kFusedUpdateMax];
-  __shared__ uint8_t s_ok[kFusedUpdateMax];  // the entry's key still lives in its slot
   __shared__ int s_len, s_np, s_ovf, s_last;
   __shared__ double s_ch[kUpdPairs][64];  // children of each prefetched node
   __shared__ int64_t s_node[kUpdPairs];
   __shared__ int s_lvl[kUpdPairs];
+  __shared__ int64_t s_nk[kUpdPairs];  // node << 3 | level: one LDS read per match test
   __shared__ double s_val[kUpdPairs];
   const int first = a.job.s ? 1 : 0;
   auto stamp = [&](int ph) {
@@ -716,18 +754,32 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
   bool skip = !verdict && gate_skip(a.gate);
   if (tid == 0) s_len = 0;
   __syncthreads();
-  // Round 1: every update's key (all workgroups read all of them; L2-resident after the
-  // first), its slot and owner; this workgroup's updates join the list in atomic order.  Their
-  // stale-key check waits for round 2, so it shares that round with the children rows
-  // (round 6: three dependent rounds of global loads became two).
+  // Round 1: every update's key and priority (all workgroups read all of them; L2-resident
+  // after the first), its slot and owner; this workgroup's updates join the list in atomic
+  // order, and the thread that read an update keeps it (key, priority, list entry) in
+  // registers.  Its stale-key check shares round 2 with the children rows, and its leaf
+  // p^alpha is computed while those loads are in flight (round 6: three dependent rounds of
+  // global loads became two, and the f64 power left the critical path).
+  constexpr int R = kFusedUpdateMax / 256;
+  uint64_t kv[R];
+  double pr[R];
+  int64_t sl[R];
+  int my_e[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    my_e[i] = -1;
+    kv[i] = 0;
+    pr[i] = 0.0;
+    sl[i] = 0;
+  }
   if (!skip) {
-    constexpr int R = kFusedUpdateMax / 256;
-    uint64_t kv[R];
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       if (i * nt >= a.n) break;  // workgroup-uniform
       const int j = tid + i * nt;
-      kv[i] = a.upd_keys[j < a.n ? j : a.n - 1];
+      const int jc = j < a.n ? j : a.n - 1;
+      kv[i] = a.upd_keys[jc];
+      pr[i] = a.prios[jc];
     }
 #pragma unroll
     for (int i = 0; i < R; ++i) {
@@ -736,8 +788,9 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
       const int64_t slot = (int64_t)(kv[i] % (uint64_t)a.capacity);
       if (j < a.n && (int)((slot >> (6 * h)) % G) == bid) {
         const int e = atomicAdd(&s_len, 1);
-        s_j[e] = j;
         s_slot[e] = slot;
+        my_e[i] = e;
+        sl[i] = slot;
       }
     }
   }
@@ -767,6 +820,7 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
       if (q < kUpdPairs) {
         s_lvl[q] = l;
         s_node[q] = node;
+        s_nk[q] = (node << 3) | l;
       } else {
         s_ovf = 1;
       }
@@ -777,60 +831,77 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
     stamp(2);
     const int np = s_np;
     const bool pre = !s_ovf;
-    // Round 2, one batch of loads: each list entry's stored key (the stale check), its own
-    // key and priority again (L2 hits), and each node's 64 children (a wave per node).
-    constexpr int R = kFusedUpdateMax / 256;
-    double pv[R];
-    uint64_t kt[R], ku[R];
+    // Round 2, one batch of loads: the stored key of each of this thread's updates (the stale
+    // check) and each node's 64 children (a wave per node); the leaves computed meanwhile.
+    // (Loops over a thread's updates stop at the workgroup-uniform count, so nothing is
+    // evaluated for the unused register slots: the f64 power below for all 16 measured
+    // 17 us.)
+    uint64_t kt[R];
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      const int e = tid + i * nt;
-      const bool in = e < len;
-      kt[i] = in ? a.keys[s_slot[e]] : 0;
-      ku[i] = in ? a.upd_keys[s_j[e]] : 1;
-      pv[i] = in ? a.prios[s_j[e]] : 0.0;
+      if (i * nt >= a.n) break;
+      kt[i] = my_e[i] >= 0 ? a.keys[sl[i]] : 0;
     }
     if (pre) {
       for (int q = wave; q < np; q += nw)
         s_ch[q][lane] = a.level[s_lvl[q] - 1][s_node[q] * 64 + lane];
     }
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      const int e = tid + i * nt;
-      if (e < len) s_ok[e] = kt[i] == ku[i] ? 1 : 0;  // evicted since sampled: ignored
-    }
-    __syncthreads();
-    // Everything but the stores before the verdict: the last valid update of each slot wins
-    // (its leaf p^alpha kept in registers and substituted into its level-1 node's children)
-    // and, on the prefetched path, every node's new value rescanned level by level in LDS.
-    bool winv[R];
     double leafv[R];
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      const int e = tid + i * nt;
-      if (e >= len) break;
-      const int64_t slot = s_slot[e];
-      const int j = s_j[e];
-      bool win = s_ok[e] != 0;
-      for (int f = 0; f < len && win; ++f)
-        if (s_slot[f] == slot && s_ok[f] && s_j[f] > j) win = false;
+      if (i * nt >= a.n) break;
+      leafv[i] = 0.0;
+      if (my_e[i] >= 0) leafv[i] = det_pow_priority(pr[i], a.alpha);
+    }
+    // Each entry repacked in place as slot << 13 | valid << 12 | j (the node list is built,
+    // so s_slot's plain form is no longer read): the election below reads one word per entry.
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      if (i * nt >= a.n) break;
+      if (my_e[i] >= 0)  // valid: the key still lives in its slot (evicted since sampled: ignored)
+        s_slot[my_e[i]] = (sl[i] << 13) | ((kt[i] == kv[i] ? 1 : 0) << 12) | (tid + i * nt);
+    }
+    __syncthreads();
+    stamp(4);
+    // The verdict's first poll now (thread 0), landing while the LDS work below runs: the
+    // barriers below order LDS only, so they do not wait for it.
+    uint32_t vfirst = 0;
+    if (verdict && tid == 0)
+      vfirst = __hip_atomic_load(&a.job.rg.g->vseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // Everything but the stores before the verdict: the last valid update of each slot wins
+    // (substituted into its level-1 node's children) and, on the prefetched path, every
+    // node's new value rescanned level by level in LDS.
+    bool winv[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) winv[i] = false;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      if (i * nt >= a.n) break;
+      const int e = my_e[i];
+      bool win = e >= 0 && kt[i] == kv[i];
+      const int j = tid + i * nt;
+      const int64_t me = (sl[i] << 1) | 1;  // same slot, valid
+#pragma unroll 4
+      for (int f = 0; f < len; ++f) {
+        const int64_t x = s_slot[f];
+        if ((x >> 12) == me && (int)(x & 4095) > j) win = false;
+      }
       winv[i] = win;
-      if (win) leafv[i] = det_pow_priority(pv[i], a.alpha);
     }
     // (The children rows were filled by wave q % nw before the barrier above, so the
     // substitutions below by any wave follow them: ADVICE r5's race.)
     if (pre) {
 #pragma unroll
       for (int i = 0; i < R; ++i) {
-        const int e = tid + i * nt;
-        if (e >= len) break;
+        if (i * nt >= a.n) break;
         if (!winv[i]) continue;
-        const int64_t slot = s_slot[e];
+        const int64_t k1 = ((sl[i] >> 6) << 3) | 1;
+#pragma unroll 4
         for (int q = 0; q < np; ++q)
-          if (s_lvl[q] == 1 && s_node[q] == (slot >> 6)) s_ch[q][slot & 63] = leafv[i];
+          if (s_nk[q] == k1) s_ch[q][sl[i] & 63] = leafv[i];
       }
     }
-    __syncthreads();
+    lds_barrier();
     if (pre) {
       for (int l = 1; l <= h; ++l) {
         for (int q = wave; q < np; q += nw) {
@@ -838,30 +909,29 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
           const double v = wave_scan64(s_ch[q][lane]);
           if (lane == 63) s_val[q] = v;
         }
-        __syncthreads();
-        if (tid < np && s_lvl[tid] == l)  // into the parent's children
+        lds_barrier();
+        if (tid < np && s_lvl[tid] == l) {  // into the parent's children
+          const int64_t kp = ((s_node[tid] >> 6) << 3) | (l + 1);
+#pragma unroll 4
           for (int q = 0; q < np; ++q)
-            if (s_lvl[q] == l + 1 && s_node[q] == (s_node[tid] >> 6))
-              s_ch[q][s_node[tid] & 63] = s_val[tid];
-        __syncthreads();
+            if (s_nk[q] == kp) s_ch[q][s_node[tid] & 63] = s_val[tid];
+        }
+        lds_barrier();
       }
     }
     // The step's verdict (published by workgroup 0's rescale while this workgroup resolved
     // its keys, loaded and computed), before the first store.
-    if (verdict) skip = wait_verdict_skip(a.job.rg.g, a.job.rg.seq);
+    if (verdict) skip = wait_verdict_skip(a.job.rg.g, a.job.rg.seq, vfirst);
     stamp(3);
     if (!skip) {
 #pragma unroll
       for (int i = 0; i < R; ++i) {
-        const int e = tid + i * nt;
-        if (e >= len) break;
+        if (i * nt >= a.n) break;
         if (!winv[i]) continue;
-        const int64_t slot = s_slot[e];
-        a.raw_prio[slot] = pv[i];
-        if (h == 0 && !a.top_computed) store_shared_level(a.level[0] + slot, leafv[i]);
-        else a.level[0][slot] = leafv[i];
+        a.raw_prio[sl[i]] = pr[i];
+        if (h == 0 && !a.top_computed) store_shared_level(a.level[0] + sl[i], leafv[i]);
+        else a.level[0][sl[i]] = leafv[i];
       }
-      stamp(4);
       if (pre) {
         for (int q = tid; q < np; q += nt) {
           const int l = s_lvl[q];
@@ -872,7 +942,7 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
         __syncthreads();
         for (int l = 1; l <= h; ++l) {  // read back what this workgroup stored (levels below are its own)
           for (int e = wave; e < len; e += nw) {
-            const int64_t node = s_slot[e] >> (6 * l);
+            const int64_t node = (s_slot[e] >> 13) >> (6 * l);
             const double v = wave_scan64(a.level[l - 1][node * 64 + lane]);
             if (lane == 63) {
               if (l == h && !a.top_computed) store_shared_level(a.level[l] + node, v);

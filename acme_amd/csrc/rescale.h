@@ -54,7 +54,8 @@ __device__ __forceinline__ void rescale_block(const RescaleJob& j) {
   __shared__ float s_w0[kMax], s_r0[kMax], s_wi0[kMax];
   __shared__ int s_shift[kMax];
   __shared__ int s_bad;
-  __shared__ uint32_t s_gv[5];
+  __shared__ uint32_t s_gv[6];
+  __shared__ int64_t s_cnt[2];  // the guard's applied / skipped counts, read up front
   __shared__ float s_dp, s_cwi;
   gemm::PScale* s = j.s;
   const int n = j.n;
@@ -78,14 +79,18 @@ __device__ __forceinline__ void rescale_block(const RescaleJob& j) {
     s_bad = 0;
     s_cwi = j.copy_to >= 0 ? s[j.copy_from].wi : 0.f;
     const RescaleGuard& rg = j.rg;
-    s_gv[0] = s_gv[1] = s_gv[2] = s_gv[3] = s_gv[4] = 0u;
+    s_gv[0] = s_gv[1] = s_gv[2] = s_gv[3] = s_gv[4] = s_gv[5] = 0u;
+    s_cnt[0] = s_cnt[1] = 0;
     s_dp = 0.f;
-    if (rg.g) {  // the guard's inputs, read before any store
+    if (rg.g) {  // the guard's inputs, read before any store (with the slots: one round trip)
       s_gv[0] = rg.g->on;
       s_gv[1] = rg.g->tt;
       s_gv[2] = rg.g->t[rg.gate.par & 1];
       s_gv[3] = rg.g->prm;
       s_gv[4] = rg.g->hold;
+      s_gv[5] = rg.tmo ? rg.tmo[0] : 0u;
+      s_cnt[0] = rg.g->applied;
+      s_cnt[1] = rg.g->skipped;
       if (rg.gate.dp) s_dp = *rg.gate.dp;
     }
   }
@@ -161,27 +166,29 @@ __device__ __forceinline__ void rescale_block(const RescaleJob& j) {
       if (bad) g->on = 1u;
     } else if (g && rg.mode == kRgStep) {
       // The flags (on, prm) are cleared by the step's Adam launch, after every reader.
-      const bool timed_out = rg.tmo && rg.tmo[0] != 0u;
+      const bool timed_out = rg.tmo && s_gv[5] != 0u;
       const bool skip =
           (s_gv[0] | s_gv[2] | s_gv[4] | bad) != 0u || s_dp > 0.f || timed_out;
+      // The verdict first (the same launch's update workgroups wait for it), then the
+      // counts from the values read up front: no load between the decision and the store.
+      const uint32_t v = (rg.seq << 1) | (skip ? 1u : 0u);
+      __hip_atomic_store(&g->vseq, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (rg.host_verdicts)
+        __hip_atomic_store(rg.host_verdicts + (rg.seq & 63u), v, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
       if (timed_out) {
         rg.tmo[0] = 0u;
         rg.tmo[1] += 1u;
       }
       g->last = skip ? 1u : 0u;
       if (skip) {
-        const int64_t k = g->skipped + 1;
+        const int64_t k = s_cnt[1] + 1;
         g->skipped = k;
         if (rg.host_skipped) *rg.host_skipped = k;
         if (rg.sticky) g->hold = 1u;
       } else {
-        g->applied += 1;
+        g->applied = s_cnt[0] + 1;
       }
-      const uint32_t v = (rg.seq << 1) | (skip ? 1u : 0u);
-      __hip_atomic_store(&g->vseq, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (rg.host_verdicts)
-        __hip_atomic_store(rg.host_verdicts + (rg.seq & 63u), v, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
     } else if (g && rg.mode == kRgClear) {
       g->hold = 0u;
       g->on = g->tt = g->prm = g->last = g->qv = 0u;

@@ -270,6 +270,10 @@ def setup_dqn(args, world, rank, dev):
                 "parallelism": f"dp{world}"})
     meta["_table"] = table
     meta["_set_staged"] = lambda on: setattr(learner, "_staged", bool(on))
+    # Adam against SURVEY §8(d)'s algorithmic bytes (7 x 4 B per parameter: p, m, v read and
+    # written, g read) beside the kernel's design bytes (also the parameter planes it writes
+    # and the conv weight gradients' split-K slabs it reduces), VERDICT r5 item 4.
+    meta["_adam_survey_bytes"] = 28.0 * sum(int(np.prod(s)) for _, s in net.tensor_shapes())
 
     def guard():  # synchronises: read outside the timed window
         g = learner.native.guard_state()
@@ -1025,6 +1029,10 @@ def main():
             gbs = by.value / cnt.value / (avg_ms * 1e-3) / 1e9
             rec.update(bound="hbm", achieved=round(gbs, 1), unit="GB/s",
                        frac=round(gbs / HBM_PEAK_GBS, 4))
+            if rec["name"] == "adam" and "_adam_survey_bytes" in meta:
+                sb = meta["_adam_survey_bytes"]
+                rec.update(design_bytes=round(by.value / cnt.value), survey_bytes=round(sb),
+                           frac_survey_bytes=round(sb / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
         sections.append(rec)
     sections.sort(key=lambda r: -r["total_ms"])
     # Sum of the profiled kernel durations per step: ms_per_step minus this is launch gaps

@@ -82,7 +82,8 @@ def ref_tensors(params, target, b, A=18):
     nhwc = lambda z: z.permute(0, 2, 3, 1).reshape(z.shape[0], -1).detach().cpu().numpy()  # noqa
     out = {"dz1": nhwc(pre[0].grad), "dz2": nhwc(pre[1].grad), "dz3": nhwc(pre[2].grad),
            "dzh": zh.grad.detach().cpu().numpy(),
-           "x1": nhwc(acts[0]), "x2": nhwc(acts[1]), "x3": nhwc(acts[2])}
+           "x1": nhwc(acts[0]), "x2": nhwc(acts[1]), "x3": nhwc(acts[2]),
+           "hid": h.detach().cpu().numpy()}
     return out
 
 

@@ -3,7 +3,7 @@ ACME_V_STAMPS=1): the bench's DQN path (GPU table -> dataset -> DQNLearner.step(
 update_priorities) runs some steps, then every workgroup's s_memrealtime stamps (100 MHz,
 comparable across workgroups) of the last launch are summarised against the launch's first
 entry: workgroup 0 runs the step's rescale (entry, done), the update workgroups their phases
-(entry, keys resolved, node list, verdict, leaves, levels, exit).
+(entry, keys resolved, node list, verdict, round-2 loads landed, levels, exit).
 Run under gpurun: python3 tools/update_stamps.py"""
 import os
 import sys
@@ -13,7 +13,7 @@ import numpy as np
 os.environ["ACME_V_STAMPS"] = "1"
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-PHASES = ("entry", "keys", "nodes", "verdict", "leaves", "levels", "exit")
+PHASES = ("entry", "keys", "nodes", "verdict", "round2", "levels", "exit")
 
 
 def main():
