@@ -167,6 +167,11 @@ _SIGS = {
                                           ctypes.POINTER(c_vp), c_vp]),
     "acme_replay_sample_gather_frames": (c_i32, [c_vp, c_i64, c_u64, c_vp, c_vp, c_vp, c_vp,
                                                  c_vp, ctypes.POINTER(c_vp), c_vp, c_vp]),
+    "acme_replay_pipe_open": (c_i32, [c_vp, ctypes.POINTER(c_i32)]),
+    "acme_replay_pipe_close": (c_i32, [c_vp, c_i32]),
+    "acme_replay_pipe_flush": (c_i32, [c_vp, c_i32]),
+    "acme_replay_sample_gather_pipe": (c_i32, [c_vp, c_i32, c_i64, c_u64, c_vp, c_vp, c_vp, c_vp,
+                                               c_vp, ctypes.POINTER(c_vp), c_vp]),
     "acme_r2d2_priorities": (c_i32, [c_vp, c_i32, c_i32, ctypes.c_double, c_vp, c_vp]),
     "acme_r2d2_importance_weights": (c_i32, [c_vp, c_i32, c_i64, ctypes.c_double, c_vp, c_vp]),
     "acme_frames_expand": (c_i32, [c_vp, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp, c_vp]),

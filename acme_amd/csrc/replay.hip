@@ -66,6 +66,7 @@ using namespace acme;
 constexpr int kStageChunks = 4;
 constexpr int64_t kStageBytes = 32ll << 20;  // per chunk
 constexpr int kMaxReaders = 8;
+constexpr int kMaxPipes = 8;
 
 struct acme_replay {
   acme_replay_config cfg;
@@ -107,6 +108,17 @@ struct acme_replay {
   } readers[kMaxReaders] = {};
   int nreaders = 0;
   std::mutex order_mu;
+  // Pipelined readers (acme_replay_sample_gather_pipe): each holds at most one drawn batch
+  // whose rows are not copied yet.  Every operation that writes rows issues those copies
+  // first (flush_pipes), so a pending batch always gets the rows of its drawn keys.
+  struct Pipe {
+    bool open, pending;
+    hipEvent_t ev;  // orders a new stream after copies flushed on the pipe's previous one
+    hipStream_t st;
+    int64_t batch;
+    const int64_t* slots;
+    void* out[ACME_MAX_FIELDS];
+  } pipes[kMaxPipes] = {};
 };
 
 namespace {
@@ -551,6 +563,73 @@ __global__ void __launch_bounds__(T) sample_gather_pair_kernel(
           reinterpret_cast<const uint32_t*>(sm.src[q] + slot * 4 * sm.words[q])[w];
   }
 }
+
+// Pipelined draw + gather (round 6; acme_replay_sample_gather_pipe): workgroup j's first wave
+// draws item j of the NEW batch (the sampling arithmetic above) and writes its record, while
+// waves 1-3 copy row j of the batch the previous launch drew (its slots already in memory,
+// one load away).  The descent's chain of dependent tree loads thus runs under the previous
+// batch's row copy instead of in front of it, and no barrier ties the two together.
+template <bool PRIO, int MAXC>
+__global__ void __launch_bounds__(256) sample_gather_pipe_kernel(
+    TreeView tree, const double* __restrict__ raw_prio, const uint64_t* __restrict__ keys,
+    int64_t size, uint64_t seed, uint64_t step, int64_t batch, int64_t* out_slots,
+    uint64_t* out_keys, double* out_probs, int64_t* out_size, double* out_prio,
+    const int64_t* __restrict__ pend_slots, int64_t pend_batch, const uint8_t* __restrict__ s0,
+    const uint8_t* __restrict__ s1, uint8_t* __restrict__ d0, uint8_t* __restrict__ d1,
+    int32_t nvec, SmallFields sm) {
+  constexpr int T = 192;  // copy threads (waves 1-3)
+  const int64_t r = blockIdx.x;
+  if (threadIdx.x < 64) {
+    if (r >= batch) return;  // wave-uniform
+    int64_t slot;
+    double prob;
+    if (PRIO) {
+      draw_prioritized(tree, size, seed, step, r, &slot, &prob);
+    } else {
+      const double u = sample_uniform(seed, step, (uint32_t)r);
+      slot = (int64_t)(u * (double)size);
+      if (slot >= size) slot = size - 1;
+      prob = 1.0 / (double)size;
+    }
+    if (threadIdx.x == 0) {
+      out_slots[r] = slot;
+      if (out_probs) out_probs[r] = prob;
+      if (out_size) out_size[r] = size;
+      if (out_keys) out_keys[r] = keys[slot];
+      if (out_prio) out_prio[r] = raw_prio[slot];
+    }
+    return;
+  }
+  if (r >= pend_batch) return;  // workgroup-uniform
+  const int t = threadIdx.x - 64;
+  const int64_t slot = pend_slots[r];
+  const int64_t rb = (int64_t)nvec * 16;
+  const vu4* a0 = reinterpret_cast<const vu4*>(s0 + slot * rb);
+  const vu4* a1 = reinterpret_cast<const vu4*>(s1 + slot * rb);
+  vu4* b0 = reinterpret_cast<vu4*>(d0 + r * rb);
+  vu4* b1 = reinterpret_cast<vu4*>(d1 + r * rb);
+  vu4 v[MAXC];
+#pragma unroll
+  for (int k = 0; k < MAXC; ++k) {
+    const int32_t c = min(t + k * T, 2 * nvec - 1);  // unconditional (see gather_pair_kernel)
+    const vu4* p = c < nvec ? a0 + c : a1 + (c - nvec);
+    v[k] = __builtin_nontemporal_load(p);
+  }
+#pragma unroll
+  for (int k = 0; k < MAXC; ++k) {
+    const int32_t c = t + k * T;
+    vu4* p = c < nvec ? b0 + c : b1 + (c - nvec);
+    if (c < 2 * nvec) *p = v[k];
+  }
+#pragma unroll
+  for (int q = 0; q < ACME_MAX_FIELDS; ++q) {
+    if (q >= sm.n) break;
+    for (int w = t; w < sm.words[q]; w += T)
+      reinterpret_cast<uint32_t*>(sm.dst[q] + r * 4 * sm.words[q])[w] =
+          reinterpret_cast<const uint32_t*>(sm.src[q] + slot * 4 * sm.words[q])[w];
+  }
+}
+constexpr int kPipeChunks = 19;  // 16-B chunks per copy thread: rows up to 192 x 19 x 8 B
 
 // Sample + gather fused for rows of small fields only (the control-suite transitions:
 // every field under 1 KB): one wave per sampled row draws it (the sampling kernels'
@@ -1164,6 +1243,26 @@ int order_after_inserts(acme_replay* r, hipStream_t st, int64_t* size_out = null
   return ACME_OK;
 }
 
+// Issues pipe p's pending row copies now, on its stream (the caller holds r->mu).
+int flush_pipe(acme_replay* r, acme_replay::Pipe& p) {
+  if (!p.pending) return ACME_OK;
+  p.pending = false;
+  return acme_replay_gather(r, p.slots, p.batch, p.out, p.st);
+}
+
+// Before any operation that writes rows: every pipe's pending copies (the caller holds r->mu).
+// A commit fences the copies' streams as readers; the setup-time writers (synthetic fill,
+// checkpoint restore) pass wait = true and the host waits for the copies instead.
+int flush_pipes(acme_replay* r, bool wait = false) {
+  for (auto& p : r->pipes) {
+    const bool had = p.pending;
+    const int rc = flush_pipe(r, p);
+    if (rc != ACME_OK) return rc;
+    if (had && wait) ACME_HIP_TRY(hipStreamSynchronize(p.st));
+  }
+  return ACME_OK;
+}
+
 // Byte layout of a staging chunk of n items: each field's rows, then keys, raw priorities
 // and leaf weights (8 B per item each), every block 256-B aligned.  Returns the chunk bytes.
 int64_t stage_layout(const acme_replay_config& cfg, int64_t n, int64_t* off) {
@@ -1265,6 +1364,8 @@ int commit_chunk(acme_replay* r, const Chunk& ch, int64_t n, const double* prior
                    : 1.0;
   }
   if (out_keys) std::memcpy(out_keys, hkeys, n * sizeof(uint64_t));
+  const int frc = flush_pipes(r);
+  if (frc != ACME_OK) return frc;
   {
     std::lock_guard<std::mutex> lock(r->order_mu);
     acme_replay::Reader* rd;
@@ -1444,6 +1545,8 @@ int acme_replay_destroy(acme_replay* r) {
     if (r->stage_up[c]) (void)hipEventDestroy(r->stage_up[c]);
   }
   for (int i = 0; i < r->nreaders; ++i) (void)hipEventDestroy(r->readers[i].ev);
+  for (auto& p : r->pipes)
+    if (p.ev) (void)hipEventDestroy(p.ev);
   if (r->insert_event) (void)hipEventDestroy(r->insert_event);
   if (r->side) (void)hipStreamDestroy(r->side);
   if (r->upload) (void)hipStreamDestroy(r->upload);
@@ -1467,9 +1570,14 @@ int acme_replay_debug_leaves(const acme_replay* r, const double** leaf_values,
   return ACME_OK;
 }
 
-int acme_replay_storage(const acme_replay* r, int32_t field, void** out) {
+int acme_replay_storage(acme_replay* r, int32_t field, void** out) {
   ACME_CHECK_ARG(r && out, "null argument");
   ACME_CHECK_ARG(field >= 0 && field < r->cfg.num_fields, "field %d out of range", field);
+  {  // the caller may write rows through the pointer (checkpoint restore)
+    std::lock_guard<std::mutex> lock(r->mu);
+    const int rc = flush_pipes(r, true);
+    if (rc != ACME_OK) return rc;
+  }
   *out = r->fields[field];
   return ACME_OK;
 }
@@ -1481,7 +1589,9 @@ int acme_replay_restore(acme_replay* r, int64_t inserted, void* stream) {
   ACME_CHECK_ARG(inserted >= 0, "negative insert count");
   std::lock_guard<std::mutex> lock(r->mu);
   hipStream_t st = as_stream(stream);
-  int rc = order_after_inserts(r, st);
+  int rc = flush_pipes(r, true);
+  if (rc != ACME_OK) return rc;
+  rc = order_after_inserts(r, st);
   if (rc != ACME_OK) return rc;
   const int64_t C = r->cfg.capacity, live = std::min(inserted, C);
   const int64_t n = r->level_size[0];
@@ -1625,7 +1735,9 @@ int acme_replay_fill_synthetic(acme_replay* r, int64_t n, int32_t layout, int32_
   if (n == 0) return ACME_OK;
   std::lock_guard<std::mutex> lock(r->mu);
   hipStream_t st = as_stream(stream);
-  int rc0 = order_after_inserts(r, st);
+  int rc0 = flush_pipes(r, true);
+  if (rc0 != ACME_OK) return rc0;
+  rc0 = order_after_inserts(r, st);
   if (rc0 != ACME_OK) return rc0;
   const int64_t C = r->cfg.capacity;
   const int64_t first_key = r->inserted;
@@ -1981,6 +2093,117 @@ int acme_replay_sample_gather_frames(acme_replay* r, int64_t batch, uint64_t ste
   std::lock_guard<std::mutex> lock(r->mu);
   return sample_gather_impl(r, batch, step_counter, 1.0, slots, keys, probabilities, table_size,
                             priorities, out_fields, stream, frames_f16);
+}
+
+int acme_replay_pipe_open(acme_replay* r, int32_t* pipe) {
+  ACME_CHECK_ARG(r && pipe, "null argument");
+  std::lock_guard<std::mutex> lock(r->mu);
+  for (int i = 0; i < kMaxPipes; ++i)
+    if (!r->pipes[i].open) {
+      acme_replay::Pipe& p = r->pipes[i];
+      if (!p.ev) ACME_HIP_TRY(hipEventCreateWithFlags(&p.ev, hipEventDisableTiming));
+      const hipEvent_t ev = p.ev;  // kept across close / open
+      p = acme_replay::Pipe{};
+      p.ev = ev;
+      p.open = true;
+      *pipe = i;
+      return ACME_OK;
+    }
+  set_error("all %d pipes of this table are open", kMaxPipes);
+  return ACME_ERR_INVALID;
+}
+
+int acme_replay_pipe_close(acme_replay* r, int32_t pipe) {
+  ACME_CHECK_ARG(r, "null replay");
+  ACME_CHECK_ARG(pipe >= 0 && pipe < kMaxPipes, "pipe %d out of range", pipe);
+  std::lock_guard<std::mutex> lock(r->mu);
+  r->pipes[pipe].open = false;
+  r->pipes[pipe].pending = false;
+  return ACME_OK;
+}
+
+int acme_replay_pipe_flush(acme_replay* r, int32_t pipe) {
+  ACME_CHECK_ARG(r, "null replay");
+  ACME_CHECK_ARG(pipe >= 0 && pipe < kMaxPipes, "pipe %d out of range", pipe);
+  std::lock_guard<std::mutex> lock(r->mu);
+  ACME_CHECK_ARG(r->pipes[pipe].open, "pipe %d is not open", pipe);
+  return flush_pipe(r, r->pipes[pipe]);
+}
+
+int acme_replay_sample_gather_pipe(acme_replay* r, int32_t pipe, int64_t batch,
+                                   uint64_t step_counter, int64_t* slots, uint64_t* keys,
+                                   double* probabilities, int64_t* table_size,
+                                   double* priorities, void* const* out_fields, void* stream) {
+  ACME_CHECK_ARG(r && slots && out_fields, "null argument");
+  ACME_CHECK_ARG(pipe >= 0 && pipe < kMaxPipes, "pipe %d out of range", pipe);
+  ACME_CHECK_ARG(batch > 0 && batch < (int64_t(1) << 31), "bad batch");
+  std::lock_guard<std::mutex> lock(r->mu);
+  acme_replay::Pipe& p = r->pipes[pipe];
+  ACME_CHECK_ARG(p.open, "pipe %d is not open", pipe);
+  hipStream_t st = as_stream(stream);
+  int f0, f1;
+  SmallFields sm;
+  const bool pair = pair_layout(r, out_fields, &f0, &f1, &sm);
+  const int32_t nvec = pair ? (int32_t)(r->cfg.field_bytes[f0] / 16) : 0;
+  // The pending copy rides with this draw when it is this stream's and writes none of the
+  // buffers this draw writes; otherwise it is issued on its own first.
+  bool ride = p.pending && pair && p.st == st && p.slots != slots;
+  for (int f = 0; ride && f < r->cfg.num_fields; ++f) ride = p.out[f] != out_fields[f];
+  if (p.pending && !ride) {
+    const hipStream_t old = p.st;
+    const int rc = flush_pipe(r, p);
+    if (rc != ACME_OK) return rc;
+    if (old != st) {  // the batch is complete where this stream's later events are recorded
+      ACME_HIP_TRY(hipEventRecord(p.ev, old));
+      ACME_HIP_TRY(hipStreamWaitEvent(st, p.ev, 0));
+    }
+  }
+  if (!pair || 2 * nvec > 192 * kPipeChunks) {  // no pipelining for this layout
+    return sample_gather_impl(r, batch, step_counter, 1.0, slots, keys, probabilities,
+                              table_size, priorities, out_fields, stream);
+  }
+  int64_t size = 0;
+  int rc = order_after_inserts(r, st, &size);
+  if (rc != ACME_OK) return rc;
+  if (size <= 0) {
+    set_error("cannot sample from an empty table (rate limiter MinSize(1))");
+    return ACME_ERR_EMPTY;
+  }
+  // The pending batch's outputs (same layout: the pipe only ever holds pair-layout batches).
+  const int64_t pend = ride ? p.batch : 0;
+  SmallFields psm = {};
+  uint8_t *pd0 = nullptr, *pd1 = nullptr;
+  if (ride) {
+    void* po[ACME_MAX_FIELDS];
+    for (int f = 0; f < r->cfg.num_fields; ++f) po[f] = p.out[f];
+    int g0, g1;
+    pair_layout(r, po, &g0, &g1, &psm);
+    pd0 = static_cast<uint8_t*>(po[g0]);
+    pd1 = static_cast<uint8_t*>(po[g1]);
+  }
+  double row_bytes = 0;
+  for (int k = 0; k < r->cfg.num_fields; ++k) row_bytes += (double)r->cfg.field_bytes[k];
+  const bool prio = r->cfg.sampler == ACME_SAMPLER_PRIORITIZED;
+  ACME_PROF("replay_sample_gather", st, 0.0,
+            (double)batch * (40.0 + (prio ? 512.0 * r->nlevels : 0.0)) +
+                (double)pend * 2.0 * row_bytes);
+  const TreeView tv = tree_view(r);
+  const unsigned grid = (unsigned)std::max(batch, pend);
+#define ACME_SGPIPE(PRIO)                                                                       \
+  sample_gather_pipe_kernel<PRIO, kPipeChunks><<<grid, 256, 0, st>>>(                           \
+      tv, r->raw_prio, r->keys, size, r->cfg.seed, step_counter, batch, slots, keys,            \
+      probabilities, table_size, priorities, ride ? p.slots : nullptr, pend, r->fields[f0],     \
+      r->fields[f1], pd0, pd1, nvec, psm)
+  if (prio) ACME_SGPIPE(true);
+  else ACME_SGPIPE(false);
+#undef ACME_SGPIPE
+  ACME_LAUNCH_CHECK();
+  p.pending = true;
+  p.st = st;
+  p.batch = batch;
+  p.slots = slots;
+  for (int f = 0; f < ACME_MAX_FIELDS; ++f) p.out[f] = f < r->cfg.num_fields ? out_fields[f] : nullptr;
+  return ACME_OK;
 }
 
 }  // extern "C"

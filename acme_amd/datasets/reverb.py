@@ -17,7 +17,10 @@ issued prefetch (Table._after_readers), and host inserts are ordered after every
 that has read the table (inside the native table, csrc/replay.hip), so a queued draw never
 overlaps a tree update or a slot overwrite; a draw and its row gather are one unit with
 respect to inserts (acme_replay_sample_gather).  The draw order, and so every sampled
-index, is deterministic for a given interleaving of inserts.
+index, is deterministic for a given interleaving of inserts.  With P >= 2 on the transition
+layout the draws are pipelined (acme_replay_sample_gather_pipe): batch k + P's rows are
+copied by batch k + P + 1's launch, beside that draw's tree descent; an insert issues the
+pending copy before it lands, so the rows are still those of the drawn keys.
 
 `server_address` may be the in-process address ('localhost:<port>'), a Server, a Table
 or a Client.  Sampling is deterministic given the table seed: draw i uses Philox
@@ -225,6 +228,7 @@ class _TableIterator:
             self._issued = OrderEvent()
             self._ready = [OrderEvent() for _ in range(self._P + 2)]
             self._next_slot = 0
+            self._open_pipe()
         if self._shard is not None:
             import torch.distributed as dist
             world = self._shard[0]
@@ -265,6 +269,38 @@ class _TableIterator:
             self._fb.append(torch.empty(2 * self._rows, fields[0].row_bytes, dtype=torch.int16,
                                         device=dev) if self._f16_frames() else None)
         self._which = 0
+
+    def _open_pipe(self) -> None:
+        """Pipelined draws (round 6, acme_replay_sample_gather_pipe): a prefetched batch's rows
+        are copied by the NEXT draw's launch, beside that draw's tree descent, so its ready
+        event is recorded after that launch.  Same draws, keys and rows as the unpipelined
+        path; single-table transition layouts only (not shards, FrameTable or the f16 copy),
+        and prefetch_size >= 2 (at 1 the batch handed out would wait for the launch issued
+        in the same next() call).  ACME_REPLAY_PIPE=0 turns it off (A/B)."""
+        self._pipe = None
+        self._pending = None  # buffer slot whose rows the next launch copies
+        if (self._P < 2 or self._shard is not None
+                or isinstance(self._t, (replay.FrameTable, replay.QueueTable))
+                or self._f16_frames() or os.environ.get("ACME_REPLAY_PIPE", "1") == "0"):
+            return
+        import ctypes
+        from acme_amd._lib import check, lib
+        pid = ctypes.c_int32()
+        check(lib().acme_replay_pipe_open(self._t.native.handle, ctypes.byref(pid)), "replay pipe")
+        self._pipe = pid.value
+        self._pipe_native = self._t.native  # closed before the table is destroyed
+
+    def __del__(self):
+        pipe = getattr(self, "_pipe", None)
+        if pipe is not None:
+            try:
+                from acme_amd._lib import lib
+                h = self._pipe_native.handle
+                if h is not None and h.value:
+                    lib().acme_replay_pipe_close(h, pipe)
+            except Exception:  # interpreter shutdown
+                pass
+            self._pipe = None
 
     def _f16_frames(self) -> bool:
         """The fused kernel's f16 copy applies to uint8 transition tables whose only large
@@ -319,6 +355,9 @@ class _TableIterator:
         elif fb is not None:
             check(L.acme_replay_sample_gather_frames(h, self._B, step, *raw, ptrs, fb.data_ptr(),
                                                      st), "replay sample")
+        elif stream is not None and getattr(self, "_pipe", None) is not None:
+            check(L.acme_replay_sample_gather_pipe(h, self._pipe, self._B, step, *raw, ptrs, st),
+                  "replay sample")
         else:
             check(L.acme_replay_sample_gather(h, self._B, step, *raw, ptrs, st),
                   "replay sample")
@@ -397,9 +436,15 @@ class _TableIterator:
             self._next_slot = (i + 1) % (self._P + 2)
             raw, ptrs = self._slots[i][:2]
             self._share[i] = self._draw(L, h, raw, ptrs, st, side, fb=self._fb[i])
-            self._ready[i].record(side)
+            # Pipelined: this launch completed the previous batch's rows; the new batch's
+            # event is recorded after the launch that copies them.
+            done = i
+            if self._pipe is not None:
+                done = i if self._pending is None else self._pending
+                self._pending = i
+            self._ready[done].record(side)
             self._queue.append(i)
-            t.set_reader_event(self._ready[i])
+            t.set_reader_event(self._ready[done])
         i = self._queue.pop(0)
         # A batch issued P steps ago has normally landed: ordering the caller's stream
         # after a completed event is a no-op, and skipping the wait saves its queue-side

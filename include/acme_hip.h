@@ -207,6 +207,25 @@ int acme_replay_sample_gather_frames(acme_replay* r, int64_t batch, uint64_t ste
                                      void* const* out_fields, uint16_t* frames_f16,
                                      void* stream);
 
+/* Pipelined sample + gather for a prefetching reader (round 6; the reference's prefetched
+ * dataset iterator, acme/datasets/reverb.py:136-137, issues draws ahead of their use).
+ * acme_replay_sample_gather_pipe draws a batch exactly as acme_replay_sample_gather (same
+ * keys, slots, probabilities and rows) but copies its rows in the pipe's NEXT call, in the
+ * same launch as that call's draw, so the draw's dependent tree loads overlap a row copy.
+ * A batch's rows are therefore complete only after the following call on its pipe (or
+ * acme_replay_pipe_flush); every operation that writes table rows (insert, commit,
+ * synthetic fill, acme_replay_storage) issues the pending copies first, so each batch
+ * gets the rows of its drawn keys.  A pipe is one reader on one stream; the transition
+ * layout only (two equal big fields): other layouts sample + gather at once.
+ * acme_replay_pipe_close drops a pending copy (its batch was never handed out). */
+int acme_replay_pipe_open(acme_replay* r, int32_t* pipe);
+int acme_replay_pipe_close(acme_replay* r, int32_t pipe);
+int acme_replay_pipe_flush(acme_replay* r, int32_t pipe);
+int acme_replay_sample_gather_pipe(acme_replay* r, int32_t pipe, int64_t batch,
+                                   uint64_t step_counter, int64_t* slots, uint64_t* keys,
+                                   double* probabilities, int64_t* table_size,
+                                   double* priorities, void* const* out_fields, void* stream);
+
 /* Data-parallel global-probability sampling: one table per rank holds a
  * shard of the global replay.  acme_replay_total writes the shard's sampling mass S_r
  * (sum of p^alpha, or the item count for Uniform) to out[0] on the device; the ranks
@@ -273,7 +292,7 @@ int acme_replay_debug_leaves(const acme_replay* r, const double** leaf_values,
  * after the caller wrote field rows, keys and raw priorities (device pointers from
  * acme_replay_storage / acme_replay_debug_leaves), sets the insert counter and rebuilds the
  * leaves (p^alpha) and every level of the sum tree on `stream`. */
-int acme_replay_storage(const acme_replay* r, int32_t field, void** out);
+int acme_replay_storage(acme_replay* r, int32_t field, void** out);
 int64_t acme_replay_inserted(const acme_replay* r);
 int acme_replay_restore(acme_replay* r, int64_t inserted, void* stream);
 

@@ -140,23 +140,27 @@ def test_device_rows_insert_matches_host_insert():
         np.testing.assert_array_equal(sa[k], sb[k])
 
 
-def test_concurrent_actor_inserts_with_prefetching_learner():
+@pytest.mark.parametrize("width", [16, 256])
+def test_concurrent_actor_inserts_with_prefetching_learner(width):
     """An actor thread writes items (payload = its key) through Table.insert / flush while
     the learner thread draws prefetched batches and writes priorities back, with no host
-    synchronisation: every gathered row carries the key the sampler reported for it."""
+    synchronisation: every gathered row carries the key the sampler reported for it.
+    width 256 (1 KiB rows: the transition layout) runs the pipelined draws, whose pending
+    row copies each commit issues before it lands (acme_replay_sample_gather_pipe)."""
     from acme_amd import replay, specs
     from acme_amd.adders import reverb as adders
     from acme_amd.datasets import make_reverb_dataset
     cap, B = 4096, 256
-    sig = (specs.Array((16,), np.int32), specs.Array((), np.int32), specs.Array((), np.float32),
-           specs.Array((), np.float32), specs.Array((16,), np.int32))
+    sig = (specs.Array((width,), np.int32), specs.Array((), np.int32),
+           specs.Array((), np.float32), specs.Array((), np.float32),
+           specs.Array((width,), np.int32))
     table = replay.Table(adders.DEFAULT_PRIORITY_TABLE, replay.selectors.Prioritized(0.6),
                          replay.selectors.Fifo(), cap, replay.rate_limiters.MinSize(1),
                          signature=sig, seed=5, device=torch.device("cuda"), flush_every=64)
     next_key = [0]
 
     def item(k):
-        row = np.full(16, k, np.int32)
+        row = np.full(width, k, np.int32)
         return (row, np.int32(k % 18), np.float32(k), np.float32(0.5), row + 1)
 
     def insert_some(n, rng):

@@ -297,6 +297,69 @@ def test_gather_kernels_bit_identical(fields):
         np.testing.assert_array_equal(outs[2][f], outs[0][f])
 
 
+def _pipe_buffers(r, B, fields):
+    import ctypes
+    info = r.alloc_sample_info(B)
+    outs = [torch.zeros(B, b, dtype=torch.uint8, device="cuda") for b in fields]
+    ptrs = (ctypes.c_void_p * len(outs))(*[x.data_ptr() for x in outs])
+    raw = [info[k].data_ptr() for k in ("slots", "keys", "probabilities", "table_size",
+                                          "priorities")]
+    return info, outs, ptrs, raw
+
+
+@pytest.mark.parametrize("prioritized", [True, False])
+@pytest.mark.parametrize("fields", [[28224, 4, 4, 4, 28224], [2048, 4, 2048], [96, 24, 4, 4, 96]])
+def test_pipelined_sample_gather(prioritized, fields):
+    """acme_replay_sample_gather_pipe (round 6): batch k's rows are copied by call k + 1's
+    launch (or a flush); every batch equals the oracle's draw of its step counter and the
+    rows of its keys.  Three buffer sets in rotation, a batch-size change mid-stream, and
+    an insert between a draw and its copy (the commit issues the pending copy first, so the
+    batch still gets the rows of its drawn keys, not the new items')."""
+    import ctypes
+    from acme_amd._lib import lib
+    L = lib()
+    rng = np.random.default_rng(9)
+    cap, n = 3000, 3000
+    data = [rng.integers(0, 256, (n, b), dtype=np.uint8) for b in fields]
+    pr = rng.uniform(0.0, 2.0, n)
+    o = OracleTable(cap, prioritized, 0.6, 1234)
+    o.insert(pr)
+    r = _native(cap, fields, prioritized)
+    r.insert(data, pr)
+    pid = ctypes.c_int32()
+    assert L.acme_replay_pipe_open(r.handle, ctypes.byref(pid)) == 0
+    st = torch.cuda.Stream()
+    sets = [_pipe_buffers(r, 300, fields) for _ in range(3)]
+    plan = [(0, 257, 11), (1, 257, 12), (2, 300, 13), (0, 64, 14), (1, 257, 15)]
+
+    def check(k):
+        s, B, step = plan[k]
+        info, outs = sets[s][0], sets[s][1]
+        ref = o.sample(B, step)
+        for key in ("slots", "probabilities", "table_size", "priorities"):
+            np.testing.assert_array_equal(info[key][:B].cpu().numpy(), ref[key])
+        keys = info["keys"][:B].cpu().numpy().view(np.int64)
+        for f in range(len(fields)):
+            np.testing.assert_array_equal(outs[f][:B].cpu().numpy(), data[f][keys % cap])
+
+    with torch.cuda.stream(st):
+        for k, (s, B, step) in enumerate(plan):
+            _, _, ptrs, raw = sets[s]
+            assert L.acme_replay_sample_gather_pipe(r.handle, pid.value, B, step, *raw, ptrs,
+                                                    ctypes.c_void_p(st.cuda_stream)) == 0
+            if k > 0:
+                st.synchronize()
+                check(k - 1)
+        # An insert while the last batch's copy is pending: overwrite every slot.
+        new = [rng.integers(0, 256, (cap, b), dtype=np.uint8) for b in fields]
+        r.insert(new, rng.uniform(0.1, 1.0, cap))
+        torch.cuda.synchronize()
+        check(len(plan) - 1)
+        assert L.acme_replay_pipe_flush(r.handle, pid.value) == 0  # nothing pending: no-op
+    assert L.acme_replay_pipe_close(r.handle, pid.value) == 0
+    torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("prioritized", [True, False])
 @pytest.mark.parametrize("fields", [[28224, 4, 4, 4, 28224], [2048, 4, 2048],
                                     [96, 24, 4, 4, 96], [1020, 8]])

@@ -1,6 +1,7 @@
 """Where the fused draw + gather's time goes (round 6): the configs[1] table (1M slots, uint8
 Atari transitions, prioritized), B = 512, timed alone with HIP events over 50 launches each:
-the fused sample + gather (acme_replay_sample_gather), the draw alone (acme_replay_sample),
+the fused sample + gather (acme_replay_sample_gather), the pipelined launch
+(acme_replay_sample_gather_pipe: this batch's draw + the previous batch's rows), the draw alone (acme_replay_sample),
 the gather alone (acme_replay_gather of the draw's slots) and a device-to-device copy of the
 same bytes (torch), plus the priority update alone.
 
@@ -53,6 +54,24 @@ def main():
     def gather():
         r.gather(info["slots"], outs)
 
+    # The pipelined launch (acme_replay_sample_gather_pipe): two buffer sets in rotation, each
+    # launch draws one batch and copies the rows of the one before.
+    pid = ctypes.c_int32()
+    check(lib().acme_replay_pipe_open(r.handle, ctypes.byref(pid)))
+    sets = []
+    for _ in range(2):
+        inf = r.alloc_sample_info(B)
+        o = [torch.empty(B, n, dtype=torch.uint8, device="cuda") for n in (row, 4, 4, 4, row)]
+        sets.append(([inf[k].data_ptr() for k in ("slots", "keys", "probabilities", "table_size",
+                                                  "priorities")],
+                     (ctypes.c_void_p * 5)(*[x.data_ptr() for x in o]), inf, o))
+
+    def pipe():
+        step[0] += 1
+        rw, pt = sets[step[0] & 1][:2]
+        check(lib().acme_replay_sample_gather_pipe(r.handle, pid.value, B, step[0], *rw, pt,
+                                                   stream_ptr()))
+
     src = torch.empty(2 * B * row, dtype=torch.uint8, device="cuda")
     dst = torch.empty_like(src)
     prios = torch.rand(B, dtype=torch.float64, device="cuda") + 0.1
@@ -61,7 +80,8 @@ def main():
         r.update_priorities(info["keys"], prios)
 
     mb = 2 * B * (2 * row + 12) / 1e6
-    for name, fn in (("fused sample+gather", fused), ("sample", draw), ("gather", gather),
+    for name, fn in (("fused sample+gather", fused), ("pipelined sample+gather", pipe),
+                     ("sample", draw), ("gather", gather),
                      ("torch d2d copy of the rows", lambda: dst.copy_(src)),
                      ("update_priorities", update)):
         us = timed(fn)
