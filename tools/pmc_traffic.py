@@ -82,7 +82,7 @@ SECTIONS = [
     (r"ConvDgradSub", "conv2_dgrad"),
     (r"ConvDgrad<", "conv3_dgrad"),
     (r"(?<!clip_)adam_kernel|adam_slabs_kernel", "adam"),
-    (r"sample_gather_pair_kernel", "replay_sample_gather"),
+    (r"sample_gather_pair_kernel|sample_gather_pipe_kernel", "replay_sample_gather"),
     (r"gather_fields_kernel|gather_pair_kernel|gather_pieces_kernel", "replay_gather"),
     (r"sample_prioritized_kernel", "replay_sample"),
     (r"prio_update_fused_kernel", "replay_update"),
