@@ -50,50 +50,62 @@ __device__ __forceinline__ int rescale_exp(float a) {
 // the workgroup calls.  All loads are issued before the first store.
 __device__ __forceinline__ void rescale_block(const RescaleJob& j) {
   constexpr int kMax = 16;
-  __shared__ uint32_t s_a[kMax];   // each record's maximum (f32 bits)
-  __shared__ float s_w0[kMax], s_r0[kMax], s_wi0[kMax];
+  __shared__ uint32_t s_a[kMax];  // each record's maximum (f32 bits)
   __shared__ int s_shift[kMax];
   __shared__ int s_bad;
-  __shared__ uint32_t s_gv[6];
-  __shared__ int64_t s_cnt[2];  // the guard's applied / skipped counts, read up front
-  __shared__ float s_dp, s_cwi;
   gemm::PScale* s = j.s;
   const int n = j.n;
   const int nw = blockDim.x >> 6, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const bool last = threadIdx.x == blockDim.x - 1;
+  const RescaleGuard& rg = j.rg;
+  // Every load in one round, before any LDS store (the records are reached through generic
+  // pointers, which the compiler must order against LDS stores): each wave's records' slots,
+  // thread i's record i, and the guard's inputs in the last thread.  The slots were written
+  // by atomics from every XCD, so each round trip goes past the local L2; one record per
+  // wave round (four rounds at 15 records) made this workgroup 6 us long and the priority
+  // write-back waited on its verdict (profiles/r06/replay/update_stamps.log).
+  constexpr int kPerWave = kMax;  // >= records per wave at any wave count
+  uint32_t av[kPerWave];
+#pragma unroll
+  for (int k = 0; k < kPerWave; ++k) {
+    const int i = wv + k * nw;
+    av[k] = i < n ? s[i].slot[lane].v : 0u;
+  }
+  const int ti = threadIdx.x;
+  float w0 = 0.f, r0 = 0.f, wi0 = 0.f;
+  if (ti < n) {
+    w0 = s[ti].w;
+    r0 = s[ti].r;
+    wi0 = s[ti].wi;
+  }
+  uint32_t gv[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+  int64_t cnt[2] = {0, 0};
+  float dpv = 0.f, cwi = 0.f;
+  if (last) {
+    cwi = j.copy_to >= 0 ? s[j.copy_from].wi : 0.f;
+    if (rg.g) {
+      gv[0] = rg.g->on;
+      gv[1] = rg.g->tt;
+      gv[2] = rg.g->t[rg.gate.par & 1];
+      gv[3] = rg.g->prm;
+      gv[4] = rg.g->hold;
+      gv[5] = rg.tmo ? rg.tmo[0] : 0u;
+      cnt[0] = rg.g->applied;
+      cnt[1] = rg.g->skipped;
+      if (rg.gate.dp) dpv = *rg.gate.dp;
+    }
+  }
   // Phase 1: every record's slot maximum (a wave per record, records strided over waves).
 #pragma unroll
-  for (int k = 0; k < kMax; ++k) {
+  for (int k = 0; k < kPerWave; ++k) {
     const int i = wv + k * nw;
     if (i >= n) break;
-    uint32_t a = s[i].slot[lane].v;
+    uint32_t a = av[k];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) a = max(a, (uint32_t)__shfl_xor((int)a, o, 64));
-    if (lane == 0) {
-      s_a[i] = a;
-      s_w0[i] = s[i].w;
-      s_r0[i] = s[i].r;
-      s_wi0[i] = s[i].wi;
-    }
+    if (lane == 0) s_a[i] = a;
   }
-  if (threadIdx.x == 0) {
-    s_bad = 0;
-    s_cwi = j.copy_to >= 0 ? s[j.copy_from].wi : 0.f;
-    const RescaleGuard& rg = j.rg;
-    s_gv[0] = s_gv[1] = s_gv[2] = s_gv[3] = s_gv[4] = s_gv[5] = 0u;
-    s_cnt[0] = s_cnt[1] = 0;
-    s_dp = 0.f;
-    if (rg.g) {  // the guard's inputs, read before any store (with the slots: one round trip)
-      s_gv[0] = rg.g->on;
-      s_gv[1] = rg.g->tt;
-      s_gv[2] = rg.g->t[rg.gate.par & 1];
-      s_gv[3] = rg.g->prm;
-      s_gv[4] = rg.g->hold;
-      s_gv[5] = rg.tmo ? rg.tmo[0] : 0u;
-      s_cnt[0] = rg.g->applied;
-      s_cnt[1] = rg.g->skipped;
-      if (rg.gate.dp) s_dp = *rg.gate.dp;
-    }
-  }
+  if (threadIdx.x == 0) s_bad = 0;
   __syncthreads();
   // Phase 2: per record, the overflow shift and the bad flag.
   if (threadIdx.x < n) {
@@ -102,8 +114,8 @@ __device__ __forceinline__ void rescale_block(const RescaleJob& j) {
     const bool live = !(i >= j.skip_lo && i < j.skip_hi);
     const bool finite = a <= 3.0e38f;
     int wexp;
-    (void)frexpf(s_w0[i], &wexp);  // w0 = 2^(wexp - 1)
-    const float aw = a * s_w0[i];
+    (void)frexpf(w0, &wexp);  // w0 = 2^(wexp - 1)
+    const float aw = a * w0;
     s_shift[i] = live && finite && a > 0.f && !(aw < 65520.f) ? rescale_exp(a) - (wexp - 1) : 0;
     // Overflowed (max w >= 65520, or not finite) or underflowed (0 < max w < 1: the
     // largest element's low plane is subnormal, so the planes carry less than an f32
@@ -122,9 +134,8 @@ __device__ __forceinline__ void rescale_block(const RescaleJob& j) {
   if (threadIdx.x < n && !(threadIdx.x >= j.skip_lo && threadIdx.x < j.skip_hi)) {
     const int i = threadIdx.x;
     const float a = __builtin_bit_cast(float, s_a[i]);
-    const float w0 = s_w0[i], wi0 = s_wi0[i];
     const bool persistent = i >= j.nt;
-    const float stored = persistent ? wi0 : s_r0[i];  // the read scale of the planes stored now
+    const float stored = persistent ? wi0 : r0;  // the read scale of the planes stored now
     gemm::PScale* rec = s + i;
     if (a == 0.f) {  // no maximum taken: the scale stays
       if (persistent) rec->r = rec->rl = stored;
@@ -148,27 +159,26 @@ __device__ __forceinline__ void rescale_block(const RescaleJob& j) {
       else if (!j.defer_r) rec->r = wi;
     }
   }
-  if (threadIdx.x == blockDim.x - 1) {
+  if (last) {
     if (j.copy_to >= 0) {
-      s[j.copy_to].r = s_cwi;
-      s[j.copy_to].rl = s_cwi;
+      s[j.copy_to].r = cwi;
+      s[j.copy_to].rl = cwi;
     }
-    const RescaleGuard& rg = j.rg;
     StepGuard* g = rg.g;
     const uint32_t bad = s_bad ? 1u : 0u;
     if (g && rg.mode == kRgTarget) {
-      g->t[rg.gate.par & 1] = s_gv[1] | bad;
+      g->t[rg.gate.par & 1] = gv[1] | bad;
       g->tt = 0u;
     } else if (g && rg.mode == kRgQValues) {
-      g->qv = s_gv[1] | bad;
+      g->qv = gv[1] | bad;
       g->tt = 0u;
     } else if (g && rg.mode == kRgFlag) {
       if (bad) g->on = 1u;
     } else if (g && rg.mode == kRgStep) {
       // The flags (on, prm) are cleared by the step's Adam launch, after every reader.
-      const bool timed_out = rg.tmo && s_gv[5] != 0u;
+      const bool timed_out = rg.tmo && gv[5] != 0u;
       const bool skip =
-          (s_gv[0] | s_gv[2] | s_gv[4] | bad) != 0u || s_dp > 0.f || timed_out;
+          (gv[0] | gv[2] | gv[4] | bad) != 0u || dpv > 0.f || timed_out;
       // The verdict first (the same launch's update workgroups wait for it), then the
       // counts from the values read up front: no load between the decision and the store.
       const uint32_t v = (rg.seq << 1) | (skip ? 1u : 0u);
@@ -182,12 +192,12 @@ __device__ __forceinline__ void rescale_block(const RescaleJob& j) {
       }
       g->last = skip ? 1u : 0u;
       if (skip) {
-        const int64_t k = s_cnt[1] + 1;
+        const int64_t k = cnt[1] + 1;
         g->skipped = k;
         if (rg.host_skipped) *rg.host_skipped = k;
         if (rg.sticky) g->hold = 1u;
       } else {
-        g->applied = s_cnt[0] + 1;
+        g->applied = cnt[0] + 1;
       }
     } else if (g && rg.mode == kRgClear) {
       g->hold = 0u;
