@@ -4,7 +4,9 @@ update_priorities) runs some steps, then every workgroup's s_memrealtime stamps 
 comparable across workgroups) of the last launch are summarised against the launch's first
 entry: workgroup 0 runs the step's rescale (entry, done), the update workgroups their phases
 (entry, keys resolved, node list, verdict, round-2 loads landed, levels, exit).
-Run under gpurun: python3 tools/update_stamps.py"""
+Run under gpurun: python3 tools/update_stamps.py [--steady]
+--steady: the steps run back to back (the host ahead of the GPU, as in the bench's timed
+region) and only the last launch is summarised; otherwise each step is synchronised."""
 import os
 import sys
 
@@ -18,6 +20,9 @@ PHASES = ("entry", "keys", "nodes", "verdict", "round2", "levels", "exit")
 
 def main():
     import torch
+    steady = "--steady" in sys.argv
+    if "--abs" in sys.argv:
+        os.environ["STAMPS_ABS"] = "1"
     sys.argv = [sys.argv[0], "--no-cpu-baseline"]
     import bench
     args = bench.parse()
@@ -26,6 +31,8 @@ def main():
     learner = step.__self__
     for i in range(30):
         step()
+        if steady and i < 29:
+            continue
         torch.cuda.synchronize()
         st = learner.native.debug_buffer("gemm_stamps").view(np.int64).reshape(5, 4096, 8)[4]
         used = st[:257]
@@ -34,6 +41,9 @@ def main():
         t0 = used[used[:, 0] != 0, 0].min()  # every workgroup stamps its entry each launch
         rel = np.where(used >= t0, (used - t0) * 0.01, np.nan)  # us; older launches' stamps out
         print(f"step {i}: launch span {np.nanmax(rel):.2f} us")
+        if "--abs" in sys.argv[1:] or os.environ.get("STAMPS_ABS"):
+            last = used[used >= t0].max()
+            print(f"  abs first entry {int(t0)} last stamp {int(last)} (100 MHz ticks)")
         print(f"  workgroup 0 (rescale): entry {rel[0, 0]:.2f}, done {rel[0, 1]:.2f}")
         upd = rel[1:]
         busy = ~np.isnan(upd[:, 2])
