@@ -806,8 +806,16 @@ __device__ __forceinline__ void lds_barrier() {
 __device__ __forceinline__ void store_shared_level(double* p, double v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// R: updates per thread the launch holds (n <= 256 R).  The small form (R = 2, up to 512
+// updates: a DQN batch) takes 21 KB of LDS and few registers, so its workgroups fit beside
+// the next step's target forward (gemm_p3c12_kernel, 121 KB of LDS per CU), which the
+// early start runs at the same time on the side stream; at R = 16 (49 KB, 200 VGPRs) they
+// waited for its blocks to retire (24 us in the two-stream trace against 12 us alone,
+// profiles/r06/schedule/).
+template <int R>
 __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs a) {
-  __shared__ int64_t s_slot[kFusedUpdateMax];
+  static_assert(R * 256 <= kFusedUpdateMax, "update capacity");
+  __shared__ int64_t s_slot[R * 256];
   __shared__ int s_len, s_np, s_ovf, s_last;
   __shared__ double s_ch[kUpdPairs][64];  // children of each prefetched node
   __shared__ int64_t s_node[kUpdPairs];
@@ -839,7 +847,6 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
   // registers.  Its stale-key check shares round 2 with the children rows, and its leaf
   // p^alpha is computed while those loads are in flight (round 6: three dependent rounds of
   // global loads became two, and the f64 power left the critical path).
-  constexpr int R = kFusedUpdateMax / 256;
   uint64_t kv[R];
   double pr[R];
   int64_t sl[R];
@@ -2257,7 +2264,9 @@ int acme::replay_update_priorities_gated(acme_replay* r, const uint64_t* keys,
     a.top_computed = computed_top_nodes(r) > 0 ? 1 : 0;
     a.done = r->upd_done;
     a.stamps = g_update_stamps;
-    prio_update_fused_kernel<<<kFusedUpdateBlocks + (a.job.s ? 1 : 0), 256, 0, st>>>(a);
+    const unsigned blocks = kFusedUpdateBlocks + (a.job.s ? 1 : 0);
+    if (n <= 2 * 256) prio_update_fused_kernel<2><<<blocks, 256, 0, st>>>(a);
+    else prio_update_fused_kernel<kFusedUpdateMax / 256><<<blocks, 256, 0, st>>>(a);
     ACME_LAUNCH_CHECK();
     return ACME_OK;
   }
