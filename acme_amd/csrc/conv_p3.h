@@ -69,6 +69,20 @@ __device__ __forceinline__ void st8(float* p, const V8& v) {
   *reinterpret_cast<float4*>(p) = float4{v[0], v[1], v[2], v[3]};
   *reinterpret_cast<float4*>(p + 4) = float4{v[4], v[5], v[6], v[7]};
 }
+#ifndef ACME_NT_SLABS
+#define ACME_NT_SLABS 0
+#endif
+// The same as non-temporal stores when bit `which` of ACME_NT_SLABS is set (experiment).
+template <int which>
+__device__ __forceinline__ void st8_slab(float* p, const V8& v) {
+  if constexpr ((ACME_NT_SLABS & which) != 0) {
+    using f4 = __attribute__((ext_vector_type(4))) float;
+    __builtin_nontemporal_store(f4{v[0], v[1], v[2], v[3]}, reinterpret_cast<f4*>(p));
+    __builtin_nontemporal_store(f4{v[4], v[5], v[6], v[7]}, reinterpret_cast<f4*>(p + 4));
+  } else {
+    st8(p, v);
+  }
+}
 // ReLU mask of 8 stored activations (their f16 h plane; x > 0 <=> h > 0): dz where x > 0.
 __device__ __forceinline__ void relu_mask8(const CPlanes& x, int64_t e, V8& v) {
   const uint4 w = *reinterpret_cast<const uint4*>(x.p + e);
@@ -252,7 +266,7 @@ struct P3ConvWgrad {
     V8 v;
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = NPA == 1 ? (acc[j] * rs) / 255.0f : acc[j] * rs;
-    st8(slab + ((size_t)split * (M + 1) + i) * N + n, v);
+    st8_slab<1>(slab + ((size_t)split * (M + 1) + i) * N + n, v);
     return 0.f;
   }
   __device__ void store_colsum(int n, float v, int split) const {
@@ -447,7 +461,7 @@ struct P3DenseFwd {
     V8 v;
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = acc[j] * rs;
-    st8(slab + ((size_t)split * M + m) * N + n, v);
+    st8_slab<2>(slab + ((size_t)split * M + m) * N + n, v);
     return 0.f;
   }
 };
@@ -484,7 +498,7 @@ struct P3DenseWgrad {
     V8 v;
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = acc[j] * rs;
-    st8(out + (size_t)i * N + n, v);
+    st8_slab<1>(out + (size_t)i * N + n, v);
     return 0.f;
   }
   __device__ void store_colsum(int n, float v, int) const {

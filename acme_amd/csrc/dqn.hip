@@ -1266,6 +1266,12 @@ static int forward_backward_stage(acme_dqn* l, const acme_transition_batch* batc
                         P(l, l->params, l->t_c2b), P(l, l->params, l->t_c3b)};
       torso::Side sd;
       sd.single_role = l->single_role;
+      // conv1's weight gradient on the single-role kernel: its two 20-KB stages (40 KB of
+      // LDS) fit beside the next step's fused target convolution (121 KB) that runs on the
+      // side stream at the same time; the producer / consumer kernel's three stages (60 KB)
+      // do not.  Step 0.4957 -> 0.4920 ms (three alternating 300-step pairs, round 6,
+      // profiles/r06/schedule/ab_conv1_wgrad_single_role.log).
+      sd.conv1_single = true;
       if (side_stream(l)) {
         sd.side = l->side;
         sd.slab = l->side_slab;

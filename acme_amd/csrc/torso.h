@@ -116,6 +116,7 @@ struct Side {
   // conv1's weight gradient on the single-role kernel instead of the producer / consumer one
   // (the same bits; tests, ACME_V_WSN=1 at the learner's creation).
   bool single_role = false;
+  bool conv1_single = false;  // conv1's weight gradient on the single-role kernel (the DQN step)
 };
 // dz3: conv3's dZ planes [rows][kFlat] (masked); dz2 / dz1 plane scratch.
 int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int rows,

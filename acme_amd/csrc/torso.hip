@@ -395,14 +395,14 @@ int backward_p3(const PWeights& w, const Grads& g, const Frames& frames, int row
     int M1, N1;
     if (frames.u8) {
       P3ConvWgrad<G1, 1, true> p;
-      if ((rc = conv1_wgrad_p3<true>(frames, rows, dz1, slab, splits, sd.single_role, p, st)))
+      if ((rc = conv1_wgrad_p3<true>(frames, rows, dz1, slab, splits, sd.conv1_single, p, st)))
         return rc;
       M1 = p.M, N1 = p.N;
       if (!defer && (rc = p3_wgrad_reduce(p, splits, slab, g.w1, g.b1, "conv1_wgrad_reduce", st)))
         return rc;
     } else {
       P3ConvWgrad<G1, 1> p;
-      if ((rc = conv1_wgrad_p3<false>(frames, rows, dz1, slab, splits, sd.single_role, p, st)))
+      if ((rc = conv1_wgrad_p3<false>(frames, rows, dz1, slab, splits, sd.conv1_single, p, st)))
         return rc;
       M1 = p.M, N1 = p.N;
       if (!defer && (rc = p3_wgrad_reduce(p, splits, slab, g.w1, g.b1, "conv1_wgrad_reduce", st)))
