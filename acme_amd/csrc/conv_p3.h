@@ -69,19 +69,16 @@ __device__ __forceinline__ void st8(float* p, const V8& v) {
   *reinterpret_cast<float4*>(p) = float4{v[0], v[1], v[2], v[3]};
   *reinterpret_cast<float4*>(p + 4) = float4{v[4], v[5], v[6], v[7]};
 }
-#ifndef ACME_NT_SLABS
-#define ACME_NT_SLABS 0
-#endif
-// The same as non-temporal stores when bit `which` of ACME_NT_SLABS is set (experiment).
-template <int which>
-__device__ __forceinline__ void st8_slab(float* p, const V8& v) {
-  if constexpr ((ACME_NT_SLABS & which) != 0) {
-    using f4 = __attribute__((ext_vector_type(4))) float;
-    __builtin_nontemporal_store(f4{v[0], v[1], v[2], v[3]}, reinterpret_cast<f4*>(p));
-    __builtin_nontemporal_store(f4{v[4], v[5], v[6], v[7]}, reinterpret_cast<f4*>(p + 4));
-  } else {
-    st8(p, v);
-  }
+// The same with non-temporal stores: weight-gradient results (the conv split-K slabs, the
+// dense weight gradient), which only the end-of-step Adam reads.  They stream to memory
+// during the kernel instead of sitting dirty in the L2 until its end-of-kernel writeback:
+// step 0.4920 -> 0.4895 ms over six alternating 300-step pairs (Adam, which reads them
+// later, 51.6 -> 56.7 us; the weight gradients 2-4 us each faster; round 6,
+// profiles/r06/schedule/ab_nt_wgrad_slabs.log).
+__device__ __forceinline__ void st8_nt(float* p, const V8& v) {
+  using f4 = __attribute__((ext_vector_type(4))) float;
+  __builtin_nontemporal_store(f4{v[0], v[1], v[2], v[3]}, reinterpret_cast<f4*>(p));
+  __builtin_nontemporal_store(f4{v[4], v[5], v[6], v[7]}, reinterpret_cast<f4*>(p + 4));
 }
 // ReLU mask of 8 stored activations (their f16 h plane; x > 0 <=> h > 0): dz where x > 0.
 __device__ __forceinline__ void relu_mask8(const CPlanes& x, int64_t e, V8& v) {
@@ -266,7 +263,7 @@ struct P3ConvWgrad {
     V8 v;
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = NPA == 1 ? (acc[j] * rs) / 255.0f : acc[j] * rs;
-    st8_slab<1>(slab + ((size_t)split * (M + 1) + i) * N + n, v);
+    st8_nt(slab + ((size_t)split * (M + 1) + i) * N + n, v);
     return 0.f;
   }
   __device__ void store_colsum(int n, float v, int split) const {
@@ -461,7 +458,7 @@ struct P3DenseFwd {
     V8 v;
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = acc[j] * rs;
-    st8_slab<2>(slab + ((size_t)split * M + m) * N + n, v);
+    st8(slab + ((size_t)split * M + m) * N + n, v);
     return 0.f;
   }
 };
@@ -498,7 +495,7 @@ struct P3DenseWgrad {
     V8 v;
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = acc[j] * rs;
-    st8_slab<1>(out + (size_t)i * N + n, v);
+    st8_nt(out + (size_t)i * N + n, v);
     return 0.f;
   }
   __device__ void store_colsum(int n, float v, int) const {
