@@ -444,12 +444,16 @@ int nature_forward_p3(acme_dqn* l, const float* prm, uint16_t* wpl, const torso:
     // (per-CU L2 intake): fc_fwd 47.0 -> 45.3 us, step 0.5037 -> 0.5028 ms
     // over 200 steps and 0.5146 -> 0.5084 ms over 20-step windows (three alternating pairs,
     // round 4; it had split-K 4 on 128x128 tiles).
-    // The target forward at the headline batch (512 rows) on 256x128 tiles too, at split-K
-    // 16 (2 x 8 x 16 blocks; its head sums 16 partials): fc_fwd 45.2 -> 43.9 us averaged over
-    // both launches, the step unchanged (0.5040 vs 0.5037 ms, three alternating pairs).
+    // The target forward at the headline batch (512 rows) on 256x128 tiles too, at split-K 8
+    // (2 x 8 x 8 = 128 blocks, half the CUs; its head sums 8 partials).  It runs on the side
+    // stream with ~100 us of slack before the loss, beside the online conv1 / conv2 forward:
+    // with half the blocks it leaves half the CUs to them and writes half the partial tile
+    // bytes.  Round 6: step 0.4744 -> 0.4678 ms (six alternating 300-step pairs) and 0.4803
+    // -> 0.4729 ms over the driver's 20-step window (three pairs) against split-K 16 (256
+    // blocks; round 4 had measured 16 against 8 as equal on that schedule); split-K 4: 0.4709.
     const bool tall = rows > 512;
     const bool ttall = rows == 512 && !defer_head;
-    const int splits = ttall ? 16 : kFcFwdSplits;
+    const int splits = kFcFwdSplits;
     p.M = rows; p.N = 2 * kHidden; p.K = kFlat; p.k_chunk = chunk_for(kFlat, splits);
     p.a_src = SRC(x3, (int64_t)rows * kFlat); p.ldx = kFlat;
     p.b_src = SRC(WP(l, wpl, l->t_fcw), (int64_t)kFlat * 2 * kHidden); p.slab = slab;
