@@ -842,6 +842,27 @@ def impala_process_actors(args, dev, pool, queue, learner, B, T, A, H, env_us):
     print(json.dumps(out))
 
 
+def merge_launch_sections(sections, name, other, labels):
+    """One record for a kernel profiled as two sections (the DQN fc_fwd: the online launch,
+    256 blocks over the whole chip, and the target launch, 128 blocks by design, DESIGN.md
+    4.1): summed time and FLOPs under `name`, each launch kept under "per_launch"."""
+    a = next((r for r in sections if r["name"] == name), None)
+    b = next((r for r in sections if r["name"] == other), None)
+    if a is None or b is None or a.get("bound") != "mfma" or b.get("bound") != "mfma":
+        return
+    parts = []
+    for lab, r in zip(labels, (a, b)):
+        parts.append(dict(launch=lab, launches=r["launches"], avg_us=r["avg_us"],
+                          achieved=r["achieved"], frac=r["frac"]))
+    fl = sum(r["achieved"] * 1e12 * r["avg_us"] * 1e-6 * r["launches"] for r in (a, b))
+    ms = a["total_ms"] + b["total_ms"]
+    n = a["launches"] + b["launches"]
+    tf = fl / (ms * 1e-3) / 1e12
+    a.update(launches=n, avg_us=round(1e3 * ms / n, 2), total_ms=round(ms, 3),
+             achieved=round(tf, 2), frac=round(tf / a["peak"], 4), per_launch=parts)
+    sections.remove(b)
+
+
 def pmc_traffic(workload: str, section: str):
     """HBM bytes per launch of `section` from the newest committed PMC summary
     (profiles/<round>/pmc_traffic_<workload>.json, written by tools/pmc_traffic.py from
@@ -1034,6 +1055,7 @@ def main():
                 rec.update(design_bytes=round(by.value / cnt.value), survey_bytes=round(sb),
                            frac_survey_bytes=round(sb / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
         sections.append(rec)
+    merge_launch_sections(sections, "fc_fwd", "fc_fwd_target", ("online", "target"))
     sections.sort(key=lambda r: -r["total_ms"])
     # Sum of the profiled kernel durations per step: ms_per_step minus this is launch gaps
     # and host time the GPU waited on.
@@ -1052,6 +1074,8 @@ def main():
                         peak=dom["peak"], unit="TFLOP/s", frac=dom["frac"],
                         traffic=traffic, traffic_unit="bytes/launch", traffic_source=src,
                         avg_us=dom["avg_us"])
+        if "per_launch" in dom:
+            roofline["per_launch"] = dom["per_launch"]
     if rank == 0:
         for s in sections:
             print(f"[bench] {s['name']:16s} {s['launches']:6d} x {s['avg_us']:9.2f} us  "
