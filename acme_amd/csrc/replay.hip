@@ -619,7 +619,10 @@ __global__ void __launch_bounds__(256) sample_gather_pipe_kernel(
   for (int k = 0; k < MAXC; ++k) {
     const int32_t c = t + k * T;
     vu4* p = c < nvec ? b0 + c : b1 + (c - nvec);
-    if (c < 2 * nvec) *p = v[k];
+    // Non-temporal: a prefetching reader's learner reads these rows steps later (six
+    // alternating 300-step pairs, DQN 0.4701 -> 0.4679 ms; round 6,
+    // profiles/r06/replay/ab_nt_row_stores.log).
+    if (c < 2 * nvec) __builtin_nontemporal_store(v[k], p);
   }
 #pragma unroll
   for (int q = 0; q < ACME_MAX_FIELDS; ++q) {
