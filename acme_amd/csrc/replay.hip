@@ -136,6 +136,37 @@ __device__ __forceinline__ double wave_scan64(double x) {
   return x;
 }
 
+// The scan's total (its lane-63 value) in every lane, with the same bits: lane 63 of the
+// scan adds aligned blocks pairwise (round d: the block of d lanes ending at 63 - d to the one
+// ending at 63), and so does this butterfly (each round adds the aligned neighbour block of
+// the same size; f64 addition is commutative).  DPP moves for blocks of 1..8 lanes, a swizzle
+// for 16 and two lane reads for 32 replace six rounds of LDS permutes.  The whole wave must
+// be active (as for wave_scan64).
+template <int Ctrl>
+__device__ __forceinline__ double dpp_f64(double x) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, x);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)u, Ctrl, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), Ctrl, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+__device__ __forceinline__ double wave_total64(double x) {
+  x = x + dpp_f64<0xB1>(x);   // quad_perm [1,0,3,2]: pairs
+  x = x + dpp_f64<0x4E>(x);   // quad_perm [2,3,0,1]: quads
+  x = x + dpp_f64<0x141>(x);  // row_half_mirror: blocks of 8
+  x = x + dpp_f64<0x140>(x);  // row_mirror: blocks of 16
+  const uint64_t u = __builtin_bit_cast(uint64_t, x);
+  const int lo = __builtin_amdgcn_ds_swizzle((int)(uint32_t)u, 0x401F);  // lane ^ 16
+  const int hi = __builtin_amdgcn_ds_swizzle((int)(uint32_t)(u >> 32), 0x401F);
+  x = x + __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+  const uint64_t v = __builtin_bit_cast(uint64_t, x);
+  const uint32_t a0 = __builtin_amdgcn_readlane((int)(uint32_t)v, 31);
+  const uint32_t a1 = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 31);
+  const uint32_t b0 = __builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+  const uint32_t b1 = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63);
+  return __builtin_bit_cast(double, ((uint64_t)a1 << 32) | a0) +
+         __builtin_bit_cast(double, ((uint64_t)b1 << 32) | b0);
+}
+
 __device__ __forceinline__ int select_child(double v, double s, double t) {
   const uint64_t le = __ballot(s <= t);
   const uint64_t nz = __ballot(v > 0.0);
@@ -169,7 +200,7 @@ __device__ __forceinline__ double top_entry(const double* const* level, int nlev
 #pragma unroll
   for (int g = 0; g < kTopComputed; ++g) {
     if (g >= top_nodes) break;  // wave-uniform
-    const double t = __shfl(wave_scan64(ch[g]), 63, 64);
+    const double t = wave_total64(ch[g]);
     if (lane == g) v = t;
   }
   return v;
@@ -202,7 +233,7 @@ __device__ __forceinline__ void draw_prioritized(const TreeView& tree, int64_t s
 #pragma unroll
         for (int g = 0; g < kTopComputed; ++g) {
           if (g >= tree.top_nodes) break;  // wave-uniform
-          const double tt = __shfl(wave_scan64(ch[g]), 63, 64);
+          const double tt = wave_total64(ch[g]);
           if (lane == g) v = tt;
         }
       } else {
@@ -305,7 +336,7 @@ __global__ void total_kernel(TreeView tree, int prioritized, int64_t size,
     if (lane == 0) *out = (double)size;
     return;
   }
-  const double s = wave_scan64(top_entry(tree.level, tree.nlevels, tree.top_nodes));
+  const double s = wave_total64(top_entry(tree.level, tree.nlevels, tree.top_nodes));
   if (lane == 63) *out = s;
 }
 
@@ -691,7 +722,7 @@ __global__ void __launch_bounds__(256) level_update_kernel(
     node = node_begin + j;
   }
   const double v = child[node * 64 + lane];
-  const double s = wave_scan64(v);
+  const double s = wave_total64(v);
   if (lane == 63) parent[node] = s;
 }
 
@@ -995,7 +1026,7 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
       for (int l = 1; l <= h; ++l) {
         for (int q = wave; q < np; q += nw) {
           if (s_lvl[q] != l) continue;
-          const double v = wave_scan64(s_ch[q][lane]);
+          const double v = wave_total64(s_ch[q][lane]);
           if (lane == 63) s_val[q] = v;
         }
         lds_barrier();
@@ -1010,6 +1041,7 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
     }
     // The step's verdict (published by workgroup 0's rescale while this workgroup resolved
     // its keys, loaded and computed), before the first store.
+    stamp(7);
     if (verdict) skip = wait_verdict_skip(a.job.rg.g, a.job.rg.seq, vfirst);
     stamp(3);
     if (!skip) {
@@ -1032,7 +1064,7 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
         for (int l = 1; l <= h; ++l) {  // read back what this workgroup stored (levels below are its own)
           for (int e = wave; e < len; e += nw) {
             const int64_t node = (s_slot[e] >> 13) >> (6 * l);
-            const double v = wave_scan64(a.level[l - 1][node * 64 + lane]);
+            const double v = wave_total64(a.level[l - 1][node * 64 + lane]);
             if (lane == 63) {
               if (l == h && !a.top_computed) store_shared_level(a.level[l] + node, v);
               else a.level[l][node] = v;
@@ -1062,7 +1094,7 @@ __global__ void __launch_bounds__(256) prio_update_fused_kernel(FusedUpdateArgs 
   for (int64_t node = wave; node < a.top_nodes; node += nw) {
     const double c = __hip_atomic_load(a.level[top - 1] + node * 64 + lane, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
-    const double v = wave_scan64(c);
+    const double v = wave_total64(c);
     if (lane == 63) a.level[top][node] = v;
   }
   if (tid == 0) __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

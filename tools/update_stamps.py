@@ -3,7 +3,8 @@ ACME_V_STAMPS=1): the bench's DQN path (GPU table -> dataset -> DQNLearner.step(
 update_priorities) runs some steps, then every workgroup's s_memrealtime stamps (100 MHz,
 comparable across workgroups) of the last launch are summarised against the launch's first
 entry: workgroup 0 runs the step's rescale (entry, done), the update workgroups their phases
-(entry, keys resolved, node list, verdict, round-2 loads landed, levels, exit).
+(entry, keys resolved, node list, verdict, round-2 loads landed, levels, exit, LDS work
+done before the verdict wait).
 Run under gpurun: python3 tools/update_stamps.py [--steady]
 --steady: the steps run back to back (the host ahead of the GPU, as in the bench's timed
 region) and only the last launch is summarised; otherwise each step is synchronised."""
@@ -15,7 +16,7 @@ import numpy as np
 os.environ["ACME_V_STAMPS"] = "1"
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-PHASES = ("entry", "keys", "nodes", "verdict", "round2", "levels", "exit")
+PHASES = ("entry", "keys", "nodes", "verdict", "round2", "levels", "exit", "lds")
 
 
 def main():
@@ -49,7 +50,7 @@ def main():
         busy = ~np.isnan(upd[:, 2])
         print(f"  update workgroups with work: {busy.sum()} of {len(upd)}")
         for p, name in enumerate(PHASES):
-            col = upd[busy, p] if p >= 2 and p <= 5 else upd[:, p]
+            col = upd[busy, p] if p in (2, 3, 4, 5, 7) else upd[:, p]
             col = col[~np.isnan(col)]
             if len(col):
                 print(f"  {name:8s} min {col.min():6.2f}  median {np.median(col):6.2f}  "
